@@ -1,0 +1,511 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by RUNNING the reference.
+
+Test infrastructure only.  This script imports BoogaQ/PPO-exploration from
+/root/reference (read-only; it exists only in the build container, never on the
+GPU box) and records inputs + outputs of the functions on the hot path as small
+.npz files.  No reference source is copied: the reference is imported and
+called, and only arrays are written.
+
+  buffer.py, util.py, models.py, logger.py import cleanly.
+  ppo.py imports gym / stable_baselines3 / mujoco_py at module level
+  (ppo.py:2,20; env.py:1-2).  None of them is installed; the minimal
+  sys.modules entries below only satisfy those import statements (a
+  `spaces` namespace and an empty `VecEnv` base class).  Nothing the
+  algorithm computes comes from them: the environment is a FakeVec defined
+  here whose outputs are recorded into the fixtures, so the oracle replays
+  exactly the same env stream.  (SURVEY.md §8c documents this recipe.)
+
+Run:  python tests/golden/make_golden.py        (skips if /root/reference absent)
+"""
+import os
+import sys
+import types
+import importlib.util
+
+import numpy as np
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+# --------------------------------------------------------------------------
+# import plumbing
+# --------------------------------------------------------------------------
+def _install_import_stubs():
+    """Satisfy ppo.py's third-party import statements (not its computation)."""
+    class VecEnv:  # ppo.py:20 uses it only for isinstance()
+        pass
+
+    gym = types.ModuleType("gym")
+    gym.spaces = types.SimpleNamespace()
+    sys.modules.setdefault("gym", gym)
+    sys.modules.setdefault("gym.spaces", types.ModuleType("gym.spaces"))
+    sys.modules.setdefault("mujoco_py", types.ModuleType("mujoco_py"))
+    sb3 = types.ModuleType("stable_baselines3")
+    common = types.ModuleType("stable_baselines3.common")
+    vec = types.ModuleType("stable_baselines3.common.vec_env")
+    base = types.ModuleType("stable_baselines3.common.vec_env.base_vec_env")
+    cmd = types.ModuleType("stable_baselines3.common.cmd_util")
+    base.VecEnv = VecEnv
+    for name in ("SubprocVecEnv", "VecFrameStack", "VecTransposeImage", "VecNormalize"):
+        setattr(vec, name, type(name, (), {}))
+    cmd.make_atari_env = cmd.make_vec_env = lambda *a, **k: None
+    for m in (sb3, common, vec, base, cmd):
+        sys.modules.setdefault(m.__name__, m)
+    return VecEnv
+
+
+def import_reference():
+    sys.dont_write_bytecode = True
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    VecEnv = _install_import_stubs()
+    import util, buffer, models, logger  # noqa: E401
+    import ppo
+    return types.SimpleNamespace(util=util, buffer=buffer, models=models, logger=logger,
+                                 ppo=ppo, VecEnv=VecEnv)
+
+
+# Space duck types: the reference dispatches on __class__.__name__
+# (models.py:20, buffer.py:38, util.py:53).
+class Discrete:
+    def __init__(self, n):
+        self.n = n
+        self.shape = ()
+
+
+class Box:
+    def __init__(self, shape):
+        self.shape = tuple(shape)
+
+
+def make_fakevec(VecEnv, n_envs, obs_dim, action_space, seed, done_p=0.05, obs_shape=None):
+    """Action-independent env with a PRIVATE RandomState (does not touch np's
+    global RNG, so the reference's own np.random consumption is undisturbed)."""
+    shape = obs_shape if obs_shape is not None else (obs_dim,)
+
+    class FakeVec(VecEnv):
+        def __init__(self):
+            self.num_envs = n_envs
+            self.observation_space = Box(shape)
+            self.action_space = action_space
+            self.rs = np.random.RandomState(seed)
+            self.trace = {"obs": [], "rew": [], "done": []}
+
+        def _obs(self):
+            return self.rs.randn(n_envs, *shape).astype(np.float32)
+
+        def reset(self):
+            o = self._obs()
+            self.trace["obs"].append(o.copy())
+            return o
+
+        def step(self, actions):
+            o = self._obs()
+            r = (self.rs.rand(n_envs) < 0.3).astype(np.float32) * self.rs.rand(n_envs).astype(np.float32)
+            d = self.rs.rand(n_envs) < done_p
+            infos = [{"episode": {"r": float(i), "l": 1}} if d[i] else {} for i in range(n_envs)]
+            self.trace["obs"].append(o.copy())
+            self.trace["rew"].append(r.copy())
+            self.trace["done"].append(d.copy())
+            return o, r, d, infos
+
+        def unnormalize_obs(self, obs):
+            return obs
+
+    return FakeVec()
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    print("wrote", os.path.relpath(path, OUT), sum(a.nbytes for a in map(np.asarray, arrays.values())), "B")
+
+
+# --------------------------------------------------------------------------
+# (1) GAE, one stream: RolloutStorage.compute_returns_and_advantages
+#     buffer.py:203-230, called as ppo.py:196 (last_value = V(s_{T-1}))
+# --------------------------------------------------------------------------
+def gen_gae(R):
+    import torch
+    cases = [  # (T, N, gamma, lam, done_p, seed)
+        (1, 1, 0.99, 0.95, 0.0, 0),
+        (5, 3, 0.99, 0.95, 0.3, 1),
+        (128, 8, 0.99, 0.95, 0.02, 2),
+        (16, 33, 0.999, 0.95, 0.1, 3),
+        (64, 64, 0.99, 1.0, 0.05, 4),
+        (32, 17, 0.9, 0.0, 0.5, 5),
+        (7, 5, 0.99, 0.95, 1.0, 6),       # every step terminal
+        (256, 16, 0.997, 0.9, 0.001, 7),
+    ]
+    out = {}
+    for k, (T, N, g, lam, dp, seed) in enumerate(cases):
+        rs = np.random.RandomState(100 + seed)
+        st = R.buffer.RolloutStorage(T, N, Box((2,)), Discrete(3), gae_lam=lam, gamma=g)
+        rew = (rs.randn(T, N) * 2).astype(np.float32)
+        val = (rs.randn(T, N) * 3).astype(np.float32)
+        done = rs.rand(T, N) < dp
+        for t in range(T):
+            st.add(np.zeros((N, 2), np.float32), np.zeros((N, 1)), rew[t].copy(),
+                   torch.from_numpy(val[t].copy()), done[t], torch.zeros(N, 1))
+        last_v = (rs.randn(N) * 3).astype(np.float32)
+        last_done = done[-1]  # ppo.py:196 passes the dones of the last env step
+        st.compute_returns_and_advantages(torch.from_numpy(last_v), dones=last_done)
+        p = f"c{k}_"
+        out.update({p + "T": np.int64(T), p + "N": np.int64(N), p + "gamma": np.float64(g),
+                    p + "lam": np.float64(lam), p + "rewards": rew, p + "values": val,
+                    p + "dones": done, p + "last_value": last_v, p + "last_done": last_done,
+                    p + "advantages": st.advantages.copy(), p + "returns": st.returns.copy()})
+    out["ncases"] = np.int64(len(cases))
+    save("gae_single", **out)
+
+
+# --------------------------------------------------------------------------
+# (2) GAE, two streams: IntrinsicStorage (buffer.py:321-362)
+# --------------------------------------------------------------------------
+def gen_gae_dual(R):
+    import torch
+    R.logger.record = lambda *a, **k: None  # buffer.py:335 side effect not needed
+    cases = [(1, 1, 0.99, 0.99, 0.95, 0.0, 0), (9, 4, 0.99, 0.999, 0.95, 0.2, 1),
+             (128, 16, 0.99, 0.99, 0.95, 0.01, 2), (33, 7, 0.999, 0.9, 1.0, 0.1, 3),
+             (64, 32, 0.97, 0.995, 0.8, 0.05, 4)]
+    out = {}
+    for k, (T, N, g, ig, lam, dp, seed) in enumerate(cases):
+        rs = np.random.RandomState(200 + seed)
+        st = R.buffer.IntrinsicStorage(T, N, Box((2,)), Discrete(3), gae_lam=lam, gamma=g, int_gamma=ig)
+        st.reset()  # IntrinsicStorage.__init__ nulls its int arrays (buffer.py:285)
+        rew = (rs.randn(T, N)).astype(np.float32)
+        irew = np.abs(rs.randn(T, N)).astype(np.float32)
+        val = (rs.randn(T, N) * 2).astype(np.float32)
+        ival = (rs.randn(T, N)).astype(np.float32)
+        done = rs.rand(T, N) < dp
+        for t in range(T):
+            st.add(np.zeros((N, 2), np.float32), np.zeros((N, 1)), rew[t].copy(), irew[t].copy(),
+                   torch.from_numpy(val[t].copy()), torch.from_numpy(ival[t].copy()), done[t],
+                   torch.zeros(N, 1))
+        lv = rs.randn(N).astype(np.float32)
+        liv = rs.randn(N).astype(np.float32)
+        st.compute_returns_and_advantages(torch.from_numpy(lv), torch.from_numpy(liv), done[-1])
+        p = f"c{k}_"
+        out.update({p + "T": np.int64(T), p + "N": np.int64(N), p + "gamma": np.float64(g),
+                    p + "int_gamma": np.float64(ig), p + "lam": np.float64(lam),
+                    p + "rewards": rew, p + "int_rewards": irew, p + "values": val,
+                    p + "int_values": ival, p + "dones": done, p + "last_value": lv,
+                    p + "last_int_value": liv, p + "last_done": done[-1],
+                    p + "advantages": st.advantages.copy(), p + "returns": st.returns.copy(),
+                    p + "int_advantages": st.int_advantages.copy(),
+                    p + "int_returns": st.int_returns.copy()})
+    out["ncases"] = np.int64(len(cases))
+    save("gae_dual", **out)
+
+
+# --------------------------------------------------------------------------
+# (3) RunningMeanStd sequences (util.py:9-44) and normalize_obs (ppo.py:111-118)
+# --------------------------------------------------------------------------
+def gen_rms(R):
+    rs = np.random.RandomState(300)
+    out = {}
+    # a) feature vectors, float32 batches of varying size (obs_rms path, ppo.py:392)
+    rms = R.util.RunningMeanStd()
+    batches = [(rs.randn(n, 6) * 3 + 1).astype(np.float32) for n in (4, 1, 17, 64, 3)]
+    for i, b in enumerate(batches):
+        rms.update(b)
+        out[f"f32_b{i}"] = b
+        out[f"f32_mean{i}"] = np.asarray(rms.mean, np.float64)
+        out[f"f32_var{i}"] = np.asarray(rms.var, np.float64)
+        out[f"f32_count{i}"] = np.float64(rms.count)
+    out["f32_n"] = np.int64(len(batches))
+    # b) uint8 frames (Atari last frame, 84x84 flattened to 7056 features)
+    rms = R.util.RunningMeanStd()
+    frames = [rs.randint(0, 256, size=(n, 7056)).astype(np.uint8) for n in (8, 5)]
+    for i, b in enumerate(frames):
+        rms.update(b)
+        out[f"u8_b{i}"] = b
+        out[f"u8_mean{i}"] = np.asarray(rms.mean, np.float64)
+        out[f"u8_var{i}"] = np.asarray(rms.var, np.float64)
+        out[f"u8_count{i}"] = np.float64(rms.count)
+    out["u8_n"] = np.int64(len(frames))
+    # c) scalar stream (int_rew_rms, ppo.py:396): shape () state, (N,) batches
+    rms = R.util.RunningMeanStd()
+    for i in range(6):
+        b = np.abs(rs.randn(16)).astype(np.float32) * (i + 1)
+        rms.update(b)
+        out[f"sc_b{i}"] = b
+        out[f"sc_mean{i}"] = np.asarray(rms.mean, np.float64)
+        out[f"sc_var{i}"] = np.asarray(rms.var, np.float64)
+        out[f"sc_count{i}"] = np.float64(rms.count)
+    out["sc_n"] = np.int64(6)
+    # d) normalize_obs with the state from (a): BaseAlgorithm.normalize_obs
+    alg = types.SimpleNamespace(obs_rms=R.util.RunningMeanStd())
+    for b in batches:
+        alg.obs_rms.update(b)
+    x = (rs.randn(32, 6) * 10).astype(np.float32)
+    out["norm_in"] = x
+    out["norm_mean"] = np.asarray(alg.obs_rms.mean)
+    out["norm_var"] = np.asarray(alg.obs_rms.var)
+    out["norm_out"] = R.ppo.BaseAlgorithm.normalize_obs(alg, x)
+    save("rms", **out)
+
+
+# --------------------------------------------------------------------------
+# (4) get(): swap_and_flatten + np.random.permutation minibatching
+#     buffer.py:41-52, 137, 233-267 — including the construction-time randn
+# --------------------------------------------------------------------------
+def gen_get(R):
+    import torch
+    out = {}
+    for k, (T, N, D, B, E, seed) in enumerate([(8, 3, 2, 5, 3, 11), (4, 4, 3, None, 2, 12),
+                                               (16, 5, 1, 16, 2, 13)]):
+        np.random.seed(seed)
+        st = R.buffer.RolloutStorage(T, N, Box((D,)), Discrete(4))  # draws randn(16, D)
+        obs = np.arange(T * N * D, dtype=np.float32).reshape(T, N, D)
+        for t in range(T):
+            st.add(obs[t], np.full((N, 1), t), np.zeros(N, np.float32),
+                   torch.arange(N, dtype=torch.float32) + 100 * t, np.zeros(N, bool),
+                   torch.full((N, 1), float(t)))
+        st.compute_returns_and_advantages(torch.zeros(N), dones=np.zeros(N, bool))
+        p = f"c{k}_"
+        out[p + "cfg"] = np.array([T, N, D, -1 if B is None else B, E, seed], np.int64)
+        mb = 0
+        for e in range(E):
+            for batch in st.get(B):
+                out[p + f"obs{mb}"] = batch.observations.numpy()
+                out[p + f"act{mb}"] = batch.actions.numpy()
+                out[p + f"oldv{mb}"] = batch.old_values.numpy()
+                out[p + f"oldlp{mb}"] = batch.old_log_probs.numpy()
+                out[p + f"adv{mb}"] = batch.advantages.numpy()
+                out[p + f"ret{mb}"] = batch.returns.numpy()
+                mb += 1
+        out[p + "nmb"] = np.int64(mb)
+        out[p + "A"] = st.A.copy()
+    save("get_perm", **out)
+
+
+# --------------------------------------------------------------------------
+# (5) One full PPO.train() (ppo.py:200-259) on fixed weights: losses, dL/dlogits,
+#     dL/dvalues per minibatch, post-update weights.  Discrete and Box.
+# --------------------------------------------------------------------------
+def _record_logger(R):
+    rec = {}
+    R.logger.record = lambda k, v: rec.__setitem__(k, v)
+    R.logger.configure = lambda *a, **k: None
+    R.logger.dump = lambda *a, **k: None
+    return rec
+
+
+def _net_grad_hooks(net, store):
+    def fwd_hook(mod, inp, outp):
+        outs = outp if isinstance(outp, tuple) else (outp,)
+        store["inputs"].append(inp[0].detach().clone())
+        grads = []
+        store["grads"].append(grads)
+        for o in outs:
+            if o.requires_grad:
+                o.register_hook(lambda g, grads=grads: grads.append(g.detach().clone()))
+    return net.register_forward_hook(fwd_hook)
+
+
+def gen_train(R):
+    import torch
+    out = {}
+    cases = [  # name, action_space, obs_dim, n_envs, nstep, batch, epochs, hidden, seed, kwargs
+        ("disc2", Discrete(2), 4, 4, 16, 16, 2, 32, 21, {}),
+        ("disc4sat", Discrete(4), 5, 3, 8, 12, 1, 16, 22, {"sat": True}),
+        ("box2", Box((2,)), 3, 4, 8, 8, 2, 16, 23, {}),
+        ("disc18", Discrete(18), 6, 2, 12, 24, 1, 16, 24, {}),
+    ]
+    for name, aspace, D, N, T, B, E, H, seed, kw in cases:
+        rec = _record_logger(R)
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+        env = make_fakevec(R.VecEnv, N, D, aspace, seed=1000 + seed)
+        R.ppo.make_env = lambda env_id, n_envs=4, env=env: env
+        alg = R.ppo.PPO(env_id="Fake-v0", nstep=T, batch_size=B, n_epochs=E, hidden_size=H,
+                        max_grad_norm=0.5, ent_coef=0.01, vf_coef=1.0)
+        if kw.get("sat"):
+            with torch.no_grad():  # push the actor into softmax saturation (eps clamp)
+                alg.policy.net.actor[-1].weight.mul_(60.0)
+        init = {k: v.detach().clone().numpy() for k, v in alg.policy.net.state_dict().items()}
+        alg.collect_samples()
+        st = alg.rollout
+        store = {"inputs": [], "grads": []}
+        h = _net_grad_hooks(alg.policy.net, store)
+        # capture per-minibatch batches too (the inputs of train's loss)
+        batches = []
+        orig_get = st.get
+
+        def get_rec(bs, orig_get=orig_get):
+            for b in orig_get(bs):
+                batches.append(b)
+                yield b
+        st.get = get_rec
+        if aspace.__class__.__name__ == "Box":
+            # Box path goes through forward_continuous, not forward: hook the actor/critic
+            h.remove()
+            store = {"inputs": [], "grads": []}
+            hs = []
+            for sub in (alg.policy.net.actor, alg.policy.net.critic):
+                hs.append(_net_grad_hooks(sub, store))
+        alg.train()
+        p = name + "_"
+        out[p + "cfg"] = np.array([D, N, T, B, E, H, seed, aspace.n if hasattr(aspace, "n") else -aspace.shape[0]],
+                                  np.int64)
+        for k, v in init.items():
+            out[p + "w0_" + k] = v
+        for k, v in alg.policy.net.state_dict().items():
+            out[p + "w1_" + k] = v.detach().numpy()
+        tr = env.trace
+        out[p + "env_obs"] = np.stack(tr["obs"])
+        out[p + "env_rew"] = np.stack(tr["rew"])
+        out[p + "env_done"] = np.stack(tr["done"])
+        # rollout after collect (before get() flattened it we cannot see it; use batches)
+        for i, b in enumerate(batches):
+            for f in b._fields:
+                out[p + f"mb{i}_{f}"] = getattr(b, f).numpy()
+        for i, gs in enumerate(store["grads"]):
+            for j, g in enumerate(gs):
+                out[p + f"mb{i}_grad{j}"] = g.numpy()
+        out[p + "nmb"] = np.int64(len(batches))
+        for k in ("train/entropy_loss", "train/policy_gradient_loss", "train/value_loss", "train/total_loss"):
+            out[p + k.split("/")[1]] = np.float64(rec[k])
+    save("train_ppo", **out)
+
+
+# --------------------------------------------------------------------------
+# (6) PPO_RND: collect (warm-up + normalize_obs + rnd.int_reward + int_rew_rms
+#     scaling, ppo.py:367-407) and train (ppo.py:409-502, incl. randn<0.25 gate)
+# --------------------------------------------------------------------------
+def gen_rnd(R):
+    import torch
+    out = {}
+    rec = _record_logger(R)
+    R.buffer.logger.record = R.logger.record
+    D, N, T, B, E, H, IH, seed = 5, 4, 8, 16, 2, 16, 16, 31
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    env = make_fakevec(R.VecEnv, N, D, Discrete(3), seed=2000 + seed)
+    R.ppo.make_env = lambda env_id, n_envs=4: env
+    alg = R.ppo.PPO_RND(env_id="Fake-v0", nstep=T, batch_size=B, n_epochs=E, hidden_size=H,
+                        int_hidden_size=IH, rnd_start=3, max_grad_norm=0.5)
+    init = {k: v.detach().clone().numpy() for k, v in alg.policy.net.state_dict().items()}
+    rinit = {k: v.detach().clone().numpy() for k, v in alg.rnd.state_dict().items()}
+    alg.collect_samples()  # first iteration: 2 warm-up steps then RND
+    it1 = {"int_rewards": alg.rollout.int_rewards.copy(), "rewards": alg.rollout.rewards.copy(),
+           "int_values": alg.rollout.int_values.copy(), "values": alg.rollout.values.copy(),
+           "adv": alg.rollout.advantages.copy(), "iadv": alg.rollout.int_advantages.copy(),
+           "obs_mean": np.asarray(alg.obs_rms.mean), "obs_var": np.asarray(alg.obs_rms.var),
+           "obs_count": np.float64(alg.obs_rms.count), "ir_mean": np.asarray(alg.int_rew_rms.mean),
+           "ir_var": np.asarray(alg.int_rew_rms.var), "ir_count": np.float64(alg.int_rew_rms.count)}
+    alg.train()
+    p = "rnd_"
+    out[p + "cfg"] = np.array([D, N, T, B, E, H, IH, seed, 3], np.int64)
+    for k, v in init.items():
+        out[p + "w0_" + k] = v
+    for k, v in rinit.items():
+        out[p + "r0_" + k] = v
+    for k, v in alg.policy.net.state_dict().items():
+        out[p + "w1_" + k] = v.detach().numpy()
+    for k, v in alg.rnd.state_dict().items():
+        out[p + "r1_" + k] = v.detach().numpy()
+    for k, v in it1.items():
+        out[p + "it1_" + k] = v
+    tr = env.trace
+    out[p + "env_obs"] = np.stack(tr["obs"])
+    out[p + "env_rew"] = np.stack(tr["rew"])
+    out[p + "env_done"] = np.stack(tr["done"])
+    for k in ("train/intrinsic_loss", "train/entropy_loss", "train/policy_gradient_loss",
+              "train/value_loss", "train/total_loss"):
+        out[p + k.split("/")[1]] = np.float64(rec[k])
+    out[p + "mean_int_reward"] = np.float64(rec["rollout/mean_int_reward"])
+    out[p + "np_state_after"] = np.random.get_state()[1].copy()
+    save("train_rnd", **out)
+
+
+# --------------------------------------------------------------------------
+# (7) PPO_ICM: collect (int reward mix, ppo.py:603-649) + train (ppo.py:651-713)
+# --------------------------------------------------------------------------
+def gen_icm(R):
+    import torch
+    out = {}
+    for name, aspace in (("icm_disc", Discrete(3)), ("icm_box", Box((2,)))):
+        rec = _record_logger(R)
+        D, N, T, B, E, H, IH, seed = 4, 3, 8, 12, 2, 16, 8, 41
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+        env = make_fakevec(R.VecEnv, N, D, aspace, seed=3000 + seed)
+        R.ppo.make_env = lambda env_id, n_envs=4, env=env: env
+        alg = R.ppo.PPO_ICM(env_id="Fake-v0", nstep=T, batch_size=B, n_epochs=E, hidden_size=H,
+                            int_hidden_size=IH, max_grad_norm=0.5, int_rew_integration=0.1)
+        init = {k: v.detach().clone().numpy() for k, v in alg.policy.net.state_dict().items()}
+        iinit = {k: v.detach().clone().numpy() for k, v in alg.intrinsic_module.state_dict().items()}
+        alg.collect_samples()
+        roll = {"rewards": alg.rollout.rewards.copy(), "adv": alg.rollout.advantages.copy(),
+                "actions": alg.rollout.actions.copy()}
+        alg.train()
+        p = name + "_"
+        out[p + "cfg"] = np.array([D, N, T, B, E, H, IH, seed], np.int64)
+        for k, v in init.items():
+            out[p + "w0_" + k] = v
+        for k, v in iinit.items():
+            out[p + "i0_" + k] = v
+        for k, v in alg.policy.net.state_dict().items():
+            out[p + "w1_" + k] = v.detach().numpy()
+        for k, v in alg.intrinsic_module.state_dict().items():
+            out[p + "i1_" + k] = v.detach().numpy()
+        for k, v in roll.items():
+            out[p + "roll_" + k] = v
+        tr = env.trace
+        out[p + "env_obs"] = np.stack(tr["obs"])
+        out[p + "env_rew"] = np.stack(tr["rew"])
+        out[p + "env_done"] = np.stack(tr["done"])
+        for k in ("train/entropy_loss", "train/policy_gradient_loss", "train/value_loss",
+                  "train/total_loss", "train/icm_loss", "rollout/mean_int_reward"):
+            out[p + k.split("/")[1]] = np.float64(rec[k])
+    save("train_icm", **out)
+
+
+# --------------------------------------------------------------------------
+# (8) NatureCNN actor-critic architecture (.ipynb_checkpoints/models-checkpoint.py:48-90)
+# --------------------------------------------------------------------------
+def gen_cnn(R):
+    import torch
+    spec = importlib.util.spec_from_file_location(
+        "models_checkpoint", os.path.join(REF, ".ipynb_checkpoints", "models-checkpoint.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    torch.manual_seed(51)
+    net = mod.CnnActorCritic(4, 4)
+    rs = np.random.RandomState(52)
+    x = rs.randint(0, 256, size=(3, 4, 84, 84)).astype(np.uint8)
+    with torch.no_grad():
+        logits, value = net(torch.from_numpy(x.astype(np.float32)))
+    out = {"x": x, "logits": logits.numpy(), "value": value.numpy()}
+    # weights are NOT stored (7.8 MB): the oracle re-creates them from the same
+    # torch seed + module order; per-tensor checksums pin that init.
+    for k, v in net.state_dict().items():
+        out["wsum_" + k] = np.float64(v.double().sum())
+        out["wabs_" + k] = np.float64(v.double().abs().sum())
+        out["whead_" + k] = v.flatten()[:16].numpy()
+    out["param_count"] = np.int64(sum(p.numel() for p in net.parameters()))
+    save("cnn", **out)
+
+
+def main():
+    if not os.path.isdir(REF):
+        print("reference not present; fixtures are committed — nothing to do")
+        return 0
+    R = import_reference()
+    gen_gae(R)
+    gen_gae_dual(R)
+    gen_rms(R)
+    gen_get(R)
+    gen_train(R)
+    gen_rnd(R)
+    gen_icm(R)
+    gen_cnn(R)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

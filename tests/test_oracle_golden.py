@@ -1,0 +1,169 @@
+"""Pin the CPU oracle against golden vectors produced by running the reference
+(tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gae as G
+from oracle import rms as RM
+from oracle import models as M
+from oracle.algos import OraclePPO, OracleRND, OracleICM
+from oracle.storage import Rollout
+from replay_env import ReplayVecEnv, space_from_code, Box, Discrete
+
+
+def _cases(f):
+    return [f"c{k}_" for k in range(int(f["ncases"]))]
+
+
+def test_gae_single_bitexact(golden):
+    f = golden("gae_single")
+    for p in _cases(f):
+        adv, ret = G.gae_single(f[p + "rewards"], f[p + "values"], f[p + "dones"], f[p + "last_value"],
+                                f[p + "last_done"], float(f[p + "gamma"]), float(f[p + "lam"]))
+        assert np.array_equal(adv, f[p + "advantages"]), p
+        assert np.array_equal(ret, f[p + "returns"]), p
+
+
+def test_gae_dual_bitexact(golden):
+    f = golden("gae_dual")
+    for p in _cases(f):
+        a, r, ia, ir = G.gae_dual(f[p + "rewards"], f[p + "int_rewards"], f[p + "values"],
+                                  f[p + "int_values"], f[p + "dones"], f[p + "last_value"],
+                                  f[p + "last_int_value"], f[p + "last_done"], float(f[p + "gamma"]),
+                                  float(f[p + "int_gamma"]), float(f[p + "lam"]))
+        for got, key in ((a, "advantages"), (r, "returns"), (ia, "int_advantages"), (ir, "int_returns")):
+            assert np.array_equal(got, f[p + key]), (p, key)
+
+
+@pytest.mark.parametrize("kind", ["f32", "u8", "sc"])
+def test_running_moments(golden, kind):
+    f = golden("rms")
+    rm = RM.RunningMoments()
+    for i in range(int(f[kind + "_n"])):
+        rm.update(f[f"{kind}_b{i}"])
+        np.testing.assert_array_equal(rm.mean, f[f"{kind}_mean{i}"])
+        np.testing.assert_array_equal(rm.var, f[f"{kind}_var{i}"])
+        assert rm.count == f[f"{kind}_count{i}"]
+
+
+def test_normalize_obs(golden):
+    f = golden("rms")
+    out = RM.normalize_obs(f["norm_in"], f["norm_mean"], f["norm_var"])
+    assert out.dtype == np.float64
+    np.testing.assert_array_equal(out, f["norm_out"])
+
+
+def test_minibatch_permutation_bitexact(golden):
+    f = golden("get_perm")
+    for k in range(3):
+        p = f"c{k}_"
+        T, N, D, B, E, seed = (int(x) for x in f[p + "cfg"])
+        B = None if B < 0 else B
+        np.random.seed(seed)
+        st = Rollout(T, N, (D,), 1)
+        np.testing.assert_array_equal(st.hash_matrix, f[p + "A"])
+        obs = np.arange(T * N * D, dtype=np.float32).reshape(T, N, D)
+        for t in range(T):
+            st.add(obs[t], np.full((N, 1), t), np.zeros(N, np.float32),
+                   np.arange(N, dtype=np.float32) + 100 * t, np.zeros(N, bool), np.full((N, 1), float(t)))
+        st.finish(np.zeros(N, np.float32), np.zeros(N, bool))
+        mb = 0
+        for _ in range(E):
+            for _idx, b in st.minibatches(B):
+                np.testing.assert_array_equal(b["observations"], f[p + f"obs{mb}"])
+                np.testing.assert_array_equal(b["actions"], f[p + f"act{mb}"])
+                np.testing.assert_array_equal(b["old_values"], f[p + f"oldv{mb}"])
+                np.testing.assert_array_equal(b["old_log_probs"], f[p + f"oldlp{mb}"])
+                np.testing.assert_array_equal(b["advantages"], f[p + f"adv{mb}"])
+                np.testing.assert_array_equal(b["returns"], f[p + f"ret{mb}"])
+                mb += 1
+        assert mb == int(f[p + "nmb"])
+
+
+def _state_close(sd, f, prefix, rtol=1e-5, atol=1e-6):
+    for k, v in sd.items():
+        np.testing.assert_allclose(v.detach().numpy(), f[prefix + k], rtol=rtol, atol=atol, err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["disc2", "disc4sat", "box2", "disc18"])
+def test_ppo_train_iteration(golden, name):
+    """Full collect + GAE + train() replayed against the reference's run."""
+    f = golden("train_ppo")
+    p = name + "_"
+    D, N, T, B, E, H, seed, code = (int(x) for x in f[p + "cfg"])
+    env = ReplayVecEnv(f[p + "env_obs"], f[p + "env_rew"], f[p + "env_done"], space_from_code(code))
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    alg = OraclePPO(env, nstep=T, batch_size=B, n_epochs=E, hidden_size=H, max_grad_norm=0.5,
+                    ent_coef=0.01, vf_coef=1.0)
+    if name == "disc4sat":
+        with torch.no_grad():
+            alg.net.actor[-1].weight.mul_(60.0)
+    _state_close(alg.net.state_dict(), f, p + "w0_", rtol=0, atol=0)
+    alg.collect()
+    alg.train()
+    _state_close(alg.net.state_dict(), f, p + "w1_")
+    np.testing.assert_allclose(alg.stats["loss"], f[p + "total_loss"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(alg.stats["pl"], f[p + "policy_gradient_loss"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(alg.stats["vl"], f[p + "value_loss"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(alg.stats["el"], f[p + "entropy_loss"], rtol=1e-5, atol=1e-7)
+
+
+def test_rnd_iteration(golden):
+    f = golden("train_rnd")
+    p = "rnd_"
+    D, N, T, B, E, H, IH, seed, rnd_start = (int(x) for x in f[p + "cfg"])
+    env = ReplayVecEnv(f[p + "env_obs"], f[p + "env_rew"], f[p + "env_done"], Discrete(3))
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    alg = OracleRND(env, nstep=T, batch_size=B, n_epochs=E, hidden_size=H, int_hidden_size=IH,
+                    rnd_start=rnd_start, max_grad_norm=0.5)
+    _state_close(alg.net.state_dict(), f, p + "w0_", rtol=0, atol=0)
+    _state_close(alg.rnd.state_dict(), f, p + "r0_", rtol=0, atol=0)
+    alg.collect()
+    np.testing.assert_allclose(alg.rollout.int_rewards, f[p + "it1_int_rewards"], rtol=1e-6)
+    np.testing.assert_array_equal(alg.obs_rms.mean, f[p + "it1_obs_mean"])
+    np.testing.assert_allclose(alg.int_rew_rms.var, f[p + "it1_ir_var"], rtol=1e-6)
+    np.testing.assert_allclose(alg.rollout.iadv, f[p + "it1_iadv"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(alg.mean_int_reward, f[p + "mean_int_reward"], rtol=1e-6)
+    alg.train()
+    _state_close(alg.net.state_dict(), f, p + "w1_")
+    _state_close(alg.rnd.state_dict(), f, p + "r1_", rtol=1e-4, atol=1e-5)
+    np.testing.assert_array_equal(np.random.get_state()[1], f[p + "np_state_after"])
+    np.testing.assert_allclose(alg.stats["ivl"], f[p + "intrinsic_loss"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(alg.stats["loss"], f[p + "total_loss"], rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("name,space", [("icm_disc", Discrete(3)), ("icm_box", Box((2,)))])
+def test_icm_iteration(golden, name, space):
+    f = golden("train_icm")
+    p = name + "_"
+    D, N, T, B, E, H, IH, seed = (int(x) for x in f[p + "cfg"])
+    env = ReplayVecEnv(f[p + "env_obs"], f[p + "env_rew"], f[p + "env_done"], space)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    alg = OracleICM(env, nstep=T, batch_size=B, n_epochs=E, hidden_size=H, int_hidden_size=IH,
+                    max_grad_norm=0.5, int_rew_integration=0.1)
+    _state_close(alg.icm.state_dict(), f, p + "i0_", rtol=0, atol=0)
+    alg.collect()
+    np.testing.assert_allclose(alg.rollout.rewards, f[p + "roll_rewards"], rtol=1e-6, atol=1e-7)
+    alg.train()
+    _state_close(alg.net.state_dict(), f, p + "w1_")
+    _state_close(alg.icm.state_dict(), f, p + "i1_")
+    np.testing.assert_allclose(alg.stats["icm"], f[p + "icm_loss"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(alg.stats["loss"], f[p + "total_loss"], rtol=1e-5, atol=1e-7)
+
+
+def test_nature_cnn_architecture(golden):
+    f = golden("cnn")
+    torch.manual_seed(51)
+    net = M.NatureCNN(4, 4)
+    assert sum(p.numel() for p in net.parameters()) == int(f["param_count"]) == 1949349
+    for k, v in net.state_dict().items():
+        np.testing.assert_array_equal(v.flatten()[:16].numpy(), f["whead_" + k])
+        np.testing.assert_allclose(float(v.double().sum()), float(f["wsum_" + k]), rtol=1e-12, atol=1e-9)
+    with torch.no_grad():
+        logits, _, value, _ = net.heads(torch.from_numpy(f["x"].astype(np.float32)))
+    np.testing.assert_allclose(logits.numpy(), f["logits"], rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(value.numpy(), f["value"], rtol=1e-5, atol=1e-4)
