@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of one PPO iteration (collect + GAE + PPO update) on the
+BASELINE.json workload, 4096 envs x 128 steps, synthetic Breakout-shaped
+(4x84x84 uint8) envs on the device, NatureCNN actor-critic, fp32.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+             --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+A "step" is one full PPO iteration over the 4096 x 128 rollout.  The total env
+count is fixed as N grows (strong scaling): rank g steps envs [g*4096/N, ...).
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ppo-exploration_amd"))
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (= f32 vector) dense peak
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--algo", default="ppo", choices=["ppo", "rnd", "icm"])
+    p.add_argument("--envs", type=int, default=4096)
+    p.add_argument("--nstep", type=int, default=128)
+    p.add_argument("--epochs", type=int, default=10)
+    p.add_argument("--batch-size", type=int, default=16384)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=0)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as tdist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+
+    import native
+    import ppo
+    import logger
+
+    env_id = {"ppo": "BreakoutNoFrameskip-v4", "icm": "BreakoutNoFrameskip-v4",
+              "rnd": "MontezumaRevengeNoFrameskip-v4"}[args.algo]
+    cls = {"ppo": ppo.PPO, "icm": ppo.PPO_ICM, "rnd": ppo.PPO_RND}[args.algo]
+    np.random.seed(0)
+    torch.manual_seed(0)
+    kw = dict(rnd_start=0) if args.algo == "rnd" else {}
+    alg = cls(env_id=env_id, n_envs=args.envs, nstep=args.nstep, batch_size=args.batch_size,
+              n_epochs=args.epochs, seed=1234, quiet=True, **kw)
+    logger.configure("bench", env_id, quiet=True)
+
+    def iteration():
+        alg.collect_samples()
+        alg.train()
+
+    for _ in range(args.warmup):
+        iteration()
+
+    # event timing of the roofline kernel on the stream it is launched on
+    prof_kernel = "ppox_gae" if args.algo != "rnd" else "ppox_gae_dual"
+    native.enable_event_timing([prof_kernel])
+
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        iteration()
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    dt = time.perf_counter() - t0
+    kt = native.event_times_ms(prof_kernel)
+    native.enable_event_timing([])
+    if world > 1:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    env_steps = args.steps * args.envs * args.nstep
+    value = env_steps / dt
+    out = {
+        "metric": "env-steps/sec (collect+GAE+PPO update), 4096 envs×128 steps @ 1/2/4/8 GPU",
+        "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (Philox uint8 4x84x84 frames, Bernoulli rewards/dones, device envs)",
+        "config": {"workload": f"{env_id} {args.algo.upper()} NatureCNN {args.envs} envs x {args.nstep} steps",
+                   "n_envs": args.envs, "n_steps": args.nstep, "n_epochs": args.epochs,
+                   "batch_size": args.batch_size, "minibatches_per_epoch": -(-args.envs * args.nstep // args.batch_size),
+                   "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)" if world > 1 else "single GPU"},
+    }
+    # roofline of the profiled kernel: ALGORITHMIC bytes per launch / mean launch duration
+    if kt:
+        n_local = args.envs // world
+        bytes_per_elem = 17 if prof_kernel == "ppox_gae" else 33
+        alg_bytes = bytes_per_elem * args.nstep * n_local
+        mean_ms = float(np.mean(kt))
+        ach = alg_bytes / (mean_ms * 1e-3) / 1e9
+        out["roofline"] = {"kernel": prof_kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                           "launches": len(kt), "mean_us": round(mean_ms * 1e3, 2),
+                           "alg_bytes_per_launch": alg_bytes}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        from oracle.baseline import atari_ppo_rate
+        out["cpu_baseline"] = atari_ppo_rate(args.envs, args.nstep, args.epochs, args.batch_size,
+                                             threads=args.cpu_threads or None)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

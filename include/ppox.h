@@ -1,0 +1,191 @@
+/*
+ * ppox.h — C ABI of libppox.so, the MI355X (gfx950) hot path of the PPO +
+ * exploration training loop (BoogaQ/PPO-exploration drop-in).
+ *
+ * Conventions (every entry point):
+ *   - plain pointers + sizes; every array pointer is a DEVICE pointer unless
+ *     the parameter name ends in _host;
+ *   - `stream` is a hipStream_t passed as void* (NULL = legacy default stream);
+ *     the call only enqueues work on it: no allocation, no host sync, so every
+ *     entry point is hipGraph-capturable;
+ *   - return 0 on success, PPOX_EINVAL on a rejected argument, or
+ *     -(hipError_t) when a launch fails; ppox_last_error() describes the most
+ *     recent failure on the calling thread;
+ *   - the library never allocates; scratch comes from caller workspaces.
+ *
+ * Rollout arrays are STEP-MAJOR, element (t, n) at t*N + n, exactly the
+ * reference's (buffer_size, n_envs) layout (buffer.py:153-161).  Minibatch
+ * indices are the reference's ENV-MAJOR flat indices i = n*T + t
+ * (swap_and_flatten, buffer.py:41-52); kernels map i -> (t = i % T, n = i / T)
+ * so the rollout is never physically flattened.
+ *
+ * The reference has no FFI: each function below replaces a Python/numpy/torch
+ * site, cited as file:line relative to the reference repository.
+ */
+#ifndef PPOX_H
+#define PPOX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PPOX_OK 0
+#define PPOX_EINVAL (-1000)
+
+/* Library identification and error reporting. */
+const char* ppox_version(void);
+const char* ppox_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * K1  GAE(lambda) backward scan.
+ * Replaces RolloutStorage.compute_returns_and_advantages (buffer.py:203-230).
+ *   rewards, values : (T, N) f32        dones : (T, N) u8 — done flag stored by
+ *   add() at step t (the reference's `masks`, ppo.py:192)
+ *   last_value : (N,) f32 — V(s_{T-1}) as passed by ppo.py:196
+ *   last_done  : (N,) u8  — dones of the last env step (ppo.py:196)
+ * Output advantages/returns (T, N) f32 are BIT-IDENTICAL to the reference:
+ * f32 gamma*next_value, float64 carry, returns = adv + values in f32.
+ * -------------------------------------------------------------------------*/
+int ppox_gae(const float* rewards, const float* values, const uint8_t* dones,
+             const float* last_value, const uint8_t* last_done, int64_t T, int64_t N,
+             double gamma, double lam, float* advantages, float* returns, void* stream);
+
+/* Two reward streams.  Replaces IntrinsicStorage.compute_returns_and_advantages
+ * (buffer.py:321-362): extrinsic stream as ppox_gae; intrinsic stream is
+ * non-episodic (no done mask) and computed in f32 with f32(int_gamma*lam). */
+int ppox_gae_dual(const float* rewards, const float* values, const uint8_t* dones,
+                  const float* last_value, const uint8_t* last_done,
+                  const float* int_rewards, const float* int_values, const float* last_int_value,
+                  int64_t T, int64_t N, double gamma, double int_gamma, double lam,
+                  float* advantages, float* returns, float* int_advantages, float* int_returns,
+                  void* stream);
+
+
+/* ---------------------------------------------------------------------------
+ * K2/K3  Running moments and observation normalisation.
+ * Replace RunningMeanStd.update/update_from_moments (util.py:20-44) and
+ * BaseAlgorithm.normalize_obs (ppo.py:111-118).  State (mean, var: float64
+ * per feature) lives on the device; `count` is the host-side float the
+ * reference keeps in Python (util.py:18), passed by value (the caller adds
+ * `rows` to it afterwards, exactly like util.py:40-44).
+ * -------------------------------------------------------------------------*/
+/* u8 batch (rows, cols) with row stride (bytes): exact integer column sums;
+ * optional batch_mean/batch_var outputs (nullable); mean/var nullable together
+ * (moments only).  Workspace: ppox_rms_u8_workspace_bytes(rows, cols). */
+int64_t ppox_rms_u8_workspace_bytes(int64_t rows, int64_t cols);
+int ppox_rms_update_u8(const uint8_t* x, int64_t rows, int64_t cols, int64_t row_stride,
+                       double* mean, double* var, double count, void* workspace,
+                       int64_t workspace_bytes, double* batch_mean, double* batch_var, void* stream);
+/* f32 batch: numpy's own summation order (bit-identical batch moments). */
+int ppox_rms_update_f32(const float* x, int64_t rows, int64_t cols, int64_t row_stride,
+                        double* mean, double* var, double count, void* stream);
+/* int_rew_rms.update(r); r /= sqrt(var) + 1e-8  (ppo.py:396-398), in place on (n,) f32. */
+int ppox_rms_scale_int_rewards(float* int_rewards, int64_t n, double* mean, double* var,
+                               double count, void* stream);
+/* out (rows, cols) f32 = f32(clip((x - mean) / sqrt(var + 1e-10), -5, 5)) computed in f64. */
+int ppox_normalize_obs_u8(const uint8_t* x, int64_t rows, int64_t cols, int64_t row_stride,
+                          const double* mean, const double* var, float* out, void* stream);
+int ppox_normalize_obs_f32(const float* x, int64_t rows, int64_t cols, int64_t row_stride,
+                           const double* mean, const double* var, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K4  Fused PPO minibatch loss (ppo.py:216-238; RND ppo.py:428-460; ICM policy
+ * part ppo.py:668-692) and the collect-time categorical head (models.py:30-41).
+ * Minibatch rows come from the network outputs (logits (B, A), values (B,),
+ * int_values (B,) or NULL for one stream) and from the rollout through the
+ * env-major indices idx (B,) — never a gathered copy of the scalar fields.
+ * adv_stats (device, [4] f64): mean, unbiased std of the minibatch advantages
+ * (and of the intrinsic ones) — see ppox_minibatch_adv_stats.
+ * -------------------------------------------------------------------------*/
+#define PPOX_LOSS_PARTIALS 64
+/* Per-minibatch advantage mean / unbiased std (ppo.py:219) for every slice
+ * [k*batch, (k+1)*batch) of the epoch permutation; stats_out [n_mb][4]. */
+int ppox_minibatch_adv_stats(const float* advantages, const float* int_advantages,
+                             const int64_t* perm, int64_t total, int64_t batch_size,
+                             int64_t T, int64_t N, double* stats_out, void* stream);
+/* Forward partial sums -> partials [PPOX_LOSS_PARTIALS][8] f64 (sum-reducible
+ * across data-parallel ranks). */
+int ppox_ppo_loss_partials(const float* logits, const float* values, const float* int_values,
+                           int64_t B, int32_t A, const int64_t* idx, int64_t T, int64_t N,
+                           const int32_t* actions, const float* old_logp, const float* old_values,
+                           const float* advantages, const float* returns,
+                           const float* old_int_values, const float* int_advantages,
+                           const float* int_returns, const double* adv_stats, float clip,
+                           double* partials, void* stream);
+/* Backward: dL/dlogits (B, A), dL/dvalues (B,), dL/dint_values (B,) for the loss
+ * scale * (policy + ent_coef*entropy + vf_coef*value [+ int_vf_coef*int_value]),
+ * means taken over B_global rows.  loss_accum (nullable, [8] f64) += this
+ * minibatch's [policy, value, entropy, total, int_value, 1]. */
+int ppox_ppo_loss_backward(const float* logits, const float* values, const float* int_values,
+                           int64_t B, int32_t A, const int64_t* idx, int64_t T, int64_t N,
+                           const int32_t* actions, const float* old_logp, const float* old_values,
+                           const float* advantages, const float* returns,
+                           const float* old_int_values, const float* int_advantages,
+                           const float* int_returns, const double* adv_stats, float clip,
+                           const double* partials, int64_t B_global, float ent_coef,
+                           float vf_coef, float int_vf_coef, float scale, float* dlogits,
+                           float* dvalues, float* dint_values, double* loss_accum, void* stream);
+/* a ~ Categorical(probs=softmax(logits)) (Philox, counter-based), log_prob(a). */
+int ppox_categorical_sample(const float* logits, int64_t N, int32_t A, int64_t env_offset,
+                            uint64_t seed, int64_t counter, int32_t* actions, float* log_probs,
+                            void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K5  Minibatch gather (buffer.py:41-52, 256-267): dst[r] = rollout row of the
+ * env-major index idx[r]; rows of row_bytes at src_row_stride (step-major).
+ * -------------------------------------------------------------------------*/
+int ppox_gather_rows(const void* src, int64_t T, int64_t N, int64_t row_bytes,
+                     int64_t src_row_stride, const int64_t* idx, int64_t nrows, void* dst,
+                     void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Optimiser over flat buffers: clip_grad_norm_ + Adam.step (ppo.py:241-244).
+ * ppox_grad_sumsq writes PPOX_NORM_PARTIALS f64 partial sums of g^2 (caller may
+ * sum-reduce them across ranks only if grads are NOT yet all-reduced — normally
+ * they are, and the partials are used as-is).
+ * -------------------------------------------------------------------------*/
+#define PPOX_NORM_PARTIALS 256
+int ppox_grad_sumsq(const float* grads, int64_t n, double* partials, void* stream);
+int ppox_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                   const double* norm_partials, float max_norm, double lr, double beta1,
+                   double beta2, double eps, int64_t step, float* total_norm_out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Synthetic device environments (replace SB3 SubprocVecEnv + gym/ALE, env.py:7-12).
+ * Philox4x32-10 keyed by seed, counter (block, env_offset + n, step, action).
+ * -------------------------------------------------------------------------*/
+int ppox_atari_env_reset(uint8_t* obs, int64_t N, int64_t env_offset, uint64_t seed,
+                         float* ep_ret, int32_t* ep_len, void* stream);
+int ppox_atari_env_step(const uint8_t* obs_in, uint8_t* obs_out, const int32_t* actions,
+                        int64_t N, int64_t env_offset, uint64_t seed, int64_t step,
+                        float p_reward, float p_done, float* rewards, uint8_t* dones,
+                        float* ep_ret, int32_t* ep_len, float* done_ret, int32_t* done_len,
+                        void* stream);
+int ppox_vec_env_reset(float* obs, int64_t N, int32_t D, int64_t env_offset, uint64_t seed,
+                       float* ep_ret, int32_t* ep_len, void* stream);
+int ppox_vec_env_step(float* obs, const int32_t* actions, int64_t N, int32_t D,
+                      int64_t env_offset, uint64_t seed, int64_t step, float p_done,
+                      int32_t max_len, float* rewards, uint8_t* dones, float* ep_ret,
+                      int32_t* ep_len, float* done_ret, int32_t* done_len, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * K6  NatureCNN convolutions (checkpoint models-checkpoint.py:52-58) as fp32
+ * MFMA implicit GEMMs with fused bias + ReLU.
+ *   layer 1: x = uint8 frames (batch, 4, 84, 84) [or rollout rows through idx:
+ *            sample b = step-major row (idx[b] % T, idx[b] / T) of a (T, N_env, ...)
+ *            array] -> y (batch, 20, 20, 32) f32 NHWC
+ *   layer 2: x (batch, 20, 20, 32) NHWC -> y (batch, 9, 9, 64) NHWC
+ *   layer 3: x (batch, 9, 9, 64) NHWC -> y (batch, 64, 7, 7) NCHW (Flatten order)
+ * wp = weights packed by ppox_nature_pack_weights (PyTorch [co][ci][ky][kx] in). */
+int ppox_nature_pack_weights(const float* w1, const float* w2, const float* w3, float* wp1,
+                             float* wp2, float* wp3, void* stream);
+int ppox_nature_conv_fwd(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
+                         int64_t T, int64_t N_env, int64_t x_sample_stride, const float* wp,
+                         const float* bias, float* y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPOX_H */

@@ -1,0 +1,47 @@
+// Internal helpers shared by the libppox translation units (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/ppox.h"
+
+namespace ppox {
+
+void set_error(const char* fmt, ...);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+inline unsigned ceil_div(long long a, long long b) { return static_cast<unsigned>((a + b - 1) / b); }
+
+}  // namespace ppox
+
+#define PPOX_REQUIRE(cond, ...)                    \
+    do {                                           \
+        if (!(cond)) {                             \
+            ::ppox::set_error(__VA_ARGS__);        \
+            return PPOX_EINVAL;                    \
+        }                                          \
+    } while (0)
+
+#define PPOX_LAUNCHED(name)                                                         \
+    do {                                                                            \
+        hipError_t e_ = hipGetLastError();                                          \
+        if (e_ != hipSuccess) {                                                     \
+            ::ppox::set_error("%s: launch failed: %s", name, hipGetErrorString(e_)); \
+            return -static_cast<int>(e_);                                           \
+        }                                                                           \
+        return PPOX_OK;                                                             \
+    } while (0)
+
+#define PPOX_HIP(call, name)                                                         \
+    do {                                                                             \
+        hipError_t e_ = (call);                                                      \
+        if (e_ != hipSuccess) {                                                      \
+            ::ppox::set_error("%s: %s failed: %s", name, #call, hipGetErrorString(e_)); \
+            return -static_cast<int>(e_);                                            \
+        }                                                                            \
+    } while (0)

@@ -1,0 +1,121 @@
+// Optimiser step over the FLAT parameter/gradient buffers:
+//   clip_grad_norm_(params, max_norm)   ppo.py:243 (torch.nn.utils.clip_grad_norm_)
+//   Adam(lr, betas=(0.9, 0.999), eps=1e-8).step()   ppo.py:244 (torch.optim.Adam)
+// All parameters of a network live in one contiguous f32 buffer (and their
+// gradients in another), so the data-parallel all-reduce is one bucket and the
+// update is one streaming pass: read p, g, m, v; write p, m, v (28 B/param).
+//
+// torch semantics kept: total_norm = ||g||_2 over all parameters;
+// coef = max_norm / (total_norm + 1e-6) clamped to <= 1 and ALWAYS multiplied
+// in; m.lerp_(g, 1-beta1); v = v*beta2 + (1-beta2)*g*g;
+// p += -step_size * m / (sqrt(v)/sqrt(bc2) + eps),  step_size = lr / bc1.
+// The bias corrections depend only on the step count and are computed on the
+// host in float64 exactly like torch's Python code and passed in.
+#include "common.h"
+
+namespace {
+
+constexpr int P = PPOX_NORM_PARTIALS;
+
+__global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g, long long n,
+                                                    double* __restrict__ partials) {
+    __shared__ double red[4];
+    double acc = 0.0;
+    const long long n4 = n / 4;
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        const float4 v = g4[i];
+        acc += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+    if (blockIdx.x == 0)
+        for (long long i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) acc += (double)g[i] * g[i];
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__device__ inline float adam_one(float& p, float g, float& m, float& v, float coef, float w1, float b2, float w2,
+                                 float neg_step, float bc2s, float eps) {
+    g = g * coef;
+    m = m + w1 * (g - m);  // lerp with weight < 0.5
+    v = v * b2 + w2 * g * g;
+    const float denom = sqrtf(v) / bc2s + eps;
+    p = p + neg_step * (m / denom);
+    return g;
+}
+
+__global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                                   float* __restrict__ v, long long n,
+                                                   const double* __restrict__ partials, float max_norm, float w1,
+                                                   float b2, float w2, float neg_step, float bc2s, float eps,
+                                                   float* __restrict__ norm_out) {
+    __shared__ float coef_sh;
+    if (threadIdx.x == 0) {
+        float coef = 1.0f;
+        if (max_norm > 0.f) {
+            double s = 0.0;
+            for (int k = 0; k < P; ++k) s += partials[k];
+            const float total = (float)sqrt(s);
+            coef = fminf(max_norm / (total + 1e-6f), 1.0f);
+            if (blockIdx.x == 0 && norm_out) *norm_out = total;
+        }
+        coef_sh = coef;
+    }
+    __syncthreads();
+    const float coef = coef_sh;
+    const long long n4 = n / 4;
+    float4* p4 = reinterpret_cast<float4*>(p);
+    float4* g4 = reinterpret_cast<float4*>(g);
+    float4* m4 = reinterpret_cast<float4*>(m);
+    float4* v4 = reinterpret_cast<float4*>(v);
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
+        gg.x = adam_one(pp.x, gg.x, mm.x, vv.x, coef, w1, b2, w2, neg_step, bc2s, eps);
+        gg.y = adam_one(pp.y, gg.y, mm.y, vv.y, coef, w1, b2, w2, neg_step, bc2s, eps);
+        gg.z = adam_one(pp.z, gg.z, mm.z, vv.z, coef, w1, b2, w2, neg_step, bc2s, eps);
+        gg.w = adam_one(pp.w, gg.w, mm.w, vv.w, coef, w1, b2, w2, neg_step, bc2s, eps);
+        p4[i] = pp;
+        m4[i] = mm;
+        v4[i] = vv;
+    }
+    if (blockIdx.x == 0)
+        for (long long i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
+            float pp = p[i], mm = m[i], vv = v[i];
+            adam_one(pp, g[i], mm, vv, coef, w1, b2, w2, neg_step, bc2s, eps);
+            p[i] = pp;
+            m[i] = mm;
+            v[i] = vv;
+        }
+}
+
+}  // namespace
+
+extern "C" int ppox_grad_sumsq(const float* grads, int64_t n, double* partials, void* stream) {
+    PPOX_REQUIRE(grads && partials && n > 0, "ppox_grad_sumsq: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(grads), "ppox_grad_sumsq: grads must be 16-byte aligned");
+    sumsq_kernel<<<P, 256, 0, ppox::as_stream(stream)>>>(grads, n, partials);
+    PPOX_LAUNCHED("ppox_grad_sumsq");
+}
+
+extern "C" int ppox_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                              const double* norm_partials, float max_norm, double lr, double beta1, double beta2,
+                              double eps, int64_t step, float* total_norm_out, void* stream) {
+    PPOX_REQUIRE(params && grads && exp_avg && exp_avg_sq && n > 0 && step >= 1, "ppox_adam_step: bad arguments");
+    PPOX_REQUIRE(max_norm <= 0.f || norm_partials, "ppox_adam_step: clipping needs norm partials");
+    PPOX_REQUIRE(ppox::aligned16(params) && ppox::aligned16(grads) && ppox::aligned16(exp_avg) &&
+                     ppox::aligned16(exp_avg_sq),
+                 "ppox_adam_step: buffers must be 16-byte aligned");
+    // torch/optim/adam.py _single_tensor_adam scalar math, in Python-float (f64) precision
+    const double bc1 = 1.0 - std::pow(beta1, (double)step);
+    const double bc2 = 1.0 - std::pow(beta2, (double)step);
+    const double step_size = lr / bc1;
+    const double bc2s = std::sqrt(bc2);
+    const long long n4 = n / 4;
+    const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(ppox::ceil_div(n4, 256), 2048));
+    adam_kernel<<<grid, 256, 0, ppox::as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq, n, norm_partials,
+                                                           max_norm, (float)(1.0 - beta1), (float)beta2,
+                                                           (float)(1.0 - beta2), (float)(-step_size), (float)bc2s,
+                                                           (float)eps, total_norm_out);
+    PPOX_LAUNCHED("ppox_adam_step");
+}

@@ -1,0 +1,86 @@
+"""Data-parallel context: one process per GPU, envs sharded by index.
+
+The reference is single-process (no DP).  Here rank g owns envs
+[g*N/G, (g+1)*N/G).  The update stays EXACTLY the single-GPU update: every rank
+draws the same global numpy permutation (same seed), processes the rows of each
+global minibatch it owns, and the only per-minibatch exchanges are a 4 KB
+all-reduce of the loss partial sums (global advantage moments are all-gathered
+once per rollout) and the all-reduce of the flat gradient bucket.  On ROCm the
+torch "nccl" backend is RCCL over xGMI; CPU tests use "gloo".
+"""
+import os
+
+import numpy as np
+import torch
+import torch.distributed as tdist
+
+
+class DistContext:
+    def __init__(self, rank=0, world=1, group=None):
+        self.rank, self.world, self.group = rank, world, group
+
+    @property
+    def enabled(self):
+        return self.world > 1
+
+    @classmethod
+    def current(cls):
+        if tdist.is_available() and tdist.is_initialized():
+            return cls(tdist.get_rank(), tdist.get_world_size())
+        return cls()
+
+    def all_reduce_(self, t):
+        if self.enabled:
+            tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def all_gather_cat(self, t, dim):
+        """Concatenate every rank's `t` along `dim` in rank order."""
+        if not self.enabled:
+            return t
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        tdist.all_gather(parts, t.contiguous(), group=self.group)
+        return torch.cat(parts, dim=dim)
+
+    def barrier(self):
+        if self.enabled:
+            tdist.barrier(group=self.group)
+
+
+def init_from_env(backend=None):
+    """Initialise the default process group from torchrun's env vars (no-op at world 1)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1 or tdist.is_initialized():
+        return DistContext.current()
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    tdist.init_process_group(backend=backend)
+    return DistContext.current()
+
+
+def shard_range(n_envs, rank, world):
+    if n_envs % world:
+        raise ValueError(f"n_envs={n_envs} must be divisible by world size {world}")
+    per = n_envs // world
+    return rank * per, per
+
+
+def owned_minibatch_indices(perm, T, env_lo, n_local, batch_size):
+    """Split the GLOBAL env-major permutation into per-minibatch LOCAL indices.
+
+    perm holds flat indices i = n*T + t over all envs; this rank owns envs
+    [env_lo, env_lo + n_local).  Returns (local_flat_indices int64, offsets) where
+    minibatch k's owned rows are local[offsets[k]:offsets[k+1]], in permutation
+    order, re-based to the local flat index (n - env_lo)*T + t.
+    """
+    perm = np.asarray(perm, dtype=np.int64)
+    total = perm.shape[0]
+    env = perm // T
+    own = (env >= env_lo) & (env < env_lo + n_local)
+    local = perm[own] - env_lo * T
+    mb_of = (np.nonzero(own)[0] // batch_size)
+    n_mb = (total + batch_size - 1) // batch_size
+    counts = np.bincount(mb_of, minlength=n_mb)
+    offsets = np.concatenate([[0], np.cumsum(counts)])
+    return local, offsets

@@ -1,0 +1,211 @@
+"""Networks of the PPO + exploration path, with parameters packed in ONE flat
+device buffer per optimiser (so the data-parallel gradient all-reduce is one
+bucket and the Adam step one streaming kernel, libppox ppox_adam_step).
+
+Architectures (reference file:line):
+  MlpNetwork / MlpIntrinsic   models.py:137-213 (tanh MLPs, orthogonal sqrt(2) init :130-134)
+  RndNetwork                  models.py:216-267 (constant init, target frozen)
+  IntrinsicCuriosityModule    models.py:270-320
+  CnnActorCritic (NatureCNN)  .ipynb_checkpoints/models-checkpoint.py:48-90; the
+                              intrinsic value head (RND) mirrors MlpIntrinsic's
+                              extra critic.
+Modules are constructed on the CPU first so that a given torch seed yields the
+reference's exact initial weights (same construction order => same torch RNG
+consumption), then re-homed into the flat device buffers.
+The NatureCNN convolutions run on the libppox MFMA implicit-GEMM kernels when
+available (see convs.py); the small linear layers use PyTorch-ROCm (rocBLAS).
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import native
+
+
+def orthogonal_init(module, gain=math.sqrt(2)):
+    for m in module.modules():
+        if isinstance(m, (nn.Linear, nn.Conv2d)):
+            nn.init.orthogonal_(m.weight, gain)
+            nn.init.constant_(m.bias, 0)
+
+
+def _seq(sizes, act):
+    layers = []
+    for i in range(len(sizes) - 1):
+        layers.append(nn.Linear(sizes[i], sizes[i + 1]))
+        if i < len(sizes) - 2:
+            layers.append(act())
+    return nn.Sequential(*layers)
+
+
+class MlpNetwork(nn.Module):
+    """models.py:137-170 (+ MlpIntrinsic :173-213 with intrinsic=True)."""
+
+    def __init__(self, input_size, output_size, hidden_size=128, intrinsic=False):
+        super().__init__()
+        self.actor = _seq([input_size, hidden_size, hidden_size, output_size], nn.Tanh)
+        self.critic = _seq([input_size, hidden_size, hidden_size, 1], nn.Tanh)
+        if intrinsic:
+            self.int_critic = _seq([input_size, hidden_size, hidden_size, 1], nn.Tanh)
+        self.intrinsic = intrinsic
+        self.action_log_std = nn.Parameter(torch.zeros(1, output_size))
+        orthogonal_init(self)
+
+    def forward(self, x):
+        """-> (actor output, value (B,), int value (B,) or None)."""
+        x = x.float()
+        iv = self.int_critic(x).squeeze(-1) if self.intrinsic else None
+        return self.actor(x), self.critic(x).squeeze(-1), iv
+
+
+class CnnActorCritic(nn.Module):
+    """NatureCNN actor-critic (checkpoint models-checkpoint.py:48-90)."""
+
+    def __init__(self, input_size=4, output_size=4, hidden_size=512, intrinsic=False):
+        super().__init__()
+        self.feature_extractor = nn.Sequential(
+            nn.Conv2d(input_size, 32, 8, 4), nn.ReLU(), nn.Conv2d(32, 64, 4, 2), nn.ReLU(),
+            nn.Conv2d(64, 64, 3, 1), nn.ReLU(), nn.Flatten(), nn.Linear(7 * 7 * 64, hidden_size), nn.ReLU())
+        self.actor = nn.Sequential(nn.Linear(hidden_size, output_size))
+        self.extra_layer = nn.Sequential(nn.Linear(hidden_size, hidden_size), nn.ReLU())
+        self.critic_ext = nn.Linear(hidden_size, 1)
+        self.intrinsic = intrinsic
+        if intrinsic:
+            self.int_extra_layer = nn.Sequential(nn.Linear(hidden_size, hidden_size), nn.ReLU())
+            self.critic_int = nn.Linear(hidden_size, 1)
+        orthogonal_init(self)
+        self.conv_impl = None  # set by convs.attach()
+
+    def trunk(self, x):
+        if self.conv_impl is not None:
+            h = self.conv_impl(x)
+        else:
+            fe = self.feature_extractor
+            h = F.relu(fe[0](x.float()))
+            h = F.relu(fe[2](h))
+            h = F.relu(fe[4](h))
+        fc = self.feature_extractor[7]
+        return F.relu(F.linear(h.flatten(1), fc.weight, fc.bias))
+
+    def forward(self, x):
+        f = self.trunk(x)
+        v = self.critic_ext(self.extra_layer(f)).squeeze(-1)
+        iv = self.critic_int(self.int_extra_layer(f)).squeeze(-1) if self.intrinsic else None
+        return self.actor(f), v, iv
+
+
+class RndNetwork(nn.Module):
+    """models.py:216-267: predictor 3 hidden (LeakyReLU, LeakyReLU, ELU) -> 1,
+    target 2 hidden -> 1, constant init (target W=0.01 b=1; predictor W=1 b=0.01)."""
+
+    def __init__(self, input_size, hidden_size=32):
+        super().__init__()
+        self.predictor = nn.Sequential(
+            nn.Linear(input_size, hidden_size), nn.LeakyReLU(), nn.Linear(hidden_size, hidden_size), nn.LeakyReLU(),
+            nn.Linear(hidden_size, hidden_size), nn.ELU(), nn.Linear(hidden_size, 1))
+        self.target = nn.Sequential(
+            nn.Linear(input_size, hidden_size), nn.LeakyReLU(), nn.Linear(hidden_size, hidden_size), nn.LeakyReLU(),
+            nn.Linear(hidden_size, 1))
+        for n, p in self.target.named_parameters():
+            nn.init.constant_(p, 1.0 if "bias" in n else 0.01)
+        for n, p in self.predictor.named_parameters():
+            nn.init.constant_(p, 0.01 if "bias" in n else 1.0)
+        for p in self.target.parameters():
+            p.requires_grad = False
+
+    def forward(self, x):
+        return self.predictor(x), self.target(x)
+
+    def int_reward(self, x):
+        p, t = self(x)
+        return (p - t).pow(2).squeeze(-1)
+
+
+class IntrinsicCuriosityModule(nn.Module):
+    """models.py:270-320."""
+
+    def __init__(self, input_size, action_converter, hidden_size):
+        super().__init__()
+        self.action_converter = action_converter
+        self.discrete = action_converter.action_type == "Discrete"
+        self.feature_size = hidden_size
+        self.n_actions = action_converter.num_actions
+        self.state_encoder = nn.Sequential(nn.Linear(input_size, hidden_size), nn.LeakyReLU(),
+                                           nn.Linear(hidden_size, hidden_size))
+        self.forward_model = nn.Sequential(nn.Linear(self.n_actions + hidden_size, hidden_size), nn.LeakyReLU(),
+                                           nn.Linear(hidden_size, hidden_size))
+        self.inverse_model = nn.Sequential(nn.Linear(2 * hidden_size, hidden_size), nn.LeakyReLU(),
+                                           nn.Linear(hidden_size, self.n_actions))
+        if self.discrete:
+            self.action_encoder = nn.Embedding(self.n_actions, self.n_actions)
+        else:
+            self.action_encoder = nn.Linear(self.n_actions, self.n_actions)
+        orthogonal_init(self)
+
+    def encode_action(self, a):
+        return self.action_encoder(a.reshape(-1).long() if self.discrete else a.float())
+
+    def forward(self, state, next_state, action):
+        """models.py:300-309 -> (action_hat, next_state_hat, next_state_ft)."""
+        ae = self.encode_action(action)
+        f = self.state_encoder(state)
+        fn = self.state_encoder(next_state).view(-1, self.feature_size)
+        return self.inverse_model(torch.cat((f, fn), 1)), self.forward_model(torch.cat((f, ae), 1)), fn
+
+    def int_reward(self, state, next_state, action):
+        """models.py:311-320: clamp(mean((phi_hat(s,a) - phi(s'))^2), -5, 5)."""
+        ae = self.encode_action(action)
+        f = self.state_encoder(state)
+        fn = self.state_encoder(next_state)
+        nh = self.forward_model(torch.cat((f, ae), 1))
+        return torch.clamp((nh - fn).pow(2).mean(dim=-1), -5, 5)
+
+
+class FlatParams:
+    """Re-homes a module's trainable parameters into one contiguous f32 device
+    buffer (+ gradient and Adam moment buffers of the same layout).  Autograd
+    accumulates straight into the flat gradient buffer."""
+
+    def __init__(self, module, device="cuda"):
+        self.module = module
+        self.device = torch.device(device)
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        frozen = [p for p in module.parameters() if not p.requires_grad]
+        sizes = [p.numel() for p in self.params]
+        self.n = int(sum(sizes))
+        npad = (self.n + 63) // 64 * 64
+        self.data = torch.zeros(npad, device=self.device)
+        self.grad = torch.zeros(npad, device=self.device)
+        self.exp_avg = torch.zeros(npad, device=self.device)
+        self.exp_avg_sq = torch.zeros(npad, device=self.device)
+        self.norm_partials = torch.zeros(native.NORM_PARTIALS, dtype=torch.float64, device=self.device)
+        off = 0
+        with torch.no_grad():
+            for p in self.params:
+                k = p.numel()
+                self.data[off:off + k].copy_(p.detach().reshape(-1))
+                p.data = self.data[off:off + k].view(p.shape)
+                p.grad = self.grad[off:off + k].view(p.shape)
+                off += k
+            for p in frozen:
+                p.data = p.data.to(self.device)
+        for b in module.buffers():
+            b.data = b.data.to(self.device)
+        self.step_count = 0
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def adam_step(self, lr, max_grad_norm, betas=(0.9, 0.999), eps=1e-8):
+        """clip_grad_norm_(max_grad_norm) + Adam.step (ppo.py:243-244)."""
+        self.step_count += 1
+        if max_grad_norm is not None and max_grad_norm > 0:
+            native.grad_sumsq(self.grad, self.norm_partials)
+        native.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, self.norm_partials,
+                         max_grad_norm if max_grad_norm else 0.0, lr, betas[0], betas[1], eps, self.step_count)
+
+    def state_dict(self):
+        return {k: v.detach() for k, v in self.module.state_dict().items()}

@@ -1,0 +1,290 @@
+"""ctypes binding of libppox.so (the C ABI declared in include/ppox.h).
+
+This is the ONLY way the product reaches its compute: there is no CPU or
+PyTorch fallback.  If the library or a GPU is missing, `lib()` raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libppox.so")
+
+_vp, _i64, _i32, _f64, _f32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, ctypes.c_float
+_u64 = ctypes.c_uint64
+
+LOSS_PARTIALS = 64   # PPOX_LOSS_PARTIALS
+NORM_PARTIALS = 256  # PPOX_NORM_PARTIALS
+
+# name -> argtypes (restype is int unless listed in _RESTYPES)
+SIGNATURES = {
+    "ppox_gae": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _f64, _f64, _vp, _vp, _vp],
+    "ppox_gae_dual": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f64, _f64, _f64,
+                      _vp, _vp, _vp, _vp, _vp],
+    "ppox_rms_update_u8": [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp, _i64, _vp, _vp, _vp],
+    "ppox_rms_update_f32": [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp],
+    "ppox_rms_scale_int_rewards": [_vp, _i64, _vp, _vp, _f64, _vp],
+    "ppox_normalize_obs_u8": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "ppox_normalize_obs_f32": [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "ppox_minibatch_adv_stats": [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp],
+    "ppox_ppo_loss_partials": [_vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
+                               _vp, _vp, _vp, _vp, _f32, _vp, _vp],
+    "ppox_ppo_loss_backward": [_vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
+                               _vp, _vp, _vp, _vp, _f32, _vp, _i64, _f32, _f32, _f32, _f32,
+                               _vp, _vp, _vp, _vp, _vp],
+    "ppox_categorical_sample": [_vp, _i64, _i32, _i64, _u64, _i64, _vp, _vp, _vp],
+    "ppox_gather_rows": [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
+    "ppox_grad_sumsq": [_vp, _i64, _vp, _vp],
+    "ppox_adam_step": [_vp, _vp, _vp, _vp, _i64, _vp, _f32, _f64, _f64, _f64, _f64, _i64, _vp, _vp],
+    "ppox_atari_env_reset": [_vp, _i64, _i64, _u64, _vp, _vp, _vp],
+    "ppox_atari_env_step": [_vp, _vp, _vp, _i64, _i64, _u64, _i64, _f32, _f32, _vp, _vp, _vp, _vp,
+                            _vp, _vp, _vp],
+    "ppox_nature_pack_weights": [_vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_fwd": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
+    "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
+                          _vp, _vp, _vp],
+}
+_RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p,
+             "ppox_rms_u8_workspace_bytes": ctypes.c_int64}
+_RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64]}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load and bind the library (no GPU needed: used by the CPU ABI tests)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"libppox.so not built at {path}: run `make -C ppo-exploration_amd` "
+                          "(or __graft_entry__.build()); there is no fallback path")
+    lib = ctypes.CDLL(path)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    for name, rt in _RESTYPES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = _RESTYPE_ARGS.get(name, [])
+        fn.restype = rt
+    _lib = lib
+    return lib
+
+
+def lib():
+    """The library, for compute calls: also requires a visible GPU."""
+    l = load()
+    if not torch.cuda.is_available():
+        raise RuntimeError("ppo-exploration_amd needs an MI355X (HIP device); none is visible")
+    return l
+
+
+def version():
+    return load().ppox_version().decode()
+
+
+_timed = set()
+_events = {}
+
+
+def enable_event_timing(names):
+    """Bracket every launch of the named entry points with HIP events recorded on
+    the stream the kernel is launched on (bench.py roofline measurement)."""
+    _timed.clear()
+    _timed.update(names)
+    for n in names:
+        _events[n] = []
+
+
+def event_times_ms(name):
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) for a, b in _events.get(name, [])]
+
+
+def call(name, *args):
+    if name in _timed:
+        s = torch.cuda.current_stream()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        rc = getattr(lib(), name)(*args)
+        b.record(s)
+        _events[name].append((a, b))
+    else:
+        rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise NativeError(f"{name} failed ({rc}): {load().ppox_last_error().decode()}")
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return _vp(s.cuda_stream)
+
+
+def ptr(t, dtype=None, numel=None, name="tensor"):
+    """Device pointer of a contiguous tensor (validated)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name} has {t.numel()} elements, expected {numel}")
+    return _vp(t.data_ptr())
+
+
+# ---------------------------------------------------------------------------
+# K1 GAE
+# ---------------------------------------------------------------------------
+def gae(rewards, values, dones, last_value, last_done, gamma, lam, advantages, returns, stream=None):
+    T, N = rewards.shape
+    f32, u8 = torch.float32, torch.uint8
+    call("ppox_gae", ptr(rewards, f32, T * N, "rewards"), ptr(values, f32, T * N, "values"),
+         ptr(dones, u8, T * N, "dones"), ptr(last_value, f32, N, "last_value"),
+         ptr(last_done, u8, N, "last_done"), T, N, float(gamma), float(lam),
+         ptr(advantages, f32, T * N, "advantages"), ptr(returns, f32, T * N, "returns"), stream_ptr(stream))
+
+
+def gae_dual(rewards, values, dones, last_value, last_done, int_rewards, int_values, last_int_value,
+             gamma, int_gamma, lam, advantages, returns, int_advantages, int_returns, stream=None):
+    T, N = rewards.shape
+    f32, u8 = torch.float32, torch.uint8
+    call("ppox_gae_dual", ptr(rewards, f32, T * N, "rewards"), ptr(values, f32, T * N, "values"),
+         ptr(dones, u8, T * N, "dones"), ptr(last_value, f32, N, "last_value"),
+         ptr(last_done, u8, N, "last_done"), ptr(int_rewards, f32, T * N, "int_rewards"),
+         ptr(int_values, f32, T * N, "int_values"), ptr(last_int_value, f32, N, "last_int_value"),
+         T, N, float(gamma), float(int_gamma), float(lam),
+         ptr(advantages, f32, T * N, "advantages"), ptr(returns, f32, T * N, "returns"),
+         ptr(int_advantages, f32, T * N, "int_advantages"), ptr(int_returns, f32, T * N, "int_returns"),
+         stream_ptr(stream))
+
+
+def _p(t):
+    """Unchecked device pointer (hot loops; shapes were validated at setup)."""
+    return None if t is None else _vp(t.data_ptr())
+
+
+# ---------------------------------------------------------------------------
+# K2/K3 running moments + normalisation
+# ---------------------------------------------------------------------------
+def rms_u8_workspace_bytes(rows, cols):
+    return int(load().ppox_rms_u8_workspace_bytes(rows, cols))
+
+
+def rms_update_u8(x, rows, cols, row_stride, mean, var, count, workspace, batch_mean=None, batch_var=None,
+                  stream=None):
+    call("ppox_rms_update_u8", _p(x), rows, cols, row_stride, _p(mean), _p(var), float(count), _p(workspace),
+         workspace.numel() * workspace.element_size(), _p(batch_mean), _p(batch_var), stream_ptr(stream))
+
+
+def rms_update_f32(x, rows, cols, row_stride, mean, var, count, stream=None):
+    call("ppox_rms_update_f32", _p(x), rows, cols, row_stride, _p(mean), _p(var), float(count), stream_ptr(stream))
+
+
+def rms_scale_int_rewards(int_rewards, mean, var, count, stream=None):
+    call("ppox_rms_scale_int_rewards", ptr(int_rewards, torch.float32, name="int_rewards"), int_rewards.numel(),
+         _p(mean), _p(var), float(count), stream_ptr(stream))
+
+
+def normalize_obs(x, rows, cols, row_stride, mean, var, out, stream=None):
+    name = "ppox_normalize_obs_u8" if x.dtype == torch.uint8 else "ppox_normalize_obs_f32"
+    call(name, _p(x), rows, cols, row_stride, _p(mean), _p(var), ptr(out, torch.float32, rows * cols, "out"),
+         stream_ptr(stream))
+
+
+# ---------------------------------------------------------------------------
+# K4 loss + categorical head
+# ---------------------------------------------------------------------------
+def minibatch_adv_stats(adv, int_adv, perm, total, batch_size, T, N, out, stream=None):
+    call("ppox_minibatch_adv_stats", _p(adv), _p(int_adv), _p(perm), total, batch_size, T, N, _p(out),
+         stream_ptr(stream))
+
+
+def ppo_loss_partials(logits, values, int_values, B, A, idx, T, N, roll, adv_stats, clip, partials, stream=None):
+    """roll: dict of step-major rollout tensors (actions i32, log_probs, values, advantages, returns,
+    int_values, int_advantages, int_returns)."""
+    g = roll.get
+    call("ppox_ppo_loss_partials", _p(logits), _p(values), _p(int_values), B, A, _p(idx), T, N,
+         _p(g("actions")), _p(g("log_probs")), _p(g("values")), _p(g("advantages")), _p(g("returns")),
+         _p(g("int_values") if int_values is not None else None),
+         _p(g("int_advantages") if int_values is not None else None),
+         _p(g("int_returns") if int_values is not None else None), _p(adv_stats), float(clip), _p(partials),
+         stream_ptr(stream))
+
+
+def ppo_loss_backward(logits, values, int_values, B, A, idx, T, N, roll, adv_stats, clip, partials, B_global,
+                      ent_coef, vf_coef, int_vf_coef, scale, dlogits, dvalues, dint_values, loss_accum,
+                      stream=None):
+    g = roll.get
+    call("ppox_ppo_loss_backward", _p(logits), _p(values), _p(int_values), B, A, _p(idx), T, N,
+         _p(g("actions")), _p(g("log_probs")), _p(g("values")), _p(g("advantages")), _p(g("returns")),
+         _p(g("int_values") if int_values is not None else None),
+         _p(g("int_advantages") if int_values is not None else None),
+         _p(g("int_returns") if int_values is not None else None), _p(adv_stats), float(clip), _p(partials),
+         int(B_global), float(ent_coef), float(vf_coef), float(int_vf_coef), float(scale), _p(dlogits),
+         _p(dvalues), _p(dint_values), _p(loss_accum), stream_ptr(stream))
+
+
+def categorical_sample(logits, N, A, env_offset, seed, counter, actions, log_probs, stream=None):
+    call("ppox_categorical_sample", _p(logits), N, A, env_offset, seed & 0xFFFFFFFFFFFFFFFF, counter,
+         _p(actions), _p(log_probs), stream_ptr(stream))
+
+
+# ---------------------------------------------------------------------------
+# K5 gather, optimiser, envs
+# ---------------------------------------------------------------------------
+def gather_rows(src, T, N, row_bytes, src_row_stride, idx, nrows, dst, stream=None):
+    call("ppox_gather_rows", _p(src), T, N, row_bytes, src_row_stride, _p(idx), nrows, _p(dst), stream_ptr(stream))
+
+
+def grad_sumsq(grads, partials, stream=None):
+    call("ppox_grad_sumsq", _p(grads), grads.numel(), _p(partials), stream_ptr(stream))
+
+
+def adam_step(params, grads, m, v, norm_partials, max_norm, lr, beta1, beta2, eps, step, norm_out=None,
+              stream=None):
+    call("ppox_adam_step", _p(params), _p(grads), _p(m), _p(v), params.numel(), _p(norm_partials),
+         float(max_norm), float(lr), float(beta1), float(beta2), float(eps), int(step), _p(norm_out),
+         stream_ptr(stream))
+
+
+def atari_env_reset(obs, N, env_offset, seed, ep_ret=None, ep_len=None, stream=None):
+    call("ppox_atari_env_reset", _p(obs), N, env_offset, seed, _p(ep_ret), _p(ep_len), stream_ptr(stream))
+
+
+def atari_env_step(obs_in, obs_out, actions, N, env_offset, seed, step, p_reward, p_done, rewards, dones,
+                   ep_ret=None, ep_len=None, done_ret=None, done_len=None, stream=None):
+    call("ppox_atari_env_step", _p(obs_in), _p(obs_out), _p(actions), N, env_offset, seed, step, float(p_reward),
+         float(p_done), _p(rewards), _p(dones), _p(ep_ret), _p(ep_len), _p(done_ret), _p(done_len),
+         stream_ptr(stream))
+
+
+def vec_env_reset(obs, N, D, env_offset, seed, ep_ret=None, ep_len=None, stream=None):
+    call("ppox_vec_env_reset", _p(obs), N, D, env_offset, seed, _p(ep_ret), _p(ep_len), stream_ptr(stream))
+
+
+def vec_env_step(obs, actions, N, D, env_offset, seed, step, p_done, max_len, rewards, dones, ep_ret=None,
+                 ep_len=None, done_ret=None, done_len=None, stream=None):
+    call("ppox_vec_env_step", _p(obs), _p(actions), N, D, env_offset, seed, step, float(p_done), int(max_len),
+         _p(rewards), _p(dones), _p(ep_ret), _p(ep_len), _p(done_ret), _p(done_len), stream_ptr(stream))
+
+
+# ---------------------------------------------------------------------------
+# K6 NatureCNN convolutions
+# ---------------------------------------------------------------------------
+def nature_pack_weights(w1, w2, w3, wp1, wp2, wp3, stream=None):
+    call("ppox_nature_pack_weights", _p(w1), _p(w2), _p(w3), _p(wp1), _p(wp2), _p(wp3), stream_ptr(stream))
+
+
+def nature_conv_fwd(layer, x, batch, idx, T, N_env, x_sample_stride, wp, bias, y, stream=None):
+    call("ppox_nature_conv_fwd", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env), int(x_sample_stride),
+         _p(wp), _p(bias), _p(y), stream_ptr(stream))

@@ -1,0 +1,566 @@
+"""PPO, PPO+RND and PPO+ICM on MI355X — the reference's algorithm API
+(reference: ppo.py / algorithms.py:22-756) over the libppox hot path.
+
+    PPO(env_id=..., lr=3e-4, nstep=128, batch_size=128, n_epochs=10, ...)
+        .collect_samples()  (alias collect_rollouts)   ppo.py:166-198
+        .train()                                       ppo.py:200-259
+        .learn(total_timesteps, log_interval, reward_target=None, log_to_file=False)
+
+Keyword arguments and defaults are the reference's; added keywords:
+n_envs (the reference hard-codes 4, ppo.py:52), seed, device, env (a device env
+object; default: the synthetic env for env_id), quiet.
+
+Per iteration on each rank:
+  collect: T x [net forward (rocBLAS + MFMA convs) -> ppox_categorical_sample ->
+            ppox_*_env_step writing slot t+1]            (+ RND / ICM rewards)
+  GAE:     ppox_gae / ppox_gae_dual (bit-identical to buffer.py:203-230)
+  train:   per epoch one numpy permutation (buffer.py:239) + ppox_minibatch_adv_stats;
+           per minibatch ppox_gather_rows -> forward -> ppox_ppo_loss_partials
+           -> [all-reduce 4 KB] -> ppox_ppo_loss_backward -> backward into the flat
+           grad bucket -> [all-reduce] -> ppox_grad_sumsq + ppox_adam_step.
+There is no CPU fallback: every step needs libppox.so and a GPU.
+"""
+import time
+from collections import deque
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+import logger
+import native
+import convs
+from buffer import IntrinsicStorage, RolloutStorage
+from dist import DistContext, owned_minibatch_indices, shard_range
+from env import make_env
+from models import CnnActorCritic, FlatParams, IntrinsicCuriosityModule, MlpNetwork, RndNetwork
+from util import ActionConverter, RunningMeanStd
+
+
+def _is_image(space):
+    return len(space.shape) == 3
+
+
+class Policy:
+    """models.py:15-124 interface (act / evaluate) over a device network."""
+
+    def __init__(self, env, hidden_size, intrinsic_model=False):
+        self.env = env
+        self.action_type = env.action_space.__class__.__name__
+        self.action_dim = env.action_space.n if self.action_type == "Discrete" else env.action_space.shape[0]
+        self.intrinsic = intrinsic_model
+        shape = env.observation_space.shape
+        if _is_image(env.observation_space):
+            self.net = CnnActorCritic(shape[0], self.action_dim, intrinsic=intrinsic_model)
+        else:
+            self.net = MlpNetwork(shape[0], self.action_dim, hidden_size, intrinsic=intrinsic_model)
+
+    def parameters(self):
+        return self.net.parameters()
+
+    def _dist(self, out):
+        if self.action_type == "Discrete":
+            return torch.distributions.Categorical(F.softmax(out, dim=-1))
+        mean = out.tanh()
+        return torch.distributions.Normal(mean, torch.exp(self.net.action_log_std.expand_as(mean)))
+
+    def act(self, obs):
+        """models.py:30-50 / 75-99."""
+        out, v, iv = self.net(torch.as_tensor(obs, device=self.net.action_log_std.device
+                                              if hasattr(self.net, "action_log_std") else None))
+        d = self._dist(out)
+        a = d.sample()
+        lp = d.log_prob(a)
+        return (a, v, iv, lp) if self.intrinsic else (a, v, lp)
+
+    def evaluate(self, obs, actions):
+        """models.py:52-73 / 101-124."""
+        out, v, iv = self.net(obs)
+        d = self._dist(out)
+        if self.action_type == "Discrete":
+            lp = d.log_prob(actions.flatten()).unsqueeze(1)
+        else:
+            lp = d.log_prob(actions)
+        return (v, iv, lp, d.entropy()) if self.intrinsic else (v, lp, d.entropy())
+
+
+class BaseAlgorithm:
+    """ppo.py:22-118."""
+
+    def __init__(self, env_id, lr, nstep, batch_size, n_epochs, gamma, gae_lam, clip_range, ent_coef, vf_coef,
+                 max_grad_norm, n_envs=4, seed=0, device=None, env=None, quiet=False):
+        self.env_id = env_id
+        self.dist = DistContext.current()
+        self.device = torch.device(device or "cuda")
+        native.lib()  # fail loudly: no GPU / no libppox => no product path
+        self.num_envs = n_envs
+        self.env_offset, self.local_envs = shard_range(n_envs, self.dist.rank, self.dist.world)
+        self.seed = seed
+        self.env = env if env is not None else make_env(env_id, n_envs=self.local_envs, seed=seed,
+                                                        env_offset=self.env_offset, device=self.device)
+        self.state_dim = self.env.observation_space.shape[0]
+        self.action_converter = ActionConverter(self.env.action_space)
+        self.discrete = self.action_converter.action_type == "Discrete"
+        self.n_actions = self.action_converter.num_actions
+        self.lr, self.nstep, self.batch_size, self.n_epochs = lr, nstep, batch_size, n_epochs
+        self.gamma, self.gae_lam, self.clip_range = gamma, gae_lam, clip_range
+        self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
+        self.ep_info_buffer = deque(maxlen=50)
+        self._n_updates = 0
+        self.num_timesteps = 0
+        self.num_episodes = 0
+        self.quiet = quiet
+        self.obs_rms = RunningMeanStd(device=self.device)
+        self._sample_counter = 0
+        self._started = False
+
+    # ---------------------------------------------------------------- helpers
+    def _attach_convs(self):
+        if isinstance(self.policy.net, CnnActorCritic):
+            convs.attach(self.policy.net, self.flat)
+
+    def _new_rollout(self, cls, **kw):
+        return cls(self.nstep, self.local_envs, self.env.observation_space, self.env.action_space,
+                   device=self.device, **kw)
+
+    def _alloc_train_state(self):
+        d = self.device
+        self.loss_partials = torch.zeros(native.LOSS_PARTIALS * 8, dtype=torch.float64, device=d)
+        self.loss_accum = torch.zeros(8, dtype=torch.float64, device=d)
+
+    def _ensure_started(self):
+        if not self._started:
+            self.env.reset_into(self.rollout.obs_slots[0])
+            self._started = True
+        else:
+            self.rollout.obs_slots[0].copy_(self.rollout.obs_slots[self.nstep])
+
+    def _sample_actions(self, out, t):
+        ro = self.rollout
+        if self.discrete:
+            native.categorical_sample(out, self.local_envs, self.n_actions, self.env_offset, self.seed,
+                                      self._sample_counter, ro.actions[t], ro.log_probs[t])
+        else:
+            mean = out.tanh()
+            std = torch.exp(self.policy.net.action_log_std).expand_as(mean)
+            d = torch.distributions.Normal(mean, std)
+            a = d.sample()
+            ro.actions[t].copy_(a)
+            ro.log_probs[t].copy_(d.log_prob(a))
+        self._sample_counter += 1
+
+    def _finish_episodes(self):
+        ro = self.rollout
+        fin = ~torch.isnan(ro.done_ret)
+        self.num_episodes += int(ro.masks.sum().item()) * 1  # local envs (ppo.py:180-181)
+        if bool(fin.any()):
+            r = ro.done_ret[fin].cpu().numpy()
+            ln = ro.done_len[fin].cpu().numpy()
+            for x, y in zip(r, ln):
+                self.ep_info_buffer.append({"r": float(x), "l": int(y)})
+
+    def _epoch_minibatches(self, total):
+        """One global numpy permutation (buffer.py:239) -> per-minibatch (local idx, global size)."""
+        perm = np.random.permutation(total)
+        bs = total if self.batch_size is None else self.batch_size
+        sizes = [min(bs, total - s) for s in range(0, total, bs)]
+        perm_dev = torch.from_numpy(perm).to(self.device, non_blocking=True)
+        if not self.dist.enabled:
+            offs = np.concatenate([[0], np.cumsum(sizes)])
+            return perm_dev, perm_dev, offs, sizes
+        local, offs = owned_minibatch_indices(perm, self.nstep, self.env_offset, self.local_envs, bs)
+        return perm_dev, torch.from_numpy(local).to(self.device, non_blocking=True), offs, sizes
+
+    def _global_advantages(self, ro, intrinsic=False):
+        adv = self.dist.all_gather_cat(ro.advantages, dim=1)
+        iadv = self.dist.all_gather_cat(ro.int_advantages, dim=1) if intrinsic else None
+        return adv, iadv
+
+    def _record_train(self, extra=None):
+        acc = self.loss_accum.cpu().numpy()
+        n = max(acc[5], 1.0)
+        logger.record("train/entropy_loss", acc[2] / n)
+        logger.record("train/policy_gradient_loss", acc[0] / n)
+        logger.record("train/value_loss", acc[1] / n)
+        logger.record("train/total_loss", (acc[3] + (extra or 0.0)) / n)
+        return acc
+
+    def normalize_obs(self, obs):
+        """ppo.py:111-118 -> f32 device tensor (rows, features)."""
+        x = obs.reshape(obs.shape[0], -1)
+        out = torch.empty(x.shape, dtype=torch.float32, device=self.device)
+        native.normalize_obs(x, x.shape[0], x.shape[1], x.stride(0), self.obs_rms.mean, self.obs_rms.var, out)
+        return out
+
+    def update_info_buffer(self, infos, dones=None):
+        for info in infos:
+            ep = info.get("episode")
+            if ep is not None:
+                self.ep_info_buffer.extend([ep])
+
+    # ------------------------------------------------------------------ learn
+    def _log_iteration(self, start_time, extra=None):
+        logger.record("time/total timesteps", self.num_timesteps)
+        if len(self.ep_info_buffer) > 0:
+            logger.record("rollout/ep_rew_mean", float(np.mean([e["r"] for e in self.ep_info_buffer])))
+            logger.record("rollout/num_episodes", self.num_episodes)
+        if extra:
+            for k, v in extra.items():
+                logger.record(k, v)
+        el = time.time() - start_time
+        logger.record("time/total_time", el)
+        logger.record("time/env_steps_per_s", self.num_timesteps / max(el, 1e-9))
+        logger.dump(step=self.num_timesteps)
+
+    def _learn(self, algo_name, total_timesteps, log_interval, reward_target, log_to_file, progress=False):
+        if self.dist.rank == 0:
+            logger.configure(algo_name, self.env_id, log_to_file, quiet=self.quiet)
+        else:
+            logger.configure(algo_name, self.env_id, False, quiet=True)
+        start = time.time()
+        it = 0
+        while self.num_timesteps < total_timesteps:
+            prog = round(self.num_timesteps / total_timesteps * 100, 2)
+            self.collect_samples()
+            it += 1
+            if log_interval is not None and it % log_interval == 0:
+                self._log_iteration(start, {"Progress": f"{prog}%"} if progress else None)
+            self.train()
+            if reward_target is not None and len(self.ep_info_buffer) and \
+                    np.mean([e["r"] for e in self.ep_info_buffer]) > reward_target:
+                self._log_iteration(start)
+                break
+        return self
+
+    def collect_rollouts(self):
+        """north_star name for collect_samples (ppo.py:80 docstring)."""
+        return self.collect_samples()
+
+
+class PPO(BaseAlgorithm):
+    """ppo.py:121-308."""
+
+    def __init__(self, *, env_id, lr=3e-4, nstep=128, batch_size=128, n_epochs=10, gamma=0.99, gae_lam=0.95,
+                 clip_range=0.2, ent_coef=.01, vf_coef=1, max_grad_norm=0.2, hidden_size=128, sim_hash=False,
+                 sil=False, n_envs=4, seed=0, device=None, env=None, quiet=False):
+        if sil:
+            raise NotImplementedError("self-imitation (sil=True) is broken in the reference "
+                                      "(sil_module.py:14 vs buffer.py:406) and out of scope")
+        super().__init__(env_id, lr, nstep, batch_size, n_epochs, gamma, gae_lam, clip_range, ent_coef, vf_coef,
+                         max_grad_norm, n_envs=n_envs, seed=seed, device=device, env=env, quiet=quiet)
+        self.policy = Policy(self.env, hidden_size)
+        self.rollout = self._new_rollout(RolloutStorage, gae_lam=gae_lam, gamma=gamma, sim_hash=sim_hash)
+        self.flat = FlatParams(self.policy.net, self.device)
+        self._attach_convs()
+        self.optimizer = self.flat
+        self.sim_hash, self.sil = sim_hash, sil
+        self._alloc_train_state()
+        self.last_obs = None
+
+    def collect_samples(self):
+        ro = self.rollout
+        self._ensure_started()
+        ro.reset()
+        net = self.policy.net
+        for t in range(self.nstep):
+            with torch.no_grad():
+                out, v, _ = net(ro.obs_slots[t])
+            self._sample_actions(out, t)
+            ro.values[t].copy_(v)
+            self.env.step_into(ro.obs_slots[t], ro.obs_slots[t + 1], ro.actions[t], ro.rewards[t], ro.masks[t],
+                               ro.done_ret[t], ro.done_len[t])
+            self.num_timesteps += self.num_envs
+        ro.pos, ro.full = self.nstep, True
+        # ppo.py:196 bootstraps with V(s_{T-1}) and the last step's dones
+        ro.compute_returns_and_advantages(ro.values[self.nstep - 1], ro.masks[self.nstep - 1])
+        self._finish_episodes()
+        self.last_obs = ro.obs_slots[self.nstep]
+        return True
+
+    def _minibatch(self, idx, adv_stats, B_global, scale=1.0, extra_backward=None):
+        """Forward + fused loss + backward into the flat grad bucket (no step)."""
+        ro = self.rollout
+        Bl = idx.numel()
+        net = self.policy.net
+        self.flat.zero_grad()
+        if Bl > 0:
+            obs = ro._gather(ro.observations, idx)
+            out, v, _ = net(obs)
+            out_d, v_d = out.detach().contiguous(), v.detach().contiguous()
+        else:
+            out_d = torch.zeros(0, self.n_actions, device=self.device)
+            v_d = torch.zeros(0, device=self.device)
+        roll = ro.tensors()
+        native.ppo_loss_partials(out_d, v_d, None, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
+                                 adv_stats, self.clip_range, self.loss_partials)
+        self.dist.all_reduce_(self.loss_partials)
+        dout = torch.empty_like(out_d)
+        dv = torch.empty_like(v_d)
+        native.ppo_loss_backward(out_d, v_d, None, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
+                                 adv_stats, self.clip_range, self.loss_partials, B_global, self.ent_coef,
+                                 self.vf_coef, 0.0, scale, dout, dv, None, self.loss_accum)
+        if Bl > 0:
+            tensors, grads = [out, v], [dout, dv]
+            if extra_backward is not None:
+                tensors.append(extra_backward)
+                grads.append(None)
+            torch.autograd.backward(tensors, grads)
+        self.dist.all_reduce_(self.flat.grad)
+
+    def train(self):
+        if not self.discrete:
+            raise NotImplementedError("Box action spaces: fused continuous loss lands in a later round")
+        ro = self.rollout
+        total = self.nstep * self.num_envs
+        self.loss_accum.zero_()
+        adv, _ = self._global_advantages(ro)
+        n_mb = (total + self.batch_size - 1) // self.batch_size
+        stats = torch.empty(n_mb, 4, dtype=torch.float64, device=self.device)
+        for _ in range(self.n_epochs):
+            perm_dev, local, offs, sizes = self._epoch_minibatches(total)
+            native.minibatch_adv_stats(adv, None, perm_dev, total, self.batch_size, self.nstep, self.num_envs, stats)
+            for k, B in enumerate(sizes):
+                idx = local[offs[k]:offs[k + 1]]
+                self._minibatch(idx, stats[k], B)
+                self.flat.adam_step(self.lr, self.max_grad_norm)
+        self._record_train()
+        self._n_updates += self.n_epochs
+
+    def learn(self, total_timesteps, log_interval, reward_target=None, log_to_file=False):
+        name = "PPO_SimHash" if self.sim_hash else ("PPO_SIL" if self.sil else "PPO")
+        return self._learn(name, total_timesteps, log_interval, reward_target, log_to_file)
+
+
+class PPO_RND(BaseAlgorithm):
+    """ppo.py:310-543.  On image envs the RND nets read the normalised LAST frame
+    (the checkpoint's RND input, .ipynb_checkpoints/ppo-checkpoint.py:290)."""
+
+    def __init__(self, *, env_id, lr=3e-4, nstep=128, batch_size=128, n_epochs=10, gamma=0.99, int_gamma=0.99,
+                 gae_lam=0.95, clip_range=0.2, ent_coef=.01, vf_coef=0.5, int_vf_coef=0.5, max_grad_norm=0.2,
+                 hidden_size=128, int_hidden_size=128, int_lr=3e-4, rnd_start=1e+3, n_envs=4, seed=0, device=None,
+                 env=None, quiet=False):
+        super().__init__(env_id, lr, nstep, batch_size, n_epochs, gamma, gae_lam, clip_range, ent_coef, vf_coef,
+                         max_grad_norm, n_envs=n_envs, seed=seed, device=device, env=env, quiet=quiet)
+        self.policy = Policy(self.env, hidden_size, intrinsic_model=True)
+        self.image = _is_image(self.env.observation_space)
+        self.rnd_features = 84 * 84 if self.image else self.state_dim
+        self.rnd = RndNetwork(self.rnd_features, hidden_size=int_hidden_size)
+        self.rollout = self._new_rollout(IntrinsicStorage, gae_lam=gae_lam, gamma=gamma, int_gamma=int_gamma)
+        self.flat = FlatParams(self.policy.net, self.device)
+        self._attach_convs()
+        self.rnd_flat = FlatParams(self.rnd, self.device)
+        self.optimizer, self.rnd_optimizer = self.flat, self.rnd_flat
+        self.int_lr, self.rnd_start, self.int_vf_coef = int_lr, rnd_start, int_vf_coef
+        self.int_rew_rms = RunningMeanStd(device=self.device)
+        self._alloc_train_state()
+
+    def _rnd_input(self, obs):
+        """(N, F) view of the features RND sees: last frame (image) or the obs vector."""
+        if self.image:
+            return obs[:, 3].reshape(obs.shape[0], -1)
+        return obs.reshape(obs.shape[0], -1)
+
+    def collect_samples(self):
+        ro = self.rollout
+        self._ensure_started()
+        ro.reset()
+        net = self.policy.net
+        for t in range(self.nstep):
+            with torch.no_grad():
+                out, v, iv = net(ro.obs_slots[t])
+            self._sample_actions(out, t)
+            ro.values[t].copy_(v)
+            ro.int_values[t].copy_(iv)
+            self.env.step_into(ro.obs_slots[t], ro.obs_slots[t + 1], ro.actions[t], ro.rewards[t], ro.masks[t],
+                               ro.done_ret[t], ro.done_len[t])
+            self.num_timesteps += self.num_envs
+            if (self.num_timesteps / self.num_envs) < self.rnd_start:        # ppo.py:390-392
+                ro.int_rewards[t].zero_()
+                self._update_obs_rms(self._rnd_input(ro.obs_slots[t]))
+            else:                                                              # ppo.py:394-398
+                with torch.no_grad():
+                    ir = self.rnd.int_reward(self.normalize_obs(self._rnd_input(ro.obs_slots[t + 1])))
+                self._scale_int_rewards(ir)
+                ro.int_rewards[t].copy_(ir)
+        ro.pos, ro.full = self.nstep, True
+        T1 = self.nstep - 1
+        ro.compute_returns_and_advantages(ro.values[T1], ro.int_values[T1], ro.masks[T1])
+        self._finish_episodes()
+        return True
+
+    def _update_obs_rms(self, x):
+        if not self.dist.enabled:
+            self.obs_rms.update(x)
+            return
+        # exact across ranks: gather every rank's rows (rank order == env order)
+        self.obs_rms.update(self.dist.all_gather_cat(x.contiguous(), dim=0))
+
+    def _scale_int_rewards(self, ir):
+        ir = ir.contiguous()
+        full = self.dist.all_gather_cat(ir, dim=0) if self.dist.enabled else ir
+        native.rms_scale_int_rewards(full, self.int_rew_rms.mean, self.int_rew_rms.var, self.int_rew_rms.count)
+        self.int_rew_rms.count = full.numel() + self.int_rew_rms.count
+        if self.dist.enabled:
+            ir.copy_(full[self.env_offset:self.env_offset + self.local_envs])
+        elif full.data_ptr() != ir.data_ptr():
+            ir.copy_(full)
+
+    def train_rnd(self, obs):
+        """ppo.py:487-502."""
+        x = self.normalize_obs(self._rnd_input(obs))
+        p, tgt = self.rnd(x)
+        loss = F.mse_loss(p, tgt)
+        self.rnd_flat.zero_grad()
+        loss.backward()
+        self.dist.all_reduce_(self.rnd_flat.grad)
+        self.rnd_flat.adam_step(self.int_lr, self.max_grad_norm)
+
+    def train(self):
+        if not self.discrete:
+            raise NotImplementedError("Box action spaces: fused continuous loss lands in a later round")
+        ro = self.rollout
+        total = self.nstep * self.num_envs
+        self.loss_accum.zero_()
+        adv, iadv = self._global_advantages(ro, intrinsic=True)
+        n_mb = (total + self.batch_size - 1) // self.batch_size
+        stats = torch.empty(n_mb, 4, dtype=torch.float64, device=self.device)
+        net = self.policy.net
+        roll = ro.tensors()
+        for _ in range(self.n_epochs):
+            perm_dev, local, offs, sizes = self._epoch_minibatches(total)
+            native.minibatch_adv_stats(adv, iadv, perm_dev, total, self.batch_size, self.nstep, self.num_envs, stats)
+            for k, B in enumerate(sizes):
+                idx = local[offs[k]:offs[k + 1]]
+                Bl = idx.numel()
+                self.flat.zero_grad()
+                obs = ro._gather(ro.observations, idx)
+                out, v, iv = net(obs)
+                od, vd, ivd = out.detach().contiguous(), v.detach().contiguous(), iv.detach().contiguous()
+                native.ppo_loss_partials(od, vd, ivd, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
+                                         stats[k], self.clip_range, self.loss_partials)
+                self.dist.all_reduce_(self.loss_partials)
+                dout, dv, div = torch.empty_like(od), torch.empty_like(vd), torch.empty_like(ivd)
+                native.ppo_loss_backward(od, vd, ivd, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
+                                         stats[k], self.clip_range, self.loss_partials, B, self.ent_coef,
+                                         self.vf_coef, self.int_vf_coef, 1.0, dout, dv, div, self.loss_accum)
+                if Bl > 0:
+                    torch.autograd.backward([out, v, iv], [dout, dv, div])
+                self.dist.all_reduce_(self.flat.grad)
+                self.flat.adam_step(self.lr, self.max_grad_norm)
+                if np.random.randn() < 0.25:                                   # ppo.py:468-469
+                    self.train_rnd(obs)
+        acc = self._record_train()
+        logger.record("train/intrinsic_loss", acc[4] / max(acc[5], 1.0))
+        self._n_updates += self.n_epochs
+
+    def learn(self, total_timesteps, log_interval, reward_target=None, log_to_file=False):
+        return self._learn("RND", total_timesteps, log_interval, reward_target, log_to_file)
+
+
+class PPO_ICM(BaseAlgorithm):
+    """ppo.py:546-756.  Quirks kept: beta is fixed at 0.2 (ppo.py:600); the
+    rollout uses the default gamma 0.99 (ppo.py:591); ICM pairs are consecutive
+    rows of the permuted minibatch (ppo.py:684).  On image envs the ICM MLP reads
+    the flattened frame stack (input 4*84*84)."""
+
+    def __init__(self, *, env_id, lr=3e-4, int_lr=3e-4, nstep=128, batch_size=128, n_epochs=10, gamma=0.99,
+                 gae_lam=0.95, clip_range=0.2, ent_coef=.01, vf_coef=0.5, max_grad_norm=0.2, hidden_size=128,
+                 int_hidden_size=32, int_rew_integration=0.05, beta=0.2, policy_weight=1, n_envs=4, seed=0,
+                 device=None, env=None, quiet=False):
+        super().__init__(env_id, lr, nstep, batch_size, n_epochs, gamma, gae_lam, clip_range, ent_coef, vf_coef,
+                         max_grad_norm, n_envs=n_envs, seed=seed, device=device, env=env, quiet=quiet)
+        self.int_rew_integration = int_rew_integration
+        self.policy = Policy(self.env, hidden_size)
+        self.rollout = self._new_rollout(RolloutStorage, gae_lam=gae_lam)
+        icm_in = int(np.prod(self.env.observation_space.shape))
+        self.intrinsic_module = IntrinsicCuriosityModule(icm_in, self.action_converter, hidden_size=int_hidden_size)
+        self.flat = FlatParams(self.policy.net, self.device)
+        self._attach_convs()
+        self.icm_flat = FlatParams(self.intrinsic_module, self.device)
+        self.optimizer, self.icm_optimizer = self.flat, self.icm_flat
+        self.int_lr = int_lr
+        self.policy_weight = policy_weight
+        self.beta = 0.2
+        self._alloc_train_state()
+        self.icm_accum = torch.zeros(1, dtype=torch.float64, device=self.device)
+
+    def _icm_x(self, obs):
+        return obs.reshape(obs.shape[0], -1).float()
+
+    def collect_samples(self):
+        ro = self.rollout
+        self._ensure_started()
+        ro.reset()
+        net = self.policy.net
+        ir_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+        eta = self.int_rew_integration
+        for t in range(self.nstep):
+            with torch.no_grad():
+                out, v, _ = net(ro.obs_slots[t])
+            self._sample_actions(out, t)
+            ro.values[t].copy_(v)
+            self.env.step_into(ro.obs_slots[t], ro.obs_slots[t + 1], ro.actions[t], ro.rewards[t], ro.masks[t],
+                               ro.done_ret[t], ro.done_len[t])
+            self.num_timesteps += self.num_envs
+            with torch.no_grad():                                              # ppo.py:629-630
+                ir = self.intrinsic_module.int_reward(self._icm_x(ro.obs_slots[t]), self._icm_x(ro.obs_slots[t + 1]),
+                                                      ro.actions[t])
+            ro.rewards[t].copy_((1 - eta) * ro.rewards[t] + eta * ir)
+            ir_sum += ir.double().mean()
+        logger.record("rollout/mean_int_reward", float(ir_sum.item()) / self.nstep)
+        ro.pos, ro.full = self.nstep, True
+        ro.compute_returns_and_advantages(ro.values[self.nstep - 1], ro.masks[self.nstep - 1])
+        self._finish_episodes()
+        return True
+
+    def train(self):
+        if not self.discrete:
+            raise NotImplementedError("Box action spaces: fused continuous loss lands in a later round")
+        ro = self.rollout
+        total = self.nstep * self.num_envs
+        self.loss_accum.zero_()
+        self.icm_accum.zero_()
+        adv, _ = self._global_advantages(ro)
+        n_mb = (total + self.batch_size - 1) // self.batch_size
+        stats = torch.empty(n_mb, 4, dtype=torch.float64, device=self.device)
+        net, icm = self.policy.net, self.intrinsic_module
+        roll = ro.tensors()
+        for _ in range(self.n_epochs):
+            perm_dev, local, offs, sizes = self._epoch_minibatches(total)
+            native.minibatch_adv_stats(adv, None, perm_dev, total, self.batch_size, self.nstep, self.num_envs, stats)
+            for k, B in enumerate(sizes):
+                idx = local[offs[k]:offs[k + 1]]
+                Bl = idx.numel()
+                self.flat.zero_grad()
+                self.icm_flat.zero_grad()
+                obs = ro._gather(ro.observations, idx)
+                out, v, _ = net(obs)
+                od, vd = out.detach().contiguous(), v.detach().contiguous()
+                native.ppo_loss_partials(od, vd, None, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
+                                         stats[k], self.clip_range, self.loss_partials)
+                self.dist.all_reduce_(self.loss_partials)
+                dout, dv = torch.empty_like(od), torch.empty_like(vd)
+                native.ppo_loss_backward(od, vd, None, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
+                                         stats[k], self.clip_range, self.loss_partials, B, self.ent_coef,
+                                         self.vf_coef, 0.0, float(self.policy_weight), dout, dv, None,
+                                         self.loss_accum)
+                # ICM on consecutive rows of the (owned part of the) permuted minibatch (ppo.py:684-688)
+                acts = ro.actions.reshape(-1)[(idx % self.nstep) * self.local_envs + idx // self.nstep]
+                x = self._icm_x(obs)
+                a_hat, f_next, f_next_hat = icm(x[:-1], x[1:], acts[:-1])
+                fwd = F.mse_loss(f_next, f_next_hat)
+                inv = F.cross_entropy(a_hat, acts[:-1].long())
+                icm_loss = (1 - self.beta) * inv + self.beta * fwd
+                self.icm_accum += icm_loss.detach().double()
+                torch.autograd.backward([out, v, icm_loss], [dout, dv, None])
+                self.dist.all_reduce_(self.flat.grad)
+                self.dist.all_reduce_(self.icm_flat.grad)
+                self.flat.adam_step(self.lr, self.max_grad_norm)               # ppo.py:697-698
+                self.icm_flat.adam_step(self.int_lr, None)                     # ppo.py:699 (no clipping)
+        icm_mean = float(self.icm_accum.item())
+        acc = self._record_train(extra=icm_mean)
+        logger.record("train/icm_loss", icm_mean / max(acc[5], 1.0))
+        self._n_updates += self.n_epochs
+
+    def learn(self, total_timesteps, log_interval=5, reward_target=None, log_to_file=False):
+        return self._learn("ICM", total_timesteps, log_interval, reward_target, log_to_file, progress=True)

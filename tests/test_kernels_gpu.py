@@ -1,0 +1,338 @@
+"""libppox kernels vs the CPU oracle through the C ABI (GPU box only)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import algos as OA
+from oracle import philox as PH
+from oracle import rms as RM
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a, dtype=None):
+    t = torch.as_tensor(np.ascontiguousarray(a))
+    return (t.to(dtype) if dtype is not None else t).cuda()
+
+
+# ----------------------------------------------------------------- K4 loss
+def _oracle_loss(logits, values, acts, old_lp, old_v, adv, ret, clip, ent_coef, vf_coef,
+                 iv=None, old_iv=None, iadv=None, iret=None, int_vf_coef=0.5, scale=1.0):
+    """torch-CPU autograd of ppo.py:216-238 (+ RND terms :431-460)."""
+    z = torch.tensor(logits, requires_grad=True)
+    v = torch.tensor(values, requires_grad=True)
+    d = torch.distributions.Categorical(torch.softmax(z, dim=-1))
+    lp = d.log_prob(torch.tensor(acts, dtype=torch.float64).flatten()).unsqueeze(1)
+    ent = d.entropy()
+    a = OA.normalized(torch.tensor(adv).reshape(-1, 1))
+    if iv is not None:
+        a = a + OA.normalized(torch.tensor(iadv).reshape(-1, 1))
+    pl = OA.surrogate(a, torch.exp(lp - torch.tensor(old_lp).reshape(-1, 1)), clip)
+    vl = OA.clipped_value_loss(torch.tensor(ret), v, torch.tensor(old_v), clip)
+    el = -torch.mean(ent)
+    loss = pl + ent_coef * el + vf_coef * vl
+    ivt = None
+    if iv is not None:
+        ivt = torch.tensor(iv, requires_grad=True)
+        ivl = OA.clipped_value_loss(torch.tensor(iret), ivt, torch.tensor(old_iv), clip)
+        loss = loss + int_vf_coef * ivl
+    (scale * loss).backward()
+    out = {"dz": z.grad.numpy(), "dv": v.grad.numpy(), "pl": pl.item(), "vl": vl.item(), "el": el.item(),
+           "loss": loss.item()}
+    if ivt is not None:
+        out["div"] = ivt.grad.numpy()
+        out["ivl"] = ivl.item()
+    return out
+
+
+@pytest.mark.parametrize("A,B,dual,sat", [(4, 333, False, False), (2, 64, False, True), (18, 1000, False, False),
+                                          (4, 517, True, False), (6, 2048, True, True)])
+def test_ppo_loss_fwd_bwd_vs_torch(A, B, dual, sat):
+    import native
+    rs = np.random.RandomState(A * 1000 + B)
+    T, N = 32, 64
+    total = T * N
+    clip, ent_coef, vf_coef, ivf = 0.2, 0.01, 0.5, 0.5
+    roll = {"actions": rs.randint(0, A, (T, N)).astype(np.int32),
+            "log_probs": (np.log(rs.dirichlet(np.ones(A), (T, N))).max(-1) - rs.rand(T, N)).astype(np.float32),
+            "values": rs.randn(T, N).astype(np.float32), "advantages": rs.randn(T, N).astype(np.float32) * 2,
+            "returns": rs.randn(T, N).astype(np.float32), "int_values": rs.randn(T, N).astype(np.float32),
+            "int_advantages": rs.randn(T, N).astype(np.float32), "int_returns": rs.randn(T, N).astype(np.float32)}
+    perm = rs.permutation(total)[:B]
+    t_of, n_of = perm % T, perm // T
+    logits = rs.randn(B, A).astype(np.float32) * (40.0 if sat else 1.5)
+    values = (roll["values"][t_of, n_of] + rs.randn(B).astype(np.float32) * 0.3).astype(np.float32)
+    ivals = (roll["int_values"][t_of, n_of] + rs.randn(B).astype(np.float32) * 0.3).astype(np.float32)
+    g = {k: v[t_of, n_of] for k, v in roll.items()}
+    ref = _oracle_loss(logits, values, g["actions"], g["log_probs"], g["values"], g["advantages"], g["returns"], clip,
+                       ent_coef, vf_coef, ivals if dual else None, g["int_values"], g["int_advantages"],
+                       g["int_returns"], ivf, scale=0.7)
+    droll = {k: dev(v) for k, v in roll.items()}
+    idx = dev(perm.astype(np.int64))
+    stats = torch.empty(1, 4, dtype=torch.float64, device="cuda")
+    native.minibatch_adv_stats(droll["advantages"], droll["int_advantages"] if dual else None, idx, B, B, T, N, stats)
+    partials = torch.zeros(native.LOSS_PARTIALS * 8, dtype=torch.float64, device="cuda")
+    accum = torch.zeros(8, dtype=torch.float64, device="cuda")
+    z, v, iv = dev(logits), dev(values), dev(ivals) if dual else None
+    native.ppo_loss_partials(z, v, iv, B, A, idx, T, N, droll, stats[0], clip, partials)
+    dz, dv = torch.empty_like(z), torch.empty_like(v)
+    div = torch.empty_like(iv) if dual else None
+    native.ppo_loss_backward(z, v, iv, B, A, idx, T, N, droll, stats[0], clip, partials, B, ent_coef, vf_coef, ivf,
+                             0.7, dz, dv, div, accum)
+    torch.cuda.synchronize()
+    acc = accum.cpu().numpy()
+    np.testing.assert_allclose(acc[0], ref["pl"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(acc[1], ref["vl"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(acc[2], ref["el"], rtol=1e-5, atol=1e-7)
+    scale_g = max(np.abs(ref["dz"]).max(), 1e-30)
+    np.testing.assert_allclose(dz.cpu().numpy(), ref["dz"], rtol=1e-4, atol=1e-5 * scale_g)
+    np.testing.assert_allclose(dv.cpu().numpy(), ref["dv"], rtol=1e-5, atol=1e-8)
+    if dual:
+        np.testing.assert_allclose(acc[4], ref["ivl"], rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(div.cpu().numpy(), ref["div"], rtol=1e-5, atol=1e-8)
+
+
+def test_adv_stats_remainder_and_singleton():
+    """Minibatch slices incl. a remainder of 1 (unbiased std of one sample -> nan, as torch)."""
+    import native
+    T, N, B = 8, 5, 13
+    rs = np.random.RandomState(3)
+    adv = rs.randn(T, N).astype(np.float32)
+    perm = rs.permutation(T * N)  # 40 = 3*13 + 1
+    stats = torch.empty(4, 4, dtype=torch.float64, device="cuda")
+    native.minibatch_adv_stats(dev(adv), None, dev(perm.astype(np.int64)), T * N, B, T, N, stats)
+    st = stats.cpu().numpy()
+    for k in range(4):
+        sl = perm[k * B:(k + 1) * B]
+        x = torch.tensor(adv[sl % T, sl // T])
+        np.testing.assert_allclose(st[k, 0], x.double().mean().item(), rtol=1e-12)
+        if len(sl) > 1:
+            np.testing.assert_allclose(st[k, 1], x.double().std().item(), rtol=1e-10)
+        else:
+            assert np.isnan(st[k, 1])
+
+
+def test_categorical_sample_distribution():
+    import native
+    N, A = 200000, 4
+    logits = torch.tensor([[0.0, 1.0, 2.0, -1.0]], device="cuda").repeat(N, 1)
+    acts = torch.empty(N, dtype=torch.int32, device="cuda")
+    lp = torch.empty(N, device="cuda")
+    native.categorical_sample(logits, N, A, 0, 1234, 7, acts, lp)
+    p = torch.softmax(logits[0].cpu(), -1).numpy()
+    freq = np.bincount(acts.cpu().numpy(), minlength=A) / N
+    np.testing.assert_allclose(freq, p, atol=4e-3)
+    np.testing.assert_allclose(lp.cpu().numpy(), np.log(p)[acts.cpu().numpy()], rtol=1e-5)
+
+
+# ----------------------------------------------------------------- envs
+def test_atari_env_matches_numpy_twin():
+    import native
+    N, off, seed = 6, 100, 0xDEADBEEF12345
+    twin = PH.SyntheticAtari(N, seed, p_reward=0.3, p_done=0.2, env_offset=off)
+    o0 = twin.reset()
+    obs = torch.empty((N, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    native.atari_env_reset(obs, N, off, seed)
+    assert np.array_equal(obs.cpu().numpy(), o0)
+    rs = np.random.RandomState(0)
+    nxt = torch.empty_like(obs)
+    rew = torch.empty(N, device="cuda")
+    done = torch.empty(N, dtype=torch.uint8, device="cuda")
+    for k in range(1, 12):
+        a = rs.randint(0, 4, N).astype(np.int32)
+        o, r, d, _ = twin.step(a)
+        native.atari_env_step(obs, nxt, dev(a), N, off, seed, k, 0.3, 0.2, rew, done)
+        assert np.array_equal(nxt.cpu().numpy(), o), k
+        assert np.array_equal(rew.cpu().numpy(), r)
+        assert np.array_equal(done.cpu().numpy().astype(bool), d)
+        obs, nxt = nxt, obs
+
+
+def test_atari_env_in_place_and_sharding():
+    """Stepping in place equals stepping out of place; a shard equals the slice of the full run."""
+    import native
+    N, seed = 8, 77
+    full = torch.empty((N, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    native.atari_env_reset(full, N, 0, seed)
+    shard = full[4:].clone()
+    acts = torch.arange(N, dtype=torch.int32, device="cuda") % 4
+    rew = torch.empty(N, device="cuda")
+    done = torch.empty(N, dtype=torch.uint8, device="cuda")
+    out = torch.empty_like(full)
+    native.atari_env_step(full, out, acts, N, 0, seed, 1, 0.5, 0.5, rew, done)
+    native.atari_env_step(full, full, acts, N, 0, seed, 1, 0.5, 0.5, rew, done)
+    assert torch.equal(out, full)
+    srew = torch.empty(4, device="cuda")
+    sdone = torch.empty(4, dtype=torch.uint8, device="cuda")
+    native.atari_env_step(shard, shard, acts[4:].contiguous(), 4, 4, seed, 1, 0.5, 0.5, srew, sdone)
+    assert torch.equal(shard, full[4:])
+
+
+# ----------------------------------------------------------------- RMS
+def test_rms_u8_vs_numpy():
+    import native
+    rs = np.random.RandomState(1)
+    rm = RM.RunningMoments()
+    mean = torch.zeros(7056, dtype=torch.float64, device="cuda")
+    var = torch.ones(7056, dtype=torch.float64, device="cuda")
+    count = 1e-4
+    for n in (100, 1, 257):
+        x = rs.randint(0, 256, (n, 4, 84, 84)).astype(np.uint8)
+        last = x[:, 3].reshape(n, -1)
+        rm.update(last)
+        xd = dev(x)
+        view = xd[:, 3].reshape(n, -1)
+        ws = torch.empty(native.rms_u8_workspace_bytes(n, 7056), dtype=torch.uint8, device="cuda")
+        native.rms_update_u8(view, n, 7056, view.stride(0), mean, var, count, ws)
+        count += n
+        np.testing.assert_array_equal(mean.cpu().numpy(), rm.mean)
+        np.testing.assert_allclose(var.cpu().numpy(), rm.var, rtol=1e-12)
+
+
+def test_rms_f32_and_scalar_bitexact(golden):
+    import native
+    f = golden("rms")
+    mean = torch.zeros(6, dtype=torch.float64, device="cuda")
+    var = torch.ones(6, dtype=torch.float64, device="cuda")
+    count = 1e-4
+    for i in range(int(f["f32_n"])):
+        b = f[f"f32_b{i}"]
+        native.rms_update_f32(dev(b), b.shape[0], 6, 6, mean, var, count)
+        count += b.shape[0]
+        np.testing.assert_array_equal(mean.cpu().numpy(), f[f"f32_mean{i}"])
+        np.testing.assert_array_equal(var.cpu().numpy(), f[f"f32_var{i}"])
+    m1 = torch.zeros((), dtype=torch.float64, device="cuda")
+    v1 = torch.ones((), dtype=torch.float64, device="cuda")
+    count = 1e-4
+    for i in range(int(f["sc_n"])):
+        b = f[f"sc_b{i}"]
+        native.rms_update_f32(dev(b), b.shape[0], 1, 1, m1, v1, count)
+        count += b.shape[0]
+        np.testing.assert_array_equal(m1.cpu().numpy(), f[f"sc_mean{i}"])
+        np.testing.assert_array_equal(v1.cpu().numpy(), f[f"sc_var{i}"])
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 100, 129, 1024, 4096, 5000])
+def test_int_reward_scaling_bitexact(n):
+    """ppo.py:396-398: int_rew_rms.update + in-place scaling, incl. numpy pairwise order."""
+    import native
+    rs = np.random.RandomState(n)
+    rm = RM.RunningMoments()
+    mean = torch.zeros((), dtype=torch.float64, device="cuda")
+    var = torch.ones((), dtype=torch.float64, device="cuda")
+    count = 1e-4
+    for it in range(3):
+        ir = (np.abs(rs.randn(n)) * (it + 1) * 1e3).astype(np.float32)
+        exp = ir.copy()
+        rm.update(exp)
+        exp /= (np.sqrt(rm.var) + 1e-08)
+        d = dev(ir)
+        native.rms_scale_int_rewards(d, mean, var, count)
+        count += n
+        np.testing.assert_array_equal(mean.cpu().numpy(), rm.mean)
+        np.testing.assert_array_equal(var.cpu().numpy(), rm.var)
+        np.testing.assert_array_equal(d.cpu().numpy(), exp)
+
+
+def test_normalize_obs_bitexact(golden):
+    import native
+    f = golden("rms")
+    x = f["norm_in"]
+    out = torch.empty(x.shape, device="cuda")
+    native.normalize_obs(dev(x), x.shape[0], x.shape[1], x.shape[1], dev(f["norm_mean"]), dev(f["norm_var"]), out)
+    np.testing.assert_array_equal(out.cpu().numpy(), f["norm_out"].astype(np.float32))
+    # u8 frames
+    rs = np.random.RandomState(2)
+    u = rs.randint(0, 256, (5, 7056)).astype(np.uint8)
+    m, v = rs.rand(7056) * 255, rs.rand(7056) * 5000 + 1
+    out = torch.empty(u.shape, device="cuda")
+    native.normalize_obs(dev(u), 5, 7056, 7056, dev(m), dev(v), out)
+    np.testing.assert_array_equal(out.cpu().numpy(), RM.normalize_obs(u, m, v).astype(np.float32))
+
+
+# ----------------------------------------------------------------- gather + Adam
+def test_gather_rows_env_major():
+    import native
+    T, N, F = 16, 12, 4 * 84 * 84
+    rs = np.random.RandomState(4)
+    obs = rs.randint(0, 256, (T, N, F)).astype(np.uint8)
+    idx = rs.permutation(T * N)[:50]
+    out = torch.empty((50, F), dtype=torch.uint8, device="cuda")
+    native.gather_rows(dev(obs), T, N, F, F, dev(idx.astype(np.int64)), 50, out)
+    assert np.array_equal(out.cpu().numpy(), obs[idx % T, idx // T])
+
+
+@pytest.mark.parametrize("max_norm", [0.2, 1e9, 0.0])
+def test_adam_clip_vs_torch(max_norm):
+    import native
+    rs = np.random.RandomState(5)
+    sizes = [(64, 33), (33,), (7, 5, 3)]
+    ps = [torch.tensor(rs.randn(*s).astype(np.float32), requires_grad=True) for s in sizes]
+    opt = torch.optim.Adam(ps, lr=3e-4)
+    n = sum(p.numel() for p in ps)
+    npad = (n + 63) // 64 * 64
+    flat = torch.zeros(npad, device="cuda")
+    flat[:n] = torch.cat([p.detach().reshape(-1) for p in ps]).cuda()
+    m = torch.zeros_like(flat)
+    v = torch.zeros_like(flat)
+    g = torch.zeros_like(flat)
+    part = torch.zeros(native.NORM_PARTIALS, dtype=torch.float64, device="cuda")
+    for step in range(1, 4):
+        grads = [rs.randn(*s).astype(np.float32) for s in sizes]
+        for p, gg in zip(ps, grads):
+            p.grad = torch.tensor(gg)
+        if max_norm > 0:
+            torch.nn.utils.clip_grad_norm_(ps, max_norm)
+        opt.step()
+        g.zero_()
+        g[:n] = torch.cat([torch.tensor(gg).reshape(-1) for gg in grads]).cuda()
+        if max_norm > 0:
+            native.grad_sumsq(g, part)
+        native.adam_step(flat, g, m, v, part, max_norm, 3e-4, 0.9, 0.999, 1e-8, step)
+    ref = torch.cat([p.detach().reshape(-1) for p in ps]).numpy()
+    np.testing.assert_allclose(flat[:n].cpu().numpy(), ref, rtol=1e-6, atol=1e-7)
+
+
+# ----------------------------------------------------------------- K6 convs
+@pytest.mark.parametrize("B", [1, 3, 37, 256])
+def test_nature_conv_fwd_vs_torch_fp32(B):
+    """MFMA implicit-GEMM conv trunk vs torch fp32 convs (tolerance: fp32 re-association)."""
+    import models
+    import convs
+    torch.manual_seed(B)
+    net = models.CnnActorCritic(4, 4)
+    ref = models.CnnActorCritic(4, 4)
+    ref.load_state_dict(net.state_dict())
+    flat = models.FlatParams(net, "cuda")
+    ref = ref.cuda()
+    convs.attach(net, flat)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    with torch.no_grad():
+        h = net.conv_impl(x)
+        fe = ref.feature_extractor
+        e = torch.relu(fe[4](torch.relu(fe[2](torch.relu(fe[0](x.float()))))))
+    err = (h - e).abs().max().item()
+    assert err <= 2e-5 * e.abs().max().item() + 1e-4, err
+
+
+def test_nature_trunk_backward_vs_torch():
+    import models
+    import convs
+    torch.manual_seed(0)
+    net = models.CnnActorCritic(4, 4)
+    ref = models.CnnActorCritic(4, 4)
+    ref.load_state_dict(net.state_dict())
+    flat = models.FlatParams(net, "cuda")
+    ref = ref.cuda()
+    convs.attach(net, flat)
+    x = torch.randint(0, 256, (50, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    g = torch.randn(50, 64, 7, 7, device="cuda")
+    flat.zero_grad()
+    net.conv_impl(x).backward(g)
+    fe = ref.feature_extractor
+    torch.relu(fe[4](torch.relu(fe[2](torch.relu(fe[0](x.float())))))).backward(g)
+    for mine, theirs in ((fe[0], net.feature_extractor[0]), (fe[2], net.feature_extractor[2]),
+                         (fe[4], net.feature_extractor[4])):
+        for a, b in ((theirs.weight.grad, mine.weight.grad), (theirs.bias.grad, mine.bias.grad)):
+            scale = b.abs().max().item()
+            assert (a - b).abs().max().item() <= 1e-4 * scale + 1e-6

@@ -1,0 +1,121 @@
+"""End-to-end parity of the product API (ppo.PPO / buffer.RolloutStorage) on the GPU
+against the reference's own recorded runs (tests/golden/train_ppo.npz) and the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import models as OM
+from oracle.algos import OraclePPO
+from replay_env import ReplayVecEnv, space_from_code
+
+pytestmark = pytest.mark.gpu
+
+
+def _load_weights(module, f, prefix):
+    sd = module.state_dict()
+    with torch.no_grad():
+        for k, v in sd.items():
+            v.copy_(torch.from_numpy(f[prefix + k]).to(v.device))
+
+
+@pytest.mark.parametrize("name", ["disc2", "disc4sat", "disc18"])
+def test_ppo_train_matches_reference_run(golden, name):
+    """Same rollout + same weights + same numpy seed => product train() reproduces the
+    reference's post-update weights (ppo.py:200-259)."""
+    import ppo
+    import env as E
+    f = golden("train_ppo")
+    p = name + "_"
+    D, N, T, B, E_, H, seed, code = (int(x) for x in f[p + "cfg"])
+    # oracle regenerates the reference rollout bit-for-bit (pinned by test_oracle_golden)
+    renv = ReplayVecEnv(f[p + "env_obs"], f[p + "env_rew"], f[p + "env_done"], space_from_code(code))
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    orc = OraclePPO(renv, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H, max_grad_norm=0.5,
+                    ent_coef=0.01, vf_coef=1.0)
+    if name == "disc4sat":
+        with torch.no_grad():
+            orc.net.actor[-1].weight.mul_(60.0)
+    orc.collect()
+    ro_ref = orc.rollout
+    # product on the GPU
+    np.random.seed(seed)  # RolloutStorage draws randn(16, D) at construction (buffer.py:137)
+    denv = E.DeviceVecEnv("custom", N, obs_dim=D, action_space=E.Discrete(code))
+    alg = ppo.PPO(env_id="custom", env=denv, n_envs=N, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H,
+                  max_grad_norm=0.5, ent_coef=0.01, vf_coef=1.0, quiet=True)
+    _load_weights(alg.policy.net, f, p + "w0_")
+    ro = alg.rollout
+    for t in range(T):
+        ro.add(ro_ref.obs[t], ro_ref.actions[t], ro_ref.rewards[t], ro_ref.values[t], ro_ref.masks[t],
+               ro_ref.log_probs[t])
+    ro.compute_returns_and_advantages(ro_ref.values[T - 1], ro_ref.masks[T - 1])
+    np.testing.assert_array_equal(ro.advantages.cpu().numpy(), ro_ref.adv)
+    alg.train()
+    sd = alg.policy.net.state_dict()
+    for k, v in sd.items():
+        np.testing.assert_allclose(v.cpu().numpy(), f[p + "w1_" + k], rtol=2e-5, atol=2e-6, err_msg=k)
+    acc = alg.loss_accum.cpu().numpy()
+    n = acc[5]
+    np.testing.assert_allclose(acc[0] / n, f[p + "policy_gradient_loss"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(acc[1] / n, f[p + "value_loss"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(acc[2] / n, f[p + "entropy_loss"], rtol=1e-4, atol=1e-6)
+
+
+def test_get_yields_reference_minibatches(golden):
+    """buffer.get(): same permutation + env-major order as buffer.py:233-267."""
+    import buffer
+    import env as E
+    f = golden("get_perm")
+    p = "c0_"
+    T, N, D, B, Ep, seed = (int(x) for x in f[p + "cfg"])
+    np.random.seed(seed)
+    st = buffer.RolloutStorage(T, N, E.Box((D,)), E.Discrete(4))
+    obs = np.arange(T * N * D, dtype=np.float32).reshape(T, N, D)
+    for t in range(T):
+        st.add(obs[t], np.full((N, 1), t), np.zeros(N, np.float32), np.arange(N, dtype=np.float32) + 100 * t,
+               np.zeros(N, bool), np.full((N, 1), float(t)))
+    st.compute_returns_and_advantages(np.zeros(N, np.float32), np.zeros(N, bool))
+    mb = 0
+    for _ in range(Ep):
+        for b in st.get(B):
+            np.testing.assert_array_equal(b.observations.cpu().numpy(), f[p + f"obs{mb}"])
+            np.testing.assert_array_equal(b.actions.cpu().numpy(), f[p + f"act{mb}"])
+            np.testing.assert_array_equal(b.old_values.cpu().numpy(), f[p + f"oldv{mb}"])
+            np.testing.assert_array_equal(b.old_log_probs.cpu().numpy(), f[p + f"oldlp{mb}"])
+            np.testing.assert_array_equal(b.advantages.cpu().numpy(), f[p + f"adv{mb}"])
+            np.testing.assert_array_equal(b.returns.cpu().numpy(), f[p + f"ret{mb}"])
+            mb += 1
+    assert mb == int(f[p + "nmb"])
+
+
+def test_nature_cnn_forward_matches_oracle(golden):
+    import models
+    f = golden("cnn")
+    torch.manual_seed(51)
+    net = models.CnnActorCritic(4, 4)
+    models.FlatParams(net, "cuda")
+    x = torch.from_numpy(f["x"]).cuda()
+    with torch.no_grad():
+        logits, v, _ = net(x)
+    np.testing.assert_allclose(logits.cpu().numpy(), f["logits"], rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(v.cpu().numpy(), f["value"][:, 0], rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("algo", ["PPO", "PPO_RND", "PPO_ICM"])
+def test_atari_iteration_runs(algo):
+    """One tiny Breakout/Montezuma iteration through every kernel: finite losses, params move."""
+    import ppo
+    import logger
+    cls = getattr(ppo, algo)
+    env_id = "MontezumaRevengeNoFrameskip-v4" if algo == "PPO_RND" else "BreakoutNoFrameskip-v4"
+    kw = dict(rnd_start=4) if algo == "PPO_RND" else {}
+    alg = cls(env_id=env_id, n_envs=8, nstep=16, batch_size=32, n_epochs=2, quiet=True, seed=3, **kw)
+    w0 = alg.flat.data.clone()
+    logger.configure("t", env_id, quiet=True)
+    alg.collect_samples()
+    assert torch.isfinite(alg.rollout.advantages).all()
+    alg.train()
+    acc = alg.loss_accum.cpu().numpy()
+    assert acc[5] == 2 * 4 and np.isfinite(acc[:5]).all()
+    assert not torch.equal(w0, alg.flat.data)
+    alg.collect_samples()  # second rollout continues from slot T
