@@ -171,19 +171,39 @@ int ppox_vec_env_step(float* obs, const int32_t* actions, int64_t N, int32_t D,
                       int32_t* ep_len, float* done_ret, int32_t* done_len, void* stream);
 
 /* ---------------------------------------------------------------------------
- * K6  NatureCNN convolutions (checkpoint models-checkpoint.py:52-58) as fp32
- * MFMA implicit GEMMs with fused bias + ReLU.
+ * K6  NatureCNN convolutions (checkpoint models-checkpoint.py:52-58) and their
+ * backward, as fp32 MFMA implicit GEMMs (v_mfma_f32_32x32x2_f32).
  *   layer 1: x = uint8 frames (batch, 4, 84, 84) [or rollout rows through idx:
  *            sample b = step-major row (idx[b] % T, idx[b] / T) of a (T, N_env, ...)
  *            array] -> y (batch, 20, 20, 32) f32 NHWC
  *   layer 2: x (batch, 20, 20, 32) NHWC -> y (batch, 9, 9, 64) NHWC
  *   layer 3: x (batch, 9, 9, 64) NHWC -> y (batch, 64, 7, 7) NCHW (Flatten order)
- * wp = weights packed by ppox_nature_pack_weights (PyTorch [co][ci][ky][kx] in). */
+ * Forward fuses + bias and ReLU.  Weights are PyTorch [co][ci][ky][kx]; the
+ * kernels read copies packed by ppox_nature_pack_weights (once per optimizer
+ * step): wp1 [256][32], wp2 [512][64], wp3 [576][64] (forward), wpd2 [4][256][32],
+ * wpd3 [576][64] (dgrad; nullable if no backward is needed).
+ * -------------------------------------------------------------------------*/
 int ppox_nature_pack_weights(const float* w1, const float* w2, const float* w3, float* wp1,
-                             float* wp2, float* wp3, void* stream);
+                             float* wp2, float* wp3, float* wpd2, float* wpd3, void* stream);
 int ppox_nature_conv_fwd(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
                          int64_t T, int64_t N_env, int64_t x_sample_stride, const float* wp,
                          const float* bias, float* y, void* stream);
+/* grad_in (NHWC, layer input shape) = conv_transpose(grad_out NHWC, W) * (prev_act > 0):
+ * the ReLU backward of the previous layer is fused (prev_act = its NHWC output). */
+int ppox_nature_conv_dgrad(int32_t layer, const float* grad_out, int64_t batch, const float* wpd,
+                           const float* prev_act, float* grad_in, void* stream);
+/* dW (PyTorch layout) and db from the layer input x (as in ppox_nature_conv_fwd) and
+ * the ReLU-masked output grad (NHWC).  Split-K over pixels into a workspace of
+ * ppox_nature_wgrad_workspace_bytes(layer, batch), reduced in a fixed order. */
+int64_t ppox_nature_wgrad_splits(int32_t layer, int64_t batch);
+int64_t ppox_nature_wgrad_workspace_bytes(int32_t layer, int64_t batch);
+int ppox_nature_conv_wgrad(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
+                           int64_t T, int64_t N_env, int64_t x_sample_stride,
+                           const float* grad_out, void* workspace, int64_t workspace_bytes,
+                           float* dw, float* db, void* stream);
+/* (batch, 64, 7, 7) NCHW grad of the trunk output -> NHWC, times (act > 0). */
+int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, int64_t batch, float* out,
+                                void* stream);
 
 #ifdef __cplusplus
 }

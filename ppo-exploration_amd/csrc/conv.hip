@@ -1,23 +1,34 @@
 // K6 — NatureCNN convolutions as implicit GEMMs on the fp32 matrix cores
-// (v_mfma_f32_32x32x2_f32: exact f32 FMAs, the gfx950 fp32 matrix rate,
-// 157 TF/s dense).  Replaces torch.nn.Conv2d + ReLU of
-// .ipynb_checkpoints/models-checkpoint.py:52-58 (conv1 4->32 k8 s4,
-// conv2 32->64 k4 s2, conv3 64->64 k3 s1 on 84x84x4 frames).
+// (v_mfma_f32_32x32x2_f32: exact f32 FMAs at the gfx950 fp32 matrix rate,
+// 157 TF/s dense).  Replaces torch.nn.Conv2d + ReLU (forward) and their
+// autograd (backward) of .ipynb_checkpoints/models-checkpoint.py:52-58:
+//   conv1 4->32 k8 s4 (84x84 -> 20x20), conv2 32->64 k4 s2 (-> 9x9),
+//   conv3 64->64 k3 s1 (-> 7x7).
 //
-// GEMM view of one layer: M = batch*OH*OW output pixels, N = COUT, K = CIN*KH*KW.
-//   A[m][k]  im2col of the input, gathered on the fly (never materialised)
-//   B[k][co] weights, pre-packed once per optimizer step into the kernel's K order
-// One 256-thread workgroup owns BM = 128 output pixels x all COUT channels; each
-// wave 32 pixels x COUT (COUT/32 MFMA tiles).  K is walked in BK = 32 chunks,
-// register-staged and double-buffered in LDS (one barrier per chunk), so the
-// global gathers of chunk c+1 fly under the MFMAs of chunk c.
-// Epilogue fuses + bias and ReLU and writes NHWC (conv1, conv2 — the next
-// layer's gather reads 128-B channel rows) or NCHW (conv3 — the reference's
-// Flatten order feeding Linear(3136, 512)).
+// Activation layout: NHWC between layers (a 32-channel run = one 128-byte row
+// segment, so every im2col gather is coalesced); the trunk output is NCHW (the
+// reference's Flatten order feeding Linear(3136, 512)).  conv1 reads the uint8
+// frame stack (N, 4, 84, 84) directly: the torch.FloatTensor(obs) conversion is
+// fused (u8 -> f32 is exact), and so is the minibatch gather (rows via idx).
 //
-// Input layouts: conv1 reads the uint8 frame stack (N, 4, 84, 84) directly (the
-// reference's torch.FloatTensor(obs) conversion is fused: u8 -> f32 is exact),
-// through an env-major index list when given (the minibatch gather is fused too).
+// Forward / dgrad: M = output rows, N = channels, K = taps x channels.  One
+// 256-thread workgroup owns BM = 128 rows x all N channels; each wave 32 rows
+// (N/32 MFMA tiles).  K is walked in BK = 32 chunks, register-staged and
+// double-buffered in LDS (one barrier per chunk) so the gathers of chunk c+1 fly
+// under the MFMAs of chunk c.  Each thread's four staged rows are fixed for the
+// whole K walk, so their base addresses are computed once.
+//   forward epilogue: + bias, ReLU
+//   dgrad epilogue:   x (previous activation > 0) — the previous layer's ReLU
+//                     backward is fused, the result is that layer's output grad
+//   conv2 dgrad (stride 2) runs as 4 parity classes of the input grid, each a
+//   dense GEMM over its 2x2 contributing taps (no zero MACs).
+// Wgrad: dW[k][co] = sum_m A[m][k] G[m][co] — a GEMM whose reduction runs over
+// all output pixels.  Workgroups own a K-block and a slice of M (split-K over
+// pixels), write partial slabs, and a reduce kernel sums the slabs in a FIXED
+// order (deterministic) straight into the PyTorch [co][ci][ky][kx] layout; the
+// bias gradient is fused into the k-block-0 workgroups.  The k-blocks of one
+// M-slice are mapped to one XCD (blockIdx % 8) so their shared G rows and
+// overlapping input patches are served from that XCD's L2.
 #include "common.h"
 
 namespace {
@@ -28,79 +39,54 @@ constexpr int BM = 128;
 constexpr int BK = 32;
 constexpr int AST = BK + 1;  // padded LDS row stride (floats): conflict-free column reads
 
-struct ConvArgs {
-    const void* x;          // input activations
-    const long long* idx;   // optional env-major row indices (conv1 only): sample b = rollout row idx[b]
-    long long T, Nenv;      // rollout dims for idx mapping
-    long long x_sample_stride;  // elements between samples when idx == nullptr
-    const float* wp;        // packed weights [K][COUT]
-    const float* bias;      // [COUT]
-    float* y;               // output
-    long long batch;        // samples
-};
-
-template <int CIN_, int IH_, int IW_, int KH_, int KW_, int S_, int COUT_, bool IN_U8_NCHW, bool OUT_NCHW>
-struct Layer {
+template <int CIN_, int IH_, int IW_, int KH_, int KW_, int S_, int COUT_>
+struct Geo {
     static constexpr int CIN = CIN_, IH = IH_, IW = IW_, KH = KH_, KW = KW_, S = S_, COUT = COUT_;
-    static constexpr bool OUT_NCHW_ = OUT_NCHW;
-    static constexpr int OH = (IH - KH) / S + 1;
-    static constexpr int OW = (IW - KW) / S + 1;
-    static constexpr int P = OH * OW;
+    static constexpr int OH = (IH - KH) / S + 1, OW = (IW - KW) / S + 1, P = OH * OW;
     static constexpr int K = CIN * KH * KW;
-    static constexpr int NCHUNK = K / BK;
-    static constexpr int NT = COUT / 32;
-    static_assert(K % BK == 0, "K must be a multiple of BK");
-    static_assert(COUT % 32 == 0, "COUT must be a multiple of 32");
+};
+using G1 = Geo<4, 84, 84, 8, 8, 4, 32>;
+using G2 = Geo<32, 20, 20, 4, 4, 2, 64>;
+using G3 = Geo<64, 9, 9, 3, 3, 1, 64>;
+
+struct Args {
+    const void* x;            // forward input / dgrad: output grad G (NHWC)
+    const long long* idx;     // conv1 forward/wgrad: optional env-major rollout rows
+    long long T, Nenv;        // rollout dims for idx
+    long long sample_stride;  // conv1 input: bytes between samples (idx == nullptr)
+    const float* wp;          // packed weights [K][N]
+    const float* bias;        // forward bias
+    const float* mask;        // dgrad: previous activation (ReLU mask source)
+    float* y;                 // output
+    long long batch;
 };
 
-// ---- A staging: global -> registers -> LDS -----------------------------------
-// f32 NHWC input: K order (ky, kx, ci); a chunk is 32 consecutive channels of one
-// (ky, kx) tap, i.e. one 128-byte row segment per output pixel.
-template <class L>
-struct StageF32 {
-    float4 r[4];
-    __device__ inline void load(const ConvArgs& a, long long m0, long long M, int chunk) {
-        constexpr int CPT = L::CIN / BK;  // chunks per tap
-        const int tap = chunk / CPT, ci0 = (chunk % CPT) * BK;
-        const int ky = tap / L::KW, kx = tap % L::KW;
-        const float* x = reinterpret_cast<const float*>(a.x);
+__device__ inline f32x16 zero16() {
+    f32x16 z;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int w = i * 256 + threadIdx.x;
-            const int row = w >> 3, q = w & 7;
-            const long long m = m0 + row;
-            if (m < M) {
-                const long long n = m / L::P;
-                const int p = (int)(m - n * L::P);
-                const int oy = p / L::OW, ox = p % L::OW;
-                const float* src = x + ((n * L::IH + (oy * L::S + ky)) * L::IW + (ox * L::S + kx)) * L::CIN + ci0;
-                r[i] = reinterpret_cast<const float4*>(src)[q];
-            } else {
-                r[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-        }
-    }
-    __device__ inline void store(float* As) const {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int w = i * 256 + threadIdx.x;
-            const int row = w >> 3, q = w & 7;
-            float* d = As + row * AST + q * 4;
-            d[0] = r[i].x;
-            d[1] = r[i].y;
-            d[2] = r[i].z;
-            d[3] = r[i].w;
-        }
-    }
-};
+    for (int i = 0; i < 16; ++i) z[i] = 0.f;
+    return z;
+}
 
-// u8 NCHW frame input (conv1): K order (ci, ky, kx) = the weight's own order; a
-// chunk is one channel x 4 kernel rows x 8 columns: 4 runs of 8 bytes per pixel.
-template <class L>
-struct StageU8 {
+__device__ inline long long u8_sample_base(const Args& a, long long n, long long sample_bytes) {
+    if (a.idx) {
+        const long long i = a.idx[n];
+        return ((i % a.T) * a.Nenv + i / a.T) * sample_bytes;
+    }
+    return n * a.sample_stride;
+}
+
+// ---------------------------------------------------------------------------
+// A stagers: global -> registers (load) -> LDS (store), 4 slots per thread.
+// Slot i of thread t covers element w = i*256 + t of the BM x BK chunk.
+// ---------------------------------------------------------------------------
+// conv1 forward: uint8 NCHW frames, K order (ci, ky, kx); chunk = 1 channel x 4
+// kernel rows x 8 columns -> 4 runs of 8 bytes per row (2 words each).
+struct StageFwd1 {
+    using L = G1;
+    const uint8_t* base[4];
     uint32_t r[4];
-    __device__ inline void load(const ConvArgs& a, long long m0, long long M, int chunk) {
-        const int ci = chunk / (L::KH / 4), ky0 = (chunk % (L::KH / 4)) * 4;
+    __device__ StageFwd1(const Args& a, long long m0, long long M) {
         const uint8_t* x = reinterpret_cast<const uint8_t*>(a.x);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -109,21 +95,18 @@ struct StageU8 {
             const long long m = m0 + row;
             if (m < M) {
                 const long long n = m / L::P;
-                const int p = (int)(m - n * L::P);
-                const int oy = p / L::OW, ox = p % L::OW;
-                long long base;
-                if (a.idx) {
-                    const long long i_env = a.idx[n];
-                    base = ((i_env % a.T) * a.Nenv + i_env / a.T) * (long long)(L::CIN * L::IH * L::IW);
-                } else {
-                    base = n * a.x_sample_stride;
-                }
-                const uint8_t* src = x + base + (ci * L::IH + oy * L::S + ky0 + seg) * L::IW + ox * L::S + half * 4;
-                r[i] = *reinterpret_cast<const uint32_t*>(src);
+                const int p = (int)(m - n * L::P), oy = p / L::OW, ox = p % L::OW;
+                base[i] = x + u8_sample_base(a, n, (long long)L::CIN * L::IH * L::IW) + (oy * L::S + seg) * L::IW +
+                          ox * L::S + half * 4;
             } else {
-                r[i] = 0u;
+                base[i] = nullptr;
             }
         }
+    }
+    __device__ inline void load(int chunk) {
+        const int off = (chunk >> 1) * (L::IH * L::IW) + (chunk & 1) * 4 * L::IW;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = base[i] ? *reinterpret_cast<const uint32_t*>(base[i] + off) : 0u;
     }
     __device__ inline void store(float* As) const {
 #pragma unroll
@@ -139,14 +122,113 @@ struct StageU8 {
     }
 };
 
+// NHWC f32 forward (conv2, conv3): K order (ky, kx, ci); chunk = 32 channels of one tap.
 template <class L>
-struct StageB {
-    static constexpr int V = BK * L::COUT / 4 / 256;  // float4 per thread
-    float4 r[V];
-    __device__ inline void load(const float* wp, int chunk) {
-        const float4* src = reinterpret_cast<const float4*>(wp + (long long)chunk * BK * L::COUT);
+struct StageFwdNHWC {
+    const float* base[4];
+    float4 r[4];
+    __device__ StageFwdNHWC(const Args& a, long long m0, long long M) {
+        const float* x = reinterpret_cast<const float*>(a.x);
 #pragma unroll
-        for (int i = 0; i < V; ++i) r[i] = src[i * 256 + threadIdx.x];
+        for (int i = 0; i < 4; ++i) {
+            const int w = i * 256 + threadIdx.x;
+            const int row = w >> 3, q = w & 7;
+            const long long m = m0 + row;
+            if (m < M) {
+                const long long n = m / L::P;
+                const int p = (int)(m - n * L::P), oy = p / L::OW, ox = p % L::OW;
+                base[i] = x + ((n * L::IH + oy * L::S) * L::IW + ox * L::S) * L::CIN + q * 4;
+            } else {
+                base[i] = nullptr;
+            }
+        }
+    }
+    __device__ inline void load(int chunk) {
+        constexpr int CPT = L::CIN / BK;
+        const int tap = chunk / CPT, ky = tap / L::KW, kx = tap % L::KW;
+        const int off = (ky * L::IW + kx) * L::CIN + (chunk % CPT) * BK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            r[i] = base[i] ? *reinterpret_cast<const float4*>(base[i] + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __device__ inline void store(float* As) const {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int w = i * 256 + threadIdx.x;
+            float* d = As + (w >> 3) * AST + (w & 7) * 4;
+            d[0] = r[i].x;
+            d[1] = r[i].y;
+            d[2] = r[i].z;
+            d[3] = r[i].w;
+        }
+    }
+};
+
+// dgrad (transposed conv) gather of the output grad G (NHWC, OH x OW x COUT).
+// Rows are input pixels of one parity class (py, px): iy = S*jy + py.  Taps are
+// the TY x TX kernel offsets ky = py + S*ty contributing to that class; the
+// source pixel is oy = jy - ty, ox = jx - tx, zero outside the output grid.
+// K' order (ty, tx, co); chunk = 32 output channels of one tap.
+template <class L>
+struct StageDgrad {
+    static constexpr int JH = L::IH / L::S, JW = L::IW / L::S;  // class grid
+    static constexpr int TY = L::KH / L::S, TX = L::KW / L::S;  // taps per class
+    const float* base[4];
+    int jy[4], jx[4];
+    float4 r[4];
+    __device__ StageDgrad(const Args& a, long long m0, long long M) {
+        const float* g = reinterpret_cast<const float*>(a.x);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int w = i * 256 + threadIdx.x;
+            const int row = w >> 3, q = w & 7;
+            const long long m = m0 + row;
+            if (m < M) {
+                const long long n = m / (JH * JW);
+                const int p = (int)(m - n * (JH * JW));
+                jy[i] = p / JW;
+                jx[i] = p % JW;
+                base[i] = g + n * (L::P * L::COUT) + q * 4;
+            } else {
+                base[i] = nullptr;
+                jy[i] = jx[i] = -100;
+            }
+        }
+    }
+    __device__ inline void load(int chunk) {
+        constexpr int CPT = L::COUT / BK;
+        const int tap = chunk / CPT, ty = tap / TX, tx = tap % TX;
+        const int co0 = (chunk % CPT) * BK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int oy = jy[i] - ty, ox = jx[i] - tx;
+            const bool ok = base[i] && oy >= 0 && oy < L::OH && ox >= 0 && ox < L::OW;
+            r[i] = ok ? *reinterpret_cast<const float4*>(base[i] + (oy * L::OW + ox) * L::COUT + co0)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    __device__ inline void store(float* As) const {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int w = i * 256 + threadIdx.x;
+            float* d = As + (w >> 3) * AST + (w & 7) * 4;
+            d[0] = r[i].x;
+            d[1] = r[i].y;
+            d[2] = r[i].z;
+            d[3] = r[i].w;
+        }
+    }
+};
+
+template <int NOUT>
+struct StageB {
+    static constexpr int V = BK * NOUT / 4 / 256;  // float4 per thread
+    const float4* src;
+    float4 r[V];
+    __device__ explicit StageB(const float* wp) : src(reinterpret_cast<const float4*>(wp)) {}
+    __device__ inline void load(int chunk) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) r[i] = src[(long long)chunk * (BK * NOUT / 4) + i * 256 + threadIdx.x];
     }
     __device__ inline void store(float* Bs) const {
 #pragma unroll
@@ -154,113 +236,395 @@ struct StageB {
     }
 };
 
-template <class L, class SA>
-__global__ void __launch_bounds__(256, 2) conv_fwd_kernel(ConvArgs a) {
+// ---------------------------------------------------------------------------
+// Problems: row count, stager, packed-B pointer, chunk count, epilogue.
+// ---------------------------------------------------------------------------
+template <class L, class SA, bool OUT_NCHW>
+struct FwdProblem {
+    static constexpr int NOUT = L::COUT, NCHUNK = L::K / BK;
+    using Stager = SA;
+    __device__ static long long rows(const Args& a) { return a.batch * L::P; }
+    __device__ static const float* bpack(const Args& a) { return a.wp; }
+    __device__ static void store(const Args& a, long long m, int co, float acc) {
+        const float v = fmaxf(acc + a.bias[co], 0.f);
+        if constexpr (OUT_NCHW) {
+            const long long n = m / L::P;
+            a.y[(n * L::COUT + co) * L::P + (m - n * L::P)] = v;
+        } else {
+            a.y[m * L::COUT + co] = v;
+        }
+    }
+};
+
+// dgrad of layer L: output = grad of L's input (NHWC IH x IW x CIN), masked by
+// the previous activation (a.mask, same layout).  blockIdx.y = parity class.
+template <class L>
+struct DgradProblem {
+    using St = StageDgrad<L>;
+    static constexpr int NOUT = L::CIN, NCHUNK = St::TY * St::TX * L::COUT / BK;
+    using Stager = St;
+    __device__ static long long rows(const Args& a) { return a.batch * St::JH * St::JW; }
+    __device__ static const float* bpack(const Args& a) {
+        return a.wp + (long long)blockIdx.y * (St::TY * St::TX * L::COUT) * L::CIN;
+    }
+    __device__ static void store(const Args& a, long long m, int ci, float acc) {
+        const long long n = m / (St::JH * St::JW);
+        const int p = (int)(m - n * (St::JH * St::JW));
+        const int py = blockIdx.y / L::S, px = blockIdx.y % L::S;
+        const int iy = (p / St::JW) * L::S + py, ix = (p % St::JW) * L::S + px;
+        const long long o = ((n * L::IH + iy) * L::IW + ix) * L::CIN + ci;
+        a.y[o] = a.mask[o] > 0.f ? acc : 0.f;
+    }
+};
+
+template <class Prob>
+__global__ void __launch_bounds__(256, 2) igemm_kernel(Args a) {
+    constexpr int NOUT = Prob::NOUT, NT = NOUT / 32, NCHUNK = Prob::NCHUNK;
     __shared__ float As[2][BM * AST];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BK * L::COUT];
-    const long long M = a.batch * L::P;
+    __shared__ __attribute__((aligned(16))) float Bs[2][BK * NOUT];
+    const long long M = Prob::rows(a);
     const long long m0 = (long long)blockIdx.x * BM;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
-    f32x16 acc[L::NT];
+    f32x16 acc[NT];
 #pragma unroll
-    for (int j = 0; j < L::NT; ++j) acc[j] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NT; ++j) acc[j] = zero16();
 
-    SA sa;
-    StageB<L> sb;
-    sa.load(a, m0, M, 0);
-    sb.load(a.wp, 0);
+    typename Prob::Stager sa(a, m0, M);
+    StageB<NOUT> sb(Prob::bpack(a));
+    sa.load(0);
+    sb.load(0);
     sa.store(As[0]);
     sb.store(Bs[0]);
     __syncthreads();
 
     const int arow = wave * 32 + (lane & 31);
     const int khalf = lane >> 5;
-    for (int c = 0; c < L::NCHUNK; ++c) {
+    for (int c = 0; c < NCHUNK; ++c) {
         const int cur = c & 1;
-        if (c + 1 < L::NCHUNK) {
-            sa.load(a, m0, M, c + 1);
-            sb.load(a.wp, c + 1);
+        if (c + 1 < NCHUNK) {
+            sa.load(c + 1);
+            sb.load(c + 1);
         }
         const float* A = As[cur] + arow * AST + khalf;
-        const float* B = Bs[cur] + khalf * L::COUT + (lane & 31);
+        const float* B = Bs[cur] + khalf * NOUT + (lane & 31);
 #pragma unroll
         for (int kk = 0; kk < BK / 2; ++kk) {
             const float av = A[kk * 2];
 #pragma unroll
-            for (int j = 0; j < L::NT; ++j) {
-                const float bv = B[kk * 2 * L::COUT + j * 32];
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[j], 0, 0, 0);
-            }
+            for (int j = 0; j < NT; ++j)
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, B[kk * 2 * NOUT + j * 32], acc[j], 0, 0, 0);
         }
-        if (c + 1 < L::NCHUNK) {
+        if (c + 1 < NCHUNK) {
             sa.store(As[cur ^ 1]);
             sb.store(Bs[cur ^ 1]);
         }
         __syncthreads();
     }
-
-    // epilogue: bias + ReLU, C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    // C/D map: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
 #pragma unroll
-    for (int j = 0; j < L::NT; ++j) {
-        const int co = j * 32 + (lane & 31);
-        const float b = a.bias[co];
+    for (int j = 0; j < NT; ++j) {
+        const int col = j * 32 + (lane & 31);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            const long long m = m0 + row;
-            if (m < M) {
-                const float v = fmaxf(acc[j][r] + b, 0.f);
-                if constexpr (L::OUT_NCHW_) {
-                    const long long n = m / L::P;
-                    const int p = (int)(m - n * L::P);
-                    a.y[(n * L::COUT + co) * L::P + p] = v;
-                } else {
-                    a.y[m * L::COUT + co] = v;
-                }
-            }
+            const long long m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            if (m < M) Prob::store(a, m, col, acc[j][r]);
         }
     }
 }
 
-// pack PyTorch weights [COUT][CIN][KH][KW] into [K][COUT] in the kernel's K order
-template <int CIN, int KH, int KW, int COUT, bool NHWC_ORDER>
-__global__ void pack_kernel(const float* __restrict__ w, float* __restrict__ wp) {
-    constexpr int K = CIN * KH * KW;
+// ---------------------------------------------------------------------------
+// Wgrad.  WG = (k-block of KT rows of K) x (all COUT) x (slice of output pixels).
+// Per step of MS = 32 pixels: stage X[32][KT] (im2col) and G[32][COUT] in LDS,
+// then D(k x co) += X^T G on the MFMA (A operand = X^T: lane i <-> k, kk <-> pixel).
+// ---------------------------------------------------------------------------
+constexpr int MS = 32;
+
+template <class L, bool U8>
+struct WgCfg {
+    static constexpr int KT = (L::COUT == 32) ? 128 : 64;  // 4 tiles of 32x32 per WG
+    static constexpr int KB = L::K / KT;
+    static constexpr int XST = KT + 1, GST = L::COUT + 1;
+};
+
+struct WArgs {
+    const void* x;          // layer input (u8 frames for conv1, NHWC f32 otherwise)
+    const long long* idx;   // conv1: optional env-major rollout rows
+    long long T, Nenv, sample_stride;
+    const float* g;         // output grad, NHWC (batch, OH, OW, COUT), ReLU mask already applied
+    float* slab;            // [splits][K][COUT]
+    float* bslab;           // [splits][COUT]
+    long long batch;
+    long long px_per_split;
+    int splits;
+};
+
+template <class L, bool U8>
+__global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
+    using C = WgCfg<L, U8>;
+    constexpr int KT = C::KT, KB = C::KB, XST = C::XST, GST = C::GST, COUT = L::COUT;
+    __shared__ float Xs[2][MS * XST];
+    __shared__ float Gs[2][MS * GST];
+    // XCD-aware block -> (split, kb): the KB k-blocks of a split share blockIdx % 8
+    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+    const int kb = q % KB, split = (q / KB) * 8 + xcd;
+    const long long M = a.batch * L::P;
+    const long long mbeg = (long long)split * a.px_per_split;
+    const long long mend = min(M, mbeg + a.px_per_split);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int kt = (COUT == 32) ? wave : (wave >> 1), ct = (COUT == 32) ? 0 : (wave & 1);
+    f32x16 acc = zero16();
+
+    // staging geometry (per thread, fixed across steps)
+    constexpr int XV = MS * KT / 4 / 256;  // 4-element units per thread for X (float4 or u32)
+    constexpr int GV = MS * COUT / 4 / 256;
+    float4 xr[XV];
+    uint32_t xu[XV];
+    float4 gr[GV];
+    float bsum[GV][4];
+#pragma unroll
+    for (int j = 0; j < GV; ++j) bsum[j][0] = bsum[j][1] = bsum[j][2] = bsum[j][3] = 0.f;
+
+    auto load = [&](long long ms) {
+#pragma unroll
+        for (int i = 0; i < XV; ++i) {
+            const int w = i * 256 + threadIdx.x;
+            const long long m = ms + w / (KT / 4);
+            const int u = w % (KT / 4);  // 4-element unit within the pixel's KT k-values
+            if (m < mend) {
+                const long long n = m / L::P;
+                const int p = (int)(m - n * L::P), oy = p / L::OW, ox = p % L::OW;
+                if constexpr (U8) {
+                    // k = kb*128 + u*4 + e: ci = k / 64, ky = (k / 8) % 8, kx = k % 8 (kx run of 4)
+                    const int k = kb * KT + u * 4;
+                    const int ci = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
+                    const uint8_t* x = reinterpret_cast<const uint8_t*>(a.x);
+                    long long base;
+                    if (a.idx) {
+                        const long long ie = a.idx[n];
+                        base = ((ie % a.T) * a.Nenv + ie / a.T) * (long long)(L::CIN * L::IH * L::IW);
+                    } else {
+                        base = n * a.sample_stride;
+                    }
+                    xu[i] = *reinterpret_cast<const uint32_t*>(
+                        x + base + (ci * L::IH + oy * L::S + ky) * L::IW + ox * L::S + kx);
+                } else {
+                    // k = (ky, kx, ci) NHWC order
+                    const int k = kb * KT + u * 4;
+                    const int tap = k / L::CIN, ci = k % L::CIN, ky = tap / L::KW, kx = tap % L::KW;
+                    const float* x = reinterpret_cast<const float*>(a.x);
+                    xr[i] = *reinterpret_cast<const float4*>(
+                        x + ((n * L::IH + oy * L::S + ky) * L::IW + ox * L::S + kx) * L::CIN + ci);
+                }
+            } else {
+                xr[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+                xu[i] = 0u;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < GV; ++j) {
+            const int w = j * 256 + threadIdx.x;
+            const long long m = ms + w / (COUT / 4);
+            gr[j] = m < mend ? reinterpret_cast<const float4*>(a.g + m * COUT)[w % (COUT / 4)]
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < XV; ++i) {
+            const int w = i * 256 + threadIdx.x;
+            float* d = Xs[buf] + (w / (KT / 4)) * XST + (w % (KT / 4)) * 4;
+            if constexpr (U8) {
+                d[0] = (float)(xu[i] & 0xFFu);
+                d[1] = (float)((xu[i] >> 8) & 0xFFu);
+                d[2] = (float)((xu[i] >> 16) & 0xFFu);
+                d[3] = (float)(xu[i] >> 24);
+            } else {
+                d[0] = xr[i].x;
+                d[1] = xr[i].y;
+                d[2] = xr[i].z;
+                d[3] = xr[i].w;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < GV; ++j) {
+            const int w = j * 256 + threadIdx.x;
+            float* d = Gs[buf] + (w / (COUT / 4)) * GST + (w % (COUT / 4)) * 4;
+            d[0] = gr[j].x;
+            d[1] = gr[j].y;
+            d[2] = gr[j].z;
+            d[3] = gr[j].w;
+            if (kb == 0) {
+                bsum[j][0] += gr[j].x;
+                bsum[j][1] += gr[j].y;
+                bsum[j][2] += gr[j].z;
+                bsum[j][3] += gr[j].w;
+            }
+        }
+    };
+
+    const long long nsteps = mend > mbeg ? (mend - mbeg + MS - 1) / MS : 0;
+    if (nsteps > 0) {
+        load(mbeg);
+        store(0);
+    }
+    __syncthreads();
+    for (long long s = 0; s < nsteps; ++s) {
+        const int cur = (int)(s & 1);
+        if (s + 1 < nsteps) load(mbeg + (s + 1) * MS);
+        const float* X = Xs[cur] + (lane >> 5) * XST + kt * 32 + (lane & 31);
+        const float* G = Gs[cur] + (lane >> 5) * GST + ct * 32 + (lane & 31);
+#pragma unroll
+        for (int kk = 0; kk < MS / 2; ++kk)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(X[kk * 2 * XST], G[kk * 2 * GST], acc, 0, 0, 0);
+        if (s + 1 < nsteps) store(cur ^ 1);
+        __syncthreads();
+    }
+    // partial slab [split][K][COUT]: row (k) = kb*KT + kt*32 + C-row, col (co) = ct*32 + (lane & 31)
+    float* slab = a.slab + (long long)split * L::K * COUT;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int k = kb * KT + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        slab[k * COUT + ct * 32 + (lane & 31)] = acc[r];
+    }
+    if (kb == 0) {
+        // bias grad partial: column sums of this split's G rows
+        __shared__ float bred[256 / (COUT / 4) * COUT];
+        constexpr int ROWS_PER_PASS = 256 / (COUT / 4);
+        float tot[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < GV; ++j)
+            for (int e = 0; e < 4; ++e) tot[e] += bsum[j][e];
+        const int rgrp = threadIdx.x / (COUT / 4), c4 = threadIdx.x % (COUT / 4);
+        for (int e = 0; e < 4; ++e) bred[rgrp * COUT + c4 * 4 + e] = tot[e];
+        __syncthreads();
+        if (threadIdx.x < COUT) {
+            float s = 0.f;
+            for (int g = 0; g < ROWS_PER_PASS; ++g) s += bred[g * COUT + threadIdx.x];
+            a.bslab[(long long)split * COUT + threadIdx.x] = s;
+        }
+    }
+}
+
+// sum the slabs in split order, scatter to PyTorch [co][ci][ky][kx] (+ bias)
+template <class L, bool NHWC_ORDER>
+__global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ slab, const float* __restrict__ bslab,
+                                                    int splits, float* __restrict__ dw, float* __restrict__ db) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= K * COUT) return;
-    const int k = i / COUT, co = i % COUT;
+    constexpr int KC = L::K * L::COUT;
+    if (i < KC) {
+        float s = 0.f;
+        for (int sp = 0; sp < splits; ++sp) s += slab[(long long)sp * KC + i];
+        const int k = i / L::COUT, co = i % L::COUT;
+        int ci, ky, kx;
+        if (NHWC_ORDER) {
+            ci = k % L::CIN;
+            const int tap = k / L::CIN;
+            ky = tap / L::KW;
+            kx = tap % L::KW;
+        } else {
+            kx = k % L::KW;
+            ky = (k / L::KW) % L::KH;
+            ci = k / (L::KW * L::KH);
+        }
+        dw[((co * L::CIN + ci) * L::KH + ky) * L::KW + kx] = s;
+    } else if (i < KC + L::COUT) {
+        const int co = i - KC;
+        float s = 0.f;
+        for (int sp = 0; sp < splits; ++sp) s += bslab[(long long)sp * L::COUT + co];
+        db[co] = s;
+    }
+}
+
+// conv3 output grad: NCHW (Flatten order) -> NHWC, times the ReLU mask of h3 (NCHW)
+__global__ void __launch_bounds__(256) nchw_to_nhwc_mask(const float* __restrict__ g, const float* __restrict__ h,
+                                                         long long batch, float* __restrict__ out) {
+    __shared__ float t[64 * 50];
+    const long long n = blockIdx.x;
+    const float* gs = g + n * 3136;
+    const float* hs = h + n * 3136;
+    for (int i = threadIdx.x; i < 3136; i += 256) {
+        const int c = i / 49, p = i % 49;
+        t[c * 50 + p] = hs[i] > 0.f ? gs[i] : 0.f;
+    }
+    __syncthreads();
+    float* o = out + n * 3136;
+    for (int i = threadIdx.x; i < 3136; i += 256) {
+        const int p = i / 64, c = i % 64;
+        o[i] = t[c * 50 + p];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// weight packing (once per optimizer step)
+// ---------------------------------------------------------------------------
+// forward: [K][COUT] in the kernel's K order
+template <class L, bool NHWC_ORDER>
+__global__ void pack_fwd(const float* __restrict__ w, float* __restrict__ wp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L::K * L::COUT) return;
+    const int k = i / L::COUT, co = i % L::COUT;
     int ci, ky, kx;
     if (NHWC_ORDER) {
-        ci = k % CIN;
-        const int tap = k / CIN;
-        ky = tap / KW;
-        kx = tap % KW;
+        ci = k % L::CIN;
+        const int tap = k / L::CIN;
+        ky = tap / L::KW;
+        kx = tap % L::KW;
     } else {
-        kx = k % KW;
-        ky = (k / KW) % KH;
-        ci = k / (KW * KH);
+        kx = k % L::KW;
+        ky = (k / L::KW) % L::KH;
+        ci = k / (L::KW * L::KH);
     }
-    wp[i] = w[((co * CIN + ci) * KH + ky) * KW + kx];
+    wp[i] = w[((co * L::CIN + ci) * L::KH + ky) * L::KW + kx];
+}
+
+// dgrad: per parity class (py, px): [(ty, tx, co)][ci], ky = py + S*ty
+template <class L>
+__global__ void pack_dgrad(const float* __restrict__ w, float* __restrict__ wp) {
+    constexpr int TY = L::KH / L::S, TX = L::KW / L::S, KC = TY * TX * L::COUT;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L::S * L::S * KC * L::CIN) return;
+    const int cls = i / (KC * L::CIN), rem = i % (KC * L::CIN);
+    const int kp = rem / L::CIN, ci = rem % L::CIN;
+    const int tap = kp / L::COUT, co = kp % L::COUT;
+    const int ky = cls / L::S + L::S * (tap / TX), kx = cls % L::S + L::S * (tap % TX);
+    wp[i] = w[((co * L::CIN + ci) * L::KH + ky) * L::KW + kx];
+}
+
+template <class Prob>
+int launch_igemm(const Args& a, long long rows, int classes, hipStream_t s, const char* name) {
+    if (rows == 0) return PPOX_OK;
+    igemm_kernel<Prob><<<dim3(ppox::ceil_div(rows, BM), classes), 256, 0, s>>>(a);
+    PPOX_LAUNCHED(name);
+}
+
+template <class L, bool U8, bool NHWC_ORDER>
+int launch_wgrad(const WArgs& wa_in, float* dw, float* db, hipStream_t s) {
+    WArgs wa = wa_in;
+    using C = WgCfg<L, U8>;
+    const long long M = wa.batch * L::P;
+    const int splits = wa.splits;
+    wa.px_per_split = (M + splits - 1) / splits;
+    wgrad_kernel<L, U8><<<(unsigned)(C::KB * splits), 256, 0, s>>>(wa);
+    wgrad_reduce<L, NHWC_ORDER><<<ppox::ceil_div(L::K * L::COUT + L::COUT, 256), 256, 0, s>>>(
+        wa.slab, wa.bslab, splits, dw, db);
+    PPOX_LAUNCHED("ppox_nature_conv_wgrad");
 }
 
 }  // namespace
 
-namespace {
-using Conv1 = Layer<4, 84, 84, 8, 8, 4, 32, true, false>;   // -> (B, 20, 20, 32) NHWC
-using Conv2 = Layer<32, 20, 20, 4, 4, 2, 64, false, false>;  // -> (B, 9, 9, 64) NHWC
-using Conv3 = Layer<64, 9, 9, 3, 3, 1, 64, false, true>;     // -> (B, 64, 7, 7) NCHW
-}  // namespace
-
 extern "C" int ppox_nature_pack_weights(const float* w1, const float* w2, const float* w3, float* wp1, float* wp2,
-                                        float* wp3, void* stream) {
+                                        float* wp3, float* wpd2, float* wpd3, void* stream) {
     PPOX_REQUIRE(w1 && w2 && w3 && wp1 && wp2 && wp3, "ppox_nature_pack_weights: null pointer");
-    PPOX_REQUIRE(ppox::aligned16(wp1) && ppox::aligned16(wp2) && ppox::aligned16(wp3),
+    PPOX_REQUIRE(ppox::aligned16(wp1) && ppox::aligned16(wp2) && ppox::aligned16(wp3) &&
+                     (!wpd2 || ppox::aligned16(wpd2)) && (!wpd3 || ppox::aligned16(wpd3)),
                  "ppox_nature_pack_weights: packed buffers must be 16-byte aligned");
     hipStream_t s = ppox::as_stream(stream);
-    pack_kernel<4, 8, 8, 32, false><<<ppox::ceil_div(256 * 32, 256), 256, 0, s>>>(w1, wp1);
-    pack_kernel<32, 4, 4, 64, true><<<ppox::ceil_div(512 * 64, 256), 256, 0, s>>>(w2, wp2);
-    pack_kernel<64, 3, 3, 64, true><<<ppox::ceil_div(576 * 64, 256), 256, 0, s>>>(w3, wp3);
+    pack_fwd<G1, false><<<ppox::ceil_div(G1::K * 32, 256), 256, 0, s>>>(w1, wp1);
+    pack_fwd<G2, true><<<ppox::ceil_div(G2::K * 64, 256), 256, 0, s>>>(w2, wp2);
+    pack_fwd<G3, true><<<ppox::ceil_div(G3::K * 64, 256), 256, 0, s>>>(w3, wp3);
+    if (wpd2) pack_dgrad<G2><<<ppox::ceil_div(G2::K * G2::COUT / G2::CIN * G2::CIN, 256), 256, 0, s>>>(w2, wpd2);
+    if (wpd3) pack_dgrad<G3><<<ppox::ceil_div(G3::K * G3::COUT / G3::CIN * G3::CIN, 256), 256, 0, s>>>(w3, wpd3);
     PPOX_LAUNCHED("ppox_nature_pack_weights");
 }
 
@@ -271,22 +635,74 @@ extern "C" int ppox_nature_conv_fwd(int32_t layer, const void* x, int64_t batch,
     PPOX_REQUIRE(x && wp && bias && y && batch >= 0, "ppox_nature_conv_fwd: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(wp), "ppox_nature_conv_fwd: packed weights must be 16-byte aligned");
     if (batch == 0) return PPOX_OK;
-    ConvArgs a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, wp, bias, y, batch};
+    Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, wp, bias, nullptr, y, batch};
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 1) {
         PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && (idx || x_sample_stride % 4 == 0),
                      "ppox_nature_conv_fwd: u8 input must be 4-byte aligned");
         if (idx) PPOX_REQUIRE(T > 0 && N_env > 0, "ppox_nature_conv_fwd: idx needs T and N_env");
-        const long long M = batch * Conv1::P;
-        conv_fwd_kernel<Conv1, StageU8<Conv1>><<<ppox::ceil_div(M, BM), 256, 0, s>>>(a);
-    } else if (layer == 2) {
-        PPOX_REQUIRE(ppox::aligned16(x) && !idx, "ppox_nature_conv_fwd: layer 2 input must be 16B aligned NHWC");
-        const long long M = batch * Conv2::P;
-        conv_fwd_kernel<Conv2, StageF32<Conv2>><<<ppox::ceil_div(M, BM), 256, 0, s>>>(a);
-    } else {
-        PPOX_REQUIRE(ppox::aligned16(x) && !idx, "ppox_nature_conv_fwd: layer 3 input must be 16B aligned NHWC");
-        const long long M = batch * Conv3::P;
-        conv_fwd_kernel<Conv3, StageF32<Conv3>><<<ppox::ceil_div(M, BM), 256, 0, s>>>(a);
+        return launch_igemm<FwdProblem<G1, StageFwd1, false>>(a, batch * G1::P, 1, s, "ppox_nature_conv_fwd");
     }
-    PPOX_LAUNCHED("ppox_nature_conv_fwd");
+    PPOX_REQUIRE(ppox::aligned16(x) && !idx, "ppox_nature_conv_fwd: layer 2/3 input must be 16B-aligned NHWC");
+    if (layer == 2)
+        return launch_igemm<FwdProblem<G2, StageFwdNHWC<G2>, false>>(a, batch * G2::P, 1, s, "ppox_nature_conv_fwd");
+    return launch_igemm<FwdProblem<G3, StageFwdNHWC<G3>, true>>(a, batch * G3::P, 1, s, "ppox_nature_conv_fwd");
+}
+
+extern "C" int ppox_nature_conv_dgrad(int32_t layer, const float* grad_out, int64_t batch, const float* wpd,
+                                      const float* prev_act, float* grad_in, void* stream) {
+    PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad: layer must be 2 or 3");
+    PPOX_REQUIRE(grad_out && wpd && prev_act && grad_in && batch >= 0, "ppox_nature_conv_dgrad: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wpd), "ppox_nature_conv_dgrad: 16B alignment");
+    if (batch == 0) return PPOX_OK;
+    Args a{grad_out, nullptr, 0, 0, 0, wpd, nullptr, prev_act, grad_in, batch};
+    hipStream_t s = ppox::as_stream(stream);
+    if (layer == 2)
+        return launch_igemm<DgradProblem<G2>>(a, batch * (G2::IH / 2) * (G2::IW / 2), 4, s, "ppox_nature_conv_dgrad");
+    return launch_igemm<DgradProblem<G3>>(a, batch * G3::IH * G3::IW, 1, s, "ppox_nature_conv_dgrad");
+}
+
+extern "C" int64_t ppox_nature_wgrad_splits(int32_t layer, int64_t batch) {
+    const long long P = layer == 1 ? G1::P : (layer == 2 ? G2::P : G3::P);
+    long long s = (batch * P + 4095) / 4096;
+    s = s < 8 ? 8 : (s > 512 ? 512 : s);
+    return (s + 7) / 8 * 8;
+}
+
+extern "C" int64_t ppox_nature_wgrad_workspace_bytes(int32_t layer, int64_t batch) {
+    const long long splits = ppox_nature_wgrad_splits(layer, batch);
+    const long long kc = layer == 1 ? G1::K * G1::COUT : (layer == 2 ? G2::K * G2::COUT : G3::K * G3::COUT);
+    const long long c = layer == 1 ? G1::COUT : 64;
+    return splits * (kc + c) * (long long)sizeof(float);
+}
+
+extern "C" int ppox_nature_conv_wgrad(int32_t layer, const void* x, int64_t batch, const int64_t* idx, int64_t T,
+                                      int64_t N_env, int64_t x_sample_stride, const float* grad_out, void* workspace,
+                                      int64_t workspace_bytes, float* dw, float* db, void* stream) {
+    PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_conv_wgrad: layer must be 1, 2 or 3");
+    PPOX_REQUIRE(x && grad_out && workspace && dw && db && batch > 0, "ppox_nature_conv_wgrad: bad arguments");
+    PPOX_REQUIRE(workspace_bytes >= ppox_nature_wgrad_workspace_bytes(layer, batch),
+                 "ppox_nature_conv_wgrad: workspace too small");
+    PPOX_REQUIRE(ppox::aligned16(grad_out), "ppox_nature_conv_wgrad: grad_out must be 16B aligned");
+    const int splits = (int)ppox_nature_wgrad_splits(layer, batch);
+    const long long kc = layer == 1 ? G1::K * G1::COUT : (layer == 2 ? G2::K * G2::COUT : G3::K * G3::COUT);
+    float* slab = reinterpret_cast<float*>(workspace);
+    WArgs wa{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, grad_out, slab,
+             slab + (long long)splits * kc, batch, 0, splits};
+    hipStream_t s = ppox::as_stream(stream);
+    if (layer == 1) {
+        PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3), "ppox_nature_conv_wgrad: u8 input 4-byte aligned");
+        return launch_wgrad<G1, true, false>(wa, dw, db, s);
+    }
+    PPOX_REQUIRE(ppox::aligned16(x) && !idx, "ppox_nature_conv_wgrad: layer 2/3 input must be 16B-aligned NHWC");
+    if (layer == 2) return launch_wgrad<G2, false, true>(wa, dw, db, s);
+    return launch_wgrad<G3, false, true>(wa, dw, db, s);
+}
+
+extern "C" int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, int64_t batch, float* out,
+                                           void* stream) {
+    PPOX_REQUIRE(grad && act && out && batch >= 0, "ppox_nchw_to_nhwc_relu_grad: bad arguments");
+    if (batch == 0) return PPOX_OK;
+    nchw_to_nhwc_mask<<<(unsigned)batch, 256, 0, ppox::as_stream(stream)>>>(grad, act, batch, out);
+    PPOX_LAUNCHED("ppox_nchw_to_nhwc_relu_grad");
 }

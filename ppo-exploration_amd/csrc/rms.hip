@@ -17,13 +17,15 @@
 
 namespace {
 
-__device__ inline void chan_merge(double& mean, double& var, double count, double bmean, double bvar, double bcount) {
+// m_b = batch_var * batch_count is passed in: numpy evaluates it in the batch
+// variance's dtype (float32 for float32 batches: np.float32 * Python int stays
+// f32 under NEP 50; float64 for uint8 batches), util.py:36.
+__device__ inline void chan_merge(double& mean, double& var, double count, double bmean, double m_b, double bcount) {
     // util.py:31-44, same association as the Python expressions
     const double delta = bmean - mean;
     const double tot = count + bcount;
     const double new_mean = mean + delta * bcount / tot;
     const double m_a = var * count;
-    const double m_b = bvar * bcount;
     const double m2 = m_a + m_b + delta * delta * count * bcount / (count + bcount);
     mean = new_mean;
     var = m2 / (count + bcount);
@@ -67,7 +69,7 @@ __global__ void __launch_bounds__(256) u8_finalize(const unsigned long long* __r
     if (bvar_out) bvar_out[c] = bvar;
     if (mean && var) {
         double mu = mean[c], vv = var[c];
-        chan_merge(mu, vv, count, m, bvar, n);
+        chan_merge(mu, vv, count, m, bvar * n, n);
         mean[c] = mu;
         var[c] = vv;
     }
@@ -89,7 +91,7 @@ __global__ void __launch_bounds__(256) f32_columns(const float* __restrict__ x, 
     }
     const float bv = q / (float)rows;
     double mu = mean[c], vv = var[c];
-    chan_merge(mu, vv, count, (double)m, (double)bv, (double)rows);
+    chan_merge(mu, vv, count, (double)m, (double)(bv * (float)rows), (double)rows);
     mean[c] = mu;
     var[c] = vv;
 }
@@ -201,7 +203,7 @@ __global__ void __launch_bounds__(256) scalar_rms_scale(float* __restrict__ x, i
     if (threadIdx.x == 0) {
         const float bv = q / (float)n;
         double mu = *mean, vv = *var;
-        chan_merge(mu, vv, count, (double)bm, (double)bv, (double)n);
+        chan_merge(mu, vv, count, (double)bm, (double)(bv * (float)n), (double)n);
         *mean = mu;
         *var = vv;
         denom_sh = sqrt(vv) + 1e-08;  // ppo.py:398

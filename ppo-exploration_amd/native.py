@@ -40,15 +40,20 @@ SIGNATURES = {
     "ppox_atari_env_reset": [_vp, _i64, _i64, _u64, _vp, _vp, _vp],
     "ppox_atari_env_step": [_vp, _vp, _vp, _i64, _i64, _u64, _i64, _f32, _f32, _vp, _vp, _vp, _vp,
                             _vp, _vp, _vp],
-    "ppox_nature_pack_weights": [_vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_pack_weights": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_dgrad": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_wgrad": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
+    "ppox_nchw_to_nhwc_relu_grad": [_vp, _vp, _i64, _vp, _vp],
     "ppox_nature_conv_fwd": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
 }
 _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p,
-             "ppox_rms_u8_workspace_bytes": ctypes.c_int64}
-_RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64]}
+             "ppox_rms_u8_workspace_bytes": ctypes.c_int64, "ppox_nature_wgrad_splits": ctypes.c_int64,
+             "ppox_nature_wgrad_workspace_bytes": ctypes.c_int64}
+_RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
+                 "ppox_nature_wgrad_workspace_bytes": [_i32, _i64]}
 
 _lib = None
 
@@ -281,8 +286,28 @@ def vec_env_step(obs, actions, N, D, env_offset, seed, step, p_done, max_len, re
 # ---------------------------------------------------------------------------
 # K6 NatureCNN convolutions
 # ---------------------------------------------------------------------------
-def nature_pack_weights(w1, w2, w3, wp1, wp2, wp3, stream=None):
-    call("ppox_nature_pack_weights", _p(w1), _p(w2), _p(w3), _p(wp1), _p(wp2), _p(wp3), stream_ptr(stream))
+def nature_pack_weights(w1, w2, w3, wp1, wp2, wp3, wpd2=None, wpd3=None, stream=None):
+    call("ppox_nature_pack_weights", _p(w1), _p(w2), _p(w3), _p(wp1), _p(wp2), _p(wp3), _p(wpd2), _p(wpd3),
+         stream_ptr(stream))
+
+
+def nature_conv_dgrad(layer, grad_out, batch, wpd, prev_act, grad_in, stream=None):
+    call("ppox_nature_conv_dgrad", int(layer), _p(grad_out), int(batch), _p(wpd), _p(prev_act), _p(grad_in),
+         stream_ptr(stream))
+
+
+def nature_wgrad_workspace_bytes(layer, batch):
+    return int(load().ppox_nature_wgrad_workspace_bytes(int(layer), int(batch)))
+
+
+def nature_conv_wgrad(layer, x, batch, idx, T, N_env, x_sample_stride, grad_out, workspace, dw, db, stream=None):
+    call("ppox_nature_conv_wgrad", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env), int(x_sample_stride),
+         _p(grad_out), _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db),
+         stream_ptr(stream))
+
+
+def nchw_to_nhwc_relu_grad(grad, act, batch, out, stream=None):
+    call("ppox_nchw_to_nhwc_relu_grad", _p(grad), _p(act), int(batch), _p(out), stream_ptr(stream))
 
 
 def nature_conv_fwd(layer, x, batch, idx, T, N_env, x_sample_stride, wp, bias, y, stream=None):
