@@ -76,9 +76,11 @@ def main():
     for _ in range(args.warmup):
         iteration()
 
-    # event timing of the roofline kernel on the stream it is launched on
-    prof_kernel = "ppox_gae" if args.algo != "rnd" else "ppox_gae_dual"
-    native.enable_event_timing([prof_kernel])
+    # event timing of the dominant kernel (conv1 weight-gradient MFMA GEMM)
+    # on the stream it is launched on, plus the GAE scan (K1) for its HBM roofline
+    prof_kernel = "ppox_nature_conv_wgrad:1"
+    gae_kernel = "ppox_gae" if args.algo != "rnd" else "ppox_gae_dual"
+    native.enable_event_timing([prof_kernel, gae_kernel])
 
     torch.cuda.synchronize()
     if world > 1:
@@ -91,6 +93,7 @@ def main():
         tdist.barrier()
     dt = time.perf_counter() - t0
     kt = native.event_times_ms(prof_kernel)
+    gt = native.event_times_ms(gae_kernel)
     native.enable_event_timing([])
     if world > 1:
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
@@ -110,17 +113,26 @@ def main():
                    "batch_size": args.batch_size, "minibatches_per_epoch": -(-args.envs * args.nstep // args.batch_size),
                    "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)" if world > 1 else "single GPU"},
     }
-    # roofline of the profiled kernel: ALGORITHMIC bytes per launch / mean launch duration
+    # roofline of the dominant kernel: ALGORITHMIC flops per launch / mean launch duration.
+    # conv1 wgrad = 2 * batch * 400 output pixels * 256 (ci,ky,kx) * 32 output channels
     if kt:
+        flops = [2.0 * a[2] * 400 * 256 * 32 for _, a in kt]
+        mean_ms = float(np.mean([t for t, _ in kt]))
+        ach = float(np.mean(flops)) / (mean_ms * 1e-3) / 1e12
+        out["roofline"] = {"kernel": "wgrad_kernel<conv1> (ppox_nature_conv_wgrad layer 1)", "bound": "mfma",
+                           "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                           "launches": len(kt), "mean_us": round(mean_ms * 1e3, 1),
+                           "alg_flops_per_launch": float(np.mean(flops))}
+    if gt:
         n_local = args.envs // world
-        bytes_per_elem = 17 if prof_kernel == "ppox_gae" else 33
-        alg_bytes = bytes_per_elem * args.nstep * n_local
-        mean_ms = float(np.mean(kt))
+        alg_bytes = (17 if gae_kernel == "ppox_gae" else 33) * args.nstep * n_local
+        mean_ms = float(np.mean([t for t, _ in gt]))
         ach = alg_bytes / (mean_ms * 1e-3) / 1e9
-        out["roofline"] = {"kernel": prof_kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                           "launches": len(kt), "mean_us": round(mean_ms * 1e3, 2),
-                           "alg_bytes_per_launch": alg_bytes}
+        out["gae_roofline"] = {"kernel": gae_kernel, "bound": "hbm", "achieved": round(ach, 1),
+                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                               "mean_us": round(mean_ms * 1e3, 2), "alg_bytes_per_launch": alg_bytes,
+                               "note": "config-size launch is latency-bound; tools/gae_sweep.py sweeps N"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, ROOT)
         from oracle.baseline import atari_ppo_rate

@@ -193,14 +193,18 @@ int ppox_nature_conv_fwd(int32_t layer, const void* x, int64_t batch, const int6
 int ppox_nature_conv_dgrad(int32_t layer, const float* grad_out, int64_t batch, const float* wpd,
                            const float* prev_act, float* grad_in, void* stream);
 /* dW (PyTorch layout) and db from the layer input x (as in ppox_nature_conv_fwd) and
- * the ReLU-masked output grad (NHWC).  Split-K over pixels into a workspace of
- * ppox_nature_wgrad_workspace_bytes(layer, batch), reduced in a fixed order. */
+ * the ReLU-masked output grad (NHWC), in two launches: ppox_nature_conv_wgrad writes
+ * split-K partial slabs (over output pixels) into a workspace of
+ * ppox_nature_wgrad_workspace_bytes(layer, batch); ppox_nature_wgrad_reduce sums
+ * them in a fixed order (deterministic) into dw [co][ci][ky][kx] and db. */
 int64_t ppox_nature_wgrad_splits(int32_t layer, int64_t batch);
 int64_t ppox_nature_wgrad_workspace_bytes(int32_t layer, int64_t batch);
 int ppox_nature_conv_wgrad(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
                            int64_t T, int64_t N_env, int64_t x_sample_stride,
                            const float* grad_out, void* workspace, int64_t workspace_bytes,
-                           float* dw, float* db, void* stream);
+                           void* stream);
+int ppox_nature_wgrad_reduce(int32_t layer, int64_t batch, const void* workspace, float* dw,
+                             float* db, void* stream);
 /* (batch, 64, 7, 7) NCHW grad of the trunk output -> NHWC, times (act > 0). */
 int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, int64_t batch, float* out,
                                 void* stream);

@@ -598,17 +598,22 @@ int launch_igemm(const Args& a, long long rows, int classes, hipStream_t s, cons
     PPOX_LAUNCHED(name);
 }
 
-template <class L, bool U8, bool NHWC_ORDER>
-int launch_wgrad(const WArgs& wa_in, float* dw, float* db, hipStream_t s) {
+template <class L, bool U8>
+int launch_wgrad(const WArgs& wa_in, hipStream_t s) {
     WArgs wa = wa_in;
     using C = WgCfg<L, U8>;
     const long long M = wa.batch * L::P;
     const int splits = wa.splits;
     wa.px_per_split = (M + splits - 1) / splits;
     wgrad_kernel<L, U8><<<(unsigned)(C::KB * splits), 256, 0, s>>>(wa);
-    wgrad_reduce<L, NHWC_ORDER><<<ppox::ceil_div(L::K * L::COUT + L::COUT, 256), 256, 0, s>>>(
-        wa.slab, wa.bslab, splits, dw, db);
     PPOX_LAUNCHED("ppox_nature_conv_wgrad");
+}
+
+template <class L, bool NHWC_ORDER>
+int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float* dw, float* db, hipStream_t s) {
+    wgrad_reduce<L, NHWC_ORDER><<<ppox::ceil_div(L::K * L::COUT + L::COUT, 256), 256, 0, s>>>(slab, bslab, splits, dw,
+                                                                                             db);
+    PPOX_LAUNCHED("ppox_nature_wgrad_reduce");
 }
 
 }  // namespace
@@ -678,9 +683,9 @@ extern "C" int64_t ppox_nature_wgrad_workspace_bytes(int32_t layer, int64_t batc
 
 extern "C" int ppox_nature_conv_wgrad(int32_t layer, const void* x, int64_t batch, const int64_t* idx, int64_t T,
                                       int64_t N_env, int64_t x_sample_stride, const float* grad_out, void* workspace,
-                                      int64_t workspace_bytes, float* dw, float* db, void* stream) {
+                                      int64_t workspace_bytes, void* stream) {
     PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_conv_wgrad: layer must be 1, 2 or 3");
-    PPOX_REQUIRE(x && grad_out && workspace && dw && db && batch > 0, "ppox_nature_conv_wgrad: bad arguments");
+    PPOX_REQUIRE(x && grad_out && workspace && batch > 0, "ppox_nature_conv_wgrad: bad arguments");
     PPOX_REQUIRE(workspace_bytes >= ppox_nature_wgrad_workspace_bytes(layer, batch),
                  "ppox_nature_conv_wgrad: workspace too small");
     PPOX_REQUIRE(ppox::aligned16(grad_out), "ppox_nature_conv_wgrad: grad_out must be 16B aligned");
@@ -692,11 +697,25 @@ extern "C" int ppox_nature_conv_wgrad(int32_t layer, const void* x, int64_t batc
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 1) {
         PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3), "ppox_nature_conv_wgrad: u8 input 4-byte aligned");
-        return launch_wgrad<G1, true, false>(wa, dw, db, s);
+        return launch_wgrad<G1, true>(wa, s);
     }
     PPOX_REQUIRE(ppox::aligned16(x) && !idx, "ppox_nature_conv_wgrad: layer 2/3 input must be 16B-aligned NHWC");
-    if (layer == 2) return launch_wgrad<G2, false, true>(wa, dw, db, s);
-    return launch_wgrad<G3, false, true>(wa, dw, db, s);
+    if (layer == 2) return launch_wgrad<G2, false>(wa, s);
+    return launch_wgrad<G3, false>(wa, s);
+}
+
+extern "C" int ppox_nature_wgrad_reduce(int32_t layer, int64_t batch, const void* workspace, float* dw, float* db,
+                                        void* stream) {
+    PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_wgrad_reduce: layer must be 1, 2 or 3");
+    PPOX_REQUIRE(workspace && dw && db && batch > 0, "ppox_nature_wgrad_reduce: bad arguments");
+    const int splits = (int)ppox_nature_wgrad_splits(layer, batch);
+    const long long kc = layer == 1 ? G1::K * G1::COUT : (layer == 2 ? G2::K * G2::COUT : G3::K * G3::COUT);
+    const float* slab = reinterpret_cast<const float*>(workspace);
+    const float* bslab = slab + (long long)splits * kc;
+    hipStream_t s = ppox::as_stream(stream);
+    if (layer == 1) return launch_wgrad_reduce<G1, false>(slab, bslab, splits, dw, db, s);
+    if (layer == 2) return launch_wgrad_reduce<G2, true>(slab, bslab, splits, dw, db, s);
+    return launch_wgrad_reduce<G3, true>(slab, bslab, splits, dw, db, s);
 }
 
 extern "C" int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, int64_t batch, float* out,

@@ -42,7 +42,8 @@ SIGNATURES = {
                             _vp, _vp, _vp],
     "ppox_nature_pack_weights": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_dgrad": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
-    "ppox_nature_conv_wgrad": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
+    "ppox_nature_conv_wgrad": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _i64, _vp],
+    "ppox_nature_wgrad_reduce": [_i32, _i64, _vp, _vp, _vp, _vp],
     "ppox_nchw_to_nhwc_relu_grad": [_vp, _vp, _i64, _vp, _vp],
     "ppox_nature_conv_fwd": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
@@ -109,18 +110,23 @@ def enable_event_timing(names):
 
 
 def event_times_ms(name):
+    """[(ms, args)] for every timed launch of `name` (or 'name:layer' for the conv entry points)."""
     torch.cuda.synchronize()
-    return [a.elapsed_time(b) for a, b in _events.get(name, [])]
+    return [(a.elapsed_time(b), args) for a, b, args in _events.get(name, [])]
+
+
+_LAYERED = ("ppox_nature_conv_fwd", "ppox_nature_conv_dgrad", "ppox_nature_conv_wgrad")
 
 
 def call(name, *args):
-    if name in _timed:
+    key = f"{name}:{args[0]}" if name in _LAYERED else name
+    if key in _timed:
         s = torch.cuda.current_stream()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(s)
         rc = getattr(lib(), name)(*args)
         b.record(s)
-        _events[name].append((a, b))
+        _events[key].append((a, b, args))
     else:
         rc = getattr(lib(), name)(*args)
     if rc != 0:
@@ -302,8 +308,8 @@ def nature_wgrad_workspace_bytes(layer, batch):
 
 def nature_conv_wgrad(layer, x, batch, idx, T, N_env, x_sample_stride, grad_out, workspace, dw, db, stream=None):
     call("ppox_nature_conv_wgrad", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env), int(x_sample_stride),
-         _p(grad_out), _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db),
-         stream_ptr(stream))
+         _p(grad_out), _p(workspace), workspace.numel() * workspace.element_size(), stream_ptr(stream))
+    call("ppox_nature_wgrad_reduce", int(layer), int(batch), _p(workspace), _p(dw), _p(db), stream_ptr(stream))
 
 
 def nchw_to_nhwc_relu_grad(grad, act, batch, out, stream=None):
