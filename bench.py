@@ -24,6 +24,20 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (= f32 vector) dense peak
 
 
+def pmc_traffic(kernel="wgrad_kernel<4, 84, 84, 8, 8, 4, 32>"):
+    """HBM bytes per launch of the dominant kernel from the latest committed rocprofv3 --pmc
+    summary (profiles/rNN_pmc_summary.json: separate FETCH_SIZE / WRITE_SIZE passes of this
+    bench command, gfx950-corrected 2*FETCH + WRITE, KB -> B)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f).get(kernel)
+    return None if d is None else {"bytes_per_launch": d["hbm_bytes_per_launch_corrected"],
+                                   "source": os.path.relpath(files[-1], ROOT)}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -121,7 +135,7 @@ def main():
         ach = float(np.mean(flops)) / (mean_ms * 1e-3) / 1e12
         out["roofline"] = {"kernel": "wgrad_kernel<conv1> (ppox_nature_conv_wgrad layer 1)", "bound": "mfma",
                            "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                           "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": pmc_traffic(),
                            "launches": len(kt), "mean_us": round(mean_ms * 1e3, 1),
                            "alg_flops_per_launch": float(np.mean(flops))}
     if gt:

@@ -1,0 +1,77 @@
+"""Per-kernel timing of the NatureCNN conv kernels (fwd / dgrad / wgrad) at the
+training minibatch size, HIP events on the launch stream, vs algorithmic FLOPs.
+Usage: python tools/conv_bench.py [B]"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+import native  # noqa: E402
+
+PEAK = 157.3
+MAC = {1: 400 * 256 * 32, 2: 81 * 512 * 64, 3: 49 * 576 * 64}
+
+
+def t_ms(fn, iters=10):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    d = "cuda"
+    w1, w2, w3 = torch.randn(32, 4, 8, 8, device=d) * 0.05, torch.randn(64, 32, 4, 4, device=d) * 0.05, \
+        torch.randn(64, 64, 3, 3, device=d) * 0.05
+    b1, b2, b3 = torch.randn(32, device=d), torch.randn(64, device=d), torch.randn(64, device=d)
+    wp1, wp2, wp3 = torch.empty(256 * 32, device=d), torch.empty(512 * 64, device=d), torch.empty(576 * 64, device=d)
+    wpd2, wpd3 = torch.empty(4 * 256 * 32, device=d), torch.empty(576 * 64, device=d)
+    native.nature_pack_weights(w1, w2, w3, wp1, wp2, wp3, wpd2, wpd3)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=d)
+    h1 = torch.empty(B, 20, 20, 32, device=d)
+    h2 = torch.empty(B, 9, 9, 64, device=d)
+    h3 = torch.empty(B, 64, 7, 7, device=d)
+    g1, g2, g3 = torch.randn_like(h1), torch.randn(B, 9, 9, 64, device=d), torch.randn(B, 7, 7, 64, device=d)
+    dw = {1: torch.empty_like(w1), 2: torch.empty_like(w2), 3: torch.empty_like(w3)}
+    db = {1: torch.empty_like(b1), 2: torch.empty_like(b2), 3: torch.empty_like(b3)}
+    ws = {k: torch.empty(native.nature_wgrad_workspace_bytes(k, B), dtype=torch.uint8, device=d) for k in (1, 2, 3)}
+    lib = native.lib()
+    sp = native.stream_ptr()
+    res = []
+
+    def rec(name, layer, ms, mac):
+        tf = 2 * B * mac / (ms * 1e-3) / 1e12
+        res.append({"kernel": name, "layer": layer, "B": B, "ms": round(ms, 3), "TF/s": round(tf, 1),
+                    "frac": round(tf / PEAK, 3)})
+        print(json.dumps(res[-1]), flush=True)
+
+    rec("fwd", 1, t_ms(lambda: native.nature_conv_fwd(1, x, B, None, 0, 0, 28224, wp1, b1, h1)), MAC[1])
+    rec("fwd", 2, t_ms(lambda: native.nature_conv_fwd(2, h1, B, None, 0, 0, 0, wp2, b2, h2)), MAC[2])
+    rec("fwd", 3, t_ms(lambda: native.nature_conv_fwd(3, h2, B, None, 0, 0, 0, wp3, b3, h3)), MAC[3])
+    rec("dgrad", 3, t_ms(lambda: native.nature_conv_dgrad(3, g3, B, wpd3, h2, g2)), MAC[3])
+    rec("dgrad", 2, t_ms(lambda: native.nature_conv_dgrad(2, g2, B, wpd2, h1, g1)), MAC[2])
+    for L, xin, g, stride in ((3, h2, g3, 0), (2, h1, g2, 0), (1, x, g1, 28224)):
+        f = lambda: lib.ppox_nature_conv_wgrad(L, native._p(xin), B, None, 0, 0, stride, native._p(g),
+                                               native._p(ws[L]), ws[L].numel(), sp)
+        rec("wgrad", L, t_ms(f), MAC[L])
+        rec("wgrad_reduce", L, t_ms(lambda: native.call("ppox_nature_wgrad_reduce", L, B, native._p(ws[L]),
+                                                        native._p(dw[L]), native._p(db[L]), sp)), 0)
+    # library reference (MIOpen) for the same shapes
+    xf = x.float()
+    import torch.nn.functional as F
+    rec("miopen_fwd", 1, t_ms(lambda: F.conv2d(xf, w1, b1, stride=4), 5), MAC[1])
+    tot = sum(r["ms"] for r in res if not r["kernel"].startswith("miopen"))
+    print(json.dumps({"total_conv_ms_per_minibatch": round(tot, 3)}))
+
+
+if __name__ == "__main__":
+    main()
