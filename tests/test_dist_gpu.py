@@ -1,0 +1,98 @@
+"""Product data-parallel path on the GPU: 2 ranks (gloo, both on cuda:0) running
+ppo.PPO.train() on their env shards of one rollout must reproduce the 1-rank run
+(SURVEY.md §8e).  RCCL cannot put two ranks on one device, so the collectives
+here go through gloo; the code path (sharding, owned-row minibatches, partial
+all-reduce, flat-gradient all-reduce) is the one bench.py runs over RCCL."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+CFG = dict(env_id="BreakoutNoFrameskip-v4", n_envs=8, nstep=16, batch_size=48, n_epochs=2, seed=5, quiet=True)
+FIELDS = ("actions", "log_probs", "values", "rewards", "masks")
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _load_shard(alg, data, lo, n):
+    ro = alg.rollout
+    ro.obs_slots.copy_(torch.from_numpy(data["obs"][:, lo:lo + n]).cuda())
+    for f in FIELDS:
+        getattr(ro, f).copy_(torch.from_numpy(data[f][:, lo:lo + n]).cuda())
+    ro.pos, ro.full = ro.buffer_size, True
+    T = ro.buffer_size
+    ro.compute_returns_and_advantages(ro.values[T - 1], ro.masks[T - 1])
+
+
+def _rank(rank, world, port, path, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "ppo-exploration_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as tdist
+    torch.cuda.set_device(0)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import ppo
+        data = dict(np.load(path))
+        np.random.seed(11)
+        torch.manual_seed(11)
+        alg = ppo.PPO(**CFG)
+        _load_shard(alg, data, alg.env_offset, alg.local_envs)
+        alg.train()
+        q.put((rank, alg.flat.data[:alg.flat.n].cpu().numpy(), alg.loss_accum.cpu().numpy()))
+    except Exception as e:  # surface the failure to the parent
+        q.put((rank, repr(e), None))
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_two_ranks_match_one_rank():
+    import ppo
+    np.random.seed(11)
+    torch.manual_seed(11)
+    ref = ppo.PPO(**CFG)
+    ref.collect_samples()
+    ro = ref.rollout
+    data = {"obs": ro.obs_slots.cpu().numpy()}
+    for f in FIELDS:
+        data[f] = getattr(ro, f).cpu().numpy()
+    # 1-rank reference train on exactly this rollout (fresh agent, same seeds)
+    np.random.seed(11)
+    torch.manual_seed(11)
+    one = ppo.PPO(**CFG)
+    _load_shard(one, data, 0, CFG["n_envs"])
+    one.train()
+    w_one = one.flat.data[:one.flat.n].cpu().numpy()
+    acc_one = one.loss_accum.cpu().numpy()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "rollout.npz")
+        np.savez(path, **data)
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _port()
+        procs = [ctx.Process(target=_rank, args=(r, 2, port, path, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=300) for _ in range(2)]
+        for p in procs:
+            p.join(timeout=60)
+    for rank, w, acc in res:
+        if isinstance(w, str):
+            if "gloo" in w.lower() and "cuda" in w.lower():
+                pytest.skip(f"gloo without device-tensor support on this build: {w}")
+            raise AssertionError(f"rank {rank}: {w}")
+        np.testing.assert_allclose(acc, acc_one, rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(w, w_one, rtol=1e-4, atol=1e-5)

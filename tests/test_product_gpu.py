@@ -119,3 +119,76 @@ def test_atari_iteration_runs(algo):
     assert acc[5] == 2 * 4 and np.isfinite(acc[:5]).all()
     assert not torch.equal(w0, alg.flat.data)
     alg.collect_samples()  # second rollout continues from slot T
+
+
+def test_rnd_train_matches_reference_run(golden):
+    """PPO_RND.train() (ppo.py:409-502: two normalised advantage streams, clipped int value
+    loss, randn()<0.25-gated RND updates) on the reference's rollout."""
+    import ppo
+    import env as E
+    from oracle.algos import OracleRND
+    f = golden("train_rnd")
+    p = "rnd_"
+    D, N, T, B, E_, H, IH, seed, rnd_start = (int(x) for x in f[p + "cfg"])
+    renv = ReplayVecEnv(f[p + "env_obs"], f[p + "env_rew"], f[p + "env_done"], space_from_code(3))
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    orc = OracleRND(renv, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H, int_hidden_size=IH,
+                    rnd_start=rnd_start, max_grad_norm=0.5)
+    orc.collect()
+    r = orc.rollout
+    np.random.seed(seed)
+    alg = ppo.PPO_RND(env_id="custom", env=E.DeviceVecEnv("custom", N, obs_dim=D, action_space=E.Discrete(3)),
+                      n_envs=N, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H, int_hidden_size=IH,
+                      rnd_start=rnd_start, max_grad_norm=0.5, quiet=True)
+    _load_weights(alg.policy.net, f, p + "w0_")
+    _load_weights(alg.rnd, f, p + "r0_")
+    ro = alg.rollout
+    for t in range(T):
+        ro.add(r.obs[t], r.actions[t], r.rewards[t], r.int_rewards[t], r.values[t], r.int_values[t], r.masks[t],
+               r.log_probs[t])
+    ro.compute_returns_and_advantages(r.values[T - 1], r.int_values[T - 1], r.masks[T - 1])
+    np.testing.assert_array_equal(ro.int_advantages.cpu().numpy(), r.iadv)
+    alg.obs_rms._mean = torch.from_numpy(np.asarray(orc.obs_rms.mean, np.float64)).cuda()
+    alg.obs_rms._var = torch.from_numpy(np.asarray(orc.obs_rms.var, np.float64)).cuda()
+    alg.obs_rms.count = orc.obs_rms.count
+    alg.train()
+    for k, v in alg.policy.net.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), f[p + "w1_" + k], rtol=2e-5, atol=2e-6, err_msg=k)
+    for k, v in alg.rnd.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), f[p + "r1_" + k], rtol=1e-4, atol=1e-5, err_msg=k)
+    np.testing.assert_array_equal(np.random.get_state()[1], f[p + "np_state_after"])
+    acc = alg.loss_accum.cpu().numpy()
+    np.testing.assert_allclose(acc[4] / acc[5], f[p + "intrinsic_loss"], rtol=1e-4, atol=1e-6)
+
+
+def test_icm_train_matches_reference_run(golden):
+    """PPO_ICM.train() (ppo.py:651-713) on the reference's rollout (Discrete)."""
+    import ppo
+    import env as E
+    from oracle.algos import OracleICM
+    f = golden("train_icm")
+    p = "icm_disc_"
+    D, N, T, B, E_, H, IH, seed = (int(x) for x in f[p + "cfg"])
+    renv = ReplayVecEnv(f[p + "env_obs"], f[p + "env_rew"], f[p + "env_done"], space_from_code(3))
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    orc = OracleICM(renv, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H, int_hidden_size=IH,
+                    max_grad_norm=0.5, int_rew_integration=0.1)
+    orc.collect()
+    r = orc.rollout
+    np.random.seed(seed)
+    alg = ppo.PPO_ICM(env_id="custom", env=E.DeviceVecEnv("custom", N, obs_dim=D, action_space=E.Discrete(3)),
+                      n_envs=N, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H, int_hidden_size=IH,
+                      max_grad_norm=0.5, int_rew_integration=0.1, quiet=True)
+    _load_weights(alg.policy.net, f, p + "w0_")
+    _load_weights(alg.intrinsic_module, f, p + "i0_")
+    ro = alg.rollout
+    for t in range(T):
+        ro.add(r.obs[t], r.actions[t], r.rewards[t], r.values[t], r.masks[t], r.log_probs[t])
+    ro.compute_returns_and_advantages(r.values[T - 1], r.masks[T - 1])
+    alg.train()
+    for k, v in alg.policy.net.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), f[p + "w1_" + k], rtol=2e-5, atol=2e-6, err_msg=k)
+    for k, v in alg.intrinsic_module.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), f[p + "i1_" + k], rtol=2e-5, atol=2e-6, err_msg=k)
