@@ -82,9 +82,13 @@ __device__ inline long long u8_sample_base(const Args& a, long long n, long long
 // ---------------------------------------------------------------------------
 // conv1 forward: uint8 NCHW frames, K order (ci, ky, kx); chunk = 1 channel x 4
 // kernel rows x 8 columns -> 4 runs of 8 bytes per row (2 words each).
+// Rows past M read a valid clamped address and are zeroed by a select: a
+// conditional load would make hipcc branch around every load (execz) and
+// serialise them.
 struct StageFwd1 {
     using L = G1;
     const uint8_t* base[4];
+    bool ok[4];
     uint32_t r[4];
     __device__ StageFwd1(const Args& a, long long m0, long long M) {
         const uint8_t* x = reinterpret_cast<const uint8_t*>(a.x);
@@ -93,20 +97,21 @@ struct StageFwd1 {
             const int w = i * 256 + threadIdx.x;
             const int row = w >> 3, seg = (w & 7) >> 1, half = w & 1;
             const long long m = m0 + row;
-            if (m < M) {
-                const long long n = m / L::P;
-                const int p = (int)(m - n * L::P), oy = p / L::OW, ox = p % L::OW;
-                base[i] = x + u8_sample_base(a, n, (long long)L::CIN * L::IH * L::IW) + (oy * L::S + seg) * L::IW +
-                          ox * L::S + half * 4;
-            } else {
-                base[i] = nullptr;
-            }
+            ok[i] = m < M;
+            const long long mm = ok[i] ? m : m0;
+            const long long n = mm / L::P;
+            const int p = (int)(mm - n * L::P), oy = p / L::OW, ox = p % L::OW;
+            base[i] = x + u8_sample_base(a, n, (long long)L::CIN * L::IH * L::IW) + (oy * L::S + seg) * L::IW +
+                      ox * L::S + half * 4;
         }
     }
     __device__ inline void load(int chunk) {
         const int off = (chunk >> 1) * (L::IH * L::IW) + (chunk & 1) * 4 * L::IW;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = base[i] ? *reinterpret_cast<const uint32_t*>(base[i] + off) : 0u;
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(base[i] + off);
+            r[i] = ok[i] ? v : 0u;
+        }
     }
     __device__ inline void store(float* As) const {
 #pragma unroll
@@ -126,6 +131,7 @@ struct StageFwd1 {
 template <class L>
 struct StageFwdNHWC {
     const float* base[4];
+    bool ok[4];
     float4 r[4];
     __device__ StageFwdNHWC(const Args& a, long long m0, long long M) {
         const float* x = reinterpret_cast<const float*>(a.x);
@@ -134,22 +140,23 @@ struct StageFwdNHWC {
             const int w = i * 256 + threadIdx.x;
             const int row = w >> 3, q = w & 7;
             const long long m = m0 + row;
-            if (m < M) {
-                const long long n = m / L::P;
-                const int p = (int)(m - n * L::P), oy = p / L::OW, ox = p % L::OW;
-                base[i] = x + ((n * L::IH + oy * L::S) * L::IW + ox * L::S) * L::CIN + q * 4;
-            } else {
-                base[i] = nullptr;
-            }
+            ok[i] = m < M;
+            const long long mm = ok[i] ? m : m0;
+            const long long n = mm / L::P;
+            const int p = (int)(mm - n * L::P), oy = p / L::OW, ox = p % L::OW;
+            base[i] = x + ((n * L::IH + oy * L::S) * L::IW + ox * L::S) * L::CIN + q * 4;
         }
     }
     __device__ inline void load(int chunk) {
         constexpr int CPT = L::CIN / BK;
         const int tap = chunk / CPT, ky = tap / L::KW, kx = tap % L::KW;
         const int off = (ky * L::IW + kx) * L::CIN + (chunk % CPT) * BK;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            r[i] = base[i] ? *reinterpret_cast<const float4*>(base[i] + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < 4; ++i) {
+            const float4 v = *reinterpret_cast<const float4*>(base[i] + off);
+            r[i] = ok[i] ? v : z;
+        }
     }
     __device__ inline void store(float* As) const {
 #pragma unroll
@@ -183,28 +190,26 @@ struct StageDgrad {
             const int w = i * 256 + threadIdx.x;
             const int row = w >> 3, q = w & 7;
             const long long m = m0 + row;
-            if (m < M) {
-                const long long n = m / (JH * JW);
-                const int p = (int)(m - n * (JH * JW));
-                jy[i] = p / JW;
-                jx[i] = p % JW;
-                base[i] = g + n * (L::P * L::COUT) + q * 4;
-            } else {
-                base[i] = nullptr;
-                jy[i] = jx[i] = -100;
-            }
+            const bool in = m < M;
+            const long long mm = in ? m : m0;
+            const long long n = mm / (JH * JW);
+            const int p = (int)(mm - n * (JH * JW));
+            jy[i] = in ? p / JW : -100;  // out-of-range rows never pass the tap test
+            jx[i] = p % JW;
+            base[i] = g + n * (L::P * L::COUT) + q * 4;
         }
     }
     __device__ inline void load(int chunk) {
         constexpr int CPT = L::COUT / BK;
         const int tap = chunk / CPT, ty = tap / TX, tx = tap % TX;
         const int co0 = (chunk % CPT) * BK;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int oy = jy[i] - ty, ox = jx[i] - tx;
-            const bool ok = base[i] && oy >= 0 && oy < L::OH && ox >= 0 && ox < L::OW;
-            r[i] = ok ? *reinterpret_cast<const float4*>(base[i] + (oy * L::OW + ox) * L::COUT + co0)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
+            const bool ok = oy >= 0 && oy < L::OH && ox >= 0 && ox < L::OW;
+            const float4 v = *reinterpret_cast<const float4*>(base[i] + (ok ? (oy * L::OW + ox) * L::COUT : 0) + co0);
+            r[i] = ok ? v : z;
         }
     }
     __device__ inline void store(float* As) const {
@@ -337,6 +342,10 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(Args a) {
 // Wgrad.  WG = (k-block of KT rows of K) x (all COUT) x (slice of output pixels).
 // Per step of MS = 32 pixels: stage X[32][KT] (im2col) and G[32][COUT] in LDS,
 // then D(k x co) += X^T G on the MFMA (A operand = X^T: lane i <-> k, kk <-> pixel).
+// Each thread's X unit (4 consecutive k) is fixed for the whole kernel, so its
+// within-sample offset is computed once; its pixels advance by MS per step with
+// 32-bit (sample, pixel) counters (MS <= P, so at most one wrap) — no divisions
+// of 64-bit indices in the loop.
 // ---------------------------------------------------------------------------
 constexpr int MS = 32;
 
@@ -345,15 +354,21 @@ struct WgCfg {
     static constexpr int KT = (L::COUT == 32) ? 128 : 64;  // 4 tiles of 32x32 per WG
     static constexpr int KB = L::K / KT;
     static constexpr int XST = KT + 1, GST = L::COUT + 1;
+    static constexpr int UPR = KT / 4;         // 4-element X units per pixel
+    static constexpr int XV = MS * UPR / 256;  // X units per thread per step
+    static constexpr int XPS = 256 / UPR;      // pixel stride between a thread's X units
+    static constexpr int GUPR = L::COUT / 4;
+    static constexpr int GV = MS * GUPR / 256;
+    static constexpr int GPS = 256 / GUPR;
+    static_assert(MS <= L::P, "one wrap per step");
 };
 
 struct WArgs {
-    const void* x;          // layer input (u8 frames for conv1, NHWC f32 otherwise)
-    const long long* idx;   // conv1: optional env-major rollout rows
-    long long T, Nenv, sample_stride;
-    const float* g;         // output grad, NHWC (batch, OH, OW, COUT), ReLU mask already applied
-    float* slab;            // [splits][K][COUT]
-    float* bslab;           // [splits][COUT]
+    const void* x;        // layer input (u8 frames for conv1, NHWC f32 otherwise)
+    long long sample_stride;  // conv1: bytes between samples
+    const float* g;       // output grad, NHWC (batch, OH, OW, COUT), ReLU mask already applied
+    float* slab;          // [splits][K][COUT]
+    float* bslab;         // [splits][COUT]
     long long batch;
     long long px_per_split;
     int splits;
@@ -363,82 +378,87 @@ template <class L, bool U8>
 __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
     using C = WgCfg<L, U8>;
     constexpr int KT = C::KT, KB = C::KB, XST = C::XST, GST = C::GST, COUT = L::COUT;
+    constexpr int XV = C::XV, GV = C::GV, UPR = C::UPR, GUPR = C::GUPR;
     __shared__ float Xs[2][MS * XST];
     __shared__ float Gs[2][MS * GST];
     // XCD-aware block -> (split, kb): the KB k-blocks of a split share blockIdx % 8
     const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
     const int kb = q % KB, split = (q / KB) * 8 + xcd;
-    const long long M = a.batch * L::P;
-    const long long mbeg = (long long)split * a.px_per_split;
-    const long long mend = min(M, mbeg + a.px_per_split);
+    const unsigned M = (unsigned)(a.batch * L::P);
+    const unsigned long long mb64 = (unsigned long long)split * (unsigned long long)a.px_per_split;
+    const unsigned mbeg = mb64 < M ? (unsigned)mb64 : M;
+    const unsigned mend = (unsigned)min((unsigned long long)M, (unsigned long long)mbeg + a.px_per_split);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int kt = (COUT == 32) ? wave : (wave >> 1), ct = (COUT == 32) ? 0 : (wave & 1);
     f32x16 acc = zero16();
 
-    // staging geometry (per thread, fixed across steps)
-    constexpr int XV = MS * KT / 4 / 256;  // 4-element units per thread for X (float4 or u32)
-    constexpr int GV = MS * COUT / 4 / 256;
-    float4 xr[XV];
-    uint32_t xu[XV];
-    float4 gr[GV];
-    float bsum[GV][4];
+    // ---- fixed per-thread X unit ----
+    const int u = threadIdx.x % UPR, px0 = threadIdx.x / UPR;
+    const int k = kb * KT + u * 4;
+    unsigned koff;
+    if constexpr (U8) {
+        koff = ((k >> 6) * L::IH + ((k >> 3) & 7)) * L::IW + (k & 7);  // (ci, ky, kx) in a NCHW frame stack
+    } else {
+        const int tap = k / L::CIN;
+        koff = ((tap / L::KW) * L::IW + (tap % L::KW)) * L::CIN + (k % L::CIN);  // (ky, kx, ci) NHWC
+    }
+    unsigned xn[XV], xp[XV];
 #pragma unroll
-    for (int j = 0; j < GV; ++j) bsum[j][0] = bsum[j][1] = bsum[j][2] = bsum[j][3] = 0.f;
+    for (int i = 0; i < XV; ++i) {
+        const unsigned m = mbeg + px0 + i * C::XPS;
+        xn[i] = m / L::P;
+        xp[i] = m - xn[i] * L::P;
+    }
+    const unsigned xn0 = mbeg / L::P, xp0 = mbeg - xn0 * L::P;  // a pixel that always exists
+    const int c4 = threadIdx.x % GUPR, gpx0 = threadIdx.x / GUPR;
+    const uint8_t* xu8 = reinterpret_cast<const uint8_t*>(a.x);
+    const float* xf = reinterpret_cast<const float*>(a.x);
 
-    auto load = [&](long long ms) {
+    float4 xr[XV];
+    uint32_t xw[XV];
+    float4 gr[GV];
+    float bsum0 = 0.f, bsum1 = 0.f, bsum2 = 0.f, bsum3 = 0.f;
+
+    auto load = [&](unsigned ms) {
 #pragma unroll
         for (int i = 0; i < XV; ++i) {
-            const int w = i * 256 + threadIdx.x;
-            const long long m = ms + w / (KT / 4);
-            const int u = w % (KT / 4);  // 4-element unit within the pixel's KT k-values
-            if (m < mend) {
-                const long long n = m / L::P;
-                const int p = (int)(m - n * L::P), oy = p / L::OW, ox = p % L::OW;
-                if constexpr (U8) {
-                    // k = kb*128 + u*4 + e: ci = k / 64, ky = (k / 8) % 8, kx = k % 8 (kx run of 4)
-                    const int k = kb * KT + u * 4;
-                    const int ci = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
-                    const uint8_t* x = reinterpret_cast<const uint8_t*>(a.x);
-                    long long base;
-                    if (a.idx) {
-                        const long long ie = a.idx[n];
-                        base = ((ie % a.T) * a.Nenv + ie / a.T) * (long long)(L::CIN * L::IH * L::IW);
-                    } else {
-                        base = n * a.sample_stride;
-                    }
-                    xu[i] = *reinterpret_cast<const uint32_t*>(
-                        x + base + (ci * L::IH + oy * L::S + ky) * L::IW + ox * L::S + kx);
-                } else {
-                    // k = (ky, kx, ci) NHWC order
-                    const int k = kb * KT + u * 4;
-                    const int tap = k / L::CIN, ci = k % L::CIN, ky = tap / L::KW, kx = tap % L::KW;
-                    const float* x = reinterpret_cast<const float*>(a.x);
-                    xr[i] = *reinterpret_cast<const float4*>(
-                        x + ((n * L::IH + oy * L::S + ky) * L::IW + ox * L::S + kx) * L::CIN + ci);
-                }
+            const unsigned m = ms + px0 + i * C::XPS;
+            const bool ok = m < mend;  // past the slice end: clamp to its first pixel, zero by select
+            const unsigned n = ok ? xn[i] : xn0, pp = ok ? xp[i] : xp0;
+            const unsigned oy = pp / L::OW, ox = pp - oy * L::OW;
+            if constexpr (U8) {
+                const unsigned long long off = (unsigned long long)n * (unsigned long long)a.sample_stride +
+                                               (oy * L::S * L::IW + ox * L::S + koff);
+                const uint32_t v = *reinterpret_cast<const uint32_t*>(xu8 + off);
+                xw[i] = ok ? v : 0u;
             } else {
-                xr[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-                xu[i] = 0u;
+                const unsigned off = ((n * L::IH + oy * L::S) * L::IW + ox * L::S) * L::CIN + koff;
+                const float4 v = *reinterpret_cast<const float4*>(xf + off);
+                xr[i] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            xp[i] += MS;  // advance to the next step's pixel
+            if (xp[i] >= (unsigned)L::P) {
+                xp[i] -= L::P;
+                xn[i] += 1;
             }
         }
 #pragma unroll
         for (int j = 0; j < GV; ++j) {
-            const int w = j * 256 + threadIdx.x;
-            const long long m = ms + w / (COUT / 4);
-            gr[j] = m < mend ? reinterpret_cast<const float4*>(a.g + m * COUT)[w % (COUT / 4)]
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+            const unsigned m = ms + gpx0 + j * C::GPS;
+            const bool ok = m < mend;
+            const float4 v = *reinterpret_cast<const float4*>(a.g + (ok ? m : mbeg) * COUT + c4 * 4);
+            gr[j] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
     auto store = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < XV; ++i) {
-            const int w = i * 256 + threadIdx.x;
-            float* d = Xs[buf] + (w / (KT / 4)) * XST + (w % (KT / 4)) * 4;
+            float* d = Xs[buf] + (px0 + i * C::XPS) * XST + u * 4;
             if constexpr (U8) {
-                d[0] = (float)(xu[i] & 0xFFu);
-                d[1] = (float)((xu[i] >> 8) & 0xFFu);
-                d[2] = (float)((xu[i] >> 16) & 0xFFu);
-                d[3] = (float)(xu[i] >> 24);
+                d[0] = (float)(xw[i] & 0xFFu);
+                d[1] = (float)((xw[i] >> 8) & 0xFFu);
+                d[2] = (float)((xw[i] >> 16) & 0xFFu);
+                d[3] = (float)(xw[i] >> 24);
             } else {
                 d[0] = xr[i].x;
                 d[1] = xr[i].y;
@@ -448,32 +468,31 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
         }
 #pragma unroll
         for (int j = 0; j < GV; ++j) {
-            const int w = j * 256 + threadIdx.x;
-            float* d = Gs[buf] + (w / (COUT / 4)) * GST + (w % (COUT / 4)) * 4;
+            float* d = Gs[buf] + (gpx0 + j * C::GPS) * GST + c4 * 4;
             d[0] = gr[j].x;
             d[1] = gr[j].y;
             d[2] = gr[j].z;
             d[3] = gr[j].w;
-            if (kb == 0) {
-                bsum[j][0] += gr[j].x;
-                bsum[j][1] += gr[j].y;
-                bsum[j][2] += gr[j].z;
-                bsum[j][3] += gr[j].w;
-            }
+            bsum0 += gr[j].x;
+            bsum1 += gr[j].y;
+            bsum2 += gr[j].z;
+            bsum3 += gr[j].w;
         }
     };
 
-    const long long nsteps = mend > mbeg ? (mend - mbeg + MS - 1) / MS : 0;
+    const unsigned nsteps = mend > mbeg ? (mend - mbeg + MS - 1) / MS : 0;
     if (nsteps > 0) {
         load(mbeg);
         store(0);
     }
     __syncthreads();
-    for (long long s = 0; s < nsteps; ++s) {
+    const float* Xbase = &Xs[0][0] + (lane >> 5) * XST + kt * 32 + (lane & 31);
+    const float* Gbase = &Gs[0][0] + (lane >> 5) * GST + ct * 32 + (lane & 31);
+    for (unsigned s = 0; s < nsteps; ++s) {
         const int cur = (int)(s & 1);
         if (s + 1 < nsteps) load(mbeg + (s + 1) * MS);
-        const float* X = Xs[cur] + (lane >> 5) * XST + kt * 32 + (lane & 31);
-        const float* G = Gs[cur] + (lane >> 5) * GST + ct * 32 + (lane & 31);
+        const float* X = Xbase + cur * (MS * XST);
+        const float* G = Gbase + cur * (MS * GST);
 #pragma unroll
         for (int kk = 0; kk < MS / 2; ++kk)
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(X[kk * 2 * XST], G[kk * 2 * GST], acc, 0, 0, 0);
@@ -484,24 +503,22 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
     float* slab = a.slab + (long long)split * L::K * COUT;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int k = kb * KT + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        slab[k * COUT + ct * 32 + (lane & 31)] = acc[r];
+        const int kr = kb * KT + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        slab[kr * COUT + ct * 32 + (lane & 31)] = acc[r];
     }
     if (kb == 0) {
-        // bias grad partial: column sums of this split's G rows
-        __shared__ float bred[256 / (COUT / 4) * COUT];
-        constexpr int ROWS_PER_PASS = 256 / (COUT / 4);
-        float tot[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < GV; ++j)
-            for (int e = 0; e < 4; ++e) tot[e] += bsum[j][e];
-        const int rgrp = threadIdx.x / (COUT / 4), c4 = threadIdx.x % (COUT / 4);
-        for (int e = 0; e < 4; ++e) bred[rgrp * COUT + c4 * 4 + e] = tot[e];
+        // bias grad partial: column sums of this split's G rows (each thread owns columns c4*4..+3)
+        constexpr int GROUPS = 256 / GUPR;
+        __shared__ float bred[GROUPS * COUT];
+        bred[gpx0 * COUT + c4 * 4 + 0] = bsum0;
+        bred[gpx0 * COUT + c4 * 4 + 1] = bsum1;
+        bred[gpx0 * COUT + c4 * 4 + 2] = bsum2;
+        bred[gpx0 * COUT + c4 * 4 + 3] = bsum3;
         __syncthreads();
         if (threadIdx.x < COUT) {
-            float s = 0.f;
-            for (int g = 0; g < ROWS_PER_PASS; ++g) s += bred[g * COUT + threadIdx.x];
-            a.bslab[(long long)split * COUT + threadIdx.x] = s;
+            float t = 0.f;
+            for (int g = 0; g < GROUPS; ++g) t += bred[g * COUT + threadIdx.x];
+            a.bslab[(long long)split * COUT + threadIdx.x] = t;
         }
     }
 }
@@ -692,11 +709,14 @@ extern "C" int ppox_nature_conv_wgrad(int32_t layer, const void* x, int64_t batc
     const int splits = (int)ppox_nature_wgrad_splits(layer, batch);
     const long long kc = layer == 1 ? G1::K * G1::COUT : (layer == 2 ? G2::K * G2::COUT : G3::K * G3::COUT);
     float* slab = reinterpret_cast<float*>(workspace);
-    WArgs wa{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, grad_out, slab,
-             slab + (long long)splits * kc, batch, 0, splits};
+    WArgs wa{x, x_sample_stride, grad_out, slab, slab + (long long)splits * kc, batch, 0, splits};
     hipStream_t s = ppox::as_stream(stream);
+    PPOX_REQUIRE(!idx, "ppox_nature_conv_wgrad: gathered (idx) input not supported; gather first");
+    PPOX_REQUIRE(batch * (layer == 1 ? G1::P : layer == 2 ? G2::P : G3::P) < (1LL << 31) / 64,
+                 "ppox_nature_conv_wgrad: batch too large for 32-bit pixel indexing");
     if (layer == 1) {
-        PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3), "ppox_nature_conv_wgrad: u8 input 4-byte aligned");
+        PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && x_sample_stride % 4 == 0,
+                     "ppox_nature_conv_wgrad: u8 input 4-byte aligned");
         return launch_wgrad<G1, true>(wa, s);
     }
     PPOX_REQUIRE(ppox::aligned16(x) && !idx, "ppox_nature_conv_wgrad: layer 2/3 input must be 16B-aligned NHWC");
