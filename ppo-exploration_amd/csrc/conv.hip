@@ -35,8 +35,13 @@ namespace {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-constexpr int BM = 128;
 constexpr int BK = 32;
+#ifndef FWD1_MT
+#define FWD1_MT 1  // rows per wave / 32 for the NT = 1 (32-channel) kernels
+#endif
+#ifndef DGRAD2_MT
+#define DGRAD2_MT 1
+#endif
 constexpr int AST = BK + 1;  // padded LDS row stride (floats): conflict-free column reads
 
 template <int CIN_, int IH_, int IW_, int KH_, int KW_, int S_, int COUT_>
@@ -77,28 +82,34 @@ __device__ inline long long u8_sample_base(const Args& a, long long n, long long
 }
 
 // ---------------------------------------------------------------------------
-// A stagers: global -> registers (load) -> LDS (store), 4 slots per thread.
-// Slot i of thread t covers element w = i*256 + t of the BM x BK chunk.
-// ---------------------------------------------------------------------------
-// conv1 forward: uint8 NCHW frames, K order (ci, ky, kx); chunk = 1 channel x 4
-// kernel rows x 8 columns -> 4 runs of 8 bytes per row (2 words each).
-// Rows past M read a valid clamped address and are zeroed by a select: a
+// A stagers: global -> registers (load) -> LDS (store), 4*MT slots per thread.
+// Slot i of thread t covers element w = i*256 + t of the (128*MT) x BK chunk.
+// Rows past the end read a valid clamped address and are zeroed by a select: a
 // conditional load would make hipcc branch around every load (execz) and
 // serialise them.
+// ---------------------------------------------------------------------------
+struct RowTile {  // forward: a contiguous run of output pixels
+    long long m0, M;
+};
+
+// conv1 forward: uint8 NCHW frames, K order (ci, ky, kx); chunk = 1 channel x 4
+// kernel rows x 8 columns -> 4 runs of 8 bytes per row (2 words each).
+template <int MT>
 struct StageFwd1 {
     using L = G1;
-    const uint8_t* base[4];
-    bool ok[4];
-    uint32_t r[4];
-    __device__ StageFwd1(const Args& a, long long m0, long long M) {
+    static constexpr int SL = 4 * MT;
+    const uint8_t* base[SL];
+    bool ok[SL];
+    uint32_t r[SL];
+    __device__ StageFwd1(const Args& a, const RowTile& t) {
         const uint8_t* x = reinterpret_cast<const uint8_t*>(a.x);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < SL; ++i) {
             const int w = i * 256 + threadIdx.x;
             const int row = w >> 3, seg = (w & 7) >> 1, half = w & 1;
-            const long long m = m0 + row;
-            ok[i] = m < M;
-            const long long mm = ok[i] ? m : m0;
+            const long long m = t.m0 + row;
+            ok[i] = m < t.M;
+            const long long mm = ok[i] ? m : t.m0;
             const long long n = mm / L::P;
             const int p = (int)(mm - n * L::P), oy = p / L::OW, ox = p % L::OW;
             base[i] = x + u8_sample_base(a, n, (long long)L::CIN * L::IH * L::IW) + (oy * L::S + seg) * L::IW +
@@ -108,14 +119,14 @@ struct StageFwd1 {
     __device__ inline void load(int chunk) {
         const int off = (chunk >> 1) * (L::IH * L::IW) + (chunk & 1) * 4 * L::IW;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < SL; ++i) {
             const uint32_t v = *reinterpret_cast<const uint32_t*>(base[i] + off);
             r[i] = ok[i] ? v : 0u;
         }
     }
     __device__ inline void store(float* As) const {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < SL; ++i) {
             const int w = i * 256 + threadIdx.x;
             const int row = w >> 3, seg = (w & 7) >> 1, half = w & 1;
             float* d = As + row * AST + seg * 8 + half * 4;
@@ -127,21 +138,36 @@ struct StageFwd1 {
     }
 };
 
+// f32 rows of 32 floats (8 float4 per row) -> LDS
+template <int SL>
+__device__ inline void store_rows_f4(float* As, const float4 (&r)[SL]) {
+#pragma unroll
+    for (int i = 0; i < SL; ++i) {
+        const int w = i * 256 + threadIdx.x;
+        float* d = As + (w >> 3) * AST + (w & 7) * 4;
+        d[0] = r[i].x;
+        d[1] = r[i].y;
+        d[2] = r[i].z;
+        d[3] = r[i].w;
+    }
+}
+
 // NHWC f32 forward (conv2, conv3): K order (ky, kx, ci); chunk = 32 channels of one tap.
-template <class L>
+template <class L, int MT>
 struct StageFwdNHWC {
-    const float* base[4];
-    bool ok[4];
-    float4 r[4];
-    __device__ StageFwdNHWC(const Args& a, long long m0, long long M) {
+    static constexpr int SL = 4 * MT;
+    const float* base[SL];
+    bool ok[SL];
+    float4 r[SL];
+    __device__ StageFwdNHWC(const Args& a, const RowTile& t) {
         const float* x = reinterpret_cast<const float*>(a.x);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < SL; ++i) {
             const int w = i * 256 + threadIdx.x;
             const int row = w >> 3, q = w & 7;
-            const long long m = m0 + row;
-            ok[i] = m < M;
-            const long long mm = ok[i] ? m : m0;
+            const long long m = t.m0 + row;
+            ok[i] = m < t.M;
+            const long long mm = ok[i] ? m : t.m0;
             const long long n = mm / L::P;
             const int p = (int)(mm - n * L::P), oy = p / L::OW, ox = p % L::OW;
             base[i] = x + ((n * L::IH + oy * L::S) * L::IW + ox * L::S) * L::CIN + q * 4;
@@ -153,87 +179,22 @@ struct StageFwdNHWC {
         const int off = (ky * L::IW + kx) * L::CIN + (chunk % CPT) * BK;
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < SL; ++i) {
             const float4 v = *reinterpret_cast<const float4*>(base[i] + off);
             r[i] = ok[i] ? v : z;
         }
     }
-    __device__ inline void store(float* As) const {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int w = i * 256 + threadIdx.x;
-            float* d = As + (w >> 3) * AST + (w & 7) * 4;
-            d[0] = r[i].x;
-            d[1] = r[i].y;
-            d[2] = r[i].z;
-            d[3] = r[i].w;
-        }
-    }
-};
-
-// dgrad (transposed conv) gather of the output grad G (NHWC, OH x OW x COUT).
-// Rows are input pixels of one parity class (py, px): iy = S*jy + py.  Taps are
-// the TY x TX kernel offsets ky = py + S*ty contributing to that class; the
-// source pixel is oy = jy - ty, ox = jx - tx, zero outside the output grid.
-// K' order (ty, tx, co); chunk = 32 output channels of one tap.
-template <class L>
-struct StageDgrad {
-    static constexpr int JH = L::IH / L::S, JW = L::IW / L::S;  // class grid
-    static constexpr int TY = L::KH / L::S, TX = L::KW / L::S;  // taps per class
-    const float* base[4];
-    int jy[4], jx[4];
-    float4 r[4];
-    __device__ StageDgrad(const Args& a, long long m0, long long M) {
-        const float* g = reinterpret_cast<const float*>(a.x);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int w = i * 256 + threadIdx.x;
-            const int row = w >> 3, q = w & 7;
-            const long long m = m0 + row;
-            const bool in = m < M;
-            const long long mm = in ? m : m0;
-            const long long n = mm / (JH * JW);
-            const int p = (int)(mm - n * (JH * JW));
-            jy[i] = in ? p / JW : -100;  // out-of-range rows never pass the tap test
-            jx[i] = p % JW;
-            base[i] = g + n * (L::P * L::COUT) + q * 4;
-        }
-    }
-    __device__ inline void load(int chunk) {
-        constexpr int CPT = L::COUT / BK;
-        const int tap = chunk / CPT, ty = tap / TX, tx = tap % TX;
-        const int co0 = (chunk % CPT) * BK;
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int oy = jy[i] - ty, ox = jx[i] - tx;
-            const bool ok = oy >= 0 && oy < L::OH && ox >= 0 && ox < L::OW;
-            const float4 v = *reinterpret_cast<const float4*>(base[i] + (ok ? (oy * L::OW + ox) * L::COUT : 0) + co0);
-            r[i] = ok ? v : z;
-        }
-    }
-    __device__ inline void store(float* As) const {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int w = i * 256 + threadIdx.x;
-            float* d = As + (w >> 3) * AST + (w & 7) * 4;
-            d[0] = r[i].x;
-            d[1] = r[i].y;
-            d[2] = r[i].z;
-            d[3] = r[i].w;
-        }
-    }
+    __device__ inline void store(float* As) const { store_rows_f4<SL>(As, r); }
 };
 
 template <int NOUT>
 struct StageB {
     static constexpr int V = BK * NOUT / 4 / 256;  // float4 per thread
-    const float4* src;
     float4 r[V];
-    __device__ explicit StageB(const float* wp) : src(reinterpret_cast<const float4*>(wp)) {}
-    __device__ inline void load(int chunk) {
+    __device__ inline void load(const float* chunk_base) {
+        const float4* src = reinterpret_cast<const float4*>(chunk_base);
 #pragma unroll
-        for (int i = 0; i < V; ++i) r[i] = src[(long long)chunk * (BK * NOUT / 4) + i * 256 + threadIdx.x];
+        for (int i = 0; i < V; ++i) r[i] = src[i * 256 + threadIdx.x];
     }
     __device__ inline void store(float* Bs) const {
 #pragma unroll
@@ -242,15 +203,22 @@ struct StageB {
 };
 
 // ---------------------------------------------------------------------------
-// Problems: row count, stager, packed-B pointer, chunk count, epilogue.
+// Problems: tile of a block, chunk count, stagers, packed-B chunk, epilogue.
 // ---------------------------------------------------------------------------
-template <class L, class SA, bool OUT_NCHW>
-struct FwdProblem {
-    static constexpr int NOUT = L::COUT, NCHUNK = L::K / BK;
-    using Stager = SA;
-    __device__ static long long rows(const Args& a) { return a.batch * L::P; }
-    __device__ static const float* bpack(const Args& a) { return a.wp; }
-    __device__ static void store(const Args& a, long long m, int co, float acc) {
+template <class L, bool OUT_NCHW, int MT_>
+struct FwdBase {
+    static constexpr int NOUT = L::COUT, MT = MT_, BMR = 128 * MT;
+    using Tile = RowTile;
+    __device__ static bool tile(const Args& a, Tile& t) {
+        t.m0 = (long long)blockIdx.x * BMR;
+        t.M = a.batch * L::P;
+        return true;
+    }
+    __device__ static int nchunk(const Tile&) { return L::K / BK; }
+    __device__ static const float* bchunk(const Args& a, const Tile&, int c) { return a.wp + (long long)c * BK * NOUT; }
+    __device__ static void store(const Args& a, const Tile& t, int row, int co, float acc) {
+        const long long m = t.m0 + row;
+        if (m >= t.M) return;
         const float v = fmaxf(acc + a.bias[co], 0.f);
         if constexpr (OUT_NCHW) {
             const long long n = m / L::P;
@@ -261,66 +229,161 @@ struct FwdProblem {
     }
 };
 
-// dgrad of layer L: output = grad of L's input (NHWC IH x IW x CIN), masked by
-// the previous activation (a.mask, same layout).  blockIdx.y = parity class.
-template <class L>
-struct DgradProblem {
-    using St = StageDgrad<L>;
-    static constexpr int NOUT = L::CIN, NCHUNK = St::TY * St::TX * L::COUT / BK;
-    using Stager = St;
-    __device__ static long long rows(const Args& a) { return a.batch * St::JH * St::JW; }
-    __device__ static const float* bpack(const Args& a) {
-        return a.wp + (long long)blockIdx.y * (St::TY * St::TX * L::COUT) * L::CIN;
+template <int MT>
+struct Fwd1Problem : FwdBase<G1, false, MT> {
+    using Stager = StageFwd1<MT>;
+};
+template <class L, bool OUT_NCHW, int MT>
+struct FwdNHWCProblem : FwdBase<L, OUT_NCHW, MT> {
+    using Stager = StageFwdNHWC<L, MT>;
+};
+
+// dgrad (transposed conv) of layer L, position-major: a block owns ONE input
+// pixel (iy, ix) of 128*MT consecutive samples, so every row of the tile has the
+// same contributing taps — exactly those (ky, kx) with iy = S*oy + ky inside the
+// output grid.  The K walk covers only those taps (no zero MACs: conv3 borders
+// have 4-6 of 9, every conv2 pixel 1-4 of 16).  K order (tap, co); chunk = 32
+// output channels of one tap, gathered from the NHWC output grad G at the same
+// (oy, ox) for every row.  Epilogue: x (previous activation > 0), NHWC.
+// Blocks -> (sample tile, pixel) XCD-aware: one XCD walks the pixels of one
+// sample tile, whose G rows then stay in that XCD's L2.
+struct PixelTile {
+    long long n0;
+    int pos, iy, ix, ky0, kx0, nx, nchunk;
+};
+
+__device__ inline long long xcd_remap(long long b, long long nwg) {
+    const long long q = nwg / 8, r = nwg % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// first tap index k with k == i (mod S), S*o + k == i for some 0 <= o < O, and its count
+template <int S, int O, int KN>
+__device__ inline void tap_range(int i, int& k0, int& cnt) {
+    int lo = i - S * (O - 1);
+    lo = lo < 0 ? 0 : lo;
+    k0 = lo + ((i - lo) % S);
+    const int hi = i < KN - 1 ? i : KN - 1;
+    cnt = hi >= k0 ? (hi - k0) / S + 1 : 0;
+}
+
+template <class L, int MT>
+struct StageDgradPM {
+    static constexpr int SL = 4 * MT, CPT = L::COUT / BK;
+    const float* base[SL];
+    bool ok[SL];
+    float4 r[SL];
+    int iy, ix, ky0, kx0, nx;
+    __device__ StageDgradPM(const Args& a, const PixelTile& t)
+        : iy(t.iy), ix(t.ix), ky0(t.ky0), kx0(t.kx0), nx(t.nx) {
+        const float* g = reinterpret_cast<const float*>(a.x);
+#pragma unroll
+        for (int i = 0; i < SL; ++i) {
+            const int w = i * 256 + threadIdx.x;
+            const long long n = t.n0 + (w >> 3);
+            ok[i] = n < a.batch;
+            base[i] = g + (ok[i] ? n : t.n0) * (L::P * L::COUT) + (w & 7) * 4;
+        }
     }
-    __device__ static void store(const Args& a, long long m, int ci, float acc) {
-        const long long n = m / (St::JH * St::JW);
-        const int p = (int)(m - n * (St::JH * St::JW));
-        const int py = blockIdx.y / L::S, px = blockIdx.y % L::S;
-        const int iy = (p / St::JW) * L::S + py, ix = (p % St::JW) * L::S + px;
-        const long long o = ((n * L::IH + iy) * L::IW + ix) * L::CIN + ci;
+    __device__ inline void load(int chunk) {
+        const int tap = chunk / CPT, ty = tap / nx, tx = tap - ty * nx;
+        const int oy = (iy - ky0) / L::S - ty, ox = (ix - kx0) / L::S - tx;
+        const int off = (oy * L::OW + ox) * L::COUT + (chunk % CPT) * BK;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < SL; ++i) {
+            const float4 v = *reinterpret_cast<const float4*>(base[i] + off);
+            r[i] = ok[i] ? v : z;
+        }
+    }
+    __device__ inline void store(float* As) const { store_rows_f4<SL>(As, r); }
+};
+
+template <class L, int MT_>
+struct DgradPMProblem {
+    static constexpr int NOUT = L::CIN, MT = MT_, BMR = 128 * MT, NPOS = L::IH * L::IW, CPT = L::COUT / BK;
+    using Tile = PixelTile;
+    using Stager = StageDgradPM<L, MT>;
+    __device__ static bool tile(const Args& a, Tile& t) {
+        const long long w = xcd_remap(blockIdx.x, gridDim.x);
+        t.n0 = (w / NPOS) * BMR;
+        t.pos = (int)(w % NPOS);
+        t.iy = t.pos / L::IW;
+        t.ix = t.pos % L::IW;
+        int ny, nx;
+        tap_range<L::S, L::OH, L::KH>(t.iy, t.ky0, ny);
+        tap_range<L::S, L::OW, L::KW>(t.ix, t.kx0, nx);
+        t.nx = nx;
+        t.nchunk = ny * nx * CPT;
+        return true;
+    }
+    __device__ static int nchunk(const Tile& t) { return t.nchunk; }
+    __device__ static const float* bchunk(const Args& a, const Tile& t, int c) {
+        const int tap = c / CPT, ty = tap / t.nx, tx = tap - ty * t.nx;
+        const int ky = t.ky0 + L::S * ty, kx = t.kx0 + L::S * tx;
+        return a.wp + ((long long)(ky * L::KW + kx) * L::COUT + (c % CPT) * BK) * L::CIN;
+    }
+    __device__ static void store(const Args& a, const Tile& t, int row, int ci, float acc) {
+        const long long n = t.n0 + row;
+        if (n >= a.batch) return;
+        const long long o = (n * NPOS + t.pos) * L::CIN + ci;
         a.y[o] = a.mask[o] > 0.f ? acc : 0.f;
     }
 };
 
+// One 256-thread workgroup: 128*MT rows x NOUT columns; each wave 32*MT rows
+// (MT x NT MFMA tiles).  K walked in BK = 32 chunks, register-staged and
+// double-buffered in LDS, one barrier per chunk.
 template <class Prob>
 __global__ void __launch_bounds__(256, 2) igemm_kernel(Args a) {
-    constexpr int NOUT = Prob::NOUT, NT = NOUT / 32, NCHUNK = Prob::NCHUNK;
-    __shared__ float As[2][BM * AST];
+    constexpr int NOUT = Prob::NOUT, NT = NOUT / 32, MT = Prob::MT, BMR = 128 * MT;
+    __shared__ float As[2][BMR * AST];
     __shared__ __attribute__((aligned(16))) float Bs[2][BK * NOUT];
-    const long long M = Prob::rows(a);
-    const long long m0 = (long long)blockIdx.x * BM;
+    typename Prob::Tile t;
+    if (!Prob::tile(a, t)) return;
+    const int nchunk = Prob::nchunk(t);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
-    f32x16 acc[NT];
+    f32x16 acc[MT][NT];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[j] = zero16();
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = zero16();
 
-    typename Prob::Stager sa(a, m0, M);
-    StageB<NOUT> sb(Prob::bpack(a));
-    sa.load(0);
-    sb.load(0);
-    sa.store(As[0]);
-    sb.store(Bs[0]);
+    typename Prob::Stager sa(a, t);
+    StageB<NOUT> sb;
+    if (nchunk > 0) {
+        sa.load(0);
+        sb.load(Prob::bchunk(a, t, 0));
+        sa.store(As[0]);
+        sb.store(Bs[0]);
+    }
     __syncthreads();
 
-    const int arow = wave * 32 + (lane & 31);
+    const int arow = wave * 32 * MT + (lane & 31);
     const int khalf = lane >> 5;
-    for (int c = 0; c < NCHUNK; ++c) {
+    for (int c = 0; c < nchunk; ++c) {
         const int cur = c & 1;
-        if (c + 1 < NCHUNK) {
+        if (c + 1 < nchunk) {
             sa.load(c + 1);
-            sb.load(c + 1);
+            sb.load(Prob::bchunk(a, t, c + 1));
         }
         const float* A = As[cur] + arow * AST + khalf;
         const float* B = Bs[cur] + khalf * NOUT + (lane & 31);
 #pragma unroll
         for (int kk = 0; kk < BK / 2; ++kk) {
-            const float av = A[kk * 2];
+            float av[MT];
 #pragma unroll
-            for (int j = 0; j < NT; ++j)
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, B[kk * 2 * NOUT + j * 32], acc[j], 0, 0, 0);
+            for (int i = 0; i < MT; ++i) av[i] = A[i * 32 * AST + kk * 2];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const float bv = B[kk * 2 * NOUT + j * 32];
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv, acc[i][j], 0, 0, 0);
+            }
         }
-        if (c + 1 < NCHUNK) {
+        if (c + 1 < nchunk) {
             sa.store(As[cur ^ 1]);
             sb.store(Bs[cur ^ 1]);
         }
@@ -328,14 +391,15 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(Args a) {
     }
     // C/D map: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-        const int col = j * 32 + (lane & 31);
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const long long m = m0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            if (m < M) Prob::store(a, m, col, acc[j][r]);
+        for (int j = 0; j < NT; ++j) {
+            const int col = j * 32 + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                Prob::store(a, t, wave * 32 * MT + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), col,
+                            acc[i][j][r]);
         }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -595,23 +659,19 @@ __global__ void pack_fwd(const float* __restrict__ w, float* __restrict__ wp) {
     wp[i] = w[((co * L::CIN + ci) * L::KH + ky) * L::KW + kx];
 }
 
-// dgrad: per parity class (py, px): [(ty, tx, co)][ci], ky = py + S*ty
+// dgrad: [(ky, kx, co)][ci] — chunk (tap, 32 co) is a contiguous 32 x CIN block
 template <class L>
 __global__ void pack_dgrad(const float* __restrict__ w, float* __restrict__ wp) {
-    constexpr int TY = L::KH / L::S, TX = L::KW / L::S, KC = TY * TX * L::COUT;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= L::S * L::S * KC * L::CIN) return;
-    const int cls = i / (KC * L::CIN), rem = i % (KC * L::CIN);
-    const int kp = rem / L::CIN, ci = rem % L::CIN;
-    const int tap = kp / L::COUT, co = kp % L::COUT;
-    const int ky = cls / L::S + L::S * (tap / TX), kx = cls % L::S + L::S * (tap % TX);
-    wp[i] = w[((co * L::CIN + ci) * L::KH + ky) * L::KW + kx];
+    if (i >= L::KH * L::KW * L::COUT * L::CIN) return;
+    const int ci = i % L::CIN, co = (i / L::CIN) % L::COUT, tap = i / (L::CIN * L::COUT);
+    wp[i] = w[((co * L::CIN + ci) * L::KH + tap / L::KW) * L::KW + tap % L::KW];
 }
 
 template <class Prob>
-int launch_igemm(const Args& a, long long rows, int classes, hipStream_t s, const char* name) {
-    if (rows == 0) return PPOX_OK;
-    igemm_kernel<Prob><<<dim3(ppox::ceil_div(rows, BM), classes), 256, 0, s>>>(a);
+int launch_igemm(const Args& a, long long blocks, hipStream_t s, const char* name) {
+    if (blocks == 0) return PPOX_OK;
+    igemm_kernel<Prob><<<(unsigned)blocks, 256, 0, s>>>(a);
     PPOX_LAUNCHED(name);
 }
 
@@ -645,8 +705,8 @@ extern "C" int ppox_nature_pack_weights(const float* w1, const float* w2, const 
     pack_fwd<G1, false><<<ppox::ceil_div(G1::K * 32, 256), 256, 0, s>>>(w1, wp1);
     pack_fwd<G2, true><<<ppox::ceil_div(G2::K * 64, 256), 256, 0, s>>>(w2, wp2);
     pack_fwd<G3, true><<<ppox::ceil_div(G3::K * 64, 256), 256, 0, s>>>(w3, wp3);
-    if (wpd2) pack_dgrad<G2><<<ppox::ceil_div(G2::K * G2::COUT / G2::CIN * G2::CIN, 256), 256, 0, s>>>(w2, wpd2);
-    if (wpd3) pack_dgrad<G3><<<ppox::ceil_div(G3::K * G3::COUT / G3::CIN * G3::CIN, 256), 256, 0, s>>>(w3, wpd3);
+    if (wpd2) pack_dgrad<G2><<<ppox::ceil_div(G2::K * G2::COUT, 256), 256, 0, s>>>(w2, wpd2);
+    if (wpd3) pack_dgrad<G3><<<ppox::ceil_div(G3::K * G3::COUT, 256), 256, 0, s>>>(w3, wpd3);
     PPOX_LAUNCHED("ppox_nature_pack_weights");
 }
 
@@ -663,12 +723,16 @@ extern "C" int ppox_nature_conv_fwd(int32_t layer, const void* x, int64_t batch,
         PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && (idx || x_sample_stride % 4 == 0),
                      "ppox_nature_conv_fwd: u8 input must be 4-byte aligned");
         if (idx) PPOX_REQUIRE(T > 0 && N_env > 0, "ppox_nature_conv_fwd: idx needs T and N_env");
-        return launch_igemm<FwdProblem<G1, StageFwd1, false>>(a, batch * G1::P, 1, s, "ppox_nature_conv_fwd");
+        using P1 = Fwd1Problem<FWD1_MT>;
+        return launch_igemm<P1>(a, ppox::ceil_div(batch * G1::P, P1::BMR), s, "ppox_nature_conv_fwd");
     }
     PPOX_REQUIRE(ppox::aligned16(x) && !idx, "ppox_nature_conv_fwd: layer 2/3 input must be 16B-aligned NHWC");
-    if (layer == 2)
-        return launch_igemm<FwdProblem<G2, StageFwdNHWC<G2>, false>>(a, batch * G2::P, 1, s, "ppox_nature_conv_fwd");
-    return launch_igemm<FwdProblem<G3, StageFwdNHWC<G3>, true>>(a, batch * G3::P, 1, s, "ppox_nature_conv_fwd");
+    if (layer == 2) {
+        using P2 = FwdNHWCProblem<G2, false, 1>;
+        return launch_igemm<P2>(a, ppox::ceil_div(batch * G2::P, P2::BMR), s, "ppox_nature_conv_fwd");
+    }
+    using P3 = FwdNHWCProblem<G3, true, 1>;
+    return launch_igemm<P3>(a, ppox::ceil_div(batch * G3::P, P3::BMR), s, "ppox_nature_conv_fwd");
 }
 
 extern "C" int ppox_nature_conv_dgrad(int32_t layer, const float* grad_out, int64_t batch, const float* wpd,
@@ -679,9 +743,12 @@ extern "C" int ppox_nature_conv_dgrad(int32_t layer, const float* grad_out, int6
     if (batch == 0) return PPOX_OK;
     Args a{grad_out, nullptr, 0, 0, 0, wpd, nullptr, prev_act, grad_in, batch};
     hipStream_t s = ppox::as_stream(stream);
-    if (layer == 2)
-        return launch_igemm<DgradProblem<G2>>(a, batch * (G2::IH / 2) * (G2::IW / 2), 4, s, "ppox_nature_conv_dgrad");
-    return launch_igemm<DgradProblem<G3>>(a, batch * G3::IH * G3::IW, 1, s, "ppox_nature_conv_dgrad");
+    if (layer == 2) {
+        using D2 = DgradPMProblem<G2, DGRAD2_MT>;
+        return launch_igemm<D2>(a, ppox::ceil_div(batch, D2::BMR) * D2::NPOS, s, "ppox_nature_conv_dgrad");
+    }
+    using D3 = DgradPMProblem<G3, 1>;
+    return launch_igemm<D3>(a, ppox::ceil_div(batch, D3::BMR) * D3::NPOS, s, "ppox_nature_conv_dgrad");
 }
 
 extern "C" int64_t ppox_nature_wgrad_splits(int32_t layer, int64_t batch) {

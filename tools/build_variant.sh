@@ -1,0 +1,18 @@
+#!/bin/bash
+# Build a libppox variant with extra -D flags for kernel A/B timing (dev tool).
+# Usage: tools/build_variant.sh NAME "-DFWD1_MT=2 -DDGRAD2_MT=2"
+set -e
+name=$1; shift
+root=$(cd "$(dirname "$0")/.." && pwd)
+out=$root/tools/variants/$name
+mkdir -p "$out"
+objs=()
+for f in "$root"/ppo-exploration_amd/csrc/*.hip "$root"/ppo-exploration_amd/csrc/*.cpp; do
+  o=$out/$(basename "$f").o
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -munsafe-fp-atomics \
+    -I"$root/include" $* -c "$f" -o "$o" &
+  objs+=("$o")
+done
+wait
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$out/libppox.so" "${objs[@]}"
+echo "$out/libppox.so"

@@ -1,6 +1,6 @@
 """Per-kernel timing of the NatureCNN conv kernels (fwd / dgrad / wgrad) at the
 training minibatch size, HIP events on the launch stream, vs algorithmic FLOPs.
-Usage: python tools/conv_bench.py [B]"""
+Usage: python tools/conv_bench.py [B] [path/to/libppox variant .so]"""
 import json
 import os
 import sys
@@ -29,6 +29,9 @@ def t_ms(fn, iters=10):
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    if len(sys.argv) > 2:
+        native.load(sys.argv[2])
+        print(json.dumps({"lib": sys.argv[2]}))
     d = "cuda"
     w1, w2, w3 = torch.randn(32, 4, 8, 8, device=d) * 0.05, torch.randn(64, 32, 4, 4, device=d) * 0.05, \
         torch.randn(64, 64, 3, 3, device=d) * 0.05
