@@ -417,7 +417,9 @@ template <class L, bool U8>
 struct WgCfg {
     static constexpr int KT = (L::COUT == 32) ? 128 : 64;  // 4 tiles of 32x32 per WG
     static constexpr int KB = L::K / KT;
-    static constexpr int XST = KT + 1, GST = L::COUT + 1;
+    // row strides: +4 floats keeps the 16-B stores aligned and conflict-free (a half-wave's
+    // 32 lanes write 512 contiguous bytes) and puts the two MFMA k-halves 4 banks apart
+    static constexpr int XST = KT + 4, GST = L::COUT + 4;
     static constexpr int UPR = KT / 4;         // 4-element X units per pixel
     static constexpr int XV = MS * UPR / 256;  // X units per thread per step
     static constexpr int XPS = 256 / UPR;      // pixel stride between a thread's X units
@@ -443,8 +445,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
     using C = WgCfg<L, U8>;
     constexpr int KT = C::KT, KB = C::KB, XST = C::XST, GST = C::GST, COUT = L::COUT;
     constexpr int XV = C::XV, GV = C::GV, UPR = C::UPR, GUPR = C::GUPR;
-    __shared__ float Xs[2][MS * XST];
-    __shared__ float Gs[2][MS * GST];
+    __shared__ __attribute__((aligned(16))) float Xs[2][MS * XST];
+    __shared__ __attribute__((aligned(16))) float Gs[2][MS * GST];
     // XCD-aware block -> (split, kb): the KB k-blocks of a split share blockIdx % 8
     const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
     const int kb = q % KB, split = (q / KB) * 8 + xcd;
@@ -517,26 +519,17 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
     auto store = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < XV; ++i) {
-            float* d = Xs[buf] + (px0 + i * C::XPS) * XST + u * 4;
+            float4* d = reinterpret_cast<float4*>(Xs[buf] + (px0 + i * C::XPS) * XST + u * 4);
             if constexpr (U8) {
-                d[0] = (float)(xw[i] & 0xFFu);
-                d[1] = (float)((xw[i] >> 8) & 0xFFu);
-                d[2] = (float)((xw[i] >> 16) & 0xFFu);
-                d[3] = (float)(xw[i] >> 24);
+                *d = make_float4((float)(xw[i] & 0xFFu), (float)((xw[i] >> 8) & 0xFFu), (float)((xw[i] >> 16) & 0xFFu),
+                                 (float)(xw[i] >> 24));
             } else {
-                d[0] = xr[i].x;
-                d[1] = xr[i].y;
-                d[2] = xr[i].z;
-                d[3] = xr[i].w;
+                *d = xr[i];
             }
         }
 #pragma unroll
         for (int j = 0; j < GV; ++j) {
-            float* d = Gs[buf] + (gpx0 + j * C::GPS) * GST + c4 * 4;
-            d[0] = gr[j].x;
-            d[1] = gr[j].y;
-            d[2] = gr[j].z;
-            d[3] = gr[j].w;
+            *reinterpret_cast<float4*>(Gs[buf] + (gpx0 + j * C::GPS) * GST + c4 * 4) = gr[j];
             bsum0 += gr[j].x;
             bsum1 += gr[j].y;
             bsum2 += gr[j].z;

@@ -1,0 +1,18 @@
+#!/bin/bash
+# SQ/GRBM counters for the conv kernels of tools/conv_bench.py (run via gpurun).
+# Usage: tools/conv_pmc.sh TAG [lib.so]
+TAG=${1:-conv}
+LIB=${2:-}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+export TMPDIR=/tmp
+mkdir -p gpurun_out/$TAG
+timeout -k 10 120 rocprofv3 -L > gpurun_out/$TAG/counters_list.txt 2>&1 || exit $?
+i=0
+for SET in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS" \
+           "GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVES SQ_ACTIVE_INST_LDS"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $SET --kernel-include-regex "igemm|wgrad_kernel" -d /tmp/$TAG-p$i -o run \
+      --output-format csv -- python3 $R/tools/conv_bench.py 16384 $LIB > gpurun_out/$TAG/pmc_p$i.log 2>&1 || exit $?
+  cp /tmp/$TAG-p$i/*counter_collection* gpurun_out/$TAG/pmc_p$i.csv
+done
+echo done > gpurun_out/$TAG/DONE
