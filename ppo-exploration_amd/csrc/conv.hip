@@ -403,6 +403,252 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(Args a) {
 }
 
 // ---------------------------------------------------------------------------
+// Register-direct implicit GEMM (the default forward / dgrad path).
+// Each wave owns 32*MT rows x all NOUT columns and is independent: no LDS, no
+// barriers.  Within a 32-wide K chunk the MFMA k-slice of step kk is
+// {kk, 16 + kk}: lane half h = lane >> 5 supplies k = 16h + kk, so every lane
+// reads its row's 16 contiguous K values (4 x 16 B) straight into VGPRs.  B is
+// packed so that load q of column tile j is one contiguous 1 KB run across the
+// wave (lane L takes floats 4L..4L+3: k = 16h + 4q..4q+3 of column l32) —
+// fully coalesced (rg_index).  Chunk c+1 is loaded while chunk c runs on the
+// matrix cores.  Used for conv1 forward (u8 input); the f32 layers keep the
+// LDS-staged igemm: their 32-row x 32-B fragment loads cost more TA cycles than
+// the LDS round trip (measured: profiles/README.md).
+// Rows past the end load a clamped (valid) address; their C rows are never
+// stored, and a GEMM row only ever reaches its own C row.
+// ---------------------------------------------------------------------------
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+// packed-B position of natural element (k, col) of a [K][NOUT] matrix
+__host__ __device__ constexpr int rg_index(int k, int col, int nout) {
+    return (k >> 5) * 32 * nout + (col >> 5) * 1024 + ((k & 15) >> 2) * 256 + (((k >> 4) & 1) * 32 + (col & 31)) * 4 +
+           (k & 3);
+}
+
+template <class L, int MT_>
+struct RgFwdNHWC {
+    static constexpr int NOUT = L::COUT, MT = MT_, ROWS = 128 * MT, CPT = L::CIN / BK;
+    using Raw = f32x4[MT][4];
+    struct Tile {
+        unsigned m0, M;  // this wave's first row, total rows (< 2^31, host-checked)
+    };
+    __device__ static bool tile(const Args& a, Tile& t, int wave) {
+        const long long w = xcd_remap(blockIdx.x, gridDim.x);
+        t.M = (unsigned)(a.batch * L::P);
+        t.m0 = (unsigned)(w * ROWS) + wave * 32 * MT;
+        return t.m0 < t.M;
+    }
+    __device__ static int nchunk(const Tile&) { return L::K / BK; }
+    __device__ static const float* bchunk(const Args& a, const Tile&, int c) { return a.wp + c * BK * NOUT; }
+    struct Loader {
+        const float* base[MT];
+        __device__ Loader(const Args& a, const Tile& t, int lane) {
+            const float* x = reinterpret_cast<const float*>(a.x);
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                unsigned m = t.m0 + i * 32 + (lane & 31);
+                m = m < t.M ? m : t.m0;
+                const unsigned n = m / L::P, p = m - n * L::P, oy = p / L::OW, ox = p % L::OW;
+                base[i] = x + (long long)((n * L::IH + oy * L::S) * L::IW + ox * L::S) * L::CIN + (lane >> 5) * 16;
+            }
+        }
+        __device__ inline void load(int c, Raw& r) const {
+            const int tap = c / CPT;
+            const int off = ((tap / L::KW) * L::IW + tap % L::KW) * L::CIN + (c % CPT) * BK;
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) r[i][q] = *reinterpret_cast<const f32x4*>(base[i] + off + q * 4);
+        }
+        __device__ static inline float elem(const Raw& r, int i, int kk) { return r[i][kk >> 2][kk & 3]; }
+    };
+    __device__ static void store(const Args& a, const Tile& t, int row, int co, float acc, bool out_nchw) {
+        const unsigned m = t.m0 + row;
+        if (m >= t.M) return;
+        const float v = fmaxf(acc + a.bias[co], 0.f);
+        if (out_nchw) {
+            const unsigned n = m / L::P;
+            a.y[((long long)n * L::COUT + co) * L::P + (m - n * L::P)] = v;
+        } else {
+            a.y[(long long)m * L::COUT + co] = v;
+        }
+    }
+};
+
+// conv1: u8 NCHW frames; chunk c = channel c/2, kernel rows 4(c&1)..+3; lane
+// half h takes kernel rows 4(c&1)+2h, +1: two 8-byte runs = four words
+template <int MT_>
+struct RgFwd1 {
+    using L = G1;
+    static constexpr int NOUT = L::COUT, MT = MT_, ROWS = 128 * MT;
+    using Raw = uint32_t[MT][4];
+    using Tile = typename RgFwdNHWC<G2, 1>::Tile;
+    __device__ static bool tile(const Args& a, Tile& t, int wave) {
+        const long long w = xcd_remap(blockIdx.x, gridDim.x);
+        t.M = (unsigned)(a.batch * L::P);
+        t.m0 = (unsigned)(w * ROWS) + wave * 32 * MT;
+        return t.m0 < t.M;
+    }
+    __device__ static int nchunk(const Tile&) { return L::K / BK; }
+    __device__ static const float* bchunk(const Args& a, const Tile&, int c) { return a.wp + c * BK * NOUT; }
+    struct Loader {
+        const uint8_t* base[MT];
+        __device__ Loader(const Args& a, const Tile& t, int lane) {
+            const uint8_t* x = reinterpret_cast<const uint8_t*>(a.x);
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                unsigned m = t.m0 + i * 32 + (lane & 31);
+                m = m < t.M ? m : t.m0;
+                const unsigned n = m / L::P, p = m - n * L::P, oy = p / L::OW, ox = p % L::OW;
+                base[i] = x + u8_sample_base(a, n, (long long)L::CIN * L::IH * L::IW) +
+                          (oy * L::S + (lane >> 5) * 2) * L::IW + ox * L::S;
+            }
+        }
+        __device__ inline void load(int c, Raw& r) const {
+            const int off = (c >> 1) * (L::IH * L::IW) + (c & 1) * 4 * L::IW;
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const uint8_t* p = base[i] + off;
+                r[i][0] = *reinterpret_cast<const uint32_t*>(p);
+                r[i][1] = *reinterpret_cast<const uint32_t*>(p + 4);
+                r[i][2] = *reinterpret_cast<const uint32_t*>(p + L::IW);
+                r[i][3] = *reinterpret_cast<const uint32_t*>(p + L::IW + 4);
+            }
+        }
+        __device__ static inline float elem(const Raw& r, int i, int kk) {
+            return (float)((r[i][kk >> 2] >> (8 * (kk & 3))) & 0xFFu);
+        }
+    };
+    __device__ static void store(const Args& a, const Tile& t, int row, int co, float acc, bool) {
+        const unsigned m = t.m0 + row;
+        if (m >= t.M) return;
+        a.y[(long long)m * L::COUT + co] = fmaxf(acc + a.bias[co], 0.f);
+    }
+};
+
+// dgrad, position-major (see DgradPMProblem): a wave owns 32*MT samples of one input pixel
+template <class L, int MT_>
+struct RgDgrad {
+    static constexpr int NOUT = L::CIN, MT = MT_, ROWS = 128 * MT, NPOS = L::IH * L::IW, CPT = L::COUT / BK;
+    using Raw = f32x4[MT][4];
+    struct Tile {
+        long long n0;  // this wave's first sample
+        int pos, iy, ix, ky0, kx0, nx, nchunk;
+    };
+    __device__ static bool tile(const Args& a, Tile& t, int wave) {
+        const long long w = xcd_remap(blockIdx.x, gridDim.x);
+        t.n0 = (w / NPOS) * ROWS + wave * 32 * MT;
+        t.pos = (int)(w % NPOS);
+        t.iy = t.pos / L::IW;
+        t.ix = t.pos % L::IW;
+        int ny, nx;
+        tap_range<L::S, L::OH, L::KH>(t.iy, t.ky0, ny);
+        tap_range<L::S, L::OW, L::KW>(t.ix, t.kx0, nx);
+        t.nx = nx;
+        t.nchunk = ny * nx * CPT;
+        return t.n0 < a.batch;
+    }
+    __device__ static int nchunk(const Tile& t) { return t.nchunk; }
+    __device__ static const float* bchunk(const Args& a, const Tile& t, int c) {
+        const int tap = c / CPT, ty = tap / t.nx, tx = tap - ty * t.nx;
+        const int ky = t.ky0 + L::S * ty, kx = t.kx0 + L::S * tx;
+        return a.wp + ((ky * L::KW + kx) * CPT + c % CPT) * BK * NOUT;
+    }
+    struct Loader {
+        const float* base[MT];
+        int iy, ix, ky0, kx0, nx;
+        __device__ Loader(const Args& a, const Tile& t, int lane) : iy(t.iy), ix(t.ix), ky0(t.ky0), kx0(t.kx0), nx(t.nx) {
+            const float* g = reinterpret_cast<const float*>(a.x);
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                long long n = t.n0 + i * 32 + (lane & 31);
+                n = n < a.batch ? n : t.n0;
+                base[i] = g + n * (L::P * L::COUT) + (lane >> 5) * 16;
+            }
+        }
+        __device__ inline void load(int c, Raw& r) const {
+            const int tap = c / CPT, ty = tap / nx, tx = tap - ty * nx;
+            const int oy = (iy - ky0) / L::S - ty, ox = (ix - kx0) / L::S - tx;
+            const int off = (oy * L::OW + ox) * L::COUT + (c % CPT) * BK;
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) r[i][q] = *reinterpret_cast<const f32x4*>(base[i] + off + q * 4);
+        }
+        __device__ static inline float elem(const Raw& r, int i, int kk) { return r[i][kk >> 2][kk & 3]; }
+    };
+    __device__ static void store(const Args& a, const Tile& t, int row, int ci, float acc, bool) {
+        const long long n = t.n0 + row;
+        if (n >= a.batch) return;
+        const long long o = (n * NPOS + t.pos) * L::CIN + ci;
+        a.y[o] = a.mask[o] > 0.f ? acc : 0.f;
+    }
+};
+
+template <class Prob, bool OUT_NCHW = false>
+__global__ void __launch_bounds__(256, 2) rgemm_kernel(Args a) {
+    constexpr int NOUT = Prob::NOUT, NT = NOUT / 32, MT = Prob::MT;
+    using Ld = typename Prob::Loader;
+    using Raw = typename Prob::Raw;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    typename Prob::Tile t;
+    if (!Prob::tile(a, t, wave)) return;  // wave-uniform; nothing below synchronises
+    const int n = Prob::nchunk(t);
+    const Ld ld(a, t, lane);
+
+    f32x16 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = zero16();
+
+    Raw a0, a1;
+    f32x4 b0[NT][4], b1[NT][4];
+    auto loadB = [&](int c, f32x4 (&b)[NT][4]) {
+        const f32x4* p = reinterpret_cast<const f32x4*>(Prob::bchunk(a, t, c)) + lane;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[j][q] = p[j * 256 + q * 64];
+    };
+    auto compute = [&](const Raw& ar, const f32x4 (&b)[NT][4]) {
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(Ld::elem(ar, i, kk), b[j][kk >> 2][kk & 3],
+                                                                     acc[i][j], 0, 0, 0);
+    };
+    if (n > 0) {
+        ld.load(0, a0);
+        loadB(0, b0);
+    }
+    for (int c = 0; c < n; c += 2) {
+        if (c + 1 < n) {
+            ld.load(c + 1, a1);
+            loadB(c + 1, b1);
+        }
+        compute(a0, b0);
+        if (c + 2 < n) {
+            ld.load(c + 2, a0);
+            loadB(c + 2, b0);
+        }
+        if (c + 1 < n) compute(a1, b1);
+    }
+    // C/D map: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                Prob::store(a, t, i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), j * 32 + (lane & 31),
+                            acc[i][j][r], OUT_NCHW);
+}
+
+// ---------------------------------------------------------------------------
 // Wgrad.  WG = (k-block of KT rows of K) x (all COUT) x (slice of output pixels).
 // Per step of MS = 32 pixels: stage X[32][KT] (im2col) and G[32][COUT] in LDS,
 // then D(k x co) += X^T G on the MFMA (A operand = X^T: lane i <-> k, kk <-> pixel).
@@ -632,8 +878,20 @@ __global__ void __launch_bounds__(256) nchw_to_nhwc_mask(const float* __restrict
 // ---------------------------------------------------------------------------
 // weight packing (once per optimizer step)
 // ---------------------------------------------------------------------------
+#ifndef RG_F32  // 1: the f32 layers (fwd2/3, dgrad) on rgemm too (experiments)
+#define RG_F32 0
+#endif
+#ifndef RG_FWD1
+#define RG_FWD1 1
+#endif
+// RG: rgemm layout (rg_index); else the igemm's natural [K][NOUT]
+template <bool RG>
+__device__ inline int pack_pos(int k, int col, int nout, int i) {
+    if constexpr (RG) return rg_index(k, col, nout);
+    return i;
+}
 // forward: [K][COUT] in the kernel's K order
-template <class L, bool NHWC_ORDER>
+template <class L, bool NHWC_ORDER, bool RG>
 __global__ void pack_fwd(const float* __restrict__ w, float* __restrict__ wp) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= L::K * L::COUT) return;
@@ -649,16 +907,16 @@ __global__ void pack_fwd(const float* __restrict__ w, float* __restrict__ wp) {
         ky = (k / L::KW) % L::KH;
         ci = k / (L::KW * L::KH);
     }
-    wp[i] = w[((co * L::CIN + ci) * L::KH + ky) * L::KW + kx];
+    wp[pack_pos<RG>(k, co, L::COUT, i)] = w[((co * L::CIN + ci) * L::KH + ky) * L::KW + kx];
 }
 
 // dgrad: [(ky, kx, co)][ci] — chunk (tap, 32 co) is a contiguous 32 x CIN block
-template <class L>
+template <class L, bool RG>
 __global__ void pack_dgrad(const float* __restrict__ w, float* __restrict__ wp) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= L::KH * L::KW * L::COUT * L::CIN) return;
     const int ci = i % L::CIN, co = (i / L::CIN) % L::COUT, tap = i / (L::CIN * L::COUT);
-    wp[i] = w[((co * L::CIN + ci) * L::KH + tap / L::KW) * L::KW + tap % L::KW];
+    wp[pack_pos<RG>(tap * L::COUT + co, ci, L::CIN, i)] = w[((co * L::CIN + ci) * L::KH + tap / L::KW) * L::KW + tap % L::KW];
 }
 
 template <class Prob>
@@ -667,6 +925,25 @@ int launch_igemm(const Args& a, long long blocks, hipStream_t s, const char* nam
     igemm_kernel<Prob><<<(unsigned)blocks, 256, 0, s>>>(a);
     PPOX_LAUNCHED(name);
 }
+
+template <class Prob, bool OUT_NCHW = false>
+int launch_rgemm(const Args& a, long long blocks, hipStream_t s, const char* name) {
+    if (blocks == 0) return PPOX_OK;
+    rgemm_kernel<Prob, OUT_NCHW><<<(unsigned)blocks, 256, 0, s>>>(a);
+    PPOX_LAUNCHED(name);
+}
+#ifndef RG_FWD1_MT
+#define RG_FWD1_MT 2
+#endif
+#ifndef RG_FWD_MT
+#define RG_FWD_MT 1
+#endif
+#ifndef RG_DGRAD2_MT
+#define RG_DGRAD2_MT 2
+#endif
+#ifndef RG_DGRAD3_MT
+#define RG_DGRAD3_MT 1
+#endif
 
 template <class L, bool U8>
 int launch_wgrad(const WArgs& wa_in, hipStream_t s) {
@@ -695,11 +972,11 @@ extern "C" int ppox_nature_pack_weights(const float* w1, const float* w2, const 
                      (!wpd2 || ppox::aligned16(wpd2)) && (!wpd3 || ppox::aligned16(wpd3)),
                  "ppox_nature_pack_weights: packed buffers must be 16-byte aligned");
     hipStream_t s = ppox::as_stream(stream);
-    pack_fwd<G1, false><<<ppox::ceil_div(G1::K * 32, 256), 256, 0, s>>>(w1, wp1);
-    pack_fwd<G2, true><<<ppox::ceil_div(G2::K * 64, 256), 256, 0, s>>>(w2, wp2);
-    pack_fwd<G3, true><<<ppox::ceil_div(G3::K * 64, 256), 256, 0, s>>>(w3, wp3);
-    if (wpd2) pack_dgrad<G2><<<ppox::ceil_div(G2::K * G2::COUT, 256), 256, 0, s>>>(w2, wpd2);
-    if (wpd3) pack_dgrad<G3><<<ppox::ceil_div(G3::K * G3::COUT, 256), 256, 0, s>>>(w3, wpd3);
+    pack_fwd<G1, false, RG_FWD1><<<ppox::ceil_div(G1::K * 32, 256), 256, 0, s>>>(w1, wp1);
+    pack_fwd<G2, true, RG_F32><<<ppox::ceil_div(G2::K * 64, 256), 256, 0, s>>>(w2, wp2);
+    pack_fwd<G3, true, RG_F32><<<ppox::ceil_div(G3::K * 64, 256), 256, 0, s>>>(w3, wp3);
+    if (wpd2) pack_dgrad<G2, RG_F32><<<ppox::ceil_div(G2::K * G2::COUT, 256), 256, 0, s>>>(w2, wpd2);
+    if (wpd3) pack_dgrad<G3, RG_F32><<<ppox::ceil_div(G3::K * G3::COUT, 256), 256, 0, s>>>(w3, wpd3);
     PPOX_LAUNCHED("ppox_nature_pack_weights");
 }
 
@@ -710,22 +987,37 @@ extern "C" int ppox_nature_conv_fwd(int32_t layer, const void* x, int64_t batch,
     PPOX_REQUIRE(x && wp && bias && y && batch >= 0, "ppox_nature_conv_fwd: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(wp), "ppox_nature_conv_fwd: packed weights must be 16-byte aligned");
     if (batch == 0) return PPOX_OK;
+    PPOX_REQUIRE(batch * G1::P < (1LL << 31), "ppox_nature_conv_fwd: batch too large for 32-bit row indexing");
     Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, wp, bias, nullptr, y, batch};
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 1) {
         PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && (idx || x_sample_stride % 4 == 0),
                      "ppox_nature_conv_fwd: u8 input must be 4-byte aligned");
         if (idx) PPOX_REQUIRE(T > 0 && N_env > 0, "ppox_nature_conv_fwd: idx needs T and N_env");
+#if !RG_FWD1
         using P1 = Fwd1Problem<FWD1_MT>;
         return launch_igemm<P1>(a, ppox::ceil_div(batch * G1::P, P1::BMR), s, "ppox_nature_conv_fwd");
+#else
+        using R1 = RgFwd1<RG_FWD1_MT>;
+        return launch_rgemm<R1>(a, ppox::ceil_div(batch * G1::P, R1::ROWS), s, "ppox_nature_conv_fwd");
+#endif
     }
     PPOX_REQUIRE(ppox::aligned16(x) && !idx, "ppox_nature_conv_fwd: layer 2/3 input must be 16B-aligned NHWC");
+#if !RG_F32
     if (layer == 2) {
         using P2 = FwdNHWCProblem<G2, false, 1>;
         return launch_igemm<P2>(a, ppox::ceil_div(batch * G2::P, P2::BMR), s, "ppox_nature_conv_fwd");
     }
     using P3 = FwdNHWCProblem<G3, true, 1>;
     return launch_igemm<P3>(a, ppox::ceil_div(batch * G3::P, P3::BMR), s, "ppox_nature_conv_fwd");
+#else
+    if (layer == 2) {
+        using R2 = RgFwdNHWC<G2, RG_FWD_MT>;
+        return launch_rgemm<R2>(a, ppox::ceil_div(batch * G2::P, R2::ROWS), s, "ppox_nature_conv_fwd");
+    }
+    using R3 = RgFwdNHWC<G3, RG_FWD_MT>;
+    return launch_rgemm<R3, true>(a, ppox::ceil_div(batch * G3::P, R3::ROWS), s, "ppox_nature_conv_fwd");
+#endif
 }
 
 extern "C" int ppox_nature_conv_dgrad(int32_t layer, const float* grad_out, int64_t batch, const float* wpd,
@@ -736,12 +1028,21 @@ extern "C" int ppox_nature_conv_dgrad(int32_t layer, const float* grad_out, int6
     if (batch == 0) return PPOX_OK;
     Args a{grad_out, nullptr, 0, 0, 0, wpd, nullptr, prev_act, grad_in, batch};
     hipStream_t s = ppox::as_stream(stream);
+#if !RG_F32
     if (layer == 2) {
         using D2 = DgradPMProblem<G2, DGRAD2_MT>;
         return launch_igemm<D2>(a, ppox::ceil_div(batch, D2::BMR) * D2::NPOS, s, "ppox_nature_conv_dgrad");
     }
     using D3 = DgradPMProblem<G3, 1>;
     return launch_igemm<D3>(a, ppox::ceil_div(batch, D3::BMR) * D3::NPOS, s, "ppox_nature_conv_dgrad");
+#else
+    if (layer == 2) {
+        using D2 = RgDgrad<G2, RG_DGRAD2_MT>;
+        return launch_rgemm<D2>(a, ppox::ceil_div(batch, D2::ROWS) * D2::NPOS, s, "ppox_nature_conv_dgrad");
+    }
+    using D3 = RgDgrad<G3, RG_DGRAD3_MT>;
+    return launch_rgemm<D3>(a, ppox::ceil_div(batch, D3::ROWS) * D3::NPOS, s, "ppox_nature_conv_dgrad");
+#endif
 }
 
 extern "C" int64_t ppox_nature_wgrad_splits(int32_t layer, int64_t batch) {
