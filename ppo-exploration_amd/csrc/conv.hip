@@ -29,6 +29,8 @@
 // bias gradient is fused into the k-block-0 workgroups.  The k-blocks of one
 // M-slice are mapped to one XCD (blockIdx % 8) so their shared G rows and
 // overlapping input patches are served from that XCD's L2.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -216,10 +218,11 @@ struct FwdBase {
     }
     __device__ static int nchunk(const Tile&) { return L::K / BK; }
     __device__ static const float* bchunk(const Args& a, const Tile&, int c) { return a.wp + (long long)c * BK * NOUT; }
-    __device__ static void store(const Args& a, const Tile& t, int row, int co, float acc) {
+    __device__ static float prefetch(const Args& a, const Tile&, int, int co) { return a.bias[co]; }
+    __device__ static void store_pre(const Args& a, const Tile& t, int row, int co, float acc, float bias) {
         const long long m = t.m0 + row;
         if (m >= t.M) return;
-        const float v = fmaxf(acc + a.bias[co], 0.f);
+        const float v = fmaxf(acc + bias, 0.f);
         if constexpr (OUT_NCHW) {
             const long long n = m / L::P;
             a.y[(n * L::COUT + co) * L::P + (m - n * L::P)] = v;
@@ -323,11 +326,17 @@ struct DgradPMProblem {
         const int ky = t.ky0 + L::S * ty, kx = t.kx0 + L::S * tx;
         return a.wp + ((long long)(ky * L::KW + kx) * L::COUT + (c % CPT) * BK) * L::CIN;
     }
-    __device__ static void store(const Args& a, const Tile& t, int row, int ci, float acc) {
+    // the epilogue's ReLU-mask values are loaded before the K walk (their latency
+    // hides under it) — 16 per lane per column tile, in the C/D layout
+    __device__ static float prefetch(const Args& a, const Tile& t, int row, int ci) {
+        long long n = t.n0 + row;
+        n = n < a.batch ? n : t.n0;
+        return a.mask[(n * NPOS + t.pos) * L::CIN + ci];
+    }
+    __device__ static void store_pre(const Args& a, const Tile& t, int row, int ci, float acc, float m) {
         const long long n = t.n0 + row;
         if (n >= a.batch) return;
-        const long long o = (n * NPOS + t.pos) * L::CIN + ci;
-        a.y[o] = a.mask[o] > 0.f ? acc : 0.f;
+        a.y[(n * NPOS + t.pos) * L::CIN + ci] = m > 0.f ? acc : 0.f;
     }
 };
 
@@ -349,6 +358,16 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(Args a) {
     for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[i][j] = zero16();
+    // epilogue operands (bias / ReLU mask) in the C/D layout, loaded up front
+    f32x16 pre[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                pre[i][j][r] = Prob::prefetch(a, t, wave * 32 * MT + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5),
+                                              j * 32 + (lane & 31));
 
     typename Prob::Stager sa(a, t);
     StageB<NOUT> sb;
@@ -397,8 +416,8 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(Args a) {
             const int col = j * 32 + (lane & 31);
 #pragma unroll
             for (int r = 0; r < 16; ++r)
-                Prob::store(a, t, wave * 32 * MT + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), col,
-                            acc[i][j][r]);
+                Prob::store_pre(a, t, wave * 32 * MT + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), col,
+                                acc[i][j][r], pre[i][j][r]);
         }
 }
 
@@ -714,14 +733,21 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
         const int tap = k / L::CIN;
         koff = ((tap / L::KW) * L::IW + (tap % L::KW)) * L::CIN + (k % L::CIN);  // (ky, kx, ci) NHWC
     }
-    unsigned xn[XV], xp[XV];
+    // per X slot: its sample's base (bytes for u8, elements for f32) and its pixel in
+    // that sample; both advance by MS pixels per step (at most one wrap: MS <= P)
+    constexpr unsigned long long SAMPLE_F32 = (unsigned long long)L::IH * L::IW * L::CIN;
+    const unsigned long long sstride = U8 ? (unsigned long long)a.sample_stride : SAMPLE_F32;
+    unsigned long long sb[XV];
+    unsigned xp[XV];
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
         const unsigned m = mbeg + px0 + i * C::XPS;
-        xn[i] = m / L::P;
-        xp[i] = m - xn[i] * L::P;
+        const unsigned n = m / L::P;
+        xp[i] = m - n * L::P;
+        sb[i] = n * sstride;
     }
     const unsigned xn0 = mbeg / L::P, xp0 = mbeg - xn0 * L::P;  // a pixel that always exists
+    const unsigned long long sb0 = xn0 * sstride;
     const int c4 = threadIdx.x % GUPR, gpx0 = threadIdx.x / GUPR;
     const uint8_t* xu8 = reinterpret_cast<const uint8_t*>(a.x);
     const float* xf = reinterpret_cast<const float*>(a.x);
@@ -731,36 +757,51 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
     float4 gr[GV];
     float bsum0 = 0.f, bsum1 = 0.f, bsum2 = 0.f, bsum3 = 0.f;
 
-    auto load = [&](unsigned ms) {
+    // FULL: every pixel of the step is inside the slice (all steps but possibly the
+    // last of the last slice — splits are whole steps long); otherwise pixels past
+    // the end read the slice's first pixel and are zeroed by a select
+    auto load = [&](unsigned ms, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
 #pragma unroll
         for (int i = 0; i < XV; ++i) {
-            const unsigned m = ms + px0 + i * C::XPS;
-            const bool ok = m < mend;  // past the slice end: clamp to its first pixel, zero by select
-            const unsigned n = ok ? xn[i] : xn0, pp = ok ? xp[i] : xp0;
+            bool ok = true;
+            unsigned long long sbi = sb[i];
+            unsigned pp = xp[i];
+            if constexpr (!FULL) {
+                ok = ms + px0 + i * C::XPS < mend;
+                sbi = ok ? sbi : sb0;
+                pp = ok ? pp : xp0;
+            }
             const unsigned oy = pp / L::OW, ox = pp - oy * L::OW;
             if constexpr (U8) {
-                const unsigned long long off = (unsigned long long)n * (unsigned long long)a.sample_stride +
-                                               (oy * L::S * L::IW + ox * L::S + koff);
-                const uint32_t v = *reinterpret_cast<const uint32_t*>(xu8 + off);
+                const uint32_t v =
+                    *reinterpret_cast<const uint32_t*>(xu8 + sbi + (oy * L::S * L::IW + ox * L::S + koff));
                 xw[i] = ok ? v : 0u;
             } else {
-                const unsigned off = ((n * L::IH + oy * L::S) * L::IW + ox * L::S) * L::CIN + koff;
-                const float4 v = *reinterpret_cast<const float4*>(xf + off);
+                const float4 v = *reinterpret_cast<const float4*>(
+                    xf + sbi + ((oy * L::S) * L::IW + ox * L::S) * L::CIN + koff);
                 xr[i] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
             }
             xp[i] += MS;  // advance to the next step's pixel
             if (xp[i] >= (unsigned)L::P) {
                 xp[i] -= L::P;
-                xn[i] += 1;
+                sb[i] += sstride;
             }
         }
 #pragma unroll
         for (int j = 0; j < GV; ++j) {
             const unsigned m = ms + gpx0 + j * C::GPS;
-            const bool ok = m < mend;
+            bool ok = true;
+            if constexpr (!FULL) ok = m < mend;
             const float4 v = *reinterpret_cast<const float4*>(a.g + (ok ? m : mbeg) * COUT + c4 * 4);
             gr[j] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+    };
+    auto load_step = [&](unsigned ms) {
+        if (ms + MS <= mend)
+            load(ms, std::true_type{});
+        else
+            load(ms, std::false_type{});
     };
     auto store = [&](int buf) {
 #pragma unroll
@@ -785,7 +826,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
 
     const unsigned nsteps = mend > mbeg ? (mend - mbeg + MS - 1) / MS : 0;
     if (nsteps > 0) {
-        load(mbeg);
+        load_step(mbeg);
         store(0);
     }
     __syncthreads();
@@ -793,7 +834,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
     const float* Gbase = &Gs[0][0] + (lane >> 5) * GST + ct * 32 + (lane & 31);
     for (unsigned s = 0; s < nsteps; ++s) {
         const int cur = (int)(s & 1);
-        if (s + 1 < nsteps) load(mbeg + (s + 1) * MS);
+        if (s + 1 < nsteps) load_step(mbeg + (s + 1) * MS);
         const float* X = Xbase + cur * (MS * XST);
         const float* G = Gbase + cur * (MS * GST);
 #pragma unroll
@@ -951,7 +992,7 @@ int launch_wgrad(const WArgs& wa_in, hipStream_t s) {
     using C = WgCfg<L, U8>;
     const long long M = wa.batch * L::P;
     const int splits = wa.splits;
-    wa.px_per_split = (M + splits - 1) / splits;
+    wa.px_per_split = ppox::ceil_div(ppox::ceil_div(M, splits), MS) * MS;  // whole steps
     wgrad_kernel<L, U8><<<(unsigned)(C::KB * splits), 256, 0, s>>>(wa);
     PPOX_LAUNCHED("ppox_nature_conv_wgrad");
 }
