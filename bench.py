@@ -24,18 +24,17 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (= f32 vector) dense peak
 
 
-def pmc_traffic(kernel="wgrad_kernel<4, 84, 84, 8, 8, 4, 32>"):
+def pmc_traffic(kernel="wgrad_kernel<4, 84, 84, 8, 8, 4, 32, true>"):
     """HBM bytes per launch of the dominant kernel from the latest committed rocprofv3 --pmc
-    summary (profiles/rNN_pmc_summary.json: separate FETCH_SIZE / WRITE_SIZE passes of this
-    bench command, gfx950-corrected 2*FETCH + WRITE, KB -> B)."""
+    summary (profiles/rNN_pmc_summary.json, made by tools/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes of this bench command, gfx950-corrected 2*FETCH + WRITE)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
     if not files:
-        return None
+        return None, None
     with open(files[-1]) as f:
         d = json.load(f).get(kernel)
-    return None if d is None else {"bytes_per_launch": d["hbm_bytes_per_launch_corrected"],
-                                   "source": os.path.relpath(files[-1], ROOT)}
+    return (None, None) if d is None else (d["hbm_bytes_per_launch_corrected"], os.path.relpath(files[-1], ROOT))
 
 
 def parse():
@@ -133,11 +132,15 @@ def main():
         flops = [2.0 * a[2] * 400 * 256 * 32 for _, a in kt]
         mean_ms = float(np.mean([t for t, _ in kt]))
         ach = float(np.mean(flops)) / (mean_ms * 1e-3) / 1e12
+        traffic, src = pmc_traffic()
+        # algorithmic HBM bytes: u8 input (28224 B/sample) + f32 output grad (400*32*4 B/sample)
+        alg_bytes = float(np.mean([a[2] for _, a in kt])) * (28224 + 400 * 32 * 4)
         out["roofline"] = {"kernel": "wgrad_kernel<conv1> (ppox_nature_conv_wgrad layer 1)", "bound": "mfma",
                            "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": pmc_traffic(),
-                           "launches": len(kt), "mean_us": round(mean_ms * 1e3, 1),
-                           "alg_flops_per_launch": float(np.mean(flops))}
+                           "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                           "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)", "traffic_source": src,
+                           "alg_bytes_per_launch": alg_bytes, "launches": len(kt),
+                           "mean_us": round(mean_ms * 1e3, 1), "alg_flops_per_launch": float(np.mean(flops))}
     if gt:
         n_local = args.envs // world
         alg_bytes = (17 if gae_kernel == "ppox_gae" else 33) * args.nstep * n_local
