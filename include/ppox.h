@@ -127,6 +127,37 @@ int ppox_ppo_loss_backward(const float* logits, const float* values, const float
                            const double* partials, int64_t B_global, float ent_coef,
                            float vf_coef, float int_vf_coef, float scale, float* dlogits,
                            float* dvalues, float* dint_values, double* loss_accum, void* stream);
+/* Box action spaces (models.py:40-46, 66-71: Normal(tanh(mu), exp(action_log_std)),
+ * per-dimension surrogate, ppo.py:216-238).  mu = actor pre-activations (B, D);
+ * actions / old_logp are the rollout's (T, N, D) step-major arrays.  log_prob,
+ * ratio and surrogate run in f64 (the reference's f64 actions promote them,
+ * buffer.py:156); clip is the Python float clip_range.  The backward also
+ * returns dL/d(action_log_std) (D,) = the fixed-order sum of
+ * dlog_std_partials [PPOX_LOSS_PARTIALS][D] f64 (caller workspace). */
+int ppox_ppo_box_loss_partials(const float* mu, const float* log_std, const float* values,
+                               const float* int_values, int64_t B, int32_t D, const int64_t* idx,
+                               int64_t T, int64_t N, const float* actions, const float* old_logp,
+                               const float* old_values, const float* advantages,
+                               const float* returns, const float* old_int_values,
+                               const float* int_advantages, const float* int_returns,
+                               const double* adv_stats, double clip, double* partials,
+                               void* stream);
+int ppox_ppo_box_loss_backward(const float* mu, const float* log_std, const float* values,
+                               const float* int_values, int64_t B, int32_t D, const int64_t* idx,
+                               int64_t T, int64_t N, const float* actions, const float* old_logp,
+                               const float* old_values, const float* advantages,
+                               const float* returns, const float* old_int_values,
+                               const float* int_advantages, const float* int_returns,
+                               const double* adv_stats, double clip, const double* partials,
+                               int64_t B_global, float ent_coef, float vf_coef, float int_vf_coef,
+                               float scale, float* dmu, double* dlog_std_partials, float* dlog_std,
+                               float* dvalues, float* dint_values, double* loss_accum,
+                               void* stream);
+/* a ~ Normal(tanh(mu), exp(log_std)) per dimension (Philox + Box-Muller), f32
+ * log_prob(a) (models.py:42-45). */
+int ppox_normal_sample(const float* mu, const float* log_std, int64_t N, int32_t D,
+                       int64_t env_offset, uint64_t seed, int64_t counter, float* actions,
+                       float* log_probs, void* stream);
 /* a ~ Categorical(probs=softmax(logits)) (Philox, counter-based), log_prob(a). */
 int ppox_categorical_sample(const float* logits, int64_t N, int32_t A, int64_t env_offset,
                             uint64_t seed, int64_t counter, int32_t* actions, float* log_probs,

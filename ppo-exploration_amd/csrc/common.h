@@ -37,6 +37,16 @@ inline unsigned ceil_div(long long a, long long b) { return static_cast<unsigned
         return PPOX_OK;                                                             \
     } while (0)
 
+// launch check that falls through on success (for entry points launching several kernels)
+#define PPOX_LAUNCHED_NORET(name)                                                   \
+    do {                                                                            \
+        hipError_t e_ = hipGetLastError();                                          \
+        if (e_ != hipSuccess) {                                                     \
+            ::ppox::set_error("%s: launch failed: %s", name, hipGetErrorString(e_)); \
+            return -static_cast<int>(e_);                                           \
+        }                                                                           \
+    } while (0)
+
 #define PPOX_HIP(call, name)                                                         \
     do {                                                                             \
         hipError_t e_ = (call);                                                      \

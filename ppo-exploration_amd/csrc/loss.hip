@@ -368,6 +368,225 @@ Minibatch make_mb(const float* logits, const float* values, const float* int_val
     return m;
 }
 
+// ---------------------------------------------------------------------------
+// Box (continuous) head: Normal(tanh(mu), exp(action_log_std)) — models.py:40-46
+// / :66-71 / :159-164.  The buffer's actions are f64 (buffer.py:156), so
+// Normal.log_prob promotes to f64 and so do the ratio and the surrogate
+// (ppo.py:222-226): those run in f64 here, and every gradient is cast back to
+// f32 where it reaches an f32 tensor (loc, 2*var, log_scale), as autograd does.
+// The surrogate and entropy are per action dimension (ratio (B,D) x adv (B,1)).
+// ---------------------------------------------------------------------------
+constexpr double LOG_SQRT_2PI = 0.91893853320467274178;  // math.log(math.sqrt(2 * math.pi))
+constexpr int MAXD = 64;
+
+struct BoxMinibatch {
+    Minibatch m;              // logits = actor pre-activations (B, D); actions unused
+    const float* log_std;     // (D,)
+    const float* box_actions; // (T, N, D) step-major
+    int D;
+    double clip64;            // the Python float clip_range (f64 ratio clamp)
+};
+
+__device__ inline float box_entropy(float log_scale) {
+    return (float)(0.5 + LOG_SQRT_2PI) + log_scale;  // 0.5 + 0.5*log(2*pi) + log(scale), f32
+}
+
+template <bool DUAL>
+__global__ void __launch_bounds__(256) box_partials_kernel(BoxMinibatch bm, double* __restrict__ partials) {
+    __shared__ double red[NS][256 / 64];
+    const Minibatch& mb = bm.m;
+    const Scalars st = load_stats(mb.adv_stats, DUAL);
+    const int D = bm.D;
+    double acc[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) acc[k] = 0.0;
+    const double lo = 1.0 - bm.clip64, hi = 1.0 + bm.clip64;
+    for (long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x; b < mb.B; b += (long long)gridDim.x * blockDim.x) {
+        const long long e = elem(mb.idx[b], mb.T, mb.N);
+        float advn = norm_adv(mb.adv[e], st.mean, st.std);
+        if (DUAL) advn = advn + norm_adv(mb.int_adv[e], st.imean, st.istd);
+        for (int d = 0; d < D; ++d) {
+            const float loc = tanhf(mb.logits[b * D + d]);
+            const float sc = expf(bm.log_std[d]);
+            const float var = sc * sc, log_scale = logf(sc);
+            const double diff = (double)bm.box_actions[e * D + d] - (double)loc;
+            const double lp = -(diff * diff) / (double)(2.f * var) - (double)log_scale - LOG_SQRT_2PI;
+            const double ratio = exp(lp - (double)mb.old_logp[e * D + d]);
+            const double s1 = (double)advn * ratio;
+            const double s2 = (double)advn * fmin(fmax(ratio, lo), hi);
+            acc[0] += fmin(s1, s2);
+            acc[3] += (double)box_entropy(log_scale);
+        }
+        const float v = mb.values[b], ov = mb.old_values[e], rt = mb.ret[e];
+        const float vc = ov + clampf(v - ov, -mb.clip, mb.clip);
+        acc[1] += (double)((rt - v) * (rt - v));
+        acc[2] += (double)((rt - vc) * (rt - vc));
+        if (DUAL) {
+            const float iv = mb.int_values[b], oiv = mb.old_int_values[e], irt = mb.int_ret[e];
+            const float ivc = oiv + clampf(iv - oiv, -mb.clip, mb.clip);
+            acc[4] += (double)((irt - iv) * (irt - iv));
+            acc[5] += (double)((irt - ivc) * (irt - ivc));
+        }
+        acc[6] += 1.0;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        double x = acc[k];
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+        if (lane == 0) red[k][wv] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < NS) {
+        double x = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) x += red[threadIdx.x][w];
+        partials[blockIdx.x * NS + threadIdx.x] = x;
+    }
+}
+
+// dmu (B, D) = dL/d(actor pre-activation); dls_part [P][D] f64 = this block's
+// share of dL/d(action_log_std) (reduced in block order by box_logstd_reduce)
+template <bool DUAL>
+__global__ void __launch_bounds__(256) box_backward_kernel(BoxMinibatch bm, const double* __restrict__ partials,
+                                                           double Bglob, float ent_coef, float vf_coef,
+                                                           float int_vf_coef, float scale, float* __restrict__ dmu,
+                                                           double* __restrict__ dls_part, float* __restrict__ dvalues,
+                                                           float* __restrict__ dint_values,
+                                                           double* __restrict__ loss_accum) {
+    __shared__ double tot[NS];
+    __shared__ double dls[4][MAXD];
+    const Minibatch& mb = bm.m;
+    const int D = bm.D;
+    if (threadIdx.x < NS) {
+        double x = 0.0;
+        for (int p = 0; p < P; ++p) x += partials[p * NS + threadIdx.x];
+        tot[threadIdx.x] = x;
+    }
+    __syncthreads();
+    const double BD = Bglob * D;
+    const float vl1 = (float)(tot[1] / Bglob), vl2 = (float)(tot[2] / Bglob);
+    const float wA = vl1 == vl2 ? 0.5f : (vl1 > vl2 ? 1.f : 0.f);
+    const float wB = vl1 == vl2 ? 0.5f : (vl2 > vl1 ? 1.f : 0.f);
+    float iwA = 0.f, iwB = 0.f;
+    const float ivl1 = (float)(tot[4] / Bglob), ivl2 = (float)(tot[5] / Bglob);
+    if (DUAL) {
+        iwA = ivl1 == ivl2 ? 0.5f : (ivl1 > ivl2 ? 1.f : 0.f);
+        iwB = ivl1 == ivl2 ? 0.5f : (ivl2 > ivl1 ? 1.f : 0.f);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && loss_accum) {
+        const double pl = -(tot[0] / BD);  // f64 in the reference (f64 ratio)
+        const double vl = (double)fmaxf(vl1, vl2);
+        const double el = -(double)(float)(tot[3] / BD);
+        const double ivl = DUAL ? (double)fmaxf(ivl1, ivl2) : 0.0;
+        loss_accum[0] += pl;
+        loss_accum[1] += vl;
+        loss_accum[2] += el;
+        loss_accum[3] += pl + (double)ent_coef * el + (double)vf_coef * vl + (DUAL ? (double)int_vf_coef * ivl : 0.0);
+        loss_accum[4] += ivl;
+        loss_accum[5] += 1.0;
+    }
+    const Scalars st = load_stats(mb.adv_stats, DUAL);
+    const double lo = 1.0 - bm.clip64, hi = 1.0 + bm.clip64;
+    const double g_min = -(double)scale / BD;                   // d(-mean(min))
+    const float g_entropy = -(ent_coef * scale) / (float)BD;   // d(ent_coef * -mean(entropy)), f32
+    const float two_invB = (float)(2.0 / Bglob);
+    double my_dls[MAXD];
+    for (int d = 0; d < D; ++d) my_dls[d] = 0.0;
+    for (long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x; b < mb.B; b += (long long)gridDim.x * blockDim.x) {
+        const long long e = elem(mb.idx[b], mb.T, mb.N);
+        float advn = norm_adv(mb.adv[e], st.mean, st.std);
+        if (DUAL) advn = advn + norm_adv(mb.int_adv[e], st.imean, st.istd);
+        for (int d = 0; d < D; ++d) {
+            const float loc = tanhf(mb.logits[b * D + d]);
+            const float sc = expf(bm.log_std[d]);
+            const float var = sc * sc, log_scale = logf(sc);
+            const float var2 = 2.f * var;
+            const double diff = (double)bm.box_actions[e * D + d] - (double)loc;
+            const double num = -(diff * diff);
+            const double lp = num / (double)var2 - (double)log_scale - LOG_SQRT_2PI;
+            const double ratio = exp(lp - (double)mb.old_logp[e * D + d]);
+            const double s1 = (double)advn * ratio;
+            const double rc = fmin(fmax(ratio, lo), hi);
+            const double s2 = (double)advn * rc;
+            const double g1 = s1 < s2 ? g_min : (s1 == s2 ? g_min * 0.5 : 0.0);
+            const double g2 = s2 < s1 ? g_min : (s1 == s2 ? g_min * 0.5 : 0.0);
+            const double g_ratio = g1 * (double)advn + ((ratio >= lo && ratio <= hi) ? g2 * (double)advn : 0.0);
+            const double g_lp = g_ratio * ratio;
+            // lp = num / var2 - log_scale - c
+            const float g_var2 = (float)(-g_lp * num / ((double)var2 * (double)var2));
+            const float g_log_scale = (float)(-g_lp);
+            const double g_num = g_lp / (double)var2;
+            const float g_loc = (float)(-(-g_num * 2.0 * diff));  // num = -(diff^2), diff = a - loc
+            dmu[b * D + d] = g_loc * (1.f - loc * loc);          // tanh backward
+            // scale: var = scale^2, log_scale = log(scale) (twice: log_prob and entropy)
+            const float g_scale = (g_var2 * 2.f) * (2.f * sc) + g_log_scale / sc + g_entropy / sc;
+            my_dls[d] += (double)(g_scale * sc);  // scale = exp(log_std): grad * result
+        }
+        const float v = mb.values[b], ov = mb.old_values[e], rt = mb.ret[e];
+        const float dv = v - ov;
+        const float vc = ov + clampf(dv, -mb.clip, mb.clip);
+        const float gvl = vf_coef * scale;
+        float gv = wA * gvl * (-(two_invB * (rt - v)));
+        if (dv >= -mb.clip && dv <= mb.clip) gv += wB * gvl * (-(two_invB * (rt - vc)));
+        dvalues[b] = gv;
+        if (DUAL) {
+            const float iv = mb.int_values[b], oiv = mb.old_int_values[e], irt = mb.int_ret[e];
+            const float div = iv - oiv;
+            const float ivc = oiv + clampf(div, -mb.clip, mb.clip);
+            const float givl = int_vf_coef * scale;
+            float giv = iwA * givl * (-(two_invB * (irt - iv)));
+            if (div >= -mb.clip && div <= mb.clip) giv += iwB * givl * (-(two_invB * (irt - ivc)));
+            dint_values[b] = giv;
+        }
+    }
+    // block partial of d(action_log_std): wave shuffles, then waves in order
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int d = 0; d < D; ++d) {
+        double x = my_dls[d];
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
+        if (lane == 0) dls[wv][d] = x;
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < D; d += blockDim.x)
+        dls_part[blockIdx.x * D + d] = dls[0][d] + dls[1][d] + dls[2][d] + dls[3][d];
+}
+
+__global__ void box_logstd_reduce(const double* __restrict__ dls_part, int D, float* __restrict__ dlog_std) {
+    const int d = threadIdx.x;
+    if (d >= D) return;
+    double x = 0.0;
+    for (int p = 0; p < P; ++p) x += dls_part[p * D + d];
+    dlog_std[d] = (float)x;
+}
+
+// collect-time head: a ~ Normal(tanh(mu), exp(log_std)) by Box-Muller on Philox,
+// log_prob(a) in f32 (the sampled actions are f32 there, models.py:42-45)
+__global__ void __launch_bounds__(256) normal_sample_kernel(const float* __restrict__ mu, const float* __restrict__ log_std,
+                                                            long long N, int D, long long env_offset, uint64_t seed,
+                                                            long long counter, float* __restrict__ actions,
+                                                            float* __restrict__ logp) {
+    const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    for (int d = 0; d < D; d += 2) {
+        const ppox::u32x4 w = ppox::philox4x32_10(
+            ppox::u32x4{0x5A5A0000u | (uint32_t)d, (uint32_t)(env_offset + n), (uint32_t)counter,
+                        (uint32_t)(counter >> 32)},
+            (uint32_t)seed, (uint32_t)(seed >> 32));
+        const float u1 = fmaxf(ppox::u01(w.x), 1e-12f), u2 = ppox::u01(w.y);
+        const float r = sqrtf(-2.f * logf(u1));
+        const float z[2] = {r * cosf(6.283185307179586f * u2), r * sinf(6.283185307179586f * u2)};
+        for (int k = 0; k < 2 && d + k < D; ++k) {
+            const int j = d + k;
+            const float loc = tanhf(mu[n * D + j]);
+            const float sc = expf(log_std[j]);
+            const float a = loc + sc * z[k];
+            const float diff = a - loc;
+            actions[n * D + j] = a;
+            logp[n * D + j] = -(diff * diff) / (2.f * (sc * sc)) - logf(sc) - (float)LOG_SQRT_2PI;
+        }
+    }
+}
+
 #define PPOX_DISPATCH_A(A, MAXA_NAME, ...)      \
     if ((A) <= 4) {                             \
         constexpr int MAXA_NAME = 4;            \
@@ -461,6 +680,72 @@ extern "C" int ppox_ppo_loss_backward(const float* logits, const float* values, 
                                                               loss_accum);
     });
     PPOX_LAUNCHED("ppox_ppo_loss_backward");
+}
+
+extern "C" int ppox_ppo_box_loss_partials(const float* mu, const float* log_std, const float* values,
+                                          const float* int_values, int64_t B, int32_t D, const int64_t* idx, int64_t T,
+                                          int64_t N, const float* actions, const float* old_logp,
+                                          const float* old_values, const float* advantages, const float* returns,
+                                          const float* old_int_values, const float* int_advantages,
+                                          const float* int_returns, const double* adv_stats, double clip,
+                                          double* partials, void* stream) {
+    const bool dual = int_values != nullptr;
+    BoxMinibatch bm{make_mb(mu, values, int_values, B, 1, idx, T, N, nullptr, old_logp, old_values, advantages,
+                            returns, old_int_values, int_advantages, int_returns, adv_stats, (float)clip),
+                    log_std, actions, D, clip};
+    PPOX_REQUIRE(D >= 1 && D <= MAXD, "ppox_ppo_box_loss_partials: action dim %d outside [1,%d]", D, MAXD);
+    PPOX_REQUIRE(mu && log_std && values && idx && actions && old_logp && old_values && advantages && returns &&
+                     adv_stats && partials && (!dual || (old_int_values && int_advantages && int_returns)),
+                 "ppox_ppo_box_loss_partials: null pointer");
+    PPOX_REQUIRE(B >= 0 && T > 0 && N > 0, "ppox_ppo_box_loss_partials: bad sizes");
+    hipStream_t s = ppox::as_stream(stream);
+    if (dual)
+        box_partials_kernel<true><<<P, 256, 0, s>>>(bm, partials);
+    else
+        box_partials_kernel<false><<<P, 256, 0, s>>>(bm, partials);
+    PPOX_LAUNCHED("ppox_ppo_box_loss_partials");
+}
+
+extern "C" int ppox_ppo_box_loss_backward(const float* mu, const float* log_std, const float* values,
+                                          const float* int_values, int64_t B, int32_t D, const int64_t* idx, int64_t T,
+                                          int64_t N, const float* actions, const float* old_logp,
+                                          const float* old_values, const float* advantages, const float* returns,
+                                          const float* old_int_values, const float* int_advantages,
+                                          const float* int_returns, const double* adv_stats, double clip,
+                                          const double* partials, int64_t B_global, float ent_coef, float vf_coef,
+                                          float int_vf_coef, float scale, float* dmu, double* dlog_std_partials,
+                                          float* dlog_std, float* dvalues, float* dint_values, double* loss_accum,
+                                          void* stream) {
+    const bool dual = int_values != nullptr;
+    BoxMinibatch bm{make_mb(mu, values, int_values, B, 1, idx, T, N, nullptr, old_logp, old_values, advantages,
+                            returns, old_int_values, int_advantages, int_returns, adv_stats, (float)clip),
+                    log_std, actions, D, clip};
+    PPOX_REQUIRE(D >= 1 && D <= MAXD, "ppox_ppo_box_loss_backward: action dim %d outside [1,%d]", D, MAXD);
+    PPOX_REQUIRE(mu && log_std && values && idx && actions && old_logp && old_values && advantages && returns &&
+                     adv_stats && partials && dmu && dlog_std_partials && dlog_std && dvalues &&
+                     (!dual || (old_int_values && int_advantages && int_returns && dint_values)),
+                 "ppox_ppo_box_loss_backward: null pointer");
+    PPOX_REQUIRE(B >= 0 && T > 0 && N > 0 && B_global >= 1, "ppox_ppo_box_loss_backward: bad sizes");
+    hipStream_t s = ppox::as_stream(stream);
+    if (dual)
+        box_backward_kernel<true><<<P, 256, 0, s>>>(bm, partials, (double)B_global, ent_coef, vf_coef, int_vf_coef,
+                                                    scale, dmu, dlog_std_partials, dvalues, dint_values, loss_accum);
+    else
+        box_backward_kernel<false><<<P, 256, 0, s>>>(bm, partials, (double)B_global, ent_coef, vf_coef, int_vf_coef,
+                                                     scale, dmu, dlog_std_partials, dvalues, dint_values, loss_accum);
+    PPOX_LAUNCHED_NORET("ppox_ppo_box_loss_backward");
+    box_logstd_reduce<<<1, 64, 0, s>>>(dlog_std_partials, D, dlog_std);
+    PPOX_LAUNCHED("ppox_ppo_box_loss_backward");
+}
+
+extern "C" int ppox_normal_sample(const float* mu, const float* log_std, int64_t N, int32_t D, int64_t env_offset,
+                                  uint64_t seed, int64_t counter, float* actions, float* log_probs, void* stream) {
+    PPOX_REQUIRE(mu && log_std && actions && log_probs, "ppox_normal_sample: null pointer");
+    PPOX_REQUIRE(D >= 1 && D <= MAXD && N >= 0, "ppox_normal_sample: bad sizes");
+    if (N == 0) return PPOX_OK;
+    normal_sample_kernel<<<ppox::ceil_div(N, 256), 256, 0, ppox::as_stream(stream)>>>(mu, log_std, N, D, env_offset,
+                                                                                     seed, counter, actions, log_probs);
+    PPOX_LAUNCHED("ppox_normal_sample");
 }
 
 extern "C" int ppox_categorical_sample(const float* logits, int64_t N, int32_t A, int64_t env_offset, uint64_t seed,

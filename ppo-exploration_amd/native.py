@@ -34,6 +34,12 @@ SIGNATURES = {
                                _vp, _vp, _vp, _vp, _f32, _vp, _i64, _f32, _f32, _f32, _f32,
                                _vp, _vp, _vp, _vp, _vp],
     "ppox_categorical_sample": [_vp, _i64, _i32, _i64, _u64, _i64, _vp, _vp, _vp],
+    "ppox_ppo_box_loss_partials": [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _vp, _vp, _vp, _f64, _vp, _vp],
+    "ppox_ppo_box_loss_backward": [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _vp, _vp, _vp, _f64, _vp, _i64, _f32, _f32, _f32, _f32,
+                                   _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_normal_sample": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _vp, _vp, _vp],
     "ppox_gather_rows": [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
     "ppox_grad_sumsq": [_vp, _i64, _vp, _vp],
     "ppox_adam_step": [_vp, _vp, _vp, _vp, _i64, _vp, _f32, _f64, _f64, _f64, _f64, _i64, _vp, _vp],
@@ -243,6 +249,35 @@ def ppo_loss_backward(logits, values, int_values, B, A, idx, T, N, roll, adv_sta
          _p(g("int_returns") if int_values is not None else None), _p(adv_stats), float(clip), _p(partials),
          int(B_global), float(ent_coef), float(vf_coef), float(int_vf_coef), float(scale), _p(dlogits),
          _p(dvalues), _p(dint_values), _p(loss_accum), stream_ptr(stream))
+
+
+def _box_roll_args(int_values, roll):
+    g = roll.get
+    dual = int_values is not None
+    return (_p(g("actions")), _p(g("log_probs")), _p(g("values")), _p(g("advantages")), _p(g("returns")),
+            _p(g("int_values") if dual else None), _p(g("int_advantages") if dual else None),
+            _p(g("int_returns") if dual else None))
+
+
+def ppo_box_loss_partials(mu, log_std, values, int_values, B, D, idx, T, N, roll, adv_stats, clip, partials,
+                          stream=None):
+    """Box head: roll["actions"] / roll["log_probs"] are (T, N, D) f32."""
+    call("ppox_ppo_box_loss_partials", _p(mu), _p(log_std), _p(values), _p(int_values), B, D, _p(idx), T, N,
+         *_box_roll_args(int_values, roll), _p(adv_stats), float(clip), _p(partials), stream_ptr(stream))
+
+
+def ppo_box_loss_backward(mu, log_std, values, int_values, B, D, idx, T, N, roll, adv_stats, clip, partials,
+                          B_global, ent_coef, vf_coef, int_vf_coef, scale, dmu, dls_partials, dlog_std, dvalues,
+                          dint_values, loss_accum, stream=None):
+    call("ppox_ppo_box_loss_backward", _p(mu), _p(log_std), _p(values), _p(int_values), B, D, _p(idx), T, N,
+         *_box_roll_args(int_values, roll), _p(adv_stats), float(clip), _p(partials), int(B_global),
+         float(ent_coef), float(vf_coef), float(int_vf_coef), float(scale), _p(dmu), _p(dls_partials),
+         _p(dlog_std), _p(dvalues), _p(dint_values), _p(loss_accum), stream_ptr(stream))
+
+
+def normal_sample(mu, log_std, N, D, env_offset, seed, counter, actions, log_probs, stream=None):
+    call("ppox_normal_sample", _p(mu), _p(log_std), N, D, env_offset, seed & 0xFFFFFFFFFFFFFFFF, counter,
+         _p(actions), _p(log_probs), stream_ptr(stream))
 
 
 def categorical_sample(logits, N, A, env_offset, seed, counter, actions, log_probs, stream=None):

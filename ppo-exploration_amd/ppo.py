@@ -127,6 +127,36 @@ class BaseAlgorithm:
         d = self.device
         self.loss_partials = torch.zeros(native.LOSS_PARTIALS * 8, dtype=torch.float64, device=d)
         self.loss_accum = torch.zeros(8, dtype=torch.float64, device=d)
+        if not self.discrete:
+            self.dls_partials = torch.zeros(native.LOSS_PARTIALS * self.n_actions, dtype=torch.float64, device=d)
+            self.dls = torch.zeros(self.n_actions, device=d)
+
+    def _loss_grads(self, od, vd, ivd, idx, roll, stats, B_global, int_vf_coef, scale):
+        """K4 for one minibatch: partial sums -> all-reduce -> backward to the head outputs
+        (ppo.py:216-238).  Discrete: Categorical kernels; Box: Normal kernels, whose
+        dL/d(action_log_std) goes straight into the flat gradient (before its all-reduce).
+        Returns (d_out, d_value, d_int_value or None)."""
+        Bl, A, T, N = idx.numel(), self.n_actions, self.nstep, self.local_envs
+        if self.discrete:
+            native.ppo_loss_partials(od, vd, ivd, Bl, A, idx, T, N, roll, stats, self.clip_range, self.loss_partials)
+        else:
+            ls = self.policy.net.action_log_std.detach()
+            native.ppo_box_loss_partials(od, ls, vd, ivd, Bl, A, idx, T, N, roll, stats, self.clip_range,
+                                         self.loss_partials)
+        self.dist.all_reduce_(self.loss_partials)
+        dout, dv = torch.empty_like(od), torch.empty_like(vd)
+        div = torch.empty_like(ivd) if ivd is not None else None
+        if self.discrete:
+            native.ppo_loss_backward(od, vd, ivd, Bl, A, idx, T, N, roll, stats, self.clip_range, self.loss_partials,
+                                     B_global, self.ent_coef, self.vf_coef, int_vf_coef, scale, dout, dv, div,
+                                     self.loss_accum)
+        else:
+            native.ppo_box_loss_backward(od, ls, vd, ivd, Bl, A, idx, T, N, roll, stats, self.clip_range,
+                                         self.loss_partials, B_global, self.ent_coef, self.vf_coef, int_vf_coef,
+                                         scale, dout, self.dls_partials, self.dls, dv, div, self.loss_accum)
+            g = self.policy.net.action_log_std.grad
+            g.add_(self.dls.view_as(g))
+        return dout, dv, div
 
     def _ensure_started(self):
         if not self._started:
@@ -140,13 +170,10 @@ class BaseAlgorithm:
         if self.discrete:
             native.categorical_sample(out, self.local_envs, self.n_actions, self.env_offset, self.seed,
                                       self._sample_counter, ro.actions[t], ro.log_probs[t])
-        else:
-            mean = out.tanh()
-            std = torch.exp(self.policy.net.action_log_std).expand_as(mean)
-            d = torch.distributions.Normal(mean, std)
-            a = d.sample()
-            ro.actions[t].copy_(a)
-            ro.log_probs[t].copy_(d.log_prob(a))
+        else:  # Normal(tanh(mu), exp(action_log_std)) (models.py:42-45), Philox + Box-Muller
+            native.normal_sample(out.contiguous(), self.policy.net.action_log_std.detach(), self.local_envs,
+                                 self.n_actions, self.env_offset, self.seed, self._sample_counter, ro.actions[t],
+                                 ro.log_probs[t])
         self._sample_counter += 1
 
     def _finish_episodes(self):
@@ -290,15 +317,7 @@ class PPO(BaseAlgorithm):
         else:
             out_d = torch.zeros(0, self.n_actions, device=self.device)
             v_d = torch.zeros(0, device=self.device)
-        roll = ro.tensors()
-        native.ppo_loss_partials(out_d, v_d, None, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
-                                 adv_stats, self.clip_range, self.loss_partials)
-        self.dist.all_reduce_(self.loss_partials)
-        dout = torch.empty_like(out_d)
-        dv = torch.empty_like(v_d)
-        native.ppo_loss_backward(out_d, v_d, None, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
-                                 adv_stats, self.clip_range, self.loss_partials, B_global, self.ent_coef,
-                                 self.vf_coef, 0.0, scale, dout, dv, None, self.loss_accum)
+        dout, dv, _ = self._loss_grads(out_d, v_d, None, idx, ro.tensors(), adv_stats, B_global, 0.0, scale)
         if Bl > 0:
             tensors, grads = [out, v], [dout, dv]
             if extra_backward is not None:
@@ -308,8 +327,6 @@ class PPO(BaseAlgorithm):
         self.dist.all_reduce_(self.flat.grad)
 
     def train(self):
-        if not self.discrete:
-            raise NotImplementedError("Box action spaces: fused continuous loss lands in a later round")
         ro = self.rollout
         total = self.nstep * self.num_envs
         self.loss_accum.zero_()
@@ -416,8 +433,6 @@ class PPO_RND(BaseAlgorithm):
         self.rnd_flat.adam_step(self.int_lr, self.max_grad_norm)
 
     def train(self):
-        if not self.discrete:
-            raise NotImplementedError("Box action spaces: fused continuous loss lands in a later round")
         ro = self.rollout
         total = self.nstep * self.num_envs
         self.loss_accum.zero_()
@@ -436,13 +451,7 @@ class PPO_RND(BaseAlgorithm):
                 obs = ro._gather(ro.observations, idx)
                 out, v, iv = net(obs)
                 od, vd, ivd = out.detach().contiguous(), v.detach().contiguous(), iv.detach().contiguous()
-                native.ppo_loss_partials(od, vd, ivd, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
-                                         stats[k], self.clip_range, self.loss_partials)
-                self.dist.all_reduce_(self.loss_partials)
-                dout, dv, div = torch.empty_like(od), torch.empty_like(vd), torch.empty_like(ivd)
-                native.ppo_loss_backward(od, vd, ivd, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
-                                         stats[k], self.clip_range, self.loss_partials, B, self.ent_coef,
-                                         self.vf_coef, self.int_vf_coef, 1.0, dout, dv, div, self.loss_accum)
+                dout, dv, div = self._loss_grads(od, vd, ivd, idx, roll, stats[k], B, self.int_vf_coef, 1.0)
                 if Bl > 0:
                     torch.autograd.backward([out, v, iv], [dout, dv, div])
                 self.dist.all_reduce_(self.flat.grad)
@@ -514,8 +523,6 @@ class PPO_ICM(BaseAlgorithm):
         return True
 
     def train(self):
-        if not self.discrete:
-            raise NotImplementedError("Box action spaces: fused continuous loss lands in a later round")
         ro = self.rollout
         total = self.nstep * self.num_envs
         self.loss_accum.zero_()
@@ -536,20 +543,18 @@ class PPO_ICM(BaseAlgorithm):
                 obs = ro._gather(ro.observations, idx)
                 out, v, _ = net(obs)
                 od, vd = out.detach().contiguous(), v.detach().contiguous()
-                native.ppo_loss_partials(od, vd, None, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
-                                         stats[k], self.clip_range, self.loss_partials)
-                self.dist.all_reduce_(self.loss_partials)
-                dout, dv = torch.empty_like(od), torch.empty_like(vd)
-                native.ppo_loss_backward(od, vd, None, Bl, self.n_actions, idx, self.nstep, self.local_envs, roll,
-                                         stats[k], self.clip_range, self.loss_partials, B, self.ent_coef,
-                                         self.vf_coef, 0.0, float(self.policy_weight), dout, dv, None,
-                                         self.loss_accum)
+                dout, dv, _ = self._loss_grads(od, vd, None, idx, roll, stats[k], B, 0.0, float(self.policy_weight))
                 # ICM on consecutive rows of the (owned part of the) permuted minibatch (ppo.py:684-688)
-                acts = ro.actions.reshape(-1)[(idx % self.nstep) * self.local_envs + idx // self.nstep]
+                rows = (idx % self.nstep) * self.local_envs + idx // self.nstep
+                if self.discrete:
+                    acts = ro.actions.reshape(-1)[rows]
+                else:
+                    acts = ro.actions.reshape(-1, self.n_actions)[rows]
                 x = self._icm_x(obs)
                 a_hat, f_next, f_next_hat = icm(x[:-1], x[1:], acts[:-1])
                 fwd = F.mse_loss(f_next, f_next_hat)
-                inv = F.cross_entropy(a_hat, acts[:-1].long())
+                # inverse loss: CrossEntropy (Discrete) / MSE (Box) (util.py:61-69)
+                inv = F.cross_entropy(a_hat, acts[:-1].long()) if self.discrete else F.mse_loss(a_hat, acts[:-1])
                 icm_loss = (1 - self.beta) * inv + self.beta * fwd
                 self.icm_accum += icm_loss.detach().double()
                 torch.autograd.backward([out, v, icm_loss], [dout, dv, None])

@@ -2,6 +2,7 @@
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
 from oracle import algos as OA
 from oracle import philox as PH
@@ -90,6 +91,105 @@ def test_ppo_loss_fwd_bwd_vs_torch(A, B, dual, sat):
     if dual:
         np.testing.assert_allclose(acc[4], ref["ivl"], rtol=1e-5, atol=1e-7)
         np.testing.assert_allclose(div.cpu().numpy(), ref["div"], rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("D,B,dual", [(2, 512, False), (3, 777, True), (6, 2048, False), (1, 1, False)])
+def test_box_loss_fwd_bwd_vs_torch(D, B, dual):
+    """Normal head (models.py:66-71) + per-dimension surrogate (ppo.py:216-238) vs torch-CPU
+    autograd with the reference's dtypes: f64 actions (buffer.py:156) => f64 log_prob, ratio,
+    surrogate; f32 entropy / values.  Tolerance: 1e-5 rel on losses, 1e-4 rel on grads."""
+    import native
+    rs = np.random.RandomState(D * 1000 + B)
+    T, N = 32, 64
+    clip, ent_coef, vf_coef, ivf, scale = 0.2, 0.01, 0.5, 0.5, 0.7
+    roll = {"actions": (np.tanh(rs.randn(T, N, D)) + 0.5 * rs.randn(T, N, D)).astype(np.float32),
+            "log_probs": (-1.0 - 0.5 * rs.rand(T, N, D)).astype(np.float32),
+            "values": rs.randn(T, N).astype(np.float32), "advantages": rs.randn(T, N).astype(np.float32) * 2,
+            "returns": rs.randn(T, N).astype(np.float32), "int_values": rs.randn(T, N).astype(np.float32),
+            "int_advantages": rs.randn(T, N).astype(np.float32), "int_returns": rs.randn(T, N).astype(np.float32)}
+    perm = rs.permutation(T * N)[:B]
+    t_of, n_of = perm % T, perm // T
+    g = {k: v[t_of, n_of] for k, v in roll.items()}
+    mu = rs.randn(B, D).astype(np.float32)
+    log_std = (0.3 * rs.randn(D)).astype(np.float32)
+    values = (g["values"] + rs.randn(B).astype(np.float32) * 0.3).astype(np.float32)
+    ivals = (g["int_values"] + rs.randn(B).astype(np.float32) * 0.3).astype(np.float32)
+    # torch reference, op by op as the reference builds it
+    mu_t = torch.tensor(mu, requires_grad=True)
+    ls_t = torch.tensor(log_std.reshape(1, D), requires_grad=True)
+    v_t = torch.tensor(values, requires_grad=True)
+    iv_t = torch.tensor(ivals, requires_grad=True)
+    mean = mu_t.tanh()
+    dist = torch.distributions.Normal(mean, torch.exp(ls_t.expand_as(mean)))
+    lp = dist.log_prob(torch.tensor(g["actions"]).double())
+    assert lp.dtype == torch.float64
+
+    def norm(x):
+        x = torch.tensor(x).unsqueeze(1)
+        return (x - x.mean()) / (x.std() + 1e-8)
+    adv = norm(g["advantages"]) + (norm(g["int_advantages"]) if dual else 0)
+    ratio = torch.exp(lp - torch.tensor(g["log_probs"]))
+    pl = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+
+    def vloss(v, ov, ret):
+        ov, ret = torch.tensor(ov), torch.tensor(ret)
+        vc = ov + (v - ov).clamp(-clip, clip)
+        return torch.max(F.mse_loss(ret, v), F.mse_loss(ret, vc))
+    vl = vloss(v_t, g["values"], g["returns"])
+    el = -torch.mean(dist.entropy())
+    loss = pl + ent_coef * el + vf_coef * vl
+    if dual:
+        ivl = vloss(iv_t, g["int_values"], g["int_returns"])
+        loss = loss + ivf * ivl
+    (scale * loss).backward()
+    # device
+    droll = {k: dev(v) for k, v in roll.items()}
+    idx = dev(perm.astype(np.int64))
+    stats = torch.empty(1, 4, dtype=torch.float64, device="cuda")
+    native.minibatch_adv_stats(droll["advantages"], droll["int_advantages"] if dual else None, idx, B, B, T, N, stats)
+    partials = torch.zeros(native.LOSS_PARTIALS * 8, dtype=torch.float64, device="cuda")
+    accum = torch.zeros(8, dtype=torch.float64, device="cuda")
+    z, ls, v, iv = dev(mu), dev(log_std), dev(values), dev(ivals) if dual else None
+    native.ppo_box_loss_partials(z, ls, v, iv, B, D, idx, T, N, droll, stats[0], clip, partials)
+    dz, dv = torch.empty_like(z), torch.empty_like(v)
+    div = torch.empty_like(iv) if dual else None
+    dlsp = torch.empty(native.LOSS_PARTIALS * D, dtype=torch.float64, device="cuda")
+    dls = torch.empty(D, device="cuda")
+    native.ppo_box_loss_backward(z, ls, v, iv, B, D, idx, T, N, droll, stats[0], clip, partials, B, ent_coef,
+                                 vf_coef, ivf, scale, dz, dlsp, dls, dv, div, accum)
+    torch.cuda.synchronize()
+    acc = accum.cpu().numpy()
+    if B > 1:
+        np.testing.assert_allclose(acc[0], pl.item(), rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(acc[1], vl.item(), rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(acc[2], el.item(), rtol=1e-5, atol=1e-7)
+        sg = max(np.abs(mu_t.grad.numpy()).max(), 1e-30)
+        np.testing.assert_allclose(dz.cpu().numpy(), mu_t.grad.numpy(), rtol=1e-4, atol=1e-5 * sg)
+        np.testing.assert_allclose(dls.cpu().numpy(), ls_t.grad.numpy()[0], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(dv.cpu().numpy(), v_t.grad.numpy(), rtol=1e-5, atol=1e-8)
+        if dual:
+            np.testing.assert_allclose(div.cpu().numpy(), iv_t.grad.numpy(), rtol=1e-5, atol=1e-8)
+    else:  # one row: unbiased std is nan, as in torch — everything downstream of the surrogate is nan
+        assert np.isnan(acc[0]) and np.isnan(pl.item())
+        np.testing.assert_allclose(acc[1], vl.item(), rtol=1e-5, atol=1e-7)
+
+
+def test_normal_sample_moments_and_logprob():
+    """Collect-time Normal head: Philox Box-Muller samples have the head's mean / std, and
+    log_prob matches torch's Normal.log_prob of the sampled (f32) action."""
+    import native
+    N, D = 100000, 3
+    mu = torch.tensor([[0.3, -1.2, 2.0]], device="cuda").repeat(N, 1)
+    ls = torch.tensor([-0.5, 0.0, 0.4], device="cuda")
+    a = torch.empty(N, D, device="cuda")
+    lp = torch.empty(N, D, device="cuda")
+    native.normal_sample(mu, ls, N, D, 0, 99, 5, a, lp)
+    loc, sc = torch.tanh(mu[0]).cpu(), torch.exp(ls).cpu()
+    ac = a.cpu()
+    np.testing.assert_allclose(ac.mean(0).numpy(), loc.numpy(), atol=4 * sc.numpy().max() / np.sqrt(N) * 3)
+    np.testing.assert_allclose(ac.std(0).numpy(), sc.numpy(), rtol=2e-2)
+    ref = torch.distributions.Normal(loc, sc).log_prob(ac)
+    np.testing.assert_allclose(lp.cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
 
 
 def test_adv_stats_remainder_and_singleton():

@@ -11,6 +11,11 @@ from replay_env import ReplayVecEnv, space_from_code
 pytestmark = pytest.mark.gpu
 
 
+def _space(E, code):
+    """fixture space code -> the product's space type (n > 0: Discrete(n); -k: Box((k,)))."""
+    return E.Discrete(int(code)) if code > 0 else E.Box((int(-code),))
+
+
 def _load_weights(module, f, prefix):
     sd = module.state_dict()
     with torch.no_grad():
@@ -18,10 +23,11 @@ def _load_weights(module, f, prefix):
             v.copy_(torch.from_numpy(f[prefix + k]).to(v.device))
 
 
-@pytest.mark.parametrize("name", ["disc2", "disc4sat", "disc18"])
+@pytest.mark.parametrize("name", ["disc2", "disc4sat", "disc18", "box2"])
 def test_ppo_train_matches_reference_run(golden, name):
     """Same rollout + same weights + same numpy seed => product train() reproduces the
-    reference's post-update weights (ppo.py:200-259)."""
+    reference's post-update weights (ppo.py:200-259).  box2: the Normal head with the
+    reference's f64 log_prob / ratio / surrogate (models.py:66-71)."""
     import ppo
     import env as E
     f = golden("train_ppo")
@@ -40,7 +46,7 @@ def test_ppo_train_matches_reference_run(golden, name):
     ro_ref = orc.rollout
     # product on the GPU
     np.random.seed(seed)  # RolloutStorage draws randn(16, D) at construction (buffer.py:137)
-    denv = E.DeviceVecEnv("custom", N, obs_dim=D, action_space=E.Discrete(code))
+    denv = E.DeviceVecEnv("custom", N, obs_dim=D, action_space=_space(E, code))
     alg = ppo.PPO(env_id="custom", env=denv, n_envs=N, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H,
                   max_grad_norm=0.5, ent_coef=0.01, vf_coef=1.0, quiet=True)
     _load_weights(alg.policy.net, f, p + "w0_")
@@ -162,15 +168,17 @@ def test_rnd_train_matches_reference_run(golden):
     np.testing.assert_allclose(acc[4] / acc[5], f[p + "intrinsic_loss"], rtol=1e-4, atol=1e-6)
 
 
-def test_icm_train_matches_reference_run(golden):
-    """PPO_ICM.train() (ppo.py:651-713) on the reference's rollout (Discrete)."""
+@pytest.mark.parametrize("name,code", [("icm_disc", 3), ("icm_box", -2)])
+def test_icm_train_matches_reference_run(golden, name, code):
+    """PPO_ICM.train() (ppo.py:651-713) on the reference's rollout (Discrete: CrossEntropy
+    inverse loss; Box: MSE inverse loss, util.py:61-69)."""
     import ppo
     import env as E
     from oracle.algos import OracleICM
     f = golden("train_icm")
-    p = "icm_disc_"
+    p = name + "_"
     D, N, T, B, E_, H, IH, seed = (int(x) for x in f[p + "cfg"])
-    renv = ReplayVecEnv(f[p + "env_obs"], f[p + "env_rew"], f[p + "env_done"], space_from_code(3))
+    renv = ReplayVecEnv(f[p + "env_obs"], f[p + "env_rew"], f[p + "env_done"], space_from_code(code))
     np.random.seed(seed)
     torch.manual_seed(seed)
     orc = OracleICM(renv, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H, int_hidden_size=IH,
@@ -178,7 +186,7 @@ def test_icm_train_matches_reference_run(golden):
     orc.collect()
     r = orc.rollout
     np.random.seed(seed)
-    alg = ppo.PPO_ICM(env_id="custom", env=E.DeviceVecEnv("custom", N, obs_dim=D, action_space=E.Discrete(3)),
+    alg = ppo.PPO_ICM(env_id="custom", env=E.DeviceVecEnv("custom", N, obs_dim=D, action_space=_space(E, code)),
                       n_envs=N, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H, int_hidden_size=IH,
                       max_grad_norm=0.5, int_rew_integration=0.1, quiet=True)
     _load_weights(alg.policy.net, f, p + "w0_")
