@@ -867,15 +867,32 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
     }
 }
 
-// sum the slabs in split order, scatter to PyTorch [co][ci][ky][kx] (+ bias)
+// sum the slabs, scatter to PyTorch [co][ci][ky][kx] (+ bias).  A block owns 32
+// consecutive outputs (one 128-B row of every slab) x 8 split groups; thread
+// (e, g) sums splits g, g+8, g+16, ... in order, then the 8 group sums are added
+// in group order — a fixed order, so the result is deterministic.
+constexpr int RED_E = 32, RED_G = 8;
+
 template <class L, bool NHWC_ORDER>
 __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ slab, const float* __restrict__ bslab,
                                                     int splits, float* __restrict__ dw, float* __restrict__ db) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ float part[RED_G][RED_E];
     constexpr int KC = L::K * L::COUT;
+    const int e = threadIdx.x % RED_E, grp = threadIdx.x / RED_E;
+    const int i = blockIdx.x * RED_E + e;
+    float s = 0.f;
     if (i < KC) {
-        float s = 0.f;
-        for (int sp = 0; sp < splits; ++sp) s += slab[(long long)sp * KC + i];
+        for (int sp = grp; sp < splits; sp += RED_G) s += slab[(long long)sp * KC + i];
+    } else if (i < KC + L::COUT) {
+        for (int sp = grp; sp < splits; sp += RED_G) s += bslab[(long long)sp * L::COUT + (i - KC)];
+    }
+    part[grp][e] = s;
+    __syncthreads();
+    if (grp != 0) return;
+    float t = part[0][e];
+#pragma unroll
+    for (int g = 1; g < RED_G; ++g) t += part[g][e];
+    if (i < KC) {
         const int k = i / L::COUT, co = i % L::COUT;
         int ci, ky, kx;
         if (NHWC_ORDER) {
@@ -888,12 +905,9 @@ __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ sl
             ky = (k / L::KW) % L::KH;
             ci = k / (L::KW * L::KH);
         }
-        dw[((co * L::CIN + ci) * L::KH + ky) * L::KW + kx] = s;
+        dw[((co * L::CIN + ci) * L::KH + ky) * L::KW + kx] = t;
     } else if (i < KC + L::COUT) {
-        const int co = i - KC;
-        float s = 0.f;
-        for (int sp = 0; sp < splits; ++sp) s += bslab[(long long)sp * L::COUT + co];
-        db[co] = s;
+        db[i - KC] = t;
     }
 }
 
@@ -999,8 +1013,8 @@ int launch_wgrad(const WArgs& wa_in, hipStream_t s) {
 
 template <class L, bool NHWC_ORDER>
 int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float* dw, float* db, hipStream_t s) {
-    wgrad_reduce<L, NHWC_ORDER><<<ppox::ceil_div(L::K * L::COUT + L::COUT, 256), 256, 0, s>>>(slab, bslab, splits, dw,
-                                                                                             db);
+    wgrad_reduce<L, NHWC_ORDER><<<ppox::ceil_div(L::K * L::COUT + L::COUT, RED_E), 256, 0, s>>>(slab, bslab, splits,
+                                                                                                dw, db);
     PPOX_LAUNCHED("ppox_nature_wgrad_reduce");
 }
 
