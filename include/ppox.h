@@ -164,6 +164,20 @@ int ppox_categorical_sample(const float* logits, int64_t N, int32_t A, int64_t e
                             void* stream);
 
 /* ---------------------------------------------------------------------------
+ * K8  SimHash count bonus (buffer.py:188-200, RolloutStorage(sim_hash=True)).
+ * keys[n] = sign bits of A @ obs[n] (A: 16 x D f64 row-major, bit b <- row b).
+ * apply: for the local envs [offset, offset + n_local) of the step's n_total
+ * keys (global env order), rewards[i] += beta / sqrt(count) with the count the
+ * reference's sequential dictionary update gives that env; then counts (65,536
+ * u32, replicated per rank) += every key of the step.
+ * -------------------------------------------------------------------------*/
+#define PPOX_SIMHASH_KEYS 65536
+int ppox_simhash_keys(const float* obs, int64_t N, int64_t D, int64_t obs_stride,
+                      const double* A, int32_t* keys, void* stream);
+int ppox_simhash_apply(const int32_t* keys_all, int64_t n_total, int64_t offset, int64_t n_local,
+                       uint32_t* counts, double beta, float* rewards, void* stream);
+
+/* ---------------------------------------------------------------------------
  * K5  Minibatch gather (buffer.py:41-52, 256-267): dst[r] = rollout row of the
  * env-major index idx[r]; rows of row_bytes at src_row_stride (step-major).
  * -------------------------------------------------------------------------*/

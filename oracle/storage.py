@@ -108,3 +108,28 @@ class Rollout:
             if self.dual:
                 mb["int_returns"] = f["iret"][idx].flatten()
             yield idx, mb
+
+
+class SimHashCounter:
+    """SimHash count bonus, buffer.py:188-200 (RolloutStorage(sim_hash=True).add):
+    key = sign bits of A @ obs (A = randn(16, D) f64, obs promoted to f64); the
+    count table outlives reset(); envs are processed in index order, each
+    incrementing its key's count and adding beta / sqrt(count) to its reward
+    (f32 reward + f64 bonus, stored back as f32).  Vector observations only."""
+
+    def __init__(self, A, beta=0.1):
+        self.A = np.asarray(A, np.float64)
+        self.beta = beta
+        self.count_table = {}
+
+    def keys(self, obs):
+        bits = (np.dot(self.A, np.asarray(obs).T).T > 0).astype(np.int64)
+        return bits @ (1 << np.arange(bits.shape[1], dtype=np.int64))
+
+    def apply(self, obs, rewards):
+        r = np.array(rewards, dtype=np.float32, copy=True)
+        for i, k in enumerate(self.keys(obs)):
+            c = self.count_table.get(int(k), 0) + 1
+            self.count_table[int(k)] = c
+            r[i] = np.float32(np.float64(r[i]) + self.beta / np.sqrt(c))
+        return r

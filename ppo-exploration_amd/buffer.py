@@ -23,6 +23,7 @@ import torch
 
 import logger
 import native
+from dist import DistContext
 
 
 def _space_dim(space):
@@ -66,8 +67,6 @@ class RolloutStorage(BaseBuffer):
     def __init__(self, buffer_size, n_envs, obs_space, action_space, gae_lam=0.95, gamma=0.99, sim_hash=False,
                  device="cuda", obs_dtype=None, draw_hash_matrix=True):
         super().__init__(buffer_size, obs_space, action_space, n_envs=n_envs)
-        if sim_hash:
-            raise NotImplementedError("SimHash count bonus (buffer.py:188-200) is SURVEY.md §8f 'next' scope")
         self.gae_lam = gae_lam
         self.gamma = gamma
         self.device = torch.device(device)
@@ -79,6 +78,14 @@ class RolloutStorage(BaseBuffer):
         # construction; keep the draw so every later permutation matches.
         self.A = np.random.randn(16, self.obs_shape[0]) if draw_hash_matrix else None
         T, N, d = buffer_size, n_envs, self.device
+        self.do_hash, self.beta = bool(sim_hash), 0.1                  # buffer.py:141-146
+        if self.do_hash:
+            if len(self.obs_shape) != 1 or self.A is None:
+                raise NotImplementedError("sim_hash needs vector observations (A = randn(16, obs_dim), "
+                                          "buffer.py:137); image observations are out of scope")
+            self.hash_A = torch.from_numpy(self.A).to(d)
+            # the count table (buffer.py:136) as one u32 counter per 16-bit key; outlives reset()
+            self.count_table = torch.zeros(native.SIMHASH_KEYS, dtype=torch.int32, device=d)
         self.obs_slots = torch.zeros((T + 1, N) + self.obs_shape, dtype=obs_dtype, device=d)
         if self.discrete:
             self.actions = torch.zeros((T, N), dtype=torch.int32, device=d)
@@ -122,11 +129,31 @@ class RolloutStorage(BaseBuffer):
             self.actions[t].copy_(_to_dev(action, self.device).reshape(self.n_envs, self.action_dim))
             self.log_probs[t].copy_(_to_dev(log_prob, self.device).reshape(self.n_envs, self.action_dim))
         self.rewards[t].copy_(_to_dev(reward, self.device).reshape(self.n_envs))
+        if self.do_hash:
+            self.sim_hash(self.obs_slots[t], self.rewards[t])
         self.masks[t].copy_(_to_dev(mask, self.device).reshape(self.n_envs))
         self.values[t].copy_(_to_dev(value, self.device).reshape(self.n_envs))
         self.pos += 1
         if self.pos == self.buffer_size:
             self.full = True
+
+    def sim_hash(self, obs, rewards):
+        """buffer.py:188-200 on the device: count bonus added to `rewards` (this rank's
+        (n_envs,) f32 row, mutated in place and returned).  Keys of all ranks are
+        gathered so the replicated count table advances exactly as in one process."""
+        x = obs.reshape(self.n_envs, -1)
+        if x.dtype != torch.float32 or x.stride(-1) != 1:
+            x = x.float().contiguous()
+        keys = torch.empty(self.n_envs, dtype=torch.int32, device=self.device)
+        native.simhash_keys(x, self.n_envs, x.shape[1], x.stride(0), self.hash_A, keys)
+        ctx = DistContext.current()
+        if ctx.enabled:
+            keys_all, offset, total = ctx.all_gather_cat(keys, dim=0), ctx.rank * self.n_envs, \
+                self.n_envs * ctx.world
+        else:
+            keys_all, offset, total = keys, 0, self.n_envs
+        native.simhash_apply(keys_all, total, offset, self.n_envs, self.count_table, self.beta, rewards)
+        return rewards
 
     def compute_returns_and_advantages(self, last_value, dones):
         """buffer.py:203-230 on the device (bit-identical), libppox ppox_gae."""

@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libppox.so")
 _vp, _i64, _i32, _f64, _f32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, ctypes.c_float
 _u64 = ctypes.c_uint64
 
+SIMHASH_KEYS = 65536  # include/ppox.h PPOX_SIMHASH_KEYS
 LOSS_PARTIALS = 64   # PPOX_LOSS_PARTIALS
 NORM_PARTIALS = 256  # PPOX_NORM_PARTIALS
 
@@ -40,6 +41,8 @@ SIGNATURES = {
                                    _vp, _vp, _vp, _vp, _f64, _vp, _i64, _f32, _f32, _f32, _f32,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_normal_sample": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _vp, _vp, _vp],
+    "ppox_simhash_keys": [_vp, _i64, _i64, _i64, _vp, _vp, _vp],
+    "ppox_simhash_apply": [_vp, _i64, _i64, _i64, _vp, _f64, _vp, _vp],
     "ppox_gather_rows": [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
     "ppox_grad_sumsq": [_vp, _i64, _vp, _vp],
     "ppox_adam_step": [_vp, _vp, _vp, _vp, _i64, _vp, _f32, _f64, _f64, _f64, _f64, _i64, _vp, _vp],
@@ -278,6 +281,15 @@ def ppo_box_loss_backward(mu, log_std, values, int_values, B, D, idx, T, N, roll
 def normal_sample(mu, log_std, N, D, env_offset, seed, counter, actions, log_probs, stream=None):
     call("ppox_normal_sample", _p(mu), _p(log_std), N, D, env_offset, seed & 0xFFFFFFFFFFFFFFFF, counter,
          _p(actions), _p(log_probs), stream_ptr(stream))
+
+
+def simhash_keys(obs, N, D, stride, A, keys, stream=None):
+    call("ppox_simhash_keys", _p(obs), N, D, stride, _p(A), _p(keys), stream_ptr(stream))
+
+
+def simhash_apply(keys_all, n_total, offset, n_local, counts, beta, rewards, stream=None):
+    call("ppox_simhash_apply", _p(keys_all), n_total, offset, n_local, _p(counts), float(beta), _p(rewards),
+         stream_ptr(stream))
 
 
 def categorical_sample(logits, N, A, env_offset, seed, counter, actions, log_probs, stream=None):

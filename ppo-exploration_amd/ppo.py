@@ -296,6 +296,8 @@ class PPO(BaseAlgorithm):
             ro.values[t].copy_(v)
             self.env.step_into(ro.obs_slots[t], ro.obs_slots[t + 1], ro.actions[t], ro.rewards[t], ro.masks[t],
                                ro.done_ret[t], ro.done_len[t])
+            if ro.do_hash:                                  # rollout.add -> sim_hash(last_obs), buffer.py:176
+                ro.sim_hash(ro.obs_slots[t], ro.rewards[t])
             self.num_timesteps += self.num_envs
         ro.pos, ro.full = self.nstep, True
         # ppo.py:196 bootstraps with V(s_{T-1}) and the last step's dones

@@ -283,6 +283,41 @@ def gen_get(R):
 
 
 # --------------------------------------------------------------------------
+# (4b) SimHash count bonus (buffer.py:188-200) through RolloutStorage.add with
+#      sim_hash=True: keys of A.obs, a count table persisting across reset(),
+#      rewards mutated in env-index order.  Duplicated rows force collisions
+#      within one step.
+# --------------------------------------------------------------------------
+def gen_simhash(R):
+    import torch
+    out = {}
+    for k, (T, N, D, rollouts, seed) in enumerate([(5, 16, 2, 2, 31), (4, 64, 6, 3, 32), (3, 7, 1, 2, 33)]):
+        np.random.seed(seed)
+        st = R.buffer.RolloutStorage(T, N, Box((D,)), Discrete(2), sim_hash=True)  # draws A = randn(16, D)
+        rs = np.random.RandomState(seed + 100)
+        p = f"s{k}_"
+        out[p + "cfg"] = np.array([T, N, D, rollouts, seed], np.int64)
+        out[p + "A"] = st.A.copy()
+        obs_all, rin_all, rout_all = [], [], []
+        for r in range(rollouts):
+            st.reset()
+            for t in range(T):
+                obs = rs.randn(N, D).astype(np.float32)
+                dup = rs.rand(N) < 0.5
+                obs[dup] = obs[rs.randint(0, max(1, N // 4), dup.sum())]
+                rew = rs.randn(N).astype(np.float32)
+                obs_all.append(obs.copy())
+                rin_all.append(rew.copy())
+                st.add(obs, np.zeros((N, 1)), rew, torch.zeros(N), np.zeros(N, bool), torch.zeros(N, 1))
+                rout_all.append(st.rewards[t].copy())
+        out[p + "obs"] = np.stack(obs_all)
+        out[p + "rew_in"] = np.stack(rin_all)
+        out[p + "rew_out"] = np.stack(rout_all)
+        out[p + "n_keys"] = np.int64(len(st.count_table))
+    save("simhash", **out)
+
+
+# --------------------------------------------------------------------------
 # (5) One full PPO.train() (ppo.py:200-259) on fixed weights: losses, dL/dlogits,
 #     dL/dvalues per minibatch, post-update weights.  Discrete and Box.
 # --------------------------------------------------------------------------
@@ -496,10 +531,15 @@ def main():
         print("reference not present; fixtures are committed — nothing to do")
         return 0
     R = import_reference()
+    if len(sys.argv) > 1:  # regenerate selected fixtures only, e.g. `simhash`
+        for name in sys.argv[1:]:
+            globals()["gen_" + name](R)
+        return 0
     gen_gae(R)
     gen_gae_dual(R)
     gen_rms(R)
     gen_get(R)
+    gen_simhash(R)
     gen_train(R)
     gen_rnd(R)
     gen_icm(R)

@@ -167,3 +167,17 @@ def test_nature_cnn_architecture(golden):
         logits, _, value, _ = net.heads(torch.from_numpy(f["x"].astype(np.float32)))
     np.testing.assert_allclose(logits.numpy(), f["logits"], rtol=1e-5, atol=1e-4)
     np.testing.assert_allclose(value.numpy(), f["value"], rtol=1e-5, atol=1e-4)
+
+
+def test_simhash_bonus_bitexact(golden):
+    """oracle SimHash (buffer.py:188-200) vs the reference's own add() runs: rewards after
+    the bonus bit-exact, count table persisting across reset(), same number of keys."""
+    from oracle.storage import SimHashCounter
+    f = golden("simhash")
+    for k in range(3):
+        p = f"s{k}_"
+        sh = SimHashCounter(f[p + "A"])
+        for step in range(f[p + "obs"].shape[0]):
+            out = sh.apply(f[p + "obs"][step], f[p + "rew_in"][step])
+            np.testing.assert_array_equal(out, f[p + "rew_out"][step])
+        assert len(sh.count_table) == int(f[p + "n_keys"])

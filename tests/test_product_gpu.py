@@ -200,3 +200,53 @@ def test_icm_train_matches_reference_run(golden, name, code):
         np.testing.assert_allclose(v.cpu().numpy(), f[p + "w1_" + k], rtol=2e-5, atol=2e-6, err_msg=k)
     for k, v in alg.intrinsic_module.state_dict().items():
         np.testing.assert_allclose(v.cpu().numpy(), f[p + "i1_" + k], rtol=2e-5, atol=2e-6, err_msg=k)
+
+
+def test_simhash_matches_reference(golden):
+    """RolloutStorage(sim_hash=True).add (buffer.py:165-200): same A draw, rewards after the
+    count bonus bit-exact vs the reference's own runs, table persisting across reset()."""
+    import buffer
+    import env as E
+    f = golden("simhash")
+    for k in range(3):
+        p = f"s{k}_"
+        T, N, D, rollouts, seed = (int(x) for x in f[p + "cfg"])
+        np.random.seed(seed)
+        st = buffer.RolloutStorage(T, N, E.Box((D,)), E.Discrete(2), sim_hash=True)
+        np.testing.assert_array_equal(st.A, f[p + "A"])
+        step = 0
+        for _ in range(rollouts):
+            st.reset()
+            for t in range(T):
+                st.add(f[p + "obs"][step], np.zeros(N), f[p + "rew_in"][step], np.zeros(N, np.float32),
+                       np.zeros(N, bool), np.zeros(N, np.float32))
+                np.testing.assert_array_equal(st.rewards[t].cpu().numpy(), f[p + "rew_out"][step])
+                step += 1
+        assert int((st.count_table > 0).sum().item()) == int(f[p + "n_keys"])
+
+
+def test_simhash_sharded_apply_equals_single():
+    """Two env shards with replicated count tables (the multi-GPU path: keys all-gathered,
+    each rank applies the bonus to its own envs) == one process over all envs."""
+    import native
+    rs = np.random.RandomState(5)
+    N, D, steps = 1000, 3, 4
+    A = torch.tensor(rs.randn(16, D), device="cuda")
+    one = torch.zeros(native.SIMHASH_KEYS, dtype=torch.int32, device="cuda")
+    tabs = [torch.zeros_like(one), torch.zeros_like(one)]
+    for _ in range(steps):
+        obs = rs.randn(N, D).astype(np.float32)
+        obs[rs.rand(N) < 0.6] = obs[0]
+        x = torch.tensor(obs, device="cuda")
+        rew = torch.tensor(rs.randn(N).astype(np.float32), device="cuda")
+        keys = torch.empty(N, dtype=torch.int32, device="cuda")
+        native.simhash_keys(x, N, D, D, A, keys)
+        r_one = rew.clone()
+        native.simhash_apply(keys, N, 0, N, one, 0.1, r_one)
+        halves = []
+        for rank in range(2):
+            r = rew[rank * N // 2:(rank + 1) * N // 2].clone()
+            native.simhash_apply(keys, N, rank * N // 2, N // 2, tabs[rank], 0.1, r)
+            halves.append(r)
+        assert torch.equal(torch.cat(halves), r_one)
+        assert torch.equal(tabs[0], one) and torch.equal(tabs[1], one)
