@@ -84,3 +84,12 @@ def owned_minibatch_indices(perm, T, env_lo, n_local, batch_size):
     counts = np.bincount(mb_of, minlength=n_mb)
     offsets = np.concatenate([[0], np.cumsum(counts)])
     return local, offsets
+
+
+def owned_minibatch_positions(perm, T, env_lo, n_local, batch_size):
+    """Positions inside their global minibatch (0..B-1) of the rows owned_minibatch_indices
+    returns, in the same order."""
+    perm = np.asarray(perm, dtype=np.int64)
+    env = perm // T
+    own = np.nonzero((env >= env_lo) & (env < env_lo + n_local))[0]
+    return own - (own // batch_size) * batch_size

@@ -31,7 +31,7 @@ import logger
 import native
 import convs
 from buffer import IntrinsicStorage, RolloutStorage
-from dist import DistContext, owned_minibatch_indices, shard_range
+from dist import DistContext, owned_minibatch_indices, owned_minibatch_positions, shard_range
 from env import make_env
 from models import CnnActorCritic, FlatParams, IntrinsicCuriosityModule, MlpNetwork, RndNetwork
 from util import ActionConverter, RunningMeanStd
@@ -39,6 +39,46 @@ from util import ActionConverter, RunningMeanStd
 
 def _is_image(space):
     return len(space.shape) == 3
+
+
+def icm_loss_sharded(icm, x, acts, pos, B, beta, ctx):
+    """ICM loss of one GLOBAL minibatch whose rows are spread over ranks (ppo.py:684-692):
+    pairs are consecutive rows of the permuted minibatch, (row j, row j+1), j < B-1,
+    whatever rank owns them.  x / acts: this rank's owned rows (permutation order),
+    pos: their positions in the minibatch.  Encoder features and actions are summed
+    into global positions (all-reduce of B x h f32 + B actions), each rank evaluates
+    the pairs whose first row it owns, and the feature gradient is all-reduced back to
+    the owners — so the gradients equal the single-process ones.  Backpropagates into
+    the ICM parameters' .grad and returns this rank's share of the loss (sum over ranks
+    = the reference's icm_loss)."""
+    h = icm.feature_size
+    phi = icm.state_encoder(x)
+    full = torch.zeros(B, h, dtype=phi.dtype, device=phi.device)
+    full[pos] = phi.detach()
+    ctx.all_reduce_(full)
+    phi_all = full.requires_grad_(True)
+    if icm.discrete:
+        a_full = torch.zeros(B, dtype=torch.int64, device=phi.device)
+        a_full[pos] = acts.reshape(-1).long()
+    else:
+        a_full = torch.zeros(B, acts.shape[-1], dtype=torch.float32, device=phi.device)
+        a_full[pos] = acts.float()
+    ctx.all_reduce_(a_full)
+    j = pos[pos < B - 1]
+    s_ft, n_ft = phi_all[j], phi_all[j + 1]
+    a_hat = icm.inverse_model(torch.cat((s_ft, n_ft), 1))
+    n_hat = icm.forward_model(torch.cat((s_ft, icm.encode_action(a_full[j])), 1))
+    npair = B - 1
+    fwd = ((n_hat - n_ft) ** 2).sum() / (npair * h)                    # F.mse_loss, mean over (B-1) x h
+    if icm.discrete:
+        inv = F.cross_entropy(a_hat, a_full[j], reduction="sum") / npair
+    else:
+        inv = ((a_hat - a_full[j]) ** 2).sum() / (npair * a_hat.shape[1])
+    loss = (1 - beta) * inv + beta * fwd
+    loss.backward()
+    g = ctx.all_reduce_(phi_all.grad)
+    phi.backward(g[pos])
+    return loss.detach()
 
 
 class Policy:
@@ -196,6 +236,8 @@ class BaseAlgorithm:
             offs = np.concatenate([[0], np.cumsum(sizes)])
             return perm_dev, perm_dev, offs, sizes
         local, offs = owned_minibatch_indices(perm, self.nstep, self.env_offset, self.local_envs, bs)
+        self._epoch_pos = torch.from_numpy(
+            owned_minibatch_positions(perm, self.nstep, self.env_offset, self.local_envs, bs)).to(self.device)
         return perm_dev, torch.from_numpy(local).to(self.device, non_blocking=True), offs, sizes
 
     def _global_advantages(self, ro, intrinsic=False):
@@ -553,18 +595,23 @@ class PPO_ICM(BaseAlgorithm):
                 else:
                     acts = ro.actions.reshape(-1, self.n_actions)[rows]
                 x = self._icm_x(obs)
-                a_hat, f_next, f_next_hat = icm(x[:-1], x[1:], acts[:-1])
-                fwd = F.mse_loss(f_next, f_next_hat)
-                # inverse loss: CrossEntropy (Discrete) / MSE (Box) (util.py:61-69)
-                inv = F.cross_entropy(a_hat, acts[:-1].long()) if self.discrete else F.mse_loss(a_hat, acts[:-1])
-                icm_loss = (1 - self.beta) * inv + self.beta * fwd
-                self.icm_accum += icm_loss.detach().double()
-                torch.autograd.backward([out, v, icm_loss], [dout, dv, None])
+                if self.dist.enabled:  # pairs cross rank boundaries: exchange features (icm_loss_sharded)
+                    torch.autograd.backward([out, v], [dout, dv])
+                    pos = self._epoch_pos[offs[k]:offs[k + 1]]
+                    self.icm_accum += icm_loss_sharded(icm, x, acts, pos, B, self.beta, self.dist).double()
+                else:
+                    a_hat, f_next, f_next_hat = icm(x[:-1], x[1:], acts[:-1])
+                    fwd = F.mse_loss(f_next, f_next_hat)
+                    # inverse loss: CrossEntropy (Discrete) / MSE (Box) (util.py:61-69)
+                    inv = F.cross_entropy(a_hat, acts[:-1].long()) if self.discrete else F.mse_loss(a_hat, acts[:-1])
+                    icm_loss = (1 - self.beta) * inv + self.beta * fwd
+                    self.icm_accum += icm_loss.detach().double()
+                    torch.autograd.backward([out, v, icm_loss], [dout, dv, None])
                 self.dist.all_reduce_(self.flat.grad)
                 self.dist.all_reduce_(self.icm_flat.grad)
                 self.flat.adam_step(self.lr, self.max_grad_norm)               # ppo.py:697-698
                 self.icm_flat.adam_step(self.int_lr, None)                     # ppo.py:699 (no clipping)
-        icm_mean = float(self.icm_accum.item())
+        icm_mean = float(self.dist.all_reduce_(self.icm_accum).item())
         acc = self._record_train(extra=icm_mean)
         logger.record("train/icm_loss", icm_mean / max(acc[5], 1.0))
         self._n_updates += self.n_epochs

@@ -145,3 +145,61 @@ def test_two_rank_gradients_equal_single_process():
         ref = torch.cat([p.grad.reshape(-1) for p in net.parameters()]).numpy()
         for r in range(world):
             np.testing.assert_allclose(res[r][k], ref, rtol=2e-5, atol=1e-7)
+
+
+def _icm_worker(rank, world, port, out_q, discrete, seed):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ppo import icm_loss_sharded
+        icm, x, a, owner = _icm_case(discrete, seed)
+        mine = np.nonzero(owner == rank)[0]  # positions this rank owns, in minibatch order
+        pos = torch.from_numpy(mine)
+        loss = icm_loss_sharded(icm, x[pos], a[pos], pos, x.shape[0], 0.2, DistContext.current())
+        g = torch.cat([p.grad.reshape(-1) for p in icm.parameters()])
+        tdist.all_reduce(g)
+        out_q.put((rank, float(loss), g.numpy()))
+    finally:
+        tdist.destroy_process_group()
+
+
+def _icm_case(discrete, seed):
+    from models import IntrinsicCuriosityModule
+    from util import ActionConverter
+    import env as E
+    torch.manual_seed(seed)
+    rs = np.random.RandomState(seed)
+    B, F_, A = 23, 10, 3
+    space = E.Discrete(A) if discrete else E.Box((A,))
+    icm = IntrinsicCuriosityModule(F_, ActionConverter(space), hidden_size=8)
+    x = torch.tensor(rs.randn(B, F_).astype(np.float32))
+    a = torch.tensor(rs.randint(0, A, B)) if discrete else torch.tensor(rs.randn(B, A).astype(np.float32))
+    owner = rs.randint(0, 2, B)  # a random, interleaved row ownership
+    return icm, x, a, owner
+
+
+@pytest.mark.parametrize("discrete", [True, False])
+def test_icm_sharded_pairs_equal_single_process(discrete):
+    """PPO_ICM pairs (row j, row j+1) of the permuted minibatch (ppo.py:684-692) across two
+    ranks with interleaved row ownership == the one-process loss and gradients."""
+    import torch.nn.functional as F
+    seed = 17
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_icm_worker, args=(r, 2, port, q, discrete, seed)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (l, g)) for r, l, g in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+    icm, x, a, _ = _icm_case(discrete, seed)
+    a_hat, nf, nfh = icm(x[:-1], x[1:], a[:-1])
+    inv = F.cross_entropy(a_hat, a[:-1].long()) if discrete else F.mse_loss(a_hat, a[:-1])
+    loss = 0.8 * inv + 0.2 * F.mse_loss(nf, nfh)
+    loss.backward()
+    ref = torch.cat([p.grad.reshape(-1) for p in icm.parameters()]).numpy()
+    np.testing.assert_allclose(res[0][0] + res[1][0], loss.item(), rtol=1e-5)
+    for r in range(2):
+        np.testing.assert_allclose(res[r][1], ref, rtol=1e-4, atol=1e-6)
