@@ -1100,9 +1100,16 @@ extern "C" int ppox_nature_conv_dgrad(int32_t layer, const float* grad_out, int6
 #endif
 }
 
+// split-K factor over pixels: ~4096 pixels per split, but enough splits that the
+// grid (splits x k-blocks) fills the chip (>= ~1536 workgroups, 2 rounds of the
+// ~768 resident slots) at small per-rank batches; at least 4 steps per split
 extern "C" int64_t ppox_nature_wgrad_splits(int32_t layer, int64_t batch) {
     const long long P = layer == 1 ? G1::P : (layer == 2 ? G2::P : G3::P);
-    long long s = (batch * P + 4095) / 4096;
+    const long long kb = layer == 1 ? WgCfg<G1, true>::KB : (layer == 2 ? WgCfg<G2, false>::KB : WgCfg<G3, false>::KB);
+    const long long px = batch * P;
+    long long s = (px + 4095) / 4096;
+    const long long fill = (1536 + kb - 1) / kb, most = px / (4 * MS);
+    if (s < fill) s = fill < most ? fill : most;
     s = s < 8 ? 8 : (s > 512 ? 512 : s);
     return (s + 7) / 8 * 8;
 }
