@@ -595,18 +595,13 @@ class PPO_ICM(BaseAlgorithm):
                 else:
                     acts = ro.actions.reshape(-1, self.n_actions)[rows]
                 x = self._icm_x(obs)
-                if self.dist.enabled:  # pairs cross rank boundaries: exchange features (icm_loss_sharded)
-                    torch.autograd.backward([out, v], [dout, dv])
-                    pos = self._epoch_pos[offs[k]:offs[k + 1]]
-                    self.icm_accum += icm_loss_sharded(icm, x, acts, pos, B, self.beta, self.dist).double()
-                else:
-                    a_hat, f_next, f_next_hat = icm(x[:-1], x[1:], acts[:-1])
-                    fwd = F.mse_loss(f_next, f_next_hat)
-                    # inverse loss: CrossEntropy (Discrete) / MSE (Box) (util.py:61-69)
-                    inv = F.cross_entropy(a_hat, acts[:-1].long()) if self.discrete else F.mse_loss(a_hat, acts[:-1])
-                    icm_loss = (1 - self.beta) * inv + self.beta * fwd
-                    self.icm_accum += icm_loss.detach().double()
-                    torch.autograd.backward([out, v, icm_loss], [dout, dv, None])
+                torch.autograd.backward([out, v], [dout, dv])
+                # pairs (row j, row j+1) of the permuted minibatch; each row is encoded once
+                # (the reference encodes s and s' separately: same rows, same math) and at
+                # world > 1 the pairs cross rank boundaries (icm_loss_sharded)
+                pos = self._epoch_pos[offs[k]:offs[k + 1]] if self.dist.enabled else \
+                    torch.arange(Bl, device=self.device)
+                self.icm_accum += icm_loss_sharded(icm, x, acts, pos, B, self.beta, self.dist).double()
                 self.dist.all_reduce_(self.flat.grad)
                 self.dist.all_reduce_(self.icm_flat.grad)
                 self.flat.adam_step(self.lr, self.max_grad_norm)               # ppo.py:697-698
