@@ -37,6 +37,41 @@ def pmc_traffic(kernel="wgrad_kernel<4, 84, 84, 8, 8, 4, 32, true>"):
     return (None, None) if d is None else (d["hbm_bytes_per_launch_corrected"], os.path.relpath(files[-1], ROOT))
 
 
+def gae_kernel_ms(alg, dual, reps=20):
+    """Kernel time of the rollout's GAE launch (K1) at the config size: the same call on the
+    rollout's own buffers, captured `reps` times in a graph and replayed, so the host's
+    per-launch cost (~10 us, longer than the kernel) is not counted.  GAE is idempotent on
+    its inputs, so re-running it after the timed region changes nothing."""
+    import torch
+    import native
+    ro = alg.rollout
+    T = alg.nstep - 1
+    if dual:
+        call = lambda: native.gae_dual(ro.rewards, ro.values, ro.masks, ro.values[T], ro.masks[T], ro.int_rewards,
+                                       ro.int_values, ro.int_values[T], ro.gamma, ro.int_gamma, ro.gae_lam,
+                                       ro.advantages, ro.returns, ro.int_advantages, ro.int_returns)
+    else:
+        call = lambda: native.gae(ro.rewards, ro.values, ro.masks, ro.values[T], ro.masks[T], ro.gamma, ro.gae_lam,
+                                  ro.advantages, ro.returns)
+    try:
+        call()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                call()
+        g.replay()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        g.replay()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps
+    except Exception:  # capture not possible here: report no GAE roofline rather than a wrong one
+        return None
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -90,10 +125,10 @@ def main():
         iteration()
 
     # event timing of the dominant kernel (conv1 weight-gradient MFMA GEMM)
-    # on the stream it is launched on, plus the GAE scan (K1) for its HBM roofline
+    # on the stream it is launched on
     prof_kernel = "ppox_nature_conv_wgrad:1"
     gae_kernel = "ppox_gae" if args.algo != "rnd" else "ppox_gae_dual"
-    native.enable_event_timing([prof_kernel, gae_kernel])
+    native.enable_event_timing([prof_kernel])
 
     torch.cuda.synchronize()
     if world > 1:
@@ -106,8 +141,8 @@ def main():
         tdist.barrier()
     dt = time.perf_counter() - t0
     kt = native.event_times_ms(prof_kernel)
-    gt = native.event_times_ms(gae_kernel)
     native.enable_event_timing([])
+    gae_ms = gae_kernel_ms(alg, args.algo == "rnd")
     if world > 1:
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
@@ -141,15 +176,16 @@ def main():
                            "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)", "traffic_source": src,
                            "alg_bytes_per_launch": alg_bytes, "launches": len(kt),
                            "mean_us": round(mean_ms * 1e3, 1), "alg_flops_per_launch": float(np.mean(flops))}
-    if gt:
+    if gae_ms:
         n_local = args.envs // world
         alg_bytes = (17 if gae_kernel == "ppox_gae" else 33) * args.nstep * n_local
-        mean_ms = float(np.mean([t for t, _ in gt]))
+        mean_ms = gae_ms
         ach = alg_bytes / (mean_ms * 1e-3) / 1e9
         out["gae_roofline"] = {"kernel": gae_kernel, "bound": "hbm", "achieved": round(ach, 1),
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                                "mean_us": round(mean_ms * 1e3, 2), "alg_bytes_per_launch": alg_bytes,
-                               "note": "config-size launch is latency-bound; tools/gae_sweep.py sweeps N"}
+                               "note": "config-size launch (graph replay of the rollout's own GAE call, "
+                                       "kernel time only) is latency-bound; tools/gae_sweep.py sweeps N"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, ROOT)
         from oracle.baseline import atari_ppo_rate

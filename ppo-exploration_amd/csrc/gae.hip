@@ -122,6 +122,143 @@ __global__ void __launch_bounds__(256) gae_kernel(
     }
 }
 
+// Small-N form (N up to a few 10k envs, T <= STAGED_TMAX): a 256-thread block owns
+// EB = 16 envs (8 for two streams) x all T steps.  Phase 1 (all threads): coalesced loads of the
+// block's (t, env) tile, delta and the f64 decay factor (gl * nnt) per element
+// into LDS.  Phase 2 (16 lanes, +16 for the intrinsic stream): the sequential
+// carry chain per env reading LDS — the same operations in the same order as
+// the lane-per-env form, so the result is bit-identical.  Phase 3 (all
+// threads): adv / ret stores.  N / 16 blocks instead of N / 64 waves: the
+// latency of the loads is paid once per block, not once per step.
+template <bool DUAL>
+constexpr int staged_eb() { return DUAL ? 8 : 16; }  // envs per block (LDS <= 64 KB at T = 128)
+constexpr int STAGED_TMAX = 256;
+constexpr int CH = 16;  // chain steps per register chunk
+#ifndef STAGED_NMAX
+#define STAGED_NMAX 8192  // measured crossover (tools/gae_sweep.py): above it the lane-per-env form wins
+#endif
+
+template <bool DUAL>
+__global__ void __launch_bounds__(256) gae_staged_kernel(
+    const float* __restrict__ rew, const float* __restrict__ val, const uint8_t* __restrict__ done,
+    const float* __restrict__ last_v, const uint8_t* __restrict__ last_done,
+    const float* __restrict__ irew, const float* __restrict__ ival, const float* __restrict__ last_iv,
+    int T, long long N, float g32, double gl, float ig32, float igl32,
+    float* __restrict__ adv, float* __restrict__ ret, float* __restrict__ iadv, float* __restrict__ iret) {
+    constexpr int EB = staged_eb<DUAL>();
+    constexpr int PER = STAGED_TMAX / (256 / EB);  // steps per thread
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double* sdelta = reinterpret_cast<double*>(smem);        // [T][EB]
+    double* sdecay = sdelta + T * EB;                         // [T][EB] gl * nnt
+    float* sadv = reinterpret_cast<float*>(sdecay + T * EB);  // [T][EB] adv, then ret
+    float* sv = sadv + T * EB;                                // [T][EB] values
+    float* sid = sv + T * EB;                                 // [T][EB] intrinsic delta (DUAL)
+    float* siadv = sid + (DUAL ? T * EB : 0);                 // [T][EB] (DUAL)
+    float* siv = siadv + (DUAL ? T * EB : 0);                 // [T][EB] (DUAL)
+    const long long n0 = (long long)blockIdx.x * EB;
+    const int e = threadIdx.x % EB, t0 = threadIdx.x / EB;
+    const long long n = n0 + e;
+    const bool ok = n < N;
+    const long long nc = ok ? n : n0;  // clamped: loads stay in bounds, results unused
+    // phase 1: every load of this thread's (t, e) elements in flight at once
+    float r[PER], v[PER], nv[PER], ir[PER], iv[PER], niv[PER];
+    uint8_t dn[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int t = t0 + k * (256 / EB);
+        if (t < T) {
+            const long long o = (long long)t * N + nc;
+            const bool last = t == T - 1;
+            r[k] = rew[o];
+            v[k] = val[o];
+            nv[k] = last ? last_v[nc] : val[o + N];
+            dn[k] = last ? last_done[nc] : done[o + N];
+            if constexpr (DUAL) {
+                ir[k] = irew[o];
+                iv[k] = ival[o];
+                niv[k] = last ? last_iv[nc] : ival[o + N];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int t = t0 + k * (256 / EB);
+        if (t < T) {
+            const double nnt = 1.0 - (double)dn[k];
+            const float gv = g32 * nv[k];
+            sdelta[t * EB + e] = ((double)r[k] + (double)gv * nnt) - (double)v[k];
+            sdecay[t * EB + e] = gl * nnt;
+            sv[t * EB + e] = v[k];
+            if constexpr (DUAL) {
+                sid[t * EB + e] = (ir[k] + ig32 * niv[k]) - iv[k];
+                siv[t * EB + e] = iv[k];
+            }
+        }
+    }
+    __syncthreads();
+    // phase 2: the carry chains (extrinsic on wave 0, intrinsic on wave 1, concurrently).
+    // Each chunk of CH steps is read into registers first, so the LDS latency is paid
+    // once per chunk, not once per step (a store in the loop would otherwise order
+    // every next load behind it).
+    if (threadIdx.x < EB) {
+        double carry = 0.0;
+        for (int hi = T - 1; hi >= 0; hi -= CH) {
+            double dl[CH], dc[CH];
+            float out[CH];
+#pragma unroll
+            for (int j = 0; j < CH; ++j)
+                if (hi - j >= 0) {
+                    dl[j] = sdelta[(hi - j) * EB + e];
+                    dc[j] = sdecay[(hi - j) * EB + e];
+                }
+#pragma unroll
+            for (int j = 0; j < CH; ++j)
+                if (hi - j >= 0) {
+                    carry = dl[j] + dc[j] * carry;
+                    out[j] = (float)carry;
+                }
+#pragma unroll
+            for (int j = 0; j < CH; ++j)
+                if (hi - j >= 0) sadv[(hi - j) * EB + e] = out[j];
+        }
+    } else if (DUAL && threadIdx.x >= 64 && threadIdx.x < 64 + EB) {
+        float icarry = 0.f;
+        for (int hi = T - 1; hi >= 0; hi -= CH) {
+            float d[CH];
+#pragma unroll
+            for (int j = 0; j < CH; ++j)
+                if (hi - j >= 0) d[j] = sid[(hi - j) * EB + e];
+#pragma unroll
+            for (int j = 0; j < CH; ++j)
+                if (hi - j >= 0) {
+                    icarry = (hi - j == T - 1) ? (d[j] + 0.0f) : (d[j] + igl32 * icarry);
+                    d[j] = icarry;
+                }
+#pragma unroll
+            for (int j = 0; j < CH; ++j)
+                if (hi - j >= 0) siadv[(hi - j) * EB + e] = d[j];
+        }
+    }
+    __syncthreads();
+    // phase 3: stores
+    if (!ok) return;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int t = t0 + k * (256 / EB);
+        if (t < T) {
+            const long long o = (long long)t * N + n;
+            const float a = sadv[t * EB + e];
+            adv[o] = a;
+            ret[o] = a + sv[t * EB + e];
+            if constexpr (DUAL) {
+                const float ia = siadv[t * EB + e];
+                iadv[o] = ia;
+                iret[o] = ia + siv[t * EB + e];
+            }
+        }
+    }
+}
+
 template <bool DUAL>
 int launch_gae(const float* rew, const float* val, const uint8_t* done, const float* last_v,
                const uint8_t* last_done, const float* irew, const float* ival, const float* last_iv,
@@ -143,7 +280,13 @@ int launch_gae(const float* rew, const float* val, const uint8_t* done, const fl
     for (const void* p : ptrs)
         if (p && !ppox::aligned16(p)) vec4 = false;
     if (reinterpret_cast<uintptr_t>(done) % 4 || reinterpret_cast<uintptr_t>(last_done) % 4) vec4 = false;
-    if (vec4) {
+    constexpr int EB = staged_eb<DUAL>();
+    const size_t lds = (size_t)T * EB * (16 + 8 + (DUAL ? 12 : 0));
+    if (N <= STAGED_NMAX && T <= STAGED_TMAX && lds <= 65536) {
+        gae_staged_kernel<DUAL><<<ppox::ceil_div(N, EB), 256, lds, s>>>(
+            rew, val, done, last_v, last_done, irew, ival, last_iv, (int)T, N, g32, gl, ig32, igl32, adv, ret,
+            iadv, iret);
+    } else if (vec4) {
         const long long lanes = N / 4;
         const int bs = 256;
         gae_kernel<4, DUAL><<<ppox::ceil_div(lanes, bs), bs, 0, s>>>(

@@ -15,22 +15,30 @@ HBM_PEAK = 8000.0
 
 
 def time_ms(fn, iters=20):
-    for _ in range(3):
-        fn()
+    """Kernel time per launch: `iters` launches captured in one graph and replayed, so
+    the host's per-launch cost (ctypes + HIP API, ~10 us) is not in the measurement."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(iters):
-        fn()
+    g.replay()
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / iters
 
 
 def main():
+    if len(sys.argv) > 1:  # optional libppox variant (tools/build_variant.sh)
+        native.load(sys.argv[1])
     T = 128
     rows = []
-    for N in (4096, 65536, 262144, 1 << 20, 1 << 21, 1 << 22):
+    for N in (1024, 4096, 16384, 65536, 131072, 262144, 1 << 20, 1 << 21, 1 << 22):
         f = lambda: torch.randn(T, N, device="cuda")
         r, v, ir, iv = f(), f(), f(), f()
         d = (torch.rand(T, N, device="cuda") < 0.01).to(torch.uint8)
