@@ -254,6 +254,26 @@ int ppox_nature_wgrad_reduce(int32_t layer, int64_t batch, const void* workspace
 int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, int64_t batch, float* out,
                                 void* stream);
 
+/* ---------------------------------------------------------------------------
+ * K6, split-bf16 forms (csrc/conv_split.hip): the same ops, layouts and fused
+ * epilogues as above, on the bf16 matrix cores (v_mfma_f32_32x32x16_bf16) with
+ * every f32 operand split exactly into three bf16 planes (a = a0 + a1 + a2).
+ * Products a*b keep the six terms a_i*b_j with i + j <= 2 (dropped terms
+ * < 3*2^-22 |ab|); large and small terms accumulate separately in f32.  The
+ * uint8 frames of layer 1 are exact in one plane.  Accuracy: fp32-class (error
+ * vs fp64 at or below the f32-MFMA kernels', tests/test_kernels_gpu.py).
+ * Weights are packed by ppox_nature_pack_split into bf16 planes (uint16
+ * storage) of ppox_nature_split_pack_elems(which) elements: which = 1, 2, 3
+ * (forward weights of that layer), 12, 13 (dgrad weights of conv2 / conv3).
+ * Replaces the same reference sites as the f32 forms.
+ * -------------------------------------------------------------------------*/
+int64_t ppox_nature_split_pack_elems(int32_t which);
+int ppox_nature_pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1,
+                           uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3, void* stream);
+int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
+                               int64_t T, int64_t N_env, int64_t x_sample_stride,
+                               const uint16_t* wq, const float* bias, float* y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,15 +1,35 @@
 """NatureCNN conv trunk on the libppox MFMA implicit-GEMM kernels.
 
-Forward: ppox_nature_conv_fwd (fp32 MFMA, fused u8->f32, bias, ReLU) for the
-three convolutions of .ipynb_checkpoints/models-checkpoint.py:52-58, with
-activations laid out NHWC between layers and NCHW at the trunk output (the
-reference's Flatten order for Linear(3136, 512)).
+Forward: ppox_nature_conv_fwd[_split] (fused u8->f32, bias, ReLU) for the three
+convolutions of .ipynb_checkpoints/models-checkpoint.py:52-58, with activations
+laid out NHWC between layers and NCHW at the trunk output (the reference's
+Flatten order for Linear(3136, 512)).
 Backward: libppox MFMA dgrad (ReLU backward of the layer below fused) and
 split-K wgrad (+ bias grad, deterministic fixed-order reduction) kernels.
+
+Math modes (PPOX_CONV_MATH, default "split"):
+  "split" — f32 operands split exactly into three bf16 planes on the bf16 matrix
+            cores (csrc/conv_split.hip): fp32-class accuracy (measured below the
+            f32-MFMA kernels' error vs fp64, tools/split_probe.py) at up to 16x
+            the f32-input MFMA rate.  Ops without a split kernel yet use "f32".
+  "f32"   — v_mfma_f32_32x32x2_f32: every product an exact f32 FMA (csrc/conv.hip).
 """
+import os
+
 import torch
 
 import native
+
+MATHS = ("split", "f32")
+# ops that have a split-bf16 kernel: ("fwd" | "dgrad" | "wgrad", layer)
+SPLIT_OPS = {("fwd", 1)}
+
+
+def default_math():
+    m = os.environ.get("PPOX_CONV_MATH", "split")
+    if m not in MATHS:
+        raise ValueError(f"PPOX_CONV_MATH must be one of {MATHS}, got {m!r}")
+    return m
 
 
 class _NatureTrunk(torch.autograd.Function):
@@ -22,9 +42,9 @@ class _NatureTrunk(torch.autograd.Function):
         h2 = torch.empty((B, 9, 9, 64), device=dev)
         h3 = torch.empty((B, 64, 7, 7), device=dev)
         if B:
-            native.nature_conv_fwd(1, x, B, None, 0, 0, 4 * 84 * 84, convs.wp1, b1, h1)
-            native.nature_conv_fwd(2, h1, B, None, 0, 0, 0, convs.wp2, b2, h2)
-            native.nature_conv_fwd(3, h2, B, None, 0, 0, 0, convs.wp3, b3, h3)
+            convs.fwd(1, x, B, b1, h1)
+            convs.fwd(2, h1, B, b2, h2)
+            convs.fwd(3, h2, B, b3, h3)
         ctx.convs = convs
         ctx.save_for_backward(x, h1, h2, h3)
         return h3
@@ -43,31 +63,40 @@ class _NatureTrunk(torch.autograd.Function):
         dh3 = dh3.contiguous()
         g3 = torch.empty((B, 7, 7, 64), device=dev)
         native.nchw_to_nhwc_relu_grad(dh3, h3, B, g3)          # ReLU backward of conv3, to NHWC
-        native.nature_conv_wgrad(3, h2, B, None, 0, 0, 0, g3, convs.workspace(3, B), dw3, db3)
+        convs.wgrad(3, h2, B, g3, dw3, db3)
         g2 = torch.empty((B, 9, 9, 64), device=dev)
-        native.nature_conv_dgrad(3, g3, B, convs.wpd3, h2, g2)  # dX of conv3, times ReLU'(conv2)
-        native.nature_conv_wgrad(2, h1, B, None, 0, 0, 0, g2, convs.workspace(2, B), dw2, db2)
+        convs.dgrad(3, g3, B, h2, g2)                           # dX of conv3, times ReLU'(conv2)
+        convs.wgrad(2, h1, B, g2, dw2, db2)
         g1 = torch.empty((B, 20, 20, 32), device=dev)
-        native.nature_conv_dgrad(2, g2, B, convs.wpd2, h1, g1)  # dX of conv2, times ReLU'(conv1)
-        native.nature_conv_wgrad(1, x, B, None, 0, 0, 4 * 84 * 84, g1, convs.workspace(1, B), dw1, db1)
+        convs.dgrad(2, g2, B, h1, g1)                           # dX of conv2, times ReLU'(conv1)
+        convs.wgrad(1, x, B, g1, dw1, db1)
         return None, None, dw1, db1, dw2, db2, dw3, db3
 
 
 class NatureConvs:
     """Callable conv trunk bound to a CnnActorCritic whose parameters live in a FlatParams."""
 
-    def __init__(self, net, flat):
+    def __init__(self, net, flat, math=None):
         fe = net.feature_extractor
         self.c1, self.c2, self.c3 = fe[0], fe[2], fe[4]
         self.flat = flat
+        self.math = math or default_math()
+        if self.math not in MATHS:
+            raise ValueError(f"math must be one of {MATHS}")
         dev = flat.device
         self.wp1 = torch.empty(256 * 32, device=dev)
         self.wp2 = torch.empty(512 * 64, device=dev)
         self.wp3 = torch.empty(576 * 64, device=dev)
         self.wpd2 = torch.empty(4 * 256 * 32, device=dev)
         self.wpd3 = torch.empty(576 * 64, device=dev)
+        # split-bf16 planes (int16 storage), packed by ppox_nature_pack_split
+        self.q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device=dev)
+                  for k in (1, 2, 3, 12, 13)}
         self._ws = {}
         self._version = None
+
+    def uses_split(self, op, layer):
+        return self.math == "split" and (op, layer) in SPLIT_OPS
 
     def workspace(self, layer, batch):
         need = native.nature_wgrad_workspace_bytes(layer, batch)
@@ -80,12 +109,31 @@ class NatureConvs:
     def pack(self):
         v = (self.flat.step_count, self.flat.data.data_ptr())
         if v != self._version:
-            native.nature_pack_weights(self.c1.weight, self.c2.weight, self.c3.weight, self.wp1, self.wp2, self.wp3,
-                                       self.wpd2, self.wpd3)
+            w1, w2, w3 = self.c1.weight, self.c2.weight, self.c3.weight
+            native.nature_pack_weights(w1, w2, w3, self.wp1, self.wp2, self.wp3, self.wpd2, self.wpd3)
+            if self.math == "split":
+                q = self.q
+                native.nature_pack_split(w1, w2, w3, q[1], q[2], q[3], q[12], q[13])
             self._version = v
 
     def invalidate(self):
         self._version = None
+
+    # -- per-op dispatch (layer 1 input: uint8 frames, sample stride 4*84*84 bytes)
+    def fwd(self, layer, x, B, bias, y):
+        stride = 4 * 84 * 84 if layer == 1 else 0
+        if self.uses_split("fwd", layer):
+            native.nature_conv_fwd_split(layer, x, B, None, 0, 0, stride, self.q[layer], bias, y)
+        else:
+            wp = (self.wp1, self.wp2, self.wp3)[layer - 1]
+            native.nature_conv_fwd(layer, x, B, None, 0, 0, stride, wp, bias, y)
+
+    def dgrad(self, layer, g, B, prev_act, out):
+        native.nature_conv_dgrad(layer, g, B, self.wpd2 if layer == 2 else self.wpd3, prev_act, out)
+
+    def wgrad(self, layer, x, B, g, dw, db):
+        stride = 4 * 84 * 84 if layer == 1 else 0
+        native.nature_conv_wgrad(layer, x, B, None, 0, 0, stride, g, self.workspace(layer, B), dw, db)
 
     def __call__(self, x):
         if x.dtype != torch.uint8:
@@ -95,7 +143,7 @@ class NatureConvs:
                                   self.c3.weight, self.c3.bias)
 
 
-def attach(net, flat):
+def attach(net, flat, math=None):
     """Route a CnnActorCritic's convolutions through libppox."""
-    net.conv_impl = NatureConvs(net, flat)
+    net.conv_impl = NatureConvs(net, flat, math)
     return net.conv_impl

@@ -1,0 +1,238 @@
+// K6, split-bf16 form — the NatureCNN convolutions on the bf16 matrix cores with
+// fp32-class accuracy (v_mfma_f32_32x32x16_bf16 runs 16x the f32-input MFMA rate).
+//
+// Every f32 operand is split EXACTLY into three bf16 planes by truncation:
+//   a0 = hi16(a), a1 = hi16(a - a0), a2 = a - a0 - a1   (a == a0 + a1 + a2, bitwise)
+// so every bf16 x bf16 product below is exact in f32.  A product a*b is then
+//   a0b0 + (a0b1 + a1b0) + (a0b2 + a1b1 + a2b0)       [+ a1b2 + a2b1 + a2b2 dropped]
+// whose dropped terms are < 3 * 2^-22 |ab| — one f32 rounding's worth.  The a0b0
+// terms accumulate in their own f32 accumulator, the small terms in a second
+// one, and the two are added once in the epilogue.  conv1's input is a uint8
+// frame (0..255): exact in ONE bf16 plane, so conv1 fwd/wgrad need only three
+// products (x*w0 + x*w1 + x*w2), each exact.  Accuracy is therefore that of an
+// f32 FMA chain up to summation order (tests: tests/test_kernels_gpu.py, split
+// vs f32 MFMA vs fp64).  Same layers, layouts and fused epilogues as conv.hip.
+#include <algorithm>
+
+#include "conv_common.h"
+
+namespace {
+
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+
+__device__ inline f32x16 mfma_bf16(const u32x4& a, const u32x4& b, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
+
+// two f32 whose low 16 bits are zero (exact bf16 values) -> packed bf16x2 (e0 low)
+__device__ inline uint32_t pack_hi(float e0, float e1) {
+    return __builtin_amdgcn_perm(__float_as_uint(e1), __float_as_uint(e0), 0x07060302);
+}
+
+// eight uint8 (two words) -> a bf16x8 fragment (exact: 0..255 have <= 8 significant bits)
+__device__ inline u32x4 u8x8_to_bf16(uint32_t w0, uint32_t w1) {
+    u32x4 r;
+    r[0] = pack_hi((float)(w0 & 0xFFu), (float)((w0 >> 8) & 0xFFu));
+    r[1] = pack_hi((float)((w0 >> 16) & 0xFFu), (float)(w0 >> 24));
+    r[2] = pack_hi((float)(w1 & 0xFFu), (float)((w1 >> 8) & 0xFFu));
+    r[3] = pack_hi((float)((w1 >> 16) & 0xFFu), (float)(w1 >> 24));
+    return r;
+}
+
+// exact three-way truncation split of one f32 (host+device; used by the packers)
+__host__ __device__ inline void split3(float a, uint16_t& p0, uint16_t& p1, uint16_t& p2) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, a);
+    const float a0 = __builtin_bit_cast(float, u & 0xFFFF0000u);
+    const float r1 = a - a0;
+    const uint32_t v = __builtin_bit_cast(uint32_t, r1);
+    const float a1 = __builtin_bit_cast(float, v & 0xFFFF0000u);
+    const float r2 = r1 - a1;
+    p0 = (uint16_t)(u >> 16);
+    p1 = (uint16_t)(v >> 16);
+    p2 = (uint16_t)(__builtin_bit_cast(uint32_t, r2) >> 16);
+}
+
+// ---------------------------------------------------------------------------
+// conv1 forward, register-direct: each wave owns 32*MT output pixels x 32
+// channels, no LDS.  K chunk c (32 values) = input channel c/2, kernel rows
+// 4(c&1)..+3.  A lane of half h loads two 8-byte runs (kernel rows 4(c&1)+2h
+// and +1); MFMA step s of the chunk takes the run of row 4(c&1)+2h+s, so the
+// MFMA k index (s, h, e) is natural k = (c/2)*64 + (4(c&1) + 2h + s)*8 + e.
+// The weights are packed in that order, plane by plane (pack_fwd1_split).
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int fwd1_split_index(int c, int s, int p, int lane, int e) {
+    return (((c * 2 + s) * 3 + p) * 64 + lane) * 8 + e;
+}
+
+// Persistent: the whole split weight set (48 KB) is staged in LDS once per
+// workgroup (B fragments then cost LDS, not TA, bandwidth), and each wave walks
+// a contiguous range of row tiles.  The kernel is load-latency bound, so the
+// input of the NEXT tile (all 8 chunks, 16*MT dwords per lane) is loaded while
+// the current tile runs its 48*MT MFMAs.  Workgroups with adjacent row ranges
+// share an XCD (xcd_remap): the overlapping input windows of one frame stack
+// are read through one L2.
+template <int MT>
+__global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a, unsigned tiles_per_wave) {
+    using L = G1;
+    constexpr int NCH = L::K / 32, NQ = NCH * 6;
+    __shared__ u32x4 Wl[NQ * 64];
+    {
+        const u32x4* wq = reinterpret_cast<const u32x4*>(a.wp);
+        for (int i = threadIdx.x; i < NQ * 64; i += 256) Wl[i] = wq[i];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned M = (unsigned)(a.batch * L::P);
+    const unsigned ntile = (M + 32 * MT - 1) / (32 * MT);
+    const unsigned wid = (unsigned)xcd_remap(blockIdx.x, gridDim.x) * 4 + wave;
+    const unsigned t_begin = wid * tiles_per_wave;
+    const unsigned t_end = min(ntile, t_begin + tiles_per_wave);
+    if (t_begin >= t_end) return;  // wave-uniform; nothing below synchronises
+    const uint8_t* x = reinterpret_cast<const uint8_t*>(a.x);
+    const u32x4* Wlane = Wl + lane;
+
+    // the whole K extent of a tile: per row slot i and chunk c, two 8-byte runs
+    using Raw = uint32_t[MT][NCH][4];
+    auto load_tile = [&](unsigned tile, Raw& r) {
+        const unsigned m0 = tile * 32 * MT;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            unsigned m = m0 + i * 32 + (lane & 31);
+            m = m < M ? m : m0;  // clamped rows are computed but never stored
+            const unsigned n = m / L::P, p = m - n * L::P, oy = p / L::OW, ox = p % L::OW;
+            const uint8_t* b = x + u8_sample_base(a, n, (long long)L::CIN * L::IH * L::IW) +
+                               (oy * L::S + (lane >> 5) * 2) * L::IW + ox * L::S;
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                const uint8_t* q = b + (c >> 1) * (L::IH * L::IW) + (c & 1) * 4 * L::IW;
+                const uint2 v0 = *reinterpret_cast<const uint2*>(q);
+                const uint2 v1 = *reinterpret_cast<const uint2*>(q + L::IW);
+                r[i][c][0] = v0.x;
+                r[i][c][1] = v0.y;
+                r[i][c][2] = v1.x;
+                r[i][c][3] = v1.y;
+            }
+        }
+    };
+    const int co = lane & 31;
+    const float bias = a.bias[co];
+    auto run_tile = [&](unsigned tile, const Raw& r) {
+        f32x16 hi[MT], lo[MT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) hi[i] = lo[i] = zero16();
+        // B fragments are read from LDS one (chunk, step) ahead of their MFMAs
+        u32x4 rb[2][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) rb[0][p] = Wlane[p * 64];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int q = c * 2 + s, cur = q & 1;
+                if (q + 1 < 2 * NCH) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) rb[cur ^ 1][p] = Wlane[((q + 1) * 3 + p) * 64];
+                }
+#pragma unroll
+                for (int i = 0; i < MT; ++i) {
+                    const u32x4 av = u8x8_to_bf16(r[i][c][2 * s], r[i][c][2 * s + 1]);
+                    hi[i] = mfma_bf16(av, rb[cur][0], hi[i]);
+                    lo[i] = mfma_bf16(av, rb[cur][1], lo[i]);
+                    lo[i] = mfma_bf16(av, rb[cur][2], lo[i]);
+                }
+                // keep the scheduler from hoisting every chunk's LDS reads (192 VGPRs)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        const unsigned m0 = tile * 32 * MT;
+        // C/D map: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const unsigned m = m0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+                if (m < M) a.y[(long long)m * L::COUT + co] = fmaxf((hi[i][e] + lo[i][e]) + bias, 0.f);
+            }
+    };
+    Raw r0, r1;
+    load_tile(t_begin, r0);
+#pragma unroll 1
+    for (unsigned tile = t_begin; tile < t_end; tile += 2) {
+        if (tile + 1 < t_end) load_tile(tile + 1, r1);
+        run_tile(tile, r0);
+        if (tile + 1 >= t_end) break;
+        if (tile + 2 < t_end) load_tile(tile + 2, r0);
+        run_tile(tile + 1, r1);
+    }
+}
+
+// [co][ci][ky][kx] f32 -> conv1 split planes in fwd1_split_index order
+__global__ void pack_fwd1_split(const float* __restrict__ w, uint16_t* __restrict__ q) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;  // (c, s, lane, e)
+    if (t >= 8 * 2 * 64 * 8) return;
+    const int e = t & 7, lane = (t >> 3) & 63, s = (t >> 9) & 1, c = t >> 10;
+    const int h = lane >> 5, co = lane & 31;
+    const int k = (c >> 1) * 64 + (4 * (c & 1) + 2 * h + s) * 8 + e;  // natural (ci, ky, kx)
+    uint16_t p0, p1, p2;
+    split3(w[co * G1::K + k], p0, p1, p2);
+    q[fwd1_split_index(c, s, 0, lane, e)] = p0;
+    q[fwd1_split_index(c, s, 1, lane, e)] = p1;
+    q[fwd1_split_index(c, s, 2, lane, e)] = p2;
+}
+
+#ifndef SPLIT_FWD1_MT
+#define SPLIT_FWD1_MT 1
+#endif
+// waves the persistent kernel spreads its tiles over: 256 CUs x resident waves per CU
+// (LDS: 3 workgroups of 48 KB at MT = 1; VGPRs: 2 at MT = 2)
+#ifndef SPLIT_RESIDENT_WAVES
+#define SPLIT_RESIDENT_WAVES (SPLIT_FWD1_MT == 1 ? 3072 : 2048)
+#endif
+
+}  // namespace
+
+extern "C" int64_t ppox_nature_split_pack_elems(int32_t which) {
+    switch (which) {
+        case 1: return 3LL * G1::K * G1::COUT;
+        case 2: return 3LL * G2::K * G2::COUT;
+        case 3: return 3LL * G3::K * G3::COUT;
+        case 12: return 3LL * G2::K * G2::COUT;
+        case 13: return 3LL * G3::K * G3::COUT;
+        default: return -1;
+    }
+}
+
+extern "C" int ppox_nature_pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1, uint16_t* q2,
+                                      uint16_t* q3, uint16_t* qd2, uint16_t* qd3, void* stream) {
+    PPOX_REQUIRE(w1 && q1, "ppox_nature_pack_split: null pointer");
+    PPOX_REQUIRE(ppox::aligned16(q1) && (!q2 || ppox::aligned16(q2)) && (!q3 || ppox::aligned16(q3)) &&
+                     (!qd2 || ppox::aligned16(qd2)) && (!qd3 || ppox::aligned16(qd3)),
+                 "ppox_nature_pack_split: packed buffers must be 16-byte aligned");
+    (void)w2; (void)w3;
+    hipStream_t s = ppox::as_stream(stream);
+    pack_fwd1_split<<<ppox::ceil_div(8 * 2 * 64 * 8, 256), 256, 0, s>>>(w1, q1);
+    PPOX_LAUNCHED("ppox_nature_pack_split");
+}
+
+extern "C" int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx, int64_t T,
+                                          int64_t N_env, int64_t x_sample_stride, const uint16_t* wq,
+                                          const float* bias, float* y, void* stream) {
+    PPOX_REQUIRE(layer == 1, "ppox_nature_conv_fwd_split: layer must be 1");
+    PPOX_REQUIRE(x && wq && bias && y && batch >= 0, "ppox_nature_conv_fwd_split: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(wq), "ppox_nature_conv_fwd_split: packed weights must be 16-byte aligned");
+    if (batch == 0) return PPOX_OK;
+    PPOX_REQUIRE(batch * G1::P < (1LL << 31), "ppox_nature_conv_fwd_split: batch too large for 32-bit rows");
+    Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride,
+           reinterpret_cast<const float*>(wq), bias, nullptr, y, batch};
+    hipStream_t s = ppox::as_stream(stream);
+    PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && (idx || x_sample_stride % 4 == 0),
+                 "ppox_nature_conv_fwd_split: u8 input must be 4-byte aligned");
+    if (idx) PPOX_REQUIRE(T > 0 && N_env > 0, "ppox_nature_conv_fwd_split: idx needs T and N_env");
+    constexpr int MT = SPLIT_FWD1_MT;
+    const long long ntile = ppox::ceil_div(batch * G1::P, 32 * MT);
+    const long long waves = std::min<long long>(ntile, SPLIT_RESIDENT_WAVES);
+    const unsigned per = ppox::ceil_div(ntile, waves);
+    fwd1_split_kernel<MT><<<ppox::ceil_div(ppox::ceil_div(ntile, per), 4), 256, 0, s>>>(a, per);
+    PPOX_LAUNCHED("ppox_nature_conv_fwd_split");
+}

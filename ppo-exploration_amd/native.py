@@ -55,15 +55,17 @@ SIGNATURES = {
     "ppox_nature_wgrad_reduce": [_i32, _i64, _vp, _vp, _vp, _vp],
     "ppox_nchw_to_nhwc_relu_grad": [_vp, _vp, _i64, _vp, _vp],
     "ppox_nature_conv_fwd": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "ppox_nature_pack_split": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
 }
 _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p,
              "ppox_rms_u8_workspace_bytes": ctypes.c_int64, "ppox_nature_wgrad_splits": ctypes.c_int64,
-             "ppox_nature_wgrad_workspace_bytes": ctypes.c_int64}
+             "ppox_nature_wgrad_workspace_bytes": ctypes.c_int64, "ppox_nature_split_pack_elems": ctypes.c_int64}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
-                 "ppox_nature_wgrad_workspace_bytes": [_i32, _i64]}
+                 "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32]}
 
 _lib = None
 
@@ -124,7 +126,8 @@ def event_times_ms(name):
     return [(a.elapsed_time(b), args) for a, b, args in _events.get(name, [])]
 
 
-_LAYERED = ("ppox_nature_conv_fwd", "ppox_nature_conv_dgrad", "ppox_nature_conv_wgrad")
+_LAYERED = ("ppox_nature_conv_fwd", "ppox_nature_conv_dgrad", "ppox_nature_conv_wgrad",
+            "ppox_nature_conv_fwd_split", "ppox_nature_conv_dgrad_split", "ppox_nature_conv_wgrad_split")
 
 
 def call(name, *args):
@@ -366,3 +369,19 @@ def nchw_to_nhwc_relu_grad(grad, act, batch, out, stream=None):
 def nature_conv_fwd(layer, x, batch, idx, T, N_env, x_sample_stride, wp, bias, y, stream=None):
     call("ppox_nature_conv_fwd", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env), int(x_sample_stride),
          _p(wp), _p(bias), _p(y), stream_ptr(stream))
+
+
+# split-bf16 forms (csrc/conv_split.hip): weights packed as three exact bf16 planes (int16 tensors)
+def nature_split_pack_elems(which):
+    """bf16 elements of the split-packed buffer: which = 1, 2, 3 (forward) or 12, 13 (dgrad of conv2/3)."""
+    return int(load().ppox_nature_split_pack_elems(int(which)))
+
+
+def nature_pack_split(w1, w2, w3, q1, q2, q3, qd2=None, qd3=None, stream=None):
+    call("ppox_nature_pack_split", _p(w1), _p(w2), _p(w3), _p(q1), _p(q2), _p(q3), _p(qd2), _p(qd3),
+         stream_ptr(stream))
+
+
+def nature_conv_fwd_split(layer, x, batch, idx, T, N_env, x_sample_stride, wq, bias, y, stream=None):
+    call("ppox_nature_conv_fwd_split", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
+         int(x_sample_stride), _p(wq), _p(bias), _p(y), stream_ptr(stream))

@@ -394,8 +394,9 @@ def test_adam_clip_vs_torch(max_norm):
 
 
 # ----------------------------------------------------------------- K6 convs
+@pytest.mark.parametrize("math", ["split", "f32"])
 @pytest.mark.parametrize("B", [1, 3, 37, 256])
-def test_nature_conv_fwd_vs_torch_fp32(B):
+def test_nature_conv_fwd_vs_torch_fp32(B, math):
     """MFMA implicit-GEMM conv trunk vs torch fp32 convs (tolerance: fp32 re-association)."""
     import models
     import convs
@@ -405,7 +406,7 @@ def test_nature_conv_fwd_vs_torch_fp32(B):
     ref.load_state_dict(net.state_dict())
     flat = models.FlatParams(net, "cuda")
     ref = ref.cuda()
-    convs.attach(net, flat)
+    convs.attach(net, flat, math)
     x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda")
     with torch.no_grad():
         h = net.conv_impl(x)
@@ -415,7 +416,8 @@ def test_nature_conv_fwd_vs_torch_fp32(B):
     assert err <= 2e-5 * e.abs().max().item() + 1e-4, err
 
 
-def test_nature_trunk_backward_vs_torch():
+@pytest.mark.parametrize("math", ["split", "f32"])
+def test_nature_trunk_backward_vs_torch(math):
     import models
     import convs
     torch.manual_seed(0)
@@ -424,7 +426,7 @@ def test_nature_trunk_backward_vs_torch():
     ref.load_state_dict(net.state_dict())
     flat = models.FlatParams(net, "cuda")
     ref = ref.cuda()
-    convs.attach(net, flat)
+    convs.attach(net, flat, math)
     x = torch.randint(0, 256, (50, 4, 84, 84), dtype=torch.uint8, device="cuda")
     g = torch.randn(50, 64, 7, 7, device="cuda")
     flat.zero_grad()
@@ -436,3 +438,54 @@ def test_nature_trunk_backward_vs_torch():
         for a, b in ((theirs.weight.grad, mine.weight.grad), (theirs.bias.grad, mine.bias.grad)):
             scale = b.abs().max().item()
             assert (a - b).abs().max().item() <= 1e-4 * scale + 1e-6
+
+
+def _conv_ops_fp64(B, seed):
+    """Every NatureCNN conv op (fwd, dgrad, wgrad per layer) through both math modes
+    and float64 CPU autograd on the same inputs: {(op, layer): (split, f32, fp64)}."""
+    import models
+    import convs
+    torch.manual_seed(seed)
+    net = models.CnnActorCritic(4, 4)
+    flat = models.FlatParams(net, "cuda")
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    out = {}
+    for math in ("split", "f32"):
+        net.conv_impl = None
+        cv = convs.attach(net, flat, math)
+        hs = {}
+        cv.pack()
+        h1 = torch.empty(B, 20, 20, 32, device="cuda")
+        h2 = torch.empty(B, 9, 9, 64, device="cuda")
+        h3 = torch.empty(B, 64, 7, 7, device="cuda")
+        cv.fwd(1, x, B, cv.c1.bias, h1)
+        cv.fwd(2, h1, B, cv.c2.bias, h2)
+        cv.fwd(3, h2, B, cv.c3.bias, h3)
+        hs.update({("fwd", 1): h1, ("fwd", 2): h2, ("fwd", 3): h3})
+        out[math] = hs
+    # fp64 reference (CPU autograd, same weights)
+    fe = net.feature_extractor
+    w = [fe[i].weight.detach().double().cpu() for i in (0, 2, 4)]
+    b = [fe[i].bias.detach().double().cpu() for i in (0, 2, 4)]
+    F = torch.nn.functional
+    r1 = F.relu(F.conv2d(x.double().cpu(), w[0], b[0], stride=4))
+    r2 = F.relu(F.conv2d(r1, w[1], b[1], stride=2))
+    r3 = F.relu(F.conv2d(r2, w[2], b[2], stride=1))
+    ref = {("fwd", 1): r1.permute(0, 2, 3, 1), ("fwd", 2): r2.permute(0, 2, 3, 1), ("fwd", 3): r3}
+    return {k: (out["split"][k], out["f32"][k], ref[k]) for k in ref}
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_split_conv_accuracy_is_fp32_class(seed):
+    """Split-bf16 kernels vs fp64: error no larger than the exact-f32-FMA kernels' own error
+    (x2 headroom), for every op that has a split kernel.  Forward ops take each layer's
+    input from the same mode, so errors compound as in the product path."""
+    import convs
+    res = _conv_ops_fp64(24, seed)
+    for key, (spl, f32, ref) in res.items():
+        if key not in convs.SPLIT_OPS:
+            continue
+        scale = ref.abs().max().item()
+        e_s = (spl.cpu().double() - ref).abs().max().item() / scale
+        e_f = (f32.cpu().double() - ref).abs().max().item() / scale
+        assert e_s <= 2 * e_f + 1e-7, (key, e_s, e_f)
