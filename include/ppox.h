@@ -273,6 +273,10 @@ int ppox_nature_pack_split(const float* w1, const float* w2, const float* w3, ui
 int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
                                int64_t T, int64_t N_env, int64_t x_sample_stride,
                                const uint16_t* wq, const float* bias, float* y, void* stream);
+/* layers 2/3: LDS-staged implicit GEMM; every activation fragment split in registers. */
+int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch,
+                                 const uint16_t* wqd, const float* prev_act, float* grad_in,
+                                 void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,8 @@ Math modes (PPOX_CONV_MATH, default "split"):
             cores (csrc/conv_split.hip): fp32-class accuracy (measured below the
             f32-MFMA kernels' error vs fp64, tools/split_probe.py) at up to 16x
             the f32-input MFMA rate.  Ops without a split kernel yet use "f32".
+  "split_all" — every op that has a split kernel, including those measured slower
+            than their f32 kernel at the training batch (SPLIT_SLOWER; tests).
   "f32"   — v_mfma_f32_32x32x2_f32: every product an exact f32 FMA (csrc/conv.hip).
 """
 import os
@@ -20,9 +22,12 @@ import torch
 
 import native
 
-MATHS = ("split", "f32")
+MATHS = ("split", "split_all", "f32")
 # ops that have a split-bf16 kernel: ("fwd" | "dgrad" | "wgrad", layer)
-SPLIT_OPS = {("fwd", 1)}
+SPLIT_OPS = {("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 3)}
+# ops whose split kernel exists but is not faster than the f32 one at the training batch
+# (measured, tools/conv_bench.py); "split" mode runs them in f32
+SPLIT_SLOWER = {("dgrad", 2)}
 
 
 def default_math():
@@ -96,6 +101,8 @@ class NatureConvs:
         self._version = None
 
     def uses_split(self, op, layer):
+        if self.math == "split_all":  # every op that has a split kernel (tests, benchmarks)
+            return (op, layer) in SPLIT_OPS or (op, layer) in SPLIT_SLOWER
         return self.math == "split" and (op, layer) in SPLIT_OPS
 
     def workspace(self, layer, batch):
@@ -111,7 +118,7 @@ class NatureConvs:
         if v != self._version:
             w1, w2, w3 = self.c1.weight, self.c2.weight, self.c3.weight
             native.nature_pack_weights(w1, w2, w3, self.wp1, self.wp2, self.wp3, self.wpd2, self.wpd3)
-            if self.math == "split":
+            if self.math != "f32":
                 q = self.q
                 native.nature_pack_split(w1, w2, w3, q[1], q[2], q[3], q[12], q[13])
             self._version = v
@@ -129,7 +136,10 @@ class NatureConvs:
             native.nature_conv_fwd(layer, x, B, None, 0, 0, stride, wp, bias, y)
 
     def dgrad(self, layer, g, B, prev_act, out):
-        native.nature_conv_dgrad(layer, g, B, self.wpd2 if layer == 2 else self.wpd3, prev_act, out)
+        if self.uses_split("dgrad", layer):
+            native.nature_conv_dgrad_split(layer, g, B, self.q[10 + layer], prev_act, out)
+        else:
+            native.nature_conv_dgrad(layer, g, B, self.wpd2 if layer == 2 else self.wpd3, prev_act, out)
 
     def wgrad(self, layer, x, B, g, dw, db):
         stride = 4 * 84 * 84 if layer == 1 else 0

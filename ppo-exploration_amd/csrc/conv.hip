@@ -141,12 +141,9 @@ struct StageFwdNHWC {
         constexpr int CPT = L::CIN / BK;
         const int tap = chunk / CPT, ky = tap / L::KW, kx = tap % L::KW;
         const int off = (ky * L::IW + kx) * L::CIN + (chunk % CPT) * BK;
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        // rows past the end read a clamped valid row; their C rows are never stored
 #pragma unroll
-        for (int i = 0; i < SL; ++i) {
-            const float4 v = *reinterpret_cast<const float4*>(base[i] + off);
-            r[i] = ok[i] ? v : z;
-        }
+        for (int i = 0; i < SL; ++i) r[i] = *reinterpret_cast<const float4*>(base[i] + off);
     }
     __device__ inline void store(float* As) const { store_rows_f4<SL>(As, r); }
 };
@@ -180,6 +177,7 @@ struct FwdBase {
     }
     __device__ static int nchunk(const Tile&) { return L::K / BK; }
     __device__ static const float* bchunk(const Args& a, const Tile&, int c) { return a.wp + (long long)c * BK * NOUT; }
+    __device__ static int bchunk_id(const Tile&, int c) { return c; }  // 32-row block of the packed [K][NOUT]
     __device__ static float prefetch(const Args& a, const Tile&, int, int co) { return a.bias[co]; }
     __device__ static void store_pre(const Args& a, const Tile& t, int row, int co, float acc, float bias) {
         const long long m = t.m0 + row;
@@ -239,12 +237,9 @@ struct StageDgradPM {
         const int tap = chunk / CPT, ty = tap / nx, tx = tap - ty * nx;
         const int oy = (iy - ky0) / L::S - ty, ox = (ix - kx0) / L::S - tx;
         const int off = (oy * L::OW + ox) * L::COUT + (chunk % CPT) * BK;
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        // rows past the end read a clamped valid row; their C rows are never stored
 #pragma unroll
-        for (int i = 0; i < SL; ++i) {
-            const float4 v = *reinterpret_cast<const float4*>(base[i] + off);
-            r[i] = ok[i] ? v : z;
-        }
+        for (int i = 0; i < SL; ++i) r[i] = *reinterpret_cast<const float4*>(base[i] + off);
     }
     __device__ inline void store(float* As) const { store_rows_f4<SL>(As, r); }
 };
@@ -272,6 +267,10 @@ struct DgradPMProblem {
         const int tap = c / CPT, ty = tap / t.nx, tx = tap - ty * t.nx;
         const int ky = t.ky0 + L::S * ty, kx = t.kx0 + L::S * tx;
         return a.wp + ((long long)(ky * L::KW + kx) * L::COUT + (c % CPT) * BK) * L::CIN;
+    }
+    __device__ static int bchunk_id(const Tile& t, int c) {
+        const int tap = c / CPT, ty = tap / t.nx, tx = tap - ty * t.nx;
+        return ((t.ky0 + L::S * ty) * L::KW + t.kx0 + L::S * tx) * CPT + c % CPT;
     }
     // the epilogue's ReLU-mask values are loaded before the K walk (their latency
     // hides under it) — 16 per lane per column tile, in the C/D layout
@@ -366,6 +365,151 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(Args a) {
                 Prob::store_pre(a, t, wave * 32 * MT + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), col,
                                 acc[i][j][r], pre[i][j][r]);
         }
+}
+
+
+// ---------------------------------------------------------------------------
+// Split-bf16 form of igemm_kernel (same Problems: tiles, K walk, fused epilogues)
+// on v_mfma_f32_32x32x16_bf16.  A chunk (128 rows x 32 f32) is staged in LDS as
+// f32 (rows of 36 floats: 16-B aligned, conflict-free b128 row reads); each wave
+// reads its rows' 8-value fragments and splits them into three exact bf16 planes
+// in registers (every A value is read by exactly one wave, so the split costs the
+// same as splitting at the store).  B chunks come pre-split and pre-packed in
+// fragment order (split_frag_index) and are staged in LDS.  Per 16-k step and
+// column tile: six MFMAs (mfma_split6), a0*b0 into hi, the rest into lo.
+// ---------------------------------------------------------------------------
+constexpr int SAST = 36;
+
+// packed position of natural element (row k, col) of a [K][nout] matrix, plane p:
+// chunk (k / 32) x k-step s x column tile j x plane x lane (h, col & 31) x e
+__host__ __device__ constexpr long long split_frag_index(int k, int col, int nout, int p) {
+    const int ch = k >> 5, kl = k & 31, s = kl >> 4, h = (kl >> 3) & 1, e = kl & 7;
+    const int nt = nout / 32, j = col >> 5, l = h * 32 + (col & 31);
+    return ((((long long)(ch * 2 + s) * nt + j) * 3 + p) * 64 + l) * 8 + e;
+}
+
+template <class Prob>
+__global__ void __launch_bounds__(256, 2) igemm_split_kernel(Args a, const u32x4* __restrict__ wq) {
+    constexpr int NOUT = Prob::NOUT, NT = NOUT / 32, BMR = 128;
+    static_assert(Prob::MT == 1, "split igemm: 32 rows per wave");
+    constexpr int BQ = 2 * NT * 3 * 64;  // u32x4 per B chunk
+    constexpr int BV = (BQ + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float As[2][BMR * SAST];
+    __shared__ u32x4 Bs[2][BQ];
+    typename Prob::Tile t;
+    if (!Prob::tile(a, t)) return;
+    const int nchunk = Prob::nchunk(t);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+    f32x16 hi[NT], lo[NT], pre[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        hi[j] = lo[j] = zero16();
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            pre[j][r] = Prob::prefetch(a, t, wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), j * 32 + (lane & 31));
+    }
+    typename Prob::Stager sa(a, t);
+    static_assert(decltype(sa)::SL == 4, "four float4 slots per thread");
+    // three-stage pipeline: chunk c in LDS buffer c&1, chunk c+1 held in registers
+    // (pa, pb), chunk c+2's loads in flight while chunk c runs on the matrix cores
+    auto loadB = [&](int c, u32x4 (&br)[BV]) {
+        const u32x4* src = wq + (long long)Prob::bchunk_id(t, c) * BQ;
+#pragma unroll
+        for (int i = 0; i < BV; ++i)
+            if (i * 256 + (int)threadIdx.x < BQ) br[i] = src[i * 256 + threadIdx.x];
+    };
+    auto store = [&](int buf, const float4 (&ar)[4], const u32x4 (&br)[BV]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int w = i * 256 + threadIdx.x;
+            *reinterpret_cast<float4*>(As[buf] + (w >> 3) * SAST + (w & 7) * 4) = ar[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BV; ++i)
+            if (i * 256 + (int)threadIdx.x < BQ) Bs[buf][i * 256 + threadIdx.x] = br[i];
+    };
+    float4 pa[4];
+    u32x4 pb[BV], nb[BV];
+    if (nchunk > 0) {
+        sa.load(0);
+        loadB(0, pb);
+        store(0, sa.r, pb);
+    }
+    if (nchunk > 1) {
+        sa.load(1);
+        loadB(1, pb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pa[i] = sa.r[i];
+    }
+    __syncthreads();
+    const int aoff = (wave * 32 + (lane & 31)) * SAST + (lane >> 5) * 8;
+    for (int c = 0; c < nchunk; ++c) {
+        const int cur = c & 1;
+        if (c + 2 < nchunk) {
+            sa.load(c + 2);
+            loadB(c + 2, nb);
+        }
+        const float* A = As[cur] + aoff;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            u32x4 af[3];
+            split8(*reinterpret_cast<const float4*>(A + 16 * s), *reinterpret_cast<const float4*>(A + 16 * s + 4), af[0],
+                   af[1], af[2]);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const u32x4* B = Bs[cur] + ((s * NT + j) * 3) * 64 + lane;
+                const u32x4 bf[3] = {B[0], B[64], B[128]};
+                mfma_split6(af, bf, hi[j], lo[j]);
+            }
+        }
+        if (c + 1 < nchunk) store(cur ^ 1, pa, pb);
+        if (c + 2 < nchunk) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pa[i] = sa.r[i];
+#pragma unroll
+            for (int i = 0; i < BV; ++i) pb[i] = nb[i];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            Prob::store_pre(a, t, wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), j * 32 + (lane & 31),
+                            hi[j][r] + lo[j][r], pre[j][r]);
+}
+
+// split-pack: forward [K][COUT] (NHWC K order) / dgrad [(tap, co)][ci] of layer L,
+// from the PyTorch [co][ci][ky][kx] weights, into split_frag_index order
+template <class L, bool DGRAD>
+__global__ void pack_split_gemm(const float* __restrict__ w, uint16_t* __restrict__ q) {
+    constexpr int NOUT = DGRAD ? L::CIN : L::COUT;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L::K * L::COUT) return;
+    const int k = i / NOUT, col = i % NOUT;
+    int co, ci, tap;
+    if (DGRAD) {
+        ci = col;
+        co = k % L::COUT;
+        tap = k / L::COUT;
+    } else {
+        co = col;
+        ci = k % L::CIN;
+        tap = k / L::CIN;
+    }
+    uint16_t p0, p1, p2;
+    split3(w[((co * L::CIN + ci) * L::KH + tap / L::KW) * L::KW + tap % L::KW], p0, p1, p2);
+    q[split_frag_index(k, col, NOUT, 0)] = p0;
+    q[split_frag_index(k, col, NOUT, 1)] = p1;
+    q[split_frag_index(k, col, NOUT, 2)] = p2;
+}
+
+template <class Prob>
+int launch_igemm_split(const Args& a, const uint16_t* wq, long long blocks, hipStream_t s, const char* name) {
+    if (blocks == 0) return PPOX_OK;
+    igemm_split_kernel<Prob><<<(unsigned)blocks, 256, 0, s>>>(a, reinterpret_cast<const u32x4*>(wq));
+    PPOX_LAUNCHED(name);
 }
 
 // ---------------------------------------------------------------------------
@@ -1103,4 +1247,45 @@ extern "C" int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, 
     if (batch == 0) return PPOX_OK;
     nchw_to_nhwc_mask<<<(unsigned)batch, 256, 0, ppox::as_stream(stream)>>>(grad, act, batch, out);
     PPOX_LAUNCHED("ppox_nchw_to_nhwc_relu_grad");
+}
+
+namespace ppox_conv {
+// split-bf16 layers 2/3 (called from conv_split.hip's entry points)
+int split_pack23(const float* w2, const float* w3, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
+                 hipStream_t s) {
+    if (q2) pack_split_gemm<G2, false><<<ppox::ceil_div(G2::K * G2::COUT, 256), 256, 0, s>>>(w2, q2);
+    if (q3) pack_split_gemm<G3, false><<<ppox::ceil_div(G3::K * G3::COUT, 256), 256, 0, s>>>(w3, q3);
+    if (qd2) pack_split_gemm<G2, true><<<ppox::ceil_div(G2::K * G2::COUT, 256), 256, 0, s>>>(w2, qd2);
+    if (qd3) pack_split_gemm<G3, true><<<ppox::ceil_div(G3::K * G3::COUT, 256), 256, 0, s>>>(w3, qd3);
+    PPOX_LAUNCHED("ppox_nature_pack_split");
+}
+
+int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq, const float* bias, float* y,
+                hipStream_t s) {
+    PPOX_REQUIRE(ppox::aligned16(x), "ppox_nature_conv_fwd_split: layer 2/3 input must be 16B-aligned NHWC");
+    Args a{x, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch};
+    if (layer == 2) {
+        using P2 = FwdNHWCProblem<G2, false, 1>;
+        return launch_igemm_split<P2>(a, wq, ppox::ceil_div(batch * G2::P, P2::BMR), s, "ppox_nature_conv_fwd_split");
+    }
+    using P3 = FwdNHWCProblem<G3, true, 1>;
+    return launch_igemm_split<P3>(a, wq, ppox::ceil_div(batch * G3::P, P3::BMR), s, "ppox_nature_conv_fwd_split");
+}
+}  // namespace ppox_conv
+
+extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch, const uint16_t* wqd,
+                                            const float* prev_act, float* grad_in, void* stream) {
+    PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad_split: layer must be 2 or 3");
+    PPOX_REQUIRE(grad_out && wqd && prev_act && grad_in && batch >= 0, "ppox_nature_conv_dgrad_split: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wqd), "ppox_nature_conv_dgrad_split: 16B alignment");
+    if (batch == 0) return PPOX_OK;
+    Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch};
+    hipStream_t s = ppox::as_stream(stream);
+    if (layer == 2) {
+        using D2 = DgradPMProblem<G2, 1>;
+        return launch_igemm_split<D2>(a, wqd, ppox::ceil_div(batch, D2::BMR) * D2::NPOS, s,
+                                      "ppox_nature_conv_dgrad_split");
+    }
+    using D3 = DgradPMProblem<G3, 1>;
+    return launch_igemm_split<D3>(a, wqd, ppox::ceil_div(batch, D3::BMR) * D3::NPOS, s, "ppox_nature_conv_dgrad_split");
 }

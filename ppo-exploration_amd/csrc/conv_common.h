@@ -59,6 +59,77 @@ __device__ inline void tap_range(int i, int& k0, int& cnt) {
     cnt = hi >= k0 ? (hi - k0) / S + 1 : 0;
 }
 
+// ---- split-bf16 helpers (conv_split.hip and the split kernels of conv.hip) ----
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+
+__device__ inline f32x16 mfma_bf16(const u32x4& a, const u32x4& b, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
+
+// two f32 whose low 16 bits are zero (exact bf16 values) -> packed bf16x2 (e0 low)
+__device__ inline uint32_t pack_hi(float e0, float e1) {
+    return __builtin_amdgcn_perm(__float_as_uint(e1), __float_as_uint(e0), 0x07060302);
+}
+
+// eight uint8 (two words) -> a bf16x8 fragment (exact: 0..255 have <= 8 significant bits)
+__device__ inline u32x4 u8x8_to_bf16(uint32_t w0, uint32_t w1) {
+    u32x4 r;
+    r[0] = pack_hi((float)(w0 & 0xFFu), (float)((w0 >> 8) & 0xFFu));
+    r[1] = pack_hi((float)((w0 >> 16) & 0xFFu), (float)(w0 >> 24));
+    r[2] = pack_hi((float)(w1 & 0xFFu), (float)((w1 >> 8) & 0xFFu));
+    r[3] = pack_hi((float)((w1 >> 16) & 0xFFu), (float)(w1 >> 24));
+    return r;
+}
+
+// exact three-way truncation split of one f32 (host+device; used by the packers)
+__host__ __device__ inline void split3(float a, uint16_t& p0, uint16_t& p1, uint16_t& p2) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, a);
+    const float a0 = __builtin_bit_cast(float, u & 0xFFFF0000u);
+    const float r1 = a - a0;
+    const uint32_t v = __builtin_bit_cast(uint32_t, r1);
+    const float a1 = __builtin_bit_cast(float, v & 0xFFFF0000u);
+    const float r2 = r1 - a1;
+    p0 = (uint16_t)(u >> 16);
+    p1 = (uint16_t)(v >> 16);
+    p2 = (uint16_t)(__builtin_bit_cast(uint32_t, r2) >> 16);
+}
+
+// eight f32 -> their three exact bf16 planes as MFMA fragments (element e of the
+// fragment = value e): a = a0 + a1 + a2 bitwise (see conv_split.hip)
+__device__ inline void split8(const float4& v0, const float4& v1, u32x4& p0, u32x4& p1, u32x4& p2) {
+    const float x[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    uint32_t h0[8], h1[8], h2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const uint32_t u0 = __float_as_uint(x[e]) & 0xFFFF0000u;
+        const float r1 = x[e] - __uint_as_float(u0);
+        const uint32_t u1 = __float_as_uint(r1) & 0xFFFF0000u;
+        const float r2 = r1 - __uint_as_float(u1);
+        h0[e] = u0;
+        h1[e] = u1;
+        h2[e] = __float_as_uint(r2);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        p0[q] = __builtin_amdgcn_perm(h0[2 * q + 1], h0[2 * q], 0x07060302);
+        p1[q] = __builtin_amdgcn_perm(h1[2 * q + 1], h1[2 * q], 0x07060302);
+        p2[q] = __builtin_amdgcn_perm(h2[2 * q + 1], h2[2 * q], 0x07060302);
+    }
+}
+
+// a*b on split operands: the six products a_i*b_j with i + j <= 2; a0*b0 into hi,
+// the rest into lo (both f32 accumulators; the result is hi + lo)
+__device__ inline void mfma_split6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16& hi, f32x16& lo) {
+    hi = mfma_bf16(a[0], b[0], hi);
+    lo = mfma_bf16(a[0], b[1], lo);
+    lo = mfma_bf16(a[1], b[0], lo);
+    lo = mfma_bf16(a[0], b[2], lo);
+    lo = mfma_bf16(a[1], b[1], lo);
+    lo = mfma_bf16(a[2], b[0], lo);
+}
+
 constexpr int MS = 32;
 
 struct WArgs {
@@ -73,3 +144,10 @@ struct WArgs {
 };
 
 }  // namespace
+
+namespace ppox_conv {
+int split_pack23(const float* w2, const float* w3, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
+                 hipStream_t s);
+int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq, const float* bias, float* y,
+                hipStream_t s);
+}  // namespace ppox_conv

@@ -18,42 +18,6 @@
 
 namespace {
 
-using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
-using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
-
-__device__ inline f32x16 mfma_bf16(const u32x4& a, const u32x4& b, const f32x16& c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
-                                                   0, 0, 0);
-}
-
-// two f32 whose low 16 bits are zero (exact bf16 values) -> packed bf16x2 (e0 low)
-__device__ inline uint32_t pack_hi(float e0, float e1) {
-    return __builtin_amdgcn_perm(__float_as_uint(e1), __float_as_uint(e0), 0x07060302);
-}
-
-// eight uint8 (two words) -> a bf16x8 fragment (exact: 0..255 have <= 8 significant bits)
-__device__ inline u32x4 u8x8_to_bf16(uint32_t w0, uint32_t w1) {
-    u32x4 r;
-    r[0] = pack_hi((float)(w0 & 0xFFu), (float)((w0 >> 8) & 0xFFu));
-    r[1] = pack_hi((float)((w0 >> 16) & 0xFFu), (float)(w0 >> 24));
-    r[2] = pack_hi((float)(w1 & 0xFFu), (float)((w1 >> 8) & 0xFFu));
-    r[3] = pack_hi((float)((w1 >> 16) & 0xFFu), (float)(w1 >> 24));
-    return r;
-}
-
-// exact three-way truncation split of one f32 (host+device; used by the packers)
-__host__ __device__ inline void split3(float a, uint16_t& p0, uint16_t& p1, uint16_t& p2) {
-    const uint32_t u = __builtin_bit_cast(uint32_t, a);
-    const float a0 = __builtin_bit_cast(float, u & 0xFFFF0000u);
-    const float r1 = a - a0;
-    const uint32_t v = __builtin_bit_cast(uint32_t, r1);
-    const float a1 = __builtin_bit_cast(float, v & 0xFFFF0000u);
-    const float r2 = r1 - a1;
-    p0 = (uint16_t)(u >> 16);
-    p1 = (uint16_t)(v >> 16);
-    p2 = (uint16_t)(__builtin_bit_cast(uint32_t, r2) >> 16);
-}
-
 // ---------------------------------------------------------------------------
 // conv1 forward, register-direct: each wave owns 32*MT output pixels x 32
 // channels, no LDS.  K chunk c (32 values) = input channel c/2, kernel rows
@@ -209,19 +173,24 @@ extern "C" int ppox_nature_pack_split(const float* w1, const float* w2, const fl
     PPOX_REQUIRE(ppox::aligned16(q1) && (!q2 || ppox::aligned16(q2)) && (!q3 || ppox::aligned16(q3)) &&
                      (!qd2 || ppox::aligned16(qd2)) && (!qd3 || ppox::aligned16(qd3)),
                  "ppox_nature_pack_split: packed buffers must be 16-byte aligned");
-    (void)w2; (void)w3;
+    PPOX_REQUIRE((!q2 || w2) && (!q3 || w3) && (!qd2 || w2) && (!qd3 || w3), "ppox_nature_pack_split: null weights");
     hipStream_t s = ppox::as_stream(stream);
     pack_fwd1_split<<<ppox::ceil_div(8 * 2 * 64 * 8, 256), 256, 0, s>>>(w1, q1);
-    PPOX_LAUNCHED("ppox_nature_pack_split");
+    PPOX_LAUNCHED_NORET("ppox_nature_pack_split");
+    return ppox_conv::split_pack23(w2, w3, q2, q3, qd2, qd3, s);
 }
 
 extern "C" int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx, int64_t T,
                                           int64_t N_env, int64_t x_sample_stride, const uint16_t* wq,
                                           const float* bias, float* y, void* stream) {
-    PPOX_REQUIRE(layer == 1, "ppox_nature_conv_fwd_split: layer must be 1");
+    PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_conv_fwd_split: layer must be 1, 2 or 3");
     PPOX_REQUIRE(x && wq && bias && y && batch >= 0, "ppox_nature_conv_fwd_split: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(wq), "ppox_nature_conv_fwd_split: packed weights must be 16-byte aligned");
     if (batch == 0) return PPOX_OK;
+    if (layer != 1) {
+        PPOX_REQUIRE(!idx, "ppox_nature_conv_fwd_split: idx is for layer 1 only");
+        return ppox_conv::split_fwd23(layer, x, batch, wq, bias, y, ppox::as_stream(stream));
+    }
     PPOX_REQUIRE(batch * G1::P < (1LL << 31), "ppox_nature_conv_fwd_split: batch too large for 32-bit rows");
     Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride,
            reinterpret_cast<const float*>(wq), bias, nullptr, y, batch};

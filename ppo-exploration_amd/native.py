@@ -57,6 +57,7 @@ SIGNATURES = {
     "ppox_nature_conv_fwd": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_pack_split": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
@@ -385,3 +386,8 @@ def nature_pack_split(w1, w2, w3, q1, q2, q3, qd2=None, qd3=None, stream=None):
 def nature_conv_fwd_split(layer, x, batch, idx, T, N_env, x_sample_stride, wq, bias, y, stream=None):
     call("ppox_nature_conv_fwd_split", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
          int(x_sample_stride), _p(wq), _p(bias), _p(y), stream_ptr(stream))
+
+
+def nature_conv_dgrad_split(layer, grad_out, batch, wqd, prev_act, grad_in, stream=None):
+    call("ppox_nature_conv_dgrad_split", int(layer), _p(grad_out), int(batch), _p(wqd), _p(prev_act), _p(grad_in),
+         stream_ptr(stream))

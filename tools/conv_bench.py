@@ -62,6 +62,14 @@ def main():
     rec("fwd", 3, t_ms(lambda: native.nature_conv_fwd(3, h2, B, None, 0, 0, 0, wp3, b3, h3)), MAC[3])
     rec("dgrad", 3, t_ms(lambda: native.nature_conv_dgrad(3, g3, B, wpd3, h2, g2)), MAC[3])
     rec("dgrad", 2, t_ms(lambda: native.nature_conv_dgrad(2, g2, B, wpd2, h1, g1)), MAC[2])
+    # split-bf16 forms
+    q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device=d) for k in (1, 2, 3, 12, 13)}
+    native.nature_pack_split(w1, w2, w3, q[1], q[2], q[3], q[12], q[13])
+    rec("fwd_split", 1, t_ms(lambda: native.nature_conv_fwd_split(1, x, B, None, 0, 0, 28224, q[1], b1, h1)), MAC[1])
+    rec("fwd_split", 2, t_ms(lambda: native.nature_conv_fwd_split(2, h1, B, None, 0, 0, 0, q[2], b2, h2)), MAC[2])
+    rec("fwd_split", 3, t_ms(lambda: native.nature_conv_fwd_split(3, h2, B, None, 0, 0, 0, q[3], b3, h3)), MAC[3])
+    rec("dgrad_split", 3, t_ms(lambda: native.nature_conv_dgrad_split(3, g3, B, q[13], h2, g2)), MAC[3])
+    rec("dgrad_split", 2, t_ms(lambda: native.nature_conv_dgrad_split(2, g2, B, q[12], h1, g1)), MAC[2])
     for L, xin, g, stride in ((3, h2, g3, 0), (2, h1, g2, 0), (1, x, g1, 28224)):
         f = lambda: lib.ppox_nature_conv_wgrad(L, native._p(xin), B, None, 0, 0, stride, native._p(g),
                                                native._p(ws[L]), ws[L].numel(), sp)
@@ -72,7 +80,7 @@ def main():
     xf = x.float()
     import torch.nn.functional as F
     rec("miopen_fwd", 1, t_ms(lambda: F.conv2d(xf, w1, b1, stride=4), 5), MAC[1])
-    tot = sum(r["ms"] for r in res if not r["kernel"].startswith("miopen"))
+    tot = sum(r["ms"] for r in res if not r["kernel"].startswith("miopen") and "split" not in r["kernel"])
     print(json.dumps({"total_conv_ms_per_minibatch": round(tot, 3)}))
 
 
