@@ -273,10 +273,18 @@ int ppox_nature_pack_split(const float* w1, const float* w2, const float* w3, ui
 int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
                                int64_t T, int64_t N_env, int64_t x_sample_stride,
                                const uint16_t* wq, const float* bias, float* y, void* stream);
-/* layers 2/3: LDS-staged implicit GEMM; every activation fragment split in registers. */
+/* dgrad (as ppox_nature_conv_dgrad) of conv2/conv3 with split weights (which = 12, 13). */
 int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch,
                                  const uint16_t* wqd, const float* prev_act, float* grad_in,
                                  void* stream);
+/* dW [co][ci][ky][kx] and db (as ppox_nature_conv_wgrad + ppox_nature_wgrad_reduce, in one
+ * call): split-K slabs into a workspace of ppox_nature_wgrad_split_workspace_bytes(layer,
+ * batch), reduced in a fixed order (deterministic).  x: u8 frames (layer 1, samples
+ * x_sample_stride bytes apart) or NHWC f32; grad_out: ReLU-masked NHWC output grad. */
+int64_t ppox_nature_wgrad_split_workspace_bytes(int32_t layer, int64_t batch);
+int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_t batch,
+                                 int64_t x_sample_stride, const float* grad_out, void* workspace,
+                                 int64_t workspace_bytes, float* dw, float* db, void* stream);
 
 #ifdef __cplusplus
 }

@@ -24,7 +24,7 @@ import native
 
 MATHS = ("split", "split_all", "f32")
 # ops that have a split-bf16 kernel: ("fwd" | "dgrad" | "wgrad", layer)
-SPLIT_OPS = {("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 3)}
+SPLIT_OPS = {("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 3), ("wgrad", 1), ("wgrad", 2), ("wgrad", 3)}
 # ops whose split kernel exists but is not faster than the f32 one at the training batch
 # (measured, tools/conv_bench.py); "split" mode runs them in f32
 SPLIT_SLOWER = {("dgrad", 2)}
@@ -105,8 +105,8 @@ class NatureConvs:
             return (op, layer) in SPLIT_OPS or (op, layer) in SPLIT_SLOWER
         return self.math == "split" and (op, layer) in SPLIT_OPS
 
-    def workspace(self, layer, batch):
-        need = native.nature_wgrad_workspace_bytes(layer, batch)
+    def workspace(self, layer, batch, split=False):
+        need = (native.nature_wgrad_split_workspace_bytes if split else native.nature_wgrad_workspace_bytes)(layer, batch)
         ws = self._ws.get(layer)
         if ws is None or ws.numel() < need:
             ws = torch.empty(need, dtype=torch.uint8, device=self.flat.device)
@@ -143,7 +143,10 @@ class NatureConvs:
 
     def wgrad(self, layer, x, B, g, dw, db):
         stride = 4 * 84 * 84 if layer == 1 else 0
-        native.nature_conv_wgrad(layer, x, B, None, 0, 0, stride, g, self.workspace(layer, B), dw, db)
+        if self.uses_split("wgrad", layer):
+            native.nature_conv_wgrad_split(layer, x, B, stride, g, self.workspace(layer, B, True), dw, db)
+        else:
+            native.nature_conv_wgrad(layer, x, B, None, 0, 0, stride, g, self.workspace(layer, B), dw, db)
 
     def __call__(self, x):
         if x.dtype != torch.uint8:

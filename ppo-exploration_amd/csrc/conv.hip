@@ -991,6 +991,248 @@ __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ sl
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Wgrad, split-bf16.  Same decomposition as wgrad_kernel (WG = k-block of KT rows x
+// all COUT x a slice of output pixels; partial slabs reduced by wgrad_reduce), on
+// v_mfma_f32_32x32x16_bf16.  Per step of MS = 32 pixels the X (im2col) and G tiles
+// are staged in LDS as bf16 planes, row-major [pixel][k] / [pixel][co] (each f32
+// value split once per workgroup into its three exact planes; conv1's u8 frames are
+// one exact plane), and the MFMA fragments — 8 consecutive pixels of one k (A) or
+// one co (B) per lane — come straight out of LDS with the transposing read
+// ds_read_b64_tr_b16 (two per fragment).  32-byte chunks of a row are XOR-swizzled
+// (tr_swz) so each 32-lane half's 4 rows x 2 chunks hit 8 distinct bank groups.
+// conv1: 3 MFMAs per tile and k-step (x*g0, x*g1, x*g2, all exact); f32 layers: the
+// six products of mfma_split6.  Loads of step s+1 fly under the MFMAs of step s.
+// ---------------------------------------------------------------------------
+template <class L, bool U8, int KT_>
+struct WsCfg {
+    static constexpr int KT = KT_, KB = L::K / KT, COUT = L::COUT;
+    static constexpr int XP = U8 ? 1 : 3;                        // X planes
+    static constexpr int NKT = KT / 32, NCT = COUT / 32, TPW = NKT * NCT / 4;
+    static constexpr int WKT = NCT == 1 ? TPW : 1, WCT = TPW / WKT;  // k- and co-tiles per wave
+    static constexpr int XR = KT * 2, GR = COUT * 2;             // LDS row bytes
+    static constexpr int XPB = MS * XR, GPB = MS * GR;           // LDS plane bytes
+    static constexpr int STAGE = XP * XPB + 3 * GPB;
+    static constexpr int UPX = KT / 8, XU = MS * UPX / 256;      // X units (8 k) per pixel / per thread
+    static constexpr int GUPX = COUT / 8, GU = MS * GUPX;        // G units (8 co) per pixel / per step
+    static_assert(KB * KT == L::K && (NKT * NCT) % 4 == 0 && XU * 256 == MS * UPX && GU <= 256, "wgrad split shape");
+    static_assert(WKT * WCT == TPW && (NCT == 1 || WKT == 1), "wave tiling");
+};
+
+// XOR on the 32-byte chunk index of row px (rows of ROWB bytes): the transposed reads
+// of a 32-lane half (rows px..px+3, chunks 2t and 2t+1) then cover all 64 banks once
+template <int ROWB>
+__device__ inline int tr_swz(int px) {
+    constexpr int m = (ROWB / 32) & 7;
+    static_assert(m == 0 || m == 4 || m == 2, "tr_swz: row stride");
+    if constexpr (m == 0) return 2 * (px & 3);
+    else if constexpr (m == 4) return 2 * ((px >> 1) & 1);
+    else return 0;
+}
+
+typedef short v4s16 __attribute__((ext_vector_type(4)));
+__device__ inline uint2 lds_tr16(const uint8_t* p) {
+    const v4s16 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s16*)p);
+    return __builtin_bit_cast(uint2, r);
+}
+
+template <class L, bool U8, int KT>
+__global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
+    using C = WsCfg<L, U8, KT>;
+    constexpr int COUT = L::COUT, XP = C::XP, XR = C::XR, GR = C::GR, XU = C::XU, UPX = C::UPX;
+    constexpr int WKT = C::WKT, WCT = C::WCT, GUPX = C::GUPX;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * C::STAGE];
+    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+    const int kb = q % C::KB, split = (q / C::KB) * 8 + xcd;
+    const unsigned M = (unsigned)(a.batch * L::P);
+    const unsigned long long mb64 = (unsigned long long)split * (unsigned long long)a.px_per_split;
+    const unsigned mbeg = mb64 < M ? (unsigned)mb64 : M;
+    const unsigned mend = (unsigned)min((unsigned long long)M, (unsigned long long)mbeg + a.px_per_split);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kt0 = (wave * C::TPW) / C::NCT, ct0 = (wave * C::TPW) % C::NCT;
+
+    f32x16 hi[WKT][WCT], lo[WKT][WCT];
+#pragma unroll
+    for (int i = 0; i < WKT; ++i)
+#pragma unroll
+        for (int j = 0; j < WCT; ++j) hi[i][j] = lo[i][j] = zero16();
+
+    constexpr unsigned long long SAMPLE_F32 = (unsigned long long)L::IH * L::IW * L::CIN;
+    const uint8_t* xu8 = reinterpret_cast<const uint8_t*>(a.x);
+    const float* xf = reinterpret_cast<const float*>(a.x);
+    uint32_t xw[XU][2];
+    float4 xr[XU][2];
+    float4 gr[2];
+    float bsum[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bsum[e] = 0.f;
+    const bool gthread = tid < C::GU;
+    const int gpx = tid / GUPX, gco = 8 * (tid % GUPX);
+
+    auto load = [&](unsigned ms, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
+#pragma unroll
+        for (int i = 0; i < XU; ++i) {
+            const int w = i * 256 + tid, pxl = w / UPX, j = w % UPX;
+            const unsigned m0 = ms + pxl;
+            const bool ok = FULL || m0 < mend;
+            const unsigned m = ok ? m0 : mbeg;
+            const unsigned n = m / L::P, p = m - n * L::P, oy = p / L::OW, ox = p - oy * L::OW;
+            const int k = kb * KT + 8 * j;
+            if constexpr (U8) {
+                const uint8_t* s = xu8 + (unsigned long long)n * a.sample_stride +
+                                   ((k >> 6) * L::IH + oy * L::S + ((k >> 3) & 7)) * L::IW + ox * L::S;
+                const uint32_t v0 = *reinterpret_cast<const uint32_t*>(s);
+                const uint32_t v1 = *reinterpret_cast<const uint32_t*>(s + 4);
+                xw[i][0] = ok ? v0 : 0u;
+                xw[i][1] = ok ? v1 : 0u;
+            } else {
+                const int tap = k / L::CIN, ci0 = k % L::CIN, ky = tap / L::KW, kx = tap % L::KW;
+                const float* s = xf + n * SAMPLE_F32 + ((oy * L::S + ky) * L::IW + ox * L::S + kx) * L::CIN + ci0;
+                const float4 v0 = *reinterpret_cast<const float4*>(s);
+                const float4 v1 = *reinterpret_cast<const float4*>(s + 4);
+                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                xr[i][0] = ok ? v0 : z;
+                xr[i][1] = ok ? v1 : z;
+            }
+        }
+        if (gthread) {
+            const unsigned m0 = ms + gpx;
+            const bool ok = FULL || m0 < mend;
+            const float* s = a.g + (unsigned long long)(ok ? m0 : mbeg) * COUT + gco;
+            const float4 v0 = *reinterpret_cast<const float4*>(s);
+            const float4 v1 = *reinterpret_cast<const float4*>(s + 4);
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            gr[0] = ok ? v0 : z;
+            gr[1] = ok ? v1 : z;
+        }
+    };
+    auto load_step = [&](unsigned ms) {
+        if (ms + MS <= mend)
+            load(ms, std::true_type{});
+        else
+            load(ms, std::false_type{});
+    };
+    auto store = [&](int buf) {
+        uint8_t* base = lds + buf * C::STAGE;
+#pragma unroll
+        for (int i = 0; i < XU; ++i) {
+            const int w = i * 256 + tid, pxl = w / UPX, j = w % UPX;
+            const int off = pxl * XR + (((j >> 1) ^ tr_swz<XR>(pxl)) << 5) + ((j & 1) << 4);
+            if constexpr (U8) {
+                *reinterpret_cast<u32x4*>(base + off) = u8x8_to_bf16(xw[i][0], xw[i][1]);
+            } else {
+                u32x4 p0, p1, p2;
+                split8(xr[i][0], xr[i][1], p0, p1, p2);
+                *reinterpret_cast<u32x4*>(base + off) = p0;
+                *reinterpret_cast<u32x4*>(base + C::XPB + off) = p1;
+                *reinterpret_cast<u32x4*>(base + 2 * C::XPB + off) = p2;
+            }
+        }
+        if (gthread) {
+            u32x4 p0, p1, p2;
+            split8(gr[0], gr[1], p0, p1, p2);
+            uint8_t* gb = base + XP * C::XPB;
+            const int off = gpx * GR + (((gco >> 4) ^ tr_swz<GR>(gpx)) << 5) + (((gco >> 3) & 1) << 4);
+            *reinterpret_cast<u32x4*>(gb + off) = p0;
+            *reinterpret_cast<u32x4*>(gb + C::GPB + off) = p1;
+            *reinterpret_cast<u32x4*>(gb + 2 * C::GPB + off) = p2;
+            bsum[0] += gr[0].x;
+            bsum[1] += gr[0].y;
+            bsum[2] += gr[0].z;
+            bsum[3] += gr[0].w;
+            bsum[4] += gr[1].x;
+            bsum[5] += gr[1].y;
+            bsum[6] += gr[1].z;
+            bsum[7] += gr[1].w;
+        }
+    };
+    // per-lane transposed-read offsets (T10): lane 4qq+pp of each 16-lane group supplies
+    // row qq, columns 4pp..4pp+3 of its 4-row x 16-column block; the block's rows are
+    // pixels 16ks + 8h + 4r + qq, its columns chunk 2t + g16 of the row
+    const int g16 = (lane >> 4) & 1, h = lane >> 5, qq = (lane >> 2) & 3, pp = lane & 3;
+    const int rowx = (8 * h + qq) * XR + pp * 8, rowg = (8 * h + qq) * GR + pp * 8;
+    const int swx = tr_swz<XR>(qq), swg = tr_swz<GR>(qq);
+    auto frag = [&](const uint8_t* plane, int rowoff, int rowb, int chunk, int ks) {
+        const uint8_t* p = plane + rowoff + 16 * ks * rowb + (chunk << 5);
+        const uint2 r0 = lds_tr16(p), r1 = lds_tr16(p + 4 * rowb);
+        u32x4 f;
+        f[0] = r0.x;
+        f[1] = r0.y;
+        f[2] = r1.x;
+        f[3] = r1.y;
+        return f;
+    };
+    auto compute = [&](int buf) {
+        const uint8_t* base = lds + buf * C::STAGE;
+        const uint8_t* gb = base + XP * C::XPB;
+#pragma unroll
+        for (int ks = 0; ks < MS / 16; ++ks) {
+            u32x4 bq[WCT][3];
+#pragma unroll
+            for (int j = 0; j < WCT; ++j)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    bq[j][p] = frag(gb + p * C::GPB, rowg, GR, (2 * (ct0 + j) + g16) ^ swg, ks);
+#pragma unroll
+            for (int i = 0; i < WKT; ++i) {
+                u32x4 aq[3];
+#pragma unroll
+                for (int p = 0; p < XP; ++p) aq[p] = frag(base + p * C::XPB, rowx, XR, (2 * (kt0 + i) + g16) ^ swx, ks);
+#pragma unroll
+                for (int j = 0; j < WCT; ++j) {
+                    if constexpr (U8) {
+                        hi[i][j] = mfma_bf16(aq[0], bq[j][0], hi[i][j]);
+                        lo[i][j] = mfma_bf16(aq[0], bq[j][1], lo[i][j]);
+                        lo[i][j] = mfma_bf16(aq[0], bq[j][2], lo[i][j]);
+                    } else {
+                        mfma_split6(aq, bq[j], hi[i][j], lo[i][j]);
+                    }
+                }
+            }
+        }
+    };
+
+    const unsigned nsteps = mend > mbeg ? (mend - mbeg + MS - 1) / MS : 0;
+    if (nsteps > 0) {
+        load_step(mbeg);
+        store(0);
+    }
+    __syncthreads();
+    for (unsigned s = 0; s < nsteps; ++s) {
+        const int cur = (int)(s & 1);
+        if (s + 1 < nsteps) load_step(mbeg + (s + 1) * MS);
+        compute(cur);
+        if (s + 1 < nsteps) store(cur ^ 1);
+        __syncthreads();
+    }
+    float* slab = a.slab + (long long)split * L::K * COUT;
+#pragma unroll
+    for (int i = 0; i < WKT; ++i)
+#pragma unroll
+        for (int j = 0; j < WCT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int kr = kb * KT + (kt0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                slab[kr * COUT + (ct0 + j) * 32 + (lane & 31)] = hi[i][j][r] + lo[i][j][r];
+            }
+    if (kb == 0) {
+        // bias grad partial: column sums of this split's G rows, combined in a fixed order
+        float* bred = reinterpret_cast<float*>(lds);  // the loop ended on a barrier
+        if (gthread) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bred[gpx * COUT + gco + e] = bsum[e];
+        }
+        __syncthreads();
+        if (tid < COUT) {
+            float t = 0.f;
+            for (int g = 0; g < MS; ++g) t += bred[g * COUT + tid];
+            a.bslab[(long long)split * COUT + tid] = t;
+        }
+    }
+}
+
 // conv3 output grad: NCHW (Flatten order) -> NHWC, times the ReLU mask of h3 (NCHW)
 __global__ void __launch_bounds__(256) nchw_to_nhwc_mask(const float* __restrict__ g, const float* __restrict__ h,
                                                          long long batch, float* __restrict__ out) {
@@ -1098,6 +1340,43 @@ int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float
     PPOX_LAUNCHED("ppox_nature_wgrad_reduce");
 }
 
+
+#ifndef WS_KT2
+#define WS_KT2 128
+#endif
+#ifndef WS_KT3
+#define WS_KT3 64
+#endif
+// split wgrad: its own split-K count (~2048 pixels per split so the grid fills the chip)
+template <class L, bool U8, int KT>
+struct WsLaunch {
+    using C = WsCfg<L, U8, KT>;
+    static long long splits(long long batch) {
+        const long long px = batch * L::P;
+        long long s = (px + 2047) / 2048;
+        const long long most = (px + MS - 1) / MS;  // at least one step per split
+        s = s > most ? most : s;
+        s = s < 8 ? 8 : (s > 2048 ? 2048 : s);
+        return (s + 7) / 8 * 8;
+    }
+    static long long workspace_bytes(long long batch) {
+        return splits(batch) * (long long)(L::K * L::COUT + L::COUT) * (long long)sizeof(float);
+    }
+    static int run(const void* x, long long sample_stride, const float* g, long long batch, void* ws, float* dw,
+                   float* db, hipStream_t s) {
+        const int sp = (int)splits(batch);
+        float* slab = reinterpret_cast<float*>(ws);
+        WArgs wa{x, sample_stride, g, slab, slab + (long long)sp * L::K * L::COUT, batch, 0, sp};
+        const long long M = batch * L::P;
+        wa.px_per_split = ppox::ceil_div(ppox::ceil_div(M, sp), MS) * MS;
+        wgrad_split_kernel<L, U8, KT><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
+        PPOX_LAUNCHED_NORET("ppox_nature_conv_wgrad_split");
+        return launch_wgrad_reduce<L, !U8>(slab, wa.bslab, sp, dw, db, s);
+    }
+};
+using Ws1 = WsLaunch<G1, true, 256>;
+using Ws2 = WsLaunch<G2, false, WS_KT2>;
+using Ws3 = WsLaunch<G3, false, WS_KT3>;
 }  // namespace
 
 extern "C" int ppox_nature_pack_weights(const float* w1, const float* w2, const float* w3, float* wp1, float* wp2,
@@ -1239,6 +1518,34 @@ extern "C" int ppox_nature_wgrad_reduce(int32_t layer, int64_t batch, const void
     if (layer == 1) return launch_wgrad_reduce<G1, false>(slab, bslab, splits, dw, db, s);
     if (layer == 2) return launch_wgrad_reduce<G2, true>(slab, bslab, splits, dw, db, s);
     return launch_wgrad_reduce<G3, true>(slab, bslab, splits, dw, db, s);
+}
+
+
+extern "C" int64_t ppox_nature_wgrad_split_workspace_bytes(int32_t layer, int64_t batch) {
+    if (batch <= 0) return 0;
+    return layer == 1 ? Ws1::workspace_bytes(batch) : layer == 2 ? Ws2::workspace_bytes(batch)
+                      : layer == 3 ? Ws3::workspace_bytes(batch) : -1;
+}
+
+extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_t batch, int64_t x_sample_stride,
+                                            const float* grad_out, void* workspace, int64_t workspace_bytes, float* dw,
+                                            float* db, void* stream) {
+    PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_conv_wgrad_split: layer must be 1, 2 or 3");
+    PPOX_REQUIRE(x && grad_out && workspace && dw && db && batch > 0, "ppox_nature_conv_wgrad_split: bad arguments");
+    PPOX_REQUIRE(workspace_bytes >= ppox_nature_wgrad_split_workspace_bytes(layer, batch),
+                 "ppox_nature_conv_wgrad_split: workspace too small");
+    PPOX_REQUIRE(ppox::aligned16(grad_out), "ppox_nature_conv_wgrad_split: grad_out must be 16B aligned");
+    PPOX_REQUIRE(batch * (layer == 1 ? G1::P : layer == 2 ? G2::P : G3::P) < (1LL << 31) / 64,
+                 "ppox_nature_conv_wgrad_split: batch too large for 32-bit pixel indexing");
+    hipStream_t s = ppox::as_stream(stream);
+    if (layer == 1) {
+        PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && x_sample_stride % 4 == 0,
+                     "ppox_nature_conv_wgrad_split: u8 input 4-byte aligned");
+        return Ws1::run(x, x_sample_stride, grad_out, batch, workspace, dw, db, s);
+    }
+    PPOX_REQUIRE(ppox::aligned16(x), "ppox_nature_conv_wgrad_split: layer 2/3 input must be 16B-aligned NHWC");
+    if (layer == 2) return Ws2::run(x, 0, grad_out, batch, workspace, dw, db, s);
+    return Ws3::run(x, 0, grad_out, batch, workspace, dw, db, s);
 }
 
 extern "C" int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, int64_t batch, float* out,

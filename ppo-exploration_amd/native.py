@@ -58,15 +58,18 @@ SIGNATURES = {
     "ppox_nature_pack_split": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_wgrad_split": [_i32, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
 }
 _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p,
              "ppox_rms_u8_workspace_bytes": ctypes.c_int64, "ppox_nature_wgrad_splits": ctypes.c_int64,
-             "ppox_nature_wgrad_workspace_bytes": ctypes.c_int64, "ppox_nature_split_pack_elems": ctypes.c_int64}
+             "ppox_nature_wgrad_workspace_bytes": ctypes.c_int64, "ppox_nature_split_pack_elems": ctypes.c_int64,
+             "ppox_nature_wgrad_split_workspace_bytes": ctypes.c_int64}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
-                 "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32]}
+                 "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32],
+                 "ppox_nature_wgrad_split_workspace_bytes": [_i32, _i64]}
 
 _lib = None
 
@@ -386,6 +389,16 @@ def nature_pack_split(w1, w2, w3, q1, q2, q3, qd2=None, qd3=None, stream=None):
 def nature_conv_fwd_split(layer, x, batch, idx, T, N_env, x_sample_stride, wq, bias, y, stream=None):
     call("ppox_nature_conv_fwd_split", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
          int(x_sample_stride), _p(wq), _p(bias), _p(y), stream_ptr(stream))
+
+
+def nature_wgrad_split_workspace_bytes(layer, batch):
+    return int(load().ppox_nature_wgrad_split_workspace_bytes(int(layer), int(batch)))
+
+
+def nature_conv_wgrad_split(layer, x, batch, x_sample_stride, grad_out, workspace, dw, db, stream=None):
+    """dW, db of one conv layer (slabs + fixed-order reduce in one call), split-bf16 MFMA."""
+    call("ppox_nature_conv_wgrad_split", int(layer), _p(x), int(batch), int(x_sample_stride), _p(grad_out),
+         _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db), stream_ptr(stream))
 
 
 def nature_conv_dgrad_split(layer, grad_out, batch, wqd, prev_act, grad_in, stream=None):

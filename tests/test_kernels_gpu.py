@@ -477,6 +477,12 @@ def _conv_ops_fp64(B, seed):
         cv.dgrad(3, g3, B, h2f, d2)
         cv.dgrad(2, g2r, B, h1f, d1)
         out[math].update({("dgrad", 3): d2, ("dgrad", 2): d1})
+        g1r = torch.randn(B, 20, 20, 32, device="cuda", generator=torch.Generator(device="cuda").manual_seed(seed + 7))
+        for L, xin, gg in ((1, x, g1r), (2, h1f, g2r), (3, h2f, g3)):
+            wl = (cv.c1, cv.c2, cv.c3)[L - 1]
+            dw, db = torch.empty_like(wl.weight), torch.empty_like(wl.bias)
+            cv.wgrad(L, xin, B, gg, dw, db)
+            out[math].update({("wgrad", L): dw, ("wgrad_bias", L): db})
     # fp64 reference (CPU autograd, same weights)
     fe = net.feature_extractor
     w = [fe[i].weight.detach().double().cpu() for i in (0, 2, 4)]
@@ -491,6 +497,10 @@ def _conv_ops_fp64(B, seed):
     ci2 = torch.nn.grad.conv2d_input((B, 32, 20, 20), w[1], nchw(g2r), stride=2)
     ref[("dgrad", 3)] = (ci3 * (nchw(h2f) > 0)).permute(0, 2, 3, 1)
     ref[("dgrad", 2)] = (ci2 * (nchw(h1f) > 0)).permute(0, 2, 3, 1)
+    g1r = torch.randn(B, 20, 20, 32, device="cuda", generator=torch.Generator(device="cuda").manual_seed(seed + 7))
+    for L, xin, gg, st in ((1, x.double().cpu(), g1r, 4), (2, nchw(h1f), g2r, 2), (3, nchw(h2f), g3, 1)):
+        ref[("wgrad", L)] = torch.nn.grad.conv2d_weight(xin, w[L - 1].shape, nchw(gg), stride=st)
+        ref[("wgrad_bias", L)] = nchw(gg).sum(dim=(0, 2, 3))
     return {k: (out["split_all"][k], out["f32"][k], ref[k]) for k in ref}
 
 
@@ -502,7 +512,8 @@ def test_split_conv_accuracy_is_fp32_class(seed):
     import convs
     res = _conv_ops_fp64(24, seed)
     for key, (spl, f32, ref) in res.items():
-        if key not in convs.SPLIT_OPS and key not in convs.SPLIT_SLOWER:
+        op = ("wgrad", key[1]) if key[0] == "wgrad_bias" else key
+        if op not in convs.SPLIT_OPS and op not in convs.SPLIT_SLOWER:
             continue
         scale = ref.abs().max().item()
         e_s = (spl.cpu().double() - ref).abs().max().item() / scale

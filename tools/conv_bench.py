@@ -71,6 +71,10 @@ def main():
     rec("dgrad_split", 3, t_ms(lambda: native.nature_conv_dgrad_split(3, g3, B, q[13], h2, g2)), MAC[3])
     rec("dgrad_split", 2, t_ms(lambda: native.nature_conv_dgrad_split(2, g2, B, q[12], h1, g1)), MAC[2])
     for L, xin, g, stride in ((3, h2, g3, 0), (2, h1, g2, 0), (1, x, g1, 28224)):
+        wsp = torch.empty(native.nature_wgrad_split_workspace_bytes(L, B), dtype=torch.uint8, device=d)
+        rec("wgrad_split", L, t_ms(lambda: native.nature_conv_wgrad_split(L, xin, B, stride, g, wsp, dw[L], db[L])),
+            MAC[L])
+    for L, xin, g, stride in ((3, h2, g3, 0), (2, h1, g2, 0), (1, x, g1, 28224)):
         f = lambda: lib.ppox_nature_conv_wgrad(L, native._p(xin), B, None, 0, 0, stride, native._p(g),
                                                native._p(ws[L]), ws[L].numel(), sp)
         rec("wgrad", L, t_ms(f), MAC[L])
