@@ -1014,9 +1014,10 @@ struct WsCfg {
     static constexpr int XR = KT * 2, GR = COUT * 2;             // LDS row bytes
     static constexpr int XPB = MS * XR, GPB = MS * GR;           // LDS plane bytes
     static constexpr int STAGE = XP * XPB + 3 * GPB;
-    static constexpr int UPX = KT / 8, XU = MS * UPX / 256;      // X units (8 k) per pixel / per thread
-    static constexpr int GUPX = COUT / 8, GU = MS * GUPX;        // G units (8 co) per pixel / per step
-    static_assert(KB * KT == L::K && (NKT * NCT) % 4 == 0 && XU * 256 == MS * UPX && GU <= 256, "wgrad split shape");
+    // staging: 8 threads per pixel row; a thread stages XU units of 8 consecutive k and GW
+    // consecutive co of one pixel, so its addresses come from one (sample, pixel) pair
+    static constexpr int UPX = KT / 8, XU = UPX / 8, GW = COUT / 8;
+    static_assert(KB * KT == L::K && (NKT * NCT) % 4 == 0 && XU * 8 == UPX && (GW == 4 || GW == 8), "wgrad split shape");
     static_assert(WKT * WCT == TPW && (NCT == 1 || WKT == 1), "wave tiling");
 };
 
@@ -1041,7 +1042,7 @@ template <class L, bool U8, int KT>
 __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     using C = WsCfg<L, U8, KT>;
     constexpr int COUT = L::COUT, XP = C::XP, XR = C::XR, GR = C::GR, XU = C::XU, UPX = C::UPX;
-    constexpr int WKT = C::WKT, WCT = C::WCT, GUPX = C::GUPX;
+    constexpr int WKT = C::WKT, WCT = C::WCT;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * C::STAGE];
     const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
     const int kb = q % C::KB, split = (q / C::KB) * 8 + xcd;
@@ -1061,64 +1062,94 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     constexpr unsigned long long SAMPLE_F32 = (unsigned long long)L::IH * L::IW * L::CIN;
     const uint8_t* xu8 = reinterpret_cast<const uint8_t*>(a.x);
     const float* xf = reinterpret_cast<const float*>(a.x);
+    constexpr int GW = C::GW;
     uint32_t xw[XU][2];
     float4 xr[XU][2];
     float4 gr[2];
-    float bsum[8];
+    float bsum[GW];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) bsum[e] = 0.f;
-    const bool gthread = tid < C::GU;
-    const int gpx = tid / GUPX, gco = 8 * (tid % GUPX);
+    for (int e = 0; e < GW; ++e) bsum[e] = 0.f;
+    // this thread's pixel row and units; the pixel advances by MS per step (at most one
+    // wrap into the next sample: MS <= P), so no 64-bit index is divided in the loop
+    // unit i of the thread is j = 8i + (tid & 7): the 8 threads of a pixel row write 128
+    // contiguous bytes per store instruction (bank-conflict-free)
+    const int pxl = tid >> 3, ju = tid & 7, gco = (tid & 7) * GW;
+    const unsigned long long sstride = U8 ? (unsigned long long)a.sample_stride : SAMPLE_F32;
+    unsigned xp, mcur = mbeg + pxl;
+    unsigned long long sb;
+    {
+        const unsigned m = mcur < M ? mcur : mbeg;
+        const unsigned n = m / L::P;
+        xp = m - n * L::P;
+        sb = n * sstride;
+    }
+    const unsigned xp0 = mbeg - (mbeg / L::P) * L::P;  // a pixel that always exists
+    const unsigned long long sb00 = (unsigned long long)(mbeg / L::P) * sstride;
+    int koff[XU];
+#pragma unroll
+    for (int i = 0; i < XU; ++i) {
+        const int k = kb * KT + 8 * (8 * i + ju);
+        if constexpr (U8) {
+            koff[i] = ((k >> 6) * L::IH + ((k >> 3) & 7)) * L::IW;
+        } else {
+            const int tap = k / L::CIN;
+            koff[i] = ((tap / L::KW) * L::IW + tap % L::KW) * L::CIN + k % L::CIN;
+        }
+    }
 
-    auto load = [&](unsigned ms, auto full_tag) {
+    // loads of the next step (steps are loaded in order; the state above advances)
+    auto load = [&](auto full_tag) {
         constexpr bool FULL = decltype(full_tag)::value;
+        const bool ok = FULL || mcur < mend;
+        const unsigned p = ok ? xp : xp0;
+        const unsigned long long s0 = ok ? sb : sb00;
+        const unsigned oy = p / L::OW, ox = p - oy * L::OW;
+        if constexpr (U8) {
+            const uint8_t* s = xu8 + s0 + oy * L::S * L::IW + ox * L::S;
 #pragma unroll
-        for (int i = 0; i < XU; ++i) {
-            const int w = i * 256 + tid, pxl = w / UPX, j = w % UPX;
-            const unsigned m0 = ms + pxl;
-            const bool ok = FULL || m0 < mend;
-            const unsigned m = ok ? m0 : mbeg;
-            const unsigned n = m / L::P, p = m - n * L::P, oy = p / L::OW, ox = p - oy * L::OW;
-            const int k = kb * KT + 8 * j;
-            if constexpr (U8) {
-                const uint8_t* s = xu8 + (unsigned long long)n * a.sample_stride +
-                                   ((k >> 6) * L::IH + oy * L::S + ((k >> 3) & 7)) * L::IW + ox * L::S;
-                const uint32_t v0 = *reinterpret_cast<const uint32_t*>(s);
-                const uint32_t v1 = *reinterpret_cast<const uint32_t*>(s + 4);
+            for (int i = 0; i < XU; ++i) {
+                const uint32_t v0 = *reinterpret_cast<const uint32_t*>(s + koff[i]);
+                const uint32_t v1 = *reinterpret_cast<const uint32_t*>(s + koff[i] + 4);
                 xw[i][0] = ok ? v0 : 0u;
                 xw[i][1] = ok ? v1 : 0u;
-            } else {
-                const int tap = k / L::CIN, ci0 = k % L::CIN, ky = tap / L::KW, kx = tap % L::KW;
-                const float* s = xf + n * SAMPLE_F32 + ((oy * L::S + ky) * L::IW + ox * L::S + kx) * L::CIN + ci0;
-                const float4 v0 = *reinterpret_cast<const float4*>(s);
-                const float4 v1 = *reinterpret_cast<const float4*>(s + 4);
-                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        } else {
+            const float* s = xf + s0 + (oy * L::S * L::IW + ox * L::S) * L::CIN;
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int i = 0; i < XU; ++i) {
+                const float4 v0 = *reinterpret_cast<const float4*>(s + koff[i]);
+                const float4 v1 = *reinterpret_cast<const float4*>(s + koff[i] + 4);
                 xr[i][0] = ok ? v0 : z;
                 xr[i][1] = ok ? v1 : z;
             }
         }
-        if (gthread) {
-            const unsigned m0 = ms + gpx;
-            const bool ok = FULL || m0 < mend;
-            const float* s = a.g + (unsigned long long)(ok ? m0 : mbeg) * COUT + gco;
-            const float4 v0 = *reinterpret_cast<const float4*>(s);
-            const float4 v1 = *reinterpret_cast<const float4*>(s + 4);
-            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-            gr[0] = ok ? v0 : z;
-            gr[1] = ok ? v1 : z;
+        const float* sg = a.g + (unsigned long long)(ok ? mcur : mbeg) * COUT + gco;
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 g0 = *reinterpret_cast<const float4*>(sg);
+        gr[0] = ok ? g0 : z;
+        if constexpr (GW == 8) {
+            const float4 g1 = *reinterpret_cast<const float4*>(sg + 4);
+            gr[1] = ok ? g1 : z;
+        }
+        mcur += MS;
+        xp += MS;
+        if (xp >= (unsigned)L::P) {
+            xp -= L::P;
+            sb += sstride;
         }
     };
     auto load_step = [&](unsigned ms) {
         if (ms + MS <= mend)
-            load(ms, std::true_type{});
+            load(std::true_type{});
         else
-            load(ms, std::false_type{});
+            load(std::false_type{});
     };
     auto store = [&](int buf) {
         uint8_t* base = lds + buf * C::STAGE;
 #pragma unroll
         for (int i = 0; i < XU; ++i) {
-            const int w = i * 256 + tid, pxl = w / UPX, j = w % UPX;
+            const int j = 8 * i + ju;
             const int off = pxl * XR + (((j >> 1) ^ tr_swz<XR>(pxl)) << 5) + ((j & 1) << 4);
             if constexpr (U8) {
                 *reinterpret_cast<u32x4*>(base + off) = u8x8_to_bf16(xw[i][0], xw[i][1]);
@@ -1130,18 +1161,26 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
                 *reinterpret_cast<u32x4*>(base + 2 * C::XPB + off) = p2;
             }
         }
-        if (gthread) {
+        uint8_t* gb = base + XP * C::XPB;
+        const int goff = pxl * GR + (((gco >> 4) ^ tr_swz<GR>(pxl)) << 5) + (gco & 15) * 2;
+        if constexpr (GW == 8) {
             u32x4 p0, p1, p2;
             split8(gr[0], gr[1], p0, p1, p2);
-            uint8_t* gb = base + XP * C::XPB;
-            const int off = gpx * GR + (((gco >> 4) ^ tr_swz<GR>(gpx)) << 5) + (((gco >> 3) & 1) << 4);
-            *reinterpret_cast<u32x4*>(gb + off) = p0;
-            *reinterpret_cast<u32x4*>(gb + C::GPB + off) = p1;
-            *reinterpret_cast<u32x4*>(gb + 2 * C::GPB + off) = p2;
-            bsum[0] += gr[0].x;
-            bsum[1] += gr[0].y;
-            bsum[2] += gr[0].z;
-            bsum[3] += gr[0].w;
+            *reinterpret_cast<u32x4*>(gb + goff) = p0;
+            *reinterpret_cast<u32x4*>(gb + C::GPB + goff) = p1;
+            *reinterpret_cast<u32x4*>(gb + 2 * C::GPB + goff) = p2;
+        } else {
+            uint2 p0, p1, p2;
+            split4(gr[0], p0, p1, p2);
+            *reinterpret_cast<uint2*>(gb + goff) = p0;
+            *reinterpret_cast<uint2*>(gb + C::GPB + goff) = p1;
+            *reinterpret_cast<uint2*>(gb + 2 * C::GPB + goff) = p2;
+        }
+        bsum[0] += gr[0].x;
+        bsum[1] += gr[0].y;
+        bsum[2] += gr[0].z;
+        bsum[3] += gr[0].w;
+        if constexpr (GW == 8) {
             bsum[4] += gr[1].x;
             bsum[5] += gr[1].y;
             bsum[6] += gr[1].z;
@@ -1220,10 +1259,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     if (kb == 0) {
         // bias grad partial: column sums of this split's G rows, combined in a fixed order
         float* bred = reinterpret_cast<float*>(lds);  // the loop ended on a barrier
-        if (gthread) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) bred[gpx * COUT + gco + e] = bsum[e];
-        }
+        for (int e = 0; e < GW; ++e) bred[pxl * COUT + gco + e] = bsum[e];
         __syncthreads();
         if (tid < COUT) {
             float t = 0.f;

@@ -119,6 +119,24 @@ __device__ inline void split8(const float4& v0, const float4& v1, u32x4& p0, u32
     }
 }
 
+// four f32 -> three exact bf16 planes, two bf16x2 words each
+__device__ inline void split4(const float4& v, uint2& p0, uint2& p1, uint2& p2) {
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    uint32_t h0[4], h1[4], h2[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const uint32_t u0 = __float_as_uint(x[e]) & 0xFFFF0000u;
+        const float r1 = x[e] - __uint_as_float(u0);
+        const uint32_t u1 = __float_as_uint(r1) & 0xFFFF0000u;
+        h0[e] = u0;
+        h1[e] = u1;
+        h2[e] = __float_as_uint(r1 - __uint_as_float(u1));
+    }
+    p0 = make_uint2(__builtin_amdgcn_perm(h0[1], h0[0], 0x07060302), __builtin_amdgcn_perm(h0[3], h0[2], 0x07060302));
+    p1 = make_uint2(__builtin_amdgcn_perm(h1[1], h1[0], 0x07060302), __builtin_amdgcn_perm(h1[3], h1[2], 0x07060302));
+    p2 = make_uint2(__builtin_amdgcn_perm(h2[1], h2[0], 0x07060302), __builtin_amdgcn_perm(h2[3], h2[2], 0x07060302));
+}
+
 // a*b on split operands: the six products a_i*b_j with i + j <= 2; a0*b0 into hi,
 // the rest into lo (both f32 accumulators; the result is hi + lo)
 __device__ inline void mfma_split6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16& hi, f32x16& lo) {

@@ -11,7 +11,7 @@ i=0
 for SET in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS" \
            "GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVES SQ_ACTIVE_INST_LDS"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $SET --kernel-include-regex "gemm|wgrad_kernel|split" -d /tmp/$TAG-p$i -o run \
+  timeout -k 10 300 rocprofv3 --pmc $SET --kernel-include-regex "gemm|wgrad|split" -d /tmp/$TAG-p$i -o run \
       --output-format csv -- python3 $R/tools/conv_bench.py 16384 $LIB > gpurun_out/$TAG/pmc_p$i.log 2>&1 || exit $?
   cp /tmp/$TAG-p$i/*counter_collection* gpurun_out/$TAG/pmc_p$i.csv
 done
