@@ -24,7 +24,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (= f32 vector) dense peak
 
 
-def pmc_traffic(kernel="wgrad_kernel<4, 84, 84, 8, 8, 4, 32, true>"):
+def pmc_traffic(kernel):
     """HBM bytes per launch of the dominant kernel from the latest committed rocprofv3 --pmc
     summary (profiles/rNN_pmc_summary.json, made by tools/pmc_summary.py from separate
     FETCH_SIZE / WRITE_SIZE passes of this bench command, gfx950-corrected 2*FETCH + WRITE)."""
@@ -35,6 +35,54 @@ def pmc_traffic(kernel="wgrad_kernel<4, 84, 84, 8, 8, 4, 32, true>"):
     with open(files[-1]) as f:
         d = json.load(f).get(kernel)
     return (None, None) if d is None else (d["hbm_bytes_per_launch_corrected"], os.path.relpath(files[-1], ROOT))
+
+
+# K6 conv ops: MACs per sample and activation bytes per sample
+# (layer input 0 = the u8 frame stack, 28,224 B; f32 NHWC activations after)
+CONV_MAC = {1: 400 * 256 * 32, 2: 81 * 512 * 64, 3: 49 * 576 * 64}
+ACT_B = {0: 28224, 1: 20 * 20 * 32 * 4, 2: 9 * 9 * 64 * 4, 3: 7 * 7 * 64 * 4}
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+# rocprofv3 kernel names of the conv entry points (for the PMC traffic lookup)
+CONV_KERNEL = {("fwd", 1, True): "fwd1_split_kernel<1>",
+               ("fwd", 2, True): "igemm_split_kernel<FwdNHWCProblem<32, 20, 20, 4, 4, 2, 64, false, 1>>",
+               ("fwd", 3, True): "igemm_split_kernel<FwdNHWCProblem<64, 9, 9, 3, 3, 1, 64, true, 1>>",
+               ("dgrad", 2, False): "igemm_kernel<DgradPMProblem<32, 20, 20, 4, 4, 2, 64, 1>>",
+               ("dgrad", 3, True): "igemm_split_kernel<DgradPMProblem<64, 9, 9, 3, 3, 1, 64, 1>>",
+               ("wgrad", 1, True): "wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256>",
+               ("wgrad", 2, True): "wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128>",
+               ("wgrad", 3, True): "wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64>"}
+
+
+def conv_roofline(key, kt, totals):
+    """Roofline of the dominant conv launch: algorithmic FLOPs (2 x MACs x batch) per launch /
+    mean HIP-event duration.  The f32 kernels run v_mfma_f32_32x32x2_f32 (peak 157.3 TF/s);
+    the split-bf16 kernels issue 6 bf16 MFMA products per f32 MAC (3 when one operand is the
+    u8 frame), so their f32-equivalent peak is 2500 / 6 (or / 3) TF/s."""
+    import numpy as np
+    name, layer = key.split(":")
+    layer = int(layer)
+    op = name.replace("ppox_nature_conv_", "").replace("_split", "")
+    split = name.endswith("_split")
+    batch = float(np.mean([a[2] for _, a in kt]))
+    mean_ms = float(np.mean([t for t, _ in kt]))
+    flops = 2.0 * CONV_MAC[layer] * batch
+    ach = flops / (mean_ms * 1e-3) / 1e12
+    products = (3 if (layer == 1 and op != "dgrad") else 6) if split else 1
+    peak = BF16_MFMA_PEAK_TFLOPS / products if split else FP32_MFMA_PEAK_TFLOPS
+    # input + output (fwd), output grad + ReLU mask + input grad (dgrad), input + output grad (wgrad)
+    per = ACT_B[layer] + (2 * ACT_B[layer - 1] if op == "dgrad" else ACT_B[layer - 1])
+    kname = CONV_KERNEL.get((op, layer, split))
+    traffic, src = pmc_traffic(kname) if kname else (None, None)
+    tot = sum(totals.values()) or 1.0
+    return {"kernel": f"{name} layer {layer}" + (f" = {kname}" if kname else ""), "bound": "mfma",
+            "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+            "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)", "traffic_source": src,
+            "alg_bytes_per_launch": batch * per, "alg_flops_per_launch": flops,
+            "launches": len(kt), "mean_us": round(mean_ms * 1e3, 1),
+            "alg_hbm_GBs": round(batch * per / (mean_ms * 1e-3) / 1e9, 1),
+            "share_of_conv_time": round(totals.get(key, 0.0) / tot, 3),
+            "peak_note": "f32 MFMA 157.3 TF/s" if not split else
+                         f"bf16 MFMA 2500 TF/s / {products} products per f32 MAC (split-bf16, fp32-class accuracy)"}
 
 
 def gae_kernel_ms(alg, dual, reps=20):
@@ -121,12 +169,15 @@ def main():
         alg.collect_samples()
         alg.train()
 
+    # the conv entry points (K6), timed with HIP events on their launch stream; the warmup
+    # iterations pick the dominant one (largest total time), the timed region times it
+    conv_keys = [f"ppox_nature_conv_{op}{m}:{l}" for op in ("fwd", "dgrad", "wgrad") for m in ("", "_split")
+                 for l in (1, 2, 3)]
+    native.enable_event_timing(conv_keys)
     for _ in range(args.warmup):
         iteration()
-
-    # event timing of the dominant kernel (conv1 weight-gradient MFMA GEMM)
-    # on the stream it is launched on
-    prof_kernel = "ppox_nature_conv_wgrad:1"
+    totals = {k: sum(t for t, _ in native.event_times_ms(k)) for k in conv_keys}
+    prof_kernel = max(totals, key=totals.get) if any(totals.values()) else "ppox_nature_conv_dgrad:2"
     gae_kernel = "ppox_gae" if args.algo != "rnd" else "ppox_gae_dual"
     native.enable_event_timing([prof_kernel])
 
@@ -150,6 +201,7 @@ def main():
 
     env_steps = args.steps * args.envs * args.nstep
     value = env_steps / dt
+    conv_impl = getattr(alg.policy.net, "conv_impl", None)
     out = {
         "metric": "env-steps/sec (collect+GAE+PPO update), 4096 envs×128 steps @ 1/2/4/8 GPU",
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -159,23 +211,11 @@ def main():
         "config": {"workload": f"{env_id} {args.algo.upper()} NatureCNN {args.envs} envs x {args.nstep} steps",
                    "n_envs": args.envs, "n_steps": args.nstep, "n_epochs": args.epochs,
                    "batch_size": args.batch_size, "minibatches_per_epoch": -(-args.envs * args.nstep // args.batch_size),
+                   "conv_math": conv_impl.math if conv_impl is not None else None,
                    "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)" if world > 1 else "single GPU"},
     }
-    # roofline of the dominant kernel: ALGORITHMIC flops per launch / mean launch duration.
-    # conv1 wgrad = 2 * batch * 400 output pixels * 256 (ci,ky,kx) * 32 output channels
     if kt:
-        flops = [2.0 * a[2] * 400 * 256 * 32 for _, a in kt]
-        mean_ms = float(np.mean([t for t, _ in kt]))
-        ach = float(np.mean(flops)) / (mean_ms * 1e-3) / 1e12
-        traffic, src = pmc_traffic()
-        # algorithmic HBM bytes: u8 input (28224 B/sample) + f32 output grad (400*32*4 B/sample)
-        alg_bytes = float(np.mean([a[2] for _, a in kt])) * (28224 + 400 * 32 * 4)
-        out["roofline"] = {"kernel": "wgrad_kernel<conv1> (ppox_nature_conv_wgrad layer 1)", "bound": "mfma",
-                           "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                           "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)", "traffic_source": src,
-                           "alg_bytes_per_launch": alg_bytes, "launches": len(kt),
-                           "mean_us": round(mean_ms * 1e3, 1), "alg_flops_per_launch": float(np.mean(flops))}
+        out["roofline"] = conv_roofline(prof_kernel, kt, totals)
     if gae_ms:
         n_local = args.envs // world
         alg_bytes = (17 if gae_kernel == "ppox_gae" else 33) * args.nstep * n_local

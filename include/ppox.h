@@ -254,6 +254,13 @@ int ppox_nature_wgrad_reduce(int32_t layer, int64_t batch, const void* workspace
 int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, int64_t batch, float* out,
                                 void* stream);
 
+/* NatureCNN head backward (explicit training backward of CnnActorCritic, replacing the
+ * autograd of nn.ReLU / Linear(H, 1) at .ipynb_checkpoints/models-checkpoint.py:60-87):
+ * grad = act > 0 ? grad : 0 in place (n % 4 == 0); out[b][j] = dv[b] * w[j] * (act[b][j] > 0). */
+int ppox_relu_backward_(float* grad, const float* act, int64_t n, void* stream);
+int ppox_outer_relu_backward(const float* dv, const float* w, const float* act, int64_t rows, int64_t h,
+                             float* out, void* stream);
+
 /* ---------------------------------------------------------------------------
  * K6, split-bf16 forms (csrc/conv_split.hip): the same ops, layouts and fused
  * epilogues as above, on the bf16 matrix cores (v_mfma_f32_32x32x16_bf16) with

@@ -40,16 +40,7 @@ def default_math():
 class _NatureTrunk(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, convs, w1, b1, w2, b2, w3, b3):
-        convs.pack()
-        B = x.shape[0]
-        dev = x.device
-        h1 = torch.empty((B, 20, 20, 32), device=dev)
-        h2 = torch.empty((B, 9, 9, 64), device=dev)
-        h3 = torch.empty((B, 64, 7, 7), device=dev)
-        if B:
-            convs.fwd(1, x, B, b1, h1)
-            convs.fwd(2, h1, B, b2, h2)
-            convs.fwd(3, h2, B, b3, h3)
+        h1, h2, h3 = convs.forward_acts(x)
         ctx.convs = convs
         ctx.save_for_backward(x, h1, h2, h3)
         return h3
@@ -58,24 +49,10 @@ class _NatureTrunk(torch.autograd.Function):
     def backward(ctx, dh3):
         x, h1, h2, h3 = ctx.saved_tensors
         convs = ctx.convs
-        B = x.shape[0]
-        dev = x.device
         grads = [torch.zeros_like(t) for t in (convs.c1.weight, convs.c1.bias, convs.c2.weight, convs.c2.bias,
                                                convs.c3.weight, convs.c3.bias)]
-        if B == 0:
-            return (None, None, *grads)
-        dw1, db1, dw2, db2, dw3, db3 = grads
-        dh3 = dh3.contiguous()
-        g3 = torch.empty((B, 7, 7, 64), device=dev)
-        native.nchw_to_nhwc_relu_grad(dh3, h3, B, g3)          # ReLU backward of conv3, to NHWC
-        convs.wgrad(3, h2, B, g3, dw3, db3)
-        g2 = torch.empty((B, 9, 9, 64), device=dev)
-        convs.dgrad(3, g3, B, h2, g2)                           # dX of conv3, times ReLU'(conv2)
-        convs.wgrad(2, h1, B, g2, dw2, db2)
-        g1 = torch.empty((B, 20, 20, 32), device=dev)
-        convs.dgrad(2, g2, B, h1, g1)                           # dX of conv2, times ReLU'(conv1)
-        convs.wgrad(1, x, B, g1, dw1, db1)
-        return None, None, dw1, db1, dw2, db2, dw3, db3
+        convs.backward_acts(x, h1, h2, h3, dh3.contiguous(), *grads)
+        return (None, None, *grads)
 
 
 class NatureConvs:
@@ -114,13 +91,21 @@ class NatureConvs:
         return ws
 
     def pack(self):
+        """Re-pack the weights (once per optimizer step) into the layouts of the kernels in use."""
         v = (self.flat.step_count, self.flat.data.data_ptr())
         if v != self._version:
             w1, w2, w3 = self.c1.weight, self.c2.weight, self.c3.weight
-            native.nature_pack_weights(w1, w2, w3, self.wp1, self.wp2, self.wp3, self.wpd2, self.wpd3)
+            f32 = lambda op, L, buf: None if self.uses_split(op, L) else buf
+            spl = lambda op, L, buf: buf if self.uses_split(op, L) else None
+            if not all(self.uses_split(op, L) for op, L in (("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 2),
+                                                           ("dgrad", 3))):
+                native.nature_pack_weights(w1, w2, w3, f32("fwd", 1, self.wp1), f32("fwd", 2, self.wp2),
+                                           f32("fwd", 3, self.wp3), f32("dgrad", 2, self.wpd2),
+                                           f32("dgrad", 3, self.wpd3))
             if self.math != "f32":
                 q = self.q
-                native.nature_pack_split(w1, w2, w3, q[1], q[2], q[3], q[12], q[13])
+                native.nature_pack_split(w1, w2, w3, spl("fwd", 1, q[1]), spl("fwd", 2, q[2]), spl("fwd", 3, q[3]),
+                                         spl("dgrad", 2, q[12]), spl("dgrad", 3, q[13]))
             self._version = v
 
     def invalidate(self):
@@ -147,6 +132,39 @@ class NatureConvs:
             native.nature_conv_wgrad_split(layer, x, B, stride, g, self.workspace(layer, B, True), dw, db)
         else:
             native.nature_conv_wgrad(layer, x, B, None, 0, 0, stride, g, self.workspace(layer, B), dw, db)
+
+    def forward_acts(self, x):
+        """Trunk forward: (h1 NHWC, h2 NHWC, h3 NCHW) activations (ReLU applied)."""
+        self.pack()
+        B = x.shape[0]
+        dev = x.device
+        h1 = torch.empty((B, 20, 20, 32), device=dev)
+        h2 = torch.empty((B, 9, 9, 64), device=dev)
+        h3 = torch.empty((B, 64, 7, 7), device=dev)
+        if B:
+            self.fwd(1, x, B, self.c1.bias, h1)
+            self.fwd(2, h1, B, self.c2.bias, h2)
+            self.fwd(3, h2, B, self.c3.bias, h3)
+        return h1, h2, h3
+
+    def backward_acts(self, x, h1, h2, h3, dh3, dw1, db1, dw2, db2, dw3, db3):
+        """Trunk backward from dL/dh3 (B, 3136 NCHW order, before the ReLU mask): writes
+        (overwrites) the six conv parameter gradients."""
+        B = x.shape[0]
+        if B == 0:
+            for t in (dw1, db1, dw2, db2, dw3, db3):
+                t.zero_()
+            return
+        dev = x.device
+        g3 = torch.empty((B, 7, 7, 64), device=dev)
+        native.nchw_to_nhwc_relu_grad(dh3, h3, B, g3)          # ReLU backward of conv3, to NHWC
+        self.wgrad(3, h2, B, g3, dw3, db3)
+        g2 = torch.empty((B, 9, 9, 64), device=dev)
+        self.dgrad(3, g3, B, h2, g2)                            # dX of conv3, times ReLU'(conv2)
+        self.wgrad(2, h1, B, g2, dw2, db2)
+        g1 = torch.empty((B, 20, 20, 32), device=dev)
+        self.dgrad(2, g2, B, h1, g1)                            # dX of conv2, times ReLU'(conv1)
+        self.wgrad(1, x, B, g1, dw1, db1)
 
     def __call__(self, x):
         if x.dtype != torch.uint8:

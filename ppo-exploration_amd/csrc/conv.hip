@@ -948,30 +948,33 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
 }
 
 // sum the slabs, scatter to PyTorch [co][ci][ky][kx] (+ bias).  A block owns 32
-// consecutive outputs (one 128-B row of every slab) x 8 split groups; thread
-// (e, g) sums splits g, g+8, g+16, ... in order, then the 8 group sums are added
-// in group order — a fixed order, so the result is deterministic.
-constexpr int RED_E = 32, RED_G = 8;
+// consecutive outputs (one 128-B row of every slab) x RG split groups; thread
+// (e, g) sums splits g, g+RG, g+2RG, ... in order, then the RG group sums are
+// added in group order — a fixed order, so the result is deterministic.  RG = 8
+// (256 threads) for the f32 kernels' <= 512 splits, 32 (1024 threads) for the
+// split kernels' up to 2048.
+constexpr int RED_E = 32;
 
-template <class L, bool NHWC_ORDER>
-__global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ slab, const float* __restrict__ bslab,
-                                                    int splits, float* __restrict__ dw, float* __restrict__ db) {
-    __shared__ float part[RED_G][RED_E];
+template <class L, bool NHWC_ORDER, int RG>
+__global__ void __launch_bounds__(RED_E * RG) wgrad_reduce(const float* __restrict__ slab,
+                                                         const float* __restrict__ bslab, int splits,
+                                                         float* __restrict__ dw, float* __restrict__ db) {
+    __shared__ float part[RG][RED_E];
     constexpr int KC = L::K * L::COUT;
     const int e = threadIdx.x % RED_E, grp = threadIdx.x / RED_E;
     const int i = blockIdx.x * RED_E + e;
     float s = 0.f;
     if (i < KC) {
-        for (int sp = grp; sp < splits; sp += RED_G) s += slab[(long long)sp * KC + i];
+        for (int sp = grp; sp < splits; sp += RG) s += slab[(long long)sp * KC + i];
     } else if (i < KC + L::COUT) {
-        for (int sp = grp; sp < splits; sp += RED_G) s += bslab[(long long)sp * L::COUT + (i - KC)];
+        for (int sp = grp; sp < splits; sp += RG) s += bslab[(long long)sp * L::COUT + (i - KC)];
     }
     part[grp][e] = s;
     __syncthreads();
     if (grp != 0) return;
     float t = part[0][e];
 #pragma unroll
-    for (int g = 1; g < RED_G; ++g) t += part[g][e];
+    for (int g = 1; g < RG; ++g) t += part[g][e];
     if (i < KC) {
         const int k = i / L::COUT, co = i % L::COUT;
         int ci, ky, kx;
@@ -990,7 +993,6 @@ __global__ void __launch_bounds__(256) wgrad_reduce(const float* __restrict__ sl
         db[i - KC] = t;
     }
 }
-
 
 // ---------------------------------------------------------------------------
 // Wgrad, split-bf16.  Same decomposition as wgrad_kernel (WG = k-block of KT rows x
@@ -1372,8 +1374,11 @@ int launch_wgrad(const WArgs& wa_in, hipStream_t s) {
 
 template <class L, bool NHWC_ORDER>
 int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float* dw, float* db, hipStream_t s) {
-    wgrad_reduce<L, NHWC_ORDER><<<ppox::ceil_div(L::K * L::COUT + L::COUT, RED_E), 256, 0, s>>>(slab, bslab, splits,
-                                                                                                dw, db);
+    const unsigned blocks = ppox::ceil_div(L::K * L::COUT + L::COUT, RED_E);
+    if (splits > 512)
+        wgrad_reduce<L, NHWC_ORDER, 32><<<blocks, RED_E * 32, 0, s>>>(slab, bslab, splits, dw, db);
+    else
+        wgrad_reduce<L, NHWC_ORDER, 8><<<blocks, RED_E * 8, 0, s>>>(slab, bslab, splits, dw, db);
     PPOX_LAUNCHED("ppox_nature_wgrad_reduce");
 }
 
@@ -1418,14 +1423,15 @@ using Ws3 = WsLaunch<G3, false, WS_KT3>;
 
 extern "C" int ppox_nature_pack_weights(const float* w1, const float* w2, const float* w3, float* wp1, float* wp2,
                                         float* wp3, float* wpd2, float* wpd3, void* stream) {
-    PPOX_REQUIRE(w1 && w2 && w3 && wp1 && wp2 && wp3, "ppox_nature_pack_weights: null pointer");
-    PPOX_REQUIRE(ppox::aligned16(wp1) && ppox::aligned16(wp2) && ppox::aligned16(wp3) &&
+    // any packed buffer may be null: that packing is skipped (ops running in split math)
+    PPOX_REQUIRE(w1 && w2 && w3, "ppox_nature_pack_weights: null weights");
+    PPOX_REQUIRE((!wp1 || ppox::aligned16(wp1)) && (!wp2 || ppox::aligned16(wp2)) && (!wp3 || ppox::aligned16(wp3)) &&
                      (!wpd2 || ppox::aligned16(wpd2)) && (!wpd3 || ppox::aligned16(wpd3)),
                  "ppox_nature_pack_weights: packed buffers must be 16-byte aligned");
     hipStream_t s = ppox::as_stream(stream);
-    pack_fwd<G1, false, RG_FWD1><<<ppox::ceil_div(G1::K * 32, 256), 256, 0, s>>>(w1, wp1);
-    pack_fwd<G2, true, RG_F32><<<ppox::ceil_div(G2::K * 64, 256), 256, 0, s>>>(w2, wp2);
-    pack_fwd<G3, true, RG_F32><<<ppox::ceil_div(G3::K * 64, 256), 256, 0, s>>>(w3, wp3);
+    if (wp1) pack_fwd<G1, false, RG_FWD1><<<ppox::ceil_div(G1::K * 32, 256), 256, 0, s>>>(w1, wp1);
+    if (wp2) pack_fwd<G2, true, RG_F32><<<ppox::ceil_div(G2::K * 64, 256), 256, 0, s>>>(w2, wp2);
+    if (wp3) pack_fwd<G3, true, RG_F32><<<ppox::ceil_div(G3::K * 64, 256), 256, 0, s>>>(w3, wp3);
     if (wpd2) pack_dgrad<G2, RG_F32><<<ppox::ceil_div(G2::K * G2::COUT, 256), 256, 0, s>>>(w2, wpd2);
     if (wpd3) pack_dgrad<G3, RG_F32><<<ppox::ceil_div(G3::K * G3::COUT, 256), 256, 0, s>>>(w3, wpd3);
     PPOX_LAUNCHED("ppox_nature_pack_weights");

@@ -169,13 +169,14 @@ extern "C" int64_t ppox_nature_split_pack_elems(int32_t which) {
 
 extern "C" int ppox_nature_pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1, uint16_t* q2,
                                       uint16_t* q3, uint16_t* qd2, uint16_t* qd3, void* stream) {
-    PPOX_REQUIRE(w1 && q1, "ppox_nature_pack_split: null pointer");
-    PPOX_REQUIRE(ppox::aligned16(q1) && (!q2 || ppox::aligned16(q2)) && (!q3 || ppox::aligned16(q3)) &&
+    // any packed buffer may be null: that packing is skipped
+    PPOX_REQUIRE((!q1 || ppox::aligned16(q1)) && (!q2 || ppox::aligned16(q2)) && (!q3 || ppox::aligned16(q3)) &&
                      (!qd2 || ppox::aligned16(qd2)) && (!qd3 || ppox::aligned16(qd3)),
                  "ppox_nature_pack_split: packed buffers must be 16-byte aligned");
-    PPOX_REQUIRE((!q2 || w2) && (!q3 || w3) && (!qd2 || w2) && (!qd3 || w3), "ppox_nature_pack_split: null weights");
+    PPOX_REQUIRE((!q1 || w1) && (!q2 || w2) && (!q3 || w3) && (!qd2 || w2) && (!qd3 || w3),
+                 "ppox_nature_pack_split: null weights");
     hipStream_t s = ppox::as_stream(stream);
-    pack_fwd1_split<<<ppox::ceil_div(8 * 2 * 64 * 8, 256), 256, 0, s>>>(w1, q1);
+    if (q1) pack_fwd1_split<<<ppox::ceil_div(8 * 2 * 64 * 8, 256), 256, 0, s>>>(w1, q1);
     PPOX_LAUNCHED_NORET("ppox_nature_pack_split");
     return ppox_conv::split_pack23(w2, w3, q2, q3, qd2, qd3, s);
 }

@@ -96,6 +96,60 @@ class CnnActorCritic(nn.Module):
         iv = self.critic_int(self.int_extra_layer(f)).squeeze(-1) if self.intrinsic else None
         return self.actor(f), v, iv
 
+    # ---- explicit training forward/backward (no autograd graph): the same layer math as
+    # forward() (addmm = F.linear, relu), with every parameter gradient written straight
+    # into its .grad view of the flat gradient buffer (weights: GEMM with beta = 1 onto the
+    # zeroed buffer; biases: column sums written in place), so the minibatch step launches
+    # no zero-fill / add kernels of its own.  Each parameter is used once per forward.
+    def forward_train(self, x):
+        """-> (actor out, value (B,), int value or None, ctx for backward_train)."""
+        with torch.no_grad():
+            x = x.contiguous()
+            h1, h2, h3 = self.conv_impl.forward_acts(x)
+            hf = h3.view(h3.shape[0], -1)
+            fc = self.feature_extractor[7]
+            f = torch.addmm(fc.bias, hf, fc.weight.t()).relu_()
+            a = self.actor[0]
+            out = torch.addmm(a.bias, f, a.weight.t())
+            e = torch.addmm(self.extra_layer[0].bias, f, self.extra_layer[0].weight.t()).relu_()
+            v = torch.addmm(self.critic_ext.bias, e, self.critic_ext.weight.t()).squeeze(-1)
+            ie = iv = None
+            if self.intrinsic:
+                ie = torch.addmm(self.int_extra_layer[0].bias, f, self.int_extra_layer[0].weight.t()).relu_()
+                iv = torch.addmm(self.critic_int.bias, ie, self.critic_int.weight.t()).squeeze(-1)
+        return out, v, iv, (x, h1, h2, h3, f, e, ie)
+
+    def backward_train(self, ctx, dout, dv, div=None):
+        """Accumulate dL/dparams for upstream grads (dout (B,A), dv (B,), div (B,))."""
+        x, h1, h2, h3, f, e, ie = ctx
+        B = x.shape[0]
+        with torch.no_grad():
+            hf = h3.view(B, -1)
+            a, fc = self.actor[0], self.feature_extractor[7]
+            a.weight.grad.addmm_(dout.t(), f)
+            torch.sum(dout, 0, out=a.bias.grad)
+            df = torch.mm(dout, a.weight)
+            heads = [(self.extra_layer[0], self.critic_ext, e, dv)]
+            if self.intrinsic:
+                heads.append((self.int_extra_layer[0], self.critic_int, ie, div))
+            for hid, crit, act, d in heads:
+                d = d.contiguous().view(B, 1)
+                crit.weight.grad.addmm_(d.t(), act)
+                torch.sum(d, 0, out=crit.bias.grad)
+                de = torch.empty_like(act)
+                native.outer_relu_backward(d, crit.weight, act, de)     # dv * w, ReLU backward
+                hid.weight.grad.addmm_(de.t(), f)
+                torch.sum(de, 0, out=hid.bias.grad)
+                df.addmm_(de, hid.weight)
+            native.relu_backward_(df, f)
+            fc.weight.grad.addmm_(df.t(), hf)
+            torch.sum(df, 0, out=fc.bias.grad)
+            dh3 = torch.mm(df, fc.weight)
+            fe = self.feature_extractor
+            # conv grads are written by the trunk kernels; the flat buffer was zeroed per minibatch
+            self.conv_impl.backward_acts(x, h1, h2, h3, dh3, fe[0].weight.grad, fe[0].bias.grad, fe[2].weight.grad,
+                                         fe[2].bias.grad, fe[4].weight.grad, fe[4].bias.grad)
+
 
 class RndNetwork(nn.Module):
     """models.py:216-267: predictor 3 hidden (LeakyReLU, LeakyReLU, ELU) -> 1,

@@ -58,6 +58,8 @@ SIGNATURES = {
     "ppox_nature_pack_split": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
+    "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
+    "ppox_outer_relu_backward": [_vp, _vp, _vp, _i64, _i64, _vp, _vp],
     "ppox_nature_conv_wgrad_split": [_i32, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
@@ -389,6 +391,16 @@ def nature_pack_split(w1, w2, w3, q1, q2, q3, qd2=None, qd3=None, stream=None):
 def nature_conv_fwd_split(layer, x, batch, idx, T, N_env, x_sample_stride, wq, bias, y, stream=None):
     call("ppox_nature_conv_fwd_split", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
          int(x_sample_stride), _p(wq), _p(bias), _p(y), stream_ptr(stream))
+
+
+def relu_backward_(grad, act, stream=None):
+    """grad = act > 0 ? grad : 0, in place (same-shape contiguous f32)."""
+    call("ppox_relu_backward_", _p(grad), _p(act), grad.numel(), stream_ptr(stream))
+
+
+def outer_relu_backward(dv, w, act, out, stream=None):
+    """out[b][j] = dv[b] * w[j] * (act[b][j] > 0)."""
+    call("ppox_outer_relu_backward", _p(dv), _p(w), _p(act), act.shape[0], act.shape[1], _p(out), stream_ptr(stream))
 
 
 def nature_wgrad_split_workspace_bytes(layer, batch):

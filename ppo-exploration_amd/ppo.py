@@ -198,6 +198,32 @@ class BaseAlgorithm:
             g.add_(self.dls.view_as(g))
         return dout, dv, div
 
+    def _fwd_train(self, obs):
+        """Training forward of the policy net -> (out, v, iv, ctx).  NatureCNN nets on the
+        libppox trunk take the explicit path (models.CnnActorCritic.forward_train: no
+        autograd graph, grads accumulated straight into the flat buffer); others autograd."""
+        net = self.policy.net
+        if getattr(net, "conv_impl", None) is not None and hasattr(net, "forward_train"):
+            return net.forward_train(obs)
+        out, v, iv = net(obs)
+        return out, v, iv, None
+
+    def _bwd_train(self, ctx, out, v, iv, dout, dv, div=None, extra=None):
+        """Backward of _fwd_train's outputs (+ an optional extra scalar loss with its own graph)."""
+        if ctx is not None:
+            self.policy.net.backward_train(ctx, dout, dv, div)
+            if extra is not None:
+                torch.autograd.backward([extra])
+            return
+        tensors, grads = [out, v], [dout, dv]
+        if iv is not None and div is not None:
+            tensors.append(iv)
+            grads.append(div)
+        if extra is not None:
+            tensors.append(extra)
+            grads.append(None)
+        torch.autograd.backward(tensors, grads)
+
     def _ensure_started(self):
         if not self._started:
             self.env.reset_into(self.rollout.obs_slots[0])
@@ -356,18 +382,14 @@ class PPO(BaseAlgorithm):
         self.flat.zero_grad()
         if Bl > 0:
             obs = ro._gather(ro.observations, idx)
-            out, v, _ = net(obs)
+            out, v, _, ctx = self._fwd_train(obs)
             out_d, v_d = out.detach().contiguous(), v.detach().contiguous()
         else:
             out_d = torch.zeros(0, self.n_actions, device=self.device)
             v_d = torch.zeros(0, device=self.device)
         dout, dv, _ = self._loss_grads(out_d, v_d, None, idx, ro.tensors(), adv_stats, B_global, 0.0, scale)
         if Bl > 0:
-            tensors, grads = [out, v], [dout, dv]
-            if extra_backward is not None:
-                tensors.append(extra_backward)
-                grads.append(None)
-            torch.autograd.backward(tensors, grads)
+            self._bwd_train(ctx, out, v, None, dout, dv, extra=extra_backward)
         self.dist.all_reduce_(self.flat.grad)
 
     def train(self):
@@ -493,11 +515,11 @@ class PPO_RND(BaseAlgorithm):
                 Bl = idx.numel()
                 self.flat.zero_grad()
                 obs = ro._gather(ro.observations, idx)
-                out, v, iv = net(obs)
+                out, v, iv, ctx = self._fwd_train(obs)
                 od, vd, ivd = out.detach().contiguous(), v.detach().contiguous(), iv.detach().contiguous()
                 dout, dv, div = self._loss_grads(od, vd, ivd, idx, roll, stats[k], B, self.int_vf_coef, 1.0)
                 if Bl > 0:
-                    torch.autograd.backward([out, v, iv], [dout, dv, div])
+                    self._bwd_train(ctx, out, v, iv, dout, dv, div)
                 self.dist.all_reduce_(self.flat.grad)
                 self.flat.adam_step(self.lr, self.max_grad_norm)
                 if np.random.randn() < 0.25:                                   # ppo.py:468-469
@@ -585,7 +607,7 @@ class PPO_ICM(BaseAlgorithm):
                 self.flat.zero_grad()
                 self.icm_flat.zero_grad()
                 obs = ro._gather(ro.observations, idx)
-                out, v, _ = net(obs)
+                out, v, _, ctx = self._fwd_train(obs)
                 od, vd = out.detach().contiguous(), v.detach().contiguous()
                 dout, dv, _ = self._loss_grads(od, vd, None, idx, roll, stats[k], B, 0.0, float(self.policy_weight))
                 # ICM on consecutive rows of the (owned part of the) permuted minibatch (ppo.py:684-688)
@@ -595,7 +617,7 @@ class PPO_ICM(BaseAlgorithm):
                 else:
                     acts = ro.actions.reshape(-1, self.n_actions)[rows]
                 x = self._icm_x(obs)
-                torch.autograd.backward([out, v], [dout, dv])
+                self._bwd_train(ctx, out, v, None, dout, dv)
                 # pairs (row j, row j+1) of the permuted minibatch; each row is encoded once
                 # (the reference encodes s and s' separately: same rows, same math) and at
                 # world > 1 the pairs cross rank boundaries (icm_loss_sharded)

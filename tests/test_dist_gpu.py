@@ -66,11 +66,16 @@ def _rank(rank, world, port, path, q, algo):
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("algo", ["PPO", "PPO_ICM"])
-def test_two_ranks_match_one_rank(algo):
+@pytest.mark.parametrize("algo,math", [("PPO", "split"), ("PPO", "f32"), ("PPO_ICM", "f32")])
+def test_two_ranks_match_one_rank(algo, math, monkeypatch):
     """PPO_ICM: the ICM pairs (row j, row j+1) of each global minibatch cross the rank
-    boundary; icm_loss_sharded exchanges features so the update equals one rank's."""
+    boundary; icm_loss_sharded exchanges features so the update equals one rank's.
+    The decomposition is checked with exact-f32 conv math; split-bf16 math reorders
+    more (3 x 2^-22 per product): after Adam's sign-normalised first steps a few
+    near-zero-gradient weights can then land ~2 lr apart between the 1- and 2-rank
+    runs, so the strict weight tolerance is applied to it on PPO only."""
     import ppo
+    monkeypatch.setenv("PPOX_CONV_MATH", math)  # inherited by the spawned ranks
     np.random.seed(11)
     torch.manual_seed(11)
     ref = getattr(ppo, algo)(**CFG)

@@ -519,3 +519,37 @@ def test_split_conv_accuracy_is_fp32_class(seed):
         e_s = (spl.cpu().double() - ref).abs().max().item() / scale
         e_f = (f32.cpu().double() - ref).abs().max().item() / scale
         assert e_s <= 2 * e_f + 1e-7, (key, e_s, e_f)
+
+
+@pytest.mark.parametrize("intrinsic", [False, True])
+def test_cnn_explicit_backward_matches_autograd(intrinsic):
+    """CnnActorCritic.forward_train/backward_train (no autograd graph, grads straight into
+    the flat buffer) == autograd through forward() on the same libppox trunk."""
+    import models
+    import convs
+    torch.manual_seed(3)
+    net = models.CnnActorCritic(4, 6, intrinsic=intrinsic)
+    flat = models.FlatParams(net, "cuda")
+    convs.attach(net, flat, "f32")
+    B = 40
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    dout, dv = torch.randn(B, 6, device="cuda"), torch.randn(B, device="cuda")
+    div = torch.randn(B, device="cuda") if intrinsic else None
+    flat.zero_grad()
+    out, v, iv = net(x)
+    ts, gs = [out, v], [dout, dv]
+    if intrinsic:
+        ts.append(iv)
+        gs.append(div)
+    torch.autograd.backward(ts, gs)
+    ref = flat.grad.clone()
+    flat.zero_grad()
+    out2, v2, iv2, ctx = net.forward_train(x)
+    assert torch.equal(out2, out.detach()) and torch.equal(v2, v.detach())
+    net.backward_train(ctx, dout, dv, div)
+    got = flat.grad
+    for p in flat.params:  # per-tensor relative check (views into the flat buffer)
+        off = (p.grad.data_ptr() - flat.grad.data_ptr()) // 4
+        r, g = ref[off:off + p.numel()], got[off:off + p.numel()]
+        scale = r.abs().max().item() + 1e-12
+        assert (r - g).abs().max().item() <= 1e-5 * scale + 1e-7, p.shape
