@@ -28,6 +28,10 @@ SPLIT_OPS = {("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 3), ("wgrad", 1), ("w
 # ops whose split kernel exists but is not faster than the f32 one at the training batch
 # (measured, tools/conv_bench.py); "split" mode runs them in f32
 SPLIT_SLOWER = {("dgrad", 2)}
+# bf16-plane hand-off of conv2's output grad (dgrad3 -> dgrad2/wgrad2, no split arithmetic
+# in the consumers): implemented and tested, but measured slower at B = 16384 (dgrad2 is
+# bound by its operand traffic at 32 output channels, not by the split), so off by default
+PLANES_HANDOFF = False
 
 
 def default_math():
@@ -159,6 +163,15 @@ class NatureConvs:
         g3 = torch.empty((B, 7, 7, 64), device=dev)
         native.nchw_to_nhwc_relu_grad(dh3, h3, B, g3)          # ReLU backward of conv3, to NHWC
         self.wgrad(3, h2, B, g3, dw3, db3)
+        if self.math == "split" and PLANES_HANDOFF:
+            # conv2's output grad handed over as bf16 planes (3, B, 9, 9, 64)
+            g2p = torch.empty((3, B, 9, 9, 64), dtype=torch.int16, device=dev)
+            native.nature_conv_dgrad_split_ex(3, g3, 0, B, self.q[13], h2, g2p, 1)
+            native.nature_conv_wgrad_split_ex(2, h1, B, 0, g2p, 1, self.workspace(2, B, True), dw2, db2)
+            g1 = torch.empty((B, 20, 20, 32), device=dev)
+            native.nature_conv_dgrad_split_ex(2, g2p, 1, B, self.q[12], h1, g1, 0)
+            self.wgrad(1, x, B, g1, dw1, db1)
+            return
         g2 = torch.empty((B, 9, 9, 64), device=dev)
         self.dgrad(3, g3, B, h2, g2)                            # dX of conv3, times ReLU'(conv2)
         self.wgrad(2, h1, B, g2, dw2, db2)

@@ -505,6 +505,172 @@ __global__ void pack_split_gemm(const float* __restrict__ w, uint16_t* __restric
     q[split_frag_index(k, col, NOUT, 2)] = p2;
 }
 
+// dgrad whose output (the previous layer's ReLU-masked output grad) is written as its
+// three exact bf16 planes [3][batch][pos][ci] (plane stride batch * NPOS * CIN) for
+// consumers that take split operands (dgrad/wgrad of the layer below: no split there)
+template <class L>
+struct DgradPMSplitOut : DgradPMProblem<L, 1> {
+    using Base = DgradPMProblem<L, 1>;
+    __device__ static void store_pre(const Args& a, const typename Base::Tile& t, int row, int ci, float acc,
+                                     float m) {
+        const long long n = t.n0 + row;
+        if (n >= a.batch) return;
+        const long long o = (n * Base::NPOS + t.pos) * L::CIN + ci, ps = a.batch * Base::NPOS * L::CIN;
+        uint16_t p0, p1, p2;
+        split3(m > 0.f ? acc : 0.f, p0, p1, p2);
+        uint16_t* y = reinterpret_cast<uint16_t*>(a.y);
+        y[o] = p0;
+        y[o + ps] = p1;
+        y[o + 2 * ps] = p2;
+    }
+};
+
+// Dgrad (position-major, as DgradPMProblem) whose input output-grad G comes as bf16
+// planes, ROW-PERSISTENT: a workgroup owns 128 samples x one input row iy and walks the
+// row's IW positions, their K chunks (1-4 taps x 32 channels each) forming one pipelined
+// stream — a lone position has only 2-8 chunks, too few to amortise a pipeline fill.
+// The A chunk (128 rows x 32 channels x 3 planes) is staged in LDS as planes (80-B rows:
+// conflict-free b128 reads) and read as MFMA fragments directly (no split arithmetic);
+// B as igemm_split_kernel.  A position's ReLU-mask operands are loaded when its first
+// chunk starts, its outputs stored after its last.
+constexpr int PAST = 40;  // bf16 per LDS row (32 + 8 pad)
+
+template <class L>
+__global__ void __launch_bounds__(256, 2) igemm_planes_kernel(Args a, const u32x4* __restrict__ wq) {
+    using Prob = DgradPMProblem<L, 1>;
+    constexpr int NOUT = Prob::NOUT, NT = NOUT / 32, BMR = 128, CPT = Prob::CPT, NPOS = Prob::NPOS;
+    constexpr int BQ = 2 * NT * 3 * 64, BV = (BQ + 255) / 256;
+    constexpr int APL = BMR * PAST;  // bf16 per LDS plane
+    __shared__ __attribute__((aligned(16))) uint16_t As[2][3 * APL];
+    __shared__ u32x4 Bs[2][BQ];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    // block -> (sample tile, input row), XCD-aware: one XCD walks the rows of a sample tile
+    const long long w = xcd_remap(blockIdx.x, gridDim.x);
+    const long long n0 = (w / L::IH) * BMR;
+    const int iy = (int)(w % L::IH);
+    int ky0, ny;
+    tap_range<L::S, L::OH, L::KH>(iy, ky0, ny);
+    auto xtaps = [](int ix, int& kx0, int& nx) { tap_range<L::S, L::OW, L::KW>(ix, kx0, nx); };
+
+    // A units: 3 planes x 128 rows x 4 groups of 8 channels = 1536 x 16 B, 6 per thread
+    const uint16_t* g = reinterpret_cast<const uint16_t*>(a.x);
+    const long long ps = a.batch * (long long)(L::P * L::COUT);
+    const uint16_t* base[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const int u = i * 256 + tid, p = u >> 9, row = (u & 511) >> 2, q = u & 3;
+        long long n = n0 + row;
+        n = n < a.batch ? n : n0;  // rows past the end: a valid clamped row, never stored
+        base[i] = g + p * ps + n * (L::P * L::COUT) + q * 8;
+    }
+    auto loadA = [&](int ix, int kx0, int nx, int c, u32x4 (&r)[6]) {
+        const int tap = c / CPT, ty = tap / nx, tx = tap - ty * nx;
+        const int oy = (iy - ky0) / L::S - ty, ox = (ix - kx0) / L::S - tx;
+        const int off = (oy * L::OW + ox) * L::COUT + (c % CPT) * BK;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) r[i] = *reinterpret_cast<const u32x4*>(base[i] + off);
+    };
+    auto loadB = [&](int kx0, int nx, int c, u32x4 (&br)[BV]) {
+        const int tap = c / CPT, ty = tap / nx, tx = tap - ty * nx;
+        const int id = ((ky0 + L::S * ty) * L::KW + kx0 + L::S * tx) * CPT + c % CPT;
+        const u32x4* src = wq + (long long)id * BQ;
+#pragma unroll
+        for (int i = 0; i < BV; ++i)
+            if (i * 256 + tid < BQ) br[i] = src[i * 256 + tid];
+    };
+    auto store = [&](int buf, const u32x4 (&r)[6], const u32x4 (&br)[BV]) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int u = i * 256 + tid, p = u >> 9, row = (u & 511) >> 2, q = u & 3;
+            *reinterpret_cast<u32x4*>(&As[buf][p * APL + row * PAST + q * 8]) = r[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BV; ++i)
+            if (i * 256 + tid < BQ) Bs[buf][i * 256 + tid] = br[i];
+    };
+    // output rows / columns of this lane in the C/D layout
+    long long orow[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) orow[r] = n0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+
+    f32x16 hi[NT], lo[NT], msk[NT];
+    auto load_mask = [&](int ix) {
+        const int pos = iy * L::IW + ix;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const long long n = orow[r] < a.batch ? orow[r] : n0;
+                msk[j][r] = a.mask[(n * NPOS + pos) * L::CIN + j * 32 + (lane & 31)];
+            }
+    };
+    auto epilogue = [&](int ix) {
+        const int pos = iy * L::IW + ix;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (orow[r] < a.batch)
+                    a.y[(orow[r] * NPOS + pos) * L::CIN + j * 32 + (lane & 31)] =
+                        msk[j][r] > 0.f ? hi[j][r] + lo[j][r] : 0.f;
+            hi[j] = lo[j] = zero16();
+        }
+    };
+
+    int ix = 0, kx0, nx;
+    xtaps(0, kx0, nx);
+    int c = 0, nchunk = ny * nx * CPT;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) hi[j] = lo[j] = zero16();
+    u32x4 ra[6], rb[BV];
+    loadA(ix, kx0, nx, 0, ra);
+    loadB(kx0, nx, 0, rb);
+    store(0, ra, rb);
+    __syncthreads();
+    const int aoff = (wave * 32 + (lane & 31)) * PAST + (lane >> 5) * 8;
+    int cur = 0;
+    for (;;) {
+        // next chunk of the row's stream
+        int nix = ix, nc = c + 1, nkx0 = kx0, nnx = nx, nn = nchunk;
+        if (nc == nchunk) {
+            nix = ix + 1;
+            nc = 0;
+            if (nix < L::IW) {
+                xtaps(nix, nkx0, nnx);
+                nn = ny * nnx * CPT;
+            }
+        }
+        const bool more = nix < L::IW;
+        if (more) {
+            loadA(nix, nkx0, nnx, nc, ra);
+            loadB(nkx0, nnx, nc, rb);
+        }
+        if (c == 0) load_mask(ix);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const u32x4 af[3] = {*reinterpret_cast<const u32x4*>(&As[cur][aoff + 16 * s]),
+                                 *reinterpret_cast<const u32x4*>(&As[cur][APL + aoff + 16 * s]),
+                                 *reinterpret_cast<const u32x4*>(&As[cur][2 * APL + aoff + 16 * s])};
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+                const u32x4* B = Bs[cur] + ((s * NT + j) * 3) * 64 + lane;
+                const u32x4 bf[3] = {B[0], B[64], B[128]};
+                mfma_split6(af, bf, hi[j], lo[j]);
+            }
+        }
+        if (c + 1 == nchunk) epilogue(ix);
+        if (!more) break;
+        store(cur ^ 1, ra, rb);
+        __syncthreads();
+        cur ^= 1;
+        ix = nix;
+        c = nc;
+        kx0 = nkx0;
+        nx = nnx;
+        nchunk = nn;
+    }
+}
+
 template <class Prob>
 int launch_igemm_split(const Args& a, const uint16_t* wq, long long blocks, hipStream_t s, const char* name) {
     if (blocks == 0) return PPOX_OK;
@@ -1040,8 +1206,10 @@ __device__ inline uint2 lds_tr16(const uint8_t* p) {
     return __builtin_bit_cast(uint2, r);
 }
 
-template <class L, bool U8, int KT>
+template <class L, bool U8, int KT, bool GPL = false>
 __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
+    // GPL: the output grad G arrives as its three bf16 planes [3][batch * P][COUT]
+    // (DgradPMSplitOut); staged as is, its f32 values (bias grad) rebuilt exactly
     using C = WsCfg<L, U8, KT>;
     constexpr int COUT = L::COUT, XP = C::XP, XR = C::XR, GR = C::GR, XU = C::XU, UPX = C::UPX;
     constexpr int WKT = C::WKT, WCT = C::WCT;
@@ -1068,6 +1236,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     uint32_t xw[XU][2];
     float4 xr[XU][2];
     float4 gr[2];
+    u32x4 gq[3];
     float bsum[GW];
 #pragma unroll
     for (int e = 0; e < GW; ++e) bsum[e] = 0.f;
@@ -1126,13 +1295,24 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
                 xr[i][1] = ok ? v1 : z;
             }
         }
-        const float* sg = a.g + (unsigned long long)(ok ? mcur : mbeg) * COUT + gco;
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 g0 = *reinterpret_cast<const float4*>(sg);
-        gr[0] = ok ? g0 : z;
-        if constexpr (GW == 8) {
-            const float4 g1 = *reinterpret_cast<const float4*>(sg + 4);
-            gr[1] = ok ? g1 : z;
+        if constexpr (GPL) {
+            static_assert(GW == 8, "planes G: 8 channels per thread");
+            const unsigned long long ps = (unsigned long long)M * COUT;
+            const uint16_t* sg = reinterpret_cast<const uint16_t*>(a.g) + (unsigned long long)(ok ? mcur : mbeg) * COUT + gco;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(sg + p * ps);
+                gq[p] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+            }
+        } else {
+            const float* sg = a.g + (unsigned long long)(ok ? mcur : mbeg) * COUT + gco;
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 g0 = *reinterpret_cast<const float4*>(sg);
+            gr[0] = ok ? g0 : z;
+            if constexpr (GW == 8) {
+                const float4 g1 = *reinterpret_cast<const float4*>(sg + 4);
+                gr[1] = ok ? g1 : z;
+            }
         }
         mcur += MS;
         xp += MS;
@@ -1165,7 +1345,19 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         }
         uint8_t* gb = base + XP * C::XPB;
         const int goff = pxl * GR + (((gco >> 4) ^ tr_swz<GR>(pxl)) << 5) + (gco & 15) * 2;
-        if constexpr (GW == 8) {
+        if constexpr (GPL) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(gb + p * C::GPB + goff) = gq[p];
+            // f32 values for the bias grad: g = p0 + p1 + p2 (exact: the planes are a split)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int q = e >> 1, sh = (e & 1) * 16;
+                const float v0 = __uint_as_float(((gq[0][q] >> sh) & 0xFFFFu) << 16);
+                const float v1 = __uint_as_float(((gq[1][q] >> sh) & 0xFFFFu) << 16);
+                const float v2 = __uint_as_float(((gq[2][q] >> sh) & 0xFFFFu) << 16);
+                bsum[e] += (v0 + v1) + v2;
+            }
+        } else if constexpr (GW == 8) {
             u32x4 p0, p1, p2;
             split8(gr[0], gr[1], p0, p1, p2);
             *reinterpret_cast<u32x4*>(gb + goff) = p0;
@@ -1178,15 +1370,17 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
             *reinterpret_cast<uint2*>(gb + C::GPB + goff) = p1;
             *reinterpret_cast<uint2*>(gb + 2 * C::GPB + goff) = p2;
         }
-        bsum[0] += gr[0].x;
-        bsum[1] += gr[0].y;
-        bsum[2] += gr[0].z;
-        bsum[3] += gr[0].w;
-        if constexpr (GW == 8) {
-            bsum[4] += gr[1].x;
-            bsum[5] += gr[1].y;
-            bsum[6] += gr[1].z;
-            bsum[7] += gr[1].w;
+        if constexpr (!GPL) {
+            bsum[0] += gr[0].x;
+            bsum[1] += gr[0].y;
+            bsum[2] += gr[0].z;
+            bsum[3] += gr[0].w;
+            if constexpr (GW == 8) {
+                bsum[4] += gr[1].x;
+                bsum[5] += gr[1].y;
+                bsum[6] += gr[1].z;
+                bsum[7] += gr[1].w;
+            }
         }
     };
     // per-lane transposed-read offsets (T10): lane 4qq+pp of each 16-lane group supplies
@@ -1390,7 +1584,7 @@ int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float
 #define WS_KT3 64
 #endif
 // split wgrad: its own split-K count (~2048 pixels per split so the grid fills the chip)
-template <class L, bool U8, int KT>
+template <class L, bool U8, int KT, bool GPL = false>
 struct WsLaunch {
     using C = WsCfg<L, U8, KT>;
     static long long splits(long long batch) {
@@ -1411,7 +1605,7 @@ struct WsLaunch {
         WArgs wa{x, sample_stride, g, slab, slab + (long long)sp * L::K * L::COUT, batch, 0, sp};
         const long long M = batch * L::P;
         wa.px_per_split = ppox::ceil_div(ppox::ceil_div(M, sp), MS) * MS;
-        wgrad_split_kernel<L, U8, KT><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
+        wgrad_split_kernel<L, U8, KT, GPL><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
         PPOX_LAUNCHED_NORET("ppox_nature_conv_wgrad_split");
         return launch_wgrad_reduce<L, !U8>(slab, wa.bslab, sp, dw, db, s);
     }
@@ -1419,6 +1613,7 @@ struct WsLaunch {
 using Ws1 = WsLaunch<G1, true, 256>;
 using Ws2 = WsLaunch<G2, false, WS_KT2>;
 using Ws3 = WsLaunch<G3, false, WS_KT3>;
+using Ws2P = WsLaunch<G2, false, WS_KT2, true>;
 }  // namespace
 
 extern "C" int ppox_nature_pack_weights(const float* w1, const float* w2, const float* w3, float* wp1, float* wp2,
@@ -1591,6 +1786,22 @@ extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_
     return Ws3::run(x, 0, grad_out, batch, workspace, dw, db, s);
 }
 
+// as ppox_nature_conv_wgrad_split; grad_out_planes = 1: grad_out is the three bf16 planes
+// [3][batch][OH][OW][COUT] written by ppox_nature_conv_dgrad_split_ex (layer 2 only)
+extern "C" int ppox_nature_conv_wgrad_split_ex(int32_t layer, const void* x, int64_t batch, int64_t x_sample_stride,
+                                               const void* grad_out, int32_t grad_out_planes, void* workspace,
+                                               int64_t workspace_bytes, float* dw, float* db, void* stream) {
+    if (!grad_out_planes)
+        return ppox_nature_conv_wgrad_split(layer, x, batch, x_sample_stride, reinterpret_cast<const float*>(grad_out),
+                                            workspace, workspace_bytes, dw, db, stream);
+    PPOX_REQUIRE(layer == 2, "ppox_nature_conv_wgrad_split_ex: planes grad_out only for layer 2");
+    PPOX_REQUIRE(x && grad_out && workspace && dw && db && batch > 0, "ppox_nature_conv_wgrad_split_ex: bad arguments");
+    PPOX_REQUIRE(workspace_bytes >= Ws2P::workspace_bytes(batch), "ppox_nature_conv_wgrad_split_ex: workspace too small");
+    PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(x), "ppox_nature_conv_wgrad_split_ex: 16B alignment");
+    PPOX_REQUIRE(batch * G2::P < (1LL << 31) / 64, "ppox_nature_conv_wgrad_split_ex: batch too large");
+    return Ws2P::run(x, 0, reinterpret_cast<const float*>(grad_out), batch, workspace, dw, db, ppox::as_stream(stream));
+}
+
 extern "C" int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, int64_t batch, float* out,
                                            void* stream) {
     PPOX_REQUIRE(grad && act && out && batch >= 0, "ppox_nchw_to_nhwc_relu_grad: bad arguments");
@@ -1638,4 +1849,32 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
     }
     using D3 = DgradPMProblem<G3, 1>;
     return launch_igemm_split<D3>(a, wqd, ppox::ceil_div(batch, D3::BMR) * D3::NPOS, s, "ppox_nature_conv_dgrad_split");
+}
+
+extern "C" int ppox_nature_conv_dgrad_split_ex(int32_t layer, const void* grad_out, int32_t grad_out_planes,
+                                               int64_t batch, const uint16_t* wqd, const float* prev_act,
+                                               void* grad_in, int32_t grad_in_planes, void* stream) {
+    PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad_split_ex: layer must be 2 or 3");
+    PPOX_REQUIRE(grad_out && wqd && prev_act && grad_in && batch >= 0, "ppox_nature_conv_dgrad_split_ex: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wqd), "ppox_nature_conv_dgrad_split_ex: 16B alignment");
+    // supported forms: conv3 (f32 in) -> planes out; conv2 planes in -> f32 out
+    PPOX_REQUIRE((layer == 3 && !grad_out_planes) || (layer == 2 && !grad_in_planes),
+                 "ppox_nature_conv_dgrad_split_ex: planes in/out combination not supported for this layer");
+    if (batch == 0) return PPOX_OK;
+    Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, reinterpret_cast<float*>(grad_in), batch};
+    hipStream_t s = ppox::as_stream(stream);
+    if (layer == 3) {
+        if (!grad_in_planes)
+            return ppox_nature_conv_dgrad_split(3, reinterpret_cast<const float*>(grad_out), batch, wqd, prev_act,
+                                                reinterpret_cast<float*>(grad_in), stream);
+        using D3 = DgradPMSplitOut<G3>;
+        return launch_igemm_split<D3>(a, wqd, ppox::ceil_div(batch, D3::BMR) * D3::NPOS, s,
+                                      "ppox_nature_conv_dgrad_split_ex");
+    }
+    if (!grad_out_planes)
+        return ppox_nature_conv_dgrad_split(2, reinterpret_cast<const float*>(grad_out), batch, wqd, prev_act,
+                                            reinterpret_cast<float*>(grad_in), stream);
+    igemm_planes_kernel<G2><<<(unsigned)(ppox::ceil_div(batch, 128) * G2::IH), 256, 0, s>>>(
+        a, reinterpret_cast<const u32x4*>(wqd));
+    PPOX_LAUNCHED("ppox_nature_conv_dgrad_split_ex");
 }

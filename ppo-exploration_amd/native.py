@@ -59,6 +59,8 @@ SIGNATURES = {
     "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
+    "ppox_nature_conv_dgrad_split_ex": [_i32, _vp, _i32, _i64, _vp, _vp, _vp, _i32, _vp],
+    "ppox_nature_conv_wgrad_split_ex": [_i32, _vp, _i64, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp],
     "ppox_outer_relu_backward": [_vp, _vp, _vp, _i64, _i64, _vp, _vp],
     "ppox_nature_conv_wgrad_split": [_i32, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
@@ -133,7 +135,8 @@ def event_times_ms(name):
 
 
 _LAYERED = ("ppox_nature_conv_fwd", "ppox_nature_conv_dgrad", "ppox_nature_conv_wgrad",
-            "ppox_nature_conv_fwd_split", "ppox_nature_conv_dgrad_split", "ppox_nature_conv_wgrad_split")
+            "ppox_nature_conv_fwd_split", "ppox_nature_conv_dgrad_split", "ppox_nature_conv_wgrad_split",
+            "ppox_nature_conv_dgrad_split_ex", "ppox_nature_conv_wgrad_split_ex")
 
 
 def call(name, *args):
@@ -411,6 +414,20 @@ def nature_conv_wgrad_split(layer, x, batch, x_sample_stride, grad_out, workspac
     """dW, db of one conv layer (slabs + fixed-order reduce in one call), split-bf16 MFMA."""
     call("ppox_nature_conv_wgrad_split", int(layer), _p(x), int(batch), int(x_sample_stride), _p(grad_out),
          _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db), stream_ptr(stream))
+
+
+def nature_conv_dgrad_split_ex(layer, grad_out, grad_out_planes, batch, wqd, prev_act, grad_in, grad_in_planes,
+                               stream=None):
+    """dgrad with bf16-plane hand-off: *_planes = 1 marks an int16 (3, batch, H, W, C) tensor."""
+    call("ppox_nature_conv_dgrad_split_ex", int(layer), _p(grad_out), int(grad_out_planes), int(batch), _p(wqd),
+         _p(prev_act), _p(grad_in), int(grad_in_planes), stream_ptr(stream))
+
+
+def nature_conv_wgrad_split_ex(layer, x, batch, x_sample_stride, grad_out, grad_out_planes, workspace, dw, db,
+                               stream=None):
+    call("ppox_nature_conv_wgrad_split_ex", int(layer), _p(x), int(batch), int(x_sample_stride), _p(grad_out),
+         int(grad_out_planes), _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db),
+         stream_ptr(stream))
 
 
 def nature_conv_dgrad_split(layer, grad_out, batch, wqd, prev_act, grad_in, stream=None):
