@@ -254,6 +254,19 @@ int ppox_nature_wgrad_reduce(int32_t layer, int64_t batch, const void* workspace
 int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, int64_t batch, float* out,
                                 void* stream);
 
+/* SB3 VecNormalize (the reference's env wrapper, env.py:10-11: VecNormalize(env,
+ * norm_reward=True); stable_baselines3 0.x, not vendored — restated, parity unpinned):
+ * observations: f32(clip((x - mean) / sqrt(var + eps), -clip, clip)) in f64 (obs_rms
+ * updated with ppox_rms_update_f32 first); rewards, in place: ret = ret * gamma + r,
+ * ret_rms.update(ret) (float64 pairwise moments, Chan merge; skipped when update = 0),
+ * r = clip(r / sqrt(ret_rms.var + eps), -clip, clip), ret[dones] = 0.  n <= 524288. */
+int ppox_normalize_obs_f32_ex(const float* x, int64_t rows, int64_t cols, int64_t row_stride,
+                              const double* mean, const double* var, double eps, double clip,
+                              float* out, void* stream);
+int ppox_vecnorm_reward(float* rewards, const uint8_t* dones, double* ret, int64_t n, double gamma,
+                        double* mean, double* var, double count, double eps, double clip,
+                        int32_t update, void* stream);
+
 /* NatureCNN head backward (explicit training backward of CnnActorCritic, replacing the
  * autograd of nn.ReLU / Linear(H, 1) at .ipynb_checkpoints/models-checkpoint.py:60-87):
  * grad = act > 0 ? grad : 0 in place (n % 4 == 0); out[b][j] = dv[b] * w[j] * (act[b][j] > 0). */

@@ -13,6 +13,8 @@
 // pairwise float32 summation reproduced exactly (leaves of <= 128 elements with
 // 8 accumulators, combined in the recursion's order).
 // The Chan merge into the float64 state follows util.py:30-44 op for op.
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -105,26 +107,28 @@ struct Frame {
 };
 
 // leaf: numpy's 8-accumulator loop for 8 <= n <= 128, plain loop below 8
-template <typename F>
-__device__ float pw_leaf(F get, int off, int n) {
+// (T = float for float32 arrays, double for float64 ones: numpy's pairwise_sum is
+// the same algorithm for both)
+template <typename T = float, typename F>
+__device__ T pw_leaf(F get, int off, int n) {
     if (n < 8) {
-        float res = 0.f;
+        T res = 0;
         for (int i = 0; i < n; ++i) res = res + get(off + i);
         return res;
     }
-    float r[8];
+    T r[8];
     for (int j = 0; j < 8; ++j) r[j] = get(off + j);
     int i = 8;
     for (; i < n - (n % 8); i += 8)
         for (int j = 0; j < 8; ++j) r[j] = r[j] + get(off + i + j);
-    float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
     for (; i < n; ++i) res = res + get(off + i);
     return res;
 }
 
 // Enumerate leaves (thread 0), sum them in parallel, combine in recursion order (thread 0).
-template <typename F>
-__device__ float pairwise_sum_block(F get, int n, int* leaf_off, int* leaf_len, float* leaf_sum, int* nleaves_sh) {
+template <typename T = float, typename F>
+__device__ T pairwise_sum_block(F get, int n, int* leaf_off, int* leaf_len, T* leaf_sum, int* nleaves_sh) {
     if (threadIdx.x == 0) {
         Frame st[40];
         int sp = 0, nl = 0;
@@ -146,13 +150,13 @@ __device__ float pairwise_sum_block(F get, int n, int* leaf_off, int* leaf_len, 
     }
     __syncthreads();
     const int nl = *nleaves_sh;
-    for (int k = threadIdx.x; k < nl; k += blockDim.x) leaf_sum[k] = pw_leaf(get, leaf_off[k], leaf_len[k]);
+    for (int k = threadIdx.x; k < nl; k += blockDim.x) leaf_sum[k] = pw_leaf<T>(get, leaf_off[k], leaf_len[k]);
     __syncthreads();
-    float result = 0.f;
+    T result = 0;
     if (threadIdx.x == 0) {
         // post-order combine with a value stack
         Frame st[40];
-        float vs[40];
+        T vs[40];
         int sp = 0, vp = 0, k = 0;
         st[sp++] = Frame{0, n, 0};
         while (sp) {
@@ -171,7 +175,7 @@ __device__ float pairwise_sum_block(F get, int n, int* leaf_off, int* leaf_len, 
                 f.state = 2;
                 st[sp++] = Frame{f.off + n2, f.n - n2, 0};
             } else {
-                const float b = vs[--vp], a = vs[--vp];
+                const T b = vs[--vp], a = vs[--vp];
                 vs[vp++] = a + b;
                 --sp;
             }
@@ -215,17 +219,65 @@ __global__ void __launch_bounds__(256) scalar_rms_scale(float* __restrict__ x, i
     }
 }
 
-// ---- normalize_obs (ppo.py:117): f32(clip((x - mean) / sqrt(var + 1e-10), -5, 5)) in f64
+// ---- normalize_obs (ppo.py:117): f32(clip((x - mean) / sqrt(var + 1e-10), -5, 5)) in f64;
+// SB3 VecNormalize.normalize_obs: eps 1e-8, clip 10
 template <typename T>
 __global__ void __launch_bounds__(256) normalize_kernel(const T* __restrict__ x, long long rows, long long cols,
                                                         long long row_stride, const double* __restrict__ mean,
-                                                        const double* __restrict__ var, float* __restrict__ out) {
+                                                        const double* __restrict__ var, float* __restrict__ out,
+                                                        double eps = 1e-10, double clip = 5.0) {
     const long long total = rows * cols;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (long long)gridDim.x * blockDim.x) {
         const long long r = i / cols, c = i - r * cols;
-        const double y = ((double)x[r * row_stride + c] - mean[c]) / sqrt(var[c] + 1e-10);
-        out[i] = (float)fmin(fmax(y, -5.0), 5.0);
+        const double y = ((double)x[r * row_stride + c] - mean[c]) / sqrt(var[c] + eps);
+        out[i] = (float)fmin(fmax(y, -clip), clip);
+    }
+}
+
+// ---- SB3 VecNormalize reward path (VecNormalize.step_wait, 0.x series):
+//   ret = ret * gamma + reward                 (float64 returns, float32 rewards)
+//   ret_rms.update(ret)                        (np.mean / np.var of a float64 array:
+//                                               pairwise float64 sums; Chan merge)
+//   reward = clip(reward / sqrt(ret_rms.var + eps), -clip, clip)   (float64 -> the f32 buffer)
+//   ret[dones] = 0
+// One block (the env count per rank is a few thousand at most).
+__global__ void __launch_bounds__(256) vecnorm_reward_kernel(float* __restrict__ rew, const uint8_t* __restrict__ dones,
+                                                             double* __restrict__ ret, int n, double gamma,
+                                                             double* __restrict__ mean, double* __restrict__ var,
+                                                             double count, double eps, double clip, int update) {
+    __shared__ int leaf_off[MAX_LEAVES], leaf_len[MAX_LEAVES];
+    __shared__ double leaf_sum[MAX_LEAVES];
+    __shared__ int nl;
+    __shared__ double bm_sh, denom_sh;
+    if (update) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) ret[i] = ret[i] * gamma + (double)rew[i];
+        __syncthreads();
+        const double s = pairwise_sum_block<double>([&](int i) { return ret[i]; }, n, leaf_off, leaf_len, leaf_sum, &nl);
+        if (threadIdx.x == 0) bm_sh = s / (double)n;
+        __syncthreads();
+        const double bm = bm_sh;
+        const double q = pairwise_sum_block<double>(
+            [&](int i) {
+                const double d = ret[i] - bm;
+                return d * d;
+            },
+            n, leaf_off, leaf_len, leaf_sum, &nl);
+        if (threadIdx.x == 0) {
+            const double bv = q / (double)n;
+            double mu = *mean, vv = *var;
+            chan_merge(mu, vv, count, bm, bv * (double)n, (double)n);
+            *mean = mu;
+            *var = vv;
+        }
+    }
+    if (threadIdx.x == 0) denom_sh = sqrt(*var + eps);
+    __syncthreads();
+    const double d = denom_sh;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const double r = (double)rew[i] / d;
+        rew[i] = (float)fmin(fmax(r, -clip), clip);
+        if (dones && dones[i]) ret[i] = 0.0;
     }
 }
 
@@ -297,4 +349,27 @@ extern "C" int ppox_normalize_obs_f32(const float* x, int64_t rows, int64_t cols
     const unsigned grid = (unsigned)std::min<long long>(ppox::ceil_div(total, 256), 4096);
     normalize_kernel<float><<<grid, 256, 0, ppox::as_stream(stream)>>>(x, rows, cols, row_stride, mean, var, out);
     PPOX_LAUNCHED("ppox_normalize_obs_f32");
+}
+
+extern "C" int ppox_normalize_obs_f32_ex(const float* x, int64_t rows, int64_t cols, int64_t row_stride,
+                                         const double* mean, const double* var, double eps, double clip, float* out,
+                                         void* stream) {
+    PPOX_REQUIRE(x && mean && var && out && rows >= 0 && cols > 0 && row_stride >= cols,
+                 "ppox_normalize_obs_f32_ex: bad arguments");
+    if (rows == 0) return PPOX_OK;
+    const long long total = rows * cols;
+    const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 8192);
+    normalize_kernel<float><<<blocks, 256, 0, ppox::as_stream(stream)>>>(x, rows, cols, row_stride, mean, var, out, eps,
+                                                                         clip);
+    PPOX_LAUNCHED("ppox_normalize_obs_f32_ex");
+}
+
+extern "C" int ppox_vecnorm_reward(float* rewards, const uint8_t* dones, double* ret, int64_t n, double gamma,
+                                   double* mean, double* var, double count, double eps, double clip, int32_t update,
+                                   void* stream) {
+    PPOX_REQUIRE(rewards && ret && mean && var && n > 0, "ppox_vecnorm_reward: bad arguments");
+    PPOX_REQUIRE(n <= (int64_t)MAX_LEAVES * PW_BLOCK, "ppox_vecnorm_reward: too many envs for one block");
+    vecnorm_reward_kernel<<<1, 256, 0, ppox::as_stream(stream)>>>(rewards, dones, ret, (int)n, gamma, mean, var, count,
+                                                                  eps, clip, update);
+    PPOX_LAUNCHED("ppox_vecnorm_reward");
 }

@@ -163,6 +163,95 @@ class DeviceVecEnv:
 DeviceAtariEnv.unnormalize_obs = DeviceVecEnv.unnormalize_obs
 
 
+class VecNormalize:
+    """env.py:10-11 wraps every env in stable_baselines3's VecNormalize(env,
+    norm_reward=True).  SB3 is not vendored in the reference (README.md:19, unpinned;
+    the cmd_util import dates it to the 2020 0.x series) and is not installed here, so
+    its published algorithm is restated on the device — parity unpinned (oracle:
+    oracle/vecnorm.py restates the same numpy program; tests check the kernels against it):
+      step: obs_rms.update(obs); obs = clip((obs - mean) / sqrt(var + eps), +-clip_obs)
+            ret = ret * gamma + r; ret_rms.update(ret); r = clip(r / sqrt(ret_rms.var + eps),
+            +-clip_reward); ret[dones] = 0
+      reset: ret = 0; (training) ret_rms.update(ret); obs normalised with the current stats
+    The wrapped env's raw state stays in this wrapper (the device envs step in place);
+    episode infos keep the raw returns (Monitor sits inside VecNormalize in SB3)."""
+
+    def __init__(self, venv, training=True, norm_obs=True, norm_reward=True, clip_obs=10.0, clip_reward=10.0,
+                 gamma=0.99, epsilon=1e-8):
+        from util import RunningMeanStd
+        self.venv = venv
+        self.num_envs = venv.num_envs
+        self.observation_space, self.action_space = venv.observation_space, venv.action_space
+        self.obs_dtype = torch.float32
+        self.device = venv.device
+        self.training, self.norm_obs, self.norm_reward = training, norm_obs, norm_reward
+        self.clip_obs, self.clip_reward, self.gamma, self.epsilon = clip_obs, clip_reward, gamma, epsilon
+        D = int(np.prod(venv.observation_space.shape))
+        self.obs_rms = RunningMeanStd(shape=(D,), device=self.device)
+        self.ret_rms = RunningMeanStd(shape=(), device=self.device)
+        self.ret = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        self.raw = torch.zeros((self.num_envs, D), device=self.device)
+        self._obs = None
+
+    def __getattr__(self, name):  # env_id, seed, ... of the wrapped env
+        return getattr(self.__dict__["venv"], name)
+
+    def _normalize_into(self, out):
+        if self.norm_obs:
+            native.normalize_obs_f32_ex(self.raw, self.num_envs, self.raw.shape[1], self.raw.shape[1],
+                                        self.obs_rms.mean, self.obs_rms.var, self.epsilon, self.clip_obs, out)
+        elif out.data_ptr() != self.raw.data_ptr():
+            out.copy_(self.raw.view_as(out))
+
+    def _reward(self, rewards, dones, update):
+        """Return accumulator + ret_rms update; rewards normalised in place (norm_reward)."""
+        target = rewards if self.norm_reward else rewards.clone()
+        native.vecnorm_reward(target, dones, self.ret, self.gamma, self.ret_rms._mean, self.ret_rms._var,
+                              self.ret_rms.count, self.epsilon, self.clip_reward, update)
+        if update:
+            self.ret_rms.count += self.num_envs
+
+    def reset_into(self, obs):
+        self.venv.reset_into(self.raw)
+        self.ret.zero_()
+        if self.training and self.norm_reward:
+            zero = torch.zeros(self.num_envs, device=self.device)
+            self._reward(zero, None, True)
+        self._normalize_into(obs)
+
+    def step_into(self, obs_in, obs_out, actions, rewards, dones, done_ret=None, done_len=None):
+        self.venv.step_into(self.raw, self.raw, actions, rewards, dones, done_ret, done_len)
+        if self.training and self.norm_obs:
+            self.obs_rms.update(self.raw)
+        self._normalize_into(obs_out)
+        self._reward(rewards, dones, self.training)
+
+    def reset(self):
+        self._obs = torch.empty_like(self.raw)
+        self.reset_into(self._obs)
+        return self._obs
+
+    def step(self, actions):
+        a = torch.as_tensor(actions, device=self.device)
+        a = a.to(torch.int32).reshape(-1).contiguous() if self.action_space.__class__.__name__ == "Discrete" else None
+        nxt = torch.empty_like(self.raw)
+        rew = torch.empty(self.num_envs, device=self.device)
+        done = torch.empty(self.num_envs, dtype=torch.uint8, device=self.device)
+        dret = torch.empty(self.num_envs, device=self.device)
+        dlen = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
+        self.step_into(None, nxt, a, rew, done, dret, dlen)
+        self._obs = nxt
+        return nxt, rew, done.bool(), episode_infos(dret, dlen)
+
+    def get_original_obs(self):
+        return self.raw.clone()
+
+    def unnormalize_obs(self, obs):
+        """obs * sqrt(var + eps) + mean (ppo.py:392 feeds this to the RND obs_rms)."""
+        o = torch.as_tensor(obs, device=self.device).reshape(self.num_envs, -1).double()
+        return (o * torch.sqrt(self.obs_rms.var + self.epsilon) + self.obs_rms.mean).float()
+
+
 def episode_infos(done_ret, done_len):
     """SB3 Monitor-style infos for envs whose episode ended this step."""
     r = done_ret.cpu().numpy()
@@ -170,8 +259,11 @@ def episode_infos(done_ret, done_len):
     return [{"episode": {"r": float(r[i]), "l": int(ln[i])}} if not np.isnan(r[i]) else {} for i in range(len(r))]
 
 
-def make_env(env_id, n_envs=4, seed=0, env_offset=0, device="cuda", **kw):
-    """env.py:7-12 counterpart: the synthetic device env for env_id."""
+def make_env(env_id, n_envs=4, seed=0, env_offset=0, device="cuda", normalize=True, **kw):
+    """env.py:7-12 counterpart: the synthetic device env for env_id; vector envs are wrapped
+    in VecNormalize(norm_reward=True) as in env.py:11 (Atari envs, which the reference
+    builds in env-checkpoint.py without it, are not)."""
     if is_atari(env_id):
         return DeviceAtariEnv(env_id, n_envs, seed=seed, env_offset=env_offset, device=device, **kw)
-    return DeviceVecEnv(env_id, n_envs, seed=seed, env_offset=env_offset, device=device, **kw)
+    env = DeviceVecEnv(env_id, n_envs, seed=seed, env_offset=env_offset, device=device, **kw)
+    return VecNormalize(env, norm_reward=True) if normalize else env

@@ -59,6 +59,8 @@ SIGNATURES = {
     "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
+    "ppox_normalize_obs_f32_ex": [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _f64, _vp, _vp],
+    "ppox_vecnorm_reward": [_vp, _vp, _vp, _i64, _f64, _vp, _vp, _f64, _f64, _f64, _i32, _vp],
     "ppox_nature_conv_dgrad_split_ex": [_i32, _vp, _i32, _i64, _vp, _vp, _vp, _i32, _vp],
     "ppox_nature_conv_wgrad_split_ex": [_i32, _vp, _i64, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp],
     "ppox_outer_relu_backward": [_vp, _vp, _vp, _i64, _i64, _vp, _vp],
@@ -394,6 +396,16 @@ def nature_pack_split(w1, w2, w3, q1, q2, q3, qd2=None, qd3=None, stream=None):
 def nature_conv_fwd_split(layer, x, batch, idx, T, N_env, x_sample_stride, wq, bias, y, stream=None):
     call("ppox_nature_conv_fwd_split", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
          int(x_sample_stride), _p(wq), _p(bias), _p(y), stream_ptr(stream))
+
+
+def normalize_obs_f32_ex(x, rows, cols, row_stride, mean, var, eps, clip, out, stream=None):
+    call("ppox_normalize_obs_f32_ex", _p(x), int(rows), int(cols), int(row_stride), _p(mean), _p(var), float(eps),
+         float(clip), _p(out), stream_ptr(stream))
+
+
+def vecnorm_reward(rewards, dones, ret, gamma, mean, var, count, eps, clip, update=True, stream=None):
+    call("ppox_vecnorm_reward", _p(rewards), _p(dones), _p(ret), rewards.numel(), float(gamma), _p(mean), _p(var),
+         float(count), float(eps), float(clip), int(bool(update)), stream_ptr(stream))
 
 
 def relu_backward_(grad, act, stream=None):

@@ -580,3 +580,40 @@ def test_cnn_explicit_backward_matches_autograd(intrinsic):
         r, g = ref[off:off + p.numel()], got[off:off + p.numel()]
         scale = r.abs().max().item() + 1e-12
         assert (r - g).abs().max().item() <= 1e-5 * scale + 1e-7, p.shape
+
+
+def test_vecnormalize_matches_numpy_restatement():
+    """env.VecNormalize (device) vs oracle/vecnorm.py (SB3 0.x VecNormalize restated in
+    numpy; parity unpinned): normalised obs and rewards, returns and both running stats
+    bit-exact over 12 steps with episode ends, on a synthetic vector env."""
+    import env as E
+    from oracle.vecnorm import VecNormalizeNumpy
+    N, D = 300, 11
+    rew = torch.empty(N, device="cuda")
+    done = torch.empty(N, dtype=torch.uint8, device="cuda")
+    # full-sequence check on recorded raw inputs (kernels vs numpy, same inputs)
+    venv2 = E.DeviceVecEnv("Hopper-v2", N, seed=3, p_done=0.05)
+    raw_obs = torch.empty(N, D, device="cuda")
+    venv2.reset_into(raw_obs)
+    vn2 = E.VecNormalize(E.DeviceVecEnv("Hopper-v2", N, seed=3, p_done=0.05), norm_reward=True)
+    out = torch.empty(N, D, device="cuda")
+    vn2.reset_into(out)
+    ref2 = VecNormalizeNumpy(N, D)
+    ref2.reset(raw_obs.cpu().numpy())
+    r_raw = torch.empty(N, device="cuda")
+    d_raw = torch.empty(N, dtype=torch.uint8, device="cuda")
+    for t in range(12):
+        venv2.step_into(raw_obs, raw_obs, None, r_raw, d_raw)
+        vn2.step_into(out, out, None, rew, done)
+        assert torch.equal(d_raw, done)
+        o_r, r_r = ref2.step(raw_obs.cpu().numpy(), r_raw.cpu().numpy(), d_raw.cpu().numpy().astype(bool))
+        np.testing.assert_array_equal(out.cpu().numpy(), o_r.astype(np.float32))
+        np.testing.assert_array_equal(rew.cpu().numpy(), r_r.astype(np.float32))
+        np.testing.assert_array_equal(vn2.ret.cpu().numpy(), ref2.ret)
+        np.testing.assert_array_equal(vn2.obs_rms.mean.cpu().numpy(), ref2.obs_rms.mean)
+        np.testing.assert_array_equal(vn2.obs_rms.var.cpu().numpy(), ref2.obs_rms.var)
+        assert float(vn2.ret_rms.var.cpu()) == float(ref2.ret_rms.var)
+        assert float(vn2.ret_rms.mean.cpu()) == float(ref2.ret_rms.mean)
+    # unnormalize_obs inverts the normalisation (up to f32 rounding of the stored obs)
+    back = vn2.unnormalize_obs(out).cpu().numpy()
+    np.testing.assert_allclose(back, vn2.raw.cpu().numpy(), rtol=1e-5, atol=1e-4)

@@ -250,3 +250,20 @@ def test_simhash_sharded_apply_equals_single():
             halves.append(r)
         assert torch.equal(torch.cat(halves), r_one)
         assert torch.equal(tabs[0], one) and torch.equal(tabs[1], one)
+
+
+def test_vector_env_ppo_runs_through_vecnormalize():
+    """make_env wraps vector envs in VecNormalize (env.py:10-11): a PPO iteration on a
+    MuJoCo-shaped synthetic env trains on normalised obs/rewards (|x| <= 10)."""
+    import ppo
+    import env as E
+    np.random.seed(0)
+    torch.manual_seed(0)
+    alg = ppo.PPO(env_id="Swimmer-v3", n_envs=16, nstep=32, batch_size=64, n_epochs=2, quiet=True)
+    assert isinstance(alg.env, E.VecNormalize)
+    alg.collect_samples()
+    ro = alg.rollout
+    assert float(ro.obs_slots.abs().max()) <= 10.0 and float(ro.rewards.abs().max()) <= 10.0
+    assert alg.env.ret_rms.count > 16 * 32
+    alg.train()
+    assert np.isfinite(alg.loss_accum.cpu().numpy()).all()
