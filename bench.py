@@ -125,7 +125,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--algo", default="ppo", choices=["ppo", "rnd", "icm"])
+    p.add_argument("--algo", default="ppo", choices=["ppo", "rnd", "icm", "es"])
+    p.add_argument("--population", type=int, default=10000, help="ES: perturbations per generation")
+    p.add_argument("--es-hidden", default="64,64", help="ES: hidden layer sizes")
     p.add_argument("--envs", type=int, default=4096)
     p.add_argument("--nstep", type=int, default=128)
     p.add_argument("--epochs", type=int, default=10)
@@ -154,6 +156,9 @@ def main():
     import native
     import ppo
     import logger
+
+    if args.algo == "es":
+        return bench_es(args, world, rank, tdist)
 
     env_id = {"ppo": "BreakoutNoFrameskip-v4", "icm": "BreakoutNoFrameskip-v4",
               "rnd": "MontezumaRevengeNoFrameskip-v4"}[args.algo]
@@ -231,6 +236,67 @@ def main():
         from oracle.baseline import atari_ppo_rate
         out["cpu_baseline"] = atari_ppo_rate(args.envs, args.nstep, args.epochs, args.batch_size,
                                              threads=args.cpu_threads or None)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # AMD MI355X spec (FP64 vector); not listed in MI355X_MICROARCH.md
+
+
+def bench_es(args, world, rank, tdist):
+    """BASELINE.json config 5: ES-NSRA on Swimmer-v3 (synthetic SwimmerLike episodes of the
+    Swimmer shape, 1000 steps), --population perturbations per generation, members sharded
+    across ranks.  A step = one generation (noise, every member's episode, update, novelty
+    bookkeeping); value = population x episode steps / s (all ranks)."""
+    import numpy as np
+    import torch
+    import native
+    import logger
+    import evolution_strategies as ES
+    np.random.seed(0)
+    hidden = [int(x) for x in args.es_hidden.split(",")]
+    es = ES.EvolutionStrategy("Swimmer-v3", hidden_sizes=hidden, population_size=args.population, seed=1)
+    logger.configure("bench", "Swimmer-v3", quiet=True)
+    native.enable_event_timing(["ppox_es_evaluate"])
+    es.run(args.warmup, log_interval=10 ** 9)
+    native.enable_event_timing(["ppox_es_evaluate"])
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    t0 = time.perf_counter()
+    es.run(args.steps, log_interval=10 ** 9)
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    kt = [(ms, a) for ms, a in native.event_times_ms("ppox_es_evaluate") if a[3] > 1]  # population launches
+    native.enable_event_timing([])
+    steps = args.steps * args.population * es.T
+    out = {"metric": "env-steps/sec (ES-NSRA: population episodes + update), Swimmer-v3 shape",
+           "value": round(steps / dt, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic SwimmerLike episodes (oracle/es.py dynamics), Philox perturbations",
+           "config": {"workload": f"Swimmer-v3 ES-NSRA, {args.population} perturbations/generation",
+                      "population": args.population, "hidden": hidden, "episode_len": es.T,
+                      "n_params": es.n_params, "parallelism": f"dp{world} (members sharded)" if world > 1 else
+                      "single GPU"}}
+    if kt:
+        mean_ms = float(np.mean([t for t, _ in kt]))
+        members = float(np.mean([a[3] for _, a in kt]))
+        flops = 2.0 * members * es.T * es.n_params  # one FMA per weight per env step
+        ach = flops / (mean_ms * 1e-3) / 1e12
+        out["roofline"] = {"kernel": "ppox_es_evaluate (es_eval_kernel)", "bound": "valu-f64", "achieved": round(ach, 2),
+                           "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(ach / FP64_VECTOR_PEAK_TFLOPS, 4), "traffic": None,
+                           "mean_us": round(mean_ms * 1e3, 1), "launches": len(kt),
+                           "alg_flops_per_launch": flops}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

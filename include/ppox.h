@@ -267,6 +267,25 @@ int ppox_vecnorm_reward(float* rewards, const uint8_t* dones, double* ret, int64
                         double* mean, double* var, double count, double eps, double clip,
                         int32_t update, void* stream);
 
+/* ES-NSRA (evolution_strategies.py:103-384, csrc/es.hip), float64 throughout.
+ * ppox_es_noise: eps[p][j] ~ N(0,1) for members member0..member0+P-1 of a generation
+ *   (the population draw of :167-177; Philox, shard-invariant).
+ * ppox_es_env_noise: the synthetic env's shared noise table xi[T][D].
+ * ppox_es_evaluate: episode return of each perturbed policy w + sigma*eps[p] (eps null:
+ *   w itself, P = 1) — :147-195 evaluate/_get_rewards with the arctan MLP of :50-63 (two
+ *   hidden layers <= 64, D <= 32, A <= 8, Box/tanh head); bc (nullable, P x 2): final
+ *   state[0:2] (get_behavior_char :248-271).
+ * ppox_es_update: out[j] = sum_p coef[p] * eps[p][j], fixed order (the P^T r of :237-242). */
+int ppox_es_noise(int64_t P, int64_t n_params, int64_t member0, int64_t generation, uint64_t seed,
+                  double* eps, void* stream);
+int ppox_es_env_noise(int32_t T, int32_t D, uint64_t env_seed, double* xi, void* stream);
+int ppox_es_evaluate(const double* w, const double* eps, double sigma, int64_t P, int32_t D, int32_t H1,
+                     int32_t H2, int32_t A, int32_t T, uint64_t env_seed, const double* xi,
+                     double* fitness, double* bc, void* stream);
+int64_t ppox_es_update_workspace_bytes(int64_t P, int64_t n_params);
+int ppox_es_update(const double* eps, const double* coef, int64_t P, int64_t n_params,
+                   double* workspace, int64_t workspace_bytes, double* out, void* stream);
+
 /* NatureCNN head backward (explicit training backward of CnnActorCritic, replacing the
  * autograd of nn.ReLU / Linear(H, 1) at .ipynb_checkpoints/models-checkpoint.py:60-87):
  * grad = act > 0 ? grad : 0 in place (n % 4 == 0); out[b][j] = dv[b] * w[j] * (act[b][j] > 0). */

@@ -59,6 +59,10 @@ SIGNATURES = {
     "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
+    "ppox_es_noise": [_i64, _i64, _i64, _i64, _u64, _vp, _vp],
+    "ppox_es_env_noise": [_i32, _i32, _u64, _vp, _vp],
+    "ppox_es_evaluate": [_vp, _vp, _f64, _i64, _i32, _i32, _i32, _i32, _i32, _u64, _vp, _vp, _vp, _vp],
+    "ppox_es_update": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp],
     "ppox_normalize_obs_f32_ex": [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _f64, _vp, _vp],
     "ppox_vecnorm_reward": [_vp, _vp, _vp, _i64, _f64, _vp, _vp, _f64, _f64, _f64, _i32, _vp],
     "ppox_nature_conv_dgrad_split_ex": [_i32, _vp, _i32, _i64, _vp, _vp, _vp, _i32, _vp],
@@ -72,10 +76,12 @@ SIGNATURES = {
 _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p,
              "ppox_rms_u8_workspace_bytes": ctypes.c_int64, "ppox_nature_wgrad_splits": ctypes.c_int64,
              "ppox_nature_wgrad_workspace_bytes": ctypes.c_int64, "ppox_nature_split_pack_elems": ctypes.c_int64,
-             "ppox_nature_wgrad_split_workspace_bytes": ctypes.c_int64}
+             "ppox_nature_wgrad_split_workspace_bytes": ctypes.c_int64,
+             "ppox_es_update_workspace_bytes": ctypes.c_int64}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
                  "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32],
-                 "ppox_nature_wgrad_split_workspace_bytes": [_i32, _i64]}
+                 "ppox_nature_wgrad_split_workspace_bytes": [_i32, _i64],
+                 "ppox_es_update_workspace_bytes": [_i64, _i64]}
 
 _lib = None
 
@@ -406,6 +412,30 @@ def normalize_obs_f32_ex(x, rows, cols, row_stride, mean, var, eps, clip, out, s
 def vecnorm_reward(rewards, dones, ret, gamma, mean, var, count, eps, clip, update=True, stream=None):
     call("ppox_vecnorm_reward", _p(rewards), _p(dones), _p(ret), rewards.numel(), float(gamma), _p(mean), _p(var),
          float(count), float(eps), float(clip), int(bool(update)), stream_ptr(stream))
+
+
+# ES-NSRA (csrc/es.hip)
+def es_noise(P, n_params, member0, generation, seed, eps, stream=None):
+    call("ppox_es_noise", int(P), int(n_params), int(member0), int(generation), int(seed) & 0xFFFFFFFFFFFFFFFF,
+         _p(eps), stream_ptr(stream))
+
+
+def es_env_noise(T, D, env_seed, xi, stream=None):
+    call("ppox_es_env_noise", int(T), int(D), int(env_seed) & 0xFFFFFFFFFFFFFFFF, _p(xi), stream_ptr(stream))
+
+
+def es_evaluate(w, eps, sigma, P, D, H1, H2, A, T, env_seed, xi, fitness, bc=None, stream=None):
+    call("ppox_es_evaluate", _p(w), _p(eps), float(sigma), int(P), int(D), int(H1), int(H2), int(A), int(T),
+         int(env_seed) & 0xFFFFFFFFFFFFFFFF, _p(xi), _p(fitness), _p(bc), stream_ptr(stream))
+
+
+def es_update_workspace_bytes(P, n_params):
+    return int(load().ppox_es_update_workspace_bytes(int(P), int(n_params)))
+
+
+def es_update(eps, coef, P, n_params, workspace, out, stream=None):
+    call("ppox_es_update", _p(eps), _p(coef), int(P), int(n_params), _p(workspace),
+         workspace.numel() * workspace.element_size(), _p(out), stream_ptr(stream))
 
 
 def relu_backward_(grad, act, stream=None):

@@ -526,6 +526,63 @@ def gen_cnn(R):
     save("cnn", **out)
 
 
+
+# --------------------------------------------------------------------------
+# (10) ES-NSRA pieces: FeedForwardNetwork.predict (evolution_strategies.py:50-63),
+#      EvolutionStrategy._update_weights (:224-246), get_kNN (:273-289),
+#      calc_noveltiy_distribution (:291-297).  evolution_strategies.py imports gym and
+#      pybulletgym at module level (:8-9); the stubs below only satisfy those imports and
+#      gym.make (called by __init__, :121) — evaluate()/get_behavior_char() need MuJoCo
+#      and are not recorded.
+# --------------------------------------------------------------------------
+def gen_es(R):
+    class FakeEnv:
+        def __init__(self, obs_dim, act_dim):
+            self.observation_space = Box((obs_dim,))
+            self.action_space = Box((act_dim,))
+
+    gym = sys.modules["gym"]
+    gym.make = lambda env_id: FakeEnv(8, 2)
+    sys.modules.setdefault("pybulletgym", types.ModuleType("pybulletgym"))
+    import evolution_strategies as ES
+    out = {}
+    # predict: f64 arctan MLP, tanh head (Box)
+    np.random.seed(21)
+    net = ES.FeedForwardNetwork(FakeEnv(8, 2), hidden_sizes=[16, 12])
+    obs = np.random.randn(20, 8)
+    out["pred_w0"], out["pred_w1"], out["pred_w2"] = [w.copy() for w in net.get_weights()]
+    out["pred_obs"] = obs
+    out["pred_act"] = np.stack([net.predict(o) for o in obs]).reshape(20, -1)
+    # _update_weights on a recorded population (numpy RNG: layer-major per member, :176-186)
+    for tag, novelty, npar in (("a", 0.37, 0.5), ("b", 1.0, 0.8)):
+        np.random.seed(5 if tag == "a" else 6)
+        es = ES.EvolutionStrategy("Swimmer-v3", hidden_sizes=[16, 12], population_size=40, sigma=0.1,
+                                  learning_rate=0.01, decay=0.9995, novelty_param=npar)
+        w_before = [w.copy() for w in es.get_weights()]
+        pop = es._get_population()
+        rewards = np.random.randn(40) * 3 + 1
+        es._update_weights(rewards, pop, novelty)
+        for i in range(3):
+            out[f"upd_{tag}_w{i}_before"] = w_before[i]
+            out[f"upd_{tag}_w{i}_after"] = es.get_weights()[i].copy()
+            out[f"upd_{tag}_pop{i}"] = np.array([p[i] for p in pop])
+        out[f"upd_{tag}_rewards"] = rewards
+        out[f"upd_{tag}_meta"] = np.array([novelty, npar, 0.01, 40, 0.1, es.learning_rate])
+    # kNN novelty distance: sum of the S nearest Euclidean distances (sklearn NearestNeighbors)
+    np.random.seed(9)
+    for n in (1, 3, 10, 57):
+        arch = [np.random.randn(1, 2) for _ in range(n)]
+        bc = np.random.randn(1, 2)
+        S = min(10, n)
+        es.K = 10
+        out[f"knn_{n}_archive"] = np.concatenate(arch)
+        out[f"knn_{n}_bc"] = bc
+        out[f"knn_{n}_dist"] = np.array(es.get_kNN(arch, bc, S))
+    nov = np.abs(np.random.randn(2)) + 0.01
+    out["probs_in"] = nov
+    out["probs_out"] = np.array(es.calc_noveltiy_distribution(list(nov)))
+    save("es", **out)
+
 def main():
     if not os.path.isdir(REF):
         print("reference not present; fixtures are committed — nothing to do")
@@ -544,6 +601,7 @@ def main():
     gen_rnd(R)
     gen_icm(R)
     gen_cnn(R)
+    gen_es(R)
     return 0
 
 
