@@ -267,6 +267,18 @@ int ppox_vecnorm_reward(float* rewards, const uint8_t* dones, double* ret, int64
                         double* mean, double* var, double count, double eps, double clip,
                         int32_t update, void* stream);
 
+/* NatureCNN hidden layer Linear(3136, 512) + ReLU (.ipynb_checkpoints/models-checkpoint.py:58-59)
+ * on the split-bf16 GEMM: weights packed (once per optimizer step) by ppox_nature_fc_pack into
+ * ppox_nature_fc_pack_elems() uint16 each for the forward (W^T) and the dgrad (W) operand.
+ * fwd: f = relu(h3 @ W^T + b); dgrad: g3 (NHWC (B,7,7,64)) = (df @ W)[Flatten order] * (h3 > 0)
+ * (df = dL/df already ReLU-masked) — the trunk's ReLU backward and NCHW->NHWC fused. */
+int64_t ppox_nature_fc_pack_elems(void);
+int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_dgrad, void* stream);
+int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
+                       void* stream);
+int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
+                         void* stream);
+
 /* ES-NSRA (evolution_strategies.py:103-384, csrc/es.hip), float64 throughout.
  * ppox_es_noise: eps[p][j] ~ N(0,1) for members member0..member0+P-1 of a generation
  *   (the population draw of :167-177; Philox, shard-invariant).

@@ -32,6 +32,15 @@ SPLIT_SLOWER = {("dgrad", 2)}
 # in the consumers): implemented and tested, but measured slower at B = 16384 (dgrad2 is
 # bound by its operand traffic at 32 output channels, not by the split), so off by default
 PLANES_HANDOFF = False
+# fc forward: split-bf16 GEMM from this batch up (PPOX_FC_SPLIT_MIN overrides; measured
+# tools/fc_bench.py: 0.41 vs rocBLAS 0.45 ms at B = 16384, underfilled below ~8192)
+# fc forward: the split-bf16 GEMM is faster in isolation (tools/fc_bench.py: 0.41 vs rocBLAS
+# 0.45 ms at B = 16384) but measured slower inside the training step (same-box A/B,
+# tools/ab_fc.sh: +48 ms per iteration), so rocBLAS unless PPOX_FC_SPLIT_MIN lowers this bound
+FC_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_SPLIT_MIN", str(1 << 62)))
+# fc dgrad fused with the trunk's ReLU backward + NHWC transpose: -8 ms per iteration at the
+# 8-GPU per-rank minibatch (2048), +38 ms at 16384 (A/B, tools/ab_fc.sh) -> below this batch
+FC_DGRAD_FUSED_MAX_BATCH = int(os.environ.get("PPOX_FC_DGRAD_FUSED_MAX", "8192"))
 
 
 def default_math():
@@ -78,6 +87,11 @@ class NatureConvs:
         # split-bf16 planes (int16 storage), packed by ppox_nature_pack_split
         self.q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device=dev)
                   for k in (1, 2, 3, 12, 13)}
+        # fc layer (feature_extractor[7], 3136 -> 512) split-bf16 operands (split math only)
+        self.fc = net.feature_extractor[7]
+        nfc = native.nature_fc_pack_elems()
+        self.qfc = (torch.empty(nfc, dtype=torch.int16, device=dev), torch.empty(nfc, dtype=torch.int16, device=dev)) \
+            if self.math != "f32" else None
         self._ws = {}
         self._version = None
 
@@ -110,6 +124,7 @@ class NatureConvs:
                 q = self.q
                 native.nature_pack_split(w1, w2, w3, spl("fwd", 1, q[1]), spl("fwd", 2, q[2]), spl("fwd", 3, q[3]),
                                          spl("dgrad", 2, q[12]), spl("dgrad", 3, q[13]))
+                native.nature_fc_pack(self.fc.weight, self.qfc[0], self.qfc[1])
             self._version = v
 
     def invalidate(self):
@@ -151,17 +166,37 @@ class NatureConvs:
             self.fwd(3, h2, B, self.c3.bias, h3)
         return h1, h2, h3
 
-    def backward_acts(self, x, h1, h2, h3, dh3, dw1, db1, dw2, db2, dw3, db3):
-        """Trunk backward from dL/dh3 (B, 3136 NCHW order, before the ReLU mask): writes
-        (overwrites) the six conv parameter gradients."""
+    # ---- fc layer (split math): forward and the dgrad fused with the trunk's ReLU backward
+    def fc_forward(self, h3):
+        """f = relu(h3 @ W^T + b), h3 (B, 64, 7, 7): the split-bf16 GEMM when the batch fills
+        the chip (ceil(B/128) row tiles x 8 column blocks >= ~512 workgroups), rocBLAS below."""
+        self.pack()
+        B = h3.shape[0]
+        if B < FC_SPLIT_MIN_BATCH:
+            return torch.addmm(self.fc.bias, h3.view(B, -1), self.fc.weight.t()).relu_()
+        f = torch.empty((B, 512), device=h3.device)
+        native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f)
+        return f
+
+    def fc_dgrad_g3(self, df, h3):
+        """g3 (B, 7, 7, 64) NHWC = (df @ W) * (h3 > 0), df = dL/df after the fc ReLU."""
+        B = df.shape[0]
+        g3 = torch.empty((B, 7, 7, 64), device=df.device)
+        native.nature_fc_dgrad(df.contiguous(), B, self.qfc[1], h3, g3)
+        return g3
+
+    def backward_acts(self, x, h1, h2, h3, dh3, dw1, db1, dw2, db2, dw3, db3, g3=None):
+        """Trunk backward from dL/dh3 (B, 3136 NCHW order, before the ReLU mask) — or from
+        g3, the already masked NHWC grad: writes (overwrites) the six conv gradients."""
         B = x.shape[0]
         if B == 0:
             for t in (dw1, db1, dw2, db2, dw3, db3):
                 t.zero_()
             return
         dev = x.device
-        g3 = torch.empty((B, 7, 7, 64), device=dev)
-        native.nchw_to_nhwc_relu_grad(dh3, h3, B, g3)          # ReLU backward of conv3, to NHWC
+        if g3 is None:
+            g3 = torch.empty((B, 7, 7, 64), device=dev)
+            native.nchw_to_nhwc_relu_grad(dh3, h3, B, g3)      # ReLU backward of conv3, to NHWC
         self.wgrad(3, h2, B, g3, dw3, db3)
         if self.math == "split" and PLANES_HANDOFF:
             # conv2's output grad handed over as bf16 planes (3, B, 9, 9, 64)

@@ -388,6 +388,13 @@ __host__ __device__ constexpr long long split_frag_index(int k, int col, int nou
     return ((((long long)(ch * 2 + s) * nt + j) * 3 + p) * 64 + l) * 8 + e;
 }
 
+// Problems with LATE_EPILOGUE load their epilogue operands after the K walk (saves 16 VGPRs
+// per column tile when the walk holds many tiles)
+template <class P, class = void>
+struct late_epilogue : std::false_type {};
+template <class P>
+struct late_epilogue<P, std::void_t<decltype(P::LATE_EPILOGUE)>> : std::bool_constant<P::LATE_EPILOGUE> {};
+
 template <class Prob>
 __global__ void __launch_bounds__(256, 2) igemm_split_kernel(Args a, const u32x4* __restrict__ wq) {
     constexpr int NOUT = Prob::NOUT, NT = NOUT / 32, BMR = 128;
@@ -401,13 +408,17 @@ __global__ void __launch_bounds__(256, 2) igemm_split_kernel(Args a, const u32x4
     const int nchunk = Prob::nchunk(t);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 
-    f32x16 hi[NT], lo[NT], pre[NT];
+    constexpr bool LATE = late_epilogue<Prob>::value;
+    f32x16 hi[NT], lo[NT], pre[LATE ? 1 : NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         hi[j] = lo[j] = zero16();
+        if constexpr (!LATE) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-            pre[j][r] = Prob::prefetch(a, t, wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), j * 32 + (lane & 31));
+            for (int r = 0; r < 16; ++r)
+                pre[j][r] =
+                    Prob::prefetch(a, t, wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), j * 32 + (lane & 31));
+        }
     }
     typename Prob::Stager sa(a, t);
     static_assert(decltype(sa)::SL == 4, "four float4 slots per thread");
@@ -475,9 +486,11 @@ __global__ void __launch_bounds__(256, 2) igemm_split_kernel(Args a, const u32x4
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-            Prob::store_pre(a, t, wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), j * 32 + (lane & 31),
-                            hi[j][r] + lo[j][r], pre[j][r]);
+        for (int r = 0; r < 16; ++r) {
+            const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), col = j * 32 + (lane & 31);
+            const float e = LATE ? Prob::prefetch(a, t, row, col) : pre[LATE ? 0 : j][r];
+            Prob::store_pre(a, t, row, col, hi[j][r] + lo[j][r], e);
+        }
 }
 
 // split-pack: forward [K][COUT] (NHWC K order) / dgrad [(tap, co)][ci] of layer L,
@@ -669,6 +682,108 @@ __global__ void __launch_bounds__(256, 2) igemm_planes_kernel(Args a, const u32x
         nx = nnx;
         nchunk = nn;
     }
+}
+
+// ---------------------------------------------------------------------------
+// NatureCNN hidden linear layer Linear(3136, 512) (.ipynb_checkpoints/
+// models-checkpoint.py:58-59) on the split-bf16 implicit-GEMM kernel: a plain GEMM
+// C[M][N] = A[M][K] B[K][N] with A f32 rows (split in registers), B pre-split per
+// column block of NB (zero-padded), workgroups over (row tile, column block), the
+// column blocks of a row tile on one XCD (its A rows then come from that XCD's L2).
+//   FC_FWD:   A = h3 (M x 3136, Flatten order), B = W^T; epilogue relu(acc + bias)
+//   FC_DGRAD: A = dL/df * relu'(f) (M x 512), B = W; epilogue: the element (m, c*49 + p)
+//             goes to g3[m][p][c] (NHWC) times (h3 > 0) — the trunk's ReLU backward and
+//             NCHW -> NHWC transpose fused (replaces the dh3 round trip + nchw_to_nhwc_mask)
+// ---------------------------------------------------------------------------
+enum { FC_FWD = 0, FC_DGRAD = 1 };
+struct GemmTile {
+    long long m0, M;
+    int cb;
+};
+
+template <int K>
+struct StageGemmRows {
+    static constexpr int SL = 4;
+    const float* base[SL];
+    float4 r[SL];
+    __device__ StageGemmRows(const Args& a, const GemmTile& t) {
+        const float* x = reinterpret_cast<const float*>(a.x);
+#pragma unroll
+        for (int i = 0; i < SL; ++i) {
+            const int w = i * 256 + threadIdx.x;
+            long long m = t.m0 + (w >> 3);
+            m = m < t.M ? m : t.m0;  // rows past the end: a valid clamped row, never stored
+            base[i] = x + m * K + (w & 7) * 4;
+        }
+    }
+    __device__ inline void load(int c) {
+#pragma unroll
+        for (int i = 0; i < SL; ++i) r[i] = *reinterpret_cast<const float4*>(base[i] + c * BK);
+    }
+};
+
+template <int K_, int N_, int NB, int MODE>
+struct GemmRowsProblem {
+    static constexpr int K = K_, N = N_, NOUT = NB, MT = 1, BMR = 128, NCB = (N + NB - 1) / NB, KC = K / BK;
+    static constexpr bool LATE_EPILOGUE = true;
+    static_assert(K % BK == 0, "K multiple of 32");
+    using Tile = GemmTile;
+    using Stager = StageGemmRows<K>;
+    __device__ static bool tile(const Args& a, Tile& t) {
+        const long long w = xcd_remap(blockIdx.x, gridDim.x);
+        t.cb = (int)(w % NCB);
+        t.m0 = (w / NCB) * BMR;
+        t.M = a.batch;
+        return true;
+    }
+    __device__ static int nchunk(const Tile&) { return KC; }
+    __device__ static int bchunk_id(const Tile& t, int c) { return t.cb * KC + c; }
+    __device__ static float prefetch(const Args& a, const Tile& t, int row, int col) {
+        const int n = t.cb * NB + col;
+        if (n >= N) return 0.f;
+        if constexpr (MODE == FC_FWD) {
+            return a.bias[n];
+        } else {
+            long long m = t.m0 + row;
+            m = m < t.M ? m : t.m0;
+            return a.mask[m * N + n];
+        }
+    }
+    __device__ static void store_pre(const Args& a, const Tile& t, int row, int col, float acc, float e) {
+        const long long m = t.m0 + row;
+        const int n = t.cb * NB + col;
+        if (m >= t.M || n >= N) return;
+        if constexpr (MODE == FC_FWD) {
+            a.y[m * N + n] = fmaxf(acc + e, 0.f);
+        } else {
+            const int c = n / 49, p = n - c * 49;  // Flatten order of (64, 7, 7)
+            a.y[(m * 49 + p) * 64 + c] = e > 0.f ? acc : 0.f;
+        }
+    }
+};
+
+#ifndef FC_NB
+#define FC_NB 64  // 128 measured no faster (one workgroup per CU: 86 KB LDS, 324 registers)
+#endif
+using FcFwd = GemmRowsProblem<3136, 512, FC_NB, FC_FWD>;
+using FcDgrad = GemmRowsProblem<512, 3136, FC_NB, FC_DGRAD>;
+
+// packs B (element (k, n) = w[n * ldw + k] when TRANS, w[k * ldw + n] otherwise) into
+// split_frag_index order per column block, zero beyond N
+template <class Prob, bool TRANS>
+__global__ void pack_split_gemm_rows(const float* __restrict__ w, uint16_t* __restrict__ q) {
+    constexpr int NB = Prob::NOUT, K = Prob::K, N = Prob::N;
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)Prob::NCB * K * NB) return;
+    const int cb = (int)(i / ((long long)K * NB)), rem = (int)(i % ((long long)K * NB));
+    const int k = rem / NB, col = rem % NB, n = cb * NB + col;
+    const float v = n < N ? (TRANS ? w[(long long)n * K + k] : w[(long long)k * N + n]) : 0.f;
+    uint16_t p0, p1, p2;
+    split3(v, p0, p1, p2);
+    const long long base = (long long)cb * K * NB * 3;
+    q[base + split_frag_index(k, col, NB, 0)] = p0;
+    q[base + split_frag_index(k, col, NB, 1)] = p1;
+    q[base + split_frag_index(k, col, NB, 2)] = p2;
 }
 
 template <class Prob>
@@ -1877,4 +1992,41 @@ extern "C" int ppox_nature_conv_dgrad_split_ex(int32_t layer, const void* grad_o
     igemm_planes_kernel<G2><<<(unsigned)(ppox::ceil_div(batch, 128) * G2::IH), 256, 0, s>>>(
         a, reinterpret_cast<const u32x4*>(wqd));
     PPOX_LAUNCHED("ppox_nature_conv_dgrad_split_ex");
+}
+
+// ---- NatureCNN fc layer (3136 -> 512) on the split-bf16 GEMM ----------------------
+extern "C" int64_t ppox_nature_fc_pack_elems(void) { return 3LL * FcFwd::NCB * FcFwd::K * FcFwd::NOUT; }
+
+extern "C" int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_dgrad, void* stream) {
+    PPOX_REQUIRE(w && (q_fwd || q_dgrad), "ppox_nature_fc_pack: bad arguments");
+    PPOX_REQUIRE((!q_fwd || ppox::aligned16(q_fwd)) && (!q_dgrad || ppox::aligned16(q_dgrad)),
+                 "ppox_nature_fc_pack: 16B alignment");
+    hipStream_t s = ppox::as_stream(stream);
+    if (q_fwd)
+        pack_split_gemm_rows<FcFwd, true><<<ppox::ceil_div((long long)FcFwd::NCB * FcFwd::K * FcFwd::NOUT, 256), 256, 0,
+                                            s>>>(w, q_fwd);
+    if (q_dgrad)
+        pack_split_gemm_rows<FcDgrad, false><<<ppox::ceil_div((long long)FcDgrad::NCB * FcDgrad::K * FcDgrad::NOUT, 256),
+                                               256, 0, s>>>(w, q_dgrad);
+    PPOX_LAUNCHED("ppox_nature_fc_pack");
+}
+
+extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
+                                  void* stream) {
+    PPOX_REQUIRE(h3 && q_fwd && bias && f && batch >= 0, "ppox_nature_fc_fwd: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd), "ppox_nature_fc_fwd: 16B alignment");
+    if (batch == 0) return PPOX_OK;
+    Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch};
+    return launch_igemm_split<FcFwd>(a, q_fwd, ppox::ceil_div(batch, 128) * FcFwd::NCB, ppox::as_stream(stream),
+                                     "ppox_nature_fc_fwd");
+}
+
+extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
+                                    void* stream) {
+    PPOX_REQUIRE(df && q_dgrad && h3 && g3 && batch >= 0, "ppox_nature_fc_dgrad: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(q_dgrad), "ppox_nature_fc_dgrad: 16B alignment");
+    if (batch == 0) return PPOX_OK;
+    Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch};
+    return launch_igemm_split<FcDgrad>(a, q_dgrad, ppox::ceil_div(batch, 128) * FcDgrad::NCB, ppox::as_stream(stream),
+                                       "ppox_nature_fc_dgrad");
 }

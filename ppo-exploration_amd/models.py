@@ -80,6 +80,10 @@ class CnnActorCritic(nn.Module):
         self.conv_impl = None  # set by convs.attach()
 
     def trunk(self, x):
+        if self.conv_impl is not None and self.conv_impl.math != "f32" and not torch.is_grad_enabled():
+            # inference (collect): the split-bf16 fc GEMM straight off the conv trunk
+            h1, h2, h3 = self.conv_impl.forward_acts(x.contiguous())
+            return self.conv_impl.fc_forward(h3)
         if self.conv_impl is not None:
             h = self.conv_impl(x)
         else:
@@ -108,7 +112,10 @@ class CnnActorCritic(nn.Module):
             h1, h2, h3 = self.conv_impl.forward_acts(x)
             hf = h3.view(h3.shape[0], -1)
             fc = self.feature_extractor[7]
-            f = torch.addmm(fc.bias, hf, fc.weight.t()).relu_()
+            if self.conv_impl.math != "f32":
+                f = self.conv_impl.fc_forward(h3)
+            else:
+                f = torch.addmm(fc.bias, hf, fc.weight.t()).relu_()
             a = self.actor[0]
             out = torch.addmm(a.bias, f, a.weight.t())
             e = torch.addmm(self.extra_layer[0].bias, f, self.extra_layer[0].weight.t()).relu_()
@@ -144,11 +151,15 @@ class CnnActorCritic(nn.Module):
             native.relu_backward_(df, f)
             fc.weight.grad.addmm_(df.t(), hf)
             torch.sum(df, 0, out=fc.bias.grad)
-            dh3 = torch.mm(df, fc.weight)
             fe = self.feature_extractor
+            import convs as _convs
+            if self.conv_impl.math != "f32" and B < _convs.FC_DGRAD_FUSED_MAX_BATCH:  # masked NHWC grad directly
+                dh3, g3 = None, self.conv_impl.fc_dgrad_g3(df, h3)
+            else:
+                dh3, g3 = torch.mm(df, fc.weight), None
             # conv grads are written by the trunk kernels; the flat buffer was zeroed per minibatch
             self.conv_impl.backward_acts(x, h1, h2, h3, dh3, fe[0].weight.grad, fe[0].bias.grad, fe[2].weight.grad,
-                                         fe[2].bias.grad, fe[4].weight.grad, fe[4].bias.grad)
+                                         fe[2].bias.grad, fe[4].weight.grad, fe[4].bias.grad, g3=g3)
 
 
 class RndNetwork(nn.Module):

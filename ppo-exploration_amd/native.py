@@ -59,6 +59,9 @@ SIGNATURES = {
     "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
+    "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
+    "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp],
+    "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_es_noise": [_i64, _i64, _i64, _i64, _u64, _vp, _vp],
     "ppox_es_env_noise": [_i32, _i32, _u64, _vp, _vp],
     "ppox_es_evaluate": [_vp, _vp, _f64, _i64, _i32, _i32, _i32, _i32, _i32, _u64, _vp, _vp, _vp, _vp],
@@ -77,11 +80,13 @@ _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p
              "ppox_rms_u8_workspace_bytes": ctypes.c_int64, "ppox_nature_wgrad_splits": ctypes.c_int64,
              "ppox_nature_wgrad_workspace_bytes": ctypes.c_int64, "ppox_nature_split_pack_elems": ctypes.c_int64,
              "ppox_nature_wgrad_split_workspace_bytes": ctypes.c_int64,
-             "ppox_es_update_workspace_bytes": ctypes.c_int64}
+             "ppox_es_update_workspace_bytes": ctypes.c_int64,
+             "ppox_nature_fc_pack_elems": ctypes.c_int64}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
                  "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32],
                  "ppox_nature_wgrad_split_workspace_bytes": [_i32, _i64],
-                 "ppox_es_update_workspace_bytes": [_i64, _i64]}
+                 "ppox_es_update_workspace_bytes": [_i64, _i64],
+                 "ppox_nature_fc_pack_elems": []}
 
 _lib = None
 
@@ -412,6 +417,25 @@ def normalize_obs_f32_ex(x, rows, cols, row_stride, mean, var, eps, clip, out, s
 def vecnorm_reward(rewards, dones, ret, gamma, mean, var, count, eps, clip, update=True, stream=None):
     call("ppox_vecnorm_reward", _p(rewards), _p(dones), _p(ret), rewards.numel(), float(gamma), _p(mean), _p(var),
          float(count), float(eps), float(clip), int(bool(update)), stream_ptr(stream))
+
+
+# NatureCNN fc layer 3136 -> 512 (split-bf16 GEMM, csrc/conv.hip)
+def nature_fc_pack_elems():
+    return int(load().ppox_nature_fc_pack_elems())
+
+
+def nature_fc_pack(w, q_fwd, q_dgrad, stream=None):
+    call("ppox_nature_fc_pack", _p(w), _p(q_fwd), _p(q_dgrad), stream_ptr(stream))
+
+
+def nature_fc_fwd(h3, batch, q_fwd, bias, f, stream=None):
+    """f = relu(h3 @ W^T + b), h3 (batch, 3136) in Flatten order."""
+    call("ppox_nature_fc_fwd", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(f), stream_ptr(stream))
+
+
+def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, stream=None):
+    """g3 (batch, 7, 7, 64) NHWC = ((df @ W) in Flatten order) * (h3 > 0)."""
+    call("ppox_nature_fc_dgrad", _p(df), int(batch), _p(q_dgrad), _p(h3), _p(g3), stream_ptr(stream))
 
 
 # ES-NSRA (csrc/es.hip)

@@ -617,3 +617,31 @@ def test_vecnormalize_matches_numpy_restatement():
     # unnormalize_obs inverts the normalisation (up to f32 rounding of the stored obs)
     back = vn2.unnormalize_obs(out).cpu().numpy()
     np.testing.assert_allclose(back, vn2.raw.cpu().numpy(), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("B", [1, 130, 1000])
+def test_fc_split_gemm_vs_fp64(B):
+    """Split-bf16 fc GEMM (3136 -> 512) forward and fused dgrad vs float64, error no
+    larger than torch's f32 GEMM's (x2 headroom)."""
+    import native
+    torch.manual_seed(B)
+    W = torch.randn(512, 3136, device="cuda") * 0.02
+    b = torch.randn(512, device="cuda") * 0.1
+    h3 = torch.relu(torch.randn(B, 3136, device="cuda"))
+    df = torch.randn(B, 512, device="cuda")
+    n = native.nature_fc_pack_elems()
+    qf, qd = torch.empty(n, dtype=torch.int16, device="cuda"), torch.empty(n, dtype=torch.int16, device="cuda")
+    native.nature_fc_pack(W, qf, qd)
+    f = torch.empty(B, 512, device="cuda")
+    native.nature_fc_fwd(h3, B, qf, b, f)
+    ref = torch.relu(h3.double() @ W.double().t() + b.double())
+    e_s = (f.double() - ref).abs().max() / ref.abs().max()
+    e_f = (torch.relu(torch.addmm(b, h3, W.t())).double() - ref).abs().max() / ref.abs().max()
+    assert e_s <= 2 * e_f + 1e-7, (float(e_s), float(e_f))
+    g3 = torch.empty(B, 7, 7, 64, device="cuda")
+    native.nature_fc_dgrad(df, B, qd, h3, g3)
+    mask = (h3.view(B, 64, 7, 7).permute(0, 2, 3, 1) > 0)
+    refd = (df.double() @ W.double()).view(B, 64, 7, 7).permute(0, 2, 3, 1) * mask
+    e_s = (g3.double() - refd).abs().max() / refd.abs().max()
+    e_f = ((df @ W).view(B, 64, 7, 7).permute(0, 2, 3, 1) * mask).double().sub(refd).abs().max() / refd.abs().max()
+    assert e_s <= 2 * e_f + 1e-7, (float(e_s), float(e_f))

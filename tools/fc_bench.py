@@ -1,0 +1,66 @@
+"""fc layer (3136 -> 512) split-bf16 GEMM vs rocBLAS f32 (torch) at the training batch:
+time and error vs float64.  Usage: python tools/fc_bench.py [B] [lib.so]"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+import native  # noqa: E402
+
+
+def t_ms(fn, iters=10):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    if len(sys.argv) > 2:
+        native.load(sys.argv[2])
+    d = "cuda"
+    torch.manual_seed(0)
+    W = torch.randn(512, 3136, device=d) * 0.02
+    b = torch.randn(512, device=d) * 0.1
+    h3 = torch.relu(torch.randn(B, 3136, device=d))
+    df = torch.randn(B, 512, device=d)
+    n = native.nature_fc_pack_elems()
+    qf, qd = torch.empty(n, dtype=torch.int16, device=d), torch.empty(n, dtype=torch.int16, device=d)
+    native.nature_fc_pack(W, qf, qd)
+    f = torch.empty(B, 512, device=d)
+    g3 = torch.empty(B, 7, 7, 64, device=d)
+    flop = 2.0 * B * 3136 * 512
+    res = {"B": B}
+    res["split_fwd_ms"] = t_ms(lambda: native.nature_fc_fwd(h3, B, qf, b, f))
+    res["rocblas_fwd_ms"] = t_ms(lambda: torch.relu(torch.addmm(b, h3, W.t())))
+    res["split_dgrad_ms"] = t_ms(lambda: native.nature_fc_dgrad(df, B, qd, h3, g3))
+    res["rocblas_dgrad_ms"] = t_ms(lambda: torch.mm(df, W))
+    for k in list(res):
+        if k.endswith("_ms"):
+            res[k.replace("_ms", "_TFs")] = round(flop / (res[k] * 1e-3) / 1e12, 1)
+            res[k] = round(res[k], 3)
+    # accuracy vs float64 (first 512 rows)
+    r = 512
+    ref = torch.relu(h3[:r].double() @ W.double().t() + b.double())
+    native.nature_fc_fwd(h3, B, qf, b, f)
+    f32 = torch.relu(torch.addmm(b, h3[:r], W.t()))
+    res["fwd_err_split"] = float((f[:r].double() - ref).abs().max() / ref.abs().max())
+    res["fwd_err_f32"] = float((f32.double() - ref).abs().max() / ref.abs().max())
+    refd = (df[:r].double() @ W.double()).view(r, 64, 7, 7).permute(0, 2, 3, 1) * (h3[:r].view(r, 64, 7, 7)
+                                                                                      .permute(0, 2, 3, 1) > 0)
+    native.nature_fc_dgrad(df, B, qd, h3, g3)
+    res["dgrad_err_split"] = float((g3[:r].double() - refd).abs().max() / refd.abs().max())
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
