@@ -762,6 +762,9 @@ struct GemmRowsProblem {
     }
 };
 
+#ifndef DGRAD2_BLOCK
+#define DGRAD2_BLOCK 0  // 1: conv2 split dgrad as the 2x2-block kernel (measured 2.26 ms vs 0.97 position-major at B = 16384: 12,800 one-per-CU workgroups of <= 8 chunks, latency-bound)
+#endif
 #ifndef FC_NB
 #define FC_NB 64  // 128 measured no faster (one workgroup per CU: 86 KB LDS, 324 registers)
 #endif
@@ -784,6 +787,130 @@ __global__ void pack_split_gemm_rows(const float* __restrict__ w, uint16_t* __re
     q[base + split_frag_index(k, col, NB, 0)] = p0;
     q[base + split_frag_index(k, col, NB, 1)] = p1;
     q[base + split_frag_index(k, col, NB, 2)] = p2;
+}
+
+// ---------------------------------------------------------------------------
+// conv2 dgrad, split-bf16, 2x2-BLOCK form.  conv2 is k4 s2, so the four input pixels
+// (2bi+u, 2bj+v) of a 2x2 block are fed by the SAME output-grad pixels (oy, ox) in
+// {bi-1, bi} x {bj-1, bj}, each through a different tap (u + 2(bi-oy), v + 2(bj-ox)).
+// A workgroup owns 128 samples x one block: every A chunk (g2 rows at one (oy, ox), 32
+// channels) is loaded and split ONCE and multiplied into four accumulator pairs (one per
+// block pixel) — 4x the MFMA work per A byte and per split of the position-major form,
+// whose 32-output-channel tiles left it bound by operand traffic.  B = the four taps'
+// split weight chunks (ppox_nature_pack_split's dgrad2 packing), staged in LDS.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256, 1) dgrad2_block_kernel(Args a, const u32x4* __restrict__ wq) {
+    using L = G2;
+    constexpr int NBLK = L::IW / 2, BMR = 128, CPT = L::COUT / BK, NPOS = L::IH * L::IW;
+    constexpr int BQ = 2 * 3 * 64;  // u32x4 per (tap, 32-co chunk): NT = 1
+    constexpr int BQ4 = 4 * BQ, BV = BQ4 / 256;
+    __shared__ __attribute__((aligned(16))) float As[2][BMR * SAST];
+    __shared__ u32x4 Bs[2][BQ4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+    const long long w = xcd_remap(blockIdx.x, gridDim.x);
+    const long long n0 = (w / (NBLK * NBLK)) * BMR;
+    const int blk = (int)(w % (NBLK * NBLK)), bi = blk / NBLK, bj = blk % NBLK;
+    // contributing output-grad pixels (at most 4), in a fixed order
+    int pys[4], pxs[4], npix = 0;
+#pragma unroll
+    for (int dy = 1; dy >= 0; --dy)
+#pragma unroll
+        for (int dx = 1; dx >= 0; --dx) {
+            const int oy = bi - dy, ox = bj - dx;
+            if (oy >= 0 && oy < L::OH && ox >= 0 && ox < L::OW) {
+                pys[npix] = oy;
+                pxs[npix] = ox;
+                ++npix;
+            }
+        }
+    const int nchunk = npix * CPT;
+    const float* g = reinterpret_cast<const float*>(a.x);
+    const float* abase[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int u = i * 256 + tid;
+        long long n = n0 + (u >> 3);
+        n = n < a.batch ? n : n0;  // rows past the end: a valid clamped row, never stored
+        abase[i] = g + n * (L::P * L::COUT) + (u & 7) * 4;
+    }
+    auto pix = [&](int c, int& oy, int& ox, int& cc) {
+        const int pi = c / CPT;
+        cc = c - pi * CPT;
+        oy = pi == 0 ? pys[0] : pi == 1 ? pys[1] : pi == 2 ? pys[2] : pys[3];
+        ox = pi == 0 ? pxs[0] : pi == 1 ? pxs[1] : pi == 2 ? pxs[2] : pxs[3];
+    };
+    auto loadA = [&](int c, float4 (&r)[4]) {
+        int oy, ox, cc;
+        pix(c, oy, ox, cc);
+        const int off = (oy * L::OW + ox) * L::COUT + cc * BK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] = *reinterpret_cast<const float4*>(abase[i] + off);
+    };
+    auto loadB = [&](int c, u32x4 (&br)[BV]) {
+        int oy, ox, cc;
+        pix(c, oy, ox, cc);
+#pragma unroll
+        for (int i = 0; i < BV; ++i) {
+            const int e = i * 256 + tid, q = e / BQ, within = e - q * BQ;  // q = block pixel (u, v)
+            const int ky = (q >> 1) + 2 * (bi - oy), kx = (q & 1) + 2 * (bj - ox);
+            br[i] = wq[(long long)((ky * L::KW + kx) * CPT + cc) * BQ + within];
+        }
+    };
+    auto store = [&](int buf, const float4 (&r)[4], const u32x4 (&br)[BV]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int u = i * 256 + tid;
+            *reinterpret_cast<float4*>(As[buf] + (u >> 3) * SAST + (u & 7) * 4) = r[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BV; ++i) Bs[buf][i * 256 + tid] = br[i];
+    };
+    f32x16 hi[4], lo[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hi[q] = lo[q] = zero16();
+    float4 ra[4];
+    u32x4 rb[BV];
+    if (nchunk > 0) {
+        loadA(0, ra);
+        loadB(0, rb);
+        store(0, ra, rb);
+    }
+    __syncthreads();
+    const int aoff = (wave * 32 + (lane & 31)) * SAST + (lane >> 5) * 8;
+    for (int c = 0; c < nchunk; ++c) {
+        const int cur = c & 1;
+        if (c + 1 < nchunk) {
+            loadA(c + 1, ra);
+            loadB(c + 1, rb);
+        }
+        const float* A = As[cur] + aoff;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            u32x4 af[3];
+            split8(*reinterpret_cast<const float4*>(A + 16 * s), *reinterpret_cast<const float4*>(A + 16 * s + 4), af[0],
+                   af[1], af[2]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const u32x4* B = Bs[cur] + q * BQ + s * 3 * 64 + lane;
+                const u32x4 bf[3] = {B[0], B[64], B[128]};
+                mfma_split6(af, bf, hi[q], lo[q]);
+            }
+        }
+        if (c + 1 < nchunk) store(cur ^ 1, ra, rb);
+        __syncthreads();
+    }
+    // epilogue: block pixel q = (u, v) -> input pixel (2bi+u, 2bj+v); x (h1 > 0)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int pos = (2 * bi + (q >> 1)) * L::IW + 2 * bj + (q & 1);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const long long n = n0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            if (n >= a.batch) continue;
+            const long long o = (n * NPOS + pos) * L::CIN + (lane & 31);
+            a.y[o] = a.mask[o] > 0.f ? hi[q][r] + lo[q][r] : 0.f;
+        }
+    }
 }
 
 template <class Prob>
@@ -1958,9 +2085,15 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
     Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch};
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 2) {
+#if DGRAD2_BLOCK
+        dgrad2_block_kernel<<<(unsigned)(ppox::ceil_div(batch, 128) * (G2::IH / 2) * (G2::IW / 2)), 256, 0, s>>>(
+            a, reinterpret_cast<const u32x4*>(wqd));
+        PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
+#else
         using D2 = DgradPMProblem<G2, 1>;
         return launch_igemm_split<D2>(a, wqd, ppox::ceil_div(batch, D2::BMR) * D2::NPOS, s,
                                       "ppox_nature_conv_dgrad_split");
+#endif
     }
     using D3 = DgradPMProblem<G3, 1>;
     return launch_igemm_split<D3>(a, wqd, ppox::ceil_div(batch, D3::BMR) * D3::NPOS, s, "ppox_nature_conv_dgrad_split");
