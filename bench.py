@@ -120,6 +120,43 @@ def gae_kernel_ms(alg, dual, reps=20):
         return None
 
 
+def gae_large_n(dual, T=128, N=1 << 20, reps=10):
+    """K1 at a size where HBM, not latency, bounds it: kernel time by graph replay."""
+    import torch
+    import native
+    f = lambda: torch.randn(T, N, device="cuda")
+    r, v = f(), f()
+    d = (torch.rand(T, N, device="cuda") < 0.01).to(torch.uint8)
+    lv, ld = torch.randn(N, device="cuda"), d[-1].contiguous()
+    outs = [torch.empty(T, N, device="cuda") for _ in range(4 if dual else 2)]
+    if dual:
+        ir, iv, liv = f(), f(), torch.randn(N, device="cuda")
+        call = lambda: native.gae_dual(r, v, d, lv, ld, ir, iv, liv, 0.99, 0.99, 0.95, *outs)
+    else:
+        call = lambda: native.gae(r, v, d, lv, ld, 0.99, 0.95, outs[0], outs[1])
+    try:
+        call()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                call()
+        g.replay()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        g.replay()
+        e.record()
+        torch.cuda.synchronize()
+    except Exception:
+        return None
+    ms = s.elapsed_time(e) / reps
+    bpe = 33 if dual else 17
+    gbs = bpe * T * N / (ms * 1e-3) / 1e9
+    return {"T": T, "N": N, "mean_us": round(ms * 1e3, 1), "alg_bytes_per_launch": bpe * T * N,
+            "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -230,7 +267,12 @@ def main():
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                                "mean_us": round(mean_ms * 1e3, 2), "alg_bytes_per_launch": alg_bytes,
                                "note": "config-size launch (graph replay of the rollout's own GAE call, "
-                                       "kernel time only) is latency-bound; tools/gae_sweep.py sweeps N"}
+                                       "kernel time only) is latency-bound; large_n: the same kernel on "
+                                       "T=128 x N=1,048,576 synthetic streams, timed live here; "
+                                       "tools/gae_sweep.py sweeps N"}
+        large = gae_large_n(gae_kernel != "ppox_gae")
+        if large:
+            out["gae_roofline"]["large_n"] = large
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, ROOT)
         from oracle.baseline import atari_ppo_rate

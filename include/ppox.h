@@ -273,6 +273,12 @@ int ppox_vecnorm_reward(float* rewards, const uint8_t* dones, double* ret, int64
  * fwd: f = relu(h3 @ W^T + b); dgrad: g3 (NHWC (B,7,7,64)) = (df @ W)[Flatten order] * (h3 > 0)
  * (df = dL/df already ReLU-masked) — the trunk's ReLU backward and NCHW->NHWC fused. */
 int64_t ppox_nature_fc_pack_elems(void);
+/* All weight packings of one optimizer step in a single launch (any output may be null):
+ * wpd2 = f32 conv2 dgrad ([(ky,kx,co)][ci]); q1..q3 / qd2, qd3 = split forms (as
+ * ppox_nature_pack_split); qfc_fwd / qfc_dgrad = fc split forms (as ppox_nature_fc_pack). */
+int ppox_nature_pack_all(const float* w1, const float* w2, const float* w3, const float* wfc, float* wpd2,
+                         uint16_t* q1, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
+                         uint16_t* qfc_fwd, uint16_t* qfc_dgrad, void* stream);
 int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_dgrad, void* stream);
 int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
                        void* stream);

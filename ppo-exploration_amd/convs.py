@@ -109,12 +109,21 @@ class NatureConvs:
         return ws
 
     def pack(self):
-        """Re-pack the weights (once per optimizer step) into the layouts of the kernels in use."""
+        """Re-pack the weights (once per optimizer step) into the layouts of the kernels in use
+        — one launch for all of them in split math (ppox_nature_pack_all)."""
         v = (self.flat.step_count, self.flat.data.data_ptr())
-        if v != self._version:
-            w1, w2, w3 = self.c1.weight, self.c2.weight, self.c3.weight
-            f32 = lambda op, L, buf: None if self.uses_split(op, L) else buf
-            spl = lambda op, L, buf: buf if self.uses_split(op, L) else None
+        if v == self._version:
+            return
+        w1, w2, w3 = self.c1.weight, self.c2.weight, self.c3.weight
+        f32 = lambda op, L, buf: None if self.uses_split(op, L) else buf
+        spl = lambda op, L, buf: buf if self.uses_split(op, L) else None
+        if self.math != "f32" and all(self.uses_split("fwd", L) for L in (1, 2, 3)) and self.uses_split("dgrad", 3):
+            q = self.q
+            native.nature_pack_all(w1, w2, w3, self.fc.weight, f32("dgrad", 2, self.wpd2), q[1], q[2], q[3],
+                                   spl("dgrad", 2, q[12]), q[13],
+                                   self.qfc[0] if FC_SPLIT_MIN_BATCH < (1 << 40) else None,
+                                   self.qfc[1] if FC_DGRAD_FUSED_MAX_BATCH > 0 else None)
+        else:
             if not all(self.uses_split(op, L) for op, L in (("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 2),
                                                            ("dgrad", 3))):
                 native.nature_pack_weights(w1, w2, w3, f32("fwd", 1, self.wp1), f32("fwd", 2, self.wp2),
@@ -125,7 +134,7 @@ class NatureConvs:
                 native.nature_pack_split(w1, w2, w3, spl("fwd", 1, q[1]), spl("fwd", 2, q[2]), spl("fwd", 3, q[3]),
                                          spl("dgrad", 2, q[12]), spl("dgrad", 3, q[13]))
                 native.nature_fc_pack(self.fc.weight, self.qfc[0], self.qfc[1])
-            self._version = v
+        self._version = v
 
     def invalidate(self):
         self._version = None

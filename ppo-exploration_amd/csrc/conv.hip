@@ -29,6 +29,7 @@
 // bias gradient is fused into the k-block-0 workgroups.  The k-blocks of one
 // M-slice are mapped to one XCD (blockIdx % 8) so their shared G rows and
 // overlapping input patches are served from that XCD's L2.
+#include <algorithm>
 #include <type_traits>
 
 #include "conv_common.h"
@@ -496,9 +497,8 @@ __global__ void __launch_bounds__(256, 2) igemm_split_kernel(Args a, const u32x4
 // split-pack: forward [K][COUT] (NHWC K order) / dgrad [(tap, co)][ci] of layer L,
 // from the PyTorch [co][ci][ky][kx] weights, into split_frag_index order
 template <class L, bool DGRAD>
-__global__ void pack_split_gemm(const float* __restrict__ w, uint16_t* __restrict__ q) {
+__device__ inline void pack_split_gemm_elem(const float* __restrict__ w, uint16_t* __restrict__ q, int i) {
     constexpr int NOUT = DGRAD ? L::CIN : L::COUT;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= L::K * L::COUT) return;
     const int k = i / NOUT, col = i % NOUT;
     int co, ci, tap;
@@ -516,6 +516,10 @@ __global__ void pack_split_gemm(const float* __restrict__ w, uint16_t* __restric
     q[split_frag_index(k, col, NOUT, 0)] = p0;
     q[split_frag_index(k, col, NOUT, 1)] = p1;
     q[split_frag_index(k, col, NOUT, 2)] = p2;
+}
+template <class L, bool DGRAD>
+__global__ void pack_split_gemm(const float* __restrict__ w, uint16_t* __restrict__ q) {
+    pack_split_gemm_elem<L, DGRAD>(w, q, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // dgrad whose output (the previous layer's ReLU-masked output grad) is written as its
@@ -774,9 +778,8 @@ using FcDgrad = GemmRowsProblem<512, 3136, FC_NB, FC_DGRAD>;
 // packs B (element (k, n) = w[n * ldw + k] when TRANS, w[k * ldw + n] otherwise) into
 // split_frag_index order per column block, zero beyond N
 template <class Prob, bool TRANS>
-__global__ void pack_split_gemm_rows(const float* __restrict__ w, uint16_t* __restrict__ q) {
+__device__ inline void pack_split_gemm_rows_elem(const float* __restrict__ w, uint16_t* __restrict__ q, long long i) {
     constexpr int NB = Prob::NOUT, K = Prob::K, N = Prob::N;
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (long long)Prob::NCB * K * NB) return;
     const int cb = (int)(i / ((long long)K * NB)), rem = (int)(i % ((long long)K * NB));
     const int k = rem / NB, col = rem % NB, n = cb * NB + col;
@@ -787,6 +790,10 @@ __global__ void pack_split_gemm_rows(const float* __restrict__ w, uint16_t* __re
     q[base + split_frag_index(k, col, NB, 0)] = p0;
     q[base + split_frag_index(k, col, NB, 1)] = p1;
     q[base + split_frag_index(k, col, NB, 2)] = p2;
+}
+template <class Prob, bool TRANS>
+__global__ void pack_split_gemm_rows(const float* __restrict__ w, uint16_t* __restrict__ q) {
+    pack_split_gemm_rows_elem<Prob, TRANS>(w, q, (long long)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -1764,11 +1771,14 @@ __global__ void pack_fwd(const float* __restrict__ w, float* __restrict__ wp) {
 
 // dgrad: [(ky, kx, co)][ci] — chunk (tap, 32 co) is a contiguous 32 x CIN block
 template <class L, bool RG>
-__global__ void pack_dgrad(const float* __restrict__ w, float* __restrict__ wp) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ inline void pack_dgrad_elem(const float* __restrict__ w, float* __restrict__ wp, int i) {
     if (i >= L::KH * L::KW * L::COUT * L::CIN) return;
     const int ci = i % L::CIN, co = (i / L::CIN) % L::COUT, tap = i / (L::CIN * L::COUT);
     wp[pack_pos<RG>(tap * L::COUT + co, ci, L::CIN, i)] = w[((co * L::CIN + ci) * L::KH + tap / L::KW) * L::KW + tap % L::KW];
+}
+template <class L, bool RG>
+__global__ void pack_dgrad(const float* __restrict__ w, float* __restrict__ wp) {
+    pack_dgrad_elem<L, RG>(w, wp, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 template <class Prob>
@@ -1856,6 +1866,39 @@ using Ws1 = WsLaunch<G1, true, 256>;
 using Ws2 = WsLaunch<G2, false, WS_KT2>;
 using Ws3 = WsLaunch<G3, false, WS_KT3>;
 using Ws2P = WsLaunch<G2, false, WS_KT2, true>;
+// Every per-optimizer-step weight packing of the training step in ONE launch (the
+// minibatch loop is launch-bound at small per-rank batches): element ranges of the
+// jobs laid end to end, null outputs skipped.
+struct PackAll {
+    const float *w1, *w2, *w3, *wfc;
+    float* wpd2;                                  // f32 dgrad2 [(tap, co)][ci]
+    uint16_t *q1, *q2, *q3, *qd2, *qd3, *qfcf, *qfcd;  // split planes
+};
+constexpr long long PA_N1 = 8 * 2 * 64 * 8, PA_N2 = (long long)G2::K * G2::COUT, PA_N3 = (long long)G3::K * G3::COUT;
+constexpr long long PA_NFC = (long long)FcFwd::NCB * FcFwd::K * FcFwd::NOUT;
+constexpr long long PA_NFCD = (long long)FcDgrad::NCB * FcDgrad::K * FcDgrad::NOUT;
+
+__global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long total) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+        long long j = i;
+        if (j < PA_N1) { if (p.q1) pack_fwd1_split_elem(p.w1, p.q1, (int)j); continue; }
+        j -= PA_N1;
+        if (j < PA_N2) { if (p.q2) pack_split_gemm_elem<G2, false>(p.w2, p.q2, (int)j); continue; }
+        j -= PA_N2;
+        if (j < PA_N3) { if (p.q3) pack_split_gemm_elem<G3, false>(p.w3, p.q3, (int)j); continue; }
+        j -= PA_N3;
+        if (j < PA_N2) { if (p.qd2) pack_split_gemm_elem<G2, true>(p.w2, p.qd2, (int)j); continue; }
+        j -= PA_N2;
+        if (j < PA_N3) { if (p.qd3) pack_split_gemm_elem<G3, true>(p.w3, p.qd3, (int)j); continue; }
+        j -= PA_N3;
+        if (j < PA_N2) { if (p.wpd2) pack_dgrad_elem<G2, RG_F32>(p.w2, p.wpd2, (int)j); continue; }
+        j -= PA_N2;
+        if (j < PA_NFC) { if (p.qfcf) pack_split_gemm_rows_elem<FcFwd, true>(p.wfc, p.qfcf, j); continue; }
+        j -= PA_NFC;
+        if (p.qfcd) pack_split_gemm_rows_elem<FcDgrad, false>(p.wfc, p.qfcd, j);
+    }
+}
+
 }  // namespace
 
 extern "C" int ppox_nature_pack_weights(const float* w1, const float* w2, const float* w3, float* wp1, float* wp2,
@@ -2162,4 +2205,18 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
     Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch};
     return launch_igemm_split<FcDgrad>(a, q_dgrad, ppox::ceil_div(batch, 128) * FcDgrad::NCB, ppox::as_stream(stream),
                                        "ppox_nature_fc_dgrad");
+}
+
+extern "C" int ppox_nature_pack_all(const float* w1, const float* w2, const float* w3, const float* wfc, float* wpd2,
+                                    uint16_t* q1, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
+                                    uint16_t* qfc_fwd, uint16_t* qfc_dgrad, void* stream) {
+    PPOX_REQUIRE(w1 && w2 && w3 && (wfc || (!qfc_fwd && !qfc_dgrad)), "ppox_nature_pack_all: null weights");
+    for (const void* q : {(const void*)wpd2, (const void*)q1, (const void*)q2, (const void*)q3, (const void*)qd2,
+                          (const void*)qd3, (const void*)qfc_fwd, (const void*)qfc_dgrad})
+        PPOX_REQUIRE(!q || ppox::aligned16(q), "ppox_nature_pack_all: packed buffers must be 16-byte aligned");
+    PackAll p{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad};
+    const long long total = PA_N1 + 3 * PA_N2 + 2 * PA_N3 + PA_NFC + (qfc_dgrad ? PA_NFCD : 0);
+    const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 4096);
+    pack_all_kernel<<<blocks, 256, 0, ppox::as_stream(stream)>>>(p, total);
+    PPOX_LAUNCHED("ppox_nature_pack_all");
 }

@@ -148,6 +148,23 @@ __device__ inline void mfma_split6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32
     lo = mfma_bf16(a[2], b[0], lo);
 }
 
+__host__ __device__ constexpr int fwd1_split_index(int c, int s, int p, int lane, int e) {
+    return (((c * 2 + s) * 3 + p) * 64 + lane) * 8 + e;
+}
+
+// one element of the conv1 forward split packing (8 chunks x 2 steps x 64 lanes x 8)
+__device__ inline void pack_fwd1_split_elem(const float* __restrict__ w, uint16_t* __restrict__ q, int t) {
+    if (t >= 8 * 2 * 64 * 8) return;
+    const int e = t & 7, lane = (t >> 3) & 63, s = (t >> 9) & 1, c = t >> 10;
+    const int h = lane >> 5, co = lane & 31;
+    const int k = (c >> 1) * 64 + (4 * (c & 1) + 2 * h + s) * 8 + e;  // natural (ci, ky, kx)
+    uint16_t p0, p1, p2;
+    split3(w[co * G1::K + k], p0, p1, p2);
+    q[fwd1_split_index(c, s, 0, lane, e)] = p0;
+    q[fwd1_split_index(c, s, 1, lane, e)] = p1;
+    q[fwd1_split_index(c, s, 2, lane, e)] = p2;
+}
+
 constexpr int MS = 32;
 
 struct WArgs {

@@ -26,9 +26,6 @@ namespace {
 // MFMA k index (s, h, e) is natural k = (c/2)*64 + (4(c&1) + 2h + s)*8 + e.
 // The weights are packed in that order, plane by plane (pack_fwd1_split).
 // ---------------------------------------------------------------------------
-__host__ __device__ constexpr int fwd1_split_index(int c, int s, int p, int lane, int e) {
-    return (((c * 2 + s) * 3 + p) * 64 + lane) * 8 + e;
-}
 
 // Persistent: the whole split weight set (48 KB) is staged in LDS once per
 // workgroup (B fragments then cost LDS, not TA, bandwidth), and each wave walks
@@ -133,16 +130,7 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
 
 // [co][ci][ky][kx] f32 -> conv1 split planes in fwd1_split_index order
 __global__ void pack_fwd1_split(const float* __restrict__ w, uint16_t* __restrict__ q) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;  // (c, s, lane, e)
-    if (t >= 8 * 2 * 64 * 8) return;
-    const int e = t & 7, lane = (t >> 3) & 63, s = (t >> 9) & 1, c = t >> 10;
-    const int h = lane >> 5, co = lane & 31;
-    const int k = (c >> 1) * 64 + (4 * (c & 1) + 2 * h + s) * 8 + e;  // natural (ci, ky, kx)
-    uint16_t p0, p1, p2;
-    split3(w[co * G1::K + k], p0, p1, p2);
-    q[fwd1_split_index(c, s, 0, lane, e)] = p0;
-    q[fwd1_split_index(c, s, 1, lane, e)] = p1;
-    q[fwd1_split_index(c, s, 2, lane, e)] = p2;
+    pack_fwd1_split_elem(w, q, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 #ifndef SPLIT_FWD1_MT

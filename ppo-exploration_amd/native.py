@@ -60,6 +60,7 @@ SIGNATURES = {
     "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
     "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
+    "ppox_nature_pack_all": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_es_noise": [_i64, _i64, _i64, _i64, _u64, _vp, _vp],
@@ -426,6 +427,12 @@ def nature_fc_pack_elems():
 
 def nature_fc_pack(w, q_fwd, q_dgrad, stream=None):
     call("ppox_nature_fc_pack", _p(w), _p(q_fwd), _p(q_dgrad), stream_ptr(stream))
+
+
+def nature_pack_all(w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, stream=None):
+    """Every weight packing of a training step in one launch (None = skip)."""
+    call("ppox_nature_pack_all", _p(w1), _p(w2), _p(w3), _p(wfc), _p(wpd2), _p(q1), _p(q2), _p(q3), _p(qd2),
+         _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), stream_ptr(stream))
 
 
 def nature_fc_fwd(h3, batch, q_fwd, bias, f, stream=None):
