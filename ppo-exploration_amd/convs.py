@@ -32,15 +32,15 @@ SPLIT_SLOWER = {("dgrad", 2)}
 # in the consumers): implemented and tested, but measured slower at B = 16384 (dgrad2 is
 # bound by its operand traffic at 32 output channels, not by the split), so off by default
 PLANES_HANDOFF = False
-# fc forward: split-bf16 GEMM from this batch up (PPOX_FC_SPLIT_MIN overrides; measured
-# tools/fc_bench.py: 0.41 vs rocBLAS 0.45 ms at B = 16384, underfilled below ~8192)
-# fc forward: the split-bf16 GEMM is faster in isolation (tools/fc_bench.py: 0.41 vs rocBLAS
-# 0.45 ms at B = 16384) but measured slower inside the training step (same-box A/B,
-# tools/ab_fc.sh: +48 ms per iteration), so rocBLAS unless PPOX_FC_SPLIT_MIN lowers this bound
-FC_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_SPLIT_MIN", str(1 << 62)))
-# fc dgrad fused with the trunk's ReLU backward + NHWC transpose: -8 ms per iteration at the
-# 8-GPU per-rank minibatch (2048), +38 ms at 16384 (A/B, tools/ab_fc.sh) -> below this batch
-FC_DGRAD_FUSED_MAX_BATCH = int(os.environ.get("PPOX_FC_DGRAD_FUSED_MAX", "8192"))
+# fc forward: the split-bf16 GEMM from this batch up, rocBLAS below (PPOX_FC_SPLIT_MIN
+# overrides).  Same-box A/B of the whole training step (tools/ab_fc.sh, after the split
+# kernel's two-deep load pipeline): -40 ms per iteration at B = 16384, +17 ms at the 8-GPU
+# per-rank minibatch (2048: 128-row tiles x 8 column blocks under-fill the chip)
+FC_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_SPLIT_MIN", "8192"))
+# fc dgrad fused with the trunk's ReLU backward + NHWC transpose (split-bf16) up to this
+# batch (PPOX_FC_DGRAD_FUSED_MAX overrides): faster than rocBLAS + nchw_to_nhwc_mask at
+# every measured batch (A/B: -33 ms per iteration at 16384, -2 ms at 2048)
+FC_DGRAD_FUSED_MAX_BATCH = int(os.environ.get("PPOX_FC_DGRAD_FUSED_MAX", str(1 << 62)))
 
 
 def default_math():

@@ -138,7 +138,8 @@ struct StageFwdNHWC {
             base[i] = x + ((n * L::IH + oy * L::S) * L::IW + ox * L::S) * L::CIN + q * 4;
         }
     }
-    __device__ inline void load(int chunk) {
+    __device__ inline void load(int chunk) { load_to(chunk, r); }
+    __device__ inline void load_to(int chunk, float4 (&r)[SL]) const {
         constexpr int CPT = L::CIN / BK;
         const int tap = chunk / CPT, ky = tap / L::KW, kx = tap % L::KW;
         const int off = (ky * L::IW + kx) * L::CIN + (chunk % CPT) * BK;
@@ -234,7 +235,8 @@ struct StageDgradPM {
             base[i] = g + (ok[i] ? n : t.n0) * (L::P * L::COUT) + (w & 7) * 4;
         }
     }
-    __device__ inline void load(int chunk) {
+    __device__ inline void load(int chunk) { load_to(chunk, r); }
+    __device__ inline void load_to(int chunk, float4 (&r)[SL]) const {
         const int tap = chunk / CPT, ty = tap / nx, tx = tap - ty * nx;
         const int oy = (iy - ky0) / L::S - ty, ox = (ix - kx0) / L::S - tx;
         const int off = (oy * L::OW + ox) * L::COUT + (chunk % CPT) * BK;
@@ -423,45 +425,33 @@ __global__ void __launch_bounds__(256, 2) igemm_split_kernel(Args a, const u32x4
     }
     typename Prob::Stager sa(a, t);
     static_assert(decltype(sa)::SL == 4, "four float4 slots per thread");
-    // three-stage pipeline: chunk c in LDS buffer c&1, chunk c+1 held in registers
-    // (pa, pb), chunk c+2's loads in flight while chunk c runs on the matrix cores
-    auto loadB = [&](int c, u32x4 (&br)[BV]) {
+    struct Stage {
+        float4 a[4];
+        u32x4 b[BV];
+    };
+    auto load = [&](int c) {
+        Stage r;
+        sa.load(c);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r.a[i] = sa.r[i];
         const u32x4* src = wq + (long long)Prob::bchunk_id(t, c) * BQ;
 #pragma unroll
         for (int i = 0; i < BV; ++i)
-            if (i * 256 + (int)threadIdx.x < BQ) br[i] = src[i * 256 + threadIdx.x];
+            if (BQ % 256 == 0 || i * 256 + (int)threadIdx.x < BQ) r.b[i] = src[i * 256 + threadIdx.x];
+        return r;
     };
-    auto store = [&](int buf, const float4 (&ar)[4], const u32x4 (&br)[BV]) {
+    auto store = [&](int buf, const Stage& r) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int w = i * 256 + threadIdx.x;
-            *reinterpret_cast<float4*>(As[buf] + (w >> 3) * SAST + (w & 7) * 4) = ar[i];
+            *reinterpret_cast<float4*>(As[buf] + (w >> 3) * SAST + (w & 7) * 4) = r.a[i];
         }
 #pragma unroll
         for (int i = 0; i < BV; ++i)
-            if (i * 256 + (int)threadIdx.x < BQ) Bs[buf][i * 256 + threadIdx.x] = br[i];
+            if (BQ % 256 == 0 || i * 256 + (int)threadIdx.x < BQ) Bs[buf][i * 256 + threadIdx.x] = r.b[i];
     };
-    float4 pa[4];
-    u32x4 pb[BV], nb[BV];
-    if (nchunk > 0) {
-        sa.load(0);
-        loadB(0, pb);
-        store(0, sa.r, pb);
-    }
-    if (nchunk > 1) {
-        sa.load(1);
-        loadB(1, pb);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pa[i] = sa.r[i];
-    }
-    __syncthreads();
     const int aoff = (wave * 32 + (lane & 31)) * SAST + (lane >> 5) * 8;
-    for (int c = 0; c < nchunk; ++c) {
-        const int cur = c & 1;
-        if (c + 2 < nchunk) {
-            sa.load(c + 2);
-            loadB(c + 2, nb);
-        }
+    auto compute = [&](int cur) {
         const float* A = As[cur] + aoff;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -475,23 +465,59 @@ __global__ void __launch_bounds__(256, 2) igemm_split_kernel(Args a, const u32x4
                 mfma_split6(af, bf, hi[j], lo[j]);
             }
         }
-        if (c + 1 < nchunk) store(cur ^ 1, pa, pb);
-        if (c + 2 < nchunk) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) pa[i] = sa.r[i];
-#pragma unroll
-            for (int i = 0; i < BV; ++i) pb[i] = nb[i];
-        }
+    };
+    // Pipeline: LDS double buffer + two register stages (x, y) that alternate roles, the
+    // walk unrolled by two, so a chunk's global loads are issued two compute phases before
+    // the LDS store that consumes them.  Loads and stores are unconditional (past the end:
+    // the last chunk again, never computed): a conditional load, or a register copy of
+    // just-loaded values, makes the compiler wait for every outstanding load.
+    if (nchunk > 0) {
+        const int last = nchunk - 1;
+        store(0, load(0));
+        Stage y = load(min(1, last));
         __syncthreads();
-    }
-#pragma unroll
-    for (int j = 0; j < NT; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), col = j * 32 + (lane & 31);
-            const float e = LATE ? Prob::prefetch(a, t, row, col) : pre[LATE ? 0 : j][r];
-            Prob::store_pre(a, t, row, col, hi[j][r] + lo[j][r], e);
+        for (int c = 0; c < nchunk; c += 2) {
+            // LDS buffer 0 holds chunk c, y chunk c + 1
+            // (sched_barrier: keep the loads ahead of, and the LDS stores behind, the MFMAs)
+            const Stage x = load(min(c + 2, last));
+            __builtin_amdgcn_sched_barrier(0);
+            compute(0);
+            __builtin_amdgcn_sched_barrier(0);
+            store(1, y);
+            __syncthreads();
+            // LDS buffer 1 holds chunk c + 1, x chunk c + 2
+            y = load(min(c + 3, last));
+            __builtin_amdgcn_sched_barrier(0);
+            if (c + 1 < nchunk) compute(1);
+            __builtin_amdgcn_sched_barrier(0);
+            store(0, x);
+            __syncthreads();
         }
+    }
+    if constexpr (LATE) {
+        // every epilogue operand load issued before the first store
+        f32x16 e[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                e[j][r] = Prob::prefetch(a, t, wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), j * 32 + (lane & 31));
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), col = j * 32 + (lane & 31);
+                Prob::store_pre(a, t, row, col, hi[j][r] + lo[j][r], e[j][r]);
+            }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), col = j * 32 + (lane & 31);
+                Prob::store_pre(a, t, row, col, hi[j][r] + lo[j][r], pre[j][r]);
+            }
+    }
 }
 
 // split-pack: forward [K][COUT] (NHWC K order) / dgrad [(tap, co)][ci] of layer L,
@@ -593,7 +619,7 @@ __global__ void __launch_bounds__(256, 2) igemm_planes_kernel(Args a, const u32x
         const u32x4* src = wq + (long long)id * BQ;
 #pragma unroll
         for (int i = 0; i < BV; ++i)
-            if (i * 256 + tid < BQ) br[i] = src[i * 256 + tid];
+            if (BQ % 256 == 0 || i * 256 + tid < BQ) br[i] = src[i * 256 + tid];
     };
     auto store = [&](int buf, const u32x4 (&r)[6], const u32x4 (&br)[BV]) {
 #pragma unroll
@@ -603,7 +629,7 @@ __global__ void __launch_bounds__(256, 2) igemm_planes_kernel(Args a, const u32x
         }
 #pragma unroll
         for (int i = 0; i < BV; ++i)
-            if (i * 256 + tid < BQ) Bs[buf][i * 256 + tid] = br[i];
+            if (BQ % 256 == 0 || i * 256 + tid < BQ) Bs[buf][i * 256 + tid] = br[i];
     };
     // output rows / columns of this lane in the C/D layout
     long long orow[16];
@@ -720,7 +746,8 @@ struct StageGemmRows {
             base[i] = x + m * K + (w & 7) * 4;
         }
     }
-    __device__ inline void load(int c) {
+    __device__ inline void load(int c) { load_to(c, r); }
+    __device__ inline void load_to(int c, float4 (&r)[SL]) const {
 #pragma unroll
         for (int i = 0; i < SL; ++i) r[i] = *reinterpret_cast<const float4*>(base[i] + c * BK);
     }
@@ -742,15 +769,15 @@ struct GemmRowsProblem {
     }
     __device__ static int nchunk(const Tile&) { return KC; }
     __device__ static int bchunk_id(const Tile& t, int c) { return t.cb * KC + c; }
+    // branch-free (clamped indices), so an epilogue can issue all its loads before any wait
     __device__ static float prefetch(const Args& a, const Tile& t, int row, int col) {
-        const int n = t.cb * NB + col;
-        if (n >= N) return 0.f;
+        const int n = t.cb * NB + col, nc = n < N ? n : N - 1;
         if constexpr (MODE == FC_FWD) {
-            return a.bias[n];
+            return a.bias[nc];
         } else {
             long long m = t.m0 + row;
             m = m < t.M ? m : t.m0;
-            return a.mask[m * N + n];
+            return a.mask[m * N + nc];
         }
     }
     __device__ static void store_pre(const Args& a, const Tile& t, int row, int col, float acc, float e) {

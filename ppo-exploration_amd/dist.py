@@ -34,6 +34,13 @@ class DistContext:
             tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=self.group)
         return t
 
+    def all_reduce_async_(self, t):
+        """Start a SUM all-reduce of `t` ordered after the work already on the current
+        stream; returns the work handle (None at world 1).  Call .wait() before reading t."""
+        if self.enabled:
+            return tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=self.group, async_op=True)
+        return None
+
     def all_gather_cat(self, t, dim):
         """Concatenate every rank's `t` along `dim` in rank order."""
         if not self.enabled:

@@ -126,8 +126,10 @@ class CnnActorCritic(nn.Module):
                 iv = torch.addmm(self.critic_int.bias, ie, self.critic_int.weight.t()).squeeze(-1)
         return out, v, iv, (x, h1, h2, h3, f, e, ie)
 
-    def backward_train(self, ctx, dout, dv, div=None):
-        """Accumulate dL/dparams for upstream grads (dout (B,A), dv (B,), div (B,))."""
+    def backward_train(self, ctx, dout, dv, div=None, dense_ready=None):
+        """Accumulate dL/dparams for upstream grads (dout (B,A), dv (B,), div (B,)).
+        `dense_ready()` is called once every non-conv gradient (fc + heads) is enqueued,
+        before the conv backward (ppo.BaseAlgorithm._bwd_reduce overlaps its all-reduce)."""
         x, h1, h2, h3, f, e, ie = ctx
         B = x.shape[0]
         with torch.no_grad():
@@ -151,6 +153,8 @@ class CnnActorCritic(nn.Module):
             native.relu_backward_(df, f)
             fc.weight.grad.addmm_(df.t(), hf)
             torch.sum(df, 0, out=fc.bias.grad)
+            if dense_ready is not None:
+                dense_ready()
             fe = self.feature_extractor
             import convs as _convs
             if self.conv_impl.math != "f32" and B < _convs.FC_DGRAD_FUSED_MAX_BATCH:  # masked NHWC grad directly

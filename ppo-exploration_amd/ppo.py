@@ -208,6 +208,25 @@ class BaseAlgorithm:
         out, v, iv = net(obs)
         return out, v, iv, None
 
+    def _bwd_reduce(self, ctx, out, v, iv, dout, dv, div=None, has_rows=True):
+        """Backward into the flat grad bucket + its all-reduce over ranks.  On the explicit
+        NatureCNN path at world > 1 the bucket is reduced in two pieces: the fc + head part
+        (flat params after the convs, 96 % of the bytes) asynchronously as soon as backward_train
+        has produced it, overlapping the conv backward, then the conv part."""
+        if has_rows and ctx is not None and self.dist.enabled:
+            net = self.policy.net
+            n0 = (net.feature_extractor[7].weight.data_ptr() - self.flat.data.data_ptr()) // 4
+            work = []
+            net.backward_train(ctx, dout, dv, div,
+                               dense_ready=lambda: work.append(self.dist.all_reduce_async_(self.flat.grad[n0:])))
+            self.dist.all_reduce_(self.flat.grad[:n0])
+            for w in work:
+                w.wait()
+            return
+        if has_rows:
+            self._bwd_train(ctx, out, v, iv, dout, dv, div)
+        self.dist.all_reduce_(self.flat.grad)
+
     def _bwd_train(self, ctx, out, v, iv, dout, dv, div=None, extra=None):
         """Backward of _fwd_train's outputs (+ an optional extra scalar loss with its own graph)."""
         if ctx is not None:
@@ -388,6 +407,9 @@ class PPO(BaseAlgorithm):
             out_d = torch.zeros(0, self.n_actions, device=self.device)
             v_d = torch.zeros(0, device=self.device)
         dout, dv, _ = self._loss_grads(out_d, v_d, None, idx, ro.tensors(), adv_stats, B_global, 0.0, scale)
+        if extra_backward is None:
+            self._bwd_reduce(ctx, out, v, None, dout, dv, has_rows=Bl > 0)
+            return
         if Bl > 0:
             self._bwd_train(ctx, out, v, None, dout, dv, extra=extra_backward)
         self.dist.all_reduce_(self.flat.grad)
@@ -518,9 +540,7 @@ class PPO_RND(BaseAlgorithm):
                 out, v, iv, ctx = self._fwd_train(obs)
                 od, vd, ivd = out.detach().contiguous(), v.detach().contiguous(), iv.detach().contiguous()
                 dout, dv, div = self._loss_grads(od, vd, ivd, idx, roll, stats[k], B, self.int_vf_coef, 1.0)
-                if Bl > 0:
-                    self._bwd_train(ctx, out, v, iv, dout, dv, div)
-                self.dist.all_reduce_(self.flat.grad)
+                self._bwd_reduce(ctx, out, v, iv, dout, dv, div, has_rows=Bl > 0)
                 self.flat.adam_step(self.lr, self.max_grad_norm)
                 if np.random.randn() < 0.25:                                   # ppo.py:468-469
                     self.train_rnd(obs)
