@@ -308,6 +308,18 @@ int ppox_es_update(const double* eps, const double* coef, int64_t P, int64_t n_p
  * autograd of nn.ReLU / Linear(H, 1) at .ipynb_checkpoints/models-checkpoint.py:60-87):
  * grad = act > 0 ? grad : 0 in place (n % 4 == 0); out[b][j] = dv[b] * w[j] * (act[b][j] > 0). */
 int ppox_relu_backward_(float* grad, const float* act, int64_t n, void* stream);
+/* Column-reduction gradients of the NatureCNN heads (models-checkpoint.py:60-87; the
+ * explicit backward of models.CnnActorCritic) in one pass over f, e, de, df (rows x h):
+ * w_actor (A x h) = dout^T f, b_actor = sum dout, w_critic (h) = dv^T e, b_critic = sum dv,
+ * b_extra = sum de, b_fc = sum df; with ie != NULL also the intrinsic head's
+ * w_critic_int = div^T ie, b_critic_int = sum div, b_int_extra = sum die.  Outputs are
+ * overwritten.  h <= 512, A <= 18.  Workspace: ppox_head_grads_workspace_bytes. */
+int64_t ppox_head_grads_workspace_bytes(int64_t rows, int64_t h, int64_t n_actions, int32_t intrinsic);
+int ppox_head_grads(const float* f, const float* e, const float* dout, const float* dv, const float* de,
+                    const float* df, const float* ie, const float* div, const float* die, int64_t rows, int64_t h,
+                    int64_t n_actions, void* workspace, float* w_actor, float* b_actor, float* w_critic,
+                    float* b_critic, float* b_extra, float* b_fc, float* w_critic_int, float* b_critic_int,
+                    float* b_int_extra, void* stream);
 int ppox_outer_relu_backward(const float* dv, const float* w, const float* act, int64_t rows, int64_t h,
                              float* out, void* stream);
 

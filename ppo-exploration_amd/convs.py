@@ -94,6 +94,7 @@ class NatureConvs:
             if self.math != "f32" else None
         self._ws = {}
         self._version = None
+        self._fc_fwd_packed = False
 
     def uses_split(self, op, layer):
         if self.math == "split_all":  # every op that has a split kernel (tests, benchmarks)
@@ -108,12 +109,18 @@ class NatureConvs:
             self._ws[layer] = ws
         return ws
 
-    def pack(self):
+    def pack(self, batch=0):
         """Re-pack the weights (once per optimizer step) into the layouts of the kernels in use
-        — one launch for all of them in split math (ppox_nature_pack_all)."""
+        — one launch for all of them in split math (ppox_nature_pack_all).  The fc forward's
+        split form only when a batch of `batch` rows uses it (packed late if a later call needs it)."""
         v = (self.flat.step_count, self.flat.data.data_ptr())
+        fc_fwd = self.math != "f32" and batch >= FC_SPLIT_MIN_BATCH
         if v == self._version:
+            if fc_fwd and not self._fc_fwd_packed:
+                native.nature_fc_pack(self.fc.weight, self.qfc[0], None)
+                self._fc_fwd_packed = True
             return
+        self._fc_fwd_packed = fc_fwd
         w1, w2, w3 = self.c1.weight, self.c2.weight, self.c3.weight
         f32 = lambda op, L, buf: None if self.uses_split(op, L) else buf
         spl = lambda op, L, buf: buf if self.uses_split(op, L) else None
@@ -121,7 +128,7 @@ class NatureConvs:
             q = self.q
             native.nature_pack_all(w1, w2, w3, self.fc.weight, f32("dgrad", 2, self.wpd2), q[1], q[2], q[3],
                                    spl("dgrad", 2, q[12]), q[13],
-                                   self.qfc[0] if FC_SPLIT_MIN_BATCH < (1 << 40) else None,
+                                   self.qfc[0] if fc_fwd else None,
                                    self.qfc[1] if FC_DGRAD_FUSED_MAX_BATCH > 0 else None)
         else:
             if not all(self.uses_split(op, L) for op, L in (("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 2),
@@ -133,7 +140,7 @@ class NatureConvs:
                 q = self.q
                 native.nature_pack_split(w1, w2, w3, spl("fwd", 1, q[1]), spl("fwd", 2, q[2]), spl("fwd", 3, q[3]),
                                          spl("dgrad", 2, q[12]), spl("dgrad", 3, q[13]))
-                native.nature_fc_pack(self.fc.weight, self.qfc[0], self.qfc[1])
+                native.nature_fc_pack(self.fc.weight, self.qfc[0] if fc_fwd else None, self.qfc[1])
         self._version = v
 
     def invalidate(self):
@@ -163,7 +170,7 @@ class NatureConvs:
 
     def forward_acts(self, x):
         """Trunk forward: (h1 NHWC, h2 NHWC, h3 NCHW) activations (ReLU applied)."""
-        self.pack()
+        self.pack(x.shape[0])
         B = x.shape[0]
         dev = x.device
         h1 = torch.empty((B, 20, 20, 32), device=dev)
@@ -179,7 +186,7 @@ class NatureConvs:
     def fc_forward(self, h3):
         """f = relu(h3 @ W^T + b), h3 (B, 64, 7, 7): the split-bf16 GEMM when the batch fills
         the chip (ceil(B/128) row tiles x 8 column blocks >= ~512 workgroups), rocBLAS below."""
-        self.pack()
+        self.pack(h3.shape[0])
         B = h3.shape[0]
         if B < FC_SPLIT_MIN_BATCH:
             return torch.addmm(self.fc.bias, h3.view(B, -1), self.fc.weight.t()).relu_()

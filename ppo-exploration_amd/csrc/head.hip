@@ -4,6 +4,10 @@
 //   ppox_outer_relu_backward: d[b][j] = dv[b] * w[j] * (act[b][j] > 0) — the grad of
 //       a ReLU layer feeding a Linear(H, 1) critic (extra_layer -> critic_ext)
 // One pass each, float4 lanes (HBM-bound: 12 B / element).
+//   ppox_head_grads: every column-reduction parameter gradient of the heads in one pass
+//       over f, e, de, df (+ the intrinsic head's): actor weight/bias (dout^T f, sum dout),
+//       critic weight/bias (dv^T e, sum dv), extra-layer bias (sum de), fc bias (sum df).
+//       Fixed-order two-level sums (row chunks, then chunks in order): deterministic.
 #include "common.h"
 
 namespace {
@@ -19,6 +23,130 @@ __global__ void __launch_bounds__(256) relu_bwd_kernel(float* __restrict__ g, co
         v.w = a.w > 0.f ? v.w : 0.f;
         reinterpret_cast<float4*>(g)[i] = v;
     }
+}
+
+// partial row of chunk c: [A*H actor W | A actor b | H critic W | 1 critic b | H extra b |
+//                         H fc b | (intrinsic) H critic_int W | 1 critic_int b | H int_extra b]
+struct HeadGrads {
+    const float *f, *e, *ie, *dout, *dv, *div, *de, *die, *df;
+    long long B, R;  // rows, rows per chunk
+    int H, A;
+};
+constexpr int HG_MAXA = 18, HG_MAXH = 512;  // actions (Montezuma 18), hidden width
+
+__host__ __device__ inline long long head_grads_len(int H, int A, bool intr) {
+    return (long long)A * H + A + H + 1 + 2LL * H + (intr ? 2LL * H + 1 : 0);
+}
+
+// thread t owns columns 2t, 2t + 1 (float2 loads); H even, H <= 512
+__global__ void __launch_bounds__(256) head_grads_partials(HeadGrads g, float* __restrict__ part) {
+    const long long r0 = (long long)blockIdx.x * g.R, r1 = min(g.B, r0 + g.R);
+    const int tid = threadIdx.x, H = g.H, A = g.A, j = 2 * tid;
+    const bool intr = g.ie != nullptr, col = j < H;
+    float2 wa[HG_MAXA], wc = {0.f, 0.f}, be = {0.f, 0.f}, bf = {0.f, 0.f}, wci = {0.f, 0.f}, bie = {0.f, 0.f};
+    float ba[HG_MAXA], bc = 0.f, bci = 0.f;
+#pragma unroll
+    for (int a = 0; a < HG_MAXA; ++a) {
+        wa[a] = make_float2(0.f, 0.f);
+        ba[a] = 0.f;
+    }
+    const int jc = col ? j : 0;
+    auto ld = [&](const float* p, long long b) { return *reinterpret_cast<const float2*>(p + b * H + jc); };
+#pragma unroll 4
+    for (long long b = r0; b < r1; ++b) {
+        const float dv = g.dv[b], div = intr ? g.div[b] : 0.f;
+        const float2 fv = ld(g.f, b), ev = ld(g.e, b), dev = ld(g.de, b), dfv = ld(g.df, b);
+#pragma unroll
+        for (int a = 0; a < HG_MAXA; ++a)
+            if (a < A) {
+                const float d = g.dout[b * A + a];
+                wa[a].x = fmaf(d, fv.x, wa[a].x);
+                wa[a].y = fmaf(d, fv.y, wa[a].y);
+                ba[a] += d;
+            }
+        wc.x = fmaf(dv, ev.x, wc.x);
+        wc.y = fmaf(dv, ev.y, wc.y);
+        be.x += dev.x;
+        be.y += dev.y;
+        bf.x += dfv.x;
+        bf.y += dfv.y;
+        bc += dv;
+        if (intr) {
+            const float2 iev = ld(g.ie, b), diev = ld(g.die, b);
+            wci.x = fmaf(div, iev.x, wci.x);
+            wci.y = fmaf(div, iev.y, wci.y);
+            bie.x += diev.x;
+            bie.y += diev.y;
+            bci += div;
+        }
+    }
+    float* p = part + (long long)blockIdx.x * head_grads_len(H, A, intr);
+    const long long o = (long long)A * H + A;
+    auto st = [&](long long at, float2 v) {
+        p[at] = v.x;
+        p[at + 1] = v.y;
+    };
+    if (col) {
+#pragma unroll
+        for (int a = 0; a < HG_MAXA; ++a)
+            if (a < A) st((long long)a * H + j, wa[a]);
+        st(o + j, wc);
+        st(o + H + 1 + j, be);
+        st(o + 2 * H + 1 + j, bf);
+        if (intr) {
+            st(o + 3 * H + 1 + j, wci);
+            st(o + 4 * H + 2 + j, bie);
+        }
+    }
+    if (tid == 0) {
+        for (int a = 0; a < A; ++a) p[(long long)A * H + a] = ba[a];
+        p[o + H] = bc;
+        if (intr) p[o + 4 * H + 1] = bci;
+    }
+}
+
+struct HeadGradOut {
+    float *wa, *ba, *wc, *bc, *be, *bfc, *wci, *bci, *bie;
+};
+
+// 64 outputs per block; wave w sums chunks w, w + 4, ... (eight independent partial sums,
+// combined in a fixed order), then the four waves' sums are combined in order: deterministic
+__global__ void __launch_bounds__(256) head_grads_reduce(const float* __restrict__ part, long long nchunk, long long len,
+                                                         int H, int A, HeadGradOut out) {
+    __shared__ float red[4][64];
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long i0 = (long long)blockIdx.x * 64 + l, ic = i0 < len ? i0 : len - 1;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    long long c = w;
+    for (; c + 28 < nchunk; c += 32)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += part[(c + 4 * k) * len + ic];
+    for (int k = 0; c < nchunk; c += 4, ++k) acc[k & 7] += part[c * len + ic];
+    red[w][l] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    __syncthreads();
+    if (w != 0 || i0 >= len) return;
+    const float s = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+    const long long i = i0;
+    // segment of element i (layout of head_grads_partials)
+    long long o = i;
+    const long long nwa = (long long)A * H;
+    if (o < nwa) { out.wa[o] = s; return; }
+    o -= nwa;
+    if (o < A) { out.ba[o] = s; return; }
+    o -= A;
+    if (o < H) { out.wc[o] = s; return; }
+    o -= H;
+    if (o < 1) { out.bc[0] = s; return; }
+    o -= 1;
+    if (o < H) { out.be[o] = s; return; }
+    o -= H;
+    if (o < H) { out.bfc[o] = s; return; }
+    o -= H;
+    if (o < H) { out.wci[o] = s; return; }
+    o -= H;
+    if (o < 1) { out.bci[0] = s; return; }
+    o -= 1;
+    out.bie[o] = s;
 }
 
 __global__ void __launch_bounds__(256) outer_relu_kernel(const float* __restrict__ dv, const float* __restrict__ w,
@@ -53,6 +181,38 @@ extern "C" int ppox_relu_backward_(float* grad, const float* act, int64_t n, voi
     if (n == 0) return PPOX_OK;
     relu_bwd_kernel<<<grid_for(n / 4), 256, 0, ppox::as_stream(stream)>>>(grad, act, n / 4);
     PPOX_LAUNCHED("ppox_relu_backward_");
+}
+
+extern "C" int64_t ppox_head_grads_workspace_bytes(int64_t rows, int64_t h, int64_t n_actions, int32_t intrinsic) {
+    if (rows < 0 || h <= 0 || h > HG_MAXH || h % 2 || n_actions <= 0 || n_actions > HG_MAXA) return -1;
+    const long long R = std::max<long long>(8, (rows + 511) / 512), nchunk = std::max<long long>(1, (rows + R - 1) / R);
+    return nchunk * head_grads_len((int)h, (int)n_actions, intrinsic != 0) * (long long)sizeof(float);
+}
+
+extern "C" int ppox_head_grads(const float* f, const float* e, const float* dout, const float* dv, const float* de,
+                               const float* df, const float* ie, const float* div, const float* die, int64_t rows,
+                               int64_t h, int64_t n_actions, void* workspace, float* w_actor, float* b_actor,
+                               float* w_critic, float* b_critic, float* b_extra, float* b_fc, float* w_critic_int,
+                               float* b_critic_int, float* b_int_extra, void* stream) {
+    PPOX_REQUIRE(f && e && dout && dv && de && df && workspace && rows >= 0, "ppox_head_grads: null input");
+    PPOX_REQUIRE(h > 0 && h <= HG_MAXH && h % 2 == 0 && n_actions > 0 && n_actions <= HG_MAXA,
+                 "ppox_head_grads: h must be even and <= 512, n_actions <= 18");
+    PPOX_REQUIRE(ppox::aligned16(f) && ppox::aligned16(e) && ppox::aligned16(de) && ppox::aligned16(df),
+                 "ppox_head_grads: 16B alignment");
+    PPOX_REQUIRE(w_actor && b_actor && w_critic && b_critic && b_extra && b_fc, "ppox_head_grads: null output");
+    const bool intr = ie != nullptr;
+    PPOX_REQUIRE(!intr || (div && die && w_critic_int && b_critic_int && b_int_extra),
+                 "ppox_head_grads: intrinsic head needs div, die and its three outputs");
+    const long long R = std::max<long long>(8, (rows + 511) / 512), nchunk = std::max<long long>(1, (rows + R - 1) / R);
+    const long long len = head_grads_len((int)h, (int)n_actions, intr);
+    hipStream_t s = ppox::as_stream(stream);
+    float* part = reinterpret_cast<float*>(workspace);
+    HeadGrads g{f, e, ie, dout, dv, div, de, die, df, rows, R, (int)h, (int)n_actions};
+    head_grads_partials<<<(unsigned)nchunk, 256, 0, s>>>(g, part);
+    PPOX_LAUNCHED_NORET("ppox_head_grads");
+    HeadGradOut o{w_actor, b_actor, w_critic, b_critic, b_extra, b_fc, w_critic_int, b_critic_int, b_int_extra};
+    head_grads_reduce<<<(unsigned)((len + 63) / 64), 256, 0, s>>>(part, nchunk, len, (int)h, (int)n_actions, o);
+    PPOX_LAUNCHED("ppox_head_grads");
 }
 
 extern "C" int ppox_outer_relu_backward(const float* dv, const float* w, const float* act, int64_t rows, int64_t h,

@@ -126,6 +126,14 @@ class CnnActorCritic(nn.Module):
                 iv = torch.addmm(self.critic_int.bias, ie, self.critic_int.weight.t()).squeeze(-1)
         return out, v, iv, (x, h1, h2, h3, f, e, ie)
 
+    def _head_ws(self, rows, h, n_actions):
+        need = native.head_grads_workspace_bytes(rows, h, n_actions, self.intrinsic)
+        ws = getattr(self, "_hg_ws", None)
+        if ws is None or ws.numel() < need or ws.device != self.actor[0].weight.device:
+            ws = torch.empty(need, dtype=torch.uint8, device=self.actor[0].weight.device)
+            self._hg_ws = ws
+        return ws
+
     def backward_train(self, ctx, dout, dv, div=None, dense_ready=None):
         """Accumulate dL/dparams for upstream grads (dout (B,A), dv (B,), div (B,)).
         `dense_ready()` is called once every non-conv gradient (fc + heads) is enqueued,
@@ -135,24 +143,30 @@ class CnnActorCritic(nn.Module):
         with torch.no_grad():
             hf = h3.view(B, -1)
             a, fc = self.actor[0], self.feature_extractor[7]
-            a.weight.grad.addmm_(dout.t(), f)
-            torch.sum(dout, 0, out=a.bias.grad)
+            dout = dout.contiguous()
             df = torch.mm(dout, a.weight)
             heads = [(self.extra_layer[0], self.critic_ext, e, dv)]
             if self.intrinsic:
                 heads.append((self.int_extra_layer[0], self.critic_int, ie, div))
+            des = []
             for hid, crit, act, d in heads:
                 d = d.contiguous().view(B, 1)
-                crit.weight.grad.addmm_(d.t(), act)
-                torch.sum(d, 0, out=crit.bias.grad)
                 de = torch.empty_like(act)
                 native.outer_relu_backward(d, crit.weight, act, de)     # dv * w, ReLU backward
                 hid.weight.grad.addmm_(de.t(), f)
-                torch.sum(de, 0, out=hid.bias.grad)
                 df.addmm_(de, hid.weight)
+                des.append((de, d))
             native.relu_backward_(df, f)
             fc.weight.grad.addmm_(df.t(), hf)
-            torch.sum(df, 0, out=fc.bias.grad)
+            # every column-reduction gradient (actor W/b, critic W/b, extra-layer b, fc b) in one pass
+            ws = self._head_ws(B, f.shape[1], dout.shape[1])
+            (de, d), intr = des[0], des[1] if self.intrinsic else (None, None)
+            native.head_grads(f, e, dout, d, de, df, ws, a.weight.grad, a.bias.grad, self.critic_ext.weight.grad,
+                              self.critic_ext.bias.grad, self.extra_layer[0].bias.grad, fc.bias.grad,
+                              ie=ie, div=intr[1], die=intr[0],
+                              w_critic_int=self.critic_int.weight.grad if self.intrinsic else None,
+                              b_critic_int=self.critic_int.bias.grad if self.intrinsic else None,
+                              b_int_extra=self.int_extra_layer[0].bias.grad if self.intrinsic else None)
             if dense_ready is not None:
                 dense_ready()
             fe = self.feature_extractor

@@ -59,6 +59,7 @@ SIGNATURES = {
     "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
+    "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 11,
     "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
     "ppox_nature_pack_all": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp],
@@ -82,12 +83,12 @@ _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p
              "ppox_nature_wgrad_workspace_bytes": ctypes.c_int64, "ppox_nature_split_pack_elems": ctypes.c_int64,
              "ppox_nature_wgrad_split_workspace_bytes": ctypes.c_int64,
              "ppox_es_update_workspace_bytes": ctypes.c_int64,
-             "ppox_nature_fc_pack_elems": ctypes.c_int64}
+             "ppox_nature_fc_pack_elems": ctypes.c_int64, "ppox_head_grads_workspace_bytes": ctypes.c_int64}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
                  "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32],
                  "ppox_nature_wgrad_split_workspace_bytes": [_i32, _i64],
                  "ppox_es_update_workspace_bytes": [_i64, _i64],
-                 "ppox_nature_fc_pack_elems": []}
+                 "ppox_nature_fc_pack_elems": [], "ppox_head_grads_workspace_bytes": [_i64, _i64, _i64, _i32]}
 
 _lib = None
 
@@ -472,6 +473,21 @@ def es_update(eps, coef, P, n_params, workspace, out, stream=None):
 def relu_backward_(grad, act, stream=None):
     """grad = act > 0 ? grad : 0, in place (same-shape contiguous f32)."""
     call("ppox_relu_backward_", _p(grad), _p(act), grad.numel(), stream_ptr(stream))
+
+
+def head_grads_workspace_bytes(rows, h, n_actions, intrinsic):
+    n = int(lib().ppox_head_grads_workspace_bytes(int(rows), int(h), int(n_actions), int(bool(intrinsic))))
+    if n < 0:
+        raise RuntimeError("ppox_head_grads_workspace_bytes: unsupported head shape")
+    return n
+
+
+def head_grads(f, e, dout, dv, de, df, ws, w_actor, b_actor, w_critic, b_critic, b_extra, b_fc,
+               ie=None, div=None, die=None, w_critic_int=None, b_critic_int=None, b_int_extra=None, stream=None):
+    """Column-reduction head gradients (see include/ppox.h ppox_head_grads); outputs overwritten."""
+    call("ppox_head_grads", _p(f), _p(e), _p(dout), _p(dv), _p(de), _p(df), _p(ie), _p(div), _p(die),
+         f.shape[0], f.shape[1], dout.shape[1], _p(ws), _p(w_actor), _p(b_actor), _p(w_critic), _p(b_critic),
+         _p(b_extra), _p(b_fc), _p(w_critic_int), _p(b_critic_int), _p(b_int_extra), stream_ptr(stream))
 
 
 def outer_relu_backward(dv, w, act, out, stream=None):

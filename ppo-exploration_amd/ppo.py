@@ -276,14 +276,21 @@ class BaseAlgorithm:
         perm = np.random.permutation(total)
         bs = total if self.batch_size is None else self.batch_size
         sizes = [min(bs, total - s) for s in range(0, total, bs)]
-        perm_dev = torch.from_numpy(perm).to(self.device, non_blocking=True)
+        # pinned staging: a pageable host->device copy blocks the host until the stream
+        # drains, idling the GPU while the next epoch's permutation is drawn
+        perm_dev = self._h2d(perm)
         if not self.dist.enabled:
             offs = np.concatenate([[0], np.cumsum(sizes)])
             return perm_dev, perm_dev, offs, sizes
         local, offs = owned_minibatch_indices(perm, self.nstep, self.env_offset, self.local_envs, bs)
-        self._epoch_pos = torch.from_numpy(
-            owned_minibatch_positions(perm, self.nstep, self.env_offset, self.local_envs, bs)).to(self.device)
-        return perm_dev, torch.from_numpy(local).to(self.device, non_blocking=True), offs, sizes
+        self._epoch_pos = self._h2d(owned_minibatch_positions(perm, self.nstep, self.env_offset, self.local_envs, bs))
+        return perm_dev, self._h2d(local), offs, sizes
+
+    def _h2d(self, a):
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        if self.device.type == "cuda":
+            t = t.pin_memory()
+        return t.to(self.device, non_blocking=True)
 
     def _global_advantages(self, ro, intrinsic=False):
         adv = self.dist.all_gather_cat(ro.advantages, dim=1)

@@ -548,8 +548,8 @@ def test_split_conv_accuracy_is_fp32_class(seed):
         assert e_s <= 2 * e_f + 1e-7, (key, e_s, e_f)
 
 
-@pytest.mark.parametrize("intrinsic", [False, True])
-def test_cnn_explicit_backward_matches_autograd(intrinsic):
+@pytest.mark.parametrize("intrinsic,B", [(False, 40), (True, 40), (False, 600)])
+def test_cnn_explicit_backward_matches_autograd(intrinsic, B):
     """CnnActorCritic.forward_train/backward_train (no autograd graph, grads straight into
     the flat buffer) == autograd through forward() on the same libppox trunk."""
     import models
@@ -558,7 +558,6 @@ def test_cnn_explicit_backward_matches_autograd(intrinsic):
     net = models.CnnActorCritic(4, 6, intrinsic=intrinsic)
     flat = models.FlatParams(net, "cuda")
     convs.attach(net, flat, "f32")
-    B = 40
     x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda")
     dout, dv = torch.randn(B, 6, device="cuda"), torch.randn(B, device="cuda")
     div = torch.randn(B, device="cuda") if intrinsic else None
@@ -580,6 +579,31 @@ def test_cnn_explicit_backward_matches_autograd(intrinsic):
         r, g = ref[off:off + p.numel()], got[off:off + p.numel()]
         scale = r.abs().max().item() + 1e-12
         assert (r - g).abs().max().item() <= 1e-5 * scale + 1e-7, p.shape
+
+
+@pytest.mark.parametrize("rows,A,intrinsic", [(1, 4, False), (5000, 18, True), (16384, 4, False)])
+def test_head_grads_match_fp64(rows, A, intrinsic):
+    """ppox_head_grads (fused column reductions of the head backward) vs float64 torch."""
+    import native
+    H = 512
+    g = torch.Generator(device="cuda").manual_seed(rows)
+    mk = lambda *s: torch.randn(*s, device="cuda", generator=g)
+    f, e, de, df, dout, dv = mk(rows, H).relu(), mk(rows, H).relu(), mk(rows, H), mk(rows, H), mk(rows, A), mk(rows)
+    ie, die, div = (mk(rows, H).relu(), mk(rows, H), mk(rows)) if intrinsic else (None, None, None)
+    outs = [torch.full(s, float("nan"), device="cuda") for s in [(A, H), (A,), (1, H), (1,), (H,), (H,)]]
+    iouts = [torch.full(s, float("nan"), device="cuda") for s in [(1, H), (1,), (H,)]] if intrinsic else [None] * 3
+    ws = torch.empty(native.head_grads_workspace_bytes(rows, H, A, intrinsic), dtype=torch.uint8, device="cuda")
+    native.head_grads(f, e, dout, dv, de, df, ws, *outs, ie=ie, div=div, die=die, w_critic_int=iouts[0],
+                      b_critic_int=iouts[1], b_int_extra=iouts[2])
+    d = lambda t: t.double()
+    refs = [d(dout).t() @ d(f), d(dout).sum(0), (d(dv) @ d(e)).view(1, H), d(dv).sum().view(1), d(de).sum(0),
+            d(df).sum(0)]
+    if intrinsic:
+        refs += [(d(div) @ d(ie)).view(1, H), d(div).sum().view(1), d(die).sum(0)]
+        outs += iouts
+    for o, r in zip(outs, refs):
+        scale = r.abs().max().item() + 1.0
+        assert (o.double() - r).abs().max().item() <= 2e-5 * scale * max(1.0, (rows / 1000) ** 0.5), o.shape
 
 
 def test_vecnormalize_matches_numpy_restatement():
