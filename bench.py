@@ -183,10 +183,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PPOX_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU
+    # (RCCL refuses two ranks on one device); the driver's runs use RCCL, one GPU per rank
+    backend = os.environ.get("PPOX_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
 
@@ -258,6 +266,11 @@ def main():
     }
     if kt:
         out["roofline"] = conv_roofline(prof_kernel, kt, totals)
+        if world > 1 and out["roofline"].get("traffic") is not None:
+            # the committed PMC passes ran the 1-GPU workload (launches of 16384 rows); the
+            # per-rank launches here are smaller, so that per-launch figure does not apply
+            out["roofline"]["traffic"] = None
+            out["roofline"]["traffic_note"] = "PMC traffic is measured on the 1-GPU workload (profiles/); n/a per rank"
     if gae_ms:
         n_local = args.envs // world
         alg_bytes = (17 if gae_kernel == "ppox_gae" else 33) * args.nstep * n_local
