@@ -1869,6 +1869,13 @@ struct WsLaunch {
     static long long splits(long long batch) {
         const long long px = batch * L::P;
         long long s = (px + 2047) / 2048;
+        // small batches (the 8-GPU per-rank minibatch): enough splits for two workgroups per CU
+        // where the k-blocks are few (conv1/conv2 at B = 2048: 0.082 -> 0.074 / 0.100 -> 0.078 ms;
+        // conv3's nine k-blocks already give 441 workgroups, and more splits measured slower)
+        if constexpr (C::KB <= 4) {
+            const long long fill = (512 + C::KB - 1) / C::KB;
+            s = s < fill ? fill : s;
+        }
         const long long most = (px + MS - 1) / MS;  // at least one step per split
         s = s > most ? most : s;
         s = s < 8 ? 8 : (s > 2048 ? 2048 : s);
