@@ -181,6 +181,8 @@ int ppox_simhash_apply(const int32_t* keys_all, int64_t n_total, int64_t offset,
  * K5  Minibatch gather (buffer.py:41-52, 256-267): dst[r] = rollout row of the
  * env-major index idx[r]; rows of row_bytes at src_row_stride (step-major).
  * -------------------------------------------------------------------------*/
+/* dst[i] = (float)src[i], n a multiple of 16, 16B-aligned (the ICM encoder's float input). */
+int ppox_u8_to_f32(const void* src, int64_t n, float* dst, void* stream);
 int ppox_gather_rows(const void* src, int64_t T, int64_t N, int64_t row_bytes,
                      int64_t src_row_stride, const int64_t* idx, int64_t nrows, void* dst,
                      void* stream);

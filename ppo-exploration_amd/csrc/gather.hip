@@ -22,7 +22,31 @@ __global__ void __launch_bounds__(256) gather_rows(const uint8_t* __restrict__ s
     }
 }
 
+// u8 -> f32 widening (the ICM encoder's input, ppo.py:629-633 / 684-688 feed float
+// observations): 16 bytes in, 64 out per lane, grid-stride; HBM-bound (5 B per element)
+__global__ void __launch_bounds__(256) u8_to_f32(const uint4* __restrict__ src, long long n16, float4* __restrict__ dst) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)gridDim.x * 256) {
+        const uint4 v = src[i];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            dst[i * 4 + q] = make_float4((float)(w[q] & 0xFFu), (float)((w[q] >> 8) & 0xFFu),
+                                         (float)((w[q] >> 16) & 0xFFu), (float)(w[q] >> 24));
+    }
+}
+
 }  // namespace
+
+extern "C" int ppox_u8_to_f32(const void* src, int64_t n, float* dst, void* stream) {
+    PPOX_REQUIRE(src && dst && n >= 0 && n % 16 == 0, "ppox_u8_to_f32: n must be a multiple of 16");
+    PPOX_REQUIRE(ppox::aligned16(src) && ppox::aligned16(dst), "ppox_u8_to_f32: 16B alignment");
+    if (n == 0) return PPOX_OK;
+    const long long n16 = n / 16;
+    const unsigned blocks = (unsigned)std::min<long long>((n16 + 255) / 256, 8192);
+    u8_to_f32<<<blocks, 256, 0, ppox::as_stream(stream)>>>(reinterpret_cast<const uint4*>(src), n16,
+                                                           reinterpret_cast<float4*>(dst));
+    PPOX_LAUNCHED("ppox_u8_to_f32");
+}
 
 extern "C" int ppox_gather_rows(const void* src, int64_t T, int64_t N, int64_t row_bytes, int64_t src_row_stride,
                                 const int64_t* idx, int64_t nrows, void* dst, void* stream) {

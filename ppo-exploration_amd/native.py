@@ -59,6 +59,7 @@ SIGNATURES = {
     "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
+    "ppox_u8_to_f32": [_vp, _i64, _vp, _vp],
     "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 11,
     "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
     "ppox_nature_pack_all": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -473,6 +474,13 @@ def es_update(eps, coef, P, n_params, workspace, out, stream=None):
 def relu_backward_(grad, act, stream=None):
     """grad = act > 0 ? grad : 0, in place (same-shape contiguous f32)."""
     call("ppox_relu_backward_", _p(grad), _p(act), grad.numel(), stream_ptr(stream))
+
+
+def u8_to_f32(x, out=None, stream=None):
+    """float copy of a contiguous uint8 tensor (same shape)."""
+    out = torch.empty(x.shape, dtype=torch.float32, device=x.device) if out is None else out
+    call("ppox_u8_to_f32", _p(x), x.numel(), _p(out), stream_ptr(stream))
+    return out
 
 
 def head_grads_workspace_bytes(rows, h, n_actions, intrinsic):

@@ -587,7 +587,10 @@ class PPO_ICM(BaseAlgorithm):
         self.icm_accum = torch.zeros(1, dtype=torch.float64, device=self.device)
 
     def _icm_x(self, obs):
-        return obs.reshape(obs.shape[0], -1).float()
+        x = obs.reshape(obs.shape[0], -1)
+        if x.dtype == torch.uint8 and x.is_cuda and x.is_contiguous() and x.numel() % 16 == 0:
+            return native.u8_to_f32(x)
+        return x.float()
 
     def collect_samples(self):
         ro = self.rollout

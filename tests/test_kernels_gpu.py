@@ -606,6 +606,12 @@ def test_head_grads_match_fp64(rows, A, intrinsic):
         assert (o.double() - r).abs().max().item() <= 2e-5 * scale * max(1.0, (rows / 1000) ** 0.5), o.shape
 
 
+def test_u8_to_f32_exact():
+    import native
+    x = torch.randint(0, 256, (37, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    assert torch.equal(native.u8_to_f32(x), x.float())
+
+
 def test_vecnormalize_matches_numpy_restatement():
     """env.VecNormalize (device) vs oracle/vecnorm.py (SB3 0.x VecNormalize restated in
     numpy; parity unpinned): normalised obs and rewards, returns and both running stats
