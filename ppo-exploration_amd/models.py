@@ -240,9 +240,12 @@ class IntrinsicCuriosityModule(nn.Module):
 
     def int_reward(self, state, next_state, action):
         """models.py:311-320: clamp(mean((phi_hat(s,a) - phi(s'))^2), -5, 5)."""
+        return self.int_reward_features(self.state_encoder(state), self.state_encoder(next_state), action)
+
+    def int_reward_features(self, f, fn, action):
+        """int_reward from already encoded phi(s), phi(s') (the collect loop encodes each
+        observation once: s_{t+1} of step t is s_t of step t + 1)."""
         ae = self.encode_action(action)
-        f = self.state_encoder(state)
-        fn = self.state_encoder(next_state)
         nh = self.forward_model(torch.cat((f, ae), 1))
         return torch.clamp((nh - fn).pow(2).mean(dim=-1), -5, 5)
 

@@ -599,6 +599,8 @@ class PPO_ICM(BaseAlgorithm):
         net = self.policy.net
         ir_sum = torch.zeros((), dtype=torch.float64, device=self.device)
         eta = self.int_rew_integration
+        icm = self.intrinsic_module
+        f_next = None  # phi(s_{t+1}) of the previous step = phi(s_t) of this one (same rows, same math)
         for t in range(self.nstep):
             with torch.no_grad():
                 out, v, _ = net(ro.obs_slots[t])
@@ -608,8 +610,9 @@ class PPO_ICM(BaseAlgorithm):
                                ro.done_ret[t], ro.done_len[t])
             self.num_timesteps += self.num_envs
             with torch.no_grad():                                              # ppo.py:629-630
-                ir = self.intrinsic_module.int_reward(self._icm_x(ro.obs_slots[t]), self._icm_x(ro.obs_slots[t + 1]),
-                                                      ro.actions[t])
+                f = icm.state_encoder(self._icm_x(ro.obs_slots[t])) if f_next is None else f_next
+                f_next = icm.state_encoder(self._icm_x(ro.obs_slots[t + 1]))
+                ir = icm.int_reward_features(f, f_next, ro.actions[t])
             ro.rewards[t].copy_((1 - eta) * ro.rewards[t] + eta * ir)
             ir_sum += ir.double().mean()
         logger.record("rollout/mean_int_reward", float(ir_sum.item()) / self.nstep)
