@@ -189,7 +189,7 @@ class NatureConvs:
         self.pack(h3.shape[0])
         B = h3.shape[0]
         if B < FC_SPLIT_MIN_BATCH:
-            return torch.addmm(self.fc.bias, h3.view(B, -1), self.fc.weight.t()).relu_()
+            return torch._addmm_activation(self.fc.bias, h3.view(B, -1), self.fc.weight.t())  # bias+ReLU fused
         f = torch.empty((B, 512), device=h3.device)
         native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f)
         return f

@@ -61,6 +61,12 @@ class MlpNetwork(nn.Module):
         return self.actor(x), self.critic(x).squeeze(-1), iv
 
 
+def linear_relu(x, weight, bias):
+    """relu(x W^T + b) as one library GEMM with a bias+ReLU epilogue (hipBLASLt through
+    torch._addmm_activation: bitwise equal to addmm().relu_(), one launch instead of two)."""
+    return torch._addmm_activation(bias, x, weight.t())
+
+
 class CnnActorCritic(nn.Module):
     """NatureCNN actor-critic (checkpoint models-checkpoint.py:48-90)."""
 
@@ -96,15 +102,23 @@ class CnnActorCritic(nn.Module):
 
     def forward(self, x):
         f = self.trunk(x)
+        if not torch.is_grad_enabled():  # collect: fused bias+ReLU GEMMs for the hidden heads
+            el = self.extra_layer[0]
+            v = self.critic_ext(linear_relu(f, el.weight, el.bias)).squeeze(-1)
+            iv = None
+            if self.intrinsic:
+                il = self.int_extra_layer[0]
+                iv = self.critic_int(linear_relu(f, il.weight, il.bias)).squeeze(-1)
+            return self.actor(f), v, iv
         v = self.critic_ext(self.extra_layer(f)).squeeze(-1)
         iv = self.critic_int(self.int_extra_layer(f)).squeeze(-1) if self.intrinsic else None
         return self.actor(f), v, iv
 
     # ---- explicit training forward/backward (no autograd graph): the same layer math as
     # forward() (addmm = F.linear, relu), with every parameter gradient written straight
-    # into its .grad view of the flat gradient buffer (weights: GEMM with beta = 1 onto the
-    # zeroed buffer; biases: column sums written in place), so the minibatch step launches
-    # no zero-fill / add kernels of its own.  Each parameter is used once per forward.
+    # into its .grad view of the flat gradient buffer (weights: GEMMs with out=, conv kernels
+    # and ppox_head_grads overwrite theirs), so a minibatch with rows needs no zero-fill of
+    # the buffer (ppo.BaseAlgorithm._zero_policy_grad).  Each parameter is used once per forward.
     def forward_train(self, x):
         """-> (actor out, value (B,), int value or None, ctx for backward_train)."""
         with torch.no_grad():
@@ -115,14 +129,14 @@ class CnnActorCritic(nn.Module):
             if self.conv_impl.math != "f32":
                 f = self.conv_impl.fc_forward(h3)
             else:
-                f = torch.addmm(fc.bias, hf, fc.weight.t()).relu_()
+                f = linear_relu(hf, fc.weight, fc.bias)
             a = self.actor[0]
             out = torch.addmm(a.bias, f, a.weight.t())
-            e = torch.addmm(self.extra_layer[0].bias, f, self.extra_layer[0].weight.t()).relu_()
+            e = linear_relu(f, self.extra_layer[0].weight, self.extra_layer[0].bias)
             v = torch.addmm(self.critic_ext.bias, e, self.critic_ext.weight.t()).squeeze(-1)
             ie = iv = None
             if self.intrinsic:
-                ie = torch.addmm(self.int_extra_layer[0].bias, f, self.int_extra_layer[0].weight.t()).relu_()
+                ie = linear_relu(f, self.int_extra_layer[0].weight, self.int_extra_layer[0].bias)
                 iv = torch.addmm(self.critic_int.bias, ie, self.critic_int.weight.t()).squeeze(-1)
         return out, v, iv, (x, h1, h2, h3, f, e, ie)
 
@@ -153,11 +167,11 @@ class CnnActorCritic(nn.Module):
                 d = d.contiguous().view(B, 1)
                 de = torch.empty_like(act)
                 native.outer_relu_backward(d, crit.weight, act, de)     # dv * w, ReLU backward
-                hid.weight.grad.addmm_(de.t(), f)
+                torch.mm(de.t(), f, out=hid.weight.grad)
                 df.addmm_(de, hid.weight)
                 des.append((de, d))
             native.relu_backward_(df, f)
-            fc.weight.grad.addmm_(df.t(), hf)
+            torch.mm(df.t(), hf, out=fc.weight.grad)
             # every column-reduction gradient (actor W/b, critic W/b, extra-layer b, fc b) in one pass
             ws = self._head_ws(B, f.shape[1], dout.shape[1])
             (de, d), intr = des[0], des[1] if self.intrinsic else (None, None)

@@ -208,6 +208,14 @@ class BaseAlgorithm:
         out, v, iv = net(obs)
         return out, v, iv, None
 
+    def _zero_policy_grad(self, rows):
+        """The explicit NatureCNN backward overwrites every policy gradient (models.py
+        CnnActorCritic.backward_train), so the flat buffer is zeroed only for autograd nets
+        or a minibatch with no rows on this rank (its all-reduce contribution is zero)."""
+        net = self.policy.net
+        if rows == 0 or getattr(net, "conv_impl", None) is None or not hasattr(net, "backward_train"):
+            self.flat.zero_grad()
+
     def _bwd_reduce(self, ctx, out, v, iv, dout, dv, div=None, has_rows=True):
         """Backward into the flat grad bucket + its all-reduce over ranks.  On the explicit
         NatureCNN path at world > 1 the bucket is reduced in two pieces: the fc + head part
@@ -405,7 +413,7 @@ class PPO(BaseAlgorithm):
         ro = self.rollout
         Bl = idx.numel()
         net = self.policy.net
-        self.flat.zero_grad()
+        self._zero_policy_grad(Bl)
         if Bl > 0:
             obs = ro._gather(ro.observations, idx)
             out, v, _, ctx = self._fwd_train(obs)
@@ -542,7 +550,7 @@ class PPO_RND(BaseAlgorithm):
             for k, B in enumerate(sizes):
                 idx = local[offs[k]:offs[k + 1]]
                 Bl = idx.numel()
-                self.flat.zero_grad()
+                self._zero_policy_grad(Bl)
                 obs = ro._gather(ro.observations, idx)
                 out, v, iv, ctx = self._fwd_train(obs)
                 od, vd, ivd = out.detach().contiguous(), v.detach().contiguous(), iv.detach().contiguous()
@@ -637,7 +645,7 @@ class PPO_ICM(BaseAlgorithm):
             for k, B in enumerate(sizes):
                 idx = local[offs[k]:offs[k + 1]]
                 Bl = idx.numel()
-                self.flat.zero_grad()
+                self._zero_policy_grad(Bl)
                 self.icm_flat.zero_grad()
                 obs = ro._gather(ro.observations, idx)
                 out, v, _, ctx = self._fwd_train(obs)
