@@ -243,8 +243,14 @@ def rms_scale_int_rewards(int_rewards, mean, var, count, stream=None):
          _p(mean), _p(var), float(count), stream_ptr(stream))
 
 
+def _check_moments(name, cols, mean, var):
+    if mean.numel() != cols or var.numel() != cols or mean.dtype != torch.float64 or var.dtype != torch.float64:
+        raise ValueError(f"{name}: mean/var must be {cols} float64 values (got {mean.numel()}, {var.numel()})")
+
+
 def normalize_obs(x, rows, cols, row_stride, mean, var, out, stream=None):
     name = "ppox_normalize_obs_u8" if x.dtype == torch.uint8 else "ppox_normalize_obs_f32"
+    _check_moments(name, cols, mean, var)
     call(name, _p(x), rows, cols, row_stride, _p(mean), _p(var), ptr(out, torch.float32, rows * cols, "out"),
          stream_ptr(stream))
 
@@ -413,6 +419,7 @@ def nature_conv_fwd_split(layer, x, batch, idx, T, N_env, x_sample_stride, wq, b
 
 
 def normalize_obs_f32_ex(x, rows, cols, row_stride, mean, var, eps, clip, out, stream=None):
+    _check_moments("ppox_normalize_obs_f32_ex", cols, mean, var)
     call("ppox_normalize_obs_f32_ex", _p(x), int(rows), int(cols), int(row_stride), _p(mean), _p(var), float(eps),
          float(clip), _p(out), stream_ptr(stream))
 

@@ -317,6 +317,9 @@ class BaseAlgorithm:
     def normalize_obs(self, obs):
         """ppo.py:111-118 -> f32 device tensor (rows, features)."""
         x = obs.reshape(obs.shape[0], -1)
+        # a never-updated shape-() RunningMeanStd normalises by broadcasting, as numpy does in
+        # the reference: give it its per-feature (identical-valued) state first
+        self.obs_rms._features(x.shape[1])
         out = torch.empty(x.shape, dtype=torch.float32, device=self.device)
         native.normalize_obs(x, x.shape[0], x.shape[1], x.stride(0), self.obs_rms.mean, self.obs_rms.var, out)
         return out

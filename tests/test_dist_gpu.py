@@ -26,20 +26,32 @@ def _port():
     return p
 
 
+INT_FIELDS = ("int_rewards", "int_values")
+
+
+def _fields(alg):
+    return FIELDS + (INT_FIELDS if hasattr(alg, "rnd_flat") else ())
+
+
 def _load_shard(alg, data, lo, n):
     ro = alg.rollout
     ro.obs_slots.copy_(torch.from_numpy(data["obs"][:, lo:lo + n]).cuda())
-    for f in FIELDS:
+    for f in _fields(alg):
         getattr(ro, f).copy_(torch.from_numpy(data[f][:, lo:lo + n]).cuda())
     ro.pos, ro.full = ro.buffer_size, True
     T = ro.buffer_size
-    ro.compute_returns_and_advantages(ro.values[T - 1], ro.masks[T - 1])
+    if hasattr(alg, "rnd_flat"):
+        ro.compute_returns_and_advantages(ro.values[T - 1], ro.int_values[T - 1], ro.masks[T - 1])
+    else:
+        ro.compute_returns_and_advantages(ro.values[T - 1], ro.masks[T - 1])
 
 
 def _weights(alg):
     w = alg.flat.data[:alg.flat.n].cpu().numpy()
-    if hasattr(alg, "icm_flat"):
-        w = np.concatenate([w, alg.icm_flat.data[:alg.icm_flat.n].cpu().numpy()])
+    for extra in ("icm_flat", "rnd_flat"):
+        if hasattr(alg, extra):
+            fl = getattr(alg, extra)
+            w = np.concatenate([w, fl.data[:fl.n].cpu().numpy()])
     return w
 
 
@@ -66,9 +78,12 @@ def _rank(rank, world, port, path, q, algo):
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("algo,math", [("PPO", "split"), ("PPO", "f32"), ("PPO_ICM", "f32")])
+@pytest.mark.parametrize("algo,math", [("PPO", "split"), ("PPO", "f32"), ("PPO_ICM", "f32"), ("PPO_RND", "f32")])
 def test_two_ranks_match_one_rank(algo, math, monkeypatch):
-    """PPO_ICM: the ICM pairs (row j, row j+1) of each global minibatch cross the rank
+    """Two ranks (gloo, one GPU) train() == one rank on the same rollout.  PPO_RND covers
+    the intrinsic head, the two-piece overlapped gradient all-reduce and train_rnd's own
+    all-reduce (its obs_rms is never updated here: the shape-() state broadcasts).
+    PPO_ICM: the ICM pairs (row j, row j+1) of each global minibatch cross the rank
     boundary; icm_loss_sharded exchanges features so the update equals one rank's.
     The decomposition is checked with exact-f32 conv math; split-bf16 math reorders
     more (3 x 2^-22 per product): after Adam's sign-normalised first steps a few
@@ -82,7 +97,7 @@ def test_two_ranks_match_one_rank(algo, math, monkeypatch):
     ref.collect_samples()
     ro = ref.rollout
     data = {"obs": ro.obs_slots.cpu().numpy()}
-    for f in FIELDS:
+    for f in _fields(ref):
         data[f] = getattr(ro, f).cpu().numpy()
     # 1-rank reference train on exactly this rollout (fresh agent, same seeds)
     np.random.seed(11)

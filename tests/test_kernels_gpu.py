@@ -606,6 +606,23 @@ def test_head_grads_match_fp64(rows, A, intrinsic):
         assert (o.double() - r).abs().max().item() <= 2e-5 * scale * max(1.0, (rows / 1000) ** 0.5), o.shape
 
 
+def test_normalize_obs_with_fresh_scalar_rms():
+    """ppo.py:111-118 with the shape-() RunningMeanStd never updated (train before any
+    collect): numpy broadcasts the scalar moments; the device path expands them first
+    (the kernel reads per-feature moments) and the wrapper rejects mismatched sizes."""
+    import native
+    import ppo
+    alg = ppo.PPO_RND(env_id="MontezumaRevengeNoFrameskip-v4", n_envs=4, nstep=8, batch_size=16, n_epochs=1, quiet=True)
+    obs = torch.randint(0, 256, (6, 84 * 84), dtype=torch.uint8, device="cuda")
+    out = alg.normalize_obs(obs)
+    u = obs.cpu().numpy()
+    ref = RM.normalize_obs(u, np.zeros(()), np.ones(())).astype(np.float32)  # numpy broadcasting
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    with pytest.raises(ValueError):
+        native.normalize_obs(obs, 6, 7056, 7056, torch.zeros(1, dtype=torch.float64, device="cuda"),
+                             torch.ones(1, dtype=torch.float64, device="cuda"), out)
+
+
 def test_u8_to_f32_exact():
     import native
     x = torch.randint(0, 256, (37, 4, 84, 84), dtype=torch.uint8, device="cuda")
