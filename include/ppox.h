@@ -322,6 +322,13 @@ int ppox_head_grads(const float* f, const float* e, const float* dout, const flo
                     int64_t n_actions, void* workspace, float* w_actor, float* b_actor, float* w_critic,
                     float* b_critic, float* b_extra, float* b_fc, float* w_critic_int, float* b_critic_int,
                     float* b_int_extra, void* stream);
+/* Skinny heads (models-checkpoint.py:60-87 actor / critic Linear layers, n_out <= 8):
+ * ppox_skinny_linear: y (rows x n_out) = x (rows x h) w^T + bias, one wave per row;
+ * ppox_skinny_dgrad:  d (rows x h) = g (rows x n_out) w (n_out x h) — overwritten. */
+int ppox_skinny_linear(const float* x, const float* w, const float* bias, int64_t rows, int64_t h, int64_t n_out,
+                       float* y, void* stream);
+int ppox_skinny_dgrad(const float* g, const float* w, int64_t rows, int64_t h, int64_t n_out, float* d,
+                      void* stream);
 int ppox_outer_relu_backward(const float* dv, const float* w, const float* act, int64_t rows, int64_t h,
                              float* out, void* stream);
 

@@ -149,6 +149,64 @@ __global__ void __launch_bounds__(256) head_grads_reduce(const float* __restrict
     out.bie[o] = s;
 }
 
+// skinny linear y[b][o] = x[b] . w[o] + bias[o] for NO <= 8 outputs (actor / critic heads,
+// models-checkpoint.py:60-87): one wave per row, lane l holds x[b][8l .. 8l+7] of each
+// 512-wide chunk, wave-reduces the NO dot products (fixed butterfly order: deterministic)
+template <int NO>
+__global__ void __launch_bounds__(256) skinny_linear_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, long long rows, int h,
+                                                            float* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= rows) return;
+    float acc[NO];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) acc[o] = 0.f;
+    for (int k = lane * 4; k < h; k += 256) {
+        const float4 xv = *reinterpret_cast<const float4*>(x + b * h + k);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            const float4 wv = *reinterpret_cast<const float4*>(w + (long long)o * h + k);
+            acc[o] = fmaf(xv.x, wv.x, acc[o]);
+            acc[o] = fmaf(xv.y, wv.y, acc[o]);
+            acc[o] = fmaf(xv.z, wv.z, acc[o]);
+            acc[o] = fmaf(xv.w, wv.w, acc[o]);
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) acc[o] += __shfl_xor(acc[o], m, 64);
+    if (lane < NO) {
+        float r = acc[0];
+#pragma unroll
+        for (int o = 1; o < NO; ++o) r = lane == o ? acc[o] : r;
+        y[b * NO + lane] = r + bias[lane];
+    }
+}
+
+// skinny dgrad d[b][j] = sum_o g[b][o] w[o][j] (o < NO): the actor head's input grad
+template <int NO>
+__global__ void __launch_bounds__(256) skinny_dgrad_kernel(const float* __restrict__ g, const float* __restrict__ w,
+                                                           long long rows, int h4, float* __restrict__ d) {
+    const long long n4 = rows * h4;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+        const long long b = i / h4;
+        const int j = (int)(i - b * h4);
+        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            const float go = g[b * NO + o];
+            const float4 wv = reinterpret_cast<const float4*>(w)[(long long)o * h4 + j];
+            r.x = fmaf(go, wv.x, r.x);
+            r.y = fmaf(go, wv.y, r.y);
+            r.z = fmaf(go, wv.z, r.z);
+            r.w = fmaf(go, wv.w, r.w);
+        }
+        reinterpret_cast<float4*>(d)[i] = r;
+    }
+}
+
 __global__ void __launch_bounds__(256) outer_relu_kernel(const float* __restrict__ dv, const float* __restrict__ w,
                                                          const float* __restrict__ act, long long rows, int h4,
                                                          float* __restrict__ d) {
@@ -213,6 +271,41 @@ extern "C" int ppox_head_grads(const float* f, const float* e, const float* dout
     HeadGradOut o{w_actor, b_actor, w_critic, b_critic, b_extra, b_fc, w_critic_int, b_critic_int, b_int_extra};
     head_grads_reduce<<<(unsigned)((len + 63) / 64), 256, 0, s>>>(part, nchunk, len, (int)h, (int)n_actions, o);
     PPOX_LAUNCHED("ppox_head_grads");
+}
+
+#define PPOX_SKINNY_CASES(M) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8)
+
+extern "C" int ppox_skinny_linear(const float* x, const float* w, const float* bias, int64_t rows, int64_t h,
+                                  int64_t n_out, float* y, void* stream) {
+    PPOX_REQUIRE(x && w && bias && y && rows >= 0 && h > 0 && h % 4 == 0 && n_out >= 1 && n_out <= 8,
+                 "ppox_skinny_linear: n_out must be 1..8, h a multiple of 4");
+    PPOX_REQUIRE(ppox::aligned16(x) && ppox::aligned16(w), "ppox_skinny_linear: 16B alignment");
+    if (rows == 0) return PPOX_OK;
+    const unsigned blocks = (unsigned)((rows + 3) / 4);
+    hipStream_t s = ppox::as_stream(stream);
+    switch (n_out) {
+#define PPOX_SL(N) \
+    case N: skinny_linear_kernel<N><<<blocks, 256, 0, s>>>(x, w, bias, rows, (int)h, y); break;
+        PPOX_SKINNY_CASES(PPOX_SL)
+#undef PPOX_SL
+    }
+    PPOX_LAUNCHED("ppox_skinny_linear");
+}
+
+extern "C" int ppox_skinny_dgrad(const float* g, const float* w, int64_t rows, int64_t h, int64_t n_out, float* d,
+                                 void* stream) {
+    PPOX_REQUIRE(g && w && d && rows >= 0 && h > 0 && h % 4 == 0 && n_out >= 1 && n_out <= 8,
+                 "ppox_skinny_dgrad: n_out must be 1..8, h a multiple of 4");
+    PPOX_REQUIRE(ppox::aligned16(w) && ppox::aligned16(d), "ppox_skinny_dgrad: 16B alignment");
+    if (rows == 0) return PPOX_OK;
+    hipStream_t s = ppox::as_stream(stream);
+    switch (n_out) {
+#define PPOX_SD(N) \
+    case N: skinny_dgrad_kernel<N><<<grid_for(rows * h / 4), 256, 0, s>>>(g, w, rows, (int)(h / 4), d); break;
+        PPOX_SKINNY_CASES(PPOX_SD)
+#undef PPOX_SD
+    }
+    PPOX_LAUNCHED("ppox_skinny_dgrad");
 }
 
 extern "C" int ppox_outer_relu_backward(const float* dv, const float* w, const float* act, int64_t rows, int64_t h,

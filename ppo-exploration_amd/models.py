@@ -102,14 +102,8 @@ class CnnActorCritic(nn.Module):
 
     def forward(self, x):
         f = self.trunk(x)
-        if not torch.is_grad_enabled():  # collect: fused bias+ReLU GEMMs for the hidden heads
-            el = self.extra_layer[0]
-            v = self.critic_ext(linear_relu(f, el.weight, el.bias)).squeeze(-1)
-            iv = None
-            if self.intrinsic:
-                il = self.int_extra_layer[0]
-                iv = self.critic_int(linear_relu(f, il.weight, il.bias)).squeeze(-1)
-            return self.actor(f), v, iv
+        if not torch.is_grad_enabled():  # collect: the same head kernels as forward_train
+            return self._heads(f)[:3]
         v = self.critic_ext(self.extra_layer(f)).squeeze(-1)
         iv = self.critic_int(self.int_extra_layer(f)).squeeze(-1) if self.intrinsic else None
         return self.actor(f), v, iv
@@ -130,15 +124,22 @@ class CnnActorCritic(nn.Module):
                 f = self.conv_impl.fc_forward(h3)
             else:
                 f = linear_relu(hf, fc.weight, fc.bias)
-            a = self.actor[0]
-            out = torch.addmm(a.bias, f, a.weight.t())
-            e = linear_relu(f, self.extra_layer[0].weight, self.extra_layer[0].bias)
-            v = torch.addmm(self.critic_ext.bias, e, self.critic_ext.weight.t()).squeeze(-1)
-            ie = iv = None
-            if self.intrinsic:
-                ie = linear_relu(f, self.int_extra_layer[0].weight, self.int_extra_layer[0].bias)
-                iv = torch.addmm(self.critic_int.bias, ie, self.critic_int.weight.t()).squeeze(-1)
+            out, v, iv, e, ie = self._heads(f)
         return out, v, iv, (x, h1, h2, h3, f, e, ie)
+
+    def _heads(self, f):
+        """actor logits, value, int value, and the hidden activations (no autograd): fused
+        bias+ReLU GEMMs for the 512-wide layers, skinny-row kernels for the narrow heads."""
+        a, el, ce = self.actor[0], self.extra_layer[0], self.critic_ext
+        out = native.head_linear(f, a.weight, a.bias)
+        e = linear_relu(f, el.weight, el.bias)
+        v = native.head_linear(e, ce.weight, ce.bias).squeeze(-1)
+        ie = iv = None
+        if self.intrinsic:
+            il, ci = self.int_extra_layer[0], self.critic_int
+            ie = linear_relu(f, il.weight, il.bias)
+            iv = native.head_linear(ie, ci.weight, ci.bias).squeeze(-1)
+        return out, v, iv, e, ie
 
     def _head_ws(self, rows, h, n_actions):
         need = native.head_grads_workspace_bytes(rows, h, n_actions, self.intrinsic)
@@ -158,7 +159,7 @@ class CnnActorCritic(nn.Module):
             hf = h3.view(B, -1)
             a, fc = self.actor[0], self.feature_extractor[7]
             dout = dout.contiguous()
-            df = torch.mm(dout, a.weight)
+            df = native.head_dgrad(dout, a.weight)
             heads = [(self.extra_layer[0], self.critic_ext, e, dv)]
             if self.intrinsic:
                 heads.append((self.int_extra_layer[0], self.critic_int, ie, div))

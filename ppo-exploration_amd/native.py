@@ -60,6 +60,8 @@ SIGNATURES = {
     "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
     "ppox_u8_to_f32": [_vp, _i64, _vp, _vp],
+    "ppox_skinny_linear": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
+    "ppox_skinny_dgrad": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 11,
     "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
     "ppox_nature_pack_all": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -481,6 +483,33 @@ def es_update(eps, coef, P, n_params, workspace, out, stream=None):
 def relu_backward_(grad, act, stream=None):
     """grad = act > 0 ? grad : 0, in place (same-shape contiguous f32)."""
     call("ppox_relu_backward_", _p(grad), _p(act), grad.numel(), stream_ptr(stream))
+
+
+def _aligned(t):
+    return t.data_ptr() % 16 == 0
+
+
+def head_linear(x, w, b):
+    """x w^T + b for the actor / critic heads: the skinny-row kernel for <= 8 outputs on
+    16-byte-aligned operands, the library GEMM otherwise (e.g. 18 Montezuma actions)."""
+    rows, h = x.shape
+    n = w.shape[0]
+    if n <= 8 and h % 4 == 0 and x.is_contiguous() and _aligned(x) and _aligned(w) and w.is_contiguous():
+        y = torch.empty(rows, n, device=x.device)
+        call("ppox_skinny_linear", _p(x), _p(w), _p(b), rows, h, n, _p(y), stream_ptr(None))
+        return y
+    return torch.addmm(b, x, w.t())
+
+
+def head_dgrad(g, w):
+    """g (rows x n) @ w (n x h) for the actor head's input grad (same dispatch as head_linear)."""
+    rows, n = g.shape
+    h = w.shape[1]
+    if n <= 8 and h % 4 == 0 and g.is_contiguous() and _aligned(w) and w.is_contiguous():
+        d = torch.empty(rows, h, device=g.device)
+        call("ppox_skinny_dgrad", _p(g), _p(w), rows, h, n, _p(d), stream_ptr(None))
+        return d
+    return torch.mm(g, w)
 
 
 def u8_to_f32(x, out=None, stream=None):

@@ -571,7 +571,13 @@ def test_cnn_explicit_backward_matches_autograd(intrinsic, B):
     ref = flat.grad.clone()
     flat.zero_grad()
     out2, v2, iv2, ctx = net.forward_train(x)
-    assert torch.equal(out2, out.detach()) and torch.equal(v2, v.detach())
+    # the explicit heads run the skinny-row kernels (fixed reduction order), autograd's nn.Linear
+    # rocBLAS: two f32 evaluations of 512-term dot products (un-normalised u8 frames: large terms)
+    for a_, b_ in ((out2, out.detach()), (v2, v.detach())):
+        torch.testing.assert_close(a_, b_, rtol=1e-4, atol=1e-5 * (b_.abs().max().item() + 1))
+    with torch.no_grad():  # the collect forward runs the same head kernels as forward_train
+        out3, v3, _ = net(x)
+    assert torch.equal(out3, out2) and torch.equal(v3, v2)
     net.backward_train(ctx, dout, dv, div)
     got = flat.grad
     for p in flat.params:  # per-tensor relative check (views into the flat buffer)
@@ -621,6 +627,22 @@ def test_normalize_obs_with_fresh_scalar_rms():
     with pytest.raises(ValueError):
         native.normalize_obs(obs, 6, 7056, 7056, torch.zeros(1, dtype=torch.float64, device="cuda"),
                              torch.ones(1, dtype=torch.float64, device="cuda"), out)
+
+
+@pytest.mark.parametrize("rows,n", [(1, 1), (2048, 4), (777, 8)])
+def test_skinny_heads_match_fp64(rows, n):
+    import native
+    g = torch.Generator(device="cuda").manual_seed(rows)
+    x = torch.randn(rows, 512, device="cuda", generator=g)
+    w = torch.randn(n, 512, device="cuda", generator=g)
+    b = torch.randn(n, device="cuda", generator=g)
+    y = native.head_linear(x, w, b)
+    ref = x.double() @ w.double().t() + b.double()
+    assert (y.double() - ref).abs().max().item() <= 1e-5 * (ref.abs().max().item() + 1)
+    gr = torch.randn(rows, n, device="cuda", generator=g)
+    d = native.head_dgrad(gr, w)
+    refd = gr.double() @ w.double()
+    assert (d.double() - refd).abs().max().item() <= 1e-5 * (refd.abs().max().item() + 1)
 
 
 def test_u8_to_f32_exact():
