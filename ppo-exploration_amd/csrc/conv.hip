@@ -1848,7 +1848,7 @@ int launch_wgrad(const WArgs& wa_in, hipStream_t s) {
 template <class L, bool NHWC_ORDER>
 int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float* dw, float* db, hipStream_t s) {
     const unsigned blocks = ppox::ceil_div(L::K * L::COUT + L::COUT, RED_E);
-    if (splits > 512)
+    if (splits >= 256)  // 32 split groups per element: shorter sequential chains (conv1 at B = 2048: 512 splits)
         wgrad_reduce<L, NHWC_ORDER, 32><<<blocks, RED_E * 32, 0, s>>>(slab, bslab, splits, dw, db);
     else
         wgrad_reduce<L, NHWC_ORDER, 8><<<blocks, RED_E * 8, 0, s>>>(slab, bslab, splits, dw, db);
