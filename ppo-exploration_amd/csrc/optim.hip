@@ -17,9 +17,11 @@ namespace {
 
 constexpr int P = PPOX_NORM_PARTIALS;
 
-__global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g, long long n,
-                                                    double* __restrict__ partials) {
-    __shared__ double red[4];
+constexpr int SUMSQ_T = 1024;  // threads per partial: more loads in flight (the buffer is only ~8 MB)
+
+__global__ void __launch_bounds__(SUMSQ_T) sumsq_kernel(const float* __restrict__ g, long long n,
+                                                        double* __restrict__ partials) {
+    __shared__ double red[SUMSQ_T / 64];
     double acc = 0.0;
     const long long n4 = n / 4;
     const float4* g4 = reinterpret_cast<const float4*>(g);
@@ -32,7 +34,12 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g,
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < SUMSQ_T / 64; ++w) t += red[w];
+        partials[blockIdx.x] = t;
+    }
 }
 
 __device__ inline float adam_one(float& p, float g, float& m, float& v, float coef, float w1, float b2, float w2,
@@ -50,20 +57,26 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
                                                    const double* __restrict__ partials, float max_norm, float w1,
                                                    float b2, float w2, float neg_step, float bc2s, float eps,
                                                    float* __restrict__ norm_out) {
+    // clip coefficient: every block sums the P partials in the same fixed tree order
+    // (thread t loads partial t; 64-lane butterflies, then the 4 wave sums in order)
+    static_assert(P == 256, "one partial per thread");
+    __shared__ double red[4];
     __shared__ float coef_sh;
-    if (threadIdx.x == 0) {
-        float coef = 1.0f;
-        if (max_norm > 0.f) {
-            double s = 0.0;
-            for (int k = 0; k < P; ++k) s += partials[k];
-            const float total = (float)sqrt(s);
-            coef = fminf(max_norm / (total + 1e-6f), 1.0f);
+    float coef = 1.0f;
+    if (max_norm > 0.f) {
+        double s = partials[threadIdx.x];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const float total = (float)sqrt((red[0] + red[1]) + (red[2] + red[3]));
+            coef_sh = fminf(max_norm / (total + 1e-6f), 1.0f);
             if (blockIdx.x == 0 && norm_out) *norm_out = total;
         }
-        coef_sh = coef;
+        __syncthreads();
+        coef = coef_sh;
     }
-    __syncthreads();
-    const float coef = coef_sh;
     const long long n4 = n / 4;
     float4* p4 = reinterpret_cast<float4*>(p);
     float4* g4 = reinterpret_cast<float4*>(g);
@@ -94,7 +107,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
 extern "C" int ppox_grad_sumsq(const float* grads, int64_t n, double* partials, void* stream) {
     PPOX_REQUIRE(grads && partials && n > 0, "ppox_grad_sumsq: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(grads), "ppox_grad_sumsq: grads must be 16-byte aligned");
-    sumsq_kernel<<<P, 256, 0, ppox::as_stream(stream)>>>(grads, n, partials);
+    sumsq_kernel<<<P, SUMSQ_T, 0, ppox::as_stream(stream)>>>(grads, n, partials);
     PPOX_LAUNCHED("ppox_grad_sumsq");
 }
 
@@ -112,7 +125,7 @@ extern "C" int ppox_adam_step(float* params, float* grads, float* exp_avg, float
     const double step_size = lr / bc1;
     const double bc2s = std::sqrt(bc2);
     const long long n4 = n / 4;
-    const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(ppox::ceil_div(n4, 256), 2048));
+    const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(ppox::ceil_div(n4, 256), 1024));
     adam_kernel<<<grid, 256, 0, ppox::as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq, n, norm_partials,
                                                            max_norm, (float)(1.0 - beta1), (float)beta2,
                                                            (float)(1.0 - beta2), (float)(-step_size), (float)bc2s,
