@@ -28,6 +28,9 @@ SPLIT_OPS = {("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 3), ("wgrad", 1), ("w
 # ops whose split kernel exists but is not faster than the f32 one at the training batch
 # (measured, tools/conv_bench.py); "split" mode runs them in f32
 SPLIT_SLOWER = {("dgrad", 2)}
+# conv2 dgrad in split math: the split kernel below this batch (tools/conv_bench.py at B = 2048, the 8-GPU
+# per-rank minibatch: 0.120 vs 0.134 ms f32), the f32 kernel from it (0.98 vs 0.96 ms at 16384)
+DGRAD2_SPLIT_MAX_BATCH = int(os.environ.get("PPOX_DGRAD2_SPLIT_MAX", "8192"))
 # bf16-plane hand-off of conv2's output grad (dgrad3 -> dgrad2/wgrad2, no split arithmetic
 # in the consumers): implemented and tested, but measured slower at B = 16384 (dgrad2 is
 # bound by its operand traffic at 32 output channels, not by the split), so off by default
@@ -94,12 +97,16 @@ class NatureConvs:
             if self.math != "f32" else None
         self._ws = {}
         self._version = None
-        self._fc_fwd_packed = False
+        self._packed = set()
 
-    def uses_split(self, op, layer):
+    def uses_split(self, op, layer, batch=None):
         if self.math == "split_all":  # every op that has a split kernel (tests, benchmarks)
             return (op, layer) in SPLIT_OPS or (op, layer) in SPLIT_SLOWER
-        return self.math == "split" and (op, layer) in SPLIT_OPS
+        if self.math != "split":
+            return False
+        if (op, layer) == ("dgrad", 2):  # split only below DGRAD2_SPLIT_MAX_BATCH rows
+            return batch is not None and batch < DGRAD2_SPLIT_MAX_BATCH
+        return (op, layer) in SPLIT_OPS
 
     def workspace(self, layer, batch, split=False):
         need = (native.nature_wgrad_split_workspace_bytes if split else native.nature_wgrad_workspace_bytes)(layer, batch)
@@ -109,42 +116,45 @@ class NatureConvs:
             self._ws[layer] = ws
         return ws
 
+    def _forms(self, batch):
+        """Weight layouts the kernels of a `batch`-row pass use: f32-packed ('wp1' .. 'wpd3'),
+        split-packed ('q1' .. 'qd3') and the fc's split forms ('qfcf', 'qfcd')."""
+        forms = set()
+        for op, L in (("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 2), ("dgrad", 3)):
+            split = self.uses_split(op, L, batch)
+            forms.add(("q" if split else "wp") + ("d" if op == "dgrad" else "") + str(L))
+        if self.math != "f32":
+            forms.add("qfcd")
+            if batch >= FC_SPLIT_MIN_BATCH:
+                forms.add("qfcf")
+        return forms
+
     def pack(self, batch=0):
-        """Re-pack the weights (once per optimizer step) into the layouts of the kernels in use
-        — one launch for all of them in split math (ppox_nature_pack_all).  The fc forward's
-        split form only when a batch of `batch` rows uses it (packed late if a later call needs it)."""
+        """Pack the weights (once per optimizer step) into the layouts the kernels of a
+        `batch`-row pass use; a later pass of another size packs only the forms still missing
+        (one ppox_nature_pack_all launch for the split and fc forms)."""
         v = (self.flat.step_count, self.flat.data.data_ptr())
-        fc_fwd = self.math != "f32" and batch >= FC_SPLIT_MIN_BATCH
-        if v == self._version:
-            if fc_fwd and not self._fc_fwd_packed:
-                native.nature_fc_pack(self.fc.weight, self.qfc[0], None)
-                self._fc_fwd_packed = True
+        if v != self._version:
+            self._version, self._packed = v, set()
+        missing = self._forms(batch) - self._packed
+        if not missing:
             return
-        self._fc_fwd_packed = fc_fwd
         w1, w2, w3 = self.c1.weight, self.c2.weight, self.c3.weight
-        f32 = lambda op, L, buf: None if self.uses_split(op, L) else buf
-        spl = lambda op, L, buf: buf if self.uses_split(op, L) else None
-        if self.math != "f32" and all(self.uses_split("fwd", L) for L in (1, 2, 3)) and self.uses_split("dgrad", 3):
+        pick = lambda name, buf: buf if name in missing else None
+        if missing & {"wp1", "wp2", "wp3", "wpd3"}:
+            native.nature_pack_weights(w1, w2, w3, pick("wp1", self.wp1), pick("wp2", self.wp2), pick("wp3", self.wp3),
+                                       None, pick("wpd3", self.wpd3))
+        if missing & {"wpd2", "q1", "q2", "q3", "qd2", "qd3", "qfcf", "qfcd"}:
             q = self.q
-            native.nature_pack_all(w1, w2, w3, self.fc.weight, f32("dgrad", 2, self.wpd2), q[1], q[2], q[3],
-                                   spl("dgrad", 2, q[12]), q[13],
-                                   self.qfc[0] if fc_fwd else None,
-                                   self.qfc[1] if FC_DGRAD_FUSED_MAX_BATCH > 0 else None)
-        else:
-            if not all(self.uses_split(op, L) for op, L in (("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 2),
-                                                           ("dgrad", 3))):
-                native.nature_pack_weights(w1, w2, w3, f32("fwd", 1, self.wp1), f32("fwd", 2, self.wp2),
-                                           f32("fwd", 3, self.wp3), f32("dgrad", 2, self.wpd2),
-                                           f32("dgrad", 3, self.wpd3))
-            if self.math != "f32":
-                q = self.q
-                native.nature_pack_split(w1, w2, w3, spl("fwd", 1, q[1]), spl("fwd", 2, q[2]), spl("fwd", 3, q[3]),
-                                         spl("dgrad", 2, q[12]), spl("dgrad", 3, q[13]))
-                native.nature_fc_pack(self.fc.weight, self.qfc[0] if fc_fwd else None, self.qfc[1])
-        self._version = v
+            qfc = self.qfc or (None, None)
+            native.nature_pack_all(w1, w2, w3, self.fc.weight, pick("wpd2", self.wpd2), pick("q1", q[1]),
+                                   pick("q2", q[2]), pick("q3", q[3]), pick("qd2", q[12]), pick("qd3", q[13]),
+                                   pick("qfcf", qfc[0]), pick("qfcd", qfc[1]))
+        self._packed |= missing
 
     def invalidate(self):
         self._version = None
+        self._packed = set()
 
     # -- per-op dispatch (layer 1 input: uint8 frames, sample stride 4*84*84 bytes)
     def fwd(self, layer, x, B, bias, y):
@@ -156,7 +166,8 @@ class NatureConvs:
             native.nature_conv_fwd(layer, x, B, None, 0, 0, stride, wp, bias, y)
 
     def dgrad(self, layer, g, B, prev_act, out):
-        if self.uses_split("dgrad", layer):
+        self.pack(B)  # the conv2 dgrad form depends on the batch
+        if self.uses_split("dgrad", layer, B):
             native.nature_conv_dgrad_split(layer, g, B, self.q[10 + layer], prev_act, out)
         else:
             native.nature_conv_dgrad(layer, g, B, self.wpd2 if layer == 2 else self.wpd3, prev_act, out)
