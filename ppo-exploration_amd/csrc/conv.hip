@@ -391,6 +391,29 @@ __host__ __device__ constexpr long long split_frag_index(int k, int col, int nou
     return ((((long long)(ch * 2 + s) * nt + j) * 3 + p) * 64 + l) * 8 + e;
 }
 
+// Output-major split packing: unit u = one 16-B fragment run (8 consecutive k of one
+// column, all three planes) of the split_frag_index layout of a [K][NOUT] matrix — its
+// eight source values are gathered (coalesced across lanes: adjacent units are adjacent
+// columns) and written as three 16-B stores, instead of 2-B stores scattered 16 B apart.
+template <int NOUT, class Src>
+__device__ inline void pack_frag_unit(const Src& src, uint16_t* __restrict__ q, long long u) {
+    constexpr int NT = NOUT / 32;
+    const int l = (int)(u & 63);
+    const long long r = u >> 6;
+    const int j = (int)(r % NT);
+    const long long cs = r / NT;  // 32-row chunk * 2 + 16-row step
+    const int col = j * 32 + (l & 31), k0 = (int)(cs * 16) + (l >> 5) * 8;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = src(k0 + e, col);
+    u32x4 p0, p1, p2;
+    split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), p0, p1, p2);
+    u32x4* d = reinterpret_cast<u32x4*>(q + ((cs * NT + j) * 3) * 512) + l;
+    d[0] = p0;
+    d[64] = p1;
+    d[128] = p2;
+}
+
 // Problems with LATE_EPILOGUE load their epilogue operands after the K walk (saves 16 VGPRs
 // per column tile when the walk holds many tiles)
 template <class P, class = void>
@@ -1911,25 +1934,63 @@ struct PackAll {
 constexpr long long PA_N1 = 8 * 2 * 64 * 8, PA_N2 = (long long)G2::K * G2::COUT, PA_N3 = (long long)G3::K * G3::COUT;
 constexpr long long PA_NFC = (long long)FcFwd::NCB * FcFwd::K * FcFwd::NOUT;
 constexpr long long PA_NFCD = (long long)FcDgrad::NCB * FcDgrad::K * FcDgrad::NOUT;
+// the split-GEMM jobs run in 8-element units (pack_frag_unit); q1 and wpd2 per element
+constexpr long long PU_2 = PA_N2 / 8, PU_3 = PA_N3 / 8, PU_FC = PA_NFC / 8, PU_FCD = PA_NFCD / 8;
+
+// source value (k, col) of layer L's forward [K][COUT] (NHWC K order) or dgrad [(tap, co)][ci]
+// matrix, from the PyTorch [co][ci][ky][kx] weights
+template <class L, bool DGRAD>
+struct ConvSrc {
+    const float* w;
+    __device__ float operator()(int k, int col) const {
+        int co, ci, tap;
+        if (DGRAD) {
+            ci = col;
+            co = k % L::COUT;
+            tap = k / L::COUT;
+        } else {
+            co = col;
+            ci = k % L::CIN;
+            tap = k / L::CIN;
+        }
+        return w[((co * L::CIN + ci) * L::KH + tap / L::KW) * L::KW + tap % L::KW];
+    }
+};
+// source value (k, col) of column block cb of a GemmRows B (w[n][k] when TRANS, w[k][n] otherwise)
+template <class Prob, bool TRANS>
+struct RowsSrc {
+    const float* w;
+    int cb;
+    __device__ float operator()(int k, int col) const {
+        const int n = cb * Prob::NOUT + col;
+        return n < Prob::N ? (TRANS ? w[(long long)n * Prob::K + k] : w[(long long)k * Prob::N + n]) : 0.f;
+    }
+};
+template <class Prob, bool TRANS>
+__device__ inline void pack_rows_unit(const float* w, uint16_t* q, long long u) {
+    constexpr long long per = (long long)Prob::K * Prob::NOUT / 8;
+    const int cb = (int)(u / per);
+    pack_frag_unit<Prob::NOUT>(RowsSrc<Prob, TRANS>{w, cb}, q + (long long)cb * Prob::K * Prob::NOUT * 3, u - cb * per);
+}
 
 __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long total) {
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
         long long j = i;
         if (j < PA_N1) { if (p.q1) pack_fwd1_split_elem(p.w1, p.q1, (int)j); continue; }
         j -= PA_N1;
-        if (j < PA_N2) { if (p.q2) pack_split_gemm_elem<G2, false>(p.w2, p.q2, (int)j); continue; }
-        j -= PA_N2;
-        if (j < PA_N3) { if (p.q3) pack_split_gemm_elem<G3, false>(p.w3, p.q3, (int)j); continue; }
-        j -= PA_N3;
-        if (j < PA_N2) { if (p.qd2) pack_split_gemm_elem<G2, true>(p.w2, p.qd2, (int)j); continue; }
-        j -= PA_N2;
-        if (j < PA_N3) { if (p.qd3) pack_split_gemm_elem<G3, true>(p.w3, p.qd3, (int)j); continue; }
-        j -= PA_N3;
+        if (j < PU_2) { if (p.q2) pack_frag_unit<G2::COUT>(ConvSrc<G2, false>{p.w2}, p.q2, j); continue; }
+        j -= PU_2;
+        if (j < PU_3) { if (p.q3) pack_frag_unit<G3::COUT>(ConvSrc<G3, false>{p.w3}, p.q3, j); continue; }
+        j -= PU_3;
+        if (j < PU_2) { if (p.qd2) pack_frag_unit<G2::CIN>(ConvSrc<G2, true>{p.w2}, p.qd2, j); continue; }
+        j -= PU_2;
+        if (j < PU_3) { if (p.qd3) pack_frag_unit<G3::CIN>(ConvSrc<G3, true>{p.w3}, p.qd3, j); continue; }
+        j -= PU_3;
         if (j < PA_N2) { if (p.wpd2) pack_dgrad_elem<G2, RG_F32>(p.w2, p.wpd2, (int)j); continue; }
         j -= PA_N2;
-        if (j < PA_NFC) { if (p.qfcf) pack_split_gemm_rows_elem<FcFwd, true>(p.wfc, p.qfcf, j); continue; }
-        j -= PA_NFC;
-        if (p.qfcd) pack_split_gemm_rows_elem<FcDgrad, false>(p.wfc, p.qfcd, j);
+        if (j < PU_FC) { if (p.qfcf) pack_rows_unit<FcFwd, true>(p.wfc, p.qfcf, j); continue; }
+        j -= PU_FC;
+        if (p.qfcd) pack_rows_unit<FcDgrad, false>(p.wfc, p.qfcd, j);
     }
 }
 
@@ -2249,7 +2310,7 @@ extern "C" int ppox_nature_pack_all(const float* w1, const float* w2, const floa
                           (const void*)qd3, (const void*)qfc_fwd, (const void*)qfc_dgrad})
         PPOX_REQUIRE(!q || ppox::aligned16(q), "ppox_nature_pack_all: packed buffers must be 16-byte aligned");
     PackAll p{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad};
-    const long long total = PA_N1 + 3 * PA_N2 + 2 * PA_N3 + PA_NFC + (qfc_dgrad ? PA_NFCD : 0);
+    const long long total = PA_N1 + 2 * PU_2 + 2 * PU_3 + PA_N2 + PU_FC + (qfc_dgrad ? PU_FCD : 0);
     const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 4096);
     pack_all_kernel<<<blocks, 256, 0, ppox::as_stream(stream)>>>(p, total);
     PPOX_LAUNCHED("ppox_nature_pack_all");

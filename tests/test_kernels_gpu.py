@@ -645,6 +645,27 @@ def test_skinny_heads_match_fp64(rows, n):
     assert (d.double() - refd).abs().max().item() <= 1e-5 * (refd.abs().max().item() + 1)
 
 
+def test_pack_all_matches_separate_packers():
+    """ppox_nature_pack_all (one launch, output-major 16-B units) == the per-layout packers."""
+    import native
+    torch.manual_seed(0)
+    w1, w2, w3 = torch.randn(32, 4, 8, 8, device="cuda"), torch.randn(64, 32, 4, 4, device="cuda"), \
+        torch.randn(64, 64, 3, 3, device="cuda")
+    wfc = torch.randn(512, 3136, device="cuda")
+    q = lambda k: torch.zeros(native.nature_split_pack_elems(k), dtype=torch.int16, device="cuda")
+    nfc = native.nature_fc_pack_elems()
+    fc = lambda: torch.zeros(nfc, dtype=torch.int16, device="cuda")
+    a = [q(1), q(2), q(3), q(12), q(13), fc(), fc(), torch.zeros(16 * 64 * 32, device="cuda")]
+    b = [q(1), q(2), q(3), q(12), q(13), fc(), fc(), torch.zeros(16 * 64 * 32, device="cuda")]
+    native.nature_pack_all(w1, w2, w3, wfc, a[7], a[0], a[1], a[2], a[3], a[4], a[5], a[6])
+    native.nature_pack_split(w1, w2, w3, b[0], b[1], b[2], b[3], b[4])
+    native.nature_fc_pack(wfc, b[5], b[6])
+    wp = [torch.empty(n, device="cuda") for n in (256 * 32, 512 * 64, 576 * 64)]
+    native.nature_pack_weights(w1, w2, w3, wp[0], wp[1], wp[2], b[7], None)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
 def test_u8_to_f32_exact():
     import native
     x = torch.randint(0, 256, (37, 4, 84, 84), dtype=torch.uint8, device="cuda")
