@@ -47,7 +47,7 @@ CONV_KERNEL = {("fwd", 1, True): "fwd1_split_kernel<1>",
                ("fwd", 2, True): "igemm_split_kernel<FwdNHWCProblem<32, 20, 20, 4, 4, 2, 64, false, 1>>",
                ("fwd", 3, True): "igemm_split_kernel<FwdNHWCProblem<64, 9, 9, 3, 3, 1, 64, true, 1>>",
                ("dgrad", 2, False): "igemm_kernel<DgradPMProblem<32, 20, 20, 4, 4, 2, 64, 1>>",
-               ("dgrad", 2, True): "igemm_split_kernel<DgradPMProblem<32, 20, 20, 4, 4, 2, 64, 1>>",
+               ("dgrad", 2, True): "dgrad2_col_kernel",
                ("dgrad", 3, True): "igemm_split_kernel<DgradPMProblem<64, 9, 9, 3, 3, 1, 64, 1>>",
                ("wgrad", 1, True): "wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256>",
                ("wgrad", 2, True): "wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128>",

@@ -24,13 +24,15 @@ import native
 
 MATHS = ("split", "split_all", "f32")
 # ops that have a split-bf16 kernel: ("fwd" | "dgrad" | "wgrad", layer)
-SPLIT_OPS = {("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 3), ("wgrad", 1), ("wgrad", 2), ("wgrad", 3)}
+SPLIT_OPS = {("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 2), ("dgrad", 3), ("wgrad", 1), ("wgrad", 2), ("wgrad", 3)}
 # ops whose split kernel exists but is not faster than the f32 one at the training batch
-# (measured, tools/conv_bench.py); "split" mode runs them in f32
-SPLIT_SLOWER = {("dgrad", 2)}
-# conv2 dgrad in split math: the split kernel below this batch (tools/conv_bench.py at B = 2048, the 8-GPU
-# per-rank minibatch: 0.120 vs 0.134 ms f32), the f32 kernel from it (0.98 vs 0.96 ms at 16384)
-DGRAD2_SPLIT_MAX_BATCH = int(os.environ.get("PPOX_DGRAD2_SPLIT_MAX", "8192"))
+# (measured, tools/conv_bench.py); "split" mode runs them in f32.  conv2 dgrad left this set
+# with its col2im-form kernel (dgrad2_col_kernel: 0.68 vs 0.97 ms f32 at B = 16384, 0.091 vs
+# 0.136 ms at the 8-GPU per-rank minibatch of 2048)
+SPLIT_SLOWER = set()
+# conv2 dgrad in split math: the split kernel below this batch, the f32 kernel from it
+# (PPOX_DGRAD2_SPLIT_MAX overrides; default: split at every batch)
+DGRAD2_SPLIT_MAX_BATCH = int(os.environ.get("PPOX_DGRAD2_SPLIT_MAX", str(1 << 62)))
 # bf16-plane hand-off of conv2's output grad (dgrad3 -> dgrad2/wgrad2, no split arithmetic
 # in the consumers): implemented and tested, but measured slower at B = 16384 (dgrad2 is
 # bound by its operand traffic at 32 output channels, not by the split), so off by default

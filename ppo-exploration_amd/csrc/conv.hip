@@ -970,6 +970,161 @@ __global__ void __launch_bounds__(256, 1) dgrad2_block_kernel(Args a, const u32x
     }
 }
 
+// ---------------------------------------------------------------------------
+// conv2 dgrad in the col2im form (split-bf16), the default conv2 split dgrad.
+// GEMM rows = output-grad pixels (n, oy, ox), K = the 64 output channels, columns =
+// (tap, ci): 16 taps x 32 = 512.  Every A value (one G row of 64 floats) is loaded
+// once, split once into its three bf16 planes and kept in registers for all 512
+// columns — 16x the MFMA work per A byte of the position-major form, whose
+// 32-column tiles re-gathered each G row for every one of its 16 input pixels.
+// A workgroup (8 waves, 32 rows each) owns 3 whole samples (243 of its 256 rows),
+// so the col2im overlap stays inside it: four passes, one per input-pixel parity
+// class (py, px), each computing the class's four taps (ky in {py, py+2}, kx in
+// {px, px+2}) and adding them, in the fixed tap order, into an LDS image of the
+// class's 10x10 pixels (tap (ky, kx) sends row (oy, ox) to class pixel
+// (oy + ky/2, ox + kx/2)).  The class image is then masked with the ReLU of the
+// layer below and written NHWC.  B (the class's four taps, split-packed as the
+// position-major dgrad form: ppox_nature_pack_split which = 12) is staged in LDS,
+// double-buffered across passes.  Deterministic: a fixed sum order per output.
+// ---------------------------------------------------------------------------
+#ifndef DGRAD2_COL
+#define DGRAD2_COL 1  // 0: conv2 split dgrad as the position-major DgradPMProblem kernel
+#endif
+constexpr int C2S = 3, C2ROWS = C2S * 81, C2PIX = 100;
+constexpr int C2BQ = 4 * 4 * 3 * 64;  // u32x4 per pass: 4 taps x 4 k-steps x 3 planes x 64 lanes
+constexpr int C2BV = C2BQ / 512;
+constexpr int C2OV = (C2S * C2PIX * 8 + 511) / 512;  // float4 outputs per thread per pass
+
+// workgroup barrier that waits only for this wave's LDS operations: global loads and
+// stores stay in flight across it (__syncthreads also drains vmcnt, which would expose
+// every output store and prefetch of dgrad2_col_kernel at each of its col2im steps)
+__device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__global__ void __launch_bounds__(512, 1) dgrad2_col_kernel(Args a, const u32x4* __restrict__ wq) {
+    using L = G2;
+    static_assert(L::COUT == 64 && L::CIN == 32 && L::OH == 9 && L::IH == 20 && L::S == 2 && L::KH == 4,
+                  "dgrad2_col_kernel is written for NatureCNN conv2");
+    __shared__ u32x4 Bs[2][C2BQ];
+    __shared__ __attribute__((aligned(16))) float Ds[C2S * C2PIX * 32 + 32];  // + dummy slot
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long n0 = (long long)blockIdx.x * C2S;
+    const long long rows_total = a.batch * L::P;
+
+    auto loadB = [&](int pass, u32x4 (&br)[C2BV]) {
+        const int py = pass >> 1, px = pass & 1;
+#pragma unroll
+        for (int j = 0; j < C2BV; ++j) {
+            const int e = j * 512 + tid, i = e / 768, within = e - i * 768;
+            const int tap = (py + 2 * (i >> 1)) * L::KW + px + 2 * (i & 1);
+            br[j] = wq[tap * 768 + within];
+        }
+    };
+    u32x4 br[C2BV];
+    loadB(0, br);
+    // A: this lane's row, k = 16q + 8h .. +8 for the four k-steps q
+    u32x4 af[4][3];
+    {
+        long long grow = n0 * L::P + wave * 32 + (lane & 31);
+        grow = grow < rows_total ? grow : rows_total - 1;  // rows past the end: clamped, never stored
+        const float* g = reinterpret_cast<const float*>(a.x) + grow * L::COUT + (lane >> 5) * 8;
+        float4 ar[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ar[2 * q] = *reinterpret_cast<const float4*>(g + 16 * q);
+            ar[2 * q + 1] = *reinterpret_cast<const float4*>(g + 16 * q + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < C2BV; ++j) Bs[0][j * 512 + tid] = br[j];
+        for (int e = tid; e < C2S * C2PIX * 8; e += 512) reinterpret_cast<float4*>(Ds)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) split8(ar[2 * q], ar[2 * q + 1], af[q][0], af[q][1], af[q][2]);
+    }
+    __syncthreads();
+
+#pragma unroll 1
+    for (int pass = 0; pass < 4; ++pass) {
+        const int py = pass >> 1, px = pass & 1, buf = pass & 1;
+        float4 mk[C2OV];
+        // the class's taps in two pairs (same ky): MFMAs of the pair, then its col2im adds
+        // in the fixed tap order, one barrier apart (64 accumulator VGPRs live, not 128)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            // one f32 accumulator per tap for all six split products (hi/lo pairs would
+            // need 64 more VGPRs than the 2-waves-per-SIMD budget leaves)
+            f32x16 acc[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) acc[u] = zero16();
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const u32x4* B = Bs[buf] + ((2 * h + u) * 4 + q) * 3 * 64 + lane;
+                    const u32x4 bf[3] = {B[0], B[64], B[128]};
+                    mfma_split6(af[q], bf, acc[u], acc[u]);
+                }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int toff = (h * 10 + u) * 32 + (lane & 31);
+                // eight reads, then eight writes (two LDS round trips, not 16 dependent ones);
+                // rows past the workgroup's samples add into a dummy slot past the image
+#pragma unroll
+                for (int r0 = 0; r0 < 16; r0 += 8) {
+                    int di[8];
+                    float dv[8];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const int rho = wave * 32 + ((r0 + r) & 3) + 8 * ((r0 + r) >> 2) + 4 * (lane >> 5);
+                        const int s = rho / 81, p = rho - s * 81, oy = p / 9, ox = p - oy * 9;
+                        di[r] = rho < C2ROWS ? (s * C2PIX + oy * 10 + ox) * 32 + toff : C2S * C2PIX * 32 + (lane & 31);
+                        dv[r] = Ds[di[r]];
+                    }
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) Ds[di[r]] = dv[r] + acc[u][r0 + r];
+                }
+                lds_barrier();
+                if (h == 0 && u == 0) {
+                    // ReLU-mask operands of this class's outputs (issued here, not hoisted into the MFMAs)
+#pragma unroll
+                    for (int j = 0; j < C2OV; ++j) {
+                        const int e = j * 512 + tid, s = e / 800, rem = e - s * 800, pix = rem >> 3, c4 = rem & 7;
+                        const long long n = n0 + s;
+                        const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
+                        // unconditional load from a clamped valid address (a conditional one
+                        // becomes a branch with a vmcnt(0) wait behind every load)
+                        const bool ok = e < C2S * C2PIX * 8 && n < a.batch;
+                        const long long o = ok ? ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4 : n0 * L::IH * L::IW * L::CIN;
+                        mk[j] = *reinterpret_cast<const float4*>(a.mask + o);
+                    }
+                }
+            }
+        }
+        if (pass < 3) loadB(pass + 1, br);
+        // masked class image -> dX (NHWC), image re-zeroed for the next class
+#pragma unroll
+        for (int j = 0; j < C2OV; ++j) {
+            const int e = j * 512 + tid, s = e / 800, rem = e - s * 800, pix = rem >> 3, c4 = rem & 7;
+            const long long n = n0 + s;
+            if (e < C2S * C2PIX * 8) {
+                float4* dp = reinterpret_cast<float4*>(Ds) + e;
+                const float4 d = *dp;
+                *dp = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (n < a.batch) {
+                    const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
+                    const float4 m = mk[j];
+                    *reinterpret_cast<float4*>(a.y + ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4) =
+                        make_float4(m.x > 0.f ? d.x : 0.f, m.y > 0.f ? d.y : 0.f, m.z > 0.f ? d.z : 0.f,
+                                    m.w > 0.f ? d.w : 0.f);
+                }
+            }
+        }
+        if (pass < 3) {
+#pragma unroll
+            for (int j = 0; j < C2BV; ++j) Bs[buf ^ 1][j * 512 + tid] = br[j];
+        }
+        lds_barrier();
+    }
+}
+
 template <class Prob>
 int launch_igemm_split(const Args& a, const uint16_t* wq, long long blocks, hipStream_t s, const char* name) {
     if (blocks == 0) return PPOX_OK;
@@ -2223,7 +2378,10 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
     Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch};
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 2) {
-#if DGRAD2_BLOCK
+#if DGRAD2_COL
+        dgrad2_col_kernel<<<(unsigned)ppox::ceil_div(batch, C2S), 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd));
+        PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
+#elif DGRAD2_BLOCK
         dgrad2_block_kernel<<<(unsigned)(ppox::ceil_div(batch, 128) * (G2::IH / 2) * (G2::IW / 2)), 256, 0, s>>>(
             a, reinterpret_cast<const u32x4*>(wqd));
         PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");

@@ -548,6 +548,41 @@ def test_split_conv_accuracy_is_fp32_class(seed):
         assert e_s <= 2 * e_f + 1e-7, (key, e_s, e_f)
 
 
+@pytest.mark.parametrize("B", [1, 2, 4, 7, 301])
+def test_conv2_split_dgrad_col2im_ragged(B):
+    """conv2 split dgrad (col2im form: 3 samples per workgroup, four parity-class passes)
+    at batches that leave a partial last workgroup, vs float64 CPU: error no larger than the
+    exact-f32-FMA kernel's (x2 headroom), rows outside the batch untouched, deterministic."""
+    import native
+    torch.manual_seed(B)
+    w2 = torch.randn(64, 32, 4, 4, device="cuda") * 0.05
+    w3 = torch.randn(64, 64, 3, 3, device="cuda") * 0.05
+    w1 = torch.randn(32, 4, 8, 8, device="cuda") * 0.05
+    q1, q2, q3, qd2, qd3 = (torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device="cuda")
+                            for k in (1, 2, 3, 12, 13))
+    native.nature_pack_split(w1, w2, w3, q1, q2, q3, qd2, qd3)
+    wp = [torch.empty(n, device="cuda") for n in (256 * 32, 512 * 64, 576 * 64, 4 * 256 * 32, 576 * 64)]
+    native.nature_pack_weights(w1, w2, w3, *wp)
+    g = torch.randn(B, 9, 9, 64, device="cuda")
+    h1 = torch.relu(torch.randn(B, 20, 20, 32, device="cuda"))
+    out = torch.full((B + 1, 20, 20, 32), 7.0, device="cuda")
+    out2 = torch.empty(B, 20, 20, 32, device="cuda")
+    f32 = torch.empty(B, 20, 20, 32, device="cuda")
+    native.nature_conv_dgrad_split(2, g, B, qd2, h1, out)
+    native.nature_conv_dgrad_split(2, g, B, qd2, h1, out2)
+    native.nature_conv_dgrad(2, g, B, wp[3], h1, f32)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:B], out2), "run-to-run"
+    assert bool((out[B] == 7.0).all()), "wrote past the batch"
+    ref = torch.nn.grad.conv2d_input((B, 32, 20, 20), w2.double().cpu(), g.double().cpu().permute(0, 3, 1, 2),
+                                     stride=2) * (h1.double().cpu().permute(0, 3, 1, 2) > 0)
+    ref = ref.permute(0, 2, 3, 1)
+    scale = ref.abs().max().item()
+    e_s = (out[:B].double().cpu() - ref).abs().max().item() / scale
+    e_f = (f32.double().cpu() - ref).abs().max().item() / scale
+    assert e_s <= 2 * e_f + 1e-7, (e_s, e_f)
+
+
 @pytest.mark.parametrize("intrinsic,B", [(False, 40), (True, 40), (False, 600)])
 def test_cnn_explicit_backward_matches_autograd(intrinsic, B):
     """CnnActorCritic.forward_train/backward_train (no autograd graph, grads straight into
