@@ -990,6 +990,19 @@ __global__ void __launch_bounds__(256, 1) dgrad2_block_kernel(Args a, const u32x
 #ifndef DGRAD2_COL
 #define DGRAD2_COL 1  // 0: conv2 split dgrad as the position-major DgradPMProblem kernel
 #endif
+// timing-probe switches (tools/build_variant.sh), all 0 in the product build
+#ifndef C2_NOMASK
+#define C2_NOMASK 0
+#endif
+#ifndef C2_NOSTORE
+#define C2_NOSTORE 0
+#endif
+#ifndef C2_NOMFMA
+#define C2_NOMFMA 0
+#endif
+#ifndef C2_NORMW
+#define C2_NORMW 0
+#endif
 constexpr int C2S = 3, C2ROWS = C2S * 81, C2PIX = 100;
 constexpr int C2BQ = 4 * 4 * 3 * 64;  // u32x4 per pass: 4 taps x 4 k-steps x 3 planes x 64 lanes
 constexpr int C2BV = C2BQ / 512;
@@ -1004,23 +1017,30 @@ __global__ void __launch_bounds__(512, 1) dgrad2_col_kernel(Args a, const u32x4*
     using L = G2;
     static_assert(L::COUT == 64 && L::CIN == 32 && L::OH == 9 && L::IH == 20 && L::S == 2 && L::KH == 4,
                   "dgrad2_col_kernel is written for NatureCNN conv2");
-    __shared__ u32x4 Bs[2][C2BQ];
-    __shared__ __attribute__((aligned(16))) float Ds[C2S * C2PIX * 32 + 32];  // + dummy slot
+    // all LDS in ONE __shared__ object (a second one can make hipcc wait vmcnt(0) before
+    // the first ds_read of each MFMA phase): B double buffer, then the class image + dummy slot
+    __shared__ u32x4 lds[2 * C2BQ + (C2S * C2PIX * 32 + 32) / 4];
+    u32x4(*Bs)[C2BQ] = reinterpret_cast<u32x4(*)[C2BQ]>(lds);
+    float* Ds = reinterpret_cast<float*>(lds + 2 * C2BQ);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const long long n0 = (long long)blockIdx.x * C2S;
     const long long rows_total = a.batch * L::P;
 
-    auto loadB = [&](int pass, u32x4 (&br)[C2BV]) {
+    // a class's B (its four taps' 12 KB split chunks) global -> LDS by LDS-DMA (no VGPRs;
+    // LDS destination = wave-uniform base + lane x 16 B, so each wave fills 1 KB runs)
+    auto loadB = [&](int pass, int buf) {
         const int py = pass >> 1, px = pass & 1;
 #pragma unroll
         for (int j = 0; j < C2BV; ++j) {
             const int e = j * 512 + tid, i = e / 768, within = e - i * 768;
             const int tap = (py + 2 * (i >> 1)) * L::KW + px + 2 * (i & 1);
-            br[j] = wq[tap * 768 + within];
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(wq + tap * 768 + within),
+                (__attribute__((address_space(3))) void*)(Bs[buf] + j * 512 + wave * 64), 16, 0, 0);
         }
     };
-    u32x4 br[C2BV];
-    loadB(0, br);
+    loadB(0, 0);
+    loadB(1, 1);
     // A: this lane's row, k = 16q + 8h .. +8 for the four k-steps q
     u32x4 af[4][3];
     {
@@ -1033,95 +1053,112 @@ __global__ void __launch_bounds__(512, 1) dgrad2_col_kernel(Args a, const u32x4*
             ar[2 * q] = *reinterpret_cast<const float4*>(g + 16 * q);
             ar[2 * q + 1] = *reinterpret_cast<const float4*>(g + 16 * q + 4);
         }
-#pragma unroll
-        for (int j = 0; j < C2BV; ++j) Bs[0][j * 512 + tid] = br[j];
         for (int e = tid; e < C2S * C2PIX * 8; e += 512) reinterpret_cast<float4*>(Ds)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int q = 0; q < 4; ++q) split8(ar[2 * q], ar[2 * q + 1], af[q][0], af[q][1], af[q][2]);
     }
-    __syncthreads();
 
-#pragma unroll 1
-    for (int pass = 0; pass < 4; ++pass) {
-        const int py = pass >> 1, px = pass & 1, buf = pass & 1;
-        float4 mk[C2OV];
-        // the class's taps in two pairs (same ky): MFMAs of the pair, then its col2im adds
-        // in the fixed tap order, one barrier apart (64 accumulator VGPRs live, not 128)
+    // tap k = 4 * class + i; class (py, px) = (k >> 3, (k >> 2) & 1), tap i of the class =
+    // (ky, kx) = (py + 2 (i >> 1), px + 2 (i & 1)): one f32 accumulator for all six split
+    // products (hi/lo pairs would not fit the 2-waves-per-SIMD register budget)
+    auto mfma_tap = [&](int k, f32x16& c) {
+        const u32x4* Bt = Bs[(k >> 2) & 1] + (k & 3) * 4 * 3 * 64 + lane;
+        c = zero16();
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            // one f32 accumulator per tap for all six split products (hi/lo pairs would
-            // need 64 more VGPRs than the 2-waves-per-SIMD budget leaves)
-            f32x16 acc[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) acc[u] = zero16();
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const u32x4* B = Bs[buf] + ((2 * h + u) * 4 + q) * 3 * 64 + lane;
-                    const u32x4 bf[3] = {B[0], B[64], B[128]};
-                    mfma_split6(af[q], bf, acc[u], acc[u]);
-                }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int toff = (h * 10 + u) * 32 + (lane & 31);
-                // eight reads, then eight writes (two LDS round trips, not 16 dependent ones);
-                // rows past the workgroup's samples add into a dummy slot past the image
-#pragma unroll
-                for (int r0 = 0; r0 < 16; r0 += 8) {
-                    int di[8];
-                    float dv[8];
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        const int rho = wave * 32 + ((r0 + r) & 3) + 8 * ((r0 + r) >> 2) + 4 * (lane >> 5);
-                        const int s = rho / 81, p = rho - s * 81, oy = p / 9, ox = p - oy * 9;
-                        di[r] = rho < C2ROWS ? (s * C2PIX + oy * 10 + ox) * 32 + toff : C2S * C2PIX * 32 + (lane & 31);
-                        dv[r] = Ds[di[r]];
-                    }
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) Ds[di[r]] = dv[r] + acc[u][r0 + r];
-                }
-                lds_barrier();
-                if (h == 0 && u == 0) {
-                    // ReLU-mask operands of this class's outputs (issued here, not hoisted into the MFMAs)
-#pragma unroll
-                    for (int j = 0; j < C2OV; ++j) {
-                        const int e = j * 512 + tid, s = e / 800, rem = e - s * 800, pix = rem >> 3, c4 = rem & 7;
-                        const long long n = n0 + s;
-                        const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
-                        // unconditional load from a clamped valid address (a conditional one
-                        // becomes a branch with a vmcnt(0) wait behind every load)
-                        const bool ok = e < C2S * C2PIX * 8 && n < a.batch;
-                        const long long o = ok ? ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4 : n0 * L::IH * L::IW * L::CIN;
-                        mk[j] = *reinterpret_cast<const float4*>(a.mask + o);
-                    }
-                }
-            }
+        for (int q = 0; q < 4; ++q) {
+            const u32x4 bf[3] = {Bt[q * 192], Bt[q * 192 + 64], Bt[q * 192 + 128]};
+            mfma_split6(af[q], bf, c, c);
         }
-        if (pass < 3) loadB(pass + 1, br);
-        // masked class image -> dX (NHWC), image re-zeroed for the next class
+    };
+    // col2im add of tap k into the class image: row (oy, ox) -> class pixel (oy + (i >> 1),
+    // ox + (i & 1)); eight reads, then eight writes; rows past the samples -> dummy slot
+    auto rmw_tap = [&](int k, const f32x16& c) {
+        const int i = k & 3, toff = ((i >> 1) * 10 + (i & 1)) * 32 + (lane & 31);
+#pragma unroll
+        for (int r0 = 0; r0 < 16; r0 += 8) {
+            int di[8];
+            float dv[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int rho = wave * 32 + ((r0 + r) & 3) + 8 * ((r0 + r) >> 2) + 4 * (lane >> 5);
+                const int s = rho / 81, p = rho - s * 81, oy = p / 9, ox = p - oy * 9;
+                di[r] = rho < C2ROWS ? (s * C2PIX + oy * 10 + ox) * 32 + toff : C2S * C2PIX * 32 + (lane & 31);
+                dv[r] = Ds[di[r]];
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) Ds[di[r]] = dv[r] + c[r0 + r];
+        }
+    };
+    // ReLU-mask operands of class p's outputs: unconditional loads from clamped valid
+    // addresses (a conditional load becomes a branch with a vmcnt(0) wait behind it)
+    float4 mk[C2OV];
+    auto load_mask = [&](int cls) {
+        const int py = cls >> 1, px = cls & 1;
 #pragma unroll
         for (int j = 0; j < C2OV; ++j) {
             const int e = j * 512 + tid, s = e / 800, rem = e - s * 800, pix = rem >> 3, c4 = rem & 7;
             const long long n = n0 + s;
-            if (e < C2S * C2PIX * 8) {
-                float4* dp = reinterpret_cast<float4*>(Ds) + e;
-                const float4 d = *dp;
-                *dp = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (n < a.batch) {
-                    const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
-                    const float4 m = mk[j];
-                    *reinterpret_cast<float4*>(a.y + ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4) =
-                        make_float4(m.x > 0.f ? d.x : 0.f, m.y > 0.f ? d.y : 0.f, m.z > 0.f ? d.z : 0.f,
-                                    m.w > 0.f ? d.w : 0.f);
-                }
+            const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
+            const bool ok = e < C2S * C2PIX * 8 && n < a.batch;
+            const long long o = ok ? ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4 : n0 * L::IH * L::IW * L::CIN;
+#if C2_NOMASK
+            mk[j] = make_float4(1.f, 1.f, 1.f, (float)o);
+#else
+            mk[j] = *reinterpret_cast<const float4*>(a.mask + o);
+#endif
+        }
+    };
+    // masked class image -> dX (NHWC), image re-zeroed for the next class; uniform control
+    // flow up to the store (threads past the image use the dummy slot)
+    auto output = [&](int cls) {
+        const int py = cls >> 1, px = cls & 1;
+#pragma unroll
+        for (int j = 0; j < C2OV; ++j) {
+            const int e = j * 512 + tid, s = e / 800, rem = e - s * 800, pix = rem >> 3, c4 = rem & 7;
+            const bool in = e < C2S * C2PIX * 8;
+            float4* dp = reinterpret_cast<float4*>(Ds) + (in ? e : C2S * C2PIX * 8);
+            const float4 d = *dp;
+            *dp = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 m = mk[j];
+            const float4 y = make_float4(m.x > 0.f ? d.x : 0.f, m.y > 0.f ? d.y : 0.f, m.z > 0.f ? d.z : 0.f,
+                                         m.w > 0.f ? d.w : 0.f);
+            const long long n = n0 + s;
+            if (in && n < a.batch && !C2_NOSTORE) {
+                const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
+                *reinterpret_cast<float4*>(a.y + ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4) = y;
             }
         }
-        if (pass < 3) {
-#pragma unroll
-            for (int j = 0; j < C2BV; ++j) Bs[buf ^ 1][j * 512 + tid] = br[j];
+    };
+    load_mask(0);
+    __syncthreads();  // B of classes 0 and 1, the zeroed image
+
+    // Software pipeline over the 16 taps: step k issues tap k+1's MFMAs beside tap k's col2im
+    // adds (no dependence between them), so the matrix cores run through the add phases; one
+    // LDS-only barrier per step orders the adds (fixed tap order per output).  B of class c+1
+    // (c = 1, 2) is DMA'd at step 4c into the buffer class c-1 finished reading at step 4c-2,
+    // and waited for at the end of step 4c+2, before tap 4c+4's MFMAs at step 4c+3.
+    auto step = [&](int k, f32x16& next, const f32x16& cur) {
+        const int cls = k >> 2, i = k & 3;
+        if (i == 0 && k > 0) {
+            load_mask(cls);
+            if (cls == 1 || cls == 2) loadB(cls + 1, (cls + 1) & 1);
         }
+        if (k + 1 < 16 && !C2_NOMFMA) mfma_tap(k + 1, next);
+        if (!C2_NORMW) rmw_tap(k, cur);
+        if (i == 2 && (cls == 1 || cls == 2)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
+        if (i == 3) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this class's mask operands
+            output(cls);
+            lds_barrier();
+        }
+    };
+    f32x16 acc0, acc1;
+    mfma_tap(0, acc0);
+#pragma unroll 1
+    for (int k = 0; k < 16; k += 2) {  // accumulators alternate roles with static names
+        step(k, acc1, acc0);
+        step(k + 1, acc0, acc1);
     }
 }
 
