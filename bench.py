@@ -75,12 +75,25 @@ def conv_roofline(key, kt, totals):
     kname = CONV_KERNEL.get((op, layer, split))
     traffic, src = pmc_traffic(kname) if kname else (None, None)
     tot = sum(totals.values()) or 1.0
-    return {"kernel": f"{name} layer {layer}" + (f" = {kname}" if kname else ""), "bound": "mfma",
-            "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+    # the binding roofline is the larger of the two lower bounds on the launch: MFMA work at
+    # the MFMA peak, or the algorithmic bytes at the HBM peak (conv2 dgrad moves 2.0 GB per
+    # 87 GFLOP at B = 16384: 252 us of HBM vs 209 us of split-bf16 MFMA)
+    alg_bytes = batch * per
+    t_mfma, t_hbm = flops / (peak * 1e12), alg_bytes / (HBM_PEAK_GBS * 1e9)
+    mfma_frac = ach / peak
+    hbm_ach = alg_bytes / (mean_ms * 1e-3) / 1e9
+    if t_hbm > t_mfma:
+        bound, a_val, p_val, unit = "hbm", round(hbm_ach, 1), HBM_PEAK_GBS, "GB/s"
+    else:
+        bound, a_val, p_val, unit = "mfma", round(ach, 2), round(peak, 1), "TFLOP/s"
+    return {"kernel": f"{name} layer {layer}" + (f" = {kname}" if kname else ""), "bound": bound,
+            "achieved": a_val, "peak": p_val, "unit": unit, "frac": round(a_val / p_val, 4),
             "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)", "traffic_source": src,
-            "alg_bytes_per_launch": batch * per, "alg_flops_per_launch": flops,
+            "alg_bytes_per_launch": alg_bytes, "alg_flops_per_launch": flops,
             "launches": len(kt), "mean_us": round(mean_ms * 1e3, 1),
-            "alg_hbm_GBs": round(batch * per / (mean_ms * 1e-3) / 1e9, 1),
+            "mfma_achieved_tflops": round(ach, 2), "mfma_peak_tflops": round(peak, 1), "mfma_frac": round(mfma_frac, 4),
+            "alg_hbm_GBs": round(hbm_ach, 1), "hbm_frac": round(hbm_ach / HBM_PEAK_GBS, 4),
+            "lower_bound_us": {"mfma": round(t_mfma * 1e6, 1), "hbm": round(t_hbm * 1e6, 1)},
             "share_of_conv_time": round(totals.get(key, 0.0) / tot, 3),
             "peak_note": "f32 MFMA 157.3 TF/s" if not split else
                          f"bf16 MFMA 2500 TF/s / {products} products per f32 MAC (split-bf16, fp32-class accuracy)"}
