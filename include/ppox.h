@@ -374,6 +374,14 @@ int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_t batch,
                                  int64_t x_sample_stride, const float* grad_out, void* workspace,
                                  int64_t workspace_bytes, float* dw, float* db, void* stream);
 
+/* conv1 split wgrad with the minibatch gather fused: sample n is env-major row idx[n]
+ * (i = env * T + step) of the step-major (T, N_env, 4, 84, 84) uint8 rollout frames x.
+ * Replaces ppox_gather_rows + ppox_nature_conv_wgrad_split(1, ...) on the minibatch
+ * observations of buffer.py:97-109 / models-checkpoint.py:52-58 (Conv2d(4, 32, 8, 4) backward). */
+int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
+                                     int64_t T, int64_t N_env, const float* grad_out, void* workspace,
+                                     int64_t workspace_bytes, float* dw, float* db, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,6 +55,25 @@ def default_math():
     return m
 
 
+class RolloutRows:
+    """Minibatch observations left in the rollout: rows idx (env-major i = env * T + step,
+    device int64) of the step-major (T, N, 4, 84, 84) uint8 frame buffer.  The split conv1
+    kernels read them in place (ppox_nature_conv_fwd_split / _wgrad_split_idx with idx), so
+    the minibatch gather (ppox_gather_rows, 2 x 28,224 B per row) is not run."""
+
+    dtype = torch.uint8
+
+    def __init__(self, frames, idx):
+        assert frames.dtype == torch.uint8 and frames.dim() == 5 and frames.is_contiguous()
+        self.frames, self.idx = frames, idx.contiguous()
+        self.T, self.N = int(frames.shape[0]), int(frames.shape[1])
+        self.shape = (int(idx.numel()),) + tuple(frames.shape[2:])
+        self.device = frames.device
+
+    def contiguous(self):
+        return self
+
+
 class _NatureTrunk(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, convs, w1, b1, w2, b2, w3, b3):
@@ -161,6 +180,10 @@ class NatureConvs:
     # -- per-op dispatch (layer 1 input: uint8 frames, sample stride 4*84*84 bytes)
     def fwd(self, layer, x, B, bias, y):
         stride = 4 * 84 * 84 if layer == 1 else 0
+        if isinstance(x, RolloutRows):
+            assert layer == 1 and self.uses_split("fwd", 1)
+            native.nature_conv_fwd_split(1, x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y)
+            return
         if self.uses_split("fwd", layer):
             native.nature_conv_fwd_split(layer, x, B, None, 0, 0, stride, self.q[layer], bias, y)
         else:
@@ -176,6 +199,10 @@ class NatureConvs:
 
     def wgrad(self, layer, x, B, g, dw, db):
         stride = 4 * 84 * 84 if layer == 1 else 0
+        if isinstance(x, RolloutRows):
+            assert layer == 1 and self.uses_split("wgrad", 1)
+            native.nature_conv_wgrad_split_idx(1, x.frames, B, x.idx, x.T, x.N, g, self.workspace(1, B, True), dw, db)
+            return
         if self.uses_split("wgrad", layer):
             native.nature_conv_wgrad_split(layer, x, B, stride, g, self.workspace(layer, B, True), dw, db)
         else:

@@ -1737,16 +1737,29 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     // contiguous bytes per store instruction (bank-conflict-free)
     const int pxl = tid >> 3, ju = tid & 7, gco = (tid & 7) * GW;
     const unsigned long long sstride = U8 ? (unsigned long long)a.sample_stride : SAMPLE_F32;
-    unsigned xp, mcur = mbeg + pxl;
-    unsigned long long sb;
+    // byte (u8) / float offset of sample n: through the rollout rows when a.idx is set (u8
+    // only); the next sample's base is fetched one wrap ahead, so the idx load's latency
+    // hides under the steps in between
+    const bool rows = U8 && a.idx != nullptr;
+    auto sbase = [&](unsigned n) -> unsigned long long {
+        if (rows) {
+            const unsigned nc = n < (unsigned)a.batch ? n : (unsigned)a.batch - 1;
+            const long long i = a.idx[nc];
+            return (unsigned long long)(((i % a.T) * a.Nenv + i / a.T) * (long long)(L::CIN * L::IH * L::IW));
+        }
+        return n * sstride;
+    };
+    unsigned xp, mcur = mbeg + pxl, ncur;
+    unsigned long long sb, sbn;
     {
         const unsigned m = mcur < M ? mcur : mbeg;
-        const unsigned n = m / L::P;
-        xp = m - n * L::P;
-        sb = n * sstride;
+        ncur = m / L::P;
+        xp = m - ncur * L::P;
+        sb = sbase(ncur);
+        sbn = sbase(ncur + 1);
     }
     const unsigned xp0 = mbeg - (mbeg / L::P) * L::P;  // a pixel that always exists
-    const unsigned long long sb00 = (unsigned long long)(mbeg / L::P) * sstride;
+    const unsigned long long sb00 = sbase(mbeg / L::P);
     int koff[XU];
 #pragma unroll
     for (int i = 0; i < XU; ++i) {
@@ -1809,7 +1822,13 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         xp += MS;
         if (xp >= (unsigned)L::P) {
             xp -= L::P;
-            sb += sstride;
+            if (rows) {
+                ++ncur;
+                sb = sbn;
+                sbn = sbase(ncur + 1);
+            } else {
+                sb += sstride;
+            }
         }
     };
     auto load_step = [&](unsigned ms) {
@@ -2100,10 +2119,10 @@ struct WsLaunch {
         return splits(batch) * (long long)(L::K * L::COUT + L::COUT) * (long long)sizeof(float);
     }
     static int run(const void* x, long long sample_stride, const float* g, long long batch, void* ws, float* dw,
-                   float* db, hipStream_t s) {
+                   float* db, hipStream_t s, const long long* idx = nullptr, long long T = 0, long long Nenv = 0) {
         const int sp = (int)splits(batch);
         float* slab = reinterpret_cast<float*>(ws);
-        WArgs wa{x, sample_stride, g, slab, slab + (long long)sp * L::K * L::COUT, batch, 0, sp};
+        WArgs wa{x, sample_stride, g, slab, slab + (long long)sp * L::K * L::COUT, batch, 0, sp, idx, T, Nenv};
         const long long M = batch * L::P;
         wa.px_per_split = ppox::ceil_div(ppox::ceil_div(M, sp), MS) * MS;
         wgrad_split_kernel<L, U8, KT, GPL><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
@@ -2360,6 +2379,24 @@ extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_
 
 // as ppox_nature_conv_wgrad_split; grad_out_planes = 1: grad_out is the three bf16 planes
 // [3][batch][OH][OW][COUT] written by ppox_nature_conv_dgrad_split_ex (layer 2 only)
+// conv1 split wgrad reading its frames straight from the rollout (sample n = env-major row
+// idx[n] of the step-major (T, N_env, 4, 84, 84) buffer): the minibatch gather fused, as in
+// ppox_nature_conv_fwd_split's idx form (replaces ppox_gather_rows + the strided call)
+extern "C" int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
+                                                int64_t T, int64_t N_env, const float* grad_out, void* workspace,
+                                                int64_t workspace_bytes, float* dw, float* db, void* stream) {
+    PPOX_REQUIRE(layer == 1, "ppox_nature_conv_wgrad_split_idx: layer must be 1 (u8 frames)");
+    PPOX_REQUIRE(x && idx && grad_out && workspace && dw && db && batch > 0 && T > 0 && N_env > 0,
+                 "ppox_nature_conv_wgrad_split_idx: bad arguments");
+    PPOX_REQUIRE(workspace_bytes >= ppox_nature_wgrad_split_workspace_bytes(layer, batch),
+                 "ppox_nature_conv_wgrad_split_idx: workspace too small");
+    PPOX_REQUIRE(ppox::aligned16(grad_out) && !(reinterpret_cast<uintptr_t>(x) & 3),
+                 "ppox_nature_conv_wgrad_split_idx: alignment");
+    PPOX_REQUIRE(batch * G1::P < (1LL << 31) / 64, "ppox_nature_conv_wgrad_split_idx: batch too large");
+    return Ws1::run(x, 0, grad_out, batch, workspace, dw, db, ppox::as_stream(stream),
+                    reinterpret_cast<const long long*>(idx), T, N_env);
+}
+
 extern "C" int ppox_nature_conv_wgrad_split_ex(int32_t layer, const void* x, int64_t batch, int64_t x_sample_stride,
                                                const void* grad_out, int32_t grad_out_planes, void* workspace,
                                                int64_t workspace_bytes, float* dw, float* db, void* stream) {

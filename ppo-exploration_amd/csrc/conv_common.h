@@ -176,6 +176,10 @@ struct WArgs {
     long long batch;
     long long px_per_split;
     int splits;
+    // conv1 (u8) only: optional env-major rollout rows — sample n is row idx[n] of the
+    // step-major (T, Nenv, ...) frame buffer x (the minibatch gather fused into the load)
+    const long long* idx = nullptr;
+    long long T = 0, Nenv = 0;
 };
 
 }  // namespace

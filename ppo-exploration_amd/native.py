@@ -77,6 +77,7 @@ SIGNATURES = {
     "ppox_nature_conv_wgrad_split_ex": [_i32, _vp, _i64, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp],
     "ppox_outer_relu_backward": [_vp, _vp, _vp, _i64, _i64, _vp, _vp],
     "ppox_nature_conv_wgrad_split": [_i32, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
+    "ppox_nature_conv_wgrad_split_idx": [_i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
@@ -154,7 +155,7 @@ def event_times_ms(name):
 
 _LAYERED = ("ppox_nature_conv_fwd", "ppox_nature_conv_dgrad", "ppox_nature_conv_wgrad",
             "ppox_nature_conv_fwd_split", "ppox_nature_conv_dgrad_split", "ppox_nature_conv_wgrad_split",
-            "ppox_nature_conv_dgrad_split_ex", "ppox_nature_conv_wgrad_split_ex")
+            "ppox_nature_conv_dgrad_split_ex", "ppox_nature_conv_wgrad_split_ex", "ppox_nature_conv_wgrad_split_idx")
 
 
 def call(name, *args):
@@ -547,6 +548,14 @@ def nature_conv_wgrad_split(layer, x, batch, x_sample_stride, grad_out, workspac
     """dW, db of one conv layer (slabs + fixed-order reduce in one call), split-bf16 MFMA."""
     call("ppox_nature_conv_wgrad_split", int(layer), _p(x), int(batch), int(x_sample_stride), _p(grad_out),
          _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db), stream_ptr(stream))
+
+
+def nature_conv_wgrad_split_idx(layer, x, batch, idx, T, N_env, grad_out, workspace, dw, db, stream=None):
+    """conv1 dW, db from the step-major (T, N_env, 4, 84, 84) rollout frames through env-major
+    rows idx (the minibatch gather fused), split-bf16 MFMA."""
+    call("ppox_nature_conv_wgrad_split_idx", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
+         _p(grad_out), _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db),
+         stream_ptr(stream))
 
 
 def nature_conv_dgrad_split_ex(layer, grad_out, grad_out_planes, batch, wqd, prev_act, grad_in, grad_in_planes,

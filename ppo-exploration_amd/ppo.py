@@ -208,6 +208,19 @@ class BaseAlgorithm:
         out, v, iv = net(obs)
         return out, v, iv, None
 
+    def _train_obs(self, ro, idx):
+        """Minibatch observations for the policy's training forward: the rows left in the
+        rollout (convs.RolloutRows: the split conv1 forward and weight-gradient kernels read
+        them through idx, no gather) when the NatureCNN trunk runs conv1 in split math on uint8
+        frames; otherwise the gathered rows (buffer.py:97-109)."""
+        net = self.policy.net
+        cv = getattr(net, "conv_impl", None)
+        obs = ro.observations
+        if (cv is not None and hasattr(net, "forward_train") and obs.dtype == torch.uint8 and obs.dim() == 5
+                and cv.uses_split("fwd", 1) and cv.uses_split("wgrad", 1)):
+            return convs.RolloutRows(obs, idx)
+        return ro._gather(obs, idx)
+
     def _zero_policy_grad(self, rows):
         """The explicit NatureCNN backward overwrites every policy gradient (models.py
         CnnActorCritic.backward_train), so the flat buffer is zeroed only for autograd nets
@@ -418,8 +431,7 @@ class PPO(BaseAlgorithm):
         net = self.policy.net
         self._zero_policy_grad(Bl)
         if Bl > 0:
-            obs = ro._gather(ro.observations, idx)
-            out, v, _, ctx = self._fwd_train(obs)
+            out, v, _, ctx = self._fwd_train(self._train_obs(ro, idx))
             out_d, v_d = out.detach().contiguous(), v.detach().contiguous()
         else:
             out_d = torch.zeros(0, self.n_actions, device=self.device)

@@ -548,6 +548,39 @@ def test_split_conv_accuracy_is_fp32_class(seed):
         assert e_s <= 2 * e_f + 1e-7, (key, e_s, e_f)
 
 
+@pytest.mark.parametrize("T,N,B", [(5, 7, 33), (128, 16, 1000), (3, 2, 1)])
+def test_conv1_split_reads_rollout_rows(T, N, B):
+    """conv1 split forward and weight gradient reading the minibatch rows in place
+    (convs.RolloutRows: idx into the step-major rollout frames) == the same kernels on the
+    gathered rows (ppox_gather_rows), bitwise."""
+    import convs
+    import native
+    torch.manual_seed(T * 100 + B)
+    frames = torch.randint(0, 256, (T, N, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    idx = torch.randperm(T * N, device="cuda")[:B].to(torch.int64) if B <= T * N else \
+        torch.randint(0, T * N, (B,), device="cuda")
+    rows = torch.empty(B, 4, 84, 84, dtype=torch.uint8, device="cuda")
+    native.gather_rows(frames, T, N, 28224, 28224, idx, B, rows)
+    w1 = torch.randn(32, 4, 8, 8, device="cuda") * 0.05
+    w2, w3 = torch.randn(64, 32, 4, 4, device="cuda"), torch.randn(64, 64, 3, 3, device="cuda")
+    q = [torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device="cuda") for k in (1, 2, 3, 12, 13)]
+    native.nature_pack_split(w1, w2, w3, *q)
+    b1 = torch.randn(32, device="cuda")
+    y_rows, y_idx = (torch.empty(B, 20, 20, 32, device="cuda") for _ in range(2))
+    native.nature_conv_fwd_split(1, rows, B, None, 0, 0, 28224, q[0], b1, y_rows)
+    rr = convs.RolloutRows(frames, idx)
+    native.nature_conv_fwd_split(1, rr.frames, B, rr.idx, rr.T, rr.N, 0, q[0], b1, y_idx)
+    g1 = torch.randn(B, 20, 20, 32, device="cuda")
+    ws = torch.empty(native.nature_wgrad_split_workspace_bytes(1, B), dtype=torch.uint8, device="cuda")
+    dw_rows, dw_idx = torch.empty_like(w1), torch.empty_like(w1)
+    db_rows, db_idx = torch.empty_like(b1), torch.empty_like(b1)
+    native.nature_conv_wgrad_split(1, rows, B, 28224, g1, ws, dw_rows, db_rows)
+    native.nature_conv_wgrad_split_idx(1, frames, B, idx, T, N, g1, ws, dw_idx, db_idx)
+    torch.cuda.synchronize()
+    assert torch.equal(y_rows, y_idx)
+    assert torch.equal(dw_rows, dw_idx) and torch.equal(db_rows, db_idx)
+
+
 @pytest.mark.parametrize("B", [1, 2, 4, 7, 301])
 def test_conv2_split_dgrad_col2im_ragged(B):
     """conv2 split dgrad (col2im form: 3 samples per workgroup, four parity-class passes)

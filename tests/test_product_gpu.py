@@ -127,6 +127,29 @@ def test_atari_iteration_runs(algo):
     alg.collect_samples()  # second rollout continues from slot T
 
 
+def test_ppo_train_rollout_rows_equals_gathered():
+    """The CNN minibatch read in place from the rollout (convs.RolloutRows) and the gathered
+    minibatch (buffer._gather) give bitwise-identical post-train weights."""
+    import ppo
+    import logger
+    res = []
+    for force_gather in (False, True):
+        np.random.seed(5)
+        torch.manual_seed(5)
+        alg = ppo.PPO(env_id="BreakoutNoFrameskip-v4", n_envs=8, nstep=16, batch_size=40, n_epochs=2, quiet=True,
+                      seed=3)
+        if force_gather:
+            alg._train_obs = lambda ro, idx: ro._gather(ro.observations, idx)
+        else:
+            import convs
+            assert isinstance(alg._train_obs(alg.rollout, torch.arange(4, device="cuda")), convs.RolloutRows)
+        logger.configure("t", "BreakoutNoFrameskip-v4", quiet=True)
+        alg.collect_samples()
+        alg.train()
+        res.append(alg.flat.data.clone())
+    assert torch.equal(res[0], res[1])
+
+
 def test_rnd_train_matches_reference_run(golden):
     """PPO_RND.train() (ppo.py:409-502: two normalised advantage streams, clipped int value
     loss, randn()<0.25-gated RND updates) on the reference's rollout."""
