@@ -122,11 +122,18 @@ def load(path=LIB_PATH):
     return lib
 
 
+_gpu_ok = False
+
+
 def lib():
-    """The library, for compute calls: also requires a visible GPU."""
+    """The library, for compute calls: also requires a visible GPU (checked once: the
+    per-launch host cost matters where the minibatch / collect loops are launch-bound)."""
+    global _gpu_ok
     l = load()
-    if not torch.cuda.is_available():
-        raise RuntimeError("ppo-exploration_amd needs an MI355X (HIP device); none is visible")
+    if not _gpu_ok:
+        if not torch.cuda.is_available():
+            raise RuntimeError("ppo-exploration_amd needs an MI355X (HIP device); none is visible")
+        _gpu_ok = True
     return l
 
 
@@ -174,8 +181,12 @@ def call(name, *args):
 
 
 def stream_ptr(stream=None):
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return _vp(s.cuda_stream)
+    """Raw HIP stream of `stream`, default torch's current stream on the current device
+    (read through the raw-stream accessor: torch.cuda.current_stream() costs several us of
+    host time per launch)."""
+    if stream is not None:
+        return _vp(stream.cuda_stream)
+    return _vp(torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice()))
 
 
 def ptr(t, dtype=None, numel=None, name="tensor"):

@@ -803,3 +803,14 @@ def test_fc_split_gemm_vs_fp64(B):
     e_s = (g3.double() - refd).abs().max() / refd.abs().max()
     e_f = ((df @ W).view(B, 64, 7, 7).permute(0, 2, 3, 1) * mask).double().sub(refd).abs().max() / refd.abs().max()
     assert e_s <= 2 * e_f + 1e-7, (float(e_s), float(e_f))
+
+
+def test_stream_ptr_is_torch_current_stream():
+    """native.stream_ptr() (raw-stream accessor) == torch.cuda.current_stream().cuda_stream,
+    on the default stream and inside a side-stream context."""
+    import native
+    assert native.stream_ptr().value == torch.cuda.current_stream().cuda_stream
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        assert native.stream_ptr().value == s.cuda_stream == torch.cuda.current_stream().cuda_stream
+    assert native.stream_ptr(s).value == s.cuda_stream
