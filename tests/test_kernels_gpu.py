@@ -809,8 +809,9 @@ def test_stream_ptr_is_torch_current_stream():
     """native.stream_ptr() (raw-stream accessor) == torch.cuda.current_stream().cuda_stream,
     on the default stream and inside a side-stream context."""
     import native
-    assert native.stream_ptr().value == torch.cuda.current_stream().cuda_stream
+    raw = lambda p: p.value or 0  # the legacy default stream is the null pointer
+    assert raw(native.stream_ptr()) == torch.cuda.current_stream().cuda_stream
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
-        assert native.stream_ptr().value == s.cuda_stream == torch.cuda.current_stream().cuda_stream
-    assert native.stream_ptr(s).value == s.cuda_stream
+        assert raw(native.stream_ptr()) == s.cuda_stream == torch.cuda.current_stream().cuda_stream != 0
+    assert raw(native.stream_ptr(s)) == s.cuda_stream
