@@ -581,7 +581,7 @@ def test_conv1_split_reads_rollout_rows(T, N, B):
     assert torch.equal(dw_rows, dw_idx) and torch.equal(db_rows, db_idx)
 
 
-@pytest.mark.parametrize("B", [1, 2, 4, 7, 301])
+@pytest.mark.parametrize("B", [1, 2, 4, 7, 301, 2311])
 def test_conv2_split_dgrad_col2im_ragged(B):
     """conv2 split dgrad (col2im form: 3 samples per workgroup, four parity-class passes)
     at batches that leave a partial last workgroup, vs float64 CPU: error no larger than the
