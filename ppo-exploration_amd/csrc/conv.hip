@@ -2226,10 +2226,10 @@ extern "C" int ppox_nature_pack_weights(const float* w1, const float* w2, const 
 extern "C" int ppox_nature_conv_fwd(int32_t layer, const void* x, int64_t batch, const int64_t* idx, int64_t T,
                                     int64_t N_env, int64_t x_sample_stride, const float* wp, const float* bias,
                                     float* y, void* stream) {
+    if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_conv_fwd: layer must be 1, 2 or 3");
     PPOX_REQUIRE(x && wp && bias && y && batch >= 0, "ppox_nature_conv_fwd: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(wp), "ppox_nature_conv_fwd: packed weights must be 16-byte aligned");
-    if (batch == 0) return PPOX_OK;
     PPOX_REQUIRE(batch * G1::P < (1LL << 31), "ppox_nature_conv_fwd: batch too large for 32-bit row indexing");
     Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, wp, bias, nullptr, y, batch};
     hipStream_t s = ppox::as_stream(stream);
@@ -2265,10 +2265,10 @@ extern "C" int ppox_nature_conv_fwd(int32_t layer, const void* x, int64_t batch,
 
 extern "C" int ppox_nature_conv_dgrad(int32_t layer, const float* grad_out, int64_t batch, const float* wpd,
                                       const float* prev_act, float* grad_in, void* stream) {
+    if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad: layer must be 2 or 3");
     PPOX_REQUIRE(grad_out && wpd && prev_act && grad_in && batch >= 0, "ppox_nature_conv_dgrad: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wpd), "ppox_nature_conv_dgrad: 16B alignment");
-    if (batch == 0) return PPOX_OK;
     Args a{grad_out, nullptr, 0, 0, 0, wpd, nullptr, prev_act, grad_in, batch};
     hipStream_t s = ppox::as_stream(stream);
 #if !RG_F32
@@ -2413,8 +2413,8 @@ extern "C" int ppox_nature_conv_wgrad_split_ex(int32_t layer, const void* x, int
 
 extern "C" int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, int64_t batch, float* out,
                                            void* stream) {
+    if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(grad && act && out && batch >= 0, "ppox_nchw_to_nhwc_relu_grad: bad arguments");
-    if (batch == 0) return PPOX_OK;
     nchw_to_nhwc_mask<<<(unsigned)batch, 256, 0, ppox::as_stream(stream)>>>(grad, act, batch, out);
     PPOX_LAUNCHED("ppox_nchw_to_nhwc_relu_grad");
 }
@@ -2445,10 +2445,10 @@ int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq,
 
 extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch, const uint16_t* wqd,
                                             const float* prev_act, float* grad_in, void* stream) {
+    if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad_split: layer must be 2 or 3");
     PPOX_REQUIRE(grad_out && wqd && prev_act && grad_in && batch >= 0, "ppox_nature_conv_dgrad_split: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wqd), "ppox_nature_conv_dgrad_split: 16B alignment");
-    if (batch == 0) return PPOX_OK;
     Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch};
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 2) {
@@ -2472,13 +2472,13 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
 extern "C" int ppox_nature_conv_dgrad_split_ex(int32_t layer, const void* grad_out, int32_t grad_out_planes,
                                                int64_t batch, const uint16_t* wqd, const float* prev_act,
                                                void* grad_in, int32_t grad_in_planes, void* stream) {
+    if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad_split_ex: layer must be 2 or 3");
     PPOX_REQUIRE(grad_out && wqd && prev_act && grad_in && batch >= 0, "ppox_nature_conv_dgrad_split_ex: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wqd), "ppox_nature_conv_dgrad_split_ex: 16B alignment");
     // supported forms: conv3 (f32 in) -> planes out; conv2 planes in -> f32 out
     PPOX_REQUIRE((layer == 3 && !grad_out_planes) || (layer == 2 && !grad_in_planes),
                  "ppox_nature_conv_dgrad_split_ex: planes in/out combination not supported for this layer");
-    if (batch == 0) return PPOX_OK;
     Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, reinterpret_cast<float*>(grad_in), batch};
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 3) {
@@ -2516,9 +2516,9 @@ extern "C" int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_
 
 extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
                                   void* stream) {
+    if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(h3 && q_fwd && bias && f && batch >= 0, "ppox_nature_fc_fwd: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd), "ppox_nature_fc_fwd: 16B alignment");
-    if (batch == 0) return PPOX_OK;
     Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch};
     return launch_igemm_split<FcFwd>(a, q_fwd, ppox::ceil_div(batch, 128) * FcFwd::NCB, ppox::as_stream(stream),
                                      "ppox_nature_fc_fwd");
@@ -2526,9 +2526,9 @@ extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t
 
 extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
                                     void* stream) {
+    if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(df && q_dgrad && h3 && g3 && batch >= 0, "ppox_nature_fc_dgrad: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(q_dgrad), "ppox_nature_fc_dgrad: 16B alignment");
-    if (batch == 0) return PPOX_OK;
     Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch};
     return launch_igemm_split<FcDgrad>(a, q_dgrad, ppox::ceil_div(batch, 128) * FcDgrad::NCB, ppox::as_stream(stream),
                                        "ppox_nature_fc_dgrad");

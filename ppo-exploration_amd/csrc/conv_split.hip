@@ -172,10 +172,10 @@ extern "C" int ppox_nature_pack_split(const float* w1, const float* w2, const fl
 extern "C" int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx, int64_t T,
                                           int64_t N_env, int64_t x_sample_stride, const uint16_t* wq,
                                           const float* bias, float* y, void* stream) {
+    if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_conv_fwd_split: layer must be 1, 2 or 3");
     PPOX_REQUIRE(x && wq && bias && y && batch >= 0, "ppox_nature_conv_fwd_split: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(wq), "ppox_nature_conv_fwd_split: packed weights must be 16-byte aligned");
-    if (batch == 0) return PPOX_OK;
     if (layer != 1) {
         PPOX_REQUIRE(!idx, "ppox_nature_conv_fwd_split: idx is for layer 1 only");
         return ppox_conv::split_fwd23(layer, x, batch, wq, bias, y, ppox::as_stream(stream));

@@ -38,9 +38,9 @@ __global__ void __launch_bounds__(256) u8_to_f32(const uint4* __restrict__ src, 
 }  // namespace
 
 extern "C" int ppox_u8_to_f32(const void* src, int64_t n, float* dst, void* stream) {
+    if (n == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(src && dst && n >= 0 && n % 16 == 0, "ppox_u8_to_f32: n must be a multiple of 16");
     PPOX_REQUIRE(ppox::aligned16(src) && ppox::aligned16(dst), "ppox_u8_to_f32: 16B alignment");
-    if (n == 0) return PPOX_OK;
     const long long n16 = n / 16;
     const unsigned blocks = (unsigned)std::min<long long>((n16 + 255) / 256, 8192);
     u8_to_f32<<<blocks, 256, 0, ppox::as_stream(stream)>>>(reinterpret_cast<const uint4*>(src), n16,
@@ -50,10 +50,10 @@ extern "C" int ppox_u8_to_f32(const void* src, int64_t n, float* dst, void* stre
 
 extern "C" int ppox_gather_rows(const void* src, int64_t T, int64_t N, int64_t row_bytes, int64_t src_row_stride,
                                 const int64_t* idx, int64_t nrows, void* dst, void* stream) {
+    if (nrows == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(src && idx && dst, "ppox_gather_rows: null pointer");
     PPOX_REQUIRE(T > 0 && N > 0 && row_bytes > 0 && src_row_stride >= row_bytes && nrows >= 0,
                  "ppox_gather_rows: bad sizes");
-    if (nrows == 0) return PPOX_OK;
     const unsigned grid = (unsigned)std::min<long long>(nrows, 8192);
     hipStream_t s = ppox::as_stream(stream);
     const auto* sp = reinterpret_cast<const uint8_t*>(src);

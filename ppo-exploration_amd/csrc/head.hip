@@ -234,9 +234,9 @@ unsigned grid_for(long long n4) {
 }  // namespace
 
 extern "C" int ppox_relu_backward_(float* grad, const float* act, int64_t n, void* stream) {
+    if (n == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(grad && act && n >= 0 && n % 4 == 0, "ppox_relu_backward_: bad arguments (n % 4 == 0)");
     PPOX_REQUIRE(ppox::aligned16(grad) && ppox::aligned16(act), "ppox_relu_backward_: 16B alignment");
-    if (n == 0) return PPOX_OK;
     relu_bwd_kernel<<<grid_for(n / 4), 256, 0, ppox::as_stream(stream)>>>(grad, act, n / 4);
     PPOX_LAUNCHED("ppox_relu_backward_");
 }
@@ -277,10 +277,10 @@ extern "C" int ppox_head_grads(const float* f, const float* e, const float* dout
 
 extern "C" int ppox_skinny_linear(const float* x, const float* w, const float* bias, int64_t rows, int64_t h,
                                   int64_t n_out, float* y, void* stream) {
+    if (rows == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(x && w && bias && y && rows >= 0 && h > 0 && h % 4 == 0 && n_out >= 1 && n_out <= 8,
                  "ppox_skinny_linear: n_out must be 1..8, h a multiple of 4");
     PPOX_REQUIRE(ppox::aligned16(x) && ppox::aligned16(w), "ppox_skinny_linear: 16B alignment");
-    if (rows == 0) return PPOX_OK;
     const unsigned blocks = (unsigned)((rows + 3) / 4);
     hipStream_t s = ppox::as_stream(stream);
     switch (n_out) {
@@ -294,10 +294,10 @@ extern "C" int ppox_skinny_linear(const float* x, const float* w, const float* b
 
 extern "C" int ppox_skinny_dgrad(const float* g, const float* w, int64_t rows, int64_t h, int64_t n_out, float* d,
                                  void* stream) {
+    if (rows == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(g && w && d && rows >= 0 && h > 0 && h % 4 == 0 && n_out >= 1 && n_out <= 8,
                  "ppox_skinny_dgrad: n_out must be 1..8, h a multiple of 4");
     PPOX_REQUIRE(ppox::aligned16(w) && ppox::aligned16(d), "ppox_skinny_dgrad: 16B alignment");
-    if (rows == 0) return PPOX_OK;
     hipStream_t s = ppox::as_stream(stream);
     switch (n_out) {
 #define PPOX_SD(N) \
@@ -310,10 +310,10 @@ extern "C" int ppox_skinny_dgrad(const float* g, const float* w, int64_t rows, i
 
 extern "C" int ppox_outer_relu_backward(const float* dv, const float* w, const float* act, int64_t rows, int64_t h,
                                         float* out, void* stream) {
+    if (rows == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(dv && w && act && out && rows >= 0 && h > 0 && h % 4 == 0, "ppox_outer_relu_backward: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(act) && ppox::aligned16(out),
                  "ppox_outer_relu_backward: 16B alignment");
-    if (rows == 0) return PPOX_OK;
     outer_relu_kernel<<<grid_for(rows * h / 4), 256, 0, ppox::as_stream(stream)>>>(dv, w, act, rows, (int)(h / 4), out);
     PPOX_LAUNCHED("ppox_outer_relu_backward");
 }

@@ -740,9 +740,9 @@ extern "C" int ppox_ppo_box_loss_backward(const float* mu, const float* log_std,
 
 extern "C" int ppox_normal_sample(const float* mu, const float* log_std, int64_t N, int32_t D, int64_t env_offset,
                                   uint64_t seed, int64_t counter, float* actions, float* log_probs, void* stream) {
+    if (N == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(mu && log_std && actions && log_probs, "ppox_normal_sample: null pointer");
     PPOX_REQUIRE(D >= 1 && D <= MAXD && N >= 0, "ppox_normal_sample: bad sizes");
-    if (N == 0) return PPOX_OK;
     normal_sample_kernel<<<ppox::ceil_div(N, 256), 256, 0, ppox::as_stream(stream)>>>(mu, log_std, N, D, env_offset,
                                                                                      seed, counter, actions, log_probs);
     PPOX_LAUNCHED("ppox_normal_sample");
@@ -750,9 +750,9 @@ extern "C" int ppox_normal_sample(const float* mu, const float* log_std, int64_t
 
 extern "C" int ppox_categorical_sample(const float* logits, int64_t N, int32_t A, int64_t env_offset, uint64_t seed,
                                        int64_t counter, int32_t* actions, float* log_probs, void* stream) {
+    if (N == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(logits && actions && log_probs, "ppox_categorical_sample: null pointer");
     PPOX_REQUIRE(A >= 1 && A <= 64 && N >= 0, "ppox_categorical_sample: bad sizes");
-    if (N == 0) return PPOX_OK;
     hipStream_t s = ppox::as_stream(stream);
     PPOX_DISPATCH_A(A, MA, {
         categorical_sample_kernel<MA><<<ppox::ceil_div(N, 256), 256, 0, s>>>(logits, N, A, env_offset, seed, counter,

@@ -331,9 +331,9 @@ extern "C" int ppox_rms_scale_int_rewards(float* int_rewards, int64_t n, double*
 
 extern "C" int ppox_normalize_obs_u8(const uint8_t* x, int64_t rows, int64_t cols, int64_t row_stride,
                                      const double* mean, const double* var, float* out, void* stream) {
+    if (rows == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(x && mean && var && out, "ppox_normalize_obs_u8: null pointer");
     PPOX_REQUIRE(rows >= 0 && cols > 0 && row_stride >= cols, "ppox_normalize_obs_u8: bad sizes");
-    if (rows == 0) return PPOX_OK;
     const long long total = rows * cols;
     const unsigned grid = (unsigned)std::min<long long>(ppox::ceil_div(total, 256), 4096);
     normalize_kernel<uint8_t><<<grid, 256, 0, ppox::as_stream(stream)>>>(x, rows, cols, row_stride, mean, var, out);
@@ -342,9 +342,9 @@ extern "C" int ppox_normalize_obs_u8(const uint8_t* x, int64_t rows, int64_t col
 
 extern "C" int ppox_normalize_obs_f32(const float* x, int64_t rows, int64_t cols, int64_t row_stride,
                                       const double* mean, const double* var, float* out, void* stream) {
+    if (rows == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(x && mean && var && out, "ppox_normalize_obs_f32: null pointer");
     PPOX_REQUIRE(rows >= 0 && cols > 0 && row_stride >= cols, "ppox_normalize_obs_f32: bad sizes");
-    if (rows == 0) return PPOX_OK;
     const long long total = rows * cols;
     const unsigned grid = (unsigned)std::min<long long>(ppox::ceil_div(total, 256), 4096);
     normalize_kernel<float><<<grid, 256, 0, ppox::as_stream(stream)>>>(x, rows, cols, row_stride, mean, var, out);
@@ -354,9 +354,9 @@ extern "C" int ppox_normalize_obs_f32(const float* x, int64_t rows, int64_t cols
 extern "C" int ppox_normalize_obs_f32_ex(const float* x, int64_t rows, int64_t cols, int64_t row_stride,
                                          const double* mean, const double* var, double eps, double clip, float* out,
                                          void* stream) {
+    if (rows == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(x && mean && var && out && rows >= 0 && cols > 0 && row_stride >= cols,
                  "ppox_normalize_obs_f32_ex: bad arguments");
-    if (rows == 0) return PPOX_OK;
     const long long total = rows * cols;
     const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 8192);
     normalize_kernel<float><<<blocks, 256, 0, ppox::as_stream(stream)>>>(x, rows, cols, row_stride, mean, var, out, eps,

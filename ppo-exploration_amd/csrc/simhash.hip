@@ -59,19 +59,19 @@ __global__ void __launch_bounds__(256) simhash_count_kernel(const int32_t* __res
 
 extern "C" int ppox_simhash_keys(const float* obs, int64_t N, int64_t D, int64_t obs_stride, const double* A,
                                  int32_t* keys, void* stream) {
+    if (N == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(obs && A && keys, "ppox_simhash_keys: null pointer");
     PPOX_REQUIRE(N >= 0 && D >= 1 && obs_stride >= D, "ppox_simhash_keys: bad sizes");
-    if (N == 0) return PPOX_OK;
     simhash_keys_kernel<<<ppox::ceil_div(N, 256), 256, 0, ppox::as_stream(stream)>>>(obs, N, D, obs_stride, A, keys);
     PPOX_LAUNCHED("ppox_simhash_keys");
 }
 
 extern "C" int ppox_simhash_apply(const int32_t* keys_all, int64_t n_total, int64_t offset, int64_t n_local,
                                   uint32_t* counts, double beta, float* rewards, void* stream) {
+    if (n_total == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(keys_all && counts && (rewards || n_local == 0), "ppox_simhash_apply: null pointer");
     PPOX_REQUIRE(n_total >= 0 && offset >= 0 && n_local >= 0 && offset + n_local <= n_total,
                  "ppox_simhash_apply: bad sizes");
-    if (n_total == 0) return PPOX_OK;
     hipStream_t s = ppox::as_stream(stream);
     if (n_local > 0) {
         simhash_bonus_kernel<<<ppox::ceil_div(n_local, 256), 256, 0, s>>>(keys_all, offset, n_local, counts, beta,

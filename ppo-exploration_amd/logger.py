@@ -8,40 +8,72 @@ import sys
 
 
 class CSVWriter:
+    """CSV rows of the dumped key/values (logger.py:13-58): a key's 'prefix/' is dropped
+    (its second '/'-separated field is the column), columns are appended when new keys
+    appear — the file is then rewritten with the wider header and the earlier rows padded
+    with empty fields — and every other dump appends one row.  The reference appends new
+    columns in set order (hash order: it varies from run to run); here in first-seen order."""
+
     def __init__(self, path):
         self.path = path
         self.keys = []
         self.rows = []
+        self.file = open(path, "w+t")
+
+    @staticmethod
+    def _line(keys, row):
+        return ",".join("" if row.get(k) is None else str(row.get(k)) for k in keys) + "\n"
 
     def write(self, kv):
         flat = {}
         for k, v in kv.items():
-            flat[k.split("/", 1)[1] if k.find("/") > 0 else k] = v
+            flat[k.split("/")[1] if k.find("/") > 0 else k] = v
         new = [k for k in flat if k not in self.keys]
+        self.rows.append(flat)
         if new:
             self.keys.extend(new)
-        self.rows.append(flat)
-        with open(self.path, "w") as f:  # rewrite: header grows with new keys
-            f.write(",".join(self.keys) + "\n")
+            self.file.seek(0)
+            self.file.truncate()
+            self.file.write(",".join(self.keys) + "\n")
             for r in self.rows:
-                f.write(",".join("" if r.get(k) is None else str(r.get(k)) for k in self.keys) + "\n")
+                self.file.write(self._line(self.keys, r))
+        else:
+            self.file.write(self._line(self.keys, flat))
+        self.file.flush()
 
     def close(self):
-        pass
+        self.file.close()
 
 
 class TableWriter:
-    def __init__(self, stream=sys.stdout):
-        self.stream = stream
+    """The stdout table (logger.py:61-130): keys sorted, grouped under their 'tag/' header
+    rows, names and values truncated to 23 characters, floats as {:<8.3g}."""
+
+    def __init__(self, stream=None):
+        self.stream = stream if stream is not None else sys.stdout
+
+    @staticmethod
+    def _truncate(s, max_length=23):
+        return s[: max_length - 3] + "..." if len(s) > max_length else s
 
     def write(self, kv):
-        if not kv:
+        key2str = {}
+        tag = None
+        for key, value in sorted(kv.items()):
+            value_str = f"{value:<8.3g}" if isinstance(value, float) else str(value)
+            if key.find("/") > 0:
+                tag = key[: key.find("/") + 1]
+                key2str[self._truncate(tag)] = ""
+            if tag is not None and tag in key:
+                key = "   " + key[len(tag):]
+            key2str[self._truncate(key)] = self._truncate(value_str)
+        if not key2str:
             return
-        items = [(str(k), f"{v:<8.3g}" if isinstance(v, float) else str(v)) for k, v in sorted(kv.items())]
-        kw = max(len(k) for k, _ in items)
-        vw = max(len(v) for _, v in items)
-        bar = "-" * (kw + vw + 7)
-        lines = [bar] + [f"| {k:<{kw}} | {v:<{vw}} |" for k, v in items] + [bar]
+        kw = max(map(len, key2str.keys()))
+        vw = max(map(len, key2str.values()))
+        dashes = "-" * (kw + vw + 7)
+        lines = [dashes] + [f"| {k}{' ' * (kw - len(k))} | {v}{' ' * (vw - len(v))} |" for k, v in key2str.items()]
+        lines.append(dashes)
         self.stream.write("\n".join(lines) + "\n")
         self.stream.flush()
 
@@ -64,6 +96,13 @@ class Logger:
         for o in self.outputs:
             o.write(dict(self.kv))
         self.kv.clear()
+
+    def get_dir(self):
+        return self.folder
+
+    def close(self):
+        for o in self.outputs:
+            o.close()
 
 
 Logger.CURRENT = Logger([TableWriter()])
@@ -88,6 +127,8 @@ def configure(algorithm, environment, log_to_file=False, folder=None, quiet=Fals
         os.makedirs(folder, exist_ok=True)
         name = "run" + datetime.datetime.now().strftime("-%Y-%m-%d-%H-%M-%S-%f") + ".csv"
         outputs.append(CSVWriter(os.path.join(folder, name)))
+    if Logger.CURRENT is not None:
+        Logger.CURRENT.close()  # a reconfigure ends the previous run's CSV file
     Logger.CURRENT = Logger(outputs, folder=folder)
     if not quiet:
         print(f"Logging to {folder}")

@@ -76,8 +76,10 @@ def icm_loss_sharded(icm, x, acts, pos, B, beta, ctx):
         inv = ((a_hat - a_full[j]) ** 2).sum() / (npair * a_hat.shape[1])
     loss = (1 - beta) * inv + beta * fwd
     loss.backward()
-    g = ctx.all_reduce_(phi_all.grad)
-    phi.backward(g[pos])
+    g = phi_all.grad if phi_all.grad is not None else torch.zeros_like(full)
+    g = ctx.all_reduce_(g)
+    if phi.shape[0]:
+        phi.backward(g[pos])
     return loss.detach()
 
 
@@ -198,6 +200,11 @@ class BaseAlgorithm:
             g.add_(self.dls.view_as(g))
         return dout, dv, div
 
+    def _empty_outputs(self, intrinsic=False):
+        """Zero-row head outputs (out, value, int value) for a rank that owns no rows of a minibatch."""
+        z = torch.zeros(0, device=self.device)
+        return torch.zeros(0, self.n_actions, device=self.device), z, (z if intrinsic else None)
+
     def _fwd_train(self, obs):
         """Training forward of the policy net -> (out, v, iv, ctx).  NatureCNN nets on the
         libppox trunk take the explicit path (models.CnnActorCritic.forward_train: no
@@ -234,12 +241,18 @@ class BaseAlgorithm:
         NatureCNN path at world > 1 the bucket is reduced in two pieces: the fc + head part
         (flat params after the convs, 96 % of the bytes) asynchronously as soon as backward_train
         has produced it, overlapping the conv backward, then the conv part."""
-        if has_rows and ctx is not None and self.dist.enabled:
-            net = self.policy.net
+        net = self.policy.net
+        if self.dist.enabled and getattr(net, "conv_impl", None) is not None and hasattr(net, "backward_train"):
+            # the collective sequence depends only on state every rank shares (world size and the
+            # net type), never on this rank's row count: a rank with no rows of the minibatch
+            # issues the same two all-reduces on its zeroed bucket (otherwise the ranks mismatch)
             n0 = (net.feature_extractor[7].weight.data_ptr() - self.flat.data.data_ptr()) // 4
             work = []
-            net.backward_train(ctx, dout, dv, div,
-                               dense_ready=lambda: work.append(self.dist.all_reduce_async_(self.flat.grad[n0:])))
+            start = lambda: work.append(self.dist.all_reduce_async_(self.flat.grad[n0:]))  # noqa: E731
+            if has_rows:
+                net.backward_train(ctx, dout, dv, div, dense_ready=start)
+            else:
+                start()
             self.dist.all_reduce_(self.flat.grad[:n0])
             for w in work:
                 w.wait()
@@ -283,19 +296,28 @@ class BaseAlgorithm:
         self._sample_counter += 1
 
     def _finish_episodes(self):
+        """Episode bookkeeping of one rollout over ALL envs (ppo.py:180-183, 98-109): every rank
+        gathers the (T, N_global) episode returns / lengths, so num_episodes, ep_info_buffer and
+        the reward_target decision of learn() are identical on every rank (the reference's
+        step-then-env order: row-major over (t, env))."""
         ro = self.rollout
-        fin = ~torch.isnan(ro.done_ret)
-        self.num_episodes += int(ro.masks.sum().item()) * 1  # local envs (ppo.py:180-181)
-        if bool(fin.any()):
-            r = ro.done_ret[fin].cpu().numpy()
-            ln = ro.done_len[fin].cpu().numpy()
-            for x, y in zip(r, ln):
+        ret = self.dist.all_gather_cat(ro.done_ret, dim=1)
+        ln = self.dist.all_gather_cat(ro.done_len, dim=1)
+        fin = ~torch.isnan(ret)
+        n_fin = int(fin.sum().item())
+        self.num_episodes += n_fin
+        if n_fin:
+            for x, y in zip(ret[fin].cpu().numpy(), ln[fin].cpu().numpy()):
                 self.ep_info_buffer.append({"r": float(x), "l": int(y)})
+
+    def _batch(self, total):
+        """Minibatch size: batch_size=None is one full-rollout minibatch (buffer.py:248-249)."""
+        return total if self.batch_size is None else int(self.batch_size)
 
     def _epoch_minibatches(self, total):
         """One global numpy permutation (buffer.py:239) -> per-minibatch (local idx, global size)."""
         perm = np.random.permutation(total)
-        bs = total if self.batch_size is None else self.batch_size
+        bs = self._batch(total)
         sizes = [min(bs, total - s) for s in range(0, total, bs)]
         # pinned staging: a pageable host->device copy blocks the host until the stream
         # drains, idling the GPU while the next epoch's permutation is drawn
@@ -430,12 +452,12 @@ class PPO(BaseAlgorithm):
         Bl = idx.numel()
         net = self.policy.net
         self._zero_policy_grad(Bl)
+        ctx = out = v = None
         if Bl > 0:
             out, v, _, ctx = self._fwd_train(self._train_obs(ro, idx))
             out_d, v_d = out.detach().contiguous(), v.detach().contiguous()
         else:
-            out_d = torch.zeros(0, self.n_actions, device=self.device)
-            v_d = torch.zeros(0, device=self.device)
+            out_d, v_d, _ = self._empty_outputs()
         dout, dv, _ = self._loss_grads(out_d, v_d, None, idx, ro.tensors(), adv_stats, B_global, 0.0, scale)
         if extra_backward is None:
             self._bwd_reduce(ctx, out, v, None, dout, dv, has_rows=Bl > 0)
@@ -449,11 +471,11 @@ class PPO(BaseAlgorithm):
         total = self.nstep * self.num_envs
         self.loss_accum.zero_()
         adv, _ = self._global_advantages(ro)
-        n_mb = (total + self.batch_size - 1) // self.batch_size
-        stats = torch.empty(n_mb, 4, dtype=torch.float64, device=self.device)
+        bs = self._batch(total)
+        stats = torch.empty((total + bs - 1) // bs, 4, dtype=torch.float64, device=self.device)
         for _ in range(self.n_epochs):
             perm_dev, local, offs, sizes = self._epoch_minibatches(total)
-            native.minibatch_adv_stats(adv, None, perm_dev, total, self.batch_size, self.nstep, self.num_envs, stats)
+            native.minibatch_adv_stats(adv, None, perm_dev, total, bs, self.nstep, self.num_envs, stats)
             for k, B in enumerate(sizes):
                 idx = local[offs[k]:offs[k + 1]]
                 self._minibatch(idx, stats[k], B)
@@ -540,11 +562,18 @@ class PPO_RND(BaseAlgorithm):
         elif full.data_ptr() != ir.data_ptr():
             ir.copy_(full)
 
-    def train_rnd(self, obs):
-        """ppo.py:487-502."""
-        x = self.normalize_obs(self._rnd_input(obs))
+    def train_rnd(self, obs, B_global=None):
+        """ppo.py:487-502.  MSE(pred, target) over the GLOBAL minibatch: this rank's squared
+        errors summed and divided by the global row count B_global, so the all-reduced gradient
+        is the reference's mean over all B rows (a per-rank mean would weight ranks' rows
+        unequally).  obs None: this rank owns no rows (it still joins the all-reduce)."""
+        if obs is None or obs.shape[0] == 0:
+            x = torch.zeros(0, self.rnd_features, device=self.device)
+        else:
+            x = self.normalize_obs(self._rnd_input(obs))
         p, tgt = self.rnd(x)
-        loss = F.mse_loss(p, tgt)
+        n = p.numel() if B_global is None else int(B_global)
+        loss = F.mse_loss(p, tgt, reduction="sum") / n
         self.rnd_flat.zero_grad()
         loss.backward()
         self.dist.all_reduce_(self.rnd_flat.grad)
@@ -555,25 +584,29 @@ class PPO_RND(BaseAlgorithm):
         total = self.nstep * self.num_envs
         self.loss_accum.zero_()
         adv, iadv = self._global_advantages(ro, intrinsic=True)
-        n_mb = (total + self.batch_size - 1) // self.batch_size
-        stats = torch.empty(n_mb, 4, dtype=torch.float64, device=self.device)
+        bs = self._batch(total)
+        stats = torch.empty((total + bs - 1) // bs, 4, dtype=torch.float64, device=self.device)
         net = self.policy.net
         roll = ro.tensors()
         for _ in range(self.n_epochs):
             perm_dev, local, offs, sizes = self._epoch_minibatches(total)
-            native.minibatch_adv_stats(adv, iadv, perm_dev, total, self.batch_size, self.nstep, self.num_envs, stats)
+            native.minibatch_adv_stats(adv, iadv, perm_dev, total, bs, self.nstep, self.num_envs, stats)
             for k, B in enumerate(sizes):
                 idx = local[offs[k]:offs[k + 1]]
                 Bl = idx.numel()
                 self._zero_policy_grad(Bl)
-                obs = ro._gather(ro.observations, idx)
-                out, v, iv, ctx = self._fwd_train(obs)
-                od, vd, ivd = out.detach().contiguous(), v.detach().contiguous(), iv.detach().contiguous()
+                obs = ctx = out = v = iv = None
+                if Bl > 0:
+                    obs = ro._gather(ro.observations, idx)
+                    out, v, iv, ctx = self._fwd_train(obs)
+                    od, vd, ivd = out.detach().contiguous(), v.detach().contiguous(), iv.detach().contiguous()
+                else:  # no rows of this minibatch on this rank: zero contributions, same collectives
+                    od, vd, ivd = self._empty_outputs(intrinsic=True)
                 dout, dv, div = self._loss_grads(od, vd, ivd, idx, roll, stats[k], B, self.int_vf_coef, 1.0)
                 self._bwd_reduce(ctx, out, v, iv, dout, dv, div, has_rows=Bl > 0)
                 self.flat.adam_step(self.lr, self.max_grad_norm)
                 if np.random.randn() < 0.25:                                   # ppo.py:468-469
-                    self.train_rnd(obs)
+                    self.train_rnd(obs, B)
         acc = self._record_train()
         logger.record("train/intrinsic_loss", acc[4] / max(acc[5], 1.0))
         self._n_updates += self.n_epochs
@@ -610,7 +643,7 @@ class PPO_ICM(BaseAlgorithm):
         self.icm_accum = torch.zeros(1, dtype=torch.float64, device=self.device)
 
     def _icm_x(self, obs):
-        x = obs.reshape(obs.shape[0], -1)
+        x = obs.reshape(obs.shape[0], int(np.prod(obs.shape[1:])))
         if x.dtype == torch.uint8 and x.is_cuda and x.is_contiguous() and x.numel() % 16 == 0:
             return native.u8_to_f32(x)
         return x.float()
@@ -650,21 +683,25 @@ class PPO_ICM(BaseAlgorithm):
         self.loss_accum.zero_()
         self.icm_accum.zero_()
         adv, _ = self._global_advantages(ro)
-        n_mb = (total + self.batch_size - 1) // self.batch_size
-        stats = torch.empty(n_mb, 4, dtype=torch.float64, device=self.device)
+        bs = self._batch(total)
+        stats = torch.empty((total + bs - 1) // bs, 4, dtype=torch.float64, device=self.device)
         net, icm = self.policy.net, self.intrinsic_module
         roll = ro.tensors()
         for _ in range(self.n_epochs):
             perm_dev, local, offs, sizes = self._epoch_minibatches(total)
-            native.minibatch_adv_stats(adv, None, perm_dev, total, self.batch_size, self.nstep, self.num_envs, stats)
+            native.minibatch_adv_stats(adv, None, perm_dev, total, bs, self.nstep, self.num_envs, stats)
             for k, B in enumerate(sizes):
                 idx = local[offs[k]:offs[k + 1]]
                 Bl = idx.numel()
                 self._zero_policy_grad(Bl)
                 self.icm_flat.zero_grad()
                 obs = ro._gather(ro.observations, idx)
-                out, v, _, ctx = self._fwd_train(obs)
-                od, vd = out.detach().contiguous(), v.detach().contiguous()
+                ctx = out = v = None
+                if Bl > 0:
+                    out, v, _, ctx = self._fwd_train(obs)
+                    od, vd = out.detach().contiguous(), v.detach().contiguous()
+                else:  # no rows of this minibatch on this rank: zero contributions, same collectives
+                    od, vd, _ = self._empty_outputs()
                 dout, dv, _ = self._loss_grads(od, vd, None, idx, roll, stats[k], B, 0.0, float(self.policy_weight))
                 # ICM on consecutive rows of the (owned part of the) permuted minibatch (ppo.py:684-688)
                 rows = (idx % self.nstep) * self.local_envs + idx // self.nstep
@@ -673,7 +710,8 @@ class PPO_ICM(BaseAlgorithm):
                 else:
                     acts = ro.actions.reshape(-1, self.n_actions)[rows]
                 x = self._icm_x(obs)
-                self._bwd_train(ctx, out, v, None, dout, dv)
+                if Bl > 0:
+                    self._bwd_train(ctx, out, v, None, dout, dv)
                 # pairs (row j, row j+1) of the permuted minibatch; each row is encoded once
                 # (the reference encodes s and s' separately: same rows, same math) and at
                 # world > 1 the pairs cross rank boundaries (icm_loss_sharded)

@@ -80,9 +80,12 @@ class Box:
         self.shape = tuple(shape)
 
 
-def make_fakevec(VecEnv, n_envs, obs_dim, action_space, seed, done_p=0.05, obs_shape=None):
+def make_fakevec(VecEnv, n_envs, obs_dim, action_space, seed, done_p=0.05, obs_shape=None, frames=False):
     """Action-independent env with a PRIVATE RandomState (does not touch np's
-    global RNG, so the reference's own np.random consumption is undisturbed)."""
+    global RNG, so the reference's own np.random consumption is undisturbed).
+    frames=True: (4, 84, 84) frame stacks of integer pixel values 0..255 as float32 (what
+    the reference feeds the NatureCNN: VecFrameStack frames through torch.FloatTensor),
+    made of 7x7-pixel blocks so the recorded fixture compresses."""
     shape = obs_shape if obs_shape is not None else (obs_dim,)
 
     class FakeVec(VecEnv):
@@ -94,6 +97,9 @@ def make_fakevec(VecEnv, n_envs, obs_dim, action_space, seed, done_p=0.05, obs_s
             self.trace = {"obs": [], "rew": [], "done": []}
 
         def _obs(self):
+            if frames:
+                blocks = self.rs.randint(0, 256, size=(n_envs, 4, 12, 12))
+                return np.repeat(np.repeat(blocks, 7, axis=2), 7, axis=3).astype(np.float32)
             return self.rs.randn(n_envs, *shape).astype(np.float32)
 
         def reset(self):
@@ -349,6 +355,9 @@ def gen_train(R):
         ("disc4sat", Discrete(4), 5, 3, 8, 12, 1, 16, 22, {"sat": True}),
         ("box2", Box((2,)), 3, 4, 8, 8, 2, 16, 23, {}),
         ("disc18", Discrete(18), 6, 2, 12, 24, 1, 16, 24, {}),
+        # BASELINE config 1 (CartPole-v1 shape): 8 envs x 128 steps, MLP hidden 128, the
+        # reference's default batch 128 and 10 epochs (80 optimizer steps); batches not recorded
+        ("cartpole", Discrete(2), 4, 8, 128, 128, 10, 128, 25, {"no_batches": True, "defaults": True}),
     ]
     for name, aspace, D, N, T, B, E, H, seed, kw in cases:
         rec = _record_logger(R)
@@ -356,8 +365,11 @@ def gen_train(R):
         torch.manual_seed(seed)
         env = make_fakevec(R.VecEnv, N, D, aspace, seed=1000 + seed)
         R.ppo.make_env = lambda env_id, n_envs=4, env=env: env
-        alg = R.ppo.PPO(env_id="Fake-v0", nstep=T, batch_size=B, n_epochs=E, hidden_size=H,
-                        max_grad_norm=0.5, ent_coef=0.01, vf_coef=1.0)
+        if kw.get("defaults"):  # the reference's own defaults (ppo.py:139-153) for the rest
+            alg = R.ppo.PPO(env_id="Fake-v0", nstep=T, batch_size=B, n_epochs=E, hidden_size=H)
+        else:
+            alg = R.ppo.PPO(env_id="Fake-v0", nstep=T, batch_size=B, n_epochs=E, hidden_size=H,
+                            max_grad_norm=0.5, ent_coef=0.01, vf_coef=1.0)
         if kw.get("sat"):
             with torch.no_grad():  # push the actor into softmax saturation (eps clamp)
                 alg.policy.net.actor[-1].weight.mul_(60.0)
@@ -395,13 +407,15 @@ def gen_train(R):
         out[p + "env_rew"] = np.stack(tr["rew"])
         out[p + "env_done"] = np.stack(tr["done"])
         # rollout after collect (before get() flattened it we cannot see it; use batches)
-        for i, b in enumerate(batches):
-            for f in b._fields:
-                out[p + f"mb{i}_{f}"] = getattr(b, f).numpy()
-        for i, gs in enumerate(store["grads"]):
-            for j, g in enumerate(gs):
-                out[p + f"mb{i}_grad{j}"] = g.numpy()
+        if not kw.get("no_batches"):
+            for i, b in enumerate(batches):
+                for f in b._fields:
+                    out[p + f"mb{i}_{f}"] = getattr(b, f).numpy()
+            for i, gs in enumerate(store["grads"]):
+                for j, g in enumerate(gs):
+                    out[p + f"mb{i}_grad{j}"] = g.numpy()
         out[p + "nmb"] = np.int64(len(batches))
+        out[p + "np_state_after"] = np.random.get_state()[1].copy()
         for k in ("train/entropy_loss", "train/policy_gradient_loss", "train/value_loss", "train/total_loss"):
             out[p + k.split("/")[1]] = np.float64(rec[k])
     save("train_ppo", **out)
@@ -526,6 +540,115 @@ def gen_cnn(R):
     save("cnn", **out)
 
 
+# --------------------------------------------------------------------------
+# (9) One PPO iteration of the NatureCNN (the benchmarked Atari path): the live
+#     ppo.PPO (ppo.py:121-259) with the checkpoint CnnActorCritic
+#     (.ipynb_checkpoints/models-checkpoint.py:48-90) as policy.net.  Policy.act /
+#     evaluate are net-agnostic for Discrete (models.py:30-73: self.net(obs) ->
+#     (logits, values)), so only the net and its Adam are swapped after construction.
+#     Frames are integer-valued float32 (4, 84, 84) stacks.  Recorded: the rollout after
+#     collect (obs as uint8), the init checksums (the net is re-created from its torch
+#     seed), post-train() weights (full small tensors, a fixed index sample of the large
+#     ones + whole-tensor update sums), the loss scalars and numpy's RNG state.
+# --------------------------------------------------------------------------
+def _load_checkpoint_models():
+    spec = importlib.util.spec_from_file_location(
+        "models_checkpoint", os.path.join(REF, ".ipynb_checkpoints", "models-checkpoint.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def weight_sample_index(numel, k):
+    """Fixed sample of flat indices of a large tensor (also recomputed by the tests)."""
+    if numel <= 8192:
+        return np.arange(numel, dtype=np.int64)
+    return np.sort(np.random.RandomState(1000 + k).choice(numel, 8192, replace=False)).astype(np.int64)
+
+
+def gen_cnn_train(R):
+    import torch
+    ck = _load_checkpoint_models()
+    out = {}
+    for name, A, N, T, B, E, seed, net_seed in (("cnn4", 4, 4, 16, 24, 2, 61, 62),
+                                                ("cnn18", 18, 2, 16, 12, 1, 63, 64)):
+        rec = _record_logger(R)
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+        env = make_fakevec(R.VecEnv, N, None, Discrete(A), seed=4000 + seed, obs_shape=(4, 84, 84), frames=True)
+        R.ppo.make_env = lambda env_id, n_envs=4, env=env: env
+        alg = R.ppo.PPO(env_id="Fake-v0", nstep=T, batch_size=B, n_epochs=E)  # reference defaults otherwise
+        torch.manual_seed(net_seed)
+        net = ck.CnnActorCritic(4, A)
+        alg.policy.net = net
+        alg.optimizer = torch.optim.Adam(net.parameters(), lr=alg.lr)
+        init = {k: v.detach().clone() for k, v in net.state_dict().items()}
+        alg.collect_samples()
+        st = alg.rollout
+        p = name + "_"
+        out[p + "cfg"] = np.array([N, T, B, E, A, seed, net_seed], np.int64)
+        out[p + "obs"] = st.observations.astype(np.uint8)                   # (T, N, 4, 84, 84), integer-valued
+        assert np.array_equal(out[p + "obs"].astype(np.float32), st.observations)
+        for f in ("actions", "rewards", "values", "masks", "action_log_probs", "advantages", "returns"):
+            out[p + "roll_" + f] = np.asarray(getattr(st, f)).copy()
+        out[p + "last_obs"] = np.asarray(alg.last_obs).astype(np.uint8)
+        alg.train()
+        for k, (key, v0) in enumerate(init.items()):
+            v1 = net.state_dict()[key].detach()
+            out[p + "wsum0_" + key] = np.float64(v0.double().sum())
+            out[p + "whead0_" + key] = v0.flatten()[:16].numpy()
+            idx = weight_sample_index(v1.numel(), k)
+            out[p + "w1idx_" + key] = idx
+            out[p + "w1_" + key] = v1.flatten().numpy()[idx]
+            d = (v1 - v0).double()
+            out[p + "dsum_" + key] = np.float64(d.sum())
+            out[p + "dabs_" + key] = np.float64(d.abs().sum())
+        for k in ("train/entropy_loss", "train/policy_gradient_loss", "train/value_loss", "train/total_loss"):
+            out[p + k.split("/")[1]] = np.float64(rec[k])
+        out[p + "np_state_after"] = np.random.get_state()[1].copy()
+    save("train_cnn", **out)
+
+
+# --------------------------------------------------------------------------
+# (9b) logger CSV schema (logger.py:13-58, 195-234): configure(log_to_file=True) and
+#      three dumps whose later ones bring new keys (the header is rewritten and the
+#      earlier rows padded); the stdout table of the first dump is recorded too.
+# --------------------------------------------------------------------------
+def gen_logger(R):
+    import io
+    import tempfile
+    import contextlib
+    lg = importlib.reload(R.logger)  # earlier generators replaced record/dump/configure
+    dumps = [
+        {"time/total timesteps": 512, "time/total_time": 1.25},
+        {"time/total timesteps": 1024, "rollout/ep_rew_mean": 3.5, "rollout/num_episodes": 7,
+         "time/total_time": 2.5, "train/entropy_loss": -1.3862, "train/policy_gradient_loss": -0.0125,
+         "train/value_loss": 0.5, "train/total_loss": 0.48},
+        {"Progress": "66.67%", "time/total timesteps": 1536, "rollout/mean_int_reward": 0.03125,
+         "train/icm_loss": 0.25, "time/total_time": 3.75},
+    ]
+    with tempfile.TemporaryDirectory() as d:
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            lg.configure("PPO", "Fake-v0", log_to_file=True, folder=d)
+        lg.Logger.CURRENT.outputs[0].file = buf   # stdout table into the buffer
+        tables = []
+        for kv in dumps:
+            start = len(buf.getvalue())
+            for k, v in kv.items():
+                lg.record(k, v)
+            lg.dump(step=0)
+            tables.append(buf.getvalue()[start:])
+        folder = os.path.join(d, "PPO", "Fake-v0")
+        (csv_name,) = os.listdir(folder)
+        text = open(os.path.join(folder, csv_name)).read()
+    out = {"n_dumps": np.int64(len(dumps)), "csv": np.array(text), "table0": np.array(tables[0]),
+           "table1": np.array(tables[1])}
+    for i, kv in enumerate(dumps):
+        out[f"d{i}_keys"] = np.array(list(kv.keys()))
+        out[f"d{i}_vals"] = np.array([repr(v) for v in kv.values()])
+    save("logger", **out)
+
 
 # --------------------------------------------------------------------------
 # (10) ES-NSRA pieces: FeedForwardNetwork.predict (evolution_strategies.py:50-63),
@@ -601,6 +724,8 @@ def main():
     gen_rnd(R)
     gen_icm(R)
     gen_cnn(R)
+    gen_cnn_train(R)
+    gen_logger(R)
     gen_es(R)
     return 0
 

@@ -55,7 +55,11 @@ def _weights(alg):
     return w
 
 
-def _rank(rank, world, port, path, q, algo):
+def _rnd_weights(alg):
+    return alg.rnd_flat.data[:alg.rnd_flat.n].cpu().numpy() if hasattr(alg, "rnd_flat") else None
+
+
+def _rank(rank, world, port, path, q, algo, cfg):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "ppo-exploration_amd"))
@@ -68,32 +72,40 @@ def _rank(rank, world, port, path, q, algo):
         data = dict(np.load(path))
         np.random.seed(11)
         torch.manual_seed(11)
-        alg = getattr(ppo, algo)(**CFG)
+        alg = getattr(ppo, algo)(**cfg)
         _load_shard(alg, data, alg.env_offset, alg.local_envs)
         alg.train()
-        q.put((rank, _weights(alg), alg.loss_accum.cpu().numpy()))
+        q.put((rank, _weights(alg), alg.loss_accum.cpu().numpy(), _rnd_weights(alg)))
     except Exception as e:  # surface the failure to the parent
-        q.put((rank, repr(e), None))
+        q.put((rank, repr(e), None, None))
     finally:
         tdist.destroy_process_group()
 
 
-@pytest.mark.parametrize("algo,math", [("PPO", "split"), ("PPO", "f32"), ("PPO_ICM", "f32"), ("PPO_RND", "f32")])
-def test_two_ranks_match_one_rank(algo, math, monkeypatch):
+@pytest.mark.parametrize("algo,math,batch", [("PPO", "split", 48), ("PPO", "f32", 48), ("PPO_ICM", "f32", 48),
+                                              ("PPO_RND", "f32", 48), ("PPO", "split", 127),
+                                              ("PPO_ICM", "f32", 127), ("PPO_RND", "f32", 127)])
+def test_two_ranks_match_one_rank(algo, math, batch, monkeypatch):
     """Two ranks (gloo, one GPU) train() == one rank on the same rollout.  PPO_RND covers
     the intrinsic head, the two-piece overlapped gradient all-reduce and train_rnd's own
     all-reduce (its obs_rms is never updated here: the shape-() state broadcasts).
     PPO_ICM: the ICM pairs (row j, row j+1) of each global minibatch cross the rank
     boundary; icm_loss_sharded exchanges features so the update equals one rank's.
+    batch 127 over 128 rows: the last minibatch has ONE row, so one rank owns no rows of it
+    and must still issue the same collectives (a mismatch hangs or fails here).
     The decomposition is checked with exact-f32 conv math; split-bf16 math reorders
     more (3 x 2^-22 per product): after Adam's sign-normalised first steps a few
     near-zero-gradient weights can then land ~2 lr apart between the 1- and 2-rank
-    runs, so the strict weight tolerance is applied to it on PPO only."""
+    runs, so the strict weight tolerance is applied to it on PPO only.
+    The RND weights are compared on their own, as updates (w - w0) against 1 % of the
+    learning rate: a per-rank instead of global MSE mean (rows weighted by 1/B_rank) moves
+    them by a sizeable fraction of lr and cannot pass."""
     import ppo
     monkeypatch.setenv("PPOX_CONV_MATH", math)  # inherited by the spawned ranks
+    cfg = dict(CFG, batch_size=batch)
     np.random.seed(11)
     torch.manual_seed(11)
-    ref = getattr(ppo, algo)(**CFG)
+    ref = getattr(ppo, algo)(**cfg)
     ref.collect_samples()
     ro = ref.rollout
     data = {"obs": ro.obs_slots.cpu().numpy()}
@@ -102,10 +114,12 @@ def test_two_ranks_match_one_rank(algo, math, monkeypatch):
     # 1-rank reference train on exactly this rollout (fresh agent, same seeds)
     np.random.seed(11)
     torch.manual_seed(11)
-    one = getattr(ppo, algo)(**CFG)
-    _load_shard(one, data, 0, CFG["n_envs"])
+    one = getattr(ppo, algo)(**cfg)
+    rnd0 = _rnd_weights(one)
+    _load_shard(one, data, 0, cfg["n_envs"])
     one.train()
     w_one = _weights(one)
+    rnd_one = _rnd_weights(one)
     acc_one = one.loss_accum.cpu().numpy()
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "rollout.npz")
@@ -113,16 +127,19 @@ def test_two_ranks_match_one_rank(algo, math, monkeypatch):
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
         port = _port()
-        procs = [ctx.Process(target=_rank, args=(r, 2, port, path, q, algo)) for r in range(2)]
+        procs = [ctx.Process(target=_rank, args=(r, 2, port, path, q, algo, cfg)) for r in range(2)]
         for p in procs:
             p.start()
         res = [q.get(timeout=300) for _ in range(2)]
         for p in procs:
             p.join(timeout=60)
-    for rank, w, acc in res:
+    for rank, w, acc, rnd in res:
         if isinstance(w, str):
             if "gloo" in w.lower() and "cuda" in w.lower():
                 pytest.skip(f"gloo without device-tensor support on this build: {w}")
             raise AssertionError(f"rank {rank}: {w}")
         np.testing.assert_allclose(acc, acc_one, rtol=1e-4, atol=1e-6)
         np.testing.assert_allclose(w, w_one, rtol=1e-4, atol=1e-5)
+        if rnd is not None:
+            assert not np.array_equal(rnd_one, rnd0), "no RND update happened"
+            np.testing.assert_allclose(rnd - rnd0, rnd_one - rnd0, rtol=0, atol=0.01 * one.int_lr)

@@ -86,7 +86,13 @@ def _state_close(sd, f, prefix, rtol=1e-5, atol=1e-6):
         np.testing.assert_allclose(v.detach().numpy(), f[prefix + k], rtol=rtol, atol=atol, err_msg=k)
 
 
-@pytest.mark.parametrize("name", ["disc2", "disc4sat", "box2", "disc18"])
+def train_kwargs(name):
+    """Hyper-parameters of a train_ppo fixture case beyond its cfg row: 'cartpole' (BASELINE
+    config 1) ran with the reference's defaults, the others with max_grad_norm 0.5."""
+    return {} if name == "cartpole" else dict(max_grad_norm=0.5, ent_coef=0.01, vf_coef=1.0)
+
+
+@pytest.mark.parametrize("name", ["disc2", "disc4sat", "box2", "disc18", "cartpole"])
 def test_ppo_train_iteration(golden, name):
     """Full collect + GAE + train() replayed against the reference's run."""
     f = golden("train_ppo")
@@ -95,8 +101,7 @@ def test_ppo_train_iteration(golden, name):
     env = ReplayVecEnv(f[p + "env_obs"], f[p + "env_rew"], f[p + "env_done"], space_from_code(code))
     np.random.seed(seed)
     torch.manual_seed(seed)
-    alg = OraclePPO(env, nstep=T, batch_size=B, n_epochs=E, hidden_size=H, max_grad_norm=0.5,
-                    ent_coef=0.01, vf_coef=1.0)
+    alg = OraclePPO(env, nstep=T, batch_size=B, n_epochs=E, hidden_size=H, **train_kwargs(name))
     if name == "disc4sat":
         with torch.no_grad():
             alg.net.actor[-1].weight.mul_(60.0)
@@ -104,6 +109,7 @@ def test_ppo_train_iteration(golden, name):
     alg.collect()
     alg.train()
     _state_close(alg.net.state_dict(), f, p + "w1_")
+    np.testing.assert_array_equal(np.random.get_state()[1], f[p + "np_state_after"])
     np.testing.assert_allclose(alg.stats["loss"], f[p + "total_loss"], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(alg.stats["pl"], f[p + "policy_gradient_loss"], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(alg.stats["vl"], f[p + "value_loss"], rtol=1e-5, atol=1e-7)
@@ -181,3 +187,33 @@ def test_simhash_bonus_bitexact(golden):
             out = sh.apply(f[p + "obs"][step], f[p + "rew_in"][step])
             np.testing.assert_array_equal(out, f[p + "rew_out"][step])
         assert len(sh.count_table) == int(f[p + "n_keys"])
+
+
+@pytest.mark.parametrize("name", ["cnn4", "cnn18"])
+def test_cnn_train_iteration(golden, name):
+    """The benchmarked Atari path on the oracle: NatureCNN collect + GAE + train() replayed
+    against the reference's own run (live ppo.PPO with the checkpoint CnnActorCritic as
+    policy.net, make_golden.py gen_cnn_train)."""
+    f = golden("train_cnn")
+    p = name + "_"
+    N, T, B, E, A, seed, net_seed = (int(x) for x in f[p + "cfg"])
+    obs = np.concatenate([f[p + "obs"], f[p + "last_obs"][None]])
+    env = ReplayVecEnv(obs, f[p + "roll_rewards"], f[p + "roll_masks"].astype(bool), Discrete(A))
+    np.random.seed(seed)
+    torch.manual_seed(net_seed)
+    net = M.NatureCNN(4, A)
+    for k, v in net.state_dict().items():
+        np.testing.assert_array_equal(v.flatten()[:16].numpy(), f[p + "whead0_" + k])
+    alg = OraclePPO(env, nstep=T, batch_size=B, n_epochs=E, net=net)
+    alg.collect()
+    np.testing.assert_array_equal(alg.rollout.actions, f[p + "roll_actions"])
+    np.testing.assert_allclose(alg.rollout.values, f[p + "roll_values"], rtol=1e-6, atol=1e-4)
+    np.testing.assert_array_equal(alg.rollout.adv, f[p + "roll_advantages"])
+    alg.train()
+    for k, v in net.state_dict().items():
+        idx = f[p + "w1idx_" + k]
+        np.testing.assert_allclose(v.flatten().numpy()[idx], f[p + "w1_" + k], rtol=1e-5, atol=1e-7, err_msg=k)
+    np.testing.assert_array_equal(np.random.get_state()[1], f[p + "np_state_after"])
+    for key, st in (("total_loss", "loss"), ("policy_gradient_loss", "pl"), ("value_loss", "vl"),
+                    ("entropy_loss", "el")):
+        np.testing.assert_allclose(alg.stats[st], f[p + key], rtol=1e-5, atol=1e-7)

@@ -23,11 +23,18 @@ def _load_weights(module, f, prefix):
             v.copy_(torch.from_numpy(f[prefix + k]).to(v.device))
 
 
-@pytest.mark.parametrize("name", ["disc2", "disc4sat", "disc18", "box2"])
+def _train_kwargs(name):
+    """'cartpole' (BASELINE config 1: 8 envs x 128 steps, hidden 128, batch 128, 10 epochs)
+    ran with the reference's defaults; the other train_ppo cases with max_grad_norm 0.5."""
+    return {} if name == "cartpole" else dict(max_grad_norm=0.5, ent_coef=0.01, vf_coef=1.0)
+
+
+@pytest.mark.parametrize("name", ["disc2", "disc4sat", "disc18", "box2", "cartpole"])
 def test_ppo_train_matches_reference_run(golden, name):
     """Same rollout + same weights + same numpy seed => product train() reproduces the
     reference's post-update weights (ppo.py:200-259).  box2: the Normal head with the
-    reference's f64 log_prob / ratio / surrogate (models.py:66-71)."""
+    reference's f64 log_prob / ratio / surrogate (models.py:66-71).  cartpole: BASELINE
+    config 1 at its full size (80 optimizer steps)."""
     import ppo
     import env as E
     f = golden("train_ppo")
@@ -37,8 +44,7 @@ def test_ppo_train_matches_reference_run(golden, name):
     renv = ReplayVecEnv(f[p + "env_obs"], f[p + "env_rew"], f[p + "env_done"], space_from_code(code))
     np.random.seed(seed)
     torch.manual_seed(seed)
-    orc = OraclePPO(renv, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H, max_grad_norm=0.5,
-                    ent_coef=0.01, vf_coef=1.0)
+    orc = OraclePPO(renv, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H, **_train_kwargs(name))
     if name == "disc4sat":
         with torch.no_grad():
             orc.net.actor[-1].weight.mul_(60.0)
@@ -48,7 +54,7 @@ def test_ppo_train_matches_reference_run(golden, name):
     np.random.seed(seed)  # RolloutStorage draws randn(16, D) at construction (buffer.py:137)
     denv = E.DeviceVecEnv("custom", N, obs_dim=D, action_space=_space(E, code))
     alg = ppo.PPO(env_id="custom", env=denv, n_envs=N, nstep=T, batch_size=B, n_epochs=E_, hidden_size=H,
-                  max_grad_norm=0.5, ent_coef=0.01, vf_coef=1.0, quiet=True)
+                  quiet=True, **_train_kwargs(name))
     _load_weights(alg.policy.net, f, p + "w0_")
     ro = alg.rollout
     for t in range(T):
@@ -60,6 +66,7 @@ def test_ppo_train_matches_reference_run(golden, name):
     sd = alg.policy.net.state_dict()
     for k, v in sd.items():
         np.testing.assert_allclose(v.cpu().numpy(), f[p + "w1_" + k], rtol=2e-5, atol=2e-6, err_msg=k)
+    np.testing.assert_array_equal(np.random.get_state()[1], f[p + "np_state_after"])
     acc = alg.loss_accum.cpu().numpy()
     n = acc[5]
     np.testing.assert_allclose(acc[0] / n, f[p + "policy_gradient_loss"], rtol=1e-4, atol=1e-6)
@@ -290,3 +297,118 @@ def test_vector_env_ppo_runs_through_vecnormalize():
     assert alg.env.ret_rms.count > 16 * 32
     alg.train()
     assert np.isfinite(alg.loss_accum.cpu().numpy()).all()
+
+
+def _weight_sample_index(numel, k):
+    """tests/golden/make_golden.py weight_sample_index (the fixture stores it too)."""
+    if numel <= 8192:
+        return np.arange(numel, dtype=np.int64)
+    return np.sort(np.random.RandomState(1000 + k).choice(numel, 8192, replace=False)).astype(np.int64)
+
+
+@pytest.mark.parametrize("math,rtol", [("split", 1e-4), ("f32", 2e-5)])
+@pytest.mark.parametrize("name", ["cnn4", "cnn18"])
+def test_cnn_train_matches_reference_run(golden, name, math, rtol, monkeypatch):
+    """The benchmarked Atari path end to end against the reference: the product PPO.train()
+    (NatureCNN on the libppox conv kernels in `math`, rollout rows read in place by conv1,
+    fused loss, explicit backward, head-gradient kernel, flat Adam) on the rollout of the
+    reference's own run (live ppo.PPO with the checkpoint CnnActorCritic as policy.net,
+    ppo.py:200-259, models-checkpoint.py:48-90) reproduces its post-update weights and
+    losses.  Tolerances: weights rtol 1e-4 (split-bf16 convs) / 2e-5 (exact-f32 MFMA) with
+    atol 2e-6 (1 % of one Adam step, lr 3e-4); losses 1e-5 relative."""
+    import env as E
+    import models
+    import ppo
+    monkeypatch.setenv("PPOX_CONV_MATH", math)
+    f = golden("train_cnn")
+    p = name + "_"
+    N, T, B, E_, A, seed, net_seed = (int(x) for x in f[p + "cfg"])
+    np.random.seed(seed)  # RolloutStorage draws randn(16, 4) at construction (buffer.py:137)
+    env_id = "BreakoutNoFrameskip-v4" if A == 4 else "MontezumaRevengeNoFrameskip-v4"
+    alg = ppo.PPO(env_id=env_id, env=E.DeviceAtariEnv(env_id, N), n_envs=N, nstep=T, batch_size=B, n_epochs=E_,
+                  quiet=True)
+    assert alg.policy.net.conv_impl.math == math
+    torch.manual_seed(net_seed)
+    init = models.CnnActorCritic(4, A).state_dict()  # the reference's init from the same torch seed
+    sd = alg.policy.net.state_dict()
+    with torch.no_grad():
+        for k, v in sd.items():
+            np.testing.assert_array_equal(init[k].flatten()[:16].numpy(), f[p + "whead0_" + k])
+            v.copy_(init[k].to(v.device))
+    alg.policy.net.conv_impl.invalidate()
+    ro = alg.rollout
+    obs = f[p + "obs"]
+    for t in range(T):
+        ro.add(obs[t], f[p + "roll_actions"][t], f[p + "roll_rewards"][t], f[p + "roll_values"][t],
+               f[p + "roll_masks"][t], f[p + "roll_action_log_probs"][t])
+    ro.compute_returns_and_advantages(f[p + "roll_values"][T - 1], f[p + "roll_masks"][T - 1])
+    np.testing.assert_array_equal(ro.advantages.cpu().numpy(), f[p + "roll_advantages"])
+    np.testing.assert_array_equal(ro.returns.cpu().numpy(), f[p + "roll_returns"])
+    alg.train()
+    sd = alg.policy.net.state_dict()
+    for k, (key, v) in enumerate(sd.items()):
+        idx = f[p + "w1idx_" + key]
+        assert np.array_equal(idx, _weight_sample_index(v.numel(), k))
+        np.testing.assert_allclose(v.flatten().cpu().numpy()[idx], f[p + "w1_" + key], rtol=rtol, atol=2e-6,
+                                   err_msg=key)
+        d = (v.double().cpu() - init[key].double())
+        np.testing.assert_allclose(float(d.abs().sum()), float(f[p + "dabs_" + key]), rtol=2e-3, err_msg=key)
+    np.testing.assert_array_equal(np.random.get_state()[1], f[p + "np_state_after"])
+    acc = alg.loss_accum.cpu().numpy()
+    n = acc[5]
+    for i, key in ((0, "policy_gradient_loss"), (1, "value_loss"), (2, "entropy_loss"), (3, "total_loss")):
+        np.testing.assert_allclose(acc[i] / n, f[p + key], rtol=1e-5, atol=1e-7, err_msg=key)
+
+
+def _read_csv(folder):
+    import csv
+    import os
+    (name,) = os.listdir(folder)
+    with open(os.path.join(folder, name)) as fh:
+        rows = list(csv.reader(fh))
+    return rows[0], [dict(zip(rows[0], r)) for r in rows[1:]]
+
+
+REF_LEARN_KEYS = {"total timesteps", "total_time", "ep_rew_mean", "num_episodes", "entropy_loss",
+                  "policy_gradient_loss", "value_loss", "total_loss"}
+
+
+def test_learn_logs_reference_schema(tmp_path, monkeypatch):
+    """PPO.learn() (ppo.py:261-308) with log_interval=1 and log_to_file=True: the CSV under
+    ./logs/PPO/<env>/ carries the reference's columns (prefixes dropped, logger.py:26-29), the
+    train/* columns join from the second dump (header rewrite), and the logged counters are
+    the run's own.  Also the north_star aliases collect_rollouts / RolloutBuffer."""
+    import buffer
+    import env as E
+    import ppo
+    monkeypatch.chdir(tmp_path)
+    N, T = 8, 16
+    env_id = "BreakoutNoFrameskip-v4"
+    alg = ppo.PPO(env_id=env_id, env=E.DeviceAtariEnv(env_id, N, seed=1, p_done=0.2), n_envs=N, nstep=T,
+                  batch_size=64, n_epochs=1, quiet=True)
+    assert buffer.RolloutBuffer is buffer.RolloutStorage and isinstance(alg.rollout, buffer.RolloutBuffer)
+    assert alg.collect_rollouts() is True and alg.num_timesteps == N * T
+    assert alg.learn(total_timesteps=4 * N * T, log_interval=1, log_to_file=True) is alg
+    header, rows = _read_csv(tmp_path / "logs" / "PPO" / env_id)
+    assert REF_LEARN_KEYS <= set(header) and len(header) == len(set(header))
+    assert [int(r["total timesteps"]) for r in rows] == [2 * N * T, 3 * N * T, 4 * N * T]
+    assert rows[0]["total_loss"] == "" and all(r["total_loss"] != "" for r in rows[1:])
+    assert int(rows[-1]["num_episodes"]) == alg.num_episodes > 0
+    assert abs(float(rows[-1]["ep_rew_mean"]) - np.mean([e["r"] for e in alg.ep_info_buffer])) < 1e-9
+    assert len(alg.ep_info_buffer) == min(50, alg.num_episodes)
+
+
+def test_learn_reward_target_stops_early(tmp_path, monkeypatch):
+    """reward_target (ppo.py:296-306): the first iteration whose ep_rew_mean exceeds it logs a
+    final row and ends learn()."""
+    import env as E
+    import ppo
+    monkeypatch.chdir(tmp_path)
+    N, T = 8, 16
+    env_id = "BreakoutNoFrameskip-v4"
+    alg = ppo.PPO(env_id=env_id, env=E.DeviceAtariEnv(env_id, N, seed=2, p_done=0.3), n_envs=N, nstep=T,
+                  batch_size=64, n_epochs=1, quiet=True)
+    alg.learn(total_timesteps=100 * N * T, log_interval=1, reward_target=-1.0, log_to_file=True)
+    assert alg.num_timesteps == N * T
+    header, rows = _read_csv(tmp_path / "logs" / "PPO" / env_id)
+    assert len(rows) == 2 and rows[1]["total timesteps"] == str(N * T)
