@@ -53,8 +53,13 @@ def ppo_loss(v, lp, ent, mb, clip, ent_coef, vf_coef):
     return pl + ent_coef * el + vf_coef * vl, pl, vl, el
 
 
-def _tensors(mb):
-    return {k: torch.tensor(v) for k, v in mb.items()}
+def _tensors(mb, dtype=torch.float32):
+    """Minibatch arrays as tensors; float32 fields promoted to `dtype` (float64 runs)."""
+    out = {}
+    for k, v in mb.items():
+        t = torch.tensor(v)
+        out[k] = t.to(dtype) if t.dtype == torch.float32 else t
+    return out
 
 
 class OraclePPO:
@@ -62,7 +67,9 @@ class OraclePPO:
 
     def __init__(self, env, lr=3e-4, nstep=128, batch_size=128, n_epochs=10, gamma=0.99,
                  gae_lam=0.95, clip_range=0.2, ent_coef=0.01, vf_coef=1.0, max_grad_norm=0.2,
-                 hidden_size=128, net=None):
+                 hidden_size=128, net=None, train_dtype=torch.float32):
+        self.train_dtype = train_dtype  # float64: train() in double (collect stays f32, as the reference)
+        self.lr = lr
         self.env = env
         self.N = env.num_envs
         self.obs_shape = tuple(env.observation_space.shape)
@@ -91,10 +98,14 @@ class OraclePPO:
 
     def train(self):
         hist = {"loss": [], "pl": [], "vl": [], "el": []}
+        dt = getattr(self, "train_dtype", torch.float32)
+        if dt != torch.float32 and next(self.net.parameters()).dtype != dt:
+            self.net.to(dt)
+            self.opt = torch.optim.Adam(self.net.parameters(), lr=self.lr)
         for _ in range(self.n_epochs):
             for _idx, mb in self.rollout.minibatches(self.batch_size):
-                mb = _tensors(mb)
-                v, _, lp, ent = M.evaluate(self.net, mb["observations"], mb["actions"], self.box)
+                mb = _tensors(mb, dt)
+                v, _, lp, ent = M.evaluate(self.net, mb["observations"], mb["actions"], self.box, dt)
                 loss, pl, vl, el = ppo_loss(v, lp, ent, mb, self.clip, self.ent_coef, self.vf_coef)
                 self.opt.zero_grad()
                 loss.backward()

@@ -175,9 +175,10 @@ def act(net, obs, box=False):
     return actions, v, iv, lp
 
 
-def evaluate(net, obs, actions, box=False):
-    """models.py:52-73 / 101-124 -> values, [int_values], log_probs, entropy."""
-    a, ls, v, iv = net.heads(torch.as_tensor(obs, dtype=torch.float32), box)
+def evaluate(net, obs, actions, box=False, dtype=torch.float32):
+    """models.py:52-73 / 101-124 -> values, [int_values], log_probs, entropy.
+    dtype float64: the same program in exact-er arithmetic (conditioning checks)."""
+    a, ls, v, iv = net.heads(torch.as_tensor(obs, dtype=dtype), box)
     v = v.squeeze()
     iv = iv.squeeze() if iv is not None else None
     if box:

@@ -608,11 +608,15 @@ __global__ void __launch_bounds__(256) normal_sample_kernel(const float* __restr
 int check_mb(const Minibatch& m, bool dual, const char* name) {
     PPOX_REQUIRE(m.A >= 1 && m.A <= 64, "%s: n_actions=%d outside [1,64]", name, m.A);
     PPOX_REQUIRE(m.B >= 0 && m.T > 0 && m.N > 0, "%s: bad sizes B=%lld T=%lld N=%lld", name, m.B, m.T, m.N);
-    PPOX_REQUIRE(m.logits && m.values && m.idx && m.actions && m.old_logp && m.old_values && m.adv && m.ret &&
-                     m.adv_stats,
+    // a rank that owns no rows of a minibatch (B == 0) passes empty (null) row tensors; it still
+    // writes its zero partials for the all-reduce
+    const bool rows = m.B > 0;
+    PPOX_REQUIRE((!rows || (m.logits && m.values && m.idx)) && m.actions && m.old_logp && m.old_values && m.adv &&
+                     m.ret && m.adv_stats,
                  "%s: null pointer", name);
     if (dual)
-        PPOX_REQUIRE(m.int_values && m.old_int_values && m.int_adv && m.int_ret, "%s: null intrinsic pointer", name);
+        PPOX_REQUIRE((!rows || m.int_values) && m.old_int_values && m.int_adv && m.int_ret,
+                     "%s: null intrinsic pointer", name);
     return PPOX_OK;
 }
 
@@ -636,7 +640,7 @@ extern "C" int ppox_ppo_loss_partials(const float* logits, const float* values, 
                                       const float* advantages, const float* returns, const float* old_int_values,
                                       const float* int_advantages, const float* int_returns,
                                       const double* adv_stats, float clip, double* partials, void* stream) {
-    const bool dual = int_values != nullptr;
+    const bool dual = int_values != nullptr || (B == 0 && old_int_values != nullptr);
     Minibatch m = make_mb(logits, values, int_values, B, A, idx, T, N, actions, old_logp, old_values, advantages,
                           returns, old_int_values, int_advantages, int_returns, adv_stats, clip);
     int rc = check_mb(m, dual, "ppox_ppo_loss_partials");
@@ -661,12 +665,13 @@ extern "C" int ppox_ppo_loss_backward(const float* logits, const float* values, 
                                       int64_t B_global, float ent_coef, float vf_coef, float int_vf_coef,
                                       float scale, float* dlogits, float* dvalues, float* dint_values,
                                       double* loss_accum, void* stream) {
-    const bool dual = int_values != nullptr;
+    const bool dual = int_values != nullptr || (B == 0 && old_int_values != nullptr);
     Minibatch m = make_mb(logits, values, int_values, B, A, idx, T, N, actions, old_logp, old_values, advantages,
                           returns, old_int_values, int_advantages, int_returns, adv_stats, clip);
     int rc = check_mb(m, dual, "ppox_ppo_loss_backward");
     if (rc) return rc;
-    PPOX_REQUIRE(partials && dlogits && dvalues && (!dual || dint_values), "ppox_ppo_loss_backward: null output");
+    PPOX_REQUIRE(partials && (B == 0 || (dlogits && dvalues && (!dual || dint_values))),
+                 "ppox_ppo_loss_backward: null output");
     PPOX_REQUIRE(B_global >= 1, "ppox_ppo_loss_backward: B_global must be >= 1");
     hipStream_t s = ppox::as_stream(stream);
     PPOX_DISPATCH_A(A, MA, {
@@ -689,13 +694,13 @@ extern "C" int ppox_ppo_box_loss_partials(const float* mu, const float* log_std,
                                           const float* old_int_values, const float* int_advantages,
                                           const float* int_returns, const double* adv_stats, double clip,
                                           double* partials, void* stream) {
-    const bool dual = int_values != nullptr;
+    const bool dual = int_values != nullptr || (B == 0 && old_int_values != nullptr);
     BoxMinibatch bm{make_mb(mu, values, int_values, B, 1, idx, T, N, nullptr, old_logp, old_values, advantages,
                             returns, old_int_values, int_advantages, int_returns, adv_stats, (float)clip),
                     log_std, actions, D, clip};
     PPOX_REQUIRE(D >= 1 && D <= MAXD, "ppox_ppo_box_loss_partials: action dim %d outside [1,%d]", D, MAXD);
-    PPOX_REQUIRE(mu && log_std && values && idx && actions && old_logp && old_values && advantages && returns &&
-                     adv_stats && partials && (!dual || (old_int_values && int_advantages && int_returns)),
+    PPOX_REQUIRE((B == 0 || (mu && values && idx)) && log_std && actions && old_logp && old_values && advantages &&
+                     returns && adv_stats && partials && (!dual || (old_int_values && int_advantages && int_returns)),
                  "ppox_ppo_box_loss_partials: null pointer");
     PPOX_REQUIRE(B >= 0 && T > 0 && N > 0, "ppox_ppo_box_loss_partials: bad sizes");
     hipStream_t s = ppox::as_stream(stream);
@@ -716,14 +721,14 @@ extern "C" int ppox_ppo_box_loss_backward(const float* mu, const float* log_std,
                                           float int_vf_coef, float scale, float* dmu, double* dlog_std_partials,
                                           float* dlog_std, float* dvalues, float* dint_values, double* loss_accum,
                                           void* stream) {
-    const bool dual = int_values != nullptr;
+    const bool dual = int_values != nullptr || (B == 0 && old_int_values != nullptr);
     BoxMinibatch bm{make_mb(mu, values, int_values, B, 1, idx, T, N, nullptr, old_logp, old_values, advantages,
                             returns, old_int_values, int_advantages, int_returns, adv_stats, (float)clip),
                     log_std, actions, D, clip};
     PPOX_REQUIRE(D >= 1 && D <= MAXD, "ppox_ppo_box_loss_backward: action dim %d outside [1,%d]", D, MAXD);
-    PPOX_REQUIRE(mu && log_std && values && idx && actions && old_logp && old_values && advantages && returns &&
-                     adv_stats && partials && dmu && dlog_std_partials && dlog_std && dvalues &&
-                     (!dual || (old_int_values && int_advantages && int_returns && dint_values)),
+    PPOX_REQUIRE((B == 0 || (mu && values && idx && dmu && dvalues && (!dual || dint_values))) && log_std &&
+                     actions && old_logp && old_values && advantages && returns && adv_stats && partials &&
+                     dlog_std_partials && dlog_std && (!dual || (old_int_values && int_advantages && int_returns)),
                  "ppox_ppo_box_loss_backward: null pointer");
     PPOX_REQUIRE(B >= 0 && T > 0 && N > 0 && B_global >= 1, "ppox_ppo_box_loss_backward: bad sizes");
     hipStream_t s = ppox::as_stream(stream);

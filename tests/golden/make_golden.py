@@ -570,12 +570,18 @@ def gen_cnn_train(R):
     import torch
     ck = _load_checkpoint_models()
     out = {}
-    for name, A, N, T, B, E, seed, net_seed in (("cnn4", 4, 4, 16, 24, 2, 61, 62),
-                                                ("cnn18", 18, 2, 16, 12, 1, 63, 64)):
+    # env seeds chosen so the recorded trajectory is well-conditioned: the same program in
+    # float64 (oracle, train_dtype=float64) lands within rtol 2e-5 / atol 2e-6 of the reference's
+    # float32 weights (test_oracle_golden.test_cnn_fixture_is_well_conditioned).  With raw 0..255
+    # pixels some trajectories are not (a ratio crossing a clip boundary, a saturated softmax):
+    # there the reference's own f32 result is 10-400x further than that from exact arithmetic,
+    # and no other f32 implementation can be held to it.
+    for name, A, N, T, B, E, seed, net_seed, env_seed in (("cnn4", 4, 4, 16, 24, 2, 61, 62, 15061),
+                                                          ("cnn18", 18, 2, 16, 12, 1, 63, 64, 6063)):
         rec = _record_logger(R)
         np.random.seed(seed)
         torch.manual_seed(seed)
-        env = make_fakevec(R.VecEnv, N, None, Discrete(A), seed=4000 + seed, obs_shape=(4, 84, 84), frames=True)
+        env = make_fakevec(R.VecEnv, N, None, Discrete(A), seed=env_seed, obs_shape=(4, 84, 84), frames=True)
         R.ppo.make_env = lambda env_id, n_envs=4, env=env: env
         alg = R.ppo.PPO(env_id="Fake-v0", nstep=T, batch_size=B, n_epochs=E)  # reference defaults otherwise
         torch.manual_seed(net_seed)
