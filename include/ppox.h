@@ -360,16 +360,6 @@ int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t b
  * batch), reduced in a fixed order (deterministic).  x: u8 frames (layer 1, samples
  * x_sample_stride bytes apart) or NHWC f32; grad_out: ReLU-masked NHWC output grad. */
 int64_t ppox_nature_wgrad_split_workspace_bytes(int32_t layer, int64_t batch);
-/* Split-operand hand-off between the backward convs: conv3's dgrad can write the conv2
- * output grad as its three exact bf16 planes (uint16 [3][batch][9][9][64], grad_in_planes
- * = 1), which conv2's dgrad and wgrad then read as is (grad_out_planes = 1). */
-int ppox_nature_conv_dgrad_split_ex(int32_t layer, const void* grad_out, int32_t grad_out_planes,
-                                    int64_t batch, const uint16_t* wqd, const float* prev_act,
-                                    void* grad_in, int32_t grad_in_planes, void* stream);
-int ppox_nature_conv_wgrad_split_ex(int32_t layer, const void* x, int64_t batch,
-                                    int64_t x_sample_stride, const void* grad_out,
-                                    int32_t grad_out_planes, void* workspace, int64_t workspace_bytes,
-                                    float* dw, float* db, void* stream);
 int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_t batch,
                                  int64_t x_sample_stride, const float* grad_out, void* workspace,
                                  int64_t workspace_bytes, float* dw, float* db, void* stream);

@@ -33,10 +33,6 @@ SPLIT_SLOWER = set()
 # conv2 dgrad in split math: the split kernel below this batch, the f32 kernel from it
 # (PPOX_DGRAD2_SPLIT_MAX overrides; default: split at every batch)
 DGRAD2_SPLIT_MAX_BATCH = int(os.environ.get("PPOX_DGRAD2_SPLIT_MAX", str(1 << 62)))
-# bf16-plane hand-off of conv2's output grad (dgrad3 -> dgrad2/wgrad2, no split arithmetic
-# in the consumers): implemented and tested, but measured slower at B = 16384 (dgrad2 is
-# bound by its operand traffic at 32 output channels, not by the split), so off by default
-PLANES_HANDOFF = False
 # fc forward: the split-bf16 GEMM from this batch up, rocBLAS below (PPOX_FC_SPLIT_MIN
 # overrides).  Same-box A/B of the whole training step (tools/ab_fc.sh, after the split
 # kernel's two-deep load pipeline): -40 ms per iteration at B = 16384, +17 ms at the 8-GPU
@@ -254,15 +250,6 @@ class NatureConvs:
             g3 = torch.empty((B, 7, 7, 64), device=dev)
             native.nchw_to_nhwc_relu_grad(dh3, h3, B, g3)      # ReLU backward of conv3, to NHWC
         self.wgrad(3, h2, B, g3, dw3, db3)
-        if self.math == "split" and PLANES_HANDOFF:
-            # conv2's output grad handed over as bf16 planes (3, B, 9, 9, 64)
-            g2p = torch.empty((3, B, 9, 9, 64), dtype=torch.int16, device=dev)
-            native.nature_conv_dgrad_split_ex(3, g3, 0, B, self.q[13], h2, g2p, 1)
-            native.nature_conv_wgrad_split_ex(2, h1, B, 0, g2p, 1, self.workspace(2, B, True), dw2, db2)
-            g1 = torch.empty((B, 20, 20, 32), device=dev)
-            native.nature_conv_dgrad_split_ex(2, g2p, 1, B, self.q[12], h1, g1, 0)
-            self.wgrad(1, x, B, g1, dw1, db1)
-            return
         g2 = torch.empty((B, 9, 9, 64), device=dev)
         self.dgrad(3, g3, B, h2, g2)                            # dX of conv3, times ReLU'(conv2)
         self.wgrad(2, h1, B, g2, dw2, db2)

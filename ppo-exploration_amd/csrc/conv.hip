@@ -38,12 +38,6 @@ namespace {
 
 
 constexpr int BK = 32;
-#ifndef FWD1_MT
-#define FWD1_MT 1  // rows per wave / 32 for the NT = 1 (32-channel) kernels
-#endif
-#ifndef DGRAD2_MT
-#define DGRAD2_MT 1
-#endif
 constexpr int AST = BK + 1;  // padded LDS row stride (floats): conflict-free column reads
 
 // ---------------------------------------------------------------------------
@@ -55,52 +49,6 @@ constexpr int AST = BK + 1;  // padded LDS row stride (floats): conflict-free co
 // ---------------------------------------------------------------------------
 struct RowTile {  // forward: a contiguous run of output pixels
     long long m0, M;
-};
-
-// conv1 forward: uint8 NCHW frames, K order (ci, ky, kx); chunk = 1 channel x 4
-// kernel rows x 8 columns -> 4 runs of 8 bytes per row (2 words each).
-template <int MT>
-struct StageFwd1 {
-    using L = G1;
-    static constexpr int SL = 4 * MT;
-    const uint8_t* base[SL];
-    bool ok[SL];
-    uint32_t r[SL];
-    __device__ StageFwd1(const Args& a, const RowTile& t) {
-        const uint8_t* x = reinterpret_cast<const uint8_t*>(a.x);
-#pragma unroll
-        for (int i = 0; i < SL; ++i) {
-            const int w = i * 256 + threadIdx.x;
-            const int row = w >> 3, seg = (w & 7) >> 1, half = w & 1;
-            const long long m = t.m0 + row;
-            ok[i] = m < t.M;
-            const long long mm = ok[i] ? m : t.m0;
-            const long long n = mm / L::P;
-            const int p = (int)(mm - n * L::P), oy = p / L::OW, ox = p % L::OW;
-            base[i] = x + u8_sample_base(a, n, (long long)L::CIN * L::IH * L::IW) + (oy * L::S + seg) * L::IW +
-                      ox * L::S + half * 4;
-        }
-    }
-    __device__ inline void load(int chunk) {
-        const int off = (chunk >> 1) * (L::IH * L::IW) + (chunk & 1) * 4 * L::IW;
-#pragma unroll
-        for (int i = 0; i < SL; ++i) {
-            const uint32_t v = *reinterpret_cast<const uint32_t*>(base[i] + off);
-            r[i] = ok[i] ? v : 0u;
-        }
-    }
-    __device__ inline void store(float* As) const {
-#pragma unroll
-        for (int i = 0; i < SL; ++i) {
-            const int w = i * 256 + threadIdx.x;
-            const int row = w >> 3, seg = (w & 7) >> 1, half = w & 1;
-            float* d = As + row * AST + seg * 8 + half * 4;
-            d[0] = (float)(r[i] & 0xFFu);
-            d[1] = (float)((r[i] >> 8) & 0xFFu);
-            d[2] = (float)((r[i] >> 16) & 0xFFu);
-            d[3] = (float)(r[i] >> 24);
-        }
-    }
 };
 
 // f32 rows of 32 floats (8 float4 per row) -> LDS
@@ -194,10 +142,6 @@ struct FwdBase {
     }
 };
 
-template <int MT>
-struct Fwd1Problem : FwdBase<G1, false, MT> {
-    using Stager = StageFwd1<MT>;
-};
 template <class L, bool OUT_NCHW, int MT>
 struct FwdNHWCProblem : FwdBase<L, OUT_NCHW, MT> {
     using Stager = StageFwdNHWC<L, MT>;
@@ -571,172 +515,6 @@ __global__ void pack_split_gemm(const float* __restrict__ w, uint16_t* __restric
     pack_split_gemm_elem<L, DGRAD>(w, q, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
-// dgrad whose output (the previous layer's ReLU-masked output grad) is written as its
-// three exact bf16 planes [3][batch][pos][ci] (plane stride batch * NPOS * CIN) for
-// consumers that take split operands (dgrad/wgrad of the layer below: no split there)
-template <class L>
-struct DgradPMSplitOut : DgradPMProblem<L, 1> {
-    using Base = DgradPMProblem<L, 1>;
-    __device__ static void store_pre(const Args& a, const typename Base::Tile& t, int row, int ci, float acc,
-                                     float m) {
-        const long long n = t.n0 + row;
-        if (n >= a.batch) return;
-        const long long o = (n * Base::NPOS + t.pos) * L::CIN + ci, ps = a.batch * Base::NPOS * L::CIN;
-        uint16_t p0, p1, p2;
-        split3(m > 0.f ? acc : 0.f, p0, p1, p2);
-        uint16_t* y = reinterpret_cast<uint16_t*>(a.y);
-        y[o] = p0;
-        y[o + ps] = p1;
-        y[o + 2 * ps] = p2;
-    }
-};
-
-// Dgrad (position-major, as DgradPMProblem) whose input output-grad G comes as bf16
-// planes, ROW-PERSISTENT: a workgroup owns 128 samples x one input row iy and walks the
-// row's IW positions, their K chunks (1-4 taps x 32 channels each) forming one pipelined
-// stream — a lone position has only 2-8 chunks, too few to amortise a pipeline fill.
-// The A chunk (128 rows x 32 channels x 3 planes) is staged in LDS as planes (80-B rows:
-// conflict-free b128 reads) and read as MFMA fragments directly (no split arithmetic);
-// B as igemm_split_kernel.  A position's ReLU-mask operands are loaded when its first
-// chunk starts, its outputs stored after its last.
-constexpr int PAST = 40;  // bf16 per LDS row (32 + 8 pad)
-
-template <class L>
-__global__ void __launch_bounds__(256, 2) igemm_planes_kernel(Args a, const u32x4* __restrict__ wq) {
-    using Prob = DgradPMProblem<L, 1>;
-    constexpr int NOUT = Prob::NOUT, NT = NOUT / 32, BMR = 128, CPT = Prob::CPT, NPOS = Prob::NPOS;
-    constexpr int BQ = 2 * NT * 3 * 64, BV = (BQ + 255) / 256;
-    constexpr int APL = BMR * PAST;  // bf16 per LDS plane
-    __shared__ __attribute__((aligned(16))) uint16_t As[2][3 * APL];
-    __shared__ u32x4 Bs[2][BQ];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-    // block -> (sample tile, input row), XCD-aware: one XCD walks the rows of a sample tile
-    const long long w = xcd_remap(blockIdx.x, gridDim.x);
-    const long long n0 = (w / L::IH) * BMR;
-    const int iy = (int)(w % L::IH);
-    int ky0, ny;
-    tap_range<L::S, L::OH, L::KH>(iy, ky0, ny);
-    auto xtaps = [](int ix, int& kx0, int& nx) { tap_range<L::S, L::OW, L::KW>(ix, kx0, nx); };
-
-    // A units: 3 planes x 128 rows x 4 groups of 8 channels = 1536 x 16 B, 6 per thread
-    const uint16_t* g = reinterpret_cast<const uint16_t*>(a.x);
-    const long long ps = a.batch * (long long)(L::P * L::COUT);
-    const uint16_t* base[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const int u = i * 256 + tid, p = u >> 9, row = (u & 511) >> 2, q = u & 3;
-        long long n = n0 + row;
-        n = n < a.batch ? n : n0;  // rows past the end: a valid clamped row, never stored
-        base[i] = g + p * ps + n * (L::P * L::COUT) + q * 8;
-    }
-    auto loadA = [&](int ix, int kx0, int nx, int c, u32x4 (&r)[6]) {
-        const int tap = c / CPT, ty = tap / nx, tx = tap - ty * nx;
-        const int oy = (iy - ky0) / L::S - ty, ox = (ix - kx0) / L::S - tx;
-        const int off = (oy * L::OW + ox) * L::COUT + (c % CPT) * BK;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) r[i] = *reinterpret_cast<const u32x4*>(base[i] + off);
-    };
-    auto loadB = [&](int kx0, int nx, int c, u32x4 (&br)[BV]) {
-        const int tap = c / CPT, ty = tap / nx, tx = tap - ty * nx;
-        const int id = ((ky0 + L::S * ty) * L::KW + kx0 + L::S * tx) * CPT + c % CPT;
-        const u32x4* src = wq + (long long)id * BQ;
-#pragma unroll
-        for (int i = 0; i < BV; ++i)
-            if (BQ % 256 == 0 || i * 256 + tid < BQ) br[i] = src[i * 256 + tid];
-    };
-    auto store = [&](int buf, const u32x4 (&r)[6], const u32x4 (&br)[BV]) {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const int u = i * 256 + tid, p = u >> 9, row = (u & 511) >> 2, q = u & 3;
-            *reinterpret_cast<u32x4*>(&As[buf][p * APL + row * PAST + q * 8]) = r[i];
-        }
-#pragma unroll
-        for (int i = 0; i < BV; ++i)
-            if (BQ % 256 == 0 || i * 256 + tid < BQ) Bs[buf][i * 256 + tid] = br[i];
-    };
-    // output rows / columns of this lane in the C/D layout
-    long long orow[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) orow[r] = n0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-
-    f32x16 hi[NT], lo[NT], msk[NT];
-    auto load_mask = [&](int ix) {
-        const int pos = iy * L::IW + ix;
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const long long n = orow[r] < a.batch ? orow[r] : n0;
-                msk[j][r] = a.mask[(n * NPOS + pos) * L::CIN + j * 32 + (lane & 31)];
-            }
-    };
-    auto epilogue = [&](int ix) {
-        const int pos = iy * L::IW + ix;
-#pragma unroll
-        for (int j = 0; j < NT; ++j) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                if (orow[r] < a.batch)
-                    a.y[(orow[r] * NPOS + pos) * L::CIN + j * 32 + (lane & 31)] =
-                        msk[j][r] > 0.f ? hi[j][r] + lo[j][r] : 0.f;
-            hi[j] = lo[j] = zero16();
-        }
-    };
-
-    int ix = 0, kx0, nx;
-    xtaps(0, kx0, nx);
-    int c = 0, nchunk = ny * nx * CPT;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) hi[j] = lo[j] = zero16();
-    u32x4 ra[6], rb[BV];
-    loadA(ix, kx0, nx, 0, ra);
-    loadB(kx0, nx, 0, rb);
-    store(0, ra, rb);
-    __syncthreads();
-    const int aoff = (wave * 32 + (lane & 31)) * PAST + (lane >> 5) * 8;
-    int cur = 0;
-    for (;;) {
-        // next chunk of the row's stream
-        int nix = ix, nc = c + 1, nkx0 = kx0, nnx = nx, nn = nchunk;
-        if (nc == nchunk) {
-            nix = ix + 1;
-            nc = 0;
-            if (nix < L::IW) {
-                xtaps(nix, nkx0, nnx);
-                nn = ny * nnx * CPT;
-            }
-        }
-        const bool more = nix < L::IW;
-        if (more) {
-            loadA(nix, nkx0, nnx, nc, ra);
-            loadB(nkx0, nnx, nc, rb);
-        }
-        if (c == 0) load_mask(ix);
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const u32x4 af[3] = {*reinterpret_cast<const u32x4*>(&As[cur][aoff + 16 * s]),
-                                 *reinterpret_cast<const u32x4*>(&As[cur][APL + aoff + 16 * s]),
-                                 *reinterpret_cast<const u32x4*>(&As[cur][2 * APL + aoff + 16 * s])};
-#pragma unroll
-            for (int j = 0; j < NT; ++j) {
-                const u32x4* B = Bs[cur] + ((s * NT + j) * 3) * 64 + lane;
-                const u32x4 bf[3] = {B[0], B[64], B[128]};
-                mfma_split6(af, bf, hi[j], lo[j]);
-            }
-        }
-        if (c + 1 == nchunk) epilogue(ix);
-        if (!more) break;
-        store(cur ^ 1, ra, rb);
-        __syncthreads();
-        cur ^= 1;
-        ix = nix;
-        c = nc;
-        kx0 = nkx0;
-        nx = nnx;
-        nchunk = nn;
-    }
-}
-
 // ---------------------------------------------------------------------------
 // NatureCNN hidden linear layer Linear(3136, 512) (.ipynb_checkpoints/
 // models-checkpoint.py:58-59) on the split-bf16 implicit-GEMM kernel: a plain GEMM
@@ -816,9 +594,6 @@ struct GemmRowsProblem {
     }
 };
 
-#ifndef DGRAD2_BLOCK
-#define DGRAD2_BLOCK 0  // 1: conv2 split dgrad as the 2x2-block kernel (measured 2.26 ms vs 0.97 position-major at B = 16384: 12,800 one-per-CU workgroups of <= 8 chunks, latency-bound)
-#endif
 #ifndef FC_NB
 #define FC_NB 64  // 128 measured no faster (one workgroup per CU: 86 KB LDS, 324 registers)
 #endif
@@ -847,130 +622,6 @@ __global__ void pack_split_gemm_rows(const float* __restrict__ w, uint16_t* __re
 }
 
 // ---------------------------------------------------------------------------
-// conv2 dgrad, split-bf16, 2x2-BLOCK form.  conv2 is k4 s2, so the four input pixels
-// (2bi+u, 2bj+v) of a 2x2 block are fed by the SAME output-grad pixels (oy, ox) in
-// {bi-1, bi} x {bj-1, bj}, each through a different tap (u + 2(bi-oy), v + 2(bj-ox)).
-// A workgroup owns 128 samples x one block: every A chunk (g2 rows at one (oy, ox), 32
-// channels) is loaded and split ONCE and multiplied into four accumulator pairs (one per
-// block pixel) — 4x the MFMA work per A byte and per split of the position-major form,
-// whose 32-output-channel tiles left it bound by operand traffic.  B = the four taps'
-// split weight chunks (ppox_nature_pack_split's dgrad2 packing), staged in LDS.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256, 1) dgrad2_block_kernel(Args a, const u32x4* __restrict__ wq) {
-    using L = G2;
-    constexpr int NBLK = L::IW / 2, BMR = 128, CPT = L::COUT / BK, NPOS = L::IH * L::IW;
-    constexpr int BQ = 2 * 3 * 64;  // u32x4 per (tap, 32-co chunk): NT = 1
-    constexpr int BQ4 = 4 * BQ, BV = BQ4 / 256;
-    __shared__ __attribute__((aligned(16))) float As[2][BMR * SAST];
-    __shared__ u32x4 Bs[2][BQ4];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-    const long long w = xcd_remap(blockIdx.x, gridDim.x);
-    const long long n0 = (w / (NBLK * NBLK)) * BMR;
-    const int blk = (int)(w % (NBLK * NBLK)), bi = blk / NBLK, bj = blk % NBLK;
-    // contributing output-grad pixels (at most 4), in a fixed order
-    int pys[4], pxs[4], npix = 0;
-#pragma unroll
-    for (int dy = 1; dy >= 0; --dy)
-#pragma unroll
-        for (int dx = 1; dx >= 0; --dx) {
-            const int oy = bi - dy, ox = bj - dx;
-            if (oy >= 0 && oy < L::OH && ox >= 0 && ox < L::OW) {
-                pys[npix] = oy;
-                pxs[npix] = ox;
-                ++npix;
-            }
-        }
-    const int nchunk = npix * CPT;
-    const float* g = reinterpret_cast<const float*>(a.x);
-    const float* abase[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int u = i * 256 + tid;
-        long long n = n0 + (u >> 3);
-        n = n < a.batch ? n : n0;  // rows past the end: a valid clamped row, never stored
-        abase[i] = g + n * (L::P * L::COUT) + (u & 7) * 4;
-    }
-    auto pix = [&](int c, int& oy, int& ox, int& cc) {
-        const int pi = c / CPT;
-        cc = c - pi * CPT;
-        oy = pi == 0 ? pys[0] : pi == 1 ? pys[1] : pi == 2 ? pys[2] : pys[3];
-        ox = pi == 0 ? pxs[0] : pi == 1 ? pxs[1] : pi == 2 ? pxs[2] : pxs[3];
-    };
-    auto loadA = [&](int c, float4 (&r)[4]) {
-        int oy, ox, cc;
-        pix(c, oy, ox, cc);
-        const int off = (oy * L::OW + ox) * L::COUT + cc * BK;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] = *reinterpret_cast<const float4*>(abase[i] + off);
-    };
-    auto loadB = [&](int c, u32x4 (&br)[BV]) {
-        int oy, ox, cc;
-        pix(c, oy, ox, cc);
-#pragma unroll
-        for (int i = 0; i < BV; ++i) {
-            const int e = i * 256 + tid, q = e / BQ, within = e - q * BQ;  // q = block pixel (u, v)
-            const int ky = (q >> 1) + 2 * (bi - oy), kx = (q & 1) + 2 * (bj - ox);
-            br[i] = wq[(long long)((ky * L::KW + kx) * CPT + cc) * BQ + within];
-        }
-    };
-    auto store = [&](int buf, const float4 (&r)[4], const u32x4 (&br)[BV]) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int u = i * 256 + tid;
-            *reinterpret_cast<float4*>(As[buf] + (u >> 3) * SAST + (u & 7) * 4) = r[i];
-        }
-#pragma unroll
-        for (int i = 0; i < BV; ++i) Bs[buf][i * 256 + tid] = br[i];
-    };
-    f32x16 hi[4], lo[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) hi[q] = lo[q] = zero16();
-    float4 ra[4];
-    u32x4 rb[BV];
-    if (nchunk > 0) {
-        loadA(0, ra);
-        loadB(0, rb);
-        store(0, ra, rb);
-    }
-    __syncthreads();
-    const int aoff = (wave * 32 + (lane & 31)) * SAST + (lane >> 5) * 8;
-    for (int c = 0; c < nchunk; ++c) {
-        const int cur = c & 1;
-        if (c + 1 < nchunk) {
-            loadA(c + 1, ra);
-            loadB(c + 1, rb);
-        }
-        const float* A = As[cur] + aoff;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            u32x4 af[3];
-            split8(*reinterpret_cast<const float4*>(A + 16 * s), *reinterpret_cast<const float4*>(A + 16 * s + 4), af[0],
-                   af[1], af[2]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const u32x4* B = Bs[cur] + q * BQ + s * 3 * 64 + lane;
-                const u32x4 bf[3] = {B[0], B[64], B[128]};
-                mfma_split6(af, bf, hi[q], lo[q]);
-            }
-        }
-        if (c + 1 < nchunk) store(cur ^ 1, ra, rb);
-        __syncthreads();
-    }
-    // epilogue: block pixel q = (u, v) -> input pixel (2bi+u, 2bj+v); x (h1 > 0)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int pos = (2 * bi + (q >> 1)) * L::IW + 2 * bj + (q & 1);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const long long n = n0 + wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            if (n >= a.batch) continue;
-            const long long o = (n * NPOS + pos) * L::CIN + (lane & 31);
-            a.y[o] = a.mask[o] > 0.f ? hi[q][r] + lo[q][r] : 0.f;
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // conv2 dgrad in the col2im form (split-bf16), the default conv2 split dgrad.
 // GEMM rows = output-grad pixels (n, oy, ox), K = the 64 output channels, columns =
 // (tap, ci): 16 taps x 32 = 512.  Every A value (one G row of 64 floats) is loaded
@@ -987,22 +638,6 @@ __global__ void __launch_bounds__(256, 1) dgrad2_block_kernel(Args a, const u32x
 // position-major dgrad form: ppox_nature_pack_split which = 12) is staged in LDS,
 // double-buffered across passes.  Deterministic: a fixed sum order per output.
 // ---------------------------------------------------------------------------
-#ifndef DGRAD2_COL
-#define DGRAD2_COL 1  // 0: conv2 split dgrad as the position-major DgradPMProblem kernel
-#endif
-// timing-probe switches (tools/build_variant.sh), all 0 in the product build
-#ifndef C2_NOMASK
-#define C2_NOMASK 0
-#endif
-#ifndef C2_NOSTORE
-#define C2_NOSTORE 0
-#endif
-#ifndef C2_NOMFMA
-#define C2_NOMFMA 0
-#endif
-#ifndef C2_NORMW
-#define C2_NORMW 0
-#endif
 constexpr int C2S = 3, C2ROWS = C2S * 81, C2PIX = 100;
 constexpr int C2BQ = 4 * 4 * 3 * 64;  // u32x4 per pass: 4 taps x 4 k-steps x 3 planes x 64 lanes
 constexpr int C2BV = C2BQ / 512;
@@ -1101,11 +736,7 @@ __global__ void __launch_bounds__(512, 1) dgrad2_col_kernel(Args a, const u32x4*
             const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
             const bool ok = e < C2S * C2PIX * 8 && n < a.batch;
             const long long o = ok ? ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4 : n0 * L::IH * L::IW * L::CIN;
-#if C2_NOMASK
-            mk[j] = make_float4(1.f, 1.f, 1.f, (float)o);
-#else
             mk[j] = *reinterpret_cast<const float4*>(a.mask + o);
-#endif
         }
     };
     // masked class image -> dX (NHWC), image re-zeroed for the next class; uniform control
@@ -1123,7 +754,7 @@ __global__ void __launch_bounds__(512, 1) dgrad2_col_kernel(Args a, const u32x4*
             const float4 y = make_float4(m.x > 0.f ? d.x : 0.f, m.y > 0.f ? d.y : 0.f, m.z > 0.f ? d.z : 0.f,
                                          m.w > 0.f ? d.w : 0.f);
             const long long n = n0 + s;
-            if (in && n < a.batch && !C2_NOSTORE) {
+            if (in && n < a.batch) {
                 const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
                 *reinterpret_cast<float4*>(a.y + ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4) = y;
             }
@@ -1143,8 +774,8 @@ __global__ void __launch_bounds__(512, 1) dgrad2_col_kernel(Args a, const u32x4*
             load_mask(cls);
             if (cls == 1 || cls == 2) loadB(cls + 1, (cls + 1) & 1);
         }
-        if (k + 1 < 16 && !C2_NOMFMA) mfma_tap(k + 1, next);
-        if (!C2_NORMW) rmw_tap(k, cur);
+        if (k + 1 < 16) mfma_tap(k + 1, next);
+        rmw_tap(k, cur);
         if (i == 2 && (cls == 1 || cls == 2)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
         if (i == 3) {
@@ -1192,56 +823,6 @@ __host__ __device__ constexpr int rg_index(int k, int col, int nout) {
            (k & 3);
 }
 
-template <class L, int MT_>
-struct RgFwdNHWC {
-    static constexpr int NOUT = L::COUT, MT = MT_, ROWS = 128 * MT, CPT = L::CIN / BK;
-    using Raw = f32x4[MT][4];
-    struct Tile {
-        unsigned m0, M;  // this wave's first row, total rows (< 2^31, host-checked)
-    };
-    __device__ static bool tile(const Args& a, Tile& t, int wave) {
-        const long long w = xcd_remap(blockIdx.x, gridDim.x);
-        t.M = (unsigned)(a.batch * L::P);
-        t.m0 = (unsigned)(w * ROWS) + wave * 32 * MT;
-        return t.m0 < t.M;
-    }
-    __device__ static int nchunk(const Tile&) { return L::K / BK; }
-    __device__ static const float* bchunk(const Args& a, const Tile&, int c) { return a.wp + c * BK * NOUT; }
-    struct Loader {
-        const float* base[MT];
-        __device__ Loader(const Args& a, const Tile& t, int lane) {
-            const float* x = reinterpret_cast<const float*>(a.x);
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                unsigned m = t.m0 + i * 32 + (lane & 31);
-                m = m < t.M ? m : t.m0;
-                const unsigned n = m / L::P, p = m - n * L::P, oy = p / L::OW, ox = p % L::OW;
-                base[i] = x + (long long)((n * L::IH + oy * L::S) * L::IW + ox * L::S) * L::CIN + (lane >> 5) * 16;
-            }
-        }
-        __device__ inline void load(int c, Raw& r) const {
-            const int tap = c / CPT;
-            const int off = ((tap / L::KW) * L::IW + tap % L::KW) * L::CIN + (c % CPT) * BK;
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) r[i][q] = *reinterpret_cast<const f32x4*>(base[i] + off + q * 4);
-        }
-        __device__ static inline float elem(const Raw& r, int i, int kk) { return r[i][kk >> 2][kk & 3]; }
-    };
-    __device__ static void store(const Args& a, const Tile& t, int row, int co, float acc, bool out_nchw) {
-        const unsigned m = t.m0 + row;
-        if (m >= t.M) return;
-        const float v = fmaxf(acc + a.bias[co], 0.f);
-        if (out_nchw) {
-            const unsigned n = m / L::P;
-            a.y[((long long)n * L::COUT + co) * L::P + (m - n * L::P)] = v;
-        } else {
-            a.y[(long long)m * L::COUT + co] = v;
-        }
-    }
-};
-
 // conv1: u8 NCHW frames; chunk c = channel c/2, kernel rows 4(c&1)..+3; lane
 // half h takes kernel rows 4(c&1)+2h, +1: two 8-byte runs = four words
 template <int MT_>
@@ -1249,7 +830,9 @@ struct RgFwd1 {
     using L = G1;
     static constexpr int NOUT = L::COUT, MT = MT_, ROWS = 128 * MT;
     using Raw = uint32_t[MT][4];
-    using Tile = typename RgFwdNHWC<G2, 1>::Tile;
+    struct Tile {
+        unsigned m0, M;  // this wave's first row, total rows (< 2^31, host-checked)
+    };
     __device__ static bool tile(const Args& a, Tile& t, int wave) {
         const long long w = xcd_remap(blockIdx.x, gridDim.x);
         t.M = (unsigned)(a.batch * L::P);
@@ -1290,65 +873,6 @@ struct RgFwd1 {
         const unsigned m = t.m0 + row;
         if (m >= t.M) return;
         a.y[(long long)m * L::COUT + co] = fmaxf(acc + a.bias[co], 0.f);
-    }
-};
-
-// dgrad, position-major (see DgradPMProblem): a wave owns 32*MT samples of one input pixel
-template <class L, int MT_>
-struct RgDgrad {
-    static constexpr int NOUT = L::CIN, MT = MT_, ROWS = 128 * MT, NPOS = L::IH * L::IW, CPT = L::COUT / BK;
-    using Raw = f32x4[MT][4];
-    struct Tile {
-        long long n0;  // this wave's first sample
-        int pos, iy, ix, ky0, kx0, nx, nchunk;
-    };
-    __device__ static bool tile(const Args& a, Tile& t, int wave) {
-        const long long w = xcd_remap(blockIdx.x, gridDim.x);
-        t.n0 = (w / NPOS) * ROWS + wave * 32 * MT;
-        t.pos = (int)(w % NPOS);
-        t.iy = t.pos / L::IW;
-        t.ix = t.pos % L::IW;
-        int ny, nx;
-        tap_range<L::S, L::OH, L::KH>(t.iy, t.ky0, ny);
-        tap_range<L::S, L::OW, L::KW>(t.ix, t.kx0, nx);
-        t.nx = nx;
-        t.nchunk = ny * nx * CPT;
-        return t.n0 < a.batch;
-    }
-    __device__ static int nchunk(const Tile& t) { return t.nchunk; }
-    __device__ static const float* bchunk(const Args& a, const Tile& t, int c) {
-        const int tap = c / CPT, ty = tap / t.nx, tx = tap - ty * t.nx;
-        const int ky = t.ky0 + L::S * ty, kx = t.kx0 + L::S * tx;
-        return a.wp + ((ky * L::KW + kx) * CPT + c % CPT) * BK * NOUT;
-    }
-    struct Loader {
-        const float* base[MT];
-        int iy, ix, ky0, kx0, nx;
-        __device__ Loader(const Args& a, const Tile& t, int lane) : iy(t.iy), ix(t.ix), ky0(t.ky0), kx0(t.kx0), nx(t.nx) {
-            const float* g = reinterpret_cast<const float*>(a.x);
-#pragma unroll
-            for (int i = 0; i < MT; ++i) {
-                long long n = t.n0 + i * 32 + (lane & 31);
-                n = n < a.batch ? n : t.n0;
-                base[i] = g + n * (L::P * L::COUT) + (lane >> 5) * 16;
-            }
-        }
-        __device__ inline void load(int c, Raw& r) const {
-            const int tap = c / CPT, ty = tap / nx, tx = tap - ty * nx;
-            const int oy = (iy - ky0) / L::S - ty, ox = (ix - kx0) / L::S - tx;
-            const int off = (oy * L::OW + ox) * L::COUT + (c % CPT) * BK;
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) r[i][q] = *reinterpret_cast<const f32x4*>(base[i] + off + q * 4);
-        }
-        __device__ static inline float elem(const Raw& r, int i, int kk) { return r[i][kk >> 2][kk & 3]; }
-    };
-    __device__ static void store(const Args& a, const Tile& t, int row, int ci, float acc, bool) {
-        const long long n = t.n0 + row;
-        if (n >= a.batch) return;
-        const long long o = (n * NPOS + t.pos) * L::CIN + ci;
-        a.y[o] = a.mask[o] > 0.f ? acc : 0.f;
     }
 };
 
@@ -1697,12 +1221,10 @@ __device__ inline uint2 lds_tr16(const uint8_t* p) {
     return __builtin_bit_cast(uint2, r);
 }
 
-template <class L, bool U8, int KT, bool GPL = false>
+template <class L, bool U8, int KT>
 __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
-    // GPL: the output grad G arrives as its three bf16 planes [3][batch * P][COUT]
-    // (DgradPMSplitOut); staged as is, its f32 values (bias grad) rebuilt exactly
     using C = WsCfg<L, U8, KT>;
-    constexpr int COUT = L::COUT, XP = C::XP, XR = C::XR, GR = C::GR, XU = C::XU, UPX = C::UPX;
+    constexpr int COUT = L::COUT, XP = C::XP, XR = C::XR, GR = C::GR, XU = C::XU;
     constexpr int WKT = C::WKT, WCT = C::WCT;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * C::STAGE];
     const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
@@ -1727,7 +1249,6 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     uint32_t xw[XU][2];
     float4 xr[XU][2];
     float4 gr[2];
-    u32x4 gq[3];
     float bsum[GW];
 #pragma unroll
     for (int e = 0; e < GW; ++e) bsum[e] = 0.f;
@@ -1799,16 +1320,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
                 xr[i][1] = ok ? v1 : z;
             }
         }
-        if constexpr (GPL) {
-            static_assert(GW == 8, "planes G: 8 channels per thread");
-            const unsigned long long ps = (unsigned long long)M * COUT;
-            const uint16_t* sg = reinterpret_cast<const uint16_t*>(a.g) + (unsigned long long)(ok ? mcur : mbeg) * COUT + gco;
-#pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                const u32x4 v = *reinterpret_cast<const u32x4*>(sg + p * ps);
-                gq[p] = ok ? v : u32x4{0u, 0u, 0u, 0u};
-            }
-        } else {
+        {
             const float* sg = a.g + (unsigned long long)(ok ? mcur : mbeg) * COUT + gco;
             const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
             const float4 g0 = *reinterpret_cast<const float4*>(sg);
@@ -1855,19 +1367,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         }
         uint8_t* gb = base + XP * C::XPB;
         const int goff = pxl * GR + (((gco >> 4) ^ tr_swz<GR>(pxl)) << 5) + (gco & 15) * 2;
-        if constexpr (GPL) {
-#pragma unroll
-            for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(gb + p * C::GPB + goff) = gq[p];
-            // f32 values for the bias grad: g = p0 + p1 + p2 (exact: the planes are a split)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int q = e >> 1, sh = (e & 1) * 16;
-                const float v0 = __uint_as_float(((gq[0][q] >> sh) & 0xFFFFu) << 16);
-                const float v1 = __uint_as_float(((gq[1][q] >> sh) & 0xFFFFu) << 16);
-                const float v2 = __uint_as_float(((gq[2][q] >> sh) & 0xFFFFu) << 16);
-                bsum[e] += (v0 + v1) + v2;
-            }
-        } else if constexpr (GW == 8) {
+        if constexpr (GW == 8) {
             u32x4 p0, p1, p2;
             split8(gr[0], gr[1], p0, p1, p2);
             *reinterpret_cast<u32x4*>(gb + goff) = p0;
@@ -1880,17 +1380,15 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
             *reinterpret_cast<uint2*>(gb + C::GPB + goff) = p1;
             *reinterpret_cast<uint2*>(gb + 2 * C::GPB + goff) = p2;
         }
-        if constexpr (!GPL) {
-            bsum[0] += gr[0].x;
-            bsum[1] += gr[0].y;
-            bsum[2] += gr[0].z;
-            bsum[3] += gr[0].w;
-            if constexpr (GW == 8) {
-                bsum[4] += gr[1].x;
-                bsum[5] += gr[1].y;
-                bsum[6] += gr[1].z;
-                bsum[7] += gr[1].w;
-            }
+        bsum[0] += gr[0].x;
+        bsum[1] += gr[0].y;
+        bsum[2] += gr[0].z;
+        bsum[3] += gr[0].w;
+        if constexpr (GW == 8) {
+            bsum[4] += gr[1].x;
+            bsum[5] += gr[1].y;
+            bsum[6] += gr[1].z;
+            bsum[7] += gr[1].w;
         }
     };
     // per-lane transposed-read offsets (T10): lane 4qq+pp of each 16-lane group supplies
@@ -1998,12 +1496,6 @@ __global__ void __launch_bounds__(256) nchw_to_nhwc_mask(const float* __restrict
 // ---------------------------------------------------------------------------
 // weight packing (once per optimizer step)
 // ---------------------------------------------------------------------------
-#ifndef RG_F32  // 1: the f32 layers (fwd2/3, dgrad) on rgemm too (experiments)
-#define RG_F32 0
-#endif
-#ifndef RG_FWD1
-#define RG_FWD1 1
-#endif
 // RG: rgemm layout (rg_index); else the igemm's natural [K][NOUT]
 template <bool RG>
 __device__ inline int pack_pos(int k, int col, int nout, int i) {
@@ -2058,15 +1550,6 @@ int launch_rgemm(const Args& a, long long blocks, hipStream_t s, const char* nam
 #ifndef RG_FWD1_MT
 #define RG_FWD1_MT 2
 #endif
-#ifndef RG_FWD_MT
-#define RG_FWD_MT 1
-#endif
-#ifndef RG_DGRAD2_MT
-#define RG_DGRAD2_MT 2
-#endif
-#ifndef RG_DGRAD3_MT
-#define RG_DGRAD3_MT 1
-#endif
 
 template <class L, bool U8>
 int launch_wgrad(const WArgs& wa_in, hipStream_t s) {
@@ -2097,7 +1580,7 @@ int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float
 #define WS_KT3 64
 #endif
 // split wgrad: its own split-K count (~2048 pixels per split so the grid fills the chip)
-template <class L, bool U8, int KT, bool GPL = false>
+template <class L, bool U8, int KT>
 struct WsLaunch {
     using C = WsCfg<L, U8, KT>;
     static long long splits(long long batch) {
@@ -2125,7 +1608,7 @@ struct WsLaunch {
         WArgs wa{x, sample_stride, g, slab, slab + (long long)sp * L::K * L::COUT, batch, 0, sp, idx, T, Nenv};
         const long long M = batch * L::P;
         wa.px_per_split = ppox::ceil_div(ppox::ceil_div(M, sp), MS) * MS;
-        wgrad_split_kernel<L, U8, KT, GPL><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
+        wgrad_split_kernel<L, U8, KT><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
         PPOX_LAUNCHED_NORET("ppox_nature_conv_wgrad_split");
         return launch_wgrad_reduce<L, !U8>(slab, wa.bslab, sp, dw, db, s);
     }
@@ -2133,7 +1616,6 @@ struct WsLaunch {
 using Ws1 = WsLaunch<G1, true, 256>;
 using Ws2 = WsLaunch<G2, false, WS_KT2>;
 using Ws3 = WsLaunch<G3, false, WS_KT3>;
-using Ws2P = WsLaunch<G2, false, WS_KT2, true>;
 // Every per-optimizer-step weight packing of the training step in ONE launch (the
 // minibatch loop is launch-bound at small per-rank batches): element ranges of the
 // jobs laid end to end, null outputs skipped.
@@ -2197,7 +1679,7 @@ __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long tota
         j -= PU_2;
         if (j < PU_3) { if (p.qd3) pack_frag_unit<G3::CIN>(ConvSrc<G3, true>{p.w3}, p.qd3, j); continue; }
         j -= PU_3;
-        if (j < PA_N2) { if (p.wpd2) pack_dgrad_elem<G2, RG_F32>(p.w2, p.wpd2, (int)j); continue; }
+        if (j < PA_N2) { if (p.wpd2) pack_dgrad_elem<G2, false>(p.w2, p.wpd2, (int)j); continue; }
         j -= PA_N2;
         if (j < PU_FC) { if (p.qfcf) pack_rows_unit<FcFwd, true>(p.wfc, p.qfcf, j); continue; }
         j -= PU_FC;
@@ -2215,11 +1697,11 @@ extern "C" int ppox_nature_pack_weights(const float* w1, const float* w2, const 
                      (!wpd2 || ppox::aligned16(wpd2)) && (!wpd3 || ppox::aligned16(wpd3)),
                  "ppox_nature_pack_weights: packed buffers must be 16-byte aligned");
     hipStream_t s = ppox::as_stream(stream);
-    if (wp1) pack_fwd<G1, false, RG_FWD1><<<ppox::ceil_div(G1::K * 32, 256), 256, 0, s>>>(w1, wp1);
-    if (wp2) pack_fwd<G2, true, RG_F32><<<ppox::ceil_div(G2::K * 64, 256), 256, 0, s>>>(w2, wp2);
-    if (wp3) pack_fwd<G3, true, RG_F32><<<ppox::ceil_div(G3::K * 64, 256), 256, 0, s>>>(w3, wp3);
-    if (wpd2) pack_dgrad<G2, RG_F32><<<ppox::ceil_div(G2::K * G2::COUT, 256), 256, 0, s>>>(w2, wpd2);
-    if (wpd3) pack_dgrad<G3, RG_F32><<<ppox::ceil_div(G3::K * G3::COUT, 256), 256, 0, s>>>(w3, wpd3);
+    if (wp1) pack_fwd<G1, false, true><<<ppox::ceil_div(G1::K * 32, 256), 256, 0, s>>>(w1, wp1);
+    if (wp2) pack_fwd<G2, true, false><<<ppox::ceil_div(G2::K * 64, 256), 256, 0, s>>>(w2, wp2);
+    if (wp3) pack_fwd<G3, true, false><<<ppox::ceil_div(G3::K * 64, 256), 256, 0, s>>>(w3, wp3);
+    if (wpd2) pack_dgrad<G2, false><<<ppox::ceil_div(G2::K * G2::COUT, 256), 256, 0, s>>>(w2, wpd2);
+    if (wpd3) pack_dgrad<G3, false><<<ppox::ceil_div(G3::K * G3::COUT, 256), 256, 0, s>>>(w3, wpd3);
     PPOX_LAUNCHED("ppox_nature_pack_weights");
 }
 
@@ -2237,30 +1719,16 @@ extern "C" int ppox_nature_conv_fwd(int32_t layer, const void* x, int64_t batch,
         PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && (idx || x_sample_stride % 4 == 0),
                      "ppox_nature_conv_fwd: u8 input must be 4-byte aligned");
         if (idx) PPOX_REQUIRE(T > 0 && N_env > 0, "ppox_nature_conv_fwd: idx needs T and N_env");
-#if !RG_FWD1
-        using P1 = Fwd1Problem<FWD1_MT>;
-        return launch_igemm<P1>(a, ppox::ceil_div(batch * G1::P, P1::BMR), s, "ppox_nature_conv_fwd");
-#else
         using R1 = RgFwd1<RG_FWD1_MT>;
         return launch_rgemm<R1>(a, ppox::ceil_div(batch * G1::P, R1::ROWS), s, "ppox_nature_conv_fwd");
-#endif
     }
     PPOX_REQUIRE(ppox::aligned16(x) && !idx, "ppox_nature_conv_fwd: layer 2/3 input must be 16B-aligned NHWC");
-#if !RG_F32
     if (layer == 2) {
         using P2 = FwdNHWCProblem<G2, false, 1>;
         return launch_igemm<P2>(a, ppox::ceil_div(batch * G2::P, P2::BMR), s, "ppox_nature_conv_fwd");
     }
     using P3 = FwdNHWCProblem<G3, true, 1>;
     return launch_igemm<P3>(a, ppox::ceil_div(batch * G3::P, P3::BMR), s, "ppox_nature_conv_fwd");
-#else
-    if (layer == 2) {
-        using R2 = RgFwdNHWC<G2, RG_FWD_MT>;
-        return launch_rgemm<R2>(a, ppox::ceil_div(batch * G2::P, R2::ROWS), s, "ppox_nature_conv_fwd");
-    }
-    using R3 = RgFwdNHWC<G3, RG_FWD_MT>;
-    return launch_rgemm<R3, true>(a, ppox::ceil_div(batch * G3::P, R3::ROWS), s, "ppox_nature_conv_fwd");
-#endif
 }
 
 extern "C" int ppox_nature_conv_dgrad(int32_t layer, const float* grad_out, int64_t batch, const float* wpd,
@@ -2271,21 +1739,12 @@ extern "C" int ppox_nature_conv_dgrad(int32_t layer, const float* grad_out, int6
     PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wpd), "ppox_nature_conv_dgrad: 16B alignment");
     Args a{grad_out, nullptr, 0, 0, 0, wpd, nullptr, prev_act, grad_in, batch};
     hipStream_t s = ppox::as_stream(stream);
-#if !RG_F32
     if (layer == 2) {
-        using D2 = DgradPMProblem<G2, DGRAD2_MT>;
+        using D2 = DgradPMProblem<G2, 1>;
         return launch_igemm<D2>(a, ppox::ceil_div(batch, D2::BMR) * D2::NPOS, s, "ppox_nature_conv_dgrad");
     }
     using D3 = DgradPMProblem<G3, 1>;
     return launch_igemm<D3>(a, ppox::ceil_div(batch, D3::BMR) * D3::NPOS, s, "ppox_nature_conv_dgrad");
-#else
-    if (layer == 2) {
-        using D2 = RgDgrad<G2, RG_DGRAD2_MT>;
-        return launch_rgemm<D2>(a, ppox::ceil_div(batch, D2::ROWS) * D2::NPOS, s, "ppox_nature_conv_dgrad");
-    }
-    using D3 = RgDgrad<G3, RG_DGRAD3_MT>;
-    return launch_rgemm<D3>(a, ppox::ceil_div(batch, D3::ROWS) * D3::NPOS, s, "ppox_nature_conv_dgrad");
-#endif
 }
 
 // split-K factor over pixels: ~4096 pixels per split, but enough splits that the
@@ -2377,8 +1836,6 @@ extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_
     return Ws3::run(x, 0, grad_out, batch, workspace, dw, db, s);
 }
 
-// as ppox_nature_conv_wgrad_split; grad_out_planes = 1: grad_out is the three bf16 planes
-// [3][batch][OH][OW][COUT] written by ppox_nature_conv_dgrad_split_ex (layer 2 only)
 // conv1 split wgrad reading its frames straight from the rollout (sample n = env-major row
 // idx[n] of the step-major (T, N_env, 4, 84, 84) buffer): the minibatch gather fused, as in
 // ppox_nature_conv_fwd_split's idx form (replaces ppox_gather_rows + the strided call)
@@ -2395,20 +1852,6 @@ extern "C" int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, in
     PPOX_REQUIRE(batch * G1::P < (1LL << 31) / 64, "ppox_nature_conv_wgrad_split_idx: batch too large");
     return Ws1::run(x, 0, grad_out, batch, workspace, dw, db, ppox::as_stream(stream),
                     reinterpret_cast<const long long*>(idx), T, N_env);
-}
-
-extern "C" int ppox_nature_conv_wgrad_split_ex(int32_t layer, const void* x, int64_t batch, int64_t x_sample_stride,
-                                               const void* grad_out, int32_t grad_out_planes, void* workspace,
-                                               int64_t workspace_bytes, float* dw, float* db, void* stream) {
-    if (!grad_out_planes)
-        return ppox_nature_conv_wgrad_split(layer, x, batch, x_sample_stride, reinterpret_cast<const float*>(grad_out),
-                                            workspace, workspace_bytes, dw, db, stream);
-    PPOX_REQUIRE(layer == 2, "ppox_nature_conv_wgrad_split_ex: planes grad_out only for layer 2");
-    PPOX_REQUIRE(x && grad_out && workspace && dw && db && batch > 0, "ppox_nature_conv_wgrad_split_ex: bad arguments");
-    PPOX_REQUIRE(workspace_bytes >= Ws2P::workspace_bytes(batch), "ppox_nature_conv_wgrad_split_ex: workspace too small");
-    PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(x), "ppox_nature_conv_wgrad_split_ex: 16B alignment");
-    PPOX_REQUIRE(batch * G2::P < (1LL << 31) / 64, "ppox_nature_conv_wgrad_split_ex: batch too large");
-    return Ws2P::run(x, 0, reinterpret_cast<const float*>(grad_out), batch, workspace, dw, db, ppox::as_stream(stream));
 }
 
 extern "C" int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, int64_t batch, float* out,
@@ -2452,49 +1895,11 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
     Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch};
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 2) {
-#if DGRAD2_COL
         dgrad2_col_kernel<<<(unsigned)ppox::ceil_div(batch, C2S), 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd));
         PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
-#elif DGRAD2_BLOCK
-        dgrad2_block_kernel<<<(unsigned)(ppox::ceil_div(batch, 128) * (G2::IH / 2) * (G2::IW / 2)), 256, 0, s>>>(
-            a, reinterpret_cast<const u32x4*>(wqd));
-        PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
-#else
-        using D2 = DgradPMProblem<G2, 1>;
-        return launch_igemm_split<D2>(a, wqd, ppox::ceil_div(batch, D2::BMR) * D2::NPOS, s,
-                                      "ppox_nature_conv_dgrad_split");
-#endif
     }
     using D3 = DgradPMProblem<G3, 1>;
     return launch_igemm_split<D3>(a, wqd, ppox::ceil_div(batch, D3::BMR) * D3::NPOS, s, "ppox_nature_conv_dgrad_split");
-}
-
-extern "C" int ppox_nature_conv_dgrad_split_ex(int32_t layer, const void* grad_out, int32_t grad_out_planes,
-                                               int64_t batch, const uint16_t* wqd, const float* prev_act,
-                                               void* grad_in, int32_t grad_in_planes, void* stream) {
-    if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
-    PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad_split_ex: layer must be 2 or 3");
-    PPOX_REQUIRE(grad_out && wqd && prev_act && grad_in && batch >= 0, "ppox_nature_conv_dgrad_split_ex: bad arguments");
-    PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wqd), "ppox_nature_conv_dgrad_split_ex: 16B alignment");
-    // supported forms: conv3 (f32 in) -> planes out; conv2 planes in -> f32 out
-    PPOX_REQUIRE((layer == 3 && !grad_out_planes) || (layer == 2 && !grad_in_planes),
-                 "ppox_nature_conv_dgrad_split_ex: planes in/out combination not supported for this layer");
-    Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, reinterpret_cast<float*>(grad_in), batch};
-    hipStream_t s = ppox::as_stream(stream);
-    if (layer == 3) {
-        if (!grad_in_planes)
-            return ppox_nature_conv_dgrad_split(3, reinterpret_cast<const float*>(grad_out), batch, wqd, prev_act,
-                                                reinterpret_cast<float*>(grad_in), stream);
-        using D3 = DgradPMSplitOut<G3>;
-        return launch_igemm_split<D3>(a, wqd, ppox::ceil_div(batch, D3::BMR) * D3::NPOS, s,
-                                      "ppox_nature_conv_dgrad_split_ex");
-    }
-    if (!grad_out_planes)
-        return ppox_nature_conv_dgrad_split(2, reinterpret_cast<const float*>(grad_out), batch, wqd, prev_act,
-                                            reinterpret_cast<float*>(grad_in), stream);
-    igemm_planes_kernel<G2><<<(unsigned)(ppox::ceil_div(batch, 128) * G2::IH), 256, 0, s>>>(
-        a, reinterpret_cast<const u32x4*>(wqd));
-    PPOX_LAUNCHED("ppox_nature_conv_dgrad_split_ex");
 }
 
 // ---- NatureCNN fc layer (3136 -> 512) on the split-bf16 GEMM ----------------------

@@ -73,8 +73,6 @@ SIGNATURES = {
     "ppox_es_update": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp],
     "ppox_normalize_obs_f32_ex": [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _f64, _vp, _vp],
     "ppox_vecnorm_reward": [_vp, _vp, _vp, _i64, _f64, _vp, _vp, _f64, _f64, _f64, _i32, _vp],
-    "ppox_nature_conv_dgrad_split_ex": [_i32, _vp, _i32, _i64, _vp, _vp, _vp, _i32, _vp],
-    "ppox_nature_conv_wgrad_split_ex": [_i32, _vp, _i64, _i64, _vp, _i32, _vp, _i64, _vp, _vp, _vp],
     "ppox_outer_relu_backward": [_vp, _vp, _vp, _i64, _i64, _vp, _vp],
     "ppox_nature_conv_wgrad_split": [_i32, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
     "ppox_nature_conv_wgrad_split_idx": [_i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
@@ -162,7 +160,7 @@ def event_times_ms(name):
 
 _LAYERED = ("ppox_nature_conv_fwd", "ppox_nature_conv_dgrad", "ppox_nature_conv_wgrad",
             "ppox_nature_conv_fwd_split", "ppox_nature_conv_dgrad_split", "ppox_nature_conv_wgrad_split",
-            "ppox_nature_conv_dgrad_split_ex", "ppox_nature_conv_wgrad_split_ex", "ppox_nature_conv_wgrad_split_idx")
+            "ppox_nature_conv_wgrad_split_idx")
 
 
 def call(name, *args):
@@ -566,20 +564,6 @@ def nature_conv_wgrad_split_idx(layer, x, batch, idx, T, N_env, grad_out, worksp
     rows idx (the minibatch gather fused), split-bf16 MFMA."""
     call("ppox_nature_conv_wgrad_split_idx", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
          _p(grad_out), _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db),
-         stream_ptr(stream))
-
-
-def nature_conv_dgrad_split_ex(layer, grad_out, grad_out_planes, batch, wqd, prev_act, grad_in, grad_in_planes,
-                               stream=None):
-    """dgrad with bf16-plane hand-off: *_planes = 1 marks an int16 (3, batch, H, W, C) tensor."""
-    call("ppox_nature_conv_dgrad_split_ex", int(layer), _p(grad_out), int(grad_out_planes), int(batch), _p(wqd),
-         _p(prev_act), _p(grad_in), int(grad_in_planes), stream_ptr(stream))
-
-
-def nature_conv_wgrad_split_ex(layer, x, batch, x_sample_stride, grad_out, grad_out_planes, workspace, dw, db,
-                               stream=None):
-    call("ppox_nature_conv_wgrad_split_ex", int(layer), _p(x), int(batch), int(x_sample_stride), _p(grad_out),
-         int(grad_out_planes), _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db),
          stream_ptr(stream))
 
 

@@ -484,26 +484,6 @@ def _conv_ops_fp64(B, seed):
             dw, db = torch.empty_like(wl.weight), torch.empty_like(wl.bias)
             cv.wgrad(L, xin, B, gg, dw, db)
             out[math].update({("wgrad", L): dw, ("wgrad_bias", L): db})
-        if math == "split_all":
-            # bf16-plane hand-off (the "split" backward): dgrad3 -> planes -> dgrad2 / wgrad2
-            g2p = torch.empty((3, B, 9, 9, 64), dtype=torch.int16, device="cuda")
-            native.nature_conv_dgrad_split_ex(3, g3, 0, B, cv.q[13], h2f, g2p, 1)
-            g2rec = sum(((g2p[p].to(torch.int32) & 0xFFFF) << 16).view(torch.float32) for p in (0, 1, 2))
-            d1p = torch.empty(B, 20, 20, 32, device="cuda")
-            native.nature_conv_dgrad_split_ex(2, g2p, 1, B, cv.q[12], h1f, d1p, 0)
-            dwp, dbp = torch.empty_like(cv.c2.weight), torch.empty_like(cv.c2.bias)
-            wsp = torch.empty(native.nature_wgrad_split_workspace_bytes(2, B), dtype=torch.uint8, device="cuda")
-            native.nature_conv_wgrad_split_ex(2, h1f, B, 0, g2p, 1, wsp, dwp, dbp)
-            out[math].update({("planes_dgrad", 3): g2rec, ("planes_dgrad", 2): d1p, ("planes_wgrad", 2): dwp,
-                              ("planes_wgrad_bias", 2): dbp})
-        else:  # f32 kernels on the same (reconstructed) conv2 output grad
-            g2rec = out["split_all"][("planes_dgrad", 3)]
-            d1p = torch.empty(B, 20, 20, 32, device="cuda")
-            cv.dgrad(2, g2rec.contiguous(), B, h1f, d1p)
-            dwp, dbp = torch.empty_like(cv.c2.weight), torch.empty_like(cv.c2.bias)
-            cv.wgrad(2, h1f, B, g2rec.contiguous(), dwp, dbp)
-            out[math].update({("planes_dgrad", 3): out[math][("dgrad", 3)], ("planes_dgrad", 2): d1p,
-                              ("planes_wgrad", 2): dwp, ("planes_wgrad_bias", 2): dbp})
     # fp64 reference (CPU autograd, same weights)
     fe = net.feature_extractor
     w = [fe[i].weight.detach().double().cpu() for i in (0, 2, 4)]
@@ -522,12 +502,6 @@ def _conv_ops_fp64(B, seed):
     for L, xin, gg, st in ((1, x.double().cpu(), g1r, 4), (2, nchw(h1f), g2r, 2), (3, nchw(h2f), g3, 1)):
         ref[("wgrad", L)] = torch.nn.grad.conv2d_weight(xin, w[L - 1].shape, nchw(gg), stride=st)
         ref[("wgrad_bias", L)] = nchw(gg).sum(dim=(0, 2, 3))
-    g2rec = nchw(out["split_all"][("planes_dgrad", 3)])
-    ref[("planes_dgrad", 3)] = ref[("dgrad", 3)]
-    ref[("planes_dgrad", 2)] = (torch.nn.grad.conv2d_input((B, 32, 20, 20), w[1], g2rec, stride=2)
-                                * (nchw(h1f) > 0)).permute(0, 2, 3, 1)
-    ref[("planes_wgrad", 2)] = torch.nn.grad.conv2d_weight(nchw(h1f), w[1].shape, g2rec, stride=2)
-    ref[("planes_wgrad_bias", 2)] = g2rec.sum(dim=(0, 2, 3))
     return {k: (out["split_all"][k], out["f32"][k], ref[k]) for k in ref}
 
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build a libppox variant with extra -D flags for kernel A/B timing (dev tool).
-# Usage: tools/build_variant.sh NAME "-DFWD1_MT=2 -DDGRAD2_MT=2"
+# Usage: tools/build_variant.sh NAME "-DFC_NB=128 -DWS_KT2=64"
 set -e
 name=$1; shift
 root=$(cd "$(dirname "$0")/.." && pwd)

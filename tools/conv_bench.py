@@ -70,14 +70,6 @@ def main():
     rec("fwd_split", 3, t_ms(lambda: native.nature_conv_fwd_split(3, h2, B, None, 0, 0, 0, q[3], b3, h3)), MAC[3])
     rec("dgrad_split", 3, t_ms(lambda: native.nature_conv_dgrad_split(3, g3, B, q[13], h2, g2)), MAC[3])
     rec("dgrad_split", 2, t_ms(lambda: native.nature_conv_dgrad_split(2, g2, B, q[12], h1, g1)), MAC[2])
-    g2p = torch.empty((3, B, 9, 9, 64), dtype=torch.int16, device=d)
-    rec("dgrad_split_planes_out", 3, t_ms(lambda: native.nature_conv_dgrad_split_ex(3, g3, 0, B, q[13], h2, g2p, 1)),
-        MAC[3])
-    rec("dgrad_split_planes_in", 2, t_ms(lambda: native.nature_conv_dgrad_split_ex(2, g2p, 1, B, q[12], h1, g1, 0)),
-        MAC[2])
-    wsp2 = torch.empty(native.nature_wgrad_split_workspace_bytes(2, B), dtype=torch.uint8, device=d)
-    rec("wgrad_split_planes_in", 2, t_ms(lambda: native.nature_conv_wgrad_split_ex(2, h1, B, 0, g2p, 1, wsp2, dw[2],
-                                                                                   db[2])), MAC[2])
     for L, xin, g, stride in ((3, h2, g3, 0), (2, h1, g2, 0), (1, x, g1, 28224)):
         wsp = torch.empty(native.nature_wgrad_split_workspace_bytes(L, B), dtype=torch.uint8, device=d)
         rec("wgrad_split", L, t_ms(lambda: native.nature_conv_wgrad_split(L, xin, B, stride, g, wsp, dw[L], db[L])),
