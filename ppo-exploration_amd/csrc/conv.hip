@@ -594,11 +594,15 @@ struct GemmRowsProblem {
     }
 };
 
+#ifndef SG2
+#define SG2 1  // 0: the split GEMMs on igemm_split_kernel (register-staged, 128-row tiles)
+#endif
 #ifndef FC_NB
 #define FC_NB 64  // 128 measured no faster (one workgroup per CU: 86 KB LDS, 324 registers)
 #endif
 using FcFwd = GemmRowsProblem<3136, 512, FC_NB, FC_FWD>;
 using FcDgrad = GemmRowsProblem<512, 3136, FC_NB, FC_DGRAD>;
+static_assert(!SG2 || FC_NB == 64, "sg2 runs the fc layer in 64-column blocks");
 
 // packs B (element (k, n) = w[n * ldw + k] when TRANS, w[k * ldw + n] otherwise) into
 // split_frag_index order per column block, zero beyond N
@@ -799,6 +803,292 @@ int launch_igemm_split(const Args& a, const uint16_t* wq, long long blocks, hipS
     igemm_split_kernel<Prob><<<(unsigned)blocks, 256, 0, s>>>(a, reinterpret_cast<const u32x4*>(wq));
     PPOX_LAUNCHED(name);
 }
+
+// ---------------------------------------------------------------------------
+// Split-bf16 GEMM, LDS-DMA pipelined ("sg2"): the forward-style GEMMs (conv2/conv3
+// forward, conv3 dgrad, fc forward, fc dgrad) with the same fused epilogues as
+// igemm_split_kernel.  512-thread workgroups (8 waves, two per SIMD, one workgroup per
+// CU), 256 rows x 64 columns per workgroup, each wave 32 rows x 64 columns (hi/lo f32
+// accumulators for two 32x32 tiles: six v_mfma_f32_32x32x16_bf16 per tile and 16-k step).
+// Per 32-k chunk the A rows (f32, im2col-gathered: one 128-B run per row) and the
+// pre-split B chunk (12 KB, split_frag_index order) are copied global -> LDS by
+// global_load_lds_dwordx4 into a three-slot ring, so no VGPR staging and no ds_write:
+//   * each wave DMAs exactly its own 32 A rows (4 x 1 KB), so A needs no cross-wave
+//     ordering, only the wave's own counted vmcnt;
+//   * B is shared: waves 0-3 DMA two 1 KB pieces, waves 4-7 one;
+//   * K loop: wait for this wave's DMAs of chunk c (vmcnt = the DMAs of chunk c+1 still
+//     allowed in flight), one raw s_barrier (everyone's B of chunk c has landed; everyone
+//     has finished reading chunk c-1), DMA chunk c+2 into the slot chunk c-1 used, then
+//     split A in registers and run the 24 MFMAs of chunk c.  No ordinary global load is in
+//     flight in the loop (hipcc would wait vmcnt(0) on it): the epilogue operands are
+//     loaded after it.
+// A rows are 128 B in LDS with their 16-B pieces XOR-swizzled by (row >> 1) & 7, which
+// makes every ds_read_b128 of the fragments conflict-free (rows 0-3 / 12-15 / 20-27 of a
+// lane group land on distinct bank quads); the DMA writes LDS lane-linearly, so the
+// swizzle is applied to each lane's GLOBAL source address.
+// ---------------------------------------------------------------------------
+constexpr int SG_BQ = 2 * 2 * 3 * 64;  // u32x4 per B chunk at 64 columns (12 KB)
+
+// LDS fragment reads in inline asm: hipcc's wait insertion cannot tell a ds_read from the
+// ring slot being read apart from the DMAs in flight into the other slots, and puts a
+// vmcnt(0) before the first read of every chunk (which would drain the prefetch).  Issued
+// here, the reads are ordered by the kernel's own counted vmcnt + barrier, and their data
+// by an lgkmcnt wait that takes the destination registers as operands (so no use of them
+// can be scheduled above it).
+__device__ inline u32x4 sg_ds_read(uint32_t addr) {
+    u32x4 r;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+    return r;
+}
+template <int N>
+__device__ inline void sg_lgkm_wait(u32x4 (&v)[8]) {
+    asm volatile("s_waitcnt lgkmcnt(%8)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+                 : "n"(N));
+}
+template <int N>
+__device__ inline void sg_vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// WAVES waves x 32 rows per workgroup, SLOTS ring slots of one 32-k chunk (A: 128 B per row;
+// B: 12 KB).  8 waves / 3 slots: one workgroup per CU (132 KB), waves 4-7 staggered;
+// 4 waves / 2 slots: two workgroups per CU (56 KB each), whose K walks, prologues and
+// epilogues interleave on every SIMD.
+template <class Prob, int WAVES, int SLOTS>
+__global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, const u32x4* __restrict__ wq) {
+    constexpr int NT = 2, ROWS = 32 * WAVES, AB = ROWS * BK * 4, SLOT = AB + SG_BQ * 16;
+    constexpr int BPW = (12 + WAVES - 1) / WAVES;  // B pieces DMA'd per wave (1 KB each)
+    constexpr int NDMA = 4 + BPW;                  // this wave's DMAs per chunk
+    constexpr bool STAGGER = WAVES == 8;
+    static_assert(Prob::NOUT == 64 && Prob::ROWS == ROWS, "sg2: 32 rows per wave x 64 columns");
+    static_assert(SLOTS == 2 || SLOTS == 3, "sg2: two or three ring slots");
+    // all LDS in ONE __shared__ object (a second one can make hipcc wait vmcnt(0) in the loop)
+    __shared__ __attribute__((aligned(16))) uint8_t lds[SLOTS * SLOT];
+    typename Prob::Tile t;
+    if (!Prob::tile(a, t)) return;
+    const int nchunk = Prob::nchunk(t);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: DMA bases go to M0
+
+    // DMA sources: A instruction j of this wave covers its rows 8j + (lane >> 3), LDS piece
+    // lane & 7, which holds global piece (lane & 7) ^ swz(row)
+    const uint8_t* asrc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int r = 8 * j + (lane >> 3);
+        asrc[j] = reinterpret_cast<const uint8_t*>(Prob::row_ptr(a, t, wave * 32 + r)) +
+                  ((((lane & 7) ^ ((r >> 1) & 7))) << 4);
+    }
+    // B: 12 pieces of 1 KB per chunk, BPW per wave (pieces past 11 re-copy piece 11: the
+    // same bytes to the same place), so every wave issues NDMA DMAs per chunk
+    int bp[BPW];
+#pragma unroll
+    for (int i = 0; i < BPW; ++i) bp[i] = min(BPW * wave + i, 11);
+    // chunk c into ring slot S; the chunk index is clamped, not branched on (past the end:
+    // the last chunk again, never read)
+    auto issue = [&](int c, auto S) {
+        constexpr int slot = decltype(S)::value;
+        c = c < nchunk ? c : nchunk - 1;
+        uint8_t* base = lds + slot * SLOT;
+        const long long off = (long long)Prob::chunk_off(t, c) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(asrc[j] + off),
+                (__attribute__((address_space(3))) void*)(base + (wave * 32 + 8 * j) * 128), 16, 0, 0);
+        const u32x4* bsrc = wq + (long long)Prob::bchunk_id(t, c) * SG_BQ + lane;
+#pragma unroll
+        for (int i = 0; i < BPW; ++i)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc + bp[i] * 64),
+                                             (__attribute__((address_space(3))) void*)(base + AB + bp[i] * 1024), 16,
+                                             0, 0);
+    };
+
+    f32x16 hi[NT], lo[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) hi[j] = lo[j] = zero16();
+    const int r = lane & 31, h = lane >> 5, sw = (r >> 1) & 7;
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
+    const uint32_t a_lane = lds0 + (wave * 32 + r) * 128, b_lane = lds0 + AB + lane * 16;
+    // Stagger (8 waves: the two waves of a SIMD out of phase): waves 4-7 defer each chunk's
+    // second k-step MFMAs past the next barrier, so right after a barrier one wave of every
+    // SIMD runs matrix work (the deferred k-step) while its partner reads and splits (VALU).
+    // The deferred k-step's operands (split A planes + B fragments) stay in registers.
+    const bool late = STAGGER && wave >= 4;
+    u32x4 daf[3], dbf[6];
+    auto mfma6 = [&](const u32x4 (&af)[3], const u32x4* bf) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            const u32x4 b3[3] = {bf[3 * j], bf[3 * j + 1], bf[3 * j + 2]};
+            mfma_split6(af, b3, hi[j], lo[j]);
+        }
+    };
+    auto split_a = [&](const u32x4 (&g)[8], u32x4 (&af)[3]) {
+        split8(__builtin_bit_cast(float4, g[0]), __builtin_bit_cast(float4, g[1]), af[0], af[1], af[2]);
+    };
+    // chunk in slot S: 16 fragment reads up front (k-step 0's eight, then k-step 1's), k-step 0
+    // computed once its eight have landed (lgkmcnt(8)) while k-step 1's are in flight
+    auto compute = [&](auto S) {
+        constexpr int slot = decltype(S)::value;
+        u32x4 f[2][8];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int g0 = 4 * s + 2 * h;
+            f[s][0] = sg_ds_read(a_lane + slot * SLOT + ((g0 ^ sw) << 4));
+            f[s][1] = sg_ds_read(a_lane + slot * SLOT + (((g0 + 1) ^ sw) << 4));
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    f[s][2 + 3 * j + p] = sg_ds_read(b_lane + slot * SLOT + (((s * NT + j) * 3 + p) * 64) * 16);
+        }
+        u32x4 af[3];
+        sg_lgkm_wait<8>(f[0]);
+        split_a(f[0], af);
+        mfma6(af, f[0] + 2);
+        sg_lgkm_wait<0>(f[1]);
+        if (late) {  // k-step 1 split now, multiplied after the next barrier
+            split_a(f[1], daf);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) dbf[i] = f[1][2 + i];
+        } else {
+            split_a(f[1], af);
+            mfma6(af, f[1] + 2);
+        }
+    };
+    // one pipeline step: this wave's DMAs of chunk c waited for (those of the next SLOTS - 2
+    // chunks may stay in flight: the clamped re-issues past the end count too, so the count is
+    // the same in every step), one barrier (every wave's DMAs of chunk c landed, every wave done
+    // with chunk c - 1), chunk c + SLOTS - 1 issued into the slot chunk c - 1 used, chunk c computed
+    auto step = [&](int c, auto S, auto S2) {
+        sg_vm_wait<NDMA * (SLOTS - 2)>();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        issue(c + SLOTS - 1, S2);
+        if (late && c > 0) mfma6(daf, dbf);  // chunk c - 1's deferred k-step
+        compute(S);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    issue(0, I0{});
+    if constexpr (SLOTS == 3) {
+        issue(1, I1{});
+#pragma unroll 1
+        for (int c = 0; c < nchunk; c += 3) {
+            step(c, I0{}, I2{});
+            if (c + 1 < nchunk) step(c + 1, I1{}, I0{});
+            if (c + 2 < nchunk) step(c + 2, I2{}, I1{});
+        }
+    } else {
+#pragma unroll 1
+        for (int c = 0; c < nchunk; c += 2) {
+            step(c, I0{}, I1{});
+            if (c + 1 < nchunk) step(c + 1, I1{}, I0{});
+        }
+    }
+    if (late && nchunk > 0) mfma6(daf, dbf);
+    sg_vm_wait<0>();  // the clamped tail DMAs, before the LDS is released
+    // epilogue, per column tile: its operand loads first (all issued before its first store)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        f32x16 e;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) e[q] = Prob::prefetch(a, t, wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, j * 32 + r);
+        // one wait for all of them (a real s_waitcnt the compiler tracks): the row-bounded
+        // stores below are branches, and a load pending at a branch makes hipcc wait vmcnt(0)
+        // inside every one of them — behind every earlier store
+        __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            Prob::store_pre(a, t, wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, j * 32 + r, hi[j][q] + lo[j][q], e[q]);
+    }
+}
+
+#ifndef SG_WAVES
+#define SG_WAVES 4  // 4: two 128-row workgroups per CU (2 ring slots); 8: one 256-row workgroup (3 slots)
+#endif
+constexpr int SG_ROWS = 32 * SG_WAVES, SG_SLOTS = SG_WAVES == 8 ? 3 : 2;
+
+template <class Prob>
+int launch_sgemm(const Args& a, const uint16_t* wq, long long blocks, hipStream_t s, const char* name) {
+    if (blocks == 0) return PPOX_OK;
+    sgemm_kernel<Prob, SG_WAVES, SG_SLOTS><<<(unsigned)blocks, 64 * SG_WAVES, 0, s>>>(
+        a, reinterpret_cast<const u32x4*>(wq));
+    PPOX_LAUNCHED(name);
+}
+
+// sg2 Problems: the igemm_split Problems' chunk walk and epilogues on SG_ROWS-row tiles, plus
+// each row's A base pointer (rows past the end clamped to a valid row, never stored) and
+// the chunk's element offset within a row (the same for every row of the tile)
+template <class L, bool OUT_NCHW>
+struct SgFwd : FwdNHWCProblem<L, OUT_NCHW, 1> {
+    static constexpr int ROWS = SG_ROWS, CPT = L::CIN / BK;
+    __device__ static bool tile(const Args& a, RowTile& t) {
+        t.m0 = xcd_remap(blockIdx.x, gridDim.x) * ROWS;
+        t.M = a.batch * L::P;
+        return true;
+    }
+    __device__ static const float* row_ptr(const Args& a, const RowTile& t, int row) {
+        long long m = t.m0 + row;
+        m = m < t.M ? m : t.M - 1;
+        const long long n = m / L::P;
+        const int p = (int)(m - n * L::P), oy = p / L::OW, ox = p % L::OW;
+        return reinterpret_cast<const float*>(a.x) + ((n * L::IH + oy * L::S) * L::IW + ox * L::S) * L::CIN;
+    }
+    __device__ static int chunk_off(const RowTile&, int c) {
+        const int tap = c / CPT;
+        return ((tap / L::KW) * L::IW + tap % L::KW) * L::CIN + (c % CPT) * BK;
+    }
+};
+
+template <class L>
+struct SgDgradPM : DgradPMProblem<L, 1> {
+    using Base = DgradPMProblem<L, 1>;
+    static constexpr int ROWS = SG_ROWS, NPOS = Base::NPOS, CPT = Base::CPT;
+    __device__ static bool tile(const Args& a, PixelTile& t) {
+        const long long w = xcd_remap(blockIdx.x, gridDim.x);
+        t.n0 = (w / NPOS) * ROWS;
+        t.pos = (int)(w % NPOS);
+        t.iy = t.pos / L::IW;
+        t.ix = t.pos % L::IW;
+        int ny, nx;
+        tap_range<L::S, L::OH, L::KH>(t.iy, t.ky0, ny);
+        tap_range<L::S, L::OW, L::KW>(t.ix, t.kx0, nx);
+        t.nx = nx;
+        t.nchunk = ny * nx * CPT;
+        return true;
+    }
+    __device__ static const float* row_ptr(const Args& a, const PixelTile& t, int row) {
+        long long n = t.n0 + row;
+        n = n < a.batch ? n : a.batch - 1;
+        return reinterpret_cast<const float*>(a.x) + n * (L::P * L::COUT);
+    }
+    __device__ static int chunk_off(const PixelTile& t, int c) {
+        const int tap = c / CPT, ty = tap / t.nx, tx = tap - ty * t.nx;
+        const int oy = (t.iy - t.ky0) / L::S - ty, ox = (t.ix - t.kx0) / L::S - tx;
+        return (oy * L::OW + ox) * L::COUT + (c % CPT) * BK;
+    }
+};
+
+template <int K, int N, int MODE>
+struct SgRows : GemmRowsProblem<K, N, 64, MODE> {
+    using Base = GemmRowsProblem<K, N, 64, MODE>;
+    static constexpr int ROWS = SG_ROWS, NCB = Base::NCB;
+    __device__ static bool tile(const Args& a, GemmTile& t) {
+        const long long w = xcd_remap(blockIdx.x, gridDim.x);
+        t.cb = (int)(w % NCB);
+        t.m0 = (w / NCB) * ROWS;
+        t.M = a.batch;
+        return true;
+    }
+    __device__ static const float* row_ptr(const Args& a, const GemmTile& t, int row) {
+        long long m = t.m0 + row;
+        m = m < t.M ? m : t.M - 1;
+        return reinterpret_cast<const float*>(a.x) + m * K;
+    }
+    __device__ static int chunk_off(const GemmTile&, int c) { return c * BK; }
+};
 
 // ---------------------------------------------------------------------------
 // Register-direct implicit GEMM (the default forward / dgrad path).
@@ -1877,6 +2167,13 @@ int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq,
                 hipStream_t s) {
     PPOX_REQUIRE(ppox::aligned16(x), "ppox_nature_conv_fwd_split: layer 2/3 input must be 16B-aligned NHWC");
     Args a{x, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch};
+#if SG2
+    if (layer == 2)
+        return launch_sgemm<SgFwd<G2, false>>(a, wq, ppox::ceil_div(batch * G2::P, SG_ROWS), s,
+                                              "ppox_nature_conv_fwd_split");
+    return launch_sgemm<SgFwd<G3, true>>(a, wq, ppox::ceil_div(batch * G3::P, SG_ROWS), s,
+                                         "ppox_nature_conv_fwd_split");
+#endif
     if (layer == 2) {
         using P2 = FwdNHWCProblem<G2, false, 1>;
         return launch_igemm_split<P2>(a, wq, ppox::ceil_div(batch * G2::P, P2::BMR), s, "ppox_nature_conv_fwd_split");
@@ -1898,6 +2195,10 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
         dgrad2_col_kernel<<<(unsigned)ppox::ceil_div(batch, C2S), 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd));
         PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
     }
+#if SG2
+    return launch_sgemm<SgDgradPM<G3>>(a, wqd, ppox::ceil_div(batch, SG_ROWS) * SgDgradPM<G3>::NPOS, s,
+                                       "ppox_nature_conv_dgrad_split");
+#endif
     using D3 = DgradPMProblem<G3, 1>;
     return launch_igemm_split<D3>(a, wqd, ppox::ceil_div(batch, D3::BMR) * D3::NPOS, s, "ppox_nature_conv_dgrad_split");
 }
@@ -1925,6 +2226,10 @@ extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t
     PPOX_REQUIRE(h3 && q_fwd && bias && f && batch >= 0, "ppox_nature_fc_fwd: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd), "ppox_nature_fc_fwd: 16B alignment");
     Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch};
+#if SG2
+    return launch_sgemm<SgRows<3136, 512, FC_FWD>>(a, q_fwd, ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB,
+                                                   ppox::as_stream(stream), "ppox_nature_fc_fwd");
+#endif
     return launch_igemm_split<FcFwd>(a, q_fwd, ppox::ceil_div(batch, 128) * FcFwd::NCB, ppox::as_stream(stream),
                                      "ppox_nature_fc_fwd");
 }
@@ -1935,6 +2240,10 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
     PPOX_REQUIRE(df && q_dgrad && h3 && g3 && batch >= 0, "ppox_nature_fc_dgrad: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(q_dgrad), "ppox_nature_fc_dgrad: 16B alignment");
     Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch};
+#if SG2
+    return launch_sgemm<SgRows<512, 3136, FC_DGRAD>>(a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB,
+                                                     ppox::as_stream(stream), "ppox_nature_fc_dgrad");
+#endif
     return launch_igemm_split<FcDgrad>(a, q_dgrad, ppox::ceil_div(batch, 128) * FcDgrad::NCB, ppox::as_stream(stream),
                                        "ppox_nature_fc_dgrad");
 }
