@@ -272,8 +272,10 @@ int ppox_vecnorm_reward(float* rewards, const uint8_t* dones, double* ret, int64
 /* NatureCNN hidden layer Linear(3136, 512) + ReLU (.ipynb_checkpoints/models-checkpoint.py:58-59)
  * on the split-bf16 GEMM: weights packed (once per optimizer step) by ppox_nature_fc_pack into
  * ppox_nature_fc_pack_elems() uint16 each for the forward (W^T) and the dgrad (W) operand.
- * fwd: f = relu(h3 @ W^T + b); dgrad: g3 (NHWC (B,7,7,64)) = (df @ W)[Flatten order] * (h3 > 0)
- * (df = dL/df already ReLU-masked) — the trunk's ReLU backward and NCHW->NHWC fused. */
+ * Both run in NHWC feature order: h3 is the split conv3 forward's NHWC output (batch, 7, 7, 64)
+ * and W is packed through the permutation f = p * 64 + c <- Flatten feature c * 49 + p.
+ * fwd: f = relu(h3 @ W^T + b); dgrad: g3 (NHWC (B,7,7,64)) = (df @ W) * (h3 > 0)
+ * (df = dL/df already ReLU-masked) — the trunk's ReLU backward fused. */
 int64_t ppox_nature_fc_pack_elems(void);
 /* All weight packings of one optimizer step in a single launch (any output may be null):
  * wpd2 = f32 conv2 dgrad ([(ky,kx,co)][ci]); q1..q3 / qd2, qd3 = split forms (as
@@ -343,7 +345,10 @@ int ppox_outer_relu_backward(const float* dv, const float* w, const float* act, 
  * Weights are packed by ppox_nature_pack_split into bf16 planes (uint16
  * storage) of ppox_nature_split_pack_elems(which) elements: which = 1, 2, 3
  * (forward weights of that layer), 12, 13 (dgrad weights of conv2 / conv3).
- * Replaces the same reference sites as the f32 forms.
+ * Replaces the same reference sites as the f32 forms.  One layout difference: the split
+ * conv3 forward writes its output NHWC, y (batch, 7, 7, 64) — feature p * 64 + c instead
+ * of the reference's Flatten feature c * 49 + p — which the split fc layer below consumes
+ * (its weights are packed through that permutation).
  * -------------------------------------------------------------------------*/
 int64_t ppox_nature_split_pack_elems(int32_t which);
 int ppox_nature_pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1,

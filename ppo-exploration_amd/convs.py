@@ -71,12 +71,15 @@ class RolloutRows:
 
 
 class _NatureTrunk(torch.autograd.Function):
+    """Autograd wrapper of the trunk (tests, non-explicit nets): returns h3 in the reference's
+    (B, 64, 7, 7) layout — a permuted view of the NHWC h3 in split math."""
+
     @staticmethod
     def forward(ctx, x, convs, w1, b1, w2, b2, w3, b3):
         h1, h2, h3 = convs.forward_acts(x)
         ctx.convs = convs
         ctx.save_for_backward(x, h1, h2, h3)
-        return h3
+        return h3.permute(0, 3, 1, 2) if convs.nhwc3 else h3
 
     @staticmethod
     def backward(ctx, dh3):
@@ -84,7 +87,12 @@ class _NatureTrunk(torch.autograd.Function):
         convs = ctx.convs
         grads = [torch.zeros_like(t) for t in (convs.c1.weight, convs.c1.bias, convs.c2.weight, convs.c2.bias,
                                                convs.c3.weight, convs.c3.bias)]
-        convs.backward_acts(x, h1, h2, h3, dh3.contiguous(), *grads)
+        if convs.nhwc3:
+            g3 = dh3.permute(0, 2, 3, 1).contiguous()
+            native.relu_backward_(g3, h3)
+            convs.backward_acts(x, h1, h2, h3, None, *grads, g3=g3)
+        else:
+            convs.backward_acts(x, h1, h2, h3, dh3.contiguous(), *grads)
         return (None, None, *grads)
 
 
@@ -112,6 +120,15 @@ class NatureConvs:
         nfc = native.nature_fc_pack_elems()
         self.qfc = (torch.empty(nfc, dtype=torch.int16, device=dev), torch.empty(nfc, dtype=torch.int16, device=dev)) \
             if self.math != "f32" else None
+        # split math keeps conv3's output NHWC (B, 7, 7, 64): fc feature f = p * 64 + c is the
+        # reference's Flatten feature c * 49 + p.  The split fc kernels are packed through that
+        # permutation; the library GEMMs (fc forward below FC_SPLIT_MIN_BATCH, fc weight grad)
+        # use this permuted f32 copy of the weight / permute their result back.
+        self.nhwc3 = self.math != "f32"
+        if self.nhwc3:
+            f = torch.arange(3136, device=dev)
+            self.fc_perm = (f % 64) * 49 + f // 64  # NHWC feature -> Flatten feature
+            self.wfc_nhwc = torch.empty(512, 3136, device=dev)
         self._ws = {}
         self._version = None
         self._packed = set()
@@ -142,8 +159,7 @@ class NatureConvs:
             forms.add(("q" if split else "wp") + ("d" if op == "dgrad" else "") + str(L))
         if self.math != "f32":
             forms.add("qfcd")
-            if batch >= FC_SPLIT_MIN_BATCH:
-                forms.add("qfcf")
+            forms.add("qfcf" if batch >= FC_SPLIT_MIN_BATCH else "wfc_nhwc")
         return forms
 
     def pack(self, batch=0):
@@ -167,6 +183,8 @@ class NatureConvs:
             native.nature_pack_all(w1, w2, w3, self.fc.weight, pick("wpd2", self.wpd2), pick("q1", q[1]),
                                    pick("q2", q[2]), pick("q3", q[3]), pick("qd2", q[12]), pick("qd3", q[13]),
                                    pick("qfcf", qfc[0]), pick("qfcd", qfc[1]))
+        if "wfc_nhwc" in missing:
+            torch.index_select(self.fc.weight.detach(), 1, self.fc_perm, out=self.wfc_nhwc)
         self._packed |= missing
 
     def invalidate(self):
@@ -205,13 +223,14 @@ class NatureConvs:
             native.nature_conv_wgrad(layer, x, B, None, 0, 0, stride, g, self.workspace(layer, B), dw, db)
 
     def forward_acts(self, x):
-        """Trunk forward: (h1 NHWC, h2 NHWC, h3 NCHW) activations (ReLU applied)."""
+        """Trunk forward: (h1 NHWC, h2 NHWC, h3) activations (ReLU applied); h3 is NHWC
+        (B, 7, 7, 64) in split math (self.nhwc3), NCHW (B, 64, 7, 7) in f32 math."""
         self.pack(x.shape[0])
         B = x.shape[0]
         dev = x.device
         h1 = torch.empty((B, 20, 20, 32), device=dev)
         h2 = torch.empty((B, 9, 9, 64), device=dev)
-        h3 = torch.empty((B, 64, 7, 7), device=dev)
+        h3 = torch.empty((B, 7, 7, 64) if self.nhwc3 else (B, 64, 7, 7), device=dev)
         if B:
             self.fwd(1, x, B, self.c1.bias, h1)
             self.fwd(2, h1, B, self.c2.bias, h2)
@@ -220,26 +239,27 @@ class NatureConvs:
 
     # ---- fc layer (split math): forward and the dgrad fused with the trunk's ReLU backward
     def fc_forward(self, h3):
-        """f = relu(h3 @ W^T + b), h3 (B, 64, 7, 7): the split-bf16 GEMM when the batch fills
-        the chip (ceil(B/128) row tiles x 8 column blocks >= ~512 workgroups), rocBLAS below."""
+        """f = relu(h3 @ W^T + b), h3 (B, 7, 7, 64) NHWC (split math): the split-bf16 GEMM when
+        the batch fills the chip (ceil(B/128) row tiles x 8 column blocks >= ~512 workgroups),
+        rocBLAS on the NHWC-permuted weight below."""
         self.pack(h3.shape[0])
         B = h3.shape[0]
         if B < FC_SPLIT_MIN_BATCH:
-            return torch._addmm_activation(self.fc.bias, h3.view(B, -1), self.fc.weight.t())  # bias+ReLU fused
+            return torch._addmm_activation(self.fc.bias, h3.view(B, -1), self.wfc_nhwc.t())  # bias+ReLU fused
         f = torch.empty((B, 512), device=h3.device)
         native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f)
         return f
 
     def fc_dgrad_g3(self, df, h3):
-        """g3 (B, 7, 7, 64) NHWC = (df @ W) * (h3 > 0), df = dL/df after the fc ReLU."""
+        """g3 (B, 7, 7, 64) NHWC = (df @ W) * (h3 > 0), df = dL/df after the fc ReLU, h3 NHWC."""
         B = df.shape[0]
         g3 = torch.empty((B, 7, 7, 64), device=df.device)
         native.nature_fc_dgrad(df.contiguous(), B, self.qfc[1], h3, g3)
         return g3
 
     def backward_acts(self, x, h1, h2, h3, dh3, dw1, db1, dw2, db2, dw3, db3, g3=None):
-        """Trunk backward from dL/dh3 (B, 3136 NCHW order, before the ReLU mask) — or from
-        g3, the already masked NHWC grad: writes (overwrites) the six conv gradients."""
+        """Trunk backward from dL/dh3 (f32 math: B x 3136 in NCHW order, before the ReLU mask)
+        — or from g3, the already masked NHWC grad: writes (overwrites) the six conv gradients."""
         B = x.shape[0]
         if B == 0:
             for t in (dw1, db1, dw2, db2, dw3, db3):

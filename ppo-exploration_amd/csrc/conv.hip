@@ -527,6 +527,11 @@ __global__ void pack_split_gemm(const float* __restrict__ w, uint16_t* __restric
 //             NCHW -> NHWC transpose fused (replaces the dh3 round trip + nchw_to_nhwc_mask)
 // ---------------------------------------------------------------------------
 enum { FC_FWD = 0, FC_DGRAD = 1 };
+// The split fc kernels run in NHWC feature order: feature f = p * 64 + c of the conv3 output
+// (the layout conv3's split forward writes, 128-B channel runs) is the reference's Flatten
+// feature c * 49 + p of Linear(3136, 512) — the weights are packed through this permutation,
+// so the forward reads h3 rows and the dgrad writes g3 rows as they lie, no transposes.
+__host__ __device__ constexpr int fc_nchw_feature(int f) { return (f & 63) * 49 + (f >> 6); }
 struct GemmTile {
     long long m0, M;
     int cb;
@@ -585,15 +590,19 @@ struct GemmRowsProblem {
         const long long m = t.m0 + row;
         const int n = t.cb * NB + col;
         if (m >= t.M || n >= N) return;
-        if constexpr (MODE == FC_FWD) {
+        if constexpr (MODE == FC_FWD)
             a.y[m * N + n] = fmaxf(acc + e, 0.f);
-        } else {
-            const int c = n / 49, p = n - c * 49;  // Flatten order of (64, 7, 7)
-            a.y[(m * 49 + p) * 64 + c] = e > 0.f ? acc : 0.f;
-        }
+        else  // g3 (NHWC) times the ReLU mask of h3 (NHWC): the same element index
+            a.y[m * N + n] = e > 0.f ? acc : 0.f;
     }
 };
 
+#ifndef FC_FWD_G
+#define FC_FWD_G 2  // fc forward: column blocks per tile group (SgRows)
+#endif
+#ifndef FC_DGRAD_G
+#define FC_DGRAD_G 12  // fc dgrad: column blocks per tile group
+#endif
 #ifndef SG2
 #define SG2 1  // 0: the split GEMMs on igemm_split_kernel (register-staged, 128-row tiles)
 #endif
@@ -612,7 +621,8 @@ __device__ inline void pack_split_gemm_rows_elem(const float* __restrict__ w, ui
     if (i >= (long long)Prob::NCB * K * NB) return;
     const int cb = (int)(i / ((long long)K * NB)), rem = (int)(i % ((long long)K * NB));
     const int k = rem / NB, col = rem % NB, n = cb * NB + col;
-    const float v = n < N ? (TRANS ? w[(long long)n * K + k] : w[(long long)k * N + n]) : 0.f;
+    const float v = n < N ? (TRANS ? w[(long long)n * K + fc_nchw_feature(k)] : w[(long long)k * N + fc_nchw_feature(n)])
+                          : 0.f;
     uint16_t p0, p1, p2;
     split3(v, p0, p1, p2);
     const long long base = (long long)cb * K * NB * 3;
@@ -1071,14 +1081,21 @@ struct SgDgradPM : DgradPMProblem<L, 1> {
     }
 };
 
-template <int K, int N, int MODE>
+// Tile order: column-block groups of G outermost, then row tiles, then the G column blocks of
+// the group — so the workgroups an XCD runs together share one A row tile, and one group's B
+// (G x 196 KB / 1.2 MB for the dgrad / forward) stays in that XCD's L2 while its row tiles
+// stream past (A is read NCB / G times, B about once per XCD).
+template <int K, int N, int MODE, int G>
 struct SgRows : GemmRowsProblem<K, N, 64, MODE> {
     using Base = GemmRowsProblem<K, N, 64, MODE>;
     static constexpr int ROWS = SG_ROWS, NCB = Base::NCB;
     __device__ static bool tile(const Args& a, GemmTile& t) {
         const long long w = xcd_remap(blockIdx.x, gridDim.x);
-        t.cb = (int)(w % NCB);
-        t.m0 = (w / NCB) * ROWS;
+        const long long rt = (a.batch + ROWS - 1) / ROWS;      // row tiles
+        const long long grp = w / (rt * G), in = w - grp * rt * G;
+        const int g0 = (int)grp * G, gn = NCB - g0 < G ? NCB - g0 : G;  // the last group may be narrower
+        t.m0 = (in / gn) * ROWS;
+        t.cb = g0 + (int)(in % gn);
         t.M = a.batch;
         return true;
     }
@@ -1939,14 +1956,16 @@ struct ConvSrc {
         return w[((co * L::CIN + ci) * L::KH + tap / L::KW) * L::KW + tap % L::KW];
     }
 };
-// source value (k, col) of column block cb of a GemmRows B (w[n][k] when TRANS, w[k][n] otherwise)
+// source value (k, col) of column block cb of a GemmRows B (w[n][k] when TRANS, w[k][n] otherwise);
+// the fc's 3136-wide side (K of the forward, N of the dgrad) is taken in NHWC feature order
 template <class Prob, bool TRANS>
 struct RowsSrc {
     const float* w;
     int cb;
     __device__ float operator()(int k, int col) const {
         const int n = cb * Prob::NOUT + col;
-        return n < Prob::N ? (TRANS ? w[(long long)n * Prob::K + k] : w[(long long)k * Prob::N + n]) : 0.f;
+        if (n >= Prob::N) return 0.f;
+        return TRANS ? w[(long long)n * Prob::K + fc_nchw_feature(k)] : w[(long long)k * Prob::N + fc_nchw_feature(n)];
     }
 };
 template <class Prob, bool TRANS>
@@ -2171,14 +2190,14 @@ int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq,
     if (layer == 2)
         return launch_sgemm<SgFwd<G2, false>>(a, wq, ppox::ceil_div(batch * G2::P, SG_ROWS), s,
                                               "ppox_nature_conv_fwd_split");
-    return launch_sgemm<SgFwd<G3, true>>(a, wq, ppox::ceil_div(batch * G3::P, SG_ROWS), s,
-                                         "ppox_nature_conv_fwd_split");
+    return launch_sgemm<SgFwd<G3, false>>(a, wq, ppox::ceil_div(batch * G3::P, SG_ROWS), s,
+                                          "ppox_nature_conv_fwd_split");
 #endif
     if (layer == 2) {
         using P2 = FwdNHWCProblem<G2, false, 1>;
         return launch_igemm_split<P2>(a, wq, ppox::ceil_div(batch * G2::P, P2::BMR), s, "ppox_nature_conv_fwd_split");
     }
-    using P3 = FwdNHWCProblem<G3, true, 1>;
+    using P3 = FwdNHWCProblem<G3, false, 1>;  // split math: conv3 output NHWC (see fc_nchw_feature)
     return launch_igemm_split<P3>(a, wq, ppox::ceil_div(batch * G3::P, P3::BMR), s, "ppox_nature_conv_fwd_split");
 }
 }  // namespace ppox_conv
@@ -2227,7 +2246,7 @@ extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t
     PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd), "ppox_nature_fc_fwd: 16B alignment");
     Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch};
 #if SG2
-    return launch_sgemm<SgRows<3136, 512, FC_FWD>>(a, q_fwd, ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB,
+    return launch_sgemm<SgRows<3136, 512, FC_FWD, FC_FWD_G>>(a, q_fwd, ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB,
                                                    ppox::as_stream(stream), "ppox_nature_fc_fwd");
 #endif
     return launch_igemm_split<FcFwd>(a, q_fwd, ppox::ceil_div(batch, 128) * FcFwd::NCB, ppox::as_stream(stream),
@@ -2241,7 +2260,7 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
     PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(q_dgrad), "ppox_nature_fc_dgrad: 16B alignment");
     Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch};
 #if SG2
-    return launch_sgemm<SgRows<512, 3136, FC_DGRAD>>(a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB,
+    return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_G>>(a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB,
                                                      ppox::as_stream(stream), "ppox_nature_fc_dgrad");
 #endif
     return launch_igemm_split<FcDgrad>(a, q_dgrad, ppox::ceil_div(batch, 128) * FcDgrad::NCB, ppox::as_stream(stream),

@@ -141,6 +141,13 @@ class CnnActorCritic(nn.Module):
             iv = native.head_linear(ie, ci.weight, ci.bias).squeeze(-1)
         return out, v, iv, e, ie
 
+    def _fc_grad_buf(self, w):
+        buf = getattr(self, "_fcg", None)
+        if buf is None or buf.device != w.device:
+            buf = torch.empty_like(w)
+            self._fcg = buf
+        return buf
+
     def _head_ws(self, rows, h, n_actions):
         need = native.head_grads_workspace_bytes(rows, h, n_actions, self.intrinsic)
         ws = getattr(self, "_hg_ws", None)
@@ -172,7 +179,13 @@ class CnnActorCritic(nn.Module):
                 df.addmm_(de, hid.weight)
                 des.append((de, d))
             native.relu_backward_(df, f)
-            torch.mm(df.t(), hf, out=fc.weight.grad)
+            cv = self.conv_impl
+            if cv.nhwc3:  # NHWC features (split math): dW in NHWC order, permuted back to Flatten order
+                dwp = self._fc_grad_buf(fc.weight)
+                torch.mm(df.t(), hf, out=dwp)
+                fc.weight.grad.view(fc.weight.shape[0], 64, 49).copy_(dwp.view(-1, 49, 64).transpose(1, 2))
+            else:
+                torch.mm(df.t(), hf, out=fc.weight.grad)
             # every column-reduction gradient (actor W/b, critic W/b, extra-layer b, fc b) in one pass
             ws = self._head_ws(B, f.shape[1], dout.shape[1])
             (de, d), intr = des[0], des[1] if self.intrinsic else (None, None)
@@ -186,8 +199,13 @@ class CnnActorCritic(nn.Module):
                 dense_ready()
             fe = self.feature_extractor
             import convs as _convs
-            if self.conv_impl.math != "f32" and B < _convs.FC_DGRAD_FUSED_MAX_BATCH:  # masked NHWC grad directly
-                dh3, g3 = None, self.conv_impl.fc_dgrad_g3(df, h3)
+            if cv.nhwc3 and B < _convs.FC_DGRAD_FUSED_MAX_BATCH:  # masked NHWC grad directly
+                dh3, g3 = None, cv.fc_dgrad_g3(df, h3)
+            elif cv.nhwc3:  # library GEMM on the permuted weight: NHWC order, then the ReLU mask
+                torch.index_select(fc.weight, 1, cv.fc_perm, out=cv.wfc_nhwc)
+                g3 = torch.mm(df, cv.wfc_nhwc).view(B, 7, 7, 64)
+                native.relu_backward_(g3, h3)
+                dh3 = None
             else:
                 dh3, g3 = torch.mm(df, fc.weight), None
             # conv grads are written by the trunk kernels; the flat buffer was zeroed per minibatch

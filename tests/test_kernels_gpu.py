@@ -458,10 +458,12 @@ def _conv_ops_fp64(B, seed):
         cv.pack()
         h1 = torch.empty(B, 20, 20, 32, device="cuda")
         h2 = torch.empty(B, 9, 9, 64, device="cuda")
-        h3 = torch.empty(B, 64, 7, 7, device="cuda")
+        h3 = torch.empty((B, 7, 7, 64) if cv.nhwc3 else (B, 64, 7, 7), device="cuda")
         cv.fwd(1, x, B, cv.c1.bias, h1)
         cv.fwd(2, h1, B, cv.c2.bias, h2)
         cv.fwd(3, h2, B, cv.c3.bias, h3)
+        if cv.nhwc3:  # split math writes conv3's output NHWC
+            h3 = h3.permute(0, 3, 1, 2)
         hs.update({("fwd", 1): h1, ("fwd", 2): h2, ("fwd", 3): h3})
         out[math] = hs
     # backward ops on shared inputs (f32-mode activations as ReLU masks, random output grads)
@@ -759,20 +761,21 @@ def test_fc_split_gemm_vs_fp64(B):
     torch.manual_seed(B)
     W = torch.randn(512, 3136, device="cuda") * 0.02
     b = torch.randn(512, device="cuda") * 0.1
-    h3 = torch.relu(torch.randn(B, 3136, device="cuda"))
+    h3n = torch.relu(torch.randn(B, 7, 7, 64, device="cuda"))      # NHWC, as the split conv3 writes it
+    h3 = h3n.permute(0, 3, 1, 2).reshape(B, 3136)                    # the reference's Flatten order
     df = torch.randn(B, 512, device="cuda")
     n = native.nature_fc_pack_elems()
     qf, qd = torch.empty(n, dtype=torch.int16, device="cuda"), torch.empty(n, dtype=torch.int16, device="cuda")
     native.nature_fc_pack(W, qf, qd)
     f = torch.empty(B, 512, device="cuda")
-    native.nature_fc_fwd(h3, B, qf, b, f)
+    native.nature_fc_fwd(h3n, B, qf, b, f)
     ref = torch.relu(h3.double() @ W.double().t() + b.double())
     e_s = (f.double() - ref).abs().max() / ref.abs().max()
     e_f = (torch.relu(torch.addmm(b, h3, W.t())).double() - ref).abs().max() / ref.abs().max()
     assert e_s <= 2 * e_f + 1e-7, (float(e_s), float(e_f))
     g3 = torch.empty(B, 7, 7, 64, device="cuda")
-    native.nature_fc_dgrad(df, B, qd, h3, g3)
-    mask = (h3.view(B, 64, 7, 7).permute(0, 2, 3, 1) > 0)
+    native.nature_fc_dgrad(df, B, qd, h3n, g3)
+    mask = h3n > 0
     refd = (df.double() @ W.double()).view(B, 64, 7, 7).permute(0, 2, 3, 1) * mask
     e_s = (g3.double() - refd).abs().max() / refd.abs().max()
     e_f = ((df @ W).view(B, 64, 7, 7).permute(0, 2, 3, 1) * mask).double().sub(refd).abs().max() / refd.abs().max()

@@ -31,7 +31,8 @@ def main():
     torch.manual_seed(0)
     W = torch.randn(512, 3136, device=d) * 0.02
     b = torch.randn(512, device=d) * 0.1
-    h3 = torch.relu(torch.randn(B, 3136, device=d))
+    h3n = torch.relu(torch.randn(B, 7, 7, 64, device=d))        # NHWC (the split kernels' order)
+    h3 = h3n.permute(0, 3, 1, 2).reshape(B, 3136)               # Flatten order (rocBLAS reference)
     df = torch.randn(B, 512, device=d)
     n = native.nature_fc_pack_elems()
     qf, qd = torch.empty(n, dtype=torch.int16, device=d), torch.empty(n, dtype=torch.int16, device=d)
@@ -40,9 +41,9 @@ def main():
     g3 = torch.empty(B, 7, 7, 64, device=d)
     flop = 2.0 * B * 3136 * 512
     res = {"B": B}
-    res["split_fwd_ms"] = t_ms(lambda: native.nature_fc_fwd(h3, B, qf, b, f))
+    res["split_fwd_ms"] = t_ms(lambda: native.nature_fc_fwd(h3n, B, qf, b, f))
     res["rocblas_fwd_ms"] = t_ms(lambda: torch.relu(torch.addmm(b, h3, W.t())))
-    res["split_dgrad_ms"] = t_ms(lambda: native.nature_fc_dgrad(df, B, qd, h3, g3))
+    res["split_dgrad_ms"] = t_ms(lambda: native.nature_fc_dgrad(df, B, qd, h3n, g3))
     res["rocblas_dgrad_ms"] = t_ms(lambda: torch.mm(df, W))
     for k in list(res):
         if k.endswith("_ms"):
@@ -51,13 +52,12 @@ def main():
     # accuracy vs float64 (first 512 rows)
     r = 512
     ref = torch.relu(h3[:r].double() @ W.double().t() + b.double())
-    native.nature_fc_fwd(h3, B, qf, b, f)
+    native.nature_fc_fwd(h3n, B, qf, b, f)
     f32 = torch.relu(torch.addmm(b, h3[:r], W.t()))
     res["fwd_err_split"] = float((f[:r].double() - ref).abs().max() / ref.abs().max())
     res["fwd_err_f32"] = float((f32.double() - ref).abs().max() / ref.abs().max())
-    refd = (df[:r].double() @ W.double()).view(r, 64, 7, 7).permute(0, 2, 3, 1) * (h3[:r].view(r, 64, 7, 7)
-                                                                                      .permute(0, 2, 3, 1) > 0)
-    native.nature_fc_dgrad(df, B, qd, h3, g3)
+    refd = (df[:r].double() @ W.double()).view(r, 64, 7, 7).permute(0, 2, 3, 1) * (h3n[:r] > 0)
+    native.nature_fc_dgrad(df, B, qd, h3n, g3)
     res["dgrad_err_split"] = float((g3[:r].double() - refd).abs().max() / refd.abs().max())
     print(json.dumps(res))
 
