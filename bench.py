@@ -20,6 +20,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ppo-exploration_amd"))
 
+PMC_LAUNCH_ROWS = 16384      # rows per conv launch in the committed PMC passes (tools/gpu_profile.sh)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (= f32 vector) dense peak
 
@@ -213,6 +214,7 @@ def main():
     torch.backends.cudnn.allow_tf32 = False
 
     import native
+    import phases
     import ppo
     import logger
 
@@ -245,6 +247,7 @@ def main():
     gae_kernel = "ppox_gae" if args.algo != "rnd" else "ppox_gae_dual"
     native.enable_event_timing([prof_kernel])
 
+    phases.enable_timers()
     torch.cuda.synchronize()
     if world > 1:
         tdist.barrier()
@@ -257,6 +260,9 @@ def main():
     dt = time.perf_counter() - t0
     kt = native.event_times_ms(prof_kernel)
     native.enable_event_timing([])
+    phase_ms = {k: {"gpu_ms": round(v["gpu_ms"] / args.steps, 2), "host_ms": round(v["host_ms"] / args.steps, 2)}
+                for k, v in phases.summary().items()}
+    phases.enable_timers(False)
     gae_ms = gae_kernel_ms(alg, args.algo == "rnd")
     if world > 1:
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
@@ -278,13 +284,18 @@ def main():
                    "conv_math": conv_impl.math if conv_impl is not None else None,
                    "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)" if world > 1 else "single GPU"},
     }
+    # per iteration, rank 0: GPU stream time and host time of each phase (phases.py);
+    # gae and episodes run inside collect
+    out["phases_ms_per_step"] = phase_ms
     if kt:
         out["roofline"] = conv_roofline(prof_kernel, kt, totals)
-        if world > 1 and out["roofline"].get("traffic") is not None:
-            # the committed PMC passes ran the 1-GPU workload (launches of 16384 rows); the
-            # per-rank launches here are smaller, so that per-launch figure does not apply
+        launch_rows = float(np.mean([a[2] for _, a in kt]))
+        if out["roofline"].get("traffic") is not None and launch_rows != PMC_LAUNCH_ROWS:
+            # the committed PMC passes ran launches of PMC_LAUNCH_ROWS rows (the 1-GPU
+            # workload); a per-launch byte count of another size does not apply here
             out["roofline"]["traffic"] = None
-            out["roofline"]["traffic_note"] = "PMC traffic is measured on the 1-GPU workload (profiles/); n/a per rank"
+            out["roofline"]["traffic_note"] = (f"PMC traffic was measured on {PMC_LAUNCH_ROWS}-row launches "
+                                               f"(profiles/); these launches average {launch_rows:.0f} rows")
     if gae_ms:
         n_local = args.envs // world
         alg_bytes = (17 if gae_kernel == "ppox_gae" else 33) * args.nstep * n_local

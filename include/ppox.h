@@ -288,6 +288,14 @@ int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, co
                        void* stream);
 int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
                          void* stream);
+/* fc weight gradient dW (512 x 3136, the weight's Flatten order) = df^T @ h3 over the batch,
+ * split-bf16 (fp32-class), deterministic: df (batch, 512) is dL/df already ReLU-masked, h3 the
+ * NHWC (batch, 7, 7, 64) conv3 output of the split forward.  Replaces the library GEMM of
+ * torch.nn.Linear's backward (reference: models-checkpoint.py:58-59 trained by ppo.py:236-238).
+ * batch 0 writes a zero gradient.  workspace: ppox_nature_fc_wgrad_workspace_bytes(batch). */
+int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch);
+int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float* h3, void* workspace,
+                         int64_t workspace_bytes, float* dw, void* stream);
 
 /* ES-NSRA (evolution_strategies.py:103-384, csrc/es.hip), float64 throughout.
  * ppox_es_noise: eps[p][j] ~ N(0,1) for members member0..member0+P-1 of a generation

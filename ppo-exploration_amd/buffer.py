@@ -24,6 +24,7 @@ import torch
 import logger
 import native
 from dist import DistContext
+from phases import traced
 
 
 def _space_dim(space):
@@ -155,6 +156,7 @@ class RolloutStorage(BaseBuffer):
         native.simhash_apply(keys_all, total, offset, self.n_envs, self.count_table, self.beta, rewards)
         return rewards
 
+    @traced("gae")
     def compute_returns_and_advantages(self, last_value, dones):
         """buffer.py:203-230 on the device (bit-identical), libppox ppox_gae."""
         lv = _to_dev(last_value, self.device, torch.float32).reshape(self.n_envs).contiguous()
@@ -223,6 +225,7 @@ class IntrinsicStorage(RolloutStorage):
         self.int_values[t].copy_(_to_dev(int_value, self.device).reshape(self.n_envs))
         super().add(obs, action, reward, value, mask, log_prob)
 
+    @traced("gae")
     def compute_returns_and_advantages(self, last_value, last_int_value, dones):
         """buffer.py:321-362, libppox ppox_gae_dual (both streams bit-identical)."""
         logger.record("rollout/mean_int_reward", float(self.int_rewards.mean().item()))

@@ -42,6 +42,9 @@ FC_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_SPLIT_MIN", "8192"))
 # batch (PPOX_FC_DGRAD_FUSED_MAX overrides): faster than rocBLAS + nchw_to_nhwc_mask at
 # every measured batch (A/B: -33 ms per iteration at 16384, -2 ms at 2048)
 FC_DGRAD_FUSED_MAX_BATCH = int(os.environ.get("PPOX_FC_DGRAD_FUSED_MAX", str(1 << 62)))
+# fc weight gradient on the split wgrad kernel (ppox_nature_fc_wgrad) from this batch up,
+# the rocBLAS f32 GEMM + NHWC -> Flatten permute below (PPOX_FC_WGRAD_SPLIT_MIN overrides)
+FC_WGRAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_WGRAD_SPLIT_MIN", "0"))
 
 
 def default_math():

@@ -1500,7 +1500,9 @@ struct WsCfg {
     static constexpr int KT = KT_, KB = L::K / KT, COUT = L::COUT;
     static constexpr int XP = U8 ? 1 : 3;                        // X planes
     static constexpr int NKT = KT / 32, NCT = COUT / 32, TPW = NKT * NCT / 4;
-    static constexpr int WKT = NCT == 1 ? TPW : 1, WCT = TPW / WKT;  // k- and co-tiles per wave
+    // wave grid: WC waves along co (WCT co-tiles each) x 4/WC along k (WKT k-tiles each)
+    static constexpr int WCT = TPW % NCT == 0 ? NCT : (NCT % TPW == 0 ? TPW : 1);
+    static constexpr int WC = NCT / WCT, WKT = NKT / (4 / WC);
     static constexpr int XR = KT * 2, GR = COUT * 2;             // LDS row bytes
     static constexpr int XPB = MS * XR, GPB = MS * GR;           // LDS plane bytes
     static constexpr int STAGE = XP * XPB + 3 * GPB;
@@ -1508,7 +1510,7 @@ struct WsCfg {
     // consecutive co of one pixel, so its addresses come from one (sample, pixel) pair
     static constexpr int UPX = KT / 8, XU = UPX / 8, GW = COUT / 8;
     static_assert(KB * KT == L::K && (NKT * NCT) % 4 == 0 && XU * 8 == UPX && (GW == 4 || GW == 8), "wgrad split shape");
-    static_assert(WKT * WCT == TPW && (NCT == 1 || WKT == 1), "wave tiling");
+    static_assert(WKT * WCT == TPW && 4 % WC == 0 && NKT % (4 / WC) == 0, "wave tiling");
 };
 
 // XOR on the 32-byte chunk index of row px (rows of ROWB bytes): the transposed reads
@@ -1528,20 +1530,36 @@ __device__ inline uint2 lds_tr16(const uint8_t* p) {
     return __builtin_bit_cast(uint2, r);
 }
 
-template <class L, bool U8, int KT>
+__device__ float kZeroG[64] = {};  // the G row of a pixel past a split's end (global AS: no flat loads)
+
+// CB > 1: G rows hold CB blocks of COUT columns (row stride CB * COUT) and each
+// workgroup owns one block — the fc layer's weight gradient (K = the 512 outputs,
+// G = the NHWC conv3 activations, one 64-channel pixel per block); its grid is any
+// number of (split, k-block, column-block) items, column-block fastest within an XCD.
+template <class L, bool U8, int KT, bool ROWS, int CB = 1>
 __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     using C = WsCfg<L, U8, KT>;
     constexpr int COUT = L::COUT, XP = C::XP, XR = C::XR, GR = C::GR, XU = C::XU;
-    constexpr int WKT = C::WKT, WCT = C::WCT;
+    constexpr int WKT = C::WKT, WCT = C::WCT, GS = CB * COUT;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * C::STAGE];
-    const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
-    const int kb = q % C::KB, split = (q / C::KB) * 8 + xcd;
+    int kb, split, cb;
+    if constexpr (CB == 1) {
+        const int b = blockIdx.x, xcd = b & 7, q = b >> 3;
+        kb = q % C::KB;
+        split = (q / C::KB) * 8 + xcd;
+        cb = 0;
+    } else {
+        const long long w = xcd_remap(blockIdx.x, gridDim.x);
+        cb = (int)(w % CB);
+        kb = (int)((w / CB) % C::KB);
+        split = (int)(w / (CB * C::KB));
+    }
     const unsigned M = (unsigned)(a.batch * L::P);
     const unsigned long long mb64 = (unsigned long long)split * (unsigned long long)a.px_per_split;
     const unsigned mbeg = mb64 < M ? (unsigned)mb64 : M;
     const unsigned mend = (unsigned)min((unsigned long long)M, (unsigned long long)mbeg + a.px_per_split);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int kt0 = (wave * C::TPW) / C::NCT, ct0 = (wave * C::TPW) % C::NCT;
+    const int kt0 = (wave / C::WC) * WKT, ct0 = (wave % C::WC) * WCT;
 
     f32x16 hi[WKT][WCT], lo[WKT][WCT];
 #pragma unroll
@@ -1553,9 +1571,28 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     const uint8_t* xu8 = reinterpret_cast<const uint8_t*>(a.x);
     const float* xf = reinterpret_cast<const float*>(a.x);
     constexpr int GW = C::GW;
-    uint32_t xw[XU][2];
-    float4 xr[XU][2];
-    float4 gr[2];
+    // raw global data of one step; the pipeline holds two (steps s+1 and s+2 during step s)
+    struct Raw {
+        uint32_t xw[XU][2];
+        float4 xr[XU][2];
+        float4 gr[2];
+    };
+    // one step's bf16 planes in registers (split under the MFMAs of the step before)
+    struct Planes {
+        u32x4 x[XU][3];
+        u32x4 g[3];
+        uint2 g4[3];
+    };
+    Raw raw[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {  // defined values: the last step splits a set it never stores
+#pragma unroll
+        for (int i = 0; i < XU; ++i) {
+            raw[t].xw[i][0] = raw[t].xw[i][1] = 0u;
+            raw[t].xr[i][0] = raw[t].xr[i][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        raw[t].gr[0] = raw[t].gr[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     float bsum[GW];
 #pragma unroll
     for (int e = 0; e < GW; ++e) bsum[e] = 0.f;
@@ -1568,9 +1605,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     // byte (u8) / float offset of sample n: through the rollout rows when a.idx is set (u8
     // only); the next sample's base is fetched one wrap ahead, so the idx load's latency
     // hides under the steps in between
-    const bool rows = U8 && a.idx != nullptr;
     auto sbase = [&](unsigned n) -> unsigned long long {
-        if (rows) {
+        if constexpr (ROWS) {
             const unsigned nc = n < (unsigned)a.batch ? n : (unsigned)a.batch - 1;
             const long long i = a.idx[nc];
             return (unsigned long long)(((i % a.T) * a.Nenv + i / a.T) * (long long)(L::CIN * L::IH * L::IW));
@@ -1586,8 +1622,10 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         sb = sbase(ncur);
         sbn = sbase(ncur + 1);
     }
-    const unsigned xp0 = mbeg - (mbeg / L::P) * L::P;  // a pixel that always exists
-    const unsigned long long sb00 = sbase(mbeg / L::P);
+    // a pixel that always exists (an empty split, mbeg == M, still issues its loads)
+    const unsigned m0 = mbeg < M ? mbeg : M - 1;
+    const unsigned xp0 = m0 - (m0 / L::P) * L::P;
+    const unsigned long long sb00 = sbase(m0 / L::P);
     int koff[XU];
 #pragma unroll
     for (int i = 0; i < XU; ++i) {
@@ -1600,10 +1638,12 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         }
     }
 
-    // loads of the next step (steps are loaded in order; the state above advances)
-    auto load = [&](auto full_tag) {
-        constexpr bool FULL = decltype(full_tag)::value;
-        const bool ok = FULL || mcur < mend;
+    // loads of one step (steps are loaded in order; the state above advances).  Branch-free,
+    // so the loads, the split of the step before and the MFMAs share one basic block: a pixel
+    // past the split's end loads a valid pixel's X (finite) and a zero G row (kZeroG), so its
+    // products vanish
+    auto load = [&](Raw& r) {
+        const bool ok = mcur < mend;
         const unsigned p = ok ? xp : xp0;
         const unsigned long long s0 = ok ? sb : sb00;
         const unsigned oy = p / L::OW, ox = p - oy * L::OW;
@@ -1611,91 +1651,78 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
             const uint8_t* s = xu8 + s0 + oy * L::S * L::IW + ox * L::S;
 #pragma unroll
             for (int i = 0; i < XU; ++i) {
-                const uint32_t v0 = *reinterpret_cast<const uint32_t*>(s + koff[i]);
-                const uint32_t v1 = *reinterpret_cast<const uint32_t*>(s + koff[i] + 4);
-                xw[i][0] = ok ? v0 : 0u;
-                xw[i][1] = ok ? v1 : 0u;
+                r.xw[i][0] = *reinterpret_cast<const uint32_t*>(s + koff[i]);
+                r.xw[i][1] = *reinterpret_cast<const uint32_t*>(s + koff[i] + 4);
             }
         } else {
             const float* s = xf + s0 + (oy * L::S * L::IW + ox * L::S) * L::CIN;
-            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int i = 0; i < XU; ++i) {
-                const float4 v0 = *reinterpret_cast<const float4*>(s + koff[i]);
-                const float4 v1 = *reinterpret_cast<const float4*>(s + koff[i] + 4);
-                xr[i][0] = ok ? v0 : z;
-                xr[i][1] = ok ? v1 : z;
+                r.xr[i][0] = *reinterpret_cast<const float4*>(s + koff[i]);
+                r.xr[i][1] = *reinterpret_cast<const float4*>(s + koff[i] + 4);
             }
         }
-        {
-            const float* sg = a.g + (unsigned long long)(ok ? mcur : mbeg) * COUT + gco;
-            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 g0 = *reinterpret_cast<const float4*>(sg);
-            gr[0] = ok ? g0 : z;
-            if constexpr (GW == 8) {
-                const float4 g1 = *reinterpret_cast<const float4*>(sg + 4);
-                gr[1] = ok ? g1 : z;
-            }
-        }
+        const float* sg = ok ? a.g + (unsigned long long)mcur * GS + cb * COUT + gco : kZeroG + gco;
+        r.gr[0] = *reinterpret_cast<const float4*>(sg);
+        if constexpr (GW == 8) r.gr[1] = *reinterpret_cast<const float4*>(sg + 4);
         mcur += MS;
+        if constexpr (L::P == 1) {  // one pixel per sample (the fc layer): sample = pixel
+            sb = (unsigned long long)mcur * sstride;
+            return;
+        }
         xp += MS;
-        if (xp >= (unsigned)L::P) {
-            xp -= L::P;
-            if (rows) {
+        const bool wrap = xp >= (unsigned)L::P;
+        xp = wrap ? xp - L::P : xp;
+        if constexpr (ROWS) {
+            if (wrap) {  // rollout rows: the next sample's base was fetched one wrap ahead
                 ++ncur;
                 sb = sbn;
                 sbn = sbase(ncur + 1);
-            } else {
-                sb += sstride;
             }
+        } else {
+            sb = wrap ? sb + sstride : sb;
         }
     };
-    auto load_step = [&](unsigned ms) {
-        if (ms + MS <= mend)
-            load(std::true_type{});
+    auto to_planes = [&](const Raw& r, Planes& p) {
+#pragma unroll
+        for (int i = 0; i < XU; ++i) {
+            if constexpr (U8)
+                p.x[i][0] = u8x8_to_bf16(r.xw[i][0], r.xw[i][1]);
+            else
+                split8(r.xr[i][0], r.xr[i][1], p.x[i][0], p.x[i][1], p.x[i][2]);
+        }
+        if constexpr (GW == 8)
+            split8(r.gr[0], r.gr[1], p.g[0], p.g[1], p.g[2]);
         else
-            load(std::false_type{});
+            split4(r.gr[0], p.g4[0], p.g4[1], p.g4[2]);
     };
-    auto store = [&](int buf) {
+    auto store = [&](const Planes& p, const Raw& r, int buf) {
         uint8_t* base = lds + buf * C::STAGE;
 #pragma unroll
         for (int i = 0; i < XU; ++i) {
             const int j = 8 * i + ju;
             const int off = pxl * XR + (((j >> 1) ^ tr_swz<XR>(pxl)) << 5) + ((j & 1) << 4);
-            if constexpr (U8) {
-                *reinterpret_cast<u32x4*>(base + off) = u8x8_to_bf16(xw[i][0], xw[i][1]);
-            } else {
-                u32x4 p0, p1, p2;
-                split8(xr[i][0], xr[i][1], p0, p1, p2);
-                *reinterpret_cast<u32x4*>(base + off) = p0;
-                *reinterpret_cast<u32x4*>(base + C::XPB + off) = p1;
-                *reinterpret_cast<u32x4*>(base + 2 * C::XPB + off) = p2;
-            }
+#pragma unroll
+            for (int q = 0; q < XP; ++q) *reinterpret_cast<u32x4*>(base + q * C::XPB + off) = p.x[i][q];
         }
         uint8_t* gb = base + XP * C::XPB;
         const int goff = pxl * GR + (((gco >> 4) ^ tr_swz<GR>(pxl)) << 5) + (gco & 15) * 2;
-        if constexpr (GW == 8) {
-            u32x4 p0, p1, p2;
-            split8(gr[0], gr[1], p0, p1, p2);
-            *reinterpret_cast<u32x4*>(gb + goff) = p0;
-            *reinterpret_cast<u32x4*>(gb + C::GPB + goff) = p1;
-            *reinterpret_cast<u32x4*>(gb + 2 * C::GPB + goff) = p2;
-        } else {
-            uint2 p0, p1, p2;
-            split4(gr[0], p0, p1, p2);
-            *reinterpret_cast<uint2*>(gb + goff) = p0;
-            *reinterpret_cast<uint2*>(gb + C::GPB + goff) = p1;
-            *reinterpret_cast<uint2*>(gb + 2 * C::GPB + goff) = p2;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            if constexpr (GW == 8)
+                *reinterpret_cast<u32x4*>(gb + q * C::GPB + goff) = p.g[q];
+            else
+                *reinterpret_cast<uint2*>(gb + q * C::GPB + goff) = p.g4[q];
         }
-        bsum[0] += gr[0].x;
-        bsum[1] += gr[0].y;
-        bsum[2] += gr[0].z;
-        bsum[3] += gr[0].w;
+        bsum[0] += r.gr[0].x;
+        bsum[1] += r.gr[0].y;
+        bsum[2] += r.gr[0].z;
+        bsum[3] += r.gr[0].w;
         if constexpr (GW == 8) {
-            bsum[4] += gr[1].x;
-            bsum[5] += gr[1].y;
-            bsum[6] += gr[1].z;
-            bsum[7] += gr[1].w;
+            bsum[4] += r.gr[1].x;
+            bsum[5] += r.gr[1].y;
+            bsum[6] += r.gr[1].z;
+            bsum[7] += r.gr[1].w;
         }
     };
     // per-lane transposed-read offsets (T10): lane 4qq+pp of each 16-lane group supplies
@@ -1744,20 +1771,37 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         }
     };
 
+    // two-deep pipeline, one basic block per step: step s+1's raw registers (loaded during
+    // step s-1) are split into planes, step s+2's loads are issued into the set just freed,
+    // the compiler interleaves the split's VALU work with step s's fragment reads and MFMAs,
+    // and the planes go to the other LDS buffer after them.  Raw sets and buffers alternate,
+    // so both are static.  (Measured: 5-10 % faster than one-deep staging after the MFMAs;
+    // forcing the interleave with sched_group_barrier was slower than the compiler's.)
     const unsigned nsteps = mend > mbeg ? (mend - mbeg + MS - 1) / MS : 0;
+    load(raw[0]);
+    load(raw[1]);
     if (nsteps > 0) {
-        load_step(mbeg);
-        store(0);
+        Planes p;
+        to_planes(raw[0], p);
+        store(p, raw[0], 0);
     }
     __syncthreads();
-    for (unsigned s = 0; s < nsteps; ++s) {
-        const int cur = (int)(s & 1);
-        if (s + 1 < nsteps) load_step(mbeg + (s + 1) * MS);
-        compute(cur);
-        if (s + 1 < nsteps) store(cur ^ 1);
+    auto step = [&](unsigned s, auto cur_tag) {
+        constexpr int CUR = decltype(cur_tag)::value;  // LDS buffer and raw set of step s
+        Planes p;
+        to_planes(raw[CUR ^ 1], p);
+        load(raw[CUR]);
+        compute(CUR);
+        // unconditional (one basic block): past the last step the set holds a zero-G step,
+        // written to a buffer nothing reads again (bsum adds zeros)
+        store(p, raw[CUR ^ 1], CUR ^ 1);
         __syncthreads();
+    };
+    for (unsigned s = 0; s < nsteps; s += 2) {
+        step(s, std::integral_constant<int, 0>{});
+        if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>{});
     }
-    float* slab = a.slab + (long long)split * L::K * COUT;
+    float* slab = a.slab + (long long)split * L::K * GS + cb * COUT;
 #pragma unroll
     for (int i = 0; i < WKT; ++i)
 #pragma unroll
@@ -1765,9 +1809,9 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int kr = kb * KT + (kt0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                slab[kr * COUT + (ct0 + j) * 32 + (lane & 31)] = hi[i][j][r] + lo[i][j][r];
+                slab[kr * GS + (ct0 + j) * 32 + (lane & 31)] = hi[i][j][r] + lo[i][j][r];
             }
-    if (kb == 0) {
+    if (CB == 1 && kb == 0) {
         // bias grad partial: column sums of this split's G rows, combined in a fixed order
         float* bred = reinterpret_cast<float*>(lds);  // the loop ended on a barrier
 #pragma unroll
@@ -1915,7 +1959,10 @@ struct WsLaunch {
         WArgs wa{x, sample_stride, g, slab, slab + (long long)sp * L::K * L::COUT, batch, 0, sp, idx, T, Nenv};
         const long long M = batch * L::P;
         wa.px_per_split = ppox::ceil_div(ppox::ceil_div(M, sp), MS) * MS;
-        wgrad_split_kernel<L, U8, KT><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
+        if (U8 && idx != nullptr)
+            wgrad_split_kernel<L, U8, KT, U8><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
+        else
+            wgrad_split_kernel<L, U8, KT, false><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
         PPOX_LAUNCHED_NORET("ppox_nature_conv_wgrad_split");
         return launch_wgrad_reduce<L, !U8>(slab, wa.bslab, sp, dw, db, s);
     }
@@ -2223,6 +2270,73 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
 }
 
 // ---- NatureCNN fc layer (3136 -> 512) on the split-bf16 GEMM ----------------------
+// Weight gradient dW = df^T h3 on the split wgrad kernel: "pixels" = samples (GFc has one
+// output pixel), K = the 512 outputs (X = df rows), G = the NHWC conv3 activations in 49
+// blocks of 64 channels (one spatial position each, NHWC feature order f = p * 64 + c).
+// Split-K partial slabs [split][512][3136] are summed in a fixed order by fc_wgrad_reduce,
+// which writes dW in the Flatten order of the fc weight.
+using GFc = Geo<512, 1, 1, 1, 1, 1, 64>;
+constexpr int FCW_KT = 128, FCW_CB = 49;
+struct FcWgrad {
+    using C = WsCfg<GFc, false, FCW_KT>;
+    static constexpr long long TILES = (long long)C::KB * FCW_CB;
+    static constexpr long long SLAB = (long long)GFc::K * FCW_CB * GFc::COUT;  // floats per split
+    // the split count whose (rounds of 512 workgroup slots) x (steps per split + 3 of fixed
+    // prologue / epilogue cost) is least: 13 at B = 16384 (4.98 rounds), 5 at B = 2048
+    static int splits(long long batch) {
+        int best = 1;
+        long long best_cost = -1;
+        for (int sp = 1; sp <= 16; ++sp) {
+            const long long steps = ppox::ceil_div(ppox::ceil_div(batch, (long long)sp), (long long)MS);
+            if (sp > 1 && steps < 2) break;
+            const long long cost = ppox::ceil_div(TILES * sp, 512LL) * (steps + 3);
+            if (best_cost < 0 || cost < best_cost) {
+                best_cost = cost;
+                best = sp;
+            }
+        }
+        return best;
+    }
+    static long long workspace_bytes(long long batch) { return splits(batch) * SLAB * (long long)sizeof(float); }
+};
+
+__global__ void __launch_bounds__(256) fc_wgrad_reduce(const float* __restrict__ slab, int splits,
+                                                       float* __restrict__ dw) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;  // slab element (o, NHWC feature)
+    if (i >= FcWgrad::SLAB) return;
+    float t = 0.f;
+    for (int sp = 0; sp < splits; ++sp) t += slab[sp * FcWgrad::SLAB + i];
+    const int o = (int)(i / 3136), f = (int)(i - (long long)o * 3136);
+    dw[(long long)o * 3136 + fc_nchw_feature(f)] = t;
+}
+
+extern "C" int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch) {
+    return batch <= 0 ? 0 : FcWgrad::workspace_bytes(batch);
+}
+
+extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float* h3, void* workspace,
+                                    int64_t workspace_bytes, float* dw, void* stream) {
+    PPOX_REQUIRE(dw && batch >= 0, "ppox_nature_fc_wgrad: bad arguments");
+    hipStream_t s = ppox::as_stream(stream);
+    if (batch == 0) {  // no rows: a zero gradient
+        PPOX_REQUIRE(hipMemsetAsync(dw, 0, sizeof(float) * FcWgrad::SLAB, s) == hipSuccess,
+                     "ppox_nature_fc_wgrad: memset failed");
+        return PPOX_OK;
+    }
+    PPOX_REQUIRE(df && h3 && workspace, "ppox_nature_fc_wgrad: bad arguments");
+    PPOX_REQUIRE(workspace_bytes >= FcWgrad::workspace_bytes(batch), "ppox_nature_fc_wgrad: workspace too small");
+    PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(h3), "ppox_nature_fc_wgrad: 16B alignment");
+    PPOX_REQUIRE(batch < (1LL << 31) / 64, "ppox_nature_fc_wgrad: batch too large for 32-bit row indexing");
+    const int sp = FcWgrad::splits(batch);
+    float* slab = reinterpret_cast<float*>(workspace);
+    WArgs wa{df, 0, h3, slab, nullptr, batch, 0, sp, nullptr, 0, 0};
+    wa.px_per_split = ppox::ceil_div(ppox::ceil_div((long long)batch, (long long)sp), (long long)MS) * MS;
+    wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB><<<(unsigned)(FcWgrad::TILES * sp), 256, 0, s>>>(wa);
+    PPOX_LAUNCHED_NORET("ppox_nature_fc_wgrad");
+    fc_wgrad_reduce<<<(unsigned)ppox::ceil_div(FcWgrad::SLAB, 256LL), 256, 0, s>>>(slab, sp, dw);
+    PPOX_LAUNCHED("ppox_nature_fc_wgrad");
+}
+
 extern "C" int64_t ppox_nature_fc_pack_elems(void) { return 3LL * FcFwd::NCB * FcFwd::K * FcFwd::NOUT; }
 
 extern "C" int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_dgrad, void* stream) {

@@ -148,6 +148,14 @@ class CnnActorCritic(nn.Module):
             self._fcg = buf
         return buf
 
+    def _fc_wgrad_ws(self, rows):
+        need = native.nature_fc_wgrad_workspace_bytes(rows)
+        ws = getattr(self, "_fcw_ws", None)
+        if ws is None or ws.numel() < need or ws.device != self.actor[0].weight.device:
+            ws = torch.empty(max(need, 1), dtype=torch.uint8, device=self.actor[0].weight.device)
+            self._fcw_ws = ws
+        return ws
+
     def _head_ws(self, rows, h, n_actions):
         need = native.head_grads_workspace_bytes(rows, h, n_actions, self.intrinsic)
         ws = getattr(self, "_hg_ws", None)
@@ -180,7 +188,10 @@ class CnnActorCritic(nn.Module):
                 des.append((de, d))
             native.relu_backward_(df, f)
             cv = self.conv_impl
-            if cv.nhwc3:  # NHWC features (split math): dW in NHWC order, permuted back to Flatten order
+            import convs as _convs
+            if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-bf16 kernel, Flatten-order dW
+                native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad)
+            elif cv.nhwc3:  # NHWC features: library GEMM in NHWC order, permuted back to Flatten order
                 dwp = self._fc_grad_buf(fc.weight)
                 torch.mm(df.t(), hf, out=dwp)
                 fc.weight.grad.view(fc.weight.shape[0], 64, 49).copy_(dwp.view(-1, 49, 64).transpose(1, 2))
@@ -198,7 +209,6 @@ class CnnActorCritic(nn.Module):
             if dense_ready is not None:
                 dense_ready()
             fe = self.feature_extractor
-            import convs as _convs
             if cv.nhwc3 and B < _convs.FC_DGRAD_FUSED_MAX_BATCH:  # masked NHWC grad directly
                 dh3, g3 = None, cv.fc_dgrad_g3(df, h3)
             elif cv.nhwc3:  # library GEMM on the permuted weight: NHWC order, then the ReLU mask

@@ -9,7 +9,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libppox.so")
+# PPOX_LIB: an A/B build of the same sources (tools/build_variant.sh) for kernel tests/timing
+LIB_PATH = os.environ.get("PPOX_LIB") or os.path.join(_HERE, "libppox.so")
 
 _vp, _i64, _i32, _f64, _f32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, ctypes.c_float
 _u64 = ctypes.c_uint64
@@ -67,6 +68,7 @@ SIGNATURES = {
     "ppox_nature_pack_all": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp],
+    "ppox_nature_fc_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp],
     "ppox_es_noise": [_i64, _i64, _i64, _i64, _u64, _vp, _vp],
     "ppox_es_env_noise": [_i32, _i32, _u64, _vp, _vp],
     "ppox_es_evaluate": [_vp, _vp, _f64, _i64, _i32, _i32, _i32, _i32, _i32, _u64, _vp, _vp, _vp, _vp],
@@ -85,12 +87,14 @@ _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p
              "ppox_nature_wgrad_workspace_bytes": ctypes.c_int64, "ppox_nature_split_pack_elems": ctypes.c_int64,
              "ppox_nature_wgrad_split_workspace_bytes": ctypes.c_int64,
              "ppox_es_update_workspace_bytes": ctypes.c_int64,
-             "ppox_nature_fc_pack_elems": ctypes.c_int64, "ppox_head_grads_workspace_bytes": ctypes.c_int64}
+             "ppox_nature_fc_pack_elems": ctypes.c_int64, "ppox_head_grads_workspace_bytes": ctypes.c_int64,
+             "ppox_nature_fc_wgrad_workspace_bytes": ctypes.c_int64}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
                  "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32],
                  "ppox_nature_wgrad_split_workspace_bytes": [_i32, _i64],
                  "ppox_es_update_workspace_bytes": [_i64, _i64],
-                 "ppox_nature_fc_pack_elems": [], "ppox_head_grads_workspace_bytes": [_i64, _i64, _i64, _i32]}
+                 "ppox_nature_fc_pack_elems": [], "ppox_head_grads_workspace_bytes": [_i64, _i64, _i64, _i32],
+                 "ppox_nature_fc_wgrad_workspace_bytes": [_i64]}
 
 _lib = None
 
@@ -464,6 +468,16 @@ def nature_fc_fwd(h3, batch, q_fwd, bias, f, stream=None):
 def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, stream=None):
     """g3 (batch, 7, 7, 64) NHWC = ((df @ W) in Flatten order) * (h3 > 0)."""
     call("ppox_nature_fc_dgrad", _p(df), int(batch), _p(q_dgrad), _p(h3), _p(g3), stream_ptr(stream))
+
+
+def nature_fc_wgrad_workspace_bytes(batch):
+    return int(lib().ppox_nature_fc_wgrad_workspace_bytes(int(batch)))
+
+
+def nature_fc_wgrad(df, batch, h3, workspace, dw, stream=None):
+    """dw (512, 3136) in the fc weight's Flatten order = df^T @ h3 (h3 NHWC (batch, 7, 7, 64))."""
+    call("ppox_nature_fc_wgrad", _p(df), int(batch), _p(h3), _p(workspace), workspace.numel() * workspace.element_size(),
+         _p(dw), stream_ptr(stream))
 
 
 # ES-NSRA (csrc/es.hip)

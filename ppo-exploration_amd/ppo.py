@@ -33,6 +33,7 @@ import convs
 from buffer import IntrinsicStorage, RolloutStorage
 from dist import DistContext, owned_minibatch_indices, owned_minibatch_positions, shard_range
 from env import make_env
+from phases import traced
 from models import CnnActorCritic, FlatParams, IntrinsicCuriosityModule, MlpNetwork, RndNetwork
 from util import ActionConverter, RunningMeanStd
 
@@ -295,6 +296,7 @@ class BaseAlgorithm:
                                  ro.log_probs[t])
         self._sample_counter += 1
 
+    @traced("episodes")
     def _finish_episodes(self):
         """Episode bookkeeping of one rollout over ALL envs (ppo.py:180-183, 98-109): every rank
         gathers the (T, N_global) episode returns / lengths, so num_episodes, ep_info_buffer and
@@ -424,6 +426,7 @@ class PPO(BaseAlgorithm):
         self._alloc_train_state()
         self.last_obs = None
 
+    @traced("collect")
     def collect_samples(self):
         ro = self.rollout
         self._ensure_started()
@@ -466,6 +469,7 @@ class PPO(BaseAlgorithm):
             self._bwd_train(ctx, out, v, None, dout, dv, extra=extra_backward)
         self.dist.all_reduce_(self.flat.grad)
 
+    @traced("train")
     def train(self):
         ro = self.rollout
         total = self.nstep * self.num_envs
@@ -517,6 +521,7 @@ class PPO_RND(BaseAlgorithm):
             return obs[:, 3].reshape(obs.shape[0], -1)
         return obs.reshape(obs.shape[0], -1)
 
+    @traced("collect")
     def collect_samples(self):
         ro = self.rollout
         self._ensure_started()
@@ -579,6 +584,7 @@ class PPO_RND(BaseAlgorithm):
         self.dist.all_reduce_(self.rnd_flat.grad)
         self.rnd_flat.adam_step(self.int_lr, self.max_grad_norm)
 
+    @traced("train")
     def train(self):
         ro = self.rollout
         total = self.nstep * self.num_envs
@@ -648,6 +654,7 @@ class PPO_ICM(BaseAlgorithm):
             return native.u8_to_f32(x)
         return x.float()
 
+    @traced("collect")
     def collect_samples(self):
         ro = self.rollout
         self._ensure_started()
@@ -677,6 +684,7 @@ class PPO_ICM(BaseAlgorithm):
         self._finish_episodes()
         return True
 
+    @traced("train")
     def train(self):
         ro = self.rollout
         total = self.nstep * self.num_envs

@@ -782,6 +782,38 @@ def test_fc_split_gemm_vs_fp64(B):
     assert e_s <= 2 * e_f + 1e-7, (float(e_s), float(e_f))
 
 
+@pytest.mark.parametrize("B", [1, 33, 1000, 2048, 5000])
+def test_fc_wgrad_split_vs_fp64(B):
+    """fc weight gradient on the split wgrad kernel (ppox_nature_fc_wgrad: h3 NHWC, dW in the
+    weight's Flatten order) vs float64: error no larger than torch's f32 GEMM's (x2 headroom);
+    ragged batches (partial 32-row steps, empty splits), and bitwise run-to-run determinism."""
+    import native
+    torch.manual_seed(B + 7)
+    h3n = torch.relu(torch.randn(B, 7, 7, 64, device="cuda"))
+    h3 = h3n.permute(0, 3, 1, 2).reshape(B, 3136)
+    df = torch.randn(B, 512, device="cuda") * (torch.rand(B, 512, device="cuda") > 0.3)
+    ws = torch.empty(native.nature_fc_wgrad_workspace_bytes(B), dtype=torch.uint8, device="cuda")
+    dw = torch.full((512, 3136), float("nan"), device="cuda")
+    native.nature_fc_wgrad(df, B, h3n, ws, dw)
+    ref = df.double().t() @ h3.double()
+    scale = ref.abs().max()
+    e_s = (dw.double() - ref).abs().max() / scale
+    e_f = ((df.t() @ h3).double() - ref).abs().max() / scale
+    assert torch.isfinite(dw).all()
+    assert e_s <= 2 * e_f + 1e-7, (float(e_s), float(e_f))
+    dw2 = torch.empty_like(dw)
+    native.nature_fc_wgrad(df, B, h3n, ws, dw2)
+    assert torch.equal(dw, dw2)
+
+
+def test_fc_wgrad_zero_rows_writes_zero():
+    import native
+    dw = torch.full((512, 3136), 1.0, device="cuda")
+    native.nature_fc_wgrad(torch.empty(0, 512, device="cuda"), 0, torch.empty(0, 7, 7, 64, device="cuda"),
+                           torch.empty(1, dtype=torch.uint8, device="cuda"), dw)
+    assert not dw.any()
+
+
 def test_stream_ptr_is_torch_current_stream():
     """native.stream_ptr() (raw-stream accessor) == torch.cuda.current_stream().cuda_stream,
     on the default stream and inside a side-stream context."""

@@ -45,6 +45,10 @@ def main():
     res["rocblas_fwd_ms"] = t_ms(lambda: torch.relu(torch.addmm(b, h3, W.t())))
     res["split_dgrad_ms"] = t_ms(lambda: native.nature_fc_dgrad(df, B, qd, h3n, g3))
     res["rocblas_dgrad_ms"] = t_ms(lambda: torch.mm(df, W))
+    ws = torch.empty(native.nature_fc_wgrad_workspace_bytes(B), dtype=torch.uint8, device=d)
+    dw = torch.empty(512, 3136, device=d)
+    res["split_wgrad_ms"] = t_ms(lambda: native.nature_fc_wgrad(df, B, h3n, ws, dw))
+    res["rocblas_wgrad_ms"] = t_ms(lambda: torch.mm(df.t(), h3))
     for k in list(res):
         if k.endswith("_ms"):
             res[k.replace("_ms", "_TFs")] = round(flop / (res[k] * 1e-3) / 1e12, 1)
