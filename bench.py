@@ -45,14 +45,14 @@ ACT_B = {0: 28224, 1: 20 * 20 * 32 * 4, 2: 9 * 9 * 64 * 4, 3: 7 * 7 * 64 * 4}
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 # rocprofv3 kernel names of the conv entry points (for the PMC traffic lookup)
 CONV_KERNEL = {("fwd", 1, True): "fwd1_split_kernel<1>",
-               ("fwd", 2, True): "igemm_split_kernel<FwdNHWCProblem<32, 20, 20, 4, 4, 2, 64, false, 1>>",
-               ("fwd", 3, True): "igemm_split_kernel<FwdNHWCProblem<64, 9, 9, 3, 3, 1, 64, true, 1>>",
+               ("fwd", 2, True): "sgemm_kernel<SgFwd<32, 20, 20, 4, 4, 2, 64, false>, 4, 2>",
+               ("fwd", 3, True): "sgemm_kernel<SgFwd<64, 9, 9, 3, 3, 1, 64, false>, 4, 2>",
                ("dgrad", 2, False): "igemm_kernel<DgradPMProblem<32, 20, 20, 4, 4, 2, 64, 1>>",
                ("dgrad", 2, True): "dgrad2_col_kernel",
-               ("dgrad", 3, True): "igemm_split_kernel<DgradPMProblem<64, 9, 9, 3, 3, 1, 64, 1>>",
-               ("wgrad", 1, True): "wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256>",
-               ("wgrad", 2, True): "wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128>",
-               ("wgrad", 3, True): "wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64>"}
+               ("dgrad", 3, True): "sgemm_kernel<SgDgradPM<64, 9, 9, 3, 3, 1, 64>, 4, 2>",
+               ("wgrad", 1, True): "wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>",
+               ("wgrad", 2, True): "wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128, false, 1>",
+               ("wgrad", 3, True): "wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64, false, 1>"}
 
 
 def conv_roofline(key, kt, totals):

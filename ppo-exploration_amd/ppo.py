@@ -306,10 +306,15 @@ class BaseAlgorithm:
         ret = self.dist.all_gather_cat(ro.done_ret, dim=1)
         ln = self.dist.all_gather_cat(ro.done_len, dim=1)
         fin = ~torch.isnan(ret)
-        n_fin = int(fin.sum().item())
+        r_fin, l_fin = ret[fin], ln[fin]
+        n_fin = r_fin.numel()
         self.num_episodes += n_fin
-        if n_fin:
-            for x, y in zip(ret[fin].cpu().numpy(), ln[fin].cpu().numpy()):
+        # the buffer keeps its last maxlen entries: appending only the last maxlen finished
+        # episodes leaves it exactly as appending all of them (thousands per rollout at 4096
+        # envs: the per-episode host loop cost ~47 ms per iteration with the GPU idle)
+        k = min(n_fin, self.ep_info_buffer.maxlen)
+        if k:
+            for x, y in zip(r_fin[-k:].cpu().numpy(), l_fin[-k:].cpu().numpy()):
                 self.ep_info_buffer.append({"r": float(x), "l": int(y)})
 
     def _batch(self, total):
