@@ -598,7 +598,7 @@ struct GemmRowsProblem {
 };
 
 #ifndef FC_FWD_G
-#define FC_FWD_G 2  // fc forward: column blocks per tile group (SgRows)
+#define FC_FWD_G 8  // fc forward: column blocks per tile group (SgRows): all 8, each h3 row tile read once
 #endif
 #ifndef FC_DGRAD_G
 #define FC_DGRAD_G 12  // fc dgrad: column blocks per tile group
@@ -642,76 +642,101 @@ __global__ void pack_split_gemm_rows(const float* __restrict__ w, uint16_t* __re
 // once, split once into its three bf16 planes and kept in registers for all 512
 // columns — 16x the MFMA work per A byte of the position-major form, whose
 // 32-column tiles re-gathered each G row for every one of its 16 input pixels.
-// A workgroup (8 waves, 32 rows each) owns 3 whole samples (243 of its 256 rows),
-// so the col2im overlap stays inside it: four passes, one per input-pixel parity
-// class (py, px), each computing the class's four taps (ky in {py, py+2}, kx in
-// {px, px+2}) and adding them, in the fixed tap order, into an LDS image of the
-// class's 10x10 pixels (tap (ky, kx) sends row (oy, ox) to class pixel
-// (oy + ky/2, ox + kx/2)).  The class image is then masked with the ReLU of the
-// layer below and written NHWC.  B (the class's four taps, split-packed as the
-// position-major dgrad form: ppox_nature_pack_split which = 12) is staged in LDS,
-// double-buffered across passes.  Deterministic: a fixed sum order per output.
+// A triple (3 whole samples, 243 rows on 8 waves x 32) keeps the col2im overlap inside
+// one workgroup: four passes, one per input-pixel parity class (py, px), each computing
+// the class's four taps (ky in {py, py+2}, kx in {px, px+2}) and adding them, in the
+// fixed tap order, into an LDS image of the class's 10x10 pixels (tap (ky, kx) sends
+// row (oy, ox) to class pixel (oy + ky/2, ox + kx/2)).  The class image is then masked
+// with the ReLU of the layer below and written NHWC.  B = the taps' split planes
+// (position-major dgrad packing: ppox_nature_pack_split which = 12).  Deterministic: a
+// fixed sum order per output.
+//
+// Persistent: one 512-thread workgroup per CU walks the triples t = blockIdx.x,
+// + gridDim.x, ... so nothing is exposed at a triple's start:
+//   * B lives in a 4-slot tap ring (tap k in slot k & 3, 12 KB each) refilled two taps at
+//     a time at odd steps (taps k+3, k+4 by LDS-DMA), waited one step later;
+//   * the NEXT triple's G rows are DMA'd into LDS (64 KB, 16-B chunks XOR-swizzled by row
+//     so the boundary's b128 reads are conflict-free) during the current triple and split
+//     into the A registers at the boundary;
+//   * each class's ReLU-mask operands are loaded a class ahead (at the previous class's
+//     output step), and the output stores are unconditional (threads with nothing to store
+//     write a dummy), so every wave's vmcnt sequence is static and the waits are counted.
+// LDS: 48 KB ring + 64 KB next rows + 37.5 KB class image = 150 KB (one workgroup per CU).
+// (0.645 vs 0.695 ms for the one-triple-per-workgroup form at B = 16384, same box.)
 // ---------------------------------------------------------------------------
 constexpr int C2S = 3, C2ROWS = C2S * 81, C2PIX = 100;
-constexpr int C2BQ = 4 * 4 * 3 * 64;  // u32x4 per pass: 4 taps x 4 k-steps x 3 planes x 64 lanes
-constexpr int C2BV = C2BQ / 512;
 constexpr int C2OV = (C2S * C2PIX * 8 + 511) / 512;  // float4 outputs per thread per pass
 
 // workgroup barrier that waits only for this wave's LDS operations: global loads and
 // stores stay in flight across it (__syncthreads also drains vmcnt, which would expose
-// every output store and prefetch of dgrad2_col_kernel at each of its col2im steps)
+// every output store and prefetch at each col2im step)
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__global__ void __launch_bounds__(512, 1) dgrad2_col_kernel(Args a, const u32x4* __restrict__ wq) {
-    using L = G2;
-    static_assert(L::COUT == 64 && L::CIN == 32 && L::OH == 9 && L::IH == 20 && L::S == 2 && L::KH == 4,
-                  "dgrad2_col_kernel is written for NatureCNN conv2");
-    // all LDS in ONE __shared__ object (a second one can make hipcc wait vmcnt(0) before
-    // the first ds_read of each MFMA phase): B double buffer, then the class image + dummy slot
-    __shared__ u32x4 lds[2 * C2BQ + (C2S * C2PIX * 32 + 32) / 4];
-    u32x4(*Bs)[C2BQ] = reinterpret_cast<u32x4(*)[C2BQ]>(lds);
-    float* Ds = reinterpret_cast<float*>(lds + 2 * C2BQ);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const long long n0 = (long long)blockIdx.x * C2S;
-    const long long rows_total = a.batch * L::P;
+constexpr int C2P_TAP = 4 * 3 * 64;                    // u32x4 per tap: 4 k-steps x 3 planes x 64 lanes
+constexpr int C2P_AN = 256 * 16;                       // u32x4: 256 G rows x 64 f32
+constexpr int C2P_IMG = (C2S * C2PIX * 32 + 32) / 4;   // u32x4: class image + dummy slot
+__device__ float4 kC2Dummy[512];                       // store target of threads with nothing to store
 
-    // a class's B (its four taps' 12 KB split chunks) global -> LDS by LDS-DMA (no VGPRs;
-    // LDS destination = wave-uniform base + lane x 16 B, so each wave fills 1 KB runs)
-    auto loadB = [&](int pass, int buf) {
-        const int py = pass >> 1, px = pass & 1;
+__device__ inline int c2_nat_tap(int k) {  // class tap k (0..15) -> natural tap ky * 4 + kx
+    k &= 15;
+    const int cls = k >> 2, i = k & 3;
+    return ((cls >> 1) + 2 * (i >> 1)) * G2::KW + (cls & 1) + 2 * (i & 1);
+}
+
+__global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4* __restrict__ wq,
+                                                            long long ntriples) {
+    using L = G2;
+    __shared__ u32x4 lds[4 * C2P_TAP + C2P_AN + C2P_IMG];
+    u32x4* Bring = lds;
+    u32x4* An = lds + 4 * C2P_TAP;
+    float* Ds = reinterpret_cast<float*>(lds + 4 * C2P_TAP + C2P_AN);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const long long rows_total = a.batch * L::P;
+    const float* g2 = reinterpret_cast<const float*>(a.x);
+
+    // taps k, k+1 (class-tap indices, mod 16) -> ring slots: 3 DMAs per thread
+    auto dmaB2 = [&](int k) {
 #pragma unroll
-        for (int j = 0; j < C2BV; ++j) {
-            const int e = j * 512 + tid, i = e / 768, within = e - i * 768;
-            const int tap = (py + 2 * (i >> 1)) * L::KW + px + 2 * (i & 1);
+        for (int r = 0; r < 3; ++r) {
+            const int e0 = r * 512 + wave * 64, which = e0 / C2P_TAP, within0 = e0 - which * C2P_TAP;
+            const int kk = (k + which) & 15;
             __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(wq + tap * 768 + within),
-                (__attribute__((address_space(3))) void*)(Bs[buf] + j * 512 + wave * 64), 16, 0, 0);
+                (const __attribute__((address_space(1))) void*)(wq + c2_nat_tap(kk) * C2P_TAP + within0 + lane),
+                (__attribute__((address_space(3))) void*)(Bring + (kk & 3) * C2P_TAP + within0), 16, 0, 0);
         }
     };
-    loadB(0, 0);
-    loadB(1, 1);
-    // A: this lane's row, k = 16q + 8h .. +8 for the four k-steps q
+    // triple t's 256 G rows (rows past the batch clamped; rows 243.. are never stored) ->
+    // An, row r's 16-B chunk c at position c ^ (r & 15): 8 DMAs per thread
+    auto dmaA = [&](long long t) {
+        const long long row0 = t * C2ROWS;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int r = (wave * 8 + j) * 4 + (lane >> 4), c = (lane & 15) ^ (r & 15);
+            long long grow = row0 + r;
+            grow = grow < rows_total ? grow : rows_total - 1;
+            // uniform base + 32-bit byte offset (host-checked < 2^32): the saddr form, whose
+            // address VGPR hipcc does not make each DMA wait for (vmcnt(0)) before reusing
+            const unsigned off = (unsigned)grow * 256u + (unsigned)c * 16u;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(
+                                                 reinterpret_cast<const char*>(g2) + off),
+                                             (__attribute__((address_space(3))) void*)(An + (wave * 8 + j) * 64), 16,
+                                             0, 0);
+        }
+    };
+    // A: this lane's row of the triple in An, k = 16q + 8h .. +8 -> three bf16 planes
     u32x4 af[4][3];
-    {
-        long long grow = n0 * L::P + wave * 32 + (lane & 31);
-        grow = grow < rows_total ? grow : rows_total - 1;  // rows past the end: clamped, never stored
-        const float* g = reinterpret_cast<const float*>(a.x) + grow * L::COUT + (lane >> 5) * 8;
-        float4 ar[8];
+    auto take_A = [&]() {
+        const int r = wave * 32 + (lane & 31), sw = r & 15;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            ar[2 * q] = *reinterpret_cast<const float4*>(g + 16 * q);
-            ar[2 * q + 1] = *reinterpret_cast<const float4*>(g + 16 * q + 4);
+            const int c0 = (lane >> 5) * 2 + 4 * q;
+            const u32x4 v0 = An[r * 16 + (c0 ^ sw)], v1 = An[r * 16 + ((c0 + 1) ^ sw)];
+            split8(__builtin_bit_cast(float4, v0), __builtin_bit_cast(float4, v1), af[q][0], af[q][1], af[q][2]);
         }
-        for (int e = tid; e < C2S * C2PIX * 8; e += 512) reinterpret_cast<float4*>(Ds)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) split8(ar[2 * q], ar[2 * q + 1], af[q][0], af[q][1], af[q][2]);
-    }
-
-    // tap k = 4 * class + i; class (py, px) = (k >> 3, (k >> 2) & 1), tap i of the class =
-    // (ky, kx) = (py + 2 (i >> 1), px + 2 (i & 1)): one f32 accumulator for all six split
-    // products (hi/lo pairs would not fit the 2-waves-per-SIMD register budget)
+    };
     auto mfma_tap = [&](int k, f32x16& c) {
-        const u32x4* Bt = Bs[(k >> 2) & 1] + (k & 3) * 4 * 3 * 64 + lane;
+        const u32x4* Bt = Bring + (k & 3) * C2P_TAP + lane;
         c = zero16();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -722,7 +747,9 @@ __global__ void __launch_bounds__(512, 1) dgrad2_col_kernel(Args a, const u32x4*
     // col2im add of tap k into the class image: row (oy, ox) -> class pixel (oy + (i >> 1),
     // ox + (i & 1)); eight reads, then eight writes; rows past the samples -> dummy slot
     auto rmw_tap = [&](int k, const f32x16& c) {
-        const int i = k & 3, toff = ((i >> 1) * 10 + (i & 1)) * 32 + (lane & 31);
+        const int i = k & 3;
+        int toff = ((i >> 1) * 10 + (i & 1)) * 32 + (lane & 31);
+        asm volatile("" : "+v"(toff));  // opaque: keeps hipcc from hoisting 4 taps' address sets (spills)
 #pragma unroll
         for (int r0 = 0; r0 < 16; r0 += 8) {
             int di[8];
@@ -738,10 +765,8 @@ __global__ void __launch_bounds__(512, 1) dgrad2_col_kernel(Args a, const u32x4*
             for (int r = 0; r < 8; ++r) Ds[di[r]] = dv[r] + c[r0 + r];
         }
     };
-    // ReLU-mask operands of class p's outputs: unconditional loads from clamped valid
-    // addresses (a conditional load becomes a branch with a vmcnt(0) wait behind it)
     float4 mk[C2OV];
-    auto load_mask = [&](int cls) {
+    auto load_mask = [&](long long n0, int cls) {
         const int py = cls >> 1, px = cls & 1;
 #pragma unroll
         for (int j = 0; j < C2OV; ++j) {
@@ -749,61 +774,91 @@ __global__ void __launch_bounds__(512, 1) dgrad2_col_kernel(Args a, const u32x4*
             const long long n = n0 + s;
             const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
             const bool ok = e < C2S * C2PIX * 8 && n < a.batch;
-            const long long o = ok ? ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4 : n0 * L::IH * L::IW * L::CIN;
+            const long long o = ok ? ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4 : 0;
             mk[j] = *reinterpret_cast<const float4*>(a.mask + o);
         }
     };
-    // masked class image -> dX (NHWC), image re-zeroed for the next class; uniform control
-    // flow up to the store (threads past the image use the dummy slot)
-    auto output = [&](int cls) {
+    // the image is read and re-zeroed with inline-asm LDS ops: a C++ access here, after the
+    // step's tap DMAs, makes hipcc wait vmcnt(0) first (it cannot tell the two LDS regions apart)
+    const uint32_t img0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)Ds);
+    auto output = [&](long long n0, int cls) {
         const int py = cls >> 1, px = cls & 1;
+        const u32x4 zero4 = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int j = 0; j < C2OV; ++j) {
             const int e = j * 512 + tid, s = e / 800, rem = e - s * 800, pix = rem >> 3, c4 = rem & 7;
             const bool in = e < C2S * C2PIX * 8;
-            float4* dp = reinterpret_cast<float4*>(Ds) + (in ? e : C2S * C2PIX * 8);
-            const float4 d = *dp;
-            *dp = make_float4(0.f, 0.f, 0.f, 0.f);
+            const uint32_t da = img0 + (uint32_t)(in ? e : C2S * C2PIX * 8) * 16u;
+            u32x4 dr;
+            asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)\n\tds_write_b128 %1, %2"
+                         : "=&v"(dr) : "v"(da), "v"(zero4) : "memory");
+            const float4 d = __builtin_bit_cast(float4, dr);
             const float4 m = mk[j];
             const float4 y = make_float4(m.x > 0.f ? d.x : 0.f, m.y > 0.f ? d.y : 0.f, m.z > 0.f ? d.z : 0.f,
                                          m.w > 0.f ? d.w : 0.f);
             const long long n = n0 + s;
-            if (in && n < a.batch) {
-                const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
-                *reinterpret_cast<float4*>(a.y + ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4) = y;
-            }
+            const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
+            float4* dst = (in && n < a.batch)
+                              ? reinterpret_cast<float4*>(a.y + ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4)
+                              : kC2Dummy + tid;
+            *dst = y;
         }
     };
-    load_mask(0);
-    __syncthreads();  // B of classes 0 and 1, the zeroed image
 
-    // Software pipeline over the 16 taps: step k issues tap k+1's MFMAs beside tap k's col2im
-    // adds (no dependence between them), so the matrix cores run through the add phases; one
-    // LDS-only barrier per step orders the adds (fixed tap order per output).  B of class c+1
-    // (c = 1, 2) is DMA'd at step 4c into the buffer class c-1 finished reading at step 4c-2,
-    // and waited for at the end of step 4c+2, before tap 4c+4's MFMAs at step 4c+3.
-    auto step = [&](int k, f32x16& next, const f32x16& cur) {
-        const int cls = k >> 2, i = k & 3;
-        if (i == 0 && k > 0) {
-            load_mask(cls);
-            if (cls == 1 || cls == 2) loadB(cls + 1, (cls + 1) & 1);
-        }
-        if (k + 1 < 16) mfma_tap(k + 1, next);
+    long long t = blockIdx.x;
+    // prologue: the first triple's rows, taps 0..3, class 0's mask operands, a zero image
+    dmaA(t);
+    dmaB2(0);
+    dmaB2(2);
+    load_mask(t * C2S, 0);
+    for (int e = tid; e < C2S * C2PIX * 8; e += 512) reinterpret_cast<float4*>(Ds)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the builtin, so hipcc's own wait bookkeeping sees it
+    lds_barrier();
+    take_A();
+    lds_barrier();  // An free for the next triple's rows
+
+    // one class-tap step (i = k & 3 at compile time): tap k+1's MFMAs beside tap k's col2im
+    // adds.  vmcnt bookkeeping per wave (every count static: stores unconditional, loads
+    // clamped): i = 1, 3 DMA the tap pair k+3, k+4; i = 3 then stores the class, loads the
+    // next class's mask operands and (class 0) DMAs the next triple's rows; i = 0 waits for
+    // the pair of the step before (behind it: 5 stores + 5 mask loads (+ 8 row DMAs after
+    // class 0) = vmcnt(10) / vmcnt(18)); i = 2 drains everything (vmcnt(0)).
+    auto step = [&](long long tt, int cls, auto i_tag, f32x16& next, const f32x16& cur) {
+        constexpr int i = decltype(i_tag)::value;
+        const int k = 4 * cls + i;
+        const long long n0 = tt * C2S;
+        if constexpr (i & 1) dmaB2(k + 3);  // taps k+3, k+4 (mod 16) into the slots of k-1, k
+        if (i < 3 || cls < 3) mfma_tap(k + 1, next);
         rmw_tap(k, cur);
-        if (i == 2 && (cls == 1 || cls == 2)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (i == 0) {
+            if (cls == 1)
+                __builtin_amdgcn_s_waitcnt(0x4F72);  // vmcnt(18): + class 0's 8 row DMAs
+            else
+                __builtin_amdgcn_s_waitcnt(0x0F7A);  // vmcnt(10)
+        }
+        if constexpr (i == 2) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         lds_barrier();
-        if (i == 3) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this class's mask operands
-            output(cls);
+        if constexpr (i == 3) {
+            output(n0, cls);
+            // one load path (two paths would merge into register copies that wait vmcnt(0))
+            load_mask(cls < 3 ? n0 : (tt + gridDim.x) * C2S, (cls + 1) & 3);
+            if (cls == 0) dmaA(tt + gridDim.x);  // the next triple's rows (clamped past the end)
             lds_barrier();
         }
     };
     f32x16 acc0, acc1;
-    mfma_tap(0, acc0);
 #pragma unroll 1
-    for (int k = 0; k < 16; k += 2) {  // accumulators alternate roles with static names
-        step(k, acc1, acc0);
-        step(k + 1, acc0, acc1);
+    for (; t < ntriples; t += gridDim.x) {
+        mfma_tap(0, acc0);
+#pragma unroll 1
+        for (int cls = 0; cls < 4; ++cls) {
+            step(t, cls, std::integral_constant<int, 0>{}, acc1, acc0);
+            step(t, cls, std::integral_constant<int, 1>{}, acc0, acc1);
+            step(t, cls, std::integral_constant<int, 2>{}, acc1, acc0);
+            step(t, cls, std::integral_constant<int, 3>{}, acc0, acc1);
+        }
+        take_A();  // the next triple's rows (drained at class 1's i = 2, ordered by the barriers since)
+        lds_barrier();
     }
 }
 
@@ -1930,13 +1985,16 @@ int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float
 #ifndef WS_KT3
 #define WS_KT3 64
 #endif
-// split wgrad: its own split-K count (~2048 pixels per split so the grid fills the chip)
+#ifndef WS_PX
+#define WS_PX 2048  // split wgrad: pixels per split-K slice
+#endif
+// split wgrad: its own split-K count (~WS_PX pixels per split so the grid fills the chip)
 template <class L, bool U8, int KT>
 struct WsLaunch {
     using C = WsCfg<L, U8, KT>;
     static long long splits(long long batch) {
         const long long px = batch * L::P;
-        long long s = (px + 2047) / 2048;
+        long long s = (px + WS_PX - 1) / WS_PX;
         // small batches (the 8-GPU per-rank minibatch): enough splits for two workgroups per CU
         // where the k-blocks are few (conv1/conv2 at B = 2048: 0.082 -> 0.074 / 0.100 -> 0.078 ms;
         // conv3's nine k-blocks already give 441 workgroups, and more splits measured slower)
@@ -2258,7 +2316,18 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
     Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch};
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 2) {
-        dgrad2_col_kernel<<<(unsigned)ppox::ceil_div(batch, C2S), 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd));
+        const long long ntriples = ppox::ceil_div(batch, (long long)C2S);
+        PPOX_REQUIRE(batch * G2::P * 256 < (1LL << 32), "ppox_nature_conv_dgrad_split: batch too large (32-bit offsets)");
+        // one workgroup per CU (150 KB of LDS each), striding over the triples
+        static int cus[64] = {};
+        int dev = 0;
+        PPOX_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev < 64, "ppox_nature_conv_dgrad_split: no device");
+        if (cus[dev] == 0)
+            PPOX_REQUIRE(hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                             cus[dev] > 0,
+                         "ppox_nature_conv_dgrad_split: CU count");
+        const long long grid = std::min<long long>(ntriples, cus[dev]);
+        dgrad2_colp_kernel<<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd), ntriples);
         PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
     }
 #if SG2
