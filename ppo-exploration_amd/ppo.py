@@ -54,10 +54,28 @@ def icm_loss_sharded(icm, x, acts, pos, B, beta, ctx):
     = the reference's icm_loss)."""
     h = icm.feature_size
     phi = icm.state_encoder(x)
+    npair = B - 1
+
+    def pair_loss(s_ft, n_ft, a_s):  # a_s: the action taken at the pair's first row
+        a_hat = icm.inverse_model(torch.cat((s_ft, n_ft), 1))
+        n_hat = icm.forward_model(torch.cat((s_ft, icm.encode_action(a_s)), 1))
+        fwd = ((n_hat - n_ft) ** 2).sum() / (npair * h)                # F.mse_loss, mean over (B-1) x h
+        if icm.discrete:
+            inv = F.cross_entropy(a_hat, a_s, reduction="sum") / npair
+        else:
+            inv = ((a_hat - a_s) ** 2).sum() / (npair * a_hat.shape[1])
+        return (1 - beta) * inv + beta * fwd
+
+    if not ctx.enabled:
+        # one process: the rows are the minibatch in order, so the pairs are two slices (no
+        # gathers: torch's indexing backward on ROCm took ~190 us per minibatch of 2048)
+        a = acts.reshape(-1).long() if icm.discrete else acts.float()
+        loss = pair_loss(phi[:-1], phi[1:], a[:-1])
+        loss.backward()
+        return loss.detach()
     full = torch.zeros(B, h, dtype=phi.dtype, device=phi.device)
     full[pos] = phi.detach()
     ctx.all_reduce_(full)
-    phi_all = full.requires_grad_(True)
     if icm.discrete:
         a_full = torch.zeros(B, dtype=torch.int64, device=phi.device)
         a_full[pos] = acts.reshape(-1).long()
@@ -66,18 +84,18 @@ def icm_loss_sharded(icm, x, acts, pos, B, beta, ctx):
         a_full[pos] = acts.float()
     ctx.all_reduce_(a_full)
     j = pos[pos < B - 1]
-    s_ft, n_ft = phi_all[j], phi_all[j + 1]
-    a_hat = icm.inverse_model(torch.cat((s_ft, n_ft), 1))
-    n_hat = icm.forward_model(torch.cat((s_ft, icm.encode_action(a_full[j])), 1))
-    npair = B - 1
-    fwd = ((n_hat - n_ft) ** 2).sum() / (npair * h)                    # F.mse_loss, mean over (B-1) x h
-    if icm.discrete:
-        inv = F.cross_entropy(a_hat, a_full[j], reduction="sum") / npair
-    else:
-        inv = ((a_hat - a_full[j]) ** 2).sum() / (npair * a_hat.shape[1])
-    loss = (1 - beta) * inv + beta * fwd
+    # the pairs' features as leaves; their gradients are scattered back with index_add_ (each
+    # of j, j + 1 holds distinct rows, so each row adds at most two terms: the same sums as
+    # autograd's indexing backward, without its slow kernel)
+    s_ft = full[j].requires_grad_(True)
+    n_ft = full[j + 1].requires_grad_(True)
+    loss = pair_loss(s_ft, n_ft, a_full[j])
     loss.backward()
-    g = phi_all.grad if phi_all.grad is not None else torch.zeros_like(full)
+    g = torch.zeros_like(full)
+    if s_ft.grad is not None:
+        g.index_add_(0, j, s_ft.grad)
+    if n_ft.grad is not None:
+        g.index_add_(0, j + 1, n_ft.grad)
     g = ctx.all_reduce_(g)
     if phi.shape[0]:
         phi.backward(g[pos])
