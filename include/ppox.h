@@ -162,6 +162,12 @@ int ppox_normal_sample(const float* mu, const float* log_std, int64_t N, int32_t
 int ppox_categorical_sample(const float* logits, int64_t N, int32_t A, int64_t env_offset,
                             uint64_t seed, int64_t counter, int32_t* actions, float* log_probs,
                             void* stream);
+/* The same draw with the Philox counter read from the device: counter = *counter_base +
+ * counter_off (a graph-captured collect step keeps its counters in device memory and
+ * advances them with ppox_counters_add; ppo.py:174-194 draws one action per env per step). */
+int ppox_categorical_sample_dc(const float* logits, int64_t N, int32_t A, int64_t env_offset,
+                               uint64_t seed, const int64_t* counter_base, int64_t counter_off,
+                               int32_t* actions, float* log_probs, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K8  SimHash count bonus (buffer.py:188-200, RolloutStorage(sim_hash=True)).
@@ -210,6 +216,14 @@ int ppox_atari_env_step(const uint8_t* obs_in, uint8_t* obs_out, const int32_t* 
                         float p_reward, float p_done, float* rewards, uint8_t* dones,
                         float* ep_ret, int32_t* ep_len, float* done_ret, int32_t* done_len,
                         void* stream);
+/* step = *step_base + step_off, read on the device (graph-captured collect). */
+int ppox_atari_env_step_dc(const uint8_t* obs_in, uint8_t* obs_out, const int32_t* actions,
+                           int64_t N, int64_t env_offset, uint64_t seed, const int64_t* step_base,
+                           int64_t step_off, float p_reward, float p_done, float* rewards,
+                           uint8_t* dones, float* ep_ret, int32_t* ep_len, float* done_ret,
+                           int32_t* done_len, void* stream);
+/* counters[i] += delta for i < n (n <= 64): advances device-resident step counters. */
+int ppox_counters_add(int64_t* counters, int32_t n, int64_t delta, void* stream);
 int ppox_vec_env_reset(float* obs, int64_t N, int32_t D, int64_t env_offset, uint64_t seed,
                        float* ep_ret, int32_t* ep_len, void* stream);
 int ppox_vec_env_step(float* obs, const int32_t* actions, int64_t N, int32_t D,

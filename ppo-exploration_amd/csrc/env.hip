@@ -58,10 +58,12 @@ __global__ void __launch_bounds__(256) atari_reset_kernel(uint8_t* __restrict__ 
 
 __global__ void __launch_bounds__(256) atari_step_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                          const int32_t* __restrict__ actions, long long env_offset,
-                                                         uint32_t k0, uint32_t k1, uint32_t step, float p_reward,
+                                                         uint32_t k0, uint32_t k1, uint32_t step,
+                                                         const long long* __restrict__ sbase, float p_reward,
                                                          float p_done, float* __restrict__ rewards,
                                                          uint8_t* __restrict__ dones, Episode ep) {
     const long long n = blockIdx.x;
+    if (sbase) step += (uint32_t)*sbase;  // device-resident step counter (graph-captured collect)
     const uint32_t gid = (uint32_t)(env_offset + n);
     const uint32_t a = (uint32_t)actions[n];
     const ppox::u32x4 ev = ppox::philox4x32_10(ppox::u32x4{EVENT_BLOCK, gid, step, a}, k0, k1);
@@ -129,19 +131,46 @@ extern "C" int ppox_atari_env_reset(uint8_t* obs, int64_t N, int64_t env_offset,
     PPOX_LAUNCHED("ppox_atari_env_reset");
 }
 
+static int atari_env_step_impl(const uint8_t* obs_in, uint8_t* obs_out, const int32_t* actions, int64_t N,
+                               int64_t env_offset, uint64_t seed, int64_t step, const int64_t* step_base,
+                               float p_reward, float p_done, float* rewards, uint8_t* dones, float* ep_ret,
+                               int32_t* ep_len, float* done_ret, int32_t* done_len, void* stream) {
+    PPOX_REQUIRE(obs_in && obs_out && actions && rewards && dones && N > 0, "ppox_atari_env_step: null pointer");
+    PPOX_REQUIRE(ppox::aligned16(obs_in) && ppox::aligned16(obs_out), "ppox_atari_env_step: obs must be 16B aligned");
+    PPOX_REQUIRE(step_base || (step >= 1 && step < (1LL << 32)), "ppox_atari_env_step: step must be in [1, 2^32)");
+    PPOX_REQUIRE((ep_ret == nullptr) == (ep_len == nullptr), "ppox_atari_env_step: ep_ret/ep_len pair");
+    Episode ep{ep_ret, ep_len, done_ret, done_len};
+    atari_step_kernel<<<(unsigned)N, 256, 0, ppox::as_stream(stream)>>>(
+        obs_in, obs_out, actions, env_offset, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step,
+        reinterpret_cast<const long long*>(step_base), p_reward, p_done, rewards, dones, ep);
+    PPOX_LAUNCHED("ppox_atari_env_step");
+}
+
 extern "C" int ppox_atari_env_step(const uint8_t* obs_in, uint8_t* obs_out, const int32_t* actions, int64_t N,
                                    int64_t env_offset, uint64_t seed, int64_t step, float p_reward, float p_done,
                                    float* rewards, uint8_t* dones, float* ep_ret, int32_t* ep_len, float* done_ret,
                                    int32_t* done_len, void* stream) {
-    PPOX_REQUIRE(obs_in && obs_out && actions && rewards && dones && N > 0, "ppox_atari_env_step: null pointer");
-    PPOX_REQUIRE(ppox::aligned16(obs_in) && ppox::aligned16(obs_out), "ppox_atari_env_step: obs must be 16B aligned");
-    PPOX_REQUIRE(step >= 1 && step < (1LL << 32), "ppox_atari_env_step: step must be in [1, 2^32)");
-    PPOX_REQUIRE((ep_ret == nullptr) == (ep_len == nullptr), "ppox_atari_env_step: ep_ret/ep_len pair");
-    Episode ep{ep_ret, ep_len, done_ret, done_len};
-    atari_step_kernel<<<(unsigned)N, 256, 0, ppox::as_stream(stream)>>>(
-        obs_in, obs_out, actions, env_offset, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step, p_reward, p_done,
-        rewards, dones, ep);
-    PPOX_LAUNCHED("ppox_atari_env_step");
+    return atari_env_step_impl(obs_in, obs_out, actions, N, env_offset, seed, step, nullptr, p_reward, p_done, rewards,
+                               dones, ep_ret, ep_len, done_ret, done_len, stream);
+}
+
+extern "C" int ppox_atari_env_step_dc(const uint8_t* obs_in, uint8_t* obs_out, const int32_t* actions, int64_t N,
+                                      int64_t env_offset, uint64_t seed, const int64_t* step_base, int64_t step_off,
+                                      float p_reward, float p_done, float* rewards, uint8_t* dones, float* ep_ret,
+                                      int32_t* ep_len, float* done_ret, int32_t* done_len, void* stream) {
+    PPOX_REQUIRE(step_base, "ppox_atari_env_step_dc: null step counter");
+    return atari_env_step_impl(obs_in, obs_out, actions, N, env_offset, seed, step_off, step_base, p_reward, p_done,
+                               rewards, dones, ep_ret, ep_len, done_ret, done_len, stream);
+}
+
+__global__ void counters_add_kernel(long long* c, int n, long long delta) {
+    if ((int)threadIdx.x < n) c[threadIdx.x] += delta;
+}
+
+extern "C" int ppox_counters_add(int64_t* counters, int32_t n, int64_t delta, void* stream) {
+    PPOX_REQUIRE(counters && n >= 1 && n <= 64, "ppox_counters_add: bad arguments");
+    counters_add_kernel<<<1, 64, 0, ppox::as_stream(stream)>>>(reinterpret_cast<long long*>(counters), n, delta);
+    PPOX_LAUNCHED("ppox_counters_add");
 }
 
 extern "C" int ppox_vec_env_reset(float* obs, int64_t N, int32_t D, int64_t env_offset, uint64_t seed, float* ep_ret,

@@ -315,10 +315,12 @@ __global__ void __launch_bounds__(256) adv_stats_kernel(const float* __restrict_
 template <int MAXA>
 __global__ void __launch_bounds__(256) categorical_sample_kernel(const float* __restrict__ logits, long long N, int A,
                                                                  long long env_offset, uint64_t seed,
-                                                                 long long counter, int32_t* __restrict__ actions,
+                                                                 long long counter, const long long* __restrict__ cbase,
+                                                                 int32_t* __restrict__ actions,
                                                                  float* __restrict__ logp) {
     const long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= N) return;
+    if (cbase) counter += *cbase;  // device-resident counter (graph-captured collect)
     CatRow<MAXA> r;
     categorical_forward<MAXA>(logits + n * A, A, r);
     const ppox::u32x4 w = ppox::philox4x32_10(
@@ -753,15 +755,30 @@ extern "C" int ppox_normal_sample(const float* mu, const float* log_std, int64_t
     PPOX_LAUNCHED("ppox_normal_sample");
 }
 
-extern "C" int ppox_categorical_sample(const float* logits, int64_t N, int32_t A, int64_t env_offset, uint64_t seed,
-                                       int64_t counter, int32_t* actions, float* log_probs, void* stream) {
+static int categorical_sample_impl(const float* logits, int64_t N, int32_t A, int64_t env_offset, uint64_t seed,
+                                   int64_t counter, const int64_t* cbase, int32_t* actions, float* log_probs,
+                                   void* stream) {
     if (N == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(logits && actions && log_probs, "ppox_categorical_sample: null pointer");
     PPOX_REQUIRE(A >= 1 && A <= 64 && N >= 0, "ppox_categorical_sample: bad sizes");
     hipStream_t s = ppox::as_stream(stream);
+    const long long* cb = reinterpret_cast<const long long*>(cbase);
     PPOX_DISPATCH_A(A, MA, {
         categorical_sample_kernel<MA><<<ppox::ceil_div(N, 256), 256, 0, s>>>(logits, N, A, env_offset, seed, counter,
-                                                                             actions, log_probs);
+                                                                             cb, actions, log_probs);
     });
     PPOX_LAUNCHED("ppox_categorical_sample");
+}
+
+extern "C" int ppox_categorical_sample(const float* logits, int64_t N, int32_t A, int64_t env_offset, uint64_t seed,
+                                       int64_t counter, int32_t* actions, float* log_probs, void* stream) {
+    return categorical_sample_impl(logits, N, A, env_offset, seed, counter, nullptr, actions, log_probs, stream);
+}
+
+extern "C" int ppox_categorical_sample_dc(const float* logits, int64_t N, int32_t A, int64_t env_offset,
+                                          uint64_t seed, const int64_t* counter_base, int64_t counter_off,
+                                          int32_t* actions, float* log_probs, void* stream) {
+    PPOX_REQUIRE(counter_base || N == 0, "ppox_categorical_sample_dc: null counter");
+    return categorical_sample_impl(logits, N, A, env_offset, seed, counter_off, counter_base, actions, log_probs,
+                                   stream);
 }

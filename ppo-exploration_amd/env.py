@@ -87,6 +87,13 @@ class DeviceAtariEnv:
                               self.p_reward, self.p_done, rewards, dones, self.ep_ret, self.ep_len, done_ret,
                               done_len)
 
+    def step_into_dc(self, obs_in, obs_out, actions, rewards, dones, done_ret, done_len, step_base, step_off):
+        """step_into with the step counter read on the device (*step_base + step_off): the form a
+        captured collect graph replays; the caller advances self.k on the host."""
+        native.atari_env_step_dc(obs_in, obs_out, actions, self.num_envs, self.env_offset, self.seed, step_base,
+                                 step_off, self.p_reward, self.p_done, rewards, dones, self.ep_ret, self.ep_len,
+                                 done_ret, done_len)
+
     # VecEnv-style API (allocating; the training loop uses the *_into forms)
     def reset(self):
         self._obs = torch.empty((self.num_envs, 4, 84, 84), dtype=torch.uint8, device=self.device)

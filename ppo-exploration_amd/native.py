@@ -36,6 +36,10 @@ SIGNATURES = {
                                _vp, _vp, _vp, _vp, _f32, _vp, _i64, _f32, _f32, _f32, _f32,
                                _vp, _vp, _vp, _vp, _vp],
     "ppox_categorical_sample": [_vp, _i64, _i32, _i64, _u64, _i64, _vp, _vp, _vp],
+    "ppox_categorical_sample_dc": [_vp, _i64, _i32, _i64, _u64, _vp, _i64, _vp, _vp, _vp],
+    "ppox_atari_env_step_dc": [_vp, _vp, _vp, _i64, _i64, _u64, _vp, _i64, _f32, _f32, _vp, _vp, _vp, _vp,
+                               _vp, _vp, _vp],
+    "ppox_counters_add": [_vp, _i32, _i64, _vp],
     "ppox_ppo_box_loss_partials": [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _f64, _vp, _vp],
     "ppox_ppo_box_loss_backward": [_vp, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
@@ -169,7 +173,7 @@ _LAYERED = ("ppox_nature_conv_fwd", "ppox_nature_conv_dgrad", "ppox_nature_conv_
 
 def call(name, *args):
     key = f"{name}:{args[0]}" if name in _LAYERED else name
-    if key in _timed:
+    if key in _timed and not torch.cuda.is_current_stream_capturing():  # (captured launches replay untimed)
         s = torch.cuda.current_stream()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(s)
@@ -347,6 +351,17 @@ def categorical_sample(logits, N, A, env_offset, seed, counter, actions, log_pro
          _p(actions), _p(log_probs), stream_ptr(stream))
 
 
+def categorical_sample_dc(logits, N, A, env_offset, seed, counter_base, counter_off, actions, log_probs,
+                          stream=None):
+    """counter = *counter_base + counter_off, read on the device (counter_base: int64 device tensor)."""
+    call("ppox_categorical_sample_dc", _p(logits), N, A, env_offset, seed & 0xFFFFFFFFFFFFFFFF, _p(counter_base),
+         counter_off, _p(actions), _p(log_probs), stream_ptr(stream))
+
+
+def counters_add(counters, delta, stream=None):
+    call("ppox_counters_add", _p(counters), counters.numel(), int(delta), stream_ptr(stream))
+
+
 # ---------------------------------------------------------------------------
 # K5 gather, optimiser, envs
 # ---------------------------------------------------------------------------
@@ -374,6 +389,14 @@ def atari_env_step(obs_in, obs_out, actions, N, env_offset, seed, step, p_reward
     call("ppox_atari_env_step", _p(obs_in), _p(obs_out), _p(actions), N, env_offset, seed, step, float(p_reward),
          float(p_done), _p(rewards), _p(dones), _p(ep_ret), _p(ep_len), _p(done_ret), _p(done_len),
          stream_ptr(stream))
+
+
+def atari_env_step_dc(obs_in, obs_out, actions, N, env_offset, seed, step_base, step_off, p_reward, p_done, rewards,
+                      dones, ep_ret=None, ep_len=None, done_ret=None, done_len=None, stream=None):
+    """step = *step_base + step_off, read on the device (step_base: int64 device tensor)."""
+    call("ppox_atari_env_step_dc", _p(obs_in), _p(obs_out), _p(actions), N, env_offset, seed, _p(step_base),
+         int(step_off), float(p_reward), float(p_done), _p(rewards), _p(dones), _p(ep_ret), _p(ep_len),
+         _p(done_ret), _p(done_len), stream_ptr(stream))
 
 
 def vec_env_reset(obs, N, D, env_offset, seed, ep_ret=None, ep_len=None, stream=None):

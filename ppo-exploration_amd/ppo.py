@@ -20,6 +20,7 @@ Per iteration on each rank:
            grad bucket -> [all-reduce] -> ppox_grad_sumsq + ppox_adam_step.
 There is no CPU fallback: every step needs libppox.so and a GPU.
 """
+import os
 import time
 from collections import deque
 
@@ -32,7 +33,7 @@ import native
 import convs
 from buffer import IntrinsicStorage, RolloutStorage
 from dist import DistContext, owned_minibatch_indices, owned_minibatch_positions, shard_range
-from env import make_env
+from env import DeviceAtariEnv, make_env
 from phases import traced
 from models import CnnActorCritic, FlatParams, IntrinsicCuriosityModule, MlpNetwork, RndNetwork
 from util import ActionConverter, RunningMeanStd
@@ -448,13 +449,17 @@ class PPO(BaseAlgorithm):
         self.sim_hash, self.sil = sim_hash, sil
         self._alloc_train_state()
         self.last_obs = None
+        # the collect step loop as one captured graph (PPOX_COLLECT_GRAPH=0: eager launches)
+        self._collect_graph_enabled = os.environ.get("PPOX_COLLECT_GRAPH", "1") != "0"
+        self._cgraph = None
 
-    @traced("collect")
-    def collect_samples(self):
-        ro = self.rollout
-        self._ensure_started()
-        ro.reset()
-        net = self.policy.net
+    def _collect_graph_ok(self):
+        return (self._collect_graph_enabled and isinstance(self.env, DeviceAtariEnv) and self.discrete
+                and not self.rollout.do_hash and getattr(self.policy.net, "conv_impl", None) is not None
+                and self.device.type == "cuda")
+
+    def _collect_steps_eager(self):
+        ro, net = self.rollout, self.policy.net
         for t in range(self.nstep):
             with torch.no_grad():
                 out, v, _ = net(ro.obs_slots[t])
@@ -465,6 +470,51 @@ class PPO(BaseAlgorithm):
             if ro.do_hash:                                  # rollout.add -> sim_hash(last_obs), buffer.py:176
                 ro.sim_hash(ro.obs_slots[t], ro.rewards[t])
             self.num_timesteps += self.num_envs
+
+    def _collect_step_dc(self, t):
+        """Step t of the collect loop with both Philox counters read on the device
+        (self._ctr = [sample counter, env step] at the rollout's start)."""
+        ro = self.rollout
+        out, v, _ = self.policy.net(ro.obs_slots[t])
+        native.categorical_sample_dc(out, self.local_envs, self.n_actions, self.env_offset, self.seed, self._ctr[0:1],
+                                     t, ro.actions[t], ro.log_probs[t])
+        ro.values[t].copy_(v)
+        self.env.step_into_dc(ro.obs_slots[t], ro.obs_slots[t + 1], ro.actions[t], ro.rewards[t], ro.masks[t],
+                              ro.done_ret[t], ro.done_len[t], self._ctr[1:2], t + 1)
+
+    def _collect_graphed(self):
+        """ppo.py:174-194 as one hipGraph replay: the first collect runs eagerly (packing the
+        weights, warming the library GEMMs) and then captures the nstep steps; every later
+        collect refreshes the packed weight forms (train moved the weights), writes the two
+        Philox counters to the device and replays — the same launches, counters and results
+        as the eager loop (test_collect_graph_matches_eager), without ~20 host launches per step."""
+        T, env = self.nstep, self.env
+        if self._cgraph is None:
+            self._collect_steps_eager()
+            self._ctr = torch.zeros(2, dtype=torch.int64, device=self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(g):
+                for t in range(T):
+                    self._collect_step_dc(t)
+            self._cgraph = g
+            return
+        self.policy.net.conv_impl.pack(self.local_envs)
+        self._ctr[0].fill_(self._sample_counter)
+        self._ctr[1].fill_(env.k)
+        self._cgraph.replay()
+        self._sample_counter += T
+        env.k += T
+        self.num_timesteps += T * self.num_envs
+
+    @traced("collect")
+    def collect_samples(self):
+        ro = self.rollout
+        self._ensure_started()
+        ro.reset()
+        if self._collect_graph_ok():
+            self._collect_graphed()
+        else:
+            self._collect_steps_eager()
         ro.pos, ro.full = self.nstep, True
         # ppo.py:196 bootstraps with V(s_{T-1}) and the last step's dones
         ro.compute_returns_and_advantages(ro.values[self.nstep - 1], ro.masks[self.nstep - 1])

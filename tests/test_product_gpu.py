@@ -433,3 +433,32 @@ def test_learn_reward_target_stops_early(tmp_path, monkeypatch):
     assert alg.num_timesteps == N * T
     header, rows = _read_csv(tmp_path / "logs" / "PPO" / env_id)
     assert len(rows) == 2 and rows[1]["total timesteps"] == str(N * T)
+
+
+def test_collect_graph_matches_eager():
+    """PPO.collect_samples as one captured graph (after the first, eager, collect) == the
+    eager step loop, bitwise, across collect/train iterations (counters on the device,
+    packed weights refreshed before each replay)."""
+    import ppo
+
+    def run(graph):
+        np.random.seed(0)
+        torch.manual_seed(0)
+        alg = ppo.PPO(env_id="BreakoutNoFrameskip-v4", n_envs=16, nstep=8, batch_size=64, n_epochs=1, quiet=True,
+                      seed=5)
+        alg._collect_graph_enabled = graph
+        outs = []
+        for _ in range(3):
+            alg.collect_samples()
+            ro = alg.rollout
+            outs.append([x.clone() for x in (ro.actions, ro.rewards, ro.values, ro.log_probs, ro.masks,
+                                              ro.obs_slots, ro.advantages)])
+            alg.train()
+        return outs, alg.flat.data.clone(), alg._cgraph is not None, alg.num_timesteps
+
+    (a, wa, ga, na), (b, wb, gb, nb) = run(False), run(True)
+    assert not ga and gb and na == nb
+    for xa, xb in zip(a, b):
+        for u, v in zip(xa, xb):
+            assert torch.equal(u, v)
+    assert torch.equal(wa, wb)
