@@ -12,7 +12,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/$TAG-stats -o run --o
     python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/$TAG/stats.log 2>&1 || exit $?
 cp /tmp/$TAG-stats/*stats* gpurun_out/$TAG/
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "wgrad_kernel|gae|gemm|split_kernel|col_kernel" -d /tmp/$TAG-$C -o run \
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "wgrad_kernel|gae|gemm|split_kernel|col_kernel|colp_kernel|wgrad_reduce" -d /tmp/$TAG-$C -o run \
       --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --epochs 1 --no-cpu-baseline \
       > gpurun_out/$TAG/pmc_$C.log 2>&1 || exit $?
   cp /tmp/$TAG-$C/*counter_collection* gpurun_out/$TAG/pmc_$C.csv
