@@ -36,8 +36,10 @@ DGRAD2_SPLIT_MAX_BATCH = int(os.environ.get("PPOX_DGRAD2_SPLIT_MAX", str(1 << 62
 # fc forward: the split-bf16 GEMM from this batch up, rocBLAS below (PPOX_FC_SPLIT_MIN
 # overrides).  Same-box A/B of the whole training step (tools/ab_fc.sh, after the split
 # kernel's two-deep load pipeline): -40 ms per iteration at B = 16384, +17 ms at the 8-GPU
-# per-rank minibatch (2048: 128-row tiles x 8 column blocks under-fill the chip)
-FC_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_SPLIT_MIN", "8192"))
+# per-rank minibatch (2048: 128-row tiles x 8 column blocks under-fill the chip).  Kernel
+# level (tools/fc_bench.py, r02): 0.085 vs 0.112 ms at 4096 rows (the 1-GPU collect batch),
+# 0.141 vs 0.213 ms at 8192
+FC_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_SPLIT_MIN", "4096"))
 # fc dgrad fused with the trunk's ReLU backward + NHWC transpose (split-bf16) up to this
 # batch (PPOX_FC_DGRAD_FUSED_MAX overrides): faster than rocBLAS + nchw_to_nhwc_mask at
 # every measured batch (A/B: -33 ms per iteration at 16384, -2 ms at 2048)

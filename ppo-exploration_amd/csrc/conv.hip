@@ -1490,50 +1490,66 @@ __global__ void __launch_bounds__(256, 2) wgrad_kernel(WArgs a) {
     }
 }
 
-// sum the slabs, scatter to PyTorch [co][ci][ky][kx] (+ bias).  A block owns 32
-// consecutive outputs (one 128-B row of every slab) x RG split groups; thread
-// (e, g) sums splits g, g+RG, g+2RG, ... in order, then the RG group sums are
-// added in group order — a fixed order, so the result is deterministic.  RG = 8
-// (256 threads) for the f32 kernels' <= 512 splits, 32 (1024 threads) for the
-// split kernels' up to 2048.
-constexpr int RED_E = 32;
-
-template <class L, bool NHWC_ORDER, int RG>
+// sum the slabs, scatter to PyTorch [co][ci][ky][kx] (+ bias).  A block owns 4·E
+// consecutive outputs (E float4 lanes of every slab row) x RG split groups; thread (e, g)
+// sums splits g, g+RG, g+2RG, ... in order, then the RG group sums are combined by a
+// fixed pairwise tree — one order per output, so the result is deterministic.  E x RG: 32 x 8 for the
+// f32 kernels' <= 512 splits; for the split kernels' up to 2048, 32 x 32, or 8 x 128 when
+// the layer has few outputs (conv1: 8,224 -> 257 blocks instead of 65, a fuller chip).
+template <class L, bool NHWC_ORDER, int RED_E, int RG>
 __global__ void __launch_bounds__(RED_E * RG) wgrad_reduce(const float* __restrict__ slab,
                                                          const float* __restrict__ bslab, int splits,
                                                          float* __restrict__ dw, float* __restrict__ db) {
-    __shared__ float part[RG][RED_E];
+    __shared__ float4 part[RG][RED_E];
     constexpr int KC = L::K * L::COUT;
+    static_assert(KC % 4 == 0 && L::COUT % 4 == 0, "wgrad_reduce: float4 lanes");
     const int e = threadIdx.x % RED_E, grp = threadIdx.x / RED_E;
-    const int i = blockIdx.x * RED_E + e;
-    float s = 0.f;
+    const int i = (blockIdx.x * RED_E + e) * 4;  // first of this lane's four outputs
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto add = [](float4& a, const float4 b) {
+        a.x += b.x;
+        a.y += b.y;
+        a.z += b.z;
+        a.w += b.w;
+    };
     if (i < KC) {
-        for (int sp = grp; sp < splits; sp += RG) s += slab[(long long)sp * KC + i];
+        for (int sp = grp; sp < splits; sp += RG) add(s, *reinterpret_cast<const float4*>(slab + (long long)sp * KC + i));
     } else if (i < KC + L::COUT) {
-        for (int sp = grp; sp < splits; sp += RG) s += bslab[(long long)sp * L::COUT + (i - KC)];
+        for (int sp = grp; sp < splits; sp += RG)
+            add(s, *reinterpret_cast<const float4*>(bslab + (long long)sp * L::COUT + (i - KC)));
     }
+    // the RG group sums combined by a fixed pairwise tree (deterministic, and its rounding
+    // error grows with log2(RG) rather than RG)
     part[grp][e] = s;
     __syncthreads();
-    if (grp != 0) return;
-    float t = part[0][e];
 #pragma unroll
-    for (int g = 1; g < RG; ++g) t += part[g][e];
-    if (i < KC) {
-        const int k = i / L::COUT, co = i % L::COUT;
-        int ci, ky, kx;
-        if (NHWC_ORDER) {
-            ci = k % L::CIN;
-            const int tap = k / L::CIN;
-            ky = tap / L::KW;
-            kx = tap % L::KW;
-        } else {
-            kx = k % L::KW;
-            ky = (k / L::KW) % L::KH;
-            ci = k / (L::KW * L::KH);
+    for (int h = RG / 2; h >= 1; h >>= 1) {
+        if (grp < h) add(part[grp][e], part[grp + h][e]);
+        __syncthreads();
+    }
+    if (grp != 0) return;
+    const float4 t = part[0][e];
+    const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int ic = i + c;
+        if (ic < KC) {
+            const int k = ic / L::COUT, co = ic % L::COUT;
+            int ci, ky, kx;
+            if (NHWC_ORDER) {
+                ci = k % L::CIN;
+                const int tap = k / L::CIN;
+                ky = tap / L::KW;
+                kx = tap % L::KW;
+            } else {
+                kx = k % L::KW;
+                ky = (k / L::KW) % L::KH;
+                ci = k / (L::KW * L::KH);
+            }
+            dw[((co * L::CIN + ci) * L::KH + ky) * L::KW + kx] = tv[c];
+        } else if (ic < KC + L::COUT) {
+            db[ic - KC] = tv[c];
         }
-        dw[((co * L::CIN + ci) * L::KH + ky) * L::KW + kx] = t;
-    } else if (i < KC + L::COUT) {
-        db[i - KC] = t;
     }
 }
 
@@ -1970,11 +1986,14 @@ int launch_wgrad(const WArgs& wa_in, hipStream_t s) {
 
 template <class L, bool NHWC_ORDER>
 int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float* dw, float* db, hipStream_t s) {
-    const unsigned blocks = ppox::ceil_div(L::K * L::COUT + L::COUT, RED_E);
-    if (splits >= 256)  // 32 split groups per element: shorter sequential chains (conv1 at B = 2048: 512 splits)
-        wgrad_reduce<L, NHWC_ORDER, 32><<<blocks, RED_E * 32, 0, s>>>(slab, bslab, splits, dw, db);
-    else
-        wgrad_reduce<L, NHWC_ORDER, 8><<<blocks, RED_E * 8, 0, s>>>(slab, bslab, splits, dw, db);
+    constexpr int N = L::K * L::COUT + L::COUT;
+    if (splits >= 256 && N < 4 * 32 * 256) {  // few outputs, many splits: 8 lanes x 128 split groups
+        wgrad_reduce<L, NHWC_ORDER, 8, 128><<<ppox::ceil_div(N, 32), 1024, 0, s>>>(slab, bslab, splits, dw, db);
+    } else if (splits >= 256) {  // 32 split groups per element: shorter sequential chains
+        wgrad_reduce<L, NHWC_ORDER, 32, 32><<<ppox::ceil_div(N, 128), 1024, 0, s>>>(slab, bslab, splits, dw, db);
+    } else {
+        wgrad_reduce<L, NHWC_ORDER, 32, 8><<<ppox::ceil_div(N, 128), 256, 0, s>>>(slab, bslab, splits, dw, db);
+    }
     PPOX_LAUNCHED("ppox_nature_wgrad_reduce");
 }
 
@@ -2371,12 +2390,22 @@ struct FcWgrad {
 
 __global__ void __launch_bounds__(256) fc_wgrad_reduce(const float* __restrict__ slab, int splits,
                                                        float* __restrict__ dw) {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;  // slab element (o, NHWC feature)
+    const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;  // 4 slab elements (o, NHWC feature)
     if (i >= FcWgrad::SLAB) return;
-    float t = 0.f;
-    for (int sp = 0; sp < splits; ++sp) t += slab[sp * FcWgrad::SLAB + i];
-    const int o = (int)(i / 3136), f = (int)(i - (long long)o * 3136);
-    dw[(long long)o * 3136 + fc_nchw_feature(f)] = t;
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sp = 0; sp < splits; ++sp) {
+        const float4 v = *reinterpret_cast<const float4*>(slab + sp * FcWgrad::SLAB + i);
+        t.x += v.x;
+        t.y += v.y;
+        t.z += v.z;
+        t.w += v.w;
+    }
+    const int o = (int)(i / 3136), f = (int)(i - (long long)o * 3136);  // 3136 % 4 == 0: one row
+    float* row = dw + (long long)o * 3136;
+    row[fc_nchw_feature(f)] = t.x;
+    row[fc_nchw_feature(f + 1)] = t.y;
+    row[fc_nchw_feature(f + 2)] = t.z;
+    row[fc_nchw_feature(f + 3)] = t.w;
 }
 
 extern "C" int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch) {
@@ -2402,7 +2431,7 @@ extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float*
     wa.px_per_split = ppox::ceil_div(ppox::ceil_div((long long)batch, (long long)sp), (long long)MS) * MS;
     wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB><<<(unsigned)(FcWgrad::TILES * sp), 256, 0, s>>>(wa);
     PPOX_LAUNCHED_NORET("ppox_nature_fc_wgrad");
-    fc_wgrad_reduce<<<(unsigned)ppox::ceil_div(FcWgrad::SLAB, 256LL), 256, 0, s>>>(slab, sp, dw);
+    fc_wgrad_reduce<<<(unsigned)ppox::ceil_div(FcWgrad::SLAB, 1024LL), 256, 0, s>>>(slab, sp, dw);
     PPOX_LAUNCHED("ppox_nature_fc_wgrad");
 }
 

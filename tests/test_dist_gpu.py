@@ -139,7 +139,12 @@ def test_two_ranks_match_one_rank(algo, math, batch, monkeypatch):
                 pytest.skip(f"gloo without device-tensor support on this build: {w}")
             raise AssertionError(f"rank {rank}: {w}")
         np.testing.assert_allclose(acc, acc_one, rtol=1e-4, atol=1e-6)
-        np.testing.assert_allclose(w, w_one, rtol=1e-4, atol=1e-5)
+        # per-rank batches partition every sum differently (split-K slabs, reductions), so a
+        # few weights whose Adam steps start near eps move by a fraction of lr (measured up to
+        # 0.08 lr on 9 of 2.9M); a sharding error moves most weights, and fails the 1e-4 share
+        bad = np.abs(w - w_one) > 1e-4 * np.abs(w_one) + 1e-5
+        assert bad.mean() <= 1e-4, (int(bad.sum()), w.size)
+        np.testing.assert_allclose(w, w_one, rtol=1e-4, atol=0.2 * one.lr)
         if rnd is not None:
             assert not np.array_equal(rnd_one, rnd0), "no RND update happened"
             np.testing.assert_allclose(rnd - rnd0, rnd_one - rnd0, rtol=0, atol=0.01 * one.int_lr)
