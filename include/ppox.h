@@ -399,6 +399,59 @@ int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, int64_t batch
                                      int64_t T, int64_t N_env, const float* grad_out, void* workspace,
                                      int64_t workspace_bytes, float* dw, float* db, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * K9 ICM on image observations (csrc/icm.hip): the IntrinsicCuriosityModule of
+ * models.py:270-320 with uint8 frame-stack rows of K bytes (K % 32 == 0), Discrete actions
+ * (n_actions <= 32, int32) and feature size 32.  Replaces the torch Linear / LeakyReLU /
+ * Embedding / cross_entropy / mse_loss forward + autograd of ppo.py:629-630 (collect) and
+ * ppo.py:684-699 (train).  "seg" is the ICM's parameter segment after state_encoder[0].weight:
+ * b1, W2, b2 (state_encoder), Wf1, bf1, Wf2, bf2 (forward_model), Wi1, bi1, Wi2, bi2
+ * (inverse_model), Wae (action_encoder) contiguous in that (module) order,
+ * ppox_icm_param_elems(n_actions) floats; the gradient segment has the same layout.
+ * The encoder's Linear(K, 32) runs split-bf16 (fp32-class, as K6); everything deterministic.
+ *   ppox_icm_pack_w1:    W1 (32 x K f32) -> ppox_icm_w1_pack_elems(K) bf16 planes.
+ *   ppox_icm_encode:     pre1 = x W1^T + b1, phi = leaky(pre1) W2^T + b2 for `rows` frame rows
+ *                        (idx != NULL: env-major rollout rows of the step-major (T, N_env, ...)
+ *                        frames, as ppox_nature_conv_fwd_split); rowno (nullable, uint32 per
+ *                        row) = the frame row read.  workspace: ppox_icm_encode_workspace_bytes.
+ *   ppox_icm_pair_backward: pairs (row j, row j + 1) of a minibatch of B rows with features
+ *                        phi (B x 32): the inverse / forward models, both losses (means over
+ *                        n_pairs_global pairs, weights 1 - beta / beta) and their backward.
+ *                        actions of row j: actions[rowno ? rowno[j] : j].  pairs: the first
+ *                        rows of the evaluated pairs (NULL: all j < B - 1, n_pairs = B - 1).
+ *                        dS[j] / dN[j + 1] (B x 32) = dL/dphi through a pair's first / second
+ *                        row (with pairs == NULL every row of both is written).  partials:
+ *                        ppox_icm_partials_bytes(rows, n_actions).
+ *   ppox_icm_row_backward: dphi = dS + dN (dN nullable) of minibatch row pos[i] (pos nullable)
+ *                        -> g1 = dL/dpre1 as planes (ppox_icm_g1_pack_elems(rows) uint16)
+ *                        + partials of db1, dW2, db2.
+ *   ppox_icm_grad_reduce: partials -> grad_seg (overwritten) and, loss_accum != NULL,
+ *                        loss_accum[0] += this call's share of (1 - beta) CE + beta MSE.
+ *   ppox_icm_enc_wgrad:  dW1 (32 x K, overwritten) = g1^T x over the rows read by encode.
+ *   ppox_icm_int_reward: collect: int_rewards = clamp(mean((forward_model(phi_s, a) - phi_n)^2),
+ *                        -5, 5), rewards = (1 - eta) rewards + eta int_rewards (in place). */
+int64_t ppox_icm_param_elems(int32_t n_actions);
+int64_t ppox_icm_w1_pack_elems(int64_t K);
+int ppox_icm_pack_w1(const float* w1, int64_t K, uint16_t* q, void* stream);
+int64_t ppox_icm_encode_workspace_bytes(int64_t rows, int64_t K);
+int ppox_icm_encode(const void* x, int64_t rows, const int64_t* idx, int64_t T, int64_t N_env, int64_t K,
+                    const uint16_t* q, const float* seg, void* workspace, float* pre1, float* phi, uint32_t* rowno,
+                    void* stream);
+int64_t ppox_icm_partials_bytes(int64_t rows, int32_t n_actions);
+int64_t ppox_icm_g1_pack_elems(int64_t rows);
+int ppox_icm_pair_backward(const float* phi, int64_t B, const int32_t* actions, const uint32_t* rowno,
+                           const int64_t* pairs, int64_t n_pairs, int64_t n_pairs_global, int32_t n_actions,
+                           float beta, const float* seg, float* dS, float* dN, float* partials, void* stream);
+int ppox_icm_row_backward(const float* dS, const float* dN, const int64_t* pos, int64_t rows, const float* pre1,
+                          const float* seg, int32_t n_actions, uint16_t* g1q, float* partials, void* stream);
+int ppox_icm_grad_reduce(const float* partials, int64_t rows, int64_t n_pairs, int32_t n_actions, float beta,
+                         int64_t n_pairs_global, float* grad_seg, double* loss_accum, void* stream);
+int ppox_icm_enc_wgrad(const void* x, const uint32_t* rowno, int64_t rows, int64_t K, const uint16_t* g1q,
+                       float* dw1, void* stream);
+int ppox_icm_int_reward(const float* phi_s, const float* phi_n, const int32_t* actions, int64_t N,
+                        int32_t n_actions, const float* seg, float eta, float* rewards, float* int_rewards,
+                        void* stream);
+
 #ifdef __cplusplus
 }
 #endif

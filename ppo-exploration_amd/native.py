@@ -85,6 +85,13 @@ SIGNATURES = {
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
+    "ppox_icm_pack_w1": [_vp, _i64, _vp, _vp],
+    "ppox_icm_encode": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_icm_pair_backward": [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp],
+    "ppox_icm_row_backward": [_vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _vp],
+    "ppox_icm_grad_reduce": [_vp, _i64, _i64, _i32, _f32, _i64, _vp, _vp, _vp],
+    "ppox_icm_enc_wgrad": [_vp, _vp, _i64, _i64, _vp, _vp, _vp],
+    "ppox_icm_int_reward": [_vp, _vp, _vp, _i64, _i32, _vp, _f32, _vp, _vp, _vp],
 }
 _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p,
              "ppox_rms_u8_workspace_bytes": ctypes.c_int64, "ppox_nature_wgrad_splits": ctypes.c_int64,
@@ -92,13 +99,17 @@ _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p
              "ppox_nature_wgrad_split_workspace_bytes": ctypes.c_int64,
              "ppox_es_update_workspace_bytes": ctypes.c_int64,
              "ppox_nature_fc_pack_elems": ctypes.c_int64, "ppox_head_grads_workspace_bytes": ctypes.c_int64,
-             "ppox_nature_fc_wgrad_workspace_bytes": ctypes.c_int64}
+             "ppox_nature_fc_wgrad_workspace_bytes": ctypes.c_int64, "ppox_icm_param_elems": ctypes.c_int64,
+             "ppox_icm_w1_pack_elems": ctypes.c_int64, "ppox_icm_encode_workspace_bytes": ctypes.c_int64,
+             "ppox_icm_partials_bytes": ctypes.c_int64, "ppox_icm_g1_pack_elems": ctypes.c_int64}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
                  "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32],
                  "ppox_nature_wgrad_split_workspace_bytes": [_i32, _i64],
                  "ppox_es_update_workspace_bytes": [_i64, _i64],
                  "ppox_nature_fc_pack_elems": [], "ppox_head_grads_workspace_bytes": [_i64, _i64, _i64, _i32],
-                 "ppox_nature_fc_wgrad_workspace_bytes": [_i64]}
+                 "ppox_nature_fc_wgrad_workspace_bytes": [_i64], "ppox_icm_param_elems": [_i32],
+                 "ppox_icm_w1_pack_elems": [_i64], "ppox_icm_encode_workspace_bytes": [_i64, _i64],
+                 "ppox_icm_partials_bytes": [_i64, _i32], "ppox_icm_g1_pack_elems": [_i64]}
 
 _lib = None
 
@@ -607,3 +618,67 @@ def nature_conv_wgrad_split_idx(layer, x, batch, idx, T, N_env, grad_out, worksp
 def nature_conv_dgrad_split(layer, grad_out, batch, wqd, prev_act, grad_in, stream=None):
     call("ppox_nature_conv_dgrad_split", int(layer), _p(grad_out), int(batch), _p(wqd), _p(prev_act), _p(grad_in),
          stream_ptr(stream))
+
+
+# ---------------------------------------------------------------------------
+# K9 ICM on image observations (csrc/icm.hip; see include/ppox.h)
+# ---------------------------------------------------------------------------
+def icm_param_elems(n_actions):
+    return int(load().ppox_icm_param_elems(int(n_actions)))
+
+
+def icm_w1_pack_elems(K):
+    return int(load().ppox_icm_w1_pack_elems(int(K)))
+
+
+def icm_encode_workspace_bytes(rows, K):
+    return int(load().ppox_icm_encode_workspace_bytes(int(rows), int(K)))
+
+
+def icm_partials_bytes(rows, n_actions):
+    return int(load().ppox_icm_partials_bytes(int(rows), int(n_actions)))
+
+
+def icm_g1_pack_elems(rows):
+    return int(load().ppox_icm_g1_pack_elems(int(rows)))
+
+
+def icm_pack_w1(w1, q, stream=None):
+    call("ppox_icm_pack_w1", ptr(w1, torch.float32, name="w1"), int(w1.shape[1]), ptr(q, torch.int16, name="q"),
+         stream_ptr(stream))
+
+
+def icm_encode(x, rows, idx, T, N_env, K, q, seg, workspace, pre1, phi, rowno=None, stream=None):
+    """pre1 / phi (rows x 32) of `rows` uint8 frame rows of K bytes (x contiguous rows, or the
+    step-major rollout frames read through env-major rows idx)."""
+    call("ppox_icm_encode", _p(x), int(rows), _p(idx), int(T), int(N_env), int(K), _p(q), _p(seg), _p(workspace),
+         _p(pre1), _p(phi), _p(rowno), stream_ptr(stream))
+
+
+def icm_pair_backward(phi, B, actions, rowno, pairs, n_pairs, n_pairs_global, n_actions, beta, seg, dS, dN,
+                      partials, stream=None):
+    call("ppox_icm_pair_backward", _p(phi), int(B), ptr(actions, torch.int32, name="actions"), _p(rowno), _p(pairs),
+         int(n_pairs), int(n_pairs_global), int(n_actions), float(beta), _p(seg), _p(dS), _p(dN), _p(partials),
+         stream_ptr(stream))
+
+
+def icm_row_backward(dS, dN, pos, rows, pre1, seg, n_actions, g1q, partials, stream=None):
+    call("ppox_icm_row_backward", _p(dS), _p(dN), _p(pos), int(rows), _p(pre1), _p(seg), int(n_actions), _p(g1q),
+         _p(partials), stream_ptr(stream))
+
+
+def icm_grad_reduce(partials, rows, n_pairs, n_actions, beta, n_pairs_global, grad_seg, loss_accum=None,
+                    stream=None):
+    call("ppox_icm_grad_reduce", _p(partials), int(rows), int(n_pairs), int(n_actions), float(beta),
+         int(n_pairs_global), _p(grad_seg), ptr(loss_accum, torch.float64, name="loss_accum"), stream_ptr(stream))
+
+
+def icm_enc_wgrad(x, rowno, rows, K, g1q, dw1, stream=None):
+    call("ppox_icm_enc_wgrad", _p(x), ptr(rowno, torch.int32, name="rowno"), int(rows), int(K), _p(g1q),
+         ptr(dw1, torch.float32, name="dw1"), stream_ptr(stream))
+
+
+def icm_int_reward(phi_s, phi_n, actions, N, n_actions, seg, eta, rewards, int_rewards, stream=None):
+    call("ppox_icm_int_reward", _p(phi_s), _p(phi_n), ptr(actions, torch.int32, name="actions"), int(N),
+         int(n_actions), _p(seg), float(eta), ptr(rewards, torch.float32, name="rewards"),
+         ptr(int_rewards, torch.float32, name="int_rewards"), stream_ptr(stream))

@@ -31,6 +31,7 @@ import torch.nn.functional as F
 import logger
 import native
 import convs
+import icm as icm_native
 from buffer import IntrinsicStorage, RolloutStorage
 from dist import DistContext, owned_minibatch_indices, owned_minibatch_positions, shard_range
 from env import DeviceAtariEnv, make_env
@@ -715,6 +716,12 @@ class PPO_ICM(BaseAlgorithm):
         self._attach_convs()
         self.icm_flat = FlatParams(self.intrinsic_module, self.device)
         self.optimizer, self.icm_optimizer = self.flat, self.icm_flat
+        # image observations: the ICM on libppox kernels (icm.py, csrc/icm.hip); PPOX_ICM_NATIVE=0
+        # keeps the torch module (A/B, tests)
+        self._icm_native = None
+        if os.environ.get("PPOX_ICM_NATIVE", "1") != "0" and icm_native.supported(
+                self.intrinsic_module, self.icm_flat, self.env.observation_space.shape, self.rollout.obs_slots.dtype):
+            self._icm_native = icm_native.NativeIcm(self.intrinsic_module, self.icm_flat, icm_in)
         self.int_lr = int_lr
         self.policy_weight = policy_weight
         self.beta = 0.2
@@ -737,6 +744,7 @@ class PPO_ICM(BaseAlgorithm):
         eta = self.int_rew_integration
         icm = self.intrinsic_module
         f_next = None  # phi(s_{t+1}) of the previous step = phi(s_t) of this one (same rows, same math)
+        nat = self._icm_native
         for t in range(self.nstep):
             with torch.no_grad():
                 out, v, _ = net(ro.obs_slots[t])
@@ -745,6 +753,15 @@ class PPO_ICM(BaseAlgorithm):
             self.env.step_into(ro.obs_slots[t], ro.obs_slots[t + 1], ro.actions[t], ro.rewards[t], ro.masks[t],
                                ro.done_ret[t], ro.done_len[t])
             self.num_timesteps += self.num_envs
+            if nat is not None:  # ppo.py:629-631 on K9: encoder + forward model + reward mix, 3 launches
+                if f_next is None:
+                    f_next = nat.encode(ro.obs_slots[t], "c0")[1]
+                f = f_next
+                f_next = nat.encode(ro.obs_slots[t + 1], "c1" if t % 2 == 0 else "c0")[1]
+                ir = nat._buf("ir", (self.local_envs,))
+                nat.int_reward(f, f_next, ro.actions[t], ro.rewards[t], eta, ir)
+                ir_sum += ir.double().mean()
+                continue
             with torch.no_grad():                                              # ppo.py:629-630
                 f = icm.state_encoder(self._icm_x(ro.obs_slots[t])) if f_next is None else f_next
                 f_next = icm.state_encoder(self._icm_x(ro.obs_slots[t + 1]))
@@ -774,6 +791,9 @@ class PPO_ICM(BaseAlgorithm):
             for k, B in enumerate(sizes):
                 idx = local[offs[k]:offs[k + 1]]
                 Bl = idx.numel()
+                if self._icm_native is not None:
+                    self._minibatch_native_icm(idx, stats[k], B, roll, offs[k], offs[k + 1])
+                    continue
                 self._zero_policy_grad(Bl)
                 self.icm_flat.zero_grad()
                 obs = ro._gather(ro.observations, idx)
@@ -807,6 +827,28 @@ class PPO_ICM(BaseAlgorithm):
         acc = self._record_train(extra=icm_mean)
         logger.record("train/icm_loss", icm_mean / max(acc[5], 1.0))
         self._n_updates += self.n_epochs
+
+    def _minibatch_native_icm(self, idx, adv_stats, B, roll, o0, o1):
+        """One minibatch with the ICM on K9 kernels: the policy as PPO's minibatch (rollout rows
+        read in place, overlapped gradient all-reduce), then the ICM loss of the same rows
+        (ppo.py:684-688) straight off the rollout frames, its all-reduce and both Adam steps."""
+        ro = self.rollout
+        Bl = idx.numel()
+        self._zero_policy_grad(Bl)
+        ctx = out = v = None
+        if Bl > 0:
+            out, v, _, ctx = self._fwd_train(self._train_obs(ro, idx))
+            od, vd = out.detach().contiguous(), v.detach().contiguous()
+        else:
+            od, vd, _ = self._empty_outputs()
+        dout, dv, _ = self._loss_grads(od, vd, None, idx, roll, adv_stats, B, 0.0, float(self.policy_weight))
+        self._bwd_reduce(ctx, out, v, None, dout, dv, has_rows=Bl > 0)
+        pos = self._epoch_pos[o0:o1] if self.dist.enabled else None
+        self._icm_native.train_minibatch(convs.RolloutRows(ro.observations, idx), ro.actions, pos, B, self.beta,
+                                         self.dist, self.icm_accum)
+        self.dist.all_reduce_(self.icm_flat.grad)
+        self.flat.adam_step(self.lr, self.max_grad_norm)                       # ppo.py:697-698
+        self.icm_flat.adam_step(self.int_lr, None)                             # ppo.py:699 (no clipping)
 
     def learn(self, total_timesteps, log_interval=5, reward_target=None, log_to_file=False):
         return self._learn("ICM", total_timesteps, log_interval, reward_target, log_to_file, progress=True)

@@ -54,3 +54,34 @@ def test_argument_validation_without_gpu():
     rc = lib.ppox_gae(None, None, None, None, None, 0, 4, 0.99, 0.95, None, None, None)
     assert rc == -1000
     assert b"must be positive" in lib.ppox_last_error()
+
+
+def test_icm_segment_layout_matches_module():
+    """icm.supported(): the K9 kernels' parameter segment (ppox_icm_param_elems, include/ppox.h)
+    is the module's parameters after state_encoder[0].weight, contiguous in module order."""
+    if not os.path.exists(native.LIB_PATH):
+        pytest.skip("libppox.so not built")
+    import torch
+
+    import icm
+    from env import Box, Discrete
+    from models import FlatParams, IntrinsicCuriosityModule
+    from util import ActionConverter
+    K = 2048
+    for A in (1, 4, 18, 32):
+        m = IntrinsicCuriosityModule(K, ActionConverter(Discrete(A)), 32)
+        flat = FlatParams(m, "cpu")
+        assert flat.n == 32 * K + native.icm_param_elems(A)
+        assert icm.supported(m, flat, (K,), torch.uint8)
+        assert not icm.supported(m, flat, (K,), torch.float32)
+    assert native.icm_param_elems(33) == -1
+    m = IntrinsicCuriosityModule(K, ActionConverter(Discrete(40)), 32)
+    assert not icm.supported(m, FlatParams(m, "cpu"), (K,), torch.uint8)
+    m = IntrinsicCuriosityModule(K, ActionConverter(Discrete(4)), 64)
+    assert not icm.supported(m, FlatParams(m, "cpu"), (K,), torch.uint8)
+    m = IntrinsicCuriosityModule(K, ActionConverter(Box((3,))), 32)
+    assert not icm.supported(m, FlatParams(m, "cpu"), (K,), torch.uint8)
+    m = IntrinsicCuriosityModule(2000, ActionConverter(Discrete(4)), 32)
+    assert not icm.supported(m, FlatParams(m, "cpu"), (2000,), torch.uint8)
+    assert native.icm_w1_pack_elems(2000) == -1 and native.icm_w1_pack_elems(K) == 3 * 32 * K
+    assert native.icm_encode_workspace_bytes(2048, 4 * 84 * 84) > 0

@@ -1,0 +1,187 @@
+"""K9 ICM kernels (csrc/icm.hip, ppo-exploration_amd/icm.py) vs a float64 torch autograd of
+the reference module (models.py:270-320) and loss (ppo.py:684-688); and PPO_ICM on the
+kernels vs PPO_ICM on the torch module (PPOX_ICM_NATIVE=0).  GPU box only.
+
+Tolerances: the encoder's Linear(K, 32) runs split-bf16 (every product exact, f32
+accumulation), so its error vs fp64 is held to that of torch's own f32 GEMM (x2) on the same
+rows; gradients / losses are compared against fp64 with a per-tensor bound (2e-5 of the
+tensor's largest entry — fp32-class: the f32 product-sum errors, not bf16's 4e-3)."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+K_ATARI = 4 * 84 * 84
+
+
+def _module(K, A, seed):
+    from env import Discrete
+    from models import FlatParams, IntrinsicCuriosityModule
+    from util import ActionConverter
+    torch.manual_seed(seed)
+    icm = IntrinsicCuriosityModule(K, ActionConverter(Discrete(A)), 32)
+    ref = copy.deepcopy(icm).double()
+    flat = FlatParams(icm, "cuda")
+    return icm, ref, flat
+
+
+def _native(icm, flat, K):
+    import icm as icm_native
+    assert icm_native.supported(icm, flat, (K,), torch.uint8)
+    return icm_native.NativeIcm(icm, flat, K)
+
+
+def _frames(M, K, seed):
+    g = np.random.default_rng(seed)
+    return g.integers(0, 256, size=(M, K), dtype=np.uint8)
+
+
+def _ref_grads(ref):
+    return [p.grad.detach().numpy().reshape(-1) for p in ref.parameters()]
+
+
+@pytest.mark.parametrize("M", [1, 33, 512, 1000, 2048, 4100])
+def test_encode_vs_fp64(M):
+    K, A = K_ATARI, 4
+    icm, ref, flat = _module(K, A, 3)
+    nat = _native(icm, flat, K)
+    x = _frames(M, K, M)
+    xd = torch.from_numpy(x).cuda()
+    pre1, phi = nat.encode(xd)
+    x64 = torch.from_numpy(x).double()
+    with torch.no_grad():
+        pre_ref = ref.state_encoder[0](x64)
+        phi_ref = ref.state_encoder(x64)
+        pre_f32 = F.linear(xd.float(), icm.state_encoder[0].weight, icm.state_encoder[0].bias).cpu().double()
+    e_ours = (pre1.cpu().double() - pre_ref).abs().max().item()
+    e_f32 = (pre_f32 - pre_ref).abs().max().item()
+    assert e_ours <= max(2 * e_f32, 1e-6 * pre_ref.abs().max().item()), (e_ours, e_f32)
+    scale = phi_ref.abs().max().item()
+    np.testing.assert_allclose(phi.cpu().double().numpy(), phi_ref.numpy(), rtol=0, atol=1e-5 * scale)
+
+
+def test_encode_rollout_rows_equal_gathered():
+    """RolloutRows (env-major idx into step-major frames) read in place == the gathered rows."""
+    import convs
+    K, A, T, N = K_ATARI, 6, 8, 24
+    icm, _, flat = _module(K, A, 4)
+    nat = _native(icm, flat, K)
+    g = torch.Generator().manual_seed(1)
+    frames = torch.randint(0, 256, (T, N, 4, 84, 84), dtype=torch.uint8, generator=g).cuda()
+    idx = torch.randperm(T * N, generator=g)[:100].cuda()
+    rows = (idx % T) * N + idx // T
+    _, phi_r, rn = nat.encode(convs.RolloutRows(frames, idx), "a", rowno=True)
+    _, phi_g = nat.encode(frames.reshape(T * N, K)[rows].contiguous(), "b")
+    assert torch.equal(phi_r, phi_g)
+    assert torch.equal(rn.long(), rows)
+
+
+def _minibatch(K, A, B, seed, beta=0.2):
+    icm, ref, flat = _module(K, A, seed)
+    nat = _native(icm, flat, K)
+    x = _frames(B, K, seed + 100)
+    acts = np.random.default_rng(seed).integers(0, A, size=B).astype(np.int32)
+    acc = torch.zeros(1, dtype=torch.float64, device="cuda")
+
+    class One:
+        enabled = False
+    flat.grad.fill_(float("nan"))  # every gradient must be written
+    nat.train_minibatch(torch.from_numpy(x).cuda(), torch.from_numpy(acts).cuda(), None, B, beta, One(), acc)
+    ours = flat.grad[:flat.n].cpu().double().numpy()
+    # fp64 reference: ppo.py:684-688 on the same rows
+    x64 = torch.from_numpy(x).double()
+    a = torch.from_numpy(acts).long()
+    phi = ref.state_encoder(x64)
+    s, n, a0 = phi[:-1], phi[1:], a[:-1]
+    ahat = ref.inverse_model(torch.cat((s, n), 1))
+    nhat = ref.forward_model(torch.cat((s, ref.action_encoder(a0)), 1))
+    loss = (1 - beta) * F.cross_entropy(ahat, a0) + beta * F.mse_loss(nhat, n)
+    loss.backward()
+    return ours, _ref_grads(ref), [p.numel() for p in ref.parameters()], acc.item(), loss.item(), flat
+
+
+@pytest.mark.parametrize("K,A,B", [(K_ATARI, 4, 2048), (K_ATARI, 4, 33), (K_ATARI, 18, 300), (2048, 9, 2)])
+def test_minibatch_grads_vs_fp64(K, A, B):
+    ours, ref, sizes, loss, loss_ref, _ = _minibatch(K, A, B, 7)
+    assert np.isfinite(ours).all()
+    off = 0
+    names = ["W1", "b1", "W2", "b2", "Wf1", "bf1", "Wf2", "bf2", "Wi1", "bi1", "Wi2", "bi2", "Wae"]
+    for name, g_ref, k in zip(names, ref, sizes):
+        g = ours[off:off + k]
+        off += k
+        scale = max(np.abs(g_ref).max(), 1e-30)
+        err = np.abs(g - g_ref).max()
+        assert err <= 2e-5 * scale, (name, err, scale)
+    np.testing.assert_allclose(loss, loss_ref, rtol=1e-5)
+
+
+def test_minibatch_one_row_has_no_pairs():
+    """B = 1 (the last minibatch of an uneven split): no pairs -> zero gradients everywhere;
+    the loss is the reference's mean over zero pairs (nan)."""
+    ours, _, _, loss, _, _ = _minibatch(2048, 4, 1, 9)
+    assert (ours == 0).all()
+    assert np.isnan(loss)
+
+
+def test_minibatch_deterministic():
+    a = _minibatch(K_ATARI, 4, 2048, 11)[0]
+    b = _minibatch(K_ATARI, 4, 2048, 11)[0]
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("N,A", [(512, 4), (77, 18)])
+def test_int_reward_vs_fp64(N, A):
+    """ppo.py:629-631: int_reward(s, s', a) = clamp(mean((fwd(phi(s), a) - phi(s'))^2), -5, 5),
+    rewards <- (1 - eta) rewards + eta int_reward."""
+    K, eta = K_ATARI, 0.05
+    icm, ref, flat = _module(K, A, 5)
+    nat = _native(icm, flat, K)
+    s, s2 = _frames(N, K, 1), _frames(N, K, 2)
+    acts = np.random.default_rng(3).integers(0, A, size=N).astype(np.int32)
+    rew = np.random.default_rng(4).random(N).astype(np.float32)
+    phs = nat.encode(torch.from_numpy(s).cuda(), "s")[1]
+    phn = nat.encode(torch.from_numpy(s2).cuda(), "n")[1]
+    r = torch.from_numpy(rew).cuda()
+    ir = torch.empty(N, device="cuda")
+    nat.int_reward(phs, phn, torch.from_numpy(acts).cuda(), r, eta, ir)
+    with torch.no_grad():
+        ir_ref = ref.int_reward(torch.from_numpy(s).double(), torch.from_numpy(s2).double(),
+                                torch.from_numpy(acts).long()).numpy()
+    np.testing.assert_allclose(ir.cpu().numpy(), ir_ref, rtol=1e-4, atol=1e-6 * max(1.0, np.abs(ir_ref).max()))
+    np.testing.assert_allclose(r.cpu().numpy(), (1 - eta) * rew + eta * ir_ref, rtol=1e-5, atol=1e-6)
+
+
+def test_ppo_icm_native_matches_torch_module(monkeypatch):
+    """PPO_ICM (Breakout frames) collect + train with the ICM on K9 vs on the torch module:
+    same rollout rewards (int rewards mixed in) and ICM weights within fp32-class tolerance."""
+    import logger
+    import ppo
+    cfg = dict(env_id="BreakoutNoFrameskip-v4", n_envs=8, nstep=16, batch_size=40, n_epochs=2, seed=3, quiet=True)
+    logger.configure("ICM", "BreakoutNoFrameskip-v4", quiet=True)
+    runs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PPOX_ICM_NATIVE", flag)
+        np.random.seed(5)
+        torch.manual_seed(5)
+        alg = ppo.PPO_ICM(**cfg)
+        assert (alg._icm_native is not None) == (flag == "1")
+        alg.collect_samples()
+        rew = alg.rollout.rewards.cpu().numpy().copy()
+        alg.train()
+        runs.append((rew, alg.icm_flat.data[:alg.icm_flat.n].cpu().numpy(), alg.icm_accum.item(),
+                     alg.flat.data[:alg.flat.n].cpu().numpy()))
+    (r1, w1, l1, p1), (r0, w0, l0, p0) = runs
+    np.testing.assert_allclose(r1, r0, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(l1, l0, rtol=1e-4)
+    # Adam normalises each weight's step: near-zero gradients can land an lr-sized step
+    # apart, so the bulk is held to rtol 1e-4 and at most 1e-4 of the weights may differ more
+    bad = np.abs(w1 - w0) > 1e-4 * np.abs(w0) + 1e-5
+    assert bad.mean() <= 1e-4, (int(bad.sum()), w1.size)
+    # and no weight further apart than every Adam step (lr 3e-4, 2 epochs x 4 minibatches) in opposite directions
+    np.testing.assert_allclose(w1, w0, rtol=1e-4, atol=2 * 3e-4 * 8)
+    bad = np.abs(p1 - p0) > 1e-4 * np.abs(p0) + 1e-5
+    assert bad.mean() <= 1e-4, (int(bad.sum()), p1.size)
