@@ -61,6 +61,24 @@ class MlpNetwork(nn.Module):
         return self.actor(x), self.critic(x).squeeze(-1), iv
 
 
+# dW = d^T x of the 512-wide hidden layers: split-K (WGRAD_SPLIT row chunks as one batched
+# GEMM + an ordered sum) from WGRAD_SPLIT_MIN rows — the single GEMM has only 64 output tiles
+# of 64x64 for a 512x512 result and leaves most CUs idle over K = 16384 rows (tools/
+# gemm_split_probe.py: 104 -> 67 us at 16384 rows, no gain at 2048)
+WGRAD_SPLIT, WGRAD_SPLIT_MIN = 8, 8192
+
+
+def weight_grad(d, x, out, part=None):
+    """out = d^T x (rows summed), d (B, m), x (B, n) contiguous; part: (WGRAD_SPLIT, m, n) scratch."""
+    B = d.shape[0]
+    if B >= WGRAD_SPLIT_MIN and B % WGRAD_SPLIT == 0 and part is not None:
+        S = WGRAD_SPLIT
+        torch.bmm(d.view(S, B // S, d.shape[1]).transpose(1, 2), x.view(S, B // S, x.shape[1]), out=part)
+        torch.sum(part, 0, out=out)
+    else:
+        torch.mm(d.t(), x, out=out)
+
+
 def linear_relu(x, weight, bias):
     """relu(x W^T + b) as one library GEMM with a bias+ReLU epilogue (hipBLASLt through
     torch._addmm_activation: bitwise equal to addmm().relu_(), one launch instead of two)."""
@@ -148,6 +166,13 @@ class CnnActorCritic(nn.Module):
             self._fcg = buf
         return buf
 
+    def _wgrad_part(self, w):
+        buf = getattr(self, "_wgp", None)
+        if buf is None or buf.device != w.device:
+            buf = torch.empty((WGRAD_SPLIT,) + tuple(w.shape), device=w.device)
+            self._wgp = buf
+        return buf
+
     def _fc_wgrad_ws(self, rows):
         need = native.nature_fc_wgrad_workspace_bytes(rows)
         ws = getattr(self, "_fcw_ws", None)
@@ -183,7 +208,7 @@ class CnnActorCritic(nn.Module):
                 d = d.contiguous().view(B, 1)
                 de = torch.empty_like(act)
                 native.outer_relu_backward(d, crit.weight, act, de)     # dv * w, ReLU backward
-                torch.mm(de.t(), f, out=hid.weight.grad)
+                weight_grad(de, f, hid.weight.grad, self._wgrad_part(hid.weight))
                 df.addmm_(de, hid.weight)
                 des.append((de, d))
             native.relu_backward_(df, f)

@@ -590,9 +590,10 @@ class PPO_RND(BaseAlgorithm):
         self._alloc_train_state()
 
     def _rnd_input(self, obs):
-        """(N, F) view of the features RND sees: last frame (image) or the obs vector."""
+        """(N, F) view of the features RND sees: last frame (image) or the obs vector (rows of
+        _rnd_rows hold the last frame only)."""
         if self.image:
-            return obs[:, 3].reshape(obs.shape[0], -1)
+            return obs[:, obs.shape[1] - 1].reshape(obs.shape[0], -1)
         return obs.reshape(obs.shape[0], -1)
 
     @traced("collect")
@@ -623,6 +624,19 @@ class PPO_RND(BaseAlgorithm):
         ro.compute_returns_and_advantages(ro.values[T1], ro.int_values[T1], ro.masks[T1])
         self._finish_episodes()
         return True
+
+    def _rnd_rows(self, ro, idx):
+        """The minibatch rows RND trains on: on images only their last frame is gathered (7 KB
+        of each 28 KB frame stack; the policy reads its rows in place), else the whole rows."""
+        if not self.image:
+            return ro._gather(ro.observations, idx)
+        obs = ro.observations
+        T, N = obs.shape[0], obs.shape[1]
+        last = obs[:, :, 3]  # (T, N, 84, 84) view, frame stacks 4 * 7056 bytes apart
+        out = torch.empty((idx.numel(), 1) + tuple(last.shape[2:]), dtype=obs.dtype, device=self.device)
+        native.gather_rows(last, T, N, last[0, 0].numel() * last.element_size(), obs[0, 0].numel() * obs.element_size(),
+                           idx, idx.numel(), out)
+        return out
 
     def _update_obs_rms(self, x):
         if not self.dist.enabled:
@@ -675,10 +689,9 @@ class PPO_RND(BaseAlgorithm):
                 idx = local[offs[k]:offs[k + 1]]
                 Bl = idx.numel()
                 self._zero_policy_grad(Bl)
-                obs = ctx = out = v = iv = None
+                ctx = out = v = iv = None
                 if Bl > 0:
-                    obs = ro._gather(ro.observations, idx)
-                    out, v, iv, ctx = self._fwd_train(obs)
+                    out, v, iv, ctx = self._fwd_train(self._train_obs(ro, idx))
                     od, vd, ivd = out.detach().contiguous(), v.detach().contiguous(), iv.detach().contiguous()
                 else:  # no rows of this minibatch on this rank: zero contributions, same collectives
                     od, vd, ivd = self._empty_outputs(intrinsic=True)
@@ -686,7 +699,7 @@ class PPO_RND(BaseAlgorithm):
                 self._bwd_reduce(ctx, out, v, iv, dout, dv, div, has_rows=Bl > 0)
                 self.flat.adam_step(self.lr, self.max_grad_norm)
                 if np.random.randn() < 0.25:                                   # ppo.py:468-469
-                    self.train_rnd(obs, B)
+                    self.train_rnd(self._rnd_rows(ro, idx) if Bl > 0 else None, B)
         acc = self._record_train()
         logger.record("train/intrinsic_loss", acc[4] / max(acc[5], 1.0))
         self._n_updates += self.n_epochs
