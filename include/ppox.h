@@ -400,7 +400,7 @@ int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, int64_t batch
                                      int64_t workspace_bytes, float* dw, float* db, void* stream);
 
 /* ---------------------------------------------------------------------------
- * K9 ICM on image observations (csrc/icm.hip): the IntrinsicCuriosityModule of
+ * K11 ICM on image observations (csrc/icm.hip): the IntrinsicCuriosityModule of
  * models.py:270-320 with uint8 frame-stack rows of K bytes (K % 32 == 0), Discrete actions
  * (n_actions <= 32, int32) and feature size 32.  Replaces the torch Linear / LeakyReLU /
  * Embedding / cross_entropy / mse_loss forward + autograd of ppo.py:629-630 (collect) and

@@ -1,4 +1,4 @@
-// K9 — the Intrinsic Curiosity Module of PPO_ICM on image observations (reference
+// K11 — the Intrinsic Curiosity Module of PPO_ICM on image observations (reference
 // models.py:270-320 IntrinsicCuriosityModule, ppo.py:629-630 int_reward in collect,
 // ppo.py:684-699 the ICM loss / backward in train), for uint8 frame stacks, Discrete
 // actions and the feature size 32 (int_hidden_size).

@@ -1,4 +1,4 @@
-"""PPO_ICM's Intrinsic Curiosity Module on libppox (K9, csrc/icm.hip) for image observations.
+"""PPO_ICM's Intrinsic Curiosity Module on libppox (K11, csrc/icm.hip) for image observations.
 
 The reference's module (models.py:270-320) is a torch MLP trained by autograd
 (ppo.py:684-699) and evaluated per collect step (ppo.py:629-630).  On Atari frames

@@ -621,7 +621,7 @@ def nature_conv_dgrad_split(layer, grad_out, batch, wqd, prev_act, grad_in, stre
 
 
 # ---------------------------------------------------------------------------
-# K9 ICM on image observations (csrc/icm.hip; see include/ppox.h)
+# K11 ICM on image observations (csrc/icm.hip; see include/ppox.h)
 # ---------------------------------------------------------------------------
 def icm_param_elems(n_actions):
     return int(load().ppox_icm_param_elems(int(n_actions)))

@@ -766,7 +766,7 @@ class PPO_ICM(BaseAlgorithm):
             self.env.step_into(ro.obs_slots[t], ro.obs_slots[t + 1], ro.actions[t], ro.rewards[t], ro.masks[t],
                                ro.done_ret[t], ro.done_len[t])
             self.num_timesteps += self.num_envs
-            if nat is not None:  # ppo.py:629-631 on K9: encoder + forward model + reward mix, 3 launches
+            if nat is not None:  # ppo.py:629-631 on K11: encoder + forward model + reward mix, 3 launches
                 if f_next is None:
                     f_next = nat.encode(ro.obs_slots[t], "c0")[1]
                 f = f_next
@@ -842,7 +842,7 @@ class PPO_ICM(BaseAlgorithm):
         self._n_updates += self.n_epochs
 
     def _minibatch_native_icm(self, idx, adv_stats, B, roll, o0, o1):
-        """One minibatch with the ICM on K9 kernels: the policy as PPO's minibatch (rollout rows
+        """One minibatch with the ICM on K11 kernels: the policy as PPO's minibatch (rollout rows
         read in place, overlapped gradient all-reduce), then the ICM loss of the same rows
         (ppo.py:684-688) straight off the rollout frames, its all-reduce and both Adam steps."""
         ro = self.rollout

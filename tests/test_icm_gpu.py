@@ -1,4 +1,4 @@
-"""K9 ICM kernels (csrc/icm.hip, ppo-exploration_amd/icm.py) vs a float64 torch autograd of
+"""K11 ICM kernels (csrc/icm.hip, ppo-exploration_amd/icm.py) vs a float64 torch autograd of
 the reference module (models.py:270-320) and loss (ppo.py:684-688); and PPO_ICM on the
 kernels vs PPO_ICM on the torch module (PPOX_ICM_NATIVE=0).  GPU box only.
 
@@ -156,7 +156,7 @@ def test_int_reward_vs_fp64(N, A):
 
 
 def test_ppo_icm_native_matches_torch_module(monkeypatch):
-    """PPO_ICM (Breakout frames) collect + train with the ICM on K9 vs on the torch module:
+    """PPO_ICM (Breakout frames) collect + train with the ICM on K11 vs on the torch module:
     same rollout rewards (int rewards mixed in) and ICM weights within fp32-class tolerance."""
     import logger
     import ppo
