@@ -49,6 +49,36 @@ FC_DGRAD_FUSED_MAX_BATCH = int(os.environ.get("PPOX_FC_DGRAD_FUSED_MAX", str(1 <
 FC_WGRAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_WGRAD_SPLIT_MIN", "0"))
 
 
+# backward on two streams: each layer's weight gradient runs on a side stream beside the
+# main stream's dgrad chain (wgrad3 || dgrad3, wgrad2 || dgrad2; the fc weight gradient ||
+# the fc dgrad), joined before the optimizer reads the gradients (PPOX_BWD_STREAMS=0: one stream)
+BWD_STREAMS = os.environ.get("PPOX_BWD_STREAMS", "1") != "0"
+_side = {}
+
+
+def side_stream(device):
+    """The side stream of `device` for the concurrent weight-gradient kernels (one per device)."""
+    s = _side.get(device)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _side[device] = s
+    return s
+
+
+def fork(side):
+    """side waits for everything enqueued so far on the current stream."""
+    ev = torch.cuda.Event()
+    ev.record()
+    side.wait_event(ev)
+
+
+def join(side):
+    """The current stream waits for everything enqueued so far on side."""
+    ev = torch.cuda.Event()
+    ev.record(side)
+    torch.cuda.current_stream().wait_event(ev)
+
+
 def default_math():
     m = os.environ.get("PPOX_CONV_MATH", "split")
     if m not in MATHS:
@@ -274,13 +304,26 @@ class NatureConvs:
         if g3 is None:
             g3 = torch.empty((B, 7, 7, 64), device=dev)
             native.nchw_to_nhwc_relu_grad(dh3, h3, B, g3)      # ReLU backward of conv3, to NHWC
-        self.wgrad(3, h2, B, g3, dw3, db3)
+        side = side_stream(dev) if BWD_STREAMS and dev.type == "cuda" else None
+        if side is None:
+            self.wgrad(3, h2, B, g3, dw3, db3)
+        else:  # wgrad3 beside dgrad3 (the tensors stay referenced until the join below)
+            fork(side)
+            with torch.cuda.stream(side):
+                self.wgrad(3, h2, B, g3, dw3, db3)
         g2 = torch.empty((B, 9, 9, 64), device=dev)
         self.dgrad(3, g3, B, h2, g2)                            # dX of conv3, times ReLU'(conv2)
-        self.wgrad(2, h1, B, g2, dw2, db2)
+        if side is None:
+            self.wgrad(2, h1, B, g2, dw2, db2)
+        else:
+            fork(side)
+            with torch.cuda.stream(side):
+                self.wgrad(2, h1, B, g2, dw2, db2)
         g1 = torch.empty((B, 20, 20, 32), device=dev)
         self.dgrad(2, g2, B, h1, g1)                            # dX of conv2, times ReLU'(conv1)
         self.wgrad(1, x, B, g1, dw1, db1)
+        if side is not None:
+            join(side)
 
     def __call__(self, x):
         if x.dtype != torch.uint8:

@@ -214,14 +214,6 @@ class CnnActorCritic(nn.Module):
             native.relu_backward_(df, f)
             cv = self.conv_impl
             import convs as _convs
-            if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-bf16 kernel, Flatten-order dW
-                native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad)
-            elif cv.nhwc3:  # NHWC features: library GEMM in NHWC order, permuted back to Flatten order
-                dwp = self._fc_grad_buf(fc.weight)
-                torch.mm(df.t(), hf, out=dwp)
-                fc.weight.grad.view(fc.weight.shape[0], 64, 49).copy_(dwp.view(-1, 49, 64).transpose(1, 2))
-            else:
-                torch.mm(df.t(), hf, out=fc.weight.grad)
             # every column-reduction gradient (actor W/b, critic W/b, extra-layer b, fc b) in one pass
             ws = self._head_ws(B, f.shape[1], dout.shape[1])
             (de, d), intr = des[0], des[1] if self.intrinsic else (None, None)
@@ -231,8 +223,30 @@ class CnnActorCritic(nn.Module):
                               w_critic_int=self.critic_int.weight.grad if self.intrinsic else None,
                               b_critic_int=self.critic_int.bias.grad if self.intrinsic else None,
                               b_int_extra=self.int_extra_layer[0].bias.grad if self.intrinsic else None)
-            if dense_ready is not None:
-                dense_ready()
+            side = _convs.side_stream(df.device) if _convs.BWD_STREAMS and df.is_cuda else None
+            if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-bf16 kernel, Flatten-order dW
+                if side is None:
+                    native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad)
+                    if dense_ready is not None:
+                        dense_ready()
+                else:
+                    # on the side stream, beside the fc dgrad and the conv backward; the dense
+                    # gradients' all-reduce is started from there (ordered after it and, through the
+                    # fork, after every head gradient); backward_acts joins the side stream
+                    _convs.fork(side)
+                    with torch.cuda.stream(side):
+                        native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad)
+                        if dense_ready is not None:
+                            dense_ready()
+            else:
+                if cv.nhwc3:  # NHWC features: library GEMM in NHWC order, permuted back to Flatten order
+                    dwp = self._fc_grad_buf(fc.weight)
+                    torch.mm(df.t(), hf, out=dwp)
+                    fc.weight.grad.view(fc.weight.shape[0], 64, 49).copy_(dwp.view(-1, 49, 64).transpose(1, 2))
+                else:
+                    torch.mm(df.t(), hf, out=fc.weight.grad)
+                if dense_ready is not None:
+                    dense_ready()
             fe = self.feature_extractor
             if cv.nhwc3 and B < _convs.FC_DGRAD_FUSED_MAX_BATCH:  # masked NHWC grad directly
                 dh3, g3 = None, cv.fc_dgrad_g3(df, h3)
