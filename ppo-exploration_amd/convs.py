@@ -56,12 +56,13 @@ BWD_STREAMS = os.environ.get("PPOX_BWD_STREAMS", "1") != "0"
 _side = {}
 
 
-def side_stream(device):
-    """The side stream of `device` for the concurrent weight-gradient kernels (one per device)."""
-    s = _side.get(device)
+def side_stream(device, k=0):
+    """Side stream k of `device` (0: the concurrent weight-gradient kernels; 1: PPO_ICM's
+    curiosity-module work beside the policy minibatch)."""
+    s = _side.get((device, k))
     if s is None:
         s = torch.cuda.Stream(device=device)
-        _side[device] = s
+        _side[(device, k)] = s
     return s
 
 

@@ -847,6 +847,16 @@ class PPO_ICM(BaseAlgorithm):
         (ppo.py:684-688) straight off the rollout frames, its all-reduce and both Adam steps."""
         ro = self.rollout
         Bl = idx.numel()
+        # the ICM (independent of the policy: its own parameters, the same frames) runs on a
+        # side stream beside the policy's forward / loss / backward (one process; with ranks
+        # its collectives keep the program order on every rank, so it stays on this stream)
+        side = convs.side_stream(self.device, 1) if convs.BWD_STREAMS and not self.dist.enabled else None
+        pos = self._epoch_pos[o0:o1] if self.dist.enabled else None
+        if side is not None:
+            convs.fork(side)
+            with torch.cuda.stream(side):
+                self._icm_native.train_minibatch(convs.RolloutRows(ro.observations, idx), ro.actions, pos, B,
+                                                 self.beta, self.dist, self.icm_accum)
         self._zero_policy_grad(Bl)
         ctx = out = v = None
         if Bl > 0:
@@ -856,9 +866,11 @@ class PPO_ICM(BaseAlgorithm):
             od, vd, _ = self._empty_outputs()
         dout, dv, _ = self._loss_grads(od, vd, None, idx, roll, adv_stats, B, 0.0, float(self.policy_weight))
         self._bwd_reduce(ctx, out, v, None, dout, dv, has_rows=Bl > 0)
-        pos = self._epoch_pos[o0:o1] if self.dist.enabled else None
-        self._icm_native.train_minibatch(convs.RolloutRows(ro.observations, idx), ro.actions, pos, B, self.beta,
-                                         self.dist, self.icm_accum)
+        if side is None:
+            self._icm_native.train_minibatch(convs.RolloutRows(ro.observations, idx), ro.actions, pos, B,
+                                             self.beta, self.dist, self.icm_accum)
+        else:
+            convs.join(side)
         self.dist.all_reduce_(self.icm_flat.grad)
         self.flat.adam_step(self.lr, self.max_grad_norm)                       # ppo.py:697-698
         self.icm_flat.adam_step(self.int_lr, None)                             # ppo.py:699 (no clipping)
