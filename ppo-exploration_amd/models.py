@@ -203,17 +203,23 @@ class CnnActorCritic(nn.Module):
             heads = [(self.extra_layer[0], self.critic_ext, e, dv)]
             if self.intrinsic:
                 heads.append((self.int_extra_layer[0], self.critic_int, ie, div))
+            import convs as _convs
+            side = _convs.side_stream(df.device) if _convs.BWD_STREAMS and df.is_cuda else None
             des = []
             for hid, crit, act, d in heads:
                 d = d.contiguous().view(B, 1)
                 de = torch.empty_like(act)
                 native.outer_relu_backward(d, crit.weight, act, de)     # dv * w, ReLU backward
-                weight_grad(de, f, hid.weight.grad, self._wgrad_part(hid.weight))
+                if side is None:
+                    weight_grad(de, f, hid.weight.grad, self._wgrad_part(hid.weight))
+                else:  # the hidden layer's weight gradient beside the dgrad chain
+                    _convs.fork(side)
+                    with torch.cuda.stream(side):
+                        weight_grad(de, f, hid.weight.grad, self._wgrad_part(hid.weight))
                 df.addmm_(de, hid.weight)
                 des.append((de, d))
             native.relu_backward_(df, f)
             cv = self.conv_impl
-            import convs as _convs
             # every column-reduction gradient (actor W/b, critic W/b, extra-layer b, fc b) in one pass
             ws = self._head_ws(B, f.shape[1], dout.shape[1])
             (de, d), intr = des[0], des[1] if self.intrinsic else (None, None)
@@ -223,7 +229,6 @@ class CnnActorCritic(nn.Module):
                               w_critic_int=self.critic_int.weight.grad if self.intrinsic else None,
                               b_critic_int=self.critic_int.bias.grad if self.intrinsic else None,
                               b_int_extra=self.int_extra_layer[0].bias.grad if self.intrinsic else None)
-            side = _convs.side_stream(df.device) if _convs.BWD_STREAMS and df.is_cuda else None
             if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-bf16 kernel, Flatten-order dW
                 if side is None:
                     native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad)
@@ -245,6 +250,8 @@ class CnnActorCritic(nn.Module):
                     fc.weight.grad.view(fc.weight.shape[0], 64, 49).copy_(dwp.view(-1, 49, 64).transpose(1, 2))
                 else:
                     torch.mm(df.t(), hf, out=fc.weight.grad)
+                if side is not None:
+                    _convs.join(side)  # the hidden-layer weight gradients, before their all-reduce
                 if dense_ready is not None:
                     dense_ready()
             fe = self.feature_extractor

@@ -697,9 +697,22 @@ class PPO_RND(BaseAlgorithm):
                     od, vd, ivd = self._empty_outputs(intrinsic=True)
                 dout, dv, div = self._loss_grads(od, vd, ivd, idx, roll, stats[k], B, self.int_vf_coef, 1.0)
                 self._bwd_reduce(ctx, out, v, iv, dout, dv, div, has_rows=Bl > 0)
-                self.flat.adam_step(self.lr, self.max_grad_norm)
                 if np.random.randn() < 0.25:                                   # ppo.py:468-469
-                    self.train_rnd(self._rnd_rows(ro, idx) if Bl > 0 else None, B)
+                    # (RND's own parameters: beside the policy's Adam step on a side stream in one
+                    # process, joined before the next minibatch)
+                    side = convs.side_stream(self.device, 1) if convs.BWD_STREAMS and not self.dist.enabled \
+                        else None
+                    if side is None:
+                        self.flat.adam_step(self.lr, self.max_grad_norm)
+                        self.train_rnd(self._rnd_rows(ro, idx) if Bl > 0 else None, B)
+                    else:
+                        convs.fork(side)
+                        with torch.cuda.stream(side):
+                            self.train_rnd(self._rnd_rows(ro, idx) if Bl > 0 else None, B)
+                        self.flat.adam_step(self.lr, self.max_grad_norm)
+                        convs.join(side)
+                else:
+                    self.flat.adam_step(self.lr, self.max_grad_norm)
         acc = self._record_train()
         logger.record("train/intrinsic_loss", acc[4] / max(acc[5], 1.0))
         self._n_updates += self.n_epochs
