@@ -302,6 +302,13 @@ int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, co
                        void* stream);
 int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
                          void* stream);
+/* fc forward (as ppox_nature_fc_fwd) split over K for small batches: 2-8 K-ranges per (128-row
+ * tile, 64-column block) so the grid fills the chip, partial products into the workspace
+ * (ppox_nature_fc_fwd_splitk_workspace_bytes(batch)), then one fixed-order reduce adding the
+ * partials, the bias and the ReLU.  Replaces the same site (models-checkpoint.py:58-59). */
+int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch);
+int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias,
+                              void* workspace, int64_t workspace_bytes, float* f, void* stream);
 /* fc weight gradient dW (512 x 3136, the weight's Flatten order) = df^T @ h3 over the batch,
  * split-bf16 (fp32-class), deterministic: df (batch, 512) is dL/df already ReLU-masked, h3 the
  * NHWC (batch, 7, 7, 64) conv3 output of the split forward.  Replaces the library GEMM of

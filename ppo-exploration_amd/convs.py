@@ -33,13 +33,12 @@ SPLIT_SLOWER = set()
 # conv2 dgrad in split math: the split kernel below this batch, the f32 kernel from it
 # (PPOX_DGRAD2_SPLIT_MAX overrides; default: split at every batch)
 DGRAD2_SPLIT_MAX_BATCH = int(os.environ.get("PPOX_DGRAD2_SPLIT_MAX", str(1 << 62)))
-# fc forward: the split-bf16 GEMM from this batch up, rocBLAS below (PPOX_FC_SPLIT_MIN
-# overrides).  Same-box A/B of the whole training step (tools/ab_fc.sh, after the split
-# kernel's two-deep load pipeline): -40 ms per iteration at B = 16384, +17 ms at the 8-GPU
-# per-rank minibatch (2048: 128-row tiles x 8 column blocks under-fill the chip).  Kernel
-# level (tools/fc_bench.py, r02): 0.085 vs 0.112 ms at 4096 rows (the 1-GPU collect batch),
-# 0.141 vs 0.213 ms at 8192
-FC_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_SPLIT_MIN", "4096"))
+# fc forward: the split-bf16 GEMM from FC_SPLIT_MIN_BATCH up (rocBLAS below; PPOX_FC_SPLIT_MIN
+# overrides, default: every batch), split over K below FC_SPLITK_MAX_BATCH (tools/fc_bench.py,
+# r02: split-K 0.018 / 0.045 / 0.078 ms vs rocBLAS 0.026 / 0.062 / 0.119 ms at 512 / 2048 /
+# 4096 rows; the plain split GEMM 0.146 vs split-K 0.152 ms at 8192)
+FC_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_SPLIT_MIN", "0"))
+FC_SPLITK_MAX_BATCH = int(os.environ.get("PPOX_FC_SPLITK_MAX", "8192"))
 # fc dgrad fused with the trunk's ReLU backward + NHWC transpose (split-bf16) up to this
 # batch (PPOX_FC_DGRAD_FUSED_MAX overrides): faster than rocBLAS + nchw_to_nhwc_mask at
 # every measured batch (A/B: -33 ms per iteration at 16384, -2 ms at 2048)
@@ -283,7 +282,17 @@ class NatureConvs:
         if B < FC_SPLIT_MIN_BATCH:
             return torch._addmm_activation(self.fc.bias, h3.view(B, -1), self.wfc_nhwc.t())  # bias+ReLU fused
         f = torch.empty((B, 512), device=h3.device)
-        native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f)
+        if B < FC_SPLITK_MAX_BATCH:
+            # one workspace per batch size: the collect graph captures the collect batch's buffer
+            # (allocated by the eager first collect), which a training batch must never replace
+            ws = self._ws.get(("fc_sk", B))
+            if ws is None:
+                ws = torch.empty(max(native.nature_fc_fwd_splitk_workspace_bytes(B), 16), dtype=torch.uint8,
+                                 device=h3.device)
+                self._ws[("fc_sk", B)] = ws
+            native.nature_fc_fwd_splitk(h3, B, self.qfc[0], self.fc.bias, ws, f)
+        else:
+            native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f)
         return f
 
     def fc_dgrad_g3(self, df, h3):

@@ -1162,6 +1162,84 @@ struct SgRows : GemmRowsProblem<K, N, 64, MODE> {
     __device__ static int chunk_off(const GemmTile&, int c) { return c * BK; }
 };
 
+// fc forward split over K for small batches (128-row tiles x 8 column blocks leave most CUs
+// idle below ~8192 rows): S K-ranges per (row tile, column block), each workgroup's partial
+// product stored to slab[ks][row][512]; fc_fwd_sk_reduce adds the S partials in order, then
+// the bias, then the ReLU.
+template <int K, int N, int S>
+struct SgRowsSK : GemmRowsProblem<K, N, 64, FC_FWD> {
+    using Base = GemmRowsProblem<K, N, 64, FC_FWD>;
+    static constexpr int ROWS = SG_ROWS, NCB = Base::NCB, KC = Base::KC;
+    struct Tile {
+        long long m0, M;
+        int cb, ks, c0, nc;
+    };
+    __device__ static bool tile(const Args& a, Tile& t) {
+        const long long w = xcd_remap(blockIdx.x, gridDim.x);  // a row tile's S x 8 workgroups share an XCD
+        t.cb = (int)(w % NCB);
+        const long long r = w / NCB;
+        t.ks = (int)(r % S);
+        t.m0 = (r / S) * ROWS;
+        t.M = a.batch;
+        t.c0 = t.ks * KC / S;
+        t.nc = (t.ks + 1) * KC / S - t.c0;
+        return true;
+    }
+    __device__ static int nchunk(const Tile& t) { return t.nc; }
+    __device__ static int bchunk_id(const Tile& t, int c) { return t.cb * KC + t.c0 + c; }
+    __device__ static const float* row_ptr(const Args& a, const Tile& t, int row) {
+        long long m = t.m0 + row;
+        m = m < t.M ? m : t.M - 1;
+        return reinterpret_cast<const float*>(a.x) + m * K;
+    }
+    __device__ static int chunk_off(const Tile& t, int c) { return (t.c0 + c) * BK; }
+    __device__ static float prefetch(const Args&, const Tile&, int, int) { return 0.f; }
+    __device__ static void store_pre(const Args& a, const Tile& t, int row, int col, float acc, float) {
+        const long long m = t.m0 + row;
+        if (m >= t.M) return;
+        a.y[((long long)t.ks * t.M + m) * N + t.cb * 64 + col] = acc;
+    }
+};
+
+template <int N, int S>
+__global__ void __launch_bounds__(256) fc_fwd_sk_reduce(const float4* __restrict__ slab, long long M,
+                                                         const float* __restrict__ bias, float4* __restrict__ y) {
+    const long long i = blockIdx.x * 256LL + threadIdx.x, n4 = M * N / 4;
+    if (i >= n4) return;
+    float4 s = slab[i];
+#pragma unroll
+    for (int k = 1; k < S; ++k) {
+        const float4 v = slab[k * n4 + i];
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+    }
+    const int n = (int)((i * 4) % N);
+    y[i] = make_float4(fmaxf(s.x + bias[n], 0.f), fmaxf(s.y + bias[n + 1], 0.f), fmaxf(s.z + bias[n + 2], 0.f),
+                       fmaxf(s.w + bias[n + 3], 0.f));
+}
+
+// K-splits for a batch: enough (row tile, column block, split) workgroups for two per CU, at most 8
+inline int fc_fwd_splits(long long batch) {
+    const long long wg = ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB;
+    int s = 1;
+    while (s < 8 && wg * s < 512) s *= 2;
+    return s;
+}
+
+template <int S>
+int launch_fc_fwd_sk(const Args& a, const uint16_t* q, float* slab, const float* bias, float* f, hipStream_t st) {
+    Args b = a;
+    b.y = slab;
+    const int rc = launch_sgemm<SgRowsSK<3136, 512, S>>(b, q, ppox::ceil_div(a.batch, SG_ROWS) * FcFwd::NCB * S, st,
+                                                        "ppox_nature_fc_fwd_splitk");
+    if (rc != PPOX_OK) return rc;
+    fc_fwd_sk_reduce<512, S><<<ppox::ceil_div(a.batch * 512 / 4, 256), 256, 0, st>>>(
+        reinterpret_cast<const float4*>(slab), a.batch, bias, reinterpret_cast<float4*>(f));
+    PPOX_LAUNCHED("ppox_nature_fc_fwd_splitk");
+}
+
 // ---------------------------------------------------------------------------
 // Register-direct implicit GEMM (the default forward / dgrad path).
 // Each wave owns 32*MT rows x all NOUT columns and is independent: no LDS, no
@@ -2463,6 +2541,29 @@ extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t
 #endif
     return launch_igemm_split<FcFwd>(a, q_fwd, ppox::ceil_div(batch, 128) * FcFwd::NCB, ppox::as_stream(stream),
                                      "ppox_nature_fc_fwd");
+}
+
+extern "C" int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch) {
+    return batch <= 0 ? 0 : (int64_t)fc_fwd_splits(batch) * batch * 512 * 4;
+}
+
+extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias,
+                                         void* workspace, int64_t workspace_bytes, float* f, void* stream) {
+    if (batch == 0) return PPOX_OK;
+    PPOX_REQUIRE(h3 && q_fwd && bias && f && workspace && batch > 0, "ppox_nature_fc_fwd_splitk: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd) && ppox::aligned16(f) && ppox::aligned16(workspace),
+                 "ppox_nature_fc_fwd_splitk: 16B alignment");
+    PPOX_REQUIRE(workspace_bytes >= ppox_nature_fc_fwd_splitk_workspace_bytes(batch),
+                 "ppox_nature_fc_fwd_splitk: workspace too small");
+    Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch};
+    float* slab = reinterpret_cast<float*>(workspace);
+    hipStream_t st = ppox::as_stream(stream);
+    switch (fc_fwd_splits(batch)) {
+        case 1: return launch_fc_fwd_sk<1>(a, q_fwd, slab, bias, f, st);
+        case 2: return launch_fc_fwd_sk<2>(a, q_fwd, slab, bias, f, st);
+        case 4: return launch_fc_fwd_sk<4>(a, q_fwd, slab, bias, f, st);
+        default: return launch_fc_fwd_sk<8>(a, q_fwd, slab, bias, f, st);
+    }
 }
 
 extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,

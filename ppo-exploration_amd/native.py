@@ -85,6 +85,7 @@ SIGNATURES = {
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
+    "ppox_nature_fc_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp],
     "ppox_icm_pack_w1": [_vp, _i64, _vp, _vp],
     "ppox_icm_encode": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_icm_pair_backward": [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp],
@@ -101,7 +102,8 @@ _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p
              "ppox_nature_fc_pack_elems": ctypes.c_int64, "ppox_head_grads_workspace_bytes": ctypes.c_int64,
              "ppox_nature_fc_wgrad_workspace_bytes": ctypes.c_int64, "ppox_icm_param_elems": ctypes.c_int64,
              "ppox_icm_w1_pack_elems": ctypes.c_int64, "ppox_icm_encode_workspace_bytes": ctypes.c_int64,
-             "ppox_icm_partials_bytes": ctypes.c_int64, "ppox_icm_g1_pack_elems": ctypes.c_int64}
+             "ppox_icm_partials_bytes": ctypes.c_int64, "ppox_icm_g1_pack_elems": ctypes.c_int64,
+             "ppox_nature_fc_fwd_splitk_workspace_bytes": ctypes.c_int64}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
                  "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32],
                  "ppox_nature_wgrad_split_workspace_bytes": [_i32, _i64],
@@ -109,7 +111,8 @@ _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad
                  "ppox_nature_fc_pack_elems": [], "ppox_head_grads_workspace_bytes": [_i64, _i64, _i64, _i32],
                  "ppox_nature_fc_wgrad_workspace_bytes": [_i64], "ppox_icm_param_elems": [_i32],
                  "ppox_icm_w1_pack_elems": [_i64], "ppox_icm_encode_workspace_bytes": [_i64, _i64],
-                 "ppox_icm_partials_bytes": [_i64, _i32], "ppox_icm_g1_pack_elems": [_i64]}
+                 "ppox_icm_partials_bytes": [_i64, _i32], "ppox_icm_g1_pack_elems": [_i64],
+                 "ppox_nature_fc_fwd_splitk_workspace_bytes": [_i64]}
 
 _lib = None
 
@@ -497,6 +500,16 @@ def nature_pack_all(w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dg
 def nature_fc_fwd(h3, batch, q_fwd, bias, f, stream=None):
     """f = relu(h3 @ W^T + b), h3 (batch, 3136) in Flatten order."""
     call("ppox_nature_fc_fwd", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(f), stream_ptr(stream))
+
+
+def nature_fc_fwd_splitk_workspace_bytes(batch):
+    return int(load().ppox_nature_fc_fwd_splitk_workspace_bytes(int(batch)))
+
+
+def nature_fc_fwd_splitk(h3, batch, q_fwd, bias, workspace, f, stream=None):
+    """fc forward split over K (small batches), bias + ReLU in the fixed-order reduce."""
+    call("ppox_nature_fc_fwd_splitk", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(workspace),
+         workspace.numel() * workspace.element_size(), _p(f), stream_ptr(stream))
 
 
 def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, stream=None):

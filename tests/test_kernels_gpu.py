@@ -782,6 +782,32 @@ def test_fc_split_gemm_vs_fp64(B):
     assert e_s <= 2 * e_f + 1e-7, (float(e_s), float(e_f))
 
 
+@pytest.mark.parametrize("B", [1, 130, 512, 2048, 4000])
+def test_fc_fwd_splitk_vs_fp64(B):
+    """fc forward split over K (ppox_nature_fc_fwd_splitk: 1-8 K-ranges by batch, partials
+    reduced in order with bias + ReLU) vs float64: error no larger than torch's f32 GEMM's (x2
+    headroom), and run-to-run bitwise."""
+    import native
+    torch.manual_seed(B + 7)
+    W = torch.randn(512, 3136, device="cuda") * 0.02
+    b = torch.randn(512, device="cuda") * 0.1
+    h3n = torch.relu(torch.randn(B, 7, 7, 64, device="cuda"))
+    h3 = h3n.permute(0, 3, 1, 2).reshape(B, 3136)
+    n = native.nature_fc_pack_elems()
+    qf, qd = torch.empty(n, dtype=torch.int16, device="cuda"), torch.empty(n, dtype=torch.int16, device="cuda")
+    native.nature_fc_pack(W, qf, qd)
+    ws = torch.empty(native.nature_fc_fwd_splitk_workspace_bytes(B), dtype=torch.uint8, device="cuda")
+    f = torch.full((B, 512), float("nan"), device="cuda")
+    native.nature_fc_fwd_splitk(h3n, B, qf, b, ws, f)
+    ref = torch.relu(h3.double() @ W.double().t() + b.double())
+    e_s = (f.double() - ref).abs().max() / ref.abs().max()
+    e_f = (torch.relu(torch.addmm(b, h3, W.t())).double() - ref).abs().max() / ref.abs().max()
+    assert e_s <= 2 * e_f + 1e-7, (float(e_s), float(e_f))
+    f2 = torch.empty_like(f)
+    native.nature_fc_fwd_splitk(h3n, B, qf, b, ws, f2)
+    assert torch.equal(f, f2)
+
+
 @pytest.mark.parametrize("B", [1, 33, 1000, 2048, 5000])
 def test_fc_wgrad_split_vs_fp64(B):
     """fc weight gradient on the split wgrad kernel (ppox_nature_fc_wgrad: h3 NHWC, dW in the

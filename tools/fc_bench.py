@@ -43,6 +43,10 @@ def main():
     res = {"B": B}
     res["split_fwd_ms"] = t_ms(lambda: native.nature_fc_fwd(h3n, B, qf, b, f))
     res["rocblas_fwd_ms"] = t_ms(lambda: torch.relu(torch.addmm(b, h3, W.t())))
+    wsk = torch.empty(max(native.nature_fc_fwd_splitk_workspace_bytes(B), 16), dtype=torch.uint8, device=d)
+    fsk = torch.empty(B, 512, device=d)
+    res["splitk_fwd_ms"] = t_ms(lambda: native.nature_fc_fwd_splitk(h3n, B, qf, b, wsk, fsk))
+    res["addmm_act_fwd_ms"] = t_ms(lambda: torch._addmm_activation(b, h3, W.t()))
     res["split_dgrad_ms"] = t_ms(lambda: native.nature_fc_dgrad(df, B, qd, h3n, g3))
     res["rocblas_dgrad_ms"] = t_ms(lambda: torch.mm(df, W))
     ws = torch.empty(native.nature_fc_wgrad_workspace_bytes(B), dtype=torch.uint8, device=d)
@@ -60,6 +64,9 @@ def main():
     f32 = torch.relu(torch.addmm(b, h3[:r], W.t()))
     res["fwd_err_split"] = float((f[:r].double() - ref).abs().max() / ref.abs().max())
     res["fwd_err_f32"] = float((f32.double() - ref).abs().max() / ref.abs().max())
+    native.nature_fc_fwd_splitk(h3n, B, qf, b, wsk, fsk)
+    res["fwd_err_splitk"] = float((fsk[:r].double() - ref).abs().max() / ref.abs().max())
+    res["splitk_vs_split_maxdiff"] = float((fsk - f).abs().max() / f.abs().max())
     refd = (df[:r].double() @ W.double()).view(r, 64, 7, 7).permute(0, 2, 3, 1) * (h3n[:r] > 0)
     native.nature_fc_dgrad(df, B, qd, h3n, g3)
     res["dgrad_err_split"] = float((g3[:r].double() - refd).abs().max() / refd.abs().max())
