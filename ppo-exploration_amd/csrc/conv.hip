@@ -316,17 +316,9 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(Args a) {
 
 
 // ---------------------------------------------------------------------------
-// Split-bf16 form of igemm_kernel (same Problems: tiles, K walk, fused epilogues)
-// on v_mfma_f32_32x32x16_bf16.  A chunk (128 rows x 32 f32) is staged in LDS as
-// f32 (rows of 36 floats: 16-B aligned, conflict-free b128 row reads); each wave
-// reads its rows' 8-value fragments and splits them into three exact bf16 planes
-// in registers (every A value is read by exactly one wave, so the split costs the
-// same as splitting at the store).  B chunks come pre-split and pre-packed in
-// fragment order (split_frag_index) and are staged in LDS.  Per 16-k step and
-// column tile: six MFMAs (mfma_split6), a0*b0 into hi, the rest into lo.
+// Pre-split B operands of the split-bf16 GEMMs (sgemm_kernel): a [K][NOUT] matrix as three
+// exact bf16 planes in MFMA fragment order.
 // ---------------------------------------------------------------------------
-constexpr int SAST = 36;
-
 // packed position of natural element (row k, col) of a [K][nout] matrix, plane p:
 // chunk (k / 32) x k-step s x column tile j x plane x lane (h, col & 31) x e
 __host__ __device__ constexpr long long split_frag_index(int k, int col, int nout, int p) {
@@ -358,137 +350,6 @@ __device__ inline void pack_frag_unit(const Src& src, uint16_t* __restrict__ q, 
     d[128] = p2;
 }
 
-// Problems with LATE_EPILOGUE load their epilogue operands after the K walk (saves 16 VGPRs
-// per column tile when the walk holds many tiles)
-template <class P, class = void>
-struct late_epilogue : std::false_type {};
-template <class P>
-struct late_epilogue<P, std::void_t<decltype(P::LATE_EPILOGUE)>> : std::bool_constant<P::LATE_EPILOGUE> {};
-
-template <class Prob>
-__global__ void __launch_bounds__(256, 2) igemm_split_kernel(Args a, const u32x4* __restrict__ wq) {
-    constexpr int NOUT = Prob::NOUT, NT = NOUT / 32, BMR = 128;
-    static_assert(Prob::MT == 1, "split igemm: 32 rows per wave");
-    constexpr int BQ = 2 * NT * 3 * 64;  // u32x4 per B chunk
-    constexpr int BV = (BQ + 255) / 256;
-    __shared__ __attribute__((aligned(16))) float As[2][BMR * SAST];
-    __shared__ u32x4 Bs[2][BQ];
-    typename Prob::Tile t;
-    if (!Prob::tile(a, t)) return;
-    const int nchunk = Prob::nchunk(t);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-
-    constexpr bool LATE = late_epilogue<Prob>::value;
-    f32x16 hi[NT], lo[NT], pre[LATE ? 1 : NT];
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-        hi[j] = lo[j] = zero16();
-        if constexpr (!LATE) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                pre[j][r] =
-                    Prob::prefetch(a, t, wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), j * 32 + (lane & 31));
-        }
-    }
-    typename Prob::Stager sa(a, t);
-    static_assert(decltype(sa)::SL == 4, "four float4 slots per thread");
-    struct Stage {
-        float4 a[4];
-        u32x4 b[BV];
-    };
-    auto load = [&](int c) {
-        Stage r;
-        sa.load(c);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r.a[i] = sa.r[i];
-        const u32x4* src = wq + (long long)Prob::bchunk_id(t, c) * BQ;
-#pragma unroll
-        for (int i = 0; i < BV; ++i)
-            if (BQ % 256 == 0 || i * 256 + (int)threadIdx.x < BQ) r.b[i] = src[i * 256 + threadIdx.x];
-        return r;
-    };
-    auto store = [&](int buf, const Stage& r) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int w = i * 256 + threadIdx.x;
-            *reinterpret_cast<float4*>(As[buf] + (w >> 3) * SAST + (w & 7) * 4) = r.a[i];
-        }
-#pragma unroll
-        for (int i = 0; i < BV; ++i)
-            if (BQ % 256 == 0 || i * 256 + (int)threadIdx.x < BQ) Bs[buf][i * 256 + threadIdx.x] = r.b[i];
-    };
-    const int aoff = (wave * 32 + (lane & 31)) * SAST + (lane >> 5) * 8;
-    auto compute = [&](int cur) {
-        const float* A = As[cur] + aoff;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            u32x4 af[3];
-            split8(*reinterpret_cast<const float4*>(A + 16 * s), *reinterpret_cast<const float4*>(A + 16 * s + 4), af[0],
-                   af[1], af[2]);
-#pragma unroll
-            for (int j = 0; j < NT; ++j) {
-                const u32x4* B = Bs[cur] + ((s * NT + j) * 3) * 64 + lane;
-                const u32x4 bf[3] = {B[0], B[64], B[128]};
-                mfma_split6(af, bf, hi[j], lo[j]);
-            }
-        }
-    };
-    // Pipeline: LDS double buffer + two register stages (x, y) that alternate roles, the
-    // walk unrolled by two, so a chunk's global loads are issued two compute phases before
-    // the LDS store that consumes them.  Loads and stores are unconditional (past the end:
-    // the last chunk again, never computed): a conditional load, or a register copy of
-    // just-loaded values, makes the compiler wait for every outstanding load.
-    if (nchunk > 0) {
-        const int last = nchunk - 1;
-        store(0, load(0));
-        Stage y = load(min(1, last));
-        __syncthreads();
-        for (int c = 0; c < nchunk; c += 2) {
-            // LDS buffer 0 holds chunk c, y chunk c + 1
-            // (sched_barrier: keep the loads ahead of, and the LDS stores behind, the MFMAs)
-            const Stage x = load(min(c + 2, last));
-            __builtin_amdgcn_sched_barrier(0);
-            compute(0);
-            __builtin_amdgcn_sched_barrier(0);
-            store(1, y);
-            __syncthreads();
-            // LDS buffer 1 holds chunk c + 1, x chunk c + 2
-            y = load(min(c + 3, last));
-            __builtin_amdgcn_sched_barrier(0);
-            if (c + 1 < nchunk) compute(1);
-            __builtin_amdgcn_sched_barrier(0);
-            store(0, x);
-            __syncthreads();
-        }
-    }
-    if constexpr (LATE) {
-        // every epilogue operand load issued before the first store
-        f32x16 e[NT];
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                e[j][r] = Prob::prefetch(a, t, wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), j * 32 + (lane & 31));
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), col = j * 32 + (lane & 31);
-                Prob::store_pre(a, t, row, col, hi[j][r] + lo[j][r], e[j][r]);
-            }
-    } else {
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), col = j * 32 + (lane & 31);
-                Prob::store_pre(a, t, row, col, hi[j][r] + lo[j][r], pre[j][r]);
-            }
-    }
-}
-
-// split-pack: forward [K][COUT] (NHWC K order) / dgrad [(tap, co)][ci] of layer L,
-// from the PyTorch [co][ci][ky][kx] weights, into split_frag_index order
 template <class L, bool DGRAD>
 __device__ inline void pack_split_gemm_elem(const float* __restrict__ w, uint16_t* __restrict__ q, int i) {
     constexpr int NOUT = DGRAD ? L::CIN : L::COUT;
@@ -603,15 +464,12 @@ struct GemmRowsProblem {
 #ifndef FC_DGRAD_G
 #define FC_DGRAD_G 12  // fc dgrad: column blocks per tile group
 #endif
-#ifndef SG2
-#define SG2 1  // 0: the split GEMMs on igemm_split_kernel (register-staged, 128-row tiles)
-#endif
 #ifndef FC_NB
 #define FC_NB 64  // 128 measured no faster (one workgroup per CU: 86 KB LDS, 324 registers)
 #endif
 using FcFwd = GemmRowsProblem<3136, 512, FC_NB, FC_FWD>;
 using FcDgrad = GemmRowsProblem<512, 3136, FC_NB, FC_DGRAD>;
-static_assert(!SG2 || FC_NB == 64, "sg2 runs the fc layer in 64-column blocks");
+static_assert(FC_NB == 64, "sg2 runs the fc layer in 64-column blocks");
 
 // packs B (element (k, n) = w[n * ldw + k] when TRANS, w[k * ldw + n] otherwise) into
 // split_frag_index order per column block, zero beyond N
@@ -862,17 +720,11 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
     }
 }
 
-template <class Prob>
-int launch_igemm_split(const Args& a, const uint16_t* wq, long long blocks, hipStream_t s, const char* name) {
-    if (blocks == 0) return PPOX_OK;
-    igemm_split_kernel<Prob><<<(unsigned)blocks, 256, 0, s>>>(a, reinterpret_cast<const u32x4*>(wq));
-    PPOX_LAUNCHED(name);
-}
 
 // ---------------------------------------------------------------------------
 // Split-bf16 GEMM, LDS-DMA pipelined ("sg2"): the forward-style GEMMs (conv2/conv3
-// forward, conv3 dgrad, fc forward, fc dgrad) with the same fused epilogues as
-// igemm_split_kernel.  512-thread workgroups (8 waves, two per SIMD, one workgroup per
+// forward, conv3 dgrad, fc forward, fc dgrad) with the Problems' fused epilogues (bias +
+// ReLU, ReLU-mask, NHWC / Flatten order).  512-thread workgroups (8 waves, two per SIMD, one workgroup per
 // CU), 256 rows x 64 columns per workgroup, each wave 32 rows x 64 columns (hi/lo f32
 // accumulators for two 32x32 tiles: six v_mfma_f32_32x32x16_bf16 per tile and 16-k step).
 // Per 32-k chunk the A rows (f32, im2col-gathered: one 128-B run per row) and the
@@ -1083,7 +935,7 @@ int launch_sgemm(const Args& a, const uint16_t* wq, long long blocks, hipStream_
     PPOX_LAUNCHED(name);
 }
 
-// sg2 Problems: the igemm_split Problems' chunk walk and epilogues on SG_ROWS-row tiles, plus
+// sg2 Problems: the f32 Problems' chunk walk and epilogues on SG_ROWS-row tiles, plus
 // each row's A base pointer (rows past the end clamped to a valid row, never stored) and
 // the chunk's element offset within a row (the same for every row of the tile)
 template <class L, bool OUT_NCHW>
@@ -2388,19 +2240,11 @@ int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq,
                 hipStream_t s) {
     PPOX_REQUIRE(ppox::aligned16(x), "ppox_nature_conv_fwd_split: layer 2/3 input must be 16B-aligned NHWC");
     Args a{x, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch};
-#if SG2
     if (layer == 2)
         return launch_sgemm<SgFwd<G2, false>>(a, wq, ppox::ceil_div(batch * G2::P, SG_ROWS), s,
                                               "ppox_nature_conv_fwd_split");
     return launch_sgemm<SgFwd<G3, false>>(a, wq, ppox::ceil_div(batch * G3::P, SG_ROWS), s,
                                           "ppox_nature_conv_fwd_split");
-#endif
-    if (layer == 2) {
-        using P2 = FwdNHWCProblem<G2, false, 1>;
-        return launch_igemm_split<P2>(a, wq, ppox::ceil_div(batch * G2::P, P2::BMR), s, "ppox_nature_conv_fwd_split");
-    }
-    using P3 = FwdNHWCProblem<G3, false, 1>;  // split math: conv3 output NHWC (see fc_nchw_feature)
-    return launch_igemm_split<P3>(a, wq, ppox::ceil_div(batch * G3::P, P3::BMR), s, "ppox_nature_conv_fwd_split");
 }
 }  // namespace ppox_conv
 
@@ -2427,12 +2271,8 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
         dgrad2_colp_kernel<<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd), ntriples);
         PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
     }
-#if SG2
     return launch_sgemm<SgDgradPM<G3>>(a, wqd, ppox::ceil_div(batch, SG_ROWS) * SgDgradPM<G3>::NPOS, s,
                                        "ppox_nature_conv_dgrad_split");
-#endif
-    using D3 = DgradPMProblem<G3, 1>;
-    return launch_igemm_split<D3>(a, wqd, ppox::ceil_div(batch, D3::BMR) * D3::NPOS, s, "ppox_nature_conv_dgrad_split");
 }
 
 // ---- NatureCNN fc layer (3136 -> 512) on the split-bf16 GEMM ----------------------
@@ -2535,12 +2375,8 @@ extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t
     PPOX_REQUIRE(h3 && q_fwd && bias && f && batch >= 0, "ppox_nature_fc_fwd: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd), "ppox_nature_fc_fwd: 16B alignment");
     Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch};
-#if SG2
     return launch_sgemm<SgRows<3136, 512, FC_FWD, FC_FWD_G>>(a, q_fwd, ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB,
                                                    ppox::as_stream(stream), "ppox_nature_fc_fwd");
-#endif
-    return launch_igemm_split<FcFwd>(a, q_fwd, ppox::ceil_div(batch, 128) * FcFwd::NCB, ppox::as_stream(stream),
-                                     "ppox_nature_fc_fwd");
 }
 
 extern "C" int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch) {
@@ -2572,12 +2408,8 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
     PPOX_REQUIRE(df && q_dgrad && h3 && g3 && batch >= 0, "ppox_nature_fc_dgrad: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(q_dgrad), "ppox_nature_fc_dgrad: 16B alignment");
     Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch};
-#if SG2
     return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_G>>(a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB,
                                                      ppox::as_stream(stream), "ppox_nature_fc_dgrad");
-#endif
-    return launch_igemm_split<FcDgrad>(a, q_dgrad, ppox::ceil_div(batch, 128) * FcDgrad::NCB, ppox::as_stream(stream),
-                                       "ppox_nature_fc_dgrad");
 }
 
 extern "C" int ppox_nature_pack_all(const float* w1, const float* w2, const float* w3, const float* wfc, float* wpd2,
