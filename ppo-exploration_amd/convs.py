@@ -65,18 +65,30 @@ def side_stream(device, k=0):
     return s
 
 
-def fork(side):
-    """side waits for everything enqueued so far on the current stream."""
-    ev = torch.cuda.Event()
-    ev.record()
+_events = {}
+
+
+def _event(side, which):
+    # one reusable event per (side stream, direction): a wait takes the event's most recent
+    # record at the time it is enqueued, so re-recording it for the next fork / join is safe
+    ev = _events.get((side, which))
+    if ev is None:
+        ev = _events[(side, which)] = torch.cuda.Event()
+    return ev
+
+
+def fork(side, cur=None):
+    """side waits for everything enqueued so far on `cur` (default: the current stream)."""
+    ev = _event(side, 0)
+    ev.record(cur)
     side.wait_event(ev)
 
 
-def join(side):
-    """The current stream waits for everything enqueued so far on side."""
-    ev = torch.cuda.Event()
+def join(side, cur=None):
+    """`cur` (default: the current stream) waits for everything enqueued so far on side."""
+    ev = _event(side, 1)
     ev.record(side)
-    torch.cuda.current_stream().wait_event(ev)
+    (cur if cur is not None else torch.cuda.current_stream()).wait_event(ev)
 
 
 def default_math():
@@ -246,16 +258,17 @@ class NatureConvs:
         else:
             native.nature_conv_dgrad(layer, g, B, self.wpd2 if layer == 2 else self.wpd3, prev_act, out)
 
-    def wgrad(self, layer, x, B, g, dw, db):
+    def wgrad(self, layer, x, B, g, dw, db, stream=None):
         stride = 4 * 84 * 84 if layer == 1 else 0
         if isinstance(x, RolloutRows):
             assert layer == 1 and self.uses_split("wgrad", 1)
-            native.nature_conv_wgrad_split_idx(1, x.frames, B, x.idx, x.T, x.N, g, self.workspace(1, B, True), dw, db)
+            native.nature_conv_wgrad_split_idx(1, x.frames, B, x.idx, x.T, x.N, g, self.workspace(1, B, True), dw, db,
+                                               stream=stream)
             return
         if self.uses_split("wgrad", layer):
-            native.nature_conv_wgrad_split(layer, x, B, stride, g, self.workspace(layer, B, True), dw, db)
+            native.nature_conv_wgrad_split(layer, x, B, stride, g, self.workspace(layer, B, True), dw, db, stream=stream)
         else:
-            native.nature_conv_wgrad(layer, x, B, None, 0, 0, stride, g, self.workspace(layer, B), dw, db)
+            native.nature_conv_wgrad(layer, x, B, None, 0, 0, stride, g, self.workspace(layer, B), dw, db, stream=stream)
 
     def forward_acts(self, x):
         """Trunk forward: (h1 NHWC, h2 NHWC, h3) activations (ReLU applied); h3 is NHWC
@@ -315,25 +328,20 @@ class NatureConvs:
             g3 = torch.empty((B, 7, 7, 64), device=dev)
             native.nchw_to_nhwc_relu_grad(dh3, h3, B, g3)      # ReLU backward of conv3, to NHWC
         side = side_stream(dev) if BWD_STREAMS and dev.type == "cuda" else None
-        if side is None:
-            self.wgrad(3, h2, B, g3, dw3, db3)
-        else:  # wgrad3 beside dgrad3 (the tensors stay referenced until the join below)
-            fork(side)
-            with torch.cuda.stream(side):
-                self.wgrad(3, h2, B, g3, dw3, db3)
+        cur = torch.cuda.current_stream() if side is not None else None
+        if side is not None:  # wgrad3 beside dgrad3 (the tensors stay referenced until the join below)
+            fork(side, cur)
+        self.wgrad(3, h2, B, g3, dw3, db3, stream=side)
         g2 = torch.empty((B, 9, 9, 64), device=dev)
         self.dgrad(3, g3, B, h2, g2)                            # dX of conv3, times ReLU'(conv2)
-        if side is None:
-            self.wgrad(2, h1, B, g2, dw2, db2)
-        else:
-            fork(side)
-            with torch.cuda.stream(side):
-                self.wgrad(2, h1, B, g2, dw2, db2)
+        if side is not None:
+            fork(side, cur)
+        self.wgrad(2, h1, B, g2, dw2, db2, stream=side)
         g1 = torch.empty((B, 20, 20, 32), device=dev)
         self.dgrad(2, g2, B, h1, g1)                            # dX of conv2, times ReLU'(conv1)
         self.wgrad(1, x, B, g1, dw1, db1)
         if side is not None:
-            join(side)
+            join(side, cur)
 
     def __call__(self, x):
         if x.dtype != torch.uint8:

@@ -205,6 +205,7 @@ class CnnActorCritic(nn.Module):
                 heads.append((self.int_extra_layer[0], self.critic_int, ie, div))
             import convs as _convs
             side = _convs.side_stream(df.device) if _convs.BWD_STREAMS and df.is_cuda else None
+            cur = torch.cuda.current_stream() if side is not None else None
             des = []
             for hid, crit, act, d in heads:
                 d = d.contiguous().view(B, 1)
@@ -213,7 +214,7 @@ class CnnActorCritic(nn.Module):
                 if side is None:
                     weight_grad(de, f, hid.weight.grad, self._wgrad_part(hid.weight))
                 else:  # the hidden layer's weight gradient beside the dgrad chain
-                    _convs.fork(side)
+                    _convs.fork(side, cur)
                     with torch.cuda.stream(side):
                         weight_grad(de, f, hid.weight.grad, self._wgrad_part(hid.weight))
                 df.addmm_(de, hid.weight)
@@ -238,10 +239,10 @@ class CnnActorCritic(nn.Module):
                     # on the side stream, beside the fc dgrad and the conv backward; the dense
                     # gradients' all-reduce is started from there (ordered after it and, through the
                     # fork, after every head gradient); backward_acts joins the side stream
-                    _convs.fork(side)
-                    with torch.cuda.stream(side):
-                        native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad)
-                        if dense_ready is not None:
+                    _convs.fork(side, cur)
+                    native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, stream=side)
+                    if dense_ready is not None:
+                        with torch.cuda.stream(side):
                             dense_ready()
             else:
                 if cv.nhwc3:  # NHWC features: library GEMM in NHWC order, permuted back to Flatten order
@@ -251,7 +252,7 @@ class CnnActorCritic(nn.Module):
                 else:
                     torch.mm(df.t(), hf, out=fc.weight.grad)
                 if side is not None:
-                    _convs.join(side)  # the hidden-layer weight gradients, before their all-reduce
+                    _convs.join(side, cur)  # the hidden-layer weight gradients, before their all-reduce
                 if dense_ready is not None:
                     dense_ready()
             fe = self.feature_extractor

@@ -185,17 +185,28 @@ _LAYERED = ("ppox_nature_conv_fwd", "ppox_nature_conv_dgrad", "ppox_nature_conv_
             "ppox_nature_conv_wgrad_split_idx")
 
 
+_fns = {}
+
+
 def call(name, *args):
-    key = f"{name}:{args[0]}" if name in _LAYERED else name
-    if key in _timed and not torch.cuda.is_current_stream_capturing():  # (captured launches replay untimed)
-        s = torch.cuda.current_stream()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(s)
-        rc = getattr(lib(), name)(*args)
-        b.record(s)
-        _events[key].append((a, b, args))
-    else:
-        rc = getattr(lib(), name)(*args)
+    fn = _fns.get(name)
+    if fn is None:  # bound once per entry point (the per-launch host cost matters on the hot loops)
+        fn = _fns[name] = getattr(lib(), name)
+    if _timed:
+        key = f"{name}:{args[0]}" if name in _LAYERED else name
+        if key in _timed and not torch.cuda.is_current_stream_capturing():  # (captured launches replay untimed)
+            # events on the stream the kernel is launched on (every entry point's last argument)
+            sp = args[-1].value if isinstance(args[-1], _vp) else None
+            s = torch.cuda.ExternalStream(sp) if sp else torch.cuda.current_stream()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            rc = fn(*args)
+            b.record(s)
+            _events[key].append((a, b, args))
+            if rc != 0:
+                raise NativeError(f"{name} failed ({rc}): {load().ppox_last_error().decode()}")
+            return
+    rc = fn(*args)
     if rc != 0:
         raise NativeError(f"{name} failed ({rc}): {load().ppox_last_error().decode()}")
 
