@@ -30,16 +30,26 @@ struct Vec<1> {
     using u8 = uint8_t;
 };
 template <>
+struct Vec<2> {
+    using f = float2;
+    using u8 = uchar2;
+};
+template <>
 struct Vec<4> {
     using f = float4;
     using u8 = uchar4;
 };
 
 __device__ inline float get(const float& v, int) { return v; }
+__device__ inline float get(const float2& v, int k) { return k == 0 ? v.x : v.y; }
 __device__ inline float get(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 __device__ inline uint8_t get(const uint8_t& v, int) { return v; }
+__device__ inline uint8_t get(const uchar2& v, int k) { return k == 0 ? v.x : v.y; }
 __device__ inline uint8_t get(const uchar4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 __device__ inline void put(float& v, int, float x) { v = x; }
+__device__ inline void put(float2& v, int k, float x) {
+    if (k == 0) v.x = x; else v.y = x;
+}
 __device__ inline void put(float4& v, int k, float x) {
     if (k == 0) v.x = x; else if (k == 1) v.y = x; else if (k == 2) v.z = x; else v.w = x;
 }
@@ -273,23 +283,29 @@ int launch_gae(const float* rew, const float* val, const uint8_t* done, const fl
     const float ig32 = (float)int_gamma;
     const float igl32 = (float)(int_gamma * lam);
     hipStream_t s = ppox::as_stream(stream);
-    // EPL=4 needs 16-byte alignment of every row; only worth it when it still
-    // leaves >= 2 waves per CU worth of lanes (N/4 >= 32768).
-    bool vec4 = (N % 4 == 0) && (N / 4 >= 32768);
+    // EPL envs per lane (float4 / float2 rows): the widest that still leaves >= 65,536 lanes
+    // (4 waves per CU; the sweep dipped to 0.35 of HBM at N = 131,072 with float4 lanes on 2),
+    // given N % EPL == 0 and rows aligned to EPL floats
     const void* ptrs[] = {rew, val, last_v, adv, ret, irew, ival, last_iv, iadv, iret};
-    for (const void* p : ptrs)
-        if (p && !ppox::aligned16(p)) vec4 = false;
-    if (reinterpret_cast<uintptr_t>(done) % 4 || reinterpret_cast<uintptr_t>(last_done) % 4) vec4 = false;
+    auto fits = [&](int epl) {
+        if (N % epl || N / epl < 65536) return false;
+        for (const void* p : ptrs)
+            if (p && (reinterpret_cast<uintptr_t>(p) % (4 * epl))) return false;
+        return reinterpret_cast<uintptr_t>(done) % epl == 0 && reinterpret_cast<uintptr_t>(last_done) % epl == 0;
+    };
+    const int epl = fits(4) ? 4 : fits(2) ? 2 : 1;
     constexpr int EB = staged_eb<DUAL>();
     const size_t lds = (size_t)T * EB * (16 + 8 + (DUAL ? 12 : 0));
     if (N <= STAGED_NMAX && T <= STAGED_TMAX && lds <= 65536) {
         gae_staged_kernel<DUAL><<<ppox::ceil_div(N, EB), 256, lds, s>>>(
             rew, val, done, last_v, last_done, irew, ival, last_iv, (int)T, N, g32, gl, ig32, igl32, adv, ret,
             iadv, iret);
-    } else if (vec4) {
-        const long long lanes = N / 4;
-        const int bs = 256;
-        gae_kernel<4, DUAL><<<ppox::ceil_div(lanes, bs), bs, 0, s>>>(
+    } else if (epl == 4) {
+        gae_kernel<4, DUAL><<<ppox::ceil_div(N / 4, 256), 256, 0, s>>>(
+            rew, val, done, last_v, last_done, irew, ival, last_iv, (int)T, N, g32, gl, ig32, igl32, adv,
+            ret, iadv, iret);
+    } else if (epl == 2) {
+        gae_kernel<2, DUAL><<<ppox::ceil_div(N / 2, 256), 256, 0, s>>>(
             rew, val, done, last_v, last_done, irew, ival, last_iv, (int)T, N, g32, gl, ig32, igl32, adv,
             ret, iadv, iret);
     } else {

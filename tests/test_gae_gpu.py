@@ -53,9 +53,11 @@ def test_gae_dual_golden(golden):
             assert np.array_equal(o.cpu().numpy(), f[p + key]), (p, key)
 
 
-@pytest.mark.parametrize("T,N", [(128, 4096), (128, 131072 + 4), (128, 131072), (3, 5), (1, 200000)])
+@pytest.mark.parametrize("T,N", [(128, 4096), (128, 131072 + 4), (128, 131072), (3, 5), (1, 200000), (16, 262144),
+                                 (8, 262144 + 2), (4, 131071)])
 def test_gae_random_vs_oracle(T, N):
-    """Covers both lane widths (1 env/lane and the 4-env float4 path) and ragged N."""
+    """Covers every lane width (1 env/lane, float2 lanes from N = 131,072, float4 lanes from
+    262,144; odd N falls back to 1 env/lane) and ragged N."""
     rs = np.random.RandomState(T * 7 + N)
     rew = (rs.rand(T, N) < 0.02).astype(np.float32) + rs.randn(T, N).astype(np.float32) * 0.1
     val = rs.randn(T, N).astype(np.float32)
