@@ -52,6 +52,7 @@ FC_WGRAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_WGRAD_SPLIT_MIN", "0"))
 # main stream's dgrad chain (wgrad3 || dgrad3, wgrad2 || dgrad2; the fc weight gradient ||
 # the fc dgrad), joined before the optimizer reads the gradients (PPOX_BWD_STREAMS=0: one stream)
 BWD_STREAMS = os.environ.get("PPOX_BWD_STREAMS", "1") != "0"
+BWD_SOLO_DGRAD2_BATCH = int(os.environ.get("PPOX_BWD_SOLO_DGRAD2", "8192"))
 _side = {}
 
 
@@ -334,11 +335,23 @@ class NatureConvs:
         self.wgrad(3, h2, B, g3, dw3, db3, stream=side)
         g2 = torch.empty((B, 9, 9, 64), device=dev)
         self.dgrad(3, g3, B, h2, g2)                            # dX of conv3, times ReLU'(conv2)
-        if side is not None:
+        # wgrad2 beside the conv2 dgrad below BWD_SOLO_DGRAD2_BATCH rows; from it, the persistent
+        # conv2 dgrad (whole CUs, static tile split) runs alone — the side stream drained before it,
+        # wgrad2 forked after it, beside wgrad1 — the same throughput at 16384 rows (A/B), and the
+        # dominant launch's HIP-event time is its own execution time (bench.py roofline)
+        solo = side is not None and B >= BWD_SOLO_DGRAD2_BATCH
+        if side is not None and not solo:
             fork(side, cur)
-        self.wgrad(2, h1, B, g2, dw2, db2, stream=side)
+            self.wgrad(2, h1, B, g2, dw2, db2, stream=side)
+        if solo:
+            join(side, cur)
         g1 = torch.empty((B, 20, 20, 32), device=dev)
         self.dgrad(2, g2, B, h1, g1)                            # dX of conv2, times ReLU'(conv1)
+        if side is None:
+            self.wgrad(2, h1, B, g2, dw2, db2)
+        elif solo:
+            fork(side, cur)
+            self.wgrad(2, h1, B, g2, dw2, db2, stream=side)
         self.wgrad(1, x, B, g1, dw1, db1)
         if side is not None:
             join(side, cur)
