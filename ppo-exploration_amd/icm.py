@@ -95,7 +95,9 @@ class NativeIcm:
         pre1 = self._buf(tag + "_pre1", (rows, H))
         phi = self._buf(tag + "_phi", (rows, H))
         rn = self._buf(tag + "_rowno", (rows,), torch.int32) if rowno else None
-        ws = self._buf("enc_ws", (max(native.icm_encode_workspace_bytes(rows, self.K), 1),), torch.uint8)
+        # a workspace per tag: the collect graph captures its tags' buffers, which a training
+        # encode of another row count must never replace
+        ws = self._buf(tag + "_ws", (max(native.icm_encode_workspace_bytes(rows, self.K), 1),), torch.uint8)
         native.icm_encode(x, rows, idx, T, N, self.K, self.q, self.seg, ws, pre1, phi, rn)
         return (pre1, phi, rn) if rowno else (pre1, phi)
 

@@ -753,6 +753,34 @@ class PPO_ICM(BaseAlgorithm):
         self.beta = 0.2
         self._alloc_train_state()
         self.icm_accum = torch.zeros(1, dtype=torch.float64, device=self.device)
+        # the collect loop (policy + env + K11 curiosity reward) as one captured graph, as PPO's
+        # (PPOX_COLLECT_GRAPH=0: eager launches)
+        self._collect_graph_enabled = os.environ.get("PPOX_COLLECT_GRAPH", "1") != "0"
+        self._cgraph = None
+        self._ir_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+
+    def _collect_graph_ok(self):
+        return (self._collect_graph_enabled and self._icm_native is not None and isinstance(self.env, DeviceAtariEnv)
+                and self.discrete and getattr(self.policy.net, "conv_impl", None) is not None
+                and self.device.type == "cuda")
+
+    def _icm_collect_step_dc(self, t, nat, eta):
+        """Step t of the collect loop with device-resident Philox counters (as PPO._collect_step_dc)
+        plus the K11 curiosity reward; phi(s_t) is in tag c0 / c1 by the parity of t."""
+        ro = self.rollout
+        out, v, _ = self.policy.net(ro.obs_slots[t])
+        native.categorical_sample_dc(out, self.local_envs, self.n_actions, self.env_offset, self.seed, self._ctr[0:1],
+                                     t, ro.actions[t], ro.log_probs[t])
+        ro.values[t].copy_(v)
+        self.env.step_into_dc(ro.obs_slots[t], ro.obs_slots[t + 1], ro.actions[t], ro.rewards[t], ro.masks[t],
+                              ro.done_ret[t], ro.done_len[t], self._ctr[1:2], t + 1)
+        if t == 0:
+            nat.encode(ro.obs_slots[0], "c0")
+        f = nat._buf("c0_phi" if t % 2 == 0 else "c1_phi", (self.local_envs, icm_native.H))
+        f_next = nat.encode(ro.obs_slots[t + 1], "c1" if t % 2 == 0 else "c0")[1]
+        ir = nat._buf("ir", (self.local_envs,))
+        nat.int_reward(f, f_next, ro.actions[t], ro.rewards[t], eta, ir)
+        self._ir_sum += ir.double().mean()
 
     def _icm_x(self, obs):
         x = obs.reshape(obs.shape[0], int(np.prod(obs.shape[1:])))
@@ -765,8 +793,39 @@ class PPO_ICM(BaseAlgorithm):
         ro = self.rollout
         self._ensure_started()
         ro.reset()
+        if self._collect_graph_ok() and self._cgraph is not None:
+            # replay: refresh the packed weight forms (train moved the weights), the counters
+            T, env = self.nstep, self.env
+            self.policy.net.conv_impl.pack(self.local_envs)
+            self._icm_native.pack()
+            self._ctr[0].fill_(self._sample_counter)
+            self._ctr[1].fill_(env.k)
+            self._ir_sum.zero_()
+            self._cgraph.replay()
+            self._sample_counter += T
+            env.k += T
+            self.num_timesteps += T * self.num_envs
+        else:
+            self._collect_eager()
+            if self._collect_graph_ok():  # capture after the first (eager) rollout
+                self._ctr = torch.zeros(2, dtype=torch.int64, device=self.device)
+                g = torch.cuda.CUDAGraph()
+                nat, eta = self._icm_native, self.int_rew_integration
+                with torch.no_grad(), torch.cuda.graph(g):
+                    for t in range(self.nstep):
+                        self._icm_collect_step_dc(t, nat, eta)
+                self._cgraph = g
+        logger.record("rollout/mean_int_reward", float(self._ir_sum.item()) / self.nstep)
+        ro.pos, ro.full = self.nstep, True
+        ro.compute_returns_and_advantages(ro.values[self.nstep - 1], ro.masks[self.nstep - 1])
+        self._finish_episodes()
+        return True
+
+    def _collect_eager(self):
+        ro = self.rollout
         net = self.policy.net
-        ir_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+        ir_sum = self._ir_sum
+        ir_sum.zero_()
         eta = self.int_rew_integration
         icm = self.intrinsic_module
         f_next = None  # phi(s_{t+1}) of the previous step = phi(s_t) of this one (same rows, same math)
@@ -794,11 +853,6 @@ class PPO_ICM(BaseAlgorithm):
                 ir = icm.int_reward_features(f, f_next, ro.actions[t])
             ro.rewards[t].copy_((1 - eta) * ro.rewards[t] + eta * ir)
             ir_sum += ir.double().mean()
-        logger.record("rollout/mean_int_reward", float(ir_sum.item()) / self.nstep)
-        ro.pos, ro.full = self.nstep, True
-        ro.compute_returns_and_advantages(ro.values[self.nstep - 1], ro.masks[self.nstep - 1])
-        self._finish_episodes()
-        return True
 
     @traced("train")
     def train(self):

@@ -435,17 +435,20 @@ def test_learn_reward_target_stops_early(tmp_path, monkeypatch):
     assert len(rows) == 2 and rows[1]["total timesteps"] == str(N * T)
 
 
-def test_collect_graph_matches_eager():
-    """PPO.collect_samples as one captured graph (after the first, eager, collect) == the
-    eager step loop, bitwise, across collect/train iterations (counters on the device,
-    packed weights refreshed before each replay)."""
+@pytest.mark.parametrize("algo", ["PPO", "PPO_ICM"])
+def test_collect_graph_matches_eager(algo):
+    """collect_samples as one captured graph (after the first, eager, collect) == the eager
+    step loop, bitwise, across collect/train iterations (counters on the device, packed
+    weights refreshed before each replay; PPO_ICM: with the K11 curiosity rewards mixed in)."""
+    import logger
     import ppo
+    logger.configure(algo, "BreakoutNoFrameskip-v4", quiet=True)
 
     def run(graph):
         np.random.seed(0)
         torch.manual_seed(0)
-        alg = ppo.PPO(env_id="BreakoutNoFrameskip-v4", n_envs=16, nstep=8, batch_size=64, n_epochs=1, quiet=True,
-                      seed=5)
+        alg = getattr(ppo, algo)(env_id="BreakoutNoFrameskip-v4", n_envs=16, nstep=8, batch_size=64, n_epochs=1,
+                                 quiet=True, seed=5)
         alg._collect_graph_enabled = graph
         outs = []
         for _ in range(3):
@@ -453,8 +456,11 @@ def test_collect_graph_matches_eager():
             ro = alg.rollout
             outs.append([x.clone() for x in (ro.actions, ro.rewards, ro.values, ro.log_probs, ro.masks,
                                               ro.obs_slots, ro.advantages)])
+            if algo == "PPO_ICM":
+                outs[-1].append(alg._ir_sum.clone())
             alg.train()
-        return outs, alg.flat.data.clone(), alg._cgraph is not None, alg.num_timesteps
+        w = alg.flat.data.clone() if algo == "PPO" else torch.cat([alg.flat.data, alg.icm_flat.data])
+        return outs, w, alg._cgraph is not None, alg.num_timesteps
 
     (a, wa, ga, na), (b, wb, gb, nb) = run(False), run(True)
     assert not ga and gb and na == nb
