@@ -42,7 +42,7 @@ def pmc_traffic(kernel):
 # (layer input 0 = the u8 frame stack, 28,224 B; f32 NHWC activations after)
 CONV_MAC = {1: 400 * 256 * 32, 2: 81 * 512 * 64, 3: 49 * 576 * 64}
 ACT_B = {0: 28224, 1: 20 * 20 * 32 * 4, 2: 9 * 9 * 64 * 4, 3: 7 * 7 * 64 * 4}
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA
 # rocprofv3 kernel names of the conv entry points (for the PMC traffic lookup)
 CONV_KERNEL = {("fwd", 1, True): "fwd1_split_kernel<1>",
                ("fwd", 2, True): "sgemm_kernel<SgFwd<32, 20, 20, 4, 4, 2, 64, false>, 4, 2>",
@@ -58,8 +58,8 @@ CONV_KERNEL = {("fwd", 1, True): "fwd1_split_kernel<1>",
 def conv_roofline(key, kt, totals):
     """Roofline of the dominant conv launch: algorithmic FLOPs (2 x MACs x batch) per launch /
     mean HIP-event duration.  The f32 kernels run v_mfma_f32_32x32x2_f32 (peak 157.3 TF/s);
-    the split-bf16 kernels issue 6 bf16 MFMA products per f32 MAC (3 when one operand is the
-    u8 frame), so their f32-equivalent peak is 2500 / 6 (or / 3) TF/s."""
+    the split-f16 kernels issue 3 f16 MFMA products per f32 MAC (2 when one operand is the
+    u8 frame), so their f32-equivalent peak is 2500 / 3 (or / 2) TF/s."""
     import numpy as np
     name, layer = key.split(":")
     layer = int(layer)
@@ -69,8 +69,8 @@ def conv_roofline(key, kt, totals):
     mean_ms = float(np.mean([t for t, _ in kt]))
     flops = 2.0 * CONV_MAC[layer] * batch
     ach = flops / (mean_ms * 1e-3) / 1e12
-    products = (3 if (layer == 1 and op != "dgrad") else 6) if split else 1
-    peak = BF16_MFMA_PEAK_TFLOPS / products if split else FP32_MFMA_PEAK_TFLOPS
+    products = (2 if (layer == 1 and op != "dgrad") else 3) if split else 1
+    peak = F16_MFMA_PEAK_TFLOPS / products if split else FP32_MFMA_PEAK_TFLOPS
     # input + output (fwd), output grad + ReLU mask + input grad (dgrad), input + output grad (wgrad)
     per = ACT_B[layer] + (2 * ACT_B[layer - 1] if op == "dgrad" else ACT_B[layer - 1])
     kname = CONV_KERNEL.get((op, layer, split))
@@ -78,7 +78,7 @@ def conv_roofline(key, kt, totals):
     tot = sum(totals.values()) or 1.0
     # the binding roofline is the larger of the two lower bounds on the launch: MFMA work at
     # the MFMA peak, or the algorithmic bytes at the HBM peak (conv2 dgrad moves 2.0 GB per
-    # 87 GFLOP at B = 16384: 252 us of HBM vs 209 us of split-bf16 MFMA)
+    # 87 GFLOP at B = 16384: 252 us of HBM vs 104 us of split-f16 MFMA)
     alg_bytes = batch * per
     t_mfma, t_hbm = flops / (peak * 1e12), alg_bytes / (HBM_PEAK_GBS * 1e9)
     mfma_frac = ach / peak
@@ -103,7 +103,7 @@ def conv_roofline(key, kt, totals):
                          "iteration; the timed launches run beside the side-stream weight gradients "
                          "(convs.BWD_STREAMS), so mean_us includes any sharing of the GPU with them",
             "peak_note": "f32 MFMA 157.3 TF/s" if not split else
-                         f"bf16 MFMA 2500 TF/s / {products} products per f32 MAC (split-bf16, fp32-class accuracy)"}
+                         f"f16 MFMA 2500 TF/s / {products} products per f32 MAC (split-f16, fp32-class accuracy)"}
 
 
 def gae_kernel_ms(alg, dual, reps=20):

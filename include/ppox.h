@@ -284,8 +284,10 @@ int ppox_vecnorm_reward(float* rewards, const uint8_t* dones, double* ret, int64
                         int32_t update, void* stream);
 
 /* NatureCNN hidden layer Linear(3136, 512) + ReLU (.ipynb_checkpoints/models-checkpoint.py:58-59)
- * on the split-bf16 GEMM: weights packed (once per optimizer step) by ppox_nature_fc_pack into
- * ppox_nature_fc_pack_elems() uint16 each for the forward (W^T) and the dgrad (W) operand.
+ * on the split-f16 GEMM (see the K6 split section below for the arithmetic and the amax slots):
+ * weights packed (once per optimizer step) by ppox_nature_fc_pack into ppox_nature_fc_pack_elems()
+ * uint16 each for the forward (W^T) and the dgrad (W) operand.  amax_h3 / amax_df: the slots of
+ * the A operand (required); amax_g3: the slots the dgrad records g3's amax into (nullable).
  * Both run in NHWC feature order: h3 is the split conv3 forward's NHWC output (batch, 7, 7, 64)
  * and W is packed through the permutation f = p * 64 + c <- Flatten feature c * 49 + p.
  * fwd: f = relu(h3 @ W^T + b); dgrad: g3 (NHWC (B,7,7,64)) = (df @ W) * (h3 > 0)
@@ -299,24 +301,26 @@ int ppox_nature_pack_all(const float* w1, const float* w2, const float* w3, cons
                          uint16_t* qfc_fwd, uint16_t* qfc_dgrad, void* stream);
 int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_dgrad, void* stream);
 int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
-                       void* stream);
+                       const uint32_t* amax_h3, void* stream);
 int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
-                         void* stream);
+                         const uint32_t* amax_df, uint32_t* amax_g3, void* stream);
 /* fc forward (as ppox_nature_fc_fwd) split over K for small batches: 2-8 K-ranges per (128-row
  * tile, 64-column block) so the grid fills the chip, partial products into the workspace
  * (ppox_nature_fc_fwd_splitk_workspace_bytes(batch)), then one fixed-order reduce adding the
  * partials, the bias and the ReLU.  Replaces the same site (models-checkpoint.py:58-59). */
 int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch);
 int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias,
-                              void* workspace, int64_t workspace_bytes, float* f, void* stream);
+                              void* workspace, int64_t workspace_bytes, float* f, const uint32_t* amax_h3,
+                              void* stream);
 /* fc weight gradient dW (512 x 3136, the weight's Flatten order) = df^T @ h3 over the batch,
- * split-bf16 (fp32-class), deterministic: df (batch, 512) is dL/df already ReLU-masked, h3 the
+ * split-f16 (fp32-class; amax_df, amax_h3: the operands' slots), deterministic: df (batch, 512) is dL/df already ReLU-masked, h3 the
  * NHWC (batch, 7, 7, 64) conv3 output of the split forward.  Replaces the library GEMM of
  * torch.nn.Linear's backward (reference: models-checkpoint.py:58-59 trained by ppo.py:236-238).
  * batch 0 writes a zero gradient.  workspace: ppox_nature_fc_wgrad_workspace_bytes(batch). */
 int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch);
 int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float* h3, void* workspace,
-                         int64_t workspace_bytes, float* dw, void* stream);
+                         int64_t workspace_bytes, float* dw, const uint32_t* amax_df, const uint32_t* amax_h3,
+                         void* stream);
 
 /* ES-NSRA (evolution_strategies.py:103-384, csrc/es.hip), float64 throughout.
  * ppox_es_noise: eps[p][j] ~ N(0,1) for members member0..member0+P-1 of a generation
@@ -341,6 +345,9 @@ int ppox_es_update(const double* eps, const double* coef, int64_t P, int64_t n_p
  * autograd of nn.ReLU / Linear(H, 1) at .ipynb_checkpoints/models-checkpoint.py:60-87):
  * grad = act > 0 ? grad : 0 in place (n % 4 == 0); out[b][j] = dv[b] * w[j] * (act[b][j] > 0). */
 int ppox_relu_backward_(float* grad, const float* act, int64_t n, void* stream);
+/* as ppox_relu_backward_, also recording max |grad| into amax (split-f16 slots, below): the fc
+ * output grad df that the split fc dgrad / weight gradient take as an operand */
+int ppox_relu_backward_amax_(float* grad, const float* act, int64_t n, uint32_t* amax, void* stream);
 /* Column-reduction gradients of the NatureCNN heads (models-checkpoint.py:60-87; the
  * explicit backward of models.CnnActorCritic) in one pass over f, e, de, df (rows x h):
  * w_actor (A x h) = dout^T f, b_actor = sum dout, w_critic (h) = dv^T e, b_critic = sum dv,
@@ -364,39 +371,52 @@ int ppox_outer_relu_backward(const float* dv, const float* w, const float* act, 
                              float* out, void* stream);
 
 /* ---------------------------------------------------------------------------
- * K6, split-bf16 forms (csrc/conv_split.hip): the same ops, layouts and fused
- * epilogues as above, on the bf16 matrix cores (v_mfma_f32_32x32x16_bf16) with
- * every f32 operand split exactly into three bf16 planes (a = a0 + a1 + a2).
- * Products a*b keep the six terms a_i*b_j with i + j <= 2 (dropped terms
- * < 3*2^-22 |ab|); large and small terms accumulate separately in f32.  The
- * uint8 frames of layer 1 are exact in one plane.  Accuracy: fp32-class (error
+ * K6, split-f16 forms (csrc/conv_split.hip, csrc/conv.hip): the same ops, layouts and
+ * fused epilogues as above, on the f16 matrix cores (v_mfma_f32_32x32x16_f16).  Every f32
+ * operand x is scaled by a power of two 2^E per tensor (max|x| 2^E in [2^14, 2^15)) and split
+ * by round-to-nearest into two fp16 planes, x 2^E = h + l + r with |r| <= 2^-24 |x 2^E|; a
+ * product keeps the three terms hA hB + hA lB + lA hB (the dropped lA lB <= 2^-22 |ab|), large
+ * and small terms accumulated separately in f32, and the result is unscaled exactly.  The
+ * uint8 frames of layer 1 are exact in one plane (two products).  Accuracy: fp32-class (error
  * vs fp64 at or below the f32-MFMA kernels', tests/test_kernels_gpu.py).
- * Weights are packed by ppox_nature_pack_split into bf16 planes (uint16
- * storage) of ppox_nature_split_pack_elems(which) elements: which = 1, 2, 3
- * (forward weights of that layer), 12, 13 (dgrad weights of conv2 / conv3).
+ *
+ * Operand scales.  A tensor's "amax slots" are ppox_amax_slots() uint32 (16-B aligned) holding
+ * the f32 bits of max |x| spread over the slots (the consumer takes their maximum).  The caller
+ * zeroes them before the tensor is produced; the kernels that produce an operand of a later
+ * split GEMM record into the slots passed as amax_y / amax_out (nullable: not recorded), and
+ * ppox_amax records any other tensor's (n % 4 == 0).  Weights carry their own scale: the
+ * packers write it after the planes of ppox_nature_split_pack_elems(which) elements (which =
+ * 1, 2, 3: forward weights of that layer; 12, 13: dgrad weights of conv2 / conv3).
  * Replaces the same reference sites as the f32 forms.  One layout difference: the split
  * conv3 forward writes its output NHWC, y (batch, 7, 7, 64) — feature p * 64 + c instead
- * of the reference's Flatten feature c * 49 + p — which the split fc layer below consumes
+ * of the reference's Flatten feature c * 49 + p — which the split fc layer above consumes
  * (its weights are packed through that permutation).
  * -------------------------------------------------------------------------*/
+int32_t ppox_amax_slots(void);
+int ppox_amax(const float* x, int64_t n, uint32_t* amax, void* stream);
 int64_t ppox_nature_split_pack_elems(int32_t which);
 int ppox_nature_pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1,
                            uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3, void* stream);
+/* amax_x: slots of x (layers 2, 3; null for layer 1's frames); amax_y: y's slots (nullable) */
 int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
                                int64_t T, int64_t N_env, int64_t x_sample_stride,
-                               const uint16_t* wq, const float* bias, float* y, void* stream);
-/* dgrad (as ppox_nature_conv_dgrad) of conv2/conv3 with split weights (which = 12, 13). */
+                               const uint16_t* wq, const float* bias, float* y, const uint32_t* amax_x,
+                               uint32_t* amax_y, void* stream);
+/* dgrad (as ppox_nature_conv_dgrad) of conv2/conv3 with split weights (which = 12, 13);
+ * amax_g: grad_out's slots, amax_out: grad_in's (nullable). */
 int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch,
                                  const uint16_t* wqd, const float* prev_act, float* grad_in,
-                                 void* stream);
+                                 const uint32_t* amax_g, uint32_t* amax_out, void* stream);
 /* dW [co][ci][ky][kx] and db (as ppox_nature_conv_wgrad + ppox_nature_wgrad_reduce, in one
  * call): split-K slabs into a workspace of ppox_nature_wgrad_split_workspace_bytes(layer,
  * batch), reduced in a fixed order (deterministic).  x: u8 frames (layer 1, samples
- * x_sample_stride bytes apart) or NHWC f32; grad_out: ReLU-masked NHWC output grad. */
+ * x_sample_stride bytes apart; amax_x null) or NHWC f32; grad_out: ReLU-masked NHWC output
+ * grad (amax_g its slots). */
 int64_t ppox_nature_wgrad_split_workspace_bytes(int32_t layer, int64_t batch);
 int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_t batch,
                                  int64_t x_sample_stride, const float* grad_out, void* workspace,
-                                 int64_t workspace_bytes, float* dw, float* db, void* stream);
+                                 int64_t workspace_bytes, float* dw, float* db, const uint32_t* amax_x,
+                                 const uint32_t* amax_g, void* stream);
 
 /* conv1 split wgrad with the minibatch gather fused: sample n is env-major row idx[n]
  * (i = env * T + step) of the step-major (T, N_env, 4, 84, 84) uint8 rollout frames x.
@@ -404,7 +424,8 @@ int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_t batch,
  * observations of buffer.py:97-109 / models-checkpoint.py:52-58 (Conv2d(4, 32, 8, 4) backward). */
 int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
                                      int64_t T, int64_t N_env, const float* grad_out, void* workspace,
-                                     int64_t workspace_bytes, float* dw, float* db, void* stream);
+                                     int64_t workspace_bytes, float* dw, float* db, const uint32_t* amax_g,
+                                     void* stream);
 
 /* ---------------------------------------------------------------------------
  * K11 ICM on image observations (csrc/icm.hip): the IntrinsicCuriosityModule of

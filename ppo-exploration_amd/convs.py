@@ -8,10 +8,12 @@ Backward: libppox MFMA dgrad (ReLU backward of the layer below fused) and
 split-K wgrad (+ bias grad, deterministic fixed-order reduction) kernels.
 
 Math modes (PPOX_CONV_MATH, default "split"):
-  "split" — f32 operands split exactly into three bf16 planes on the bf16 matrix
-            cores (csrc/conv_split.hip): fp32-class accuracy (measured below the
-            f32-MFMA kernels' error vs fp64, tools/split_probe.py) at up to 16x
-            the f32-input MFMA rate.  Ops without a split kernel yet use "f32".
+  "split" — f32 operands scaled per tensor by a power of two and split into two fp16
+            planes on the f16 matrix cores, three products per multiply (csrc/conv.hip,
+            csrc/conv_split.hip): fp32-class accuracy (at or below the f32-MFMA kernels'
+            error vs fp64, tests/test_kernels_gpu.py).  The per-tensor scales come from
+            "amax slots" that each producing kernel records into (one zeroed table per
+            forward pass, AM_* rows below).  Ops without a split kernel yet use "f32".
   "split_all" — every op that has a split kernel, including those measured slower
             than their f32 kernel at the training batch (SPLIT_SLOWER; tests).
   "f32"   — v_mfma_f32_32x32x2_f32: every product an exact f32 FMA (csrc/conv.hip).
@@ -46,6 +48,11 @@ FC_DGRAD_FUSED_MAX_BATCH = int(os.environ.get("PPOX_FC_DGRAD_FUSED_MAX", str(1 <
 # fc weight gradient on the split wgrad kernel (ppox_nature_fc_wgrad) from this batch up,
 # the rocBLAS f32 GEMM + NHWC -> Flatten permute below (PPOX_FC_WGRAD_SPLIT_MIN overrides)
 FC_WGRAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_WGRAD_SPLIT_MIN", "0"))
+
+# rows of a pass's amax table (native.amax_table): the split-f16 operands of the trunk, each
+# recorded by the kernel that produces it and read by the kernels that consume it
+AM_H1, AM_H2, AM_H3, AM_DF, AM_G3, AM_G2, AM_G1 = range(7)
+AM_ROWS = 8
 
 
 # backward on two streams: each layer's weight gradient runs on a side stream beside the
@@ -124,23 +131,23 @@ class _NatureTrunk(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, convs, w1, b1, w2, b2, w3, b3):
-        h1, h2, h3 = convs.forward_acts(x)
+        h1, h2, h3, am = convs.forward_acts(x)
         ctx.convs = convs
-        ctx.save_for_backward(x, h1, h2, h3)
+        ctx.save_for_backward(x, h1, h2, h3, am)
         return h3.permute(0, 3, 1, 2) if convs.nhwc3 else h3
 
     @staticmethod
     def backward(ctx, dh3):
-        x, h1, h2, h3 = ctx.saved_tensors
+        x, h1, h2, h3, am = ctx.saved_tensors
         convs = ctx.convs
         grads = [torch.zeros_like(t) for t in (convs.c1.weight, convs.c1.bias, convs.c2.weight, convs.c2.bias,
                                                convs.c3.weight, convs.c3.bias)]
         if convs.nhwc3:
             g3 = dh3.permute(0, 2, 3, 1).contiguous()
-            native.relu_backward_(g3, h3)
-            convs.backward_acts(x, h1, h2, h3, None, *grads, g3=g3)
+            native.relu_backward_(g3, h3, amax=am[AM_G3])
+            convs.backward_acts(x, h1, h2, h3, None, *grads, g3=g3, am=am)
         else:
-            convs.backward_acts(x, h1, h2, h3, dh3.contiguous(), *grads)
+            convs.backward_acts(x, h1, h2, h3, dh3.contiguous(), *grads, am=am)
         return (None, None, *grads)
 
 
@@ -239,55 +246,70 @@ class NatureConvs:
         self._version = None
         self._packed = set()
 
-    # -- per-op dispatch (layer 1 input: uint8 frames, sample stride 4*84*84 bytes)
-    def fwd(self, layer, x, B, bias, y):
+    # -- per-op dispatch (layer 1 input: uint8 frames, sample stride 4*84*84 bytes).  am: the
+    # pass's amax table; a split kernel reads its f32 operands' rows and records its output's, an
+    # f32 kernel whose output feeds a split one has it recorded by ppox_amax
+    def fwd(self, layer, x, B, bias, y, am):
         stride = 4 * 84 * 84 if layer == 1 else 0
+        out_am = am[AM_H1 + layer - 1] if self.math != "f32" else None
         if isinstance(x, RolloutRows):
             assert layer == 1 and self.uses_split("fwd", 1)
-            native.nature_conv_fwd_split(1, x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y)
+            native.nature_conv_fwd_split(1, x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y, amax_y=out_am)
             return
         if self.uses_split("fwd", layer):
-            native.nature_conv_fwd_split(layer, x, B, None, 0, 0, stride, self.q[layer], bias, y)
+            native.nature_conv_fwd_split(layer, x, B, None, 0, 0, stride, self.q[layer], bias, y,
+                                         amax_x=am[AM_H1 + layer - 2] if layer > 1 else None, amax_y=out_am)
         else:
             wp = (self.wp1, self.wp2, self.wp3)[layer - 1]
             native.nature_conv_fwd(layer, x, B, None, 0, 0, stride, wp, bias, y)
+            if out_am is not None:
+                native.amax(y, out_am)
 
-    def dgrad(self, layer, g, B, prev_act, out):
+    def dgrad(self, layer, g, B, prev_act, out, am):
         self.pack(B)  # the conv2 dgrad form depends on the batch
+        g_am, out_am = (am[AM_G3], am[AM_G2]) if layer == 3 else (am[AM_G2], am[AM_G1])
         if self.uses_split("dgrad", layer, B):
-            native.nature_conv_dgrad_split(layer, g, B, self.q[10 + layer], prev_act, out)
+            native.nature_conv_dgrad_split(layer, g, B, self.q[10 + layer], prev_act, out, amax_g=g_am,
+                                           amax_out=out_am)
         else:
             native.nature_conv_dgrad(layer, g, B, self.wpd2 if layer == 2 else self.wpd3, prev_act, out)
+            if self.math != "f32":
+                native.amax(out, out_am)
 
-    def wgrad(self, layer, x, B, g, dw, db, stream=None):
+    def wgrad(self, layer, x, B, g, dw, db, am, stream=None):
         stride = 4 * 84 * 84 if layer == 1 else 0
+        g_am = am[(AM_G1, AM_G2, AM_G3)[layer - 1]]
         if isinstance(x, RolloutRows):
             assert layer == 1 and self.uses_split("wgrad", 1)
             native.nature_conv_wgrad_split_idx(1, x.frames, B, x.idx, x.T, x.N, g, self.workspace(1, B, True), dw, db,
-                                               stream=stream)
+                                               amax_g=g_am, stream=stream)
             return
         if self.uses_split("wgrad", layer):
-            native.nature_conv_wgrad_split(layer, x, B, stride, g, self.workspace(layer, B, True), dw, db, stream=stream)
+            native.nature_conv_wgrad_split(layer, x, B, stride, g, self.workspace(layer, B, True), dw, db,
+                                           amax_x=am[AM_H1 + layer - 2] if layer > 1 else None, amax_g=g_am,
+                                           stream=stream)
         else:
             native.nature_conv_wgrad(layer, x, B, None, 0, 0, stride, g, self.workspace(layer, B), dw, db, stream=stream)
 
     def forward_acts(self, x):
-        """Trunk forward: (h1 NHWC, h2 NHWC, h3) activations (ReLU applied); h3 is NHWC
-        (B, 7, 7, 64) in split math (self.nhwc3), NCHW (B, 64, 7, 7) in f32 math."""
+        """Trunk forward: (h1 NHWC, h2 NHWC, h3, am) — activations (ReLU applied) and the pass's
+        amax table (AM_* rows; the backward of the same pass records its gradients' rows); h3 is
+        NHWC (B, 7, 7, 64) in split math (self.nhwc3), NCHW (B, 64, 7, 7) in f32 math."""
         self.pack(x.shape[0])
         B = x.shape[0]
         dev = x.device
         h1 = torch.empty((B, 20, 20, 32), device=dev)
         h2 = torch.empty((B, 9, 9, 64), device=dev)
         h3 = torch.empty((B, 7, 7, 64) if self.nhwc3 else (B, 64, 7, 7), device=dev)
+        am = native.amax_table(AM_ROWS, dev)
         if B:
-            self.fwd(1, x, B, self.c1.bias, h1)
-            self.fwd(2, h1, B, self.c2.bias, h2)
-            self.fwd(3, h2, B, self.c3.bias, h3)
-        return h1, h2, h3
+            self.fwd(1, x, B, self.c1.bias, h1, am)
+            self.fwd(2, h1, B, self.c2.bias, h2, am)
+            self.fwd(3, h2, B, self.c3.bias, h3, am)
+        return h1, h2, h3, am
 
     # ---- fc layer (split math): forward and the dgrad fused with the trunk's ReLU backward
-    def fc_forward(self, h3):
+    def fc_forward(self, h3, am):
         """f = relu(h3 @ W^T + b), h3 (B, 7, 7, 64) NHWC (split math): the split-bf16 GEMM when
         the batch fills the chip (ceil(B/128) row tiles x 8 column blocks >= ~512 workgroups),
         rocBLAS on the NHWC-permuted weight below."""
@@ -304,21 +326,23 @@ class NatureConvs:
                 ws = torch.empty(max(native.nature_fc_fwd_splitk_workspace_bytes(B), 16), dtype=torch.uint8,
                                  device=h3.device)
                 self._ws[("fc_sk", B)] = ws
-            native.nature_fc_fwd_splitk(h3, B, self.qfc[0], self.fc.bias, ws, f)
+            native.nature_fc_fwd_splitk(h3, B, self.qfc[0], self.fc.bias, ws, f, amax_h3=am[AM_H3])
         else:
-            native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f)
+            native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f, amax_h3=am[AM_H3])
         return f
 
-    def fc_dgrad_g3(self, df, h3):
-        """g3 (B, 7, 7, 64) NHWC = (df @ W) * (h3 > 0), df = dL/df after the fc ReLU, h3 NHWC."""
+    def fc_dgrad_g3(self, df, h3, am):
+        """g3 (B, 7, 7, 64) NHWC = (df @ W) * (h3 > 0), df = dL/df after the fc ReLU (its amax in
+        am[AM_DF]), h3 NHWC; records g3's amax."""
         B = df.shape[0]
         g3 = torch.empty((B, 7, 7, 64), device=df.device)
-        native.nature_fc_dgrad(df.contiguous(), B, self.qfc[1], h3, g3)
+        native.nature_fc_dgrad(df.contiguous(), B, self.qfc[1], h3, g3, amax_df=am[AM_DF], amax_g3=am[AM_G3])
         return g3
 
-    def backward_acts(self, x, h1, h2, h3, dh3, dw1, db1, dw2, db2, dw3, db3, g3=None):
+    def backward_acts(self, x, h1, h2, h3, dh3, dw1, db1, dw2, db2, dw3, db3, g3=None, am=None):
         """Trunk backward from dL/dh3 (f32 math: B x 3136 in NCHW order, before the ReLU mask)
-        — or from g3, the already masked NHWC grad: writes (overwrites) the six conv gradients."""
+        — or from g3, the already masked NHWC grad whose amax is in am[AM_G3] (am: the forward
+        pass's table): writes (overwrites) the six conv gradients."""
         B = x.shape[0]
         if B == 0:
             for t in (dw1, db1, dw2, db2, dw3, db3):
@@ -328,13 +352,15 @@ class NatureConvs:
         if g3 is None:
             g3 = torch.empty((B, 7, 7, 64), device=dev)
             native.nchw_to_nhwc_relu_grad(dh3, h3, B, g3)      # ReLU backward of conv3, to NHWC
+            if self.math != "f32":
+                native.amax(g3, am[AM_G3])
         side = side_stream(dev) if BWD_STREAMS and dev.type == "cuda" else None
         cur = torch.cuda.current_stream() if side is not None else None
         if side is not None:  # wgrad3 beside dgrad3 (the tensors stay referenced until the join below)
             fork(side, cur)
-        self.wgrad(3, h2, B, g3, dw3, db3, stream=side)
+        self.wgrad(3, h2, B, g3, dw3, db3, am, stream=side)
         g2 = torch.empty((B, 9, 9, 64), device=dev)
-        self.dgrad(3, g3, B, h2, g2)                            # dX of conv3, times ReLU'(conv2)
+        self.dgrad(3, g3, B, h2, g2, am)                        # dX of conv3, times ReLU'(conv2)
         # wgrad2 beside the conv2 dgrad below BWD_SOLO_DGRAD2_BATCH rows; from it, the persistent
         # conv2 dgrad (whole CUs, static tile split) runs alone — the side stream drained before it,
         # wgrad2 forked after it, beside wgrad1 — the same throughput at 16384 rows (A/B), and the
@@ -342,17 +368,17 @@ class NatureConvs:
         solo = side is not None and B >= BWD_SOLO_DGRAD2_BATCH
         if side is not None and not solo:
             fork(side, cur)
-            self.wgrad(2, h1, B, g2, dw2, db2, stream=side)
+            self.wgrad(2, h1, B, g2, dw2, db2, am, stream=side)
         if solo:
             join(side, cur)
         g1 = torch.empty((B, 20, 20, 32), device=dev)
-        self.dgrad(2, g2, B, h1, g1)                            # dX of conv2, times ReLU'(conv1)
+        self.dgrad(2, g2, B, h1, g1, am)                        # dX of conv2, times ReLU'(conv1)
         if side is None:
-            self.wgrad(2, h1, B, g2, dw2, db2)
+            self.wgrad(2, h1, B, g2, dw2, db2, am)
         elif solo:
             fork(side, cur)
-            self.wgrad(2, h1, B, g2, dw2, db2, stream=side)
-        self.wgrad(1, x, B, g1, dw1, db1)
+            self.wgrad(2, h1, B, g2, dw2, db2, am, stream=side)
+        self.wgrad(1, x, B, g1, dw1, db1, am)
         if side is not None:
             join(side, cur)
 

@@ -129,9 +129,10 @@ struct FwdBase {
     __device__ static const float* bchunk(const Args& a, const Tile&, int c) { return a.wp + (long long)c * BK * NOUT; }
     __device__ static int bchunk_id(const Tile&, int c) { return c; }  // 32-row block of the packed [K][NOUT]
     __device__ static float prefetch(const Args& a, const Tile&, int, int co) { return a.bias[co]; }
-    __device__ static void store_pre(const Args& a, const Tile& t, int row, int co, float acc, float bias) {
+    // stores one output element; returns it (0 for rows past the end: the amax of the output)
+    __device__ static float store_pre(const Args& a, const Tile& t, int row, int co, float acc, float bias) {
         const long long m = t.m0 + row;
-        if (m >= t.M) return;
+        if (m >= t.M) return 0.f;
         const float v = fmaxf(acc + bias, 0.f);
         if constexpr (OUT_NCHW) {
             const long long n = m / L::P;
@@ -139,6 +140,7 @@ struct FwdBase {
         } else {
             a.y[m * L::COUT + co] = v;
         }
+        return v;
     }
 };
 
@@ -226,10 +228,12 @@ struct DgradPMProblem {
         n = n < a.batch ? n : t.n0;
         return a.mask[(n * NPOS + t.pos) * L::CIN + ci];
     }
-    __device__ static void store_pre(const Args& a, const Tile& t, int row, int ci, float acc, float m) {
+    __device__ static float store_pre(const Args& a, const Tile& t, int row, int ci, float acc, float m) {
         const long long n = t.n0 + row;
-        if (n >= a.batch) return;
-        a.y[(n * NPOS + t.pos) * L::CIN + ci] = m > 0.f ? acc : 0.f;
+        if (n >= a.batch) return 0.f;
+        const float v = m > 0.f ? acc : 0.f;
+        a.y[(n * NPOS + t.pos) * L::CIN + ci] = v;
+        return v;
     }
 };
 
@@ -316,23 +320,24 @@ __global__ void __launch_bounds__(256, 2) igemm_kernel(Args a) {
 
 
 // ---------------------------------------------------------------------------
-// Pre-split B operands of the split-bf16 GEMMs (sgemm_kernel): a [K][NOUT] matrix as three
-// exact bf16 planes in MFMA fragment order.
+// Pre-split B operands of the split-f16 GEMMs (sgemm_kernel, the wgrad-free kernels): a
+// [K][NOUT] matrix times 2^E as two fp16 planes in MFMA fragment order, followed by the
+// buffer's tail (pack_tail): the weight tensor's amax partials and the exponent E.
 // ---------------------------------------------------------------------------
 // packed position of natural element (row k, col) of a [K][nout] matrix, plane p:
 // chunk (k / 32) x k-step s x column tile j x plane x lane (h, col & 31) x e
 __host__ __device__ constexpr long long split_frag_index(int k, int col, int nout, int p) {
     const int ch = k >> 5, kl = k & 31, s = kl >> 4, h = (kl >> 3) & 1, e = kl & 7;
     const int nt = nout / 32, j = col >> 5, l = h * 32 + (col & 31);
-    return ((((long long)(ch * 2 + s) * nt + j) * 3 + p) * 64 + l) * 8 + e;
+    return ((((long long)(ch * 2 + s) * nt + j) * NPL + p) * 64 + l) * 8 + e;
 }
 
 // Output-major split packing: unit u = one 16-B fragment run (8 consecutive k of one
-// column, all three planes) of the split_frag_index layout of a [K][NOUT] matrix — its
+// column, both planes) of the split_frag_index layout of a [K][NOUT] matrix — its
 // eight source values are gathered (coalesced across lanes: adjacent units are adjacent
-// columns) and written as three 16-B stores, instead of 2-B stores scattered 16 B apart.
+// columns), scaled by s and written as two 16-B stores, instead of 2-B stores scattered.
 template <int NOUT, class Src>
-__device__ inline void pack_frag_unit(const Src& src, uint16_t* __restrict__ q, long long u) {
+__device__ inline void pack_frag_unit(const Src& src, float s, uint16_t* __restrict__ q, long long u) {
     constexpr int NT = NOUT / 32;
     const int l = (int)(u & 63);
     const long long r = u >> 6;
@@ -342,38 +347,11 @@ __device__ inline void pack_frag_unit(const Src& src, uint16_t* __restrict__ q, 
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = src(k0 + e, col);
-    u32x4 p0, p1, p2;
-    split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), p0, p1, p2);
-    u32x4* d = reinterpret_cast<u32x4*>(q + ((cs * NT + j) * 3) * 512) + l;
+    u32x4 p0, p1;
+    split8h(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), s, p0, p1);
+    u32x4* d = reinterpret_cast<u32x4*>(q + ((cs * NT + j) * NPL) * 512) + l;
     d[0] = p0;
     d[64] = p1;
-    d[128] = p2;
-}
-
-template <class L, bool DGRAD>
-__device__ inline void pack_split_gemm_elem(const float* __restrict__ w, uint16_t* __restrict__ q, int i) {
-    constexpr int NOUT = DGRAD ? L::CIN : L::COUT;
-    if (i >= L::K * L::COUT) return;
-    const int k = i / NOUT, col = i % NOUT;
-    int co, ci, tap;
-    if (DGRAD) {
-        ci = col;
-        co = k % L::COUT;
-        tap = k / L::COUT;
-    } else {
-        co = col;
-        ci = k % L::CIN;
-        tap = k / L::CIN;
-    }
-    uint16_t p0, p1, p2;
-    split3(w[((co * L::CIN + ci) * L::KH + tap / L::KW) * L::KW + tap % L::KW], p0, p1, p2);
-    q[split_frag_index(k, col, NOUT, 0)] = p0;
-    q[split_frag_index(k, col, NOUT, 1)] = p1;
-    q[split_frag_index(k, col, NOUT, 2)] = p2;
-}
-template <class L, bool DGRAD>
-__global__ void pack_split_gemm(const float* __restrict__ w, uint16_t* __restrict__ q) {
-    pack_split_gemm_elem<L, DGRAD>(w, q, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -447,14 +425,14 @@ struct GemmRowsProblem {
             return a.mask[m * N + nc];
         }
     }
-    __device__ static void store_pre(const Args& a, const Tile& t, int row, int col, float acc, float e) {
+    __device__ static float store_pre(const Args& a, const Tile& t, int row, int col, float acc, float e) {
         const long long m = t.m0 + row;
         const int n = t.cb * NB + col;
-        if (m >= t.M || n >= N) return;
-        if constexpr (MODE == FC_FWD)
-            a.y[m * N + n] = fmaxf(acc + e, 0.f);
-        else  // g3 (NHWC) times the ReLU mask of h3 (NHWC): the same element index
-            a.y[m * N + n] = e > 0.f ? acc : 0.f;
+        if (m >= t.M || n >= N) return 0.f;
+        // FC_FWD: relu(acc + bias); FC_DGRAD: g3 (NHWC) times the ReLU mask of h3 (NHWC), the same index
+        const float v = MODE == FC_FWD ? fmaxf(acc + e, 0.f) : (e > 0.f ? acc : 0.f);
+        a.y[m * N + n] = v;
+        return v;
     }
 };
 
@@ -470,28 +448,6 @@ struct GemmRowsProblem {
 using FcFwd = GemmRowsProblem<3136, 512, FC_NB, FC_FWD>;
 using FcDgrad = GemmRowsProblem<512, 3136, FC_NB, FC_DGRAD>;
 static_assert(FC_NB == 64, "sg2 runs the fc layer in 64-column blocks");
-
-// packs B (element (k, n) = w[n * ldw + k] when TRANS, w[k * ldw + n] otherwise) into
-// split_frag_index order per column block, zero beyond N
-template <class Prob, bool TRANS>
-__device__ inline void pack_split_gemm_rows_elem(const float* __restrict__ w, uint16_t* __restrict__ q, long long i) {
-    constexpr int NB = Prob::NOUT, K = Prob::K, N = Prob::N;
-    if (i >= (long long)Prob::NCB * K * NB) return;
-    const int cb = (int)(i / ((long long)K * NB)), rem = (int)(i % ((long long)K * NB));
-    const int k = rem / NB, col = rem % NB, n = cb * NB + col;
-    const float v = n < N ? (TRANS ? w[(long long)n * K + fc_nchw_feature(k)] : w[(long long)k * N + fc_nchw_feature(n)])
-                          : 0.f;
-    uint16_t p0, p1, p2;
-    split3(v, p0, p1, p2);
-    const long long base = (long long)cb * K * NB * 3;
-    q[base + split_frag_index(k, col, NB, 0)] = p0;
-    q[base + split_frag_index(k, col, NB, 1)] = p1;
-    q[base + split_frag_index(k, col, NB, 2)] = p2;
-}
-template <class Prob, bool TRANS>
-__global__ void pack_split_gemm_rows(const float* __restrict__ w, uint16_t* __restrict__ q) {
-    pack_split_gemm_rows_elem<Prob, TRANS>(w, q, (long long)blockIdx.x * blockDim.x + threadIdx.x);
-}
 
 // ---------------------------------------------------------------------------
 // conv2 dgrad in the col2im form (split-bf16), the default conv2 split dgrad.
@@ -519,7 +475,7 @@ __global__ void pack_split_gemm_rows(const float* __restrict__ w, uint16_t* __re
 //   * each class's ReLU-mask operands are loaded a class ahead (at the previous class's
 //     output step), and the output stores are unconditional (threads with nothing to store
 //     write a dummy), so every wave's vmcnt sequence is static and the waits are counted.
-// LDS: 48 KB ring + 64 KB next rows + 37.5 KB class image = 150 KB (one workgroup per CU).
+// LDS: 32 KB ring + 64 KB next rows + 37.5 KB class image = 134 KB (one workgroup per CU).
 // (0.645 vs 0.695 ms for the one-triple-per-workgroup form at B = 16384, same box.)
 // ---------------------------------------------------------------------------
 constexpr int C2S = 3, C2ROWS = C2S * 81, C2PIX = 100;
@@ -530,7 +486,7 @@ constexpr int C2OV = (C2S * C2PIX * 8 + 511) / 512;  // float4 outputs per threa
 // every output store and prefetch at each col2im step)
 __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-constexpr int C2P_TAP = 4 * 3 * 64;                    // u32x4 per tap: 4 k-steps x 3 planes x 64 lanes
+constexpr int C2P_TAP = 4 * NPL * 64;                  // u32x4 per tap: 4 k-steps x 2 planes x 64 lanes
 constexpr int C2P_AN = 256 * 16;                       // u32x4: 256 G rows x 64 f32
 constexpr int C2P_IMG = (C2S * C2PIX * 32 + 32) / 4;   // u32x4: class image + dummy slot
 __device__ float4 kC2Dummy[512];                       // store target of threads with nothing to store
@@ -553,10 +509,14 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
     const long long rows_total = a.batch * L::P;
     const float* g2 = reinterpret_cast<const float*>(a.x);
 
-    // taps k, k+1 (class-tap indices, mod 16) -> ring slots: 3 DMAs per thread
+    // operand scales: G by its tensor's amax, B as packed; the output is unscaled
+    const int ex = split_scale_exp(amax_read(a.amax_x)), ew = *a.wexp;
+    const float sg = exp2i(ex), uo = exp2i(-ex) * exp2i(-ew);
+    float om = 0.f;  // the largest |value| this thread stored (the output's amax)
+    // taps k, k+1 (class-tap indices, mod 16) -> ring slots: 2 DMAs per thread
     auto dmaB2 = [&](int k) {
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
+        for (int r = 0; r < 2 * C2P_TAP / 512; ++r) {
             const int e0 = r * 512 + wave * 64, which = e0 / C2P_TAP, within0 = e0 - which * C2P_TAP;
             const int kk = (k + which) & 15;
             __builtin_amdgcn_global_load_lds(
@@ -582,15 +542,15 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
                                              0, 0);
         }
     };
-    // A: this lane's row of the triple in An, k = 16q + 8h .. +8 -> three bf16 planes
-    u32x4 af[4][3];
+    // A: this lane's row of the triple in An, k = 16q + 8h .. +8 -> two f16 planes (scaled)
+    u32x4 af[4][NPL];
     auto take_A = [&]() {
         const int r = wave * 32 + (lane & 31), sw = r & 15;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int c0 = (lane >> 5) * 2 + 4 * q;
             const u32x4 v0 = An[r * 16 + (c0 ^ sw)], v1 = An[r * 16 + ((c0 + 1) ^ sw)];
-            split8(__builtin_bit_cast(float4, v0), __builtin_bit_cast(float4, v1), af[q][0], af[q][1], af[q][2]);
+            split8h(__builtin_bit_cast(float4, v0), __builtin_bit_cast(float4, v1), sg, af[q][0], af[q][1]);
         }
     };
     auto mfma_tap = [&](int k, f32x16& c) {
@@ -598,8 +558,8 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
         c = zero16();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const u32x4 bf[3] = {Bt[q * 192], Bt[q * 192 + 64], Bt[q * 192 + 128]};
-            mfma_split6(af[q], bf, c, c);
+            const u32x4 bf[NPL] = {Bt[q * NPL * 64], Bt[q * NPL * 64 + 64]};
+            mfma_split3(af[q], bf, c, c);
         }
     };
     // col2im add of tap k into the class image: row (oy, ox) -> class pixel (oy + (i >> 1),
@@ -652,9 +612,11 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
                          : "=&v"(dr) : "v"(da), "v"(zero4) : "memory");
             const float4 d = __builtin_bit_cast(float4, dr);
             const float4 m = mk[j];
-            const float4 y = make_float4(m.x > 0.f ? d.x : 0.f, m.y > 0.f ? d.y : 0.f, m.z > 0.f ? d.z : 0.f,
-                                         m.w > 0.f ? d.w : 0.f);
+            const float4 y = make_float4(m.x > 0.f ? d.x * uo : 0.f, m.y > 0.f ? d.y * uo : 0.f,
+                                         m.z > 0.f ? d.z * uo : 0.f, m.w > 0.f ? d.w * uo : 0.f);
             const long long n = n0 + s;
+            const float ym = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));
+            om = (in && n < a.batch) ? fmaxf(om, ym) : om;  // the dummy slot's sums are not output
             const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
             float4* dst = (in && n < a.batch)
                               ? reinterpret_cast<float4*>(a.y + ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4)
@@ -718,6 +680,7 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
         take_A();  // the next triple's rows (drained at class 1's i = 2, ordered by the barriers since)
         lds_barrier();
     }
+    amax_record(a.amax_y, om);
 }
 
 
@@ -744,7 +707,8 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
 // lane group land on distinct bank quads); the DMA writes LDS lane-linearly, so the
 // swizzle is applied to each lane's GLOBAL source address.
 // ---------------------------------------------------------------------------
-constexpr int SG_BQ = 2 * 2 * 3 * 64;  // u32x4 per B chunk at 64 columns (12 KB)
+constexpr int SG_BQ = 2 * 2 * NPL * 64;  // u32x4 per B chunk at 64 columns (8 KB)
+constexpr int SG_BP = SG_BQ / 64;        // its 1 KB DMA pieces
 
 // LDS fragment reads in inline asm: hipcc's wait insertion cannot tell a ds_read from the
 // ring slot being read apart from the DMAs in flight into the other slots, and puts a
@@ -758,9 +722,9 @@ __device__ inline u32x4 sg_ds_read(uint32_t addr) {
     return r;
 }
 template <int N>
-__device__ inline void sg_lgkm_wait(u32x4 (&v)[8]) {
-    asm volatile("s_waitcnt lgkmcnt(%8)"
-                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+__device__ inline void sg_lgkm_wait(u32x4 (&v)[6]) {
+    asm volatile("s_waitcnt lgkmcnt(%6)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5])
                  : "n"(N));
 }
 template <int N>
@@ -769,13 +733,14 @@ __device__ inline void sg_vm_wait() {
 }
 
 // WAVES waves x 32 rows per workgroup, SLOTS ring slots of one 32-k chunk (A: 128 B per row;
-// B: 12 KB).  8 waves / 3 slots: one workgroup per CU (132 KB), waves 4-7 staggered;
-// 4 waves / 2 slots: two workgroups per CU (56 KB each), whose K walks, prologues and
-// epilogues interleave on every SIMD.
+// B: 8 KB).  8 waves / 3 slots: one workgroup per CU, waves 4-7 staggered; 4 waves / 2 slots:
+// two workgroups per CU (48 KB each), whose K walks, prologues and epilogues interleave on
+// every SIMD.  A is split in registers with its tensor's scale (a.amax_x), B was packed with
+// its own (a.wexp); the epilogue unscales, and records the output's amax (a.amax_y).
 template <class Prob, int WAVES, int SLOTS>
 __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, const u32x4* __restrict__ wq) {
     constexpr int NT = 2, ROWS = 32 * WAVES, AB = ROWS * BK * 4, SLOT = AB + SG_BQ * 16;
-    constexpr int BPW = (12 + WAVES - 1) / WAVES;  // B pieces DMA'd per wave (1 KB each)
+    constexpr int BPW = (SG_BP + WAVES - 1) / WAVES;  // B pieces DMA'd per wave (1 KB each)
     constexpr int NDMA = 4 + BPW;                  // this wave's DMAs per chunk
     constexpr bool STAGGER = WAVES == 8;
     static_assert(Prob::NOUT == 64 && Prob::ROWS == ROWS, "sg2: 32 rows per wave x 64 columns");
@@ -797,11 +762,14 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
         asrc[j] = reinterpret_cast<const uint8_t*>(Prob::row_ptr(a, t, wave * 32 + r)) +
                   ((((lane & 7) ^ ((r >> 1) & 7))) << 4);
     }
-    // B: 12 pieces of 1 KB per chunk, BPW per wave (pieces past 11 re-copy piece 11: the
+    // B: SG_BP pieces of 1 KB per chunk, BPW per wave (pieces past the last re-copy it: the
     // same bytes to the same place), so every wave issues NDMA DMAs per chunk
     int bp[BPW];
 #pragma unroll
-    for (int i = 0; i < BPW; ++i) bp[i] = min(BPW * wave + i, 11);
+    for (int i = 0; i < BPW; ++i) bp[i] = min(BPW * wave + i, SG_BP - 1);
+    // operand scales: A by its tensor's amax, B as packed; the epilogue multiplies by both inverses
+    const int ex = split_scale_exp(amax_read(a.amax_x)), ew = *a.wexp;
+    const float sa = exp2i(ex), ua = exp2i(-ex), uw = exp2i(-ew);
     // chunk c into ring slot S; the chunk index is clamped, not branched on (past the end:
     // the last chunk again, never read)
     auto issue = [&](int c, auto S) {
@@ -833,22 +801,22 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
     // SIMD runs matrix work (the deferred k-step) while its partner reads and splits (VALU).
     // The deferred k-step's operands (split A planes + B fragments) stay in registers.
     const bool late = STAGGER && wave >= 4;
-    u32x4 daf[3], dbf[6];
-    auto mfma6 = [&](const u32x4 (&af)[3], const u32x4* bf) {
+    u32x4 daf[NPL], dbf[NT * NPL];
+    auto mfma3 = [&](const u32x4 (&af)[NPL], const u32x4* bf) {
 #pragma unroll
         for (int j = 0; j < NT; ++j) {
-            const u32x4 b3[3] = {bf[3 * j], bf[3 * j + 1], bf[3 * j + 2]};
-            mfma_split6(af, b3, hi[j], lo[j]);
+            const u32x4 b2[NPL] = {bf[NPL * j], bf[NPL * j + 1]};
+            mfma_split3(af, b2, hi[j], lo[j]);
         }
     };
-    auto split_a = [&](const u32x4 (&g)[8], u32x4 (&af)[3]) {
-        split8(__builtin_bit_cast(float4, g[0]), __builtin_bit_cast(float4, g[1]), af[0], af[1], af[2]);
+    auto split_a = [&](const u32x4 (&g)[6], u32x4 (&af)[NPL]) {
+        split8h(__builtin_bit_cast(float4, g[0]), __builtin_bit_cast(float4, g[1]), sa, af[0], af[1]);
     };
-    // chunk in slot S: 16 fragment reads up front (k-step 0's eight, then k-step 1's), k-step 0
-    // computed once its eight have landed (lgkmcnt(8)) while k-step 1's are in flight
+    // chunk in slot S: 12 fragment reads up front (k-step 0's six, then k-step 1's), k-step 0
+    // computed once its six have landed (lgkmcnt(6)) while k-step 1's are in flight
     auto compute = [&](auto S) {
         constexpr int slot = decltype(S)::value;
-        u32x4 f[2][8];
+        u32x4 f[2][6];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int g0 = 4 * s + 2 * h;
@@ -857,21 +825,21 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
 #pragma unroll
             for (int j = 0; j < NT; ++j)
 #pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    f[s][2 + 3 * j + p] = sg_ds_read(b_lane + slot * SLOT + (((s * NT + j) * 3 + p) * 64) * 16);
+                for (int p = 0; p < NPL; ++p)
+                    f[s][2 + NPL * j + p] = sg_ds_read(b_lane + slot * SLOT + (((s * NT + j) * NPL + p) * 64) * 16);
         }
-        u32x4 af[3];
-        sg_lgkm_wait<8>(f[0]);
+        u32x4 af[NPL];
+        sg_lgkm_wait<6>(f[0]);
         split_a(f[0], af);
-        mfma6(af, f[0] + 2);
+        mfma3(af, f[0] + 2);
         sg_lgkm_wait<0>(f[1]);
         if (late) {  // k-step 1 split now, multiplied after the next barrier
             split_a(f[1], daf);
 #pragma unroll
-            for (int i = 0; i < 6; ++i) dbf[i] = f[1][2 + i];
+            for (int i = 0; i < NT * NPL; ++i) dbf[i] = f[1][2 + i];
         } else {
             split_a(f[1], af);
-            mfma6(af, f[1] + 2);
+            mfma3(af, f[1] + 2);
         }
     };
     // one pipeline step: this wave's DMAs of chunk c waited for (those of the next SLOTS - 2
@@ -882,7 +850,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
         sg_vm_wait<NDMA * (SLOTS - 2)>();
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         issue(c + SLOTS - 1, S2);
-        if (late && c > 0) mfma6(daf, dbf);  // chunk c - 1's deferred k-step
+        if (late && c > 0) mfma3(daf, dbf);  // chunk c - 1's deferred k-step
         compute(S);
     };
     using I0 = std::integral_constant<int, 0>;
@@ -904,9 +872,11 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
             if (c + 1 < nchunk) step(c + 1, I1{}, I0{});
         }
     }
-    if (late && nchunk > 0) mfma6(daf, dbf);
+    if (late && nchunk > 0) mfma3(daf, dbf);
     sg_vm_wait<0>();  // the clamped tail DMAs, before the LDS is released
-    // epilogue, per column tile: its operand loads first (all issued before its first store)
+    // epilogue, per column tile: its operand loads first (all issued before its first store);
+    // om = the largest |value| this lane stored
+    float om = 0.f;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         f32x16 e;
@@ -918,8 +888,10 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
         __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
         for (int q = 0; q < 16; ++q)
-            Prob::store_pre(a, t, wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, j * 32 + r, hi[j][q] + lo[j][q], e[q]);
+            om = fmaxf(om, fabsf(Prob::store_pre(a, t, wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, j * 32 + r,
+                                                 (hi[j][q] + lo[j][q]) * ua * uw, e[q])));
     }
+    amax_record(a.amax_y, om);
 }
 
 #ifndef SG_WAVES
@@ -1046,10 +1018,11 @@ struct SgRowsSK : GemmRowsProblem<K, N, 64, FC_FWD> {
     }
     __device__ static int chunk_off(const Tile& t, int c) { return (t.c0 + c) * BK; }
     __device__ static float prefetch(const Args&, const Tile&, int, int) { return 0.f; }
-    __device__ static void store_pre(const Args& a, const Tile& t, int row, int col, float acc, float) {
+    __device__ static float store_pre(const Args& a, const Tile& t, int row, int col, float acc, float) {
         const long long m = t.m0 + row;
-        if (m >= t.M) return;
+        if (m >= t.M) return 0.f;
         a.y[((long long)t.ks * t.M + m) * N + t.cb * 64 + col] = acc;
+        return acc;
     }
 };
 
@@ -1499,14 +1472,14 @@ __global__ void __launch_bounds__(RED_E * RG) wgrad_reduce(const float* __restri
 template <class L, bool U8, int KT_>
 struct WsCfg {
     static constexpr int KT = KT_, KB = L::K / KT, COUT = L::COUT;
-    static constexpr int XP = U8 ? 1 : 3;                        // X planes
+    static constexpr int XP = U8 ? 1 : NPL;                      // X planes
     static constexpr int NKT = KT / 32, NCT = COUT / 32, TPW = NKT * NCT / 4;
     // wave grid: WC waves along co (WCT co-tiles each) x 4/WC along k (WKT k-tiles each)
     static constexpr int WCT = TPW % NCT == 0 ? NCT : (NCT % TPW == 0 ? TPW : 1);
     static constexpr int WC = NCT / WCT, WKT = NKT / (4 / WC);
     static constexpr int XR = KT * 2, GR = COUT * 2;             // LDS row bytes
     static constexpr int XPB = MS * XR, GPB = MS * GR;           // LDS plane bytes
-    static constexpr int STAGE = XP * XPB + 3 * GPB;
+    static constexpr int STAGE = XP * XPB + NPL * GPB;
     // staging: 8 threads per pixel row; a thread stages XU units of 8 consecutive k and GW
     // consecutive co of one pixel, so its addresses come from one (sample, pixel) pair
     static constexpr int UPX = KT / 8, XU = UPX / 8, GW = COUT / 8;
@@ -1578,12 +1551,15 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         float4 xr[XU][2];
         float4 gr[2];
     };
-    // one step's bf16 planes in registers (split under the MFMAs of the step before)
+    // one step's f16 planes in registers (split under the MFMAs of the step before)
     struct Planes {
-        u32x4 x[XU][3];
-        u32x4 g[3];
-        uint2 g4[3];
+        u32x4 x[XU][NPL];
+        u32x4 g[NPL];
+        uint2 g4[NPL];
     };
+    // operand scales from the amax slots (uint8 X: exact at scale 1); the slab is unscaled
+    const int ex = U8 ? 0 : split_scale_exp(amax_read(a.amax_x)), eg = split_scale_exp(amax_read(a.amax_g));
+    const float sx = exp2i(ex), sg = exp2i(eg), uo = exp2i(-ex) * exp2i(-eg);
     Raw raw[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {  // defined values: the last step splits a set it never stores
@@ -1688,14 +1664,14 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
 #pragma unroll
         for (int i = 0; i < XU; ++i) {
             if constexpr (U8)
-                p.x[i][0] = u8x8_to_bf16(r.xw[i][0], r.xw[i][1]);
+                p.x[i][0] = u8x8_to_f16(r.xw[i][0], r.xw[i][1]);
             else
-                split8(r.xr[i][0], r.xr[i][1], p.x[i][0], p.x[i][1], p.x[i][2]);
+                split8h(r.xr[i][0], r.xr[i][1], sx, p.x[i][0], p.x[i][1]);
         }
         if constexpr (GW == 8)
-            split8(r.gr[0], r.gr[1], p.g[0], p.g[1], p.g[2]);
+            split8h(r.gr[0], r.gr[1], sg, p.g[0], p.g[1]);
         else
-            split4(r.gr[0], p.g4[0], p.g4[1], p.g4[2]);
+            split4h(r.gr[0], sg, p.g4[0], p.g4[1]);
     };
     auto store = [&](const Planes& p, const Raw& r, int buf) {
         uint8_t* base = lds + buf * C::STAGE;
@@ -1709,7 +1685,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         uint8_t* gb = base + XP * C::XPB;
         const int goff = pxl * GR + (((gco >> 4) ^ tr_swz<GR>(pxl)) << 5) + (gco & 15) * 2;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < NPL; ++q) {
             if constexpr (GW == 8)
                 *reinterpret_cast<u32x4*>(gb + q * C::GPB + goff) = p.g[q];
             else
@@ -1747,25 +1723,24 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         const uint8_t* gb = base + XP * C::XPB;
 #pragma unroll
         for (int ks = 0; ks < MS / 16; ++ks) {
-            u32x4 bq[WCT][3];
+            u32x4 bq[WCT][NPL];
 #pragma unroll
             for (int j = 0; j < WCT; ++j)
 #pragma unroll
-                for (int p = 0; p < 3; ++p)
+                for (int p = 0; p < NPL; ++p)
                     bq[j][p] = frag(gb + p * C::GPB, rowg, GR, (2 * (ct0 + j) + g16) ^ swg, ks);
 #pragma unroll
             for (int i = 0; i < WKT; ++i) {
-                u32x4 aq[3];
+                u32x4 aq[NPL];
 #pragma unroll
                 for (int p = 0; p < XP; ++p) aq[p] = frag(base + p * C::XPB, rowx, XR, (2 * (kt0 + i) + g16) ^ swx, ks);
 #pragma unroll
                 for (int j = 0; j < WCT; ++j) {
                     if constexpr (U8) {
-                        hi[i][j] = mfma_bf16(aq[0], bq[j][0], hi[i][j]);
-                        lo[i][j] = mfma_bf16(aq[0], bq[j][1], lo[i][j]);
-                        lo[i][j] = mfma_bf16(aq[0], bq[j][2], lo[i][j]);
+                        hi[i][j] = mfma_f16(aq[0], bq[j][0], hi[i][j]);
+                        lo[i][j] = mfma_f16(aq[0], bq[j][1], lo[i][j]);
                     } else {
-                        mfma_split6(aq, bq[j], hi[i][j], lo[i][j]);
+                        mfma_split3(aq, bq[j], hi[i][j], lo[i][j]);
                     }
                 }
             }
@@ -1810,7 +1785,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int kr = kb * KT + (kt0 + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                slab[kr * GS + (ct0 + j) * 32 + (lane & 31)] = hi[i][j][r] + lo[i][j][r];
+                slab[kr * GS + (ct0 + j) * 32 + (lane & 31)] = (hi[i][j][r] + lo[i][j][r]) * uo;
             }
     if (CB == 1 && kb == 0) {
         // bias grad partial: column sums of this split's G rows, combined in a fixed order
@@ -1960,10 +1935,12 @@ struct WsLaunch {
         return splits(batch) * (long long)(L::K * L::COUT + L::COUT) * (long long)sizeof(float);
     }
     static int run(const void* x, long long sample_stride, const float* g, long long batch, void* ws, float* dw,
-                   float* db, hipStream_t s, const long long* idx = nullptr, long long T = 0, long long Nenv = 0) {
+                   float* db, const uint32_t* amax_x, const uint32_t* amax_g, hipStream_t s,
+                   const long long* idx = nullptr, long long T = 0, long long Nenv = 0) {
         const int sp = (int)splits(batch);
         float* slab = reinterpret_cast<float*>(ws);
-        WArgs wa{x, sample_stride, g, slab, slab + (long long)sp * L::K * L::COUT, batch, 0, sp, idx, T, Nenv};
+        WArgs wa{x, sample_stride, g, slab, slab + (long long)sp * L::K * L::COUT, batch, 0, sp, idx, T, Nenv,
+                 amax_x, amax_g};
         const long long M = batch * L::P;
         wa.px_per_split = ppox::ceil_div(ppox::ceil_div(M, sp), MS) * MS;
         if (U8 && idx != nullptr)
@@ -1977,12 +1954,14 @@ struct WsLaunch {
 using Ws1 = WsLaunch<G1, true, 256>;
 using Ws2 = WsLaunch<G2, false, WS_KT2>;
 using Ws3 = WsLaunch<G3, false, WS_KT3>;
-// Every per-optimizer-step weight packing of the training step in ONE launch (the
-// minibatch loop is launch-bound at small per-rank batches): element ranges of the
-// jobs laid end to end, null outputs skipped.
+// Every per-optimizer-step weight packing of the training step in two launches (the
+// minibatch loop is launch-bound at small per-rank batches): wmax_kernel (each weight
+// tensor's amax partials, into the tails of the forms packed from it), then pack_all_kernel
+// (element ranges of the jobs laid end to end, null outputs skipped; each wave derives the
+// tensors' scales from the partials, and the first wave writes every form's exponent).
 struct PackAll {
     const float *w1, *w2, *w3, *wfc;
-    float* wpd2;                                  // f32 dgrad2 [(tap, co)][ci]
+    float* wpd2;                                       // f32 dgrad2 [(tap, co)][ci]
     uint16_t *q1, *q2, *q3, *qd2, *qd3, *qfcf, *qfcd;  // split planes
 };
 constexpr long long PA_N1 = 8 * 2 * 64 * 8, PA_N2 = (long long)G2::K * G2::COUT, PA_N3 = (long long)G3::K * G3::COUT;
@@ -1990,6 +1969,10 @@ constexpr long long PA_NFC = (long long)FcFwd::NCB * FcFwd::K * FcFwd::NOUT;
 constexpr long long PA_NFCD = (long long)FcDgrad::NCB * FcDgrad::K * FcDgrad::NOUT;
 // the split-GEMM jobs run in 8-element units (pack_frag_unit); q1 and wpd2 per element
 constexpr long long PU_2 = PA_N2 / 8, PU_3 = PA_N3 / 8, PU_FC = PA_NFC / 8, PU_FCD = PA_NFCD / 8;
+// planes (uint16) of each packed form; a buffer is planes + 2 * PACK_TAIL32 uint16
+constexpr long long PL_Q1 = FWD1_PACK, PL_Q2 = NPL * PA_N2, PL_Q3 = NPL * PA_N3, PL_FCF = NPL * PA_NFC,
+                    PL_FCD = NPL * PA_NFCD;
+static_assert(PL_FCF == PL_FCD, "fc forms: one size");
 
 // source value (k, col) of layer L's forward [K][COUT] (NHWC K order) or dgrad [(tap, co)][ci]
 // matrix, from the PyTorch [co][ci][ky][kx] weights
@@ -2023,31 +2006,95 @@ struct RowsSrc {
     }
 };
 template <class Prob, bool TRANS>
-__device__ inline void pack_rows_unit(const float* w, uint16_t* q, long long u) {
+__device__ inline void pack_rows_unit(const float* w, float s, uint16_t* q, long long u) {
     constexpr long long per = (long long)Prob::K * Prob::NOUT / 8;
     const int cb = (int)(u / per);
-    pack_frag_unit<Prob::NOUT>(RowsSrc<Prob, TRANS>{w, cb}, q + (long long)cb * Prob::K * Prob::NOUT * 3, u - cb * per);
+    pack_frag_unit<Prob::NOUT>(RowsSrc<Prob, TRANS>{w, cb}, s, q + (long long)cb * Prob::K * Prob::NOUT * NPL,
+                               u - cb * per);
+}
+
+// the forms packed from weight tensor t (0: w1, 1: w2, 2: w3, 3: wfc) and their plane counts
+__device__ inline void pa_forms(const PackAll& p, int t, uint16_t* (&f)[2], long long& planes) {
+    switch (t) {
+        case 0: f[0] = p.q1; f[1] = nullptr; planes = PL_Q1; break;
+        case 1: f[0] = p.q2; f[1] = p.qd2; planes = PL_Q2; break;
+        case 2: f[0] = p.q3; f[1] = p.qd3; planes = PL_Q3; break;
+        default: f[0] = p.qfcf; f[1] = p.qfcd; planes = PL_FCF; break;
+    }
+}
+
+// 64 workgroups per weight tensor: workgroup b's max |w| over its stride into slot 4b of the
+// tails of both forms (slots 4b+1..4b+3 zeroed), so the packer's amax_read sees the tensor max
+constexpr int WMAX_WG = 64;
+__global__ void __launch_bounds__(256) wmax_kernel(PackAll p) {
+    const int t = blockIdx.x / WMAX_WG, b = blockIdx.x % WMAX_WG;
+    uint16_t* f[2];
+    long long planes;
+    pa_forms(p, t, f, planes);
+    if (!f[0] && !f[1]) return;
+    const float* w = t == 0 ? p.w1 : t == 1 ? p.w2 : t == 2 ? p.w3 : p.wfc;
+    const long long n = t == 0 ? (long long)G1::K * G1::COUT : t == 1 ? PA_N2 : t == 2 ? PA_N3 : 512LL * 3136;
+    float m = 0.f;
+    for (long long i = (long long)b * 256 + threadIdx.x; i < n; i += WMAX_WG * 256) m = fmaxf(m, fabsf(w[i]));
+    __shared__ uint32_t red[4];
+    const uint32_t wm = wave_max_u32(__float_as_uint(m));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wm;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint4 v = {max(max(red[0], red[1]), max(red[2], red[3])), 0u, 0u, 0u};
+        for (int k = 0; k < 2; ++k)
+            if (f[k]) reinterpret_cast<uint4*>(pack_tail(f[k], planes))[b] = v;
+    }
 }
 
 __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long total) {
+    // the four tensors' scales (wave-uniform), from the partials of their first packed form
+    float sc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        uint16_t* f[2];
+        long long planes;
+        pa_forms(p, t, f, planes);
+        uint16_t* src = f[0] ? f[0] : f[1];
+        const int e = src ? split_scale_exp(amax_read(pack_tail(src, planes))) : 0;
+        sc[t] = exp2i(e);
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            for (int k = 0; k < 2; ++k)
+                if (f[k]) pack_tail(f[k], planes)[AMAX_SLOTS] = (uint32_t)e;
+    }
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
         long long j = i;
-        if (j < PA_N1) { if (p.q1) pack_fwd1_split_elem(p.w1, p.q1, (int)j); continue; }
+        if (j < PA_N1) { if (p.q1) pack_fwd1_split_elem(p.w1, sc[0], p.q1, (int)j); continue; }
         j -= PA_N1;
-        if (j < PU_2) { if (p.q2) pack_frag_unit<G2::COUT>(ConvSrc<G2, false>{p.w2}, p.q2, j); continue; }
+        if (j < PU_2) { if (p.q2) pack_frag_unit<G2::COUT>(ConvSrc<G2, false>{p.w2}, sc[1], p.q2, j); continue; }
         j -= PU_2;
-        if (j < PU_3) { if (p.q3) pack_frag_unit<G3::COUT>(ConvSrc<G3, false>{p.w3}, p.q3, j); continue; }
+        if (j < PU_3) { if (p.q3) pack_frag_unit<G3::COUT>(ConvSrc<G3, false>{p.w3}, sc[2], p.q3, j); continue; }
         j -= PU_3;
-        if (j < PU_2) { if (p.qd2) pack_frag_unit<G2::CIN>(ConvSrc<G2, true>{p.w2}, p.qd2, j); continue; }
+        if (j < PU_2) { if (p.qd2) pack_frag_unit<G2::CIN>(ConvSrc<G2, true>{p.w2}, sc[1], p.qd2, j); continue; }
         j -= PU_2;
-        if (j < PU_3) { if (p.qd3) pack_frag_unit<G3::CIN>(ConvSrc<G3, true>{p.w3}, p.qd3, j); continue; }
+        if (j < PU_3) { if (p.qd3) pack_frag_unit<G3::CIN>(ConvSrc<G3, true>{p.w3}, sc[2], p.qd3, j); continue; }
         j -= PU_3;
         if (j < PA_N2) { if (p.wpd2) pack_dgrad_elem<G2, false>(p.w2, p.wpd2, (int)j); continue; }
         j -= PA_N2;
-        if (j < PU_FC) { if (p.qfcf) pack_rows_unit<FcFwd, true>(p.wfc, p.qfcf, j); continue; }
+        if (j < PU_FC) { if (p.qfcf) pack_rows_unit<FcFwd, true>(p.wfc, sc[3], p.qfcf, j); continue; }
         j -= PU_FC;
-        if (p.qfcd) pack_rows_unit<FcDgrad, false>(p.wfc, p.qfcd, j);
+        if (p.qfcd) pack_rows_unit<FcDgrad, false>(p.wfc, sc[3], p.qfcd, j);
     }
+}
+
+int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
+    for (const void* q : {(const void*)p.wpd2, (const void*)p.q1, (const void*)p.q2, (const void*)p.q3,
+                          (const void*)p.qd2, (const void*)p.qd3, (const void*)p.qfcf, (const void*)p.qfcd})
+        PPOX_REQUIRE(!q || ppox::aligned16(q), "ppox_nature_pack: packed buffers must be 16-byte aligned");
+    PPOX_REQUIRE((p.w1 || !p.q1) && (p.w2 || (!p.q2 && !p.qd2 && !p.wpd2)) && (p.w3 || (!p.q3 && !p.qd3)) &&
+                     (p.wfc || (!p.qfcf && !p.qfcd)),
+                 "ppox_nature_pack: null weights");
+    wmax_kernel<<<4 * WMAX_WG, 256, 0, s>>>(p);
+    PPOX_LAUNCHED_NORET(name);
+    const long long total = PA_N1 + 2 * PU_2 + 2 * PU_3 + PA_N2 + PU_FC + (p.qfcd ? PU_FCD : 0);
+    const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 4096);
+    pack_all_kernel<<<blocks, 256, 0, s>>>(p, total);
+    PPOX_LAUNCHED(name);
 }
 
 }  // namespace
@@ -2180,9 +2227,11 @@ extern "C" int64_t ppox_nature_wgrad_split_workspace_bytes(int32_t layer, int64_
 
 extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_t batch, int64_t x_sample_stride,
                                             const float* grad_out, void* workspace, int64_t workspace_bytes, float* dw,
-                                            float* db, void* stream) {
+                                            float* db, const uint32_t* amax_x, const uint32_t* amax_g, void* stream) {
     PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_conv_wgrad_split: layer must be 1, 2 or 3");
     PPOX_REQUIRE(x && grad_out && workspace && dw && db && batch > 0, "ppox_nature_conv_wgrad_split: bad arguments");
+    PPOX_REQUIRE(amax_g && (layer == 1 || amax_x) && ppox::aligned16(amax_g) && (!amax_x || ppox::aligned16(amax_x)),
+                 "ppox_nature_conv_wgrad_split: amax slots of the operands (16B-aligned) required");
     PPOX_REQUIRE(workspace_bytes >= ppox_nature_wgrad_split_workspace_bytes(layer, batch),
                  "ppox_nature_conv_wgrad_split: workspace too small");
     PPOX_REQUIRE(ppox::aligned16(grad_out), "ppox_nature_conv_wgrad_split: grad_out must be 16B aligned");
@@ -2192,11 +2241,11 @@ extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_
     if (layer == 1) {
         PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && x_sample_stride % 4 == 0,
                      "ppox_nature_conv_wgrad_split: u8 input 4-byte aligned");
-        return Ws1::run(x, x_sample_stride, grad_out, batch, workspace, dw, db, s);
+        return Ws1::run(x, x_sample_stride, grad_out, batch, workspace, dw, db, nullptr, amax_g, s);
     }
     PPOX_REQUIRE(ppox::aligned16(x), "ppox_nature_conv_wgrad_split: layer 2/3 input must be 16B-aligned NHWC");
-    if (layer == 2) return Ws2::run(x, 0, grad_out, batch, workspace, dw, db, s);
-    return Ws3::run(x, 0, grad_out, batch, workspace, dw, db, s);
+    if (layer == 2) return Ws2::run(x, 0, grad_out, batch, workspace, dw, db, amax_x, amax_g, s);
+    return Ws3::run(x, 0, grad_out, batch, workspace, dw, db, amax_x, amax_g, s);
 }
 
 // conv1 split wgrad reading its frames straight from the rollout (sample n = env-major row
@@ -2204,16 +2253,18 @@ extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_
 // ppox_nature_conv_fwd_split's idx form (replaces ppox_gather_rows + the strided call)
 extern "C" int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
                                                 int64_t T, int64_t N_env, const float* grad_out, void* workspace,
-                                                int64_t workspace_bytes, float* dw, float* db, void* stream) {
+                                                int64_t workspace_bytes, float* dw, float* db, const uint32_t* amax_g,
+                                                void* stream) {
     PPOX_REQUIRE(layer == 1, "ppox_nature_conv_wgrad_split_idx: layer must be 1 (u8 frames)");
     PPOX_REQUIRE(x && idx && grad_out && workspace && dw && db && batch > 0 && T > 0 && N_env > 0,
                  "ppox_nature_conv_wgrad_split_idx: bad arguments");
+    PPOX_REQUIRE(amax_g && ppox::aligned16(amax_g), "ppox_nature_conv_wgrad_split_idx: amax slots of G required");
     PPOX_REQUIRE(workspace_bytes >= ppox_nature_wgrad_split_workspace_bytes(layer, batch),
                  "ppox_nature_conv_wgrad_split_idx: workspace too small");
     PPOX_REQUIRE(ppox::aligned16(grad_out) && !(reinterpret_cast<uintptr_t>(x) & 3),
                  "ppox_nature_conv_wgrad_split_idx: alignment");
     PPOX_REQUIRE(batch * G1::P < (1LL << 31) / 64, "ppox_nature_conv_wgrad_split_idx: batch too large");
-    return Ws1::run(x, 0, grad_out, batch, workspace, dw, db, ppox::as_stream(stream),
+    return Ws1::run(x, 0, grad_out, batch, workspace, dw, db, nullptr, amax_g, ppox::as_stream(stream),
                     reinterpret_cast<const long long*>(idx), T, N_env);
 }
 
@@ -2226,20 +2277,28 @@ extern "C" int ppox_nchw_to_nhwc_relu_grad(const float* grad, const float* act, 
 }
 
 namespace ppox_conv {
-// split-bf16 layers 2/3 (called from conv_split.hip's entry points)
-int split_pack23(const float* w2, const float* w3, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
-                 hipStream_t s) {
-    if (q2) pack_split_gemm<G2, false><<<ppox::ceil_div(G2::K * G2::COUT, 256), 256, 0, s>>>(w2, q2);
-    if (q3) pack_split_gemm<G3, false><<<ppox::ceil_div(G3::K * G3::COUT, 256), 256, 0, s>>>(w3, q3);
-    if (qd2) pack_split_gemm<G2, true><<<ppox::ceil_div(G2::K * G2::COUT, 256), 256, 0, s>>>(w2, qd2);
-    if (qd3) pack_split_gemm<G3, true><<<ppox::ceil_div(G3::K * G3::COUT, 256), 256, 0, s>>>(w3, qd3);
-    PPOX_LAUNCHED("ppox_nature_pack_split");
+// split-f16 packing of the conv weights (called from conv_split.hip's entry point)
+int pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1, uint16_t* q2, uint16_t* q3,
+               uint16_t* qd2, uint16_t* qd3, hipStream_t s) {
+    return launch_pack_all(PackAll{w1, w2, w3, nullptr, nullptr, q1, q2, q3, qd2, qd3, nullptr, nullptr}, s,
+                           "ppox_nature_pack_split");
+}
+
+long long planes(int which) {
+    switch (which) {
+        case 1: return PL_Q1;
+        case 2: case 12: return PL_Q2;
+        case 3: case 13: return PL_Q3;
+        case 4: return PL_FCF;
+        default: return -1;
+    }
 }
 
 int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq, const float* bias, float* y,
-                hipStream_t s) {
+                const uint32_t* amax_x, uint32_t* amax_y, hipStream_t s) {
     PPOX_REQUIRE(ppox::aligned16(x), "ppox_nature_conv_fwd_split: layer 2/3 input must be 16B-aligned NHWC");
-    Args a{x, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch};
+    PPOX_REQUIRE(amax_x && ppox::aligned16(amax_x), "ppox_nature_conv_fwd_split: amax slots of x required (layer 2/3)");
+    Args a{x, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch, amax_x, amax_y, pack_exp(wq, planes(layer))};
     if (layer == 2)
         return launch_sgemm<SgFwd<G2, false>>(a, wq, ppox::ceil_div(batch * G2::P, SG_ROWS), s,
                                               "ppox_nature_conv_fwd_split");
@@ -2249,12 +2308,16 @@ int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq,
 }  // namespace ppox_conv
 
 extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch, const uint16_t* wqd,
-                                            const float* prev_act, float* grad_in, void* stream) {
+                                            const float* prev_act, float* grad_in, const uint32_t* amax_g,
+                                            uint32_t* amax_out, void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad_split: layer must be 2 or 3");
-    PPOX_REQUIRE(grad_out && wqd && prev_act && grad_in && batch >= 0, "ppox_nature_conv_dgrad_split: bad arguments");
-    PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wqd), "ppox_nature_conv_dgrad_split: 16B alignment");
-    Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch};
+    PPOX_REQUIRE(grad_out && wqd && prev_act && grad_in && amax_g && batch >= 0,
+                 "ppox_nature_conv_dgrad_split: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wqd) && ppox::aligned16(amax_g),
+                 "ppox_nature_conv_dgrad_split: 16B alignment");
+    Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch, amax_g, amax_out,
+           pack_exp(wqd, ppox_conv::planes(10 + layer))};
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 2) {
         const long long ntriples = ppox::ceil_div(batch, (long long)C2S);
@@ -2331,7 +2394,8 @@ extern "C" int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch) {
 }
 
 extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float* h3, void* workspace,
-                                    int64_t workspace_bytes, float* dw, void* stream) {
+                                    int64_t workspace_bytes, float* dw, const uint32_t* amax_df,
+                                    const uint32_t* amax_h3, void* stream) {
     PPOX_REQUIRE(dw && batch >= 0, "ppox_nature_fc_wgrad: bad arguments");
     hipStream_t s = ppox::as_stream(stream);
     if (batch == 0) {  // no rows: a zero gradient
@@ -2339,13 +2403,14 @@ extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float*
                      "ppox_nature_fc_wgrad: memset failed");
         return PPOX_OK;
     }
-    PPOX_REQUIRE(df && h3 && workspace, "ppox_nature_fc_wgrad: bad arguments");
+    PPOX_REQUIRE(df && h3 && workspace && amax_df && amax_h3, "ppox_nature_fc_wgrad: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(amax_df) && ppox::aligned16(amax_h3), "ppox_nature_fc_wgrad: 16B alignment");
     PPOX_REQUIRE(workspace_bytes >= FcWgrad::workspace_bytes(batch), "ppox_nature_fc_wgrad: workspace too small");
     PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(h3), "ppox_nature_fc_wgrad: 16B alignment");
     PPOX_REQUIRE(batch < (1LL << 31) / 64, "ppox_nature_fc_wgrad: batch too large for 32-bit row indexing");
     const int sp = FcWgrad::splits(batch);
     float* slab = reinterpret_cast<float*>(workspace);
-    WArgs wa{df, 0, h3, slab, nullptr, batch, 0, sp, nullptr, 0, 0};
+    WArgs wa{df, 0, h3, slab, nullptr, batch, 0, sp, nullptr, 0, 0, amax_df, amax_h3};
     wa.px_per_split = ppox::ceil_div(ppox::ceil_div((long long)batch, (long long)sp), (long long)MS) * MS;
     wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB><<<(unsigned)(FcWgrad::TILES * sp), 256, 0, s>>>(wa);
     PPOX_LAUNCHED_NORET("ppox_nature_fc_wgrad");
@@ -2353,28 +2418,22 @@ extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float*
     PPOX_LAUNCHED("ppox_nature_fc_wgrad");
 }
 
-extern "C" int64_t ppox_nature_fc_pack_elems(void) { return 3LL * FcFwd::NCB * FcFwd::K * FcFwd::NOUT; }
+extern "C" int64_t ppox_nature_fc_pack_elems(void) { return PL_FCF + 2 * PACK_TAIL32; }
 
 extern "C" int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_dgrad, void* stream) {
     PPOX_REQUIRE(w && (q_fwd || q_dgrad), "ppox_nature_fc_pack: bad arguments");
-    PPOX_REQUIRE((!q_fwd || ppox::aligned16(q_fwd)) && (!q_dgrad || ppox::aligned16(q_dgrad)),
-                 "ppox_nature_fc_pack: 16B alignment");
-    hipStream_t s = ppox::as_stream(stream);
-    if (q_fwd)
-        pack_split_gemm_rows<FcFwd, true><<<ppox::ceil_div((long long)FcFwd::NCB * FcFwd::K * FcFwd::NOUT, 256), 256, 0,
-                                            s>>>(w, q_fwd);
-    if (q_dgrad)
-        pack_split_gemm_rows<FcDgrad, false><<<ppox::ceil_div((long long)FcDgrad::NCB * FcDgrad::K * FcDgrad::NOUT, 256),
-                                               256, 0, s>>>(w, q_dgrad);
-    PPOX_LAUNCHED("ppox_nature_fc_pack");
+    return launch_pack_all(PackAll{nullptr, nullptr, nullptr, w, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                   q_fwd, q_dgrad},
+                           ppox::as_stream(stream), "ppox_nature_fc_pack");
 }
 
 extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
-                                  void* stream) {
+                                  const uint32_t* amax_h3, void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
-    PPOX_REQUIRE(h3 && q_fwd && bias && f && batch >= 0, "ppox_nature_fc_fwd: bad arguments");
-    PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd), "ppox_nature_fc_fwd: 16B alignment");
-    Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch};
+    PPOX_REQUIRE(h3 && q_fwd && bias && f && amax_h3 && batch >= 0, "ppox_nature_fc_fwd: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd) && ppox::aligned16(amax_h3),
+                 "ppox_nature_fc_fwd: 16B alignment");
+    Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, amax_h3, nullptr, pack_exp(q_fwd, PL_FCF)};
     return launch_sgemm<SgRows<3136, 512, FC_FWD, FC_FWD_G>>(a, q_fwd, ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB,
                                                    ppox::as_stream(stream), "ppox_nature_fc_fwd");
 }
@@ -2384,14 +2443,17 @@ extern "C" int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch) {
 }
 
 extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias,
-                                         void* workspace, int64_t workspace_bytes, float* f, void* stream) {
+                                         void* workspace, int64_t workspace_bytes, float* f, const uint32_t* amax_h3,
+                                         void* stream) {
     if (batch == 0) return PPOX_OK;
-    PPOX_REQUIRE(h3 && q_fwd && bias && f && workspace && batch > 0, "ppox_nature_fc_fwd_splitk: bad arguments");
-    PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd) && ppox::aligned16(f) && ppox::aligned16(workspace),
+    PPOX_REQUIRE(h3 && q_fwd && bias && f && workspace && amax_h3 && batch > 0,
+                 "ppox_nature_fc_fwd_splitk: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd) && ppox::aligned16(f) && ppox::aligned16(workspace) &&
+                     ppox::aligned16(amax_h3),
                  "ppox_nature_fc_fwd_splitk: 16B alignment");
     PPOX_REQUIRE(workspace_bytes >= ppox_nature_fc_fwd_splitk_workspace_bytes(batch),
                  "ppox_nature_fc_fwd_splitk: workspace too small");
-    Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch};
+    Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, amax_h3, nullptr, pack_exp(q_fwd, PL_FCF)};
     float* slab = reinterpret_cast<float*>(workspace);
     hipStream_t st = ppox::as_stream(stream);
     switch (fc_fwd_splits(batch)) {
@@ -2403,11 +2465,12 @@ extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const u
 }
 
 extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
-                                    void* stream) {
+                                    const uint32_t* amax_df, uint32_t* amax_g3, void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
-    PPOX_REQUIRE(df && q_dgrad && h3 && g3 && batch >= 0, "ppox_nature_fc_dgrad: bad arguments");
-    PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(q_dgrad), "ppox_nature_fc_dgrad: 16B alignment");
-    Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch};
+    PPOX_REQUIRE(df && q_dgrad && h3 && g3 && amax_df && batch >= 0, "ppox_nature_fc_dgrad: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(q_dgrad) && ppox::aligned16(amax_df),
+                 "ppox_nature_fc_dgrad: 16B alignment");
+    Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch, amax_df, amax_g3, pack_exp(q_dgrad, PL_FCD)};
     return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_G>>(a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB,
                                                      ppox::as_stream(stream), "ppox_nature_fc_dgrad");
 }
@@ -2416,12 +2479,28 @@ extern "C" int ppox_nature_pack_all(const float* w1, const float* w2, const floa
                                     uint16_t* q1, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
                                     uint16_t* qfc_fwd, uint16_t* qfc_dgrad, void* stream) {
     PPOX_REQUIRE(w1 && w2 && w3 && (wfc || (!qfc_fwd && !qfc_dgrad)), "ppox_nature_pack_all: null weights");
-    for (const void* q : {(const void*)wpd2, (const void*)q1, (const void*)q2, (const void*)q3, (const void*)qd2,
-                          (const void*)qd3, (const void*)qfc_fwd, (const void*)qfc_dgrad})
-        PPOX_REQUIRE(!q || ppox::aligned16(q), "ppox_nature_pack_all: packed buffers must be 16-byte aligned");
-    PackAll p{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad};
-    const long long total = PA_N1 + 2 * PU_2 + 2 * PU_3 + PA_N2 + PU_FC + (qfc_dgrad ? PU_FCD : 0);
-    const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 4096);
-    pack_all_kernel<<<blocks, 256, 0, ppox::as_stream(stream)>>>(p, total);
-    PPOX_LAUNCHED("ppox_nature_pack_all");
+    return launch_pack_all(PackAll{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad},
+                           ppox::as_stream(stream), "ppox_nature_pack_all");
+}
+
+// ---- amax slots (split-f16 operand scales) -------------------------------------------
+__global__ void __launch_bounds__(256) amax_kernel(const float4* __restrict__ x, long long n4,
+                                                   uint32_t* __restrict__ am) {
+    float m = 0.f;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+        const float4 v = x[i];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    amax_record(am, m);
+}
+
+extern "C" int32_t ppox_amax_slots(void) { return AMAX_SLOTS; }
+
+extern "C" int ppox_amax(const float* x, int64_t n, uint32_t* amax, void* stream) {
+    PPOX_REQUIRE(amax && n >= 0 && n % 4 == 0 && (x || n == 0), "ppox_amax: bad arguments (n % 4 == 0)");
+    PPOX_REQUIRE(ppox::aligned16(amax) && (!x || ppox::aligned16(x)), "ppox_amax: 16B alignment");
+    if (n == 0) return PPOX_OK;
+    const long long blocks = std::min<long long>(ppox::ceil_div(n / 4, 256LL), 1024);
+    amax_kernel<<<(unsigned)blocks, 256, 0, ppox::as_stream(stream)>>>(reinterpret_cast<const float4*>(x), n / 4, amax);
+    PPOX_LAUNCHED("ppox_amax");
 }

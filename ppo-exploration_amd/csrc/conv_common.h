@@ -1,5 +1,6 @@
-// Definitions shared by the NatureCNN conv translation units (conv.hip: f32 MFMA
-// kernels; conv_split.hip: bf16-split MFMA kernels).  Not part of the ABI.
+// Definitions shared by the NatureCNN conv translation units (conv.hip: f32 MFMA and
+// split-f16 kernels; conv_split.hip: the conv1 split forward) and the ICM kernels (the
+// split-bf16 helpers).  Not part of the ABI.
 #pragma once
 #include "common.h"
 
@@ -27,6 +28,11 @@ struct Args {
     const float* mask;        // dgrad: previous activation (ReLU mask source)
     float* y;                 // output
     long long batch;
+    // split-f16 kernels: the A operand's amax slots (null: uint8 frames, exact at scale 1),
+    // the output's amax slots (null: not recorded) and the packed B's scale exponent
+    const uint32_t* amax_x = nullptr;
+    uint32_t* amax_y = nullptr;
+    const int* wexp = nullptr;
 };
 
 __device__ inline f32x16 zero16() {
@@ -59,7 +65,7 @@ __device__ inline void tap_range(int i, int& k0, int& cnt) {
     cnt = hi >= k0 ? (hi - k0) / S + 1 : 0;
 }
 
-// ---- split-bf16 helpers (conv_split.hip and the split kernels of conv.hip) ----
+// ---- split-bf16 helpers (icm.hip: the ICM state encoder) ----
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
 
@@ -148,21 +154,136 @@ __device__ inline void mfma_split6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32
     lo = mfma_bf16(a[2], b[0], lo);
 }
 
-__host__ __device__ constexpr int fwd1_split_index(int c, int s, int p, int lane, int e) {
-    return (((c * 2 + s) * 3 + p) * 64 + lane) * 8 + e;
+// ---- split-f16 ("f16x2") helpers: the NatureCNN conv / fc kernels ----------------------
+// An f32 operand x of a GEMM is scaled by a power of two s (per tensor, from its running
+// absolute maximum: max|x| s in [2^14, 2^15)) and split by round-to-nearest into two fp16
+// planes:  h = rn16(x s),  l = rn16(x s - h)  (x s - h is exact in f32).  h + l carries 22+
+// significant bits (|x s - h - l| <= 2^-24 |x s| while l is a normal fp16, i.e. for every
+// |x| >= max|x| 2^-17; below that the error is an absolute 2^-25 / s, 2^-39 of the tensor's
+// max).  A product is  hA hB + (hA lB + lA hB)  [+ lA lB <= 2^-22 |ab| dropped]: three
+// v_mfma_f32_32x32x16_f16 (each product exact in f32), against six bf16 products for the
+// same accuracy.  The accumulated result is unscaled by 1 / (sA sB) (exact: powers of two).
+// uint8 frames (0..255) are exact in ONE fp16 plane (scale 1): conv1 needs two products.
+using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
+using f16x2 = __attribute__((ext_vector_type(2))) _Float16;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+constexpr int NPL = 2;  // planes of a split f32 operand
+
+__device__ inline f32x16 mfma_f16(const u32x4& a, const u32x4& b, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
 }
 
-// one element of the conv1 forward split packing (8 chunks x 2 steps x 64 lanes x 8)
-__device__ inline void pack_fwd1_split_elem(const float* __restrict__ w, uint16_t* __restrict__ q, int t) {
+// a*b on f16x2 operands: hA hB into hi, hA lB + lA hB into lo
+__device__ inline void mfma_split3(const u32x4 (&a)[2], const u32x4 (&b)[2], f32x16& hi, f32x16& lo) {
+    hi = mfma_f16(a[0], b[0], hi);
+    lo = mfma_f16(a[0], b[1], lo);
+    lo = mfma_f16(a[1], b[0], lo);
+}
+
+// Per-tensor absolute maxima ("amax"): AMAX_SLOTS uint32 (the f32 bits of max|x|: for
+// non-negative floats uint order is float order), producers atomicMax one slot per wave
+// (spread so no address takes more than a few thousand atomics), consumers reduce all
+// slots.  The owner zeroes a tensor's slots before the kernel that produces it.
+constexpr int AMAX_SLOTS = 256;
+
+__device__ inline uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+// every lane: max over the tensor's slots (one 16-B load per lane)
+__device__ inline uint32_t amax_read(const uint32_t* __restrict__ am) {
+    const uint4 v = reinterpret_cast<const uint4*>(am)[threadIdx.x & 63];
+    return __builtin_amdgcn_readfirstlane(wave_max_u32(max(max(v.x, v.y), max(v.z, v.w))));
+}
+// this wave's maximum of |values| into slot (global wave index) mod AMAX_SLOTS; am may be null
+__device__ inline void amax_record(uint32_t* __restrict__ am, float m) {
+    if (!am) return;
+    const uint32_t w = wave_max_u32(__float_as_uint(fabsf(m)));
+    if ((threadIdx.x & 63) == 0) {
+        const unsigned wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        atomicMax(am + (wid & (AMAX_SLOTS - 1)), w);
+    }
+}
+// scale exponent of a tensor from its amax bits: max|x| 2^E in [2^14, 2^15) (E in [-113, 126];
+// an all-zero or tiny tensor takes 2^126, an inf / nan one 2^-113 and stays non-finite)
+__host__ __device__ inline int split_scale_exp(uint32_t amax_bits) {
+    int e = (int)(amax_bits >> 23);
+    e = e < 15 ? 15 : (e > 254 ? 254 : e);
+    return 141 - e;
+}
+__host__ __device__ inline float exp2i(int e) { return __builtin_bit_cast(float, (uint32_t)(e + 127) << 23); }
+
+// two f32 (already scaled) -> their f16 high and low planes, packed f16x2 words (x0 low)
+__device__ inline void split2h(float x0, float x1, uint32_t& h, uint32_t& l) {
+    const f32x2 v = {x0, x1};
+    const f16x2 hv = __builtin_convertvector(v, f16x2);
+    const f32x2 r = v - __builtin_convertvector(hv, f32x2);
+    h = __builtin_bit_cast(uint32_t, hv);
+    l = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, f16x2));
+}
+// eight f32 times s -> their two f16 planes as MFMA fragments (element e = value e)
+__device__ inline void split8h(const float4& v0, const float4& v1, float s, u32x4& p0, u32x4& p1) {
+    uint32_t h[4], l[4];
+    split2h(v0.x * s, v0.y * s, h[0], l[0]);
+    split2h(v0.z * s, v0.w * s, h[1], l[1]);
+    split2h(v1.x * s, v1.y * s, h[2], l[2]);
+    split2h(v1.z * s, v1.w * s, h[3], l[3]);
+    p0 = u32x4{h[0], h[1], h[2], h[3]};
+    p1 = u32x4{l[0], l[1], l[2], l[3]};
+}
+// four f32 times s -> two f16 planes, two f16x2 words each
+__device__ inline void split4h(const float4& v, float s, uint2& p0, uint2& p1) {
+    split2h(v.x * s, v.y * s, p0.x, p1.x);
+    split2h(v.z * s, v.w * s, p0.y, p1.y);
+}
+// one f32 (scaled) -> its two f16 planes (the weight packers)
+__device__ inline void split1h(float v, uint16_t& h, uint16_t& l) {
+    const _Float16 hv = (_Float16)v;
+    h = __builtin_bit_cast(uint16_t, hv);
+    l = __builtin_bit_cast(uint16_t, (_Float16)(v - (float)hv));
+}
+// eight uint8 (two words) -> an f16x8 fragment, exact: f16 bits 0x64bb are 1024 + b, so one
+// v_perm_b32 (bytes b, 0x64 of the constant word, b', 0x64) and one packed subtract per pair
+__device__ inline u32x4 u8x8_to_f16(uint32_t w0, uint32_t w1) {
+    const f16x2 k1024 = {(_Float16)1024.f, (_Float16)1024.f};
+    const uint32_t q[4] = {__builtin_amdgcn_perm(0x64646464u, w0, 0x04010400), __builtin_amdgcn_perm(0x64646464u, w0, 0x04030402),
+                           __builtin_amdgcn_perm(0x64646464u, w1, 0x04010400), __builtin_amdgcn_perm(0x64646464u, w1, 0x04030402)};
+    u32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, q[i]) - k1024);
+    return r;
+}
+
+// Tail of a packed buffer of `planes` uint16: PACK_TAIL32 uint32 — [0, AMAX_SLOTS) the amax
+// partials of the source weights (written by wmax_kernel, read by the packer), then the scale
+// exponent E the planes were packed with (read by the GEMM kernels).
+constexpr int PACK_TAIL32 = AMAX_SLOTS + 8;
+__host__ __device__ inline uint32_t* pack_tail(uint16_t* q, long long planes) {
+    return reinterpret_cast<uint32_t*>(q + planes);
+}
+__host__ __device__ inline const int* pack_exp(const uint16_t* q, long long planes) {
+    return reinterpret_cast<const int*>(q + planes) + AMAX_SLOTS;
+}
+
+
+__host__ __device__ constexpr int fwd1_split_index(int c, int s, int p, int lane, int e) {
+    return (((c * 2 + s) * NPL + p) * 64 + lane) * 8 + e;
+}
+constexpr int FWD1_PACK = 8 * 2 * NPL * 64 * 8;  // uint16 planes of the conv1 forward packing
+
+// one element of the conv1 forward split packing (8 chunks x 2 steps x 64 lanes x 8), the
+// weights times s
+__device__ inline void pack_fwd1_split_elem(const float* __restrict__ w, float s, uint16_t* __restrict__ q, int t) {
     if (t >= 8 * 2 * 64 * 8) return;
-    const int e = t & 7, lane = (t >> 3) & 63, s = (t >> 9) & 1, c = t >> 10;
+    const int e = t & 7, lane = (t >> 3) & 63, st = (t >> 9) & 1, c = t >> 10;
     const int h = lane >> 5, co = lane & 31;
-    const int k = (c >> 1) * 64 + (4 * (c & 1) + 2 * h + s) * 8 + e;  // natural (ci, ky, kx)
-    uint16_t p0, p1, p2;
-    split3(w[co * G1::K + k], p0, p1, p2);
-    q[fwd1_split_index(c, s, 0, lane, e)] = p0;
-    q[fwd1_split_index(c, s, 1, lane, e)] = p1;
-    q[fwd1_split_index(c, s, 2, lane, e)] = p2;
+    const int k = (c >> 1) * 64 + (4 * (c & 1) + 2 * h + st) * 8 + e;  // natural (ci, ky, kx)
+    uint16_t p0, p1;
+    split1h(w[co * G1::K + k] * s, p0, p1);
+    q[fwd1_split_index(c, st, 0, lane, e)] = p0;
+    q[fwd1_split_index(c, st, 1, lane, e)] = p1;
 }
 
 constexpr int MS = 32;
@@ -180,13 +301,17 @@ struct WArgs {
     // step-major (T, Nenv, ...) frame buffer x (the minibatch gather fused into the load)
     const long long* idx = nullptr;
     long long T = 0, Nenv = 0;
+    // split-f16: amax slots of X (null: uint8 frames) and of G
+    const uint32_t* amax_x = nullptr;
+    const uint32_t* amax_g = nullptr;
 };
 
 }  // namespace
 
 namespace ppox_conv {
-int split_pack23(const float* w2, const float* w3, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
-                 hipStream_t s);
+int pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1, uint16_t* q2, uint16_t* q3,
+               uint16_t* qd2, uint16_t* qd3, hipStream_t s);
+long long planes(int which);  // uint16 planes of a split-packed form (1, 2, 3, 12, 13; 4 = fc)
 int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq, const float* bias, float* y,
-                hipStream_t s);
+                const uint32_t* amax_x, uint32_t* amax_y, hipStream_t s);
 }  // namespace ppox_conv

@@ -37,7 +37,7 @@ namespace {
 template <int MT>
 __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a, unsigned tiles_per_wave) {
     using L = G1;
-    constexpr int NCH = L::K / 32, NQ = NCH * 6;
+    constexpr int NCH = L::K / 32, NQ = NCH * 2 * NPL;
     __shared__ u32x4 Wl[NQ * 64];
     {
         const u32x4* wq = reinterpret_cast<const u32x4*>(a.wp);
@@ -79,14 +79,16 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
     };
     const int co = lane & 31;
     const float bias = a.bias[co];
+    const float uw = exp2i(-*a.wexp);  // the weights were packed times 2^E; frames are exact
+    float om = 0.f;                    // the largest value this lane stored (h1's amax)
     auto run_tile = [&](unsigned tile, const Raw& r) {
         f32x16 hi[MT], lo[MT];
 #pragma unroll
         for (int i = 0; i < MT; ++i) hi[i] = lo[i] = zero16();
         // B fragments are read from LDS one (chunk, step) ahead of their MFMAs
-        u32x4 rb[2][3];
+        u32x4 rb[2][NPL];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) rb[0][p] = Wlane[p * 64];
+        for (int p = 0; p < NPL; ++p) rb[0][p] = Wlane[p * 64];
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -94,14 +96,13 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
                 const int q = c * 2 + s, cur = q & 1;
                 if (q + 1 < 2 * NCH) {
 #pragma unroll
-                    for (int p = 0; p < 3; ++p) rb[cur ^ 1][p] = Wlane[((q + 1) * 3 + p) * 64];
+                    for (int p = 0; p < NPL; ++p) rb[cur ^ 1][p] = Wlane[((q + 1) * NPL + p) * 64];
                 }
 #pragma unroll
                 for (int i = 0; i < MT; ++i) {
-                    const u32x4 av = u8x8_to_bf16(r[i][c][2 * s], r[i][c][2 * s + 1]);
-                    hi[i] = mfma_bf16(av, rb[cur][0], hi[i]);
-                    lo[i] = mfma_bf16(av, rb[cur][1], lo[i]);
-                    lo[i] = mfma_bf16(av, rb[cur][2], lo[i]);
+                    const u32x4 av = u8x8_to_f16(r[i][c][2 * s], r[i][c][2 * s + 1]);
+                    hi[i] = mfma_f16(av, rb[cur][0], hi[i]);
+                    lo[i] = mfma_f16(av, rb[cur][1], lo[i]);
                 }
                 // keep the scheduler from hoisting every chunk's LDS reads (192 VGPRs)
                 __builtin_amdgcn_sched_barrier(0);
@@ -113,7 +114,9 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const unsigned m = m0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-                if (m < M) a.y[(long long)m * L::COUT + co] = fmaxf((hi[i][e] + lo[i][e]) + bias, 0.f);
+                const float v = fmaxf((hi[i][e] + lo[i][e]) * uw + bias, 0.f);
+                om = fmaxf(om, v);  // a row past the end recomputed row m0, which is stored
+                if (m < M) a.y[(long long)m * L::COUT + co] = v;
             }
     };
     Raw r0, r1;
@@ -126,11 +129,7 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
         if (tile + 2 < t_end) load_tile(tile + 2, r0);
         run_tile(tile + 1, r1);
     }
-}
-
-// [co][ci][ky][kx] f32 -> conv1 split planes in fwd1_split_index order
-__global__ void pack_fwd1_split(const float* __restrict__ w, uint16_t* __restrict__ q) {
-    pack_fwd1_split_elem(w, q, blockIdx.x * blockDim.x + threadIdx.x);
+    amax_record(a.amax_y, om);
 }
 
 #ifndef SPLIT_FWD1_MT
@@ -145,44 +144,35 @@ __global__ void pack_fwd1_split(const float* __restrict__ w, uint16_t* __restric
 }  // namespace
 
 extern "C" int64_t ppox_nature_split_pack_elems(int32_t which) {
-    switch (which) {
-        case 1: return 3LL * G1::K * G1::COUT;
-        case 2: return 3LL * G2::K * G2::COUT;
-        case 3: return 3LL * G3::K * G3::COUT;
-        case 12: return 3LL * G2::K * G2::COUT;
-        case 13: return 3LL * G3::K * G3::COUT;
-        default: return -1;
-    }
+    const long long p = (which >= 1 && which <= 3) || which == 12 || which == 13 ? ppox_conv::planes(which) : -1;
+    return p < 0 ? -1 : p + 2 * PACK_TAIL32;  // + the tail (amax partials, scale exponent)
 }
 
 extern "C" int ppox_nature_pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1, uint16_t* q2,
                                       uint16_t* q3, uint16_t* qd2, uint16_t* qd3, void* stream) {
     // any packed buffer may be null: that packing is skipped
-    PPOX_REQUIRE((!q1 || ppox::aligned16(q1)) && (!q2 || ppox::aligned16(q2)) && (!q3 || ppox::aligned16(q3)) &&
-                     (!qd2 || ppox::aligned16(qd2)) && (!qd3 || ppox::aligned16(qd3)),
-                 "ppox_nature_pack_split: packed buffers must be 16-byte aligned");
     PPOX_REQUIRE((!q1 || w1) && (!q2 || w2) && (!q3 || w3) && (!qd2 || w2) && (!qd3 || w3),
                  "ppox_nature_pack_split: null weights");
-    hipStream_t s = ppox::as_stream(stream);
-    if (q1) pack_fwd1_split<<<ppox::ceil_div(8 * 2 * 64 * 8, 256), 256, 0, s>>>(w1, q1);
-    PPOX_LAUNCHED_NORET("ppox_nature_pack_split");
-    return ppox_conv::split_pack23(w2, w3, q2, q3, qd2, qd3, s);
+    return ppox_conv::pack_split(w1, w2, w3, q1, q2, q3, qd2, qd3, ppox::as_stream(stream));
 }
 
 extern "C" int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx, int64_t T,
                                           int64_t N_env, int64_t x_sample_stride, const uint16_t* wq,
-                                          const float* bias, float* y, void* stream) {
+                                          const float* bias, float* y, const uint32_t* amax_x, uint32_t* amax_y,
+                                          void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_conv_fwd_split: layer must be 1, 2 or 3");
     PPOX_REQUIRE(x && wq && bias && y && batch >= 0, "ppox_nature_conv_fwd_split: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(wq), "ppox_nature_conv_fwd_split: packed weights must be 16-byte aligned");
     if (layer != 1) {
         PPOX_REQUIRE(!idx, "ppox_nature_conv_fwd_split: idx is for layer 1 only");
-        return ppox_conv::split_fwd23(layer, x, batch, wq, bias, y, ppox::as_stream(stream));
+        return ppox_conv::split_fwd23(layer, x, batch, wq, bias, y, amax_x, amax_y, ppox::as_stream(stream));
     }
+    PPOX_REQUIRE(!amax_x, "ppox_nature_conv_fwd_split: layer 1 reads uint8 frames (no amax_x)");
     PPOX_REQUIRE(batch * G1::P < (1LL << 31), "ppox_nature_conv_fwd_split: batch too large for 32-bit rows");
-    Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride,
-           reinterpret_cast<const float*>(wq), bias, nullptr, y, batch};
+    Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, nullptr, bias, nullptr, y, batch,
+           nullptr, amax_y, pack_exp(wq, ppox_conv::planes(1))};
+    a.wp = reinterpret_cast<const float*>(wq);
     hipStream_t s = ppox::as_stream(stream);
     PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && (idx || x_sample_stride % 4 == 0),
                  "ppox_nature_conv_fwd_split: u8 input must be 4-byte aligned");

@@ -8,12 +8,14 @@
 //       over f, e, de, df (+ the intrinsic head's): actor weight/bias (dout^T f, sum dout),
 //       critic weight/bias (dv^T e, sum dv), extra-layer bias (sum de), fc bias (sum df).
 //       Fixed-order two-level sums (row chunks, then chunks in order): deterministic.
-#include "common.h"
+#include "conv_common.h"  // common.h + the split-f16 amax helpers
 
 namespace {
 
+// am (nullable): the masked grad's amax slots (a split-f16 GEMM operand)
 __global__ void __launch_bounds__(256) relu_bwd_kernel(float* __restrict__ g, const float* __restrict__ act,
-                                                       long long n4) {
+                                                       long long n4, uint32_t* __restrict__ am) {
+    float m = 0.f;
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
         float4 v = reinterpret_cast<float4*>(g)[i];
         const float4 a = reinterpret_cast<const float4*>(act)[i];
@@ -22,7 +24,9 @@ __global__ void __launch_bounds__(256) relu_bwd_kernel(float* __restrict__ g, co
         v.z = a.z > 0.f ? v.z : 0.f;
         v.w = a.w > 0.f ? v.w : 0.f;
         reinterpret_cast<float4*>(g)[i] = v;
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
+    amax_record(am, m);
 }
 
 // partial row of chunk c: [A*H actor W | A actor b | H critic W | 1 critic b | H extra b |
@@ -237,8 +241,17 @@ extern "C" int ppox_relu_backward_(float* grad, const float* act, int64_t n, voi
     if (n == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(grad && act && n >= 0 && n % 4 == 0, "ppox_relu_backward_: bad arguments (n % 4 == 0)");
     PPOX_REQUIRE(ppox::aligned16(grad) && ppox::aligned16(act), "ppox_relu_backward_: 16B alignment");
-    relu_bwd_kernel<<<grid_for(n / 4), 256, 0, ppox::as_stream(stream)>>>(grad, act, n / 4);
+    relu_bwd_kernel<<<grid_for(n / 4), 256, 0, ppox::as_stream(stream)>>>(grad, act, n / 4, nullptr);
     PPOX_LAUNCHED("ppox_relu_backward_");
+}
+
+extern "C" int ppox_relu_backward_amax_(float* grad, const float* act, int64_t n, uint32_t* amax, void* stream) {
+    if (n == 0) return PPOX_OK;
+    PPOX_REQUIRE(grad && act && amax && n > 0 && n % 4 == 0, "ppox_relu_backward_amax_: bad arguments (n % 4 == 0)");
+    PPOX_REQUIRE(ppox::aligned16(grad) && ppox::aligned16(act) && ppox::aligned16(amax),
+                 "ppox_relu_backward_amax_: 16B alignment");
+    relu_bwd_kernel<<<grid_for(n / 4), 256, 0, ppox::as_stream(stream)>>>(grad, act, n / 4, amax);
+    PPOX_LAUNCHED("ppox_relu_backward_amax_");
 }
 
 extern "C" int64_t ppox_head_grads_workspace_bytes(int64_t rows, int64_t h, int64_t n_actions, int32_t intrinsic) {

@@ -106,8 +106,8 @@ class CnnActorCritic(nn.Module):
     def trunk(self, x):
         if self.conv_impl is not None and self.conv_impl.math != "f32" and not torch.is_grad_enabled():
             # inference (collect): the split-bf16 fc GEMM straight off the conv trunk
-            h1, h2, h3 = self.conv_impl.forward_acts(x.contiguous())
-            return self.conv_impl.fc_forward(h3)
+            h1, h2, h3, am = self.conv_impl.forward_acts(x.contiguous())
+            return self.conv_impl.fc_forward(h3, am)
         if self.conv_impl is not None:
             h = self.conv_impl(x)
         else:
@@ -135,15 +135,15 @@ class CnnActorCritic(nn.Module):
         """-> (actor out, value (B,), int value or None, ctx for backward_train)."""
         with torch.no_grad():
             x = x.contiguous()
-            h1, h2, h3 = self.conv_impl.forward_acts(x)
+            h1, h2, h3, am = self.conv_impl.forward_acts(x)
             hf = h3.view(h3.shape[0], -1)
             fc = self.feature_extractor[7]
             if self.conv_impl.math != "f32":
-                f = self.conv_impl.fc_forward(h3)
+                f = self.conv_impl.fc_forward(h3, am)
             else:
                 f = linear_relu(hf, fc.weight, fc.bias)
             out, v, iv, e, ie = self._heads(f)
-        return out, v, iv, (x, h1, h2, h3, f, e, ie)
+        return out, v, iv, (x, h1, h2, h3, f, e, ie, am)
 
     def _heads(self, f):
         """actor logits, value, int value, and the hidden activations (no autograd): fused
@@ -193,7 +193,7 @@ class CnnActorCritic(nn.Module):
         """Accumulate dL/dparams for upstream grads (dout (B,A), dv (B,), div (B,)).
         `dense_ready()` is called once every non-conv gradient (fc + heads) is enqueued,
         before the conv backward (ppo.BaseAlgorithm._bwd_reduce overlaps its all-reduce)."""
-        x, h1, h2, h3, f, e, ie = ctx
+        x, h1, h2, h3, f, e, ie, am = ctx
         B = x.shape[0]
         with torch.no_grad():
             hf = h3.view(B, -1)
@@ -219,8 +219,8 @@ class CnnActorCritic(nn.Module):
                         weight_grad(de, f, hid.weight.grad, self._wgrad_part(hid.weight))
                 df.addmm_(de, hid.weight)
                 des.append((de, d))
-            native.relu_backward_(df, f)
             cv = self.conv_impl
+            native.relu_backward_(df, f, amax=am[_convs.AM_DF] if cv.nhwc3 else None)
             # every column-reduction gradient (actor W/b, critic W/b, extra-layer b, fc b) in one pass
             ws = self._head_ws(B, f.shape[1], dout.shape[1])
             (de, d), intr = des[0], des[1] if self.intrinsic else (None, None)
@@ -232,7 +232,8 @@ class CnnActorCritic(nn.Module):
                               b_int_extra=self.int_extra_layer[0].bias.grad if self.intrinsic else None)
             if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-bf16 kernel, Flatten-order dW
                 if side is None:
-                    native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad)
+                    native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, amax_df=am[_convs.AM_DF],
+                                           amax_h3=am[_convs.AM_H3])
                     if dense_ready is not None:
                         dense_ready()
                 else:
@@ -240,7 +241,8 @@ class CnnActorCritic(nn.Module):
                     # gradients' all-reduce is started from there (ordered after it and, through the
                     # fork, after every head gradient); backward_acts joins the side stream
                     _convs.fork(side, cur)
-                    native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, stream=side)
+                    native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, amax_df=am[_convs.AM_DF],
+                                           amax_h3=am[_convs.AM_H3], stream=side)
                     if dense_ready is not None:
                         with torch.cuda.stream(side):
                             dense_ready()
@@ -257,17 +259,17 @@ class CnnActorCritic(nn.Module):
                     dense_ready()
             fe = self.feature_extractor
             if cv.nhwc3 and B < _convs.FC_DGRAD_FUSED_MAX_BATCH:  # masked NHWC grad directly
-                dh3, g3 = None, cv.fc_dgrad_g3(df, h3)
+                dh3, g3 = None, cv.fc_dgrad_g3(df, h3, am)
             elif cv.nhwc3:  # library GEMM on the permuted weight: NHWC order, then the ReLU mask
                 torch.index_select(fc.weight, 1, cv.fc_perm, out=cv.wfc_nhwc)
                 g3 = torch.mm(df, cv.wfc_nhwc).view(B, 7, 7, 64)
-                native.relu_backward_(g3, h3)
+                native.relu_backward_(g3, h3, amax=am[_convs.AM_G3])
                 dh3 = None
             else:
                 dh3, g3 = torch.mm(df, fc.weight), None
             # conv grads are written by the trunk kernels; the flat buffer was zeroed per minibatch
             self.conv_impl.backward_acts(x, h1, h2, h3, dh3, fe[0].weight.grad, fe[0].bias.grad, fe[2].weight.grad,
-                                         fe[2].bias.grad, fe[4].weight.grad, fe[4].bias.grad, g3=g3)
+                                         fe[2].bias.grad, fe[4].weight.grad, fe[4].bias.grad, g3=g3, am=am)
 
 
 class RndNetwork(nn.Module):

@@ -61,18 +61,20 @@ SIGNATURES = {
     "ppox_nchw_to_nhwc_relu_grad": [_vp, _vp, _i64, _vp, _vp],
     "ppox_nature_conv_fwd": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_pack_split": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
-    "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
+    "ppox_relu_backward_amax_": [_vp, _vp, _i64, _vp, _vp],
+    "ppox_amax": [_vp, _i64, _vp, _vp],
     "ppox_u8_to_f32": [_vp, _i64, _vp, _vp],
     "ppox_skinny_linear": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "ppox_skinny_dgrad": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 11,
     "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
     "ppox_nature_pack_all": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp],
-    "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp],
-    "ppox_nature_fc_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp],
+    "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_fc_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_es_noise": [_i64, _i64, _i64, _i64, _u64, _vp, _vp],
     "ppox_es_env_noise": [_i32, _i32, _u64, _vp, _vp],
     "ppox_es_evaluate": [_vp, _vp, _f64, _i64, _i32, _i32, _i32, _i32, _i32, _u64, _vp, _vp, _vp, _vp],
@@ -80,12 +82,12 @@ SIGNATURES = {
     "ppox_normalize_obs_f32_ex": [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _f64, _vp, _vp],
     "ppox_vecnorm_reward": [_vp, _vp, _vp, _i64, _f64, _vp, _vp, _f64, _f64, _f64, _i32, _vp],
     "ppox_outer_relu_backward": [_vp, _vp, _vp, _i64, _i64, _vp, _vp],
-    "ppox_nature_conv_wgrad_split": [_i32, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
-    "ppox_nature_conv_wgrad_split_idx": [_i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp],
+    "ppox_nature_conv_wgrad_split": [_i32, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_wgrad_split_idx": [_i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
-    "ppox_nature_fc_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp],
+    "ppox_nature_fc_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
     "ppox_icm_pack_w1": [_vp, _i64, _vp, _vp],
     "ppox_icm_encode": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_icm_pair_backward": [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp],
@@ -103,7 +105,7 @@ _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p
              "ppox_nature_fc_wgrad_workspace_bytes": ctypes.c_int64, "ppox_icm_param_elems": ctypes.c_int64,
              "ppox_icm_w1_pack_elems": ctypes.c_int64, "ppox_icm_encode_workspace_bytes": ctypes.c_int64,
              "ppox_icm_partials_bytes": ctypes.c_int64, "ppox_icm_g1_pack_elems": ctypes.c_int64,
-             "ppox_nature_fc_fwd_splitk_workspace_bytes": ctypes.c_int64}
+             "ppox_nature_fc_fwd_splitk_workspace_bytes": ctypes.c_int64, "ppox_amax_slots": ctypes.c_int32}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
                  "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32],
                  "ppox_nature_wgrad_split_workspace_bytes": [_i32, _i64],
@@ -466,9 +468,33 @@ def nature_conv_fwd(layer, x, batch, idx, T, N_env, x_sample_stride, wp, bias, y
          _p(wp), _p(bias), _p(y), stream_ptr(stream))
 
 
-# split-bf16 forms (csrc/conv_split.hip): weights packed as three exact bf16 planes (int16 tensors)
+# split-f16 forms (csrc/conv_split.hip, csrc/conv.hip): weights packed as two fp16 planes
+# (int16 tensors) times a power-of-two scale; f32 operands carry "amax slots" (include/ppox.h)
+AMAX_SLOTS = 256  # include/ppox.h ppox_amax_slots()
+
+
+def amax_table(n, device):
+    """n zeroed amax-slot rows (int32 storage of the uint32 slots), one per tensor."""
+    return torch.zeros((n, AMAX_SLOTS), dtype=torch.int32, device=device)
+
+
+def amax(x, slots, stream=None):
+    """Record max |x| into `slots` (an amax_table row)."""
+    call("ppox_amax", _p(x), x.numel(), _p(slots), stream_ptr(stream))
+
+
+def _amax_of(x, slots, stream=None):
+    """`slots` if given, else a fresh row holding max |x| (callers that did not record the operand)."""
+    if slots is not None:
+        return slots
+    slots = amax_table(1, x.device)[0]
+    amax(x.contiguous(), slots, stream)
+    return slots
+
+
 def nature_split_pack_elems(which):
-    """bf16 elements of the split-packed buffer: which = 1, 2, 3 (forward) or 12, 13 (dgrad of conv2/3)."""
+    """uint16 elements of a split-packed buffer (planes + scale tail): which = 1, 2, 3 (forward)
+    or 12, 13 (dgrad of conv2/3)."""
     return int(load().ppox_nature_split_pack_elems(int(which)))
 
 
@@ -477,9 +503,14 @@ def nature_pack_split(w1, w2, w3, q1, q2, q3, qd2=None, qd3=None, stream=None):
          stream_ptr(stream))
 
 
-def nature_conv_fwd_split(layer, x, batch, idx, T, N_env, x_sample_stride, wq, bias, y, stream=None):
+def nature_conv_fwd_split(layer, x, batch, idx, T, N_env, x_sample_stride, wq, bias, y, amax_x=None, amax_y=None,
+                          stream=None):
+    """amax_x: x's slots (layers 2, 3; computed here when None); amax_y: y's slots to record (or None)."""
+    if layer != 1 and batch:
+        amax_x = _amax_of(x, amax_x, stream)
     call("ppox_nature_conv_fwd_split", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
-         int(x_sample_stride), _p(wq), _p(bias), _p(y), stream_ptr(stream))
+         int(x_sample_stride), _p(wq), _p(bias), _p(y), _p(amax_x) if layer != 1 else None, _p(amax_y),
+         stream_ptr(stream))
 
 
 def normalize_obs_f32_ex(x, rows, cols, row_stride, mean, var, eps, clip, out, stream=None):
@@ -508,34 +539,43 @@ def nature_pack_all(w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dg
          _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), stream_ptr(stream))
 
 
-def nature_fc_fwd(h3, batch, q_fwd, bias, f, stream=None):
-    """f = relu(h3 @ W^T + b), h3 (batch, 3136) in Flatten order."""
-    call("ppox_nature_fc_fwd", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(f), stream_ptr(stream))
+def nature_fc_fwd(h3, batch, q_fwd, bias, f, amax_h3=None, stream=None):
+    """f = relu(h3 @ W^T + b), h3 (batch, 7, 7, 64) NHWC."""
+    if batch:
+        amax_h3 = _amax_of(h3, amax_h3, stream)
+    call("ppox_nature_fc_fwd", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(f), _p(amax_h3), stream_ptr(stream))
 
 
 def nature_fc_fwd_splitk_workspace_bytes(batch):
     return int(load().ppox_nature_fc_fwd_splitk_workspace_bytes(int(batch)))
 
 
-def nature_fc_fwd_splitk(h3, batch, q_fwd, bias, workspace, f, stream=None):
+def nature_fc_fwd_splitk(h3, batch, q_fwd, bias, workspace, f, amax_h3=None, stream=None):
     """fc forward split over K (small batches), bias + ReLU in the fixed-order reduce."""
+    if batch:
+        amax_h3 = _amax_of(h3, amax_h3, stream)
     call("ppox_nature_fc_fwd_splitk", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(workspace),
-         workspace.numel() * workspace.element_size(), _p(f), stream_ptr(stream))
+         workspace.numel() * workspace.element_size(), _p(f), _p(amax_h3), stream_ptr(stream))
 
 
-def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, stream=None):
-    """g3 (batch, 7, 7, 64) NHWC = ((df @ W) in Flatten order) * (h3 > 0)."""
-    call("ppox_nature_fc_dgrad", _p(df), int(batch), _p(q_dgrad), _p(h3), _p(g3), stream_ptr(stream))
+def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, amax_df=None, amax_g3=None, stream=None):
+    """g3 (batch, 7, 7, 64) NHWC = ((df @ W) in Flatten order) * (h3 > 0); amax_g3: g3's slots to record."""
+    if batch:
+        amax_df = _amax_of(df, amax_df, stream)
+    call("ppox_nature_fc_dgrad", _p(df), int(batch), _p(q_dgrad), _p(h3), _p(g3), _p(amax_df), _p(amax_g3),
+         stream_ptr(stream))
 
 
 def nature_fc_wgrad_workspace_bytes(batch):
     return int(lib().ppox_nature_fc_wgrad_workspace_bytes(int(batch)))
 
 
-def nature_fc_wgrad(df, batch, h3, workspace, dw, stream=None):
+def nature_fc_wgrad(df, batch, h3, workspace, dw, amax_df=None, amax_h3=None, stream=None):
     """dw (512, 3136) in the fc weight's Flatten order = df^T @ h3 (h3 NHWC (batch, 7, 7, 64))."""
+    if batch:
+        amax_df, amax_h3 = _amax_of(df, amax_df, stream), _amax_of(h3, amax_h3, stream)
     call("ppox_nature_fc_wgrad", _p(df), int(batch), _p(h3), _p(workspace), workspace.numel() * workspace.element_size(),
-         _p(dw), stream_ptr(stream))
+         _p(dw), _p(amax_df), _p(amax_h3), stream_ptr(stream))
 
 
 # ES-NSRA (csrc/es.hip)
@@ -562,9 +602,12 @@ def es_update(eps, coef, P, n_params, workspace, out, stream=None):
          workspace.numel() * workspace.element_size(), _p(out), stream_ptr(stream))
 
 
-def relu_backward_(grad, act, stream=None):
-    """grad = act > 0 ? grad : 0, in place (same-shape contiguous f32)."""
-    call("ppox_relu_backward_", _p(grad), _p(act), grad.numel(), stream_ptr(stream))
+def relu_backward_(grad, act, amax=None, stream=None):
+    """grad = act > 0 ? grad : 0, in place (same-shape contiguous f32); amax: slots recording max |grad|."""
+    if amax is None:
+        call("ppox_relu_backward_", _p(grad), _p(act), grad.numel(), stream_ptr(stream))
+    else:
+        call("ppox_relu_backward_amax_", _p(grad), _p(act), grad.numel(), _p(amax), stream_ptr(stream))
 
 
 def _aligned(t):
@@ -625,23 +668,34 @@ def nature_wgrad_split_workspace_bytes(layer, batch):
     return int(load().ppox_nature_wgrad_split_workspace_bytes(int(layer), int(batch)))
 
 
-def nature_conv_wgrad_split(layer, x, batch, x_sample_stride, grad_out, workspace, dw, db, stream=None):
-    """dW, db of one conv layer (slabs + fixed-order reduce in one call), split-bf16 MFMA."""
+def nature_conv_wgrad_split(layer, x, batch, x_sample_stride, grad_out, workspace, dw, db, amax_x=None, amax_g=None,
+                            stream=None):
+    """dW, db of one conv layer (slabs + fixed-order reduce in one call), split-f16 MFMA."""
+    amax_g = _amax_of(grad_out, amax_g, stream)
+    if layer != 1:
+        amax_x = _amax_of(x, amax_x, stream)
     call("ppox_nature_conv_wgrad_split", int(layer), _p(x), int(batch), int(x_sample_stride), _p(grad_out),
-         _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db), stream_ptr(stream))
+         _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db),
+         _p(amax_x) if layer != 1 else None, _p(amax_g), stream_ptr(stream))
 
 
-def nature_conv_wgrad_split_idx(layer, x, batch, idx, T, N_env, grad_out, workspace, dw, db, stream=None):
+def nature_conv_wgrad_split_idx(layer, x, batch, idx, T, N_env, grad_out, workspace, dw, db, amax_g=None,
+                                stream=None):
     """conv1 dW, db from the step-major (T, N_env, 4, 84, 84) rollout frames through env-major
-    rows idx (the minibatch gather fused), split-bf16 MFMA."""
+    rows idx (the minibatch gather fused), split-f16 MFMA."""
+    amax_g = _amax_of(grad_out, amax_g, stream)
     call("ppox_nature_conv_wgrad_split_idx", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
-         _p(grad_out), _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db),
+         _p(grad_out), _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db), _p(amax_g),
          stream_ptr(stream))
 
 
-def nature_conv_dgrad_split(layer, grad_out, batch, wqd, prev_act, grad_in, stream=None):
+def nature_conv_dgrad_split(layer, grad_out, batch, wqd, prev_act, grad_in, amax_g=None, amax_out=None,
+                            stream=None):
+    """amax_g: grad_out's slots (computed here when None); amax_out: grad_in's slots to record (or None)."""
+    if batch:
+        amax_g = _amax_of(grad_out, amax_g, stream)
     call("ppox_nature_conv_dgrad_split", int(layer), _p(grad_out), int(batch), _p(wqd), _p(prev_act), _p(grad_in),
-         stream_ptr(stream))
+         _p(amax_g), _p(amax_out), stream_ptr(stream))
 
 
 # ---------------------------------------------------------------------------

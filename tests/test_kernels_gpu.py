@@ -459,9 +459,10 @@ def _conv_ops_fp64(B, seed):
         h1 = torch.empty(B, 20, 20, 32, device="cuda")
         h2 = torch.empty(B, 9, 9, 64, device="cuda")
         h3 = torch.empty((B, 7, 7, 64) if cv.nhwc3 else (B, 64, 7, 7), device="cuda")
-        cv.fwd(1, x, B, cv.c1.bias, h1)
-        cv.fwd(2, h1, B, cv.c2.bias, h2)
-        cv.fwd(3, h2, B, cv.c3.bias, h3)
+        am = native.amax_table(convs.AM_ROWS, "cuda")  # each forward records its output's amax
+        cv.fwd(1, x, B, cv.c1.bias, h1, am)
+        cv.fwd(2, h1, B, cv.c2.bias, h2, am)
+        cv.fwd(3, h2, B, cv.c3.bias, h3, am)
         if cv.nhwc3:  # split math writes conv3's output NHWC
             h3 = h3.permute(0, 3, 1, 2)
         hs.update({("fwd", 1): h1, ("fwd", 2): h2, ("fwd", 3): h3})
@@ -471,20 +472,27 @@ def _conv_ops_fp64(B, seed):
     g3 = torch.randn(B, 7, 7, 64, device="cuda", generator=gen)
     g2r = torch.randn(B, 9, 9, 64, device="cuda", generator=gen)
     h1f, h2f = out["f32"][("fwd", 1)], out["f32"][("fwd", 2)]
+
+    def amax_rows(**rows):  # a fresh amax table holding the given operands' rows
+        am = native.amax_table(convs.AM_ROWS, "cuda")
+        for name, t in rows.items():
+            native.amax(t, am[getattr(convs, "AM_" + name)])
+        return am
     for math in ("split_all", "f32"):
         net.conv_impl = None
         cv = convs.attach(net, flat, math)
         cv.pack()
         d2 = torch.empty(B, 9, 9, 64, device="cuda")
         d1 = torch.empty(B, 20, 20, 32, device="cuda")
-        cv.dgrad(3, g3, B, h2f, d2)
-        cv.dgrad(2, g2r, B, h1f, d1)
+        cv.dgrad(3, g3, B, h2f, d2, amax_rows(G3=g3))
+        cv.dgrad(2, g2r, B, h1f, d1, amax_rows(G2=g2r))
         out[math].update({("dgrad", 3): d2, ("dgrad", 2): d1})
         g1r = torch.randn(B, 20, 20, 32, device="cuda", generator=torch.Generator(device="cuda").manual_seed(seed + 7))
+        am = amax_rows(G1=g1r, G2=g2r, G3=g3, H1=h1f, H2=h2f)
         for L, xin, gg in ((1, x, g1r), (2, h1f, g2r), (3, h2f, g3)):
             wl = (cv.c1, cv.c2, cv.c3)[L - 1]
             dw, db = torch.empty_like(wl.weight), torch.empty_like(wl.bias)
-            cv.wgrad(L, xin, B, gg, dw, db)
+            cv.wgrad(L, xin, B, gg, dw, db, am)
             out[math].update({("wgrad", L): dw, ("wgrad_bias", L): db})
     # fp64 reference (CPU autograd, same weights)
     fe = net.feature_extractor
@@ -509,7 +517,7 @@ def _conv_ops_fp64(B, seed):
 
 @pytest.mark.parametrize("seed", [0, 1])
 def test_split_conv_accuracy_is_fp32_class(seed):
-    """Split-bf16 kernels vs fp64: error no larger than the exact-f32-FMA kernels' own error
+    """Split-f16 kernels vs fp64: error no larger than the exact-f32-FMA kernels' own error
     (x2 headroom), for every op that has a split kernel.  Forward ops take each layer's
     input from the same mode, so errors compound as in the product path."""
     import convs
@@ -830,6 +838,55 @@ def test_fc_wgrad_split_vs_fp64(B):
     dw2 = torch.empty_like(dw)
     native.nature_fc_wgrad(df, B, h3n, ws, dw2)
     assert torch.equal(dw, dw2)
+
+
+def test_amax_slots_record_the_max():
+    """ppox_amax: the slots' maximum is max |x| (f32 bits), any sign, zeros and subnormals."""
+    import native
+    for x in (torch.randn(1000, 12, device="cuda") * 1e-3, torch.zeros(64, device="cuda"),
+              torch.full((8,), -3.5, device="cuda"), torch.tensor([1e-40, -2e-40, 0.0, 0.0], device="cuda")):
+        am = native.amax_table(1, "cuda")[0]
+        native.amax(x, am)
+        got = am.view(torch.float32).max().item()
+        assert got == x.abs().max().item()
+
+
+@pytest.mark.parametrize("mag", [1e-15, 1e-7, 1e7, 1e15, "lognormal"])
+def test_split_f16_any_operand_range(mag):
+    """Split-f16 operands are scaled per tensor by a power of two from their amax: the fc
+    forward, fused dgrad and weight gradient keep an error no larger than torch's f32 GEMM's
+    (x2 headroom) for operands of any magnitude, and for entries spread over ~13 decades."""
+    import native
+    B = 300
+    torch.manual_seed(5)
+    W = torch.randn(512, 3136, device="cuda") * 0.02
+    b = torch.zeros(512, device="cuda")
+    h3n = torch.relu(torch.randn(B, 7, 7, 64, device="cuda"))
+    df = torch.randn(B, 512, device="cuda")
+    if mag == "lognormal":
+        h3n = h3n * torch.exp(3 * torch.randn_like(h3n))
+        df = df * torch.exp(3 * torch.randn_like(df))
+    else:
+        h3n, df = h3n * mag, df * mag
+    h3 = h3n.permute(0, 3, 1, 2).reshape(B, 3136)
+    n = native.nature_fc_pack_elems()
+    qf, qd = torch.empty(n, dtype=torch.int16, device="cuda"), torch.empty(n, dtype=torch.int16, device="cuda")
+    native.nature_fc_pack(W, qf, qd)
+    rel = lambda got, ref: ((got.double() - ref).abs().max() / ref.abs().max()).item()
+    f = torch.empty(B, 512, device="cuda")
+    native.nature_fc_fwd(h3n, B, qf, b, f)
+    ref = torch.relu(h3.double() @ W.double().t())
+    assert rel(f, ref) <= 2 * rel(torch.relu(h3 @ W.t()), ref) + 1e-7
+    g3 = torch.empty(B, 7, 7, 64, device="cuda")
+    native.nature_fc_dgrad(df, B, qd, h3n, g3)
+    refd = (df.double() @ W.double()).view(B, 64, 7, 7).permute(0, 2, 3, 1) * (h3n > 0)
+    e_f = rel((df @ W).view(B, 64, 7, 7).permute(0, 2, 3, 1) * (h3n > 0), refd)
+    assert rel(g3, refd) <= 2 * e_f + 1e-7
+    ws = torch.empty(native.nature_fc_wgrad_workspace_bytes(B), dtype=torch.uint8, device="cuda")
+    dw = torch.empty(512, 3136, device="cuda")
+    native.nature_fc_wgrad(df, B, h3n, ws, dw)
+    refw = df.double().t() @ h3.double()
+    assert rel(dw, refw) <= 2 * rel(df.t() @ h3, refw) + 1e-7
 
 
 def test_fc_wgrad_zero_rows_writes_zero():

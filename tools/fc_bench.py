@@ -1,4 +1,4 @@
-"""fc layer (3136 -> 512) split-bf16 GEMM vs rocBLAS f32 (torch) at the training batch:
+"""fc layer (3136 -> 512) split-f16 GEMM vs rocBLAS f32 (torch) at the training batch:
 time and error vs float64.  Usage: python tools/fc_bench.py [B] [lib.so]"""
 import json
 import os
@@ -39,19 +39,22 @@ def main():
     native.nature_fc_pack(W, qf, qd)
     f = torch.empty(B, 512, device=d)
     g3 = torch.empty(B, 7, 7, 64, device=d)
+    am = native.amax_table(2, d)  # operand amax rows, recorded once (the product's producers record them)
+    native.amax(h3n, am[0])
+    native.amax(df, am[1])
     flop = 2.0 * B * 3136 * 512
     res = {"B": B}
-    res["split_fwd_ms"] = t_ms(lambda: native.nature_fc_fwd(h3n, B, qf, b, f))
+    res["split_fwd_ms"] = t_ms(lambda: native.nature_fc_fwd(h3n, B, qf, b, f, amax_h3=am[0]))
     res["rocblas_fwd_ms"] = t_ms(lambda: torch.relu(torch.addmm(b, h3, W.t())))
     wsk = torch.empty(max(native.nature_fc_fwd_splitk_workspace_bytes(B), 16), dtype=torch.uint8, device=d)
     fsk = torch.empty(B, 512, device=d)
-    res["splitk_fwd_ms"] = t_ms(lambda: native.nature_fc_fwd_splitk(h3n, B, qf, b, wsk, fsk))
+    res["splitk_fwd_ms"] = t_ms(lambda: native.nature_fc_fwd_splitk(h3n, B, qf, b, wsk, fsk, amax_h3=am[0]))
     res["addmm_act_fwd_ms"] = t_ms(lambda: torch._addmm_activation(b, h3, W.t()))
-    res["split_dgrad_ms"] = t_ms(lambda: native.nature_fc_dgrad(df, B, qd, h3n, g3))
+    res["split_dgrad_ms"] = t_ms(lambda: native.nature_fc_dgrad(df, B, qd, h3n, g3, amax_df=am[1]))
     res["rocblas_dgrad_ms"] = t_ms(lambda: torch.mm(df, W))
     ws = torch.empty(native.nature_fc_wgrad_workspace_bytes(B), dtype=torch.uint8, device=d)
     dw = torch.empty(512, 3136, device=d)
-    res["split_wgrad_ms"] = t_ms(lambda: native.nature_fc_wgrad(df, B, h3n, ws, dw))
+    res["split_wgrad_ms"] = t_ms(lambda: native.nature_fc_wgrad(df, B, h3n, ws, dw, amax_df=am[1], amax_h3=am[0]))
     res["rocblas_wgrad_ms"] = t_ms(lambda: torch.mm(df.t(), h3))
     for k in list(res):
         if k.endswith("_ms"):
