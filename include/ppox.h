@@ -287,7 +287,8 @@ int ppox_vecnorm_reward(float* rewards, const uint8_t* dones, double* ret, int64
  * on the split-f16 GEMM (see the K6 split section below for the arithmetic and the amax slots):
  * weights packed (once per optimizer step) by ppox_nature_fc_pack into ppox_nature_fc_pack_elems()
  * uint16 each for the forward (W^T) and the dgrad (W) operand.  amax_h3 / amax_df: the slots of
- * the A operand (required); amax_g3: the slots the dgrad records g3's amax into (nullable).
+ * the A operand (required); amax_g3 / amax_f: the slots the dgrad / forward record g3's / f's
+ * amax into (nullable).
  * Both run in NHWC feature order: h3 is the split conv3 forward's NHWC output (batch, 7, 7, 64)
  * and W is packed through the permutation f = p * 64 + c <- Flatten feature c * 49 + p.
  * fwd: f = relu(h3 @ W^T + b); dgrad: g3 (NHWC (B,7,7,64)) = (df @ W) * (h3 > 0)
@@ -298,10 +299,29 @@ int64_t ppox_nature_fc_pack_elems(void);
  * ppox_nature_pack_split); qfc_fwd / qfc_dgrad = fc split forms (as ppox_nature_fc_pack). */
 int ppox_nature_pack_all(const float* w1, const float* w2, const float* w3, const float* wfc, float* wpd2,
                          uint16_t* q1, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
-                         uint16_t* qfc_fwd, uint16_t* qfc_dgrad, void* stream);
+                         uint16_t* qfc_fwd, uint16_t* qfc_dgrad, const float* wh, uint16_t* qh_fwd,
+                         uint16_t* qh_dgrad, void* stream);
+/* The heads' hidden layer Linear(512, 512) + ReLU (models-checkpoint.py:62-66 extra_layer; the
+ * forward of forward() / evaluate and its autograd in ppo.py:216-238) on the split-f16 GEMM, with
+ * wh (512 x 512) packed by ppox_nature_pack_all into qh_fwd / qh_dgrad of
+ * ppox_head_hidden_pack_elems() uint16 each.
+ *   fwd:   e = relu(f wh^T + b)                         (amax_f: f's slots, required)
+ *   dgrad: df = (f > 0) ? df + de wh : 0, in place       (df holds the heads' other input grads;
+ *          the ReLU backward of the fc layer fused; amax_df: df's slots to record, nullable)
+ *   wgrad: dw (512 x 512) = de^T f, split-K slabs in the workspace
+ *          (ppox_head_hidden_wgrad_workspace_bytes(rows)) summed in a fixed order; rows 0 writes
+ *          a zero gradient. */
+int64_t ppox_head_hidden_pack_elems(void);
+int ppox_head_hidden_fwd(const float* f, int64_t rows, const uint16_t* q_fwd, const float* bias, float* e,
+                         const uint32_t* amax_f, void* stream);
+int ppox_head_hidden_dgrad(const float* de, int64_t rows, const uint16_t* q_dgrad, const float* f, float* df,
+                           const uint32_t* amax_de, uint32_t* amax_df, void* stream);
+int64_t ppox_head_hidden_wgrad_workspace_bytes(int64_t rows);
+int ppox_head_hidden_wgrad(const float* de, int64_t rows, const float* f, void* workspace, int64_t workspace_bytes,
+                           float* dw, const uint32_t* amax_de, const uint32_t* amax_f, void* stream);
 int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_dgrad, void* stream);
 int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
-                       const uint32_t* amax_h3, void* stream);
+                       const uint32_t* amax_h3, uint32_t* amax_f, void* stream);
 int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
                          const uint32_t* amax_df, uint32_t* amax_g3, void* stream);
 /* fc forward (as ppox_nature_fc_fwd) split over K for small batches: 2-8 K-ranges per (128-row
@@ -311,7 +331,7 @@ int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad
 int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch);
 int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias,
                               void* workspace, int64_t workspace_bytes, float* f, const uint32_t* amax_h3,
-                              void* stream);
+                              uint32_t* amax_f, void* stream);
 /* fc weight gradient dW (512 x 3136, the weight's Flatten order) = df^T @ h3 over the batch,
  * split-f16 (fp32-class; amax_df, amax_h3: the operands' slots), deterministic: df (batch, 512) is dL/df already ReLU-masked, h3 the
  * NHWC (batch, 7, 7, 64) conv3 output of the split forward.  Replaces the library GEMM of
@@ -343,7 +363,8 @@ int ppox_es_update(const double* eps, const double* coef, int64_t P, int64_t n_p
 
 /* NatureCNN head backward (explicit training backward of CnnActorCritic, replacing the
  * autograd of nn.ReLU / Linear(H, 1) at .ipynb_checkpoints/models-checkpoint.py:60-87):
- * grad = act > 0 ? grad : 0 in place (n % 4 == 0); out[b][j] = dv[b] * w[j] * (act[b][j] > 0). */
+ * grad = act > 0 ? grad : 0 in place (n % 4 == 0); out[b][j] = dv[b] * w[j] * (act[b][j] > 0)
+ * (amax: out's split-f16 amax slots to record, nullable). */
 int ppox_relu_backward_(float* grad, const float* act, int64_t n, void* stream);
 /* as ppox_relu_backward_, also recording max |grad| into amax (split-f16 slots, below): the fc
  * output grad df that the split fc dgrad / weight gradient take as an operand */
@@ -368,7 +389,7 @@ int ppox_skinny_linear(const float* x, const float* w, const float* bias, int64_
 int ppox_skinny_dgrad(const float* g, const float* w, int64_t rows, int64_t h, int64_t n_out, float* d,
                       void* stream);
 int ppox_outer_relu_backward(const float* dv, const float* w, const float* act, int64_t rows, int64_t h,
-                             float* out, void* stream);
+                             float* out, uint32_t* amax, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K6, split-f16 forms (csrc/conv_split.hip, csrc/conv.hip): the same ops, layouts and

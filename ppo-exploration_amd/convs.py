@@ -49,10 +49,14 @@ FC_DGRAD_FUSED_MAX_BATCH = int(os.environ.get("PPOX_FC_DGRAD_FUSED_MAX", str(1 <
 # the rocBLAS f32 GEMM + NHWC -> Flatten permute below (PPOX_FC_WGRAD_SPLIT_MIN overrides)
 FC_WGRAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_WGRAD_SPLIT_MIN", "0"))
 
-# rows of a pass's amax table (native.amax_table): the split-f16 operands of the trunk, each
-# recorded by the kernel that produces it and read by the kernels that consume it
-AM_H1, AM_H2, AM_H3, AM_DF, AM_G3, AM_G2, AM_G1 = range(7)
-AM_ROWS = 8
+# the heads' hidden layer Linear(512, 512) on the split-f16 GEMM (ppox_head_hidden_*) from this
+# batch up, rocBLAS f32 below (PPOX_HEAD_SPLIT_MIN overrides)
+HEAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_SPLIT_MIN", "8192"))
+
+# rows of a pass's amax table (native.amax_table): the split-f16 operands of the trunk and the
+# heads' hidden layer, each recorded by the kernel that produces it and read by its consumers
+AM_H1, AM_H2, AM_H3, AM_DF, AM_G3, AM_G2, AM_G1, AM_F, AM_DE = range(9)
+AM_ROWS = 10
 
 
 # backward on two streams: each layer's weight gradient runs on a side stream beside the
@@ -170,10 +174,15 @@ class NatureConvs:
         # split-bf16 planes (int16 storage), packed by ppox_nature_pack_split
         self.q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device=dev)
                   for k in (1, 2, 3, 12, 13)}
-        # fc layer (feature_extractor[7], 3136 -> 512) split-bf16 operands (split math only)
+        # fc layer (feature_extractor[7], 3136 -> 512) split-f16 operands (split math only)
         self.fc = net.feature_extractor[7]
         nfc = native.nature_fc_pack_elems()
         self.qfc = (torch.empty(nfc, dtype=torch.int16, device=dev), torch.empty(nfc, dtype=torch.int16, device=dev)) \
+            if self.math != "f32" else None
+        # the heads' hidden layer (extra_layer[0], 512 -> 512): split-f16 forward / dgrad forms
+        self.hid = net.extra_layer[0]
+        nh = native.head_hidden_pack_elems()
+        self.qh = (torch.empty(nh, dtype=torch.int16, device=dev), torch.empty(nh, dtype=torch.int16, device=dev)) \
             if self.math != "f32" else None
         # split math keeps conv3's output NHWC (B, 7, 7, 64): fc feature f = p * 64 + c is the
         # reference's Flatten feature c * 49 + p.  The split fc kernels are packed through that
@@ -187,6 +196,10 @@ class NatureConvs:
         self._ws = {}
         self._version = None
         self._packed = set()
+
+    def split_head(self, batch):
+        """the heads' hidden layer on the split-f16 kernels for a `batch`-row pass"""
+        return self.qh is not None and batch >= HEAD_SPLIT_MIN_BATCH
 
     def uses_split(self, op, layer, batch=None):
         if self.math == "split_all":  # every op that has a split kernel (tests, benchmarks)
@@ -215,6 +228,8 @@ class NatureConvs:
         if self.math != "f32":
             forms.add("qfcd")
             forms.add("qfcf" if batch >= FC_SPLIT_MIN_BATCH else "wfc_nhwc")
+        if self.split_head(batch):
+            forms |= {"qhf", "qhd"}
         return forms
 
     def pack(self, batch=0):
@@ -232,12 +247,14 @@ class NatureConvs:
         if missing & {"wp1", "wp2", "wp3", "wpd3"}:
             native.nature_pack_weights(w1, w2, w3, pick("wp1", self.wp1), pick("wp2", self.wp2), pick("wp3", self.wp3),
                                        None, pick("wpd3", self.wpd3))
-        if missing & {"wpd2", "q1", "q2", "q3", "qd2", "qd3", "qfcf", "qfcd"}:
+        if missing & {"wpd2", "q1", "q2", "q3", "qd2", "qd3", "qfcf", "qfcd", "qhf", "qhd"}:
             q = self.q
             qfc = self.qfc or (None, None)
+            qh = self.qh or (None, None)
             native.nature_pack_all(w1, w2, w3, self.fc.weight, pick("wpd2", self.wpd2), pick("q1", q[1]),
                                    pick("q2", q[2]), pick("q3", q[3]), pick("qd2", q[12]), pick("qd3", q[13]),
-                                   pick("qfcf", qfc[0]), pick("qfcd", qfc[1]))
+                                   pick("qfcf", qfc[0]), pick("qfcd", qfc[1]), self.hid.weight, pick("qhf", qh[0]),
+                                   pick("qhd", qh[1]))
         if "wfc_nhwc" in missing:
             torch.index_select(self.fc.weight.detach(), 1, self.fc_perm, out=self.wfc_nhwc)
         self._packed |= missing
@@ -326,9 +343,9 @@ class NatureConvs:
                 ws = torch.empty(max(native.nature_fc_fwd_splitk_workspace_bytes(B), 16), dtype=torch.uint8,
                                  device=h3.device)
                 self._ws[("fc_sk", B)] = ws
-            native.nature_fc_fwd_splitk(h3, B, self.qfc[0], self.fc.bias, ws, f, amax_h3=am[AM_H3])
+            native.nature_fc_fwd_splitk(h3, B, self.qfc[0], self.fc.bias, ws, f, amax_h3=am[AM_H3], amax_f=am[AM_F])
         else:
-            native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f, amax_h3=am[AM_H3])
+            native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f, amax_h3=am[AM_H3], amax_f=am[AM_F])
         return f
 
     def fc_dgrad_g3(self, df, h3, am):

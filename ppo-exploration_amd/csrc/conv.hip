@@ -365,7 +365,9 @@ __device__ inline void pack_frag_unit(const Src& src, float s, uint16_t* __restr
 //             goes to g3[m][p][c] (NHWC) times (h3 > 0) — the trunk's ReLU backward and
 //             NCHW -> NHWC transpose fused (replaces the dh3 round trip + nchw_to_nhwc_mask)
 // ---------------------------------------------------------------------------
-enum { FC_FWD = 0, FC_DGRAD = 1 };
+//   HEAD_DGRAD: the 512-wide hidden head layer's input grad, accumulated and masked in place:
+//             y (= df) <- (f > 0) ? y + acc : 0  (the grads of the heads before it already in y)
+enum { FC_FWD = 0, FC_DGRAD = 1, HEAD_DGRAD = 2 };
 // The split fc kernels run in NHWC feature order: feature f = p * 64 + c of the conv3 output
 // (the layout conv3's split forward writes, 128-B channel runs) is the reference's Flatten
 // feature c * 49 + p of Linear(3136, 512) — the weights are packed through this permutation,
@@ -415,22 +417,32 @@ struct GemmRowsProblem {
     __device__ static int nchunk(const Tile&) { return KC; }
     __device__ static int bchunk_id(const Tile& t, int c) { return t.cb * KC + c; }
     // branch-free (clamped indices), so an epilogue can issue all its loads before any wait
-    __device__ static float prefetch(const Args& a, const Tile& t, int row, int col) {
+    // (HEAD_DGRAD: the mask and the accumulated grad)
+    __device__ static auto prefetch(const Args& a, const Tile& t, int row, int col) {
         const int n = t.cb * NB + col, nc = n < N ? n : N - 1;
-        if constexpr (MODE == FC_FWD) {
+        long long m = t.m0 + row;
+        m = m < t.M ? m : t.m0;
+        if constexpr (MODE == FC_FWD)
             return a.bias[nc];
-        } else {
-            long long m = t.m0 + row;
-            m = m < t.M ? m : t.m0;
+        else if constexpr (MODE == FC_DGRAD)
             return a.mask[m * N + nc];
-        }
+        else
+            return make_float2(a.mask[m * N + nc], a.y[m * N + nc]);
     }
-    __device__ static float store_pre(const Args& a, const Tile& t, int row, int col, float acc, float e) {
+    template <class Pre>
+    __device__ static float store_pre(const Args& a, const Tile& t, int row, int col, float acc, Pre e) {
         const long long m = t.m0 + row;
         const int n = t.cb * NB + col;
         if (m >= t.M || n >= N) return 0.f;
-        // FC_FWD: relu(acc + bias); FC_DGRAD: g3 (NHWC) times the ReLU mask of h3 (NHWC), the same index
-        const float v = MODE == FC_FWD ? fmaxf(acc + e, 0.f) : (e > 0.f ? acc : 0.f);
+        // FC_FWD: relu(acc + bias); FC_DGRAD: g3 (NHWC) times the ReLU mask of h3 (NHWC), the same
+        // index; HEAD_DGRAD: (accumulated grad + acc) times the ReLU mask of f
+        float v;
+        if constexpr (MODE == FC_FWD)
+            v = fmaxf(acc + e, 0.f);
+        else if constexpr (MODE == FC_DGRAD)
+            v = e > 0.f ? acc : 0.f;
+        else
+            v = e.x > 0.f ? e.y + acc : 0.f;
         a.y[m * N + n] = v;
         return v;
     }
@@ -447,6 +459,9 @@ struct GemmRowsProblem {
 #endif
 using FcFwd = GemmRowsProblem<3136, 512, FC_NB, FC_FWD>;
 using FcDgrad = GemmRowsProblem<512, 3136, FC_NB, FC_DGRAD>;
+// the heads' hidden layer Linear(512, 512) + ReLU (models-checkpoint.py:62-66 extra_layer)
+using HeadFwd = GemmRowsProblem<512, 512, FC_NB, FC_FWD>;
+using HeadDgrad = GemmRowsProblem<512, 512, FC_NB, HEAD_DGRAD>;
 static_assert(FC_NB == 64, "sg2 runs the fc layer in 64-column blocks");
 
 // ---------------------------------------------------------------------------
@@ -879,7 +894,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
     float om = 0.f;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-        f32x16 e;
+        decltype(Prob::prefetch(a, t, 0, 0)) e[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) e[q] = Prob::prefetch(a, t, wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, j * 32 + r);
         // one wait for all of them (a real s_waitcnt the compiler tracks): the row-bounded
@@ -1026,23 +1041,30 @@ struct SgRowsSK : GemmRowsProblem<K, N, 64, FC_FWD> {
     }
 };
 
+// am (nullable): f's amax slots (the heads' split hidden layer reads f)
 template <int N, int S>
 __global__ void __launch_bounds__(256) fc_fwd_sk_reduce(const float4* __restrict__ slab, long long M,
-                                                         const float* __restrict__ bias, float4* __restrict__ y) {
+                                                         const float* __restrict__ bias, float4* __restrict__ y,
+                                                         uint32_t* __restrict__ am) {
     const long long i = blockIdx.x * 256LL + threadIdx.x, n4 = M * N / 4;
-    if (i >= n4) return;
-    float4 s = slab[i];
+    float m = 0.f;
+    if (i < n4) {
+        float4 s = slab[i];
 #pragma unroll
-    for (int k = 1; k < S; ++k) {
-        const float4 v = slab[k * n4 + i];
-        s.x += v.x;
-        s.y += v.y;
-        s.z += v.z;
-        s.w += v.w;
+        for (int k = 1; k < S; ++k) {
+            const float4 v = slab[k * n4 + i];
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        const int n = (int)((i * 4) % N);
+        const float4 o = make_float4(fmaxf(s.x + bias[n], 0.f), fmaxf(s.y + bias[n + 1], 0.f),
+                                     fmaxf(s.z + bias[n + 2], 0.f), fmaxf(s.w + bias[n + 3], 0.f));
+        y[i] = o;
+        m = fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w));
     }
-    const int n = (int)((i * 4) % N);
-    y[i] = make_float4(fmaxf(s.x + bias[n], 0.f), fmaxf(s.y + bias[n + 1], 0.f), fmaxf(s.z + bias[n + 2], 0.f),
-                       fmaxf(s.w + bias[n + 3], 0.f));
+    amax_record(am, m);
 }
 
 // K-splits for a batch: enough (row tile, column block, split) workgroups for two per CU, at most 8
@@ -1057,11 +1079,12 @@ template <int S>
 int launch_fc_fwd_sk(const Args& a, const uint16_t* q, float* slab, const float* bias, float* f, hipStream_t st) {
     Args b = a;
     b.y = slab;
+    b.amax_y = nullptr;  // partial products: f's amax is recorded by the reduce
     const int rc = launch_sgemm<SgRowsSK<3136, 512, S>>(b, q, ppox::ceil_div(a.batch, SG_ROWS) * FcFwd::NCB * S, st,
                                                         "ppox_nature_fc_fwd_splitk");
     if (rc != PPOX_OK) return rc;
     fc_fwd_sk_reduce<512, S><<<ppox::ceil_div(a.batch * 512 / 4, 256), 256, 0, st>>>(
-        reinterpret_cast<const float4*>(slab), a.batch, bias, reinterpret_cast<float4*>(f));
+        reinterpret_cast<const float4*>(slab), a.batch, bias, reinterpret_cast<float4*>(f), a.amax_y);
     PPOX_LAUNCHED("ppox_nature_fc_fwd_splitk");
 }
 
@@ -1963,15 +1986,18 @@ struct PackAll {
     const float *w1, *w2, *w3, *wfc;
     float* wpd2;                                       // f32 dgrad2 [(tap, co)][ci]
     uint16_t *q1, *q2, *q3, *qd2, *qd3, *qfcf, *qfcd;  // split planes
+    const float* wh = nullptr;                         // the heads' hidden layer (512 x 512)
+    uint16_t *qhf = nullptr, *qhd = nullptr;           // its forward (W^T) and dgrad (W) forms
 };
 constexpr long long PA_N1 = 8 * 2 * 64 * 8, PA_N2 = (long long)G2::K * G2::COUT, PA_N3 = (long long)G3::K * G3::COUT;
 constexpr long long PA_NFC = (long long)FcFwd::NCB * FcFwd::K * FcFwd::NOUT;
 constexpr long long PA_NFCD = (long long)FcDgrad::NCB * FcDgrad::K * FcDgrad::NOUT;
 // the split-GEMM jobs run in 8-element units (pack_frag_unit); q1 and wpd2 per element
 constexpr long long PU_2 = PA_N2 / 8, PU_3 = PA_N3 / 8, PU_FC = PA_NFC / 8, PU_FCD = PA_NFCD / 8;
+constexpr long long PA_NH = (long long)HeadFwd::NCB * HeadFwd::K * HeadFwd::NOUT, PU_H = PA_NH / 8;
 // planes (uint16) of each packed form; a buffer is planes + 2 * PACK_TAIL32 uint16
 constexpr long long PL_Q1 = FWD1_PACK, PL_Q2 = NPL * PA_N2, PL_Q3 = NPL * PA_N3, PL_FCF = NPL * PA_NFC,
-                    PL_FCD = NPL * PA_NFCD;
+                    PL_FCD = NPL * PA_NFCD, PL_H = NPL * PA_NH;
 static_assert(PL_FCF == PL_FCD, "fc forms: one size");
 
 // source value (k, col) of layer L's forward [K][COUT] (NHWC K order) or dgrad [(tap, co)][ci]
@@ -1994,22 +2020,23 @@ struct ConvSrc {
     }
 };
 // source value (k, col) of column block cb of a GemmRows B (w[n][k] when TRANS, w[k][n] otherwise);
-// the fc's 3136-wide side (K of the forward, N of the dgrad) is taken in NHWC feature order
-template <class Prob, bool TRANS>
+// PERM (the fc layer): its 3136-wide side (K of the forward, N of the dgrad) in NHWC feature order
+template <class Prob, bool TRANS, bool PERM>
 struct RowsSrc {
     const float* w;
     int cb;
     __device__ float operator()(int k, int col) const {
         const int n = cb * Prob::NOUT + col;
         if (n >= Prob::N) return 0.f;
-        return TRANS ? w[(long long)n * Prob::K + fc_nchw_feature(k)] : w[(long long)k * Prob::N + fc_nchw_feature(n)];
+        const int f = PERM ? fc_nchw_feature(TRANS ? k : n) : (TRANS ? k : n);
+        return TRANS ? w[(long long)n * Prob::K + f] : w[(long long)k * Prob::N + f];
     }
 };
-template <class Prob, bool TRANS>
+template <class Prob, bool TRANS, bool PERM = true>
 __device__ inline void pack_rows_unit(const float* w, float s, uint16_t* q, long long u) {
     constexpr long long per = (long long)Prob::K * Prob::NOUT / 8;
     const int cb = (int)(u / per);
-    pack_frag_unit<Prob::NOUT>(RowsSrc<Prob, TRANS>{w, cb}, s, q + (long long)cb * Prob::K * Prob::NOUT * NPL,
+    pack_frag_unit<Prob::NOUT>(RowsSrc<Prob, TRANS, PERM>{w, cb}, s, q + (long long)cb * Prob::K * Prob::NOUT * NPL,
                                u - cb * per);
 }
 
@@ -2019,39 +2046,45 @@ __device__ inline void pa_forms(const PackAll& p, int t, uint16_t* (&f)[2], long
         case 0: f[0] = p.q1; f[1] = nullptr; planes = PL_Q1; break;
         case 1: f[0] = p.q2; f[1] = p.qd2; planes = PL_Q2; break;
         case 2: f[0] = p.q3; f[1] = p.qd3; planes = PL_Q3; break;
-        default: f[0] = p.qfcf; f[1] = p.qfcd; planes = PL_FCF; break;
+        case 3: f[0] = p.qfcf; f[1] = p.qfcd; planes = PL_FCF; break;
+        default: f[0] = p.qhf; f[1] = p.qhd; planes = PL_H; break;
     }
 }
+constexpr int PA_TENSORS = 5;
 
-// 64 workgroups per weight tensor: workgroup b's max |w| over its stride into slot 4b of the
-// tails of both forms (slots 4b+1..4b+3 zeroed), so the packer's amax_read sees the tensor max
-constexpr int WMAX_WG = 64;
+// AMAX_SLOTS workgroups per weight tensor: workgroup b's max |w| over its stride into slot b of
+// the tails of both forms (every slot written: no zeroing), so the packer's amax_read sees the
+// tensor's max
 __global__ void __launch_bounds__(256) wmax_kernel(PackAll p) {
-    const int t = blockIdx.x / WMAX_WG, b = blockIdx.x % WMAX_WG;
+    const int t = blockIdx.x / AMAX_SLOTS, b = blockIdx.x % AMAX_SLOTS;
     uint16_t* f[2];
     long long planes;
     pa_forms(p, t, f, planes);
     if (!f[0] && !f[1]) return;
-    const float* w = t == 0 ? p.w1 : t == 1 ? p.w2 : t == 2 ? p.w3 : p.wfc;
-    const long long n = t == 0 ? (long long)G1::K * G1::COUT : t == 1 ? PA_N2 : t == 2 ? PA_N3 : 512LL * 3136;
+    const float4* w = reinterpret_cast<const float4*>(t == 0 ? p.w1 : t == 1 ? p.w2 : t == 2 ? p.w3 : t == 3 ? p.wfc : p.wh);
+    const long long n4 =
+        (t == 0 ? (long long)G1::K * G1::COUT : t == 1 ? PA_N2 : t == 2 ? PA_N3 : t == 3 ? 512LL * 3136 : PA_NH) / 4;
     float m = 0.f;
-    for (long long i = (long long)b * 256 + threadIdx.x; i < n; i += WMAX_WG * 256) m = fmaxf(m, fabsf(w[i]));
+    for (long long i = (long long)b * 256 + threadIdx.x; i < n4; i += AMAX_SLOTS * 256) {
+        const float4 v = w[i];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
     __shared__ uint32_t red[4];
     const uint32_t wm = wave_max_u32(__float_as_uint(m));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wm;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint4 v = {max(max(red[0], red[1]), max(red[2], red[3])), 0u, 0u, 0u};
+        const uint32_t v = max(max(red[0], red[1]), max(red[2], red[3]));
         for (int k = 0; k < 2; ++k)
-            if (f[k]) reinterpret_cast<uint4*>(pack_tail(f[k], planes))[b] = v;
+            if (f[k]) pack_tail(f[k], planes)[b] = v;
     }
 }
 
 __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long total) {
-    // the four tensors' scales (wave-uniform), from the partials of their first packed form
-    float sc[4];
+    // the tensors' scales (wave-uniform), from the partials of their first packed form
+    float sc[PA_TENSORS];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < PA_TENSORS; ++t) {
         uint16_t* f[2];
         long long planes;
         pa_forms(p, t, f, planes);
@@ -2078,7 +2111,11 @@ __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long tota
         j -= PA_N2;
         if (j < PU_FC) { if (p.qfcf) pack_rows_unit<FcFwd, true>(p.wfc, sc[3], p.qfcf, j); continue; }
         j -= PU_FC;
-        if (p.qfcd) pack_rows_unit<FcDgrad, false>(p.wfc, sc[3], p.qfcd, j);
+        if (j < PU_FCD) { if (p.qfcd) pack_rows_unit<FcDgrad, false>(p.wfc, sc[3], p.qfcd, j); continue; }
+        j -= PU_FCD;
+        if (j < PU_H) { if (p.qhf) pack_rows_unit<HeadFwd, true, false>(p.wh, sc[4], p.qhf, j); continue; }
+        j -= PU_H;
+        if (p.qhd) pack_rows_unit<HeadDgrad, false, false>(p.wh, sc[4], p.qhd, j);
     }
 }
 
@@ -2087,11 +2124,15 @@ int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
                           (const void*)p.qd2, (const void*)p.qd3, (const void*)p.qfcf, (const void*)p.qfcd})
         PPOX_REQUIRE(!q || ppox::aligned16(q), "ppox_nature_pack: packed buffers must be 16-byte aligned");
     PPOX_REQUIRE((p.w1 || !p.q1) && (p.w2 || (!p.q2 && !p.qd2 && !p.wpd2)) && (p.w3 || (!p.q3 && !p.qd3)) &&
-                     (p.wfc || (!p.qfcf && !p.qfcd)),
+                     (p.wfc || (!p.qfcf && !p.qfcd)) && (p.wh || (!p.qhf && !p.qhd)),
                  "ppox_nature_pack: null weights");
-    wmax_kernel<<<4 * WMAX_WG, 256, 0, s>>>(p);
+    PPOX_REQUIRE((!p.qhf || ppox::aligned16(p.qhf)) && (!p.qhd || ppox::aligned16(p.qhd)),
+                 "ppox_nature_pack: packed buffers must be 16-byte aligned");
+    wmax_kernel<<<PA_TENSORS * AMAX_SLOTS, 256, 0, s>>>(p);
     PPOX_LAUNCHED_NORET(name);
-    const long long total = PA_N1 + 2 * PU_2 + 2 * PU_3 + PA_N2 + PU_FC + (p.qfcd ? PU_FCD : 0);
+    // element ranges end at the last job present (the head and fc dgrad ranges are the longest)
+    const long long total = PA_N1 + 2 * PU_2 + 2 * PU_3 + PA_N2 + PU_FC +
+                            (p.qhf || p.qhd ? PU_FCD + 2 * PU_H : (p.qfcd ? PU_FCD : 0));
     const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 4096);
     pack_all_kernel<<<blocks, 256, 0, s>>>(p, total);
     PPOX_LAUNCHED(name);
@@ -2346,16 +2387,17 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
 // which writes dW in the Flatten order of the fc weight.
 using GFc = Geo<512, 1, 1, 1, 1, 1, 64>;
 constexpr int FCW_KT = 128, FCW_CB = 49;
-struct FcWgrad {
+template <int CB, int MAXS>
+struct RowsWgrad {
     using C = WsCfg<GFc, false, FCW_KT>;
-    static constexpr long long TILES = (long long)C::KB * FCW_CB;
-    static constexpr long long SLAB = (long long)GFc::K * FCW_CB * GFc::COUT;  // floats per split
+    static constexpr long long TILES = (long long)C::KB * CB;
+    static constexpr long long SLAB = (long long)GFc::K * CB * GFc::COUT;  // floats per split
     // the split count whose (rounds of 512 workgroup slots) x (steps per split + 3 of fixed
-    // prologue / epilogue cost) is least: 13 at B = 16384 (4.98 rounds), 5 at B = 2048
+    // prologue / epilogue cost) is least: 13 at B = 16384 (4.98 rounds), 5 at B = 2048 (fc)
     static int splits(long long batch) {
         int best = 1;
         long long best_cost = -1;
-        for (int sp = 1; sp <= 16; ++sp) {
+        for (int sp = 1; sp <= MAXS; ++sp) {
             const long long steps = ppox::ceil_div(ppox::ceil_div(batch, (long long)sp), (long long)MS);
             if (sp > 1 && steps < 2) break;
             const long long cost = ppox::ceil_div(TILES * sp, 512LL) * (steps + 3);
@@ -2368,25 +2410,37 @@ struct FcWgrad {
     }
     static long long workspace_bytes(long long batch) { return splits(batch) * SLAB * (long long)sizeof(float); }
 };
+using FcWgrad = RowsWgrad<FCW_CB, 16>;
+using HeadWgrad = RowsWgrad<512 / 64, 128>;  // the heads' hidden layer: G = f in 8 column blocks
 
-__global__ void __launch_bounds__(256) fc_wgrad_reduce(const float* __restrict__ slab, int splits,
-                                                       float* __restrict__ dw) {
-    const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;  // 4 slab elements (o, NHWC feature)
-    if (i >= FcWgrad::SLAB) return;
+// slabs [splits][512][N] summed in split order; PERM: the fc's NHWC features -> Flatten order
+template <int N, bool PERM>
+__global__ void __launch_bounds__(256) rows_wgrad_reduce(const float* __restrict__ slab, int splits,
+                                                         float* __restrict__ dw) {
+    constexpr long long SL = 512LL * N;
+    const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;  // 4 slab elements (o, feature)
+    if (i >= SL) return;
     float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int sp = 0; sp < splits; ++sp) {
-        const float4 v = *reinterpret_cast<const float4*>(slab + sp * FcWgrad::SLAB + i);
+        const float4 v = *reinterpret_cast<const float4*>(slab + sp * SL + i);
         t.x += v.x;
         t.y += v.y;
         t.z += v.z;
         t.w += v.w;
     }
-    const int o = (int)(i / 3136), f = (int)(i - (long long)o * 3136);  // 3136 % 4 == 0: one row
-    float* row = dw + (long long)o * 3136;
-    row[fc_nchw_feature(f)] = t.x;
-    row[fc_nchw_feature(f + 1)] = t.y;
-    row[fc_nchw_feature(f + 2)] = t.z;
-    row[fc_nchw_feature(f + 3)] = t.w;
+    if constexpr (PERM) {
+        const int o = (int)(i / N), f = (int)(i - (long long)o * N);  // N % 4 == 0: one row
+        float* row = dw + (long long)o * N;
+        row[fc_nchw_feature(f)] = t.x;
+        row[fc_nchw_feature(f + 1)] = t.y;
+        row[fc_nchw_feature(f + 2)] = t.z;
+        row[fc_nchw_feature(f + 3)] = t.w;
+    } else {  // dw may be a 4-B aligned view (a parameter's grad in the flat buffer)
+        dw[i] = t.x;
+        dw[i + 1] = t.y;
+        dw[i + 2] = t.z;
+        dw[i + 3] = t.w;
+    }
 }
 
 extern "C" int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch) {
@@ -2414,7 +2468,7 @@ extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float*
     wa.px_per_split = ppox::ceil_div(ppox::ceil_div((long long)batch, (long long)sp), (long long)MS) * MS;
     wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB><<<(unsigned)(FcWgrad::TILES * sp), 256, 0, s>>>(wa);
     PPOX_LAUNCHED_NORET("ppox_nature_fc_wgrad");
-    fc_wgrad_reduce<<<(unsigned)ppox::ceil_div(FcWgrad::SLAB, 1024LL), 256, 0, s>>>(slab, sp, dw);
+    rows_wgrad_reduce<3136, true><<<(unsigned)ppox::ceil_div(FcWgrad::SLAB, 1024LL), 256, 0, s>>>(slab, sp, dw);
     PPOX_LAUNCHED("ppox_nature_fc_wgrad");
 }
 
@@ -2428,12 +2482,12 @@ extern "C" int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_
 }
 
 extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
-                                  const uint32_t* amax_h3, void* stream) {
+                                  const uint32_t* amax_h3, uint32_t* amax_f, void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(h3 && q_fwd && bias && f && amax_h3 && batch >= 0, "ppox_nature_fc_fwd: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd) && ppox::aligned16(amax_h3),
                  "ppox_nature_fc_fwd: 16B alignment");
-    Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, amax_h3, nullptr, pack_exp(q_fwd, PL_FCF)};
+    Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, amax_h3, amax_f, pack_exp(q_fwd, PL_FCF)};
     return launch_sgemm<SgRows<3136, 512, FC_FWD, FC_FWD_G>>(a, q_fwd, ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB,
                                                    ppox::as_stream(stream), "ppox_nature_fc_fwd");
 }
@@ -2444,7 +2498,7 @@ extern "C" int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch) {
 
 extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias,
                                          void* workspace, int64_t workspace_bytes, float* f, const uint32_t* amax_h3,
-                                         void* stream) {
+                                         uint32_t* amax_f, void* stream) {
     if (batch == 0) return PPOX_OK;
     PPOX_REQUIRE(h3 && q_fwd && bias && f && workspace && amax_h3 && batch > 0,
                  "ppox_nature_fc_fwd_splitk: bad arguments");
@@ -2453,7 +2507,7 @@ extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const u
                  "ppox_nature_fc_fwd_splitk: 16B alignment");
     PPOX_REQUIRE(workspace_bytes >= ppox_nature_fc_fwd_splitk_workspace_bytes(batch),
                  "ppox_nature_fc_fwd_splitk: workspace too small");
-    Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, amax_h3, nullptr, pack_exp(q_fwd, PL_FCF)};
+    Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, amax_h3, amax_f, pack_exp(q_fwd, PL_FCF)};
     float* slab = reinterpret_cast<float*>(workspace);
     hipStream_t st = ppox::as_stream(stream);
     switch (fc_fwd_splits(batch)) {
@@ -2477,10 +2531,66 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
 
 extern "C" int ppox_nature_pack_all(const float* w1, const float* w2, const float* w3, const float* wfc, float* wpd2,
                                     uint16_t* q1, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
-                                    uint16_t* qfc_fwd, uint16_t* qfc_dgrad, void* stream) {
+                                    uint16_t* qfc_fwd, uint16_t* qfc_dgrad, const float* wh, uint16_t* qh_fwd,
+                                    uint16_t* qh_dgrad, void* stream) {
     PPOX_REQUIRE(w1 && w2 && w3 && (wfc || (!qfc_fwd && !qfc_dgrad)), "ppox_nature_pack_all: null weights");
-    return launch_pack_all(PackAll{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad},
-                           ppox::as_stream(stream), "ppox_nature_pack_all");
+    return launch_pack_all(
+        PackAll{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh, qh_fwd, qh_dgrad},
+        ppox::as_stream(stream), "ppox_nature_pack_all");
+}
+
+// ---- the heads' hidden layer Linear(512, 512) + ReLU on the split-f16 GEMM -------------
+extern "C" int64_t ppox_head_hidden_pack_elems(void) { return PL_H + 2 * PACK_TAIL32; }
+
+extern "C" int ppox_head_hidden_fwd(const float* f, int64_t rows, const uint16_t* q_fwd, const float* bias, float* e,
+                                    const uint32_t* amax_f, void* stream) {
+    if (rows == 0) return PPOX_OK;
+    PPOX_REQUIRE(f && q_fwd && bias && e && amax_f && rows > 0, "ppox_head_hidden_fwd: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(f) && ppox::aligned16(q_fwd) && ppox::aligned16(amax_f),
+                 "ppox_head_hidden_fwd: 16B alignment");
+    Args a{f, nullptr, 0, 0, 0, nullptr, bias, nullptr, e, rows, amax_f, nullptr, pack_exp(q_fwd, PL_H)};
+    return launch_sgemm<SgRows<512, 512, FC_FWD, 8>>(a, q_fwd, ppox::ceil_div(rows, SG_ROWS) * HeadFwd::NCB,
+                                                      ppox::as_stream(stream), "ppox_head_hidden_fwd");
+}
+
+extern "C" int ppox_head_hidden_dgrad(const float* de, int64_t rows, const uint16_t* q_dgrad, const float* f, float* df,
+                                      const uint32_t* amax_de, uint32_t* amax_df, void* stream) {
+    if (rows == 0) return PPOX_OK;
+    PPOX_REQUIRE(de && q_dgrad && f && df && amax_de && rows > 0, "ppox_head_hidden_dgrad: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(de) && ppox::aligned16(q_dgrad) && ppox::aligned16(amax_de),
+                 "ppox_head_hidden_dgrad: 16B alignment");
+    Args a{de, nullptr, 0, 0, 0, nullptr, nullptr, f, df, rows, amax_de, amax_df, pack_exp(q_dgrad, PL_H)};
+    return launch_sgemm<SgRows<512, 512, HEAD_DGRAD, 8>>(a, q_dgrad, ppox::ceil_div(rows, SG_ROWS) * HeadDgrad::NCB,
+                                                          ppox::as_stream(stream), "ppox_head_hidden_dgrad");
+}
+
+extern "C" int64_t ppox_head_hidden_wgrad_workspace_bytes(int64_t rows) {
+    return rows <= 0 ? 0 : HeadWgrad::workspace_bytes(rows);
+}
+
+extern "C" int ppox_head_hidden_wgrad(const float* de, int64_t rows, const float* f, void* workspace,
+                                      int64_t workspace_bytes, float* dw, const uint32_t* amax_de,
+                                      const uint32_t* amax_f, void* stream) {
+    PPOX_REQUIRE(dw && rows >= 0, "ppox_head_hidden_wgrad: bad arguments");
+    hipStream_t s = ppox::as_stream(stream);
+    if (rows == 0) {  // no rows: a zero gradient
+        PPOX_REQUIRE(hipMemsetAsync(dw, 0, sizeof(float) * HeadWgrad::SLAB, s) == hipSuccess,
+                     "ppox_head_hidden_wgrad: memset failed");
+        return PPOX_OK;
+    }
+    PPOX_REQUIRE(de && f && workspace && amax_de && amax_f, "ppox_head_hidden_wgrad: bad arguments");
+    PPOX_REQUIRE(workspace_bytes >= HeadWgrad::workspace_bytes(rows), "ppox_head_hidden_wgrad: workspace too small");
+    PPOX_REQUIRE(ppox::aligned16(de) && ppox::aligned16(f) && ppox::aligned16(amax_de) && ppox::aligned16(amax_f),
+                 "ppox_head_hidden_wgrad: 16B alignment");
+    PPOX_REQUIRE(rows < (1LL << 31) / 64, "ppox_head_hidden_wgrad: too many rows for 32-bit row indexing");
+    const int sp = HeadWgrad::splits(rows);
+    float* slab = reinterpret_cast<float*>(workspace);
+    WArgs wa{de, 0, f, slab, nullptr, rows, 0, sp, nullptr, 0, 0, amax_de, amax_f};
+    wa.px_per_split = ppox::ceil_div(ppox::ceil_div((long long)rows, (long long)sp), (long long)MS) * MS;
+    wgrad_split_kernel<GFc, false, FCW_KT, false, 512 / 64><<<(unsigned)(HeadWgrad::TILES * sp), 256, 0, s>>>(wa);
+    PPOX_LAUNCHED_NORET("ppox_head_hidden_wgrad");
+    rows_wgrad_reduce<512, false><<<(unsigned)ppox::ceil_div(HeadWgrad::SLAB, 1024LL), 256, 0, s>>>(slab, sp, dw);
+    PPOX_LAUNCHED("ppox_head_hidden_wgrad");
 }
 
 // ---- amax slots (split-f16 operand scales) -------------------------------------------

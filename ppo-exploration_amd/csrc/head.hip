@@ -211,10 +211,12 @@ __global__ void __launch_bounds__(256) skinny_dgrad_kernel(const float* __restri
     }
 }
 
+// am (nullable): d's amax slots (the split hidden layer's dgrad / weight gradient read d)
 __global__ void __launch_bounds__(256) outer_relu_kernel(const float* __restrict__ dv, const float* __restrict__ w,
                                                          const float* __restrict__ act, long long rows, int h4,
-                                                         float* __restrict__ d) {
+                                                         float* __restrict__ d, uint32_t* __restrict__ am) {
     const long long n4 = rows * h4;
+    float m = 0.f;
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
         const long long b = i / h4;
         const int j = (int)(i - b * h4);
@@ -227,7 +229,9 @@ __global__ void __launch_bounds__(256) outer_relu_kernel(const float* __restrict
         o.z = a.z > 0.f ? s * ww.z : 0.f;
         o.w = a.w > 0.f ? s * ww.w : 0.f;
         reinterpret_cast<float4*>(d)[i] = o;
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
     }
+    amax_record(am, m);
 }
 
 unsigned grid_for(long long n4) {
@@ -322,11 +326,12 @@ extern "C" int ppox_skinny_dgrad(const float* g, const float* w, int64_t rows, i
 }
 
 extern "C" int ppox_outer_relu_backward(const float* dv, const float* w, const float* act, int64_t rows, int64_t h,
-                                        float* out, void* stream) {
+                                        float* out, uint32_t* amax, void* stream) {
     if (rows == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(dv && w && act && out && rows >= 0 && h > 0 && h % 4 == 0, "ppox_outer_relu_backward: bad arguments");
-    PPOX_REQUIRE(ppox::aligned16(act) && ppox::aligned16(out),
+    PPOX_REQUIRE(ppox::aligned16(act) && ppox::aligned16(out) && (!amax || ppox::aligned16(amax)),
                  "ppox_outer_relu_backward: 16B alignment");
-    outer_relu_kernel<<<grid_for(rows * h / 4), 256, 0, ppox::as_stream(stream)>>>(dv, w, act, rows, (int)(h / 4), out);
+    outer_relu_kernel<<<grid_for(rows * h / 4), 256, 0, ppox::as_stream(stream)>>>(dv, w, act, rows, (int)(h / 4), out,
+                                                                                 amax);
     PPOX_LAUNCHED("ppox_outer_relu_backward");
 }

@@ -15,6 +15,7 @@ consumption), then re-homed into the flat device buffers.
 The NatureCNN convolutions run on the libppox MFMA implicit-GEMM kernels when
 available (see convs.py); the small linear layers use PyTorch-ROCm (rocBLAS).
 """
+import contextlib
 import math
 
 import numpy as np
@@ -104,10 +105,14 @@ class CnnActorCritic(nn.Module):
         self.conv_impl = None  # set by convs.attach()
 
     def trunk(self, x):
+        return self._trunk_am(x)[0]
+
+    def _trunk_am(self, x):
+        """(f, the pass's amax table or None)"""
         if self.conv_impl is not None and self.conv_impl.math != "f32" and not torch.is_grad_enabled():
-            # inference (collect): the split-bf16 fc GEMM straight off the conv trunk
+            # inference (collect): the split-f16 fc GEMM straight off the conv trunk
             h1, h2, h3, am = self.conv_impl.forward_acts(x.contiguous())
-            return self.conv_impl.fc_forward(h3, am)
+            return self.conv_impl.fc_forward(h3, am), am
         if self.conv_impl is not None:
             h = self.conv_impl(x)
         else:
@@ -116,12 +121,12 @@ class CnnActorCritic(nn.Module):
             h = F.relu(fe[2](h))
             h = F.relu(fe[4](h))
         fc = self.feature_extractor[7]
-        return F.relu(F.linear(h.flatten(1), fc.weight, fc.bias))
+        return F.relu(F.linear(h.flatten(1), fc.weight, fc.bias)), None
 
     def forward(self, x):
-        f = self.trunk(x)
+        f, am = self._trunk_am(x)
         if not torch.is_grad_enabled():  # collect: the same head kernels as forward_train
-            return self._heads(f)[:3]
+            return self._heads(f, am)[:3]
         v = self.critic_ext(self.extra_layer(f)).squeeze(-1)
         iv = self.critic_int(self.int_extra_layer(f)).squeeze(-1) if self.intrinsic else None
         return self.actor(f), v, iv
@@ -142,15 +147,23 @@ class CnnActorCritic(nn.Module):
                 f = self.conv_impl.fc_forward(h3, am)
             else:
                 f = linear_relu(hf, fc.weight, fc.bias)
-            out, v, iv, e, ie = self._heads(f)
+            out, v, iv, e, ie = self._heads(f, am)
         return out, v, iv, (x, h1, h2, h3, f, e, ie, am)
 
-    def _heads(self, f):
+    def _heads(self, f, am=None):
         """actor logits, value, int value, and the hidden activations (no autograd): fused
-        bias+ReLU GEMMs for the 512-wide layers, skinny-row kernels for the narrow heads."""
+        bias+ReLU GEMMs for the 512-wide layers (the extra layer on the split-f16 kernel for large
+        batches: f's amax in am), skinny-row kernels for the narrow heads."""
         a, el, ce = self.actor[0], self.extra_layer[0], self.critic_ext
         out = native.head_linear(f, a.weight, a.bias)
-        e = linear_relu(f, el.weight, el.bias)
+        cv = self.conv_impl
+        if am is not None and cv is not None and cv.split_head(f.shape[0]):
+            import convs as _convs
+            cv.pack(f.shape[0])
+            e = torch.empty_like(f)
+            native.head_hidden_fwd(f, cv.qh[0], el.bias, e, amax_f=am[_convs.AM_F])
+        else:
+            e = linear_relu(f, el.weight, el.bias)
         v = native.head_linear(e, ce.weight, ce.bias).squeeze(-1)
         ie = iv = None
         if self.intrinsic:
@@ -181,6 +194,14 @@ class CnnActorCritic(nn.Module):
             self._fcw_ws = ws
         return ws
 
+    def _head_wgrad_ws(self, rows):
+        need = native.head_hidden_wgrad_workspace_bytes(rows)
+        ws = getattr(self, "_hh_ws", None)
+        if ws is None or ws.numel() < need or ws.device != self.actor[0].weight.device:
+            ws = torch.empty(max(need, 16), dtype=torch.uint8, device=self.actor[0].weight.device)
+            self._hh_ws = ws
+        return ws
+
     def _head_ws(self, rows, h, n_actions):
         need = native.head_grads_workspace_bytes(rows, h, n_actions, self.intrinsic)
         ws = getattr(self, "_hg_ws", None)
@@ -206,21 +227,29 @@ class CnnActorCritic(nn.Module):
             import convs as _convs
             side = _convs.side_stream(df.device) if _convs.BWD_STREAMS and df.is_cuda else None
             cur = torch.cuda.current_stream() if side is not None else None
+            cv = self.conv_impl
+            split = cv.split_head(B)  # the extra layer's dgrad / weight gradient on the split-f16 kernels
             des = []
             for hid, crit, act, d in heads:
                 d = d.contiguous().view(B, 1)
                 de = torch.empty_like(act)
-                native.outer_relu_backward(d, crit.weight, act, de)     # dv * w, ReLU backward
-                if side is None:
-                    weight_grad(de, f, hid.weight.grad, self._wgrad_part(hid.weight))
-                else:  # the hidden layer's weight gradient beside the dgrad chain
+                sp = split and hid is self.extra_layer[0]
+                native.outer_relu_backward(d, crit.weight, act, de, amax=am[_convs.AM_DE] if sp else None)  # dv * w, ReLU'
+                if side is not None:  # the hidden layer's weight gradient beside the dgrad chain
                     _convs.fork(side, cur)
-                    with torch.cuda.stream(side):
+                with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                    if sp:
+                        native.head_hidden_wgrad(de, f, self._head_wgrad_ws(B), hid.weight.grad, amax_de=am[_convs.AM_DE],
+                                                 amax_f=am[_convs.AM_F])
+                    else:
                         weight_grad(de, f, hid.weight.grad, self._wgrad_part(hid.weight))
-                df.addmm_(de, hid.weight)
+                if not sp:
+                    df.addmm_(de, hid.weight)
                 des.append((de, d))
-            cv = self.conv_impl
-            native.relu_backward_(df, f, amax=am[_convs.AM_DF] if cv.nhwc3 else None)
+            if split:  # df = (f > 0) ? df + de W : 0, recording df's amax (the fc layer's operand)
+                native.head_hidden_dgrad(des[0][0], cv.qh[1], f, df, amax_de=am[_convs.AM_DE], amax_df=am[_convs.AM_DF])
+            else:
+                native.relu_backward_(df, f, amax=am[_convs.AM_DF] if cv.nhwc3 else None)
             # every column-reduction gradient (actor W/b, critic W/b, extra-layer b, fc b) in one pass
             ws = self._head_ws(B, f.shape[1], dout.shape[1])
             (de, d), intr = des[0], des[1] if self.intrinsic else (None, None)

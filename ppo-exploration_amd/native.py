@@ -71,8 +71,11 @@ SIGNATURES = {
     "ppox_skinny_dgrad": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 11,
     "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
-    "ppox_nature_pack_all": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_pack_all": [_vp] * 16,
+    "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_head_hidden_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp],
+    "ppox_head_hidden_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_head_hidden_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_es_noise": [_i64, _i64, _i64, _i64, _u64, _vp, _vp],
@@ -81,13 +84,13 @@ SIGNATURES = {
     "ppox_es_update": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp],
     "ppox_normalize_obs_f32_ex": [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _f64, _vp, _vp],
     "ppox_vecnorm_reward": [_vp, _vp, _vp, _i64, _f64, _vp, _vp, _f64, _f64, _f64, _i32, _vp],
-    "ppox_outer_relu_backward": [_vp, _vp, _vp, _i64, _i64, _vp, _vp],
+    "ppox_outer_relu_backward": [_vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp],
     "ppox_nature_conv_wgrad_split": [_i32, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_wgrad_split_idx": [_i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
-    "ppox_nature_fc_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
+    "ppox_nature_fc_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_icm_pack_w1": [_vp, _i64, _vp, _vp],
     "ppox_icm_encode": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_icm_pair_backward": [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp],
@@ -105,7 +108,8 @@ _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p
              "ppox_nature_fc_wgrad_workspace_bytes": ctypes.c_int64, "ppox_icm_param_elems": ctypes.c_int64,
              "ppox_icm_w1_pack_elems": ctypes.c_int64, "ppox_icm_encode_workspace_bytes": ctypes.c_int64,
              "ppox_icm_partials_bytes": ctypes.c_int64, "ppox_icm_g1_pack_elems": ctypes.c_int64,
-             "ppox_nature_fc_fwd_splitk_workspace_bytes": ctypes.c_int64, "ppox_amax_slots": ctypes.c_int32}
+             "ppox_nature_fc_fwd_splitk_workspace_bytes": ctypes.c_int64, "ppox_amax_slots": ctypes.c_int32,
+             "ppox_head_hidden_pack_elems": ctypes.c_int64, "ppox_head_hidden_wgrad_workspace_bytes": ctypes.c_int64}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
                  "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32],
                  "ppox_nature_wgrad_split_workspace_bytes": [_i32, _i64],
@@ -114,7 +118,7 @@ _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad
                  "ppox_nature_fc_wgrad_workspace_bytes": [_i64], "ppox_icm_param_elems": [_i32],
                  "ppox_icm_w1_pack_elems": [_i64], "ppox_icm_encode_workspace_bytes": [_i64, _i64],
                  "ppox_icm_partials_bytes": [_i64, _i32], "ppox_icm_g1_pack_elems": [_i64],
-                 "ppox_nature_fc_fwd_splitk_workspace_bytes": [_i64]}
+                 "ppox_nature_fc_fwd_splitk_workspace_bytes": [_i64], "ppox_head_hidden_wgrad_workspace_bytes": [_i64]}
 
 _lib = None
 
@@ -533,29 +537,66 @@ def nature_fc_pack(w, q_fwd, q_dgrad, stream=None):
     call("ppox_nature_fc_pack", _p(w), _p(q_fwd), _p(q_dgrad), stream_ptr(stream))
 
 
-def nature_pack_all(w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, stream=None):
+def nature_pack_all(w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh=None, qh_fwd=None,
+                    qh_dgrad=None, stream=None):
     """Every weight packing of a training step in one launch (None = skip)."""
     call("ppox_nature_pack_all", _p(w1), _p(w2), _p(w3), _p(wfc), _p(wpd2), _p(q1), _p(q2), _p(q3), _p(qd2),
-         _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), stream_ptr(stream))
+         _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), _p(wh), _p(qh_fwd), _p(qh_dgrad), stream_ptr(stream))
 
 
-def nature_fc_fwd(h3, batch, q_fwd, bias, f, amax_h3=None, stream=None):
-    """f = relu(h3 @ W^T + b), h3 (batch, 7, 7, 64) NHWC."""
+def nature_fc_fwd(h3, batch, q_fwd, bias, f, amax_h3=None, amax_f=None, stream=None):
+    """f = relu(h3 @ W^T + b), h3 (batch, 7, 7, 64) NHWC; amax_f: f's slots to record (or None)."""
     if batch:
         amax_h3 = _amax_of(h3, amax_h3, stream)
-    call("ppox_nature_fc_fwd", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(f), _p(amax_h3), stream_ptr(stream))
+    call("ppox_nature_fc_fwd", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(f), _p(amax_h3), _p(amax_f),
+         stream_ptr(stream))
+
+
+# the heads' hidden layer Linear(512, 512) (split-f16 GEMM, csrc/conv.hip; include/ppox.h)
+def head_hidden_pack_elems():
+    return int(load().ppox_head_hidden_pack_elems())
+
+
+def head_hidden_fwd(f, q_fwd, bias, e, amax_f=None, stream=None):
+    """e = relu(f W^T + b) (rows x 512)."""
+    rows = f.shape[0]
+    if rows:
+        amax_f = _amax_of(f, amax_f, stream)
+    call("ppox_head_hidden_fwd", _p(f), rows, _p(q_fwd), _p(bias), _p(e), _p(amax_f), stream_ptr(stream))
+
+
+def head_hidden_dgrad(de, q_dgrad, f, df, amax_de=None, amax_df=None, stream=None):
+    """df = (f > 0) ? df + de W : 0, in place; amax_df: df's slots to record (or None)."""
+    rows = de.shape[0]
+    if rows:
+        amax_de = _amax_of(de, amax_de, stream)
+    call("ppox_head_hidden_dgrad", _p(de), rows, _p(q_dgrad), _p(f), _p(df), _p(amax_de), _p(amax_df),
+         stream_ptr(stream))
+
+
+def head_hidden_wgrad_workspace_bytes(rows):
+    return int(load().ppox_head_hidden_wgrad_workspace_bytes(int(rows)))
+
+
+def head_hidden_wgrad(de, f, workspace, dw, amax_de=None, amax_f=None, stream=None):
+    """dw (512 x 512) = de^T f, deterministic."""
+    rows = de.shape[0]
+    if rows:
+        amax_de, amax_f = _amax_of(de, amax_de, stream), _amax_of(f, amax_f, stream)
+    call("ppox_head_hidden_wgrad", _p(de), rows, _p(f), _p(workspace), workspace.numel() * workspace.element_size(),
+         _p(dw), _p(amax_de), _p(amax_f), stream_ptr(stream))
 
 
 def nature_fc_fwd_splitk_workspace_bytes(batch):
     return int(load().ppox_nature_fc_fwd_splitk_workspace_bytes(int(batch)))
 
 
-def nature_fc_fwd_splitk(h3, batch, q_fwd, bias, workspace, f, amax_h3=None, stream=None):
+def nature_fc_fwd_splitk(h3, batch, q_fwd, bias, workspace, f, amax_h3=None, amax_f=None, stream=None):
     """fc forward split over K (small batches), bias + ReLU in the fixed-order reduce."""
     if batch:
         amax_h3 = _amax_of(h3, amax_h3, stream)
     call("ppox_nature_fc_fwd_splitk", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(workspace),
-         workspace.numel() * workspace.element_size(), _p(f), _p(amax_h3), stream_ptr(stream))
+         workspace.numel() * workspace.element_size(), _p(f), _p(amax_h3), _p(amax_f), stream_ptr(stream))
 
 
 def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, amax_df=None, amax_g3=None, stream=None):
@@ -659,9 +700,10 @@ def head_grads(f, e, dout, dv, de, df, ws, w_actor, b_actor, w_critic, b_critic,
          _p(b_extra), _p(b_fc), _p(w_critic_int), _p(b_critic_int), _p(b_int_extra), stream_ptr(stream))
 
 
-def outer_relu_backward(dv, w, act, out, stream=None):
-    """out[b][j] = dv[b] * w[j] * (act[b][j] > 0)."""
-    call("ppox_outer_relu_backward", _p(dv), _p(w), _p(act), act.shape[0], act.shape[1], _p(out), stream_ptr(stream))
+def outer_relu_backward(dv, w, act, out, amax=None, stream=None):
+    """out[b][j] = dv[b] * w[j] * (act[b][j] > 0); amax: out's slots to record (or None)."""
+    call("ppox_outer_relu_backward", _p(dv), _p(w), _p(act), act.shape[0], act.shape[1], _p(out), _p(amax),
+         stream_ptr(stream))
 
 
 def nature_wgrad_split_workspace_bytes(layer, batch):

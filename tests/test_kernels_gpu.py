@@ -889,6 +889,47 @@ def test_split_f16_any_operand_range(mag):
     assert rel(dw, refw) <= 2 * rel(df.t() @ h3, refw) + 1e-7
 
 
+@pytest.mark.parametrize("B", [1, 70, 2048, 9000])
+def test_head_hidden_split_vs_fp64(B):
+    """The heads' hidden layer Linear(512, 512) on the split-f16 kernels vs float64: forward
+    relu(f W^T + b), the in-place accumulated + ReLU-masked input grad (f > 0) ? df + de W : 0
+    and the weight gradient de^T f — errors no larger than torch's f32 GEMMs' (x2 headroom);
+    the weight gradient bitwise run-to-run, and zero rows give a zero gradient."""
+    import native
+    g = torch.Generator(device="cuda").manual_seed(B)
+    W = torch.randn(512, 512, device="cuda", generator=g) * 0.04
+    bias = torch.randn(512, device="cuda", generator=g) * 0.1
+    f = torch.relu(torch.randn(B, 512, device="cuda", generator=g))
+    de = torch.randn(B, 512, device="cuda", generator=g) * (torch.rand(B, 512, device="cuda", generator=g) > 0.4)
+    df0 = torch.randn(B, 512, device="cuda", generator=g) * 0.1
+    n = native.head_hidden_pack_elems()
+    qf, qd = torch.empty(n, dtype=torch.int16, device="cuda"), torch.empty(n, dtype=torch.int16, device="cuda")
+    w1, w2, w3 = torch.randn(32, 4, 8, 8, device="cuda"), torch.randn(64, 32, 4, 4, device="cuda"), \
+        torch.randn(64, 64, 3, 3, device="cuda")
+    native.nature_pack_all(w1, w2, w3, None, None, None, None, None, None, None, None, None, W, qf, qd)
+    rel = lambda got, ref: ((got.double() - ref).abs().max() / ref.abs().max()).item()
+    e = torch.empty(B, 512, device="cuda")
+    native.head_hidden_fwd(f, qf, bias, e)
+    ref = torch.relu(f.double() @ W.double().t() + bias.double())
+    assert rel(e, ref) <= 2 * rel(torch.relu(torch.addmm(bias, f, W.t())), ref) + 1e-7
+    df = df0.clone()
+    am = native.amax_table(1, "cuda")[0]
+    native.head_hidden_dgrad(de, qd, f, df, amax_df=am)
+    refd = (df0.double() + de.double() @ W.double()) * (f > 0)
+    assert rel(df, refd) <= 2 * rel((df0 + de @ W) * (f > 0), refd) + 1e-7
+    assert am.view(torch.float32).max().item() == df.abs().max().item()
+    ws = torch.empty(max(native.head_hidden_wgrad_workspace_bytes(B), 16), dtype=torch.uint8, device="cuda")
+    dw, dw2 = torch.empty(512, 512, device="cuda"), torch.empty(512, 512, device="cuda")
+    native.head_hidden_wgrad(de, f, ws, dw)
+    native.head_hidden_wgrad(de, f, ws, dw2)
+    refw = de.double().t() @ f.double()
+    assert rel(dw, refw) <= 2 * rel(de.t() @ f, refw) + 1e-7
+    assert torch.equal(dw, dw2)
+    z = torch.ones(512, 512, device="cuda")
+    native.head_hidden_wgrad(torch.empty(0, 512, device="cuda"), torch.empty(0, 512, device="cuda"), ws, z)
+    assert not z.any()
+
+
 def test_fc_wgrad_zero_rows_writes_zero():
     import native
     dw = torch.full((512, 3136), 1.0, device="cuda")
