@@ -71,8 +71,10 @@ def conv_roofline(key, kt, totals):
     ach = flops / (mean_ms * 1e-3) / 1e12
     products = (2 if (layer == 1 and op != "dgrad") else 3) if split else 1
     peak = F16_MFMA_PEAK_TFLOPS / products if split else FP32_MFMA_PEAK_TFLOPS
-    # input + output (fwd), output grad + ReLU mask + input grad (dgrad), input + output grad (wgrad)
-    per = ACT_B[layer] + (2 * ACT_B[layer - 1] if op == "dgrad" else ACT_B[layer - 1])
+    # input + output (fwd), output grad + ReLU mask + input grad (dgrad), input + output grad (wgrad);
+    # the split conv2 dgrad reads conv1's ReLU mask as the forward's bitmask (4 B per pixel)
+    mask_b = 400 * 4 if (op == "dgrad" and layer == 2 and split) else ACT_B[layer - 1]
+    per = ACT_B[layer] + (ACT_B[layer - 1] + mask_b if op == "dgrad" else ACT_B[layer - 1])
     kname = CONV_KERNEL.get((op, layer, split))
     traffic, src = pmc_traffic(kname) if kname else (None, None)
     tot = sum(totals.values()) or 1.0

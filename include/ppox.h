@@ -418,16 +418,20 @@ int ppox_amax(const float* x, int64_t n, uint32_t* amax, void* stream);
 int64_t ppox_nature_split_pack_elems(int32_t which);
 int ppox_nature_pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1,
                            uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3, void* stream);
-/* amax_x: slots of x (layers 2, 3; null for layer 1's frames); amax_y: y's slots (nullable) */
+/* amax_x: slots of x (layers 2, 3; null for layer 1's frames); amax_y: y's slots (nullable);
+ * relu_bits (layer 1, nullable): y's ReLU bitmask, uint32 word p = bit c set iff channel c of
+ * output pixel p (n * 400 + oy * 20 + ox) is > 0 — batch * 400 words, read by the conv2 dgrad */
 int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
                                int64_t T, int64_t N_env, int64_t x_sample_stride,
                                const uint16_t* wq, const float* bias, float* y, const uint32_t* amax_x,
-                               uint32_t* amax_y, void* stream);
+                               uint32_t* amax_y, uint32_t* relu_bits, void* stream);
 /* dgrad (as ppox_nature_conv_dgrad) of conv2/conv3 with split weights (which = 12, 13);
- * amax_g: grad_out's slots, amax_out: grad_in's (nullable). */
+ * amax_g: grad_out's slots, amax_out: grad_in's (nullable).  Layer 2 takes the ReLU mask of
+ * conv1 from relu_bits (the conv1 forward's bitmask) when non-null, else from prev_act. */
 int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch,
                                  const uint16_t* wqd, const float* prev_act, float* grad_in,
-                                 const uint32_t* amax_g, uint32_t* amax_out, void* stream);
+                                 const uint32_t* amax_g, uint32_t* amax_out, const uint32_t* relu_bits,
+                                 void* stream);
 /* dW [co][ci][ky][kx] and db (as ppox_nature_conv_wgrad + ppox_nature_wgrad_reduce, in one
  * call): split-K slabs into a workspace of ppox_nature_wgrad_split_workspace_bytes(layer,
  * batch), reduced in a fixed order (deterministic).  x: u8 frames (layer 1, samples

@@ -59,6 +59,20 @@ AM_H1, AM_H2, AM_H3, AM_DF, AM_G3, AM_G2, AM_G1, AM_F, AM_DE = range(9)
 AM_ROWS = 10
 
 
+class PassState:
+    """Side data of one trunk pass for the split kernels: the amax table (pass[AM_*] is its row)
+    and conv1's ReLU bitmask (int32 per output pixel, bit c = channel c > 0; None unless the conv1
+    split forward wrote it), which the conv2 dgrad reads instead of the f32 activations."""
+
+    __slots__ = ("amax", "bits1")
+
+    def __init__(self, amax, bits1=None):
+        self.amax, self.bits1 = amax, bits1
+
+    def __getitem__(self, row):
+        return self.amax[row]
+
+
 # backward on two streams: each layer's weight gradient runs on a side stream beside the
 # main stream's dgrad chain (wgrad3 || dgrad3, wgrad2 || dgrad2; the fc weight gradient ||
 # the fc dgrad), joined before the optimizer reads the gradients (PPOX_BWD_STREAMS=0: one stream)
@@ -135,14 +149,15 @@ class _NatureTrunk(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, convs, w1, b1, w2, b2, w3, b3):
-        h1, h2, h3, am = convs.forward_acts(x)
-        ctx.convs = convs
-        ctx.save_for_backward(x, h1, h2, h3, am)
+        h1, h2, h3, am = convs.forward_acts(x, train=True)
+        ctx.convs, ctx.am = convs, am
+        ctx.save_for_backward(x, h1, h2, h3)
         return h3.permute(0, 3, 1, 2) if convs.nhwc3 else h3
 
     @staticmethod
     def backward(ctx, dh3):
-        x, h1, h2, h3, am = ctx.saved_tensors
+        x, h1, h2, h3 = ctx.saved_tensors
+        am = ctx.am
         convs = ctx.convs
         grads = [torch.zeros_like(t) for t in (convs.c1.weight, convs.c1.bias, convs.c2.weight, convs.c2.bias,
                                                convs.c3.weight, convs.c3.bias)]
@@ -269,13 +284,16 @@ class NatureConvs:
     def fwd(self, layer, x, B, bias, y, am):
         stride = 4 * 84 * 84 if layer == 1 else 0
         out_am = am[AM_H1 + layer - 1] if self.math != "f32" else None
+        bits = am.bits1 if layer == 1 and isinstance(am, PassState) else None
         if isinstance(x, RolloutRows):
             assert layer == 1 and self.uses_split("fwd", 1)
-            native.nature_conv_fwd_split(1, x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y, amax_y=out_am)
+            native.nature_conv_fwd_split(1, x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y, amax_y=out_am,
+                                         relu_bits=bits)
             return
         if self.uses_split("fwd", layer):
             native.nature_conv_fwd_split(layer, x, B, None, 0, 0, stride, self.q[layer], bias, y,
-                                         amax_x=am[AM_H1 + layer - 2] if layer > 1 else None, amax_y=out_am)
+                                         amax_x=am[AM_H1 + layer - 2] if layer > 1 else None, amax_y=out_am,
+                                         relu_bits=bits)
         else:
             wp = (self.wp1, self.wp2, self.wp3)[layer - 1]
             native.nature_conv_fwd(layer, x, B, None, 0, 0, stride, wp, bias, y)
@@ -286,8 +304,9 @@ class NatureConvs:
         self.pack(B)  # the conv2 dgrad form depends on the batch
         g_am, out_am = (am[AM_G3], am[AM_G2]) if layer == 3 else (am[AM_G2], am[AM_G1])
         if self.uses_split("dgrad", layer, B):
+            bits = am.bits1 if layer == 2 and isinstance(am, PassState) else None
             native.nature_conv_dgrad_split(layer, g, B, self.q[10 + layer], prev_act, out, amax_g=g_am,
-                                           amax_out=out_am)
+                                           amax_out=out_am, relu_bits=bits)
         else:
             native.nature_conv_dgrad(layer, g, B, self.wpd2 if layer == 2 else self.wpd3, prev_act, out)
             if self.math != "f32":
@@ -308,9 +327,10 @@ class NatureConvs:
         else:
             native.nature_conv_wgrad(layer, x, B, None, 0, 0, stride, g, self.workspace(layer, B), dw, db, stream=stream)
 
-    def forward_acts(self, x):
+    def forward_acts(self, x, train=False):
         """Trunk forward: (h1 NHWC, h2 NHWC, h3, am) — activations (ReLU applied) and the pass's
-        amax table (AM_* rows; the backward of the same pass records its gradients' rows); h3 is
+        PassState (the amax table's AM_* rows — the backward of the same pass records its
+        gradients' rows — and, for a `train` pass, conv1's ReLU bitmask); h3 is
         NHWC (B, 7, 7, 64) in split math (self.nhwc3), NCHW (B, 64, 7, 7) in f32 math."""
         self.pack(x.shape[0])
         B = x.shape[0]
@@ -318,7 +338,10 @@ class NatureConvs:
         h1 = torch.empty((B, 20, 20, 32), device=dev)
         h2 = torch.empty((B, 9, 9, 64), device=dev)
         h3 = torch.empty((B, 7, 7, 64) if self.nhwc3 else (B, 64, 7, 7), device=dev)
-        am = native.amax_table(AM_ROWS, dev)
+        # conv1's ReLU bitmask when both its forward and the conv2 dgrad run split (training passes)
+        bits1 = torch.empty(B * 400, dtype=torch.int32, device=dev) \
+            if train and self.uses_split("fwd", 1) and self.uses_split("dgrad", 2, B) else None
+        am = PassState(native.amax_table(AM_ROWS, dev), bits1)
         if B:
             self.fwd(1, x, B, self.c1.bias, h1, am)
             self.fwd(2, h1, B, self.c2.bias, h2, am)

@@ -512,6 +512,9 @@ __device__ inline int c2_nat_tap(int k) {  // class tap k (0..15) -> natural tap
     return ((cls >> 1) + 2 * (i >> 1)) * G2::KW + (cls & 1) + 2 * (i & 1);
 }
 
+// BITS: the ReLU mask of conv1 from the forward's bitmask (a.bits_mask, 4 B per pixel) instead
+// of its f32 activations (a.mask, 128 B per pixel): 26 MB instead of 839 MB at B = 16384
+template <bool BITS>
 __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4* __restrict__ wq,
                                                             long long ntriples) {
     using L = G2;
@@ -598,7 +601,7 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
             for (int r = 0; r < 8; ++r) Ds[di[r]] = dv[r] + c[r0 + r];
         }
     };
-    float4 mk[C2OV];
+    std::conditional_t<BITS, uint32_t, float4> mk[C2OV];
     auto load_mask = [&](long long n0, int cls) {
         const int py = cls >> 1, px = cls & 1;
 #pragma unroll
@@ -607,8 +610,11 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
             const long long n = n0 + s;
             const int iy = 2 * (pix / 10) + py, ix = 2 * (pix % 10) + px;
             const bool ok = e < C2S * C2PIX * 8 && n < a.batch;
-            const long long o = ok ? ((n * L::IH + iy) * L::IW + ix) * L::CIN + c4 * 4 : 0;
-            mk[j] = *reinterpret_cast<const float4*>(a.mask + o);
+            const long long p = ok ? (n * L::IH + iy) * L::IW + ix : 0;
+            if constexpr (BITS)
+                mk[j] = a.bits_mask[p];  // one load either way: the counted vmcnt waits hold
+            else
+                mk[j] = *reinterpret_cast<const float4*>(a.mask + p * L::CIN + c4 * 4);
         }
     };
     // the image is read and re-zeroed with inline-asm LDS ops: a C++ access here, after the
@@ -626,9 +632,15 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
             asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)\n\tds_write_b128 %1, %2"
                          : "=&v"(dr) : "v"(da), "v"(zero4) : "memory");
             const float4 d = __builtin_bit_cast(float4, dr);
-            const float4 m = mk[j];
-            const float4 y = make_float4(m.x > 0.f ? d.x * uo : 0.f, m.y > 0.f ? d.y * uo : 0.f,
-                                         m.z > 0.f ? d.z * uo : 0.f, m.w > 0.f ? d.w * uo : 0.f);
+            bool on[4];
+            if constexpr (BITS) {
+                const uint32_t w = mk[j] >> (c4 * 4);
+                on[0] = w & 1u, on[1] = w & 2u, on[2] = w & 4u, on[3] = w & 8u;
+            } else {
+                on[0] = mk[j].x > 0.f, on[1] = mk[j].y > 0.f, on[2] = mk[j].z > 0.f, on[3] = mk[j].w > 0.f;
+            }
+            const float4 y = make_float4(on[0] ? d.x * uo : 0.f, on[1] ? d.y * uo : 0.f, on[2] ? d.z * uo : 0.f,
+                                         on[3] ? d.w * uo : 0.f);
             const long long n = n0 + s;
             const float ym = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));
             om = (in && n < a.batch) ? fmaxf(om, ym) : om;  // the dummy slot's sums are not output
@@ -2350,11 +2362,12 @@ int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq,
 
 extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch, const uint16_t* wqd,
                                             const float* prev_act, float* grad_in, const uint32_t* amax_g,
-                                            uint32_t* amax_out, void* stream) {
+                                            uint32_t* amax_out, const uint32_t* relu_bits, void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad_split: layer must be 2 or 3");
-    PPOX_REQUIRE(grad_out && wqd && prev_act && grad_in && amax_g && batch >= 0,
+    PPOX_REQUIRE(grad_out && wqd && (prev_act || relu_bits) && grad_in && amax_g && batch >= 0,
                  "ppox_nature_conv_dgrad_split: bad arguments");
+    PPOX_REQUIRE(!relu_bits || layer == 2, "ppox_nature_conv_dgrad_split: relu_bits is for layer 2 (conv1's mask)");
     PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wqd) && ppox::aligned16(amax_g),
                  "ppox_nature_conv_dgrad_split: 16B alignment");
     Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch, amax_g, amax_out,
@@ -2372,7 +2385,11 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
                              cus[dev] > 0,
                          "ppox_nature_conv_dgrad_split: CU count");
         const long long grid = std::min<long long>(ntriples, cus[dev]);
-        dgrad2_colp_kernel<<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd), ntriples);
+        a.bits_mask = relu_bits;
+        if (relu_bits)
+            dgrad2_colp_kernel<true><<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd), ntriples);
+        else
+            dgrad2_colp_kernel<false><<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd), ntriples);
         PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
     }
     return launch_sgemm<SgDgradPM<G3>>(a, wqd, ppox::ceil_div(batch, SG_ROWS) * SgDgradPM<G3>::NPOS, s,

@@ -33,6 +33,10 @@ struct Args {
     const uint32_t* amax_x = nullptr;
     uint32_t* amax_y = nullptr;
     const int* wexp = nullptr;
+    // ReLU bitmasks (bit c of word p: activation channel c of pixel p > 0): written by the conv1
+    // split forward (bits_y), read by the conv2 split dgrad instead of the f32 mask (bits_mask)
+    uint32_t* bits_y = nullptr;
+    const uint32_t* bits_mask = nullptr;
 };
 
 __device__ inline f32x16 zero16() {

@@ -108,16 +108,27 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
                 __builtin_amdgcn_sched_barrier(0);
             }
         const unsigned m0 = tile * 32 * MT;
-        // C/D map: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+        // C/D map: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5).  The ReLU
+        // bitmask word of tile row L (its 32 channels) is half (L >> 2) & 1 of the ballot of
+        // element e = (L & 3) + 4 * (L >> 3): lane L < 32 collects it and stores it
+        const int eL = (lane & 3) + 4 * ((lane >> 3) & 3), hL = (lane >> 2) & 1;
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
+        for (int i = 0; i < MT; ++i) {
+            uint32_t word = 0;
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const unsigned m = m0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
                 const float v = fmaxf((hi[i][e] + lo[i][e]) * uw + bias, 0.f);
                 om = fmaxf(om, v);  // a row past the end recomputed row m0, which is stored
                 if (m < M) a.y[(long long)m * L::COUT + co] = v;
+                if (a.bits_y) {  // uniform
+                    const unsigned long long b = __ballot(v > 0.f);
+                    word = eL == e ? (uint32_t)(hL ? b >> 32 : b) : word;
+                }
             }
+            const unsigned mw = m0 + i * 32 + lane;
+            if (a.bits_y && lane < 32 && mw < M) a.bits_y[mw] = word;
+        }
     };
     Raw r0, r1;
     load_tile(t_begin, r0);
@@ -159,13 +170,14 @@ extern "C" int ppox_nature_pack_split(const float* w1, const float* w2, const fl
 extern "C" int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx, int64_t T,
                                           int64_t N_env, int64_t x_sample_stride, const uint16_t* wq,
                                           const float* bias, float* y, const uint32_t* amax_x, uint32_t* amax_y,
-                                          void* stream) {
+                                          uint32_t* relu_bits, void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_conv_fwd_split: layer must be 1, 2 or 3");
     PPOX_REQUIRE(x && wq && bias && y && batch >= 0, "ppox_nature_conv_fwd_split: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(wq), "ppox_nature_conv_fwd_split: packed weights must be 16-byte aligned");
     if (layer != 1) {
         PPOX_REQUIRE(!idx, "ppox_nature_conv_fwd_split: idx is for layer 1 only");
+        PPOX_REQUIRE(!relu_bits, "ppox_nature_conv_fwd_split: relu_bits is for layer 1 only");
         return ppox_conv::split_fwd23(layer, x, batch, wq, bias, y, amax_x, amax_y, ppox::as_stream(stream));
     }
     PPOX_REQUIRE(!amax_x, "ppox_nature_conv_fwd_split: layer 1 reads uint8 frames (no amax_x)");
@@ -173,6 +185,7 @@ extern "C" int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t 
     Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, nullptr, bias, nullptr, y, batch,
            nullptr, amax_y, pack_exp(wq, ppox_conv::planes(1))};
     a.wp = reinterpret_cast<const float*>(wq);
+    a.bits_y = relu_bits;
     hipStream_t s = ppox::as_stream(stream);
     PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && (idx || x_sample_stride % 4 == 0),
                  "ppox_nature_conv_fwd_split: u8 input must be 4-byte aligned");

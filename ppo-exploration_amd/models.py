@@ -140,7 +140,7 @@ class CnnActorCritic(nn.Module):
         """-> (actor out, value (B,), int value or None, ctx for backward_train)."""
         with torch.no_grad():
             x = x.contiguous()
-            h1, h2, h3, am = self.conv_impl.forward_acts(x)
+            h1, h2, h3, am = self.conv_impl.forward_acts(x, train=True)
             hf = h3.view(h3.shape[0], -1)
             fc = self.feature_extractor[7]
             if self.conv_impl.math != "f32":

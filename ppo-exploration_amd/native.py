@@ -61,8 +61,8 @@ SIGNATURES = {
     "ppox_nchw_to_nhwc_relu_grad": [_vp, _vp, _i64, _vp, _vp],
     "ppox_nature_conv_fwd": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_pack_split": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
-    "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
     "ppox_relu_backward_amax_": [_vp, _vp, _i64, _vp, _vp],
     "ppox_amax": [_vp, _i64, _vp, _vp],
@@ -508,13 +508,14 @@ def nature_pack_split(w1, w2, w3, q1, q2, q3, qd2=None, qd3=None, stream=None):
 
 
 def nature_conv_fwd_split(layer, x, batch, idx, T, N_env, x_sample_stride, wq, bias, y, amax_x=None, amax_y=None,
-                          stream=None):
-    """amax_x: x's slots (layers 2, 3; computed here when None); amax_y: y's slots to record (or None)."""
+                          relu_bits=None, stream=None):
+    """amax_x: x's slots (layers 2, 3; computed here when None); amax_y: y's slots to record (or None);
+    relu_bits (layer 1): int32 (batch * 400) ReLU bitmask of y to write (or None)."""
     if layer != 1 and batch:
         amax_x = _amax_of(x, amax_x, stream)
     call("ppox_nature_conv_fwd_split", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
          int(x_sample_stride), _p(wq), _p(bias), _p(y), _p(amax_x) if layer != 1 else None, _p(amax_y),
-         stream_ptr(stream))
+         _p(relu_bits), stream_ptr(stream))
 
 
 def normalize_obs_f32_ex(x, rows, cols, row_stride, mean, var, eps, clip, out, stream=None):
@@ -732,12 +733,13 @@ def nature_conv_wgrad_split_idx(layer, x, batch, idx, T, N_env, grad_out, worksp
 
 
 def nature_conv_dgrad_split(layer, grad_out, batch, wqd, prev_act, grad_in, amax_g=None, amax_out=None,
-                            stream=None):
-    """amax_g: grad_out's slots (computed here when None); amax_out: grad_in's slots to record (or None)."""
+                            relu_bits=None, stream=None):
+    """amax_g: grad_out's slots (computed here when None); amax_out: grad_in's slots to record (or None);
+    relu_bits (layer 2): conv1's ReLU bitmask from its split forward, used instead of prev_act."""
     if batch:
         amax_g = _amax_of(grad_out, amax_g, stream)
     call("ppox_nature_conv_dgrad_split", int(layer), _p(grad_out), int(batch), _p(wqd), _p(prev_act), _p(grad_in),
-         _p(amax_g), _p(amax_out), stream_ptr(stream))
+         _p(amax_g), _p(amax_out), _p(relu_bits), stream_ptr(stream))
 
 
 # ---------------------------------------------------------------------------

@@ -600,6 +600,31 @@ def test_conv2_split_dgrad_col2im_ragged(B):
     assert e_s <= 2 * e_f + 1e-7, (e_s, e_f)
 
 
+@pytest.mark.parametrize("B", [1, 5, 301])
+def test_conv1_relu_bits_drive_conv2_dgrad(B):
+    """The conv1 split forward's ReLU bitmask (bit c of word p: channel c of pixel p > 0) equals
+    h1 > 0, and the conv2 split dgrad reading it equals the one reading h1, bitwise."""
+    import native
+    torch.manual_seed(B)
+    w1 = torch.randn(32, 4, 8, 8, device="cuda") * 0.02
+    w2 = torch.randn(64, 32, 4, 4, device="cuda") * 0.05
+    w3 = torch.randn(64, 64, 3, 3, device="cuda") * 0.05
+    q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device="cuda") for k in (1, 2, 3, 12, 13)}
+    native.nature_pack_split(w1, w2, w3, q[1], q[2], q[3], q[12], q[13])
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    b1 = torch.randn(32, device="cuda")
+    h1 = torch.empty(B, 20, 20, 32, device="cuda")
+    bits = torch.full((B * 400 + 1,), 12345, dtype=torch.int32, device="cuda")
+    native.nature_conv_fwd_split(1, x, B, None, 0, 0, 28224, q[1], b1, h1, relu_bits=bits)
+    want = ((h1 > 0).view(B * 400, 32).long() << torch.arange(32, device="cuda")).sum(1)
+    assert torch.equal(bits[:-1].long() & 0xFFFFFFFF, want) and int(bits[-1]) == 12345
+    g = torch.randn(B, 9, 9, 64, device="cuda")
+    o_act, o_bits = torch.empty_like(h1), torch.empty_like(h1)
+    native.nature_conv_dgrad_split(2, g, B, q[12], h1, o_act)
+    native.nature_conv_dgrad_split(2, g, B, q[12], None, o_bits, relu_bits=bits)
+    assert torch.equal(o_act, o_bits)
+
+
 @pytest.mark.parametrize("intrinsic,B", [(False, 40), (True, 40), (False, 600)])
 def test_cnn_explicit_backward_matches_autograd(intrinsic, B):
     """CnnActorCritic.forward_train/backward_train (no autograd graph, grads straight into
