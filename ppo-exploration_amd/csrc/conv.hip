@@ -503,7 +503,8 @@ __device__ inline void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_b
 
 constexpr int C2P_TAP = 4 * NPL * 64;                  // u32x4 per tap: 4 k-steps x 2 planes x 64 lanes
 constexpr int C2P_AN = 256 * 16;                       // u32x4: 256 G rows x 64 f32
-constexpr int C2P_IMG = (C2S * C2PIX * 32 + 32) / 4;   // u32x4: class image + dummy slot
+// u32x4: class image + the dummy region (the rows past a triple's 243 land there at any tap offset)
+constexpr int C2P_IMG = (C2S * C2PIX * 32 + (11 * 32 + 32)) / 4;
 __device__ float4 kC2Dummy[512];                       // store target of threads with nothing to store
 
 __device__ inline int c2_nat_tap(int k) {  // class tap k (0..15) -> natural tap ky * 4 + kx
@@ -582,23 +583,26 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
     };
     // col2im add of tap k into the class image: row (oy, ox) -> class pixel (oy + (i >> 1),
     // ox + (i & 1)); eight reads, then eight writes; rows past the samples -> dummy slot
-    auto rmw_tap = [&](int k, const f32x16& c) {
-        const int i = k & 3;
-        int toff = ((i >> 1) * 10 + (i & 1)) * 32 + (lane & 31);
-        asm volatile("" : "+v"(toff));  // opaque: keeps hipcc from hoisting 4 taps' address sets (spills)
+    // this lane's 16 accumulator rows -> their class-image pixel at tap offset 0 (float index,
+    // computed once: a tap adds only its constant offset, folded into the ds instructions);
+    // rows past the triple's 243 -> the dummy region
+    int dbase[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int rho = wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int s = rho / 81, p = rho - s * 81, oy = p / 9, ox = p - oy * 9;
+        dbase[r] = (rho < C2ROWS ? (s * C2PIX + oy * 10 + ox) * 32 : C2S * C2PIX * 32) + (lane & 31);
+    }
+    auto rmw_tap = [&](auto i_tag, const f32x16& c) {
+        constexpr int i = decltype(i_tag)::value;
+        constexpr int toff = ((i >> 1) * 10 + (i & 1)) * 32;
 #pragma unroll
         for (int r0 = 0; r0 < 16; r0 += 8) {
-            int di[8];
             float dv[8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const int rho = wave * 32 + ((r0 + r) & 3) + 8 * ((r0 + r) >> 2) + 4 * (lane >> 5);
-                const int s = rho / 81, p = rho - s * 81, oy = p / 9, ox = p - oy * 9;
-                di[r] = rho < C2ROWS ? (s * C2PIX + oy * 10 + ox) * 32 + toff : C2S * C2PIX * 32 + (lane & 31);
-                dv[r] = Ds[di[r]];
-            }
+            for (int r = 0; r < 8; ++r) dv[r] = Ds[dbase[r0 + r] + toff];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) Ds[di[r]] = dv[r] + c[r0 + r];
+            for (int r = 0; r < 8; ++r) Ds[dbase[r0 + r] + toff] = dv[r] + c[r0 + r];
         }
     };
     std::conditional_t<BITS, uint32_t, float4> mk[C2OV];
@@ -676,7 +680,7 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
         const long long n0 = tt * C2S;
         if constexpr (i & 1) dmaB2(k + 3);  // taps k+3, k+4 (mod 16) into the slots of k-1, k
         if (i < 3 || cls < 3) mfma_tap(k + 1, next);
-        rmw_tap(k, cur);
+        rmw_tap(i_tag, cur);
         if constexpr (i == 0) {
             if (cls == 1)
                 __builtin_amdgcn_s_waitcnt(0x4F72);  // vmcnt(18): + class 0's 8 row DMAs
