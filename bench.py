@@ -55,7 +55,7 @@ CONV_KERNEL = {("fwd", 1, True): "fwd1_split_kernel<1>",
                ("wgrad", 3, True): "wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64, false, 1>"}
 
 
-def conv_roofline(key, kt, totals):
+def conv_roofline(key, kt, totals, solo_kt=None):
     """Roofline of the dominant conv launch: algorithmic FLOPs (2 x MACs x batch) per launch /
     mean HIP-event duration.  The f32 kernels run v_mfma_f32_32x32x2_f32 (peak 157.3 TF/s);
     the split-f16 kernels issue 3 f16 MFMA products per f32 MAC (2 when one operand is the
@@ -105,7 +105,22 @@ def conv_roofline(key, kt, totals):
                          "iteration; the timed launches run beside the side-stream weight gradients "
                          "(convs.BWD_STREAMS), so mean_us includes any sharing of the GPU with them",
             "peak_note": "f32 MFMA 157.3 TF/s" if not split else
-                         f"f16 MFMA 2500 TF/s / {products} products per f32 MAC (split-f16, fp32-class accuracy)"}
+                         f"f16 MFMA 2500 TF/s / {products} products per f32 MAC (split-f16, fp32-class accuracy)",
+            # the same launches in the one-stream warmup iteration: the kernel alone on the GPU
+            "solo": _solo(solo_kt, flops / batch, alg_bytes / batch, peak, bound)}
+
+
+def _solo(kt, flops_per_row, bytes_per_row, peak, bound):
+    import numpy as np
+    if not kt:
+        return None
+    ms = float(np.mean([t for t, _ in kt]))
+    rows = float(np.mean([a[2] for _, a in kt]))
+    tf = flops_per_row * rows / (ms * 1e-3) / 1e12
+    gbs = bytes_per_row * rows / (ms * 1e-3) / 1e9
+    return {"mean_us": round(ms * 1e3, 1), "launches": len(kt),
+            "frac": round(gbs / HBM_PEAK_GBS if bound == "hbm" else tf / peak, 4),
+            "mfma_frac": round(tf / peak, 4), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
 def gae_kernel_ms(alg, dual, reps=20):
@@ -258,11 +273,12 @@ def main():
         convs.BWD_STREAMS = streams and w > 0
         iteration()
         if w == 0:
-            totals = {k: sum(t for t, _ in native.event_times_ms(k)) for k in conv_keys}
+            solo = {k: native.event_times_ms(k) for k in conv_keys}
+            totals = {k: sum(t for t, _ in v) for k, v in solo.items()}
             native.enable_event_timing([])
     convs.BWD_STREAMS = streams
     if args.warmup == 0:
-        totals = {k: 0.0 for k in conv_keys}
+        totals, solo = {k: 0.0 for k in conv_keys}, {}
     prof_kernel = max(totals, key=totals.get) if any(totals.values()) else "ppox_nature_conv_dgrad:2"
     gae_kernel = "ppox_gae" if args.algo != "rnd" else "ppox_gae_dual"
     native.enable_event_timing([prof_kernel])
@@ -308,7 +324,7 @@ def main():
     # gae and episodes run inside collect
     out["phases_ms_per_step"] = phase_ms
     if kt:
-        out["roofline"] = conv_roofline(prof_kernel, kt, totals)
+        out["roofline"] = conv_roofline(prof_kernel, kt, totals, solo.get(prof_kernel))
         launch_rows = float(np.mean([a[2] for _, a in kt]))
         if out["roofline"].get("traffic") is not None and launch_rows != PMC_LAUNCH_ROWS:
             # the committed PMC passes ran launches of PMC_LAUNCH_ROWS rows (the 1-GPU

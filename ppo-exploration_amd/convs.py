@@ -78,6 +78,10 @@ class PassState:
 # the fc dgrad), joined before the optimizer reads the gradients (PPOX_BWD_STREAMS=0: one stream)
 BWD_STREAMS = os.environ.get("PPOX_BWD_STREAMS", "1") != "0"
 BWD_SOLO_DGRAD2_BATCH = int(os.environ.get("PPOX_BWD_SOLO_DGRAD2", "8192"))
+# PPOX_BWD_SOLO_WGRAD2=1: from that batch conv2's weight gradient also runs alone on the main stream
+# (after the dgrad, before wgrad1) instead of beside wgrad1 — 1 % slower (same-box A/B), but its
+# event time is then its own execution time
+BWD_SOLO_WGRAD2 = os.environ.get("PPOX_BWD_SOLO_WGRAD2", "0") != "0"
 _side = {}
 
 
@@ -413,7 +417,7 @@ class NatureConvs:
             join(side, cur)
         g1 = torch.empty((B, 20, 20, 32), device=dev)
         self.dgrad(2, g2, B, h1, g1, am)                        # dX of conv2, times ReLU'(conv1)
-        if side is None:
+        if side is None or (solo and BWD_SOLO_WGRAD2):
             self.wgrad(2, h1, B, g2, dw2, db2, am)
         elif solo:
             fork(side, cur)

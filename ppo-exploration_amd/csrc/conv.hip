@@ -2056,6 +2056,41 @@ __device__ inline void pack_rows_unit(const float* w, float s, uint16_t* q, long
                                u - cb * per);
 }
 
+// The fc forms, enumerated so that consecutive units read consecutive floats of w (the
+// permutation f = p * 64 + c <- c * 49 + p otherwise turns every lane's reads into 49-float
+// strides across all of W): unit u = (outer, c-group or k-group, p) with p (0..48) fastest.
+//   TRANS (forward, B[k][n] = W[n][c * 49 + p], k = p * 64 + c): u = (n, g, p), values
+//     c = 8g .. 8g + 7 of column n at k0 = p * 64 + 8g;
+//   dgrad (B[k][n] = W[k][c * 49 + p], n = p * 64 + c): u = (kg, c, p), values k = 8kg .. 8kg + 7
+//     of column n (block p, column c of the block).
+template <bool TRANS>
+__device__ inline void pack_fc_unit(const float* __restrict__ w, float s, uint16_t* __restrict__ q, long long u) {
+    constexpr int K = TRANS ? 3136 : 512, NT = 2;
+    const int p = (int)(u % 49);
+    const long long r = u / 49;
+    int k0, col, cb;
+    float v[8];
+    if constexpr (TRANS) {
+        const int g = (int)(r & 7), n = (int)(r >> 3);
+        const float* src = w + (long long)n * 3136 + 8 * g * 49 + p;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = src[e * 49];
+        k0 = p * 64 + 8 * g, col = n & 63, cb = n >> 6;
+    } else {
+        const int c = (int)(r & 63), kg = (int)(r >> 6);
+        const float* src = w + (long long)(8 * kg) * 3136 + c * 49 + p;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = src[(long long)e * 3136];
+        k0 = 8 * kg, col = c, cb = p;
+    }
+    u32x4 p0, p1;
+    split8h(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), s, p0, p1);
+    const int cs = k0 >> 4, h = (k0 >> 3) & 1, j = col >> 5, l = h * 32 + (col & 31);
+    u32x4* d = reinterpret_cast<u32x4*>(q + (long long)cb * K * 64 * NPL + ((long long)(cs * NT + j) * NPL) * 512) + l;
+    d[0] = p0;
+    d[64] = p1;
+}
+
 // the forms packed from weight tensor t (0: w1, 1: w2, 2: w3, 3: wfc) and their plane counts
 __device__ inline void pa_forms(const PackAll& p, int t, uint16_t* (&f)[2], long long& planes) {
     switch (t) {
@@ -2125,9 +2160,9 @@ __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long tota
         j -= PU_3;
         if (j < PA_N2) { if (p.wpd2) pack_dgrad_elem<G2, false>(p.w2, p.wpd2, (int)j); continue; }
         j -= PA_N2;
-        if (j < PU_FC) { if (p.qfcf) pack_rows_unit<FcFwd, true>(p.wfc, sc[3], p.qfcf, j); continue; }
+        if (j < PU_FC) { if (p.qfcf) pack_fc_unit<true>(p.wfc, sc[3], p.qfcf, j); continue; }
         j -= PU_FC;
-        if (j < PU_FCD) { if (p.qfcd) pack_rows_unit<FcDgrad, false>(p.wfc, sc[3], p.qfcd, j); continue; }
+        if (j < PU_FCD) { if (p.qfcd) pack_fc_unit<false>(p.wfc, sc[3], p.qfcd, j); continue; }
         j -= PU_FCD;
         if (j < PU_H) { if (p.qhf) pack_rows_unit<HeadFwd, true, false>(p.wh, sc[4], p.qhf, j); continue; }
         j -= PU_H;
