@@ -219,13 +219,16 @@ __host__ __device__ inline int split_scale_exp(uint32_t amax_bits) {
 }
 __host__ __device__ inline float exp2i(int e) { return __builtin_bit_cast(float, (uint32_t)(e + 127) << 23); }
 
-// two f32 (already scaled) -> their f16 high and low planes, packed f16x2 words (x0 low)
+// two f32 (already scaled) -> their f16 high and low planes, packed f16x2 words (x0 low).  The
+// residual x - h is one v_fma_mix_f32 per value (h read as f16 straight from the packed word, times
+// -1, plus x: exact, so its single rounding is none); hipcc would emit a convert and a subtract
 __device__ inline void split2h(float x0, float x1, uint32_t& h, uint32_t& l) {
     const f32x2 v = {x0, x1};
-    const f16x2 hv = __builtin_convertvector(v, f16x2);
-    const f32x2 r = v - __builtin_convertvector(hv, f32x2);
-    h = __builtin_bit_cast(uint32_t, hv);
-    l = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, f16x2));
+    h = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));
+    float r0, r1;
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r0) : "v"(h), "v"(x0));
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r1) : "v"(h), "v"(x1));
+    l = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){r0, r1}, f16x2));
 }
 // eight f32 times s -> their two f16 planes as MFMA fragments (element e = value e)
 __device__ inline void split8h(const float4& v0, const float4& v1, float s, u32x4& p0, u32x4& p1) {
