@@ -48,7 +48,7 @@ CONV_KERNEL = {("fwd", 1, True): "fwd1_split_kernel<1>",
                ("fwd", 2, True): "sgemm_kernel<SgFwd<32, 20, 20, 4, 4, 2, 64, false>, 4, 2>",
                ("fwd", 3, True): "sgemm_kernel<SgFwd<64, 9, 9, 3, 3, 1, 64, false>, 4, 2>",
                ("dgrad", 2, False): "igemm_kernel<DgradPMProblem<32, 20, 20, 4, 4, 2, 64, 1>>",
-               ("dgrad", 2, True): "dgrad2_colp_kernel",
+               ("dgrad", 2, True): "dgrad2_colp_kernel<true>",
                ("dgrad", 3, True): "sgemm_kernel<SgDgradPM<64, 9, 9, 3, 3, 1, 64>, 4, 2>",
                ("wgrad", 1, True): "wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>",
                ("wgrad", 2, True): "wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128, false, 1>",

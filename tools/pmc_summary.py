@@ -15,11 +15,13 @@ def short(name):
 
 
 def load(path, counter):
-    vals = defaultdict(list)
+    """per kernel: the counter values of its launches with the largest grid (the training
+    minibatch's; the forward kernels also run at the collect batch in the same command)"""
+    vals = defaultdict(lambda: defaultdict(list))
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
-    return vals
+            vals[short(r["Kernel_Name"])][int(r["Grid_Size"])].append(float(r["Counter_Value"]))
+    return {k: v[max(v)] for k, v in vals.items()}
 
 
 def main():
