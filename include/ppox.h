@@ -288,7 +288,8 @@ int ppox_vecnorm_reward(float* rewards, const uint8_t* dones, double* ret, int64
  * weights packed (once per optimizer step) by ppox_nature_fc_pack into ppox_nature_fc_pack_elems()
  * uint16 each for the forward (W^T) and the dgrad (W) operand.  amax_h3 / amax_df: the slots of
  * the A operand (required); amax_g3 / amax_f: the slots the dgrad / forward record g3's / f's
- * amax into (nullable).
+ * amax into (nullable).  relu_bits (dgrad, nullable): h3's ReLU bitmask from the conv3 split forward,
+ * used instead of h3.
  * Both run in NHWC feature order: h3 is the split conv3 forward's NHWC output (batch, 7, 7, 64)
  * and W is packed through the permutation f = p * 64 + c <- Flatten feature c * 49 + p.
  * fwd: f = relu(h3 @ W^T + b); dgrad: g3 (NHWC (B,7,7,64)) = (df @ W) * (h3 > 0)
@@ -323,7 +324,7 @@ int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_dgrad, void
 int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
                        const uint32_t* amax_h3, uint32_t* amax_f, void* stream);
 int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
-                         const uint32_t* amax_df, uint32_t* amax_g3, void* stream);
+                         const uint32_t* amax_df, uint32_t* amax_g3, const uint32_t* relu_bits, void* stream);
 /* fc forward (as ppox_nature_fc_fwd) split over K for small batches: 2-8 K-ranges per (128-row
  * tile, 64-column block) so the grid fills the chip, partial products into the workspace
  * (ppox_nature_fc_fwd_splitk_workspace_bytes(batch)), then one fixed-order reduce adding the
@@ -419,15 +420,17 @@ int64_t ppox_nature_split_pack_elems(int32_t which);
 int ppox_nature_pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1,
                            uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3, void* stream);
 /* amax_x: slots of x (layers 2, 3; null for layer 1's frames); amax_y: y's slots (nullable);
- * relu_bits (layer 1, nullable): y's ReLU bitmask, uint32 word p = bit c set iff channel c of
- * output pixel p (n * 400 + oy * 20 + ox) is > 0 — batch * 400 words, read by the conv2 dgrad */
+ * relu_bits (nullable): y's ReLU bitmask, bit c % 32 of uint32 word p * (C / 32) + c / 32 set iff
+ * channel c of output pixel p (n * P + oy * OW + ox) is > 0 — batch * P * C / 32 words (8-B
+ * aligned), read by the next layer's split dgrad (conv1's by conv2's, conv2's by conv3's) and, for
+ * conv3, by the fc dgrad */
 int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
                                int64_t T, int64_t N_env, int64_t x_sample_stride,
                                const uint16_t* wq, const float* bias, float* y, const uint32_t* amax_x,
                                uint32_t* amax_y, uint32_t* relu_bits, void* stream);
 /* dgrad (as ppox_nature_conv_dgrad) of conv2/conv3 with split weights (which = 12, 13);
- * amax_g: grad_out's slots, amax_out: grad_in's (nullable).  Layer 2 takes the ReLU mask of
- * conv1 from relu_bits (the conv1 forward's bitmask) when non-null, else from prev_act. */
+ * amax_g: grad_out's slots, amax_out: grad_in's (nullable).  The ReLU mask of the layer below
+ * comes from relu_bits (that layer's split forward's bitmask) when non-null, else from prev_act. */
 int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch,
                                  const uint16_t* wqd, const float* prev_act, float* grad_in,
                                  const uint32_t* amax_g, uint32_t* amax_out, const uint32_t* relu_bits,

@@ -53,6 +53,10 @@ FC_WGRAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_WGRAD_SPLIT_MIN", "0"))
 # batch up, rocBLAS f32 below (PPOX_HEAD_SPLIT_MIN overrides)
 HEAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_SPLIT_MIN", "8192"))
 
+# ReLU masks of the conv outputs as bitmasks written by the split forwards for the split dgrads
+# (PPOX_RELU_BITS=0: the dgrads read the f32 activations)
+RELU_BITS = os.environ.get("PPOX_RELU_BITS", "1") != "0"
+
 # rows of a pass's amax table (native.amax_table): the split-f16 operands of the trunk and the
 # heads' hidden layer, each recorded by the kernel that produces it and read by its consumers
 AM_H1, AM_H2, AM_H3, AM_DF, AM_G3, AM_G2, AM_G1, AM_F, AM_DE = range(9)
@@ -61,13 +65,14 @@ AM_ROWS = 10
 
 class PassState:
     """Side data of one trunk pass for the split kernels: the amax table (pass[AM_*] is its row)
-    and conv1's ReLU bitmask (int32 per output pixel, bit c = channel c > 0; None unless the conv1
-    split forward wrote it), which the conv2 dgrad reads instead of the f32 activations."""
+    and the ReLU bitmasks of the three conv outputs (bits[l - 1] for layer l: int32 words per
+    output pixel, bit c % 32 of word c / 32 = channel c > 0; None unless that split forward wrote
+    it), which the next layer's dgrad reads instead of the f32 activations."""
 
-    __slots__ = ("amax", "bits1")
+    __slots__ = ("amax", "bits")
 
-    def __init__(self, amax, bits1=None):
-        self.amax, self.bits1 = amax, bits1
+    def __init__(self, amax, bits=(None, None, None)):
+        self.amax, self.bits = amax, bits
 
     def __getitem__(self, row):
         return self.amax[row]
@@ -288,7 +293,7 @@ class NatureConvs:
     def fwd(self, layer, x, B, bias, y, am):
         stride = 4 * 84 * 84 if layer == 1 else 0
         out_am = am[AM_H1 + layer - 1] if self.math != "f32" else None
-        bits = am.bits1 if layer == 1 and isinstance(am, PassState) else None
+        bits = am.bits[layer - 1] if isinstance(am, PassState) else None
         if isinstance(x, RolloutRows):
             assert layer == 1 and self.uses_split("fwd", 1)
             native.nature_conv_fwd_split(1, x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y, amax_y=out_am,
@@ -308,7 +313,7 @@ class NatureConvs:
         self.pack(B)  # the conv2 dgrad form depends on the batch
         g_am, out_am = (am[AM_G3], am[AM_G2]) if layer == 3 else (am[AM_G2], am[AM_G1])
         if self.uses_split("dgrad", layer, B):
-            bits = am.bits1 if layer == 2 and isinstance(am, PassState) else None
+            bits = am.bits[layer - 2] if isinstance(am, PassState) else None
             native.nature_conv_dgrad_split(layer, g, B, self.q[10 + layer], prev_act, out, amax_g=g_am,
                                            amax_out=out_am, relu_bits=bits)
         else:
@@ -342,10 +347,14 @@ class NatureConvs:
         h1 = torch.empty((B, 20, 20, 32), device=dev)
         h2 = torch.empty((B, 9, 9, 64), device=dev)
         h3 = torch.empty((B, 7, 7, 64) if self.nhwc3 else (B, 64, 7, 7), device=dev)
-        # conv1's ReLU bitmask when both its forward and the conv2 dgrad run split (training passes)
-        bits1 = torch.empty(B * 400, dtype=torch.int32, device=dev) \
-            if train and self.uses_split("fwd", 1) and self.uses_split("dgrad", 2, B) else None
-        am = PassState(native.amax_table(AM_ROWS, dev), bits1)
+        # the conv outputs' ReLU bitmasks where the forward and the consumer of the mask (the next
+        # layer's dgrad; for conv3 the fc dgrad) both run split (training passes)
+        consumer = (self.uses_split("dgrad", 2, B), self.uses_split("dgrad", 3, B),
+                    self.nhwc3 and B < FC_DGRAD_FUSED_MAX_BATCH)
+        bits = tuple(torch.empty(B * P * C // 32, dtype=torch.int32, device=dev)
+                     if train and RELU_BITS and self.uses_split("fwd", L) and consumer[L - 1] else None
+                     for L, P, C in ((1, 400, 32), (2, 81, 64), (3, 49, 64)))
+        am = PassState(native.amax_table(AM_ROWS, dev), bits)
         if B:
             self.fwd(1, x, B, self.c1.bias, h1, am)
             self.fwd(2, h1, B, self.c2.bias, h2, am)
@@ -380,7 +389,8 @@ class NatureConvs:
         am[AM_DF]), h3 NHWC; records g3's amax."""
         B = df.shape[0]
         g3 = torch.empty((B, 7, 7, 64), device=df.device)
-        native.nature_fc_dgrad(df.contiguous(), B, self.qfc[1], h3, g3, amax_df=am[AM_DF], amax_g3=am[AM_G3])
+        native.nature_fc_dgrad(df.contiguous(), B, self.qfc[1], h3, g3, amax_df=am[AM_DF], amax_g3=am[AM_G3],
+                               relu_bits=am.bits[2] if isinstance(am, PassState) else None)
         return g3
 
     def backward_acts(self, x, h1, h2, h3, dh3, dw1, db1, dw2, db2, dw3, db3, g3=None, am=None):

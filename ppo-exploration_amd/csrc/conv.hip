@@ -906,10 +906,15 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
     if (late && nchunk > 0) mfma3(daf, dbf);
     sg_vm_wait<0>();  // the clamped tail DMAs, before the LDS is released
     // epilogue, per column tile: its operand loads first (all issued before its first store);
-    // om = the largest |value| this lane stored
+    // om = the largest |value| this lane stored.  BITS_OUT: the ReLU bitmask word of tile row L and
+    // column tile j is half (L >> 2) & 1 of the ballot of element q = (L & 3) + 4 (L >> 3) — lane L
+    // (< 32) collects both words of its row and stores them together
     float om = 0.f;
+    uint32_t bw[NT];
+    const int qL = (lane & 3) + 4 * ((lane >> 3) & 3), hL = (lane >> 2) & 1;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
+        bw[j] = 0u;
         decltype(Prob::prefetch(a, t, 0, 0)) e[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) e[q] = Prob::prefetch(a, t, wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, j * 32 + r);
@@ -918,9 +923,22 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
         // inside every one of them — behind every earlier store
         __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
-            om = fmaxf(om, fabsf(Prob::store_pre(a, t, wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, j * 32 + r,
-                                                 (hi[j][q] + lo[j][q]) * ua * uw, e[q])));
+        for (int q = 0; q < 16; ++q) {
+            const float v = Prob::store_pre(a, t, wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, j * 32 + r,
+                                            (hi[j][q] + lo[j][q]) * ua * uw, e[q]);
+            om = fmaxf(om, fabsf(v));
+            if constexpr (Prob::BITS_OUT) {
+                if (a.bits_y) {  // uniform
+                    const unsigned long long b = __ballot(v > 0.f);
+                    bw[j] = qL == q ? (uint32_t)(hL ? b >> 32 : b) : bw[j];
+                }
+            }
+        }
+    }
+    if constexpr (Prob::BITS_OUT) {
+        static_assert(NT == 2, "bitmask: 64 channels = two words per pixel");
+        const long long m = t.m0 + wave * 32 + lane;
+        if (a.bits_y && lane < 32 && m < t.M) *reinterpret_cast<uint2*>(a.bits_y + m * 2) = make_uint2(bw[0], bw[1]);
     }
     amax_record(a.amax_y, om);
 }
@@ -944,6 +962,7 @@ int launch_sgemm(const Args& a, const uint16_t* wq, long long blocks, hipStream_
 template <class L, bool OUT_NCHW>
 struct SgFwd : FwdNHWCProblem<L, OUT_NCHW, 1> {
     static constexpr int ROWS = SG_ROWS, CPT = L::CIN / BK;
+    static constexpr bool BITS_OUT = true;  // a.bits_y: the output's ReLU bitmask (2 words per pixel)
     __device__ static bool tile(const Args& a, RowTile& t) {
         t.m0 = xcd_remap(blockIdx.x, gridDim.x) * ROWS;
         t.M = a.batch * L::P;
@@ -962,10 +981,23 @@ struct SgFwd : FwdNHWCProblem<L, OUT_NCHW, 1> {
     }
 };
 
-template <class L>
+// BITS_IN: the ReLU mask of the layer below from its forward's bitmask (a.bits_mask, CIN / 32
+// words per pixel) instead of its f32 activations
+template <class L, bool BITS_IN = false>
 struct SgDgradPM : DgradPMProblem<L, 1> {
     using Base = DgradPMProblem<L, 1>;
     static constexpr int ROWS = SG_ROWS, NPOS = Base::NPOS, CPT = Base::CPT;
+    static constexpr bool BITS_OUT = false;
+    __device__ static float prefetch(const Args& a, const PixelTile& t, int row, int ci) {
+        if constexpr (!BITS_IN) {
+            return Base::prefetch(a, t, row, ci);
+        } else {
+            long long n = t.n0 + row;
+            n = n < a.batch ? n : t.n0;
+            const uint32_t w = a.bits_mask[(n * NPOS + t.pos) * (L::CIN / 32) + (ci >> 5)];
+            return (float)((w >> (ci & 31)) & 1u);
+        }
+    }
     __device__ static bool tile(const Args& a, PixelTile& t) {
         const long long w = xcd_remap(blockIdx.x, gridDim.x);
         t.n0 = (w / NPOS) * ROWS;
@@ -995,10 +1027,24 @@ struct SgDgradPM : DgradPMProblem<L, 1> {
 // the group — so the workgroups an XCD runs together share one A row tile, and one group's B
 // (G x 196 KB / 1.2 MB for the dgrad / forward) stays in that XCD's L2 while its row tiles
 // stream past (A is read NCB / G times, B about once per XCD).
-template <int K, int N, int MODE, int G>
+// BITS_IN (FC_DGRAD): h3's ReLU mask from the conv3 forward's bitmask (N / 32 words per row)
+template <int K, int N, int MODE, int G, bool BITS_IN = false>
 struct SgRows : GemmRowsProblem<K, N, 64, MODE> {
     using Base = GemmRowsProblem<K, N, 64, MODE>;
     static constexpr int ROWS = SG_ROWS, NCB = Base::NCB;
+    static constexpr bool BITS_OUT = false;
+    __device__ static auto prefetch(const Args& a, const GemmTile& t, int row, int col) {
+        if constexpr (!BITS_IN) {
+            return Base::prefetch(a, t, row, col);
+        } else {
+            static_assert(MODE == FC_DGRAD && N % 32 == 0, "bitmask: the fc dgrad's h3 mask");
+            const int n = t.cb * 64 + col, nc = n < N ? n : N - 1;
+            long long m = t.m0 + row;
+            m = m < t.M ? m : t.m0;
+            const uint32_t w = a.bits_mask[m * (N / 32) + (nc >> 5)];
+            return (float)((w >> (nc & 31)) & 1u);
+        }
+    }
     __device__ static bool tile(const Args& a, GemmTile& t) {
         const long long w = xcd_remap(blockIdx.x, gridDim.x);
         const long long rt = (a.batch + ROWS - 1) / ROWS;      // row tiles
@@ -1025,6 +1071,7 @@ template <int K, int N, int S>
 struct SgRowsSK : GemmRowsProblem<K, N, 64, FC_FWD> {
     using Base = GemmRowsProblem<K, N, 64, FC_FWD>;
     static constexpr int ROWS = SG_ROWS, NCB = Base::NCB, KC = Base::KC;
+    static constexpr bool BITS_OUT = false;
     struct Tile {
         long long m0, M;
         int cb, ks, c0, nc;
@@ -2387,10 +2434,12 @@ long long planes(int which) {
 }
 
 int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq, const float* bias, float* y,
-                const uint32_t* amax_x, uint32_t* amax_y, hipStream_t s) {
+                const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, hipStream_t s) {
     PPOX_REQUIRE(ppox::aligned16(x), "ppox_nature_conv_fwd_split: layer 2/3 input must be 16B-aligned NHWC");
     PPOX_REQUIRE(amax_x && ppox::aligned16(amax_x), "ppox_nature_conv_fwd_split: amax slots of x required (layer 2/3)");
+    PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(relu_bits) & 7), "ppox_nature_conv_fwd_split: relu_bits 8B alignment");
     Args a{x, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch, amax_x, amax_y, pack_exp(wq, planes(layer))};
+    a.bits_y = relu_bits;
     if (layer == 2)
         return launch_sgemm<SgFwd<G2, false>>(a, wq, ppox::ceil_div(batch * G2::P, SG_ROWS), s,
                                               "ppox_nature_conv_fwd_split");
@@ -2406,7 +2455,7 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
     PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad_split: layer must be 2 or 3");
     PPOX_REQUIRE(grad_out && wqd && (prev_act || relu_bits) && grad_in && amax_g && batch >= 0,
                  "ppox_nature_conv_dgrad_split: bad arguments");
-    PPOX_REQUIRE(!relu_bits || layer == 2, "ppox_nature_conv_dgrad_split: relu_bits is for layer 2 (conv1's mask)");
+    // relu_bits: the ReLU bitmask of the layer below (conv1's for layer 2, conv2's for layer 3)
     PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wqd) && ppox::aligned16(amax_g),
                  "ppox_nature_conv_dgrad_split: 16B alignment");
     Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch, amax_g, amax_out,
@@ -2431,6 +2480,10 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
             dgrad2_colp_kernel<false><<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd), ntriples);
         PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
     }
+    a.bits_mask = relu_bits;
+    if (relu_bits)
+        return launch_sgemm<SgDgradPM<G3, true>>(a, wqd, ppox::ceil_div(batch, SG_ROWS) * SgDgradPM<G3>::NPOS, s,
+                                                 "ppox_nature_conv_dgrad_split");
     return launch_sgemm<SgDgradPM<G3>>(a, wqd, ppox::ceil_div(batch, SG_ROWS) * SgDgradPM<G3>::NPOS, s,
                                        "ppox_nature_conv_dgrad_split");
 }
@@ -2575,12 +2628,18 @@ extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const u
 }
 
 extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
-                                    const uint32_t* amax_df, uint32_t* amax_g3, void* stream) {
+                                    const uint32_t* amax_df, uint32_t* amax_g3, const uint32_t* relu_bits,
+                                    void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
-    PPOX_REQUIRE(df && q_dgrad && h3 && g3 && amax_df && batch >= 0, "ppox_nature_fc_dgrad: bad arguments");
+    PPOX_REQUIRE(df && q_dgrad && (h3 || relu_bits) && g3 && amax_df && batch >= 0,
+                 "ppox_nature_fc_dgrad: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(q_dgrad) && ppox::aligned16(amax_df),
                  "ppox_nature_fc_dgrad: 16B alignment");
     Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch, amax_df, amax_g3, pack_exp(q_dgrad, PL_FCD)};
+    a.bits_mask = relu_bits;  // h3's ReLU bitmask from the conv3 forward (instead of h3)
+    if (relu_bits)
+        return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_G, true>>(
+            a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB, ppox::as_stream(stream), "ppox_nature_fc_dgrad");
     return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_G>>(a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB,
                                                      ppox::as_stream(stream), "ppox_nature_fc_dgrad");
 }

@@ -33,8 +33,8 @@ struct Args {
     const uint32_t* amax_x = nullptr;
     uint32_t* amax_y = nullptr;
     const int* wexp = nullptr;
-    // ReLU bitmasks (bit c of word p: activation channel c of pixel p > 0): written by the conv1
-    // split forward (bits_y), read by the conv2 split dgrad instead of the f32 mask (bits_mask)
+    // ReLU bitmasks (bit c of word p * (C / 32) + c / 32: channel c of pixel p > 0): written by the
+    // split forwards (bits_y), read by the split dgrads instead of the f32 mask (bits_mask)
     uint32_t* bits_y = nullptr;
     const uint32_t* bits_mask = nullptr;
 };
@@ -320,5 +320,5 @@ int pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1, 
                uint16_t* qd2, uint16_t* qd3, hipStream_t s);
 long long planes(int which);  // uint16 planes of a split-packed form (1, 2, 3, 12, 13; 4 = fc)
 int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq, const float* bias, float* y,
-                const uint32_t* amax_x, uint32_t* amax_y, hipStream_t s);
+                const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, hipStream_t s);
 }  // namespace ppox_conv

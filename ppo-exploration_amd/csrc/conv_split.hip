@@ -177,8 +177,7 @@ extern "C" int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t 
     PPOX_REQUIRE(ppox::aligned16(wq), "ppox_nature_conv_fwd_split: packed weights must be 16-byte aligned");
     if (layer != 1) {
         PPOX_REQUIRE(!idx, "ppox_nature_conv_fwd_split: idx is for layer 1 only");
-        PPOX_REQUIRE(!relu_bits, "ppox_nature_conv_fwd_split: relu_bits is for layer 1 only");
-        return ppox_conv::split_fwd23(layer, x, batch, wq, bias, y, amax_x, amax_y, ppox::as_stream(stream));
+        return ppox_conv::split_fwd23(layer, x, batch, wq, bias, y, amax_x, amax_y, relu_bits, ppox::as_stream(stream));
     }
     PPOX_REQUIRE(!amax_x, "ppox_nature_conv_fwd_split: layer 1 reads uint8 frames (no amax_x)");
     PPOX_REQUIRE(batch * G1::P < (1LL << 31), "ppox_nature_conv_fwd_split: batch too large for 32-bit rows");

@@ -76,7 +76,7 @@ SIGNATURES = {
     "ppox_head_hidden_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
-    "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_es_noise": [_i64, _i64, _i64, _i64, _u64, _vp, _vp],
     "ppox_es_env_noise": [_i32, _i32, _u64, _vp, _vp],
@@ -510,7 +510,7 @@ def nature_pack_split(w1, w2, w3, q1, q2, q3, qd2=None, qd3=None, stream=None):
 def nature_conv_fwd_split(layer, x, batch, idx, T, N_env, x_sample_stride, wq, bias, y, amax_x=None, amax_y=None,
                           relu_bits=None, stream=None):
     """amax_x: x's slots (layers 2, 3; computed here when None); amax_y: y's slots to record (or None);
-    relu_bits (layer 1): int32 (batch * 400) ReLU bitmask of y to write (or None)."""
+    relu_bits: int32 ReLU bitmask of y to write (batch * P * C / 32 words; or None)."""
     if layer != 1 and batch:
         amax_x = _amax_of(x, amax_x, stream)
     call("ppox_nature_conv_fwd_split", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
@@ -600,12 +600,13 @@ def nature_fc_fwd_splitk(h3, batch, q_fwd, bias, workspace, f, amax_h3=None, ama
          workspace.numel() * workspace.element_size(), _p(f), _p(amax_h3), _p(amax_f), stream_ptr(stream))
 
 
-def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, amax_df=None, amax_g3=None, stream=None):
-    """g3 (batch, 7, 7, 64) NHWC = ((df @ W) in Flatten order) * (h3 > 0); amax_g3: g3's slots to record."""
+def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, amax_df=None, amax_g3=None, relu_bits=None, stream=None):
+    """g3 (batch, 7, 7, 64) NHWC = ((df @ W) in Flatten order) * (h3 > 0); amax_g3: g3's slots to record;
+    relu_bits: h3's ReLU bitmask from the conv3 split forward (used instead of h3)."""
     if batch:
         amax_df = _amax_of(df, amax_df, stream)
     call("ppox_nature_fc_dgrad", _p(df), int(batch), _p(q_dgrad), _p(h3), _p(g3), _p(amax_df), _p(amax_g3),
-         stream_ptr(stream))
+         _p(relu_bits), stream_ptr(stream))
 
 
 def nature_fc_wgrad_workspace_bytes(batch):
@@ -735,7 +736,7 @@ def nature_conv_wgrad_split_idx(layer, x, batch, idx, T, N_env, grad_out, worksp
 def nature_conv_dgrad_split(layer, grad_out, batch, wqd, prev_act, grad_in, amax_g=None, amax_out=None,
                             relu_bits=None, stream=None):
     """amax_g: grad_out's slots (computed here when None); amax_out: grad_in's slots to record (or None);
-    relu_bits (layer 2): conv1's ReLU bitmask from its split forward, used instead of prev_act."""
+    relu_bits: the ReLU bitmask of the layer below from its split forward, used instead of prev_act."""
     if batch:
         amax_g = _amax_of(grad_out, amax_g, stream)
     call("ppox_nature_conv_dgrad_split", int(layer), _p(grad_out), int(batch), _p(wqd), _p(prev_act), _p(grad_in),

@@ -625,6 +625,43 @@ def test_conv1_relu_bits_drive_conv2_dgrad(B):
     assert torch.equal(o_act, o_bits)
 
 
+@pytest.mark.parametrize("B", [1, 7, 300])
+def test_conv23_relu_bits_drive_dgrad3_and_fc_dgrad(B):
+    """The conv2 / conv3 split forwards' ReLU bitmasks (2 words per pixel, 64 channels) equal
+    h > 0, and the conv3 dgrad / fc dgrad reading them equal the ones reading h2 / h3, bitwise."""
+    import native
+    torch.manual_seed(B + 11)
+    w1 = torch.randn(32, 4, 8, 8, device="cuda") * 0.02
+    w2 = torch.randn(64, 32, 4, 4, device="cuda") * 0.05
+    w3 = torch.randn(64, 64, 3, 3, device="cuda") * 0.05
+    q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device="cuda") for k in (1, 2, 3, 12, 13)}
+    native.nature_pack_split(w1, w2, w3, q[1], q[2], q[3], q[12], q[13])
+    h1 = torch.relu(torch.randn(B, 20, 20, 32, device="cuda"))
+    b2, b3 = torch.randn(64, device="cuda") * 0.1, torch.randn(64, device="cuda") * 0.1
+    h2, h3 = torch.empty(B, 9, 9, 64, device="cuda"), torch.empty(B, 7, 7, 64, device="cuda")
+    bits2 = torch.full((B * 81 * 2 + 2,), 777, dtype=torch.int32, device="cuda")
+    bits3 = torch.full((B * 49 * 2 + 2,), 777, dtype=torch.int32, device="cuda")
+    native.nature_conv_fwd_split(2, h1, B, None, 0, 0, 0, q[2], b2, h2, relu_bits=bits2)
+    native.nature_conv_fwd_split(3, h2, B, None, 0, 0, 0, q[3], b3, h3, relu_bits=bits3)
+    for h, bits, P in ((h2, bits2, 81), (h3, bits3, 49)):
+        want = ((h > 0).view(B * P * 2, 32).long() << torch.arange(32, device="cuda")).sum(1)
+        assert torch.equal(bits[:-2].long() & 0xFFFFFFFF, want) and bits[-2:].tolist() == [777, 777]
+    g3 = torch.randn(B, 7, 7, 64, device="cuda")
+    o_act, o_bits = torch.empty_like(h2), torch.empty_like(h2)
+    native.nature_conv_dgrad_split(3, g3, B, q[13], h2, o_act)
+    native.nature_conv_dgrad_split(3, g3, B, q[13], None, o_bits, relu_bits=bits2)
+    assert torch.equal(o_act, o_bits)
+    W = torch.randn(512, 3136, device="cuda") * 0.02
+    n = native.nature_fc_pack_elems()
+    qf, qd = torch.empty(n, dtype=torch.int16, device="cuda"), torch.empty(n, dtype=torch.int16, device="cuda")
+    native.nature_fc_pack(W, qf, qd)
+    df = torch.randn(B, 512, device="cuda")
+    f_act, f_bits = torch.empty_like(h3), torch.empty_like(h3)
+    native.nature_fc_dgrad(df, B, qd, h3, f_act)
+    native.nature_fc_dgrad(df, B, qd, None, f_bits, relu_bits=bits3)
+    assert torch.equal(f_act, f_bits)
+
+
 @pytest.mark.parametrize("intrinsic,B", [(False, 40), (True, 40), (False, 600)])
 def test_cnn_explicit_backward_matches_autograd(intrinsic, B):
     """CnnActorCritic.forward_train/backward_train (no autograd graph, grads straight into
