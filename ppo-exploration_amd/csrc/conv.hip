@@ -946,12 +946,21 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
 #ifndef SG_WAVES
 #define SG_WAVES 4  // 4: two 128-row workgroups per CU (2 ring slots); 8: one 256-row workgroup (3 slots)
 #endif
-constexpr int SG_ROWS = 32 * SG_WAVES, SG_SLOTS = SG_WAVES == 8 ? 3 : 2;
+// ring slots (chunks in flight + 1) per Problem (Prob::SLOTS): 3 for the plain fc / head GEMMs
+// (their DMA latency was exposed with one chunk of lookahead: fc forward 0.190 -> 0.174 ms,
+// dgrad 0.255 -> 0.238), 2 for the conv forms (3 measured slower for the conv3 dgrad, 0.31 ->
+// 0.34 ms); 3 x 24 KB per workgroup keeps two workgroups per CU.  SG_SLOTS overrides all.
+constexpr int SG_ROWS = 32 * SG_WAVES;
 
 template <class Prob>
 int launch_sgemm(const Args& a, const uint16_t* wq, long long blocks, hipStream_t s, const char* name) {
     if (blocks == 0) return PPOX_OK;
-    sgemm_kernel<Prob, SG_WAVES, SG_SLOTS><<<(unsigned)blocks, 64 * SG_WAVES, 0, s>>>(
+#ifdef SG_SLOTS
+    constexpr int slots = SG_SLOTS;
+#else
+    constexpr int slots = SG_WAVES == 8 ? 3 : Prob::SLOTS;
+#endif
+    sgemm_kernel<Prob, SG_WAVES, slots><<<(unsigned)blocks, 64 * SG_WAVES, 0, s>>>(
         a, reinterpret_cast<const u32x4*>(wq));
     PPOX_LAUNCHED(name);
 }
@@ -963,6 +972,7 @@ template <class L, bool OUT_NCHW>
 struct SgFwd : FwdNHWCProblem<L, OUT_NCHW, 1> {
     static constexpr int ROWS = SG_ROWS, CPT = L::CIN / BK;
     static constexpr bool BITS_OUT = true;  // a.bits_y: the output's ReLU bitmask (2 words per pixel)
+    static constexpr int SLOTS = 2;
     __device__ static bool tile(const Args& a, RowTile& t) {
         t.m0 = xcd_remap(blockIdx.x, gridDim.x) * ROWS;
         t.M = a.batch * L::P;
@@ -988,6 +998,7 @@ struct SgDgradPM : DgradPMProblem<L, 1> {
     using Base = DgradPMProblem<L, 1>;
     static constexpr int ROWS = SG_ROWS, NPOS = Base::NPOS, CPT = Base::CPT;
     static constexpr bool BITS_OUT = false;
+    static constexpr int SLOTS = 2;
     __device__ static float prefetch(const Args& a, const PixelTile& t, int row, int ci) {
         if constexpr (!BITS_IN) {
             return Base::prefetch(a, t, row, ci);
@@ -1033,6 +1044,7 @@ struct SgRows : GemmRowsProblem<K, N, 64, MODE> {
     using Base = GemmRowsProblem<K, N, 64, MODE>;
     static constexpr int ROWS = SG_ROWS, NCB = Base::NCB;
     static constexpr bool BITS_OUT = false;
+    static constexpr int SLOTS = 3;
     __device__ static auto prefetch(const Args& a, const GemmTile& t, int row, int col) {
         if constexpr (!BITS_IN) {
             return Base::prefetch(a, t, row, col);
@@ -1072,6 +1084,7 @@ struct SgRowsSK : GemmRowsProblem<K, N, 64, FC_FWD> {
     using Base = GemmRowsProblem<K, N, 64, FC_FWD>;
     static constexpr int ROWS = SG_ROWS, NCB = Base::NCB, KC = Base::KC;
     static constexpr bool BITS_OUT = false;
+    static constexpr int SLOTS = 3;
     struct Tile {
         long long m0, M;
         int cb, ks, c0, nc;

@@ -219,31 +219,32 @@ __host__ __device__ inline int split_scale_exp(uint32_t amax_bits) {
 }
 __host__ __device__ inline float exp2i(int e) { return __builtin_bit_cast(float, (uint32_t)(e + 127) << 23); }
 
-// two f32 (already scaled) -> their f16 high and low planes, packed f16x2 words (x0 low).  The
-// residual x - h is one v_fma_mix_f32 per value (h read as f16 straight from the packed word, times
-// -1, plus x: exact, so its single rounding is none); hipcc would emit a convert and a subtract
-__device__ inline void split2h(float x0, float x1, uint32_t& h, uint32_t& l) {
-    const f32x2 v = {x0, x1};
+// two f32 values times s -> their f16 high and low planes, packed f16x2 words (x.x low).  The
+// scale is one v_pk_mul_f32 per pair; the residual x s - h is one v_fma_mix_f32 per value (h read
+// as f16 straight from the packed word, times -1, plus x s: exact, so its rounding is none) —
+// hipcc would emit a convert and a subtract
+__device__ inline void split2h(f32x2 x, float s, uint32_t& h, uint32_t& l) {
+    const f32x2 v = x * (f32x2){s, s};
     h = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));
     float r0, r1;
-    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r0) : "v"(h), "v"(x0));
-    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r1) : "v"(h), "v"(x1));
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r0) : "v"(h), "v"(v.x));
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r1) : "v"(h), "v"(v.y));
     l = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){r0, r1}, f16x2));
 }
 // eight f32 times s -> their two f16 planes as MFMA fragments (element e = value e)
 __device__ inline void split8h(const float4& v0, const float4& v1, float s, u32x4& p0, u32x4& p1) {
     uint32_t h[4], l[4];
-    split2h(v0.x * s, v0.y * s, h[0], l[0]);
-    split2h(v0.z * s, v0.w * s, h[1], l[1]);
-    split2h(v1.x * s, v1.y * s, h[2], l[2]);
-    split2h(v1.z * s, v1.w * s, h[3], l[3]);
+    split2h((f32x2){v0.x, v0.y}, s, h[0], l[0]);
+    split2h((f32x2){v0.z, v0.w}, s, h[1], l[1]);
+    split2h((f32x2){v1.x, v1.y}, s, h[2], l[2]);
+    split2h((f32x2){v1.z, v1.w}, s, h[3], l[3]);
     p0 = u32x4{h[0], h[1], h[2], h[3]};
     p1 = u32x4{l[0], l[1], l[2], l[3]};
 }
 // four f32 times s -> two f16 planes, two f16x2 words each
 __device__ inline void split4h(const float4& v, float s, uint2& p0, uint2& p1) {
-    split2h(v.x * s, v.y * s, p0.x, p1.x);
-    split2h(v.z * s, v.w * s, p0.y, p1.y);
+    split2h((f32x2){v.x, v.y}, s, p0.x, p1.x);
+    split2h((f32x2){v.z, v.w}, s, p0.y, p1.y);
 }
 // one f32 (scaled) -> its two f16 planes (the weight packers)
 __device__ inline void split1h(float v, uint16_t& h, uint16_t& l) {
