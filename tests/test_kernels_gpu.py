@@ -1010,3 +1010,34 @@ def test_stream_ptr_is_torch_current_stream():
     with torch.cuda.stream(s):
         assert raw(native.stream_ptr()) == s.cuda_stream == torch.cuda.current_stream().cuda_stream != 0
     assert raw(native.stream_ptr(s)) == s.cuda_stream
+
+
+@pytest.mark.parametrize("B", [8192, 9001])
+def test_conv3_wgrad_split_big_batch_vs_fp64(B):
+    """conv3 weight gradient at training-size batches (392-441 split-K slices of ~2048 pixels, 9
+    k-blocks) vs float64 on the device: error no larger than an f32 GEMM's (x2 headroom), a ragged
+    batch, the bias grad, and bitwise run-to-run determinism."""
+    import native
+    torch.manual_seed(B)
+    h2 = torch.relu(torch.randn(B, 9, 9, 64, device="cuda"))
+    g3 = torch.randn(B, 7, 7, 64, device="cuda") * (torch.rand(B, 7, 7, 64, device="cuda") > 0.4)
+    ws = torch.empty(native.nature_wgrad_split_workspace_bytes(3, B), dtype=torch.uint8, device="cuda")
+    dw = torch.full((64, 64, 3, 3), float("nan"), device="cuda")
+    db = torch.full((64,), float("nan"), device="cuda")
+    native.nature_conv_wgrad_split(3, h2, B, 0, g3, ws, dw, db)
+
+    def ref(dt):  # dW[co][ci][ky][kx] = sum_(n, p) im2col(h2)[n, p, (ci, ky, kx)] g3[n, p, co]
+        cols = torch.nn.functional.unfold(h2.permute(0, 3, 1, 2).to(dt), 3)  # (B, 576, 49)
+        g = g3.reshape(B, 49, 64).to(dt)
+        return torch.einsum("bkp,bpc->ck", cols, g).reshape(64, 64, 3, 3)
+    r64, r32 = ref(torch.float64), ref(torch.float32)
+    scale = r64.abs().max()
+    e_s = (dw.double() - r64).abs().max() / scale
+    e_f = (r32.double() - r64).abs().max() / scale
+    assert torch.isfinite(dw).all()
+    assert e_s <= 2 * e_f + 1e-7, (float(e_s), float(e_f))
+    rb = g3.double().sum(dim=(0, 1, 2))
+    assert ((db.double() - rb).abs().max() / rb.abs().max()).item() < 1e-5
+    dw2, db2 = torch.empty_like(dw), torch.empty_like(db)
+    native.nature_conv_wgrad_split(3, h2, B, 0, g3, ws, dw2, db2)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
