@@ -1041,3 +1041,60 @@ def test_conv3_wgrad_split_big_batch_vs_fp64(B):
     dw2, db2 = torch.empty_like(dw), torch.empty_like(db)
     native.nature_conv_wgrad_split(3, h2, B, 0, g3, ws, dw2, db2)
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("B", [8192, 9001])
+def test_sg2_conv_big_batch_vs_fp64(B):
+    """The sg2 split kernels at training-size batches: conv2 / conv3 forward (bias + ReLU, NHWC)
+    and the conv3 dgrad (x ReLU mask of h2) vs float64 on the device, error no larger than the
+    same math in f32 (x2 headroom), a ragged batch, bitwise run-to-run determinism, and each
+    forward's ReLU bitmask."""
+    import native
+    F = torch.nn.functional
+    torch.manual_seed(B)
+    w1 = torch.randn(32, 4, 8, 8, device="cuda") * 0.05
+    w2 = torch.randn(64, 32, 4, 4, device="cuda") * 0.05
+    w3 = torch.randn(64, 64, 3, 3, device="cuda") * 0.05
+    b2, b3 = torch.randn(64, device="cuda") * 0.1, torch.randn(64, device="cuda") * 0.1
+    q = [torch.empty(native.nature_split_pack_elems(L), dtype=torch.int16, device="cuda") for L in (1, 2, 3)]
+    qd3 = torch.empty(native.nature_split_pack_elems(13), dtype=torch.int16, device="cuda")
+    native.nature_pack_split(w1, w2, w3, q[0], q[1], q[2], None, qd3)
+    h1 = torch.randn(B, 20, 20, 32, device="cuda").relu()
+    h2 = torch.randn(B, 9, 9, 64, device="cuda").relu()
+    g3 = torch.randn(B, 7, 7, 64, device="cuda")
+
+    def fwd_ref(x, w, b, k, s, dt):  # NHWC in -> NHWC out, relu(conv + b)
+        cols = F.unfold(x.permute(0, 3, 1, 2).to(dt), k, stride=s)  # (B, CIN k k, P)
+        y = torch.einsum("ck,bkp->bpc", w.reshape(64, -1).to(dt), cols) + b.to(dt)
+        return y.relu()
+
+    def dgrad3_ref(dt):
+        cg = torch.einsum("ck,bpc->bkp", w3.reshape(64, -1).to(dt), g3.reshape(B, 49, 64).to(dt))
+        return F.fold(cg, (9, 9), 3).permute(0, 2, 3, 1) * (h2 > 0).to(dt)
+
+    def check(got, r64, r32):
+        scale = r64.abs().max()
+        e_s = (got.double() - r64).abs().max() / scale
+        e_f = (r32.double() - r64).abs().max() / scale
+        assert torch.isfinite(got).all()
+        assert e_s <= 2 * e_f + 1e-7, (float(e_s), float(e_f))
+
+    for layer, x, w, b, k, s, P in ((2, h1, w2, b2, 4, 2, 81), (3, h2, w3, b3, 3, 1, 49)):
+        ys = []
+        for _ in range(2):
+            y = torch.full((B, P, 64), float("nan"), device="cuda")
+            bits = torch.zeros(B * P * 2, dtype=torch.int32, device="cuda")
+            native.nature_conv_fwd_split(layer, x, B, None, 0, 0, 0, q[layer - 1], b, y, relu_bits=bits)
+            ys.append((y, bits))
+        check(ys[0][0], fwd_ref(x, w, b, k, s, torch.float64), fwd_ref(x, w, b, k, s, torch.float32))
+        assert torch.equal(ys[0][0], ys[1][0])
+        words = ys[0][1].view(torch.int64).view(B * P, 1)  # bit c of the pixel's 64-bit pair = channel c > 0
+        want = ((ys[0][0].reshape(B * P, 64) > 0).long() << torch.arange(64, device="cuda")).sum(1, keepdim=True)
+        assert torch.equal(words, want)
+    ds = []
+    for _ in range(2):
+        d = torch.full((B, 9, 9, 64), float("nan"), device="cuda")
+        native.nature_conv_dgrad_split(3, g3, B, qd3, h2, d)
+        ds.append(d)
+    check(ds[0], dgrad3_ref(torch.float64), dgrad3_ref(torch.float32))
+    assert torch.equal(ds[0], ds[1])
