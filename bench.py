@@ -38,89 +38,119 @@ def pmc_traffic(kernel):
     return (None, None) if d is None else (d["hbm_bytes_per_launch_corrected"], os.path.relpath(files[-1], ROOT))
 
 
-# K6 conv ops: MACs per sample and activation bytes per sample
-# (layer input 0 = the u8 frame stack, 28,224 B; f32 NHWC activations after)
+# The MFMA kernels of the NatureCNN training pass (K6 convs, K10 fc layer and the heads' hidden
+# layer), keyed by their event-timing name (native.enable_event_timing).  Per row (sample) of a
+# launch: MACs and algorithmic HBM bytes; `fixed` = bytes per launch independent of
+# the row count (weights in, weight gradient out); `products` = f16 MFMA products per f32 MAC of
+# the split-f16 form (2 when one operand is the exact u8 frame); `rows_arg` = the entry point's
+# argument holding the row count; `rocprof` = the kernel's rocprofv3 name (PMC lookup).
 CONV_MAC = {1: 400 * 256 * 32, 2: 81 * 512 * 64, 3: 49 * 576 * 64}
 ACT_B = {0: 28224, 1: 20 * 20 * 32 * 4, 2: 9 * 9 * 64 * 4, 3: 7 * 7 * 64 * 4}
+BITMASK_B = {1: 400 * 4, 2: 81 * 4, 3: 49 * 4}   # a layer's ReLU bitmask (one u32 per pixel)
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA
-# rocprofv3 kernel names of the conv entry points (for the PMC traffic lookup)
-CONV_KERNEL = {("fwd", 1, True): "fwd1_split_kernel<1>",
-               ("fwd", 2, True): "sgemm_kernel<SgFwd<32, 20, 20, 4, 4, 2, 64, false>, 4, 2>",
-               ("fwd", 3, True): "sgemm_kernel<SgFwd<64, 9, 9, 3, 3, 1, 64, false>, 4, 2>",
-               ("dgrad", 2, False): "igemm_kernel<DgradPMProblem<32, 20, 20, 4, 4, 2, 64, 1>>",
-               ("dgrad", 2, True): "dgrad2_colp_kernel<true>",
-               ("dgrad", 3, True): "sgemm_kernel<SgDgradPM<64, 9, 9, 3, 3, 1, 64>, 4, 2>",
-               ("wgrad", 1, True): "wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>",
-               ("wgrad", 2, True): "wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128, false, 1>",
-               ("wgrad", 3, True): "wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64, false, 1>"}
+FC_K, FC_N, HID = 3136, 512, 512
 
 
-def conv_roofline(key, kt, totals, solo_kt=None):
-    """Roofline of the dominant conv launch: algorithmic FLOPs (2 x MACs x batch) per launch /
-    mean HIP-event duration.  The f32 kernels run v_mfma_f32_32x32x2_f32 (peak 157.3 TF/s);
-    the split-f16 kernels issue 3 f16 MFMA products per f32 MAC (2 when one operand is the
-    u8 frame), so their f32-equivalent peak is 2500 / 3 (or / 2) TF/s."""
+def _kernels():
+    k = {}
+    roc = {("fwd", 1): "fwd1_split_kernel<1>",
+           ("fwd", 2): "sgemm_kernel<SgFwd<32, 20, 20, 4, 4, 2, 64, false>, 4, 2>",
+           ("fwd", 3): "sgemm_kernel<SgFwd<64, 9, 9, 3, 3, 1, 64, false>, 4, 2>",
+           ("dgrad", 2): "dgrad2_colp_kernel<true>",
+           ("dgrad", 3): "sgemm_kernel<SgDgradPM<64, 9, 9, 3, 3, 1, 64, true>, 4, 2>",
+           ("wgrad", 1): "wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>",
+           ("wgrad", 2): "wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128, false, 1>",
+           ("wgrad", 3): "wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64, false, 1>"}
+    for op in ("fwd", "dgrad", "wgrad"):
+        for layer in (1, 2, 3):
+            if op == "dgrad" and layer == 1:
+                continue
+            for m in ("", "_split", "_split_idx"):
+                if m == "_split_idx" and (op != "wgrad" or layer != 1):
+                    continue
+                split = m != ""
+                # input + output (fwd); output grad + input grad + the input layer's ReLU mask
+                # (dgrad: the split kernels read the forward's bitmask); input + output grad (wgrad)
+                per = ACT_B[layer] + ACT_B[layer - 1]
+                if op == "dgrad":
+                    per += BITMASK_B[layer - 1] if split else ACT_B[layer - 1]
+                k[f"ppox_nature_conv_{op}{m}:{layer}"] = dict(
+                    rows_arg=2, macs=CONV_MAC[layer], bytes=per, fixed=0,
+                    products=(2 if layer == 1 and op != "dgrad" else 3) if split else 0,
+                    rocprof=roc.get((op, layer)) if split else None, label=f"conv{layer} {op}")
+    w_fc = FC_K * FC_N * 4          # weights in as two fp16 planes (= f32 bytes) / dW out in f32
+    k["ppox_nature_fc_fwd"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=ACT_B[3] + FC_N * 4, fixed=w_fc, products=3,
+                                   rocprof="sgemm_kernel<SgRows<3136, 512, 0, 8, false>, 4, 3>", label="fc fwd")
+    k["ppox_nature_fc_fwd_splitk"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=ACT_B[3] + FC_N * 4, fixed=w_fc,
+                                          products=3, rocprof=None, label="fc fwd split-K")
+    k["ppox_nature_fc_dgrad"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=FC_N * 4 + ACT_B[3] + BITMASK_B[3],
+                                     fixed=w_fc, products=3,
+                                     rocprof="sgemm_kernel<SgRows<512, 3136, 1, 12, true>, 4, 3>", label="fc dgrad")
+    k["ppox_nature_fc_wgrad"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=FC_N * 4 + ACT_B[3], fixed=w_fc, products=3,
+                                     rocprof="wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 49>",
+                                     label="fc wgrad")
+    w_h = HID * HID * 4
+    k["ppox_head_hidden_fwd"] = dict(rows_arg=1, macs=HID * HID, bytes=2 * HID * 4, fixed=w_h, products=3,
+                                     rocprof="sgemm_kernel<SgRows<512, 512, 0, 8, false>, 4, 3>",
+                                     label="head hidden fwd")
+    # dgrad: de in, the heads' input grad read + written (accumulated in place), f read for the ReLU
+    k["ppox_head_hidden_dgrad"] = dict(rows_arg=1, macs=HID * HID, bytes=4 * HID * 4, fixed=w_h, products=3,
+                                       rocprof="sgemm_kernel<SgRows<512, 512, 2, 8, false>, 4, 3>",
+                                       label="head hidden dgrad")
+    k["ppox_head_hidden_wgrad"] = dict(rows_arg=1, macs=HID * HID, bytes=2 * HID * 4, fixed=w_h, products=3,
+                                       rocprof="wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 8>",
+                                       label="head hidden wgrad")
+    return k
+
+
+KERNELS = _kernels()
+
+
+def _launch_rows(key, args):
+    return int(args[KERNELS[key]["rows_arg"]])
+
+
+def kernel_roofline(key, kt):
+    """Roofline of one MFMA kernel over its launches kt = [(ms, args)] of ONE row count:
+    algorithmic FLOPs (2 x MACs x rows) and bytes per launch / mean HIP-event duration.
+    The f32 kernels run v_mfma_f32_32x32x2_f32 (peak 157.3 TF/s); the split-f16 kernels issue
+    `products` f16 MFMA products per f32 MAC, so their f32-equivalent peak is 2500 / products.
+    The binding bound is the larger of the two lower bounds (MFMA work at its peak, the
+    algorithmic bytes at the HBM peak)."""
     import numpy as np
-    name, layer = key.split(":")
-    layer = int(layer)
-    op = name.replace("ppox_nature_conv_", "").replace("_split", "")
-    split = name.endswith("_split")
-    batch = float(np.mean([a[2] for _, a in kt]))
+    spec = KERNELS[key]
+    rows = _launch_rows(key, kt[0][1])
     mean_ms = float(np.mean([t for t, _ in kt]))
-    flops = 2.0 * CONV_MAC[layer] * batch
-    ach = flops / (mean_ms * 1e-3) / 1e12
-    products = (2 if (layer == 1 and op != "dgrad") else 3) if split else 1
-    peak = F16_MFMA_PEAK_TFLOPS / products if split else FP32_MFMA_PEAK_TFLOPS
-    # input + output (fwd), output grad + ReLU mask + input grad (dgrad), input + output grad (wgrad);
-    # the split conv2 dgrad reads conv1's ReLU mask as the forward's bitmask (4 B per pixel)
-    mask_b = 400 * 4 if (op == "dgrad" and layer == 2 and split) else ACT_B[layer - 1]
-    per = ACT_B[layer] + (ACT_B[layer - 1] + mask_b if op == "dgrad" else ACT_B[layer - 1])
-    kname = CONV_KERNEL.get((op, layer, split))
-    traffic, src = pmc_traffic(kname) if kname else (None, None)
-    tot = sum(totals.values()) or 1.0
-    # the binding roofline is the larger of the two lower bounds on the launch: MFMA work at
-    # the MFMA peak, or the algorithmic bytes at the HBM peak (conv2 dgrad moves 2.0 GB per
-    # 87 GFLOP at B = 16384: 252 us of HBM vs 104 us of split-f16 MFMA)
-    alg_bytes = batch * per
+    flops = 2.0 * spec["macs"] * rows
+    alg_bytes = float(spec["bytes"] * rows + spec["fixed"])
+    peak = F16_MFMA_PEAK_TFLOPS / spec["products"] if spec["products"] else FP32_MFMA_PEAK_TFLOPS
     t_mfma, t_hbm = flops / (peak * 1e12), alg_bytes / (HBM_PEAK_GBS * 1e9)
-    mfma_frac = ach / peak
-    hbm_ach = alg_bytes / (mean_ms * 1e-3) / 1e9
-    if t_hbm > t_mfma:
-        bound, a_val, p_val, unit = "hbm", round(hbm_ach, 1), HBM_PEAK_GBS, "GB/s"
-    else:
-        bound, a_val, p_val, unit = "mfma", round(ach, 2), round(peak, 1), "TFLOP/s"
-    return {"kernel": f"{name} layer {layer}" + (f" = {kname}" if kname else ""), "bound": bound,
-            "achieved": a_val, "peak": p_val, "unit": unit, "frac": round(a_val / p_val, 4),
-            "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)", "traffic_source": src,
+    tf = flops / (mean_ms * 1e-3) / 1e12
+    gbs = alg_bytes / (mean_ms * 1e-3) / 1e9
+    traffic, src = pmc_traffic(spec["rocprof"]) if spec["rocprof"] else (None, None)
+    hbm = t_hbm > t_mfma
+    return {"kernel": f"{spec['label']} ({key})" + (f" = {spec['rocprof']}" if spec["rocprof"] else ""),
+            "bound": "hbm" if hbm else "mfma",
+            "achieved": round(gbs, 1) if hbm else round(tf, 2), "peak": HBM_PEAK_GBS if hbm else round(peak, 1),
+            "unit": "GB/s" if hbm else "TFLOP/s", "frac": round((gbs / HBM_PEAK_GBS) if hbm else (tf / peak), 4),
+            "traffic": traffic, "traffic_source": src,
+            "traffic_ratio": round(traffic / alg_bytes, 3) if traffic else None,
+            "rows": rows, "launches": len(kt), "mean_us": round(mean_ms * 1e3, 1),
             "alg_bytes_per_launch": alg_bytes, "alg_flops_per_launch": flops,
-            "launches": len(kt), "mean_us": round(mean_ms * 1e3, 1),
-            "timing": ("HIP events around the timed region's launches on their stream; a launch that shares "
-                       "the GPU with side-stream kernels also counts its wait for CUs held by them (the "
-                       "persistent conv2 dgrad runs alone from 8192 rows: convs.BWD_SOLO_DGRAD2_BATCH)"),
-            "mfma_achieved_tflops": round(ach, 2), "mfma_peak_tflops": round(peak, 1), "mfma_frac": round(mfma_frac, 4),
-            "alg_hbm_GBs": round(hbm_ach, 1), "hbm_frac": round(hbm_ach / HBM_PEAK_GBS, 4),
+            "mfma_achieved_tflops": round(tf, 2), "mfma_peak_tflops": round(peak, 1), "mfma_frac": round(tf / peak, 4),
+            "alg_hbm_GBs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
             "lower_bound_us": {"mfma": round(t_mfma * 1e6, 1), "hbm": round(t_hbm * 1e6, 1)},
-            "share_of_conv_time": round(totals.get(key, 0.0) / tot, 3),
-            "selection": "largest total HIP-event time among the conv entry points in a one-stream warmup "
-                         "iteration; the timed launches run beside the side-stream weight gradients "
-                         "(convs.BWD_STREAMS), so mean_us includes any sharing of the GPU with them",
-            "peak_note": "f32 MFMA 157.3 TF/s" if not split else
-                         f"f16 MFMA 2500 TF/s / {products} products per f32 MAC (split-f16, fp32-class accuracy)",
-            # the same launches in the one-stream warmup iteration: the kernel alone on the GPU
-            "solo": _solo(solo_kt, flops / batch, alg_bytes / batch, peak, bound)}
+            "peak_note": (f"f16 MFMA 2500 TF/s / {spec['products']} products per f32 MAC (split-f16, fp32-class "
+                          "accuracy)") if spec["products"] else "f32 MFMA 157.3 TF/s"}
 
 
-def _solo(kt, flops_per_row, bytes_per_row, peak, bound):
-    import numpy as np
+def same_size(key, kt):
+    """The launches of the most frequent row count (a minibatch remainder is a different size)."""
+    from collections import Counter
     if not kt:
-        return None
-    ms = float(np.mean([t for t, _ in kt]))
-    rows = float(np.mean([a[2] for _, a in kt]))
-    tf = flops_per_row * rows / (ms * 1e-3) / 1e12
-    gbs = bytes_per_row * rows / (ms * 1e-3) / 1e9
-    return {"mean_us": round(ms * 1e3, 1), "launches": len(kt),
-            "frac": round(gbs / HBM_PEAK_GBS if bound == "hbm" else tf / peak, 4),
-            "mfma_frac": round(tf / peak, 4), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+        return []
+    rows = Counter(_launch_rows(key, a) for _, a in kt).most_common(1)[0][0]
+    return [(t, a) for t, a in kt if _launch_rows(key, a) == rows]
 
 
 def gae_kernel_ms(alg, dual, reps=20):
@@ -258,28 +288,31 @@ def main():
         alg.collect_samples()
         alg.train()
 
-    # the conv entry points (K6), timed with HIP events on their launch stream; the warmup
-    # iterations pick the dominant one (largest total time), the timed region times it
-    conv_keys = [f"ppox_nature_conv_{op}{m}:{l}" for op in ("fwd", "dgrad", "wgrad") for m in ("", "_split")
-                 for l in (1, 2, 3)]
-    native.enable_event_timing(conv_keys)
-    # the dominant kernel is picked from a warmup iteration on ONE stream: with the backward's
-    # weight gradients on a side stream (convs.BWD_STREAMS) concurrent launches stretch each
-    # other's event durations, so the pick would follow the overlap, not the kernel's own work;
-    # the remaining warmup and the timed region run as configured
+    # The roofline kernel is picked the way rocprofv3's per-kernel totals rank them: from the
+    # TRAINING launches of the first warmup iteration, run on ONE stream (with the backward's
+    # weight gradients on a side stream, concurrent launches stretch each other's event
+    # durations, so the pick would follow the overlap).  Collect is not timed there: in the
+    # timed region it replays as a captured graph whose launches are a small share, while its
+    # first, eager pass is host-bound and would inflate the forward kernels' event times.
+    # The remaining warmup and the timed region run as configured; the timed region then
+    # times the picked kernel on its own stream.
     import convs
+    keys = list(KERNELS)
     streams = convs.BWD_STREAMS
+    solo = {}
     for w in range(args.warmup):
         convs.BWD_STREAMS = streams and w > 0
-        iteration()
         if w == 0:
-            solo = {k: native.event_times_ms(k) for k in conv_keys}
-            totals = {k: sum(t for t, _ in v) for k, v in solo.items()}
+            alg.collect_samples()
+            native.enable_event_timing(keys)
+            alg.train()
+            solo = {k: same_size(k, native.event_times_ms(k)) for k in keys}
             native.enable_event_timing([])
+        else:
+            iteration()
     convs.BWD_STREAMS = streams
-    if args.warmup == 0:
-        totals, solo = {k: 0.0 for k in conv_keys}, {}
-    prof_kernel = max(totals, key=totals.get) if any(totals.values()) else "ppox_nature_conv_dgrad:2"
+    totals = {k: sum(t for t, _ in v) for k, v in solo.items()}
+    prof_kernel = max(totals, key=totals.get) if any(totals.values()) else "ppox_nature_conv_wgrad_split:2"
     gae_kernel = "ppox_gae" if args.algo != "rnd" else "ppox_gae_dual"
     native.enable_event_timing([prof_kernel])
 
@@ -323,15 +356,35 @@ def main():
     # per iteration, rank 0: GPU stream time and host time of each phase (phases.py);
     # gae and episodes run inside collect
     out["phases_ms_per_step"] = phase_ms
+    kt = same_size(prof_kernel, kt)
     if kt:
-        out["roofline"] = conv_roofline(prof_kernel, kt, totals, solo.get(prof_kernel))
-        launch_rows = float(np.mean([a[2] for _, a in kt]))
-        if out["roofline"].get("traffic") is not None and launch_rows != PMC_LAUNCH_ROWS:
-            # the committed PMC passes ran launches of PMC_LAUNCH_ROWS rows (the 1-GPU
-            # workload); a per-launch byte count of another size does not apply here
-            out["roofline"]["traffic"] = None
-            out["roofline"]["traffic_note"] = (f"PMC traffic was measured on {PMC_LAUNCH_ROWS}-row launches "
-                                               f"(profiles/); these launches average {launch_rows:.0f} rows")
+        r = kernel_roofline(prof_kernel, kt)
+        r["timing"] = ("HIP events on the kernel's launch stream around its timed-region launches of "
+                       f"{r['rows']} rows; a launch beside side-stream kernels (convs.BWD_STREAMS) also counts "
+                       "its sharing of the CUs with them")
+        r["selection"] = ("largest total kernel time among the training-pass MFMA kernels in a one-stream "
+                          "warmup iteration (collect untimed)")
+        if solo.get(prof_kernel):
+            s_ = kernel_roofline(prof_kernel, solo[prof_kernel])
+            r["solo"] = {k: s_[k] for k in ("mean_us", "launches", "rows", "frac", "mfma_frac", "hbm_frac")}
+        if r.get("traffic") is not None and r["rows"] != PMC_LAUNCH_ROWS:
+            # the committed PMC passes ran launches of PMC_LAUNCH_ROWS rows (the 1-GPU workload);
+            # a per-launch byte count of another size does not apply here
+            r["traffic"] = r["traffic_ratio"] = None
+            r["traffic_note"] = (f"PMC traffic was measured on {PMC_LAUNCH_ROWS}-row launches (profiles/); "
+                                 f"these launches have {r['rows']} rows")
+        out["roofline"] = r
+    tot = sum(totals.values())
+    if tot:
+        top = []
+        for k in sorted(totals, key=totals.get, reverse=True)[:5]:
+            q = kernel_roofline(k, solo[k])
+            if q["traffic"] is not None and q["rows"] != PMC_LAUNCH_ROWS:
+                q["traffic"] = q["traffic_ratio"] = None
+            top.append({"kernel": q["kernel"], "share_of_mfma_kernel_time": round(totals[k] / tot, 3),
+                        "solo_mean_us": q["mean_us"], "rows": q["rows"], "bound": q["bound"], "frac": q["frac"],
+                        "mfma_frac": q["mfma_frac"], "hbm_frac": q["hbm_frac"], "pmc_ratio": q["traffic_ratio"]})
+        out["roofline_top"] = top
     if gae_ms:
         n_local = args.envs // world
         alg_bytes = (17 if gae_kernel == "ppox_gae" else 33) * args.nstep * n_local

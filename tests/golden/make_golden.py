@@ -612,7 +612,154 @@ def gen_cnn_train(R):
         for k in ("train/entropy_loss", "train/policy_gradient_loss", "train/value_loss", "train/total_loss"):
             out[p + k.split("/")[1]] = np.float64(rec[k])
         out[p + "np_state_after"] = np.random.get_state()[1].copy()
+        # the same iteration with train() in float64 (oracle; collect in f32 on the replayed
+        # frames, as test_oracle_golden.test_cnn_fixture_is_well_conditioned re-runs it): the
+        # exact-arithmetic losses the GPU test bounds the product's entropy against
+        out.update(_cnn_f64_losses(out, p))
     save("train_cnn", **out)
+
+
+def _cnn_f64_losses(f, p):
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    sys.path.insert(0, os.path.dirname(OUT))
+    from oracle import models as OM
+    from oracle.algos import OraclePPO
+    from replay_env import ReplayVecEnv, Discrete as RDiscrete
+    N, T, B, E, A, seed, net_seed = (int(x) for x in f[p + "cfg"])
+    obs = np.concatenate([f[p + "obs"], f[p + "last_obs"][None]])
+    env = ReplayVecEnv(obs, f[p + "roll_rewards"], f[p + "roll_masks"].astype(bool), RDiscrete(A))
+    state = np.random.get_state()
+    np.random.seed(seed)
+    torch.manual_seed(net_seed)
+    alg = OraclePPO(env, nstep=T, batch_size=B, n_epochs=E, net=OM.NatureCNN(4, A), train_dtype=torch.float64)
+    alg.collect()
+    alg.train()
+    np.random.set_state(state)
+    out = {}
+    for key, st in (("total_loss", "loss"), ("policy_gradient_loss", "pl"), ("value_loss", "vl"),
+                    ("entropy_loss", "el")):
+        out[p + "f64_" + key] = np.float64(alg.stats[st])
+    return out
+
+
+# --------------------------------------------------------------------------
+# (9a) The same NatureCNN PPO iteration at the size the benchmark dispatches: 128 envs x
+#      128 steps, ONE minibatch of 16,384 rows per epoch, 2 epochs (ppo.py:200-259 with
+#      models-checkpoint.py:48-90).  At this batch the product runs its training-size kernel
+#      forms (sg2 fc forward, the solo persistent conv2 dgrad, the split heads' hidden layer,
+#      multi-slab split-K weight gradients).  The frames are not stored (462 MB): the env is
+#      the Philox synthetic Atari env restated in oracle/philox.py (the numpy twin of the
+#      device env, action-dependent counters), so the GPU test regenerates them bitwise on the
+#      device from the recorded actions; a crc32 per step pins that.  The same iteration is
+#      also run in float64 by the oracle on the reference's recorded rollout, so the test can
+#      bound the product's error against exact arithmetic, next to the reference's own.
+# --------------------------------------------------------------------------
+def gen_cnn_train_big(R):
+    import zlib
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from oracle.philox import SyntheticAtari
+    from oracle import models as OM
+    from oracle.algos import OraclePPO
+    ck = _load_checkpoint_models()
+    out = {}
+    name, A, N, T, B, E, seed, net_seed, env_seed, p_done = "big", 4, 128, 128, 16384, 2, 71, 72, 17071, 5e-3
+
+    class PhiloxFakeVec(R.VecEnv):
+        """oracle.philox.SyntheticAtari with float32 observations (what the reference feeds its
+        NatureCNN); no episode infos (the test checks the training update, not logging)."""
+
+        def __init__(self):
+            self.env = SyntheticAtari(N, env_seed, n_actions=A, p_done=p_done)
+            self.num_envs = N
+            self.observation_space = Box((4, 84, 84))
+            self.action_space = Discrete(A)
+            self.crc = []
+
+        def _rec(self, o):
+            self.crc.append(zlib.crc32(np.ascontiguousarray(o).tobytes()))
+            return o.astype(np.float32)
+
+        def reset(self):
+            return self._rec(self.env.reset())
+
+        def step(self, actions):
+            o, r, d, _ = self.env.step(actions)
+            return self._rec(o), r, d, [{} for _ in range(N)]
+
+        def unnormalize_obs(self, obs):
+            return obs
+
+    rec = _record_logger(R)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    env = PhiloxFakeVec()
+    R.ppo.make_env = lambda env_id, n_envs=4, env=env: env
+    alg = R.ppo.PPO(env_id="Fake-v0", nstep=T, batch_size=B, n_epochs=E)  # reference defaults otherwise
+    torch.manual_seed(net_seed)
+    net = ck.CnnActorCritic(4, A)
+    alg.policy.net = net
+    alg.optimizer = torch.optim.Adam(net.parameters(), lr=alg.lr)
+    init = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    alg.collect_samples()
+    st = alg.rollout
+    p = name + "_"
+    out[p + "cfg"] = np.array([N, T, B, E, A, seed, net_seed, env_seed], np.int64)
+    out[p + "p_done"] = np.float64(p_done)
+    out[p + "obs_crc"] = np.array(env.crc, np.uint32)                      # reset + T steps
+    roll = {}
+    for f in ("actions", "rewards", "values", "masks", "action_log_probs", "advantages", "returns"):
+        roll[f] = np.asarray(getattr(st, f)).copy()
+        out[p + "roll_" + f] = roll[f]
+    obs_ref = np.asarray(st.observations).copy()                          # (T, N, 4, 84, 84) f32
+    alg.train()
+    for k, (key, v0) in enumerate(init.items()):
+        v1 = net.state_dict()[key].detach()
+        out[p + "wsum0_" + key] = np.float64(v0.double().sum())
+        out[p + "whead0_" + key] = v0.flatten()[:16].numpy()
+        idx = weight_sample_index(v1.numel(), k)
+        out[p + "w1idx_" + key] = idx
+        out[p + "w1_" + key] = v1.flatten().numpy()[idx]
+        d = (v1 - v0).double()
+        out[p + "dsum_" + key] = np.float64(d.sum())
+        out[p + "dabs_" + key] = np.float64(d.abs().sum())
+    for k in ("train/entropy_loss", "train/policy_gradient_loss", "train/value_loss", "train/total_loss"):
+        out[p + k.split("/")[1]] = np.float64(rec[k])
+    out[p + "np_state_after"] = np.random.get_state()[1].copy()
+
+    # the same train() in float64 (oracle, test infrastructure) on the reference's recorded
+    # rollout: same initial weights, same permutations (numpy seeded as the reference's run)
+    np.random.seed(seed)
+    torch.manual_seed(net_seed)
+    onet = OM.NatureCNN(4, A)
+    for key, v in onet.state_dict().items():
+        assert torch.equal(v, init[key]), key
+    oalg = OraclePPO(PhiloxFakeVec(), nstep=T, batch_size=B,
+                     n_epochs=E, net=onet, train_dtype=torch.float64)
+    ro = oalg.rollout
+    ro.obs[:] = obs_ref
+    ro.actions[:] = roll["actions"].reshape(ro.actions.shape)
+    ro.rewards[:], ro.values[:], ro.masks[:] = roll["rewards"], roll["values"], roll["masks"]
+    ro.log_probs[:] = roll["action_log_probs"].reshape(ro.log_probs.shape)
+    ro.pos = T
+    ro.finish(roll["values"][T - 1], roll["masks"][T - 1])
+    assert np.array_equal(ro.adv, roll["advantages"]) and np.array_equal(ro.ret, roll["returns"])
+    del obs_ref
+    oalg.train()
+    assert np.array_equal(np.random.get_state()[1], out[p + "np_state_after"])
+    for k, (key, v) in enumerate(onet.state_dict().items()):
+        out[p + "w64_" + key] = v.flatten().numpy()[out[p + "w1idx_" + key]]
+        out[p + "d64abs_" + key] = np.float64((v - init[key].double()).abs().sum())
+    for key, stk in (("total_loss", "loss"), ("policy_gradient_loss", "pl"), ("value_loss", "vl"),
+                     ("entropy_loss", "el")):
+        out[p + "f64_" + key] = np.float64(oalg.stats[stk])
+        print(f"  {key}: ref {float(out[p + key]):.9g}  f64 {oalg.stats[stk]:.9g}  "
+              f"rel {abs(float(out[p + key]) - oalg.stats[stk]) / abs(oalg.stats[stk]):.3g}")
+    for key in init:
+        w, w64 = out[p + "w1_" + key].astype(np.float64), out[p + "w64_" + key]
+        print(f"  {key}: max |ref - f64| {np.abs(w - w64).max():.3g}")
+    save("train_cnn_big", **out)
 
 
 # --------------------------------------------------------------------------

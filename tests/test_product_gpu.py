@@ -358,6 +358,7 @@ def test_cnn_train_matches_reference_run(golden, name, math, rtol, head_min, mon
     alg.train()
     sd = alg.policy.net.state_dict()
     lr = alg.lr
+    wstats = {}
     for k, (key, v) in enumerate(sd.items()):
         idx = f[p + "w1idx_" + key]
         assert np.array_equal(idx, _weight_sample_index(v.numel(), k))
@@ -367,22 +368,131 @@ def test_cnn_train_matches_reference_run(golden, name, math, rtol, head_min, mon
         # most 0.2 % of them beyond the strict one (atol 2e-6): an f32 reordering decides the sign
         # of a pre-activation within rounding of zero differently (a ReLU-boundary flip), which
         # moves that unit's weights by a fraction of an Adam step
-        assert (err <= rtol * np.abs(ref) + 0.05 * lr).all(), (key, float(err.max()))
         frac = float((err > rtol * np.abs(ref) + 2e-6).mean())
+        wstats[key] = {"max_err": float(err.max()), "max_err_over_lr": float(err.max()) / lr, "frac_beyond_strict": frac}
+        assert (err <= rtol * np.abs(ref) + 0.05 * lr).all(), (key, float(err.max()))
         assert frac <= 2e-3, (key, frac)
         d = (v.double().cpu() - init[key].double())
         np.testing.assert_allclose(float(d.abs().sum()), float(f[p + "dabs_" + key]), rtol=2e-3, err_msg=key)
     np.testing.assert_array_equal(np.random.get_state()[1], f[p + "np_state_after"])
     acc = alg.loss_accum.cpu().numpy()
     n = acc[5]
-    # entropy of a near-saturated softmax over raw-pixel logits (|logit| ~ 1e2) is set by the
-    # logits' last bits — its relative error is the absolute error of the logit gaps: the
-    # reference's own f32 entropy loss is 2.8e-5 (cnn18) / 2.7e-4 (cnn4) from exact arithmetic
-    # (test_oracle_golden.test_cnn_fixture_is_well_conditioned), split-bf16 convs add ~1 ulp of
-    # the logits (measured 1.1e-3 on cnn4), so it gets 3e-3; the other losses 1e-5
-    for i, key, tol in ((0, "policy_gradient_loss", 1e-5), (1, "value_loss", 1e-5), (2, "entropy_loss", 3e-3),
-                        (3, "total_loss", 1e-5)):
-        np.testing.assert_allclose(acc[i] / n, f[p + key], rtol=tol, atol=1e-7, err_msg=key)
+    # policy-gradient, value and total loss within 1e-5 of the reference; the entropy of the
+    # near-saturated softmax over raw-pixel logits (|logit| ~ 1e2) is set by the logits' last
+    # bits, so the reference's own f32 entropy loss is 2.8e-5 (cnn18) / 2.7e-4 (cnn4) from
+    # exact arithmetic (the float64 oracle run recorded in the fixture): the product's is held
+    # to within twice that distance of float64 (floor 1e-5)
+    stats = {}
+    for i, key in ((0, "policy_gradient_loss"), (1, "value_loss"), (2, "entropy_loss"), (3, "total_loss")):
+        got, ref, x64 = float(acc[i] / n), float(f[p + key]), float(f[p + "f64_" + key])
+        stats[key] = {"rel_prod_ref": abs(got - ref) / abs(ref), "rel_prod_f64": abs(got - x64) / abs(x64),
+                      "rel_ref_f64": abs(ref - x64) / abs(x64)}
+    _parity_report(f"cnn_train_{name}_{math}_{head_min}", {"losses": stats, "weights": wstats})
+    for key, st in stats.items():
+        if key == "entropy_loss":
+            assert st["rel_prod_f64"] <= max(2 * st["rel_ref_f64"], 1e-5), (key, st)
+        else:
+            assert st["rel_prod_ref"] <= 1e-5, (key, st)
+
+
+def _parity_report(name, stats):
+    """Observed errors of a parity test (PPOX_PARITY_OUT=dir writes them as JSON), so a
+    regression that stays inside the tolerance is still visible."""
+    import json
+    import os
+    d = os.environ.get("PPOX_PARITY_OUT")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name + ".json"), "w") as fh:
+            json.dump(stats, fh, indent=1)
+
+
+@pytest.mark.parametrize("math", ["split", "f32"])
+def test_cnn_train_16384_rows_matches_reference_run(golden, math, monkeypatch):
+    """The benchmark's dispatch end to end: one NatureCNN PPO iteration of 128 envs x 128
+    steps trained as ONE 16,384-row minibatch per epoch (2 epochs) — the sg2 fc forward, the
+    solo persistent conv2 dgrad, the split heads' hidden layer, multi-slab split-K weight
+    gradients — against the reference's own run (ppo.py:200-259 with the checkpoint
+    CnnActorCritic, models-checkpoint.py:48-90; tests/golden/make_golden.py gen_cnn_train_big)
+    and against the same train() in float64 (oracle, recorded in the fixture).
+
+    The frames are regenerated on the device by the synthetic Atari env from the recorded
+    actions (bitwise: a crc32 per step).  Tolerances, in terms of the reference's own float32
+    error e_ref = |ref - f64| measured on this trajectory:
+      * weights, per tensor: max |prod - f64| <= 2 max e_ref + 2e-6 and mean |prod - f64| <=
+        2 mean e_ref + 1e-8 — the product is as close to exact arithmetic as the reference is,
+        within a factor 2; plus every weight within rtol |ref| + lr of the reference (one Adam
+        step: Adam's first steps move a weight by +-lr whatever its gradient's size, so a weight
+        whose gradient is zero to rounding moves either way — the reference's own run is up to
+        a third of a step off exact arithmetic here) with at most 0.5 % beyond rtol |ref| + 2e-6;
+      * losses: policy-gradient, value, total within 1e-5 relative of the reference; the entropy
+        of the near-saturated softmax within max(2 e_ref, 1e-5 |f64|) of float64."""
+    import env as E
+    import models
+    import ppo
+    import zlib
+    monkeypatch.setenv("PPOX_CONV_MATH", math)
+    f = golden("train_cnn_big")
+    p = "big_"
+    N, T, B, E_, A, seed, net_seed, env_seed = (int(x) for x in f[p + "cfg"])
+    np.random.seed(seed)  # RolloutStorage draws randn(16, 4) at construction (buffer.py:137)
+    env_id = "BreakoutNoFrameskip-v4"
+    env = E.DeviceAtariEnv(env_id, N, seed=env_seed, p_done=float(f[p + "p_done"]))
+    alg = ppo.PPO(env_id=env_id, env=env, n_envs=N, nstep=T, batch_size=B, n_epochs=E_, quiet=True)
+    assert alg.policy.net.conv_impl.math == math
+    torch.manual_seed(net_seed)
+    init = models.CnnActorCritic(4, A).state_dict()
+    with torch.no_grad():
+        for k, v in alg.policy.net.state_dict().items():
+            np.testing.assert_allclose(init[k].flatten()[:16].numpy(), f[p + "whead0_" + k], rtol=1e-5, atol=1e-7)
+            v.copy_(init[k].to(v.device))
+    alg.policy.net.conv_impl.invalidate()
+    ro = alg.rollout
+    acts = f[p + "roll_actions"]
+    crc = f[p + "obs_crc"]
+    obs = env.reset()
+    assert zlib.crc32(obs.cpu().numpy().tobytes()) == crc[0]
+    for t in range(T):
+        ro.add(obs, acts[t], f[p + "roll_rewards"][t], f[p + "roll_values"][t], f[p + "roll_masks"][t],
+               f[p + "roll_action_log_probs"][t])
+        obs, _, done, _ = env.step(acts[t].reshape(N))
+        assert zlib.crc32(obs.cpu().numpy().tobytes()) == crc[t + 1], t
+        assert np.array_equal(done.cpu().numpy(), f[p + "roll_masks"][t].astype(bool)), t
+    ro.compute_returns_and_advantages(f[p + "roll_values"][T - 1], f[p + "roll_masks"][T - 1])
+    np.testing.assert_array_equal(ro.advantages.cpu().numpy(), f[p + "roll_advantages"])
+    np.testing.assert_array_equal(ro.returns.cpu().numpy(), f[p + "roll_returns"])
+    alg.train()
+    np.testing.assert_array_equal(np.random.get_state()[1], f[p + "np_state_after"])
+    lr = alg.lr
+    rtol = 1e-4 if math == "split" else 5e-5
+    stats, fails = {"math": math, "weights": {}, "losses": {}}, []
+    for k, (key, v) in enumerate(alg.policy.net.state_dict().items()):
+        idx = f[p + "w1idx_" + key]
+        assert np.array_equal(idx, _weight_sample_index(v.numel(), k))
+        w = v.flatten().cpu().numpy()[idx].astype(np.float64)
+        ref, w64 = f[p + "w1_" + key].astype(np.float64), f[p + "w64_" + key]
+        e_p, e_r, e_pr = np.abs(w - w64), np.abs(ref - w64), np.abs(w - ref)
+        frac = float((e_pr > rtol * np.abs(ref) + 2e-6).mean())
+        d_abs = float((v.double().cpu() - init[key].double()).abs().sum())
+        stats["weights"][key] = {"max_prod_f64": float(e_p.max()), "max_ref_f64": float(e_r.max()),
+                                 "mean_prod_f64": float(e_p.mean()), "mean_ref_f64": float(e_r.mean()),
+                                 "max_prod_ref": float(e_pr.max()), "frac_beyond_strict": frac,
+                                 "dabs_rel": abs(d_abs - float(f[p + "d64abs_" + key])) / float(f[p + "d64abs_" + key])}
+        if not (e_p.max() <= 2 * e_r.max() + 2e-6 and e_p.mean() <= 2 * e_r.mean() + 1e-8
+                and (e_pr <= rtol * np.abs(ref) + lr).all() and frac <= 5e-3):
+            fails.append((key, stats["weights"][key]))
+    acc = alg.loss_accum.cpu().numpy()
+    n = acc[5]
+    for i, key in ((0, "policy_gradient_loss"), (1, "value_loss"), (2, "entropy_loss"), (3, "total_loss")):
+        got, ref, x64 = float(acc[i] / n), float(f[p + key]), float(f[p + "f64_" + key])
+        stats["losses"][key] = {"prod": got, "ref": ref, "f64": x64, "rel_prod_ref": abs(got - ref) / abs(ref),
+                                "rel_prod_f64": abs(got - x64) / abs(x64), "rel_ref_f64": abs(ref - x64) / abs(x64)}
+        ok = (abs(got - x64) <= max(2 * abs(ref - x64), 1e-5 * abs(x64)) if key == "entropy_loss"
+              else abs(got - ref) <= 1e-5 * abs(ref))
+        if not ok:
+            fails.append((key, stats["losses"][key]))
+    _parity_report(f"cnn_train_16384_{math}", stats)
+    assert not fails, fails
 
 
 def _read_csv(folder):
