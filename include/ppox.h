@@ -298,10 +298,33 @@ int64_t ppox_nature_fc_pack_elems(void);
 /* All weight packings of one optimizer step in a single launch (any output may be null):
  * wpd2 = f32 conv2 dgrad ([(ky,kx,co)][ci]); q1..q3 / qd2, qd3 = split forms (as
  * ppox_nature_pack_split); qfc_fwd / qfc_dgrad = fc split forms (as ppox_nature_fc_pack). */
-int ppox_nature_pack_all(const float* w1, const float* w2, const float* w3, const float* wfc, float* wpd2,
-                         uint16_t* q1, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
+int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, const float* w3, const float* wfc,
+                         float* wpd2, uint16_t* q1, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
                          uint16_t* qfc_fwd, uint16_t* qfc_dgrad, const float* wh, uint16_t* qh_fwd,
                          uint16_t* qh_dgrad, void* stream);
+/* conv1 -> conv2 on H1P, the split-f16 operand form of conv1's output h1 (Conv2d(4, 32, 8, 4) + ReLU
+ * of models-checkpoint.py:52-53): per pixel (NHWC) its 32 channels' high f16 plane then their low
+ * plane, h1 * 2^E = hi + lo (128 B per pixel, the size of the f32 form), E derived by
+ * ppox_nature_pack_all (b1 required with q1) from the bound |h1| <= 255 max_c (sum |W1[c]| + |b1[c]|)
+ * and kept in q1's tail, so the producer splits its output in its epilogue and the consumers read
+ * the planes as they lie (no amax pass, no split in the consumers).
+ *   conv1_fwd_planes:  as ppox_nature_conv_fwd_split(1, ...) writing h1p (batch x 400 x 64 uint16)
+ *   conv2_fwd_planes:  as ppox_nature_conv_fwd_split(2, ...) reading h1p (q1: its exponent)
+ *   conv2_wgrad_planes: dW2 [64][32][4][4] and db2 of Conv2d(32, 64, 4, 2) from h1p and the output
+ *                      grad g2 (NHWC f32, amax_g its slots): one workgroup per CU over whole samples
+ *                      (the direct form: the H1P image and the G rows of a sample in LDS, no
+ *                      im2col), slabs in the workspace (ppox_nature_conv2_wgrad_planes_workspace_bytes)
+ *                      summed in a fixed order.  Replaces the Conv2d weight / bias autograd of
+ *                      models-checkpoint.py:54 in the training backward of ppo.py:241. */
+int ppox_nature_conv1_fwd_planes(const void* x, int64_t batch, const int64_t* idx, int64_t T, int64_t N_env,
+                                 int64_t x_sample_stride, const uint16_t* wq1, const float* bias, uint16_t* h1p,
+                                 uint32_t* relu_bits, void* stream);
+int ppox_nature_conv2_fwd_planes(const uint16_t* h1p, const uint16_t* q1, int64_t batch, const uint16_t* wq2,
+                                 const float* bias, float* y, uint32_t* amax_y, uint32_t* relu_bits, void* stream);
+int64_t ppox_nature_conv2_wgrad_planes_workspace_bytes(int64_t batch);
+int ppox_nature_conv2_wgrad_planes(const uint16_t* h1p, const uint16_t* q1, int64_t batch, const float* grad_out,
+                                   void* workspace, int64_t workspace_bytes, float* dw, float* db,
+                                   const uint32_t* amax_g, void* stream);
 /* The heads' hidden layer Linear(512, 512) + ReLU (models-checkpoint.py:62-66 extra_layer; the
  * forward of forward() / evaluate and its autograd in ppo.py:216-238) on the split-f16 GEMM, with
  * wh (512 x 512) packed by ppox_nature_pack_all into qh_fwd / qh_dgrad of

@@ -217,6 +217,10 @@ class NatureConvs:
             f = torch.arange(3136, device=dev)
             self.fc_perm = (f % 64) * 49 + f // 64  # NHWC feature -> Flatten feature
             self.wfc_nhwc = torch.empty(512, 3136, device=dev)
+        # split math: conv1's output h1 in the H1P form (its two f16 planes per value, 128 B per
+        # pixel: csrc/conv_common.h) — written split by the conv1 forward at a scale derived from the
+        # weights, read as it lies by the conv2 forward and the direct conv2 weight gradient
+        self.h1p = self.math != "f32"
         self._ws = {}
         self._version = None
         self._packed = set()
@@ -234,8 +238,23 @@ class NatureConvs:
             return batch is not None and batch < DGRAD2_SPLIT_MAX_BATCH
         return (op, layer) in SPLIT_OPS
 
+    def h1p_exponent(self):
+        """E of the current H1P packing (h1 * 2^E = hi + lo), read back from q1's tail (tests)."""
+        tail = self.q[1][native.nature_split_pack_elems(1) - 2 * native.PACK_TAIL32:].view(torch.int32)
+        return int(tail[native.AMAX_SLOTS + 1])
+
+    def empty_h1(self, B, device):
+        """conv1's output buffer of a B-row pass: H1P (int16 planes) in split math, f32 NHWC else."""
+        if self.h1p:
+            return torch.empty((B, 20, 20, 64), dtype=torch.int16, device=device)
+        return torch.empty((B, 20, 20, 32), device=device)
+
     def workspace(self, layer, batch, split=False):
-        need = (native.nature_wgrad_split_workspace_bytes if split else native.nature_wgrad_workspace_bytes)(layer, batch)
+        if split and layer == 2 and self.h1p:
+            need = native.nature_conv2_wgrad_planes_workspace_bytes(batch)
+        else:
+            need = (native.nature_wgrad_split_workspace_bytes if split else native.nature_wgrad_workspace_bytes)(layer,
+                                                                                                               batch)
         ws = self._ws.get(layer)
         if ws is None or ws.numel() < need:
             ws = torch.empty(need, dtype=torch.uint8, device=self.flat.device)
@@ -278,7 +297,7 @@ class NatureConvs:
             native.nature_pack_all(w1, w2, w3, self.fc.weight, pick("wpd2", self.wpd2), pick("q1", q[1]),
                                    pick("q2", q[2]), pick("q3", q[3]), pick("qd2", q[12]), pick("qd3", q[13]),
                                    pick("qfcf", qfc[0]), pick("qfcd", qfc[1]), self.hid.weight, pick("qhf", qh[0]),
-                                   pick("qhd", qh[1]))
+                                   pick("qhd", qh[1]), b1=self.c1.bias)
         if "wfc_nhwc" in missing:
             torch.index_select(self.fc.weight.detach(), 1, self.fc_perm, out=self.wfc_nhwc)
         self._packed |= missing
@@ -296,10 +315,17 @@ class NatureConvs:
         bits = am.bits[layer - 1] if isinstance(am, PassState) else None
         if isinstance(x, RolloutRows):
             assert layer == 1 and self.uses_split("fwd", 1)
-            native.nature_conv_fwd_split(1, x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y, amax_y=out_am,
-                                         relu_bits=bits)
+            if self.h1p:
+                native.nature_conv1_fwd_planes(x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y, relu_bits=bits)
+            else:
+                native.nature_conv_fwd_split(1, x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y, amax_y=out_am,
+                                             relu_bits=bits)
             return
-        if self.uses_split("fwd", layer):
+        if self.h1p and layer == 1:
+            native.nature_conv1_fwd_planes(x, B, None, 0, 0, stride, self.q[1], bias, y, relu_bits=bits)
+        elif self.h1p and layer == 2:
+            native.nature_conv2_fwd_planes(x, self.q[1], B, self.q[2], bias, y, amax_y=out_am, relu_bits=bits)
+        elif self.uses_split("fwd", layer):
             native.nature_conv_fwd_split(layer, x, B, None, 0, 0, stride, self.q[layer], bias, y,
                                          amax_x=am[AM_H1 + layer - 2] if layer > 1 else None, amax_y=out_am,
                                          relu_bits=bits)
@@ -314,9 +340,13 @@ class NatureConvs:
         g_am, out_am = (am[AM_G3], am[AM_G2]) if layer == 3 else (am[AM_G2], am[AM_G1])
         if self.uses_split("dgrad", layer, B):
             bits = am.bits[layer - 2] if isinstance(am, PassState) else None
+            if layer == 2 and self.h1p and bits is None:
+                raise ValueError("conv2 dgrad on H1P needs conv1's ReLU bitmask (a training pass's PassState)")
             native.nature_conv_dgrad_split(layer, g, B, self.q[10 + layer], prev_act, out, amax_g=g_am,
                                            amax_out=out_am, relu_bits=bits)
         else:
+            if layer == 2 and self.h1p:
+                raise ValueError("the f32 conv2 dgrad needs f32 activations; split math keeps h1 as H1P")
             native.nature_conv_dgrad(layer, g, B, self.wpd2 if layer == 2 else self.wpd3, prev_act, out)
             if self.math != "f32":
                 native.amax(out, out_am)
@@ -329,7 +359,10 @@ class NatureConvs:
             native.nature_conv_wgrad_split_idx(1, x.frames, B, x.idx, x.T, x.N, g, self.workspace(1, B, True), dw, db,
                                                amax_g=g_am, stream=stream)
             return
-        if self.uses_split("wgrad", layer):
+        if layer == 2 and self.h1p:
+            native.nature_conv2_wgrad_planes(x, self.q[1], B, g, self.workspace(2, B, True), dw, db, amax_g=g_am,
+                                             stream=stream)
+        elif self.uses_split("wgrad", layer):
             native.nature_conv_wgrad_split(layer, x, B, stride, g, self.workspace(layer, B, True), dw, db,
                                            amax_x=am[AM_H1 + layer - 2] if layer > 1 else None, amax_g=g_am,
                                            stream=stream)
@@ -344,15 +377,17 @@ class NatureConvs:
         self.pack(x.shape[0])
         B = x.shape[0]
         dev = x.device
-        h1 = torch.empty((B, 20, 20, 32), device=dev)
+        h1 = self.empty_h1(B, dev)
         h2 = torch.empty((B, 9, 9, 64), device=dev)
         h3 = torch.empty((B, 7, 7, 64) if self.nhwc3 else (B, 64, 7, 7), device=dev)
         # the conv outputs' ReLU bitmasks where the forward and the consumer of the mask (the next
         # layer's dgrad; for conv3 the fc dgrad) both run split (training passes)
         consumer = (self.uses_split("dgrad", 2, B), self.uses_split("dgrad", 3, B),
                     self.nhwc3 and B < FC_DGRAD_FUSED_MAX_BATCH)
+        # (conv1's is required on H1P, whose planes are no f32 mask)
         bits = tuple(torch.empty(B * P * C // 32, dtype=torch.int32, device=dev)
-                     if train and RELU_BITS and self.uses_split("fwd", L) and consumer[L - 1] else None
+                     if train and (RELU_BITS or (L == 1 and self.h1p)) and self.uses_split("fwd", L) and
+                     consumer[L - 1] else None
                      for L, P, C in ((1, 400, 32), (2, 81, 64), (3, 49, 64)))
         am = PassState(native.amax_table(AM_ROWS, dev), bits)
         if B:
@@ -426,7 +461,7 @@ class NatureConvs:
         if solo:
             join(side, cur)
         g1 = torch.empty((B, 20, 20, 32), device=dev)
-        self.dgrad(2, g2, B, h1, g1, am)                        # dX of conv2, times ReLU'(conv1)
+        self.dgrad(2, g2, B, h1 if not self.h1p else None, g1, am)                        # dX of conv2, times ReLU'(conv1)
         if side is None or (solo and BWD_SOLO_WGRAD2):
             self.wgrad(2, h1, B, g2, dw2, db2, am)
         elif solo:

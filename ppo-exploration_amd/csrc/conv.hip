@@ -119,6 +119,7 @@ struct StageB {
 template <class L, bool OUT_NCHW, int MT_>
 struct FwdBase {
     static constexpr int NOUT = L::COUT, MT = MT_, BMR = 128 * MT;
+    static constexpr bool A_PLANES = false;  // sg2: A rows are f32 (split in registers), not H1P planes
     using Tile = RowTile;
     __device__ static bool tile(const Args& a, Tile& t) {
         t.m0 = (long long)blockIdx.x * BMR;
@@ -196,6 +197,7 @@ struct StageDgradPM {
 template <class L, int MT_>
 struct DgradPMProblem {
     static constexpr int NOUT = L::CIN, MT = MT_, BMR = 128 * MT, NPOS = L::IH * L::IW, CPT = L::COUT / BK;
+    static constexpr bool A_PLANES = false;
     using Tile = PixelTile;
     using Stager = StageDgradPM<L, MT>;
     __device__ static bool tile(const Args& a, Tile& t) {
@@ -404,6 +406,7 @@ template <int K_, int N_, int NB, int MODE>
 struct GemmRowsProblem {
     static constexpr int K = K_, N = N_, NOUT = NB, MT = 1, BMR = 128, NCB = (N + NB - 1) / NB, KC = K / BK;
     static constexpr bool LATE_EPILOGUE = true;
+    static constexpr bool A_PLANES = false;
     static_assert(K % BK == 0, "K multiple of 32");
     using Tile = GemmTile;
     using Stager = StageGemmRows<K>;
@@ -798,8 +801,9 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
     int bp[BPW];
 #pragma unroll
     for (int i = 0; i < BPW; ++i) bp[i] = min(BPW * wave + i, SG_BP - 1);
-    // operand scales: A by its tensor's amax, B as packed; the epilogue multiplies by both inverses
-    const int ex = split_scale_exp(amax_read(a.amax_x)), ew = *a.wexp;
+    // operand scales: A by its tensor's amax (H1P planes: their exponent), B as packed; the epilogue
+    // multiplies by both inverses
+    const int ex = Prob::A_PLANES ? *a.xexp : split_scale_exp(amax_read(a.amax_x)), ew = *a.wexp;
     const float sa = exp2i(ex), ua = exp2i(-ex), uw = exp2i(-ew);
     // chunk c into ring slot S; the chunk index is clamped, not branched on (past the end:
     // the last chunk again, never read)
@@ -841,7 +845,12 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
         }
     };
     auto split_a = [&](const u32x4 (&g)[6], u32x4 (&af)[NPL]) {
-        split8h(__builtin_bit_cast(float4, g[0]), __builtin_bit_cast(float4, g[1]), sa, af[0], af[1]);
+        if constexpr (Prob::A_PLANES) {  // H1P: the two pieces read are the planes
+            af[0] = g[0];
+            af[1] = g[1];
+        } else {
+            split8h(__builtin_bit_cast(float4, g[0]), __builtin_bit_cast(float4, g[1]), sa, af[0], af[1]);
+        }
     };
     // chunk in slot S: 12 fragment reads up front (k-step 0's six, then k-step 1's), k-step 0
     // computed once its six have landed (lgkmcnt(6)) while k-step 1's are in flight
@@ -850,9 +859,11 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
         u32x4 f[2][6];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            const int g0 = 4 * s + 2 * h;
+            // the lane's 8 k of k-step s: f32 pieces g0, g0 + 1 (16 B = 4 values each), or H1P
+            // pieces 2s + h (hi plane: 8 f16) and 4 + 2s + h (lo plane)
+            const int g0 = Prob::A_PLANES ? 2 * s + h : 4 * s + 2 * h, g1 = Prob::A_PLANES ? 4 + g0 : g0 + 1;
             f[s][0] = sg_ds_read(a_lane + slot * SLOT + ((g0 ^ sw) << 4));
-            f[s][1] = sg_ds_read(a_lane + slot * SLOT + (((g0 + 1) ^ sw) << 4));
+            f[s][1] = sg_ds_read(a_lane + slot * SLOT + ((g1 ^ sw) << 4));
 #pragma unroll
             for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -989,6 +1000,13 @@ struct SgFwd : FwdNHWCProblem<L, OUT_NCHW, 1> {
         const int tap = c / CPT;
         return ((tap / L::KW) * L::IW + tap % L::KW) * L::CIN + (c % CPT) * BK;
     }
+};
+
+// the conv2 forward on H1P input (conv1's output as f16 planes): a pixel's 128 B are its 32 hi then
+// 32 lo f16 instead of 32 f32, so the DMA addressing is unchanged and the k-step's two pieces are
+// the fragments' planes (no split in registers)
+struct SgFwd2P : SgFwd<G2, false> {
+    static constexpr bool A_PLANES = true;
 };
 
 // BITS_IN: the ReLU mask of the layer below from its forward's bitmask (a.bits_mask, CIN / 32
@@ -1900,6 +1918,268 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// conv2 weight gradient from H1P planes, direct (no im2col):
+//   dW[tap][ci][co] = sum over samples n and output pixels p = (oy, ox) of
+//                     h1[n][2 oy + ky][2 ox + kx][ci] * g2[n][p][co]       (+ db[co] = sum g2)
+// One 512-thread workgroup per CU walks its own run of samples.  Per sample the whole H1P image
+// (20 x 20 x 32, both f16 planes: 51 KB) is DMA'd into LDS and the sample's 81 G rows (f32) are
+// split there into two f16 planes: every h1 and g2 byte is read from HBM once (the im2col form,
+// wgrad_split_kernel, re-fetched h1 ~3.2x through L2 and split every value once per k-block).
+// The reduction runs over the sample's 81 pixels in 6 k-steps of 16 (G rows 81..95 are zero):
+// wave w owns taps 2w, 2w + 1 x all 64 output channels (4 tiles, 12 MFMAs per k-step).  The A
+// fragment rows are h1 pixels (2 oy + ky, 2 ox + kx), read with the transposing LDS read: the
+// image is stored column-parity split (slot = y * 20 + (x & 1) * 10 + (x >> 1), 64 B per slot and
+// plane), so consecutive output pixels of one tap are consecutive slots (conflict-free reads) and
+// a tap is one uniform slot offset.  G rows are 128 B per plane with 32-B chunks XOR-swizzled
+// (tr_swz<128>).  Double-buffered: sample s + 1's DMAs and G loads fly under sample s's MFMAs.
+// Partial slabs per workgroup, summed in a fixed order by wgrad_reduce (deterministic).
+// LDS: G planes of both buffers first (so every B read's offset is an immediate), then the H
+// images: 2 x 24 KB + 2 x 50 KB = 148 KB.
+// ---------------------------------------------------------------------------
+constexpr int W2P_GP = 96 * 128;                 // one G plane: 96 rows x 64 co x f16
+constexpr int W2P_GB = 2 * W2P_GP;               // both G planes of one buffer
+constexpr int W2P_HP = 400 * 64;                 // one H1P plane image: 400 slots x 32 ci x f16
+constexpr int W2P_HB = 2 * W2P_HP;               // both planes of one buffer
+constexpr int W2P_H0 = 2 * W2P_GB;               // the H images follow both buffers' G planes
+constexpr int W2P_LDS = 2 * W2P_GB + 2 * W2P_HB;  // 151,552 B
+constexpr int W2P_NDMA = 7;                      // 1-KB DMAs per wave and sample (50 per sample)
+constexpr int W2P_SAMPLE = 400 * 128;            // H1P bytes per sample
+constexpr int W2P_G4 = 81 * 64 / 4;              // float4 of G per sample (1296)
+static_assert(W2P_LDS <= 160 * 1024, "wgrad2 planes: LDS");
+static_assert(8 * W2P_NDMA >= 2 * W2P_HP / 1024 && 2 * W2P_HP % 1024 == 0, "wgrad2 planes: DMA split");
+
+struct W2PArgs {
+    const uint16_t* h1p;     // H1P [batch][400][32 hi | 32 lo]
+    const int* h1_exp;       // h1 * 2^E = hi + lo
+    const float* g;          // g2 [batch][81][64] f32 NHWC (ReLU mask applied)
+    const uint32_t* amax_g;  // g2's amax slots
+    float* slab;             // [gridDim.x][512][64]
+    float* bslab;            // [gridDim.x][64]
+    long long batch;
+    int per;                 // samples per workgroup (every workgroup has at least one)
+};
+
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+// transposing LDS read in inline asm: hipcc would otherwise wait for the in-flight LDS-DMA of the
+// next sample (vmcnt(0)) before every read, exposing the prefetch
+__device__ inline u32x2v w2p_tr(uint32_t addr) {
+    u32x2v r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+    return r;
+}
+template <int OFF>
+__device__ inline u32x2v w2p_tr_o(uint32_t addr) {
+    u32x2v r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+    return r;
+}
+// one k-step's 16 fragment halves landed (tied, so the MFMAs use the post-wait values)
+__device__ inline void w2p_lgkm_wait(u32x2v (&x)[16]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+                   "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]),
+                   "+v"(x[15]));
+}
+__device__ inline int w2p_tapoff(int t) {  // uniform slot offset of tap t = ky * 4 + kx
+    const int ky = t >> 2, kx = t & 3;
+    return 20 * ky + 10 * (kx & 1) + (kx >> 1);
+}
+
+__global__ void __launch_bounds__(512, 1) wgrad2_planes_kernel(W2PArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[W2P_LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const long long s0 = (long long)blockIdx.x * a.per;
+    const long long s1 = min(a.batch, s0 + (long long)a.per);
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
+    // operand scales: G by its tensor's amax, h1 by its H1P exponent; the slab is unscaled
+    const int eg = split_scale_exp(amax_read(a.amax_g)), ex = *a.h1_exp;
+    const float sg = exp2i(eg), uo = exp2i(-eg) * exp2i(-ex);
+
+    // H1P DMA sources of this wave's pieces (byte offsets within a sample): DMA i (0..49) fills
+    // LDS bytes [1024 i, 1024 i + 1024) of the image (plane i / 25); lane l's 16 B are piece
+    // (l & 3) of slot (1024 (i % 25) + 16 l) / 64.  DMAs past the 50th re-copy the 50th.
+    uint32_t hsrc[W2P_NDMA];
+#pragma unroll
+    for (int j = 0; j < W2P_NDMA; ++j) {
+        int i = wave * W2P_NDMA + j;
+        i = i < 49 ? i : 49;
+        const int P = i / 25, within = (i % 25) * 1024 + lane * 16;
+        const int slot = within >> 6, piece = (within >> 4) & 3;
+        const int y = slot / 20, xs = slot % 20, x = xs < 10 ? 2 * xs : 2 * (xs - 10) + 1;
+        hsrc[j] = (uint32_t)((y * 20 + x) * 128 + P * 64 + piece * 16);
+    }
+    auto dma_h = [&](long long n, int buf) {
+        const uint32_t nb = (uint32_t)n * (uint32_t)W2P_SAMPLE;  // host-checked: batch * 51200 < 2^32
+#pragma unroll
+        for (int j = 0; j < W2P_NDMA; ++j) {
+            int i = wave * W2P_NDMA + j;
+            i = i < 49 ? i : 49;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(reinterpret_cast<const char*>(a.h1p) + (nb + hsrc[j])),
+                (__attribute__((address_space(3))) void*)(lds + W2P_H0 + buf * W2P_HB + i * 1024), 16, 0, 0);
+        }
+    };
+    // G: float4 q = tid + 512 r of the sample's 1296 (row q >> 4, channels 4 (q & 15) ..); the third
+    // only for tid < 272 (others re-load the last float4 and store nothing)
+    const int gc4 = tid & 15;
+    float4 graw[3];
+    auto load_g = [&](long long n) {
+        const float4* src = reinterpret_cast<const float4*>(a.g) + n * W2P_G4;
+        graw[0] = src[tid];
+        graw[1] = src[tid + 512];
+        graw[2] = src[tid < W2P_G4 - 1024 ? tid + 1024 : W2P_G4 - 1];
+    };
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    auto store_g = [&](int buf, bool add_bias) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            if (r < 2 || tid < W2P_G4 - 1024) {
+                const int row = (tid + 512 * r) >> 4, chunk = gc4 >> 2;
+                const int off = buf * W2P_GB + row * 128 + ((chunk ^ (2 * ((row >> 1) & 1))) << 5) + (gc4 & 3) * 8;
+                uint2 hv, lv;
+                split4h(graw[r], sg, hv, lv);
+                *reinterpret_cast<uint2*>(lds + off) = hv;
+                *reinterpret_cast<uint2*>(lds + off + W2P_GP) = lv;
+                if (add_bias) {
+                    bsum[0] += graw[r].x;
+                    bsum[1] += graw[r].y;
+                    bsum[2] += graw[r].z;
+                    bsum[3] += graw[r].w;
+                }
+            }
+        }
+    };
+    // zero G rows 81..95 of both buffers and planes once (the loads never write them)
+    if (tid < 480) {
+        const int pl = tid / 120, o = (tid % 120) * 16;
+        *reinterpret_cast<u32x4*>(lds + pl * W2P_GP + 81 * 128 + o) = u32x4{0u, 0u, 0u, 0u};
+    }
+
+    // fragment addresses: lane (h, g16, qq, pp) supplies row qq (+ 4 for the second read) of the
+    // 8-row group h of k-step ks, 8 B at column chunk g16
+    const int h = lane >> 5, g16 = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+    uint32_t aaddr[6][2];
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            int p = 16 * ks + 8 * h + 4 * r + qq;
+            p = p < 81 ? p : 80;  // rows past the 81 pixels: any valid slot (their G rows are zero)
+            aaddr[ks][r] = lds0 + W2P_H0 + (uint32_t)((40 * (p / 9) + p % 9) * 64 + g16 * 32 + pp * 8);
+        }
+    const uint32_t toff[2] = {(uint32_t)w2p_tapoff(2 * wave) * 64u, (uint32_t)w2p_tapoff(2 * wave + 1) * 64u};
+    const int swz = 2 * ((qq >> 1) & 1);
+    const uint32_t baddr[2] = {lds0 + (uint32_t)((8 * h + qq) * 128 + (((0 + g16) ^ swz) << 5) + pp * 8),
+                               lds0 + (uint32_t)((8 * h + qq) * 128 + (((2 + g16) ^ swz) << 5) + pp * 8)};
+
+    f32x16 hi[2][2], lo[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) hi[i][j] = lo[i][j] = zero16();
+
+    auto compute = [&](auto BUF) {
+        constexpr int buf = decltype(BUF)::value;
+#pragma unroll
+        for (int ks = 0; ks < 6; ++ks) {
+            u32x2v v[16];  // [i or j][plane][r]: A halves 0..7, B halves 8..15
+            // the k-step's two row addresses, laundered so the compiler does not hoist all 96
+            // (k-step, row, tap, plane, buffer) sums out of the sample loop into registers
+            uint32_t ab[2] = {aaddr[ks][0], aaddr[ks][1]};
+            asm volatile("" : "+v"(ab[0]), "+v"(ab[1]));
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int P = 0; P < 2; ++P)
+#pragma unroll
+                    for (int r = 0; r < 2; ++r)
+                        v[(i * 2 + P) * 2 + r] = w2p_tr(ab[r] + (toff[i] + (uint32_t)(buf * W2P_HB + P * W2P_HP)));
+            // B: co-tile j, plane P, rows +0 / +4 of the k-step (offsets are immediates)
+            constexpr int B0 = buf * W2P_GB;
+            auto bread = [&](auto KS) {
+                constexpr int o = B0 + decltype(KS)::value * 2048;
+                v[8] = w2p_tr_o<o>(baddr[0]);
+                v[9] = w2p_tr_o<o + 512>(baddr[0]);
+                v[10] = w2p_tr_o<o + W2P_GP>(baddr[0]);
+                v[11] = w2p_tr_o<o + W2P_GP + 512>(baddr[0]);
+                v[12] = w2p_tr_o<o>(baddr[1]);
+                v[13] = w2p_tr_o<o + 512>(baddr[1]);
+                v[14] = w2p_tr_o<o + W2P_GP>(baddr[1]);
+                v[15] = w2p_tr_o<o + W2P_GP + 512>(baddr[1]);
+            };
+            switch (ks) {  // ks is a constant of the unrolled loop
+                case 0: bread(std::integral_constant<int, 0>{}); break;
+                case 1: bread(std::integral_constant<int, 1>{}); break;
+                case 2: bread(std::integral_constant<int, 2>{}); break;
+                case 3: bread(std::integral_constant<int, 3>{}); break;
+                case 4: bread(std::integral_constant<int, 4>{}); break;
+                default: bread(std::integral_constant<int, 5>{}); break;
+            }
+            w2p_lgkm_wait(v);
+            u32x4 af[2][NPL], bf[2][NPL];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int P = 0; P < 2; ++P) {
+                    const u32x2v x0 = v[(i * 2 + P) * 2], x1 = v[(i * 2 + P) * 2 + 1];
+                    const u32x2v y0 = v[8 + (i * 2 + P) * 2], y1 = v[8 + (i * 2 + P) * 2 + 1];
+                    af[i][P] = u32x4{x0.x, x0.y, x1.x, x1.y};
+                    bf[i][P] = u32x4{y0.x, y0.y, y1.x, y1.y};
+                }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) mfma_split3(af[i], bf[j], hi[i][j], lo[i][j]);
+        }
+    };
+    auto barrier = [] { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+    dma_h(s0, 0);
+    load_g(s0);
+    store_g(0, true);
+    barrier();
+    // one step: sample s + 1 (clamped: past the last sample a dummy copy of s into the idle
+    // buffer, no bias) issued, sample s computed, s + 1's G split into the other buffer
+    auto step = [&](long long s, auto BUF) {
+        constexpr int buf = decltype(BUF)::value;
+        const bool nxt = s + 1 < s1;
+        const long long sn = nxt ? s + 1 : s;
+        dma_h(sn, buf ^ 1);
+        load_g(sn);
+        compute(BUF);
+        store_g(buf ^ 1, nxt);
+        barrier();
+    };
+#pragma unroll 1
+    for (long long s = s0; s < s1; s += 2) {
+        step(s, std::integral_constant<int, 0>{});
+        if (s + 1 < s1) step(s + 1, std::integral_constant<int, 1>{});
+    }
+    float* slab = a.slab + (long long)blockIdx.x * (G2::K * G2::COUT);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = (2 * wave + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                slab[k * G2::COUT + j * 32 + (lane & 31)] = (hi[i][j][r] + lo[i][j][r]) * uo;
+            }
+    // bias partial: threads with the same gc4 hold the same four channels; summed in thread order
+    float* red = reinterpret_cast<float*>(lds);  // the loop ended on a barrier
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[tid * 4 + e] = bsum[e];
+    __syncthreads();
+    if (tid < G2::COUT) {
+        const int c4 = tid >> 2, e = tid & 3;
+        float t = 0.f;
+        for (int k = 0; k < 32; ++k) t += red[(c4 + 16 * k) * 4 + e];
+        a.bslab[(long long)blockIdx.x * G2::COUT + tid] = t;
+    }
+}
+
 // conv3 output grad: NCHW (Flatten order) -> NHWC, times the ReLU mask of h3 (NCHW)
 __global__ void __launch_bounds__(256) nchw_to_nhwc_mask(const float* __restrict__ g, const float* __restrict__ h,
                                                          long long batch, float* __restrict__ out) {
@@ -2064,6 +2344,7 @@ struct PackAll {
     uint16_t *q1, *q2, *q3, *qd2, *qd3, *qfcf, *qfcd;  // split planes
     const float* wh = nullptr;                         // the heads' hidden layer (512 x 512)
     uint16_t *qhf = nullptr, *qhd = nullptr;           // its forward (W^T) and dgrad (W) forms
+    const float* b1 = nullptr;                         // conv1 bias (with q1: the H1P exponent)
 };
 constexpr long long PA_N1 = 8 * 2 * 64 * 8, PA_N2 = (long long)G2::K * G2::COUT, PA_N3 = (long long)G3::K * G3::COUT;
 constexpr long long PA_NFC = (long long)FcFwd::NCB * FcFwd::K * FcFwd::NOUT;
@@ -2230,6 +2511,30 @@ __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long tota
     }
 }
 
+// The H1P exponent of conv1's output (one workgroup): |h1| <= 255 max_c (sum_k |W1[c][k]|) +
+// |b1[c]| for uint8 frames; thread t sums k-range t & 7 of channel t >> 3 in f64.  Stored in
+// slot H1P_EXP_SLOT of q1's tail, read by the conv1 forward (output scale) and the H1P consumers.
+// The bound carries a 2^-10 margin, so every value times 2^E stays below 2^15 (f16 max 65504).
+__global__ void __launch_bounds__(256) h1p_exp_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
+                                                     uint16_t* __restrict__ q1) {
+    const int t = threadIdx.x, c = t >> 3, part = t & 7;
+    double sum = 0.0;
+    for (int k = part * 32; k < part * 32 + 32; ++k) sum += fabs((double)w1[c * G1::K + k]);
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) sum += __shfl_xor(sum, o);
+    double bound = 255.0 * sum + fabs((double)b1[c]);
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) bound = fmax(bound, __shfl_xor(bound, o));
+    __shared__ double red[4];
+    if ((t & 63) == 0) red[t >> 6] = bound;
+    __syncthreads();
+    if (t == 0) {
+        const double m = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+        const float mf = (float)(m * (1.0 + 1.0 / 1024.0));
+        pack_tail(q1, PL_Q1)[AMAX_SLOTS + H1P_EXP_SLOT] = (uint32_t)split_scale_exp(__float_as_uint(mf));
+    }
+}
+
 int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
     for (const void* q : {(const void*)p.wpd2, (const void*)p.q1, (const void*)p.q2, (const void*)p.q3,
                           (const void*)p.qd2, (const void*)p.qd3, (const void*)p.qfcf, (const void*)p.qfcd})
@@ -2246,6 +2551,10 @@ int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
                             (p.qhf || p.qhd ? PU_FCD + 2 * PU_H : (p.qfcd ? PU_FCD : 0));
     const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 4096);
     pack_all_kernel<<<blocks, 256, 0, s>>>(p, total);
+    if (p.q1 && p.b1) {
+        PPOX_LAUNCHED_NORET(name);
+        h1p_exp_kernel<<<1, 256, 0, s>>>(p.w1, p.b1, p.q1);
+    }
     PPOX_LAUNCHED(name);
 }
 
@@ -2501,6 +2810,70 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
                                        "ppox_nature_conv_dgrad_split");
 }
 
+// ---- conv2 on H1P (conv1's output as f16 planes, conv_common.h) --------------------------
+namespace {
+int cu_count() {
+    static int cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (cus[dev] == 0 && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 0;
+    return cus[dev];
+}
+// wgrad2_planes_kernel: samples per workgroup and workgroups (one per CU, none empty)
+void w2p_grid(long long batch, int& per, long long& grid) {
+    const long long cus = std::max(1, cu_count());
+    per = (int)ppox::ceil_div(batch, std::min(batch, cus));
+    grid = ppox::ceil_div(batch, (long long)per);
+}
+}  // namespace
+
+extern "C" int ppox_nature_conv2_fwd_planes(const uint16_t* h1p, const uint16_t* q1, int64_t batch,
+                                            const uint16_t* wq2, const float* bias, float* y, uint32_t* amax_y,
+                                            uint32_t* relu_bits, void* stream) {
+    if (batch == 0) return PPOX_OK;
+    PPOX_REQUIRE(h1p && q1 && wq2 && bias && y && batch > 0, "ppox_nature_conv2_fwd_planes: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(h1p) && ppox::aligned16(wq2), "ppox_nature_conv2_fwd_planes: 16B alignment");
+    PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(relu_bits) & 7), "ppox_nature_conv2_fwd_planes: relu_bits 8B alignment");
+    Args a{h1p, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch, nullptr, amax_y, pack_exp(wq2, PL_Q2)};
+    a.bits_y = relu_bits;
+    a.xexp = h1p_exp(q1, PL_Q1);
+    return launch_sgemm<SgFwd2P>(a, wq2, ppox::ceil_div(batch * G2::P, SG_ROWS), ppox::as_stream(stream),
+                                 "ppox_nature_conv2_fwd_planes");
+}
+
+extern "C" int64_t ppox_nature_conv2_wgrad_planes_workspace_bytes(int64_t batch) {
+    if (batch <= 0) return 0;
+    int per;
+    long long grid;
+    w2p_grid(batch, per, grid);
+    return grid * (long long)(G2::K * G2::COUT + G2::COUT) * (long long)sizeof(float);
+}
+
+extern "C" int ppox_nature_conv2_wgrad_planes(const uint16_t* h1p, const uint16_t* q1, int64_t batch,
+                                              const float* grad_out, void* workspace, int64_t workspace_bytes,
+                                              float* dw, float* db, const uint32_t* amax_g, void* stream) {
+    PPOX_REQUIRE(h1p && q1 && grad_out && workspace && dw && db && amax_g && batch > 0,
+                 "ppox_nature_conv2_wgrad_planes: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(h1p) && ppox::aligned16(grad_out) && ppox::aligned16(amax_g) &&
+                     ppox::aligned16(workspace),
+                 "ppox_nature_conv2_wgrad_planes: 16B alignment");
+    PPOX_REQUIRE(batch * (long long)W2P_SAMPLE < (1LL << 32), "ppox_nature_conv2_wgrad_planes: batch too large");
+    PPOX_REQUIRE(cu_count() > 0, "ppox_nature_conv2_wgrad_planes: no device");
+    PPOX_REQUIRE(workspace_bytes >= ppox_nature_conv2_wgrad_planes_workspace_bytes(batch),
+                 "ppox_nature_conv2_wgrad_planes: workspace too small");
+    int per;
+    long long grid;
+    w2p_grid(batch, per, grid);
+    float* slab = reinterpret_cast<float*>(workspace);
+    W2PArgs wa{h1p, h1p_exp(q1, PL_Q1), grad_out, amax_g, slab, slab + grid * (long long)(G2::K * G2::COUT), batch,
+               per};
+    hipStream_t s = ppox::as_stream(stream);
+    wgrad2_planes_kernel<<<(unsigned)grid, 512, 0, s>>>(wa);
+    PPOX_LAUNCHED_NORET("ppox_nature_conv2_wgrad_planes");
+    return launch_wgrad_reduce<G2, true>(slab, wa.bslab, (int)grid, dw, db, s);
+}
+
 // ---- NatureCNN fc layer (3136 -> 512) on the split-bf16 GEMM ----------------------
 // Weight gradient dW = df^T h3 on the split wgrad kernel: "pixels" = samples (GFc has one
 // output pixel), K = the 512 outputs (X = df rows), G = the NHWC conv3 activations in 49
@@ -2657,13 +3030,14 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
                                                      ppox::as_stream(stream), "ppox_nature_fc_dgrad");
 }
 
-extern "C" int ppox_nature_pack_all(const float* w1, const float* w2, const float* w3, const float* wfc, float* wpd2,
-                                    uint16_t* q1, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
-                                    uint16_t* qfc_fwd, uint16_t* qfc_dgrad, const float* wh, uint16_t* qh_fwd,
-                                    uint16_t* qh_dgrad, void* stream) {
+extern "C" int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, const float* w3,
+                                    const float* wfc, float* wpd2, uint16_t* q1, uint16_t* q2, uint16_t* q3,
+                                    uint16_t* qd2, uint16_t* qd3, uint16_t* qfc_fwd, uint16_t* qfc_dgrad,
+                                    const float* wh, uint16_t* qh_fwd, uint16_t* qh_dgrad, void* stream) {
     PPOX_REQUIRE(w1 && w2 && w3 && (wfc || (!qfc_fwd && !qfc_dgrad)), "ppox_nature_pack_all: null weights");
+    PPOX_REQUIRE(!q1 || b1, "ppox_nature_pack_all: q1 needs the conv1 bias b1 (the H1P exponent)");
     return launch_pack_all(
-        PackAll{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh, qh_fwd, qh_dgrad},
+        PackAll{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh, qh_fwd, qh_dgrad, b1},
         ppox::as_stream(stream), "ppox_nature_pack_all");
 }
 

@@ -37,7 +37,19 @@ struct Args {
     // split forwards (bits_y), read by the split dgrads instead of the f32 mask (bits_mask)
     uint32_t* bits_y = nullptr;
     const uint32_t* bits_mask = nullptr;
+    // H1P operands (conv1's output as two f16 planes, h1 * 2^E = hi + lo): the exponent E of the
+    // input (xexp: the split conv2 forward reads H1P) or of the output (yexp: the conv1 forward
+    // writes it)
+    const int* xexp = nullptr;
+    const int* yexp = nullptr;
 };
+
+// H1P (conv1's output, the split conv2 operand): per pixel 32 hi then 32 lo f16 (128 B, the size
+// of its f32 NHWC form); its exponent E (h1 * 2^E = hi + lo) lives in slot H1P_EXP_SLOT of the
+// conv1 forward pack's tail, derived once per optimizer step from the bound
+// |h1| <= 255 * max_c sum_k |W1[c][k]| + |b1[c]| (uint8 frames), so the conv1 forward can split
+// its output in its epilogue without knowing the output's max
+constexpr int H1P_EXP_SLOT = 1;  // + AMAX_SLOTS: after the weights' own exponent (h1p_exp below)
 
 __device__ inline f32x16 zero16() {
     f32x16 z;
@@ -273,6 +285,10 @@ __host__ __device__ inline uint32_t* pack_tail(uint16_t* q, long long planes) {
 }
 __host__ __device__ inline const int* pack_exp(const uint16_t* q, long long planes) {
     return reinterpret_cast<const int*>(q + planes) + AMAX_SLOTS;
+}
+// the H1P exponent stored in the conv1 forward pack's tail (Args::xexp / yexp)
+__host__ __device__ inline const int* h1p_exp(const uint16_t* q1, long long planes_q1) {
+    return reinterpret_cast<const int*>(q1 + planes_q1) + AMAX_SLOTS + H1P_EXP_SLOT;
 }
 
 

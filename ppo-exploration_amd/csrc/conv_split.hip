@@ -34,7 +34,10 @@ namespace {
 // the current tile runs its 48*MT MFMAs.  Workgroups with adjacent row ranges
 // share an XCD (xcd_remap): the overlapping input windows of one frame stack
 // are read through one L2.
-template <int MT>
+// PLANES: h1 is written as its two f16 planes (H1P: per pixel 32 hi then 32 lo f16, 128 B like f32),
+// h1 * 2^E = hi + lo with E = *a.yexp (ppox_nature_pack_all: from the weight bound of conv1's
+// output), the operand format of the split conv2 forward / weight gradient — no amax is recorded
+template <int MT, bool PLANES = false>
 __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a, unsigned tiles_per_wave) {
     using L = G1;
     constexpr int NCH = L::K / 32, NQ = NCH * 2 * NPL;
@@ -80,6 +83,7 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
     const int co = lane & 31;
     const float bias = a.bias[co];
     const float uw = exp2i(-*a.wexp);  // the weights were packed times 2^E; frames are exact
+    const float sy = PLANES ? exp2i(*a.yexp) : 1.f;  // H1P output scale
     float om = 0.f;                    // the largest value this lane stored (h1's amax)
     auto run_tile = [&](unsigned tile, const Raw& r) {
         f32x16 hi[MT], lo[MT];
@@ -120,7 +124,18 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
                 const unsigned m = m0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
                 const float v = fmaxf((hi[i][e] + lo[i][e]) * uw + bias, 0.f);
                 om = fmaxf(om, v);  // a row past the end recomputed row m0, which is stored
-                if (m < M) a.y[(long long)m * L::COUT + co] = v;
+                if constexpr (PLANES) {
+                    const float vs = v * sy;
+                    const _Float16 hv = (_Float16)vs;
+                    const _Float16 lv = (_Float16)(vs - (float)hv);  // exact in f32
+                    uint16_t* y16 = reinterpret_cast<uint16_t*>(a.y) + (long long)m * (2 * L::COUT) + co;
+                    if (m < M) {
+                        y16[0] = __builtin_bit_cast(uint16_t, hv);
+                        y16[L::COUT] = __builtin_bit_cast(uint16_t, lv);
+                    }
+                } else {
+                    if (m < M) a.y[(long long)m * L::COUT + co] = v;
+                }
                 if (a.bits_y) {  // uniform
                     const unsigned long long b = __ballot(v > 0.f);
                     word = eL == e ? (uint32_t)(hL ? b >> 32 : b) : word;
@@ -140,7 +155,7 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
         if (tile + 2 < t_end) load_tile(tile + 2, r0);
         run_tile(tile + 1, r1);
     }
-    amax_record(a.amax_y, om);
+    if constexpr (!PLANES) amax_record(a.amax_y, om);
 }
 
 #ifndef SPLIT_FWD1_MT
@@ -153,6 +168,33 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
 #endif
 
 }  // namespace
+
+// conv1 forward writing H1P (see fwd1_split_kernel<MT, true>): h1 as its two f16 planes at the
+// exponent the weight packing derived (ppox_nature_pack_all with b1)
+extern "C" int ppox_nature_conv1_fwd_planes(const void* x, int64_t batch, const int64_t* idx, int64_t T,
+                                            int64_t N_env, int64_t x_sample_stride, const uint16_t* wq1,
+                                            const float* bias, uint16_t* h1p, uint32_t* relu_bits, void* stream) {
+    if (batch == 0) return PPOX_OK;
+    PPOX_REQUIRE(x && wq1 && bias && h1p && batch > 0, "ppox_nature_conv1_fwd_planes: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(wq1), "ppox_nature_conv1_fwd_planes: packed weights must be 16-byte aligned");
+    PPOX_REQUIRE(batch * G1::P < (1LL << 31), "ppox_nature_conv1_fwd_planes: batch too large for 32-bit rows");
+    PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && (idx || x_sample_stride % 4 == 0),
+                 "ppox_nature_conv1_fwd_planes: u8 input must be 4-byte aligned");
+    if (idx) PPOX_REQUIRE(T > 0 && N_env > 0, "ppox_nature_conv1_fwd_planes: idx needs T and N_env");
+    const long long pl = ppox_conv::planes(1);
+    Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, nullptr, bias, nullptr,
+           reinterpret_cast<float*>(h1p), batch, nullptr, nullptr, pack_exp(wq1, pl)};
+    a.wp = reinterpret_cast<const float*>(wq1);
+    a.bits_y = relu_bits;
+    a.yexp = h1p_exp(wq1, pl);
+    constexpr int MT = SPLIT_FWD1_MT;
+    const long long ntile = ppox::ceil_div(batch * G1::P, 32 * MT);
+    const long long waves = std::min<long long>(ntile, SPLIT_RESIDENT_WAVES);
+    const unsigned per = ppox::ceil_div(ntile, waves);
+    fwd1_split_kernel<MT, true><<<ppox::ceil_div(ppox::ceil_div(ntile, per), 4), 256, 0, ppox::as_stream(stream)>>>(
+        a, per);
+    PPOX_LAUNCHED("ppox_nature_conv1_fwd_planes");
+}
 
 extern "C" int64_t ppox_nature_split_pack_elems(int32_t which) {
     const long long p = (which >= 1 && which <= 3) || which == 12 || which == 13 ? ppox_conv::planes(which) : -1;

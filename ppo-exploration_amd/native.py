@@ -71,7 +71,10 @@ SIGNATURES = {
     "ppox_skinny_dgrad": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 11,
     "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
-    "ppox_nature_pack_all": [_vp] * 16,
+    "ppox_nature_pack_all": [_vp] * 17,
+    "ppox_nature_conv1_fwd_planes": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv2_fwd_planes": [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv2_wgrad_planes": [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -109,7 +112,8 @@ _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p
              "ppox_icm_w1_pack_elems": ctypes.c_int64, "ppox_icm_encode_workspace_bytes": ctypes.c_int64,
              "ppox_icm_partials_bytes": ctypes.c_int64, "ppox_icm_g1_pack_elems": ctypes.c_int64,
              "ppox_nature_fc_fwd_splitk_workspace_bytes": ctypes.c_int64, "ppox_amax_slots": ctypes.c_int32,
-             "ppox_head_hidden_pack_elems": ctypes.c_int64, "ppox_head_hidden_wgrad_workspace_bytes": ctypes.c_int64}
+             "ppox_head_hidden_pack_elems": ctypes.c_int64, "ppox_head_hidden_wgrad_workspace_bytes": ctypes.c_int64,
+             "ppox_nature_conv2_wgrad_planes_workspace_bytes": ctypes.c_int64}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
                  "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32],
                  "ppox_nature_wgrad_split_workspace_bytes": [_i32, _i64],
@@ -118,7 +122,8 @@ _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad
                  "ppox_nature_fc_wgrad_workspace_bytes": [_i64], "ppox_icm_param_elems": [_i32],
                  "ppox_icm_w1_pack_elems": [_i64], "ppox_icm_encode_workspace_bytes": [_i64, _i64],
                  "ppox_icm_partials_bytes": [_i64, _i32], "ppox_icm_g1_pack_elems": [_i64],
-                 "ppox_nature_fc_fwd_splitk_workspace_bytes": [_i64], "ppox_head_hidden_wgrad_workspace_bytes": [_i64]}
+                 "ppox_nature_fc_fwd_splitk_workspace_bytes": [_i64], "ppox_head_hidden_wgrad_workspace_bytes": [_i64],
+                 "ppox_nature_conv2_wgrad_planes_workspace_bytes": [_i64]}
 
 _lib = None
 
@@ -475,6 +480,7 @@ def nature_conv_fwd(layer, x, batch, idx, T, N_env, x_sample_stride, wp, bias, y
 # split-f16 forms (csrc/conv_split.hip, csrc/conv.hip): weights packed as two fp16 planes
 # (int16 tensors) times a power-of-two scale; f32 operands carry "amax slots" (include/ppox.h)
 AMAX_SLOTS = 256  # include/ppox.h ppox_amax_slots()
+PACK_TAIL32 = AMAX_SLOTS + 8  # uint32 tail of a split-packed buffer (amax partials, exponents)
 
 
 def amax_table(n, device):
@@ -539,10 +545,33 @@ def nature_fc_pack(w, q_fwd, q_dgrad, stream=None):
 
 
 def nature_pack_all(w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh=None, qh_fwd=None,
-                    qh_dgrad=None, stream=None):
-    """Every weight packing of a training step in one launch (None = skip)."""
-    call("ppox_nature_pack_all", _p(w1), _p(w2), _p(w3), _p(wfc), _p(wpd2), _p(q1), _p(q2), _p(q3), _p(qd2),
-         _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), _p(wh), _p(qh_fwd), _p(qh_dgrad), stream_ptr(stream))
+                    qh_dgrad=None, b1=None, stream=None):
+    """Every weight packing of a training step in one launch (None = skip); q1 needs the conv1
+    bias b1 (the H1P exponent of conv1's output is derived from W1 and b1)."""
+    call("ppox_nature_pack_all", _p(w1), _p(b1), _p(w2), _p(w3), _p(wfc), _p(wpd2), _p(q1), _p(q2), _p(q3),
+         _p(qd2), _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), _p(wh), _p(qh_fwd), _p(qh_dgrad), stream_ptr(stream))
+
+
+# conv1 -> conv2 on H1P (conv1's output as two f16 planes; include/ppox.h)
+def nature_conv1_fwd_planes(x, batch, idx, T, N_env, x_sample_stride, wq1, bias, h1p, relu_bits=None, stream=None):
+    call("ppox_nature_conv1_fwd_planes", _p(x), int(batch), _p(idx), int(T), int(N_env), int(x_sample_stride),
+         _p(wq1), _p(bias), _p(h1p), _p(relu_bits), stream_ptr(stream))
+
+
+def nature_conv2_fwd_planes(h1p, q1, batch, wq2, bias, y, amax_y=None, relu_bits=None, stream=None):
+    call("ppox_nature_conv2_fwd_planes", _p(h1p), _p(q1), int(batch), _p(wq2), _p(bias), _p(y), _p(amax_y),
+         _p(relu_bits), stream_ptr(stream))
+
+
+def nature_conv2_wgrad_planes_workspace_bytes(batch):
+    return int(load().ppox_nature_conv2_wgrad_planes_workspace_bytes(int(batch)))
+
+
+def nature_conv2_wgrad_planes(h1p, q1, batch, grad_out, workspace, dw, db, amax_g=None, stream=None):
+    """dW2, db2 from H1P and the NHWC f32 output grad (slabs + fixed-order reduce in one call)."""
+    amax_g = _amax_of(grad_out, amax_g, stream)
+    call("ppox_nature_conv2_wgrad_planes", _p(h1p), _p(q1), int(batch), _p(grad_out), _p(workspace),
+         workspace.numel() * workspace.element_size(), _p(dw), _p(db), _p(amax_g), stream_ptr(stream))
 
 
 def nature_fc_fwd(h3, batch, q_fwd, bias, f, amax_h3=None, amax_f=None, stream=None):

@@ -745,7 +745,6 @@ def gen_cnn_train_big(R):
     ro.pos = T
     ro.finish(roll["values"][T - 1], roll["masks"][T - 1])
     assert np.array_equal(ro.adv, roll["advantages"]) and np.array_equal(ro.ret, roll["returns"])
-    del obs_ref
     oalg.train()
     assert np.array_equal(np.random.get_state()[1], out[p + "np_state_after"])
     for k, (key, v) in enumerate(onet.state_dict().items()):
@@ -756,9 +755,43 @@ def gen_cnn_train_big(R):
         out[p + "f64_" + key] = np.float64(oalg.stats[stk])
         print(f"  {key}: ref {float(out[p + key]):.9g}  f64 {oalg.stats[stk]:.9g}  "
               f"rel {abs(float(out[p + key]) - oalg.stats[stk]) / abs(oalg.stats[stk]):.3g}")
+    del oalg
     for key in init:
         w, w64 = out[p + "w1_" + key].astype(np.float64), out[p + "w64_" + key]
         print(f"  {key}: max |ref - f64| {np.abs(w - w64).max():.3g}")
+
+    # the FIRST minibatch's raw gradient (loss.backward(), before clip_grad_norm_ / Adam) at the
+    # initial weights, by the oracle in float32 (torch-CPU: the reference's own arithmetic) and
+    # float64, sampled like the weights: the GPU test compares the product's per-layer gradient
+    # error with the reference's (a diagnostic finer than the post-Adam weights)
+    from oracle.algos import _tensors, ppo_loss
+    for dt, tag in ((torch.float32, "g32_"), (torch.float64, "g64_")):
+        np.random.seed(seed)
+        torch.manual_seed(net_seed)
+        gnet = OM.NatureCNN(4, A).to(dt)
+        galg = OraclePPO(PhiloxFakeVec(), nstep=T, batch_size=B, n_epochs=E, net=gnet, train_dtype=dt)
+        ro = galg.rollout
+        ro.obs[:] = obs_ref
+        ro.actions[:] = roll["actions"].reshape(ro.actions.shape)
+        ro.rewards[:], ro.values[:], ro.masks[:] = roll["rewards"], roll["values"], roll["masks"]
+        ro.log_probs[:] = roll["action_log_probs"].reshape(ro.log_probs.shape)
+        ro.pos = T
+        ro.finish(roll["values"][T - 1], roll["masks"][T - 1])
+        _idx, mb = next(ro.minibatches(B))
+        mb = _tensors(mb, dt)
+        v, _, lp, ent = OM.evaluate(gnet, mb["observations"], mb["actions"], False, dt)
+        with torch.no_grad():  # the first minibatch's forward outputs, in minibatch order
+            logits = gnet.heads(mb["observations"])[0]
+        out[p + "mb0_v" + tag[1:3]] = v.detach().double().numpy()
+        out[p + "mb0_logits" + tag[1:3]] = logits.double().numpy()
+        loss, _, _, _ = ppo_loss(v, lp, ent, mb, galg.clip, galg.ent_coef, galg.vf_coef)
+        loss.backward()
+        for k, (key, prm) in enumerate(gnet.named_parameters()):
+            out[p + tag + key] = prm.grad.detach().double().flatten().numpy()[out[p + "w1idx_" + key]]
+        del galg, ro, mb
+    for key in init:
+        g32, g64 = out[p + "g32_" + key], out[p + "g64_" + key]
+        print(f"  grad {key}: max |g32 - g64| / max |g64| {np.abs(g32 - g64).max() / np.abs(g64).max():.3g}")
     save("train_cnn_big", **out)
 
 

@@ -394,6 +394,35 @@ def test_adam_clip_vs_torch(max_norm):
 
 
 # ----------------------------------------------------------------- K6 convs
+def _h1p_exponent(w1, b1):
+    """E of H1P (csrc/conv.hip h1p_exp_kernel): the bound 255 max_c sum_k |W1[c][k]| + |b1[c]|
+    (uint8 frames) with a 2^-10 margin, scaled into [2^14, 2^15)."""
+    bound = (255.0 * w1.double().abs().reshape(32, -1).sum(1) + b1.double().abs()).max().item()
+    m = np.float32(bound * (1.0 + 1.0 / 1024.0))
+    e = int(m.view(np.uint32)) >> 23
+    return 141 - min(254, max(15, e))
+
+
+def _h1_planes(h1, E):
+    """H1P of an f32 NHWC h1 at exponent E with the kernels' rounding: hi = rn16(h1 2^E),
+    lo = rn16(h1 2^E - hi) (the residual is exact in f32)."""
+    v = h1 * 2.0 ** E
+    hi = v.half()
+    lo = (v - hi.float()).half()
+    return torch.cat([hi.view(torch.int16), lo.view(torch.int16)], dim=-1).contiguous()
+
+
+def _h1_from_planes(h1p, E):
+    """(hi + lo) 2^-E: exact in f32 (two 11-bit significands 11 bits apart)."""
+    return (h1p[..., :32].contiguous().view(torch.float16).float() +
+            h1p[..., 32:].contiguous().view(torch.float16).float()) * 2.0 ** -E
+
+
+def _relu_bits(h):
+    """int32 ReLU bitmask words (bit c of word p: channel c of pixel p > 0) of a 32-channel NHWC h."""
+    w = ((h > 0).reshape(-1, 32).long() << torch.arange(32, device=h.device)).sum(1)
+    return torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32)
+
 @pytest.mark.parametrize("math", ["split", "split_all", "f32"])
 @pytest.mark.parametrize("B", [1, 3, 37, 256])
 def test_nature_conv_fwd_vs_torch_fp32(B, math):
@@ -456,7 +485,7 @@ def _conv_ops_fp64(B, seed):
         cv = convs.attach(net, flat, math)
         hs = {}
         cv.pack()
-        h1 = torch.empty(B, 20, 20, 32, device="cuda")
+        h1 = cv.empty_h1(B, "cuda")  # H1P (conv1's output as f16 planes) in split math
         h2 = torch.empty(B, 9, 9, 64, device="cuda")
         h3 = torch.empty((B, 7, 7, 64) if cv.nhwc3 else (B, 64, 7, 7), device="cuda")
         am = native.amax_table(convs.AM_ROWS, "cuda")  # each forward records its output's amax
@@ -465,6 +494,8 @@ def _conv_ops_fp64(B, seed):
         cv.fwd(3, h2, B, cv.c3.bias, h3, am)
         if cv.nhwc3:  # split math writes conv3's output NHWC
             h3 = h3.permute(0, 3, 1, 2)
+        if cv.h1p:
+            h1 = _h1_from_planes(h1, cv.h1p_exponent())
         hs.update({("fwd", 1): h1, ("fwd", 2): h2, ("fwd", 3): h3})
         out[math] = hs
     # backward ops on shared inputs (f32-mode activations as ReLU masks, random output grads)
@@ -485,11 +516,14 @@ def _conv_ops_fp64(B, seed):
         d2 = torch.empty(B, 9, 9, 64, device="cuda")
         d1 = torch.empty(B, 20, 20, 32, device="cuda")
         cv.dgrad(3, g3, B, h2f, d2, amax_rows(G3=g3))
-        cv.dgrad(2, g2r, B, h1f, d1, amax_rows(G2=g2r))
+        if cv.h1p:  # conv1's ReLU mask as the forward's bitmask (H1P is no f32 mask)
+            cv.dgrad(2, g2r, B, None, d1, convs.PassState(amax_rows(G2=g2r), (_relu_bits(h1f), None, None)))
+        else:
+            cv.dgrad(2, g2r, B, h1f, d1, amax_rows(G2=g2r))
         out[math].update({("dgrad", 3): d2, ("dgrad", 2): d1})
         g1r = torch.randn(B, 20, 20, 32, device="cuda", generator=torch.Generator(device="cuda").manual_seed(seed + 7))
         am = amax_rows(G1=g1r, G2=g2r, G3=g3, H1=h1f, H2=h2f)
-        for L, xin, gg in ((1, x, g1r), (2, h1f, g2r), (3, h2f, g3)):
+        for L, xin, gg in ((1, x, g1r), (2, _h1_planes(h1f, cv.h1p_exponent()) if cv.h1p else h1f, g2r), (3, h2f, g3)):
             wl = (cv.c1, cv.c2, cv.c3)[L - 1]
             dw, db = torch.empty_like(wl.weight), torch.empty_like(wl.bias)
             cv.wgrad(L, xin, B, gg, dw, db, am)
@@ -771,8 +805,13 @@ def test_pack_all_matches_separate_packers():
     fc = lambda: torch.zeros(nfc, dtype=torch.int16, device="cuda")
     a = [q(1), q(2), q(3), q(12), q(13), fc(), fc(), torch.zeros(16 * 64 * 32, device="cuda")]
     b = [q(1), q(2), q(3), q(12), q(13), fc(), fc(), torch.zeros(16 * 64 * 32, device="cuda")]
-    native.nature_pack_all(w1, w2, w3, wfc, a[7], a[0], a[1], a[2], a[3], a[4], a[5], a[6])
+    b1 = torch.randn(32, device="cuda")
+    native.nature_pack_all(w1, w2, w3, wfc, a[7], a[0], a[1], a[2], a[3], a[4], a[5], a[6], b1=b1)
     native.nature_pack_split(w1, w2, w3, b[0], b[1], b[2], b[3], b[4])
+    # pack_all also derives the H1P exponent of conv1's output into q1's tail (pack_split does not)
+    tail = a[0][native.nature_split_pack_elems(1) - 2 * native.PACK_TAIL32:].view(torch.int32)
+    assert int(tail[native.AMAX_SLOTS + 1]) == _h1p_exponent(w1, b1)
+    tail[native.AMAX_SLOTS + 1] = 0
     native.nature_fc_pack(wfc, b[5], b[6])
     wp = [torch.empty(n, device="cuda") for n in (256 * 32, 512 * 64, 576 * 64)]
     native.nature_pack_weights(w1, w2, w3, wp[0], wp[1], wp[2], b[7], None)
@@ -1098,3 +1137,106 @@ def test_sg2_conv_big_batch_vs_fp64(B):
         ds.append(d)
     check(ds[0], dgrad3_ref(torch.float64), dgrad3_ref(torch.float32))
     assert torch.equal(ds[0], ds[1])
+
+
+def _h1p_setup(B, seed, scale_w1=0.05):
+    """Random frames through the conv1 forward writing H1P, with the weights packed by
+    ppox_nature_pack_all (q1 carries the H1P exponent): (q, h1p, h1 as f32, E, weights)."""
+    import native
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    w1 = torch.randn(32, 4, 8, 8, device="cuda", generator=g) * scale_w1
+    w2 = torch.randn(64, 32, 4, 4, device="cuda", generator=g) * 0.05
+    w3 = torch.randn(64, 64, 3, 3, device="cuda", generator=g) * 0.05
+    b1 = torch.randn(32, device="cuda", generator=g)
+    q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device="cuda") for k in (1, 2, 3)}
+    native.nature_pack_all(w1, w2, w3, None, None, q[1], q[2], q[3], None, None, None, None, b1=b1)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda", generator=g)
+    h1p = torch.empty(B, 20, 20, 64, dtype=torch.int16, device="cuda")
+    bits = torch.empty(B * 400, dtype=torch.int32, device="cuda")
+    native.nature_conv1_fwd_planes(x, B, None, 0, 0, 28224, q[1], b1, h1p, relu_bits=bits)
+    E = _h1p_exponent(w1, b1)
+    return q, x, h1p, _h1_from_planes(h1p, E), E, (w1, b1, w2, w3), bits
+
+
+@pytest.mark.parametrize("B", [1, 3, 37, 300])
+def test_h1p_conv1_forward_is_split_of_f32_forward(B):
+    """The conv1 forward writing H1P (its output split into two f16 planes in the epilogue, at the
+    exponent ppox_nature_pack_all derived from the weights' bound) == the H1P split of the same
+    kernel's f32 output, bitwise, plain rows and rollout rows (idx); its ReLU bitmask too."""
+    import native
+    q, x, h1p, h1, E, (w1, b1, _, _), bits = _h1p_setup(B, B)
+    y = torch.empty(B, 20, 20, 32, device="cuda")
+    native.nature_conv_fwd_split(1, x, B, None, 0, 0, 28224, q[1], b1, y)
+    assert torch.equal(h1p, _h1_planes(y, E))
+    assert torch.equal(bits, _relu_bits(y))
+    assert float(y.abs().max()) * 2.0 ** E < 2 ** 15  # the bound holds
+    T, N = 3, (B + 2) // 3
+    frames = torch.randint(0, 256, (T, N, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    idx = torch.randperm(T * N, device="cuda")[:B].to(torch.int64)
+    rows = torch.empty(B, 4, 84, 84, dtype=torch.uint8, device="cuda")
+    native.gather_rows(frames, T, N, 28224, 28224, idx, B, rows)
+    a, b = torch.empty_like(h1p), torch.empty_like(h1p)
+    native.nature_conv1_fwd_planes(frames, B, idx, T, N, 0, q[1], b1, a)
+    native.nature_conv1_fwd_planes(rows, B, None, 0, 0, 28224, q[1], b1, b)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [1, 5, 300, 9001, 16384])
+def test_h1p_conv2_fwd_and_wgrad_vs_fp64(B):
+    """conv2 forward and the direct conv2 weight gradient on H1P vs float64 on the device, error no
+    larger than the same math in f32 (x2 headroom): ragged and training-size batches (16,384 rows:
+    64 samples per CU), the bias grad, each output's bitwise run-to-run determinism, the forward's
+    ReLU bitmask; the weight gradient also per element against a dot-product error bound, on an
+    output grad whose magnitudes spread over ~10 decades (log-normal)."""
+    import native
+    F = torch.nn.functional
+    q, x, h1p, h1, E, (w1, b1, w2, w3), _ = _h1p_setup(B, 1000 + B)
+    b2 = torch.randn(64, device="cuda") * 0.1
+    cols = lambda dt: F.unfold(h1.permute(0, 3, 1, 2).to(dt), 4, stride=2)  # (B, 512 = (ci, ky, kx), 81)
+
+    def check(got, r64, r32):
+        scale = r64.abs().max()
+        e_s = (got.double() - r64).abs().max() / scale
+        e_f = (r32.double() - r64).abs().max() / scale
+        assert torch.isfinite(got).all()
+        assert e_s <= 2 * e_f + 1e-7, (float(e_s), float(e_f))
+    ys = []
+    for _ in range(2):
+        y = torch.full((B, 9, 9, 64), float("nan"), device="cuda")
+        bits = torch.zeros(B * 81 * 2, dtype=torch.int32, device="cuda")
+        native.nature_conv2_fwd_planes(h1p, q[1], B, q[2], b2, y, relu_bits=bits)
+        ys.append((y, bits))
+    ref = lambda dt: (torch.einsum("ck,bkp->bpc", w2.reshape(64, -1).to(dt), cols(dt)) + b2.to(dt)).relu()
+    check(ys[0][0].reshape(B, 81, 64), ref(torch.float64), ref(torch.float32))
+    assert torch.equal(ys[0][0], ys[1][0]) and torch.equal(ys[0][1], ys[1][1])
+    words = ys[0][1].view(torch.int64).view(B * 81, 1)
+    want = ((ys[0][0].reshape(B * 81, 64) > 0).long() << torch.arange(64, device="cuda")).sum(1, keepdim=True)
+    assert torch.equal(words, want)
+    del ys
+    gen = torch.Generator(device="cuda").manual_seed(B)
+    for wide in (False, True):
+        g2 = torch.randn(B, 9, 9, 64, device="cuda", generator=gen) * (torch.rand(B, 9, 9, 64, device="cuda",
+                                                                                   generator=gen) > 0.3)
+        if wide:
+            g2 = g2 * torch.exp(3.0 * torch.randn(B, 9, 9, 64, device="cuda", generator=gen))
+        ws = torch.empty(native.nature_conv2_wgrad_planes_workspace_bytes(B), dtype=torch.uint8, device="cuda")
+        outs = []
+        for _ in range(2):
+            dw = torch.full((64, 32, 4, 4), float("nan"), device="cuda")
+            db = torch.full((64,), float("nan"), device="cuda")
+            native.nature_conv2_wgrad_planes(h1p, q[1], B, g2, ws, dw, db)
+            outs.append((dw, db))
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+        dw, db = outs[0]
+        gm = lambda dt: g2.reshape(B, 81, 64).to(dt)
+        wref = lambda dt: torch.einsum("bkp,bpc->ck", cols(dt), gm(dt)).reshape(64, 32, 4, 4)
+        r64, r32 = wref(torch.float64), wref(torch.float32)
+        check(dw, r64, r32)
+        rb = g2.double().sum(dim=(0, 1, 2))
+        assert ((db.double() - rb).abs().max() / rb.abs().max()).item() < 1e-5
+        # per element: |error| / (2^-24 sum |x||g|) no more than twice the f32 GEMM's worst + 4
+        S = torch.einsum("bkp,bpc->ck", cols(torch.float64).abs(), gm(torch.float64).abs()).reshape(64, 32, 4, 4)
+        S = S.clamp_min(1e-300) * 2.0 ** -24
+        q_s = ((dw.double() - r64).abs() / S).max().item()
+        q_f = ((r32.double() - r64).abs() / S).max().item()
+        assert q_s <= 2 * q_f + 4, (wide, q_s, q_f)
