@@ -78,6 +78,15 @@ def _kernels():
                     rows_arg=2, macs=CONV_MAC[layer], bytes=per, fixed=0,
                     products=(2 if layer == 1 and op != "dgrad" else 3) if split else 0,
                     rocprof=roc.get((op, layer)) if split else None, label=f"conv{layer} {op}")
+    # H1P (conv1's output as two f16 planes, the size of its f32 form): conv1 forward writing it,
+    # conv2 forward and the direct conv2 weight gradient reading it
+    k["ppox_nature_conv1_fwd_planes"] = dict(rows_arg=1, macs=CONV_MAC[1], bytes=ACT_B[0] + ACT_B[1], fixed=0,
+                                             products=2, rocprof="fwd1_split_kernel<1, true>", label="conv1 fwd (H1P)")
+    k["ppox_nature_conv2_fwd_planes"] = dict(rows_arg=2, macs=CONV_MAC[2], bytes=ACT_B[1] + ACT_B[2], fixed=0,
+                                             products=3, rocprof="sgemm_kernel<SgFwd2P, 4, 2>", label="conv2 fwd (H1P)")
+    k["ppox_nature_conv2_wgrad_planes"] = dict(rows_arg=2, macs=CONV_MAC[2], bytes=ACT_B[1] + ACT_B[2], fixed=0,
+                                               products=3, rocprof="wgrad2_planes_kernel",
+                                               label="conv2 wgrad (H1P, direct)")
     w_fc = FC_K * FC_N * 4          # weights in as two fp16 planes (= f32 bytes) / dW out in f32
     k["ppox_nature_fc_fwd"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=ACT_B[3] + FC_N * 4, fixed=w_fc, products=3,
                                    rocprof="sgemm_kernel<SgRows<3136, 512, 0, 8, false>, 4, 3>", label="fc fwd")
@@ -312,7 +321,7 @@ def main():
             iteration()
     convs.BWD_STREAMS = streams
     totals = {k: sum(t for t, _ in v) for k, v in solo.items()}
-    prof_kernel = max(totals, key=totals.get) if any(totals.values()) else "ppox_nature_conv_wgrad_split:2"
+    prof_kernel = max(totals, key=totals.get) if any(totals.values()) else "ppox_nature_conv2_wgrad_planes"
     gae_kernel = "ppox_gae" if args.algo != "rnd" else "ppox_gae_dual"
     native.enable_event_timing([prof_kernel])
 

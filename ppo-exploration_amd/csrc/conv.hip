@@ -30,6 +30,7 @@
 // M-slice are mapped to one XCD (blockIdx % 8) so their shared G rows and
 // overlapping input patches are served from that XCD's L2.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "conv_common.h"
@@ -498,6 +499,18 @@ static_assert(FC_NB == 64, "sg2 runs the fc layer in 64-column blocks");
 // ---------------------------------------------------------------------------
 constexpr int C2S = 3, C2ROWS = C2S * 81, C2PIX = 100;
 constexpr int C2OV = (C2S * C2PIX * 8 + 511) / 512;  // float4 outputs per thread per pass
+constexpr int C2_ROW_DMAS = 8;                       // dmaA: the next triple's G rows, DMAs per thread
+constexpr int C2_TAP_DMAS = 2;                       // dmaB2: a tap pair, DMAs per thread
+// s_waitcnt immediate (gfx9 encoding) waiting for all but the n youngest vector-memory operations:
+// vmcnt bits [3:0] and [15:14], expcnt [6:4] and lgkmcnt [11:8] left at "don't wait"
+constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
+// the class-tap step i = 0 waits for the tap pair DMA'd at the step before (i = 3 of the previous
+// class); behind it that step issued the class's C2OV output stores and the next class's C2OV
+// mask loads (one memory instruction each: the stores are unconditional, the loads clamped), and
+// after class 0 the next triple's row DMAs
+constexpr int C2_WAIT_I0 = 2 * C2OV, C2_WAIT_I0_ROWS = 2 * C2OV + C2_ROW_DMAS;
+static_assert(waitcnt_vm(0) == 0x0F70 && waitcnt_vm(10) == 0x0F7A && waitcnt_vm(18) == 0x4F72, "s_waitcnt encoding");
+static_assert(C2_WAIT_I0_ROWS < 64, "vmcnt is 6 bits");
 
 // workgroup barrier that waits only for this wave's LDS operations: global loads and
 // stores stay in flight across it (__syncthreads also drains vmcnt, which would expose
@@ -518,7 +531,8 @@ __device__ inline int c2_nat_tap(int k) {  // class tap k (0..15) -> natural tap
 
 // BITS: the ReLU mask of conv1 from the forward's bitmask (a.bits_mask, 4 B per pixel) instead
 // of its f32 activations (a.mask, 128 B per pixel): 26 MB instead of 839 MB at B = 16384
-template <bool BITS>
+// SAFE: every counted wait is vmcnt(0) (PPOX_COLP_VMCNT0=1; the tests compare both bitwise)
+template <bool BITS, bool SAFE = false>
 __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4* __restrict__ wq,
                                                             long long ntriples) {
     using L = G2;
@@ -537,8 +551,9 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
     float om = 0.f;  // the largest |value| this thread stored (the output's amax)
     // taps k, k+1 (class-tap indices, mod 16) -> ring slots: 2 DMAs per thread
     auto dmaB2 = [&](int k) {
+        static_assert(2 * C2P_TAP / 512 == C2_TAP_DMAS, "dmaB2: DMAs per thread");
 #pragma unroll
-        for (int r = 0; r < 2 * C2P_TAP / 512; ++r) {
+        for (int r = 0; r < C2_TAP_DMAS; ++r) {
             const int e0 = r * 512 + wave * 64, which = e0 / C2P_TAP, within0 = e0 - which * C2P_TAP;
             const int kk = (k + which) & 15;
             __builtin_amdgcn_global_load_lds(
@@ -550,8 +565,9 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
     // An, row r's 16-B chunk c at position c ^ (r & 15): 8 DMAs per thread
     auto dmaA = [&](long long t) {
         const long long row0 = t * C2ROWS;
+        static_assert(C2_ROW_DMAS * 512 * 16 == 256 * 256, "dmaA: 256 rows of 256 B per triple");
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < C2_ROW_DMAS; ++j) {
             const int r = (wave * 8 + j) * 4 + (lane >> 4), c = (lane & 15) ^ (r & 15);
             long long grow = row0 + r;
             grow = grow < rows_total ? grow : rows_total - 1;
@@ -666,7 +682,7 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
     dmaB2(2);
     load_mask(t * C2S, 0);
     for (int e = tid; e < C2S * C2PIX * 8; e += 512) reinterpret_cast<float4*>(Ds)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the builtin, so hipcc's own wait bookkeeping sees it
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // the builtin, so hipcc's own wait bookkeeping sees it
     lds_barrier();
     take_A();
     lds_barrier();  // An free for the next triple's rows
@@ -685,12 +701,14 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
         if (i < 3 || cls < 3) mfma_tap(k + 1, next);
         rmw_tap(i_tag, cur);
         if constexpr (i == 0) {
-            if (cls == 1)
-                __builtin_amdgcn_s_waitcnt(0x4F72);  // vmcnt(18): + class 0's 8 row DMAs
+            if (SAFE)
+                __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+            else if (cls == 1)
+                __builtin_amdgcn_s_waitcnt(waitcnt_vm(C2_WAIT_I0_ROWS));  // + class 0's row DMAs
             else
-                __builtin_amdgcn_s_waitcnt(0x0F7A);  // vmcnt(10)
+                __builtin_amdgcn_s_waitcnt(waitcnt_vm(C2_WAIT_I0));
         }
-        if constexpr (i == 2) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        if constexpr (i == 2) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
         lds_barrier();
         if constexpr (i == 3) {
             output(n0, cls);
@@ -2796,10 +2814,18 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
                          "ppox_nature_conv_dgrad_split: CU count");
         const long long grid = std::min<long long>(ntriples, cus[dev]);
         a.bits_mask = relu_bits;
-        if (relu_bits)
-            dgrad2_colp_kernel<true><<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd), ntriples);
+        // PPOX_COLP_VMCNT0=1: every counted wait of the kernel as vmcnt(0) (the same result, bitwise)
+        const char* safe_env = std::getenv("PPOX_COLP_VMCNT0");
+        const bool safe = safe_env && safe_env[0] == '1';
+        const u32x4* wqv = reinterpret_cast<const u32x4*>(wqd);
+        if (relu_bits && !safe)
+            dgrad2_colp_kernel<true><<<(unsigned)grid, 512, 0, s>>>(a, wqv, ntriples);
+        else if (relu_bits)
+            dgrad2_colp_kernel<true, true><<<(unsigned)grid, 512, 0, s>>>(a, wqv, ntriples);
+        else if (!safe)
+            dgrad2_colp_kernel<false><<<(unsigned)grid, 512, 0, s>>>(a, wqv, ntriples);
         else
-            dgrad2_colp_kernel<false><<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd), ntriples);
+            dgrad2_colp_kernel<false, true><<<(unsigned)grid, 512, 0, s>>>(a, wqv, ntriples);
         PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
     }
     a.bits_mask = relu_bits;

@@ -125,14 +125,20 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
                 const float v = fmaxf((hi[i][e] + lo[i][e]) * uw + bias, 0.f);
                 om = fmaxf(om, v);  // a row past the end recomputed row m0, which is stored
                 if constexpr (PLANES) {
+                    // channel pairs (co, co ^ 1) sit in lanes L, L ^ 1: one DPP swap, then the even
+                    // lane stores the pair's hi halves and the odd lane their lo halves, 4 B each, so a
+                    // row is two 64-B runs of 4-byte stores (as many store instructions as f32)
                     const float vs = v * sy;
                     const _Float16 hv = (_Float16)vs;
                     const _Float16 lv = (_Float16)(vs - (float)hv);  // exact in f32
-                    uint16_t* y16 = reinterpret_cast<uint16_t*>(a.y) + (long long)m * (2 * L::COUT) + co;
-                    if (m < M) {
-                        y16[0] = __builtin_bit_cast(uint16_t, hv);
-                        y16[L::COUT] = __builtin_bit_cast(uint16_t, lv);
-                    }
+                    const uint32_t w = (uint32_t)__builtin_bit_cast(uint16_t, hv) |
+                                       ((uint32_t)__builtin_bit_cast(uint16_t, lv) << 16);
+                    const uint32_t pw = (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+                    const bool odd = co & 1;
+                    const uint32_t out = odd ? ((pw >> 16) | (w & 0xFFFF0000u)) : ((w & 0xFFFFu) | (pw << 16));
+                    uint16_t* y16 = reinterpret_cast<uint16_t*>(a.y) + (long long)m * (2 * L::COUT) +
+                                    (odd ? L::COUT + co - 1 : co);
+                    if (m < M) *reinterpret_cast<uint32_t*>(y16) = out;
                 } else {
                     if (m < M) a.y[(long long)m * L::COUT + co] = v;
                 }

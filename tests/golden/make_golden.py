@@ -718,6 +718,9 @@ def gen_cnn_train_big(R):
         v1 = net.state_dict()[key].detach()
         out[p + "wsum0_" + key] = np.float64(v0.double().sum())
         out[p + "whead0_" + key] = v0.flatten()[:16].numpy()
+        # the whole initial tensor: orthogonal_ runs LAPACK's QR, whose last bits differ between
+        # CPUs, so the GPU test starts from these exact values instead of re-creating them
+        out[p + "init_" + key] = v0.numpy()
         idx = weight_sample_index(v1.numel(), k)
         out[p + "w1idx_" + key] = idx
         out[p + "w1_" + key] = v1.flatten().numpy()[idx]
