@@ -25,7 +25,7 @@ import torch
 import native
 
 MATHS = ("split", "split_all", "f32")
-# ops that have a split-bf16 kernel: ("fwd" | "dgrad" | "wgrad", layer)
+# ops that have a split-f16 kernel: ("fwd" | "dgrad" | "wgrad", layer)
 SPLIT_OPS = {("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 2), ("dgrad", 3), ("wgrad", 1), ("wgrad", 2), ("wgrad", 3)}
 # ops whose split kernel exists but is not faster than the f32 one at the training batch
 # (measured, tools/conv_bench.py); "split" mode runs them in f32.  conv2 dgrad left this set
@@ -35,13 +35,13 @@ SPLIT_SLOWER = set()
 # conv2 dgrad in split math: the split kernel below this batch, the f32 kernel from it
 # (PPOX_DGRAD2_SPLIT_MAX overrides; default: split at every batch)
 DGRAD2_SPLIT_MAX_BATCH = int(os.environ.get("PPOX_DGRAD2_SPLIT_MAX", str(1 << 62)))
-# fc forward: the split-bf16 GEMM from FC_SPLIT_MIN_BATCH up (rocBLAS below; PPOX_FC_SPLIT_MIN
+# fc forward: the split-f16 GEMM from FC_SPLIT_MIN_BATCH up (rocBLAS below; PPOX_FC_SPLIT_MIN
 # overrides, default: every batch), split over K below FC_SPLITK_MAX_BATCH (tools/fc_bench.py,
 # r02: split-K 0.018 / 0.045 / 0.078 ms vs rocBLAS 0.026 / 0.062 / 0.119 ms at 512 / 2048 /
 # 4096 rows; the plain split GEMM 0.146 vs split-K 0.152 ms at 8192)
 FC_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_SPLIT_MIN", "0"))
 FC_SPLITK_MAX_BATCH = int(os.environ.get("PPOX_FC_SPLITK_MAX", "8192"))
-# fc dgrad fused with the trunk's ReLU backward + NHWC transpose (split-bf16) up to this
+# fc dgrad fused with the trunk's ReLU backward + NHWC transpose (split-f16) up to this
 # batch (PPOX_FC_DGRAD_FUSED_MAX overrides): faster than rocBLAS + nchw_to_nhwc_mask at
 # every measured batch (A/B: -33 ms per iteration at 16384, -2 ms at 2048)
 FC_DGRAD_FUSED_MAX_BATCH = int(os.environ.get("PPOX_FC_DGRAD_FUSED_MAX", str(1 << 62)))
@@ -195,7 +195,7 @@ class NatureConvs:
         self.wp3 = torch.empty(576 * 64, device=dev)
         self.wpd2 = torch.empty(4 * 256 * 32, device=dev)
         self.wpd3 = torch.empty(576 * 64, device=dev)
-        # split-bf16 planes (int16 storage), packed by ppox_nature_pack_split
+        # split-f16 planes (int16 storage), packed by ppox_nature_pack_split
         self.q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device=dev)
                   for k in (1, 2, 3, 12, 13)}
         # fc layer (feature_extractor[7], 3136 -> 512) split-f16 operands (split math only)
@@ -398,7 +398,7 @@ class NatureConvs:
 
     # ---- fc layer (split math): forward and the dgrad fused with the trunk's ReLU backward
     def fc_forward(self, h3, am):
-        """f = relu(h3 @ W^T + b), h3 (B, 7, 7, 64) NHWC (split math): the split-bf16 GEMM when
+        """f = relu(h3 @ W^T + b), h3 (B, 7, 7, 64) NHWC (split math): the split-f16 GEMM when
         the batch fills the chip (ceil(B/128) row tiles x 8 column blocks >= ~512 workgroups),
         rocBLAS on the NHWC-permuted weight below."""
         self.pack(h3.shape[0])

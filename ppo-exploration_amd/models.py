@@ -259,7 +259,7 @@ class CnnActorCritic(nn.Module):
                               w_critic_int=self.critic_int.weight.grad if self.intrinsic else None,
                               b_critic_int=self.critic_int.bias.grad if self.intrinsic else None,
                               b_int_extra=self.int_extra_layer[0].bias.grad if self.intrinsic else None)
-            if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-bf16 kernel, Flatten-order dW
+            if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-f16 kernel, Flatten-order dW
                 if side is None:
                     native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, amax_df=am[_convs.AM_DF],
                                            amax_h3=am[_convs.AM_H3])

@@ -535,7 +535,7 @@ def vecnorm_reward(rewards, dones, ret, gamma, mean, var, count, eps, clip, upda
          float(count), float(eps), float(clip), int(bool(update)), stream_ptr(stream))
 
 
-# NatureCNN fc layer 3136 -> 512 (split-bf16 GEMM, csrc/conv.hip)
+# NatureCNN fc layer 3136 -> 512 (split-f16 GEMM, csrc/conv.hip)
 def nature_fc_pack_elems():
     return int(load().ppox_nature_fc_pack_elems())
 

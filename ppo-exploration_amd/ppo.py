@@ -168,10 +168,12 @@ class BaseAlgorithm:
         self.lr, self.nstep, self.batch_size, self.n_epochs = lr, nstep, batch_size, n_epochs
         self.gamma, self.gae_lam, self.clip_range = gamma, gae_lam, clip_range
         self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
-        self.ep_info_buffer = deque(maxlen=50)
+        self._ep_info_buffer = deque(maxlen=50)
+        self._pending_episodes = None  # a collect's (returns, lengths) host copy, booked on first read
+        self._ep_host = None
         self._n_updates = 0
         self.num_timesteps = 0
-        self.num_episodes = 0
+        self._num_episodes = 0
         self.quiet = quiet
         self.obs_rms = RunningMeanStd(device=self.device)
         self._sample_counter = 0
@@ -321,21 +323,62 @@ class BaseAlgorithm:
         """Episode bookkeeping of one rollout over ALL envs (ppo.py:180-183, 98-109): every rank
         gathers the (T, N_global) episode returns / lengths, so num_episodes, ep_info_buffer and
         the reward_target decision of learn() are identical on every rank (the reference's
-        step-then-env order: row-major over (t, env))."""
+        step-then-env order: row-major over (t, env)).  The gather is enqueued here; the host
+        reads it only when ep_info_buffer / num_episodes are next read (the reference's own
+        readers: the log line, learn()'s reward_target test) — not here, where a device->host
+        copy would stall the host behind the whole collect and delay train()'s first launches."""
         ro = self.rollout
         ret = self.dist.all_gather_cat(ro.done_ret, dim=1)
         ln = self.dist.all_gather_cat(ro.done_len, dim=1)
-        fin = ~torch.isnan(ret)
-        r_fin, l_fin = ret[fin], ln[fin]
-        n_fin = r_fin.numel()
-        self.num_episodes += n_fin
+        # an earlier collect nobody read (consecutive collects): its copy landed long ago, so this is
+        # host work only, beside this collect's kernels
+        self._book_episodes()
+        host = self._ep_host
+        if host is None or host[0].shape != ret.shape:
+            pin = self.device.type == "cuda"
+            host = self._ep_host = (torch.empty(ret.shape, dtype=ret.dtype, pin_memory=pin),
+                                    torch.empty(ln.shape, dtype=ln.dtype, pin_memory=pin))
+        host[0].copy_(ret, non_blocking=True)
+        host[1].copy_(ln, non_blocking=True)
+        ev = torch.cuda.Event() if self.device.type == "cuda" else None
+        if ev is not None:
+            ev.record()
+        self._pending_episodes = (host[0], host[1], ev)
+
+    def _book_episodes(self):
+        if self._pending_episodes is None:
+            return
+        h_ret, h_ln, ev = self._pending_episodes
+        self._pending_episodes = None
+        if ev is not None:
+            ev.synchronize()
+        ret, ln = h_ret.numpy(), h_ln.numpy()
+        fin = ~np.isnan(ret)
+        r_fin, l_fin = ret[fin], ln[fin]  # row-major over (t, env), as the reference appends
+        n_fin = int(r_fin.size)
+        self._num_episodes += n_fin
         # the buffer keeps its last maxlen entries: appending only the last maxlen finished
         # episodes leaves it exactly as appending all of them (thousands per rollout at 4096
         # envs: the per-episode host loop cost ~47 ms per iteration with the GPU idle)
-        k = min(n_fin, self.ep_info_buffer.maxlen)
+        k = min(n_fin, self._ep_info_buffer.maxlen)
         if k:
-            for x, y in zip(r_fin[-k:].cpu().numpy(), l_fin[-k:].cpu().numpy()):
-                self.ep_info_buffer.append({"r": float(x), "l": int(y)})
+            for x, y in zip(r_fin[-k:], l_fin[-k:]):
+                self._ep_info_buffer.append({"r": float(x), "l": int(y)})
+
+    @property
+    def ep_info_buffer(self):
+        """deque(maxlen=50) of the last finished episodes' {"r", "l"} (ppo.py:98-109)."""
+        self._book_episodes()
+        return self._ep_info_buffer
+
+    @property
+    def num_episodes(self):
+        self._book_episodes()
+        return self._num_episodes
+
+    @num_episodes.setter
+    def num_episodes(self, v):
+        self._num_episodes = v
 
     def _batch(self, total):
         """Minibatch size: batch_size=None is one full-rollout minibatch (buffer.py:248-249)."""

@@ -93,8 +93,8 @@ def test_two_ranks_match_one_rank(algo, math, batch, monkeypatch):
     boundary; icm_loss_sharded exchanges features so the update equals one rank's.
     batch 127 over 128 rows: the last minibatch has ONE row, so one rank owns no rows of it
     and must still issue the same collectives (a mismatch hangs or fails here).
-    The decomposition is checked with exact-f32 conv math; split-bf16 math reorders
-    more (3 x 2^-22 per product): after Adam's sign-normalised first steps a few
+    The decomposition is checked with exact-f32 conv math; split-f16 math reorders
+    more (2^-22 per product): after Adam's sign-normalised first steps a few
     near-zero-gradient weights can then land ~2 lr apart between the 1- and 2-rank
     runs, so the strict weight tolerance is applied to it on PPO only.
     The RND weights are compared on their own, as updates (w - w0) against 1 % of the

@@ -864,7 +864,7 @@ def test_vecnormalize_matches_numpy_restatement():
 
 @pytest.mark.parametrize("B", [1, 130, 1000])
 def test_fc_split_gemm_vs_fp64(B):
-    """Split-bf16 fc GEMM (3136 -> 512) forward and fused dgrad vs float64, error no
+    """Split-f16 fc GEMM (3136 -> 512) forward and fused dgrad vs float64, error no
     larger than torch's f32 GEMM's (x2 headroom)."""
     import native
     torch.manual_seed(B)

@@ -224,7 +224,7 @@ def test_cnn_fixture_is_well_conditioned(golden, name):
     """The reference's float32 post-train weights are within rtol 2e-5 / atol 2e-6 of the
     same program in float64 (collect in f32 as recorded, train() in f64): the target the GPU
     parity test holds the product to is accurate at that level, so the product's tolerance
-    (1e-4 split-bf16, 5e-5 exact-f32 MFMA) measures the product, not the reference's noise."""
+    (1e-4 split-f16, 5e-5 exact-f32 MFMA) measures the product, not the reference's noise."""
     f = golden("train_cnn")
     p = name + "_"
     N, T, B, E, A, seed, net_seed = (int(x) for x in f[p + "cfg"])
