@@ -101,6 +101,19 @@ def side_stream(device, k=0):
 
 
 _events = {}
+_cur_streams = {}
+
+
+def current_stream(device):
+    """torch.cuda.current_stream(device) without its per-call device-index and Stream-object cost
+    (~10 us: the backward forks / joins the side stream several times per minibatch): the raw
+    current stream, wrapped once per (device, stream)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    raw = torch._C._cuda_getCurrentRawStream(idx)
+    s = _cur_streams.get((idx, raw))
+    if s is None:
+        s = _cur_streams[(idx, raw)] = torch.cuda.ExternalStream(raw, device=torch.device("cuda", idx))
+    return s
 
 
 def _event(side, which):
@@ -224,6 +237,8 @@ class NatureConvs:
         self._ws = {}
         self._version = None
         self._packed = set()
+        self._last_batch = None
+        self._forms_cache = {}
 
     def split_head(self, batch):
         """the heads' hidden layer on the split-f16 kernels for a `batch`-row pass"""
@@ -280,9 +295,16 @@ class NatureConvs:
         `batch`-row pass use; a later pass of another size packs only the forms still missing
         (one ppox_nature_pack_all launch for the split and fc forms)."""
         v = (self.flat.step_count, self.flat.data.data_ptr())
+        key = (batch, HEAD_SPLIT_MIN_BATCH, FC_SPLIT_MIN_BATCH, DGRAD2_SPLIT_MAX_BATCH)  # (tests patch these)
+        if v == self._version and key == self._last_batch:  # the hot path: several times per minibatch
+            return
         if v != self._version:
             self._version, self._packed = v, set()
-        missing = self._forms(batch) - self._packed
+        self._last_batch = key
+        forms = self._forms_cache.get(key)
+        if forms is None:
+            forms = self._forms_cache[key] = frozenset(self._forms(batch))
+        missing = forms - self._packed
         if not missing:
             return
         w1, w2, w3 = self.c1.weight, self.c2.weight, self.c3.weight
@@ -305,6 +327,7 @@ class NatureConvs:
     def invalidate(self):
         self._version = None
         self._packed = set()
+        self._last_batch = None
 
     # -- per-op dispatch (layer 1 input: uint8 frames, sample stride 4*84*84 bytes).  am: the
     # pass's amax table; a split kernel reads its f32 operands' rows and records its output's, an
@@ -444,7 +467,7 @@ class NatureConvs:
             if self.math != "f32":
                 native.amax(g3, am[AM_G3])
         side = side_stream(dev) if BWD_STREAMS and dev.type == "cuda" else None
-        cur = torch.cuda.current_stream() if side is not None else None
+        cur = current_stream(dev) if side is not None else None
         if side is not None:  # wgrad3 beside dgrad3 (the tensors stay referenced until the join below)
             fork(side, cur)
         self.wgrad(3, h2, B, g3, dw3, db3, am, stream=side)

@@ -226,7 +226,7 @@ class CnnActorCritic(nn.Module):
                 heads.append((self.int_extra_layer[0], self.critic_int, ie, div))
             import convs as _convs
             side = _convs.side_stream(df.device) if _convs.BWD_STREAMS and df.is_cuda else None
-            cur = torch.cuda.current_stream() if side is not None else None
+            cur = _convs.current_stream(df.device) if side is not None else None
             cv = self.conv_impl
             split = cv.split_head(B)  # the extra layer's dgrad / weight gradient on the split-f16 kernels
             des = []
