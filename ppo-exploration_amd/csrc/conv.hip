@@ -1644,7 +1644,7 @@ __device__ float kZeroG[64] = {};  // the G row of a pixel past a split's end (g
 // CB > 1: G rows hold CB blocks of COUT columns (row stride CB * COUT) and each
 // workgroup owns one block — the fc layer's weight gradient (K = the 512 outputs,
 // G = the NHWC conv3 activations, one 64-channel pixel per block); its grid is any
-// number of (split, k-block, column-block) items, column-block fastest within an XCD.
+// number of (split, column-block, k-block) items, k-block fastest within an XCD.
 template <class L, bool U8, int KT, bool ROWS, int CB = 1>
 __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     using C = WsCfg<L, U8, KT>;
@@ -1658,9 +1658,12 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         split = (q / C::KB) * 8 + xcd;
         cb = 0;
     } else {
+        // k-block fastest: the KB workgroups that read one G column block (CB > 1: a pixel of
+        // the fc layer's h3) run together on one XCD and share it through its L2 (column-block
+        // fastest re-streamed every block from HBM once per k-block: 3.5x the algorithmic bytes)
         const long long w = xcd_remap(blockIdx.x, gridDim.x);
-        cb = (int)(w % CB);
-        kb = (int)((w / CB) % C::KB);
+        kb = (int)(w % C::KB);
+        cb = (int)((w / C::KB) % CB);
         split = (int)(w / (CB * C::KB));
     }
     const unsigned M = (unsigned)(a.batch * L::P);

@@ -1269,3 +1269,98 @@ def test_conv2_dgrad_counted_waits_equal_vmcnt0(B, monkeypatch):
         native.nature_conv_dgrad_split(2, g, B, q[12], None, o, relu_bits=bits)
         outs.append(o)
     assert torch.isfinite(outs[0]).all() and torch.equal(outs[0], outs[1])
+
+
+def _fp64_check(got, r64, r32, what):
+    """normwise error vs float64 no larger than the same math in f32 (x2 headroom)"""
+    scale = r64.abs().max()
+    e_s = (got.double() - r64).abs().max() / scale
+    e_f = (r32.double() - r64).abs().max() / scale
+    assert torch.isfinite(got).all(), what
+    assert e_s <= 2 * e_f + 1e-7, (what, float(e_s), float(e_f))
+
+
+@pytest.mark.parametrize("B", [9001, 16384])
+def test_conv1_split_training_size_vs_fp64(B):
+    """The conv1 ops at training-size batches, reading their rows from step-major rollout frames
+    through the minibatch index (the bench's form): the persistent forward writing H1P and the
+    weight gradient (split-K over ~2,048-pixel slabs, fixed-order reduce) vs float64 on the device,
+    no larger than f32 math's error (x2), bitwise run-to-run; the weight gradient also per element
+    on a log-normal output grad (the f32 dot-product bound + the split floor, as
+    test_h1p_conv2_fwd_and_wgrad_vs_fp64)."""
+    import native
+    F = torch.nn.functional
+    torch.manual_seed(B)
+    T, N = 64, (B + 63) // 64 + 3
+    frames = torch.randint(0, 256, (T, N, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    idx = torch.randperm(T * N, device="cuda")[:B].to(torch.int64)
+    w1 = torch.randn(32, 4, 8, 8, device="cuda") * 0.02
+    b1 = torch.randn(32, device="cuda") * 0.1
+    w2, w3 = torch.randn(64, 32, 4, 4, device="cuda") * 0.05, torch.randn(64, 64, 3, 3, device="cuda") * 0.05
+    q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device="cuda") for k in (1, 2, 3)}
+    native.nature_pack_all(w1, w2, w3, None, None, q[1], q[2], q[3], None, None, None, None, b1=b1)
+    E = _h1p_exponent(w1, b1)
+    outs = []
+    for _ in range(2):
+        h1p = torch.empty(B, 20, 20, 64, dtype=torch.int16, device="cuda")
+        native.nature_conv1_fwd_planes(frames, B, idx, T, N, 0, q[1], b1, h1p)
+        outs.append(h1p)
+    assert torch.equal(outs[0], outs[1])
+    rows = frames.permute(1, 0, 2, 3, 4).reshape(T * N, 4, 84, 84)[idx]  # env-major row i = n * T + t
+    ref = lambda dt: F.conv2d(rows.to(dt), w1.to(dt), b1.to(dt), stride=4).relu().permute(0, 2, 3, 1)
+    _fp64_check(_h1_from_planes(outs[0], E), ref(torch.float64), ref(torch.float32), "conv1 fwd")
+    del outs
+    gen = torch.Generator(device="cuda").manual_seed(B + 1)
+    for wide in (False, True):
+        g1 = torch.randn(B, 20, 20, 32, device="cuda", generator=gen) * (torch.rand(B, 20, 20, 32, device="cuda",
+                                                                                    generator=gen) > 0.5)
+        if wide:
+            g1 = g1 * torch.exp(3.0 * torch.randn(B, 20, 20, 32, device="cuda", generator=gen))
+        ws = torch.empty(native.nature_wgrad_split_workspace_bytes(1, B), dtype=torch.uint8, device="cuda")
+        res = []
+        for _ in range(2):
+            dw, db = torch.full_like(w1, float("nan")), torch.full_like(b1, float("nan"))
+            native.nature_conv_wgrad_split_idx(1, frames, B, idx, T, N, g1, ws, dw, db)
+            res.append((dw, db))
+        assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+        dw, db = res[0]
+        gn = g1.permute(0, 3, 1, 2)
+        wref = lambda dt: torch.nn.grad.conv2d_weight(rows.to(dt), w1.shape, gn.to(dt), stride=4)
+        r64, r32 = wref(torch.float64), wref(torch.float32)
+        _fp64_check(dw, r64, r32, f"conv1 wgrad wide={wide}")
+        rb = g1.double().sum(dim=(0, 1, 2))
+        assert ((db.double() - rb).abs().max() / rb.abs().max()).item() < 1e-5
+        # per element: frames are exact (one f16 plane), so only G carries the split floor
+        S = torch.nn.grad.conv2d_weight(rows.double(), w1.shape, gn.double().abs(), stride=4) * 2.0 ** -24
+        floor = 2.0 ** -39 * g1.double().abs().max() * torch.nn.grad.conv2d_weight(
+            rows.double(), w1.shape, torch.ones_like(gn, dtype=torch.float64), stride=4)
+        q_f = ((r32.double() - r64).abs() / S.clamp_min(1e-300)).max().item()
+        excess = (dw.double() - r64).abs() - (2 * q_f + 4) * S - 2 * floor
+        assert excess.max().item() <= 0, (wide, excess.max().item(), q_f)
+
+
+@pytest.mark.parametrize("B", [9001, 16384])
+def test_conv2_dgrad_persistent_training_size_vs_fp64(B):
+    """The persistent col2im conv2 dgrad at training-size batches (3,001 / 5,462 sample triples over
+    one workgroup per CU; conv1's ReLU mask from the forward's bitmask) vs float64 on the device:
+    no larger than f32 math's error (x2), bitwise run-to-run, nothing written past the batch."""
+    import native
+    torch.manual_seed(B)
+    w1 = torch.randn(32, 4, 8, 8, device="cuda") * 0.05
+    w2 = torch.randn(64, 32, 4, 4, device="cuda") * 0.05
+    w3 = torch.randn(64, 64, 3, 3, device="cuda") * 0.05
+    q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device="cuda") for k in (1, 2, 3, 12, 13)}
+    native.nature_pack_split(w1, w2, w3, q[1], q[2], q[3], q[12], q[13])
+    g = torch.randn(B, 9, 9, 64, device="cuda")
+    h1 = torch.relu(torch.randn(B, 20, 20, 32, device="cuda"))
+    bits = _relu_bits(h1)
+    outs = []
+    for _ in range(2):
+        o = torch.full((B + 1, 20, 20, 32), 7.0, device="cuda")
+        native.nature_conv_dgrad_split(2, g, B, q[12], None, o, relu_bits=bits)
+        outs.append(o)
+    assert torch.equal(outs[0], outs[1]) and bool((outs[0][B] == 7.0).all())
+    gn, mask = g.permute(0, 3, 1, 2), (h1.permute(0, 3, 1, 2) > 0)
+    ref = lambda dt: (torch.nn.grad.conv2d_input((B, 32, 20, 20), w2.to(dt), gn.to(dt), stride=2) * mask).permute(
+        0, 2, 3, 1)
+    _fp64_check(outs[0][:B], ref(torch.float64), ref(torch.float32), "conv2 dgrad")
