@@ -106,13 +106,15 @@ _cur_streams = {}
 
 def current_stream(device):
     """torch.cuda.current_stream(device) without its per-call device-index and Stream-object cost
-    (~10 us: the backward forks / joins the side stream several times per minibatch): the raw
-    current stream, wrapped once per (device, stream)."""
+    (~10 us: the backward forks / joins the side stream several times per minibatch): torch's own
+    Stream object of the current raw stream, looked up once per (device, raw stream).  (Not an
+    ExternalStream: wrapping the default stream's handle 0 makes a new stream, which breaks the
+    fork / join ordering — tests/test_kernels_gpu.py::test_current_stream_orders_like_torch.)"""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     raw = torch._C._cuda_getCurrentRawStream(idx)
     s = _cur_streams.get((idx, raw))
     if s is None:
-        s = _cur_streams[(idx, raw)] = torch.cuda.ExternalStream(raw, device=torch.device("cuda", idx))
+        s = _cur_streams[(idx, raw)] = torch.cuda.current_stream(idx)
     return s
 
 

@@ -1364,3 +1364,30 @@ def test_conv2_dgrad_persistent_training_size_vs_fp64(B):
     ref = lambda dt: (torch.nn.grad.conv2d_input((B, 32, 20, 20), w2.to(dt), gn.to(dt), stride=2) * mask).permute(
         0, 2, 3, 1)
     _fp64_check(outs[0][:B], ref(torch.float64), ref(torch.float32), "conv2 dgrad")
+
+
+def test_current_stream_orders_like_torch():
+    """convs.current_stream (the backward's cheap current-stream lookup) is torch's current stream:
+    a side-stream read forked after a long main-stream write sees the write, and the main stream
+    after the join sees the side stream's result (convs.fork / join)."""
+    import convs
+    dev = torch.device("cuda", 0)
+    cur = convs.current_stream(dev)
+    assert cur.cuda_stream == torch.cuda.current_stream().cuda_stream
+    side = convs.side_stream(dev)
+    a = torch.randn(4096, 4096, device=dev)
+    x = torch.zeros(1, device=dev)
+    torch.cuda.synchronize()
+    for _ in range(20):
+        a = a @ a * 1e-3
+    x.fill_(1.0)
+    convs.fork(side, cur)
+    with torch.cuda.stream(side):
+        y = x * 2
+    convs.join(side, cur)
+    z = y + 1
+    torch.cuda.synchronize()
+    assert float(y) == 2.0 and float(z) == 3.0
+    s2 = torch.cuda.Stream()
+    with torch.cuda.stream(s2):
+        assert convs.current_stream(dev).cuda_stream == s2.cuda_stream
