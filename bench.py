@@ -53,10 +53,10 @@ FC_K, FC_N, HID = 3136, 512, 512
 
 def _kernels():
     k = {}
-    roc = {("fwd", 1): "fwd1_split_kernel<1>",
+    roc = {("fwd", 1): "fwd1_split_kernel<1, false>",
            ("fwd", 2): "sgemm_kernel<SgFwd<32, 20, 20, 4, 4, 2, 64, false>, 4, 2>",
            ("fwd", 3): "sgemm_kernel<SgFwd<64, 9, 9, 3, 3, 1, 64, false>, 4, 2>",
-           ("dgrad", 2): "dgrad2_colp_kernel<true>",
+           ("dgrad", 2): "dgrad2_colp_kernel<true, false>",
            ("dgrad", 3): "sgemm_kernel<SgDgradPM<64, 9, 9, 3, 3, 1, 64, true>, 4, 2>",
            ("wgrad", 1): "wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>",
            ("wgrad", 2): "wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128, false, 1>",
