@@ -297,11 +297,13 @@ int ppox_vecnorm_reward(float* rewards, const uint8_t* dones, double* ret, int64
 int64_t ppox_nature_fc_pack_elems(void);
 /* All weight packings of one optimizer step in a single launch (any output may be null):
  * wpd2 = f32 conv2 dgrad ([(ky,kx,co)][ci]); q1..q3 / qd2, qd3 = split forms (as
- * ppox_nature_pack_split); qfc_fwd / qfc_dgrad = fc split forms (as ppox_nature_fc_pack). */
+ * ppox_nature_pack_split); qfc_fwd / qfc_dgrad = fc split forms (as ppox_nature_fc_pack).
+ * zero (nullable, 16B-aligned): zero_words uint32 set to 0 before the packing kernels finish —
+ * the next pass's amax table, so a training step needs no fill launch of its own. */
 int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, const float* w3, const float* wfc,
                          float* wpd2, uint16_t* q1, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
                          uint16_t* qfc_fwd, uint16_t* qfc_dgrad, const float* wh, uint16_t* qh_fwd,
-                         uint16_t* qh_dgrad, void* stream);
+                         uint16_t* qh_dgrad, uint32_t* zero, int64_t zero_words, void* stream);
 /* conv1 -> conv2 on H1P, the split-f16 operand form of conv1's output h1 (Conv2d(4, 32, 8, 4) + ReLU
  * of models-checkpoint.py:52-53): per pixel (NHWC) its 32 channels' high f16 plane then their low
  * plane, h1 * 2^E = hi + lo (128 B per pixel, the size of the f32 form), E derived by
@@ -488,7 +490,8 @@ int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, int64_t batch
  * (inverse_model), Wae (action_encoder) contiguous in that (module) order,
  * ppox_icm_param_elems(n_actions) floats; the gradient segment has the same layout.
  * The encoder's Linear(K, 32) runs split-bf16 (fp32-class, as K6); everything deterministic.
- *   ppox_icm_pack_w1:    W1 (32 x K f32) -> ppox_icm_w1_pack_elems(K) bf16 planes.
+ *   ppox_icm_pack_w1:    W1 (32 x K f32, K % 64 == 0) -> ppox_icm_w1_pack_elems(K) uint16: its two
+ *                        f16 planes (row n times 2^E[n]) in the forward's fragment order, then E[32].
  *   ppox_icm_encode:     pre1 = x W1^T + b1, phi = leaky(pre1) W2^T + b2 for `rows` frame rows
  *                        (idx != NULL: env-major rollout rows of the step-major (T, N_env, ...)
  *                        frames, as ppox_nature_conv_fwd_split); rowno (nullable, uint32 per
@@ -502,7 +505,8 @@ int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, int64_t batch
  *                        row (with pairs == NULL every row of both is written).  partials:
  *                        ppox_icm_partials_bytes(rows, n_actions).
  *   ppox_icm_row_backward: dphi = dS + dN (dN nullable) of minibatch row pos[i] (pos nullable)
- *                        -> g1 = dL/dpre1 as planes (ppox_icm_g1_pack_elems(rows) uint16)
+ *                        -> g1 = dL/dpre1 in fragment order (f32) + per-column max |g1| of each
+ *                        32-row block (ppox_icm_g1_pack_elems(rows) uint16)
  *                        + partials of db1, dW2, db2.
  *   ppox_icm_grad_reduce: partials -> grad_seg (overwritten) and, loss_accum != NULL,
  *                        loss_accum[0] += this call's share of (1 - beta) CE + beta MSE.

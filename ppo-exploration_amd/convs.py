@@ -292,14 +292,15 @@ class NatureConvs:
             forms |= {"qhf", "qhd"}
         return forms
 
-    def pack(self, batch=0):
+    def pack(self, batch=0, zero=None):
         """Pack the weights (once per optimizer step) into the layouts the kernels of a
         `batch`-row pass use; a later pass of another size packs only the forms still missing
-        (one ppox_nature_pack_all launch for the split and fc forms)."""
+        (one ppox_nature_pack_all call for the split and fc forms).  `zero` (int32 tensor) is
+        zeroed by that call when it runs: returns True if it did."""
         v = (self.flat.step_count, self.flat.data.data_ptr())
         key = (batch, HEAD_SPLIT_MIN_BATCH, FC_SPLIT_MIN_BATCH, DGRAD2_SPLIT_MAX_BATCH)  # (tests patch these)
         if v == self._version and key == self._last_batch:  # the hot path: several times per minibatch
-            return
+            return False
         if v != self._version:
             self._version, self._packed = v, set()
         self._last_batch = key
@@ -308,7 +309,8 @@ class NatureConvs:
             forms = self._forms_cache[key] = frozenset(self._forms(batch))
         missing = forms - self._packed
         if not missing:
-            return
+            return False
+        zeroed = False
         w1, w2, w3 = self.c1.weight, self.c2.weight, self.c3.weight
         pick = lambda name, buf: buf if name in missing else None
         if missing & {"wp1", "wp2", "wp3", "wpd3"}:
@@ -321,10 +323,12 @@ class NatureConvs:
             native.nature_pack_all(w1, w2, w3, self.fc.weight, pick("wpd2", self.wpd2), pick("q1", q[1]),
                                    pick("q2", q[2]), pick("q3", q[3]), pick("qd2", q[12]), pick("qd3", q[13]),
                                    pick("qfcf", qfc[0]), pick("qfcd", qfc[1]), self.hid.weight, pick("qhf", qh[0]),
-                                   pick("qhd", qh[1]), b1=self.c1.bias)
+                                   pick("qhd", qh[1]), b1=self.c1.bias, zero=zero)
+            zeroed = zero is not None
         if "wfc_nhwc" in missing:
             torch.index_select(self.fc.weight.detach(), 1, self.fc_perm, out=self.wfc_nhwc)
         self._packed |= missing
+        return zeroed
 
     def invalidate(self):
         self._version = None
@@ -399,9 +403,13 @@ class NatureConvs:
         PassState (the amax table's AM_* rows — the backward of the same pass records its
         gradients' rows — and, for a `train` pass, conv1's ReLU bitmask); h3 is
         NHWC (B, 7, 7, 64) in split math (self.nhwc3), NCHW (B, 64, 7, 7) in f32 math."""
-        self.pack(x.shape[0])
         B = x.shape[0]
         dev = x.device
+        # the pass's amax table: zeroed by the weight packing when this pass runs it (the first
+        # pass after an optimizer step), by a fill otherwise
+        table = torch.empty((AM_ROWS, native.AMAX_SLOTS), dtype=torch.int32, device=dev)
+        if not self.pack(B, zero=table):
+            table.zero_()
         h1 = self.empty_h1(B, dev)
         h2 = torch.empty((B, 9, 9, 64), device=dev)
         h3 = torch.empty((B, 7, 7, 64) if self.nhwc3 else (B, 64, 7, 7), device=dev)
@@ -414,7 +422,7 @@ class NatureConvs:
                      if train and (RELU_BITS or (L == 1 and self.h1p)) and self.uses_split("fwd", L) and
                      consumer[L - 1] else None
                      for L, P, C in ((1, 400, 32), (2, 81, 64), (3, 49, 64)))
-        am = PassState(native.amax_table(AM_ROWS, dev), bits)
+        am = PassState(table, bits)
         if B:
             self.fwd(1, x, B, self.c1.bias, h1, am)
             self.fwd(2, h1, B, self.c2.bias, h2, am)

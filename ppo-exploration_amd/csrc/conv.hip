@@ -2366,6 +2366,8 @@ struct PackAll {
     const float* wh = nullptr;                         // the heads' hidden layer (512 x 512)
     uint16_t *qhf = nullptr, *qhd = nullptr;           // its forward (W^T) and dgrad (W) forms
     const float* b1 = nullptr;                         // conv1 bias (with q1: the H1P exponent)
+    uint32_t* zero = nullptr;                          // words zeroed by wmax_kernel (a pass's amax table)
+    long long zero_words = 0;
 };
 constexpr long long PA_N1 = 8 * 2 * 64 * 8, PA_N2 = (long long)G2::K * G2::COUT, PA_N3 = (long long)G3::K * G3::COUT;
 constexpr long long PA_NFC = (long long)FcFwd::NCB * FcFwd::K * FcFwd::NOUT;
@@ -2465,10 +2467,48 @@ __device__ inline void pa_forms(const PackAll& p, int t, uint16_t* (&f)[2], long
 }
 constexpr int PA_TENSORS = 5;
 
+// The H1P exponent of conv1's output (one workgroup): |h1| <= 255 max_c (sum_k |W1[c][k]|) +
+// |b1[c]| for uint8 frames; thread t sums k-range t & 7 of channel t >> 3 in f64.  Stored in
+// slot H1P_EXP_SLOT of q1's tail, read by the conv1 forward (output scale) and the H1P consumers.
+// The bound carries a 2^-10 margin, so every value times 2^E stays below 2^15 (f16 max 65504).
+__device__ void h1p_exp_block(const float* __restrict__ w1, const float* __restrict__ b1, uint16_t* __restrict__ q1) {
+    const int t = threadIdx.x, c = t >> 3, part = t & 7;
+    double sum = 0.0;
+    for (int k = part * 32; k < part * 32 + 32; ++k) sum += fabs((double)w1[c * G1::K + k]);
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) sum += __shfl_xor(sum, o);
+    double bound = 255.0 * sum + fabs((double)b1[c]);
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) bound = fmax(bound, __shfl_xor(bound, o));
+    __shared__ double red[4];
+    if ((t & 63) == 0) red[t >> 6] = bound;
+    __syncthreads();
+    if (t == 0) {
+        const double m = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+        const float mf = (float)(m * (1.0 + 1.0 / 1024.0));
+        pack_tail(q1, PL_Q1)[AMAX_SLOTS + H1P_EXP_SLOT] = (uint32_t)split_scale_exp(__float_as_uint(mf));
+    }
+}
+
 // AMAX_SLOTS workgroups per weight tensor: workgroup b's max |w| over its stride into slot b of
 // the tails of both forms (every slot written: no zeroing), so the packer's amax_read sees the
-// tensor's max
+// tensor's max.  Then one workgroup for the H1P exponent (with q1 and b1), then the workgroups
+// zeroing p.zero (the next pass's amax table: no fill launch of its own)
 __global__ void __launch_bounds__(256) wmax_kernel(PackAll p) {
+    if (blockIdx.x >= PA_TENSORS * AMAX_SLOTS) {
+        const long long zb = (long long)blockIdx.x - PA_TENSORS * AMAX_SLOTS - 1;
+        if (zb < 0) {
+            if (p.q1 && p.b1) h1p_exp_block(p.w1, p.b1, p.q1);
+            return;
+        }
+        const long long i = (zb * 256 + threadIdx.x) * 4;  // this thread's four words
+        if (i + 4 <= p.zero_words) {
+            *reinterpret_cast<uint4*>(p.zero + i) = make_uint4(0u, 0u, 0u, 0u);
+        } else {
+            for (long long k = i; k < p.zero_words; ++k) p.zero[k] = 0u;  // a ragged tail
+        }
+        return;
+    }
     const int t = blockIdx.x / AMAX_SLOTS, b = blockIdx.x % AMAX_SLOTS;
     uint16_t* f[2];
     long long planes;
@@ -2532,30 +2572,6 @@ __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long tota
     }
 }
 
-// The H1P exponent of conv1's output (one workgroup): |h1| <= 255 max_c (sum_k |W1[c][k]|) +
-// |b1[c]| for uint8 frames; thread t sums k-range t & 7 of channel t >> 3 in f64.  Stored in
-// slot H1P_EXP_SLOT of q1's tail, read by the conv1 forward (output scale) and the H1P consumers.
-// The bound carries a 2^-10 margin, so every value times 2^E stays below 2^15 (f16 max 65504).
-__global__ void __launch_bounds__(256) h1p_exp_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
-                                                     uint16_t* __restrict__ q1) {
-    const int t = threadIdx.x, c = t >> 3, part = t & 7;
-    double sum = 0.0;
-    for (int k = part * 32; k < part * 32 + 32; ++k) sum += fabs((double)w1[c * G1::K + k]);
-#pragma unroll
-    for (int o = 1; o < 8; o <<= 1) sum += __shfl_xor(sum, o);
-    double bound = 255.0 * sum + fabs((double)b1[c]);
-#pragma unroll
-    for (int o = 8; o < 64; o <<= 1) bound = fmax(bound, __shfl_xor(bound, o));
-    __shared__ double red[4];
-    if ((t & 63) == 0) red[t >> 6] = bound;
-    __syncthreads();
-    if (t == 0) {
-        const double m = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-        const float mf = (float)(m * (1.0 + 1.0 / 1024.0));
-        pack_tail(q1, PL_Q1)[AMAX_SLOTS + H1P_EXP_SLOT] = (uint32_t)split_scale_exp(__float_as_uint(mf));
-    }
-}
-
 int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
     for (const void* q : {(const void*)p.wpd2, (const void*)p.q1, (const void*)p.q2, (const void*)p.q3,
                           (const void*)p.qd2, (const void*)p.qd3, (const void*)p.qfcf, (const void*)p.qfcd})
@@ -2565,17 +2581,15 @@ int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
                  "ppox_nature_pack: null weights");
     PPOX_REQUIRE((!p.qhf || ppox::aligned16(p.qhf)) && (!p.qhd || ppox::aligned16(p.qhd)),
                  "ppox_nature_pack: packed buffers must be 16-byte aligned");
-    wmax_kernel<<<PA_TENSORS * AMAX_SLOTS, 256, 0, s>>>(p);
+    PPOX_REQUIRE(!p.zero_words || (p.zero && ppox::aligned16(p.zero)), "ppox_nature_pack_all: zero buffer");
+    const long long zblocks = ppox::ceil_div(p.zero_words, 1024LL);
+    wmax_kernel<<<(unsigned)(PA_TENSORS * AMAX_SLOTS + 1 + zblocks), 256, 0, s>>>(p);
     PPOX_LAUNCHED_NORET(name);
     // element ranges end at the last job present (the head and fc dgrad ranges are the longest)
     const long long total = PA_N1 + 2 * PU_2 + 2 * PU_3 + PA_N2 + PU_FC +
                             (p.qhf || p.qhd ? PU_FCD + 2 * PU_H : (p.qfcd ? PU_FCD : 0));
     const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 4096);
     pack_all_kernel<<<blocks, 256, 0, s>>>(p, total);
-    if (p.q1 && p.b1) {
-        PPOX_LAUNCHED_NORET(name);
-        h1p_exp_kernel<<<1, 256, 0, s>>>(p.w1, p.b1, p.q1);
-    }
     PPOX_LAUNCHED(name);
 }
 
@@ -3062,11 +3076,14 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
 extern "C" int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, const float* w3,
                                     const float* wfc, float* wpd2, uint16_t* q1, uint16_t* q2, uint16_t* q3,
                                     uint16_t* qd2, uint16_t* qd3, uint16_t* qfc_fwd, uint16_t* qfc_dgrad,
-                                    const float* wh, uint16_t* qh_fwd, uint16_t* qh_dgrad, void* stream) {
+                                    const float* wh, uint16_t* qh_fwd, uint16_t* qh_dgrad, uint32_t* zero,
+                                    int64_t zero_words, void* stream) {
     PPOX_REQUIRE(w1 && w2 && w3 && (wfc || (!qfc_fwd && !qfc_dgrad)), "ppox_nature_pack_all: null weights");
     PPOX_REQUIRE(!q1 || b1, "ppox_nature_pack_all: q1 needs the conv1 bias b1 (the H1P exponent)");
+    PPOX_REQUIRE(zero_words >= 0 && (zero_words == 0 || zero), "ppox_nature_pack_all: zero buffer");
     return launch_pack_all(
-        PackAll{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh, qh_fwd, qh_dgrad, b1},
+        PackAll{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh, qh_fwd, qh_dgrad, b1, zero,
+                zero_words},
         ppox::as_stream(stream), "ppox_nature_pack_all");
 }
 

@@ -4,17 +4,22 @@
 // actions and the feature size 32 (int_hidden_size).
 //
 // The state encoder's first layer Linear(4*84*84 -> 32) is 99.6 % of the module's
-// bytes and FLOPs.  Its input is the uint8 frame row, exact in ONE bf16 plane, so both
-// of its GEMMs run on the bf16 matrix cores with the f32 operand split exactly into
-// three bf16 planes (conv_split.hip): x*w0 + x*w1 + x*w2, every product exact in f32,
-// a0 terms in one accumulator, the small terms in a second (fp32-class, see
-// conv_common.h).  The frames are read where the rollout holds them (optional env-major
-// row index, like the conv1 kernels): no gather, no u8 -> f32 copy.
-//   encoder forward   y = x W1^T : split-K MFMA partials + a finishing kernel that sums
-//                     them in a fixed order and runs the tiny rest of the encoder
+// bytes and FLOPs.  Its input is the uint8 frame row, exact in ONE f16 plane, so both of
+// its GEMMs run split-f16 on v_mfma_f32_32x32x16_f16 (conv_common.h): the f32 operand
+// times a power of two 2^E is split exactly into two f16 planes, x*h + x*l, every product
+// exact in f32, the h terms in one accumulator and the l terms in a second (fp32-class).
+// E is per output feature n (W1 row n / g1 column n: the MFMA tile's row or column, so
+// the unscale is one multiply per accumulator).  The frames are read where the rollout
+// holds them (optional env-major row index, like the conv1 kernels): no gather, no
+// u8 -> f32 copy.
+//   encoder forward   y = x W1^T : split-K MFMA partials — frame rows and W1 planes
+//                     copied global -> LDS by global_load_lds_dwordx4 into a three-slot
+//                     ring (64-B row pieces, XOR-swizzled) — + a finishing kernel that
+//                     sums them in a fixed order and runs the tiny rest of the encoder
 //                     (+ b1, LeakyReLU, Linear(32, 32)) per row;
-//   encoder wgrad     dW1 = g1^T x : MFMA over the rows, g1 pre-split into planes by the
-//                     row backward kernel, 4-wave LDS reduction in a fixed order.
+//   encoder wgrad     dW1 = g1^T x : MFMA over the rows, g1 written in fragment order by
+//                     the row backward kernel with its per-column amax partials, split in
+//                     registers; 8-wave LDS reduction in a fixed order.
 // Everything else is 32-wide per row or per pair and runs in two LDS kernels:
 //   pair kernel       inverse model + forward model + both losses (cross entropy, MSE)
 //                     and their backward for the pairs (row j, row j + 1) of the
@@ -124,35 +129,66 @@ struct Seg {
 };
 
 // ---------------------------------------------------------------------------
-// W1 [32][K] -> split planes, the B fragments of the encoder forward:
-// q[((s * 3 + p) * 64 + lane) * 8 + e] = plane p of W1[lane & 31][k],
-// k = 32 (s >> 1) + 16 (lane >> 5) + 8 (s & 1) + e  (s: MFMA k-step of 16)
+// W1 [32][K] -> its two f16 planes, row n times 2^E[n] (E[n] = split_scale_exp of the row's
+// own amax), in the B-fragment order of the encoder forward's 64-k chunks:
+// q[(((c * 4 + s) * 2 + p) * 64 + lane) * 8 + e] = plane p of W1[lane & 31][k] 2^E,
+// k = 64 c + 32 (s >> 1) + 16 (lane >> 5) + 8 (s & 1) + e; the 32 int32 exponents follow
+// the planes.  One workgroup per row n: its amax, then its 8-k runs.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) icm_pack_w1_kernel(const float* __restrict__ w, int K, u32x4* __restrict__ q) {
-    const long long t = blockIdx.x * 256LL + threadIdx.x;
-    const long long S = K / 16;
-    if (t >= S * 64) return;
-    const int lane = (int)(t & 63);
-    const long long s = t >> 6;
-    const int n = lane & 31, h = lane >> 5;
-    const long long k0 = 32 * (s >> 1) + 16 * h + 8 * (s & 1);
-    const float4* src = reinterpret_cast<const float4*>(w + (long long)n * K + k0);
-    u32x4 p0, p1, p2;
-    split8(src[0], src[1], p0, p1, p2);
-    q[(s * 3 + 0) * 64 + lane] = p0;
-    q[(s * 3 + 1) * 64 + lane] = p1;
-    q[(s * 3 + 2) * 64 + lane] = p2;
+constexpr int ENC_CK = 64;  // k (frame bytes per row) of one forward chunk
+
+__global__ void __launch_bounds__(1024) icm_pack_w1_kernel(const float* __restrict__ w, int K, u32x4* __restrict__ q) {
+    __shared__ uint32_t red[16];
+    const int n = blockIdx.x, tid = threadIdx.x;
+    const float* wr = w + (long long)n * K;
+    uint32_t m = 0u;
+    for (int k = tid * 4; k < K; k += 4096) {
+        const float4 v = *reinterpret_cast<const float4*>(wr + k);
+        m = max(max(m, max(__float_as_uint(fabsf(v.x)), __float_as_uint(fabsf(v.y)))),
+                max(__float_as_uint(fabsf(v.z)), __float_as_uint(fabsf(v.w))));
+    }
+    m = wave_max_u32(m);
+    if ((tid & 63) == 0) red[tid >> 6] = m;
+    __syncthreads();
+    m = red[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) m = max(m, red[i]);
+    const int E = split_scale_exp(m);
+    const float sc = exp2i(E);
+    for (int g = tid; g < K / 8; g += 1024) {
+        const int k0 = g * 8, c = k0 / ENC_CK, r = k0 % ENC_CK;
+        const int st = 2 * (r >> 5) + ((r >> 3) & 1), lane = n + 32 * ((r >> 4) & 1);
+        u32x4 p0, p1;
+        split8h(*reinterpret_cast<const float4*>(wr + k0), *reinterpret_cast<const float4*>(wr + k0 + 4), sc, p0, p1);
+        q[((c * 4 + st) * 2 + 0) * 64 + lane] = p0;
+        q[((c * 4 + st) * 2 + 1) * 64 + lane] = p1;
+    }
+    if (tid == 0) reinterpret_cast<int*>(q + (long long)K / 16 * 2 * 64)[n] = E;
 }
 
 // ---------------------------------------------------------------------------
-// Encoder forward partials: workgroup (K chunk kc, row group rg), 8 waves; WR waves
-// split the rows (64 each: two 32-row MFMA tiles), KG = 8 / WR waves split the chunk's K
-// (interleaved double steps, summed through LDS in wave order).  One double step = 32 k:
-// a lane loads 16 frame bytes per tile (row lane & 31, bytes 16 (lane >> 5) ..) and the
-// six W1 fragments (2 k-steps x 3 planes) — 12 MFMAs.  slab[kc][row][32] = this chunk's
-// x W1^T.  ENC_STAGES double steps are in flight per wave.
+// Encoder forward partials: workgroup (K range kc, 256 rows rg), 4 waves x 64 rows (two
+// 32-row MFMA tiles sharing each B fragment).  Per 64-k chunk the frame rows (16 KB: 64 B
+// per row) and the chunk's W1 planes (8 KB) are copied global -> LDS by
+// global_load_lds_dwordx4 into a three-slot ring: each wave copies its own 64 rows (4 x
+// 1 KB, 16 rows each) and two of the eight 1 KB W1 pieces.  K loop (as the sg2 GEMM in
+// conv.hip): wait for this wave's copies of chunk c (the next chunk's may stay in flight),
+// one barrier (every wave's copies landed, every wave done with chunk c - 1), issue chunk
+// c + 2 into chunk c - 1's slot, then 12 ds_read_b128 + 16 MFMAs.  A row's four 16-B
+// pieces sit XOR-swizzled by (row >> 2) & 3 (the copy is lane-linear in LDS, so the
+// swizzle is on each lane's global source), which makes every fragment read
+// conflict-free.  MFMA k-step s of the chunk, lane half h: k = 32 (s >> 1) + 16 h +
+// 8 (s & 1) + e, so one ds_read_b128 of piece 2 (s >> 1) + h feeds two k-steps.
+// slab[kc][row][32] = this K range's x W1^T (unscaled).  Measured (MI355X): 15.5 us at 2048 rows
+// (3.7 TB/s of frames), 104 us at 16384 (4.4 TB/s); deeper rings (4, 5 slots), 512 workgroups
+// and 128-row x 256-B super-chunks (whole 256-B runs per row, twice the W1 bytes per frame
+// byte) all measured slower.
 // ---------------------------------------------------------------------------
-constexpr int ENC_STAGES = 3;
+constexpr int ENC_WAVES = 4, ENC_ROWS = 64 * ENC_WAVES, ENC_SLOTS = 3;
+constexpr int ENC_AB = ENC_ROWS * ENC_CK;      // frame bytes of a chunk
+constexpr int ENC_BB = 4 * 2 * 64 * 16;        // W1 plane bytes of a chunk (4 k-steps x 2 planes)
+constexpr int ENC_SLOT = ENC_AB + ENC_BB;
+constexpr int ENC_NDMA = 4 + ENC_BB / 1024 / ENC_WAVES;  // copies per wave per chunk
 
 struct EncArgs {
     const uint8_t* x;
@@ -165,87 +201,133 @@ struct EncArgs {
     int nkc, nrg;
 };
 
-template <int WR, int KG>
-__global__ void __launch_bounds__(64 * WR * KG) icm_enc_fwd_kernel(EncArgs a) {
-    __shared__ float red[KG > 1 ? (KG - 1) * WR * 32 * 64 : 1];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int rgw = wave % WR, kg = wave / WR;
-    const long long j = xcd_remap(blockIdx.x, gridDim.x);  // a K chunk's row groups share an XCD (W1 in L2)
+__device__ inline u32x4 enc_ds_read(uint32_t addr) {
+    u32x4 r;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+    return r;
+}
+// wait until at most N LDS reads are outstanding; the four registers are tied, so no use of
+// them is scheduled above the wait
+template <int N>
+__device__ inline void enc_lgkm_wait(u32x4& a, u32x4& b, u32x4& c, u32x4& d) {
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N));
+}
+template <int N>
+__device__ inline void enc_vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__global__ void __launch_bounds__(64 * ENC_WAVES, 2) icm_enc_fwd_kernel(EncArgs a) {
+    // all LDS in ONE __shared__ object (a second one can make hipcc wait vmcnt(0) in the loop)
+    __shared__ __attribute__((aligned(16))) uint8_t lds[ENC_SLOTS * ENC_SLOT];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: copy bases go to M0
+    const long long j = xcd_remap(blockIdx.x, gridDim.x);  // a K range's row groups share an XCD (W1 in L2)
     const int kc = (int)(j / a.nrg), rg = (int)(j % a.nrg);
-    const int ND = a.K / 32;
-    const int d0 = (int)((long long)kc * ND / a.nkc), d1 = (int)((long long)(kc + 1) * ND / a.nkc);
-    const long long rbase = (long long)rg * (WR * 64) + rgw * 64;
-    const uint8_t* xp[2];
+    const int NC = a.K / ENC_CK;
+    const int c0 = (int)((long long)kc * NC / a.nkc), nchunk = (int)((long long)(kc + 1) * NC / a.nkc) - c0;
+    // copy sources: A copy i of this wave covers rows 64 wave + 16 i + (lane >> 2), LDS piece
+    // lane & 3, which holds global piece (lane & 3) ^ ((row >> 2) & 3) = (lane & 3) ^ ((lane >> 4) & 3)
+    const uint8_t* asrc[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        long long r = rbase + 32 * i + (lane & 31);
-        r = r < a.M ? r : a.M - 1;  // clamped rows are computed, never stored
+    for (int i = 0; i < 4; ++i) {
+        long long r = (long long)rg * ENC_ROWS + wave * 64 + 16 * i + (lane >> 2);
+        r = r < a.M ? r : a.M - 1;  // rows past the end: a valid clamped row, computed, never stored
         long long row = r;
         if (a.idx) {
             const long long s = a.idx[r];
             row = (s % a.T) * a.Nenv + s / a.T;
         }
-        xp[i] = a.x + row * a.K + 16 * (lane >> 5);
+        asrc[i] = a.x + row * a.K + (long long)c0 * ENC_CK + (((lane & 3) ^ ((lane >> 4) & 3)) << 4);
     }
-    const u32x4* qp = a.q + lane;
+    const u32x4* bsrc = a.q + (long long)c0 * (ENC_BB / 16) + lane;
+    auto issue = [&](int c, auto S) {
+        constexpr int slot = decltype(S)::value;
+        c = c < nchunk ? c : nchunk - 1;  // past the end: the last chunk again, never read
+        uint8_t* base = lds + slot * ENC_SLOT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(asrc[i] + c * ENC_CK),
+                                             (__attribute__((address_space(3))) void*)(base + (wave * 64 + 16 * i) *
+                                                                                                  ENC_CK),
+                                             16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < ENC_NDMA - 4; ++i) {
+            const int piece = (ENC_NDMA - 4) * wave + i;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void*)(bsrc + (long long)c * (ENC_BB / 16) + piece * 64),
+                (__attribute__((address_space(3))) void*)(base + ENC_AB + piece * 1024), 16, 0, 0);
+        }
+    };
+    const int r = lane & 31, h = lane >> 5, sw = (r >> 2) & 3;
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
+    const uint32_t a_lane = lds0 + (wave * 64 + r) * ENC_CK, b_lane = lds0 + ENC_AB + lane * 16;
     f32x16 hi[2], lo[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) hi[i] = lo[i] = zero16();
-    using Xs = uint4[2];
-    using Ws = u32x4[6];
-    auto load = [&](int d, Xs& xs, Ws& ws) {
+    for (int t = 0; t < 2; ++t) hi[t] = lo[t] = zero16();
+    auto compute = [&](auto S) {
+        constexpr int slot = decltype(S)::value;
+        const uint32_t ab = a_lane + slot * ENC_SLOT, bb = b_lane + slot * ENC_SLOT;
+        u32x4 f[2][4];  // k-step pair qq: A pieces of tiles 0, 1, then B planes 0, 1 of k-step 2 qq ...
+        u32x4 g[2][2];  // ... and of k-step 2 qq + 1
 #pragma unroll
-        for (int i = 0; i < 2; ++i) xs[i] = *reinterpret_cast<const uint4*>(xp[i] + 32LL * d);
+        for (int qq = 0; qq < 2; ++qq) {
 #pragma unroll
-        for (int u = 0; u < 6; ++u) ws[u] = qp[(6LL * d + u) * 64];  // (s = 2d + u / 3, plane u % 3)
-    };
-    auto step = [&](const Xs& xs, const Ws& ws) {
+            for (int t = 0; t < 2; ++t) f[qq][t] = enc_ds_read(ab + t * 32 * ENC_CK + (((2 * qq + h) ^ sw) << 4));
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+            for (int p = 0; p < 2; ++p) f[qq][2 + p] = enc_ds_read(bb + ((2 * qq) * 2 + p) * 1024);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const u32x4 av = u8x8_to_bf16(h ? xs[i].z : xs[i].x, h ? xs[i].w : xs[i].y);
-                hi[i] = mfma_bf16(av, ws[3 * h], hi[i]);
-                lo[i] = mfma_bf16(av, ws[3 * h + 1], lo[i]);
-                lo[i] = mfma_bf16(av, ws[3 * h + 2], lo[i]);
+            for (int p = 0; p < 2; ++p) g[qq][p] = enc_ds_read(bb + ((2 * qq + 1) * 2 + p) * 1024);
+        }
+        auto pair = [&](int qq) {
+#pragma unroll
+            for (int so = 0; so < 2; ++so) {
+                const u32x4 b0 = so ? g[qq][0] : f[qq][2], b1 = so ? g[qq][1] : f[qq][3];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const u32x4 av = u8x8_to_f16(f[qq][t][2 * so], f[qq][t][2 * so + 1]);
+                    hi[t] = mfma_f16(av, b0, hi[t]);
+                    lo[t] = mfma_f16(av, b1, lo[t]);
+                }
             }
+        };
+        enc_lgkm_wait<6>(f[0][0], f[0][1], f[0][2], f[0][3]);
+        enc_lgkm_wait<6>(g[0][0], g[0][1], f[0][2], f[0][3]);
+        pair(0);
+        enc_lgkm_wait<0>(f[1][0], f[1][1], f[1][2], f[1][3]);
+        enc_lgkm_wait<0>(g[1][0], g[1][1], f[1][2], f[1][3]);
+        pair(1);
     };
-    constexpr int S = ENC_STAGES;
-    Xs xs[S];
-    Ws ws[S];
-    const int ds = d0 + kg;
-    const int cnt = ds < d1 ? (d1 - ds + KG - 1) / KG : 0;  // this wave's double steps ds + KG i
-    pipeline<S>(cnt, [&](int i, int u) { load(ds + KG * i, xs[u], ws[u]); }, [&](int u) { step(xs[u], ws[u]); });
-    float acc[2][16];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][e] = hi[i][e] + lo[i][e];
-    if constexpr (KG > 1) {
-        if (kg > 0) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) red[(((kg - 1) * WR + rgw) * 32 + i * 16 + e) * 64 + lane] = acc[i][e];
-        }
-        __syncthreads();
-        if (kg == 0) {
+    // one pipeline step: this wave's copies of chunk c waited for (chunk c + 1's may stay in
+    // flight: the clamped re-issues past the end count too, so the count is the same in every
+    // step), one barrier, chunk c + 2 issued into the slot chunk c - 1 used, chunk c computed
+    auto step = [&](int c, auto S, auto S2) {
+        enc_vm_wait<ENC_NDMA * (ENC_SLOTS - 2)>();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        issue(c + ENC_SLOTS - 1, S2);
+        compute(S);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    issue(0, I0{});
+    issue(1, I1{});
 #pragma unroll 1
-            for (int g = 1; g < KG; ++g)
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) acc[i][e] += red[(((g - 1) * WR + rgw) * 32 + i * 16 + e) * 64 + lane];
-        }
+    for (int c = 0; c < nchunk; c += 3) {
+        step(c, I0{}, I2{});
+        if (c + 1 < nchunk) step(c + 1, I1{}, I0{});
+        if (c + 2 < nchunk) step(c + 2, I2{}, I1{});
     }
-    if (kg != 0) return;
-    // C/D map: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+    enc_vm_wait<0>();  // the clamped tail copies, before the LDS is released
+    // unscale by the lane's feature exponent; C/D map: col n = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 h
+    const int* wexp = reinterpret_cast<const int*>(a.q + (long long)NC * (ENC_BB / 16));
+    const float uw = exp2i(-wexp[r]);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            const long long row = rbase + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-            if (row < a.M) a.slab[((long long)kc * a.M + row) * H + (lane & 31)] = acc[i][e];
+            const long long row = (long long)rg * ENC_ROWS + wave * 64 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
+            if (row < a.M) a.slab[((long long)kc * a.M + row) * H + r] = (hi[t][e] + lo[t][e]) * uw;
         }
 }
 
@@ -473,8 +555,9 @@ __global__ void __launch_bounds__(256) icm_pair_kernel(PairArgs a) {
 // ---------------------------------------------------------------------------
 // Row kernel: RB rows per block.  dphi = dS + dN of the row's minibatch position;
 // g1 = (dphi W2) * leaky'(pre1); partials of db1, dW2 = dphi^T leaky(pre1), db2; g1
-// written as split planes in the A-fragment order of the weight-gradient MFMA:
-// gq[((rs * 3 + p) * 64 + lane) * 8 + e] = plane p of g1[16 rs + 8 (lane >> 5) + e][lane & 31].
+// written in the A-fragment order of the weight-gradient MFMA,
+// gq[(rs * 64 + lane) * 8 + e] = g1[16 rs + 8 (lane >> 5) + e][lane & 31] (f32), and each
+// block's per-column max |g1| (f32 bits) into gmax[block][32] (the split scale of column n).
 // ---------------------------------------------------------------------------
 struct RowArgs {
     const float* dS;
@@ -483,7 +566,8 @@ struct RowArgs {
     long long M;
     const float* pre1;
     const float* seg;
-    u32x4* gq;
+    float4* gq;
+    uint32_t* gmax;
     float* slab;
     int stride;
 };
@@ -518,14 +602,14 @@ __global__ void __launch_bounds__(256) icm_row_bwd_kernel(RowArgs a) {
     if (tid < 64 * (RB / 16)) {
         const int rsl = tid >> 6, lane = tid & 63, n = lane & 31, h = lane >> 5;
         const int r0 = rsl * 16 + 8 * h;
-        const float4 v0 = make_float4(G[r0][n], G[r0 + 1][n], G[r0 + 2][n], G[r0 + 3][n]);
-        const float4 v1 = make_float4(G[r0 + 4][n], G[r0 + 5][n], G[r0 + 6][n], G[r0 + 7][n]);
-        u32x4 p0, p1, p2;
-        split8(v0, v1, p0, p1, p2);
         const long long rs = blockIdx.x * (long long)(RB / 16) + rsl;
-        a.gq[(rs * 3 + 0) * 64 + lane] = p0;
-        a.gq[(rs * 3 + 1) * 64 + lane] = p1;
-        a.gq[(rs * 3 + 2) * 64 + lane] = p2;
+        a.gq[(rs * 64 + lane) * 2] = make_float4(G[r0][n], G[r0 + 1][n], G[r0 + 2][n], G[r0 + 3][n]);
+        a.gq[(rs * 64 + lane) * 2 + 1] = make_float4(G[r0 + 4][n], G[r0 + 5][n], G[r0 + 6][n], G[r0 + 7][n]);
+    } else if (tid < 64 * (RB / 16) + 32) {
+        const int n = tid - 64 * (RB / 16);
+        uint32_t m = 0u;
+        for (int rr = 0; rr < RB; ++rr) m = max(m, __float_as_uint(fabsf(G[rr][n])));
+        a.gmax[blockIdx.x * 32LL + n] = m;
     }
     float* out = a.slab + (long long)blockIdx.x * a.stride;
     for (int col = tid; col < ROW_COLS; col += 256) {
@@ -572,32 +656,69 @@ __global__ void __launch_bounds__(256) icm_grad_reduce_kernel(const float* __res
 
 // ---------------------------------------------------------------------------
 // Encoder weight gradient dW1 = g1^T x: workgroup = 128 columns of W1 (4 MFMA tiles of
-// 32 columns, column 4 j + t of the block in tile t), all rows, 8 waves.  Wave w takes the
-// 16-row steps rs = w, w + 8, ...: per step a lane loads one dword (4 columns) from each of
-// 8 rows (row 16 rs + 8 (lane >> 5) + e) — 128 contiguous bytes per row per half-wave —
-// and byte t of the 8 dwords is tile t's B fragment; the A fragments are g1's planes.
-// WG_STAGES steps are in flight per wave (the kernel is bound by HBM latency x bytes in
-// flight: 8 waves x 3 steps x 2 KB per CU).  The waves' sums are added in LDS in wave
-// order and stored as float4 rows.
+// 32 columns, column 4 j + t of the block in tile t), all rows, 8 waves.  Column n of g1 is
+// split with its own exponent E[n] (from the row blocks' gmax: every lane splits the column
+// n = lane & 31 of its A fragment, the output row n is unscaled by 2^-E[n]).  Wave w takes
+// the 16-row steps rs = w, w + 8, ...: per step a lane loads one dword (4 columns) from
+// each of 8 rows (row 16 rs + 8 (lane >> 5) + e) — 128 contiguous bytes per row per
+// half-wave — and byte t of the 8 dwords is tile t's B fragment (exact f16: 0x64bb is
+// 1024 + b); the A fragment is the lane's 8 g1 values split into two f16 planes.
+// WG_STAGES steps are in flight per wave.  The waves' sums are added in LDS in wave order
+// and stored as float4 rows.
 // ---------------------------------------------------------------------------
 constexpr int WG_CHUNK = 2048;  // rows whose frame-row numbers are staged in LDS at a time
 constexpr int WG_WAVES = 8;
-constexpr int WG_STAGES = 3;
+#ifndef ICM_WG_STAGES
+#define ICM_WG_STAGES 3
+#endif
+constexpr int WG_STAGES = ICM_WG_STAGES;
 
 struct WgArgs {
     const uint8_t* x;
     const unsigned* rowno;
     long long M;
     int K;
-    const u32x4* gq;
+    const float4* gq;
+    const uint32_t* gmax;
+    int nblk;
     float* dw;
 };
+
+// byte t of rows (w0, w1) as an exact f16 pair
+__device__ inline uint32_t u8pair_to_f16(uint32_t w0, uint32_t w1, int t) {
+    // v_perm (selector t: byte t of w0, 4 + t: of w1, 12: 0x00) -> [b0, 0, b1, 0], | the 0x64
+    // exponent bytes, minus 1024
+    const uint32_t sel = (uint32_t)t | (12u << 8) | ((uint32_t)(4 + t) << 16) | (12u << 24);
+    const uint32_t v = __builtin_amdgcn_perm(w1, w0, sel) | 0x64006400u;
+    const f16x2 k1024 = {(_Float16)1024.f, (_Float16)1024.f};
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, v) - k1024);
+}
 
 __global__ void __launch_bounds__(64 * WG_WAVES) icm_enc_wgrad_kernel(WgArgs a) {
     __shared__ unsigned rows_l[WG_CHUNK];
     __shared__ float4 red[WG_WAVES][32][32];  // [wave][n][column quad]
+    __shared__ uint32_t em[WG_WAVES * 64];
+    __shared__ int ex[32];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 31, hb = lane >> 5;
-    const long long k0 = blockIdx.x * 128LL;
+    // column n's exponent: max over the row blocks' gmax (thread tid: column tid & 31, blocks
+    // tid >> 5, + 16, ...)
+    {
+        uint32_t m = 0u;
+        for (int b = tid >> 5; b < a.nblk; b += WG_WAVES * 2) m = max(m, a.gmax[b * 32LL + (tid & 31)]);
+        em[tid] = m;
+        __syncthreads();
+        if (tid < 32) {
+            uint32_t mm = em[tid];
+#pragma unroll
+            for (int i = 1; i < WG_WAVES * 2; ++i) mm = max(mm, em[i * 32 + tid]);
+            ex[tid] = split_scale_exp(mm);
+        }
+        __syncthreads();
+    }
+    const float sg = exp2i(ex[j]);  // the lane's A column n = j
+    // an XCD's workgroups take adjacent column blocks, so the 128-B pieces of one frame row that
+    // they read at about the same time are neighbours (2048 rows: 20.0 -> 18.3 us)
+    const long long k0 = xcd_remap(blockIdx.x, gridDim.x) * 128LL;
     // columns past K (last block): a valid address, results never stored
     const uint8_t* xc = a.x + std::min<long long>(k0 + 4 * j, a.K - 4);
     f32x16 hi[4], lo[4];
@@ -605,7 +726,7 @@ __global__ void __launch_bounds__(64 * WG_WAVES) icm_enc_wgrad_kernel(WgArgs a) 
     for (int t = 0; t < 4; ++t) hi[t] = lo[t] = zero16();
     const long long RS = (a.M + 15) / 16;
     using Xs = uint32_t[8];
-    using Gs = u32x4[3];
+    using Gs = float4[2];
     auto load = [&](long long rs, long long c0, Xs& xv, Gs& gv) {
         const int rl = (int)(rs * 16 - c0) + 8 * hb;
 #pragma unroll
@@ -613,19 +734,19 @@ __global__ void __launch_bounds__(64 * WG_WAVES) icm_enc_wgrad_kernel(WgArgs a) 
             const unsigned row = rows_l[rl + e];
             xv[e] = *reinterpret_cast<const uint32_t*>(xc + (long long)row * a.K);
         }
-#pragma unroll
-        for (int p = 0; p < 3; ++p) gv[p] = a.gq[(rs * 3 + p) * 64 + lane];
+        gv[0] = a.gq[(rs * 64 + lane) * 2];
+        gv[1] = a.gq[(rs * 64 + lane) * 2 + 1];
     };
     auto step = [&](const Xs& xv, const Gs& gv) {
+        u32x4 g0, g1;
+        split8h(gv[0], gv[1], sg, g0, g1);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             u32x4 b;
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                b[q] = pack_hi((float)((xv[2 * q] >> (8 * t)) & 0xFFu), (float)((xv[2 * q + 1] >> (8 * t)) & 0xFFu));
-            hi[t] = mfma_bf16(gv[0], b, hi[t]);
-            lo[t] = mfma_bf16(gv[1], b, lo[t]);
-            lo[t] = mfma_bf16(gv[2], b, lo[t]);
+            for (int q = 0; q < 4; ++q) b[q] = u8pair_to_f16(xv[2 * q], xv[2 * q + 1], t);
+            hi[t] = mfma_f16(g0, b, hi[t]);
+            lo[t] = mfma_f16(g1, b, lo[t]);
         }
     };
     constexpr int W = WG_WAVES, S = WG_STAGES;
@@ -648,8 +769,9 @@ __global__ void __launch_bounds__(64 * WG_WAVES) icm_enc_wgrad_kernel(WgArgs a) 
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
         const int n = (e & 3) + 8 * (e >> 2) + 4 * hb;
-        red[wave][n][j] = make_float4(hi[0][e] + lo[0][e], hi[1][e] + lo[1][e], hi[2][e] + lo[2][e],
-                                      hi[3][e] + lo[3][e]);
+        const float u = exp2i(-ex[n]);
+        red[wave][n][j] = make_float4((hi[0][e] + lo[0][e]) * u, (hi[1][e] + lo[1][e]) * u,
+                                      (hi[2][e] + lo[2][e]) * u, (hi[3][e] + lo[3][e]) * u);
     }
     __syncthreads();
     for (int f = tid; f < 32 * 32; f += 64 * W) {
@@ -709,23 +831,25 @@ __global__ void __launch_bounds__(256) icm_int_reward_kernel(const float* __rest
     }
 }
 
-// host: encoder-forward launch shape for `rows`
+// host: encoder-forward launch shape for `rows`: ceil(M / 256) row groups x nkc K ranges,
+// ~ICM_FWD_WGS workgroups, at least 4 chunks per K range
 struct EncShape {
-    int wr, nrg, nkc;
+    int nrg, nkc;
 };
 #ifndef ICM_FWD_WGS
 #define ICM_FWD_WGS 256
 #endif
 EncShape enc_shape(long long M, int K) {
     EncShape s;
-    s.wr = M >= 1024 ? 4 : 1;
-    s.nrg = (int)ppox::ceil_div(M, 64LL * s.wr);
-    const int nd = K / 32, kg = 8 / s.wr;
-    s.nkc = std::max(1, std::min<int>(ppox::ceil_div(ICM_FWD_WGS, s.nrg), std::max(1, nd / kg)));
+    s.nrg = (int)ppox::ceil_div(M, (long long)ENC_ROWS);
+    const int nc = K / ENC_CK;
+    s.nkc = std::max(1, std::min<int>(ppox::ceil_div(ICM_FWD_WGS, s.nrg), std::max(1, nc / 4)));
     return s;
 }
 
-bool icm_shape_ok(long long K) { return K > 0 && K % 32 == 0 && K < (1LL << 30); }
+bool icm_shape_ok(long long K) { return K > 0 && K % ENC_CK == 0 && K < (1LL << 30); }
+long long g1_blocks(long long rows) { return ppox::ceil_div(rows, (long long)RB); }
+long long g1_frag_floats(long long rows) { return g1_blocks(rows) * (RB / 16) * 64 * 8; }
 
 }  // namespace
 
@@ -734,13 +858,12 @@ extern "C" int64_t ppox_icm_param_elems(int32_t n_actions) {
     return Seg(n_actions).n();
 }
 
-extern "C" int64_t ppox_icm_w1_pack_elems(int64_t K) { return icm_shape_ok(K) ? 3LL * H * K : -1; }
+extern "C" int64_t ppox_icm_w1_pack_elems(int64_t K) { return icm_shape_ok(K) ? 2LL * H * K + 2 * H : -1; }
 
 extern "C" int ppox_icm_pack_w1(const float* w1, int64_t K, uint16_t* q, void* stream) {
-    PPOX_REQUIRE(w1 && q && icm_shape_ok(K), "ppox_icm_pack_w1: bad arguments (K must be a positive multiple of 32)");
+    PPOX_REQUIRE(w1 && q && icm_shape_ok(K), "ppox_icm_pack_w1: bad arguments (K must be a positive multiple of 64)");
     PPOX_REQUIRE(ppox::aligned16(w1) && ppox::aligned16(q), "ppox_icm_pack_w1: 16-byte alignment");
-    icm_pack_w1_kernel<<<ppox::ceil_div(K / 16 * 64, 256), 256, 0, ppox::as_stream(stream)>>>(
-        w1, (int)K, reinterpret_cast<u32x4*>(q));
+    icm_pack_w1_kernel<<<H, 1024, 0, ppox::as_stream(stream)>>>(w1, (int)K, reinterpret_cast<u32x4*>(q));
     PPOX_LAUNCHED("ppox_icm_pack_w1");
 }
 
@@ -754,7 +877,7 @@ extern "C" int ppox_icm_encode(const void* x, int64_t rows, const int64_t* idx, 
                                uint32_t* rowno, void* stream) {
     if (rows == 0) return PPOX_OK;
     PPOX_REQUIRE(x && q && seg && workspace && pre1 && phi && rows > 0 && icm_shape_ok(K),
-                 "ppox_icm_encode: bad arguments (K must be a positive multiple of 32)");
+                 "ppox_icm_encode: bad arguments (K must be a positive multiple of 64)");
     PPOX_REQUIRE(ppox::aligned16(x) && ppox::aligned16(q), "ppox_icm_encode: 16-byte alignment");
     if (idx) PPOX_REQUIRE(T > 0 && N_env > 0 && T * N_env < (1LL << 32), "ppox_icm_encode: idx needs T, N_env");
     else PPOX_REQUIRE(rows < (1LL << 32), "ppox_icm_encode: too many rows");
@@ -763,9 +886,7 @@ extern "C" int ppox_icm_encode(const void* x, int64_t rows, const int64_t* idx, 
     float* slab = reinterpret_cast<float*>(workspace);
     EncArgs a{reinterpret_cast<const uint8_t*>(x), reinterpret_cast<const long long*>(idx), T, N_env, rows, (int)K,
               reinterpret_cast<const u32x4*>(q), slab, s.nkc, s.nrg};
-    const unsigned grid = (unsigned)(s.nkc * s.nrg);
-    if (s.wr == 4) icm_enc_fwd_kernel<4, 2><<<grid, 512, 0, st>>>(a);
-    else icm_enc_fwd_kernel<1, 8><<<grid, 512, 0, st>>>(a);
+    icm_enc_fwd_kernel<<<(unsigned)(s.nkc * s.nrg), 64 * ENC_WAVES, 0, st>>>(a);
     PPOX_LAUNCHED_NORET("ppox_icm_encode");
     icm_enc_finish_kernel<<<ppox::ceil_div(rows, 8), 256, 0, st>>>(slab, s.nkc, rows, seg,
                                                                    reinterpret_cast<const long long*>(idx), T, N_env,
@@ -779,8 +900,9 @@ extern "C" int64_t ppox_icm_partials_bytes(int64_t rows, int32_t n_actions) {
     return nb * Seg(n_actions).stride() * 4;
 }
 
+// g1 in fragment order (f32) then the row blocks' per-column gmax, in uint16 units
 extern "C" int64_t ppox_icm_g1_pack_elems(int64_t rows) {
-    return rows <= 0 ? 0 : (int64_t)ppox::ceil_div(rows, RB) * (RB / 16) * 3 * 64 * 8;
+    return rows <= 0 ? 0 : 2 * (g1_frag_floats(rows) + g1_blocks(rows) * 32);
 }
 
 extern "C" int ppox_icm_pair_backward(const float* phi, int64_t B, const int32_t* actions, const uint32_t* rowno,
@@ -805,8 +927,9 @@ extern "C" int ppox_icm_row_backward(const float* dS, const float* dN, const int
     PPOX_REQUIRE(dS && pre1 && seg && g1q && partials && rows > 0 && n_actions >= 1 && n_actions <= 32,
                  "ppox_icm_row_backward: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(g1q), "ppox_icm_row_backward: 16-byte alignment");
-    RowArgs a{dS, dN, reinterpret_cast<const long long*>(pos), rows, pre1, seg, reinterpret_cast<u32x4*>(g1q),
-              partials, Seg(n_actions).stride()};
+    float* gq = reinterpret_cast<float*>(g1q);
+    RowArgs a{dS, dN, reinterpret_cast<const long long*>(pos), rows, pre1, seg, reinterpret_cast<float4*>(gq),
+              reinterpret_cast<uint32_t*>(gq + g1_frag_floats(rows)), partials, Seg(n_actions).stride()};
     icm_row_bwd_kernel<<<ppox::ceil_div(rows, RB), 256, 0, ppox::as_stream(stream)>>>(a);
     PPOX_LAUNCHED("ppox_icm_row_backward");
 }
@@ -828,8 +951,10 @@ extern "C" int ppox_icm_enc_wgrad(const void* x, const uint32_t* rowno, int64_t 
     PPOX_REQUIRE(x && rowno && g1q && dw1 && rows >= 1 && icm_shape_ok(K), "ppox_icm_enc_wgrad: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(g1q) && ppox::aligned16(dw1) && !(reinterpret_cast<uintptr_t>(x) & 3),
                  "ppox_icm_enc_wgrad: alignment");
-    // the g1 planes cover whole RB-row blocks: the last 16-row step is inside them
-    WgArgs a{reinterpret_cast<const uint8_t*>(x), rowno, rows, (int)K, reinterpret_cast<const u32x4*>(g1q), dw1};
+    // the g1 fragments cover whole RB-row blocks: the last 16-row step is inside them
+    const float* gq = reinterpret_cast<const float*>(g1q);
+    WgArgs a{reinterpret_cast<const uint8_t*>(x), rowno, rows, (int)K, reinterpret_cast<const float4*>(gq),
+             reinterpret_cast<const uint32_t*>(gq + g1_frag_floats(rows)), (int)g1_blocks(rows), dw1};
     icm_enc_wgrad_kernel<<<ppox::ceil_div(K, 128), 64 * WG_WAVES, 0, ppox::as_stream(stream)>>>(a);
     PPOX_LAUNCHED("ppox_icm_enc_wgrad");
 }

@@ -5,16 +5,16 @@ The reference's module (models.py:270-320) is a torch MLP trained by autograd
 its state encoder's first layer, Linear(4*84*84 -> 32), reads every minibatch row's
 28,224-byte frame stack twice (forward, weight gradient), and the rest of the module is
 ~30 small 32-wide ops.  NativeIcm runs the same math as six kernels per minibatch:
-  ppox_icm_pack_w1 (once per optimizer step), ppox_icm_encode (split-bf16 MFMA encoder
+  ppox_icm_pack_w1 (once per optimizer step), ppox_icm_encode (split-f16 MFMA encoder
   straight off the uint8 rollout rows + the per-row rest of the encoder),
   ppox_icm_pair_backward (inverse / forward model, both losses and their backward for the
   pairs (row j, row j + 1), ppo.py:684), ppox_icm_row_backward, ppox_icm_grad_reduce
   (every gradient but W1's, written into the ICM's flat gradient segment) and
-  ppox_icm_enc_wgrad (W1's gradient, split-bf16 MFMA) — and collect as ppox_icm_encode +
+  ppox_icm_enc_wgrad (W1's gradient, split-f16 MFMA) — and collect as ppox_icm_encode +
   ppox_icm_int_reward.  All gradients are overwritten (no zero fill), deterministic.
 
 Supported: Discrete actions (<= 32), feature size 32, uint8 observations of K bytes,
-K % 32 == 0 — the Atari configuration.  Other PPO_ICM setups (vector observations, Box
+K % 64 == 0 — the Atari configuration.  Other PPO_ICM setups (vector observations, Box
 actions) keep the torch module (ppo.icm_loss_sharded).
 """
 import numpy as np
@@ -37,7 +37,7 @@ def supported(icm, flat, obs_shape, obs_dtype):
     if not (icm.discrete and icm.feature_size == H and 1 <= icm.n_actions <= 32 and obs_dtype == torch.uint8):
         return False
     K = int(np.prod(obs_shape))
-    if K % 32 != 0 or icm.state_encoder[0].weight.shape != (H, K):
+    if K % 64 != 0 or icm.state_encoder[0].weight.shape != (H, K):
         return False
     ps = _param_order(icm)
     if [p.data_ptr() for p in flat.params] != [p.data_ptr() for p in ps]:
@@ -75,7 +75,7 @@ class NativeIcm:
         return b[:n].view(shape)
 
     def pack(self):
-        """Split W1 into its bf16 planes once per optimizer step."""
+        """Split W1 into its f16 planes once per optimizer step."""
         v = (self.flat.step_count, self.flat.data.data_ptr())
         if v != self._version:
             native.icm_pack_w1(self.w1.detach(), self.q)

@@ -71,7 +71,7 @@ SIGNATURES = {
     "ppox_skinny_dgrad": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 11,
     "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
-    "ppox_nature_pack_all": [_vp] * 17,
+    "ppox_nature_pack_all": [_vp] * 17 + [_i64, _vp],
     "ppox_nature_conv1_fwd_planes": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv2_fwd_planes": [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv2_wgrad_planes": [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
@@ -545,11 +545,13 @@ def nature_fc_pack(w, q_fwd, q_dgrad, stream=None):
 
 
 def nature_pack_all(w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh=None, qh_fwd=None,
-                    qh_dgrad=None, b1=None, stream=None):
-    """Every weight packing of a training step in one launch (None = skip); q1 needs the conv1
-    bias b1 (the H1P exponent of conv1's output is derived from W1 and b1)."""
+                    qh_dgrad=None, b1=None, zero=None, stream=None):
+    """Every weight packing of a training step in two launches (None = skip); q1 needs the conv1
+    bias b1 (the H1P exponent of conv1's output is derived from W1 and b1); `zero` (an int32
+    tensor, e.g. the next pass's amax table) is zeroed on the way."""
     call("ppox_nature_pack_all", _p(w1), _p(b1), _p(w2), _p(w3), _p(wfc), _p(wpd2), _p(q1), _p(q2), _p(q3),
-         _p(qd2), _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), _p(wh), _p(qh_fwd), _p(qh_dgrad), stream_ptr(stream))
+         _p(qd2), _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), _p(wh), _p(qh_fwd), _p(qh_dgrad), _p(zero),
+         0 if zero is None else zero.numel(), stream_ptr(stream))
 
 
 # conv1 -> conv2 on H1P (conv1's output as two f16 planes; include/ppox.h)

@@ -83,5 +83,5 @@ def test_icm_segment_layout_matches_module():
     assert not icm.supported(m, FlatParams(m, "cpu"), (K,), torch.uint8)
     m = IntrinsicCuriosityModule(2000, ActionConverter(Discrete(4)), 32)
     assert not icm.supported(m, FlatParams(m, "cpu"), (2000,), torch.uint8)
-    assert native.icm_w1_pack_elems(2000) == -1 and native.icm_w1_pack_elems(K) == 3 * 32 * K
+    assert native.icm_w1_pack_elems(2000) == -1 and native.icm_w1_pack_elems(K) == 2 * 32 * K + 64
     assert native.icm_encode_workspace_bytes(2048, 4 * 84 * 84) > 0

@@ -2,10 +2,10 @@
 the reference module (models.py:270-320) and loss (ppo.py:684-688); and PPO_ICM on the
 kernels vs PPO_ICM on the torch module (PPOX_ICM_NATIVE=0).  GPU box only.
 
-Tolerances: the encoder's Linear(K, 32) runs split-bf16 (every product exact, f32
+Tolerances: the encoder's Linear(K, 32) runs split-f16 (every product exact, f32
 accumulation), so its error vs fp64 is held to that of torch's own f32 GEMM (x2) on the same
 rows; gradients / losses are compared against fp64 with a per-tensor bound (2e-5 of the
-tensor's largest entry — fp32-class: the f32 product-sum errors, not bf16's 4e-3)."""
+tensor's largest entry — fp32-class: the f32 product-sum errors, not f16's 5e-4)."""
 import copy
 
 import numpy as np
@@ -62,6 +62,31 @@ def test_encode_vs_fp64(M):
     assert e_ours <= max(2 * e_f32, 1e-6 * pre_ref.abs().max().item()), (e_ours, e_f32)
     scale = phi_ref.abs().max().item()
     np.testing.assert_allclose(phi.cpu().double().numpy(), phi_ref.numpy(), rtol=0, atol=1e-5 * scale)
+
+
+def test_encode_per_feature_scale_vs_fp64():
+    """W1 rows spanning 1e-6 .. 1e3 (bias zero): each feature's split uses its own exponent, so
+    every output column is held to 2x torch's f32 error on that column (and 1e-6 of its own
+    scale), not to the largest column's."""
+    K, A, M = K_ATARI, 4, 300
+    icm, ref, flat = _module(K, A, 8)
+    w = icm.state_encoder[0].weight
+    with torch.no_grad():
+        w.mul_(torch.logspace(-6, 3, 32, device=w.device)[:, None])
+        icm.state_encoder[0].bias.zero_()
+        ref.state_encoder[0].weight.copy_(w.detach().cpu().double())
+        ref.state_encoder[0].bias.zero_()
+    nat = _native(icm, flat, K)
+    x = _frames(M, K, 21)
+    xd = torch.from_numpy(x).cuda()
+    pre1, _ = nat.encode(xd)
+    with torch.no_grad():
+        pre_ref = ref.state_encoder[0](torch.from_numpy(x).double()).numpy()
+        pre_f32 = F.linear(xd.float(), w).cpu().double().numpy()
+    e_ours = np.abs(pre1.cpu().double().numpy() - pre_ref).max(0)
+    e_f32 = np.abs(pre_f32 - pre_ref).max(0)
+    scale = np.abs(pre_ref).max(0)
+    assert (e_ours <= np.maximum(2 * e_f32, 1e-6 * scale)).all(), (e_ours / scale, e_f32 / scale)
 
 
 def test_encode_rollout_rows_equal_gathered():

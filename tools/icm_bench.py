@@ -1,5 +1,5 @@
 """Per-kernel timing of the K11 ICM kernels at one minibatch (dev tool).
-Usage: [PPOX_LIB=variant.so] python tools/icm_bench.py [B]"""
+Usage: [PPOX_LIB=variant.so] [ICM_BENCH_RANDOM=1] python tools/icm_bench.py [B]"""
 import json
 import os
 import sys
@@ -34,8 +34,15 @@ torch.manual_seed(0)
 m = IntrinsicCuriosityModule(K, ActionConverter(Discrete(A)), 32)
 flat = FlatParams(m, "cuda")
 nat = icm_native.NativeIcm(m, flat, K)
-x = torch.randint(0, 256, (B, K), dtype=torch.uint8, device="cuda")
-acts = torch.randint(0, A, (B,), dtype=torch.int32, device="cuda")
+if os.environ.get("ICM_BENCH_RANDOM"):  # minibatch rows gathered from a rollout twice their size (as in train)
+    import convs
+    T = 128
+    frames = torch.randint(0, 256, (T, 2 * B // T + 1, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    x = convs.RolloutRows(frames, torch.randperm(frames.shape[0] * frames.shape[1], device="cuda")[:B])
+    xw = frames  # the weight gradient reads the frame rows numbered by rowno
+else:
+    x = xw = torch.randint(0, 256, (B, K), dtype=torch.uint8, device="cuda")
+acts = torch.randint(0, A, (B if xw is x else xw.shape[0] * xw.shape[1],), dtype=torch.int32, device="cuda")
 pre1, phi, rowno = nat.encode(x, "mb", rowno=True)
 partials = nat._buf("partials", (native.icm_partials_bytes(B, A) // 4,))
 g1q = nat._buf("g1q", (native.icm_g1_pack_elems(B),), torch.int16)
@@ -48,7 +55,7 @@ res["pair"] = t_us(lambda: native.icm_pair_backward(phi, B, acts, rowno, None, B
                                                     partials))
 res["row"] = t_us(lambda: native.icm_row_backward(dS, dN, None, B, pre1, nat.seg, A, g1q, partials))
 res["reduce"] = t_us(lambda: native.icm_grad_reduce(partials, B, B - 1, A, 0.2, B - 1, nat.gseg, acc))
-res["wgrad"] = t_us(lambda: native.icm_enc_wgrad(x, rowno, B, K, g1q, nat.w1_grad))
+res["wgrad"] = t_us(lambda: native.icm_enc_wgrad(xw, rowno, B, K, g1q, nat.w1_grad))
 
 
 class One:
