@@ -980,6 +980,9 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
 // dgrad 0.255 -> 0.238), 2 for the conv forms (3 measured slower for the conv3 dgrad, 0.31 ->
 // 0.34 ms); 3 x 24 KB per workgroup keeps two workgroups per CU.  SG_SLOTS overrides all.
 constexpr int SG_ROWS = 32 * SG_WAVES;
+#ifndef SG_FWD2_PARITY
+#define SG_FWD2_PARITY 1  // conv2 forward taps in input-parity classes (SgFwd)
+#endif
 
 template <class Prob>
 int launch_sgemm(const Args& a, const uint16_t* wq, long long blocks, hipStream_t s, const char* name) {
@@ -1014,10 +1017,24 @@ struct SgFwd : FwdNHWCProblem<L, OUT_NCHW, 1> {
         const int p = (int)(m - n * L::P), oy = p / L::OW, ox = p % L::OW;
         return reinterpret_cast<const float*>(a.x) + ((n * L::IH + oy * L::S) * L::IW + ox * L::S) * L::CIN;
     }
+    // conv2 (4x4 taps, stride 2, one chunk per tap): the taps walked in input-parity classes —
+    // (ky, kx), (ky, kx + 2), (ky + 2, kx), (ky + 2, kx + 2) read the same input pixels (one output
+    // column / row apart), so a class taken consecutively keeps a quarter of the tile's input
+    // live in L2 instead of all of it for half the K walk
+    static constexpr bool PARITY = SG_FWD2_PARITY && L::S == 2 && L::KH == 4 && L::KW == 4 && CPT == 1;
+    __device__ static int tap_of(int c) {
+        if constexpr (PARITY) {
+            const int cls = c >> 2, i = c & 3;
+            return ((cls >> 1) + 2 * (i >> 1)) * 4 + (cls & 1) + 2 * (i & 1);
+        } else {
+            return c / CPT;
+        }
+    }
     __device__ static int chunk_off(const RowTile&, int c) {
-        const int tap = c / CPT;
+        const int tap = tap_of(c);
         return ((tap / L::KW) * L::IW + tap % L::KW) * L::CIN + (c % CPT) * BK;
     }
+    __device__ static int bchunk_id(const RowTile&, int c) { return PARITY ? tap_of(c) : c; }
 };
 
 // the conv2 forward on H1P input (conv1's output as f16 planes): a pixel's 128 B are its 32 hi then
