@@ -353,11 +353,15 @@ int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad
 /* fc forward (as ppox_nature_fc_fwd) split over K for small batches: 2-8 K-ranges per (128-row
  * tile, 64-column block) so the grid fills the chip, partial products into the workspace
  * (ppox_nature_fc_fwd_splitk_workspace_bytes(batch)), then one fixed-order reduce adding the
- * partials, the bias and the ReLU.  Replaces the same site (models-checkpoint.py:58-59). */
+ * partials, the bias and the ReLU.  Replaces the same site (models-checkpoint.py:58-59).  With
+ * logits != NULL the reduce also runs the actor head Linear(512, n_actions) on each finished row
+ * (n_actions 1..8, w_actor 16B-aligned; models-checkpoint.py:60-61): logits = f w_actor^T + b_actor,
+ * bitwise as ppox_skinny_linear. */
 int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch);
 int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias,
                               void* workspace, int64_t workspace_bytes, float* f, const uint32_t* amax_h3,
-                              uint32_t* amax_f, void* stream);
+                              uint32_t* amax_f, const float* w_actor, const float* b_actor, int32_t n_actions,
+                              float* logits, void* stream);
 /* fc weight gradient dW (512 x 3136, the weight's Flatten order) = df^T @ h3 over the batch,
  * split-f16 (fp32-class; amax_df, amax_h3: the operands' slots), deterministic: df (batch, 512) is dL/df already ReLU-masked, h3 the
  * NHWC (batch, 7, 7, 64) conv3 output of the split forward.  Replaces the library GEMM of
@@ -400,13 +404,15 @@ int ppox_relu_backward_amax_(float* grad, const float* act, int64_t n, uint32_t*
  * w_actor (A x h) = dout^T f, b_actor = sum dout, w_critic (h) = dv^T e, b_critic = sum dv,
  * b_extra = sum de, b_fc = sum df; with ie != NULL also the intrinsic head's
  * w_critic_int = div^T ie, b_critic_int = sum div, b_int_extra = sum die.  Outputs are
- * overwritten.  h <= 512, A <= 18.  Workspace: ppox_head_grads_workspace_bytes. */
+ * overwritten.  h <= 512, A <= 18.  Workspace: ppox_head_grads_workspace_bytes.  relu_df != 0:
+ * df is first masked by the fc layer's ReLU, df = f > 0 ? df : 0, IN PLACE (the nn.ReLU backward
+ * of models-checkpoint.py:57, fused), its max |df| recorded into amax_df (nullable). */
 int64_t ppox_head_grads_workspace_bytes(int64_t rows, int64_t h, int64_t n_actions, int32_t intrinsic);
 int ppox_head_grads(const float* f, const float* e, const float* dout, const float* dv, const float* de,
                     const float* df, const float* ie, const float* div, const float* die, int64_t rows, int64_t h,
                     int64_t n_actions, void* workspace, float* w_actor, float* b_actor, float* w_critic,
                     float* b_critic, float* b_extra, float* b_fc, float* w_critic_int, float* b_critic_int,
-                    float* b_int_extra, void* stream);
+                    float* b_int_extra, int32_t relu_df, uint32_t* amax_df, void* stream);
 /* Skinny heads (models-checkpoint.py:60-87 actor / critic Linear layers, n_out <= 8):
  * ppox_skinny_linear: y (rows x n_out) = x (rows x h) w^T + bias, one wave per row;
  * ppox_skinny_dgrad:  d (rows x h) = g (rows x n_out) w (n_out x h) — overwritten. */
@@ -416,6 +422,11 @@ int ppox_skinny_dgrad(const float* g, const float* w, int64_t rows, int64_t h, i
                       void* stream);
 int ppox_outer_relu_backward(const float* dv, const float* w, const float* act, int64_t rows, int64_t h,
                              float* out, uint32_t* amax, void* stream);
+/* ppox_skinny_dgrad (df = dout w_actor) and ppox_outer_relu_backward (de = dv w_critic (e > 0), amax_de
+ * nullable) of the first head in one launch, bitwise the same results (models-checkpoint.py:60-87). */
+int ppox_head_dgrad_outer(const float* dout, const float* w_actor, const float* dv, const float* w_critic,
+                          const float* e, int64_t rows, int64_t h, int64_t n_out, float* df, float* de,
+                          uint32_t* amax_de, void* stream);
 
 /* ---------------------------------------------------------------------------
  * K6, split-f16 forms (csrc/conv_split.hip, csrc/conv.hip): the same ops, layouts and

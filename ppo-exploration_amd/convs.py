@@ -430,14 +430,18 @@ class NatureConvs:
         return h1, h2, h3, am
 
     # ---- fc layer (split math): forward and the dgrad fused with the trunk's ReLU backward
-    def fc_forward(self, h3, am):
+    def fc_forward(self, h3, am, actor=None):
         """f = relu(h3 @ W^T + b), h3 (B, 7, 7, 64) NHWC (split math): the split-f16 GEMM when
         the batch fills the chip (ceil(B/128) row tiles x 8 column blocks >= ~512 workgroups),
-        rocBLAS on the NHWC-permuted weight below."""
+        split over K below, rocBLAS on the NHWC-permuted weight below FC_SPLIT_MIN_BATCH.
+        actor = (w, b): returns (f, logits), logits = f w^T + b computed by the split-K form's
+        reduce (<= 8 actions) or None (the caller runs the actor head)."""
         self.pack(h3.shape[0])
         B = h3.shape[0]
+        logits = None
         if B < FC_SPLIT_MIN_BATCH:
-            return torch._addmm_activation(self.fc.bias, h3.view(B, -1), self.wfc_nhwc.t())  # bias+ReLU fused
+            f = torch._addmm_activation(self.fc.bias, h3.view(B, -1), self.wfc_nhwc.t())  # bias+ReLU fused
+            return f if actor is None else (f, logits)
         f = torch.empty((B, 512), device=h3.device)
         if B < FC_SPLITK_MAX_BATCH:
             # one workspace per batch size: the collect graph captures the collect batch's buffer
@@ -447,10 +451,13 @@ class NatureConvs:
                 ws = torch.empty(max(native.nature_fc_fwd_splitk_workspace_bytes(B), 16), dtype=torch.uint8,
                                  device=h3.device)
                 self._ws[("fc_sk", B)] = ws
-            native.nature_fc_fwd_splitk(h3, B, self.qfc[0], self.fc.bias, ws, f, amax_h3=am[AM_H3], amax_f=am[AM_F])
+            if actor is not None and actor[0].shape[0] <= 8 and actor[0].is_contiguous() and actor[0].data_ptr() % 16 == 0:
+                logits = torch.empty((B, actor[0].shape[0]), device=h3.device)
+            native.nature_fc_fwd_splitk(h3, B, self.qfc[0], self.fc.bias, ws, f, amax_h3=am[AM_H3], amax_f=am[AM_F],
+                                        actor=actor if logits is not None else None, logits=logits)
         else:
             native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f, amax_h3=am[AM_H3], amax_f=am[AM_F])
-        return f
+        return f if actor is None else (f, logits)
 
     def fc_dgrad_g3(self, df, h3, am):
         """g3 (B, 7, 7, 64) NHWC = (df @ W) * (h3 > 0), df = dL/df after the fc ReLU (its amax in

@@ -1196,6 +1196,63 @@ __global__ void __launch_bounds__(256) fc_fwd_sk_reduce(const float4* __restrict
     amax_record(am, m);
 }
 
+// the same reduce with the actor head fused (ppox_skinny_linear's arithmetic on the finished row,
+// bitwise the same logits): one wave per row, lane l owns columns 4l .. 4l + 3 and 256 + 4l .. of
+// the 512 (the skinny kernel's k order), the NO dot products wave-reduced in its butterfly order
+template <int S, int NO>
+__global__ void __launch_bounds__(256) fc_fwd_sk_reduce_actor(const float4* __restrict__ slab, long long M,
+                                                               const float* __restrict__ bias, float4* __restrict__ y,
+                                                               uint32_t* __restrict__ am, const float* __restrict__ wa,
+                                                               const float* __restrict__ ba, float* __restrict__ logits) {
+    const int lane = threadIdx.x & 63;
+    const long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    float m = 0.f;
+    if (b < M) {  // wave-uniform
+        const long long n4 = M * 128;
+        float acc[NO];
+#pragma unroll
+        for (int o = 0; o < NO; ++o) acc[o] = 0.f;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int c4 = lane + 64 * half;
+            const long long i = b * 128 + c4;
+            float4 s = slab[i];
+#pragma unroll
+            for (int k = 1; k < S; ++k) {
+                const float4 v = slab[k * n4 + i];
+                s.x += v.x;
+                s.y += v.y;
+                s.z += v.z;
+                s.w += v.w;
+            }
+            const int n = 4 * c4;
+            const float4 o = make_float4(fmaxf(s.x + bias[n], 0.f), fmaxf(s.y + bias[n + 1], 0.f),
+                                         fmaxf(s.z + bias[n + 2], 0.f), fmaxf(s.w + bias[n + 3], 0.f));
+            y[i] = o;
+            m = fmaxf(m, fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w)));
+#pragma unroll
+            for (int a = 0; a < NO; ++a) {
+                const float4 wv = reinterpret_cast<const float4*>(wa)[a * 128 + c4];
+                acc[a] = fmaf(o.x, wv.x, acc[a]);
+                acc[a] = fmaf(o.y, wv.y, acc[a]);
+                acc[a] = fmaf(o.z, wv.z, acc[a]);
+                acc[a] = fmaf(o.w, wv.w, acc[a]);
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < NO; ++a)
+#pragma unroll
+            for (int k = 32; k > 0; k >>= 1) acc[a] += __shfl_xor(acc[a], k, 64);
+        if (lane < NO) {
+            float r = acc[0];
+#pragma unroll
+            for (int a = 1; a < NO; ++a) r = lane == a ? acc[a] : r;
+            logits[b * NO + lane] = r + ba[lane];
+        }
+    }
+    amax_record(am, m);
+}
+
 // K-splits for a batch: enough (row tile, column block, split) workgroups for two per CU, at most 8
 inline int fc_fwd_splits(long long batch) {
     const long long wg = ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB;
@@ -1204,16 +1261,35 @@ inline int fc_fwd_splits(long long batch) {
     return s;
 }
 
+struct ActorHead {
+    const float *w, *b;
+    int n;          // actions (1..8); 0: no actor head fused
+    float* logits;  // rows x n
+};
+
 template <int S>
-int launch_fc_fwd_sk(const Args& a, const uint16_t* q, float* slab, const float* bias, float* f, hipStream_t st) {
+int launch_fc_fwd_sk(const Args& a, const uint16_t* q, float* slab, const float* bias, float* f, const ActorHead& act,
+                     hipStream_t st) {
     Args b = a;
     b.y = slab;
     b.amax_y = nullptr;  // partial products: f's amax is recorded by the reduce
     const int rc = launch_sgemm<SgRowsSK<3136, 512, S>>(b, q, ppox::ceil_div(a.batch, SG_ROWS) * FcFwd::NCB * S, st,
                                                         "ppox_nature_fc_fwd_splitk");
     if (rc != PPOX_OK) return rc;
-    fc_fwd_sk_reduce<512, S><<<ppox::ceil_div(a.batch * 512 / 4, 256), 256, 0, st>>>(
-        reinterpret_cast<const float4*>(slab), a.batch, bias, reinterpret_cast<float4*>(f), a.amax_y);
+    const float4* sl = reinterpret_cast<const float4*>(slab);
+    float4* f4 = reinterpret_cast<float4*>(f);
+    const unsigned rows4 = (unsigned)ppox::ceil_div(a.batch, 4LL);
+    switch (act.n) {
+#define PPOX_FSA(N)                                                                                              \
+    case N:                                                                                                      \
+        fc_fwd_sk_reduce_actor<S, N><<<rows4, 256, 0, st>>>(sl, a.batch, bias, f4, a.amax_y, act.w, act.b, act.logits); \
+        break;
+        PPOX_FSA(1) PPOX_FSA(2) PPOX_FSA(3) PPOX_FSA(4) PPOX_FSA(5) PPOX_FSA(6) PPOX_FSA(7) PPOX_FSA(8)
+#undef PPOX_FSA
+        default:
+            fc_fwd_sk_reduce<512, S><<<ppox::ceil_div(a.batch * 512 / 4, 256), 256, 0, st>>>(sl, a.batch, bias, f4,
+                                                                                             a.amax_y);
+    }
     PPOX_LAUNCHED("ppox_nature_fc_fwd_splitk");
 }
 
@@ -2329,6 +2405,9 @@ int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float
 #ifndef WS_PX
 #define WS_PX 2048  // split wgrad: pixels per split-K slice
 #endif
+#ifndef WS_FILL
+#define WS_FILL 512  // split wgrad: workgroups at least (conv1 / conv2, small batches)
+#endif
 // split wgrad: its own split-K count (~WS_PX pixels per split so the grid fills the chip)
 template <class L, bool U8, int KT>
 struct WsLaunch {
@@ -2340,7 +2419,7 @@ struct WsLaunch {
         // where the k-blocks are few (conv1/conv2 at B = 2048: 0.082 -> 0.074 / 0.100 -> 0.078 ms;
         // conv3's nine k-blocks already give 441 workgroups, and more splits measured slower)
         if constexpr (C::KB <= 4) {
-            const long long fill = (512 + C::KB - 1) / C::KB;
+            const long long fill = (WS_FILL + C::KB - 1) / C::KB;
             s = s < fill ? fill : s;
         }
         const long long most = (px + MS - 1) / MS;  // at least one step per split
@@ -3053,7 +3132,8 @@ extern "C" int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch) {
 
 extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias,
                                          void* workspace, int64_t workspace_bytes, float* f, const uint32_t* amax_h3,
-                                         uint32_t* amax_f, void* stream) {
+                                         uint32_t* amax_f, const float* w_actor, const float* b_actor,
+                                         int32_t n_actions, float* logits, void* stream) {
     if (batch == 0) return PPOX_OK;
     PPOX_REQUIRE(h3 && q_fwd && bias && f && workspace && amax_h3 && batch > 0,
                  "ppox_nature_fc_fwd_splitk: bad arguments");
@@ -3062,14 +3142,17 @@ extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const u
                  "ppox_nature_fc_fwd_splitk: 16B alignment");
     PPOX_REQUIRE(workspace_bytes >= ppox_nature_fc_fwd_splitk_workspace_bytes(batch),
                  "ppox_nature_fc_fwd_splitk: workspace too small");
+    PPOX_REQUIRE(!logits || (w_actor && b_actor && n_actions >= 1 && n_actions <= 8 && ppox::aligned16(w_actor)),
+                 "ppox_nature_fc_fwd_splitk: the fused actor head needs 1..8 actions and a 16B-aligned weight");
     Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, amax_h3, amax_f, pack_exp(q_fwd, PL_FCF)};
     float* slab = reinterpret_cast<float*>(workspace);
     hipStream_t st = ppox::as_stream(stream);
+    const ActorHead act{w_actor, b_actor, logits ? (int)n_actions : 0, logits};
     switch (fc_fwd_splits(batch)) {
-        case 1: return launch_fc_fwd_sk<1>(a, q_fwd, slab, bias, f, st);
-        case 2: return launch_fc_fwd_sk<2>(a, q_fwd, slab, bias, f, st);
-        case 4: return launch_fc_fwd_sk<4>(a, q_fwd, slab, bias, f, st);
-        default: return launch_fc_fwd_sk<8>(a, q_fwd, slab, bias, f, st);
+        case 1: return launch_fc_fwd_sk<1>(a, q_fwd, slab, bias, f, act, st);
+        case 2: return launch_fc_fwd_sk<2>(a, q_fwd, slab, bias, f, act, st);
+        case 4: return launch_fc_fwd_sk<4>(a, q_fwd, slab, bias, f, act, st);
+        default: return launch_fc_fwd_sk<8>(a, q_fwd, slab, bias, f, act, st);
     }
 }
 

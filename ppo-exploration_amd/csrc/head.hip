@@ -32,9 +32,12 @@ __global__ void __launch_bounds__(256) relu_bwd_kernel(float* __restrict__ g, co
 // partial row of chunk c: [A*H actor W | A actor b | H critic W | 1 critic b | H extra b |
 //                         H fc b | (intrinsic) H critic_int W | 1 critic_int b | H int_extra b]
 struct HeadGrads {
-    const float *f, *e, *ie, *dout, *dv, *div, *de, *die, *df;
+    const float *f, *e, *ie, *dout, *dv, *div, *de, *die;
+    float* df;
     long long B, R;  // rows, rows per chunk
     int H, A;
+    int relu_df;        // df = f > 0 ? df : 0 first, written back (the fc layer's ReLU backward)
+    uint32_t* amax_df;  // nullable: the masked df's amax slots
 };
 constexpr int HG_MAXA = 18, HG_MAXH = 512;  // actions (Montezuma 18), hidden width
 
@@ -56,10 +59,18 @@ __global__ void __launch_bounds__(256) head_grads_partials(HeadGrads g, float* _
     }
     const int jc = col ? j : 0;
     auto ld = [&](const float* p, long long b) { return *reinterpret_cast<const float2*>(p + b * H + jc); };
+    float dm = 0.f;  // the masked df's largest |value| in this thread's columns
 #pragma unroll 4
     for (long long b = r0; b < r1; ++b) {
         const float dv = g.dv[b], div = intr ? g.div[b] : 0.f;
-        const float2 fv = ld(g.f, b), ev = ld(g.e, b), dev = ld(g.de, b), dfv = ld(g.df, b);
+        const float2 fv = ld(g.f, b), ev = ld(g.e, b), dev = ld(g.de, b);
+        float2 dfv = ld(g.df, b);
+        if (g.relu_df) {  // uniform
+            dfv.x = fv.x > 0.f ? dfv.x : 0.f;
+            dfv.y = fv.y > 0.f ? dfv.y : 0.f;
+            if (col) *reinterpret_cast<float2*>(g.df + b * H + j) = dfv;
+            dm = fmaxf(dm, fmaxf(fabsf(dfv.x), fabsf(dfv.y)));
+        }
 #pragma unroll
         for (int a = 0; a < HG_MAXA; ++a)
             if (a < A) {
@@ -107,6 +118,7 @@ __global__ void __launch_bounds__(256) head_grads_partials(HeadGrads g, float* _
         p[o + H] = bc;
         if (intr) p[o + 4 * H + 1] = bci;
     }
+    if (g.relu_df) amax_record(g.amax_df, dm);
 }
 
 struct HeadGradOut {
@@ -234,6 +246,44 @@ __global__ void __launch_bounds__(256) outer_relu_kernel(const float* __restrict
     amax_record(am, m);
 }
 
+// the actor head's input grad and the critic's ReLU-layer grad in one pass (skinny_dgrad_kernel and
+// outer_relu_kernel, same arithmetic, bitwise the same results): df = dout wa, de = dv wc (e > 0)
+template <int NO>
+__global__ void __launch_bounds__(256) head_dgrad_outer_kernel(const float* __restrict__ dout, const float* __restrict__ wa,
+                                                               const float* __restrict__ dv, const float* __restrict__ wc,
+                                                               const float* __restrict__ e, long long rows, int h4,
+                                                               float* __restrict__ df, float* __restrict__ de,
+                                                               uint32_t* __restrict__ am) {
+    const long long n4 = rows * h4;
+    float m = 0.f;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+        const long long b = i / h4;
+        const int j = (int)(i - b * h4);
+        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            const float go = dout[b * NO + o];
+            const float4 wv = reinterpret_cast<const float4*>(wa)[(long long)o * h4 + j];
+            r.x = fmaf(go, wv.x, r.x);
+            r.y = fmaf(go, wv.y, r.y);
+            r.z = fmaf(go, wv.z, r.z);
+            r.w = fmaf(go, wv.w, r.w);
+        }
+        reinterpret_cast<float4*>(df)[i] = r;
+        const float s = dv[b];
+        const float4 ww = make_float4(wc[4 * j], wc[4 * j + 1], wc[4 * j + 2], wc[4 * j + 3]);  // wc may be unaligned
+        const float4 a = reinterpret_cast<const float4*>(e)[i];
+        float4 o;
+        o.x = a.x > 0.f ? s * ww.x : 0.f;
+        o.y = a.y > 0.f ? s * ww.y : 0.f;
+        o.z = a.z > 0.f ? s * ww.z : 0.f;
+        o.w = a.w > 0.f ? s * ww.w : 0.f;
+        reinterpret_cast<float4*>(de)[i] = o;
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+    }
+    amax_record(am, m);
+}
+
 unsigned grid_for(long long n4) {
     const long long g = (n4 + 255) / 256;
     return (unsigned)(g < 4096 ? (g > 0 ? g : 1) : 4096);
@@ -268,8 +318,10 @@ extern "C" int ppox_head_grads(const float* f, const float* e, const float* dout
                                const float* df, const float* ie, const float* div, const float* die, int64_t rows,
                                int64_t h, int64_t n_actions, void* workspace, float* w_actor, float* b_actor,
                                float* w_critic, float* b_critic, float* b_extra, float* b_fc, float* w_critic_int,
-                               float* b_critic_int, float* b_int_extra, void* stream) {
+                               float* b_critic_int, float* b_int_extra, int32_t relu_df, uint32_t* amax_df,
+                               void* stream) {
     PPOX_REQUIRE(f && e && dout && dv && de && df && workspace && rows >= 0, "ppox_head_grads: null input");
+    PPOX_REQUIRE(!amax_df || (relu_df && ppox::aligned16(amax_df)), "ppox_head_grads: amax_df needs relu_df (16B)");
     PPOX_REQUIRE(h > 0 && h <= HG_MAXH && h % 2 == 0 && n_actions > 0 && n_actions <= HG_MAXA,
                  "ppox_head_grads: h must be even and <= 512, n_actions <= 18");
     PPOX_REQUIRE(ppox::aligned16(f) && ppox::aligned16(e) && ppox::aligned16(de) && ppox::aligned16(df),
@@ -282,7 +334,8 @@ extern "C" int ppox_head_grads(const float* f, const float* e, const float* dout
     const long long len = head_grads_len((int)h, (int)n_actions, intr);
     hipStream_t s = ppox::as_stream(stream);
     float* part = reinterpret_cast<float*>(workspace);
-    HeadGrads g{f, e, ie, dout, dv, div, de, die, df, rows, R, (int)h, (int)n_actions};
+    HeadGrads g{f, e, ie, dout, dv, div, de, die, const_cast<float*>(df), rows, R, (int)h, (int)n_actions,
+                relu_df != 0, amax_df};
     head_grads_partials<<<(unsigned)nchunk, 256, 0, s>>>(g, part);
     PPOX_LAUNCHED_NORET("ppox_head_grads");
     HeadGradOut o{w_actor, b_actor, w_critic, b_critic, b_extra, b_fc, w_critic_int, b_critic_int, b_int_extra};
@@ -334,4 +387,25 @@ extern "C" int ppox_outer_relu_backward(const float* dv, const float* w, const f
     outer_relu_kernel<<<grid_for(rows * h / 4), 256, 0, ppox::as_stream(stream)>>>(dv, w, act, rows, (int)(h / 4), out,
                                                                                  amax);
     PPOX_LAUNCHED("ppox_outer_relu_backward");
+}
+
+extern "C" int ppox_head_dgrad_outer(const float* dout, const float* w_actor, const float* dv, const float* w_critic,
+                                     const float* e, int64_t rows, int64_t h, int64_t n_out, float* df, float* de,
+                                     uint32_t* amax_de, void* stream) {
+    if (rows == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
+    PPOX_REQUIRE(dout && w_actor && dv && w_critic && e && df && de && rows >= 0 && h > 0 && h % 4 == 0 && n_out >= 1 &&
+                     n_out <= 8,
+                 "ppox_head_dgrad_outer: n_out must be 1..8, h a multiple of 4");
+    PPOX_REQUIRE(ppox::aligned16(w_actor) && ppox::aligned16(e) && ppox::aligned16(df) && ppox::aligned16(de) &&
+                     (!amax_de || ppox::aligned16(amax_de)),
+                 "ppox_head_dgrad_outer: 16B alignment");
+    hipStream_t s = ppox::as_stream(stream);
+    const unsigned g = grid_for(rows * h / 4);
+    switch (n_out) {
+#define PPOX_HDO(N) \
+    case N: head_dgrad_outer_kernel<N><<<g, 256, 0, s>>>(dout, w_actor, dv, w_critic, e, rows, (int)(h / 4), df, de, amax_de); break;
+        PPOX_SKINNY_CASES(PPOX_HDO)
+#undef PPOX_HDO
+    }
+    PPOX_LAUNCHED("ppox_head_dgrad_outer");
 }

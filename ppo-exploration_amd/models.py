@@ -143,19 +143,21 @@ class CnnActorCritic(nn.Module):
             h1, h2, h3, am = self.conv_impl.forward_acts(x, train=True)
             hf = h3.view(h3.shape[0], -1)
             fc = self.feature_extractor[7]
-            if self.conv_impl.math != "f32":
-                f = self.conv_impl.fc_forward(h3, am)
+            logits = None
+            if self.conv_impl.math != "f32":  # (the small-batch fc form also runs the actor head)
+                f, logits = self.conv_impl.fc_forward(h3, am, actor=(self.actor[0].weight, self.actor[0].bias))
             else:
                 f = linear_relu(hf, fc.weight, fc.bias)
-            out, v, iv, e, ie = self._heads(f, am)
+            out, v, iv, e, ie = self._heads(f, am, out=logits)
         return out, v, iv, (x, h1, h2, h3, f, e, ie, am)
 
-    def _heads(self, f, am=None):
-        """actor logits, value, int value, and the hidden activations (no autograd): fused
-        bias+ReLU GEMMs for the 512-wide layers (the extra layer on the split-f16 kernel for large
-        batches: f's amax in am), skinny-row kernels for the narrow heads."""
+    def _heads(self, f, am=None, out=None):
+        """actor logits (unless `out` already holds them), value, int value, and the hidden
+        activations (no autograd): fused bias+ReLU GEMMs for the 512-wide layers (the extra layer on
+        the split-f16 kernel for large batches: f's amax in am), skinny-row kernels for the narrow heads."""
         a, el, ce = self.actor[0], self.extra_layer[0], self.critic_ext
-        out = native.head_linear(f, a.weight, a.bias)
+        if out is None:
+            out = native.head_linear(f, a.weight, a.bias)
         cv = self.conv_impl
         if am is not None and cv is not None and cv.split_head(f.shape[0]):
             import convs as _convs
@@ -220,21 +222,26 @@ class CnnActorCritic(nn.Module):
             hf = h3.view(B, -1)
             a, fc = self.actor[0], self.feature_extractor[7]
             dout = dout.contiguous()
-            df = native.head_dgrad(dout, a.weight)
             heads = [(self.extra_layer[0], self.critic_ext, e, dv)]
             if self.intrinsic:
                 heads.append((self.int_extra_layer[0], self.critic_int, ie, div))
             import convs as _convs
-            side = _convs.side_stream(df.device) if _convs.BWD_STREAMS and df.is_cuda else None
-            cur = _convs.current_stream(df.device) if side is not None else None
+            side = _convs.side_stream(dout.device) if _convs.BWD_STREAMS and dout.is_cuda else None
+            cur = _convs.current_stream(dout.device) if side is not None else None
             cv = self.conv_impl
             split = cv.split_head(B)  # the extra layer's dgrad / weight gradient on the split-f16 kernels
             des = []
+            # the actor head's input grad and the extra layer's dv * w_critic * ReLU' in one launch
+            df, de0 = native.head_dgrad_outer(dout, a.weight, dv.contiguous().view(B), self.critic_ext.weight, e,
+                                              amax_de=am[_convs.AM_DE] if split else None)
             for hid, crit, act, d in heads:
                 d = d.contiguous().view(B, 1)
-                de = torch.empty_like(act)
                 sp = split and hid is self.extra_layer[0]
-                native.outer_relu_backward(d, crit.weight, act, de, amax=am[_convs.AM_DE] if sp else None)  # dv * w, ReLU'
+                if hid is self.extra_layer[0]:
+                    de = de0
+                else:
+                    de = torch.empty_like(act)
+                    native.outer_relu_backward(d, crit.weight, act, de)  # dv * w, ReLU'
                 if side is not None:  # the hidden layer's weight gradient beside the dgrad chain
                     _convs.fork(side, cur)
                 with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
@@ -248,9 +255,8 @@ class CnnActorCritic(nn.Module):
                 des.append((de, d))
             if split:  # df = (f > 0) ? df + de W : 0, recording df's amax (the fc layer's operand)
                 native.head_hidden_dgrad(des[0][0], cv.qh[1], f, df, amax_de=am[_convs.AM_DE], amax_df=am[_convs.AM_DF])
-            else:
-                native.relu_backward_(df, f, amax=am[_convs.AM_DF] if cv.nhwc3 else None)
-            # every column-reduction gradient (actor W/b, critic W/b, extra-layer b, fc b) in one pass
+            # every column-reduction gradient (actor W/b, critic W/b, extra-layer b, fc b) in one pass; without
+            # the split hidden layer it first applies the fc ReLU's backward to df (in place, df's amax recorded)
             ws = self._head_ws(B, f.shape[1], dout.shape[1])
             (de, d), intr = des[0], des[1] if self.intrinsic else (None, None)
             native.head_grads(f, e, dout, d, de, df, ws, a.weight.grad, a.bias.grad, self.critic_ext.weight.grad,
@@ -258,7 +264,8 @@ class CnnActorCritic(nn.Module):
                               ie=ie, div=intr[1], die=intr[0],
                               w_critic_int=self.critic_int.weight.grad if self.intrinsic else None,
                               b_critic_int=self.critic_int.bias.grad if self.intrinsic else None,
-                              b_int_extra=self.int_extra_layer[0].bias.grad if self.intrinsic else None)
+                              b_int_extra=self.int_extra_layer[0].bias.grad if self.intrinsic else None,
+                              relu_df=not split, amax_df=am[_convs.AM_DF] if (cv.nhwc3 and not split) else None)
             if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-f16 kernel, Flatten-order dW
                 if side is None:
                     native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, amax_df=am[_convs.AM_DF],

@@ -69,7 +69,8 @@ SIGNATURES = {
     "ppox_u8_to_f32": [_vp, _i64, _vp, _vp],
     "ppox_skinny_linear": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "ppox_skinny_dgrad": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
-    "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 11,
+    "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 10 + [_i32, _vp, _vp],
+    "ppox_head_dgrad_outer": [_vp] * 5 + [_i64, _i64, _i64] + [_vp] * 4,
     "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
     "ppox_nature_pack_all": [_vp] * 17 + [_i64, _vp],
     "ppox_nature_conv1_fwd_planes": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp],
@@ -93,7 +94,7 @@ SIGNATURES = {
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
-    "ppox_nature_fc_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
+    "ppox_nature_fc_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp],
     "ppox_icm_pack_w1": [_vp, _i64, _vp, _vp],
     "ppox_icm_encode": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_icm_pair_backward": [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp],
@@ -623,12 +624,16 @@ def nature_fc_fwd_splitk_workspace_bytes(batch):
     return int(load().ppox_nature_fc_fwd_splitk_workspace_bytes(int(batch)))
 
 
-def nature_fc_fwd_splitk(h3, batch, q_fwd, bias, workspace, f, amax_h3=None, amax_f=None, stream=None):
-    """fc forward split over K (small batches), bias + ReLU in the fixed-order reduce."""
+def nature_fc_fwd_splitk(h3, batch, q_fwd, bias, workspace, f, amax_h3=None, amax_f=None, actor=None, logits=None,
+                         stream=None):
+    """fc forward split over K (small batches), bias + ReLU in the fixed-order reduce; with
+    actor = (w, b) (<= 8 actions) the reduce also writes the actor head's logits = f w^T + b."""
     if batch:
         amax_h3 = _amax_of(h3, amax_h3, stream)
+    wa, ba = actor if actor is not None else (None, None)
     call("ppox_nature_fc_fwd_splitk", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(workspace),
-         workspace.numel() * workspace.element_size(), _p(f), _p(amax_h3), _p(amax_f), stream_ptr(stream))
+         workspace.numel() * workspace.element_size(), _p(f), _p(amax_h3), _p(amax_f), _p(wa), _p(ba),
+         0 if wa is None else wa.shape[0], _p(logits), stream_ptr(stream))
 
 
 def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, amax_df=None, amax_g3=None, relu_bits=None, stream=None):
@@ -726,11 +731,31 @@ def head_grads_workspace_bytes(rows, h, n_actions, intrinsic):
 
 
 def head_grads(f, e, dout, dv, de, df, ws, w_actor, b_actor, w_critic, b_critic, b_extra, b_fc,
-               ie=None, div=None, die=None, w_critic_int=None, b_critic_int=None, b_int_extra=None, stream=None):
-    """Column-reduction head gradients (see include/ppox.h ppox_head_grads); outputs overwritten."""
+               ie=None, div=None, die=None, w_critic_int=None, b_critic_int=None, b_int_extra=None, relu_df=False,
+               amax_df=None, stream=None):
+    """Column-reduction head gradients (see include/ppox.h ppox_head_grads); outputs overwritten.
+    relu_df: df is first masked by f's ReLU in place (amax_df: its slots to record)."""
     call("ppox_head_grads", _p(f), _p(e), _p(dout), _p(dv), _p(de), _p(df), _p(ie), _p(div), _p(die),
          f.shape[0], f.shape[1], dout.shape[1], _p(ws), _p(w_actor), _p(b_actor), _p(w_critic), _p(b_critic),
-         _p(b_extra), _p(b_fc), _p(w_critic_int), _p(b_critic_int), _p(b_int_extra), stream_ptr(stream))
+         _p(b_extra), _p(b_fc), _p(w_critic_int), _p(b_critic_int), _p(b_int_extra), int(bool(relu_df)),
+         _p(amax_df), stream_ptr(stream))
+
+
+def head_dgrad_outer(dout, w_actor, dv, w_critic, e, amax_de=None):
+    """(df, de): the actor head's input grad dout w_actor and the critic's ReLU-layer grad
+    dv w_critic (e > 0) in one launch (ppox_head_dgrad_outer; <= 8 actions, aligned operands),
+    else the two separate kernels."""
+    rows, n = dout.shape
+    h = w_actor.shape[1]
+    df = torch.empty(rows, h, device=dout.device)
+    de = torch.empty_like(e)
+    if n <= 8 and h % 4 == 0 and dout.is_contiguous() and _aligned(w_actor) and w_actor.is_contiguous():
+        call("ppox_head_dgrad_outer", _p(dout), _p(w_actor), _p(dv), _p(w_critic), _p(e), rows, h, n, _p(df), _p(de),
+             _p(amax_de), stream_ptr(None))
+        return df, de
+    df = torch.mm(dout, w_actor)
+    outer_relu_backward(dv, w_critic, e, de, amax=amax_de)
+    return df, de
 
 
 def outer_relu_backward(dv, w, act, out, amax=None, stream=None):

@@ -778,6 +778,47 @@ def test_normalize_obs_with_fresh_scalar_rms():
 
 
 @pytest.mark.parametrize("rows,n", [(1, 1), (2048, 4), (777, 8)])
+def test_head_dgrad_outer_equals_separate_kernels(rows, n):
+    """ppox_head_dgrad_outer (the actor dgrad and the critic's ReLU-layer grad in one launch) ==
+    ppox_skinny_dgrad + ppox_outer_relu_backward, bitwise, amax slots included."""
+    import native
+    g = torch.Generator(device="cuda").manual_seed(rows + n)
+    mk = lambda *s: torch.randn(*s, device="cuda", generator=g)
+    dout, wa, dv, e = mk(rows, n), mk(n, 512), mk(rows), mk(rows, 512).relu()
+    wc = mk(1, 512)
+    am_a, am_b = native.amax_table(2, "cuda")
+    df, de = native.head_dgrad_outer(dout, wa, dv, wc, e, amax_de=am_a)
+    de2 = torch.empty_like(e)
+    native.outer_relu_backward(dv.view(rows, 1), wc, e, de2, amax=am_b)
+    assert torch.equal(df, native.head_dgrad(dout, wa)) and torch.equal(de, de2)
+    assert torch.equal(am_a.max(), am_b.max())
+
+
+@pytest.mark.parametrize("rows", [1, 2048, 5000])
+def test_head_grads_fused_relu_df(rows):
+    """ppox_head_grads with relu_df (the fc ReLU backward applied to df in place first) ==
+    ppox_relu_backward_amax_ then ppox_head_grads: df, every output and df's amax bitwise."""
+    import native
+    H, A = 512, 4
+    g = torch.Generator(device="cuda").manual_seed(rows)
+    mk = lambda *s: torch.randn(*s, device="cuda", generator=g)
+    f, e, de, df, dout, dv = mk(rows, H).relu(), mk(rows, H).relu(), mk(rows, H), mk(rows, H), mk(rows, A), mk(rows)
+    ws = torch.empty(native.head_grads_workspace_bytes(rows, H, A, False), dtype=torch.uint8, device="cuda")
+    res = []
+    for fused in (True, False):
+        d = df.clone()
+        am = native.amax_table(1, "cuda")[0]
+        outs = [torch.full(s, float("nan"), device="cuda") for s in [(A, H), (A,), (1, H), (1,), (H,), (H,)]]
+        if not fused:
+            native.relu_backward_(d, f, amax=am)
+        native.head_grads(f, e, dout, dv, de, d, ws, *outs, relu_df=fused, amax_df=am if fused else None)
+        res.append((d, am.max(), outs))
+    (d1, m1, o1), (d2, m2, o2) = res
+    assert torch.equal(d1, d2) and torch.equal(m1, m2)
+    assert all(torch.equal(x, y) for x, y in zip(o1, o2))
+
+
+@pytest.mark.parametrize("rows,n", [(1, 1), (2048, 4), (777, 8)])
 def test_skinny_heads_match_fp64(rows, n):
     import native
     g = torch.Generator(device="cuda").manual_seed(rows)
@@ -915,6 +956,16 @@ def test_fc_fwd_splitk_vs_fp64(B):
     f2 = torch.empty_like(f)
     native.nature_fc_fwd_splitk(h3n, B, qf, b, ws, f2)
     assert torch.equal(f, f2)
+    # the fused actor head (the small-batch training forward): the same f bitwise, logits bitwise
+    # those of ppox_skinny_linear on it, and f's amax slots as the plain reduce records them
+    for A in (1, 4, 8):
+        wa, ba = torch.randn(A, 512, device="cuda") * 0.05, torch.randn(A, device="cuda")
+        f3, lg = torch.empty_like(f), torch.full((B, A), float("nan"), device="cuda")
+        am_a, am_b = native.amax_table(2, "cuda")
+        native.nature_fc_fwd_splitk(h3n, B, qf, b, ws, f3, amax_f=am_a, actor=(wa, ba), logits=lg)
+        native.nature_fc_fwd_splitk(h3n, B, qf, b, ws, f2, amax_f=am_b)
+        assert torch.equal(f3, f) and torch.equal(lg, native.head_linear(f, wa, ba))
+        assert am_a.max() == am_b.max() == f.abs().max().view(torch.int32)
 
 
 @pytest.mark.parametrize("B", [1, 33, 1000, 2048, 5000])
