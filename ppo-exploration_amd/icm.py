@@ -65,11 +65,20 @@ class NativeIcm:
         self.q = torch.empty(native.icm_w1_pack_elems(self.K), dtype=torch.int16, device=flat.device)
         self._version = None
         self._bufs = {}
+        self._captured = set()
 
     def _buf(self, name, shape, dtype=torch.float32):
+        """A named workspace, grown on demand.  A buffer first handed out while a graph is
+        being captured (the collect graph's c0 / c1 / ir tags) is pinned: the replayed graph
+        writes into it, so a later request that would replace it raises instead."""
         n = int(np.prod(shape))
         b = self._bufs.get(name)
+        if torch.cuda.is_current_stream_capturing():
+            self._captured.add(name)
         if b is None or b.numel() < n or b.dtype != dtype:
+            if b is not None and name in self._captured:
+                raise RuntimeError(f"ICM workspace '{name}' is captured by the collect graph and cannot grow "
+                                   f"({b.numel()} -> {n} elements, {b.dtype} -> {dtype})")
             b = torch.empty(max(n, 1), dtype=dtype, device=self.flat.device)
             self._bufs[name] = b
         return b[:n].view(shape)

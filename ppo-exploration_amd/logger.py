@@ -10,14 +10,14 @@ import sys
 class CSVWriter:
     """CSV rows of the dumped key/values (logger.py:13-58): a key's 'prefix/' is dropped
     (its second '/'-separated field is the column), columns are appended when new keys
-    appear — the file is then rewritten with the wider header and the earlier rows padded
-    with empty fields — and every other dump appends one row.  The reference appends new
-    columns in set order (hash order: it varies from run to run); here in first-seen order."""
+    appear — the file is re-read, rewritten with the wider header and the earlier rows padded
+    with one empty field per new column, as the reference does (no rows held in memory) — and
+    every dump appends one row.  The reference appends new columns in set order (hash order:
+    it varies from run to run); here in first-seen order."""
 
     def __init__(self, path):
         self.path = path
         self.keys = []
-        self.rows = []
         self.file = open(path, "w+t")
 
     @staticmethod
@@ -29,16 +29,16 @@ class CSVWriter:
         for k, v in kv.items():
             flat[k.split("/")[1] if k.find("/") > 0 else k] = v
         new = [k for k in flat if k not in self.keys]
-        self.rows.append(flat)
         if new:
             self.keys.extend(new)
             self.file.seek(0)
+            lines = self.file.readlines()
+            self.file.seek(0)
             self.file.truncate()
             self.file.write(",".join(self.keys) + "\n")
-            for r in self.rows:
-                self.file.write(self._line(self.keys, r))
-        else:
-            self.file.write(self._line(self.keys, flat))
+            for line in lines[1:]:
+                self.file.write(line[:-1] + "," * len(new) + "\n")
+        self.file.write(self._line(self.keys, flat))
         self.file.flush()
 
     def close(self):

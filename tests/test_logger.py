@@ -52,5 +52,7 @@ def test_csv_rewrites_header_once_per_new_key_set(tmp_path):
     w.write({"time/x": 1})
     w.write({"time/x": 2})
     w.write({"time/x": 3, "train/y": 0.5})
+    w.write({"time/x": 4, "train/y": 0.25, "train/z": 7})
+    assert not hasattr(w, "rows")  # earlier rows are re-read from the file, not held
     w.close()
-    assert (tmp_path / "a.csv").read_text() == "x,y\n1,\n2,\n3,0.5\n"
+    assert (tmp_path / "a.csv").read_text() == "x,y,z\n1,,\n2,,\n3,0.5,\n4,0.25,7\n"
