@@ -2294,6 +2294,254 @@ __global__ void __launch_bounds__(512, 1) wgrad2_planes_kernel(W2PArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// conv1 weight gradient, direct (no im2col; round 3):
+//   dW1[co][ci][ky][kx] = sum over samples n and output pixels (oy, ox) of
+//                         x[n][ci][4 oy + ky][4 ox + kx] * g1[n][oy][ox][co]   (+ db1[co] = sum g1)
+// One 512-thread workgroup per CU walks its own run of samples in units of half a sample: 10 output
+// rows, whose input rows 40 hh .. 40 hh + 43 of the 4 channels are 14.8 KB of frame bytes and whose
+// 200 g1 rows are 25.6 KB — every frame and g1 byte is read from HBM once (the im2col form,
+// wgrad_split_kernel, re-read each frame byte ~3.6x through L2: 8x8 windows at stride 4, and ran
+// latency-bound at small batches).  A unit's frame rows go global -> registers -> LDS phase-split:
+// byte x of a row is stored at phase x & 3, position x >> 2, so the 8 output pixels (4 ox + kx) of
+// one tap are 8 consecutive bytes of one phase row, from position ox + (kx >> 2) (an 8-B and a
+// 4-B read, shifted by v_alignbyte).  Its g1 rows are split into two f16 planes in LDS (split-f16,
+// the scale from g1's amax slots), 24 slots per output row (ox 20..23 hold zero rows, so the
+// k-steps of 16 pixels never straddle a row).  MFMA D[k][co] += X[k][px] G[px][co], k = 64 ci +
+// 8 ky + kx: eight tiles of 32 k; wave w owns tiles 2 (w & 3) and 2 (w & 3) + 1 (input channel
+// w & 3) on the k-steps of parity w >> 2, two exact products per tile (x * g_hi, x * g_lo: frames
+// are exact in f16) in separate accumulators.  Double-buffered: unit u + 1's loads fly under unit
+// u's MFMAs.  Each workgroup writes two partial slabs (its two k-step parities), summed with the
+// others in a fixed order by wgrad_reduce (deterministic).  LDS: 2 x (23.4 + 30 KB) = 107 KB.
+// ---------------------------------------------------------------------------
+constexpr int W1F_ROWS = 44;                   // input rows of a unit (per channel)
+constexpr int W1F_PR = 32;                     // bytes per phase row (positions 0..20 real; reads reach 27)
+constexpr int W1F_YS = 4 * W1F_PR + 8;         // bytes per (ci, y): four phase rows + 8 (spreads the banks)
+constexpr int W1F_PH = 4 * W1F_ROWS * W1F_YS;  // phase image of a unit: 23,936 B
+constexpr int W1F_GP = 240 * 64;               // one G plane: 10 rows x 24 slots x 32 co x f16
+constexpr int W1F_BUF = W1F_PH + 2 * W1F_GP;   // one buffer: 54,656 B
+constexpr int W1F_LDS = 2 * W1F_BUF;           // 109,312 B
+constexpr int W1F_XU = 4 * W1F_ROWS * 6;       // frame pieces of a unit: (ci, y, 16-B group) = 1056
+constexpr int W1F_G4 = 200 * 8;                // float4 of g1 per unit: 1600
+constexpr int W1F_SAMPLE = 4 * 84 * 84;        // frame bytes per sample
+#ifndef W1F_DEPTH
+#define W1F_DEPTH 2  // units of loads in flight (register sets)
+#endif
+static_assert(W1F_DEPTH == 2 || W1F_DEPTH == 3, "wgrad1 frames: two or three register sets");
+static_assert(W1F_LDS <= 160 * 1024 && W1F_PH % 16 == 0 && W1F_YS % 8 == 0, "wgrad1 frames: LDS layout");
+static_assert(W1F_XU <= 3 * 512 && W1F_G4 <= 4 * 512, "wgrad1 frames: loads per thread");
+
+struct W1FArgs {
+    const uint8_t* x;          // frames (u8), sample n at n * sample_stride, or rollout row idx[n]
+    long long sample_stride;
+    const long long* idx;      // optional env-major rollout rows of the step-major (T, Nenv, 4, 84, 84) frames
+    long long T, Nenv;
+    const float* g;            // g1 [batch][400][32] f32 NHWC (ReLU mask applied)
+    const uint32_t* amax_g;    // g1's amax slots
+    float* slab;               // [2 gridDim.x][256][32]
+    float* bslab;              // [2 gridDim.x][32]
+    long long batch;
+    int per;                   // samples per workgroup (every workgroup has at least one)
+};
+
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+__global__ void __launch_bounds__(512, 1) wgrad1_frames_kernel(W1FArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[W1F_LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long n0 = (long long)blockIdx.x * a.per;
+    const long long n1 = min(a.batch, n0 + (long long)a.per);
+    const int nunits = (int)(2 * (n1 - n0));
+    const int eg = split_scale_exp(amax_read(a.amax_g));
+    const float sg = exp2i(eg), uo = exp2i(-eg);
+
+    // frame base of a sample; through idx the next sample's row is fetched one sample ahead
+    auto row_base = [&](long long i) -> long long { return ((i % a.T) * a.Nenv + i / a.T) * (long long)W1F_SAMPLE; };
+    long long base = a.idx ? row_base(a.idx[n0]) : n0 * a.sample_stride;
+    long long pref = a.idx ? a.idx[n0 + 1 < n1 ? n0 + 1 : n0] : 0;
+
+    // this thread's loads of a unit: frame pieces q = tid + 512 j (ci, y, 16-B group), g1 float4s
+    // q = tid + 512 j (pixel q >> 3, channels 4 (q & 7) ..); past the ends a clamped piece is loaded
+    // and not stored.  W1F_DEPTH register sets: unit v's in set v % W1F_DEPTH, loaded that many units ahead
+    struct Raw {
+        u32x4 x[3];
+        float4 g[4];
+    };
+    Raw raw[W1F_DEPTH];
+    auto load = [&](Raw& r, long long b, long long n, int hh) {
+        u32x4 (&xr)[3] = r.x;
+        float4 (&gr)[4] = r.g;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            int q = tid + 512 * j;
+            q = q < W1F_XU ? q : W1F_XU - 1;
+            const int ci = q / (W1F_ROWS * 6), rem = q - ci * (W1F_ROWS * 6), y = rem / 6, jg = rem - y * 6;
+            const long long off = b + ci * (84 * 84) + (40 * hh + y) * 84 + (jg < 5 ? 16 * jg : 68);
+            const u32x4a4 v = *reinterpret_cast<const u32x4a4*>(a.x + off);
+            xr[j] = u32x4{v.x, v.y, v.z, v.w};
+        }
+        const float4* gs = reinterpret_cast<const float4*>(a.g + (n * 400 + hh * 200) * 32);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int q = tid + 512 * j;
+            gr[j] = gs[q < W1F_G4 ? q : W1F_G4 - 1];
+        }
+    };
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    auto store = [&](const Raw& r, int buf, bool add_bias) {
+        const u32x4 (&xr)[3] = r.x;
+        const float4 (&gr)[4] = r.g;
+        uint8_t* B = lds + buf * W1F_BUF;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int q = tid + 512 * j;
+            if (q < W1F_XU) {
+                const int ci = q / (W1F_ROWS * 6), rem = q - ci * (W1F_ROWS * 6), y = rem / 6, jg = rem - y * 6;
+                // dwords d0..d3 = positions 4 jg .. 4 jg + 3 (jg = 5: only position 20, the load's last dword)
+                const bool last = jg == 5;
+                const uint32_t d0 = last ? xr[j][3] : xr[j][0], d1 = last ? 0u : xr[j][1];
+                const uint32_t d2 = last ? 0u : xr[j][2], d3 = last ? 0u : xr[j][3];
+                // 4 x 4 byte transpose: phase r's dword = byte r of d0..d3
+                const uint32_t e01 = __builtin_amdgcn_perm(d1, d0, 0x06020400u), o01 = __builtin_amdgcn_perm(d1, d0, 0x07030501u);
+                const uint32_t e23 = __builtin_amdgcn_perm(d3, d2, 0x06020400u), o23 = __builtin_amdgcn_perm(d3, d2, 0x07030501u);
+                uint8_t* dst = B + (ci * W1F_ROWS + y) * W1F_YS + 4 * jg;
+                *reinterpret_cast<uint32_t*>(dst + 0 * W1F_PR) = __builtin_amdgcn_perm(e23, e01, 0x05040100u);
+                *reinterpret_cast<uint32_t*>(dst + 1 * W1F_PR) = __builtin_amdgcn_perm(o23, o01, 0x05040100u);
+                *reinterpret_cast<uint32_t*>(dst + 2 * W1F_PR) = __builtin_amdgcn_perm(e23, e01, 0x07060302u);
+                *reinterpret_cast<uint32_t*>(dst + 3 * W1F_PR) = __builtin_amdgcn_perm(o23, o01, 0x07060302u);
+            }
+        }
+        uint8_t* G = B + W1F_PH;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int q = tid + 512 * j;
+            if (q < W1F_G4) {
+                const int px = q >> 3, slot = (px / 20) * 24 + px % 20;
+                uint2 hv, lv;
+                split4h(gr[j], sg, hv, lv);
+                *reinterpret_cast<uint2*>(G + slot * 64 + (q & 7) * 8) = hv;
+                *reinterpret_cast<uint2*>(G + W1F_GP + slot * 64 + (q & 7) * 8) = lv;
+                if (add_bias) {
+                    bsum[0] += gr[j].x;
+                    bsum[1] += gr[j].y;
+                    bsum[2] += gr[j].z;
+                    bsum[3] += gr[j].w;
+                }
+            }
+        }
+    };
+    // zero G rows of the pad slots (ox 20..23) of both buffers and planes once: 640 x 16 B
+    for (int i = tid; i < 640; i += 512) {
+        const int bp = i / 160, w = i % 160, row = w / 16, c = w % 16;  // (buffer, plane), output row, 16 B
+        *reinterpret_cast<u32x4*>(lds + (bp >> 1) * W1F_BUF + W1F_PH + (bp & 1) * W1F_GP + (row * 24 + 20) * 64 + c * 16) =
+            u32x4{0u, 0u, 0u, 0u};
+    }
+
+    // A: lane (m, h) of tile 2 tp + tt holds k = 64 tp + 32 tt + m: ky = 4 tt + (m >> 3), kx = m & 7
+    const int tp = wave & 3, par = wave >> 2, m = lane & 31, h = lane >> 5;
+    const int kx = m & 7, sh = kx >> 2;
+    int abase[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) abase[tt] = (tp * W1F_ROWS + 4 * tt + (m >> 3)) * W1F_YS + (kx & 3) * W1F_PR;
+    // B: the transposed-read lane offsets of wgrad_split_kernel (64-B rows, no swizzle)
+    const int g16 = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+    const int rowg = (8 * h + qq) * 64 + pp * 8 + (g16 << 5);
+
+    f32x16 hi[2], lo[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) hi[tt] = lo[tt] = zero16();
+
+    auto compute = [&](int buf) {
+        const uint8_t* B = lds + buf * W1F_BUF;
+        const uint8_t* G = B + W1F_PH;
+#pragma unroll
+        for (int ks2 = 0; ks2 < 8; ++ks2) {
+            const int ks = 2 * ks2 + par;  // this wave's k-steps (15 per unit: parity 1 has seven)
+            if (ks < 15) {
+                const int gi = 2 * ks + h, goff = (gi / 3) * 4 * W1F_YS + 8 * (gi % 3);
+                u32x4 af[2];
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt) {
+                    const uint8_t* p = B + abase[tt] + goff;
+                    const uint2 v = *reinterpret_cast<const uint2*>(p);
+                    const uint32_t w2 = *reinterpret_cast<const uint32_t*>(p + 8);
+                    af[tt] = u8x8_to_f16(__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(w2, v.y, sh));
+                }
+                u32x4 bq[2];
+#pragma unroll
+                for (int P = 0; P < 2; ++P) {
+                    const uint8_t* p = G + P * W1F_GP + rowg + 16 * ks * 64;
+                    const uint2 r0 = lds_tr16(p), r1 = lds_tr16(p + 4 * 64);
+                    bq[P] = u32x4{r0.x, r0.y, r1.x, r1.y};
+                }
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt) {
+                    hi[tt] = mfma_f16(af[tt], bq[0], hi[tt]);
+                    lo[tt] = mfma_f16(af[tt], bq[1], lo[tt]);
+                }
+            }
+        }
+    };
+
+    // unit v's loads into set v & 1 (past the last unit: the last again, stored to the idle buffer
+    // without its bias); a new sample's frame base from the idx value prefetched a sample ahead
+    auto issue = [&](int v, auto SET) {
+        const int vc = v < nunits ? v : nunits - 1;
+        const long long nv = n0 + (vc >> 1);
+        if ((v & 1) == 0 && v < nunits && v > 0) {
+            base = a.idx ? row_base(pref) : nv * a.sample_stride;
+            if (a.idx) pref = a.idx[nv + 1 < n1 ? nv + 1 : nv];
+        }
+        load(raw[decltype(SET)::value], base, nv, vc & 1);
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    using S2 = std::integral_constant<int, 2>;
+    issue(0, S0{});
+    issue(1, S1{});
+    if constexpr (W1F_DEPTH == 3) issue(2, S2{});
+    store(raw[0], 0, true);
+    __syncthreads();
+    // step u (set SET = u % W1F_DEPTH): unit u + W1F_DEPTH's loads into the set unit u held, unit u
+    // computed (LDS buffer u & 1), unit u + 1 (loaded earlier) split into the other buffer
+    auto step = [&](int u, auto SET) {
+        constexpr int set = decltype(SET)::value, nset = (set + 1) % W1F_DEPTH;
+        issue(u + W1F_DEPTH, SET);
+        compute(u & 1);
+        store(raw[nset], (u + 1) & 1, u + 1 < nunits);
+        __syncthreads();
+    };
+#pragma unroll 1
+    for (int u = 0; u < nunits; u += W1F_DEPTH) {
+        step(u, S0{});
+        if (u + 1 < nunits) step(u + 1, S1{});
+        if constexpr (W1F_DEPTH == 3)
+            if (u + 2 < nunits) step(u + 2, S2{});
+    }
+
+    const int split = 2 * blockIdx.x + par;
+    float* slab = a.slab + (long long)split * (G1::K * G1::COUT);
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int k = 64 * tp + 32 * tt + (r & 3) + 8 * (r >> 2) + 4 * h;
+            slab[k * G1::COUT + m] = (hi[tt][r] + lo[tt][r]) * uo;
+        }
+    // bias partial: threads with the same tid & 7 hold the same four channels; summed in thread order
+    float* red = reinterpret_cast<float*>(lds);  // the loop ended on a barrier
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[tid * 4 + e] = bsum[e];
+    __syncthreads();
+    if (tid < G1::COUT) {
+        const int c4 = tid >> 2, e = tid & 3;
+        float t = 0.f;
+        for (int k = 0; k < 64; ++k) t += red[(c4 + 8 * k) * 4 + e];
+        a.bslab[(long long)2 * blockIdx.x * G1::COUT + tid] = t;
+        a.bslab[(long long)(2 * blockIdx.x + 1) * G1::COUT + tid] = 0.f;
+    }
+}
+
 // conv3 output grad: NCHW (Flatten order) -> NHWC, times the ReLU mask of h3 (NCHW)
 __global__ void __launch_bounds__(256) nchw_to_nhwc_mask(const float* __restrict__ g, const float* __restrict__ h,
                                                          long long batch, float* __restrict__ out) {
@@ -2811,6 +3059,13 @@ extern "C" int ppox_nature_wgrad_reduce(int32_t layer, int64_t batch, const void
 }
 
 
+namespace {
+bool wgrad1_im2col();
+int launch_wgrad1_frames(const void* x, long long sample_stride, const long long* idx, long long T, long long Nenv,
+                         const float* g, long long batch, void* ws, long long ws_bytes, float* dw, float* db,
+                         const uint32_t* amax_g, hipStream_t s);
+}  // namespace
+
 extern "C" int64_t ppox_nature_wgrad_split_workspace_bytes(int32_t layer, int64_t batch) {
     if (batch <= 0) return 0;
     return layer == 1 ? Ws1::workspace_bytes(batch) : layer == 2 ? Ws2::workspace_bytes(batch)
@@ -2833,6 +3088,9 @@ extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_
     if (layer == 1) {
         PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && x_sample_stride % 4 == 0,
                      "ppox_nature_conv_wgrad_split: u8 input 4-byte aligned");
+        if (!wgrad1_im2col())
+            return launch_wgrad1_frames(x, x_sample_stride, nullptr, 0, 0, grad_out, batch, workspace, workspace_bytes,
+                                        dw, db, amax_g, s);
         return Ws1::run(x, x_sample_stride, grad_out, batch, workspace, dw, db, nullptr, amax_g, s);
     }
     PPOX_REQUIRE(ppox::aligned16(x), "ppox_nature_conv_wgrad_split: layer 2/3 input must be 16B-aligned NHWC");
@@ -2856,6 +3114,9 @@ extern "C" int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, in
     PPOX_REQUIRE(ppox::aligned16(grad_out) && !(reinterpret_cast<uintptr_t>(x) & 3),
                  "ppox_nature_conv_wgrad_split_idx: alignment");
     PPOX_REQUIRE(batch * G1::P < (1LL << 31) / 64, "ppox_nature_conv_wgrad_split_idx: batch too large");
+    if (!wgrad1_im2col())
+        return launch_wgrad1_frames(x, 0, reinterpret_cast<const long long*>(idx), T, N_env, grad_out, batch, workspace,
+                                    workspace_bytes, dw, db, amax_g, ppox::as_stream(stream));
     return Ws1::run(x, 0, grad_out, batch, workspace, dw, db, nullptr, amax_g, ppox::as_stream(stream),
                     reinterpret_cast<const long long*>(idx), T, N_env);
 }
@@ -2964,6 +3225,31 @@ void w2p_grid(long long batch, int& per, long long& grid) {
     const long long cus = std::max(1, cu_count());
     per = (int)ppox::ceil_div(batch, std::min(batch, cus));
     grid = ppox::ceil_div(batch, (long long)per);
+}
+
+// the direct conv1 weight gradient (wgrad1_frames_kernel, one workgroup per CU) + its slab reduce;
+// PPOX_WGRAD1_IM2COL=1 runs the im2col form (wgrad_split_kernel) instead
+bool wgrad1_im2col() {
+    static const int v = [] {
+        const char* e = std::getenv("PPOX_WGRAD1_IM2COL");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    return v != 0;
+}
+int launch_wgrad1_frames(const void* x, long long sample_stride, const long long* idx, long long T, long long Nenv,
+                         const float* g, long long batch, void* ws, long long ws_bytes, float* dw, float* db,
+                         const uint32_t* amax_g, hipStream_t s) {
+    int per;
+    long long grid;
+    w2p_grid(batch, per, grid);
+    PPOX_REQUIRE(2 * grid * (long long)(G1::K * G1::COUT + G1::COUT) * 4 <= ws_bytes,
+                 "ppox_nature_conv_wgrad_split: workspace too small for the direct conv1 weight gradient");
+    float* slab = reinterpret_cast<float*>(ws);
+    W1FArgs a{reinterpret_cast<const uint8_t*>(x), sample_stride, idx, T, Nenv, g, amax_g, slab,
+              slab + 2 * grid * (G1::K * G1::COUT), batch, per};
+    wgrad1_frames_kernel<<<(unsigned)grid, 512, 0, s>>>(a);
+    PPOX_LAUNCHED_NORET("ppox_nature_conv_wgrad_split");
+    return launch_wgrad_reduce<G1, false>(slab, a.bslab, (int)(2 * grid), dw, db, s);
 }
 }  // namespace
 

@@ -1390,6 +1390,50 @@ def test_conv1_split_training_size_vs_fp64(B):
         assert excess.max().item() <= 0, (wide, excess.max().item(), q_f)
 
 
+@pytest.mark.parametrize("B", [1, 2, 3, 255, 257, 2048])
+def test_conv1_wgrad_direct_ragged_vs_fp64(B):
+    """The direct conv1 weight gradient (wgrad1_frames_kernel: one workgroup per CU over runs of whole
+    samples in half-sample units, frames phase-split in LDS, two parity slabs per workgroup) at batches
+    below, at and above one sample per CU: vs float64 within 2x f32 math's error, per element within
+    the f32 dot-product bound + the split floor, the bias exact to 1e-5, bitwise run to run and
+    through the rollout index (env-major rows of step-major frames) == on gathered rows."""
+    import native
+    F = torch.nn.functional
+    torch.manual_seed(B + 7)
+    T, N = 16, (B + 15) // 16 + 1
+    frames = torch.randint(0, 256, (T, N, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    idx = torch.randperm(T * N, device="cuda")[:B].to(torch.int64)
+    rows = frames.permute(1, 0, 2, 3, 4).reshape(T * N, 4, 84, 84)[idx].contiguous()
+    w1 = torch.empty(32, 4, 8, 8, device="cuda")
+    b1 = torch.empty(32, device="cuda")
+    g1 = torch.randn(B, 20, 20, 32, device="cuda") * (torch.rand(B, 20, 20, 32, device="cuda") > 0.3)
+    g1 = g1 * torch.exp(2.0 * torch.randn(B, 20, 20, 32, device="cuda"))
+    ws = torch.empty(native.nature_wgrad_split_workspace_bytes(1, B), dtype=torch.uint8, device="cuda")
+    res = []
+    for i in range(3):
+        dw, db = torch.full_like(w1, float("nan")), torch.full_like(b1, float("nan"))
+        if i < 2:
+            native.nature_conv_wgrad_split_idx(1, frames, B, idx, T, N, g1, ws, dw, db)
+        else:
+            native.nature_conv_wgrad_split(1, rows, B, 28224, g1, ws, dw, db)
+        res.append((dw, db))
+    for d in res[1:]:
+        assert torch.equal(res[0][0], d[0]) and torch.equal(res[0][1], d[1])
+    dw, db = res[0]
+    gn = g1.permute(0, 3, 1, 2)
+    wref = lambda dt: torch.nn.grad.conv2d_weight(rows.to(dt), w1.shape, gn.to(dt), stride=4)
+    r64, r32 = wref(torch.float64), wref(torch.float32)
+    _fp64_check(dw, r64, r32, f"conv1 wgrad direct B={B}")
+    rb = g1.double().sum(dim=(0, 1, 2))
+    assert ((db.double() - rb).abs().max() / rb.abs().max()).item() < 1e-5
+    S = torch.nn.grad.conv2d_weight(rows.double(), w1.shape, gn.double().abs(), stride=4) * 2.0 ** -24
+    floor = 2.0 ** -39 * g1.double().abs().max() * torch.nn.grad.conv2d_weight(
+        rows.double(), w1.shape, torch.ones_like(gn, dtype=torch.float64), stride=4)
+    q_f = ((r32.double() - r64).abs() / S.clamp_min(1e-300)).max().item()
+    excess = (dw.double() - r64).abs() - (2 * q_f + 4) * S - 2 * floor
+    assert excess.max().item() <= 0, (excess.max().item(), q_f)
+
+
 @pytest.mark.parametrize("B", [9001, 16384])
 def test_conv2_dgrad_persistent_training_size_vs_fp64(B):
     """The persistent col2im conv2 dgrad at training-size batches (3,001 / 5,462 sample triples over
