@@ -58,7 +58,8 @@ def _kernels():
            ("fwd", 3): "sgemm_kernel<SgFwd<64, 9, 9, 3, 3, 1, 64, false>, 4, 2>",
            ("dgrad", 2): "dgrad2_colp_kernel<true, false>",
            ("dgrad", 3): "sgemm_kernel<SgDgradPM<64, 9, 9, 3, 3, 1, 64, true>, 4, 2>",
-           ("wgrad", 1): "wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>",
+           ("wgrad", 1): ("wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>"
+                          if os.environ.get("PPOX_WGRAD1_IM2COL") == "1" else "wgrad1_frames_kernel"),
            ("wgrad", 2): "wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128, false, 1>",
            ("wgrad", 3): "wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64, false, 1>"}
     for op in ("fwd", "dgrad", "wgrad"):
