@@ -2327,6 +2327,9 @@ constexpr int W1F_SAMPLE = 4 * 84 * 84;        // frame bytes per sample
 #ifndef W1F_DEPTH
 #define W1F_DEPTH 2  // units of loads in flight (register sets)
 #endif
+#ifndef W1F_FLUSH
+#define W1F_FLUSH 8  // units per partial sum (4 samples: ~960 pixels per accumulation chain and parity)
+#endif
 static_assert(W1F_DEPTH == 2 || W1F_DEPTH == 3, "wgrad1 frames: two or three register sets");
 static_assert(W1F_LDS <= 160 * 1024 && W1F_PH % 16 == 0 && W1F_YS % 8 == 0, "wgrad1 frames: LDS layout");
 static_assert(W1F_XU <= 3 * 512 && W1F_G4 <= 4 * 512, "wgrad1 frames: loads per thread");
@@ -2447,9 +2450,11 @@ __global__ void __launch_bounds__(512, 1) wgrad1_frames_kernel(W1FArgs a) {
     const int g16 = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
     const int rowg = (8 * h + qq) * 64 + pp * 8 + (g16 << 5);
 
-    f32x16 hi[2], lo[2];
+    // hi / lo: the running products of W1F_FLUSH units, then added into tot and restarted, so no
+    // f32 accumulation chain grows past ~1,000 pixels however many samples the workgroup walks
+    f32x16 hi[2], lo[2], tot[2];
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt) hi[tt] = lo[tt] = zero16();
+    for (int tt = 0; tt < 2; ++tt) hi[tt] = lo[tt] = tot[tt] = zero16();
 
     auto compute = [&](int buf) {
         const uint8_t* B = lds + buf * W1F_BUF;
@@ -2508,6 +2513,14 @@ __global__ void __launch_bounds__(512, 1) wgrad1_frames_kernel(W1FArgs a) {
         constexpr int set = decltype(SET)::value, nset = (set + 1) % W1F_DEPTH;
         issue(u + W1F_DEPTH, SET);
         compute(u & 1);
+        if ((u + 1) % W1F_FLUSH == 0 || u + 1 == nunits) {
+#pragma unroll
+            for (int tt = 0; tt < 2; ++tt) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) tot[tt][q] += hi[tt][q] + lo[tt][q];
+                hi[tt] = lo[tt] = zero16();
+            }
+        }
         store(raw[nset], (u + 1) & 1, u + 1 < nunits);
         __syncthreads();
     };
@@ -2526,7 +2539,7 @@ __global__ void __launch_bounds__(512, 1) wgrad1_frames_kernel(W1FArgs a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int k = 64 * tp + 32 * tt + (r & 3) + 8 * (r >> 2) + 4 * h;
-            slab[k * G1::COUT + m] = (hi[tt][r] + lo[tt][r]) * uo;
+            slab[k * G1::COUT + m] = tot[tt][r] * uo;
         }
     // bias partial: threads with the same tid & 7 hold the same four channels; summed in thread order
     float* red = reinterpret_cast<float*>(lds);  // the loop ended on a barrier
