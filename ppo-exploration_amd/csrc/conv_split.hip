@@ -37,7 +37,17 @@ namespace {
 // PLANES: h1 is written as its two f16 planes (H1P: per pixel 32 hi then 32 lo f16, 128 B like f32),
 // h1 * 2^E = hi + lo with E = *a.yexp (ppox_nature_pack_all: from the weight bound of conv1's
 // output), the operand format of the split conv2 forward / weight gradient — no amax is recorded
-template <int MT, bool PLANES = false>
+// IDX (rows through the rollout index, round 3): each tile's idx values are loaded one tile ahead in
+// inline asm (tile k + 1's during tile k's frame loads) and waited for by a counted vmcnt that leaves
+// the 16 frame loads issued after them in flight; a plain load there made hipcc drain every load in
+// flight (vmcnt(0)) at each tile to get the fresh idx value, then the frames' addresses.
+__device__ inline uint32_t fwd1_idx_load(const long long* p) {
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ uint32_t kFwd1Dummy[128];  // store target of the rows past the batch (never read)
+template <int MT, bool PLANES = false, bool IDX = false>
 __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a, unsigned tiles_per_wave) {
     using L = G1;
     constexpr int NCH = L::K / 32, NQ = NCH * 2 * NPL;
@@ -59,15 +69,48 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
 
     // the whole K extent of a tile: per row slot i and chunk c, two 8-byte runs
     using Raw = uint32_t[MT][NCH][4];
+    // IDX: this lane's rollout-row index of a tile's row slot i (clamped rows: the tile's first)
+    auto idx_ptr = [&](unsigned tile, int i) {
+        const unsigned m0 = tile * 32 * MT;
+        unsigned m = m0 + i * 32 + (lane & 31);
+        m = m < M ? m : m0;
+        return a.idx + m / L::P;
+    };
+    uint32_t ixv[MT];  // IDX: the idx values of the tile about to be loaded
+    if constexpr (IDX) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) ixv[i] = (uint32_t)*idx_ptr(t_begin, i);
+    }
+    const uint32_t T32 = (uint32_t)a.T, N32 = (uint32_t)a.Nenv;  // IDX: host-checked T * Nenv < 2^32
     auto load_tile = [&](unsigned tile, Raw& r) {
         const unsigned m0 = tile * 32 * MT;
+        uint32_t ix[MT];
+        if constexpr (IDX) {
+            // this tile's idx values (loaded a tile ago; the 16 * MT frame loads of the tile after them
+            // may stay in flight), then the next tile's, ahead of this tile's frame loads
+#pragma unroll
+            for (int i = 0; i < MT; ++i) ix[i] = ixv[i];
+            if constexpr (MT == 1)
+                asm volatile("s_waitcnt vmcnt(16)" : "+v"(ix[0]) :: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(32)" : "+v"(ix[0]), "+v"(ix[1]) :: "memory");
+            const unsigned nt = tile + 1 < t_end ? tile + 1 : tile;
+#pragma unroll
+            for (int i = 0; i < MT; ++i) ixv[i] = fwd1_idx_load(idx_ptr(nt, i));
+        }
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             unsigned m = m0 + i * 32 + (lane & 31);
             m = m < M ? m : m0;  // clamped rows are computed but never stored
             const unsigned n = m / L::P, p = m - n * L::P, oy = p / L::OW, ox = p % L::OW;
-            const uint8_t* b = x + u8_sample_base(a, n, (long long)L::CIN * L::IH * L::IW) +
-                               (oy * L::S + (lane >> 5) * 2) * L::IW + ox * L::S;
+            long long sb;
+            if constexpr (IDX) {
+                const uint32_t q = ix[i] / T32;
+                sb = (long long)((ix[i] - q * T32) * N32 + q) * (long long)(L::CIN * L::IH * L::IW);
+            } else {
+                sb = u8_sample_base(a, n, (long long)L::CIN * L::IH * L::IW);
+            }
+            const uint8_t* b = x + sb + (oy * L::S + (lane >> 5) * 2) * L::IW + ox * L::S;
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
                 const uint8_t* q = b + (c >> 1) * (L::IH * L::IW) + (c & 1) * 4 * L::IW;
@@ -138,9 +181,11 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
                     const uint32_t out = odd ? ((pw >> 16) | (w & 0xFFFF0000u)) : ((w & 0xFFFFu) | (pw << 16));
                     uint16_t* y16 = reinterpret_cast<uint16_t*>(a.y) + (long long)m * (2 * L::COUT) +
                                     (odd ? L::COUT + co - 1 : co);
-                    if (m < M) *reinterpret_cast<uint32_t*>(y16) = out;
+                    // unconditional (rows past the end go to a dummy word): no branch, so hipcc's
+                    // waits on the next tile's frame loads keep their counts
+                    *reinterpret_cast<uint32_t*>(m < M ? y16 : reinterpret_cast<uint16_t*>(kFwd1Dummy + lane)) = out;
                 } else {
-                    if (m < M) a.y[(long long)m * L::COUT + co] = v;
+                    *(m < M ? a.y + (long long)m * L::COUT + co : reinterpret_cast<float*>(kFwd1Dummy + lane)) = v;
                 }
                 if (a.bits_y) {  // uniform
                     const unsigned long long b = __ballot(v > 0.f);
@@ -148,17 +193,20 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
                 }
             }
             const unsigned mw = m0 + i * 32 + lane;
-            if (a.bits_y && lane < 32 && mw < M) a.bits_y[mw] = word;
+            if (a.bits_y)  // uniform
+                *(lane < 32 && mw < M ? a.bits_y + mw : kFwd1Dummy + 64 + lane) = word;
         }
     };
+    // the next tile's loads unconditional (past the last tile: the last again, never run), so every
+    // run_tile waits for its own loads only, with the next tile's in flight
     Raw r0, r1;
     load_tile(t_begin, r0);
 #pragma unroll 1
     for (unsigned tile = t_begin; tile < t_end; tile += 2) {
-        if (tile + 1 < t_end) load_tile(tile + 1, r1);
+        load_tile(tile + 1 < t_end ? tile + 1 : t_end - 1, r1);
         run_tile(tile, r0);
         if (tile + 1 >= t_end) break;
-        if (tile + 2 < t_end) load_tile(tile + 2, r0);
+        load_tile(tile + 2 < t_end ? tile + 2 : t_end - 1, r0);
         run_tile(tile + 1, r1);
     }
     if constexpr (!PLANES) amax_record(a.amax_y, om);
@@ -186,7 +234,7 @@ extern "C" int ppox_nature_conv1_fwd_planes(const void* x, int64_t batch, const 
     PPOX_REQUIRE(batch * G1::P < (1LL << 31), "ppox_nature_conv1_fwd_planes: batch too large for 32-bit rows");
     PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && (idx || x_sample_stride % 4 == 0),
                  "ppox_nature_conv1_fwd_planes: u8 input must be 4-byte aligned");
-    if (idx) PPOX_REQUIRE(T > 0 && N_env > 0, "ppox_nature_conv1_fwd_planes: idx needs T and N_env");
+    if (idx) PPOX_REQUIRE(T > 0 && N_env > 0 && T * N_env < (1LL << 31), "ppox_nature_conv1_fwd_planes: idx needs T and N_env (T * N_env < 2^31)");
     const long long pl = ppox_conv::planes(1);
     Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, nullptr, bias, nullptr,
            reinterpret_cast<float*>(h1p), batch, nullptr, nullptr, pack_exp(wq1, pl)};
@@ -197,8 +245,12 @@ extern "C" int ppox_nature_conv1_fwd_planes(const void* x, int64_t batch, const 
     const long long ntile = ppox::ceil_div(batch * G1::P, 32 * MT);
     const long long waves = std::min<long long>(ntile, SPLIT_RESIDENT_WAVES);
     const unsigned per = ppox::ceil_div(ntile, waves);
-    fwd1_split_kernel<MT, true><<<ppox::ceil_div(ppox::ceil_div(ntile, per), 4), 256, 0, ppox::as_stream(stream)>>>(
-        a, per);
+    if (idx)
+        fwd1_split_kernel<MT, true, true><<<ppox::ceil_div(ppox::ceil_div(ntile, per), 4), 256, 0,
+                                            ppox::as_stream(stream)>>>(a, per);
+    else
+        fwd1_split_kernel<MT, true><<<ppox::ceil_div(ppox::ceil_div(ntile, per), 4), 256, 0, ppox::as_stream(stream)>>>(
+            a, per);
     PPOX_LAUNCHED("ppox_nature_conv1_fwd_planes");
 }
 
@@ -236,11 +288,14 @@ extern "C" int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t 
     hipStream_t s = ppox::as_stream(stream);
     PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(x) & 3) && (idx || x_sample_stride % 4 == 0),
                  "ppox_nature_conv_fwd_split: u8 input must be 4-byte aligned");
-    if (idx) PPOX_REQUIRE(T > 0 && N_env > 0, "ppox_nature_conv_fwd_split: idx needs T and N_env");
+    if (idx) PPOX_REQUIRE(T > 0 && N_env > 0 && T * N_env < (1LL << 31), "ppox_nature_conv_fwd_split: idx needs T and N_env (T * N_env < 2^31)");
     constexpr int MT = SPLIT_FWD1_MT;
     const long long ntile = ppox::ceil_div(batch * G1::P, 32 * MT);
     const long long waves = std::min<long long>(ntile, SPLIT_RESIDENT_WAVES);
     const unsigned per = ppox::ceil_div(ntile, waves);
-    fwd1_split_kernel<MT><<<ppox::ceil_div(ppox::ceil_div(ntile, per), 4), 256, 0, s>>>(a, per);
+    if (idx)
+        fwd1_split_kernel<MT, false, true><<<ppox::ceil_div(ppox::ceil_div(ntile, per), 4), 256, 0, s>>>(a, per);
+    else
+        fwd1_split_kernel<MT><<<ppox::ceil_div(ppox::ceil_div(ntile, per), 4), 256, 0, s>>>(a, per);
     PPOX_LAUNCHED("ppox_nature_conv_fwd_split");
 }
