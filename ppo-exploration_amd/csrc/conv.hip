@@ -2349,6 +2349,7 @@ struct W1FArgs {
 
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
+template <bool IDX>
 __global__ void __launch_bounds__(512, 1) wgrad1_frames_kernel(W1FArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[W1F_LDS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2359,9 +2360,14 @@ __global__ void __launch_bounds__(512, 1) wgrad1_frames_kernel(W1FArgs a) {
     const float sg = exp2i(eg), uo = exp2i(-eg);
 
     // frame base of a sample; through idx the next sample's row is fetched one sample ahead
-    auto row_base = [&](long long i) -> long long { return ((i % a.T) * a.Nenv + i / a.T) * (long long)W1F_SAMPLE; };
-    long long base = a.idx ? row_base(a.idx[n0]) : n0 * a.sample_stride;
-    long long pref = a.idx ? a.idx[n0 + 1 < n1 ? n0 + 1 : n0] : 0;
+    // (host-checked T * Nenv < 2^31: 32-bit row arithmetic)
+    const uint32_t T32 = (uint32_t)a.T, N32 = (uint32_t)a.Nenv;
+    auto row_base = [&](long long i) -> long long {
+        const uint32_t i32 = (uint32_t)i, q = i32 / T32;
+        return (long long)((i32 - q * T32) * N32 + q) * (long long)W1F_SAMPLE;
+    };
+    long long base = IDX ? row_base(a.idx[n0]) : n0 * a.sample_stride;
+    long long pref = IDX ? a.idx[n0 + 1 < n1 ? n0 + 1 : n0] : 0;
 
     // this thread's loads of a unit: frame pieces q = tid + 512 j (ci, y, 16-B group), g1 float4s
     // q = tid + 512 j (pixel q >> 3, channels 4 (q & 7) ..); past the ends a clamped piece is loaded
@@ -2490,12 +2496,19 @@ __global__ void __launch_bounds__(512, 1) wgrad1_frames_kernel(W1FArgs a) {
 
     // unit v's loads into set v & 1 (past the last unit: the last again, stored to the idle buffer
     // without its bias); a new sample's frame base from the idx value prefetched a sample ahead
+    // branch-free (selects, and the idx load issued for every unit): a load under a branch makes
+    // hipcc's waits at the join drain every load in flight, the next units' prefetch included
     auto issue = [&](int v, auto SET) {
         const int vc = v < nunits ? v : nunits - 1;
         const long long nv = n0 + (vc >> 1);
-        if ((v & 1) == 0 && v < nunits && v > 0) {
-            base = a.idx ? row_base(pref) : nv * a.sample_stride;
-            if (a.idx) pref = a.idx[nv + 1 < n1 ? nv + 1 : nv];
+        const bool fresh = (v & 1) == 0 && v < nunits && v > 0;
+        if constexpr (IDX) {
+            // base from the idx value loaded at the previous unit (the next sample's), then the
+            // value for the sample after this one (the same load for both halves of a sample)
+            base = fresh ? row_base(pref) : base;
+            pref = a.idx[nv + 1 < n1 ? nv + 1 : n1 - 1];
+        } else {
+            base = fresh ? nv * a.sample_stride : base;
         }
         load(raw[decltype(SET)::value], base, nv, vc & 1);
     };
@@ -3257,10 +3270,14 @@ int launch_wgrad1_frames(const void* x, long long sample_stride, const long long
     w2p_grid(batch, per, grid);
     PPOX_REQUIRE(2 * grid * (long long)(G1::K * G1::COUT + G1::COUT) * 4 <= ws_bytes,
                  "ppox_nature_conv_wgrad_split: workspace too small for the direct conv1 weight gradient");
+    PPOX_REQUIRE(!idx || T * Nenv < (1LL << 31), "ppox_nature_conv_wgrad_split_idx: T * N_env must be < 2^31");
     float* slab = reinterpret_cast<float*>(ws);
     W1FArgs a{reinterpret_cast<const uint8_t*>(x), sample_stride, idx, T, Nenv, g, amax_g, slab,
               slab + 2 * grid * (G1::K * G1::COUT), batch, per};
-    wgrad1_frames_kernel<<<(unsigned)grid, 512, 0, s>>>(a);
+    if (idx)
+        wgrad1_frames_kernel<true><<<(unsigned)grid, 512, 0, s>>>(a);
+    else
+        wgrad1_frames_kernel<false><<<(unsigned)grid, 512, 0, s>>>(a);
     PPOX_LAUNCHED_NORET("ppox_nature_conv_wgrad_split");
     return launch_wgrad_reduce<G1, false>(slab, a.bslab, (int)(2 * grid), dw, db, s);
 }
