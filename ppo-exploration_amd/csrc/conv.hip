@@ -2888,7 +2888,8 @@ __global__ void __launch_bounds__(256) wmax_kernel(PackAll p) {
     const long long n4 =
         (t == 0 ? (long long)G1::K * G1::COUT : t == 1 ? PA_N2 : t == 2 ? PA_N3 : t == 3 ? 512LL * 3136 : PA_NH) / 4;
     float m = 0.f;
-    for (long long i = (long long)b * 256 + threadIdx.x; i < n4; i += AMAX_SLOTS * 256) {
+#pragma unroll 8
+    for (long long i = (long long)b * 256 + threadIdx.x; i < n4; i += AMAX_SLOTS * 256) {  // (loads issue 8 at a time)
         const float4 v = w[i];
         m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
     }
@@ -2903,16 +2904,27 @@ __global__ void __launch_bounds__(256) wmax_kernel(PackAll p) {
     }
 }
 
+__device__ uint32_t kZeroTail[AMAX_SLOTS] = {};  // the amax partials of a tensor packed into no form
+
 __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long total) {
-    // the tensors' scales (wave-uniform), from the partials of their first packed form
+    // the tensors' scales (wave-uniform), from the partials of their first packed form; the five
+    // reads are unconditional (a tensor with no form reads zeros), so they are one round trip
     float sc[PA_TENSORS];
+    uint32_t am[PA_TENSORS];
+#pragma unroll
+    for (int t = 0; t < PA_TENSORS; ++t) {  // all five loads before the exponent stores below
+        uint16_t* f[2];
+        long long planes;
+        pa_forms(p, t, f, planes);
+        uint16_t* src = f[0] ? f[0] : f[1];
+        am[t] = amax_read(src ? pack_tail(src, planes) : kZeroTail);
+    }
 #pragma unroll
     for (int t = 0; t < PA_TENSORS; ++t) {
         uint16_t* f[2];
         long long planes;
         pa_forms(p, t, f, planes);
-        uint16_t* src = f[0] ? f[0] : f[1];
-        const int e = src ? split_scale_exp(amax_read(pack_tail(src, planes))) : 0;
+        const int e = (f[0] || f[1]) ? split_scale_exp(am[t]) : 0;
         sc[t] = exp2i(e);
         if (blockIdx.x == 0 && threadIdx.x == 0)
             for (int k = 0; k < 2; ++k)
@@ -3371,7 +3383,8 @@ __global__ void __launch_bounds__(256) rows_wgrad_reduce(const float* __restrict
     const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;  // 4 slab elements (o, feature)
     if (i >= SL) return;
     float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sp = 0; sp < splits; ++sp) {
+#pragma unroll 4
+    for (int sp = 0; sp < splits; ++sp) {  // (unrolled: the splits' loads issue together)
         const float4 v = *reinterpret_cast<const float4*>(slab + sp * SL + i);
         t.x += v.x;
         t.y += v.y;
@@ -3390,6 +3403,57 @@ __global__ void __launch_bounds__(256) rows_wgrad_reduce(const float* __restrict
         dw[i + 1] = t.y;
         dw[i + 2] = t.z;
         dw[i + 3] = t.w;
+    }
+}
+
+// The fc layer's reduce: one workgroup per output row o.  The row's 3136 NHWC-ordered sums (same
+// split order as rows_wgrad_reduce: bitwise the same values) are staged in LDS, then written in
+// Flatten order q = c * 49 + p (NHWC f = p * 64 + c) as coalesced stores; the staging row is padded
+// one float per 64 (f + (f >> 6) = 65 p + c), so the strided reads of consecutive q hit distinct banks.
+// (rows_wgrad_reduce<3136, true> scattered every store across 49-float strides.)
+__global__ void __launch_bounds__(256) fc_wgrad_reduce_perm(const float* __restrict__ slab, int splits,
+                                                            float* __restrict__ dw) {
+    constexpr int N = 3136, N4 = N / 4, UPT = (N4 + 255) / 256;
+    constexpr long long SL = 512LL * N;
+    static_assert(N == 49 * 64 && UPT == 4, "fc reduce shape");
+    __shared__ float row[N + N / 64];
+    const int o = blockIdx.x, t = threadIdx.x;
+    const float* base = slab + (long long)o * N;
+    float4 acc[UPT];
+    int uo[UPT];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int u = t + 256 * k;
+        uo[k] = 4 * (u < N4 ? u : N4 - 1);  // clamped: loads unconditional, the extra unit not stored
+    }
+#pragma unroll 2
+    for (int sp = 0; sp < splits; ++sp) {
+        float4 v[UPT];
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) v[k] = *reinterpret_cast<const float4*>(base + sp * SL + uo[k]);
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+            acc[k].x += v[k].x;
+            acc[k].y += v[k].y;
+            acc[k].z += v[k].z;
+            acc[k].w += v[k].w;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+        if (t + 256 * k >= N4) break;
+        const int f = uo[k], r = f + (f >> 6);  // the 4 features share one 64-block
+        row[r] = acc[k].x;
+        row[r + 1] = acc[k].y;
+        row[r + 2] = acc[k].z;
+        row[r + 3] = acc[k].w;
+    }
+    __syncthreads();
+    float* out = dw + (long long)o * N;
+    for (int q = t; q < N; q += 256) {
+        const int c = q / 49, pp = q - 49 * c;
+        out[q] = row[65 * pp + c];
     }
 }
 
@@ -3418,7 +3482,7 @@ extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float*
     wa.px_per_split = ppox::ceil_div(ppox::ceil_div((long long)batch, (long long)sp), (long long)MS) * MS;
     wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB><<<(unsigned)(FcWgrad::TILES * sp), 256, 0, s>>>(wa);
     PPOX_LAUNCHED_NORET("ppox_nature_fc_wgrad");
-    rows_wgrad_reduce<3136, true><<<(unsigned)ppox::ceil_div(FcWgrad::SLAB, 1024LL), 256, 0, s>>>(slab, sp, dw);
+    fc_wgrad_reduce_perm<<<512, 256, 0, s>>>(slab, sp, dw);
     PPOX_LAUNCHED("ppox_nature_fc_wgrad");
 }
 

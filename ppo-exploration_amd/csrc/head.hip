@@ -45,15 +45,19 @@ __host__ __device__ inline long long head_grads_len(int H, int A, bool intr) {
     return (long long)A * H + A + H + 1 + 2LL * H + (intr ? 2LL * H + 1 : 0);
 }
 
-// thread t owns columns 2t, 2t + 1 (float2 loads); H even, H <= 512
+// thread t owns columns 2t, 2t + 1 (float2 loads); H even, H <= 512.  AM >= A actions and the
+// intrinsic head are template parameters, so every load of a row is unconditional (the dout loads
+// of actions a >= A re-read action A - 1 and are multiplied by zero into sums never stored): the
+// row's loads issue together (a load under a branch costs a full memory round trip each)
+template <int AM, bool INTR>
 __global__ void __launch_bounds__(256) head_grads_partials(HeadGrads g, float* __restrict__ part) {
     const long long r0 = (long long)blockIdx.x * g.R, r1 = min(g.B, r0 + g.R);
     const int tid = threadIdx.x, H = g.H, A = g.A, j = 2 * tid;
-    const bool intr = g.ie != nullptr, col = j < H;
-    float2 wa[HG_MAXA], wc = {0.f, 0.f}, be = {0.f, 0.f}, bf = {0.f, 0.f}, wci = {0.f, 0.f}, bie = {0.f, 0.f};
-    float ba[HG_MAXA], bc = 0.f, bci = 0.f;
+    const bool col = j < H;
+    float2 wa[AM], wc = {0.f, 0.f}, be = {0.f, 0.f}, bf = {0.f, 0.f}, wci = {0.f, 0.f}, bie = {0.f, 0.f};
+    float ba[AM], bc = 0.f, bci = 0.f;
 #pragma unroll
-    for (int a = 0; a < HG_MAXA; ++a) {
+    for (int a = 0; a < AM; ++a) {
         wa[a] = make_float2(0.f, 0.f);
         ba[a] = 0.f;
     }
@@ -62,9 +66,17 @@ __global__ void __launch_bounds__(256) head_grads_partials(HeadGrads g, float* _
     float dm = 0.f;  // the masked df's largest |value| in this thread's columns
 #pragma unroll 4
     for (long long b = r0; b < r1; ++b) {
-        const float dv = g.dv[b], div = intr ? g.div[b] : 0.f;
+        const float dv = g.dv[b], div = INTR ? g.div[b] : 0.f;
         const float2 fv = ld(g.f, b), ev = ld(g.e, b), dev = ld(g.de, b);
         float2 dfv = ld(g.df, b);
+        float d[AM];
+#pragma unroll
+        for (int a = 0; a < AM; ++a) d[a] = g.dout[b * A + (a < A ? a : A - 1)];
+        float2 iev = {0.f, 0.f}, diev = {0.f, 0.f};
+        if constexpr (INTR) {
+            iev = ld(g.ie, b);
+            diev = ld(g.die, b);
+        }
         if (g.relu_df) {  // uniform
             dfv.x = fv.x > 0.f ? dfv.x : 0.f;
             dfv.y = fv.y > 0.f ? dfv.y : 0.f;
@@ -72,13 +84,11 @@ __global__ void __launch_bounds__(256) head_grads_partials(HeadGrads g, float* _
             dm = fmaxf(dm, fmaxf(fabsf(dfv.x), fabsf(dfv.y)));
         }
 #pragma unroll
-        for (int a = 0; a < HG_MAXA; ++a)
-            if (a < A) {
-                const float d = g.dout[b * A + a];
-                wa[a].x = fmaf(d, fv.x, wa[a].x);
-                wa[a].y = fmaf(d, fv.y, wa[a].y);
-                ba[a] += d;
-            }
+        for (int a = 0; a < AM; ++a) {
+            wa[a].x = fmaf(d[a], fv.x, wa[a].x);
+            wa[a].y = fmaf(d[a], fv.y, wa[a].y);
+            ba[a] += d[a];
+        }
         wc.x = fmaf(dv, ev.x, wc.x);
         wc.y = fmaf(dv, ev.y, wc.y);
         be.x += dev.x;
@@ -86,8 +96,7 @@ __global__ void __launch_bounds__(256) head_grads_partials(HeadGrads g, float* _
         bf.x += dfv.x;
         bf.y += dfv.y;
         bc += dv;
-        if (intr) {
-            const float2 iev = ld(g.ie, b), diev = ld(g.die, b);
+        if constexpr (INTR) {
             wci.x = fmaf(div, iev.x, wci.x);
             wci.y = fmaf(div, iev.y, wci.y);
             bie.x += diev.x;
@@ -95,7 +104,7 @@ __global__ void __launch_bounds__(256) head_grads_partials(HeadGrads g, float* _
             bci += div;
         }
     }
-    float* p = part + (long long)blockIdx.x * head_grads_len(H, A, intr);
+    float* p = part + (long long)blockIdx.x * head_grads_len(H, A, INTR);
     const long long o = (long long)A * H + A;
     auto st = [&](long long at, float2 v) {
         p[at] = v.x;
@@ -103,20 +112,22 @@ __global__ void __launch_bounds__(256) head_grads_partials(HeadGrads g, float* _
     };
     if (col) {
 #pragma unroll
-        for (int a = 0; a < HG_MAXA; ++a)
+        for (int a = 0; a < AM; ++a)
             if (a < A) st((long long)a * H + j, wa[a]);
         st(o + j, wc);
         st(o + H + 1 + j, be);
         st(o + 2 * H + 1 + j, bf);
-        if (intr) {
+        if (INTR) {
             st(o + 3 * H + 1 + j, wci);
             st(o + 4 * H + 2 + j, bie);
         }
     }
     if (tid == 0) {
-        for (int a = 0; a < A; ++a) p[(long long)A * H + a] = ba[a];
+#pragma unroll
+        for (int a = 0; a < AM; ++a)
+            if (a < A) p[(long long)A * H + a] = ba[a];
         p[o + H] = bc;
-        if (intr) p[o + 4 * H + 1] = bci;
+        if (INTR) p[o + 4 * H + 1] = bci;
     }
     if (g.relu_df) amax_record(g.amax_df, dm);
 }
@@ -336,7 +347,13 @@ extern "C" int ppox_head_grads(const float* f, const float* e, const float* dout
     float* part = reinterpret_cast<float*>(workspace);
     HeadGrads g{f, e, ie, dout, dv, div, de, die, const_cast<float*>(df), rows, R, (int)h, (int)n_actions,
                 relu_df != 0, amax_df};
-    head_grads_partials<<<(unsigned)nchunk, 256, 0, s>>>(g, part);
+    if (n_actions <= 4) {
+        if (intr) head_grads_partials<4, true><<<(unsigned)nchunk, 256, 0, s>>>(g, part);
+        else head_grads_partials<4, false><<<(unsigned)nchunk, 256, 0, s>>>(g, part);
+    } else {
+        if (intr) head_grads_partials<HG_MAXA, true><<<(unsigned)nchunk, 256, 0, s>>>(g, part);
+        else head_grads_partials<HG_MAXA, false><<<(unsigned)nchunk, 256, 0, s>>>(g, part);
+    }
     PPOX_LAUNCHED_NORET("ppox_head_grads");
     HeadGradOut o{w_actor, b_actor, w_critic, b_critic, b_extra, b_fc, w_critic_int, b_critic_int, b_int_extra};
     head_grads_reduce<<<(unsigned)((len + 63) / 64), 256, 0, s>>>(part, nchunk, len, (int)h, (int)n_actions, o);

@@ -60,7 +60,12 @@ struct CatRow {
 };
 
 template <int MAXA>
-__device__ inline void categorical_forward(const float* z, int A, CatRow<MAXA>& r) {
+__device__ inline void categorical_forward(const float* zp, int A, CatRow<MAXA>& r) {
+    // the row's logits loaded unconditionally first (j >= A re-reads logit A - 1, never used):
+    // a load under the j < A branches below would cost a memory round trip per logit
+    float z[MAXA];
+#pragma unroll
+    for (int j = 0; j < MAXA; ++j) z[j] = zp[j < A ? j : A - 1];
     float m = z[0];
 #pragma unroll
     for (int j = 1; j < MAXA; ++j)

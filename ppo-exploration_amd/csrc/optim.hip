@@ -25,6 +25,8 @@ __global__ void __launch_bounds__(SUMSQ_T) sumsq_kernel(const float* __restrict_
     double acc = 0.0;
     const long long n4 = n / 4;
     const float4* g4 = reinterpret_cast<const float4*>(g);
+    // unrolled: the loads of several strides issue before the first add (same summation order)
+#pragma unroll 4
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
         const float4 v = g4[i];
         acc += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
@@ -125,7 +127,9 @@ extern "C" int ppox_adam_step(float* params, float* grads, float* exp_avg, float
     const double step_size = lr / bc1;
     const double bc2s = std::sqrt(bc2);
     const long long n4 = n / 4;
-    const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(ppox::ceil_div(n4, 256), 1024));
+    // one float4 per thread up to 2M params: a single round trip of loads per thread (the
+    // grid-stride form with 1024 blocks took two, serialised by the loop's wait)
+    const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(ppox::ceil_div(n4, 256), 2048));
     adam_kernel<<<grid, 256, 0, ppox::as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq, n, norm_partials,
                                                            max_norm, (float)(1.0 - beta1), (float)beta2,
                                                            (float)(1.0 - beta2), (float)(-step_size), (float)bc2s,

@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of variant libraries on the bench (dev tool): tools/ab.sh TAG VARIANT [VARIANT...]
 # Runs the kernel tests selected by TESTK (default: conv2_dgrad) on each variant, then base, each
-# variant, base again at the 1-GPU (F) and per-rank (R) shapes.  Writes gpurun_out/ab_TAG/.
+# variant, base again at the 1-GPU (F) and per-rank (R) shapes (PHASES, default "F R").  Writes
+# gpurun_out/ab_TAG/.
 set -o pipefail
 TAG=$1; shift
 O=gpurun_out/ab_$TAG; mkdir -p $O
@@ -11,7 +12,7 @@ for V in "$@"; do
   PPOX_LIB=tools/variants/$V/libppox.so timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -q \
       -k "${TESTK:-conv2_dgrad}" --timeout 200 --timeout-method thread > $O/tests_$V.log 2>&1 || exit $?
 done
-for P in F R; do
+for P in ${PHASES:-F R}; do
   timeout -k 10 200 python bench.py ${!P} > $O/${P}_base.json 2>>$O/e || exit $?
   for V in "$@"; do
     PPOX_LIB=tools/variants/$V/libppox.so timeout -k 10 200 python bench.py ${!P} > $O/${P}_$V.json 2>>$O/e || exit $?
