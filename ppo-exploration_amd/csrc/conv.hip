@@ -1643,9 +1643,12 @@ __global__ void __launch_bounds__(RED_E * RG) wgrad_reduce(const float* __restri
         a.z += b.z;
         a.w += b.w;
     };
+    // (unrolled: a lane's loads of several splits issue together; the adds keep split order)
     if (i < KC) {
+#pragma unroll 8
         for (int sp = grp; sp < splits; sp += RG) add(s, *reinterpret_cast<const float4*>(slab + (long long)sp * KC + i));
     } else if (i < KC + L::COUT) {
+#pragma unroll 8
         for (int sp = grp; sp < splits; sp += RG)
             add(s, *reinterpret_cast<const float4*>(bslab + (long long)sp * L::COUT + (i - KC)));
     }
