@@ -341,7 +341,16 @@ __global__ void __launch_bounds__(256) icm_enc_finish_kernel(const float* __rest
                                                               float* __restrict__ phi, unsigned* __restrict__ rowno) {
     __shared__ float w2[32][33];
     __shared__ float a1[8][32];
-    for (int i = threadIdx.x; i < 1024; i += 256) w2[i >> 5][i & 31] = seg[32 + i];
+    {
+        float v[4];  // the four loads in flight together
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = seg[32 + threadIdx.x + 256 * k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            w2[i >> 5][i & 31] = v[k];
+        }
+    }
     const int n = threadIdx.x & 31, rr = threadIdx.x >> 5;
     const long long r = blockIdx.x * 8LL + rr;
     float s = 0.f;
@@ -407,16 +416,45 @@ __global__ void __launch_bounds__(256) icm_pair_kernel(PairArgs a) {
     __shared__ long long jrow[PB];
     __shared__ float ce[PB], sq[PB];
     const float* sg = a.seg;
-    for (int i = tid; i < 32 * 64; i += 256) Wi1[i >> 6][i & 63] = sg[g.wi1() + i];
-    for (int i = tid; i < 32 * (32 + A); i += 256) Wf1[i / (32 + A)][i % (32 + A)] = sg[g.wf1() + i];
-    for (int i = tid; i < 1024; i += 256) Wf2[i >> 5][i & 31] = sg[g.wf2() + i];
-    for (int i = tid; i < 32 * A; i += 256) Wi2[i >> 5][i & 31] = sg[g.wi2() + i];
-    for (int i = tid; i < A * A; i += 256) Wae[i / A][i % A] = sg[g.wae() + i];
+    // the weight tiles staged with all of a thread's global loads in flight together (clamped
+    // indices, no branches around them; a load -> LDS store loop waits a memory round trip per
+    // iteration): Wi1 2048, Wf1 <= 2048, Wf2 1024, Wi2 and Wae <= 1024 floats (A <= 32)
+    const int nf1 = 32 * (32 + A), ni2 = 32 * A, nae = A * A, bt = tid & 31;
+    auto cl = [](int i, int n) { return i < n ? i : n - 1; };
+    float ri1[8], rf1[8], rf2[4], ri2[4], rae[4], rb[4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        ri1[k] = sg[g.wi1() + tid + 256 * k];
+        rf1[k] = sg[g.wf1() + cl(tid + 256 * k, nf1)];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        rf2[k] = sg[g.wf2() + tid + 256 * k];
+        ri2[k] = sg[g.wi2() + cl(tid + 256 * k, ni2)];
+        rae[k] = sg[g.wae() + cl(tid + 256 * k, nae)];
+    }
+    rb[0] = sg[g.bi1() + bt];
+    rb[1] = sg[g.bf1() + bt];
+    rb[2] = sg[g.bf2() + bt];
+    rb[3] = sg[g.bi2() + cl(bt, A)];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int i = tid + 256 * k;
+        Wi1[i >> 6][i & 63] = ri1[k];
+        if (i < nf1) Wf1[i / (32 + A)][i % (32 + A)] = rf1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = tid + 256 * k;
+        Wf2[i >> 5][i & 31] = rf2[k];
+        if (i < ni2) Wi2[i >> 5][i & 31] = ri2[k];
+        if (i < nae) Wae[i / A][i % A] = rae[k];
+    }
     if (tid < 32) {
-        bi1[tid] = sg[g.bi1() + tid];
-        bf1[tid] = sg[g.bf1() + tid];
-        bf2[tid] = sg[g.bf2() + tid];
-        bi2[tid] = tid < A ? sg[g.bi2() + tid] : 0.f;
+        bi1[tid] = rb[0];
+        bf1[tid] = rb[1];
+        bf2[tid] = rb[2];
+        bi2[tid] = tid < A ? rb[3] : 0.f;
     }
     if (tid < PB) {
         const long long jj = blockIdx.x * (long long)PB + tid;
@@ -575,20 +613,39 @@ struct RowArgs {
 __global__ void __launch_bounds__(256) icm_row_bwd_kernel(RowArgs a) {
     __shared__ float W2[32][33], D[RB][33], A1[RB][33], P[RB][33], G[RB][33];
     const int tid = threadIdx.x;
-    for (int i = tid; i < 1024; i += 256) W2[i >> 5][i & 31] = a.seg[32 + i];
-    for (int i = tid; i < RB * 32; i += 256) {
-        const int rr = i >> 5, c = i & 31;
-        const long long r = blockIdx.x * (long long)RB + rr;
-        float d = 0.f, pre = 0.f;
-        if (r < a.M) {
-            const long long src = a.pos ? a.pos[r] : r;
-            d = a.dS[src * H + c];
-            if (a.dN) d = d + a.dN[src * H + c];
-            pre = a.pre1[r * H + c];
-        }
-        D[rr][c] = d;
-        P[rr][c] = pre;
-        A1[rr][c] = leaky(pre);
+    // a thread's four rows loaded with no branch around the loads (clamped rows, dN read from dS
+    // when absent and not added), so they are in flight together; then the LDS stores
+    static_assert(RB * 32 == 4 * 256, "row kernel: four elements per thread");
+    const float* dN = a.dN ? a.dN : a.dS;
+    float w2v[4], dv[4], nv[4], pv[4];
+    long long src[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = tid + 256 * k;
+        const long long r = blockIdx.x * (long long)RB + (i >> 5), rc = r < a.M ? r : a.M - 1;
+        w2v[k] = a.seg[32 + i];
+        src[k] = rc;
+        pv[k] = a.pre1[rc * H + (i & 31)];
+    }
+    if (a.pos) {  // uniform
+#pragma unroll
+        for (int k = 0; k < 4; ++k) src[k] = a.pos[src[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int c = (tid + 256 * k) & 31;
+        dv[k] = a.dS[src[k] * H + c];
+        nv[k] = dN[src[k] * H + c];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = tid + 256 * k, rr = i >> 5, c = i & 31;
+        const bool ok = blockIdx.x * (long long)RB + rr < a.M;
+        W2[i >> 5][i & 31] = w2v[k];
+        const float d = a.dN ? dv[k] + nv[k] : dv[k], pre = pv[k];
+        D[rr][c] = ok ? d : 0.f;
+        P[rr][c] = ok ? pre : 0.f;
+        A1[rr][c] = leaky(ok ? pre : 0.f);
     }
     __syncthreads();
     for (int i = tid; i < RB * 32; i += 256) {
@@ -803,23 +860,45 @@ __global__ void __launch_bounds__(256) icm_int_reward_kernel(const float* __rest
     const Seg g(A);
     __shared__ float Wf1[32][65], Wf2[32][33], Y[8][65], Vv[8][33], SQ[8][33];
     const int tid = threadIdx.x, c = tid & 31, rr = tid >> 5;
-    for (int i = tid; i < 32 * (32 + A); i += 256) Wf1[i / (32 + A)][i % (32 + A)] = seg[g.wf1() + i];
-    for (int i = tid; i < 1024; i += 256) Wf2[i >> 5][i & 31] = seg[g.wf2() + i];
+    // every global load of a thread issued before its LDS stores (clamped, branch-free; see the
+    // pair kernel): Wf1 <= 2048 and Wf2 1024 floats, the row's features, action and biases
+    const int nf1 = 32 * (32 + A);
     const long long r = blockIdx.x * 8LL + rr;
     const bool ok = r < N;
-    const int act = ok ? actions[r] : 0;
-    Y[rr][c] = ok ? phi_s[r * H + c] : 0.f;
-    if (c < A) Y[rr][32 + c] = seg[g.wae() + act * A + c];
+    const long long rc = ok ? r : N - 1;
+    float rf1[8], rf2[4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int i = tid + 256 * k;
+        rf1[k] = seg[g.wf1() + (i < nf1 ? i : nf1 - 1)];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rf2[k] = seg[g.wf2() + tid + 256 * k];
+    const int act = actions[rc];
+    const float ys = phi_s[rc * H + c], yn = phi_n[rc * H + c];
+    const float b1 = seg[g.bf1() + c], b2 = seg[g.bf2() + c];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int i = tid + 256 * k;
+        if (i < nf1) Wf1[i / (32 + A)][i % (32 + A)] = rf1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = tid + 256 * k;
+        Wf2[i >> 5][i & 31] = rf2[k];
+    }
+    Y[rr][c] = ok ? ys : 0.f;
+    if (c < A) Y[rr][32 + c] = seg[g.wae() + (ok ? act : 0) * A + c];
     __syncthreads();
     float v = 0.f;
     for (int k = 0; k < 32 + A; ++k) v += Wf1[c][k] * Y[rr][k];
-    Vv[rr][c] = leaky(v + seg[g.bf1() + c]);
+    Vv[rr][c] = leaky(v + b1);
     __syncthreads();
     float nh = 0.f;
 #pragma unroll 8
     for (int k = 0; k < 32; ++k) nh += Wf2[c][k] * Vv[rr][k];
-    nh = nh + seg[g.bf2() + c];
-    const float d = nh - (ok ? phi_n[r * H + c] : 0.f);
+    nh = nh + b2;
+    const float d = nh - (ok ? yn : 0.f);
     SQ[rr][c] = d * d;
     __syncthreads();
     if (c == 0 && ok) {
