@@ -340,6 +340,14 @@ int ppox_nature_conv2_wgrad_planes(const uint16_t* h1p, const uint16_t* q1, int6
 int64_t ppox_head_hidden_pack_elems(void);
 int ppox_head_hidden_fwd(const float* f, int64_t rows, const uint16_t* q_fwd, const float* bias, float* e,
                          const uint32_t* amax_f, void* stream);
+/* fwd split over K for small batches (as ppox_nature_fc_fwd_splitk; workspace
+ * ppox_head_hidden_fwd_splitk_workspace_bytes(rows)); with value != NULL the reduce also runs the
+ * critic head Linear(512, 1) on each finished row (models-checkpoint.py:72, 85 critic_ext):
+ * value = e w_critic^T + b_critic, bitwise as ppox_skinny_linear. */
+int64_t ppox_head_hidden_fwd_splitk_workspace_bytes(int64_t rows);
+int ppox_head_hidden_fwd_splitk(const float* f, int64_t rows, const uint16_t* q_fwd, const float* bias,
+                                void* workspace, int64_t workspace_bytes, float* e, const uint32_t* amax_f,
+                                const float* w_critic, const float* b_critic, float* value, void* stream);
 int ppox_head_hidden_dgrad(const float* de, int64_t rows, const uint16_t* q_dgrad, const float* f, float* df,
                            const uint32_t* amax_de, uint32_t* amax_df, void* stream);
 int64_t ppox_head_hidden_wgrad_workspace_bytes(int64_t rows);

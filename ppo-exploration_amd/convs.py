@@ -52,6 +52,10 @@ FC_WGRAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_WGRAD_SPLIT_MIN", "0"))
 # the heads' hidden layer Linear(512, 512) on the split-f16 GEMM (ppox_head_hidden_*) from this
 # batch up, rocBLAS f32 below (PPOX_HEAD_SPLIT_MIN overrides)
 HEAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_SPLIT_MIN", "8192"))
+# below HEAD_SPLIT_MIN_BATCH the hidden layer's forward still runs on the split-f16 kernel, split over K
+# with the critic head fused into its reduce (its backward stays on the library GEMMs);
+# PPOX_HEAD_FWD_SPLITK=0 keeps the library GEMM
+HEAD_FWD_SPLITK = os.environ.get("PPOX_HEAD_FWD_SPLITK", "1") == "1"
 
 # ReLU masks of the conv outputs as bitmasks written by the split forwards for the split dgrads
 # (PPOX_RELU_BITS=0: the dgrads read the f32 activations)
@@ -246,6 +250,20 @@ class NatureConvs:
         """the heads' hidden layer on the split-f16 kernels for a `batch`-row pass"""
         return self.qh is not None and batch >= HEAD_SPLIT_MIN_BATCH
 
+    def split_head_fwd(self, batch):
+        """only the hidden layer's forward on the split-f16 kernel (split over K) for a `batch`-row pass"""
+        return self.qh is not None and HEAD_FWD_SPLITK and 0 < batch < HEAD_SPLIT_MIN_BATCH
+
+    def head_fwd_ws(self, batch):
+        """the split-K hidden forward's workspace, one per batch size (a captured collect graph keeps
+        its own)"""
+        ws = self._ws.get(("head_sk", batch))
+        if ws is None:
+            ws = torch.empty(max(native.head_hidden_fwd_splitk_workspace_bytes(batch), 16), dtype=torch.uint8,
+                             device=self.flat.device)
+            self._ws[("head_sk", batch)] = ws
+        return ws
+
     def uses_split(self, op, layer, batch=None):
         if self.math == "split_all":  # every op that has a split kernel (tests, benchmarks)
             return (op, layer) in SPLIT_OPS or (op, layer) in SPLIT_SLOWER
@@ -290,6 +308,8 @@ class NatureConvs:
             forms.add("qfcf" if batch >= FC_SPLIT_MIN_BATCH else "wfc_nhwc")
         if self.split_head(batch):
             forms |= {"qhf", "qhd"}
+        elif self.split_head_fwd(batch):
+            forms.add("qhf")
         return forms
 
     def pack(self, batch=0, zero=None):
@@ -298,7 +318,7 @@ class NatureConvs:
         (one ppox_nature_pack_all call for the split and fc forms).  `zero` (int32 tensor) is
         zeroed by that call when it runs: returns True if it did."""
         v = (self.flat.step_count, self.flat.data.data_ptr())
-        key = (batch, HEAD_SPLIT_MIN_BATCH, FC_SPLIT_MIN_BATCH, DGRAD2_SPLIT_MAX_BATCH)  # (tests patch these)
+        key = (batch, HEAD_SPLIT_MIN_BATCH, HEAD_FWD_SPLITK, FC_SPLIT_MIN_BATCH, DGRAD2_SPLIT_MAX_BATCH)  # (tests patch these)
         if v == self._version and key == self._last_batch:  # the hot path: several times per minibatch
             return False
         if v != self._version:

@@ -1267,14 +1267,15 @@ struct ActorHead {
     float* logits;  // rows x n
 };
 
-template <int S>
+// K = 3136: the fc layer (reduce: + bias, ReLU, f's amax, the actor head); K = 512: the heads' hidden
+// layer (the same reduce with the critic head Linear(512, 1) fused, no amax)
+template <int K, int S>
 int launch_fc_fwd_sk(const Args& a, const uint16_t* q, float* slab, const float* bias, float* f, const ActorHead& act,
-                     hipStream_t st) {
+                     hipStream_t st, const char* name = "ppox_nature_fc_fwd_splitk") {
     Args b = a;
     b.y = slab;
     b.amax_y = nullptr;  // partial products: f's amax is recorded by the reduce
-    const int rc = launch_sgemm<SgRowsSK<3136, 512, S>>(b, q, ppox::ceil_div(a.batch, SG_ROWS) * FcFwd::NCB * S, st,
-                                                        "ppox_nature_fc_fwd_splitk");
+    const int rc = launch_sgemm<SgRowsSK<K, 512, S>>(b, q, ppox::ceil_div(a.batch, SG_ROWS) * FcFwd::NCB * S, st, name);
     if (rc != PPOX_OK) return rc;
     const float4* sl = reinterpret_cast<const float4*>(slab);
     float4* f4 = reinterpret_cast<float4*>(f);
@@ -1290,7 +1291,7 @@ int launch_fc_fwd_sk(const Args& a, const uint16_t* q, float* slab, const float*
             fc_fwd_sk_reduce<512, S><<<ppox::ceil_div(a.batch * 512 / 4, 256), 256, 0, st>>>(sl, a.batch, bias, f4,
                                                                                              a.amax_y);
     }
-    PPOX_LAUNCHED("ppox_nature_fc_fwd_splitk");
+    PPOX_LAUNCHED(name);
 }
 
 // ---------------------------------------------------------------------------
@@ -3532,10 +3533,10 @@ extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const u
     hipStream_t st = ppox::as_stream(stream);
     const ActorHead act{w_actor, b_actor, logits ? (int)n_actions : 0, logits};
     switch (fc_fwd_splits(batch)) {
-        case 1: return launch_fc_fwd_sk<1>(a, q_fwd, slab, bias, f, act, st);
-        case 2: return launch_fc_fwd_sk<2>(a, q_fwd, slab, bias, f, act, st);
-        case 4: return launch_fc_fwd_sk<4>(a, q_fwd, slab, bias, f, act, st);
-        default: return launch_fc_fwd_sk<8>(a, q_fwd, slab, bias, f, act, st);
+        case 1: return launch_fc_fwd_sk<3136, 1>(a, q_fwd, slab, bias, f, act, st);
+        case 2: return launch_fc_fwd_sk<3136, 2>(a, q_fwd, slab, bias, f, act, st);
+        case 4: return launch_fc_fwd_sk<3136, 4>(a, q_fwd, slab, bias, f, act, st);
+        default: return launch_fc_fwd_sk<3136, 8>(a, q_fwd, slab, bias, f, act, st);
     }
 }
 
@@ -3582,6 +3583,37 @@ extern "C" int ppox_head_hidden_fwd(const float* f, int64_t rows, const uint16_t
     Args a{f, nullptr, 0, 0, 0, nullptr, bias, nullptr, e, rows, amax_f, nullptr, pack_exp(q_fwd, PL_H)};
     return launch_sgemm<SgRows<512, 512, FC_FWD, 8>>(a, q_fwd, ppox::ceil_div(rows, SG_ROWS) * HeadFwd::NCB,
                                                       ppox::as_stream(stream), "ppox_head_hidden_fwd");
+}
+
+extern "C" int64_t ppox_head_hidden_fwd_splitk_workspace_bytes(int64_t rows) {
+    return rows <= 0 ? 0 : (int64_t)fc_fwd_splits(rows) * rows * 512 * 4;
+}
+
+// small batches: split over K like ppox_nature_fc_fwd_splitk (128 workgroups of 128 rows at 2,048 rows
+// leave half the chip idle), the critic head v = e w_critic^T + b_critic fused into the reduce
+extern "C" int ppox_head_hidden_fwd_splitk(const float* f, int64_t rows, const uint16_t* q_fwd, const float* bias,
+                                           void* workspace, int64_t workspace_bytes, float* e, const uint32_t* amax_f,
+                                           const float* w_critic, const float* b_critic, float* value, void* stream) {
+    if (rows == 0) return PPOX_OK;
+    PPOX_REQUIRE(f && q_fwd && bias && e && workspace && amax_f && rows > 0, "ppox_head_hidden_fwd_splitk: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(f) && ppox::aligned16(q_fwd) && ppox::aligned16(e) && ppox::aligned16(workspace) &&
+                     ppox::aligned16(amax_f),
+                 "ppox_head_hidden_fwd_splitk: 16B alignment");
+    PPOX_REQUIRE(workspace_bytes >= ppox_head_hidden_fwd_splitk_workspace_bytes(rows),
+                 "ppox_head_hidden_fwd_splitk: workspace too small");
+    PPOX_REQUIRE(!value || (w_critic && b_critic && ppox::aligned16(w_critic)),
+                 "ppox_head_hidden_fwd_splitk: the fused critic head needs a 16B-aligned weight");
+    Args a{f, nullptr, 0, 0, 0, nullptr, bias, nullptr, e, rows, amax_f, nullptr, pack_exp(q_fwd, PL_H)};
+    float* slab = reinterpret_cast<float*>(workspace);
+    hipStream_t st = ppox::as_stream(stream);
+    const ActorHead crit{w_critic, b_critic, value ? 1 : 0, value};
+    constexpr const char* nm = "ppox_head_hidden_fwd_splitk";
+    switch (fc_fwd_splits(rows)) {
+        case 1: return launch_fc_fwd_sk<512, 1>(a, q_fwd, slab, bias, e, crit, st, nm);
+        case 2: return launch_fc_fwd_sk<512, 2>(a, q_fwd, slab, bias, e, crit, st, nm);
+        case 4: return launch_fc_fwd_sk<512, 4>(a, q_fwd, slab, bias, e, crit, st, nm);
+        default: return launch_fc_fwd_sk<512, 8>(a, q_fwd, slab, bias, e, crit, st, nm);
+    }
 }
 
 extern "C" int ppox_head_hidden_dgrad(const float* de, int64_t rows, const uint16_t* q_dgrad, const float* f, float* df,

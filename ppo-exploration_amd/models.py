@@ -159,14 +159,27 @@ class CnnActorCritic(nn.Module):
         if out is None:
             out = native.head_linear(f, a.weight, a.bias)
         cv = self.conv_impl
+        v = None
         if am is not None and cv is not None and cv.split_head(f.shape[0]):
             import convs as _convs
             cv.pack(f.shape[0])
             e = torch.empty_like(f)
             native.head_hidden_fwd(f, cv.qh[0], el.bias, e, amax_f=am[_convs.AM_F])
+        elif am is not None and cv is not None and cv.split_head_fwd(f.shape[0]) and f.is_contiguous() \
+                and f.data_ptr() % 16 == 0:
+            # small batches: split over K, the critic head fused into the reduce when its weight is aligned
+            import convs as _convs
+            B = f.shape[0]
+            cv.pack(B)
+            e = torch.empty_like(f)
+            fuse = ce.weight.is_contiguous() and ce.weight.data_ptr() % 16 == 0
+            v = torch.empty(B, device=f.device) if fuse else None
+            native.head_hidden_fwd_splitk(f, cv.qh[0], el.bias, cv.head_fwd_ws(B), e, amax_f=am[_convs.AM_F],
+                                          critic=(ce.weight, ce.bias) if fuse else None, value=v)
         else:
             e = linear_relu(f, el.weight, el.bias)
-        v = native.head_linear(e, ce.weight, ce.bias).squeeze(-1)
+        if v is None:
+            v = native.head_linear(e, ce.weight, ce.bias).squeeze(-1)
         ie = iv = None
         if self.intrinsic:
             il, ci = self.int_extra_layer[0], self.critic_int

@@ -78,6 +78,7 @@ SIGNATURES = {
     "ppox_nature_conv2_wgrad_planes": [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp],
+    "ppox_head_hidden_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -114,6 +115,7 @@ _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p
              "ppox_icm_partials_bytes": ctypes.c_int64, "ppox_icm_g1_pack_elems": ctypes.c_int64,
              "ppox_nature_fc_fwd_splitk_workspace_bytes": ctypes.c_int64, "ppox_amax_slots": ctypes.c_int32,
              "ppox_head_hidden_pack_elems": ctypes.c_int64, "ppox_head_hidden_wgrad_workspace_bytes": ctypes.c_int64,
+             "ppox_head_hidden_fwd_splitk_workspace_bytes": ctypes.c_int64,
              "ppox_nature_conv2_wgrad_planes_workspace_bytes": ctypes.c_int64}
 _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad_splits": [_i32, _i64],
                  "ppox_nature_wgrad_workspace_bytes": [_i32, _i64], "ppox_nature_split_pack_elems": [_i32],
@@ -124,6 +126,7 @@ _RESTYPE_ARGS = {"ppox_rms_u8_workspace_bytes": [_i64, _i64], "ppox_nature_wgrad
                  "ppox_icm_w1_pack_elems": [_i64], "ppox_icm_encode_workspace_bytes": [_i64, _i64],
                  "ppox_icm_partials_bytes": [_i64, _i32], "ppox_icm_g1_pack_elems": [_i64],
                  "ppox_nature_fc_fwd_splitk_workspace_bytes": [_i64], "ppox_head_hidden_wgrad_workspace_bytes": [_i64],
+                 "ppox_head_hidden_fwd_splitk_workspace_bytes": [_i64],
                  "ppox_nature_conv2_wgrad_planes_workspace_bytes": [_i64]}
 
 _lib = None
@@ -596,6 +599,22 @@ def head_hidden_fwd(f, q_fwd, bias, e, amax_f=None, stream=None):
     if rows:
         amax_f = _amax_of(f, amax_f, stream)
     call("ppox_head_hidden_fwd", _p(f), rows, _p(q_fwd), _p(bias), _p(e), _p(amax_f), stream_ptr(stream))
+
+
+def head_hidden_fwd_splitk_workspace_bytes(rows):
+    return int(load().ppox_head_hidden_fwd_splitk_workspace_bytes(int(rows)))
+
+
+def head_hidden_fwd_splitk(f, q_fwd, bias, workspace, e, amax_f=None, critic=None, value=None, stream=None):
+    """e = relu(f W^T + b) split over K (small batches); with critic = (w (1 x 512), b) the reduce
+    also writes value (rows,) = e w^T + b (bitwise as the skinny kernel)."""
+    rows = f.shape[0]
+    if rows:
+        amax_f = _amax_of(f, amax_f, stream)
+    wc, bc = critic if critic is not None else (None, None)
+    call("ppox_head_hidden_fwd_splitk", _p(f), rows, _p(q_fwd), _p(bias), _p(workspace),
+         workspace.numel() * workspace.element_size(), _p(e), _p(amax_f), _p(wc), _p(bc), _p(value),
+         stream_ptr(stream))
 
 
 def head_hidden_dgrad(de, q_dgrad, f, df, amax_de=None, amax_df=None, stream=None):

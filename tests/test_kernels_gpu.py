@@ -1082,6 +1082,36 @@ def test_head_hidden_split_vs_fp64(B):
     assert not z.any()
 
 
+@pytest.mark.parametrize("B", [1, 3, 127, 512, 2048, 4099])
+def test_head_hidden_fwd_splitk_vs_fp64(B):
+    """The hidden layer's forward split over K (small batches, every split count 8 .. 1): e vs float64
+    within 2x torch's own f32 GEMM error, bitwise the same e with and without the fused critic head,
+    the fused value bitwise equal to the skinny kernel on that e, run-to-run bitwise."""
+    import native
+    g = torch.Generator(device="cuda").manual_seed(B + 7)
+    W = torch.randn(512, 512, device="cuda", generator=g) * 0.04
+    bias = torch.randn(512, device="cuda", generator=g) * 0.1
+    f = torch.relu(torch.randn(B, 512, device="cuda", generator=g))
+    wc = torch.randn(1, 512, device="cuda", generator=g) * 0.05
+    bc = torch.randn(1, device="cuda", generator=g)
+    n = native.head_hidden_pack_elems()
+    qf = torch.empty(n, dtype=torch.int16, device="cuda")
+    w1, w2, w3 = torch.randn(32, 4, 8, 8, device="cuda"), torch.randn(64, 32, 4, 4, device="cuda"), \
+        torch.randn(64, 64, 3, 3, device="cuda")
+    native.nature_pack_all(w1, w2, w3, None, None, None, None, None, None, None, None, None, W, qf, None)
+    ws = torch.empty(max(native.head_hidden_fwd_splitk_workspace_bytes(B), 16), dtype=torch.uint8, device="cuda")
+    e, e2, e3 = (torch.empty(B, 512, device="cuda") for _ in range(3))
+    v, v2 = torch.empty(B, device="cuda"), torch.empty(B, device="cuda")
+    native.head_hidden_fwd_splitk(f, qf, bias, ws, e)
+    native.head_hidden_fwd_splitk(f, qf, bias, ws, e2, critic=(wc, bc), value=v)
+    native.head_hidden_fwd_splitk(f, qf, bias, ws, e3, critic=(wc, bc), value=v2)
+    ref = torch.relu(f.double() @ W.double().t() + bias.double())
+    rel = lambda got, r: ((got.double() - r).abs().max() / r.abs().max()).item()
+    assert rel(e, ref) <= 2 * rel(torch.relu(torch.addmm(bias, f, W.t())), ref) + 1e-7
+    assert torch.equal(e, e2) and torch.equal(e2, e3) and torch.equal(v, v2)
+    assert torch.equal(v, native.head_linear(e2, wc, bc).squeeze(-1))
+
+
 def test_fc_wgrad_zero_rows_writes_zero():
     import native
     dw = torch.full((512, 3136), 1.0, device="cuda")
