@@ -412,9 +412,9 @@ def main():
             out["gae_roofline"]["large_n"] = large
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, ROOT)
-        from oracle.baseline import atari_ppo_rate
-        out["cpu_baseline"] = atari_ppo_rate(args.envs, args.nstep, args.epochs, args.batch_size,
-                                             threads=args.cpu_threads or None)
+        from oracle.baseline import atari_ppo_iteration_rate
+        out["cpu_baseline"] = atari_ppo_iteration_rate(args.envs, args.nstep, args.epochs, args.batch_size,
+                                                       threads=args.cpu_threads or None)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

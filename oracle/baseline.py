@@ -1,7 +1,10 @@
 """CPU baseline for bench.py: the oracle's restatement of the reference PPO
 iteration (numpy step-major buffer + Python-loop GAE + per-minibatch torch-CPU
 autograd and Adam, ppo.py:166-259) timed on the host cores, on a BOUNDED sample
-of the benchmark workload, extrapolated per env-step.
+of the benchmark workload: atari_ppo_iteration_rate times one complete iteration
+(collect -> GAE -> n_epochs of minibatch updates) end to end at a reduced env count
+(bench.py's leg); atari_ppo_rate is the earlier per-phase sample extrapolated per
+env-step.
 
 Test infrastructure only (see oracle/__init__.py): imported solely by
 bench.py's cpu_baseline leg.  Kind "port" — the reference's Python cannot
@@ -73,6 +76,38 @@ def atari_ppo_rate(n_envs, nstep, n_epochs, batch_size, sample_envs=512, sample_
                        f"({t_gae*1e9:.0f} ns/elem), train {rows} rows in minibatches of {bs} "
                        f"({t_train*1e3:.2f} ms/row/epoch) x {n_epochs} epochs; extrapolated per env-step"),
             "wall_s": round(time.time() - t_start, 1)}
+
+
+def atari_ppo_iteration_rate(n_envs, nstep, n_epochs, batch_size, sample_envs=64, threads=None, seed=0):
+    """env-steps/s of ONE complete reference PPO iteration timed end to end on the CPU: collect
+    sample_envs envs x nstep steps (NatureCNN act + env + storage; GAE in the rollout's finish),
+    then n_epochs over the sample_envs * nstep rows in minibatches of min(batch_size, rows) (fwd +
+    bwd + clip + Adam).  The workload's n_envs are scaled down to sample_envs: the per-env-step cost
+    does not depend on the env count, and the minibatch is all the sample's rows when batch_size
+    exceeds them."""
+    if threads:
+        torch.set_num_threads(threads)
+    th = torch.get_num_threads()
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    env = SyntheticAtari(sample_envs, seed)
+    env.observation_space = type("Box", (), {"shape": (4, 84, 84)})()
+    env.action_space = type("Discrete", (), {"n": 4})()
+    rows = sample_envs * nstep
+    bs = min(batch_size, rows)
+    alg = OraclePPO(env, nstep=nstep, batch_size=bs, n_epochs=n_epochs, net=M.NatureCNN(4, 4))
+    t0 = time.time()
+    alg.collect()
+    t1 = time.time()
+    alg.train()
+    t2 = time.time()
+    return {"value": rows / (t2 - t0), "unit": "env-steps/s", "cores": th, "kind": "port",
+            "sample": (f"one complete oracle PPO iteration (torch-CPU NatureCNN) timed end to end on {th} threads: "
+                       f"collect {sample_envs} envs x {nstep} steps with GAE ({t1 - t0:.1f} s), {n_epochs} epochs "
+                       f"over the {rows} rows in minibatches of {bs} ({t2 - t1:.1f} s); the workload's {n_envs} "
+                       f"envs scaled down to {sample_envs} (batch {batch_size} > {rows} rows: one minibatch "
+                       f"per epoch)"),
+            "wall_s": round(t2 - t0, 1)}
 
 
 if __name__ == "__main__":
