@@ -137,9 +137,15 @@ struct Seg {
 // ---------------------------------------------------------------------------
 constexpr int ENC_CK = 64;  // k (frame bytes per row) of one forward chunk
 
+// ICM_W1_PARTS workgroups per row: each derives the row's amax from the whole row (the redundant reads hit
+// L2) and packs its own 1/ICM_W1_PARTS of the row's 8-k runs, so the launch has 32 x ICM_W1_PARTS workgroups
+// instead of one latency-bound workgroup per row (a second launch for a shared amax would cost more)
+#ifndef ICM_W1_PARTS
+#define ICM_W1_PARTS 8
+#endif
 __global__ void __launch_bounds__(1024) icm_pack_w1_kernel(const float* __restrict__ w, int K, u32x4* __restrict__ q) {
     __shared__ uint32_t red[16];
-    const int n = blockIdx.x, tid = threadIdx.x;
+    const int n = blockIdx.x / ICM_W1_PARTS, part = blockIdx.x % ICM_W1_PARTS, tid = threadIdx.x;
     const float* wr = w + (long long)n * K;
     uint32_t m = 0u;
     for (int k = tid * 4; k < K; k += 4096) {
@@ -155,7 +161,8 @@ __global__ void __launch_bounds__(1024) icm_pack_w1_kernel(const float* __restri
     for (int i = 1; i < 16; ++i) m = max(m, red[i]);
     const int E = split_scale_exp(m);
     const float sc = exp2i(E);
-    for (int g = tid; g < K / 8; g += 1024) {
+    const int per = (K / 8 + ICM_W1_PARTS - 1) / ICM_W1_PARTS, g1 = min(K / 8, (part + 1) * per);
+    for (int g = part * per + tid; g < g1; g += 1024) {
         const int k0 = g * 8, c = k0 / ENC_CK, r = k0 % ENC_CK;
         const int st = 2 * (r >> 5) + ((r >> 3) & 1), lane = n + 32 * ((r >> 4) & 1);
         u32x4 p0, p1;
@@ -163,7 +170,7 @@ __global__ void __launch_bounds__(1024) icm_pack_w1_kernel(const float* __restri
         q[((c * 4 + st) * 2 + 0) * 64 + lane] = p0;
         q[((c * 4 + st) * 2 + 1) * 64 + lane] = p1;
     }
-    if (tid == 0) reinterpret_cast<int*>(q + (long long)K / 16 * 2 * 64)[n] = E;
+    if (tid == 0 && part == 0) reinterpret_cast<int*>(q + (long long)K / 16 * 2 * 64)[n] = E;
 }
 
 // ---------------------------------------------------------------------------
@@ -942,7 +949,7 @@ extern "C" int64_t ppox_icm_w1_pack_elems(int64_t K) { return icm_shape_ok(K) ? 
 extern "C" int ppox_icm_pack_w1(const float* w1, int64_t K, uint16_t* q, void* stream) {
     PPOX_REQUIRE(w1 && q && icm_shape_ok(K), "ppox_icm_pack_w1: bad arguments (K must be a positive multiple of 64)");
     PPOX_REQUIRE(ppox::aligned16(w1) && ppox::aligned16(q), "ppox_icm_pack_w1: 16-byte alignment");
-    icm_pack_w1_kernel<<<H, 1024, 0, ppox::as_stream(stream)>>>(w1, (int)K, reinterpret_cast<u32x4*>(q));
+    icm_pack_w1_kernel<<<H * ICM_W1_PARTS, 1024, 0, ppox::as_stream(stream)>>>(w1, (int)K, reinterpret_cast<u32x4*>(q));
     PPOX_LAUNCHED("ppox_icm_pack_w1");
 }
 
