@@ -1254,10 +1254,12 @@ __global__ void __launch_bounds__(256) fc_fwd_sk_reduce_actor(const float4* __re
 }
 
 // K-splits for a batch: enough (row tile, column block, split) workgroups for two per CU, at most 8
-inline int fc_fwd_splits(long long batch) {
+// (the heads' 512-deep hidden layer: splits up to 256 workgroups — 2 at 2,048 rows: 9.5 + 5.9 µs for the
+// GEMM + reduce vs 10.9 + 6.2 with the fc layer's 512, whose K = 3136 gains from the fourth split)
+inline int fc_fwd_splits(long long batch, long long wgs = 512) {
     const long long wg = ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB;
     int s = 1;
-    while (s < 8 && wg * s < 512) s *= 2;
+    while (s < 8 && wg * s < wgs) s *= 2;
     return s;
 }
 
@@ -3586,7 +3588,7 @@ extern "C" int ppox_head_hidden_fwd(const float* f, int64_t rows, const uint16_t
 }
 
 extern "C" int64_t ppox_head_hidden_fwd_splitk_workspace_bytes(int64_t rows) {
-    return rows <= 0 ? 0 : (int64_t)fc_fwd_splits(rows) * rows * 512 * 4;
+    return rows <= 0 ? 0 : (int64_t)fc_fwd_splits(rows, 256) * rows * 512 * 4;
 }
 
 // small batches: split over K like ppox_nature_fc_fwd_splitk (128 workgroups of 128 rows at 2,048 rows
@@ -3608,7 +3610,7 @@ extern "C" int ppox_head_hidden_fwd_splitk(const float* f, int64_t rows, const u
     hipStream_t st = ppox::as_stream(stream);
     const ActorHead crit{w_critic, b_critic, value ? 1 : 0, value};
     constexpr const char* nm = "ppox_head_hidden_fwd_splitk";
-    switch (fc_fwd_splits(rows)) {
+    switch (fc_fwd_splits(rows, 256)) {
         case 1: return launch_fc_fwd_sk<512, 1>(a, q_fwd, slab, bias, e, crit, st, nm);
         case 2: return launch_fc_fwd_sk<512, 2>(a, q_fwd, slab, bias, e, crit, st, nm);
         case 4: return launch_fc_fwd_sk<512, 4>(a, q_fwd, slab, bias, e, crit, st, nm);
