@@ -25,16 +25,23 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (= f32 vector) dense peak
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of the dominant kernel from the latest committed rocprofv3 --pmc
-    summary (profiles/rNN_pmc_summary.json, made by tools/pmc_summary.py from separate
-    FETCH_SIZE / WRITE_SIZE passes of this bench command, gfx950-corrected 2*FETCH + WRITE)."""
+def pmc_traffic(pattern):
+    """HBM bytes per launch of a kernel from the latest committed rocprofv3 --pmc summary
+    (profiles/rNN_pmc_summary.json, made by tools/pmc_summary.py from separate FETCH_SIZE /
+    WRITE_SIZE passes of this bench command, gfx950-corrected 2*FETCH + WRITE).  `pattern` is a
+    regular expression over rocprof's kernel names (template arguments vary with the build's
+    forms: Px<> wrappers, IDX flags), matched in full; the summary's first matching key wins."""
     import glob
+    import re
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
-        d = json.load(f).get(kernel)
+        summary = json.load(f)
+    d = summary.get(pattern)
+    if d is None:
+        rx = re.compile(pattern)
+        d = next((v for k, v in summary.items() if rx.fullmatch(k)), None)
     return (None, None) if d is None else (d["hbm_bytes_per_launch_corrected"], os.path.relpath(files[-1], ROOT))
 
 
@@ -43,7 +50,8 @@ def pmc_traffic(kernel):
 # launch: MACs and algorithmic HBM bytes; `fixed` = bytes per launch independent of
 # the row count (weights in, weight gradient out); `products` = f16 MFMA products per f32 MAC of
 # the split-f16 form (2 when one operand is the exact u8 frame); `rows_arg` = the entry point's
-# argument holding the row count; `rocprof` = the kernel's rocprofv3 name (PMC lookup).
+# argument holding the row count; `rocprof` = a regular expression matching the kernel's rocprofv3
+# name (PMC lookup; `PX` / `IDX` below absorb the template flags of the planes / rollout-row forms).
 CONV_MAC = {1: 400 * 256 * 32, 2: 81 * 512 * 64, 3: 49 * 576 * 64}
 ACT_B = {0: 28224, 1: 20 * 20 * 32 * 4, 2: 9 * 9 * 64 * 4, 3: 7 * 7 * 64 * 4}
 BITMASK_B = {1: 400 * 4, 2: 81 * 4, 3: 49 * 4}   # a layer's ReLU bitmask (one u32 per pixel)
@@ -51,17 +59,29 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA
 FC_K, FC_N, HID = 3136, 512, 512
 
 
+def _sg(prob, tail):
+    """rocprof name pattern of an sgemm_kernel instance, with or without the Px<> wrapper (PX operands)"""
+    import re
+    return r"sgemm_kernel<(Px<)?" + re.escape(prob) + r"(, \w+(, \w+)?>)?, " + tail + ">"
+
+
+IDX = r"(, \w+)*"  # trailing template flags
+
+
 def _kernels():
+    import re
     k = {}
-    roc = {("fwd", 1): "fwd1_split_kernel<1, false>",
-           ("fwd", 2): "sgemm_kernel<SgFwd<32, 20, 20, 4, 4, 2, 64, false>, 4, 2>",
-           ("fwd", 3): "sgemm_kernel<SgFwd<64, 9, 9, 3, 3, 1, 64, false>, 4, 2>",
-           ("dgrad", 2): "dgrad2_colp_kernel<true, false>",
-           ("dgrad", 3): "sgemm_kernel<SgDgradPM<64, 9, 9, 3, 3, 1, 64, true>, 4, 2>",
-           ("wgrad", 1): ("wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>"
-                          if os.environ.get("PPOX_WGRAD1_IM2COL") == "1" else "wgrad1_frames_kernel"),
-           ("wgrad", 2): "wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128, false, 1>",
-           ("wgrad", 3): "wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64, false, 1>"}
+    # conv1 in a training pass reads its rows through the rollout index (IDX form <..., true>); the
+    # collect pass's forward of the same name without it runs at another row count
+    roc = {("fwd", 1): r"fwd1_split_kernel<1, false, true>",
+           ("fwd", 2): _sg("SgFwd<32, 20, 20, 4, 4, 2, 64, false>", "4, 2"),
+           ("fwd", 3): _sg("SgFwd<64, 9, 9, 3, 3, 1, 64, false>", "4, 2"),
+           ("dgrad", 2): r"dgrad2_colp_kernel<true, false>",
+           ("dgrad", 3): _sg("SgDgradPM<64, 9, 9, 3, 3, 1, 64, true>", "4, 2"),
+           ("wgrad", 1): (re.escape("wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>")
+                          if os.environ.get("PPOX_WGRAD1_IM2COL") == "1" else r"wgrad1_frames_kernel<true>"),
+           ("wgrad", 2): re.escape("wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128, false, 1>"),
+           ("wgrad", 3): re.escape("wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64, false, 1") + IDX + ">"}
     for op in ("fwd", "dgrad", "wgrad"):
         for layer in (1, 2, 3):
             if op == "dgrad" and layer == 1:
@@ -82,33 +102,34 @@ def _kernels():
     # H1P (conv1's output as two f16 planes, the size of its f32 form): conv1 forward writing it,
     # conv2 forward and the direct conv2 weight gradient reading it
     k["ppox_nature_conv1_fwd_planes"] = dict(rows_arg=1, macs=CONV_MAC[1], bytes=ACT_B[0] + ACT_B[1], fixed=0,
-                                             products=2, rocprof="fwd1_split_kernel<1, true>", label="conv1 fwd (H1P)")
+                                             products=2, rocprof=r"fwd1_split_kernel<1, true, true>", label="conv1 fwd (H1P)")
     k["ppox_nature_conv2_fwd_planes"] = dict(rows_arg=2, macs=CONV_MAC[2], bytes=ACT_B[1] + ACT_B[2], fixed=0,
-                                             products=3, rocprof="sgemm_kernel<SgFwd2P, 4, 2>", label="conv2 fwd (H1P)")
+                                             products=3, rocprof=_sg("SgFwd2P", "4, 2"), label="conv2 fwd (H1P)")
     k["ppox_nature_conv2_wgrad_planes"] = dict(rows_arg=2, macs=CONV_MAC[2], bytes=ACT_B[1] + ACT_B[2], fixed=0,
                                                products=3, rocprof="wgrad2_planes_kernel",
                                                label="conv2 wgrad (H1P, direct)")
     w_fc = FC_K * FC_N * 4          # weights in as two fp16 planes (= f32 bytes) / dW out in f32
     k["ppox_nature_fc_fwd"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=ACT_B[3] + FC_N * 4, fixed=w_fc, products=3,
-                                   rocprof="sgemm_kernel<SgRows<3136, 512, 0, 8, false>, 4, 3>", label="fc fwd")
+                                   rocprof=_sg("SgRows<3136, 512, 0, 8, false>", "4, 3"), label="fc fwd")
     k["ppox_nature_fc_fwd_splitk"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=ACT_B[3] + FC_N * 4, fixed=w_fc,
-                                          products=3, rocprof=None, label="fc fwd split-K")
+                                          products=3, rocprof=r"sgemm_kernel<(Px<)?SgRowsSK<3136, 512, \d+>(, \w+(, \w+)?>)?, 4, 3>",
+                                          label="fc fwd split-K")
     k["ppox_nature_fc_dgrad"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=FC_N * 4 + ACT_B[3] + BITMASK_B[3],
                                      fixed=w_fc, products=3,
-                                     rocprof="sgemm_kernel<SgRows<512, 3136, 1, 12, true>, 4, 3>", label="fc dgrad")
+                                     rocprof=_sg("SgRows<512, 3136, 1, 12, true>", "4, 3"), label="fc dgrad")
     k["ppox_nature_fc_wgrad"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=FC_N * 4 + ACT_B[3], fixed=w_fc, products=3,
-                                     rocprof="wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 49>",
+                                     rocprof=re.escape("wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 49") + IDX + ">",
                                      label="fc wgrad")
     w_h = HID * HID * 4
     k["ppox_head_hidden_fwd"] = dict(rows_arg=1, macs=HID * HID, bytes=2 * HID * 4, fixed=w_h, products=3,
-                                     rocprof="sgemm_kernel<SgRows<512, 512, 0, 8, false>, 4, 3>",
+                                     rocprof=_sg("SgRows<512, 512, 0, 8, false>", "4, 3"),
                                      label="head hidden fwd")
     # dgrad: de in, the heads' input grad read + written (accumulated in place), f read for the ReLU
     k["ppox_head_hidden_dgrad"] = dict(rows_arg=1, macs=HID * HID, bytes=4 * HID * 4, fixed=w_h, products=3,
-                                       rocprof="sgemm_kernel<SgRows<512, 512, 2, 8, false>, 4, 3>",
+                                       rocprof=_sg("SgRows<512, 512, 2, 8, false>", "4, 3"),
                                        label="head hidden dgrad")
     k["ppox_head_hidden_wgrad"] = dict(rows_arg=1, macs=HID * HID, bytes=2 * HID * 4, fixed=w_h, products=3,
-                                       rocprof="wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 8>",
+                                       rocprof=re.escape("wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 8>"),
                                        label="head hidden wgrad")
     return k
 
@@ -309,15 +330,22 @@ def main():
     import convs
     keys = list(KERNELS)
     streams = convs.BWD_STREAMS
-    solo = {}
+    # The second warmup iteration (two streams, as the timed region runs) is event-timed too: its
+    # largest kernel is the one rocprofv3's --stats ranks first ("roofline_rocprof"), whose event
+    # durations include its sharing of the CUs with the other stream's kernels.
+    solo, duo = {}, {}
     for w in range(args.warmup):
         convs.BWD_STREAMS = streams and w > 0
-        if w == 0:
+        if w == 0 or (w == 1 and streams):
             alg.collect_samples()
             native.enable_event_timing(keys)
             alg.train()
-            solo = {k: same_size(k, native.event_times_ms(k)) for k in keys}
+            times = {k: same_size(k, native.event_times_ms(k)) for k in keys}
             native.enable_event_timing([])
+            if w == 0:
+                solo = times
+            else:
+                duo = times
         else:
             iteration()
     convs.BWD_STREAMS = streams
@@ -395,6 +423,17 @@ def main():
                         "solo_mean_us": q["mean_us"], "rows": q["rows"], "bound": q["bound"], "frac": q["frac"],
                         "mfma_frac": q["mfma_frac"], "hbm_frac": q["hbm_frac"], "pmc_ratio": q["traffic_ratio"]})
         out["roofline_top"] = top
+    duo_tot = {k: sum(t for t, _ in v) for k, v in duo.items()}
+    if any(duo_tot.values()):
+        k2 = max(duo_tot, key=duo_tot.get)
+        q = kernel_roofline(k2, duo[k2])
+        out["roofline_rocprof"] = {
+            "kernel": q["kernel"], "bound": q["bound"], "frac": q["frac"], "mean_us": q["mean_us"], "rows": q["rows"],
+            "hbm_frac": q["hbm_frac"], "mfma_frac": q["mfma_frac"],
+            "share_of_mfma_kernel_time": round(duo_tot[k2] / sum(duo_tot.values()), 3),
+            "selection": ("largest total kernel time in a two-stream warmup iteration (the ranking of rocprofv3 "
+                          "--stats over the timed region); its event durations include sharing the CUs with the "
+                          "other stream's kernels")}
     if gae_ms:
         n_local = args.envs // world
         alg_bytes = (17 if gae_kernel == "ppox_gae" else 33) * args.nstep * n_local

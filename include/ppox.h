@@ -298,12 +298,15 @@ int64_t ppox_nature_fc_pack_elems(void);
 /* All weight packings of one optimizer step in a single launch (any output may be null):
  * wpd2 = f32 conv2 dgrad ([(ky,kx,co)][ci]); q1..q3 / qd2, qd3 = split forms (as
  * ppox_nature_pack_split); qfc_fwd / qfc_dgrad = fc split forms (as ppox_nature_fc_pack).
+ * With q2 / q3 / qfc_dgrad the tails also get the PX output bounds (the column l1-norms of the
+ * packed matrix and, from b2 / b3 — nullable: a PX output bounded without them comes out NaN —
+ * the bias bound), read by the producers of the PX planes h2, h3 and g3 (below).
  * zero (nullable, 16B-aligned): zero_words uint32 set to 0 before the packing kernels finish —
  * the next pass's amax table, so a training step needs no fill launch of its own. */
-int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, const float* w3, const float* wfc,
-                         float* wpd2, uint16_t* q1, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
-                         uint16_t* qfc_fwd, uint16_t* qfc_dgrad, const float* wh, uint16_t* qh_fwd,
-                         uint16_t* qh_dgrad, uint32_t* zero, int64_t zero_words, void* stream);
+int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                         const float* b3, const float* wfc, float* wpd2, uint16_t* q1, uint16_t* q2, uint16_t* q3,
+                         uint16_t* qd2, uint16_t* qd3, uint16_t* qfc_fwd, uint16_t* qfc_dgrad, const float* wh,
+                         uint16_t* qh_fwd, uint16_t* qh_dgrad, uint32_t* zero, int64_t zero_words, void* stream);
 /* conv1 -> conv2 on H1P, the split-f16 operand form of conv1's output h1 (Conv2d(4, 32, 8, 4) + ReLU
  * of models-checkpoint.py:52-53): per pixel (NHWC) its 32 channels' high f16 plane then their low
  * plane, h1 * 2^E = hi + lo (128 B per pixel, the size of the f32 form), E derived by
@@ -318,11 +321,26 @@ int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, cons
  *                      im2col), slabs in the workspace (ppox_nature_conv2_wgrad_planes_workspace_bytes)
  *                      summed in a fixed order.  Replaces the Conv2d weight / bias autograd of
  *                      models-checkpoint.py:54 in the training backward of ppo.py:241. */
+/* PX (round 4): the H1P form generalised to the trunk's other split operands.  An f32 tensor of
+ * NHWC rows is stored in the same bytes as, per aligned run of 32 elements, the 32 high f16 then
+ * the 32 low f16 of its values times 2^E (element e's halves at uint16 2 (e & ~31) + (e & 31) and
+ * + 32).  A producer writes its output this way (y_exp_out / g3_exp_out non-null: E from the bound
+ * amax(input) * max column l1-norm of its weights + max |bias|, stored to that int) and its
+ * consumers read the planes as they lie (x_exp / g_exp / h3_exp: the int holding E):
+ *   h2 — conv2 forward (conv2_fwd_planes, y_exp_out; amax_x = h1's slots) -> conv3 forward
+ *        (conv_fwd_split(3, x_exp)) and conv3 weight gradient (conv_wgrad_split(3, x_exp));
+ *   h3 — conv3 forward (conv_fwd_split(3, y_exp_out)) -> fc forward (fc_fwd[_splitk], h3_exp) and
+ *        fc weight gradient (fc_wgrad, h3_exp);
+ *   g3 — fc dgrad (fc_dgrad, g3_exp_out; relu_bits required) -> conv3 dgrad
+ *        (conv_dgrad_split(3, g_exp); relu_bits required) and conv3 weight gradient (g_exp).
+ * Null exponents select the f32 operands.  conv1_fwd_planes records h1's amax into amax_y
+ * (nullable): the start of h2's bound. */
 int ppox_nature_conv1_fwd_planes(const void* x, int64_t batch, const int64_t* idx, int64_t T, int64_t N_env,
                                  int64_t x_sample_stride, const uint16_t* wq1, const float* bias, uint16_t* h1p,
-                                 uint32_t* relu_bits, void* stream);
+                                 uint32_t* amax_y, uint32_t* relu_bits, void* stream);
 int ppox_nature_conv2_fwd_planes(const uint16_t* h1p, const uint16_t* q1, int64_t batch, const uint16_t* wq2,
-                                 const float* bias, float* y, uint32_t* amax_y, uint32_t* relu_bits, void* stream);
+                                 const float* bias, float* y, const uint32_t* amax_x, uint32_t* amax_y,
+                                 uint32_t* relu_bits, int* y_exp_out, void* stream);
 int64_t ppox_nature_conv2_wgrad_planes_workspace_bytes(int64_t batch);
 int ppox_nature_conv2_wgrad_planes(const uint16_t* h1p, const uint16_t* q1, int64_t batch, const float* grad_out,
                                    void* workspace, int64_t workspace_bytes, float* dw, float* db,
@@ -355,9 +373,10 @@ int ppox_head_hidden_wgrad(const float* de, int64_t rows, const float* f, void* 
                            float* dw, const uint32_t* amax_de, const uint32_t* amax_f, void* stream);
 int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_dgrad, void* stream);
 int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
-                       const uint32_t* amax_h3, uint32_t* amax_f, void* stream);
+                       const uint32_t* amax_h3, uint32_t* amax_f, const int* h3_exp, void* stream);
 int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
-                         const uint32_t* amax_df, uint32_t* amax_g3, const uint32_t* relu_bits, void* stream);
+                         const uint32_t* amax_df, uint32_t* amax_g3, const uint32_t* relu_bits, int* g3_exp_out,
+                         void* stream);
 /* fc forward (as ppox_nature_fc_fwd) split over K for small batches: 2-8 K-ranges per (128-row
  * tile, 64-column block) so the grid fills the chip, partial products into the workspace
  * (ppox_nature_fc_fwd_splitk_workspace_bytes(batch)), then one fixed-order reduce adding the
@@ -369,7 +388,7 @@ int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch);
 int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias,
                               void* workspace, int64_t workspace_bytes, float* f, const uint32_t* amax_h3,
                               uint32_t* amax_f, const float* w_actor, const float* b_actor, int32_t n_actions,
-                              float* logits, void* stream);
+                              float* logits, const int* h3_exp, void* stream);
 /* fc weight gradient dW (512 x 3136, the weight's Flatten order) = df^T @ h3 over the batch,
  * split-f16 (fp32-class; amax_df, amax_h3: the operands' slots), deterministic: df (batch, 512) is dL/df already ReLU-masked, h3 the
  * NHWC (batch, 7, 7, 64) conv3 output of the split forward.  Replaces the library GEMM of
@@ -378,7 +397,7 @@ int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_
 int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch);
 int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float* h3, void* workspace,
                          int64_t workspace_bytes, float* dw, const uint32_t* amax_df, const uint32_t* amax_h3,
-                         void* stream);
+                         const int* h3_exp, void* stream);
 
 /* ES-NSRA (evolution_strategies.py:103-384, csrc/es.hip), float64 throughout.
  * ppox_es_noise: eps[p][j] ~ N(0,1) for members member0..member0+P-1 of a generation
@@ -471,14 +490,15 @@ int ppox_nature_pack_split(const float* w1, const float* w2, const float* w3, ui
 int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx,
                                int64_t T, int64_t N_env, int64_t x_sample_stride,
                                const uint16_t* wq, const float* bias, float* y, const uint32_t* amax_x,
-                               uint32_t* amax_y, uint32_t* relu_bits, void* stream);
+                               uint32_t* amax_y, uint32_t* relu_bits, const int* x_exp, int* y_exp_out,
+                               void* stream);
 /* dgrad (as ppox_nature_conv_dgrad) of conv2/conv3 with split weights (which = 12, 13);
  * amax_g: grad_out's slots, amax_out: grad_in's (nullable).  The ReLU mask of the layer below
  * comes from relu_bits (that layer's split forward's bitmask) when non-null, else from prev_act. */
 int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch,
                                  const uint16_t* wqd, const float* prev_act, float* grad_in,
                                  const uint32_t* amax_g, uint32_t* amax_out, const uint32_t* relu_bits,
-                                 void* stream);
+                                 const int* g_exp, void* stream);
 /* dW [co][ci][ky][kx] and db (as ppox_nature_conv_wgrad + ppox_nature_wgrad_reduce, in one
  * call): split-K slabs into a workspace of ppox_nature_wgrad_split_workspace_bytes(layer,
  * batch), reduced in a fixed order (deterministic).  x: u8 frames (layer 1, samples
@@ -488,7 +508,7 @@ int64_t ppox_nature_wgrad_split_workspace_bytes(int32_t layer, int64_t batch);
 int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_t batch,
                                  int64_t x_sample_stride, const float* grad_out, void* workspace,
                                  int64_t workspace_bytes, float* dw, float* db, const uint32_t* amax_x,
-                                 const uint32_t* amax_g, void* stream);
+                                 const uint32_t* amax_g, const int* x_exp, const int* g_exp, void* stream);
 
 /* conv1 split wgrad with the minibatch gather fused: sample n is env-major row idx[n]
  * (i = env * T + step) of the step-major (T, N_env, 4, 84, 84) uint8 rollout frames x.

@@ -62,24 +62,39 @@ HEAD_FWD_SPLITK = os.environ.get("PPOX_HEAD_FWD_SPLITK", "1") == "1"
 RELU_BITS = os.environ.get("PPOX_RELU_BITS", "1") != "0"
 
 # rows of a pass's amax table (native.amax_table): the split-f16 operands of the trunk and the
-# heads' hidden layer, each recorded by the kernel that produces it and read by its consumers
-AM_H1, AM_H2, AM_H3, AM_DF, AM_G3, AM_G2, AM_G1, AM_F, AM_DE = range(9)
+# heads' hidden layer, each recorded by the kernel that produces it and read by its consumers;
+# row AM_EXP holds the exponents of the pass's PX tensors (slots EX_*)
+AM_H1, AM_H2, AM_H3, AM_DF, AM_G3, AM_G2, AM_G1, AM_F, AM_DE, AM_EXP = range(10)
 AM_ROWS = 10
+EX_H2, EX_H3, EX_G3 = range(3)
+
+# PX (round 4, include/ppox.h): in split math the trunk's other split operands are stored as their
+# two f16 planes too — h2 (written by the conv2 forward, read by the conv3 forward and weight
+# gradient), h3 (conv3 forward -> fc forward and fc weight gradient) and g3 (fc dgrad -> conv3
+# dgrad and weight gradient) — at exponents derived from bounds, so no consumer splits in
+# registers.  PPOX_PX=0: f32 tensors (split in the consumers).  Needs the ReLU bitmasks (the
+# dgrads' masks cannot come from planes).
+PX = os.environ.get("PPOX_PX", "1") != "0"
 
 
 class PassState:
-    """Side data of one trunk pass for the split kernels: the amax table (pass[AM_*] is its row)
-    and the ReLU bitmasks of the three conv outputs (bits[l - 1] for layer l: int32 words per
+    """Side data of one trunk pass for the split kernels: the amax table (pass[AM_*] is its row),
+    the ReLU bitmasks of the three conv outputs (bits[l - 1] for layer l: int32 words per
     output pixel, bit c % 32 of word c / 32 = channel c > 0; None unless that split forward wrote
-    it), which the next layer's dgrad reads instead of the f32 activations."""
+    it), which the next layer's dgrad reads instead of the f32 activations, and which of h2, h3,
+    g3 the pass holds as PX planes (px[EX_*]; their exponents: exp(EX_*))."""
 
-    __slots__ = ("amax", "bits")
+    __slots__ = ("amax", "bits", "px")
 
-    def __init__(self, amax, bits=(None, None, None)):
-        self.amax, self.bits = amax, bits
+    def __init__(self, amax, bits=(None, None, None), px=(False, False, False)):
+        self.amax, self.bits, self.px = amax, bits, list(px)
 
     def __getitem__(self, row):
         return self.amax[row]
+
+    def exp(self, which):
+        """the int32 element holding PX tensor `which`'s exponent, or None when it is f32"""
+        return self.amax[AM_EXP, which:which + 1] if self.px[which] else None
 
 
 # backward on two streams: each layer's weight gradient runs on a side stream beside the
@@ -177,7 +192,7 @@ class _NatureTrunk(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, convs, w1, b1, w2, b2, w3, b3):
-        h1, h2, h3, am = convs.forward_acts(x, train=True)
+        h1, h2, h3, am = convs.forward_acts(x, train=True, px=False)  # (h3 is returned to autograd as f32)
         ctx.convs, ctx.am = convs, am
         ctx.save_for_backward(x, h1, h2, h3)
         return h3.permute(0, 3, 1, 2) if convs.nhwc3 else h3
@@ -240,6 +255,8 @@ class NatureConvs:
         # pixel: csrc/conv_common.h) — written split by the conv1 forward at a scale derived from the
         # weights, read as it lies by the conv2 forward and the direct conv2 weight gradient
         self.h1p = self.math != "f32"
+        # PX planes for h2 / h3 / g3 (see PX above) where the pass's ops all run split
+        self.px = self.h1p and PX and RELU_BITS
         self._ws = {}
         self._version = None
         self._packed = set()
@@ -283,6 +300,18 @@ class NatureConvs:
         if self.h1p:
             return torch.empty((B, 20, 20, 64), dtype=torch.int16, device=device)
         return torch.empty((B, 20, 20, 32), device=device)
+
+    def px_h3(self, B, train):
+        """h3 as PX planes in a B-row pass: its consumers (the fc forward, and in training the fc weight
+        gradient and the fused fc dgrad reading h3's bitmask) all run the split kernels"""
+        return self.px and B >= FC_SPLIT_MIN_BATCH and (
+            not train or (B >= FC_WGRAD_SPLIT_MIN_BATCH and B < FC_DGRAD_FUSED_MAX_BATCH))
+
+    def px_g3(self, B, am):
+        """g3 as PX planes: the fc dgrad is the fused split kernel with h3's bitmask, the conv3 dgrad runs
+        split with conv2's bitmask"""
+        return (self.px and isinstance(am, PassState) and am.bits[2] is not None and am.bits[1] is not None
+                and B < FC_DGRAD_FUSED_MAX_BATCH and self.uses_split("dgrad", 3, B) and self.uses_split("wgrad", 3))
 
     def workspace(self, layer, batch, split=False):
         if split and layer == 2 and self.h1p:
@@ -343,7 +372,7 @@ class NatureConvs:
             native.nature_pack_all(w1, w2, w3, self.fc.weight, pick("wpd2", self.wpd2), pick("q1", q[1]),
                                    pick("q2", q[2]), pick("q3", q[3]), pick("qd2", q[12]), pick("qd3", q[13]),
                                    pick("qfcf", qfc[0]), pick("qfcd", qfc[1]), self.hid.weight, pick("qhf", qh[0]),
-                                   pick("qhd", qh[1]), b1=self.c1.bias, zero=zero)
+                                   pick("qhd", qh[1]), b1=self.c1.bias, zero=zero, b2=self.c2.bias, b3=self.c3.bias)
             zeroed = zero is not None
         if "wfc_nhwc" in missing:
             torch.index_select(self.fc.weight.detach(), 1, self.fc_perm, out=self.wfc_nhwc)
@@ -362,22 +391,28 @@ class NatureConvs:
         stride = 4 * 84 * 84 if layer == 1 else 0
         out_am = am[AM_H1 + layer - 1] if self.math != "f32" else None
         bits = am.bits[layer - 1] if isinstance(am, PassState) else None
+        px = am.px if isinstance(am, PassState) else (False, False, False)
+        # conv1 records h1's amax for the bound of a PX h2
+        h1_am = out_am if layer == 1 and px[EX_H2] else None
         if isinstance(x, RolloutRows):
             assert layer == 1 and self.uses_split("fwd", 1)
             if self.h1p:
-                native.nature_conv1_fwd_planes(x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y, relu_bits=bits)
+                native.nature_conv1_fwd_planes(x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y, relu_bits=bits,
+                                               amax_y=h1_am)
             else:
                 native.nature_conv_fwd_split(1, x.frames, B, x.idx, x.T, x.N, 0, self.q[1], bias, y, amax_y=out_am,
                                              relu_bits=bits)
             return
         if self.h1p and layer == 1:
-            native.nature_conv1_fwd_planes(x, B, None, 0, 0, stride, self.q[1], bias, y, relu_bits=bits)
+            native.nature_conv1_fwd_planes(x, B, None, 0, 0, stride, self.q[1], bias, y, relu_bits=bits, amax_y=h1_am)
         elif self.h1p and layer == 2:
-            native.nature_conv2_fwd_planes(x, self.q[1], B, self.q[2], bias, y, amax_y=out_am, relu_bits=bits)
+            native.nature_conv2_fwd_planes(x, self.q[1], B, self.q[2], bias, y, amax_y=out_am, relu_bits=bits,
+                                           amax_x=am[AM_H1] if px[EX_H2] else None, y_exp=am.exp(EX_H2) if px[EX_H2] else None)
         elif self.uses_split("fwd", layer):
             native.nature_conv_fwd_split(layer, x, B, None, 0, 0, stride, self.q[layer], bias, y,
                                          amax_x=am[AM_H1 + layer - 2] if layer > 1 else None, amax_y=out_am,
-                                         relu_bits=bits)
+                                         relu_bits=bits, x_exp=am.exp(EX_H2) if layer == 3 and px[EX_H2] else None,
+                                         y_exp=am.exp(EX_H3) if layer == 3 and px[EX_H3] else None)
         else:
             wp = (self.wp1, self.wp2, self.wp3)[layer - 1]
             native.nature_conv_fwd(layer, x, B, None, 0, 0, stride, wp, bias, y)
@@ -391,8 +426,9 @@ class NatureConvs:
             bits = am.bits[layer - 2] if isinstance(am, PassState) else None
             if layer == 2 and self.h1p and bits is None:
                 raise ValueError("conv2 dgrad on H1P needs conv1's ReLU bitmask (a training pass's PassState)")
+            g_exp = am.exp(EX_G3) if layer == 3 and isinstance(am, PassState) else None
             native.nature_conv_dgrad_split(layer, g, B, self.q[10 + layer], prev_act, out, amax_g=g_am,
-                                           amax_out=out_am, relu_bits=bits)
+                                           amax_out=out_am, relu_bits=bits, g_exp=g_exp)
         else:
             if layer == 2 and self.h1p:
                 raise ValueError("the f32 conv2 dgrad needs f32 activations; split math keeps h1 as H1P")
@@ -412,27 +448,34 @@ class NatureConvs:
             native.nature_conv2_wgrad_planes(x, self.q[1], B, g, self.workspace(2, B, True), dw, db, amax_g=g_am,
                                              stream=stream)
         elif self.uses_split("wgrad", layer):
+            px = layer == 3 and isinstance(am, PassState)
             native.nature_conv_wgrad_split(layer, x, B, stride, g, self.workspace(layer, B, True), dw, db,
                                            amax_x=am[AM_H1 + layer - 2] if layer > 1 else None, amax_g=g_am,
+                                           x_exp=am.exp(EX_H2) if px else None, g_exp=am.exp(EX_G3) if px else None,
                                            stream=stream)
         else:
             native.nature_conv_wgrad(layer, x, B, None, 0, 0, stride, g, self.workspace(layer, B), dw, db, stream=stream)
 
-    def forward_acts(self, x, train=False):
+    def forward_acts(self, x, train=False, px=None):
         """Trunk forward: (h1 NHWC, h2 NHWC, h3, am) — activations (ReLU applied) and the pass's
         PassState (the amax table's AM_* rows — the backward of the same pass records its
         gradients' rows — and, for a `train` pass, conv1's ReLU bitmask); h3 is
-        NHWC (B, 7, 7, 64) in split math (self.nhwc3), NCHW (B, 64, 7, 7) in f32 math."""
+        NHWC (B, 7, 7, 64) in split math (self.nhwc3), NCHW (B, 64, 7, 7) in f32 math.  px (default
+        self.px): h2 / h3 as PX planes (int16 (B, 9, 9, 128) / (B, 7, 7, 128)) where their consumers
+        allow; am.px says which."""
         B = x.shape[0]
         dev = x.device
+        px = self.px if px is None else (px and self.px)
         # the pass's amax table: zeroed by the weight packing when this pass runs it (the first
         # pass after an optimizer step), by a fill otherwise
         table = torch.empty((AM_ROWS, native.AMAX_SLOTS), dtype=torch.int32, device=dev)
         if not self.pack(B, zero=table):
             table.zero_()
         h1 = self.empty_h1(B, dev)
-        h2 = torch.empty((B, 9, 9, 64), device=dev)
-        h3 = torch.empty((B, 7, 7, 64) if self.nhwc3 else (B, 64, 7, 7), device=dev)
+        px2, px3 = px, px and self.px_h3(B, train)
+        h2 = torch.empty((B, 9, 9, 128), dtype=torch.int16, device=dev) if px2 else torch.empty((B, 9, 9, 64), device=dev)
+        h3 = (torch.empty((B, 7, 7, 128), dtype=torch.int16, device=dev) if px3 else
+              torch.empty((B, 7, 7, 64) if self.nhwc3 else (B, 64, 7, 7), device=dev))
         # the conv outputs' ReLU bitmasks where the forward and the consumer of the mask (the next
         # layer's dgrad; for conv3 the fc dgrad) both run split (training passes)
         consumer = (self.uses_split("dgrad", 2, B), self.uses_split("dgrad", 3, B),
@@ -442,7 +485,7 @@ class NatureConvs:
                      if train and (RELU_BITS or (L == 1 and self.h1p)) and self.uses_split("fwd", L) and
                      consumer[L - 1] else None
                      for L, P, C in ((1, 400, 32), (2, 81, 64), (3, 49, 64)))
-        am = PassState(table, bits)
+        am = PassState(table, bits, (px2, px3, False))
         if B:
             self.fwd(1, x, B, self.c1.bias, h1, am)
             self.fwd(2, h1, B, self.c2.bias, h2, am)
@@ -459,8 +502,12 @@ class NatureConvs:
         self.pack(h3.shape[0])
         B = h3.shape[0]
         logits = None
+        h3_exp = am.exp(EX_H3) if isinstance(am, PassState) else None
         if B < FC_SPLIT_MIN_BATCH:
+            assert h3_exp is None, "PX h3 feeds the split fc kernels only"
             f = torch._addmm_activation(self.fc.bias, h3.view(B, -1), self.wfc_nhwc.t())  # bias+ReLU fused
+            if am is not None:  # f's amax for the heads' split hidden layer (ppox_head_hidden_fwd*)
+                native.amax(f, am[AM_F])
             return f if actor is None else (f, logits)
         f = torch.empty((B, 512), device=h3.device)
         if B < FC_SPLITK_MAX_BATCH:
@@ -474,18 +521,26 @@ class NatureConvs:
             if actor is not None and actor[0].shape[0] <= 8 and actor[0].is_contiguous() and actor[0].data_ptr() % 16 == 0:
                 logits = torch.empty((B, actor[0].shape[0]), device=h3.device)
             native.nature_fc_fwd_splitk(h3, B, self.qfc[0], self.fc.bias, ws, f, amax_h3=am[AM_H3], amax_f=am[AM_F],
-                                        actor=actor if logits is not None else None, logits=logits)
+                                        actor=actor if logits is not None else None, logits=logits, h3_exp=h3_exp)
         else:
-            native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f, amax_h3=am[AM_H3], amax_f=am[AM_F])
+            native.nature_fc_fwd(h3, B, self.qfc[0], self.fc.bias, f, amax_h3=am[AM_H3], amax_f=am[AM_F],
+                                 h3_exp=h3_exp)
         return f if actor is None else (f, logits)
 
     def fc_dgrad_g3(self, df, h3, am):
         """g3 (B, 7, 7, 64) NHWC = (df @ W) * (h3 > 0), df = dL/df after the fc ReLU (its amax in
         am[AM_DF]), h3 NHWC; records g3's amax."""
         B = df.shape[0]
-        g3 = torch.empty((B, 7, 7, 64), device=df.device)
-        native.nature_fc_dgrad(df.contiguous(), B, self.qfc[1], h3, g3, amax_df=am[AM_DF], amax_g3=am[AM_G3],
-                               relu_bits=am.bits[2] if isinstance(am, PassState) else None)
+        px = self.px_g3(B, am)
+        if px:  # g3 as PX planes for the conv3 dgrad and weight gradient
+            am.px[EX_G3] = True
+            g3 = torch.empty((B, 7, 7, 128), dtype=torch.int16, device=df.device)
+        else:
+            g3 = torch.empty((B, 7, 7, 64), device=df.device)
+        ps = isinstance(am, PassState)
+        native.nature_fc_dgrad(df.contiguous(), B, self.qfc[1], h3 if not (ps and am.px[EX_H3]) else None, g3,
+                               amax_df=am[AM_DF], amax_g3=am[AM_G3], relu_bits=am.bits[2] if ps else None,
+                               g3_exp=am.exp(EX_G3) if px else None)
         return g3
 
     def backward_acts(self, x, h1, h2, h3, dh3, dw1, db1, dw2, db2, dw3, db3, g3=None, am=None):

@@ -121,6 +121,7 @@ template <class L, bool OUT_NCHW, int MT_>
 struct FwdBase {
     static constexpr int NOUT = L::COUT, MT = MT_, BMR = 128 * MT;
     static constexpr bool A_PLANES = false;  // sg2: A rows are f32 (split in registers), not H1P planes
+    static constexpr bool PLANES_OUT = false;  // sg2: the output as PX planes (Px<> below)
     using Tile = RowTile;
     __device__ static bool tile(const Args& a, Tile& t) {
         t.m0 = (long long)blockIdx.x * BMR;
@@ -143,6 +144,14 @@ struct FwdBase {
             a.y[m * L::COUT + co] = v;
         }
         return v;
+    }
+    // PX epilogue (NHWC output): the value (0 past the end) and its f32-layout element index (-1: none)
+    __device__ static float value(const Args&, const Tile& t, int row, int, float acc, float bias) {
+        return t.m0 + row < t.M ? fmaxf(acc + bias, 0.f) : 0.f;
+    }
+    __device__ static long long out_elem(const Args&, const Tile& t, int row, int co) {
+        const long long m = t.m0 + row;
+        return m < t.M ? m * L::COUT + co : -1;
     }
 };
 
@@ -199,6 +208,7 @@ template <class L, int MT_>
 struct DgradPMProblem {
     static constexpr int NOUT = L::CIN, MT = MT_, BMR = 128 * MT, NPOS = L::IH * L::IW, CPT = L::COUT / BK;
     static constexpr bool A_PLANES = false;
+    static constexpr bool PLANES_OUT = false;
     using Tile = PixelTile;
     using Stager = StageDgradPM<L, MT>;
     __device__ static bool tile(const Args& a, Tile& t) {
@@ -237,6 +247,13 @@ struct DgradPMProblem {
         const float v = m > 0.f ? acc : 0.f;
         a.y[(n * NPOS + t.pos) * L::CIN + ci] = v;
         return v;
+    }
+    __device__ static float value(const Args& a, const Tile& t, int row, int, float acc, float m) {
+        return t.n0 + row < a.batch && m > 0.f ? acc : 0.f;
+    }
+    __device__ static long long out_elem(const Args& a, const Tile& t, int row, int ci) {
+        const long long n = t.n0 + row;
+        return n < a.batch ? (n * NPOS + t.pos) * L::CIN + ci : -1;
     }
 };
 
@@ -408,6 +425,7 @@ struct GemmRowsProblem {
     static constexpr int K = K_, N = N_, NOUT = NB, MT = 1, BMR = 128, NCB = (N + NB - 1) / NB, KC = K / BK;
     static constexpr bool LATE_EPILOGUE = true;
     static constexpr bool A_PLANES = false;
+    static constexpr bool PLANES_OUT = false;
     static_assert(K % BK == 0, "K multiple of 32");
     using Tile = GemmTile;
     using Stager = StageGemmRows<K>;
@@ -450,6 +468,23 @@ struct GemmRowsProblem {
         a.y[m * N + n] = v;
         return v;
     }
+    // PX epilogue: the fc dgrad's masked g3 (FC_DGRAD only)
+    __device__ static float value(const Args&, const Tile& t, int row, int col, float acc, float e) {
+        static_assert(MODE == FC_DGRAD, "PX output: the fc dgrad");
+        return t.m0 + row < t.M && t.cb * NB + col < N && e > 0.f ? acc : 0.f;
+    }
+    __device__ static long long out_elem(const Args&, const Tile& t, int row, int col) {
+        const long long m = t.m0 + row;
+        const int n = t.cb * NB + col;
+        return m < t.M && n < N ? m * N + n : -1;
+    }
+};
+
+// a Problem with PX operands: A rows as f16 planes (a.xexp; no split in registers) and / or the
+// output written as planes at a bound-derived exponent (a.yexp_out, conv_common.h)
+template <class Base, bool AP, bool PO = false>
+struct Px : Base {
+    static constexpr bool A_PLANES = AP, PLANES_OUT = PO;
 };
 
 #ifndef FC_FWD_G
@@ -823,6 +858,16 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
     // multiplies by both inverses
     const int ex = Prob::A_PLANES ? *a.xexp : split_scale_exp(amax_read(a.amax_x)), ew = *a.wexp;
     const float sa = exp2i(ex), ua = exp2i(-ex), uw = exp2i(-ew);
+    // PX output: its exponent from the bound amax(x) * max column norm + max |bias| (every workgroup
+    // derives the same; workgroup 0 publishes it).  A non-finite bound makes the output NaN (loud).
+    float sy = 1.f;
+    if constexpr (Prob::PLANES_OUT) {
+        const uint32_t am = amax_read(a.amax_x), nm = amax_read(a.ynorm), bm = *a.ybias;
+        const int ey = bound_exp(am, nm, bm);
+        const float bnd = __uint_as_float(am) * __uint_as_float(nm) + __uint_as_float(bm);
+        sy = __builtin_isfinite(bnd) ? exp2i(ey) : __builtin_nanf("");
+        if (blockIdx.x == 0 && threadIdx.x == 0) *a.yexp_out = ey;
+    }
     // chunk c into ring slot S; the chunk index is clamped, not branched on (past the end:
     // the last chunk again, never read)
     auto issue = [&](int c, auto S) {
@@ -953,8 +998,18 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
         __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            const float v = Prob::store_pre(a, t, wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, j * 32 + r,
-                                            (hi[j][q] + lo[j][q]) * ua * uw, e[q]);
+            const int row = wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h, col = j * 32 + r;
+            float v;
+            if constexpr (Prob::PLANES_OUT) {
+                // every lane runs the pair swap; the pair (col & ~1, col | 1) shares its row, so both
+                // lanes store or neither does
+                v = Prob::value(a, t, row, col, (hi[j][q] + lo[j][q]) * ua * uw, e[q]);
+                const uint32_t w = px_pair_word(v * sy, lane & 1);
+                const long long el = Prob::out_elem(a, t, row, col & ~1);
+                if (el >= 0) *reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(a.y) + px_index(el) + 32 * (lane & 1)) = w;
+            } else {
+                v = Prob::store_pre(a, t, row, col, (hi[j][q] + lo[j][q]) * ua * uw, e[q]);
+            }
             om = fmaxf(om, fabsf(v));
             if constexpr (Prob::BITS_OUT) {
                 if (a.bits_y) {  // uniform
@@ -1271,13 +1326,14 @@ struct ActorHead {
 
 // K = 3136: the fc layer (reduce: + bias, ReLU, f's amax, the actor head); K = 512: the heads' hidden
 // layer (the same reduce with the critic head Linear(512, 1) fused, no amax)
-template <int K, int S>
+template <int K, int S, bool AP = false>
 int launch_fc_fwd_sk(const Args& a, const uint16_t* q, float* slab, const float* bias, float* f, const ActorHead& act,
                      hipStream_t st, const char* name = "ppox_nature_fc_fwd_splitk") {
     Args b = a;
     b.y = slab;
     b.amax_y = nullptr;  // partial products: f's amax is recorded by the reduce
-    const int rc = launch_sgemm<SgRowsSK<K, 512, S>>(b, q, ppox::ceil_div(a.batch, SG_ROWS) * FcFwd::NCB * S, st, name);
+    const int rc = launch_sgemm<Px<SgRowsSK<K, 512, S>, AP>>(b, q, ppox::ceil_div(a.batch, SG_ROWS) * FcFwd::NCB * S,
+                                                             st, name);
     if (rc != PPOX_OK) return rc;
     const float4* sl = reinterpret_cast<const float4*>(slab);
     float4* f4 = reinterpret_cast<float4*>(f);
@@ -1744,9 +1800,12 @@ __device__ float kZeroG[64] = {};  // the G row of a pixel past a split's end (g
 // workgroup owns one block — the fc layer's weight gradient (K = the 512 outputs,
 // G = the NHWC conv3 activations, one 64-channel pixel per block); its grid is any
 // number of (split, column-block, k-block) items, k-block fastest within an XCD.
-template <class L, bool U8, int KT, bool ROWS, int CB = 1>
+// XPL / GPL (round 4): X / G are PX planes (conv_common.h; a.xexp / a.gexp): each unit's 8 values
+// are read as their two 16-B plane runs and stored to LDS as they are (no split in registers)
+template <class L, bool U8, int KT, bool ROWS, int CB = 1, bool XPL = false, bool GPL = false>
 __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     using C = WsCfg<L, U8, KT>;
+    static_assert(!(XPL && U8) && (!GPL || C::GW == 8), "PX operands: f32 X, 8 G values per thread");
     constexpr int COUT = L::COUT, XP = C::XP, XR = C::XR, GR = C::GR, XU = C::XU;
     constexpr int WKT = C::WKT, WCT = C::WCT, GS = CB * COUT;
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * C::STAGE];
@@ -1795,8 +1854,10 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         uint2 g4[NPL];
     };
     // operand scales from the amax slots (uint8 X: exact at scale 1); the slab is unscaled
-    const int ex = U8 ? 0 : split_scale_exp(amax_read(a.amax_x)), eg = split_scale_exp(amax_read(a.amax_g));
+    const int ex = U8 ? 0 : (XPL ? *a.xexp : split_scale_exp(amax_read(a.amax_x)));
+    const int eg = GPL ? *a.gexp : split_scale_exp(amax_read(a.amax_g));
     const float sx = exp2i(ex), sg = exp2i(eg), uo = exp2i(-ex) * exp2i(-eg);
+    const float ub = GPL ? exp2i(-eg) : 1.f;  // GPL: the bias sums add the scaled values
     Raw raw[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {  // defined values: the last step splits a set it never stores
@@ -1868,6 +1929,15 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
                 r.xw[i][0] = *reinterpret_cast<const uint32_t*>(s + koff[i]);
                 r.xw[i][1] = *reinterpret_cast<const uint32_t*>(s + koff[i] + 4);
             }
+        } else if constexpr (XPL) {
+            // the unit's 8 channels lie in one 32-group: its high plane run, and 64 B on its low one
+            const char* s = reinterpret_cast<const char*>(xf) + 4 * (s0 + (oy * L::S * L::IW + ox * L::S) * L::CIN);
+#pragma unroll
+            for (int i = 0; i < XU; ++i) {
+                const char* q = s + 4 * (koff[i] & ~31) + 2 * (koff[i] & 31);
+                r.xr[i][0] = *reinterpret_cast<const float4*>(q);
+                r.xr[i][1] = *reinterpret_cast<const float4*>(q + 64);
+            }
         } else {
             const float* s = xf + s0 + (oy * L::S * L::IW + ox * L::S) * L::CIN;
 #pragma unroll
@@ -1876,9 +1946,17 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
                 r.xr[i][1] = *reinterpret_cast<const float4*>(s + koff[i] + 4);
             }
         }
-        const float* sg = ok ? a.g + (unsigned long long)mcur * GS + cb * COUT + gco : kZeroG + gco;
-        r.gr[0] = *reinterpret_cast<const float4*>(sg);
-        if constexpr (GW == 8) r.gr[1] = *reinterpret_cast<const float4*>(sg + 4);
+        if constexpr (GPL) {
+            const unsigned long long ge = (unsigned long long)mcur * GS + cb * COUT + gco;  // gco % 8 == 0
+            const char* q = ok ? reinterpret_cast<const char*>(a.g) + 4 * (ge & ~31ULL) + 2 * (ge & 31)
+                               : reinterpret_cast<const char*>(kZeroG) + 4 * (gco & ~31) + 2 * (gco & 31);
+            r.gr[0] = *reinterpret_cast<const float4*>(q);
+            r.gr[1] = *reinterpret_cast<const float4*>(q + 64);
+        } else {
+            const float* sg = ok ? a.g + (unsigned long long)mcur * GS + cb * COUT + gco : kZeroG + gco;
+            r.gr[0] = *reinterpret_cast<const float4*>(sg);
+            if constexpr (GW == 8) r.gr[1] = *reinterpret_cast<const float4*>(sg + 4);
+        }
         mcur += MS;
         if constexpr (L::P == 1) {  // one pixel per sample (the fc layer): sample = pixel
             sb = (unsigned long long)mcur * sstride;
@@ -1900,15 +1978,23 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
     auto to_planes = [&](const Raw& r, Planes& p) {
 #pragma unroll
         for (int i = 0; i < XU; ++i) {
-            if constexpr (U8)
+            if constexpr (U8) {
                 p.x[i][0] = u8x8_to_f16(r.xw[i][0], r.xw[i][1]);
-            else
+            } else if constexpr (XPL) {
+                p.x[i][0] = __builtin_bit_cast(u32x4, r.xr[i][0]);
+                p.x[i][1] = __builtin_bit_cast(u32x4, r.xr[i][1]);
+            } else {
                 split8h(r.xr[i][0], r.xr[i][1], sx, p.x[i][0], p.x[i][1]);
+            }
         }
-        if constexpr (GW == 8)
+        if constexpr (GPL) {
+            p.g[0] = __builtin_bit_cast(u32x4, r.gr[0]);
+            p.g[1] = __builtin_bit_cast(u32x4, r.gr[1]);
+        } else if constexpr (GW == 8) {
             split8h(r.gr[0], r.gr[1], sg, p.g[0], p.g[1]);
-        else
+        } else {
             split4h(r.gr[0], sg, p.g4[0], p.g4[1]);
+        }
     };
     auto store = [&](const Planes& p, const Raw& r, int buf) {
         uint8_t* base = lds + buf * C::STAGE;
@@ -1928,15 +2014,23 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
             else
                 *reinterpret_cast<uint2*>(gb + q * C::GPB + goff) = p.g4[q];
         }
-        bsum[0] += r.gr[0].x;
-        bsum[1] += r.gr[0].y;
-        bsum[2] += r.gr[0].z;
-        bsum[3] += r.gr[0].w;
-        if constexpr (GW == 8) {
-            bsum[4] += r.gr[1].x;
-            bsum[5] += r.gr[1].y;
-            bsum[6] += r.gr[1].z;
-            bsum[7] += r.gr[1].w;
+        if constexpr (GPL) {
+            if constexpr (CB == 1) {  // the bias gradient (the fc layer has none here): hi + lo, scaled
+                const u32x4 hw = p.g[0], lw = p.g[1];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bsum[e] += px_value(hw[e >> 1], lw[e >> 1], e & 1);
+            }
+        } else {
+            bsum[0] += r.gr[0].x;
+            bsum[1] += r.gr[0].y;
+            bsum[2] += r.gr[0].z;
+            bsum[3] += r.gr[0].w;
+            if constexpr (GW == 8) {
+                bsum[4] += r.gr[1].x;
+                bsum[5] += r.gr[1].y;
+                bsum[6] += r.gr[1].z;
+                bsum[7] += r.gr[1].w;
+            }
         }
     };
     // per-lane transposed-read offsets (T10): lane 4qq+pp of each 16-lane group supplies
@@ -2033,7 +2127,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_split_kernel(WArgs a) {
         if (tid < COUT) {
             float t = 0.f;
             for (int g = 0; g < MS; ++g) t += bred[g * COUT + tid];
-            a.bslab[(long long)split * COUT + tid] = t;
+            a.bslab[(long long)split * COUT + tid] = t * ub;
         }
     }
 }
@@ -2689,7 +2783,7 @@ int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float
 #define WS_FILL 512  // split wgrad: workgroups at least (conv1 / conv2, small batches)
 #endif
 // split wgrad: its own split-K count (~WS_PX pixels per split so the grid fills the chip)
-template <class L, bool U8, int KT>
+template <class L, bool U8, int KT, bool XPL = false, bool GPL = false>
 struct WsLaunch {
     using C = WsCfg<L, U8, KT>;
     static long long splits(long long batch) {
@@ -2712,17 +2806,20 @@ struct WsLaunch {
     }
     static int run(const void* x, long long sample_stride, const float* g, long long batch, void* ws, float* dw,
                    float* db, const uint32_t* amax_x, const uint32_t* amax_g, hipStream_t s,
-                   const long long* idx = nullptr, long long T = 0, long long Nenv = 0) {
+                   const long long* idx = nullptr, long long T = 0, long long Nenv = 0, const int* xexp = nullptr,
+                   const int* gexp = nullptr) {
         const int sp = (int)splits(batch);
         float* slab = reinterpret_cast<float*>(ws);
         WArgs wa{x, sample_stride, g, slab, slab + (long long)sp * L::K * L::COUT, batch, 0, sp, idx, T, Nenv,
                  amax_x, amax_g};
+        wa.xexp = xexp;
+        wa.gexp = gexp;
         const long long M = batch * L::P;
         wa.px_per_split = ppox::ceil_div(ppox::ceil_div(M, sp), MS) * MS;
         if (U8 && idx != nullptr)
             wgrad_split_kernel<L, U8, KT, U8><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
         else
-            wgrad_split_kernel<L, U8, KT, false><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
+            wgrad_split_kernel<L, U8, KT, false, 1, XPL, GPL><<<(unsigned)(C::KB * sp), 256, 0, s>>>(wa);
         PPOX_LAUNCHED_NORET("ppox_nature_conv_wgrad_split");
         return launch_wgrad_reduce<L, !U8>(slab, wa.bslab, sp, dw, db, s);
     }
@@ -2730,6 +2827,9 @@ struct WsLaunch {
 using Ws1 = WsLaunch<G1, true, 256>;
 using Ws2 = WsLaunch<G2, false, WS_KT2>;
 using Ws3 = WsLaunch<G3, false, WS_KT3>;
+using Ws3PP = WsLaunch<G3, false, WS_KT3, true, true>;  // PX h2 and g3
+using Ws3PF = WsLaunch<G3, false, WS_KT3, true, false>;
+using Ws3FP = WsLaunch<G3, false, WS_KT3, false, true>;
 // Every per-optimizer-step weight packing of the training step in two launches (the
 // minibatch loop is launch-bound at small per-rank batches): wmax_kernel (each weight
 // tensor's amax partials, into the tails of the forms packed from it), then pack_all_kernel
@@ -2744,6 +2844,7 @@ struct PackAll {
     const float* b1 = nullptr;                         // conv1 bias (with q1: the H1P exponent)
     uint32_t* zero = nullptr;                          // words zeroed by wmax_kernel (a pass's amax table)
     long long zero_words = 0;
+    const float *b2 = nullptr, *b3 = nullptr;          // conv2 / conv3 biases (with q2 / q3: the PX bounds)
 };
 constexpr long long PA_N1 = 8 * 2 * 64 * 8, PA_N2 = (long long)G2::K * G2::COUT, PA_N3 = (long long)G3::K * G3::COUT;
 constexpr long long PA_NFC = (long long)FcFwd::NCB * FcFwd::K * FcFwd::NOUT;
@@ -2866,13 +2967,81 @@ __device__ void h1p_exp_block(const float* __restrict__ w1, const float* __restr
     }
 }
 
+// The PX output bounds (round 4): column l1-norms sum_k |B[k][n]| of a packed form's matrix, their
+// maximum as AMAX_SLOTS partials in the form's tail (NORM_SLOT0; every slot written) and the bias
+// bound max |b| (BMAX_SLOT; NaN without a bias, so a PX output bounded without it comes out NaN).
+// Job 0: q2 (conv2 forward, n = co: W2[co][:], 512 contiguous), job 1: q3 (conv3 forward, 576),
+// job 2: qfcd (fc dgrad, n = a feature q: W[:][q] over the 512 outputs, 16 features per workgroup).
+// Fixed summation orders (f32; the bound's 2^-10 margin covers their rounding): deterministic.
+constexpr int PA_NORM_JOBS = 3;
+__device__ void norm_block(const PackAll& p, int job, int b) {
+    __shared__ float red[256];
+    const int t = threadIdx.x;
+    float colmax = 0.f;
+    if (job < 2) {
+        uint16_t* q = job == 0 ? p.q2 : p.q3;
+        if (!q) return;
+        const float* w = job == 0 ? p.w2 : p.w3;
+        const int K = job == 0 ? G2::K : G3::K;
+        const float* bias = job == 0 ? p.b2 : p.b3;
+        float sum = 0.f;
+        if (b < 64) {  // output channel b (COUT = 64): threads stride its K weights
+            for (int k = t; k < K; k += 256) sum += fabsf(w[b * K + k]);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);  // a fixed butterfly: deterministic
+        if ((t & 63) == 0) red[t >> 6] = sum;
+        __syncthreads();
+        if (t == 0) {
+            const float tot = (red[0] + red[1]) + (red[2] + red[3]);
+            uint32_t* tail = pack_tail(q, job == 0 ? PL_Q2 : PL_Q3);
+            tail[NORM_SLOT0 + b] = __float_as_uint(tot);
+            if (b == 0) {
+                float bm = bias ? 0.f : __builtin_nanf("");
+                if (bias)
+                    for (int i = 0; i < 64; ++i) bm = fmaxf(bm, fabsf(bias[i]));
+                tail[AMAX_SLOTS + BMAX_SLOT] = __float_as_uint(bm);
+            }
+        }
+        return;
+    }
+    if (!p.qfcd) return;
+    // features 16 b .. 16 b + 15 (b < 196): thread (part = t >> 4, f = t & 15) sums outputs 32 part ..
+    const int f = 16 * b + (t & 15), part = t >> 4;
+    float sum = 0.f;
+    if (f < 3136) {
+#pragma unroll 8
+        for (int k = 32 * part; k < 32 * part + 32; ++k) sum += fabsf(p.wfc[(long long)k * 3136 + f]);
+    }
+    red[t] = sum;
+    __syncthreads();
+    if (t < 16) {
+        float tot = 0.f;
+        for (int i = 0; i < 16; ++i) tot += red[16 * i + t];
+        colmax = tot;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) colmax = fmaxf(colmax, __shfl_xor(colmax, o, 16));
+        if (t == 0) {
+            uint32_t* tail = pack_tail(p.qfcd, PL_FCD);
+            tail[NORM_SLOT0 + b] = __float_as_uint(colmax);
+            if (b == 0) tail[AMAX_SLOTS + BMAX_SLOT] = 0u;  // the dgrad has no bias
+        }
+    }
+}
+
 // AMAX_SLOTS workgroups per weight tensor: workgroup b's max |w| over its stride into slot b of
 // the tails of both forms (every slot written: no zeroing), so the packer's amax_read sees the
-// tensor's max.  Then one workgroup for the H1P exponent (with q1 and b1), then the workgroups
-// zeroing p.zero (the next pass's amax table: no fill launch of its own)
+// tensor's max.  Then AMAX_SLOTS workgroups per PX norm job, one workgroup for the H1P exponent
+// (with q1 and b1), then the workgroups zeroing p.zero (the next pass's amax table: no fill launch
+// of its own)
 __global__ void __launch_bounds__(256) wmax_kernel(PackAll p) {
     if (blockIdx.x >= PA_TENSORS * AMAX_SLOTS) {
-        const long long zb = (long long)blockIdx.x - PA_TENSORS * AMAX_SLOTS - 1;
+        const int nb = (int)blockIdx.x - PA_TENSORS * AMAX_SLOTS;
+        if (nb < PA_NORM_JOBS * AMAX_SLOTS) {
+            norm_block(p, nb / AMAX_SLOTS, nb % AMAX_SLOTS);
+            return;
+        }
+        const long long zb = (long long)nb - PA_NORM_JOBS * AMAX_SLOTS - 1;
         if (zb < 0) {
             if (p.q1 && p.b1) h1p_exp_block(p.w1, p.b1, p.q1);
             return;
@@ -2971,7 +3140,7 @@ int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
                  "ppox_nature_pack: packed buffers must be 16-byte aligned");
     PPOX_REQUIRE(!p.zero_words || (p.zero && ppox::aligned16(p.zero)), "ppox_nature_pack_all: zero buffer");
     const long long zblocks = ppox::ceil_div(p.zero_words, 1024LL);
-    wmax_kernel<<<(unsigned)(PA_TENSORS * AMAX_SLOTS + 1 + zblocks), 256, 0, s>>>(p);
+    wmax_kernel<<<(unsigned)((PA_TENSORS + PA_NORM_JOBS) * AMAX_SLOTS + 1 + zblocks), 256, 0, s>>>(p);
     PPOX_LAUNCHED_NORET(name);
     // element ranges end at the last job present (the head and fc dgrad ranges are the longest)
     const long long total = PA_N1 + 2 * PU_2 + 2 * PU_3 + PA_N2 + PU_FC +
@@ -3105,6 +3274,7 @@ extern "C" int ppox_nature_wgrad_reduce(int32_t layer, int64_t batch, const void
 
 namespace {
 bool wgrad1_im2col();
+void w2p_grid(long long batch, int& per, long long& grid);
 int launch_wgrad1_frames(const void* x, long long sample_stride, const long long* idx, long long T, long long Nenv,
                          const float* g, long long batch, void* ws, long long ws_bytes, float* dw, float* db,
                          const uint32_t* amax_g, hipStream_t s);
@@ -3112,16 +3282,27 @@ int launch_wgrad1_frames(const void* x, long long sample_stride, const long long
 
 extern "C" int64_t ppox_nature_wgrad_split_workspace_bytes(int32_t layer, int64_t batch) {
     if (batch <= 0) return 0;
+    if (layer == 1 && !wgrad1_im2col()) {
+        // the direct conv1 weight gradient: two partial slabs per workgroup, one workgroup per CU
+        // (grid = min(batch, CUs): more than Ws1's 512-slab floor on a device with > 256 CUs)
+        int per;
+        long long grid;
+        w2p_grid(batch, per, grid);
+        return std::max(Ws1::workspace_bytes(batch), 2 * grid * (long long)(G1::K * G1::COUT + G1::COUT) * 4);
+    }
     return layer == 1 ? Ws1::workspace_bytes(batch) : layer == 2 ? Ws2::workspace_bytes(batch)
                       : layer == 3 ? Ws3::workspace_bytes(batch) : -1;
 }
 
 extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_t batch, int64_t x_sample_stride,
                                             const float* grad_out, void* workspace, int64_t workspace_bytes, float* dw,
-                                            float* db, const uint32_t* amax_x, const uint32_t* amax_g, void* stream) {
+                                            float* db, const uint32_t* amax_x, const uint32_t* amax_g,
+                                            const int* x_exp, const int* g_exp, void* stream) {
     PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_conv_wgrad_split: layer must be 1, 2 or 3");
     PPOX_REQUIRE(x && grad_out && workspace && dw && db && batch > 0, "ppox_nature_conv_wgrad_split: bad arguments");
-    PPOX_REQUIRE(amax_g && (layer == 1 || amax_x) && ppox::aligned16(amax_g) && (!amax_x || ppox::aligned16(amax_x)),
+    PPOX_REQUIRE((!x_exp && !g_exp) || layer == 3, "ppox_nature_conv_wgrad_split: PX operands are layer 3's (h2, g3)");
+    PPOX_REQUIRE((amax_g || g_exp) && (layer == 1 || amax_x || x_exp) && (!amax_g || ppox::aligned16(amax_g)) &&
+                     (!amax_x || ppox::aligned16(amax_x)),
                  "ppox_nature_conv_wgrad_split: amax slots of the operands (16B-aligned) required");
     PPOX_REQUIRE(workspace_bytes >= ppox_nature_wgrad_split_workspace_bytes(layer, batch),
                  "ppox_nature_conv_wgrad_split: workspace too small");
@@ -3139,6 +3320,9 @@ extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_
     }
     PPOX_REQUIRE(ppox::aligned16(x), "ppox_nature_conv_wgrad_split: layer 2/3 input must be 16B-aligned NHWC");
     if (layer == 2) return Ws2::run(x, 0, grad_out, batch, workspace, dw, db, amax_x, amax_g, s);
+    if (x_exp && g_exp) return Ws3PP::run(x, 0, grad_out, batch, workspace, dw, db, amax_x, amax_g, s, nullptr, 0, 0, x_exp, g_exp);
+    if (x_exp) return Ws3PF::run(x, 0, grad_out, batch, workspace, dw, db, amax_x, amax_g, s, nullptr, 0, 0, x_exp, g_exp);
+    if (g_exp) return Ws3FP::run(x, 0, grad_out, batch, workspace, dw, db, amax_x, amax_g, s, nullptr, 0, 0, x_exp, g_exp);
     return Ws3::run(x, 0, grad_out, batch, workspace, dw, db, amax_x, amax_g, s);
 }
 
@@ -3192,34 +3376,50 @@ long long planes(int which) {
 }
 
 int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq, const float* bias, float* y,
-                const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, hipStream_t s) {
+                const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, const int* x_exp, int* y_exp_out,
+                hipStream_t s) {
     PPOX_REQUIRE(ppox::aligned16(x), "ppox_nature_conv_fwd_split: layer 2/3 input must be 16B-aligned NHWC");
-    PPOX_REQUIRE(amax_x && ppox::aligned16(amax_x), "ppox_nature_conv_fwd_split: amax slots of x required (layer 2/3)");
+    // amax_x: the split of an f32 x and the bound of a PX output
+    PPOX_REQUIRE((amax_x || (x_exp && !y_exp_out)) && (!amax_x || ppox::aligned16(amax_x)),
+                 "ppox_nature_conv_fwd_split: amax slots of x required (layer 2/3)");
     PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(relu_bits) & 7), "ppox_nature_conv_fwd_split: relu_bits 8B alignment");
+    PPOX_REQUIRE(!x_exp || layer == 3, "ppox_nature_conv_fwd_split: PX input (x_exp) is layer 3's (h2 planes)");
     Args a{x, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch, amax_x, amax_y, pack_exp(wq, planes(layer))};
     a.bits_y = relu_bits;
-    if (layer == 2)
-        return launch_sgemm<SgFwd<G2, false>>(a, wq, ppox::ceil_div(batch * G2::P, SG_ROWS), s,
-                                              "ppox_nature_conv_fwd_split");
-    return launch_sgemm<SgFwd<G3, false>>(a, wq, ppox::ceil_div(batch * G3::P, SG_ROWS), s,
-                                          "ppox_nature_conv_fwd_split");
+    a.xexp = x_exp;
+    a.yexp_out = y_exp_out;
+    a.ynorm = pack_norm(wq, planes(layer));
+    a.ybias = pack_bmax(wq, planes(layer));
+    constexpr const char* nm = "ppox_nature_conv_fwd_split";
+    if (layer == 2) {
+        const long long blocks = ppox::ceil_div(batch * G2::P, SG_ROWS);
+        if (y_exp_out) return launch_sgemm<Px<SgFwd<G2, false>, false, true>>(a, wq, blocks, s, nm);
+        return launch_sgemm<SgFwd<G2, false>>(a, wq, blocks, s, nm);
+    }
+    const long long blocks = ppox::ceil_div(batch * G3::P, SG_ROWS);
+    if (x_exp && y_exp_out) return launch_sgemm<Px<SgFwd<G3, false>, true, true>>(a, wq, blocks, s, nm);
+    if (x_exp) return launch_sgemm<Px<SgFwd<G3, false>, true>>(a, wq, blocks, s, nm);
+    if (y_exp_out) return launch_sgemm<Px<SgFwd<G3, false>, false, true>>(a, wq, blocks, s, nm);
+    return launch_sgemm<SgFwd<G3, false>>(a, wq, blocks, s, nm);
 }
 }  // namespace ppox_conv
 
 extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch, const uint16_t* wqd,
                                             const float* prev_act, float* grad_in, const uint32_t* amax_g,
-                                            uint32_t* amax_out, const uint32_t* relu_bits, void* stream) {
+                                            uint32_t* amax_out, const uint32_t* relu_bits, const int* g_exp,
+                                            void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad_split: layer must be 2 or 3");
-    PPOX_REQUIRE(grad_out && wqd && (prev_act || relu_bits) && grad_in && amax_g && batch >= 0,
+    PPOX_REQUIRE(grad_out && wqd && (prev_act || relu_bits) && grad_in && (amax_g || g_exp) && batch >= 0,
                  "ppox_nature_conv_dgrad_split: bad arguments");
     // relu_bits: the ReLU bitmask of the layer below (conv1's for layer 2, conv2's for layer 3)
-    PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wqd) && ppox::aligned16(amax_g),
+    PPOX_REQUIRE(ppox::aligned16(grad_out) && ppox::aligned16(wqd) && (!amax_g || ppox::aligned16(amax_g)),
                  "ppox_nature_conv_dgrad_split: 16B alignment");
     Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch, amax_g, amax_out,
            pack_exp(wqd, ppox_conv::planes(10 + layer))};
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 2) {
+        PPOX_REQUIRE(!g_exp, "ppox_nature_conv_dgrad_split: layer 2 reads an f32 g2");
         const long long ntriples = ppox::ceil_div(batch, (long long)C2S);
         PPOX_REQUIRE(batch * G2::P * 256 < (1LL << 32), "ppox_nature_conv_dgrad_split: batch too large (32-bit offsets)");
         // one workgroup per CU (150 KB of LDS each), striding over the triples
@@ -3247,6 +3447,11 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
         PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
     }
     a.bits_mask = relu_bits;
+    a.xexp = g_exp;  // PX g3 (the fc dgrad's planes output)
+    PPOX_REQUIRE(!g_exp || relu_bits, "ppox_nature_conv_dgrad_split: a PX g3 needs conv2's ReLU bitmask");
+    if (g_exp)
+        return launch_sgemm<Px<SgDgradPM<G3, true>, true>>(a, wqd, ppox::ceil_div(batch, SG_ROWS) * SgDgradPM<G3>::NPOS,
+                                                           s, "ppox_nature_conv_dgrad_split");
     if (relu_bits)
         return launch_sgemm<SgDgradPM<G3, true>>(a, wqd, ppox::ceil_div(batch, SG_ROWS) * SgDgradPM<G3>::NPOS, s,
                                                  "ppox_nature_conv_dgrad_split");
@@ -3302,17 +3507,24 @@ int launch_wgrad1_frames(const void* x, long long sample_stride, const long long
 }  // namespace
 
 extern "C" int ppox_nature_conv2_fwd_planes(const uint16_t* h1p, const uint16_t* q1, int64_t batch,
-                                            const uint16_t* wq2, const float* bias, float* y, uint32_t* amax_y,
-                                            uint32_t* relu_bits, void* stream) {
+                                            const uint16_t* wq2, const float* bias, float* y, const uint32_t* amax_x,
+                                            uint32_t* amax_y, uint32_t* relu_bits, int* y_exp_out, void* stream) {
     if (batch == 0) return PPOX_OK;
     PPOX_REQUIRE(h1p && q1 && wq2 && bias && y && batch > 0, "ppox_nature_conv2_fwd_planes: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(h1p) && ppox::aligned16(wq2), "ppox_nature_conv2_fwd_planes: 16B alignment");
     PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(relu_bits) & 7), "ppox_nature_conv2_fwd_planes: relu_bits 8B alignment");
-    Args a{h1p, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch, nullptr, amax_y, pack_exp(wq2, PL_Q2)};
+    PPOX_REQUIRE(!y_exp_out || (amax_x && ppox::aligned16(amax_x)),
+                 "ppox_nature_conv2_fwd_planes: a PX output (y_exp_out) needs h1's amax slots (amax_x)");
+    Args a{h1p, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch, amax_x, amax_y, pack_exp(wq2, PL_Q2)};
     a.bits_y = relu_bits;
     a.xexp = h1p_exp(q1, PL_Q1);
-    return launch_sgemm<SgFwd2P>(a, wq2, ppox::ceil_div(batch * G2::P, SG_ROWS), ppox::as_stream(stream),
-                                 "ppox_nature_conv2_fwd_planes");
+    a.yexp_out = y_exp_out;
+    a.ynorm = pack_norm(wq2, PL_Q2);
+    a.ybias = pack_bmax(wq2, PL_Q2);
+    const long long blocks = ppox::ceil_div(batch * G2::P, SG_ROWS);
+    if (y_exp_out)
+        return launch_sgemm<Px<SgFwd2P, true, true>>(a, wq2, blocks, ppox::as_stream(stream), "ppox_nature_conv2_fwd_planes");
+    return launch_sgemm<SgFwd2P>(a, wq2, blocks, ppox::as_stream(stream), "ppox_nature_conv2_fwd_planes");
 }
 
 extern "C" int64_t ppox_nature_conv2_wgrad_planes_workspace_bytes(int64_t batch) {
@@ -3469,7 +3681,7 @@ extern "C" int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch) {
 
 extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float* h3, void* workspace,
                                     int64_t workspace_bytes, float* dw, const uint32_t* amax_df,
-                                    const uint32_t* amax_h3, void* stream) {
+                                    const uint32_t* amax_h3, const int* h3_exp, void* stream) {
     PPOX_REQUIRE(dw && batch >= 0, "ppox_nature_fc_wgrad: bad arguments");
     hipStream_t s = ppox::as_stream(stream);
     if (batch == 0) {  // no rows: a zero gradient
@@ -3477,16 +3689,20 @@ extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float*
                      "ppox_nature_fc_wgrad: memset failed");
         return PPOX_OK;
     }
-    PPOX_REQUIRE(df && h3 && workspace && amax_df && amax_h3, "ppox_nature_fc_wgrad: bad arguments");
-    PPOX_REQUIRE(ppox::aligned16(amax_df) && ppox::aligned16(amax_h3), "ppox_nature_fc_wgrad: 16B alignment");
+    PPOX_REQUIRE(df && h3 && workspace && amax_df && (amax_h3 || h3_exp), "ppox_nature_fc_wgrad: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(amax_df) && (!amax_h3 || ppox::aligned16(amax_h3)), "ppox_nature_fc_wgrad: 16B alignment");
     PPOX_REQUIRE(workspace_bytes >= FcWgrad::workspace_bytes(batch), "ppox_nature_fc_wgrad: workspace too small");
     PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(h3), "ppox_nature_fc_wgrad: 16B alignment");
     PPOX_REQUIRE(batch < (1LL << 31) / 64, "ppox_nature_fc_wgrad: batch too large for 32-bit row indexing");
     const int sp = FcWgrad::splits(batch);
     float* slab = reinterpret_cast<float*>(workspace);
     WArgs wa{df, 0, h3, slab, nullptr, batch, 0, sp, nullptr, 0, 0, amax_df, amax_h3};
+    wa.gexp = h3_exp;  // PX h3 (the G operand of this GEMM)
     wa.px_per_split = ppox::ceil_div(ppox::ceil_div((long long)batch, (long long)sp), (long long)MS) * MS;
-    wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB><<<(unsigned)(FcWgrad::TILES * sp), 256, 0, s>>>(wa);
+    if (h3_exp)
+        wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB, false, true><<<(unsigned)(FcWgrad::TILES * sp), 256, 0, s>>>(wa);
+    else
+        wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB><<<(unsigned)(FcWgrad::TILES * sp), 256, 0, s>>>(wa);
     PPOX_LAUNCHED_NORET("ppox_nature_fc_wgrad");
     fc_wgrad_reduce_perm<<<512, 256, 0, s>>>(slab, sp, dw);
     PPOX_LAUNCHED("ppox_nature_fc_wgrad");
@@ -3502,14 +3718,19 @@ extern "C" int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_
 }
 
 extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
-                                  const uint32_t* amax_h3, uint32_t* amax_f, void* stream) {
+                                  const uint32_t* amax_h3, uint32_t* amax_f, const int* h3_exp, void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
-    PPOX_REQUIRE(h3 && q_fwd && bias && f && amax_h3 && batch >= 0, "ppox_nature_fc_fwd: bad arguments");
-    PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd) && ppox::aligned16(amax_h3),
+    PPOX_REQUIRE(h3 && q_fwd && bias && f && (amax_h3 || h3_exp) && batch >= 0, "ppox_nature_fc_fwd: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd) && (!amax_h3 || ppox::aligned16(amax_h3)),
                  "ppox_nature_fc_fwd: 16B alignment");
     Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, amax_h3, amax_f, pack_exp(q_fwd, PL_FCF)};
-    return launch_sgemm<SgRows<3136, 512, FC_FWD, FC_FWD_G>>(a, q_fwd, ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB,
-                                                   ppox::as_stream(stream), "ppox_nature_fc_fwd");
+    a.xexp = h3_exp;  // PX h3 (the conv3 forward's planes output)
+    const long long blocks = ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB;
+    if (h3_exp)
+        return launch_sgemm<Px<SgRows<3136, 512, FC_FWD, FC_FWD_G>, true>>(a, q_fwd, blocks, ppox::as_stream(stream),
+                                                                          "ppox_nature_fc_fwd");
+    return launch_sgemm<SgRows<3136, 512, FC_FWD, FC_FWD_G>>(a, q_fwd, blocks, ppox::as_stream(stream),
+                                                             "ppox_nature_fc_fwd");
 }
 
 extern "C" int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch) {
@@ -3519,21 +3740,30 @@ extern "C" int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch) {
 extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias,
                                          void* workspace, int64_t workspace_bytes, float* f, const uint32_t* amax_h3,
                                          uint32_t* amax_f, const float* w_actor, const float* b_actor,
-                                         int32_t n_actions, float* logits, void* stream) {
+                                         int32_t n_actions, float* logits, const int* h3_exp, void* stream) {
     if (batch == 0) return PPOX_OK;
-    PPOX_REQUIRE(h3 && q_fwd && bias && f && workspace && amax_h3 && batch > 0,
+    PPOX_REQUIRE(h3 && q_fwd && bias && f && workspace && (amax_h3 || h3_exp) && batch > 0,
                  "ppox_nature_fc_fwd_splitk: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(h3) && ppox::aligned16(q_fwd) && ppox::aligned16(f) && ppox::aligned16(workspace) &&
-                     ppox::aligned16(amax_h3),
+                     (!amax_h3 || ppox::aligned16(amax_h3)),
                  "ppox_nature_fc_fwd_splitk: 16B alignment");
     PPOX_REQUIRE(workspace_bytes >= ppox_nature_fc_fwd_splitk_workspace_bytes(batch),
                  "ppox_nature_fc_fwd_splitk: workspace too small");
     PPOX_REQUIRE(!logits || (w_actor && b_actor && n_actions >= 1 && n_actions <= 8 && ppox::aligned16(w_actor)),
                  "ppox_nature_fc_fwd_splitk: the fused actor head needs 1..8 actions and a 16B-aligned weight");
     Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, amax_h3, amax_f, pack_exp(q_fwd, PL_FCF)};
+    a.xexp = h3_exp;  // PX h3
     float* slab = reinterpret_cast<float*>(workspace);
     hipStream_t st = ppox::as_stream(stream);
     const ActorHead act{w_actor, b_actor, logits ? (int)n_actions : 0, logits};
+    if (h3_exp) {
+        switch (fc_fwd_splits(batch)) {
+            case 1: return launch_fc_fwd_sk<3136, 1, true>(a, q_fwd, slab, bias, f, act, st);
+            case 2: return launch_fc_fwd_sk<3136, 2, true>(a, q_fwd, slab, bias, f, act, st);
+            case 4: return launch_fc_fwd_sk<3136, 4, true>(a, q_fwd, slab, bias, f, act, st);
+            default: return launch_fc_fwd_sk<3136, 8, true>(a, q_fwd, slab, bias, f, act, st);
+        }
+    }
     switch (fc_fwd_splits(batch)) {
         case 1: return launch_fc_fwd_sk<3136, 1>(a, q_fwd, slab, bias, f, act, st);
         case 2: return launch_fc_fwd_sk<3136, 2>(a, q_fwd, slab, bias, f, act, st);
@@ -3544,7 +3774,7 @@ extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const u
 
 extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
                                     const uint32_t* amax_df, uint32_t* amax_g3, const uint32_t* relu_bits,
-                                    void* stream) {
+                                    int* g3_exp_out, void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(df && q_dgrad && (h3 || relu_bits) && g3 && amax_df && batch >= 0,
                  "ppox_nature_fc_dgrad: bad arguments");
@@ -3552,6 +3782,14 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
                  "ppox_nature_fc_dgrad: 16B alignment");
     Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch, amax_df, amax_g3, pack_exp(q_dgrad, PL_FCD)};
     a.bits_mask = relu_bits;  // h3's ReLU bitmask from the conv3 forward (instead of h3)
+    if (g3_exp_out) {  // g3 as PX planes, bounded by amax(df) * the fc weight's column norms
+        PPOX_REQUIRE(relu_bits, "ppox_nature_fc_dgrad: a PX g3 needs h3's ReLU bitmask");
+        a.yexp_out = g3_exp_out;
+        a.ynorm = pack_norm(q_dgrad, PL_FCD);
+        a.ybias = pack_bmax(q_dgrad, PL_FCD);
+        return launch_sgemm<Px<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_G, true>, false, true>>(
+            a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB, ppox::as_stream(stream), "ppox_nature_fc_dgrad");
+    }
     if (relu_bits)
         return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_G, true>>(
             a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB, ppox::as_stream(stream), "ppox_nature_fc_dgrad");
@@ -3559,18 +3797,19 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
                                                      ppox::as_stream(stream), "ppox_nature_fc_dgrad");
 }
 
-extern "C" int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, const float* w3,
-                                    const float* wfc, float* wpd2, uint16_t* q1, uint16_t* q2, uint16_t* q3,
-                                    uint16_t* qd2, uint16_t* qd3, uint16_t* qfc_fwd, uint16_t* qfc_dgrad,
-                                    const float* wh, uint16_t* qh_fwd, uint16_t* qh_dgrad, uint32_t* zero,
-                                    int64_t zero_words, void* stream) {
+extern "C" int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, const float* b2,
+                                    const float* w3, const float* b3, const float* wfc, float* wpd2, uint16_t* q1,
+                                    uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3, uint16_t* qfc_fwd,
+                                    uint16_t* qfc_dgrad, const float* wh, uint16_t* qh_fwd, uint16_t* qh_dgrad,
+                                    uint32_t* zero, int64_t zero_words, void* stream) {
     PPOX_REQUIRE(w1 && w2 && w3 && (wfc || (!qfc_fwd && !qfc_dgrad)), "ppox_nature_pack_all: null weights");
     PPOX_REQUIRE(!q1 || b1, "ppox_nature_pack_all: q1 needs the conv1 bias b1 (the H1P exponent)");
     PPOX_REQUIRE(zero_words >= 0 && (zero_words == 0 || zero), "ppox_nature_pack_all: zero buffer");
-    return launch_pack_all(
-        PackAll{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh, qh_fwd, qh_dgrad, b1, zero,
-                zero_words},
-        ppox::as_stream(stream), "ppox_nature_pack_all");
+    PackAll p{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh, qh_fwd, qh_dgrad, b1, zero,
+              zero_words};
+    p.b2 = b2;
+    p.b3 = b3;
+    return launch_pack_all(p, ppox::as_stream(stream), "ppox_nature_pack_all");
 }
 
 // ---- the heads' hidden layer Linear(512, 512) + ReLU on the split-f16 GEMM -------------

@@ -42,6 +42,14 @@ struct Args {
     // writes it)
     const int* xexp = nullptr;
     const int* yexp = nullptr;
+    // planes outputs of the sg2 producers (round 4: h2, h3, g3 — "PX", the H1P form generalised):
+    // the output is written as two f16 planes at the exponent bound_exp() derives from the input's
+    // amax (amax_x), the weights' norm slots (ynorm: 256 partial maxima of the weight matrix's
+    // column l1-norms, pack tail) and the bias bound (ybias, nullable); the kernel stores it to
+    // *yexp_out for the consumers
+    int* yexp_out = nullptr;
+    const uint32_t* ynorm = nullptr;
+    const uint32_t* ybias = nullptr;
 };
 
 // H1P (conv1's output, the split conv2 operand): per pixel 32 hi then 32 lo f16 (128 B, the size
@@ -258,6 +266,41 @@ __device__ inline void split4h(const float4& v, float s, uint2& p0, uint2& p1) {
     split2h((f32x2){v.x, v.y}, s, p0.x, p1.x);
     split2h((f32x2){v.z, v.w}, s, p0.y, p1.y);
 }
+// ---- PX: f32 activations / gradients stored as their two f16 planes ---------------------
+// A tensor of f32 layout (NHWC rows, channel runs of 32 aligned to 32 elements) is stored in the
+// same bytes as, per 32-element group, the 32 high f16 then the 32 low f16 of its values times
+// 2^E: element e's high half at uint16 index 2 (e & ~31) + (e & 31), its low half 32 further.  A
+// 32-k chunk of an f32 GEMM operand row is then its two planes as they lie (conv1's H1P output is
+// the first such tensor).  E comes from a bound on the values, so the producer can split in its
+// epilogue: |y| <= amax(x) * max_n sum_k |W[k][n]| + max |b| (a ReLU or mask never increases it);
+// the 2^-10 margin covers the f32 roundings of the kernel and of the bound itself.  A bound above
+// the true amax only lowers the low plane's subnormal floor (absolute error 2^-25 2^-E per value).
+__device__ inline int bound_exp(uint32_t amax_x, uint32_t norm, uint32_t bmax) {
+    const float b = __uint_as_float(amax_x) * __uint_as_float(norm) + __uint_as_float(bmax);
+    return split_scale_exp(__float_as_uint(b * (1.f + 1.f / 1024.f)));
+}
+// uint16 index of the high half of element e (its low half: + 32)
+__host__ __device__ inline long long px_index(long long e) { return 2 * (e & ~31LL) + (e & 31); }
+// one value of a column pair (col, col ^ 1) held by lanes L, L ^ 1 (same row), times 2^E: the
+// 4-B word lane L stores after one DPP swap — the even lane the pair's two high halves, the odd
+// lane their two low halves (at px_index(e_even) and px_index(e_even) + 32): as many 4-B stores as
+// the f32 form.  Every lane of the wave must execute it (the swap reads the partner lane).
+__device__ inline uint32_t px_pair_word(float vs, bool odd) {
+    const _Float16 hv = (_Float16)vs;
+    const _Float16 lv = (_Float16)(vs - (float)hv);  // exact in f32
+    const uint32_t w = (uint32_t)__builtin_bit_cast(uint16_t, hv) | ((uint32_t)__builtin_bit_cast(uint16_t, lv) << 16);
+    const uint32_t pw = (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    return odd ? ((pw >> 16) | (w & 0xFFFF0000u)) : ((w & 0xFFFFu) | (pw << 16));
+}
+// the f32 value hi + lo (exact) of half H (0: low, 1: high) of a high-plane word and a low-plane word
+__device__ inline float px_value(uint32_t hw, uint32_t lw, int H) {
+    float r;
+    if (H)
+        asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(hw), "v"(lw));
+    else
+        asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(hw), "v"(lw));
+    return r;
+}
 // one f32 (scaled) -> its two f16 planes (the weight packers)
 __device__ inline void split1h(float v, uint16_t& h, uint16_t& l) {
     const _Float16 hv = (_Float16)v;
@@ -279,12 +322,22 @@ __device__ inline u32x4 u8x8_to_f16(uint32_t w0, uint32_t w1) {
 // Tail of a packed buffer of `planes` uint16: PACK_TAIL32 uint32 — [0, AMAX_SLOTS) the amax
 // partials of the source weights (written by wmax_kernel, read by the packer), then the scale
 // exponent E the planes were packed with (read by the GEMM kernels).
-constexpr int PACK_TAIL32 = AMAX_SLOTS + 8;
+constexpr int PACK_TAIL32 = 2 * AMAX_SLOTS + 8;
+// tail slots after the exponent (AMAX_SLOTS): the H1P exponent (q1), the bias bound max |b| (q2, q3:
+// float bits) and, from NORM_SLOT0, 256 partial maxima of the packed matrix's column l1-norms
+// sum_k |B[k][n]| (float bits; q2, q3, qfcd: the PX output bounds, written by wmax_kernel)
+constexpr int BMAX_SLOT = 2, NORM_SLOT0 = AMAX_SLOTS + 8;
 __host__ __device__ inline uint32_t* pack_tail(uint16_t* q, long long planes) {
     return reinterpret_cast<uint32_t*>(q + planes);
 }
 __host__ __device__ inline const int* pack_exp(const uint16_t* q, long long planes) {
     return reinterpret_cast<const int*>(q + planes) + AMAX_SLOTS;
+}
+__host__ __device__ inline const uint32_t* pack_norm(const uint16_t* q, long long planes) {
+    return reinterpret_cast<const uint32_t*>(q + planes) + NORM_SLOT0;
+}
+__host__ __device__ inline const uint32_t* pack_bmax(const uint16_t* q, long long planes) {
+    return reinterpret_cast<const uint32_t*>(q + planes) + AMAX_SLOTS + BMAX_SLOT;
 }
 // the H1P exponent stored in the conv1 forward pack's tail (Args::xexp / yexp)
 __host__ __device__ inline const int* h1p_exp(const uint16_t* q1, long long planes_q1) {
@@ -328,6 +381,9 @@ struct WArgs {
     // split-f16: amax slots of X (null: uint8 frames) and of G
     const uint32_t* amax_x = nullptr;
     const uint32_t* amax_g = nullptr;
+    // PX operands (f16 planes, conv_common.h): their exponents (the kernels' XPL / GPL forms)
+    const int* xexp = nullptr;
+    const int* gexp = nullptr;
 };
 
 }  // namespace
@@ -337,5 +393,6 @@ int pack_split(const float* w1, const float* w2, const float* w3, uint16_t* q1, 
                uint16_t* qd2, uint16_t* qd3, hipStream_t s);
 long long planes(int which);  // uint16 planes of a split-packed form (1, 2, 3, 12, 13; 4 = fc)
 int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq, const float* bias, float* y,
-                const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, hipStream_t s);
+                const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, const int* x_exp, int* y_exp_out,
+                hipStream_t s);
 }  // namespace ppox_conv

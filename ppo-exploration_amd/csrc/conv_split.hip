@@ -36,7 +36,8 @@ namespace {
 // are read through one L2.
 // PLANES: h1 is written as its two f16 planes (H1P: per pixel 32 hi then 32 lo f16, 128 B like f32),
 // h1 * 2^E = hi + lo with E = *a.yexp (ppox_nature_pack_all: from the weight bound of conv1's
-// output), the operand format of the split conv2 forward / weight gradient — no amax is recorded
+// output), the operand format of the split conv2 forward / weight gradient; its amax is recorded when
+// a.amax_y is set (the bound of conv2's PX output)
 // IDX (rows through the rollout index, round 3): each tile's idx values are loaded one tile ahead in
 // inline asm (tile k + 1's during tile k's frame loads) and waited for by a counted vmcnt that leaves
 // the 16 frame loads issued after them in flight; a plain load there made hipcc drain every load in
@@ -209,7 +210,7 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
         load_tile(tile + 2 < t_end ? tile + 2 : t_end - 1, r0);
         run_tile(tile + 1, r1);
     }
-    if constexpr (!PLANES) amax_record(a.amax_y, om);
+    amax_record(a.amax_y, om);  // (H1P: the bound of conv2's PX output starts from it)
 }
 
 #ifndef SPLIT_FWD1_MT
@@ -232,7 +233,8 @@ inline long long fwd1_waves(long long batch, long long ntile) {
 // exponent the weight packing derived (ppox_nature_pack_all with b1)
 extern "C" int ppox_nature_conv1_fwd_planes(const void* x, int64_t batch, const int64_t* idx, int64_t T,
                                             int64_t N_env, int64_t x_sample_stride, const uint16_t* wq1,
-                                            const float* bias, uint16_t* h1p, uint32_t* relu_bits, void* stream) {
+                                            const float* bias, uint16_t* h1p, uint32_t* amax_y, uint32_t* relu_bits,
+                                            void* stream) {
     if (batch == 0) return PPOX_OK;
     PPOX_REQUIRE(x && wq1 && bias && h1p && batch > 0, "ppox_nature_conv1_fwd_planes: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(wq1), "ppox_nature_conv1_fwd_planes: packed weights must be 16-byte aligned");
@@ -242,7 +244,7 @@ extern "C" int ppox_nature_conv1_fwd_planes(const void* x, int64_t batch, const 
     if (idx) PPOX_REQUIRE(T > 0 && N_env > 0 && T * N_env < (1LL << 31), "ppox_nature_conv1_fwd_planes: idx needs T and N_env (T * N_env < 2^31)");
     const long long pl = ppox_conv::planes(1);
     Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, nullptr, bias, nullptr,
-           reinterpret_cast<float*>(h1p), batch, nullptr, nullptr, pack_exp(wq1, pl)};
+           reinterpret_cast<float*>(h1p), batch, nullptr, amax_y, pack_exp(wq1, pl)};
     a.wp = reinterpret_cast<const float*>(wq1);
     a.bits_y = relu_bits;
     a.yexp = h1p_exp(wq1, pl);
@@ -275,16 +277,18 @@ extern "C" int ppox_nature_pack_split(const float* w1, const float* w2, const fl
 extern "C" int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, const int64_t* idx, int64_t T,
                                           int64_t N_env, int64_t x_sample_stride, const uint16_t* wq,
                                           const float* bias, float* y, const uint32_t* amax_x, uint32_t* amax_y,
-                                          uint32_t* relu_bits, void* stream) {
+                                          uint32_t* relu_bits, const int* x_exp, int* y_exp_out, void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer >= 1 && layer <= 3, "ppox_nature_conv_fwd_split: layer must be 1, 2 or 3");
     PPOX_REQUIRE(x && wq && bias && y && batch >= 0, "ppox_nature_conv_fwd_split: bad arguments");
     PPOX_REQUIRE(ppox::aligned16(wq), "ppox_nature_conv_fwd_split: packed weights must be 16-byte aligned");
     if (layer != 1) {
         PPOX_REQUIRE(!idx, "ppox_nature_conv_fwd_split: idx is for layer 1 only");
-        return ppox_conv::split_fwd23(layer, x, batch, wq, bias, y, amax_x, amax_y, relu_bits, ppox::as_stream(stream));
+        return ppox_conv::split_fwd23(layer, x, batch, wq, bias, y, amax_x, amax_y, relu_bits, x_exp, y_exp_out,
+                                      ppox::as_stream(stream));
     }
     PPOX_REQUIRE(!amax_x, "ppox_nature_conv_fwd_split: layer 1 reads uint8 frames (no amax_x)");
+    PPOX_REQUIRE(!x_exp && !y_exp_out, "ppox_nature_conv_fwd_split: layer 1's planes output is ppox_nature_conv1_fwd_planes");
     PPOX_REQUIRE(batch * G1::P < (1LL << 31), "ppox_nature_conv_fwd_split: batch too large for 32-bit rows");
     Args a{x, reinterpret_cast<const long long*>(idx), T, N_env, x_sample_stride, nullptr, bias, nullptr, y, batch,
            nullptr, amax_y, pack_exp(wq, ppox_conv::planes(1))};

@@ -49,6 +49,20 @@ class DistContext:
         tdist.all_gather(parts, t.contiguous(), group=self.group)
         return torch.cat(parts, dim=dim)
 
+    def all_gather_rows(self, t, counts):
+        """Concatenate every rank's rows in rank order when rank r holds counts[r] of them (ragged
+        shards: all_gather needs equal sizes, so each rank sends max(counts) rows, zero-padded)."""
+        if not self.enabled:
+            return t
+        m = max(counts)
+        if t.shape[0] != counts[self.rank]:
+            raise ValueError(f"rank {self.rank} holds {t.shape[0]} rows, counts says {counts[self.rank]}")
+        pad = t.new_zeros((m,) + tuple(t.shape[1:]))
+        pad[:t.shape[0]] = t
+        parts = [torch.empty_like(pad) for _ in range(self.world)]
+        tdist.all_gather(parts, pad, group=self.group)
+        return torch.cat([p[:c] for p, c in zip(parts, counts)], dim=0)
+
     def barrier(self):
         if self.enabled:
             tdist.barrier(group=self.group)

@@ -146,8 +146,9 @@ class EvolutionStrategy:
     def _get_rewards(self, pool, population):
         """:179-195: fitness of every perturbation -> (P,) numpy (all ranks' members)."""
         fit, _ = self._evaluate_dev(self._dev_weights(self.weights), population, population.shape[0])
-        if self.dist.enabled:
-            fit = self.dist.all_gather_cat(fit, dim=0)
+        if self.dist.enabled:  # members in rank order (shards may differ by one when P % world != 0)
+            P, G = self.POPULATION_SIZE, self.dist.world
+            fit = self.dist.all_gather_rows(fit, [P * (g + 1) // G - P * g // G for g in range(G)])
         return fit.cpu().numpy()
 
     def get_behavior_char(self, weights, env=None):

@@ -280,9 +280,10 @@ class CnnActorCritic(nn.Module):
                               b_int_extra=self.int_extra_layer[0].bias.grad if self.intrinsic else None,
                               relu_df=not split, amax_df=am[_convs.AM_DF] if (cv.nhwc3 and not split) else None)
             if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-f16 kernel, Flatten-order dW
+                h3_exp = am.exp(_convs.EX_H3)  # (PX h3: its planes)
                 if side is None:
                     native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, amax_df=am[_convs.AM_DF],
-                                           amax_h3=am[_convs.AM_H3])
+                                           amax_h3=am[_convs.AM_H3], h3_exp=h3_exp)
                     if dense_ready is not None:
                         dense_ready()
                 else:
@@ -291,7 +292,7 @@ class CnnActorCritic(nn.Module):
                     # fork, after every head gradient); backward_acts joins the side stream
                     _convs.fork(side, cur)
                     native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, amax_df=am[_convs.AM_DF],
-                                           amax_h3=am[_convs.AM_H3], stream=side)
+                                           amax_h3=am[_convs.AM_H3], h3_exp=h3_exp, stream=side)
                     if dense_ready is not None:
                         with torch.cuda.stream(side):
                             dense_ready()

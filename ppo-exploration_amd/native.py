@@ -61,8 +61,9 @@ SIGNATURES = {
     "ppox_nchw_to_nhwc_relu_grad": [_vp, _vp, _i64, _vp, _vp],
     "ppox_nature_conv_fwd": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_pack_split": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _vp],
+    "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
     "ppox_relu_backward_amax_": [_vp, _vp, _i64, _vp, _vp],
     "ppox_amax": [_vp, _i64, _vp, _vp],
@@ -72,17 +73,17 @@ SIGNATURES = {
     "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 10 + [_i32, _vp, _vp],
     "ppox_head_dgrad_outer": [_vp] * 5 + [_i64, _i64, _i64] + [_vp] * 4,
     "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
-    "ppox_nature_pack_all": [_vp] * 17 + [_i64, _vp],
-    "ppox_nature_conv1_fwd_planes": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp],
-    "ppox_nature_conv2_fwd_planes": [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_pack_all": [_vp] * 19 + [_i64, _vp],
+    "ppox_nature_conv1_fwd_planes": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv2_fwd_planes": [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv2_wgrad_planes": [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
-    "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
-    "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "ppox_nature_fc_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
+    "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_fc_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp],
     "ppox_es_noise": [_i64, _i64, _i64, _i64, _u64, _vp, _vp],
     "ppox_es_env_noise": [_i32, _i32, _u64, _vp, _vp],
     "ppox_es_evaluate": [_vp, _vp, _f64, _i64, _i32, _i32, _i32, _i32, _i32, _u64, _vp, _vp, _vp, _vp],
@@ -90,12 +91,12 @@ SIGNATURES = {
     "ppox_normalize_obs_f32_ex": [_vp, _i64, _i64, _i64, _vp, _vp, _f64, _f64, _vp, _vp],
     "ppox_vecnorm_reward": [_vp, _vp, _vp, _i64, _f64, _vp, _vp, _f64, _f64, _f64, _i32, _vp],
     "ppox_outer_relu_backward": [_vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp],
-    "ppox_nature_conv_wgrad_split": [_i32, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_wgrad_split": [_i32, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_wgrad_split_idx": [_i32, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_vec_env_reset": [_vp, _i64, _i32, _i64, _u64, _vp, _vp, _vp],
     "ppox_vec_env_step": [_vp, _vp, _i64, _i32, _i64, _u64, _i64, _f32, _i32, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
-    "ppox_nature_fc_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp],
+    "ppox_nature_fc_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],
     "ppox_icm_pack_w1": [_vp, _i64, _vp, _vp],
     "ppox_icm_encode": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_icm_pair_backward": [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp],
@@ -484,7 +485,7 @@ def nature_conv_fwd(layer, x, batch, idx, T, N_env, x_sample_stride, wp, bias, y
 # split-f16 forms (csrc/conv_split.hip, csrc/conv.hip): weights packed as two fp16 planes
 # (int16 tensors) times a power-of-two scale; f32 operands carry "amax slots" (include/ppox.h)
 AMAX_SLOTS = 256  # include/ppox.h ppox_amax_slots()
-PACK_TAIL32 = AMAX_SLOTS + 8  # uint32 tail of a split-packed buffer (amax partials, exponents)
+PACK_TAIL32 = 2 * AMAX_SLOTS + 8  # uint32 tail of a split-packed buffer (amax partials, exponents, PX bounds)
 
 
 def amax_table(n, device):
@@ -517,15 +518,24 @@ def nature_pack_split(w1, w2, w3, q1, q2, q3, qd2=None, qd3=None, stream=None):
          stream_ptr(stream))
 
 
+def _need_amax(x, slots, x_exp, stream, what):
+    """the amax slots of an operand: given, computed (f32 x), or an error (a PX x has no f32 to scan)"""
+    if slots is not None or x_exp is None:
+        return _amax_of(x, slots, stream)
+    raise ValueError(f"{what}: the amax slots of a PX (planes) operand must be passed (its producer records them)")
+
+
 def nature_conv_fwd_split(layer, x, batch, idx, T, N_env, x_sample_stride, wq, bias, y, amax_x=None, amax_y=None,
-                          relu_bits=None, stream=None):
+                          relu_bits=None, x_exp=None, y_exp=None, stream=None):
     """amax_x: x's slots (layers 2, 3; computed here when None); amax_y: y's slots to record (or None);
-    relu_bits: int32 ReLU bitmask of y to write (batch * P * C / 32 words; or None)."""
-    if layer != 1 and batch:
-        amax_x = _amax_of(x, amax_x, stream)
+    relu_bits: int32 ReLU bitmask of y to write (batch * P * C / 32 words; or None).  PX (layer 3):
+    x_exp — x is h2 as planes, its exponent in this int32 element; y_exp — write y as planes, storing
+    the exponent there (include/ppox.h)."""
+    if layer != 1 and batch and (x_exp is None or y_exp is not None):
+        amax_x = _need_amax(x, amax_x, x_exp, stream, "nature_conv_fwd_split")
     call("ppox_nature_conv_fwd_split", int(layer), _p(x), int(batch), _p(idx), int(T), int(N_env),
          int(x_sample_stride), _p(wq), _p(bias), _p(y), _p(amax_x) if layer != 1 else None, _p(amax_y),
-         _p(relu_bits), stream_ptr(stream))
+         _p(relu_bits), _p(x_exp), _p(y_exp), stream_ptr(stream))
 
 
 def normalize_obs_f32_ex(x, rows, cols, row_stride, mean, var, eps, clip, out, stream=None):
@@ -549,24 +559,31 @@ def nature_fc_pack(w, q_fwd, q_dgrad, stream=None):
 
 
 def nature_pack_all(w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh=None, qh_fwd=None,
-                    qh_dgrad=None, b1=None, zero=None, stream=None):
+                    qh_dgrad=None, b1=None, zero=None, b2=None, b3=None, stream=None):
     """Every weight packing of a training step in two launches (None = skip); q1 needs the conv1
-    bias b1 (the H1P exponent of conv1's output is derived from W1 and b1); `zero` (an int32
-    tensor, e.g. the next pass's amax table) is zeroed on the way."""
-    call("ppox_nature_pack_all", _p(w1), _p(b1), _p(w2), _p(w3), _p(wfc), _p(wpd2), _p(q1), _p(q2), _p(q3),
-         _p(qd2), _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), _p(wh), _p(qh_fwd), _p(qh_dgrad), _p(zero),
+    bias b1 (the H1P exponent of conv1's output is derived from W1 and b1); b2 / b3 give the PX
+    output bounds of conv2 / conv3 their bias term; `zero` (an int32 tensor, e.g. the next pass's
+    amax table) is zeroed on the way."""
+    call("ppox_nature_pack_all", _p(w1), _p(b1), _p(w2), _p(b2), _p(w3), _p(b3), _p(wfc), _p(wpd2), _p(q1), _p(q2),
+         _p(q3), _p(qd2), _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), _p(wh), _p(qh_fwd), _p(qh_dgrad), _p(zero),
          0 if zero is None else zero.numel(), stream_ptr(stream))
 
 
 # conv1 -> conv2 on H1P (conv1's output as two f16 planes; include/ppox.h)
-def nature_conv1_fwd_planes(x, batch, idx, T, N_env, x_sample_stride, wq1, bias, h1p, relu_bits=None, stream=None):
+def nature_conv1_fwd_planes(x, batch, idx, T, N_env, x_sample_stride, wq1, bias, h1p, relu_bits=None, amax_y=None,
+                            stream=None):
     call("ppox_nature_conv1_fwd_planes", _p(x), int(batch), _p(idx), int(T), int(N_env), int(x_sample_stride),
-         _p(wq1), _p(bias), _p(h1p), _p(relu_bits), stream_ptr(stream))
+         _p(wq1), _p(bias), _p(h1p), _p(amax_y), _p(relu_bits), stream_ptr(stream))
 
 
-def nature_conv2_fwd_planes(h1p, q1, batch, wq2, bias, y, amax_y=None, relu_bits=None, stream=None):
-    call("ppox_nature_conv2_fwd_planes", _p(h1p), _p(q1), int(batch), _p(wq2), _p(bias), _p(y), _p(amax_y),
-         _p(relu_bits), stream_ptr(stream))
+def nature_conv2_fwd_planes(h1p, q1, batch, wq2, bias, y, amax_y=None, relu_bits=None, amax_x=None, y_exp=None,
+                            stream=None):
+    """conv2 forward on H1P; y_exp (PX output): y written as planes, its exponent stored there (the
+    bound needs h1's amax slots amax_x, recorded by nature_conv1_fwd_planes)."""
+    if y_exp is not None and amax_x is None:
+        raise ValueError("nature_conv2_fwd_planes: a PX output needs h1's amax slots (amax_x)")
+    call("ppox_nature_conv2_fwd_planes", _p(h1p), _p(q1), int(batch), _p(wq2), _p(bias), _p(y), _p(amax_x),
+         _p(amax_y), _p(relu_bits), _p(y_exp), stream_ptr(stream))
 
 
 def nature_conv2_wgrad_planes_workspace_bytes(batch):
@@ -580,12 +597,13 @@ def nature_conv2_wgrad_planes(h1p, q1, batch, grad_out, workspace, dw, db, amax_
          workspace.numel() * workspace.element_size(), _p(dw), _p(db), _p(amax_g), stream_ptr(stream))
 
 
-def nature_fc_fwd(h3, batch, q_fwd, bias, f, amax_h3=None, amax_f=None, stream=None):
-    """f = relu(h3 @ W^T + b), h3 (batch, 7, 7, 64) NHWC; amax_f: f's slots to record (or None)."""
-    if batch:
+def nature_fc_fwd(h3, batch, q_fwd, bias, f, amax_h3=None, amax_f=None, h3_exp=None, stream=None):
+    """f = relu(h3 @ W^T + b), h3 (batch, 7, 7, 64) NHWC (h3_exp: as PX planes); amax_f: f's slots to
+    record (or None)."""
+    if batch and h3_exp is None:
         amax_h3 = _amax_of(h3, amax_h3, stream)
     call("ppox_nature_fc_fwd", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(f), _p(amax_h3), _p(amax_f),
-         stream_ptr(stream))
+         _p(h3_exp), stream_ptr(stream))
 
 
 # the heads' hidden layer Linear(512, 512) (split-f16 GEMM, csrc/conv.hip; include/ppox.h)
@@ -644,36 +662,42 @@ def nature_fc_fwd_splitk_workspace_bytes(batch):
 
 
 def nature_fc_fwd_splitk(h3, batch, q_fwd, bias, workspace, f, amax_h3=None, amax_f=None, actor=None, logits=None,
-                         stream=None):
+                         h3_exp=None, stream=None):
     """fc forward split over K (small batches), bias + ReLU in the fixed-order reduce; with
-    actor = (w, b) (<= 8 actions) the reduce also writes the actor head's logits = f w^T + b."""
-    if batch:
+    actor = (w, b) (<= 8 actions) the reduce also writes the actor head's logits = f w^T + b.
+    h3_exp: h3 is PX planes."""
+    if batch and h3_exp is None:
         amax_h3 = _amax_of(h3, amax_h3, stream)
     wa, ba = actor if actor is not None else (None, None)
     call("ppox_nature_fc_fwd_splitk", _p(h3), int(batch), _p(q_fwd), _p(bias), _p(workspace),
          workspace.numel() * workspace.element_size(), _p(f), _p(amax_h3), _p(amax_f), _p(wa), _p(ba),
-         0 if wa is None else wa.shape[0], _p(logits), stream_ptr(stream))
+         0 if wa is None else wa.shape[0], _p(logits), _p(h3_exp), stream_ptr(stream))
 
 
-def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, amax_df=None, amax_g3=None, relu_bits=None, stream=None):
+def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, amax_df=None, amax_g3=None, relu_bits=None, g3_exp=None,
+                    stream=None):
     """g3 (batch, 7, 7, 64) NHWC = ((df @ W) in Flatten order) * (h3 > 0); amax_g3: g3's slots to record;
-    relu_bits: h3's ReLU bitmask from the conv3 split forward (used instead of h3)."""
+    relu_bits: h3's ReLU bitmask from the conv3 split forward (used instead of h3); g3_exp: write g3
+    as PX planes, storing the exponent there (relu_bits required)."""
     if batch:
         amax_df = _amax_of(df, amax_df, stream)
     call("ppox_nature_fc_dgrad", _p(df), int(batch), _p(q_dgrad), _p(h3), _p(g3), _p(amax_df), _p(amax_g3),
-         _p(relu_bits), stream_ptr(stream))
+         _p(relu_bits), _p(g3_exp), stream_ptr(stream))
 
 
 def nature_fc_wgrad_workspace_bytes(batch):
     return int(lib().ppox_nature_fc_wgrad_workspace_bytes(int(batch)))
 
 
-def nature_fc_wgrad(df, batch, h3, workspace, dw, amax_df=None, amax_h3=None, stream=None):
-    """dw (512, 3136) in the fc weight's Flatten order = df^T @ h3 (h3 NHWC (batch, 7, 7, 64))."""
+def nature_fc_wgrad(df, batch, h3, workspace, dw, amax_df=None, amax_h3=None, h3_exp=None, stream=None):
+    """dw (512, 3136) in the fc weight's Flatten order = df^T @ h3 (h3 NHWC (batch, 7, 7, 64); h3_exp:
+    as PX planes)."""
     if batch:
-        amax_df, amax_h3 = _amax_of(df, amax_df, stream), _amax_of(h3, amax_h3, stream)
+        amax_df = _amax_of(df, amax_df, stream)
+        if h3_exp is None:
+            amax_h3 = _amax_of(h3, amax_h3, stream)
     call("ppox_nature_fc_wgrad", _p(df), int(batch), _p(h3), _p(workspace), workspace.numel() * workspace.element_size(),
-         _p(dw), _p(amax_df), _p(amax_h3), stream_ptr(stream))
+         _p(dw), _p(amax_df), _p(amax_h3), _p(h3_exp), stream_ptr(stream))
 
 
 # ES-NSRA (csrc/es.hip)
@@ -788,14 +812,16 @@ def nature_wgrad_split_workspace_bytes(layer, batch):
 
 
 def nature_conv_wgrad_split(layer, x, batch, x_sample_stride, grad_out, workspace, dw, db, amax_x=None, amax_g=None,
-                            stream=None):
-    """dW, db of one conv layer (slabs + fixed-order reduce in one call), split-f16 MFMA."""
-    amax_g = _amax_of(grad_out, amax_g, stream)
-    if layer != 1:
+                            x_exp=None, g_exp=None, stream=None):
+    """dW, db of one conv layer (slabs + fixed-order reduce in one call), split-f16 MFMA; x_exp / g_exp
+    (layer 3): x / grad_out are PX planes."""
+    if g_exp is None:
+        amax_g = _amax_of(grad_out, amax_g, stream)
+    if layer != 1 and x_exp is None:
         amax_x = _amax_of(x, amax_x, stream)
     call("ppox_nature_conv_wgrad_split", int(layer), _p(x), int(batch), int(x_sample_stride), _p(grad_out),
          _p(workspace), workspace.numel() * workspace.element_size(), _p(dw), _p(db),
-         _p(amax_x) if layer != 1 else None, _p(amax_g), stream_ptr(stream))
+         _p(amax_x) if layer != 1 else None, _p(amax_g), _p(x_exp), _p(g_exp), stream_ptr(stream))
 
 
 def nature_conv_wgrad_split_idx(layer, x, batch, idx, T, N_env, grad_out, workspace, dw, db, amax_g=None,
@@ -809,13 +835,14 @@ def nature_conv_wgrad_split_idx(layer, x, batch, idx, T, N_env, grad_out, worksp
 
 
 def nature_conv_dgrad_split(layer, grad_out, batch, wqd, prev_act, grad_in, amax_g=None, amax_out=None,
-                            relu_bits=None, stream=None):
+                            relu_bits=None, g_exp=None, stream=None):
     """amax_g: grad_out's slots (computed here when None); amax_out: grad_in's slots to record (or None);
-    relu_bits: the ReLU bitmask of the layer below from its split forward, used instead of prev_act."""
-    if batch:
+    relu_bits: the ReLU bitmask of the layer below from its split forward, used instead of prev_act;
+    g_exp (layer 3): grad_out is g3 as PX planes (relu_bits required)."""
+    if batch and g_exp is None:
         amax_g = _amax_of(grad_out, amax_g, stream)
     call("ppox_nature_conv_dgrad_split", int(layer), _p(grad_out), int(batch), _p(wqd), _p(prev_act), _p(grad_in),
-         _p(amax_g), _p(amax_out), _p(relu_bits), stream_ptr(stream))
+         _p(amax_g), _p(amax_out), _p(relu_bits), _p(g_exp), stream_ptr(stream))
 
 
 # ---------------------------------------------------------------------------

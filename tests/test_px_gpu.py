@@ -1,0 +1,152 @@
+"""PX (round 4): the NatureCNN trunk's split-f16 operands h2, h3 and g3 written as their two f16
+planes by their producers (conv2 forward, conv3 forward, fc dgrad) at exponents derived from
+bounds, and read as they lie by their consumers (include/ppox.h "PX").  The explicit training
+forward / backward with PX on must stay fp32-class: within 2x the error of the same pass with PX
+off (f32 operands split in the consumers, the round-3 path pinned by the reference fixtures)
+against a float64 CPU autograd of the same network."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(seed, A=4, intrinsic=False):
+    import convs
+    import models
+    torch.manual_seed(seed)
+    net = models.CnnActorCritic(4, A, intrinsic=intrinsic)
+    ref = models.CnnActorCritic(4, A, intrinsic=intrinsic)
+    ref.load_state_dict(net.state_dict())
+    flat = models.FlatParams(net, "cuda")
+    cv = convs.attach(net, flat, "split")
+    return net, ref.double(), flat, cv
+
+
+def _fp64(ref, x, dout, dv):
+    """outputs and parameter gradients of the reference architecture in float64 (CPU autograd)"""
+    F = torch.nn.functional
+    fe = ref.feature_extractor
+    for p in ref.parameters():
+        p.grad = None
+    h = F.relu(fe[0](x.double().cpu()))
+    h = F.relu(fe[2](h))
+    h = F.relu(fe[4](h))
+    f = F.relu(fe[7](h.flatten(1)))
+    out = ref.actor(f)
+    v = ref.critic_ext(ref.extra_layer(f)).squeeze(-1)
+    ((out * dout.double().cpu()).sum() + (v * dv.double().cpu()).sum()).backward()
+    return out.detach(), v.detach(), {n: p.grad.clone() for n, p in ref.named_parameters()}
+
+
+def _pass(net, flat, cv, x, dout, dv, px):
+    cv.px = px
+    flat.zero_grad()
+    out, v, _, ctx = net.forward_train(x)
+    am = ctx[-1]
+    net.backward_train(ctx, dout, dv)
+    torch.cuda.synchronize()
+    grads = {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.requires_grad}
+    return out.detach().clone(), v.detach().clone(), grads, am
+
+
+@pytest.mark.parametrize("B", [37, 600, 2048])
+def test_px_training_pass_is_fp32_class(B):
+    import convs
+    net, ref, flat, cv = _setup(B)
+    assert cv.px, "PX is the default in split math"
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(B + 1)
+    dout = torch.randn(B, 4, device="cuda", generator=g)
+    dv = torch.randn(B, device="cuda", generator=g)
+    o_off, v_off, g_off, _ = _pass(net, flat, cv, x, dout, dv, False)
+    o_on, v_on, g_on, am = _pass(net, flat, cv, x, dout, dv, True)
+    assert am.px == [True, True, True], am.px  # h2, h3, g3 all ran as planes
+    o64, v64, g64 = _fp64(ref, x, dout, dv)
+    worst = []
+    for name, r in list(g64.items()) + [("out", o64), ("v", v64)]:
+        a = o_on if name == "out" else v_on if name == "v" else g_on[name]
+        b = o_off if name == "out" else v_off if name == "v" else g_off[name]
+        scale = r.abs().max().item() + 1e-30
+        e_on = (a.cpu().double() - r).abs().max().item() / scale
+        e_off = (b.cpu().double() - r).abs().max().item() / scale
+        worst.append((e_on / max(e_off, 1e-9), name, e_on, e_off))
+        assert e_on <= 2 * e_off + 2e-7, (name, e_on, e_off)
+    print("PX/off error ratios (worst 3):", sorted(worst, reverse=True)[:3])
+
+
+@pytest.mark.parametrize("B", [8192, 9001])
+def test_px_training_pass_big_batch_matches_f32_operands(B):
+    """From 8,192 rows (the sg2 fc forward and the split hidden head): PX on vs off, no fp64 (too
+    slow on the CPU at this size) — the two fp32-class passes agree to a few f32 roundings."""
+    net, _, flat, cv = _setup(7)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(11)
+    dout = torch.randn(B, 4, device="cuda", generator=g)
+    dv = torch.randn(B, device="cuda", generator=g)
+    o_off, v_off, g_off, _ = _pass(net, flat, cv, x, dout, dv, False)
+    o_on, v_on, g_on, am = _pass(net, flat, cv, x, dout, dv, True)
+    assert am.px == [True, True, True], am.px
+    for name in g_off:
+        a, b = g_on[name], g_off[name]
+        scale = b.abs().max().item() + 1e-30
+        assert (a - b).abs().max().item() <= 2e-5 * scale, name
+    for a, b in ((o_on, o_off), (v_on, v_off)):
+        assert (a - b).abs().max().item() <= 1e-5 * (b.abs().max().item() + 1e-30)
+
+
+def _bound_exp(amax, norm, bmax):
+    """conv_common.h bound_exp in numpy f32"""
+    b = np.float32(np.float32(amax) * np.float32(norm)) + np.float32(bmax)
+    b = np.float32(b * np.float32(1.0 + 1.0 / 1024.0))
+    e = int(np.array(b, dtype=np.float32).view(np.uint32)) >> 23
+    return 141 - min(254, max(15, e))
+
+
+def _amax(am_row):
+    return float(am_row.cpu().numpy().view(np.uint32).max().view(np.float32))
+
+
+def _from_planes(p, E):
+    """f32 values of a PX tensor (..., 2C) int16: per 32-group hi then lo f16, times 2^-E"""
+    q = p.reshape(-1, 64)
+    hi = q[:, :32].contiguous().view(torch.float16).float()
+    lo = q[:, 32:].contiguous().view(torch.float16).float()
+    return ((hi + lo) * 2.0 ** -E).reshape(p.shape[:-1] + (p.shape[-1] // 2,))
+
+
+@pytest.mark.parametrize("B", [5, 300])
+def test_px_exponents_and_planes(B):
+    """The exponents are the documented bounds (amax of the input x max column l1-norm of the packed
+    weights + max |bias|, 2^-10 margin), every value lies below 2^15 in planes, and h2's planes
+    are the split of the same conv2 sums the f32 epilogue writes (|decode - f32| <= 2^-22 |v| +
+    the low plane's floor)."""
+    import convs
+    net, _, flat, cv = _setup(B)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    with torch.no_grad():
+        cv.px = False
+        _, h2f, h3f, _ = cv.forward_acts(x, train=True)
+        cv.px = True
+        _, h2p, h3p, am = cv.forward_acts(x, train=True)
+    torch.cuda.synchronize()
+    exps = am[convs.AM_EXP].cpu().numpy()
+    fe = net.feature_extractor
+    w2, b2 = fe[2].weight.detach().cpu(), fe[2].bias.detach().cpu()
+    w3, b3 = fe[4].weight.detach().cpu(), fe[4].bias.detach().cpu()
+    n2 = w2.abs().reshape(64, -1).sum(1).max().item()
+    n3 = w3.abs().reshape(64, -1).sum(1).max().item()
+    e2 = _bound_exp(_amax(am[convs.AM_H1]), n2, b2.abs().max().item())
+    e3 = _bound_exp(_amax(am[convs.AM_H2]), n3, b3.abs().max().item())
+    # (the kernel's f32 column sums may differ from torch's in the last bits: the exponent only
+    # changes when the bound sits within that of a power of two)
+    assert abs(int(exps[convs.EX_H2]) - e2) <= 1, (exps[:3], e2)
+    assert abs(int(exps[convs.EX_H3]) - e3) <= 1, (exps[:3], e3)
+    E2 = int(exps[convs.EX_H2])
+    d2 = _from_planes(h2p, E2)
+    floor = 2.0 ** (-25 - E2)
+    assert ((d2 - h2f).abs() <= 2.0 ** -22 * h2f.abs() + floor).all()
+    assert (h2p.reshape(-1, 64)[:, :32].contiguous().view(torch.float16).float().abs().max() < 2 ** 15).item()
+    d3 = _from_planes(h3p, int(exps[convs.EX_H3]))
+    assert (d3 - h3f).abs().max().item() <= 1e-5 * h3f.abs().max().item()
+    assert _amax(am[convs.AM_H2]) == h2f.abs().max().item()  # the PX producer records its true amax
