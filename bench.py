@@ -59,10 +59,16 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 / bf16 MFMA
 FC_K, FC_N, HID = 3136, 512, 512
 
 
-def _sg(prob, tail):
-    """rocprof name pattern of an sgemm_kernel instance, with or without the Px<> wrapper (PX operands)"""
+def _sg(prob, tail, raw=False):
+    """rocprof name pattern of an sgemm_kernel instance, with or without the Px<> wrapper (PX operands);
+    raw: `prob` is already a regular expression"""
     import re
-    return r"sgemm_kernel<(Px<)?" + re.escape(prob) + r"(, \w+(, \w+)?>)?, " + tail + ">"
+    return r"sgemm_kernel<(Px<)?" + (prob if raw else re.escape(prob)) + r"(, \w+(, \w+)?>)?, " + tail + ">"
+
+
+def _rows(k, n, mode, bits):
+    """SgRows<K, N, MODE, G, BITS[, NB]> with any column-group size and tile width"""
+    return _sg(f"SgRows<{k}, {n}, {mode}, \\d+, {bits}(, \\d+)?>", r"4, \d", raw=True)
 
 
 IDX = r"(, \w+)*"  # trailing template flags
@@ -110,23 +116,23 @@ def _kernels():
                                                label="conv2 wgrad (H1P, direct)")
     w_fc = FC_K * FC_N * 4          # weights in as two fp16 planes (= f32 bytes) / dW out in f32
     k["ppox_nature_fc_fwd"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=ACT_B[3] + FC_N * 4, fixed=w_fc, products=3,
-                                   rocprof=_sg("SgRows<3136, 512, 0, 8, false>", "4, 3"), label="fc fwd")
+                                   rocprof=_rows(3136, 512, 0, "false"), label="fc fwd")
     k["ppox_nature_fc_fwd_splitk"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=ACT_B[3] + FC_N * 4, fixed=w_fc,
                                           products=3, rocprof=r"sgemm_kernel<(Px<)?SgRowsSK<3136, 512, \d+>(, \w+(, \w+)?>)?, 4, 3>",
                                           label="fc fwd split-K")
     k["ppox_nature_fc_dgrad"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=FC_N * 4 + ACT_B[3] + BITMASK_B[3],
                                      fixed=w_fc, products=3,
-                                     rocprof=_sg("SgRows<512, 3136, 1, 12, true>", "4, 3"), label="fc dgrad")
+                                     rocprof=_rows(512, 3136, 1, "true"), label="fc dgrad")
     k["ppox_nature_fc_wgrad"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=FC_N * 4 + ACT_B[3], fixed=w_fc, products=3,
                                      rocprof=re.escape("wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 49") + IDX + ">",
                                      label="fc wgrad")
     w_h = HID * HID * 4
     k["ppox_head_hidden_fwd"] = dict(rows_arg=1, macs=HID * HID, bytes=2 * HID * 4, fixed=w_h, products=3,
-                                     rocprof=_sg("SgRows<512, 512, 0, 8, false>", "4, 3"),
+                                     rocprof=_rows(512, 512, 0, "false"),
                                      label="head hidden fwd")
     # dgrad: de in, the heads' input grad read + written (accumulated in place), f read for the ReLU
     k["ppox_head_hidden_dgrad"] = dict(rows_arg=1, macs=HID * HID, bytes=4 * HID * 4, fixed=w_h, products=3,
-                                       rocprof=_sg("SgRows<512, 512, 2, 8, false>", "4, 3"),
+                                       rocprof=_rows(512, 512, 2, "false"),
                                        label="head hidden dgrad")
     k["ppox_head_hidden_wgrad"] = dict(rows_arg=1, macs=HID * HID, bytes=2 * HID * 4, fixed=w_h, products=3,
                                        rocprof=re.escape("wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 8>"),
@@ -270,6 +276,9 @@ def parse():
     p.add_argument("--batch-size", type=int, default=16384)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--force-dist", action="store_true",
+                   help="one rank: run the world > 1 code paths (owned-row minibatches, every collective) over a "
+                        "one-rank RCCL communicator — the per-rank program of an 8-GPU run on one GPU")
     return p.parse_args()
 
 
@@ -294,6 +303,16 @@ def main():
             tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             tdist.init_process_group(backend)
+    elif args.force_dist:
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]))
+        sk.close()
+        tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+        sys.path.insert(0, os.path.join(ROOT, "ppo-exploration_amd"))
+        import dist as _dist
+        _dist.DistContext.enabled = property(lambda self: True)  # every world > 1 branch, one rank
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
 
@@ -389,7 +408,8 @@ def main():
                    "n_envs": args.envs, "n_steps": args.nstep, "n_epochs": args.epochs,
                    "batch_size": args.batch_size, "minibatches_per_epoch": -(-args.envs * args.nstep // args.batch_size),
                    "conv_math": conv_impl.math if conv_impl is not None else None,
-                   "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)" if world > 1 else "single GPU"},
+                   "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)" if world > 1 else
+                   ("dp code paths forced on over a one-rank RCCL communicator" if args.force_dist else "single GPU")},
     }
     # per iteration, rank 0: GPU stream time and host time of each phase (phases.py);
     # gae and episodes run inside collect
@@ -456,7 +476,7 @@ def main():
                                                        threads=args.cpu_threads or None)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 or args.force_dist:
         tdist.destroy_process_group()
 
 

@@ -32,9 +32,6 @@ SPLIT_OPS = {("fwd", 1), ("fwd", 2), ("fwd", 3), ("dgrad", 2), ("dgrad", 3), ("w
 # with its col2im-form kernel (dgrad2_col_kernel: 0.68 vs 0.97 ms f32 at B = 16384, 0.091 vs
 # 0.136 ms at the 8-GPU per-rank minibatch of 2048)
 SPLIT_SLOWER = set()
-# conv2 dgrad in split math: the split kernel below this batch, the f32 kernel from it
-# (PPOX_DGRAD2_SPLIT_MAX overrides; default: split at every batch)
-DGRAD2_SPLIT_MAX_BATCH = int(os.environ.get("PPOX_DGRAD2_SPLIT_MAX", str(1 << 62)))
 # fc forward: the split-f16 GEMM from FC_SPLIT_MIN_BATCH up (rocBLAS below; PPOX_FC_SPLIT_MIN
 # overrides, default: every batch), split over K below FC_SPLITK_MAX_BATCH (tools/fc_bench.py,
 # r02: split-K 0.018 / 0.045 / 0.078 ms vs rocBLAS 0.026 / 0.062 / 0.119 ms at 512 / 2048 /
@@ -56,6 +53,10 @@ HEAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_SPLIT_MIN", "8192"))
 # with the critic head fused into its reduce (its backward stays on the library GEMMs);
 # PPOX_HEAD_FWD_SPLITK=0 keeps the library GEMM
 HEAD_FWD_SPLITK = os.environ.get("PPOX_HEAD_FWD_SPLITK", "1") == "1"
+# the hidden layer's backward (dgrad into the fc layer's input grad + weight gradient) on the split-f16
+# kernels from this batch up, the library GEMMs below (PPOX_HEAD_BWD_SPLIT_MIN; round 4: every batch —
+# the 128-column tiles, and a library GEMM call costs ~35-60 us of host time per minibatch)
+HEAD_BWD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_BWD_SPLIT_MIN", "0"))
 
 # ReLU masks of the conv outputs as bitmasks written by the split forwards for the split dgrads
 # (PPOX_RELU_BITS=0: the dgrads read the f32 activations)
@@ -271,6 +272,10 @@ class NatureConvs:
         """only the hidden layer's forward on the split-f16 kernel (split over K) for a `batch`-row pass"""
         return self.qh is not None and HEAD_FWD_SPLITK and 0 < batch < HEAD_SPLIT_MIN_BATCH
 
+    def split_head_bwd(self, batch):
+        """the hidden layer's backward (dgrad + weight gradient) on the split-f16 kernels"""
+        return self.qh is not None and (batch >= HEAD_SPLIT_MIN_BATCH or batch >= HEAD_BWD_SPLIT_MIN_BATCH)
+
     def head_fwd_ws(self, batch):
         """the split-K hidden forward's workspace, one per batch size (a captured collect graph keeps
         its own)"""
@@ -286,8 +291,6 @@ class NatureConvs:
             return (op, layer) in SPLIT_OPS or (op, layer) in SPLIT_SLOWER
         if self.math != "split":
             return False
-        if (op, layer) == ("dgrad", 2):  # split only below DGRAD2_SPLIT_MAX_BATCH rows
-            return batch is not None and batch < DGRAD2_SPLIT_MAX_BATCH
         return (op, layer) in SPLIT_OPS
 
     def h1p_exponent(self):
@@ -339,6 +342,8 @@ class NatureConvs:
             forms |= {"qhf", "qhd"}
         elif self.split_head_fwd(batch):
             forms.add("qhf")
+        if self.split_head_bwd(batch):
+            forms.add("qhd")
         return forms
 
     def pack(self, batch=0, zero=None):
@@ -347,7 +352,7 @@ class NatureConvs:
         (one ppox_nature_pack_all call for the split and fc forms).  `zero` (int32 tensor) is
         zeroed by that call when it runs: returns True if it did."""
         v = (self.flat.step_count, self.flat.data.data_ptr())
-        key = (batch, HEAD_SPLIT_MIN_BATCH, HEAD_FWD_SPLITK, FC_SPLIT_MIN_BATCH, DGRAD2_SPLIT_MAX_BATCH)  # (tests patch these)
+        key = (batch, HEAD_SPLIT_MIN_BATCH, HEAD_FWD_SPLITK, HEAD_BWD_SPLIT_MIN_BATCH, FC_SPLIT_MIN_BATCH)  # (tests patch these)
         if v == self._version and key == self._last_batch:  # the hot path: several times per minibatch
             return False
         if v != self._version:

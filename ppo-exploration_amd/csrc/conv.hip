@@ -438,6 +438,13 @@ struct GemmRowsProblem {
     }
     __device__ static int nchunk(const Tile&) { return KC; }
     __device__ static int bchunk_id(const Tile& t, int c) { return t.cb * KC + c; }
+    // B is packed in 64-column blocks; a 128-column tile (NB = 128) reads blocks 2 cb and 2 cb + 1
+    // (past the last block: the last again, its columns never stored)
+    static constexpr int NCB64 = (N + 63) / 64;
+    __device__ static int bchunk_blk(const Tile& t, int c, int b) {
+        const int blk = t.cb * (NB / 64) + b;
+        return (blk < NCB64 ? blk : NCB64 - 1) * KC + c;
+    }
     // branch-free (clamped indices), so an epilogue can issue all its loads before any wait
     // (HEAD_DGRAD: the mask and the accumulated grad)
     __device__ static auto prefetch(const Args& a, const Tile& t, int row, int col) {
@@ -494,8 +501,14 @@ struct Px : Base {
 #define FC_DGRAD_G 12  // fc dgrad: column blocks per tile group
 #endif
 #ifndef FC_NB
-#define FC_NB 64  // 128 measured no faster (one workgroup per CU: 86 KB LDS, 324 registers)
+#define FC_NB 64  // the packed fc / head B blocks (64 columns)
 #endif
+#ifndef SG_FC_NB
+#define SG_FC_NB 128  // columns per sg2 tile of the fc / head GEMMs (64: the round-3 tiles)
+#endif
+// column-block groups of the wide tiles: the same column span per group as the 64-column FC_*_G
+constexpr int FC_FWD_GW = FC_FWD_G * 64 / SG_FC_NB, FC_DGRAD_GW = FC_DGRAD_G * 64 / SG_FC_NB;
+constexpr int HEAD_GW = 512 / SG_FC_NB;
 using FcFwd = GemmRowsProblem<3136, 512, FC_NB, FC_FWD>;
 using FcDgrad = GemmRowsProblem<512, 3136, FC_NB, FC_DGRAD>;
 // the heads' hidden layer Linear(512, 512) + ReLU (models-checkpoint.py:62-66 extra_layer)
@@ -599,18 +612,19 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
     // triple t's 256 G rows (rows past the batch clamped; rows 243.. are never stored) ->
     // An, row r's 16-B chunk c at position c ^ (r & 15): 8 DMAs per thread
     auto dmaA = [&](long long t) {
-        const long long row0 = t * C2ROWS;
+        long long row0 = t * C2ROWS;
+        row0 = row0 < rows_total ? row0 : rows_total - 1;  // (past the last triple: clamped, never stored)
+        // uniform 64-bit base at the triple's first row + 32-bit byte offset (< 64 KB): the saddr
+        // form, whose address VGPR hipcc does not make each DMA wait for (vmcnt(0)) before reusing
+        const char* base = reinterpret_cast<const char*>(g2) + row0 * 256;
+        const long long last = rows_total - 1 - row0;
         static_assert(C2_ROW_DMAS * 512 * 16 == 256 * 256, "dmaA: 256 rows of 256 B per triple");
 #pragma unroll
         for (int j = 0; j < C2_ROW_DMAS; ++j) {
             const int r = (wave * 8 + j) * 4 + (lane >> 4), c = (lane & 15) ^ (r & 15);
-            long long grow = row0 + r;
-            grow = grow < rows_total ? grow : rows_total - 1;
-            // uniform base + 32-bit byte offset (host-checked < 2^32): the saddr form, whose
-            // address VGPR hipcc does not make each DMA wait for (vmcnt(0)) before reusing
-            const unsigned off = (unsigned)grow * 256u + (unsigned)c * 16u;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(
-                                                 reinterpret_cast<const char*>(g2) + off),
+            const unsigned rr = (unsigned)(r < last ? r : last);
+            const unsigned off = rr * 256u + (unsigned)c * 16u;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + off),
                                              (__attribute__((address_space(3))) void*)(An + (wave * 8 + j) * 64), 16,
                                              0, 0);
         }
@@ -815,22 +829,38 @@ __device__ inline void sg_lgkm_wait(u32x4 (&v)[6]) {
                  : "n"(N));
 }
 template <int N>
+__device__ inline void sg_lgkm_wait(u32x4 (&v)[10]) {
+    asm volatile("s_waitcnt lgkmcnt(%10)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+                   "+v"(v[8]), "+v"(v[9])
+                 : "n"(N));
+}
+template <int N>
 __device__ inline void sg_vm_wait() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // WAVES waves x 32 rows per workgroup, SLOTS ring slots of one 32-k chunk (A: 128 B per row;
-// B: 8 KB).  8 waves / 3 slots: one workgroup per CU, waves 4-7 staggered; 4 waves / 2 slots:
+// B: 8 KB per 64 columns).  8 waves / 3 slots: one workgroup per CU, waves 4-7 staggered; 4 waves / 2 slots:
 // two workgroups per CU (48 KB each), whose K walks, prologues and epilogues interleave on
 // every SIMD.  A is split in registers with its tensor's scale (a.amax_x), B was packed with
 // its own (a.wexp); the epilogue unscales, and records the output's amax (a.amax_y).
+// Prob::NOUT = 128 (round 4, the fc layer and the heads' hidden layer: "wide" tiles): each wave
+// runs 32 rows x 128 columns, the A fragments of a k-step feeding four column tiles, so A is
+// staged once per 128 output columns instead of once per 64; B is two consecutive 64-column
+// packed blocks (Prob::bchunk_blk), 16 KB per chunk.
 template <class Prob, int WAVES, int SLOTS>
 __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, const u32x4* __restrict__ wq) {
-    constexpr int NT = 2, ROWS = 32 * WAVES, AB = ROWS * BK * 4, SLOT = AB + SG_BQ * 16;
-    constexpr int BPW = (SG_BP + WAVES - 1) / WAVES;  // B pieces DMA'd per wave (1 KB each)
+    constexpr int NT = Prob::NOUT / 32, NBLK = NT / 2;  // column tiles; 64-column packed B blocks
+    constexpr int ROWS = 32 * WAVES, AB = ROWS * BK * 4, SLOT = AB + NBLK * SG_BQ * 16;
+    constexpr int BP = NBLK * SG_BP;                 // B pieces of a chunk (1 KB each)
+    constexpr int BPW = (BP + WAVES - 1) / WAVES;    // B pieces DMA'd per wave
     constexpr int NDMA = 4 + BPW;                  // this wave's DMAs per chunk
+    constexpr int NF = 2 + NT * NPL;                 // fragment reads per k-step
     constexpr bool STAGGER = WAVES == 8;
-    static_assert(Prob::NOUT == 64 && Prob::ROWS == ROWS, "sg2: 32 rows per wave x 64 columns");
+    static_assert((Prob::NOUT == 64 || (Prob::NOUT == 128 && !STAGGER)) && Prob::ROWS == ROWS,
+                  "sg2: 32 rows per wave x 64 or 128 columns");
+    static_assert(NF <= 15, "lgkmcnt is 4 bits");
     static_assert(SLOTS == 2 || SLOTS == 3, "sg2: two or three ring slots");
     // all LDS in ONE __shared__ object (a second one can make hipcc wait vmcnt(0) in the loop)
     __shared__ __attribute__((aligned(16))) uint8_t lds[SLOTS * SLOT];
@@ -849,11 +879,12 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
         asrc[j] = reinterpret_cast<const uint8_t*>(Prob::row_ptr(a, t, wave * 32 + r)) +
                   ((((lane & 7) ^ ((r >> 1) & 7))) << 4);
     }
-    // B: SG_BP pieces of 1 KB per chunk, BPW per wave (pieces past the last re-copy it: the
-    // same bytes to the same place), so every wave issues NDMA DMAs per chunk
+    // B: BP pieces of 1 KB per chunk, BPW per wave (pieces past the last re-copy it: the
+    // same bytes to the same place), so every wave issues NDMA DMAs per chunk; piece pc is piece
+    // pc % SG_BP of the chunk of 64-column block pc / SG_BP
     int bp[BPW];
 #pragma unroll
-    for (int i = 0; i < BPW; ++i) bp[i] = min(BPW * wave + i, SG_BP - 1);
+    for (int i = 0; i < BPW; ++i) bp[i] = min(BPW * wave + i, BP - 1);
     // operand scales: A by its tensor's amax (H1P planes: their exponent), B as packed; the epilogue
     // multiplies by both inverses
     const int ex = Prob::A_PLANES ? *a.xexp : split_scale_exp(amax_read(a.amax_x)), ew = *a.wexp;
@@ -880,12 +911,22 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void*)(asrc[j] + off),
                 (__attribute__((address_space(3))) void*)(base + (wave * 32 + 8 * j) * 128), 16, 0, 0);
-        const u32x4* bsrc = wq + (long long)Prob::bchunk_id(t, c) * SG_BQ + lane;
+        if constexpr (NBLK == 1) {
+            const u32x4* bsrc = wq + (long long)Prob::bchunk_id(t, c) * SG_BQ + lane;
 #pragma unroll
-        for (int i = 0; i < BPW; ++i)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc + bp[i] * 64),
-                                             (__attribute__((address_space(3))) void*)(base + AB + bp[i] * 1024), 16,
-                                             0, 0);
+            for (int i = 0; i < BPW; ++i)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc + bp[i] * 64),
+                                                 (__attribute__((address_space(3))) void*)(base + AB + bp[i] * 1024),
+                                                 16, 0, 0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < BPW; ++i) {
+                const u32x4* bsrc = wq + (long long)Prob::bchunk_blk(t, c, bp[i] / SG_BP) * SG_BQ + lane;
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(bsrc + (bp[i] % SG_BP) * 64),
+                    (__attribute__((address_space(3))) void*)(base + AB + bp[i] * 1024), 16, 0, 0);
+            }
+        }
     };
 
     f32x16 hi[NT], lo[NT];
@@ -907,7 +948,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
             mfma_split3(af, b2, hi[j], lo[j]);
         }
     };
-    auto split_a = [&](const u32x4 (&g)[6], u32x4 (&af)[NPL]) {
+    auto split_a = [&](const u32x4 (&g)[NF], u32x4 (&af)[NPL]) {
         if constexpr (Prob::A_PLANES) {  // H1P: the two pieces read are the planes
             af[0] = g[0];
             af[1] = g[1];
@@ -915,11 +956,11 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
             split8h(__builtin_bit_cast(float4, g[0]), __builtin_bit_cast(float4, g[1]), sa, af[0], af[1]);
         }
     };
-    // chunk in slot S: 12 fragment reads up front (k-step 0's six, then k-step 1's), k-step 0
-    // computed once its six have landed (lgkmcnt(6)) while k-step 1's are in flight
+    // chunk in slot S: 2 NF fragment reads up front (k-step 0's NF, then k-step 1's), k-step 0
+    // computed once its NF have landed (lgkmcnt(NF)) while k-step 1's are in flight
     auto compute = [&](auto S) {
         constexpr int slot = decltype(S)::value;
-        u32x4 f[2][6];
+        u32x4 f[2][NF];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             // the lane's 8 k of k-step s: f32 pieces g0, g0 + 1 (16 B = 4 values each), or H1P
@@ -931,10 +972,12 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
             for (int j = 0; j < NT; ++j)
 #pragma unroll
                 for (int p = 0; p < NPL; ++p)
-                    f[s][2 + NPL * j + p] = sg_ds_read(b_lane + slot * SLOT + (((s * NT + j) * NPL + p) * 64) * 16);
+                    // column tile j: tile j & 1 of 64-column block j >> 1 (split_frag_index: [s][j][p][lane])
+                    f[s][2 + NPL * j + p] = sg_ds_read(b_lane + slot * SLOT + (j >> 1) * (SG_BQ * 16) +
+                                                       (((s * 2 + (j & 1)) * NPL + p) * 64) * 16);
         }
         u32x4 af[NPL];
-        sg_lgkm_wait<6>(f[0]);
+        sg_lgkm_wait<NF>(f[0]);
         split_a(f[0], af);
         mfma3(af, f[0] + 2);
         sg_lgkm_wait<0>(f[1]);
@@ -1004,7 +1047,7 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
                 // every lane runs the pair swap; the pair (col & ~1, col | 1) shares its row, so both
                 // lanes store or neither does
                 v = Prob::value(a, t, row, col, (hi[j][q] + lo[j][q]) * ua * uw, e[q]);
-                const uint32_t w = px_pair_word(v * sy, lane & 1);
+                const uint32_t w = px_pair_word(v, sy, lane & 1);
                 const long long el = Prob::out_elem(a, t, row, col & ~1);
                 if (el >= 0) *reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(a.y) + px_index(el) + 32 * (lane & 1)) = w;
             } else {
@@ -1147,9 +1190,9 @@ struct SgDgradPM : DgradPMProblem<L, 1> {
 // (G x 196 KB / 1.2 MB for the dgrad / forward) stays in that XCD's L2 while its row tiles
 // stream past (A is read NCB / G times, B about once per XCD).
 // BITS_IN (FC_DGRAD): h3's ReLU mask from the conv3 forward's bitmask (N / 32 words per row)
-template <int K, int N, int MODE, int G, bool BITS_IN = false>
-struct SgRows : GemmRowsProblem<K, N, 64, MODE> {
-    using Base = GemmRowsProblem<K, N, 64, MODE>;
+template <int K, int N, int MODE, int G, bool BITS_IN = false, int NB = 64>
+struct SgRows : GemmRowsProblem<K, N, NB, MODE> {
+    using Base = GemmRowsProblem<K, N, NB, MODE>;
     static constexpr int ROWS = SG_ROWS, NCB = Base::NCB;
     static constexpr bool BITS_OUT = false;
     static constexpr int SLOTS = 3;
@@ -1158,7 +1201,7 @@ struct SgRows : GemmRowsProblem<K, N, 64, MODE> {
             return Base::prefetch(a, t, row, col);
         } else {
             static_assert(MODE == FC_DGRAD && N % 32 == 0, "bitmask: the fc dgrad's h3 mask");
-            const int n = t.cb * 64 + col, nc = n < N ? n : N - 1;
+            const int n = t.cb * NB + col, nc = n < N ? n : N - 1;
             long long m = t.m0 + row;
             m = m < t.M ? m : t.m0;
             const uint32_t w = a.bits_mask[m * (N / 32) + (nc >> 5)];
@@ -2225,13 +2268,13 @@ __global__ void __launch_bounds__(512, 1) wgrad2_planes_kernel(W2PArgs a) {
         hsrc[j] = (uint32_t)((y * 20 + x) * 128 + P * 64 + piece * 16);
     }
     auto dma_h = [&](long long n, int buf) {
-        const uint32_t nb = (uint32_t)n * (uint32_t)W2P_SAMPLE;  // host-checked: batch * 51200 < 2^32
+        const char* sb = reinterpret_cast<const char*>(a.h1p) + n * W2P_SAMPLE;  // uniform 64-bit sample base
 #pragma unroll
         for (int j = 0; j < W2P_NDMA; ++j) {
             int i = wave * W2P_NDMA + j;
             i = i < 49 ? i : 49;
             __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(reinterpret_cast<const char*>(a.h1p) + (nb + hsrc[j])),
+                (const __attribute__((address_space(1))) void*)(sb + hsrc[j]),
                 (__attribute__((address_space(3))) void*)(lds + W2P_H0 + buf * W2P_HB + i * 1024), 16, 0, 0);
         }
     };
@@ -3307,7 +3350,8 @@ extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_
     PPOX_REQUIRE(workspace_bytes >= ppox_nature_wgrad_split_workspace_bytes(layer, batch),
                  "ppox_nature_conv_wgrad_split: workspace too small");
     PPOX_REQUIRE(ppox::aligned16(grad_out), "ppox_nature_conv_wgrad_split: grad_out must be 16B aligned");
-    PPOX_REQUIRE(batch * (layer == 1 ? G1::P : layer == 2 ? G2::P : G3::P) < (1LL << 31) / 64,
+    PPOX_REQUIRE((layer == 1 && !wgrad1_im2col()) ||
+                     batch * (layer == 1 ? G1::P : layer == 2 ? G2::P : G3::P) < (1LL << 31) / 64,
                  "ppox_nature_conv_wgrad_split: batch too large for 32-bit pixel indexing");
     hipStream_t s = ppox::as_stream(stream);
     if (layer == 1) {
@@ -3341,10 +3385,10 @@ extern "C" int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, in
                  "ppox_nature_conv_wgrad_split_idx: workspace too small");
     PPOX_REQUIRE(ppox::aligned16(grad_out) && !(reinterpret_cast<uintptr_t>(x) & 3),
                  "ppox_nature_conv_wgrad_split_idx: alignment");
-    PPOX_REQUIRE(batch * G1::P < (1LL << 31) / 64, "ppox_nature_conv_wgrad_split_idx: batch too large");
-    if (!wgrad1_im2col())
+    if (!wgrad1_im2col())  // (the direct form indexes in 64 bits)
         return launch_wgrad1_frames(x, 0, reinterpret_cast<const long long*>(idx), T, N_env, grad_out, batch, workspace,
                                     workspace_bytes, dw, db, amax_g, ppox::as_stream(stream));
+    PPOX_REQUIRE(batch * G1::P < (1LL << 31) / 64, "ppox_nature_conv_wgrad_split_idx: batch too large");
     return Ws1::run(x, 0, grad_out, batch, workspace, dw, db, nullptr, amax_g, ppox::as_stream(stream),
                     reinterpret_cast<const long long*>(idx), T, N_env);
 }
@@ -3421,7 +3465,6 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
     if (layer == 2) {
         PPOX_REQUIRE(!g_exp, "ppox_nature_conv_dgrad_split: layer 2 reads an f32 g2");
         const long long ntriples = ppox::ceil_div(batch, (long long)C2S);
-        PPOX_REQUIRE(batch * G2::P * 256 < (1LL << 32), "ppox_nature_conv_dgrad_split: batch too large (32-bit offsets)");
         // one workgroup per CU (150 KB of LDS each), striding over the triples
         static int cus[64] = {};
         int dev = 0;
@@ -3543,7 +3586,6 @@ extern "C" int ppox_nature_conv2_wgrad_planes(const uint16_t* h1p, const uint16_
     PPOX_REQUIRE(ppox::aligned16(h1p) && ppox::aligned16(grad_out) && ppox::aligned16(amax_g) &&
                      ppox::aligned16(workspace),
                  "ppox_nature_conv2_wgrad_planes: 16B alignment");
-    PPOX_REQUIRE(batch * (long long)W2P_SAMPLE < (1LL << 32), "ppox_nature_conv2_wgrad_planes: batch too large");
     PPOX_REQUIRE(cu_count() > 0, "ppox_nature_conv2_wgrad_planes: no device");
     PPOX_REQUIRE(workspace_bytes >= ppox_nature_conv2_wgrad_planes_workspace_bytes(batch),
                  "ppox_nature_conv2_wgrad_planes: workspace too small");
@@ -3725,12 +3767,12 @@ extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t
                  "ppox_nature_fc_fwd: 16B alignment");
     Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, amax_h3, amax_f, pack_exp(q_fwd, PL_FCF)};
     a.xexp = h3_exp;  // PX h3 (the conv3 forward's planes output)
-    const long long blocks = ppox::ceil_div(batch, SG_ROWS) * FcFwd::NCB;
+    const long long blocks = ppox::ceil_div(batch, SG_ROWS) * (512 / SG_FC_NB);
     if (h3_exp)
-        return launch_sgemm<Px<SgRows<3136, 512, FC_FWD, FC_FWD_G>, true>>(a, q_fwd, blocks, ppox::as_stream(stream),
-                                                                          "ppox_nature_fc_fwd");
-    return launch_sgemm<SgRows<3136, 512, FC_FWD, FC_FWD_G>>(a, q_fwd, blocks, ppox::as_stream(stream),
-                                                             "ppox_nature_fc_fwd");
+        return launch_sgemm<Px<SgRows<3136, 512, FC_FWD, FC_FWD_GW, false, SG_FC_NB>, true>>(
+            a, q_fwd, blocks, ppox::as_stream(stream), "ppox_nature_fc_fwd");
+    return launch_sgemm<SgRows<3136, 512, FC_FWD, FC_FWD_GW, false, SG_FC_NB>>(a, q_fwd, blocks, ppox::as_stream(stream),
+                                                                             "ppox_nature_fc_fwd");
 }
 
 extern "C" int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch) {
@@ -3782,19 +3824,21 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
                  "ppox_nature_fc_dgrad: 16B alignment");
     Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch, amax_df, amax_g3, pack_exp(q_dgrad, PL_FCD)};
     a.bits_mask = relu_bits;  // h3's ReLU bitmask from the conv3 forward (instead of h3)
+    const long long blocks = ppox::ceil_div(batch, SG_ROWS) * ppox::ceil_div(3136, SG_FC_NB);
     if (g3_exp_out) {  // g3 as PX planes, bounded by amax(df) * the fc weight's column norms
         PPOX_REQUIRE(relu_bits, "ppox_nature_fc_dgrad: a PX g3 needs h3's ReLU bitmask");
         a.yexp_out = g3_exp_out;
         a.ynorm = pack_norm(q_dgrad, PL_FCD);
         a.ybias = pack_bmax(q_dgrad, PL_FCD);
-        return launch_sgemm<Px<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_G, true>, false, true>>(
-            a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB, ppox::as_stream(stream), "ppox_nature_fc_dgrad");
+        return launch_sgemm<Px<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_GW, true, SG_FC_NB>, false, true>>(
+            a, q_dgrad, blocks, ppox::as_stream(stream), "ppox_nature_fc_dgrad");
     }
     if (relu_bits)
-        return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_G, true>>(
-            a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB, ppox::as_stream(stream), "ppox_nature_fc_dgrad");
-    return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_G>>(a, q_dgrad, ppox::ceil_div(batch, SG_ROWS) * FcDgrad::NCB,
-                                                     ppox::as_stream(stream), "ppox_nature_fc_dgrad");
+        return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_GW, true, SG_FC_NB>>(
+            a, q_dgrad, blocks, ppox::as_stream(stream), "ppox_nature_fc_dgrad");
+    return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_GW, false, SG_FC_NB>>(a, q_dgrad, blocks,
+                                                                                  ppox::as_stream(stream),
+                                                                                  "ppox_nature_fc_dgrad");
 }
 
 extern "C" int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, const float* b2,
@@ -3822,8 +3866,8 @@ extern "C" int ppox_head_hidden_fwd(const float* f, int64_t rows, const uint16_t
     PPOX_REQUIRE(ppox::aligned16(f) && ppox::aligned16(q_fwd) && ppox::aligned16(amax_f),
                  "ppox_head_hidden_fwd: 16B alignment");
     Args a{f, nullptr, 0, 0, 0, nullptr, bias, nullptr, e, rows, amax_f, nullptr, pack_exp(q_fwd, PL_H)};
-    return launch_sgemm<SgRows<512, 512, FC_FWD, 8>>(a, q_fwd, ppox::ceil_div(rows, SG_ROWS) * HeadFwd::NCB,
-                                                      ppox::as_stream(stream), "ppox_head_hidden_fwd");
+    return launch_sgemm<SgRows<512, 512, FC_FWD, HEAD_GW, false, SG_FC_NB>>(
+        a, q_fwd, ppox::ceil_div(rows, SG_ROWS) * (512 / SG_FC_NB), ppox::as_stream(stream), "ppox_head_hidden_fwd");
 }
 
 extern "C" int64_t ppox_head_hidden_fwd_splitk_workspace_bytes(int64_t rows) {
@@ -3864,8 +3908,8 @@ extern "C" int ppox_head_hidden_dgrad(const float* de, int64_t rows, const uint1
     PPOX_REQUIRE(ppox::aligned16(de) && ppox::aligned16(q_dgrad) && ppox::aligned16(amax_de),
                  "ppox_head_hidden_dgrad: 16B alignment");
     Args a{de, nullptr, 0, 0, 0, nullptr, nullptr, f, df, rows, amax_de, amax_df, pack_exp(q_dgrad, PL_H)};
-    return launch_sgemm<SgRows<512, 512, HEAD_DGRAD, 8>>(a, q_dgrad, ppox::ceil_div(rows, SG_ROWS) * HeadDgrad::NCB,
-                                                          ppox::as_stream(stream), "ppox_head_hidden_dgrad");
+    return launch_sgemm<SgRows<512, 512, HEAD_DGRAD, HEAD_GW, false, SG_FC_NB>>(
+        a, q_dgrad, ppox::ceil_div(rows, SG_ROWS) * (512 / SG_FC_NB), ppox::as_stream(stream), "ppox_head_hidden_dgrad");
 }
 
 extern "C" int64_t ppox_head_hidden_wgrad_workspace_bytes(int64_t rows) {

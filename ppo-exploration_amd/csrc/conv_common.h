@@ -281,16 +281,17 @@ __device__ inline int bound_exp(uint32_t amax_x, uint32_t norm, uint32_t bmax) {
 }
 // uint16 index of the high half of element e (its low half: + 32)
 __host__ __device__ inline long long px_index(long long e) { return 2 * (e & ~31LL) + (e & 31); }
-// one value of a column pair (col, col ^ 1) held by lanes L, L ^ 1 (same row), times 2^E: the
-// 4-B word lane L stores after one DPP swap — the even lane the pair's two high halves, the odd
+// one value v of a column pair (col, col ^ 1) held by lanes L, L ^ 1 (same row), scaled by s = 2^E:
+// the 4-B word lane L stores after one DPP swap — the even lane the pair's two high halves, the odd
 // lane their two low halves (at px_index(e_even) and px_index(e_even) + 32): as many 4-B stores as
 // the f32 form.  Every lane of the wave must execute it (the swap reads the partner lane).
-__device__ inline uint32_t px_pair_word(float vs, bool odd) {
-    const _Float16 hv = (_Float16)vs;
-    const _Float16 lv = (_Float16)(vs - (float)hv);  // exact in f32
-    const uint32_t w = (uint32_t)__builtin_bit_cast(uint16_t, hv) | ((uint32_t)__builtin_bit_cast(uint16_t, lv) << 16);
-    const uint32_t pw = (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    return odd ? ((pw >> 16) | (w & 0xFFFF0000u)) : ((w & 0xFFFFu) | (pw << 16));
+__device__ inline uint32_t px_pair_word(float v, float s, bool odd) {
+    // the partner's value (quad_perm [1,0,3,2]), then the pair (even column first) split at once:
+    // one packed scale, one packed convert per plane and one v_fma_mix per residual (split2h)
+    const float pv = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+    uint32_t h, l;
+    split2h(odd ? (f32x2){pv, v} : (f32x2){v, pv}, s, h, l);
+    return odd ? l : h;
 }
 // the f32 value hi + lo (exact) of half H (0: low, 1: high) of a high-plane word and a low-plane word
 __device__ inline float px_value(uint32_t hw, uint32_t lw, int H) {

@@ -29,6 +29,15 @@ class DistContext:
             return cls(tdist.get_rank(), tdist.get_world_size())
         return cls()
 
+    def subgroup(self):
+        """A context over the same ranks on a communicator of its own (a collective call: every rank
+        makes it, in the same order).  Its collectives are ordered only among themselves, so they
+        can run on a side stream beside this context's (PPO_ICM's curiosity-module exchange beside
+        the policy's loss and gradient all-reduces) without queueing behind them."""
+        if not (tdist.is_available() and tdist.is_initialized()):
+            return self
+        return DistContext(self.rank, self.world, group=tdist.new_group(ranks=list(range(self.world))))
+
     def all_reduce_(self, t):
         if self.enabled:
             tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=self.group)

@@ -242,7 +242,7 @@ class CnnActorCritic(nn.Module):
             side = _convs.side_stream(dout.device) if _convs.BWD_STREAMS and dout.is_cuda else None
             cur = _convs.current_stream(dout.device) if side is not None else None
             cv = self.conv_impl
-            split = cv.split_head(B)  # the extra layer's dgrad / weight gradient on the split-f16 kernels
+            split = cv.split_head_bwd(B)  # the extra layer's dgrad / weight gradient on the split-f16 kernels
             des = []
             # the actor head's input grad and the extra layer's dv * w_critic * ReLU' in one launch
             df, de0 = native.head_dgrad_outer(dout, a.weight, dv.contiguous().view(B), self.critic_ext.weight, e,

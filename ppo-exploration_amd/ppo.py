@@ -796,6 +796,10 @@ class PPO_ICM(BaseAlgorithm):
         self.beta = 0.2
         self._alloc_train_state()
         self.icm_accum = torch.zeros(1, dtype=torch.float64, device=self.device)
+        # the K11 minibatch's collectives (feature / action / feature-gradient exchange, the ICM
+        # gradient all-reduce) on a communicator of their own, so that at world > 1 they run on
+        # the side stream beside the policy minibatch as in one process (DistContext.subgroup)
+        self._icm_dist = self.dist.subgroup() if self.dist.enabled and self._icm_native is not None else self.dist
         # the collect loop (policy + env + K11 curiosity reward) as one captured graph, as PPO's
         # (PPOX_COLLECT_GRAPH=0: eager launches)
         self._collect_graph_enabled = os.environ.get("PPOX_COLLECT_GRAPH", "1") != "0"
@@ -958,15 +962,17 @@ class PPO_ICM(BaseAlgorithm):
         ro = self.rollout
         Bl = idx.numel()
         # the ICM (independent of the policy: its own parameters, the same frames) runs on a
-        # side stream beside the policy's forward / loss / backward (one process; with ranks
-        # its collectives keep the program order on every rank, so it stays on this stream)
-        side = convs.side_stream(self.device, 1) if convs.BWD_STREAMS and not self.dist.enabled else None
+        # side stream beside the policy's forward / loss / backward, its collectives (world > 1)
+        # on its own communicator (self._icm_dist), issued in the same program order on every rank
+        side = convs.side_stream(self.device, 1) if convs.BWD_STREAMS else None
         pos = self._epoch_pos[o0:o1] if self.dist.enabled else None
+        idist = self._icm_dist
         if side is not None:
             convs.fork(side)
             with torch.cuda.stream(side):
                 self._icm_native.train_minibatch(convs.RolloutRows(ro.observations, idx), ro.actions, pos, B,
-                                                 self.beta, self.dist, self.icm_accum)
+                                                 self.beta, idist, self.icm_accum)
+                idist.all_reduce_(self.icm_flat.grad)
         self._zero_policy_grad(Bl)
         ctx = out = v = None
         if Bl > 0:
@@ -978,10 +984,10 @@ class PPO_ICM(BaseAlgorithm):
         self._bwd_reduce(ctx, out, v, None, dout, dv, has_rows=Bl > 0)
         if side is None:
             self._icm_native.train_minibatch(convs.RolloutRows(ro.observations, idx), ro.actions, pos, B,
-                                             self.beta, self.dist, self.icm_accum)
+                                             self.beta, idist, self.icm_accum)
+            idist.all_reduce_(self.icm_flat.grad)
         else:
             convs.join(side)
-        self.dist.all_reduce_(self.icm_flat.grad)
         self.flat.adam_step(self.lr, self.max_grad_norm)                       # ppo.py:697-698
         self.icm_flat.adam_step(self.int_lr, None)                             # ppo.py:699 (no clipping)
 

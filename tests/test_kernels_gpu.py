@@ -1516,3 +1516,43 @@ def test_current_stream_orders_like_torch():
     s2 = torch.cuda.Stream()
     with torch.cuda.stream(s2):
         assert convs.current_stream(dev).cuda_stream == s2.cuda_stream
+
+
+def test_big_minibatch_offsets_are_64bit():
+    """the direct conv2 weight gradient (H1P samples 51,200 B apart) and the persistent
+    conv2 dgrad (G rows 256 B apart) address their operands in 64 bits, so a full-rollout minibatch
+    (batch_size=None, buffer.py:249) past the old 32-bit limits (83,886 / 207,126 rows) trains: the
+    samples beyond the limit contribute what they contribute alone (same operand scales)."""
+    import native
+    g = torch.Generator(device="cuda").manual_seed(5)
+    w1 = torch.randn(32, 4, 8, 8, device="cuda", generator=g) * 0.02
+    w2 = torch.randn(64, 32, 4, 4, device="cuda", generator=g) * 0.05
+    w3 = torch.randn(64, 64, 3, 3, device="cuda", generator=g) * 0.05
+    b1 = torch.randn(32, device="cuda", generator=g)
+    q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device="cuda") for k in (1, 2, 3, 12)}
+    native.nature_pack_all(w1, w2, w3, None, None, q[1], q[2], q[3], q[12], None, None, None, b1=b1)
+    B, cut = 90000, 80000
+    h1p = torch.zeros(B, 20, 20, 64, dtype=torch.int16, device="cuda")  # hi planes random, lo planes zero
+    h1p.view(B, 400, 64)[:, :, :32] = (torch.rand(B, 400, 32, device="cuda", generator=g) * 100).half().view(torch.int16)
+    g2 = torch.randn(B, 9, 9, 64, device="cuda", generator=g)
+    am = native.amax_table(1, "cuda")[0]
+    native.amax(g2, am)
+    ws = torch.empty(native.nature_conv2_wgrad_planes_workspace_bytes(B), dtype=torch.uint8, device="cuda")
+    res = []
+    for lo, hi in ((0, B), (0, cut), (cut, B)):
+        dw, db = torch.empty(64, 32, 4, 4, device="cuda"), torch.empty(64, device="cuda")
+        native.nature_conv2_wgrad_planes(h1p[lo:hi], q[1], hi - lo, g2[lo:hi], ws, dw, db, amax_g=am)
+        res.append((dw.double(), db.double()))
+    for k in range(2):
+        whole, parts = res[0][k], res[1][k] + res[2][k]
+        assert (whole - parts).abs().max().item() <= 1e-5 * whole.abs().max().item()
+    del h1p, ws
+    B = 210000
+    g2 = torch.randn(B, 9, 9, 64, device="cuda", generator=g)
+    bits = torch.randint(-2 ** 31, 2 ** 31 - 1, (B * 400,), dtype=torch.int32, device="cuda", generator=g)
+    native.amax(g2, am)
+    out = torch.empty(B, 20, 20, 32, device="cuda")
+    native.nature_conv_dgrad_split(2, g2, B, q[12], None, out, amax_g=am, relu_bits=bits)
+    tail = torch.empty(30, 20, 20, 32, device="cuda")
+    native.nature_conv_dgrad_split(2, g2[-30:], 30, q[12], None, tail, amax_g=am, relu_bits=bits[-30 * 400:])
+    assert torch.equal(out[-30:], tail)

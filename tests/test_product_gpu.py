@@ -358,7 +358,7 @@ def test_cnn_train_matches_reference_run(golden, name, math, rtol, head_min, mon
     alg.train()
     sd = alg.policy.net.state_dict()
     lr = alg.lr
-    wstats = {}
+    wstats, fails = {}, []
     for k, (key, v) in enumerate(sd.items()):
         idx = f[p + "w1idx_" + key]
         assert np.array_equal(idx, _weight_sample_index(v.numel(), k))
@@ -369,11 +369,12 @@ def test_cnn_train_matches_reference_run(golden, name, math, rtol, head_min, mon
         # of a pre-activation within rounding of zero differently (a ReLU-boundary flip), which
         # moves that unit's weights by a fraction of an Adam step
         frac = float((err > rtol * np.abs(ref) + 2e-6).mean())
-        wstats[key] = {"max_err": float(err.max()), "max_err_over_lr": float(err.max()) / lr, "frac_beyond_strict": frac}
-        assert (err <= rtol * np.abs(ref) + 0.05 * lr).all(), (key, float(err.max()))
-        assert frac <= 2e-3, (key, frac)
         d = (v.double().cpu() - init[key].double())
-        np.testing.assert_allclose(float(d.abs().sum()), float(f[p + "dabs_" + key]), rtol=2e-3, err_msg=key)
+        dabs_rel = abs(float(d.abs().sum()) - float(f[p + "dabs_" + key])) / float(f[p + "dabs_" + key])
+        wstats[key] = {"max_err": float(err.max()), "max_err_over_lr": float(err.max()) / lr, "frac_beyond_strict": frac,
+                       "dabs_rel": dabs_rel}
+        if not ((err <= rtol * np.abs(ref) + 0.05 * lr).all() and frac <= 2e-3 and dabs_rel <= 2e-3):
+            fails.append((key, wstats[key]))
     np.testing.assert_array_equal(np.random.get_state()[1], f[p + "np_state_after"])
     acc = alg.loss_accum.cpu().numpy()
     n = acc[5]
@@ -389,7 +390,9 @@ def test_cnn_train_matches_reference_run(golden, name, math, rtol, head_min, mon
                       "rel_ref_f64": abs(ref - x64) / abs(x64)}
     _parity_report(f"cnn_train_{name}_{math}_{head_min}", {"losses": stats, "weights": wstats})
     for i, key in ((0, "policy_gradient_loss"), (1, "value_loss"), (2, "entropy_loss"), (3, "total_loss")):
-        assert _loss_ok(key, float(acc[i] / n), float(f[p + key]), float(f[p + "f64_" + key])), (key, stats[key])
+        if not _loss_ok(key, float(acc[i] / n), float(f[p + key]), float(f[p + "f64_" + key])):
+            fails.append((key, stats[key]))
+    assert not fails, fails
 
 
 def _loss_ok(key, got, ref, x64):
@@ -432,10 +435,11 @@ def test_cnn_train_16384_rows_matches_reference_run(golden, math, monkeypatch):
     error e_ref = |ref - f64| measured on this trajectory:
       * weights, per tensor: max |prod - f64| <= 3 max e_ref + 2e-6 and mean |prod - f64| <=
         3 mean e_ref + 1e-8 — the product is as close to exact arithmetic as the reference is,
-        within a factor 3 (measured: split 0.3-2.0x, exact-f32 MFMA 0.8-2.5x); plus every weight within rtol |ref| + lr of the reference (one Adam
-        step: Adam's first steps move a weight by +-lr whatever its gradient's size, so a weight
-        whose gradient is zero to rounding moves either way — the reference's own run is up to
-        a third of a step off exact arithmetic here) with at most 0.5 % beyond rtol |ref| + 2e-6;
+        within a factor 3 (measured: split 0.3-2.0x, exact-f32 MFMA 0.8-2.5x); plus every weight within
+        rtol |ref| + 0.1 lr of the reference but for at most 0.2 % outliers, which stay within one Adam
+        step (rtol |ref| + lr: Adam's first steps move a weight by +-lr whatever its gradient's size,
+        so a weight whose gradient is zero to rounding moves either way — the reference's own run is
+        up to a third of a step off exact arithmetic here), and at most 0.5 % beyond rtol |ref| + 2e-6;
       * losses: policy-gradient, value, total within 1e-5 relative of the reference; the entropy
         of the near-saturated softmax within max(2 e_ref, 1e-5 |f64|) of float64."""
     import env as E
@@ -522,6 +526,7 @@ def test_cnn_train_16384_rows_matches_reference_run(golden, math, monkeypatch):
         ref, w64 = f[p + "w1_" + key].astype(np.float64), f[p + "w64_" + key]
         e_p, e_r, e_pr = np.abs(w - w64), np.abs(ref - w64), np.abs(w - ref)
         frac = float((e_pr > rtol * np.abs(ref) + 2e-6).mean())
+        frac_lr = float((e_pr > rtol * np.abs(ref) + 0.1 * lr).mean())
         d_abs = float((v.double().cpu() - init[key].double()).abs().sum())
         g, g32, g64 = grads[key][idx].astype(np.float64), f[p + "g32_" + key], f[p + "g64_" + key]
         gs = np.abs(g64).max()
@@ -532,10 +537,11 @@ def test_cnn_train_16384_rows_matches_reference_run(golden, math, monkeypatch):
                                               "mean_ref_f64_rel": float(np.abs(g32 - g64).mean() / gs)}
         stats["weights"][key] = {"max_prod_f64": float(e_p.max()), "max_ref_f64": float(e_r.max()),
                                  "mean_prod_f64": float(e_p.mean()), "mean_ref_f64": float(e_r.mean()),
-                                 "max_prod_ref": float(e_pr.max()), "frac_beyond_strict": frac,
+                                 "max_prod_ref": float(e_pr.max()), "max_prod_ref_over_lr": float(e_pr.max()) / lr,
+                                 "frac_beyond_strict": frac, "frac_beyond_tenth_lr": frac_lr,
                                  "dabs_rel": abs(d_abs - float(f[p + "d64abs_" + key])) / float(f[p + "d64abs_" + key])}
         if not (e_p.max() <= 3 * e_r.max() + 2e-6 and e_p.mean() <= 3 * e_r.mean() + 1e-8
-                and (e_pr <= rtol * np.abs(ref) + lr).all() and frac <= 5e-3):
+                and (e_pr <= rtol * np.abs(ref) + lr).all() and frac_lr <= 2e-3 and frac <= 5e-3):
             fails.append((key, stats["weights"][key]))
     acc = alg.loss_accum.cpu().numpy()
     n = acc[5]
