@@ -54,9 +54,8 @@ HEAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_SPLIT_MIN", "8192"))
 # PPOX_HEAD_FWD_SPLITK=0 keeps the library GEMM
 HEAD_FWD_SPLITK = os.environ.get("PPOX_HEAD_FWD_SPLITK", "1") == "1"
 # the hidden layer's backward (dgrad into the fc layer's input grad + weight gradient) on the split-f16
-# kernels from this batch up, the library GEMMs below (PPOX_HEAD_BWD_SPLIT_MIN; round 4: every batch —
-# the 128-column tiles, and a library GEMM call costs ~35-60 us of host time per minibatch)
-HEAD_BWD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_BWD_SPLIT_MIN", "0"))
+# kernels from this batch up, the library GEMMs below (PPOX_HEAD_BWD_SPLIT_MIN)
+HEAD_BWD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_BWD_SPLIT_MIN", "8192"))
 
 # ReLU masks of the conv outputs as bitmasks written by the split forwards for the split dgrads
 # (PPOX_RELU_BITS=0: the dgrads read the f32 activations)
@@ -76,6 +75,10 @@ EX_H2, EX_H3, EX_G3 = range(3)
 # registers.  PPOX_PX=0: f32 tensors (split in the consumers).  Needs the ReLU bitmasks (the
 # dgrads' masks cannot come from planes).
 PX = os.environ.get("PPOX_PX", "1") != "0"
+# ... from this batch up (PPOX_PX_MIN): at the 8-GPU per-rank minibatch of 2,048 rows PX measured
+# slower (same-box A/B 225.8 vs 219.5 ms per iteration: the producers' epilogues sit on the main
+# stream, the consumers it speeds up on the side stream), at 16,384 rows faster
+PX_MIN_BATCH = int(os.environ.get("PPOX_PX_MIN", "8192"))
 
 
 class PassState:
@@ -313,7 +316,7 @@ class NatureConvs:
     def px_g3(self, B, am):
         """g3 as PX planes: the fc dgrad is the fused split kernel with h3's bitmask, the conv3 dgrad runs
         split with conv2's bitmask"""
-        return (self.px and isinstance(am, PassState) and am.bits[2] is not None and am.bits[1] is not None
+        return (self.px and B >= PX_MIN_BATCH and isinstance(am, PassState) and am.bits[2] is not None and am.bits[1] is not None
                 and B < FC_DGRAD_FUSED_MAX_BATCH and self.uses_split("dgrad", 3, B) and self.uses_split("wgrad", 3))
 
     def workspace(self, layer, batch, split=False):
@@ -470,7 +473,7 @@ class NatureConvs:
         allow; am.px says which."""
         B = x.shape[0]
         dev = x.device
-        px = self.px if px is None else (px and self.px)
+        px = (self.px if px is None else (px and self.px)) and B >= PX_MIN_BATCH
         # the pass's amax table: zeroed by the weight packing when this pass runs it (the first
         # pass after an optimizer step), by a fill otherwise
         table = torch.empty((AM_ROWS, native.AMAX_SLOTS), dtype=torch.int32, device=dev)

@@ -504,7 +504,10 @@ struct Px : Base {
 #define FC_NB 64  // the packed fc / head B blocks (64 columns)
 #endif
 #ifndef SG_FC_NB
-#define SG_FC_NB 128  // columns per sg2 tile of the fc / head GEMMs (64: the round-3 tiles)
+// columns per sg2 tile of the fc / head GEMMs: 64; 128 (A staged once per 128 columns, four
+// column tiles per wave) measured slower — 358 registers, one wave per SIMD (round 4 same-box
+// A/B: 1-GPU 427.4k vs 439.6k env-steps/s, per-rank 225.8 vs 215.5 ms)
+#define SG_FC_NB 64
 #endif
 // column-block groups of the wide tiles: the same column span per group as the 64-column FC_*_G
 constexpr int FC_FWD_GW = FC_FWD_G * 64 / SG_FC_NB, FC_DGRAD_GW = FC_DGRAD_G * 64 / SG_FC_NB;

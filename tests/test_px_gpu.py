@@ -11,6 +11,13 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _px_at_every_batch(monkeypatch):
+    """the PX machinery at every batch size (the product turns it on from convs.PX_MIN_BATCH rows)"""
+    import convs
+    monkeypatch.setattr(convs, "PX_MIN_BATCH", 0)
+
+
 def _setup(seed, A=4, intrinsic=False):
     import convs
     import models
