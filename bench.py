@@ -284,6 +284,11 @@ def parse():
 
 def main():
     args = parse()
+    # stdout carries the one JSON line only: whatever else writes to fd 1 (RCCL prints its version
+    # banner there when a communicator is created) goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import numpy as np
     import torch
     import torch.distributed as tdist
@@ -475,7 +480,7 @@ def main():
         out["cpu_baseline"] = atari_ppo_iteration_rate(args.envs, args.nstep, args.epochs, args.batch_size,
                                                        threads=args.cpu_threads or None)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if world > 1 or args.force_dist:
         tdist.destroy_process_group()
 
@@ -536,7 +541,7 @@ def bench_es(args, world, rank, tdist):
                            "mean_us": round(mean_ms * 1e3, 1), "launches": len(kt),
                            "alg_flops_per_launch": flops}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
         tdist.destroy_process_group()
 

@@ -539,7 +539,8 @@ int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, int64_t batch
  *                        phi (B x 32): the inverse / forward models, both losses (means over
  *                        n_pairs_global pairs, weights 1 - beta / beta) and their backward.
  *                        actions of row j: actions[rowno ? rowno[j] : j].  pairs: the first
- *                        rows of the evaluated pairs (NULL: all j < B - 1, n_pairs = B - 1).
+ *                        rows of the evaluated pairs (NULL: all j < B - 1, n_pairs = B - 1;
+ *                        a listed B - 1 has no pair and is skipped, n_pairs <= B).
  *                        dS[j] / dN[j + 1] (B x 32) = dL/dphi through a pair's first / second
  *                        row (with pairs == NULL every row of both is written).  partials:
  *                        ppox_icm_partials_bytes(rows, n_actions).

@@ -467,6 +467,7 @@ __global__ void __launch_bounds__(256) icm_pair_kernel(PairArgs a) {
         const long long jj = blockIdx.x * (long long)PB + tid;
         long long j = -1;
         if (jj < a.npl) j = a.pairs ? a.pairs[jj] : jj;
+        if (j >= a.B - 1) j = -1;  // a listed position with no pair (the minibatch's last row)
         jrow[tid] = j;
         act[tid] = j >= 0 ? a.actions[a.rowno ? (long long)a.rowno[j] : j] : 0;
     }
@@ -995,7 +996,7 @@ extern "C" int ppox_icm_pair_backward(const float* phi, int64_t B, const int32_t
                                       const int64_t* pairs, int64_t n_pairs, int64_t n_pairs_global,
                                       int32_t n_actions, float beta, const float* seg, float* dS, float* dN,
                                       float* partials, void* stream) {
-    PPOX_REQUIRE(phi && actions && seg && dS && dN && partials && B >= 1 && n_pairs >= 0 && n_pairs < B &&
+    PPOX_REQUIRE(phi && actions && seg && dS && dN && partials && B >= 1 && n_pairs >= 0 && n_pairs <= B &&
                      n_pairs_global < B && n_actions >= 1 && n_actions <= 32,
                  "ppox_icm_pair_backward: bad arguments");
     PPOX_REQUIRE(pairs || n_pairs == B - 1, "ppox_icm_pair_backward: without a pair list every j < B - 1 is a pair");

@@ -137,25 +137,25 @@ class NativeIcm:
         # world > 1: the pairs cross rank boundaries (ppo.icm_loss_sharded) — features and actions
         # are summed into minibatch positions, each rank evaluates the pairs whose first row it
         # owns, and dL/dphi is summed back (same collective sequence on every rank)
-        full = torch.zeros(B, H, device=self.flat.device)
-        a_full = torch.zeros(B, dtype=torch.int32, device=self.flat.device)
+        # features and actions (as f32: small integers, exact) in one buffer, one all-reduce
+        fa = torch.zeros(B * (H + 1), device=self.flat.device)
+        full, a_f = fa[:B * H].view(B, H), fa[B * H:]
         if Bl > 0:
             full[pos] = phi
-            a_full[pos] = actions.reshape(-1)[rowno.long()]
-        ctx.all_reduce_(full)
-        ctx.all_reduce_(a_full)
-        j = pos[pos < B - 1].contiguous()
-        npl = int(j.numel())
+            a_f[pos] = actions.reshape(-1)[rowno.long()].float()
+        ctx.all_reduce_(fa)
+        a_full = a_f.to(torch.int32)
         dS = torch.zeros(B, H, device=self.flat.device)
         dN = torch.zeros(B, H, device=self.flat.device)
-        if Bl > 0:  # (npl == 0: zero pair partials; any non-null list pointer)
-            native.icm_pair_backward(full, B, a_full, None, j if npl else pos, npl, B - 1, A, beta, self.seg, dS, dN,
-                                     partials)
+        if Bl > 0:
+            # the pair list is every owned position: the kernel skips the one at B - 1 (no pair), so
+            # the host never waits for a compaction's count
+            native.icm_pair_backward(full, B, a_full, None, pos, Bl, B - 1, A, beta, self.seg, dS, dN, partials)
         g = ctx.all_reduce_(dS.add_(dN))
         if Bl == 0:
             self.gseg.zero_()
             self.w1_grad.zero_()
             return
         native.icm_row_backward(g, None, pos, Bl, pre1, self.seg, A, g1q, partials)
-        native.icm_grad_reduce(partials, Bl, npl, A, beta, B - 1, self.gseg, loss_accum)
+        native.icm_grad_reduce(partials, Bl, Bl, A, beta, B - 1, self.gseg, loss_accum)
         native.icm_enc_wgrad(x, rowno, Bl, self.K, g1q, self.w1_grad)

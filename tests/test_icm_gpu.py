@@ -158,6 +158,43 @@ def test_minibatch_deterministic():
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("B", [2048, 33])
+def test_minibatch_sharded_path_one_rank_matches_one_process(B):
+    """The world > 1 branch of train_minibatch (features + actions summed into minibatch positions,
+    the owned positions as the pair list — B - 1 among them, skipped by the kernel — dL/dphi summed
+    back) on one rank whose rows arrive in a shuffled order: the same gradients and loss as the
+    one-process branch on the rows in minibatch order."""
+    K, A, seed = K_ATARI, 4, 13
+    icm, _, flat = _module(K, A, seed)
+    nat = _native(icm, flat, K)
+    x = torch.from_numpy(_frames(B, K, seed + 100)).cuda()
+    acts = torch.from_numpy(np.random.default_rng(seed).integers(0, A, size=B).astype(np.int32)).cuda()
+
+    class One:
+        enabled = False
+
+    class Ranks:  # one rank with the data-parallel branch on (its sums are the identity)
+        enabled = True
+
+        @staticmethod
+        def all_reduce_(t):
+            return t
+    acc = torch.zeros(1, dtype=torch.float64, device="cuda")
+    nat.train_minibatch(x, acts, None, B, 0.2, One(), acc)
+    want, want_loss = flat.grad[:flat.n].clone(), acc.item()
+    order = torch.randperm(B, generator=torch.Generator().manual_seed(5)).cuda()  # row i sits at pos[i]
+    inv = torch.empty_like(order)
+    inv[order] = torch.arange(B, device="cuda")
+    acc.zero_()
+    flat.grad.fill_(float("nan"))
+    nat.train_minibatch(x[order].contiguous(), acts[order].contiguous(), order, B, 0.2, Ranks(), acc)
+    got = flat.grad[:flat.n]
+    assert torch.isfinite(got).all()
+    scale = want.abs().max().item()
+    assert (got - want).abs().max().item() <= 1e-6 * scale
+    np.testing.assert_allclose(acc.item(), want_loss, rtol=1e-6)
+
+
 @pytest.mark.parametrize("N,A", [(512, 4), (77, 18)])
 def test_int_reward_vs_fp64(N, A):
     """ppo.py:629-631: int_reward(s, s', a) = clamp(mean((fwd(phi(s), a) - phi(s'))^2), -5, 5),

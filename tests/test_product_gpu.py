@@ -382,7 +382,8 @@ def test_cnn_train_matches_reference_run(golden, name, math, rtol, head_min, mon
     # near-saturated softmax over raw-pixel logits (|logit| ~ 1e2) is set by the logits' last
     # bits, so the reference's own f32 entropy loss is 2.8e-5 (cnn18) / 2.7e-4 (cnn4) from
     # exact arithmetic (the float64 oracle run recorded in the fixture): the product's is held
-    # to within twice that distance of float64 (floor 1e-5)
+    # to within twice that distance of float64 in split math, 2.5x with the exact-f32 MFMA
+    # kernels (floor 1e-5; _loss_ok)
     stats = {}
     for i, key in ((0, "policy_gradient_loss"), (1, "value_loss"), (2, "entropy_loss"), (3, "total_loss")):
         got, ref, x64 = float(acc[i] / n), float(f[p + key]), float(f[p + "f64_" + key])
@@ -390,22 +391,24 @@ def test_cnn_train_matches_reference_run(golden, name, math, rtol, head_min, mon
                       "rel_ref_f64": abs(ref - x64) / abs(x64)}
     _parity_report(f"cnn_train_{name}_{math}_{head_min}", {"losses": stats, "weights": wstats})
     for i, key in ((0, "policy_gradient_loss"), (1, "value_loss"), (2, "entropy_loss"), (3, "total_loss")):
-        if not _loss_ok(key, float(acc[i] / n), float(f[p + key]), float(f[p + "f64_" + key])):
+        if not _loss_ok(key, float(acc[i] / n), float(f[p + key]), float(f[p + "f64_" + key]), math):
             fails.append((key, stats[key]))
     assert not fails, fails
 
 
-def _loss_ok(key, got, ref, x64):
+def _loss_ok(key, got, ref, x64, math):
     """A loss scalar matches the reference if it is within 1e-5 relative of the reference's
     value, or at most twice as far from exact arithmetic (the float64 oracle) as the reference's
     own float32 value is (a loss with cancellation — the policy-gradient mean of +-adv*ratio —
     can be further than 1e-5 from exact in the reference itself).  The entropy of the
     near-saturated softmax over raw-pixel logits is set by the logits' last bits and by the
     Adam trajectory of the earlier minibatches (a weight whose gradient is zero to rounding
-    steps +-lr either way): it is held to within 4x the reference's own distance from exact
-    (floor 1e-5 relative); measured 0.6-3.3x across the fixtures and both maths."""
+    steps +-lr either way): it is held to within 2x the reference's own distance from exact in
+    split math (the product default; measured 1.16-1.49x over the fixtures), 2.5x with the
+    exact-f32 MFMA kernels (measured 0.59-2.26x), floor 1e-5 relative (profiles/r04_parity/)."""
     if key == "entropy_loss":
-        return abs(got - x64) <= max(4 * abs(ref - x64), 1e-5 * abs(x64))
+        k = 2.0 if math == "split" else 2.5
+        return abs(got - x64) <= max(k * abs(ref - x64), 1e-5 * abs(x64))
     return abs(got - ref) <= 1e-5 * abs(ref) or abs(got - x64) <= 2 * abs(ref - x64)
 
 
@@ -436,12 +439,14 @@ def test_cnn_train_16384_rows_matches_reference_run(golden, math, monkeypatch):
       * weights, per tensor: max |prod - f64| <= 3 max e_ref + 2e-6 and mean |prod - f64| <=
         3 mean e_ref + 1e-8 — the product is as close to exact arithmetic as the reference is,
         within a factor 3 (measured: split 0.3-2.0x, exact-f32 MFMA 0.8-2.5x); plus every weight within
-        rtol |ref| + 0.1 lr of the reference but for at most 0.2 % outliers, which stay within one Adam
-        step (rtol |ref| + lr: Adam's first steps move a weight by +-lr whatever its gradient's size,
-        so a weight whose gradient is zero to rounding moves either way — the reference's own run is
-        up to a third of a step off exact arithmetic here), and at most 0.5 % beyond rtol |ref| + 2e-6;
+        rtol |ref| + 0.1 lr of the reference but for at most 0.2 % outliers (measured <= 0.061 %),
+        which stay within three quarters of one Adam step (rtol |ref| + 0.75 lr, measured <= 0.52 lr:
+        Adam's first steps move a weight by +-lr whatever its gradient's size, so a weight whose
+        gradient is zero to rounding moves either way — the reference's own run is up to a third of
+        a step off exact arithmetic here), and at most 0.5 % beyond rtol |ref| + 2e-6;
       * losses: policy-gradient, value, total within 1e-5 relative of the reference; the entropy
-        of the near-saturated softmax within max(2 e_ref, 1e-5 |f64|) of float64."""
+        of the near-saturated softmax within max(k e_ref, 1e-5 |f64|) of float64, k = 2 in split
+        math, 2.5 with the exact-f32 kernels (_loss_ok)."""
     import env as E
     import models
     import ppo
@@ -541,7 +546,7 @@ def test_cnn_train_16384_rows_matches_reference_run(golden, math, monkeypatch):
                                  "frac_beyond_strict": frac, "frac_beyond_tenth_lr": frac_lr,
                                  "dabs_rel": abs(d_abs - float(f[p + "d64abs_" + key])) / float(f[p + "d64abs_" + key])}
         if not (e_p.max() <= 3 * e_r.max() + 2e-6 and e_p.mean() <= 3 * e_r.mean() + 1e-8
-                and (e_pr <= rtol * np.abs(ref) + lr).all() and frac_lr <= 2e-3 and frac <= 5e-3):
+                and (e_pr <= rtol * np.abs(ref) + 0.75 * lr).all() and frac_lr <= 2e-3 and frac <= 5e-3):
             fails.append((key, stats["weights"][key]))
     acc = alg.loss_accum.cpu().numpy()
     n = acc[5]
@@ -549,7 +554,7 @@ def test_cnn_train_16384_rows_matches_reference_run(golden, math, monkeypatch):
         got, ref, x64 = float(acc[i] / n), float(f[p + key]), float(f[p + "f64_" + key])
         stats["losses"][key] = {"prod": got, "ref": ref, "f64": x64, "rel_prod_ref": abs(got - ref) / abs(ref),
                                 "rel_prod_f64": abs(got - x64) / abs(x64), "rel_ref_f64": abs(ref - x64) / abs(x64)}
-        ok = _loss_ok(key, got, ref, x64)
+        ok = _loss_ok(key, got, ref, x64, math)
         if not ok:
             fails.append((key, stats["losses"][key]))
     _parity_report(f"cnn_train_16384_{math}", stats)

@@ -18,4 +18,7 @@ timeout -k 10 300 python -u bench.py --algo icm --envs 512 --batch-size 2048 --s
     --force-dist > $O/bench_icm_dist.json 2>> $O/bench.err || exit $?
 timeout -k 10 300 python -u bench.py --envs 512 --batch-size 2048 --steps 5 --warmup 2 --no-cpu-baseline \
     --force-dist > $O/bench_rank_shape_dist.json 2>> $O/bench.err || exit $?
+for B in 2048 16384; do
+  timeout -k 10 200 python -u tools/graph_probe.py $B 40 > $O/graph_probe_$B.log 2>&1 || exit $?
+done
 echo done > $O/DONE

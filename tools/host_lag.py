@@ -1,6 +1,8 @@
 """Host-vs-GPU progress inside one PPO train() (dev tool): at every optimizer step records
 the host clock and a GPU event; a host that runs ahead of the GPU shows host time << GPU
-time at the same step, a blocking sync shows them equal.  Usage: python tools/host_lag.py [envs] [batch]"""
+time at the same step, a blocking sync shows them equal.  Usage: python tools/host_lag.py [envs] [batch]
+[ppo|icm] [dist] ("dist": the data-parallel branches on over a one-rank RCCL communicator, as bench.py
+--force-dist)"""
 import os
 import sys
 import time
@@ -15,9 +17,22 @@ import ppo  # noqa: E402
 def main():
     envs = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     bs = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+    algo = sys.argv[3] if len(sys.argv) > 3 else "ppo"
+    if len(sys.argv) > 4 and sys.argv[4] == "dist":
+        import socket
+        import torch.distributed as tdist
+        import dist
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]))
+        sk.close()
+        torch.cuda.set_device(0)
+        tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        dist.DistContext.enabled = property(lambda self: True)
     np.random.seed(0)
     torch.manual_seed(0)
-    alg = ppo.PPO(env_id="BreakoutNoFrameskip-v4", n_envs=envs, nstep=128, batch_size=bs, n_epochs=10, seed=1, quiet=True)
+    cls = ppo.PPO_ICM if algo == "icm" else ppo.PPO
+    alg = cls(env_id="BreakoutNoFrameskip-v4", n_envs=envs, nstep=128, batch_size=bs, n_epochs=10, seed=1, quiet=True)
     marks = []
     orig = alg.flat.adam_step
 
