@@ -374,9 +374,11 @@ int ppox_head_hidden_wgrad(const float* de, int64_t rows, const float* f, void* 
 int ppox_nature_fc_pack(const float* w, uint16_t* q_fwd, uint16_t* q_dgrad, void* stream);
 int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f,
                        const uint32_t* amax_h3, uint32_t* amax_f, const int* h3_exp, void* stream);
+/* df_exp (nullable): df is given as PX planes (ppox_px_split) with that exponent; amax_df stays
+ * required (the PX g3 bound) */
 int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
                          const uint32_t* amax_df, uint32_t* amax_g3, const uint32_t* relu_bits, int* g3_exp_out,
-                         void* stream);
+                         const int* df_exp, void* stream);
 /* fc forward (as ppox_nature_fc_fwd) split over K for small batches: 2-8 K-ranges per (128-row
  * tile, 64-column block) so the grid fills the chip, partial products into the workspace
  * (ppox_nature_fc_fwd_splitk_workspace_bytes(batch)), then one fixed-order reduce adding the
@@ -393,11 +395,17 @@ int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_
  * split-f16 (fp32-class; amax_df, amax_h3: the operands' slots), deterministic: df (batch, 512) is dL/df already ReLU-masked, h3 the
  * NHWC (batch, 7, 7, 64) conv3 output of the split forward.  Replaces the library GEMM of
  * torch.nn.Linear's backward (reference: models-checkpoint.py:58-59 trained by ppo.py:236-238).
- * batch 0 writes a zero gradient.  workspace: ppox_nature_fc_wgrad_workspace_bytes(batch). */
+ * batch 0 writes a zero gradient.  workspace: ppox_nature_fc_wgrad_workspace_bytes(batch).  h3_exp /
+ * df_exp (nullable): that operand is given as PX planes with that exponent (its amax then unused). */
 int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch);
 int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float* h3, void* workspace,
                          int64_t workspace_bytes, float* dw, const uint32_t* amax_df, const uint32_t* amax_h3,
-                         const int* h3_exp, void* stream);
+                         const int* h3_exp, const int* df_exp, void* stream);
+/* PX planes of an f32 tensor x (n % 32 == 0, as laid out in memory) whose amax slots are recorded:
+ * y (n int16 = the same bytes) = its two f16 planes at E = the split scale of amax (what a split
+ * GEMM takes for x as an f32 operand); *exp_out = E.  The fc layer's df for the fc dgrad and weight
+ * gradient, which otherwise split it in registers once per tile (round 4). */
+int ppox_px_split(const float* x, int64_t n, const uint32_t* amax, uint16_t* y, int* exp_out, void* stream);
 
 /* ES-NSRA (evolution_strategies.py:103-384, csrc/es.hip), float64 throughout.
  * ppox_es_noise: eps[p][j] ~ N(0,1) for members member0..member0+P-1 of a generation

@@ -66,7 +66,7 @@ RELU_BITS = os.environ.get("PPOX_RELU_BITS", "1") != "0"
 # row AM_EXP holds the exponents of the pass's PX tensors (slots EX_*)
 AM_H1, AM_H2, AM_H3, AM_DF, AM_G3, AM_G2, AM_G1, AM_F, AM_DE, AM_EXP = range(10)
 AM_ROWS = 10
-EX_H2, EX_H3, EX_G3 = range(3)
+EX_H2, EX_H3, EX_G3, EX_DF = range(4)
 
 # PX (round 4, include/ppox.h): in split math the trunk's other split operands are stored as their
 # two f16 planes too — h2 (written by the conv2 forward, read by the conv3 forward and weight
@@ -79,6 +79,12 @@ PX = os.environ.get("PPOX_PX", "1") != "0"
 # slower (same-box A/B 225.8 vs 219.5 ms per iteration: the producers' epilogues sit on the main
 # stream, the consumers it speeds up on the side stream), at 16,384 rows faster
 PX_MIN_BATCH = int(os.environ.get("PPOX_PX_MIN", "8192"))
+# PX df (round 4, PPOX_PX_DF=1): the fc layer's df (B x 512, its amax recorded by the head backward)
+# split into its planes by one small kernel (ppox_px_split) for the fc dgrad and weight gradient, which
+# otherwise split every df value in registers once per tile (the fc dgrad: 49 times).  Off by default:
+# same-box A/B (profiles/r04_ab.txt) 1-GPU 1,152.5 vs 1,146.8 ms, per-rank 203.9 vs 201.8 ms per
+# iteration with it on — the fc kernels are not bound by the split's VALU work
+PX_DF = os.environ.get("PPOX_PX_DF", "0") == "1"
 
 
 class PassState:
@@ -90,7 +96,7 @@ class PassState:
 
     __slots__ = ("amax", "bits", "px")
 
-    def __init__(self, amax, bits=(None, None, None), px=(False, False, False)):
+    def __init__(self, amax, bits=(None, None, None), px=(False, False, False, False)):
         self.amax, self.bits, self.px = amax, bits, list(px)
 
     def __getitem__(self, row):
@@ -313,6 +319,11 @@ class NatureConvs:
         return self.px and B >= FC_SPLIT_MIN_BATCH and (
             not train or (B >= FC_WGRAD_SPLIT_MIN_BATCH and B < FC_DGRAD_FUSED_MAX_BATCH))
 
+    def px_df(self, B):
+        """df as PX planes (ppox_px_split) for the split fc dgrad and weight gradient"""
+        return (PX_DF and self.px and self.nhwc3 and B >= FC_WGRAD_SPLIT_MIN_BATCH
+                and B < FC_DGRAD_FUSED_MAX_BATCH)
+
     def px_g3(self, B, am):
         """g3 as PX planes: the fc dgrad is the fused split kernel with h3's bitmask, the conv3 dgrad runs
         split with conv2's bitmask"""
@@ -399,7 +410,7 @@ class NatureConvs:
         stride = 4 * 84 * 84 if layer == 1 else 0
         out_am = am[AM_H1 + layer - 1] if self.math != "f32" else None
         bits = am.bits[layer - 1] if isinstance(am, PassState) else None
-        px = am.px if isinstance(am, PassState) else (False, False, False)
+        px = am.px if isinstance(am, PassState) else (False, False, False, False)
         # conv1 records h1's amax for the bound of a PX h2
         h1_am = out_am if layer == 1 and px[EX_H2] else None
         if isinstance(x, RolloutRows):
@@ -493,7 +504,7 @@ class NatureConvs:
                      if train and (RELU_BITS or (L == 1 and self.h1p)) and self.uses_split("fwd", L) and
                      consumer[L - 1] else None
                      for L, P, C in ((1, 400, 32), (2, 81, 64), (3, 49, 64)))
-        am = PassState(table, bits, (px2, px3, False))
+        am = PassState(table, bits, (px2, px3, False, False))
         if B:
             self.fwd(1, x, B, self.c1.bias, h1, am)
             self.fwd(2, h1, B, self.c2.bias, h2, am)
@@ -535,9 +546,9 @@ class NatureConvs:
                                  h3_exp=h3_exp)
         return f if actor is None else (f, logits)
 
-    def fc_dgrad_g3(self, df, h3, am):
+    def fc_dgrad_g3(self, df, h3, am, dfp=None):
         """g3 (B, 7, 7, 64) NHWC = (df @ W) * (h3 > 0), df = dL/df after the fc ReLU (its amax in
-        am[AM_DF]), h3 NHWC; records g3's amax."""
+        am[AM_DF]; dfp: its PX planes, am.px[EX_DF]), h3 NHWC; records g3's amax."""
         B = df.shape[0]
         px = self.px_g3(B, am)
         if px:  # g3 as PX planes for the conv3 dgrad and weight gradient
@@ -546,9 +557,10 @@ class NatureConvs:
         else:
             g3 = torch.empty((B, 7, 7, 64), device=df.device)
         ps = isinstance(am, PassState)
-        native.nature_fc_dgrad(df.contiguous(), B, self.qfc[1], h3 if not (ps and am.px[EX_H3]) else None, g3,
-                               amax_df=am[AM_DF], amax_g3=am[AM_G3], relu_bits=am.bits[2] if ps else None,
-                               g3_exp=am.exp(EX_G3) if px else None)
+        pdf = dfp is not None and ps and am.px[EX_DF]
+        native.nature_fc_dgrad(dfp if pdf else df.contiguous(), B, self.qfc[1], h3 if not (ps and am.px[EX_H3]) else None,
+                               g3, amax_df=am[AM_DF], amax_g3=am[AM_G3], relu_bits=am.bits[2] if ps else None,
+                               g3_exp=am.exp(EX_G3) if px else None, df_exp=am.exp(EX_DF) if pdf else None)
         return g3
 
     def backward_acts(self, x, h1, h2, h3, dh3, dw1, db1, dw2, db2, dw3, db3, g3=None, am=None):

@@ -3726,7 +3726,7 @@ extern "C" int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch) {
 
 extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float* h3, void* workspace,
                                     int64_t workspace_bytes, float* dw, const uint32_t* amax_df,
-                                    const uint32_t* amax_h3, const int* h3_exp, void* stream) {
+                                    const uint32_t* amax_h3, const int* h3_exp, const int* df_exp, void* stream) {
     PPOX_REQUIRE(dw && batch >= 0, "ppox_nature_fc_wgrad: bad arguments");
     hipStream_t s = ppox::as_stream(stream);
     if (batch == 0) {  // no rows: a zero gradient
@@ -3734,8 +3734,9 @@ extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float*
                      "ppox_nature_fc_wgrad: memset failed");
         return PPOX_OK;
     }
-    PPOX_REQUIRE(df && h3 && workspace && amax_df && (amax_h3 || h3_exp), "ppox_nature_fc_wgrad: bad arguments");
-    PPOX_REQUIRE(ppox::aligned16(amax_df) && (!amax_h3 || ppox::aligned16(amax_h3)), "ppox_nature_fc_wgrad: 16B alignment");
+    PPOX_REQUIRE(df && h3 && workspace && (amax_df || df_exp) && (amax_h3 || h3_exp), "ppox_nature_fc_wgrad: bad arguments");
+    PPOX_REQUIRE((!amax_df || ppox::aligned16(amax_df)) && (!amax_h3 || ppox::aligned16(amax_h3)),
+                 "ppox_nature_fc_wgrad: 16B alignment");
     PPOX_REQUIRE(workspace_bytes >= FcWgrad::workspace_bytes(batch), "ppox_nature_fc_wgrad: workspace too small");
     PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(h3), "ppox_nature_fc_wgrad: 16B alignment");
     PPOX_REQUIRE(batch < (1LL << 31) / 64, "ppox_nature_fc_wgrad: batch too large for 32-bit row indexing");
@@ -3743,11 +3744,17 @@ extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float*
     float* slab = reinterpret_cast<float*>(workspace);
     WArgs wa{df, 0, h3, slab, nullptr, batch, 0, sp, nullptr, 0, 0, amax_df, amax_h3};
     wa.gexp = h3_exp;  // PX h3 (the G operand of this GEMM)
+    wa.xexp = df_exp;  // PX df (the X operand)
     wa.px_per_split = ppox::ceil_div(ppox::ceil_div((long long)batch, (long long)sp), (long long)MS) * MS;
-    if (h3_exp)
-        wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB, false, true><<<(unsigned)(FcWgrad::TILES * sp), 256, 0, s>>>(wa);
+    const unsigned g = (unsigned)(FcWgrad::TILES * sp);
+    if (h3_exp && df_exp)
+        wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB, true, true><<<g, 256, 0, s>>>(wa);
+    else if (h3_exp)
+        wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB, false, true><<<g, 256, 0, s>>>(wa);
+    else if (df_exp)
+        wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB, true, false><<<g, 256, 0, s>>>(wa);
     else
-        wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB><<<(unsigned)(FcWgrad::TILES * sp), 256, 0, s>>>(wa);
+        wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB><<<g, 256, 0, s>>>(wa);
     PPOX_LAUNCHED_NORET("ppox_nature_fc_wgrad");
     fc_wgrad_reduce_perm<<<512, 256, 0, s>>>(slab, sp, dw);
     PPOX_LAUNCHED("ppox_nature_fc_wgrad");
@@ -3819,7 +3826,7 @@ extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const u
 
 extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16_t* q_dgrad, const float* h3, float* g3,
                                     const uint32_t* amax_df, uint32_t* amax_g3, const uint32_t* relu_bits,
-                                    int* g3_exp_out, void* stream) {
+                                    int* g3_exp_out, const int* df_exp, void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(df && q_dgrad && (h3 || relu_bits) && g3 && amax_df && batch >= 0,
                  "ppox_nature_fc_dgrad: bad arguments");
@@ -3827,21 +3834,23 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
                  "ppox_nature_fc_dgrad: 16B alignment");
     Args a{df, nullptr, 0, 0, 0, nullptr, nullptr, h3, g3, batch, amax_df, amax_g3, pack_exp(q_dgrad, PL_FCD)};
     a.bits_mask = relu_bits;  // h3's ReLU bitmask from the conv3 forward (instead of h3)
+    a.xexp = df_exp;          // PX df (ppox_px_split): its planes are the A rows as they lie
     const long long blocks = ppox::ceil_div(batch, SG_ROWS) * ppox::ceil_div(3136, SG_FC_NB);
+    hipStream_t s = ppox::as_stream(stream);
+    const char* nm = "ppox_nature_fc_dgrad";
+    using Bits = SgRows<512, 3136, FC_DGRAD, FC_DGRAD_GW, true, SG_FC_NB>;
+    using Acts = SgRows<512, 3136, FC_DGRAD, FC_DGRAD_GW, false, SG_FC_NB>;
     if (g3_exp_out) {  // g3 as PX planes, bounded by amax(df) * the fc weight's column norms
         PPOX_REQUIRE(relu_bits, "ppox_nature_fc_dgrad: a PX g3 needs h3's ReLU bitmask");
         a.yexp_out = g3_exp_out;
         a.ynorm = pack_norm(q_dgrad, PL_FCD);
         a.ybias = pack_bmax(q_dgrad, PL_FCD);
-        return launch_sgemm<Px<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_GW, true, SG_FC_NB>, false, true>>(
-            a, q_dgrad, blocks, ppox::as_stream(stream), "ppox_nature_fc_dgrad");
+        return df_exp ? launch_sgemm<Px<Bits, true, true>>(a, q_dgrad, blocks, s, nm)
+                      : launch_sgemm<Px<Bits, false, true>>(a, q_dgrad, blocks, s, nm);
     }
     if (relu_bits)
-        return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_GW, true, SG_FC_NB>>(
-            a, q_dgrad, blocks, ppox::as_stream(stream), "ppox_nature_fc_dgrad");
-    return launch_sgemm<SgRows<512, 3136, FC_DGRAD, FC_DGRAD_GW, false, SG_FC_NB>>(a, q_dgrad, blocks,
-                                                                                  ppox::as_stream(stream),
-                                                                                  "ppox_nature_fc_dgrad");
+        return df_exp ? launch_sgemm<Px<Bits, true>>(a, q_dgrad, blocks, s, nm) : launch_sgemm<Bits>(a, q_dgrad, blocks, s, nm);
+    return df_exp ? launch_sgemm<Px<Acts, true>>(a, q_dgrad, blocks, s, nm) : launch_sgemm<Acts>(a, q_dgrad, blocks, s, nm);
 }
 
 extern "C" int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, const float* b2,
@@ -3964,4 +3973,37 @@ extern "C" int ppox_amax(const float* x, int64_t n, uint32_t* amax, void* stream
     const long long blocks = std::min<long long>(ppox::ceil_div(n / 4, 256LL), 1024);
     amax_kernel<<<(unsigned)blocks, 256, 0, ppox::as_stream(stream)>>>(reinterpret_cast<const float4*>(x), n / 4, amax);
     PPOX_LAUNCHED("ppox_amax");
+}
+
+// ---- PX planes of an f32 tensor whose amax is recorded (round 4: the fc layer's df) ----------
+// y = the two f16 planes of x 2^E (include/ppox.h "PX"), E from x's amax slots — the scale a split
+// GEMM would take for x as an f32 operand, so the planes are the split every consumer tile made
+// in registers before (the fc dgrad split each df value once per 64-column tile: 49 times).
+// A thread splits 4 consecutive values of a 32-group: 16 B in, 8 B to each plane out.
+__global__ void __launch_bounds__(256) px_split_kernel(const float4* __restrict__ x, long long n4,
+                                                       const uint32_t* __restrict__ am, uint16_t* __restrict__ y,
+                                                       int* __restrict__ e_out) {
+    const int e = split_scale_exp(amax_read(am));
+    const float sc = exp2i(e);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *e_out = e;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+        uint2 h, l;
+        split4h(x[i], sc, h, l);
+        uint16_t* q = y + px_index(4 * i);
+        *reinterpret_cast<uint2*>(q) = h;
+        *reinterpret_cast<uint2*>(q + 32) = l;
+    }
+}
+
+extern "C" int ppox_px_split(const float* x, int64_t n, const uint32_t* amax, uint16_t* y, int* exp_out,
+                             void* stream) {
+    PPOX_REQUIRE(amax && y && exp_out && n >= 0 && n % 32 == 0 && (x || n == 0),
+                 "ppox_px_split: bad arguments (n % 32 == 0)");
+    PPOX_REQUIRE(ppox::aligned16(amax) && ppox::aligned16(y) && (!x || ppox::aligned16(x)),
+                 "ppox_px_split: 16B alignment");
+    if (n == 0) return PPOX_OK;
+    const long long blocks = std::min<long long>(ppox::ceil_div(n / 4, 256LL), 2048);
+    px_split_kernel<<<(unsigned)blocks, 256, 0, ppox::as_stream(stream)>>>(reinterpret_cast<const float4*>(x), n / 4,
+                                                                           amax, y, exp_out);
+    PPOX_LAUNCHED("ppox_px_split");
 }

@@ -48,6 +48,9 @@ __device__ inline uint32_t fwd1_idx_load(const long long* p) {
     return v;
 }
 __device__ uint32_t kFwd1Dummy[128];  // store target of the rows past the batch (never read)
+#ifndef FWD1_FAST_EPI
+#define FWD1_FAST_EPI 1  // the H1P epilogue's whole-tile form (round 4); 0: the per-row form for every tile
+#endif
 template <int MT, bool PLANES = false, bool IDX = false>
 __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a, unsigned tiles_per_wave) {
     using L = G1;
@@ -160,6 +163,49 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
         // bitmask word of tile row L (its 32 channels) is half (L >> 2) & 1 of the ballot of
         // element e = (L & 3) + 4 * (L >> 3): lane L < 32 collects it and stores it
         const int eL = (lane & 3) + 4 * ((lane >> 3) & 3), hL = (lane >> 2) & 1;
+        if constexpr (PLANES && FWD1_FAST_EPI) {
+            if (m0 + 32 * MT <= M) {  // uniform: a whole tile (every tile but a ragged last one)
+                // rows e, e + 1 (consecutive) as one pair: the value math on packed f32x2, their two
+                // splits in one split2h, one DPP swap of the hi and of the lo words for both rows, and
+                // v_perm_b32 assembles the even lane's (hi co, hi co + 1) and the odd lane's (lo co - 1,
+                // lo co) words; the stores are one base address plus immediate row offsets (no
+                // per-row 64-bit address arithmetic, no clamp).  Bitwise the rounding of the form below.
+                const bool odd = co & 1;
+                const f32x2 uw2 = {uw, uw}, b2 = {bias, bias};
+#pragma unroll
+                for (int i = 0; i < MT; ++i) {
+                    uint32_t word = 0;
+                    uint16_t* yb = reinterpret_cast<uint16_t*>(a.y) +
+                                   (long long)(m0 + i * 32 + 4 * (lane >> 5)) * (2 * L::COUT) +
+                                   (odd ? L::COUT + co - 1 : co);
+#pragma unroll
+                    for (int e = 0; e < 16; e += 2) {
+                        f32x2 v2 = ((f32x2){hi[i][e], hi[i][e + 1]} + (f32x2){lo[i][e], lo[i][e + 1]}) * uw2 + b2;
+                        v2.x = fmaxf(v2.x, 0.f);
+                        v2.y = fmaxf(v2.y, 0.f);
+                        om = fmaxf(om, fmaxf(v2.x, v2.y));
+                        uint32_t h, l;
+                        split2h(v2, sy, h, l);
+                        const uint32_t ph = (uint32_t)__builtin_amdgcn_mov_dpp((int)h, 0xB1, 0xF, 0xF, false);
+                        const uint32_t pl = (uint32_t)__builtin_amdgcn_mov_dpp((int)l, 0xB1, 0xF, 0xF, false);
+                        const uint32_t lo_w = odd ? pl : h, hi_w = odd ? l : ph;  // (low half, high half) sources
+                        const int r0 = (e & 3) + 8 * (e >> 2);                    // row of e; e + 1 is the next
+                        *reinterpret_cast<uint32_t*>(yb + r0 * (2 * L::COUT)) = __builtin_amdgcn_perm(hi_w, lo_w, 0x05040100u);
+                        *reinterpret_cast<uint32_t*>(yb + (r0 + 1) * (2 * L::COUT)) =
+                            __builtin_amdgcn_perm(hi_w, lo_w, 0x07060302u);
+                        if (a.bits_y) {  // uniform
+                            const unsigned long long b0 = __ballot(v2.x > 0.f), b1 = __ballot(v2.y > 0.f);
+                            word = eL == e ? (uint32_t)(hL ? b0 >> 32 : b0) : word;
+                            word = eL == e + 1 ? (uint32_t)(hL ? b1 >> 32 : b1) : word;
+                        }
+                    }
+                    const unsigned mw = m0 + i * 32 + lane;
+                    if (a.bits_y)  // uniform
+                        *(lane < 32 ? a.bits_y + mw : kFwd1Dummy + 64 + lane) = word;
+                }
+                return;
+            }
+        }
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
             uint32_t word = 0;

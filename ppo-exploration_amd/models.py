@@ -279,11 +279,18 @@ class CnnActorCritic(nn.Module):
                               b_critic_int=self.critic_int.bias.grad if self.intrinsic else None,
                               b_int_extra=self.int_extra_layer[0].bias.grad if self.intrinsic else None,
                               relu_df=not split, amax_df=am[_convs.AM_DF] if (cv.nhwc3 and not split) else None)
+            dfp = None
+            if cv.px_df(B) and isinstance(am, _convs.PassState):  # df's planes for the fc dgrad and weight gradient
+                am.px[_convs.EX_DF] = True
+                dfp = torch.empty((B, 2 * f.shape[1]), dtype=torch.int16, device=df.device)
+                native.px_split(df, am[_convs.AM_DF], dfp, am.exp(_convs.EX_DF))
             if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-f16 kernel, Flatten-order dW
                 h3_exp = am.exp(_convs.EX_H3)  # (PX h3: its planes)
+                df_exp = am.exp(_convs.EX_DF) if dfp is not None else None
+                dfw = dfp if dfp is not None else df
                 if side is None:
-                    native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, amax_df=am[_convs.AM_DF],
-                                           amax_h3=am[_convs.AM_H3], h3_exp=h3_exp)
+                    native.nature_fc_wgrad(dfw, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, amax_df=am[_convs.AM_DF],
+                                           amax_h3=am[_convs.AM_H3], h3_exp=h3_exp, df_exp=df_exp)
                     if dense_ready is not None:
                         dense_ready()
                 else:
@@ -291,8 +298,8 @@ class CnnActorCritic(nn.Module):
                     # gradients' all-reduce is started from there (ordered after it and, through the
                     # fork, after every head gradient); backward_acts joins the side stream
                     _convs.fork(side, cur)
-                    native.nature_fc_wgrad(df, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, amax_df=am[_convs.AM_DF],
-                                           amax_h3=am[_convs.AM_H3], h3_exp=h3_exp, stream=side)
+                    native.nature_fc_wgrad(dfw, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, amax_df=am[_convs.AM_DF],
+                                           amax_h3=am[_convs.AM_H3], h3_exp=h3_exp, df_exp=df_exp, stream=side)
                     if dense_ready is not None:
                         with torch.cuda.stream(side):
                             dense_ready()
@@ -309,7 +316,7 @@ class CnnActorCritic(nn.Module):
                     dense_ready()
             fe = self.feature_extractor
             if cv.nhwc3 and B < _convs.FC_DGRAD_FUSED_MAX_BATCH:  # masked NHWC grad directly
-                dh3, g3 = None, cv.fc_dgrad_g3(df, h3, am)
+                dh3, g3 = None, cv.fc_dgrad_g3(df, h3, am, dfp)
             elif cv.nhwc3:  # library GEMM on the permuted weight: NHWC order, then the ReLU mask
                 torch.index_select(fc.weight, 1, cv.fc_perm, out=cv.wfc_nhwc)
                 g3 = torch.mm(df, cv.wfc_nhwc).view(B, 7, 7, 64)

@@ -82,8 +82,9 @@ SIGNATURES = {
     "ppox_head_hidden_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
-    "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "ppox_nature_fc_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_fc_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_px_split": [_vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_es_noise": [_i64, _i64, _i64, _i64, _u64, _vp, _vp],
     "ppox_es_env_noise": [_i32, _i32, _u64, _vp, _vp],
     "ppox_es_evaluate": [_vp, _vp, _f64, _i64, _i32, _i32, _i32, _i32, _i32, _u64, _vp, _vp, _vp, _vp],
@@ -675,29 +676,40 @@ def nature_fc_fwd_splitk(h3, batch, q_fwd, bias, workspace, f, amax_h3=None, ama
 
 
 def nature_fc_dgrad(df, batch, q_dgrad, h3, g3, amax_df=None, amax_g3=None, relu_bits=None, g3_exp=None,
-                    stream=None):
+                    df_exp=None, stream=None):
     """g3 (batch, 7, 7, 64) NHWC = ((df @ W) in Flatten order) * (h3 > 0); amax_g3: g3's slots to record;
     relu_bits: h3's ReLU bitmask from the conv3 split forward (used instead of h3); g3_exp: write g3
-    as PX planes, storing the exponent there (relu_bits required)."""
-    if batch:
+    as PX planes, storing the exponent there (relu_bits required); df_exp: df is PX planes (px_split)
+    with that exponent (amax_df still required)."""
+    if batch and df_exp is None:
         amax_df = _amax_of(df, amax_df, stream)
     call("ppox_nature_fc_dgrad", _p(df), int(batch), _p(q_dgrad), _p(h3), _p(g3), _p(amax_df), _p(amax_g3),
-         _p(relu_bits), _p(g3_exp), stream_ptr(stream))
+         _p(relu_bits), _p(g3_exp), _p(df_exp), stream_ptr(stream))
 
 
 def nature_fc_wgrad_workspace_bytes(batch):
     return int(lib().ppox_nature_fc_wgrad_workspace_bytes(int(batch)))
 
 
-def nature_fc_wgrad(df, batch, h3, workspace, dw, amax_df=None, amax_h3=None, h3_exp=None, stream=None):
-    """dw (512, 3136) in the fc weight's Flatten order = df^T @ h3 (h3 NHWC (batch, 7, 7, 64); h3_exp:
-    as PX planes)."""
+def nature_fc_wgrad(df, batch, h3, workspace, dw, amax_df=None, amax_h3=None, h3_exp=None, df_exp=None,
+                    stream=None):
+    """dw (512, 3136) in the fc weight's Flatten order = df^T @ h3 (h3 NHWC (batch, 7, 7, 64); h3_exp /
+    df_exp: that operand as PX planes)."""
     if batch:
-        amax_df = _amax_of(df, amax_df, stream)
+        if df_exp is None:
+            amax_df = _amax_of(df, amax_df, stream)
         if h3_exp is None:
             amax_h3 = _amax_of(h3, amax_h3, stream)
     call("ppox_nature_fc_wgrad", _p(df), int(batch), _p(h3), _p(workspace), workspace.numel() * workspace.element_size(),
-         _p(dw), _p(amax_df), _p(amax_h3), _p(h3_exp), stream_ptr(stream))
+         _p(dw), _p(amax_df), _p(amax_h3), _p(h3_exp), _p(df_exp), stream_ptr(stream))
+
+
+def px_split(x, amax, y, exp_out, stream=None):
+    """y (int16, x's bytes) = the PX planes of f32 x at the split scale of its amax slots; the
+    exponent into exp_out (one int32)."""
+    assert x.is_contiguous() and x.dtype == torch.float32 and x.numel() % 32 == 0
+    assert y.dtype == torch.int16 and y.numel() == 2 * x.numel()
+    call("ppox_px_split", _p(x), x.numel(), _p(amax), _p(y), _p(exp_out), stream_ptr(stream))
 
 
 # ES-NSRA (csrc/es.hip)

@@ -1239,7 +1239,7 @@ def _h1p_setup(B, seed, scale_w1=0.05):
     return q, x, h1p, _h1_from_planes(h1p, E), E, (w1, b1, w2, w3), bits
 
 
-@pytest.mark.parametrize("B", [1, 3, 37, 300])
+@pytest.mark.parametrize("B", [1, 3, 37, 300, 2048])
 def test_h1p_conv1_forward_is_split_of_f32_forward(B):
     """The conv1 forward writing H1P (its output split into two f16 planes in the epilogue, at the
     exponent ppox_nature_pack_all derived from the weights' bound) == the H1P split of the same

@@ -1,6 +1,7 @@
 """PX (round 4): the NatureCNN trunk's split-f16 operands h2, h3 and g3 written as their two f16
 planes by their producers (conv2 forward, conv3 forward, fc dgrad) at exponents derived from
-bounds, and read as they lie by their consumers (include/ppox.h "PX").  The explicit training
+bounds, and read as they lie by their consumers (include/ppox.h "PX"); the fc layer's df split
+into its planes once (ppox_px_split) for the fc dgrad and weight gradient.  The explicit training
 forward / backward with PX on must stay fp32-class: within 2x the error of the same pass with PX
 off (f32 operands split in the consumers, the round-3 path pinned by the reference fixtures)
 against a float64 CPU autograd of the same network."""
@@ -13,9 +14,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True)
 def _px_at_every_batch(monkeypatch):
-    """the PX machinery at every batch size (the product turns it on from convs.PX_MIN_BATCH rows)"""
+    """the PX machinery at every batch size (the product turns it on from convs.PX_MIN_BATCH rows),
+    df's planes included (convs.PX_DF, off in the product)"""
     import convs
     monkeypatch.setattr(convs, "PX_MIN_BATCH", 0)
+    monkeypatch.setattr(convs, "PX_DF", True)
 
 
 def _setup(seed, A=4, intrinsic=False):
@@ -68,7 +71,7 @@ def test_px_training_pass_is_fp32_class(B):
     dv = torch.randn(B, device="cuda", generator=g)
     o_off, v_off, g_off, _ = _pass(net, flat, cv, x, dout, dv, False)
     o_on, v_on, g_on, am = _pass(net, flat, cv, x, dout, dv, True)
-    assert am.px == [True, True, True], am.px  # h2, h3, g3 all ran as planes
+    assert am.px == [True, True, True, True], am.px  # h2, h3, g3, df all ran as planes
     o64, v64, g64 = _fp64(ref, x, dout, dv)
     worst = []
     for name, r in list(g64.items()) + [("out", o64), ("v", v64)]:
@@ -93,7 +96,7 @@ def test_px_training_pass_big_batch_matches_f32_operands(B):
     dv = torch.randn(B, device="cuda", generator=g)
     o_off, v_off, g_off, _ = _pass(net, flat, cv, x, dout, dv, False)
     o_on, v_on, g_on, am = _pass(net, flat, cv, x, dout, dv, True)
-    assert am.px == [True, True, True], am.px
+    assert am.px == [True, True, True, True], am.px
     for name in g_off:
         a, b = g_on[name], g_off[name]
         scale = b.abs().max().item() + 1e-30
@@ -157,3 +160,39 @@ def test_px_exponents_and_planes(B):
     d3 = _from_planes(h3p, int(exps[convs.EX_H3]))
     assert (d3 - h3f).abs().max().item() <= 1e-5 * h3f.abs().max().item()
     assert _amax(am[convs.AM_H2]) == h2f.abs().max().item()  # the PX producer records its true amax
+
+
+@pytest.mark.parametrize("B", [64, 2048])
+def test_px_df_planes_are_the_consumers_split(B):
+    """ppox_px_split writes the planes a split GEMM makes of an f32 operand in registers (same
+    exponent, same rounding): hi + lo = df 2^E to the split's 2^-24, and the fc dgrad (g3 f32 and
+    PX g3) and the fc weight gradient on the planes are bitwise the same as on f32 df."""
+    import convs
+    import native
+    net, _, flat, cv = _setup(3)
+    cv.pack(B)
+    g = torch.Generator(device="cuda").manual_seed(B)
+    df = torch.randn(B, 512, device="cuda", generator=g) * torch.rand(B, 512, device="cuda", generator=g) ** 4
+    am = native.amax_table(convs.AM_ROWS, "cuda")
+    native.amax(df, am[convs.AM_DF])
+    e = torch.zeros(1, dtype=torch.int32, device="cuda")
+    dfp = torch.empty(B, 1024, dtype=torch.int16, device="cuda")
+    native.px_split(df, am[convs.AM_DF], dfp, e)
+    torch.cuda.synchronize()
+    E = int(e.item())
+    dec = _from_planes(dfp, E)
+    assert ((dec - df).abs() <= 2.0 ** -23 * df.abs() + 2.0 ** (-25 - E)).all()
+    amax = df.abs().max().item()
+    assert 2 ** 14 <= amax * 2.0 ** E < 2 ** 15
+    h3 = torch.relu(torch.randn(B, 7, 7, 64, device="cuda", generator=g))
+    a = torch.empty(B, 7, 7, 64, device="cuda")
+    b = torch.empty(B, 7, 7, 64, device="cuda")
+    native.nature_fc_dgrad(df, B, cv.qfc[1], h3, a, amax_df=am[convs.AM_DF])
+    native.nature_fc_dgrad(dfp, B, cv.qfc[1], h3, b, amax_df=am[convs.AM_DF], df_exp=e)
+    assert torch.equal(a, b)
+    ws = torch.empty(native.nature_fc_wgrad_workspace_bytes(B), dtype=torch.uint8, device="cuda")
+    w1 = torch.empty(512, 3136, device="cuda")
+    w2 = torch.empty(512, 3136, device="cuda")
+    native.nature_fc_wgrad(df, B, h3, ws, w1, amax_df=am[convs.AM_DF])
+    native.nature_fc_wgrad(dfp, B, h3, ws, w2, df_exp=e)
+    assert torch.equal(w1, w2)

@@ -1,5 +1,6 @@
 """Host-side profile of one PPO train() (dev tool): cProfile of the Python / ctypes launch path
-at a given shape, top functions by own time.  Usage: python tools/host_profile.py [envs] [batch] [algo]"""
+at a given shape, top functions by own time.  Usage: python tools/host_profile.py [envs] [batch] [algo] [dist]
+("dist": the data-parallel branches on over a one-rank RCCL communicator, as bench.py --force-dist)"""
 import cProfile
 import os
 import pstats
@@ -16,6 +17,17 @@ def main():
     envs = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     bs = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
     algo = sys.argv[3] if len(sys.argv) > 3 else "ppo"
+    if len(sys.argv) > 4 and sys.argv[4] == "dist":
+        import socket
+        import torch.distributed as tdist
+        import dist
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]))
+        sk.close()
+        torch.cuda.set_device(0)
+        tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        dist.DistContext.enabled = property(lambda self: True)
     np.random.seed(0)
     torch.manual_seed(0)
     cls = {"ppo": ppo.PPO, "icm": ppo.PPO_ICM, "rnd": ppo.PPO_RND}[algo]

@@ -37,7 +37,7 @@ def main():
         row = {
             "mfma_busy": get("SQ_VALU_MFMA_BUSY_CYCLES") / (get("GRBM_GUI_ACTIVE") / 8 * SIMDS),
             "valu/mfma": get("SQ_INSTS_VALU") / get("SQ_INSTS_MFMA") if get("SQ_INSTS_MFMA") else float("nan"),
-            "lds_conf": get("SQ_LDS_BANK_CONFLICT") / get("SQ_ACTIVE_INST_LDS"),
+            "lds_conf": get("SQ_LDS_BANK_CONFLICT") / get("SQ_ACTIVE_INST_LDS") if get("SQ_ACTIVE_INST_LDS") else float("nan"),
             "wait_any": get("SQ_WAIT_ANY") / get("SQ_WAVE_CYCLES"),
             "wait_lds": get("SQ_WAIT_INST_LDS") / get("SQ_WAVE_CYCLES"),
             "SQ_INSTS_MFMA": get("SQ_INSTS_MFMA"), "SQ_INSTS_VALU": get("SQ_INSTS_VALU"),
