@@ -546,12 +546,16 @@ int ppox_nature_conv_wgrad_split_idx(int32_t layer, const void* x, int64_t batch
  *   ppox_icm_pair_backward: pairs (row j, row j + 1) of a minibatch of B rows with features
  *                        phi (B x 32): the inverse / forward models, both losses (means over
  *                        n_pairs_global pairs, weights 1 - beta / beta) and their backward.
- *                        actions of row j: actions[rowno ? rowno[j] : j].  pairs: the first
- *                        rows of the evaluated pairs (NULL: all j < B - 1, n_pairs = B - 1;
- *                        a listed B - 1 has no pair and is skipped, n_pairs <= B).
+ *                        actions of row j: actions[rowno ? rowno[j] : j] (actions NULL, with a
+ *                        pair list: the B floats after phi, ppox_icm_scatter_positions' layout).
+ *                        pairs: the first rows of the evaluated pairs (NULL: all j < B - 1, n_pairs
+ *                        = B - 1; a listed B - 1 has no pair and is skipped, n_pairs <= B).
  *                        dS[j] / dN[j + 1] (B x 32) = dL/dphi through a pair's first / second
- *                        row (with pairs == NULL every row of both is written).  partials:
- *                        ppox_icm_partials_bytes(rows, n_actions).
+ *                        row (with pairs == NULL every row of both is written; with a list, dS
+ *                        and dN are zeroed first).  partials: ppox_icm_partials_bytes(rows, n_actions).
+ *   ppox_icm_scatter_positions: world > 1 — this rank's `rows` features phi (rows x 32) and actions
+ *                        (actions[rowno[i]]) at their minibatch positions pos[i] of
+ *                        fa = [B x 32 | B actions as f32], zero elsewhere (for one all-reduce).
  *   ppox_icm_row_backward: dphi = dS + dN (dN nullable) of minibatch row pos[i] (pos nullable)
  *                        -> g1 = dL/dpre1 in fragment order (f32) + per-column max |g1| of each
  *                        32-row block (ppox_icm_g1_pack_elems(rows) uint16)
@@ -573,6 +577,8 @@ int64_t ppox_icm_g1_pack_elems(int64_t rows);
 int ppox_icm_pair_backward(const float* phi, int64_t B, const int32_t* actions, const uint32_t* rowno,
                            const int64_t* pairs, int64_t n_pairs, int64_t n_pairs_global, int32_t n_actions,
                            float beta, const float* seg, float* dS, float* dN, float* partials, void* stream);
+int ppox_icm_scatter_positions(const float* phi, const int32_t* actions, const uint32_t* rowno, const int64_t* pos,
+                               int64_t rows, int64_t B, float* fa, void* stream);
 int ppox_icm_row_backward(const float* dS, const float* dN, const int64_t* pos, int64_t rows, const float* pre1,
                           const float* seg, int32_t n_actions, uint16_t* g1q, float* partials, void* stream);
 int ppox_icm_grad_reduce(const float* partials, int64_t rows, int64_t n_pairs, int32_t n_actions, float beta,

@@ -54,8 +54,11 @@ HEAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_SPLIT_MIN", "8192"))
 # PPOX_HEAD_FWD_SPLITK=0 keeps the library GEMM
 HEAD_FWD_SPLITK = os.environ.get("PPOX_HEAD_FWD_SPLITK", "1") == "1"
 # the hidden layer's backward (dgrad into the fc layer's input grad + weight gradient) on the split-f16
-# kernels from this batch up, the library GEMMs below (PPOX_HEAD_BWD_SPLIT_MIN)
-HEAD_BWD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_BWD_SPLIT_MIN", "8192"))
+# kernels from this batch up, the library GEMMs below (PPOX_HEAD_BWD_SPLIT_MIN).  Round 4: at every batch —
+# the same GPU time at the per-rank 2,048 rows (same-box A/B 199.57 vs 199.55-199.79 ms per iteration,
+# profiles/r04_ab.txt) and no library GEMM on the host's launch path (the two rocBLAS calls cost ~100 us of
+# host time per minibatch, which the 8-rank path spends on its collectives)
+HEAD_BWD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_BWD_SPLIT_MIN", "0"))
 
 # ReLU masks of the conv outputs as bitmasks written by the split forwards for the split dgrads
 # (PPOX_RELU_BITS=0: the dgrads read the f32 activations)
@@ -112,6 +115,10 @@ class PassState:
 # the fc dgrad), joined before the optimizer reads the gradients (PPOX_BWD_STREAMS=0: one stream)
 BWD_STREAMS = os.environ.get("PPOX_BWD_STREAMS", "1") != "0"
 BWD_SOLO_DGRAD2_BATCH = int(os.environ.get("PPOX_BWD_SOLO_DGRAD2", "8192"))
+# PPOX_FORK_LATE=1: below that batch the conv2 weight gradient's side-stream wait (on the point after the
+# conv3 dgrad) is enqueued after the conv2 dgrad's launch instead of before it — the same dependencies,
+# another capture order for a hipGraph of the pass (tools/graph_probe.py)
+FORK_LATE = os.environ.get("PPOX_FORK_LATE", "0") == "1"
 # PPOX_BWD_SOLO_WGRAD2=1: from that batch conv2's weight gradient also runs alone on the main stream
 # (after the dgrad, before wgrad1) instead of beside wgrad1 — 1 % slower (same-box A/B), but its
 # event time is then its own execution time
@@ -590,13 +597,21 @@ class NatureConvs:
         # wgrad2 forked after it, beside wgrad1 — the same throughput at 16384 rows (A/B), and the
         # dominant launch's HIP-event time is its own execution time (bench.py roofline)
         solo = side is not None and B >= BWD_SOLO_DGRAD2_BATCH
+        late = None
         if side is not None and not solo:
-            fork(side, cur)
-            self.wgrad(2, h1, B, g2, dw2, db2, am, stream=side)
+            if FORK_LATE:  # the fork point recorded now, the side stream's wait issued after the dgrad
+                late = _event(side, 2)
+                late.record(cur)
+            else:
+                fork(side, cur)
+                self.wgrad(2, h1, B, g2, dw2, db2, am, stream=side)
         if solo:
             join(side, cur)
         g1 = torch.empty((B, 20, 20, 32), device=dev)
         self.dgrad(2, g2, B, h1 if not self.h1p else None, g1, am)                        # dX of conv2, times ReLU'(conv1)
+        if late is not None:
+            side.wait_event(late)
+            self.wgrad(2, h1, B, g2, dw2, db2, am, stream=side)
         if side is None or (solo and BWD_SOLO_WGRAD2):
             self.wgrad(2, h1, B, g2, dw2, db2, am)
         elif solo:

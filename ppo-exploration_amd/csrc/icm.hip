@@ -469,7 +469,10 @@ __global__ void __launch_bounds__(256) icm_pair_kernel(PairArgs a) {
         if (jj < a.npl) j = a.pairs ? a.pairs[jj] : jj;
         if (j >= a.B - 1) j = -1;  // a listed position with no pair (the minibatch's last row)
         jrow[tid] = j;
-        act[tid] = j >= 0 ? a.actions[a.rowno ? (long long)a.rowno[j] : j] : 0;
+        // actions NULL: the minibatch's actions are the B floats after phi (ppox_icm_scatter_positions)
+        act[tid] = j < 0 ? 0
+                   : a.actions ? a.actions[a.rowno ? (long long)a.rowno[j] : j]
+                               : (int)a.phi[a.B * H + j];
     }
     if (!a.pairs && blockIdx.x == 0 && tid < 32) {  // rows with no pair on one side
         a.dN[tid] = 0.f;
@@ -992,18 +995,56 @@ extern "C" int64_t ppox_icm_g1_pack_elems(int64_t rows) {
     return rows <= 0 ? 0 : 2 * (g1_frag_floats(rows) + g1_blocks(rows) * 32);
 }
 
+// The sharded minibatch's features and actions at their minibatch positions (world > 1): fa = [B x 32
+// features | B actions as f32], zero where another rank owns the row, for one all-reduce.  Thread t of
+// the grid: feature float4 (t >> 3) of owned row ((t >> 3) / 8) ... one float4 per thread, the action with
+// the row's first quarter.
+__global__ void __launch_bounds__(256) icm_scatter_kernel(const float4* __restrict__ phi,
+                                                          const int32_t* __restrict__ actions,
+                                                          const uint32_t* __restrict__ rowno,
+                                                          const long long* __restrict__ pos, long long rows,
+                                                          long long B, float* __restrict__ fa) {
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;  // (row, float4 of its 8)
+    if (t >= rows * (H / 4)) return;
+    const long long i = t / (H / 4);
+    const int q = (int)(t % (H / 4));
+    const long long p = pos[i];
+    reinterpret_cast<float4*>(fa + p * H)[q] = phi[t];
+    if (q == 0) fa[B * H + p] = (float)actions[rowno[i]];
+}
+
+extern "C" int ppox_icm_scatter_positions(const float* phi, const int32_t* actions, const uint32_t* rowno,
+                                          const int64_t* pos, int64_t rows, int64_t B, float* fa, void* stream) {
+    PPOX_REQUIRE(fa && B >= 1 && rows >= 0 && rows <= B && (rows == 0 || (phi && actions && rowno && pos)),
+                 "ppox_icm_scatter_positions: bad arguments");
+    PPOX_REQUIRE(ppox::aligned16(fa) && (!phi || ppox::aligned16(phi)), "ppox_icm_scatter_positions: 16B alignment");
+    hipStream_t s = ppox::as_stream(stream);
+    PPOX_REQUIRE(hipMemsetAsync(fa, 0, sizeof(float) * B * (H + 1), s) == hipSuccess,
+                 "ppox_icm_scatter_positions: memset failed");
+    if (rows == 0) return PPOX_OK;
+    icm_scatter_kernel<<<ppox::ceil_div(rows * (H / 4), 256LL), 256, 0, s>>>(
+        reinterpret_cast<const float4*>(phi), actions, rowno, reinterpret_cast<const long long*>(pos), rows, B, fa);
+    PPOX_LAUNCHED("ppox_icm_scatter_positions");
+}
+
 extern "C" int ppox_icm_pair_backward(const float* phi, int64_t B, const int32_t* actions, const uint32_t* rowno,
                                       const int64_t* pairs, int64_t n_pairs, int64_t n_pairs_global,
                                       int32_t n_actions, float beta, const float* seg, float* dS, float* dN,
                                       float* partials, void* stream) {
-    PPOX_REQUIRE(phi && actions && seg && dS && dN && partials && B >= 1 && n_pairs >= 0 && n_pairs <= B &&
-                     n_pairs_global < B && n_actions >= 1 && n_actions <= 32,
+    PPOX_REQUIRE(phi && (actions || pairs) && seg && dS && dN && partials && B >= 1 && n_pairs >= 0 &&
+                     n_pairs <= B && n_pairs_global < B && n_actions >= 1 && n_actions <= 32,
                  "ppox_icm_pair_backward: bad arguments");
     PPOX_REQUIRE(pairs || n_pairs == B - 1, "ppox_icm_pair_backward: without a pair list every j < B - 1 is a pair");
+    hipStream_t s = ppox::as_stream(stream);
+    if (pairs) {  // only the listed pairs' rows are written: the rest of dS / dN is zero
+        PPOX_REQUIRE(hipMemsetAsync(dS, 0, sizeof(float) * B * H, s) == hipSuccess &&
+                         hipMemsetAsync(dN, 0, sizeof(float) * B * H, s) == hipSuccess,
+                     "ppox_icm_pair_backward: memset failed");
+    }
     PairArgs a{phi, B, actions, rowno, reinterpret_cast<const long long*>(pairs), n_pairs, n_pairs_global,
                1.f - beta, beta, seg, n_actions, dS, dN, partials};
     const unsigned nb = std::max(1u, ppox::ceil_div(n_pairs, PB));
-    icm_pair_kernel<<<nb, 256, 0, ppox::as_stream(stream)>>>(a);
+    icm_pair_kernel<<<nb, 256, 0, s>>>(a);
     PPOX_LAUNCHED("ppox_icm_pair_backward");
 }
 

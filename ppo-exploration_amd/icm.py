@@ -137,21 +137,17 @@ class NativeIcm:
         # world > 1: the pairs cross rank boundaries (ppo.icm_loss_sharded) — features and actions
         # are summed into minibatch positions, each rank evaluates the pairs whose first row it
         # owns, and dL/dphi is summed back (same collective sequence on every rank)
-        # features and actions (as f32: small integers, exact) in one buffer, one all-reduce
-        fa = torch.zeros(B * (H + 1), device=self.flat.device)
-        full, a_f = fa[:B * H].view(B, H), fa[B * H:]
-        if Bl > 0:
-            full[pos] = phi
-            a_f[pos] = actions.reshape(-1)[rowno.long()].float()
+        # features and actions (as f32: small integers, exact) at their positions in one buffer (one
+        # launch: zero-fill + scatter), one all-reduce
+        fa = self._buf("fa", (B * (H + 1),))
+        native.icm_scatter_positions(phi, actions.reshape(-1), rowno, pos, Bl, B, fa)
         ctx.all_reduce_(fa)
-        a_full = a_f.to(torch.int32)
-        dS = torch.zeros(B, H, device=self.flat.device)
-        dN = torch.zeros(B, H, device=self.flat.device)
+        dS, dN = self._buf("dS", (B, H)), self._buf("dN", (B, H))
         if Bl > 0:
             # the pair list is every owned position: the kernel skips the one at B - 1 (no pair), so
-            # the host never waits for a compaction's count
-            native.icm_pair_backward(full, B, a_full, None, pos, Bl, B - 1, A, beta, self.seg, dS, dN, partials)
-        g = ctx.all_reduce_(dS.add_(dN))
+            # the host never waits for a compaction's count; the actions are fa's f32 tail (NULL)
+            native.icm_pair_backward(fa, B, None, None, pos, Bl, B - 1, A, beta, self.seg, dS, dN, partials)
+        g = ctx.all_reduce_(dS.add_(dN)) if Bl > 0 else ctx.all_reduce_(dS.zero_())
         if Bl == 0:
             self.gseg.zero_()
             self.w1_grad.zero_()

@@ -102,6 +102,7 @@ SIGNATURES = {
     "ppox_icm_encode": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_icm_pair_backward": [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i32, _f32, _vp, _vp, _vp, _vp, _vp],
     "ppox_icm_row_backward": [_vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _vp],
+    "ppox_icm_scatter_positions": [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp],
     "ppox_icm_grad_reduce": [_vp, _i64, _i64, _i32, _f32, _i64, _vp, _vp, _vp],
     "ppox_icm_enc_wgrad": [_vp, _vp, _i64, _i64, _vp, _vp, _vp],
     "ppox_icm_int_reward": [_vp, _vp, _vp, _i64, _i32, _vp, _f32, _vp, _vp, _vp],
@@ -896,6 +897,12 @@ def icm_pair_backward(phi, B, actions, rowno, pairs, n_pairs, n_pairs_global, n_
                       partials, stream=None):
     call("ppox_icm_pair_backward", _p(phi), int(B), ptr(actions, torch.int32, name="actions"), _p(rowno), _p(pairs),
          int(n_pairs), int(n_pairs_global), int(n_actions), float(beta), _p(seg), _p(dS), _p(dN), _p(partials),
+         stream_ptr(stream))
+
+
+def icm_scatter_positions(phi, actions, rowno, pos, rows, B, fa, stream=None):
+    """fa = [B x 32 | B actions as f32]: this rank's rows at their minibatch positions, zero elsewhere."""
+    call("ppox_icm_scatter_positions", _p(phi), _p(actions), _p(rowno), _p(pos), int(rows), int(B), _p(fa),
          stream_ptr(stream))
 
 
