@@ -3320,7 +3320,8 @@ extern "C" int ppox_nature_wgrad_reduce(int32_t layer, int64_t batch, const void
 
 namespace {
 bool wgrad1_im2col();
-void w2p_grid(long long batch, int& per, long long& grid);
+void w2p_grid(long long batch, int& per, long long& grid, int min_per = 1);
+int w2p_min_per();
 int launch_wgrad1_frames(const void* x, long long sample_stride, const long long* idx, long long T, long long Nenv,
                          const float* g, long long batch, void* ws, long long ws_bytes, float* dw, float* db,
                          const uint32_t* amax_g, hipStream_t s);
@@ -3515,11 +3516,21 @@ int cu_count() {
         cus[dev] = 0;
     return cus[dev];
 }
-// wgrad2_planes_kernel: samples per workgroup and workgroups (one per CU, none empty)
-void w2p_grid(long long batch, int& per, long long& grid) {
+// wgrad2_planes_kernel: samples per workgroup and workgroups (one per CU, none empty); min_per > 1:
+// at least that many samples per workgroup (fewer slabs for the reduce at small batches)
+void w2p_grid(long long batch, int& per, long long& grid, int min_per) {
     const long long cus = std::max(1, cu_count());
     per = (int)ppox::ceil_div(batch, std::min(batch, cus));
+    per = std::max(per, std::min(min_per, (int)std::min<long long>(batch, 1 << 20)));
     grid = ppox::ceil_div(batch, (long long)per);
+}
+// PPOX_W2P_MIN_PER (A/B knob, default 1): the conv2 weight gradient's samples-per-workgroup floor
+int w2p_min_per() {
+    static const int v = [] {
+        const char* e = std::getenv("PPOX_W2P_MIN_PER");
+        return e ? std::max(1, std::atoi(e)) : 1;
+    }();
+    return v;
 }
 
 // the direct conv1 weight gradient (wgrad1_frames_kernel, one workgroup per CU) + its slab reduce;
@@ -3577,7 +3588,7 @@ extern "C" int64_t ppox_nature_conv2_wgrad_planes_workspace_bytes(int64_t batch)
     if (batch <= 0) return 0;
     int per;
     long long grid;
-    w2p_grid(batch, per, grid);
+    w2p_grid(batch, per, grid, w2p_min_per());
     return grid * (long long)(G2::K * G2::COUT + G2::COUT) * (long long)sizeof(float);
 }
 
@@ -3594,7 +3605,7 @@ extern "C" int ppox_nature_conv2_wgrad_planes(const uint16_t* h1p, const uint16_
                  "ppox_nature_conv2_wgrad_planes: workspace too small");
     int per;
     long long grid;
-    w2p_grid(batch, per, grid);
+    w2p_grid(batch, per, grid, w2p_min_per());
     float* slab = reinterpret_cast<float*>(workspace);
     W2PArgs wa{h1p, h1p_exp(q1, PL_Q1), grad_out, amax_g, slab, slab + grid * (long long)(G2::K * G2::COUT), batch,
                per};

@@ -14,3 +14,10 @@ A="--algo icm --envs 512 --batch-size 2048 --steps 3 --warmup 1 --no-cpu-baselin
 timeout -k 10 300 python -u bench.py $A --force-dist > $O/bench_icm_dist.json 2>> $O/err || exit $?
 timeout -k 10 300 python -u bench.py $A > $O/bench_icm.json 2>> $O/err || exit $?
 echo done > $O/DONE
+R="--envs 512 --batch-size 2048 --steps 5 --warmup 2 --no-cpu-baseline"
+for k in 1 2; do
+  timeout -k 10 300 python -u bench.py $R > $O/R_base$k.json 2>> $O/err || exit $?
+  PPOX_W2P_MIN_PER=16 timeout -k 10 300 python -u bench.py $R > $O/R_w2p16_$k.json 2>> $O/err || exit $?
+  PPOX_W2P_MIN_PER=32 timeout -k 10 300 python -u bench.py $R > $O/R_w2p32_$k.json 2>> $O/err || exit $?
+done
+echo done > $O/DONE2
