@@ -358,7 +358,9 @@ def main():
     # largest kernel is the one rocprofv3's --stats ranks first ("roofline_rocprof"), whose event
     # durations include its sharing of the CUs with the other stream's kernels.
     solo, duo = {}, {}
-    for w in range(args.warmup):
+    # (with --warmup 1 one more untimed iteration runs for the two-stream pick; the line says so)
+    n_warm = max(args.warmup, 2 if streams else 1)
+    for w in range(n_warm):
         convs.BWD_STREAMS = streams and w > 0
         if w == 0 or (w == 1 and streams):
             alg.collect_samples()
@@ -406,7 +408,8 @@ def main():
     out = {
         "metric": "env-steps/sec (collect+GAE+PPO update), 4096 envs×128 steps @ 1/2/4/8 GPU",
         "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
+        "warmup": args.warmup, "untimed_profiling_iterations": n_warm - args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 2), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (Philox uint8 4x84x84 frames, Bernoulli rewards/dones, device envs)",
         "config": {"workload": f"{env_id} {args.algo.upper()} NatureCNN {args.envs} envs x {args.nstep} steps",

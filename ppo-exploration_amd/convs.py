@@ -119,6 +119,9 @@ BWD_SOLO_DGRAD2_BATCH = int(os.environ.get("PPOX_BWD_SOLO_DGRAD2", "8192"))
 # conv3 dgrad) is enqueued after the conv2 dgrad's launch instead of before it — the same dependencies,
 # another capture order for a hipGraph of the pass (tools/graph_probe.py)
 FORK_LATE = os.environ.get("PPOX_FORK_LATE", "0") == "1"
+# PPOX_FORK_MERGE=1: the heads' hidden-layer weight gradient joins the fc weight gradient's fork to the side
+# stream (one main-stream event record per minibatch fewer; models.CnnActorCritic.backward_train)
+FORK_MERGE = os.environ.get("PPOX_FORK_MERGE", "0") == "1"
 # PPOX_BWD_SOLO_WGRAD2=1: from that batch conv2's weight gradient also runs alone on the main stream
 # (after the dgrad, before wgrad1) instead of beside wgrad1 — 1 % slower (same-box A/B), but its
 # event time is then its own execution time

@@ -244,6 +244,11 @@ class CnnActorCritic(nn.Module):
             cv = self.conv_impl
             split = cv.split_head_bwd(B)  # the extra layer's dgrad / weight gradient on the split-f16 kernels
             des = []
+            # FORK_MERGE: the hidden layers' weight gradients go to the side stream with the fc weight
+            # gradient's fork (one event record on the main stream fewer) instead of a fork of their own
+            merge = (side is not None and _convs.FORK_MERGE and split and cv.nhwc3
+                     and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH)
+            deferred = []
             # the actor head's input grad and the extra layer's dv * w_critic * ReLU' in one launch
             df, de0 = native.head_dgrad_outer(dout, a.weight, dv.contiguous().view(B), self.critic_ext.weight, e,
                                               amax_de=am[_convs.AM_DE] if split else None)
@@ -255,14 +260,17 @@ class CnnActorCritic(nn.Module):
                 else:
                     de = torch.empty_like(act)
                     native.outer_relu_backward(d, crit.weight, act, de)  # dv * w, ReLU'
-                if side is not None:  # the hidden layer's weight gradient beside the dgrad chain
-                    _convs.fork(side, cur)
-                with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-                    if sp:
-                        native.head_hidden_wgrad(de, f, self._head_wgrad_ws(B), hid.weight.grad, amax_de=am[_convs.AM_DE],
-                                                 amax_f=am[_convs.AM_F])
-                    else:
-                        weight_grad(de, f, hid.weight.grad, self._wgrad_part(hid.weight))
+                if merge and sp:
+                    deferred.append((de, hid))
+                else:
+                    if side is not None:  # the hidden layer's weight gradient beside the dgrad chain
+                        _convs.fork(side, cur)
+                    with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                        if sp:
+                            native.head_hidden_wgrad(de, f, self._head_wgrad_ws(B), hid.weight.grad,
+                                                     amax_de=am[_convs.AM_DE], amax_f=am[_convs.AM_F])
+                        else:
+                            weight_grad(de, f, hid.weight.grad, self._wgrad_part(hid.weight))
                 if not sp:
                     df.addmm_(de, hid.weight)
                 des.append((de, d))
@@ -298,6 +306,9 @@ class CnnActorCritic(nn.Module):
                     # gradients' all-reduce is started from there (ordered after it and, through the
                     # fork, after every head gradient); backward_acts joins the side stream
                     _convs.fork(side, cur)
+                    for de_, hid_ in deferred:
+                        native.head_hidden_wgrad(de_, f, self._head_wgrad_ws(B), hid_.weight.grad,
+                                                 amax_de=am[_convs.AM_DE], amax_f=am[_convs.AM_F], stream=side)
                     native.nature_fc_wgrad(dfw, B, h3, self._fc_wgrad_ws(B), fc.weight.grad, amax_df=am[_convs.AM_DF],
                                            amax_h3=am[_convs.AM_H3], h3_exp=h3_exp, df_exp=df_exp, stream=side)
                     if dense_ready is not None:
