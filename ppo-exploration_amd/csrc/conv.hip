@@ -3445,6 +3445,8 @@ int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq,
         return launch_sgemm<SgFwd<G2, false>>(a, wq, blocks, s, nm);
     }
     const long long blocks = ppox::ceil_div(batch * G3::P, SG_ROWS);
+    if (x_exp && y_exp_out && dconv_enabled(3, batch))
+        return dconv_fwd(3, x, batch, wq, bias, y, amax_x, amax_y, relu_bits, x_exp, y_exp_out, s);
     if (x_exp && y_exp_out) return launch_sgemm<Px<SgFwd<G3, false>, true, true>>(a, wq, blocks, s, nm);
     if (x_exp) return launch_sgemm<Px<SgFwd<G3, false>, true>>(a, wq, blocks, s, nm);
     if (y_exp_out) return launch_sgemm<Px<SgFwd<G3, false>, false, true>>(a, wq, blocks, s, nm);
@@ -3579,6 +3581,9 @@ extern "C" int ppox_nature_conv2_fwd_planes(const uint16_t* h1p, const uint16_t*
     a.ynorm = pack_norm(wq2, PL_Q2);
     a.ybias = pack_bmax(wq2, PL_Q2);
     const long long blocks = ppox::ceil_div(batch * G2::P, SG_ROWS);
+    if (y_exp_out && ppox_conv::dconv_enabled(2, batch))
+        return ppox_conv::dconv_fwd(2, h1p, batch, wq2, bias, y, amax_x, amax_y, relu_bits, a.xexp, y_exp_out,
+                                    ppox::as_stream(stream));
     if (y_exp_out)
         return launch_sgemm<Px<SgFwd2P, true, true>>(a, wq2, blocks, ppox::as_stream(stream), "ppox_nature_conv2_fwd_planes");
     return launch_sgemm<SgFwd2P>(a, wq2, blocks, ppox::as_stream(stream), "ppox_nature_conv2_fwd_planes");

@@ -396,4 +396,9 @@ long long planes(int which);  // uint16 planes of a split-packed form (1, 2, 3, 
 int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq, const float* bias, float* y,
                 const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, const int* x_exp, int* y_exp_out,
                 hipStream_t s);
+// conv2 / conv3 forwards on planes (H1P / h2 -> h2 / h3 planes), the direct form (dconv.hip)
+int dconv_fwd(int layer, const void* x, int64_t batch, const uint16_t* wq, const float* bias, float* y,
+              const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, const int* x_exp, int* y_exp_out,
+              hipStream_t s);
+bool dconv_enabled(int layer, long long batch);
 }  // namespace ppox_conv

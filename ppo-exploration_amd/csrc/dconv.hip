@@ -1,0 +1,429 @@
+// Direct split-f16 convolution forwards for conv2 and conv3 (round 4; .ipynb_checkpoints/
+// models-checkpoint.py:55-57, Conv2d(32, 64, 4, stride 2) / Conv2d(64, 64, 3, stride 1), each + ReLU):
+// the weights live in registers, the input images in LDS.
+//
+// Why: the im2col GEMM (sgemm_kernel<SgFwd2P> / <SgFwd<G3>>) stages every 128-row tile's A rows
+// (im2col: each input pixel copied up to 4 / 9 times) and the whole packed weight matrix (131 / 147
+// KB) through L2 -> LDS, 426 / 442 KB per tile; at the ~70 GB/s per CU that LDS-DMA path sustains,
+// staging, not the MFMA, bounds it.  Here each CU
+//   * holds the packed B (64 columns x K, hi / lo f16 planes) in VGPRs: wave w keeps the 32 columns of
+//     column tile j = w & 1 — NCH chunks x 2 k-steps x 2 planes fragments (conv2: 64 = 256 VGPRs,
+//     conv3: 72 = 288), loaded once per launch;
+//   * streams whole input sample images (PX / H1P planes: conv3 81 pixels x 256 B, conv2 400 x 128 B)
+//     into an LDS ring by LDS-DMA, each pixel read from HBM once;
+//   * walks its contiguous range of samples in phases of 64 output rows (rows = (sample, oy, ox), the
+//     im2col rows): wave w computes the 32-row block rg = w >> 1 of the phase for its column tile,
+//     the A fragments read straight from the images (implicit im2col: a row's tap (ky, kx) is the
+//     pixel (S oy + ky, S ox + kx) of its sample's image, 16 B per lane and plane).
+// Same MFMA sequence as the GEMM (its chunk order — conv2's taps in input-parity classes — and per
+// chunk k-steps 0, 1: hi += aH bH, lo += aH bL, lo += aL bH, mfma_split3), so the output is bitwise
+// the sg2 kernel's (tests/test_dconv_gpu.py).
+// LDS image layout (bank-conflict-free fragment reads): a 16-lane ds_read_b128 lane group reads 16
+// rows whose index m (within the workgroup's range) is distinct mod 16, one 16-B piece each.  Every
+// pixel gets a key from its coordinates such that a row's pixel at tap (ky, kx) has key
+// (m + const(tap)) & 15 — conv3: key(n, y, x) = (n + 7 y + x) & 15 (m = 49 n + 7 oy + ox, 49 = 1 mod 16);
+// conv2: key(n, y, x) = (n + 9 (y >> 1) + (x >> 1)) & 15 (m = 81 n + 9 oy + ox).  conv3 pixels are 256 B
+// (all 64 banks): piece p is stored at p ^ key.  conv2 pixels are 128 B (half the banks): the pixel
+// pair (x, x ^ 1) is swapped when key & 1 (the bank half), piece p stored at p ^ (key >> 1).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <utility>
+
+#include "conv_common.h"
+
+namespace {
+
+// conv3: h2 planes (81 pixels x 64 channels: per pixel hi[0:32] lo[0:32] hi[32:64] lo[32:64])
+struct DcF3 {
+    using L = G3;
+    static constexpr int PIXB = 256, NPIX = 81, DMAS = 6, NSLOT = 6, NCH = 18;
+    static constexpr int NA = 60;  // B fragments (of 72) kept in AGPRs
+    // chunk c: tap c >> 1, channel group c & 1
+    static constexpr int tap(int c) { return c >> 1; }
+    static constexpr int bchunk(int c) { return c; }
+    static constexpr int group(int c) { return c & 1; }
+};
+// conv2: H1P (400 pixels x 32 channels: per pixel hi[0:32] lo[0:32]); chunk c = one tap, walked in
+// the sg2 kernel's input-parity classes (SgFwd::tap_of, SG_FWD2_PARITY)
+struct DcF2 {
+    using L = G2;
+    static constexpr int PIXB = 128, NPIX = 400, DMAS = 13, NSLOT = 3, NCH = 16;
+    static constexpr int NA = 60;  // B fragments (of 64) kept in AGPRs
+    static constexpr int tap(int c) {
+        const int cls = c >> 2, i = c & 3;
+        return ((cls >> 1) + 2 * (i >> 1)) * 4 + (cls & 1) + 2 * (i & 1);
+    }
+    static constexpr int bchunk(int c) { return tap(c); }
+    static constexpr int group(int) { return 0; }
+};
+
+template <class F>
+struct DcGeo {
+    static constexpr int IMG = F::NPIX * F::PIXB;              // bytes per sample image
+    static constexpr int REAL_DMAS = (IMG + 1023) / 1024;      // 1-KB DMAs that cover it
+    static constexpr int SLOT = 4 * F::DMAS * 1024;            // a ring slot (every wave issues DMAS)
+    static constexpr int LDS = F::NSLOT * SLOT;
+    static_assert(REAL_DMAS <= 4 * F::DMAS, "dconv: the image fits its DMAs");
+    static_assert(LDS <= 160 * 1024, "dconv: LDS");
+    static_assert(F::L::P % 16 == 1, "dconv: the row key is m mod 16");
+};
+
+template <class Fn, int... I>
+__device__ inline void dc_unroll(Fn&& fn, std::integer_sequence<int, I...>) {
+    (fn(std::integral_constant<int, I>{}), ...);
+}
+
+template <int OFF>
+__device__ inline u32x4 dc_read(uint32_t addr) {
+    u32x4 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+    return r;
+}
+template <int N>
+__device__ inline void dc_lgkm(u32x4& a, u32x4& b) {
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
+}
+// wait until at most D k of this wave's vector-memory operations are outstanding (k uniform, < 4)
+template <int D>
+__device__ inline void dc_vm_wait(int k) {
+    static_assert(3 * D < 64, "vmcnt is 6 bits");
+    if (k <= 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (k == 1)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");
+    else if (k == 2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * D) : "memory");
+}
+
+// MFMA as inline asm, so the operands' register files are explicit: A (the LDS fragments) and the
+// accumulators in VGPRs, B in AGPRs ("a": the fragments of chunks below F::NA) or VGPRs.  hipcc does not
+// know these are MFMAs: VALU reads of an accumulator are padded by hand (dc_acc_fence), and an
+// accumulator is never written by the VALU (the first k-step takes C = 0).
+template <bool BA>
+__device__ inline void dc_mfma(f32x16& c, const u32x4& a, const u32x4& b) {
+    if constexpr (BA)
+        asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+    else
+        asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+}
+template <bool BA>
+__device__ inline void dc_mfma0(f32x16& c, const u32x4& a, const u32x4& b) {  // c = a b
+    if constexpr (BA)
+        asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "a"(b));
+    else
+        asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
+}
+// >= 18 wait states between a 16-pass MFMA writing an accumulator and a VALU reading it
+__device__ inline void dc_acc_fence(f32x16& h, f32x16& l) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 4" : "+v"(h), "+v"(l));
+}
+
+// BITS: write the output's ReLU bitmask (a.bits_y).  Input planes (a.x, exponent *a.xexp), output
+// planes (exponent from the bound, as the sg2 PX epilogue: *a.yexp_out by workgroup 0).
+template <class F, bool BITS>
+__global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* __restrict__ wq) {
+    using L = typename F::L;
+    using Gm = DcGeo<F>;
+    constexpr int NK = 2 * F::NCH;  // k-steps
+    __shared__ __attribute__((aligned(16))) uint8_t lds[Gm::LDS];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int j = wave & 1, rg = wave >> 1;  // column tile, row block of a phase
+    const int r = lane & 31, h = lane >> 5;
+    const long long S0 = blockIdx.x * a.batch / gridDim.x, S1 = (blockIdx.x + 1) * a.batch / gridDim.x;
+    const int NS = (int)(S1 - S0);
+    if (NS <= 0) return;
+    const int MR = NS * L::P;  // rows of the range
+    const int F_ = (MR + 63) / 64;
+    const uint8_t* xb = reinterpret_cast<const uint8_t*>(a.x) + S0 * Gm::IMG;
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
+
+    // DMA d = wave + 4 i (i < DMAS) of a sample covers slot bytes [1024 d, 1024 d + 1024) (past the
+    // image: the last DMA again, or its last pixel, into the slot's pad); lane -> LDS pixel u, piece
+    // position pos; the source pixel / piece follow from the sample's key
+    int dpix[F::DMAS], dkey[F::DMAS];
+#pragma unroll
+    for (int i = 0; i < F::DMAS; ++i) {
+        int d = wave + 4 * i;
+        d = d < Gm::REAL_DMAS ? d : Gm::REAL_DMAS - 1;
+        const int b = d * 1024 + lane * 16;
+        int u = b / F::PIXB;
+        u = u < F::NPIX ? u : F::NPIX - 1;
+        const int y = u / L::IW, x = u % L::IW;
+        dpix[i] = u;
+        dkey[i] = L::S == 1 ? L::OW * y + x : 9 * (y >> 1) + (x >> 1);
+    }
+    // DMA i of a sample: its image at src (uniform), ring slot dst (uniform), n & 15 = nk; a uniform base +
+    // a 32-bit lane offset
+    auto issue_at = [&](const uint8_t* src, uint8_t* dst, int nk, int i) {
+        int d = wave + 4 * i;
+        d = d < Gm::REAL_DMAS ? d : Gm::REAL_DMAS - 1;
+        const int key = (nk + dkey[i]) & 15;
+        uint32_t off;
+        if constexpr (F::PIXB == 256) {
+            off = (uint32_t)(dpix[i] * 256 + (((lane & 15) ^ key) << 4));
+        } else {  // conv2: the pixel pair swapped by key & 1, the piece by key >> 1
+            off = (uint32_t)((dpix[i] ^ (key & 1)) * 128 + (((lane & 7) ^ (key >> 1)) << 4));
+        }
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + off),
+                                         (__attribute__((address_space(3))) void*)(dst + d * 1024), 16, 0, 0);
+    };
+    auto issue_one = [&](int n, int i) {
+        issue_at(xb + (long long)n * Gm::IMG, lds + (n % F::NSLOT) * Gm::SLOT, n & 15, i);
+    };
+    auto issue_sample = [&](int n) {
+#pragma unroll
+        for (int i = 0; i < F::DMAS; ++i) issue_one(n, i);
+    };
+    // prologue: the first samples' DMAs, then the weights, the bias, the scales
+    int issued = NS < F::NSLOT ? NS : F::NSLOT;
+    for (int n = 0; n < issued; ++n) issue_sample(n);
+    u32x4 bq[F::NCH][2][2];
+#pragma unroll
+    for (int c = 0; c < F::NCH; ++c)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) bq[c][s][p] = wq[((((F::bchunk(c) * 2 + s) * 2 + j) * 2 + p) * 64) + lane];
+    const int col = j * 32 + r;
+    const float bias = a.bias[col];
+    const int ex = *a.xexp, ew = *a.wexp;
+    const float ua = exp2i(-ex), uw = exp2i(-ew);
+    const uint32_t am = amax_read(a.amax_x), nm = amax_read(a.ynorm), bm = *a.ybias;
+    const int ey = bound_exp(am, nm, bm);
+    const float bnd = __uint_as_float(am) * __uint_as_float(nm) + __uint_as_float(bm);
+    const float sy = __builtin_isfinite(bnd) ? exp2i(ey) : __builtin_nanf("");
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.yexp_out = ey;
+    __builtin_amdgcn_s_waitcnt(0);  // everything above landed (hipcc's own bookkeeping sees it)
+    asm volatile("s_nop 4" ::: "memory");  // (VALU-written B registers before the first MFMA reads them)
+
+    // output planes: element (row, col) of the range at byte 256 row + 4 (col & 32) + 2 (col & 30), its
+    // pair word's low plane 64 B further (px_index); a uniform base + a 32-bit lane offset
+    uint8_t* yb = reinterpret_cast<uint8_t*>(a.y) + 2 * px_index(S0 * L::P * 64);
+    const uint32_t ycol = 4 * (col & 32) + 2 * (col & 30) + 64 * (lane & 1);
+    uint32_t* bits = BITS ? a.bits_y + S0 * L::P * 2 : nullptr;
+    uint32_t om = 0u;  // the largest stored value's bits (values >= 0)
+    const int qL = (lane & 3) + 4 * ((lane >> 3) & 3), hL = (lane >> 2) & 1;
+    f32x16 H0, L0, H1, L1;
+
+    // epilogue element q of the 32-row block at range row pmb (the sg2 PX epilogue, one column tile):
+    // relu((hi + lo) ua uw + bias) as planes; FULL: every row of the block is in the range
+    auto epi_elem = [&](auto Q, auto FULL, const f32x16& PH, const f32x16& PL, int pmb, int& bw) {
+        constexpr int q = decltype(Q)::value, R0 = (q & 3) + 8 * (q >> 2);
+        const int row = pmb + R0 + 4 * h;
+        const bool ok = decltype(FULL)::value || row < MR;
+        float v = fmaxf((PH[q] + PL[q]) * ua * uw + bias, 0.f);
+        if constexpr (!decltype(FULL)::value) v = ok ? v : 0.f;
+        const uint32_t w = px_pair_word(v, sy, lane & 1);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(yb + ((uint32_t)(pmb + 4 * h) * 256u + ycol + R0 * 256));
+        if constexpr (decltype(FULL)::value) {
+            *dst = w;
+        } else {
+            if (ok) *dst = w;
+        }
+        om = max(om, __float_as_uint(v) & 0x7FFFFFFFu);
+        if constexpr (BITS) {
+            const unsigned long long b = __ballot(v > 0.f);
+            // lane L < 32 keeps row L's word: half hL of the ballot of element qL
+            bw = qL == q ? (int)(uint32_t)(hL ? b >> 32 : b) : bw;
+        }
+    };
+    auto epi_bits = [&](int pmb, int bw) {
+        if constexpr (BITS) {
+            const int row = pmb + lane;
+            if (lane < 32 && row < MR) bits[row * 2 + j] = (uint32_t)bw;
+        }
+    };
+    // refill DMAs of a phase: up to RMAX samples, DMA x = t * DMAS + i at k-step 16 + x (NK - 16) / (RMAX DMAS),
+    // after the epilogue's stores (k-steps 0-16), so the next wait's younger operations are the DMAs
+    constexpr int RMAX = 2, NDMA = RMAX * F::DMAS;
+    static_assert(NK > 17, "dconv: the epilogue's k-steps");
+
+    // phase f: accumulate its rows into (H, Lo); the previous phase's (PH, PL) epilogue (when prev) rides
+    // along the k walk.  Samples this phase reads: [nlo, nhi]; their DMAs waited for (the later samples'
+    // may stay in flight: samples are issued in order, and any store issued after them only makes the
+    // count more conservative), then one barrier: every wave's DMAs landed, every wave done with phase
+    // f - 1's fragment reads
+    auto phase = [&](int f, f32x16& H, f32x16& Lo, const f32x16& PH, const f32x16& PL, bool prev) {
+        const int m0 = 64 * f;
+        const int nlo = m0 / L::P, nhi = min((m0 + 63) / L::P, NS - 1);
+        dc_vm_wait<F::DMAS>(issued - 1 - nhi);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        // refill: samples up to nlo + NSLOT - 1 (the slots of samples < nlo are free), issued inside the
+        // k walk
+        const int rA = issued, nref = min(nlo + F::NSLOT, NS) - issued;
+        issued += nref;
+        const uint8_t* rsrc[RMAX];
+        uint8_t* rdst[RMAX];
+#pragma unroll
+        for (int t = 0; t < RMAX; ++t) {
+            rsrc[t] = xb + (long long)(rA + t) * Gm::IMG;
+            rdst[t] = lds + ((rA + t) % F::NSLOT) * Gm::SLOT;
+        }
+        // this lane's A row: m = m0 + 32 rg + r (past the range: its last row, never stored)
+        int m = m0 + 32 * rg + r;
+        m = m < MR ? m : MR - 1;
+        const int n = m / L::P, p = m - n * L::P, oy = p / L::OW, ox = p - oy * L::OW;
+        const uint32_t base = lds0 + (n % F::NSLOT) * Gm::SLOT + (L::S * oy * L::IW + L::S * ox) * F::PIXB;
+        const int key0 = m & 15;  // the row's key (P = 1 mod 16)
+        // k-step i = 2 c + s: its plane-pl fragment address (the tap's pixel offset: the immediate)
+        auto addr = [&](int i, int pl) {
+            const int c = i >> 1, s = i & 1, tap = F::tap(c), ky = tap / L::KW, kx = tap % L::KW;
+            const uint32_t P16 = (uint32_t)((F::group(c) << 3) | (pl << 2) | (s << 1)) << 4;
+            if constexpr (F::PIXB == 256) {
+                const uint32_t kt = (uint32_t)(((key0 + L::OW * ky + kx) & 15) ^ h) << 4;
+                return base + (P16 ^ kt);
+            } else {
+                // pixel x = 2 ox + kx (low bit kx & 1) flipped by key & 1: +-128 B
+                const int key = (key0 + 9 * (ky >> 1) + (kx >> 1)) & 15;
+                const uint32_t kt = (uint32_t)((key >> 1) ^ h) << 4;
+                const uint32_t bt = base + (uint32_t)((key & 1) * ((kx & 1) ? -128 : 128));
+                return bt + (P16 ^ kt);
+            }
+        };
+        u32x4 fa[3][2];
+        auto rd = [&](auto I) {
+            constexpr int i = decltype(I)::value;
+            constexpr int tap = F::tap(i >> 1), off = ((tap / L::KW) * L::IW + tap % L::KW) * F::PIXB;
+            fa[i % 3][0] = dc_read<off>(addr(i, 0));
+            fa[i % 3][1] = dc_read<off>(addr(i, 1));
+        };
+        rd(std::integral_constant<int, 0>{});
+        rd(std::integral_constant<int, 1>{});
+        const int pmb = m0 - 64 + 32 * rg;
+        int bw = 0;
+        // two k-steps of fragment reads in flight ahead of the MFMAs
+        dc_unroll(
+            [&](auto I) {
+                constexpr int i = decltype(I)::value;
+                if constexpr (i + 2 < NK) {
+                    rd(std::integral_constant<int, i + 2>{});
+                    dc_lgkm<4>(fa[i % 3][0], fa[i % 3][1]);
+                } else if constexpr (i + 1 < NK) {
+                    dc_lgkm<2>(fa[i % 3][0], fa[i % 3][1]);
+                } else {
+                    dc_lgkm<0>(fa[i % 3][0], fa[i % 3][1]);
+                }
+                // mfma_split3: hi += aH bH, lo += aH bL, lo += aL bH (B fragment (c, s, p) in AGPRs below NA)
+                constexpr int fb = (i >> 1) * 4 + (i & 1) * 2;
+                constexpr bool A0 = fb < F::NA, A1 = fb + 1 < F::NA;
+                const u32x4& b0 = bq[i >> 1][i & 1][0];
+                const u32x4& b1 = bq[i >> 1][i & 1][1];
+                if constexpr (i == 0) {
+                    dc_mfma0<A0>(H, fa[0][0], b0);
+                    dc_mfma0<A1>(Lo, fa[0][0], b1);
+                } else {
+                    dc_mfma<A0>(H, fa[i % 3][0], b0);
+                    dc_mfma<A1>(Lo, fa[i % 3][0], b1);
+                }
+                dc_mfma<A0>(Lo, fa[i % 3][1], b0);
+                if constexpr (i < 16) {
+                    if (prev) epi_elem(std::integral_constant<int, i>{}, std::true_type{}, PH, PL, pmb, bw);
+                } else if constexpr (i == 16) {
+                    if (prev) epi_bits(pmb, bw);
+                }
+                // the refill DMAs whose k-step this is
+                dc_unroll(
+                    [&](auto X) {
+                        constexpr int x = decltype(X)::value, t = x / F::DMAS;
+                        if constexpr (16 + x * (NK - 16) / NDMA == i) {
+                            if (t < nref) issue_at(rsrc[t], rdst[t], (rA + t) & 15, x % F::DMAS);
+                        }
+                    },
+                    std::make_integer_sequence<int, NDMA>{});
+            },
+            std::make_integer_sequence<int, NK>{});
+        // (a refill of more than RMAX samples: never after phase 0, whose samples the prologue issued)
+        for (int t = RMAX; t < nref; ++t) issue_sample(rA + t);
+        dc_acc_fence(H, Lo);
+    };
+    // the last phase's epilogue (its block may run past the range)
+    auto final_epi = [&](const f32x16& PH, const f32x16& PL) {
+        const int pmb = 64 * (F_ - 1) + 32 * rg;
+        int bw = 0;
+        dc_unroll([&](auto Q) { epi_elem(Q, std::false_type{}, PH, PL, pmb, bw); }, std::make_integer_sequence<int, 16>{});
+        epi_bits(pmb, bw);
+    };
+
+    // phases alternate between the accumulator sets (H0, L0) and (H1, L1); the previous set's epilogue
+    // runs inside the next phase
+    phase(0, H0, L0, H1, L1, false);
+    int f = 1;
+#pragma unroll 1
+    for (; f + 1 < F_; f += 2) {
+        phase(f, H1, L1, H0, L0, true);
+        phase(f + 1, H0, L0, H1, L1, true);
+    }
+    if (f < F_) phase(f, H1, L1, H0, L0, true);
+    if ((F_ - 1) & 1)
+        final_epi(H1, L1);
+    else
+        final_epi(H0, L0);
+    amax_record(a.amax_y, __uint_as_float(om));
+}
+
+int dconv_cus() {
+    static int cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (cus[dev] == 0 && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 0;
+    return cus[dev];
+}
+
+bool env_on(const char* name, long long batch, bool dflt) {
+    const char* e = std::getenv(name);
+    if (!(e ? e[0] != '0' : dflt)) return false;
+    char mn[64];
+    snprintf(mn, sizeof mn, "%s_MIN", name);
+    const char* m = std::getenv(mn);
+    return batch >= (m ? std::atoll(m) : 1);
+}
+
+template <class F>
+int launch_dconv(const Args& a, const uint16_t* wq, hipStream_t s, const char* name) {
+    const int cus = dconv_cus();
+    PPOX_REQUIRE(cus > 0, "%s: no device", name);
+    PPOX_REQUIRE(a.xexp && a.yexp_out && a.amax_x && a.ybias && a.ynorm, "%s: the direct form needs PX operands",
+                 name);
+    const long long grid = std::min<long long>(a.batch, cus);
+    const u32x4* w = reinterpret_cast<const u32x4*>(wq);
+    if (a.bits_y)
+        dconv_fwd_kernel<F, true><<<(unsigned)grid, 256, 0, s>>>(a, w);
+    else
+        dconv_fwd_kernel<F, false><<<(unsigned)grid, 256, 0, s>>>(a, w);
+    PPOX_LAUNCHED(name);
+}
+
+}  // namespace
+
+#ifndef DCONV_DEFAULT
+#define DCONV_DEFAULT false  // the direct forms unless PPOX_DCONV2 / PPOX_DCONV3 say otherwise
+#endif
+
+namespace ppox_conv {
+// PPOX_DCONV3=0 / PPOX_DCONV2=0: the im2col sg2 GEMM instead; PPOX_DCONV3_MIN / PPOX_DCONV2_MIN: the
+// smallest batch the direct form runs at (default 1).  Read at every launch: the tests switch forms
+// within one process.
+bool dconv_enabled(int layer, long long batch) {
+    return env_on(layer == 2 ? "PPOX_DCONV2" : "PPOX_DCONV3", batch, DCONV_DEFAULT);
+}
+
+// conv3 forward, h2 planes in / h3 planes out; conv2 forward, H1P in / h2 planes out (x_exp: the H1P
+// exponent) — one workgroup per CU, each a contiguous range of samples
+int dconv_fwd(int layer, const void* x, int64_t batch, const uint16_t* wq, const float* bias, float* y,
+              const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, const int* x_exp, int* y_exp_out,
+              hipStream_t s) {
+    Args a{x, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch, amax_x, amax_y, pack_exp(wq, planes(layer))};
+    a.bits_y = relu_bits;
+    a.xexp = x_exp;
+    a.yexp_out = y_exp_out;
+    a.ynorm = pack_norm(wq, planes(layer));
+    a.ybias = pack_bmax(wq, planes(layer));
+    if (layer == 2) return launch_dconv<DcF2>(a, wq, s, "ppox_nature_conv2_fwd_planes");
+    return launch_dconv<DcF3>(a, wq, s, "ppox_nature_conv_fwd_split");
+}
+}  // namespace ppox_conv

@@ -1,0 +1,56 @@
+"""Timing of the conv2 / conv3 forwards (H1P / h2 planes -> h2 / h3 planes), the direct form
+(csrc/dconv.hip) against the im2col sg2 GEMM (PPOX_DCONV2=0 / PPOX_DCONV3=0), HIP events on the launch stream.
+Usage: python tools/dconv_bench.py [B ...]"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+import convs  # noqa: E402
+import models  # noqa: E402
+
+convs.PX_MIN_BATCH = 0
+
+
+def t_ms(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    torch.manual_seed(0)
+    net = models.CnnActorCritic(4, 4)
+    cv = convs.attach(net, models.FlatParams(net, "cuda"), "split")
+    for B in [int(a) for a in sys.argv[1:]] or [2048, 16384]:
+        x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda")
+        with torch.no_grad():
+            _, h2, h3, am = cv.forward_acts(x, train=True)
+        h1 = cv.empty_h1(B, "cuda")
+        cv.fwd(1, x, B, cv.c1.bias, h1, am)
+        for layer, xin, y, bias, P, K, pin in ((2, h1, h2, cv.c2.bias, 81, 512, 400 * 32),
+                                               (3, h2, h3, cv.c3.bias, 49, 576, 81 * 64)):
+            row = {"B": B, "layer": layer}
+            for name, v in (("gemm", "0"), ("direct", "1")):
+                os.environ["PPOX_DCONV%d" % layer] = v
+                row[name + "_us"] = round(1e3 * t_ms(lambda: cv.fwd(layer, xin, B, bias, y, am)), 1)
+            flop = 2 * P * K * 64 * B
+            byt = B * (pin + P * 64) * 4
+            for name in ("gemm", "direct"):
+                t = row[name + "_us"] * 1e-6
+                row[name + "_tf"] = round(flop / t / 1e12, 1)
+                row[name + "_tbs"] = round(byt / t / 1e12, 2)
+            print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
