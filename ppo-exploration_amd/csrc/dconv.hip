@@ -34,10 +34,14 @@
 
 namespace {
 
+#ifndef DC_PD
+#define DC_PD 2  // k-steps of A-fragment reads in flight ahead of the MFMAs
+#endif
+
 // conv3: h2 planes (81 pixels x 64 channels: per pixel hi[0:32] lo[0:32] hi[32:64] lo[32:64])
 struct DcF3 {
     using L = G3;
-    static constexpr int PIXB = 256, NPIX = 81, DMAS = 6, NSLOT = 6, NCH = 18;
+    static constexpr int PIXB = 256, NPIX = 81, DMAS = 6, NSLOT = 7, NCH = 18;
     static constexpr int NA = 60;  // B fragments (of 72) kept in AGPRs
     // chunk c: tap c >> 1, channel group c & 1
     static constexpr int tap(int c) { return c >> 1; }
@@ -62,7 +66,9 @@ template <class F>
 struct DcGeo {
     static constexpr int IMG = F::NPIX * F::PIXB;              // bytes per sample image
     static constexpr int REAL_DMAS = (IMG + 1023) / 1024;      // 1-KB DMAs that cover it
-    static constexpr int SLOT = 4 * F::DMAS * 1024;            // a ring slot (every wave issues DMAS)
+    // a ring slot: the image's 1-KB DMAs (a wave's DMAs past the last re-copy it: the same bytes to the
+    // same place)
+    static constexpr int SLOT = REAL_DMAS * 1024;
     static constexpr int LDS = F::NSLOT * SLOT;
     static_assert(REAL_DMAS <= 4 * F::DMAS, "dconv: the image fits its DMAs");
     static_assert(LDS <= 160 * 1024, "dconv: LDS");
@@ -211,18 +217,21 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
 
     // epilogue element q of the 32-row block at range row pmb (the sg2 PX epilogue, one column tile):
     // relu((hi + lo) ua uw + bias) as planes; FULL: every row of the block is in the range
-    auto epi_elem = [&](auto Q, auto FULL, const f32x16& PH, const f32x16& PL, int pmb, int& bw) {
+    // (epi_val: the value and its pair word; epi_store: the store, the amax, the bitmask word — the two
+    // halves go to different MFMA gaps of a k-step)
+    auto epi_val = [&](auto Q, auto FULL, const f32x16& PH, const f32x16& PL, int pmb, float& v, uint32_t& w) {
         constexpr int q = decltype(Q)::value, R0 = (q & 3) + 8 * (q >> 2);
-        const int row = pmb + R0 + 4 * h;
-        const bool ok = decltype(FULL)::value || row < MR;
-        float v = fmaxf((PH[q] + PL[q]) * ua * uw + bias, 0.f);
-        if constexpr (!decltype(FULL)::value) v = ok ? v : 0.f;
-        const uint32_t w = px_pair_word(v, sy, lane & 1);
+        v = fmaxf((PH[q] + PL[q]) * ua * uw + bias, 0.f);
+        if constexpr (!decltype(FULL)::value) v = pmb + R0 + 4 * h < MR ? v : 0.f;
+        w = px_pair_word(v, sy, lane & 1);
+    };
+    auto epi_store = [&](auto Q, auto FULL, int pmb, float v, uint32_t w, int& bw) {
+        constexpr int q = decltype(Q)::value, R0 = (q & 3) + 8 * (q >> 2);
         uint32_t* dst = reinterpret_cast<uint32_t*>(yb + ((uint32_t)(pmb + 4 * h) * 256u + ycol + R0 * 256));
         if constexpr (decltype(FULL)::value) {
             *dst = w;
         } else {
-            if (ok) *dst = w;
+            if (pmb + R0 + 4 * h < MR) *dst = w;
         }
         om = max(om, __float_as_uint(v) & 0x7FFFFFFFu);
         if constexpr (BITS) {
@@ -230,6 +239,12 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
             // lane L < 32 keeps row L's word: half hL of the ballot of element qL
             bw = qL == q ? (int)(uint32_t)(hL ? b >> 32 : b) : bw;
         }
+    };
+    auto epi_elem = [&](auto Q, auto FULL, const f32x16& PH, const f32x16& PL, int pmb, int& bw) {
+        float v;
+        uint32_t w;
+        epi_val(Q, FULL, PH, PL, pmb, v, w);
+        epi_store(Q, FULL, pmb, v, w, bw);
     };
     auto epi_bits = [&](int pmb, int bw) {
         if constexpr (BITS) {
@@ -247,11 +262,13 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
     // may stay in flight: samples are issued in order, and any store issued after them only makes the
     // count more conservative), then one barrier: every wave's DMAs landed, every wave done with phase
     // f - 1's fragment reads
-    auto phase = [&](int f, f32x16& H, f32x16& Lo, const f32x16& PH, const f32x16& PL, bool prev) {
+    auto phase = [&](int f, f32x16& H, f32x16& Lo, const f32x16& PH, const f32x16& PL, auto PREV) {
         const int m0 = 64 * f;
         const int nlo = m0 / L::P, nhi = min((m0 + 63) / L::P, NS - 1);
+#ifndef DC_NO_BAR
         dc_vm_wait<F::DMAS>(issued - 1 - nhi);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
         // refill: samples up to nlo + NSLOT - 1 (the slots of samples < nlo are free), issued inside the
         // k walk
         const int rA = issued, nref = min(nlo + F::NSLOT, NS) - issued;
@@ -284,56 +301,74 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
                 return bt + (P16 ^ kt);
             }
         };
-        u32x4 fa[3][2];
+        constexpr int PD = DC_PD, NB = PD + 1;  // k-steps of fragment reads in flight, buffers
+        u32x4 fa[NB][2];
         auto rd = [&](auto I) {
             constexpr int i = decltype(I)::value;
             constexpr int tap = F::tap(i >> 1), off = ((tap / L::KW) * L::IW + tap % L::KW) * F::PIXB;
-            fa[i % 3][0] = dc_read<off>(addr(i, 0));
-            fa[i % 3][1] = dc_read<off>(addr(i, 1));
+            fa[i % NB][0] = dc_read<off>(addr(i, 0));
+            fa[i % NB][1] = dc_read<off>(addr(i, 1));
         };
-        rd(std::integral_constant<int, 0>{});
-        rd(std::integral_constant<int, 1>{});
+        auto rd1 = [&](auto I, auto PL) {  // one plane of k-step i's fragment
+            constexpr int i = decltype(I)::value, pl = decltype(PL)::value;
+            constexpr int tap = F::tap(i >> 1), off = ((tap / L::KW) * L::IW + tap % L::KW) * F::PIXB;
+            fa[i % NB][pl] = dc_read<off>(addr(i, pl));
+        };
+        dc_unroll([&](auto I) { rd(I); }, std::make_integer_sequence<int, PD>{});
+        dc_lgkm<2 * (PD - 1)>(fa[0][0], fa[0][1]);
         const int pmb = m0 - 64 + 32 * rg;
         int bw = 0;
-        // two k-steps of fragment reads in flight ahead of the MFMAs
+        // k-step i: its three MFMAs with the other work in their gaps (one wave per SIMD issues in order:
+        // an MFMA occupies the matrix pipe 32 cycles, of which its issue takes 8): gap 1 the read of k-step
+        // i + 2's high plane and the epilogue element's value, gap 2 the low plane's read and the element's
+        // store, gap 3 the refill DMAs; then the wait for k-step i + 1's fragments (k-step i + 2's may stay
+        // in flight)
         dc_unroll(
             [&](auto I) {
                 constexpr int i = decltype(I)::value;
-                if constexpr (i + 2 < NK) {
-                    rd(std::integral_constant<int, i + 2>{});
-                    dc_lgkm<4>(fa[i % 3][0], fa[i % 3][1]);
-                } else if constexpr (i + 1 < NK) {
-                    dc_lgkm<2>(fa[i % 3][0], fa[i % 3][1]);
-                } else {
-                    dc_lgkm<0>(fa[i % 3][0], fa[i % 3][1]);
-                }
                 // mfma_split3: hi += aH bH, lo += aH bL, lo += aL bH (B fragment (c, s, p) in AGPRs below NA)
                 constexpr int fb = (i >> 1) * 4 + (i & 1) * 2;
                 constexpr bool A0 = fb < F::NA, A1 = fb + 1 < F::NA;
                 const u32x4& b0 = bq[i >> 1][i & 1][0];
                 const u32x4& b1 = bq[i >> 1][i & 1][1];
-                if constexpr (i == 0) {
+                constexpr bool EPI = decltype(PREV)::value && i < 16;
+                float ev = 0.f;
+                uint32_t ew2 = 0u;
+                if constexpr (i == 0)
                     dc_mfma0<A0>(H, fa[0][0], b0);
+                else
+                    dc_mfma<A0>(H, fa[i % NB][0], b0);
+                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 0>{});
+#ifndef DC_NO_EPI
+                if constexpr (EPI) epi_val(std::integral_constant<int, i>{}, std::true_type{}, PH, PL, pmb, ev, ew2);
+#endif
+                if constexpr (i == 0)
                     dc_mfma0<A1>(Lo, fa[0][0], b1);
-                } else {
-                    dc_mfma<A0>(H, fa[i % 3][0], b0);
-                    dc_mfma<A1>(Lo, fa[i % 3][0], b1);
-                }
-                dc_mfma<A0>(Lo, fa[i % 3][1], b0);
-                if constexpr (i < 16) {
-                    if (prev) epi_elem(std::integral_constant<int, i>{}, std::true_type{}, PH, PL, pmb, bw);
-                } else if constexpr (i == 16) {
-                    if (prev) epi_bits(pmb, bw);
-                }
+                else
+                    dc_mfma<A1>(Lo, fa[i % NB][0], b1);
+                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 1>{});
+#ifndef DC_NO_EPI
+                if constexpr (EPI) epi_store(std::integral_constant<int, i>{}, std::true_type{}, pmb, ev, ew2, bw);
+                if constexpr (decltype(PREV)::value && i == 16) epi_bits(pmb, bw);
+#endif
+#ifdef DC_LO2  // (timing probe only: the third product into hi, no back-to-back dependent MFMAs)
+                dc_mfma<A0>(H, fa[i % NB][1], b0);
+#else
+                dc_mfma<A0>(Lo, fa[i % NB][1], b0);
+#endif
                 // the refill DMAs whose k-step this is
                 dc_unroll(
                     [&](auto X) {
                         constexpr int x = decltype(X)::value, t = x / F::DMAS;
                         if constexpr (16 + x * (NK - 16) / NDMA == i) {
+#ifndef DC_NO_DMA
                             if (t < nref) issue_at(rsrc[t], rdst[t], (rA + t) & 15, x % F::DMAS);
+#endif
                         }
                     },
                     std::make_integer_sequence<int, NDMA>{});
+                constexpr int later = (i + PD < NK ? i + PD : NK - 1) - (i + 1);  // k-steps read after i + 1
+                if constexpr (i + 1 < NK) dc_lgkm<2 * later>(fa[(i + 1) % NB][0], fa[(i + 1) % NB][1]);
             },
             std::make_integer_sequence<int, NK>{});
         // (a refill of more than RMAX samples: never after phase 0, whose samples the prologue issued)
@@ -350,14 +385,14 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
 
     // phases alternate between the accumulator sets (H0, L0) and (H1, L1); the previous set's epilogue
     // runs inside the next phase
-    phase(0, H0, L0, H1, L1, false);
+    phase(0, H0, L0, H1, L1, std::false_type{});
     int f = 1;
 #pragma unroll 1
     for (; f + 1 < F_; f += 2) {
-        phase(f, H1, L1, H0, L0, true);
-        phase(f + 1, H0, L0, H1, L1, true);
+        phase(f, H1, L1, H0, L0, std::true_type{});
+        phase(f + 1, H0, L0, H1, L1, std::true_type{});
     }
-    if (f < F_) phase(f, H1, L1, H0, L0, true);
+    if (f < F_) phase(f, H1, L1, H0, L0, std::true_type{});
     if ((F_ - 1) & 1)
         final_epi(H1, L1);
     else
@@ -401,7 +436,7 @@ int launch_dconv(const Args& a, const uint16_t* wq, hipStream_t s, const char* n
 }  // namespace
 
 #ifndef DCONV_DEFAULT
-#define DCONV_DEFAULT false  // the direct forms unless PPOX_DCONV2 / PPOX_DCONV3 say otherwise
+#define DCONV_DEFAULT true  // the direct forms unless PPOX_DCONV2 / PPOX_DCONV3 say otherwise
 #endif
 
 namespace ppox_conv {

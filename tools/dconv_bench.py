@@ -8,6 +8,10 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+import native  # noqa: E402
+
+if os.environ.get("PPOX_LIB"):
+    native.load(os.environ["PPOX_LIB"])
 import convs  # noqa: E402
 import models  # noqa: E402
 
