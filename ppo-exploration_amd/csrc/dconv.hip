@@ -53,7 +53,7 @@ struct DcF3 {
 struct DcF2 {
     using L = G2;
     static constexpr int PIXB = 128, NPIX = 400, DMAS = 13, NSLOT = 3, NCH = 16;
-    static constexpr int NA = 60;  // B fragments (of 64) kept in AGPRs
+    static constexpr int NA = 64;  // B fragments (of 64) kept in AGPRs
     static constexpr int tap(int c) {
         const int cls = c >> 2, i = c & 3;
         return ((cls >> 1) + 2 * (i >> 1)) * 4 + (cls & 1) + 2 * (i & 1);
@@ -69,7 +69,8 @@ struct DcGeo {
     // a ring slot: the image's 1-KB DMAs (a wave's DMAs past the last re-copy it: the same bytes to the
     // same place)
     static constexpr int SLOT = REAL_DMAS * 1024;
-    static constexpr int LDS = F::NSLOT * SLOT;
+    static constexpr int BIAS = F::NSLOT * SLOT;  // the output's 64 scaled biases
+    static constexpr int LDS = BIAS + 64 * 4;
     static_assert(REAL_DMAS <= 4 * F::DMAS, "dconv: the image fits its DMAs");
     static_assert(LDS <= 160 * 1024, "dconv: LDS");
     static_assert(F::L::P % 16 == 1, "dconv: the row key is m mod 16");
@@ -90,6 +91,10 @@ template <int N>
 __device__ inline void dc_lgkm(u32x4& a, u32x4& b) {
     asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
 }
+template <int N>
+__device__ inline void dc_lgkm(u32x4& a, u32x4& b, u32x4& c) {
+    asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(a), "+v"(b), "+v"(c) : "n"(N));
+}
 // wait until at most D k of this wave's vector-memory operations are outstanding (k uniform, < 4)
 template <int D>
 __device__ inline void dc_vm_wait(int k) {
@@ -104,23 +109,26 @@ __device__ inline void dc_vm_wait(int k) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * D) : "memory");
 }
 
-// MFMA as inline asm, so the operands' register files are explicit: A (the LDS fragments) and the
-// accumulators in VGPRs, B in AGPRs ("a": the fragments of chunks below F::NA) or VGPRs.  hipcc does not
-// know these are MFMAs: VALU reads of an accumulator are padded by hand (dc_acc_fence), and an
-// accumulator is never written by the VALU (the first k-step takes C = 0).
+// MFMA as inline asm, so the operands' register files are explicit: the weights are srcA (AGPRs, "a": the
+// fragments of chunks below F::NA, else VGPRs), the image fragment srcB and the accumulators VGPRs.  The
+// output tile is then channels x pixels (lane (r, h): pixel r, channels (q & 3) + 8 (q >> 2) + 4 h), so a
+// lane holds runs of 4 adjacent channels of one pixel: the PX epilogue stores 8-B plane runs with no
+// cross-lane exchange.  Per output element the products and their k order are the GEMM's (a x^T w sum
+// either way).  hipcc does not know these are MFMAs: VALU reads of an accumulator are padded by hand
+// (dc_acc_fence), and an accumulator is never written by the VALU (the first k-step takes C = 0).
 template <bool BA>
-__device__ inline void dc_mfma(f32x16& c, const u32x4& a, const u32x4& b) {
+__device__ inline void dc_mfma(f32x16& c, const u32x4& x, const u32x4& w) {
     if constexpr (BA)
-        asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+        asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %1, %0" : "+v"(c) : "v"(x), "a"(w));
     else
-        asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+        asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %1, %0" : "+v"(c) : "v"(x), "v"(w));
 }
 template <bool BA>
-__device__ inline void dc_mfma0(f32x16& c, const u32x4& a, const u32x4& b) {  // c = a b
+__device__ inline void dc_mfma0(f32x16& c, const u32x4& x, const u32x4& w) {  // c = w x
     if constexpr (BA)
-        asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "a"(b));
+        asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %1, 0" : "=&v"(c) : "v"(x), "a"(w));
     else
-        asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b));
+        asm volatile("v_mfma_f32_32x32x16_f16 %0, %2, %1, 0" : "=&v"(c) : "v"(x), "v"(w));
 }
 // >= 18 wait states between a 16-pass MFMA writing an accumulator and a VALU reading it
 __device__ inline void dc_acc_fence(f32x16& h, f32x16& l) {
@@ -150,7 +158,7 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
     // DMA d = wave + 4 i (i < DMAS) of a sample covers slot bytes [1024 d, 1024 d + 1024) (past the
     // image: the last DMA again, or its last pixel, into the slot's pad); lane -> LDS pixel u, piece
     // position pos; the source pixel / piece follow from the sample's key
-    int dpix[F::DMAS], dkey[F::DMAS];
+    int dpk[F::DMAS];  // LDS pixel u (low 16 bits) | its key offset << 16
 #pragma unroll
     for (int i = 0; i < F::DMAS; ++i) {
         int d = wave + 4 * i;
@@ -159,20 +167,19 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
         int u = b / F::PIXB;
         u = u < F::NPIX ? u : F::NPIX - 1;
         const int y = u / L::IW, x = u % L::IW;
-        dpix[i] = u;
-        dkey[i] = L::S == 1 ? L::OW * y + x : 9 * (y >> 1) + (x >> 1);
+        dpk[i] = u | ((L::S == 1 ? L::OW * y + x : 9 * (y >> 1) + (x >> 1)) << 16);
     }
     // DMA i of a sample: its image at src (uniform), ring slot dst (uniform), n & 15 = nk; a uniform base +
     // a 32-bit lane offset
     auto issue_at = [&](const uint8_t* src, uint8_t* dst, int nk, int i) {
         int d = wave + 4 * i;
         d = d < Gm::REAL_DMAS ? d : Gm::REAL_DMAS - 1;
-        const int key = (nk + dkey[i]) & 15;
+        const int key = (nk + (dpk[i] >> 16)) & 15, u = dpk[i] & 0xFFFF;
         uint32_t off;
         if constexpr (F::PIXB == 256) {
-            off = (uint32_t)(dpix[i] * 256 + (((lane & 15) ^ key) << 4));
+            off = (uint32_t)(u * 256 + (((lane & 15) ^ key) << 4));
         } else {  // conv2: the pixel pair swapped by key & 1, the piece by key >> 1
-            off = (uint32_t)((dpix[i] ^ (key & 1)) * 128 + (((lane & 7) ^ (key >> 1)) << 4));
+            off = (uint32_t)((u ^ (key & 1)) * 128 + (((lane & 7) ^ (key >> 1)) << 4));
         }
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + off),
                                          (__attribute__((address_space(3))) void*)(dst + d * 1024), 16, 0, 0);
@@ -194,62 +201,65 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
         for (int s = 0; s < 2; ++s)
 #pragma unroll
             for (int p = 0; p < 2; ++p) bq[c][s][p] = wq[((((F::bchunk(c) * 2 + s) * 2 + j) * 2 + p) * 64) + lane];
-    const int col = j * 32 + r;
-    const float bias = a.bias[col];
     const int ex = *a.xexp, ew = *a.wexp;
-    const float ua = exp2i(-ex), uw = exp2i(-ew);
     const uint32_t am = amax_read(a.amax_x), nm = amax_read(a.ynorm), bm = *a.ybias;
     const int ey = bound_exp(am, nm, bm);
     const float bnd = __uint_as_float(am) * __uint_as_float(nm) + __uint_as_float(bm);
     const float sy = __builtin_isfinite(bnd) ? exp2i(ey) : __builtin_nanf("");
+    // the epilogue in the output's scaled domain: y = relu((x ua) (uw sy) + bias sy) is the sg2 form's
+    // relu((x ua) uw + bias) sy exactly (powers of two), and its planes are y's split
+    const float ua = exp2i(-ex), uws = exp2i(-ew) * sy;
+    if (threadIdx.x < 64) reinterpret_cast<float*>(lds + Gm::BIAS)[threadIdx.x] = a.bias[threadIdx.x] * sy;
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.yexp_out = ey;
     __builtin_amdgcn_s_waitcnt(0);  // everything above landed (hipcc's own bookkeeping sees it)
+    __syncthreads();                // (the biases)
     asm volatile("s_nop 4" ::: "memory");  // (VALU-written B registers before the first MFMA reads them)
 
-    // output planes: element (row, col) of the range at byte 256 row + 4 (col & 32) + 2 (col & 30), its
-    // pair word's low plane 64 B further (px_index); a uniform base + a 32-bit lane offset
+    // output planes: pixel row p of the range at byte 256 p; lane (r, h) of column tile j writes channels
+    // 8 t + 4 h .. + 3 of it (t = q >> 2): high plane 8 B at 128 j + 16 t + 8 h, low plane 64 B further
     uint8_t* yb = reinterpret_cast<uint8_t*>(a.y) + 2 * px_index(S0 * L::P * 64);
-    const uint32_t ycol = 4 * (col & 32) + 2 * (col & 30) + 64 * (lane & 1);
+    const uint32_t ylane = (uint32_t)(r * 256 + 128 * j + 8 * h);
+    const uint32_t bias_lane = lds0 + Gm::BIAS + (uint32_t)((j * 32 + 4 * h) * 4);
     uint32_t* bits = BITS ? a.bits_y + S0 * L::P * 2 : nullptr;
-    uint32_t om = 0u;  // the largest stored value's bits (values >= 0)
-    const int qL = (lane & 3) + 4 * ((lane >> 3) & 3), hL = (lane >> 2) & 1;
+    uint32_t om = 0u;  // the largest stored scaled value's bits (values >= 0)
     f32x16 H0, L0, H1, L1;
 
-    // epilogue element q of the 32-row block at range row pmb (the sg2 PX epilogue, one column tile):
-    // relu((hi + lo) ua uw + bias) as planes; FULL: every row of the block is in the range
-    // (epi_val: the value and its pair word; epi_store: the store, the amax, the bitmask word — the two
-    // halves go to different MFMA gaps of a k-step)
-    auto epi_val = [&](auto Q, auto FULL, const f32x16& PH, const f32x16& PL, int pmb, float& v, uint32_t& w) {
-        constexpr int q = decltype(Q)::value, R0 = (q & 3) + 8 * (q >> 2);
-        v = fmaxf((PH[q] + PL[q]) * ua * uw + bias, 0.f);
-        if constexpr (!decltype(FULL)::value) v = pmb + R0 + 4 * h < MR ? v : 0.f;
-        w = px_pair_word(v, sy, lane & 1);
+    // epilogue group t (accumulator elements 4 t .. 4 t + 3) of the 32-pixel block at range row pmb:
+    // epi_val: the four scaled values (bs: their scaled biases, read from LDS a k-step before);
+    // epi_store: their planes' two 8-B runs; epi_mask: the amax and the ReLU bits.  FULL: every row of the
+    // block is in the range (else the lane's pixel pmb + r must be)
+    auto epi_val = [&](auto T, const f32x16& PH, const f32x16& PL, const u32x4& bs, float (&y)[4]) {
+        constexpr int t = decltype(T)::value;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            y[k] = fmaxf((PH[4 * t + k] + PL[4 * t + k]) * ua * uws + __uint_as_float(bs[k]), 0.f);
     };
-    auto epi_store = [&](auto Q, auto FULL, int pmb, float v, uint32_t w, int& bw) {
-        constexpr int q = decltype(Q)::value, R0 = (q & 3) + 8 * (q >> 2);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(yb + ((uint32_t)(pmb + 4 * h) * 256u + ycol + R0 * 256));
-        if constexpr (decltype(FULL)::value) {
-            *dst = w;
-        } else {
-            if (pmb + R0 + 4 * h < MR) *dst = w;
-        }
-        om = max(om, __float_as_uint(v) & 0x7FFFFFFFu);
-        if constexpr (BITS) {
-            const unsigned long long b = __ballot(v > 0.f);
-            // lane L < 32 keeps row L's word: half hL of the ballot of element qL
-            bw = qL == q ? (int)(uint32_t)(hL ? b >> 32 : b) : bw;
+    auto epi_store = [&](auto T, auto FULL, int pmb, const float (&y)[4]) {
+        constexpr int t = decltype(T)::value;
+        uint32_t hw[2], lw[2];
+        split2h((f32x2){y[0], y[1]}, 1.f, hw[0], lw[0]);
+        split2h((f32x2){y[2], y[3]}, 1.f, hw[1], lw[1]);
+        uint8_t* dst = yb + ((uint32_t)pmb * 256u + ylane + 16 * t);
+        if (decltype(FULL)::value || pmb + r < MR) {
+            *reinterpret_cast<uint2*>(dst) = make_uint2(hw[0], hw[1]);
+            *reinterpret_cast<uint2*>(dst + 64) = make_uint2(lw[0], lw[1]);
         }
     };
-    auto epi_elem = [&](auto Q, auto FULL, const f32x16& PH, const f32x16& PL, int pmb, int& bw) {
-        float v;
-        uint32_t w;
-        epi_val(Q, FULL, PH, PL, pmb, v, w);
-        epi_store(Q, FULL, pmb, v, w, bw);
-    };
-    auto epi_bits = [&](int pmb, int bw) {
+    auto epi_mask = [&](auto T, const float (&y)[4], int& bw) {
+        constexpr int t = decltype(T)::value;
+        const uint32_t u0 = __float_as_uint(y[0]), u1 = __float_as_uint(y[1]), u2 = __float_as_uint(y[2]),
+                       u3 = __float_as_uint(y[3]);
+        om = max(om, max(max(u0, u1), max(u2, u3)) & 0x7FFFFFFFu);
         if constexpr (BITS) {
-            const int row = pmb + lane;
-            if (lane < 32 && row < MR) bits[row * 2 + j] = (uint32_t)bw;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bw |= y[k] > 0.f ? (1 << (8 * t + k)) : 0;
+        }
+    };
+    // the bitmask word of the lane's pixel: its half (channels 4 h + 8 t + k) joined with lane r ^ 32's
+    auto epi_bits = [&](auto FULL, int pmb, int bw) {
+        if constexpr (BITS) {
+            const uint32_t w = (uint32_t)(bw << (4 * h)) | (uint32_t)(__shfl_xor(bw, 32) << (4 * (1 - h)));
+            if (lane < 32 && (decltype(FULL)::value || pmb + r < MR)) bits[(pmb + r) * 2 + j] = w;
         }
     };
     // refill DMAs of a phase: up to RMAX samples, DMA x = t * DMAS + i at k-step 16 + x (NK - 16) / (RMAX DMAS),
@@ -318,29 +328,36 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
         dc_lgkm<2 * (PD - 1)>(fa[0][0], fa[0][1]);
         const int pmb = m0 - 64 + 32 * rg;
         int bw = 0;
+        u32x4 bs = {0u, 0u, 0u, 0u};  // the epilogue group's scaled biases
+        float y[4];
         // k-step i: its three MFMAs with the other work in their gaps (one wave per SIMD issues in order:
-        // an MFMA occupies the matrix pipe 32 cycles, of which its issue takes 8): gap 1 the read of k-step
-        // i + 2's high plane and the epilogue element's value, gap 2 the low plane's read and the element's
-        // store, gap 3 the refill DMAs; then the wait for k-step i + 1's fragments (k-step i + 2's may stay
-        // in flight)
+        // an MFMA occupies the matrix pipe 32 cycles, of which its issue takes 8).  The previous phase's
+        // epilogue: group t's biases read at k-step 2 t (before the fragment reads, so the step's counted
+        // wait covers them), its values, stores and mask bits in the three gaps of k-step 2 t + 1, the
+        // bitmask word at k-step 8; the refill DMAs from k-step 16; then the wait for k-step i + 1's
+        // fragments (the later k-steps' may stay in flight)
         dc_unroll(
             [&](auto I) {
                 constexpr int i = decltype(I)::value;
-                // mfma_split3: hi += aH bH, lo += aH bL, lo += aL bH (B fragment (c, s, p) in AGPRs below NA)
+                // mfma_split3: hi += aH bH, lo += aH bL, lo += aL bH (weight fragment (c, s, p) in AGPRs below NA)
                 constexpr int fb = (i >> 1) * 4 + (i & 1) * 2;
                 constexpr bool A0 = fb < F::NA, A1 = fb + 1 < F::NA;
                 const u32x4& b0 = bq[i >> 1][i & 1][0];
                 const u32x4& b1 = bq[i >> 1][i & 1][1];
-                constexpr bool EPI = decltype(PREV)::value && i < 16;
-                float ev = 0.f;
-                uint32_t ew2 = 0u;
+                constexpr bool P = decltype(PREV)::value;
+                constexpr bool EPI_BIAS = P && i < 8 && (i & 1) == 0, EPI = P && i < 8 && (i & 1) == 1;
+                using T = std::integral_constant<int, i / 2>;
                 if constexpr (i == 0)
                     dc_mfma0<A0>(H, fa[0][0], b0);
                 else
                     dc_mfma<A0>(H, fa[i % NB][0], b0);
+#ifndef DC_NO_EPI
+                if constexpr (EPI_BIAS) bs = dc_read<0>(bias_lane + 32 * (i / 2));
+                if constexpr (P && i == 8) epi_bits(std::true_type{}, pmb, bw);
+#endif
                 if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 0>{});
 #ifndef DC_NO_EPI
-                if constexpr (EPI) epi_val(std::integral_constant<int, i>{}, std::true_type{}, PH, PL, pmb, ev, ew2);
+                if constexpr (EPI) epi_val(T{}, PH, PL, bs, y);
 #endif
                 if constexpr (i == 0)
                     dc_mfma0<A1>(Lo, fa[0][0], b1);
@@ -348,13 +365,15 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
                     dc_mfma<A1>(Lo, fa[i % NB][0], b1);
                 if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 1>{});
 #ifndef DC_NO_EPI
-                if constexpr (EPI) epi_store(std::integral_constant<int, i>{}, std::true_type{}, pmb, ev, ew2, bw);
-                if constexpr (decltype(PREV)::value && i == 16) epi_bits(pmb, bw);
+                if constexpr (EPI) epi_store(T{}, std::true_type{}, pmb, y);
 #endif
 #ifdef DC_LO2  // (timing probe only: the third product into hi, no back-to-back dependent MFMAs)
                 dc_mfma<A0>(H, fa[i % NB][1], b0);
 #else
                 dc_mfma<A0>(Lo, fa[i % NB][1], b0);
+#endif
+#ifndef DC_NO_EPI
+                if constexpr (EPI) epi_mask(T{}, y, bw);
 #endif
                 // the refill DMAs whose k-step this is
                 dc_unroll(
@@ -368,7 +387,12 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
                     },
                     std::make_integer_sequence<int, NDMA>{});
                 constexpr int later = (i + PD < NK ? i + PD : NK - 1) - (i + 1);  // k-steps read after i + 1
-                if constexpr (i + 1 < NK) dc_lgkm<2 * later>(fa[(i + 1) % NB][0], fa[(i + 1) % NB][1]);
+                if constexpr (i + 1 < NK) {
+                    if constexpr (EPI_BIAS)
+                        dc_lgkm<2 * later>(fa[(i + 1) % NB][0], fa[(i + 1) % NB][1], bs);
+                    else
+                        dc_lgkm<2 * later>(fa[(i + 1) % NB][0], fa[(i + 1) % NB][1]);
+                }
             },
             std::make_integer_sequence<int, NK>{});
         // (a refill of more than RMAX samples: never after phase 0, whose samples the prologue issued)
@@ -379,8 +403,17 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
     auto final_epi = [&](const f32x16& PH, const f32x16& PL) {
         const int pmb = 64 * (F_ - 1) + 32 * rg;
         int bw = 0;
-        dc_unroll([&](auto Q) { epi_elem(Q, std::false_type{}, PH, PL, pmb, bw); }, std::make_integer_sequence<int, 16>{});
-        epi_bits(pmb, bw);
+        dc_unroll(
+            [&](auto T) {
+                constexpr int t = decltype(T)::value;
+                const u32x4 bs = *reinterpret_cast<const u32x4*>(lds + Gm::BIAS + (j * 32 + 4 * h + 8 * t) * 4);
+                float y[4];
+                epi_val(T, PH, PL, bs, y);
+                epi_store(T, std::false_type{}, pmb, y);
+                epi_mask(T, y, bw);
+            },
+            std::make_integer_sequence<int, 4>{});
+        epi_bits(std::false_type{}, pmb, bw);
     };
 
     // phases alternate between the accumulator sets (H0, L0) and (H1, L1); the previous set's epilogue
@@ -397,7 +430,7 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
         final_epi(H1, L1);
     else
         final_epi(H0, L0);
-    amax_record(a.amax_y, __uint_as_float(om));
+    amax_record(a.amax_y, __uint_as_float(om) * exp2i(-ey));  // (unscaled: exact)
 }
 
 int dconv_cus() {
