@@ -78,10 +78,10 @@ EX_H2, EX_H3, EX_G3, EX_DF = range(4)
 # registers.  PPOX_PX=0: f32 tensors (split in the consumers).  Needs the ReLU bitmasks (the
 # dgrads' masks cannot come from planes).
 PX = os.environ.get("PPOX_PX", "1") != "0"
-# ... from this batch up (PPOX_PX_MIN): at the 8-GPU per-rank minibatch of 2,048 rows PX measured
-# slower (same-box A/B 225.8 vs 219.5 ms per iteration: the producers' epilogues sit on the main
-# stream, the consumers it speeds up on the side stream), at 16,384 rows faster
-PX_MIN_BATCH = int(os.environ.get("PPOX_PX_MIN", "8192"))
+# ... from this batch up (PPOX_PX_MIN): every batch since the direct conv2 / conv3 forwards (csrc/dconv.hip,
+# which need the planes; same-box A/B: 1-GPU line 478.6k vs 469.9k env-steps/s — the collect forward at 4,096
+# rows gains most — and per-rank 204.8 vs 207.3 ms; before them PX at 2,048 rows measured 225.8 vs 219.5 ms)
+PX_MIN_BATCH = int(os.environ.get("PPOX_PX_MIN", "0"))
 # PX df (round 4, PPOX_PX_DF=1): the fc layer's df (B x 512, its amax recorded by the head backward)
 # split into its planes by one small kernel (ppox_px_split) for the fc dgrad and weight gradient, which
 # otherwise split every df value in registers once per tile (the fc dgrad: 49 times).  Off by default:
