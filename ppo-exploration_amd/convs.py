@@ -84,10 +84,11 @@ PX = os.environ.get("PPOX_PX", "1") != "0"
 PX_MIN_BATCH = int(os.environ.get("PPOX_PX_MIN", "0"))
 # PX df (round 4, PPOX_PX_DF=1): the fc layer's df (B x 512, its amax recorded by the head backward)
 # split into its planes by one small kernel (ppox_px_split) for the fc dgrad and weight gradient, which
-# otherwise split every df value in registers once per tile (the fc dgrad: 49 times).  Off by default:
-# same-box A/B (profiles/r04_ab.txt) 1-GPU 1,152.5 vs 1,146.8 ms, per-rank 203.9 vs 201.8 ms per
-# iteration with it on — the fc kernels are not bound by the split's VALU work
-PX_DF = os.environ.get("PPOX_PX_DF", "0") == "1"
+# otherwise split every df value in registers once per tile (the fc dgrad: 49 times).  On by default
+# since the direct fc dgrad (csrc/dconv.hip fcd_kernel, which reads the planes: 195 vs 277 us at 16,384
+# rows); with the sg2 fc dgrad alone it measured neutral-to-slower (profiles/r04_ab.txt: 1-GPU 1,152.5
+# vs 1,146.8 ms, per-rank 203.9 vs 201.8 ms per iteration)
+PX_DF = os.environ.get("PPOX_PX_DF", "1") == "1"
 
 
 class PassState:

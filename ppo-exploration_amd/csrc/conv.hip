@@ -3861,6 +3861,9 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
         a.yexp_out = g3_exp_out;
         a.ynorm = pack_norm(q_dgrad, PL_FCD);
         a.ybias = pack_bmax(q_dgrad, PL_FCD);
+        if (df_exp && ppox_conv::dfcd_enabled(batch))
+            return ppox_conv::dfcd(df, batch, q_dgrad, g3, amax_df, amax_g3, relu_bits, g3_exp_out, df_exp, a.wexp,
+                                   a.ynorm, a.ybias, s);
         return df_exp ? launch_sgemm<Px<Bits, true, true>>(a, q_dgrad, blocks, s, nm)
                       : launch_sgemm<Px<Bits, false, true>>(a, q_dgrad, blocks, s, nm);
     }

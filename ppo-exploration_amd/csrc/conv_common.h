@@ -401,4 +401,9 @@ int dconv_fwd(int layer, const void* x, int64_t batch, const uint16_t* wq, const
               const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, const int* x_exp, int* y_exp_out,
               hipStream_t s);
 bool dconv_enabled(int layer, long long batch);
+// the fc dgrad on df planes -> g3 planes, the direct form (dconv.hip)
+bool dfcd_enabled(long long batch);
+int dfcd(const void* dfp, int64_t batch, const uint16_t* wq, float* g3, const uint32_t* amax_df, uint32_t* amax_g3,
+         const uint32_t* relu_bits, int* g3_exp_out, const int* df_exp, const int* wexp, const uint32_t* ynorm,
+         const uint32_t* ybias, hipStream_t s);
 }  // namespace ppox_conv

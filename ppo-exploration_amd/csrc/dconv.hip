@@ -433,6 +433,178 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
     amax_record(a.amax_y, __uint_as_float(om) * exp2i(-ey));  // (unscaled: exact)
 }
 
+// ---------------------------------------------------------------------------------------------
+// The fc dgrad in the same form (round 4): g3 = (h3 > 0) * (df W), df (rows x 512) as PX planes
+// (ppox_px_split), W the fc weight's dgrad packing (64-column blocks, split_frag_index), g3 written as
+// PX planes (NHWC features), .ipynb_checkpoints/models-checkpoint.py:58-59 backward.  Workgroup
+// (column group cg, row group rr): its 4 waves hold the weights of column tiles 4 cg .. 4 cg + 3 (32
+// features each, 64 fragments = 256 AGPRs), and walk the rows [r0, r1) in phases of 32; each phase's df
+// rows (2 KB each) are DMA'd into a 2-slot LDS ring (16-B pieces XOR-keyed by row & 15: conflict-free
+// b128 reads) and read by all four waves.  Same per-element MFMA sequence as the sg2 fc dgrad
+// (Px<SgRows<512, 3136, FC_DGRAD, .., true>, true, true>), so g3, its amax and exponent are bitwise its.
+constexpr int FCD_N = 3136, FCD_TILES = FCD_N / 32, FCD_ROWB = 2048, FCD_PH = 32;
+constexpr int FCD_SLOT = FCD_PH * FCD_ROWB, FCD_LDS = 2 * FCD_SLOT;
+static_assert(FCD_LDS <= 160 * 1024, "fcd: LDS");
+
+__global__ void __launch_bounds__(256, 1) fcd_kernel(Args a, const u32x4* __restrict__ wq, int nrg) {
+    constexpr int NK = 32, KC = 16;  // k-steps, 32-k chunks
+    __shared__ __attribute__((aligned(16))) uint8_t lds[FCD_LDS];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int cg = blockIdx.x / nrg, rr = blockIdx.x % nrg;
+    const int T = cg * 4 + wave;                 // this wave's column tile
+    const bool live = T < FCD_TILES;             // (the last group's waves 2, 3: DMAs and barriers only)
+    const int Tc = live ? T : FCD_TILES - 1;
+    const long long r0 = rr * a.batch / nrg, r1 = (rr + 1) * a.batch / nrg;
+    const int MR = (int)(r1 - r0);
+    if (MR <= 0) return;
+    const int F_ = (MR + FCD_PH - 1) / FCD_PH;
+    const uint8_t* xb = reinterpret_cast<const uint8_t*>(a.x) + r0 * FCD_ROWB;
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
+
+    // phase f's rows into slot f & 1: wave w DMAs rows 8 w .. 8 w + 7 (two 1-KB DMAs each; LDS piece q of
+    // row rho holds global piece q ^ (rho & 15)); rows past the range re-read the last row (never stored)
+    auto issue_phase = [&](int f) {
+        uint8_t* dst = lds + (f & 1) * FCD_SLOT;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int rho = wave * 8 + (i >> 1), d = i & 1;
+            int row = f * FCD_PH + rho;
+            row = row < MR ? row : MR - 1;
+            const uint32_t q = (uint32_t)(d * 64 + lane);
+            const uint32_t off = (uint32_t)row * FCD_ROWB + ((q ^ (uint32_t)(rho & 15)) << 4);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xb + off),
+                                             (__attribute__((address_space(3))) void*)(dst + rho * FCD_ROWB + d * 1024),
+                                             16, 0, 0);
+        }
+    };
+    issue_phase(0);
+    // the weights of tile Tc: 64-column block Tc / 2, column tile Tc & 1 of it, all 16 chunks
+    u32x4 bq[KC][2][2];
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+                bq[c][s][p] = wq[(long long)((Tc >> 1) * KC + c) * (2 * 2 * NPL * 64) + (((s * 2 + (Tc & 1)) * 2 + p) * 64) + lane];
+    const int ex = *a.xexp, ew = *a.wexp;
+    const uint32_t am = amax_read(a.amax_x), nm = amax_read(a.ynorm), bm = *a.ybias;
+    const int ey = bound_exp(am, nm, bm);
+    const float bnd = __uint_as_float(am) * __uint_as_float(nm) + __uint_as_float(bm);
+    const float sy = __builtin_isfinite(bnd) ? exp2i(ey) : __builtin_nanf("");
+    const float ua = exp2i(-ex), uws = exp2i(-ew) * sy;  // (the sg2 value (acc ua) uw, times sy: exact)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.yexp_out = ey;
+    __builtin_amdgcn_s_waitcnt(0);
+    asm volatile("s_nop 4" ::: "memory");
+
+    uint16_t* y16 = reinterpret_cast<uint16_t*>(a.y);
+    uint32_t om = 0u;
+    f32x16 H0, L0, H1, L1;
+    // epilogue group t of the 32-row block at range row pmb: lane (r, h) = row r0 + pmb + r, features
+    // 32 Tc + 8 t + 4 h .. + 3 (mask bits of word mw)
+    auto epi = [&](auto Tt, const f32x16& PH, const f32x16& PL, int pmb, uint32_t mw, auto FULL) {
+        constexpr int t = decltype(Tt)::value;
+        if (!live) return;  // (uniform: a tile past the last computed nothing)
+        float y[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            y[k] = (mw >> (8 * t + 4 * h + k)) & 1u ? (PH[4 * t + k] + PL[4 * t + k]) * ua * uws : 0.f;
+        uint32_t hw[2], lw[2];
+        split2h((f32x2){y[0], y[1]}, 1.f, hw[0], lw[0]);
+        split2h((f32x2){y[2], y[3]}, 1.f, hw[1], lw[1]);
+        const long long m = r0 + pmb + r;
+        uint16_t* dst = y16 + 2 * (m * FCD_N + Tc * 32) + 8 * t + 4 * h;
+        if (decltype(FULL)::value || pmb + r < MR) {
+            *reinterpret_cast<uint2*>(dst) = make_uint2(hw[0], hw[1]);
+            *reinterpret_cast<uint2*>(dst + 32) = make_uint2(lw[0], lw[1]);
+        }
+        om = max(om, max(max(__float_as_uint(y[0]) & 0x7FFFFFFFu, __float_as_uint(y[1]) & 0x7FFFFFFFu),
+                         max(__float_as_uint(y[2]) & 0x7FFFFFFFu, __float_as_uint(y[3]) & 0x7FFFFFFFu)));
+    };
+    auto mask_word = [&](int pmb) {
+        long long m = r0 + pmb + r;
+        m = m < r1 ? m : r1 - 1;
+        return a.bits_mask[m * FCD_TILES + Tc];
+    };
+
+    auto phase = [&](int f, f32x16& H, f32x16& Lo, const f32x16& PH, const f32x16& PL, auto PREV) {
+        // this phase's rows (DMA'd during the previous phase) landed for every wave; every wave done with
+        // the slot the next phase refills
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        constexpr bool P = decltype(PREV)::value;
+        const int pmb = FCD_PH * (f - 1);
+        const uint32_t mw = P ? mask_word(pmb) : 0u;
+        const uint32_t base = lds0 + (f & 1) * FCD_SLOT + r * FCD_ROWB;
+        const uint32_t kx = (uint32_t)((r & 15) ^ h) << 4;
+        auto addr = [&](int i, int pl) {  // k-step i = 2 c + s: piece 8 c + 4 pl + 2 s + h of row r
+            const int c = i >> 1, s = i & 1;
+            const uint32_t P16 = (uint32_t)(((c & 1) << 3) | (pl << 2) | (s << 1)) << 4;
+            return base + (P16 ^ kx);
+        };
+        constexpr int PD = 2, NB = 3;
+        u32x4 fa[NB][2];
+        auto rd1 = [&](auto I, auto PLc) {
+            constexpr int i = decltype(I)::value, pl = decltype(PLc)::value;
+            fa[i % NB][pl] = dc_read<((i >> 1) >> 1) * 256>(addr(i, pl));
+        };
+        rd1(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+        rd1(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+        rd1(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+        rd1(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+        dc_lgkm<2>(fa[0][0], fa[0][1]);
+        dc_unroll(
+            [&](auto I) {
+                constexpr int i = decltype(I)::value;
+                const u32x4& b0 = bq[i >> 1][i & 1][0];
+                const u32x4& b1 = bq[i >> 1][i & 1][1];
+                if (live) {
+                    if constexpr (i == 0)
+                        dc_mfma0<true>(H, fa[0][0], b0);
+                    else
+                        dc_mfma<true>(H, fa[i % NB][0], b0);
+                }
+                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 0>{});
+                if (live) {
+                    if constexpr (i == 0)
+                        dc_mfma0<true>(Lo, fa[0][0], b1);
+                    else
+                        dc_mfma<true>(Lo, fa[i % NB][0], b1);
+                }
+                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 1>{});
+                if constexpr (P && (i & 1) && i < 8) epi(std::integral_constant<int, i / 2>{}, PH, PL, pmb, mw, std::true_type{});
+                if (live) dc_mfma<true>(Lo, fa[i % NB][1], b0);
+                // the next phase's rows: 16 DMAs over k-steps 16 .. 31
+                if constexpr (i == 16) {
+                    if (f + 1 < F_) issue_phase(f + 1);
+                }
+                constexpr int later = (i + PD < NK ? i + PD : NK - 1) - (i + 1);
+                if constexpr (i + 1 < NK) dc_lgkm<2 * later>(fa[(i + 1) % NB][0], fa[(i + 1) % NB][1]);
+            },
+            std::make_integer_sequence<int, NK>{});
+        dc_acc_fence(H, Lo);
+    };
+    auto final_epi = [&](const f32x16& PH, const f32x16& PL) {
+        const int pmb = FCD_PH * (F_ - 1);
+        const uint32_t mw = mask_word(pmb);
+        dc_unroll([&](auto Tt) { epi(Tt, PH, PL, pmb, mw, std::false_type{}); }, std::make_integer_sequence<int, 4>{});
+    };
+    phase(0, H0, L0, H1, L1, std::false_type{});
+    int f = 1;
+#pragma unroll 1
+    for (; f + 1 < F_; f += 2) {
+        phase(f, H1, L1, H0, L0, std::true_type{});
+        phase(f + 1, H0, L0, H1, L1, std::true_type{});
+    }
+    if (f < F_) phase(f, H1, L1, H0, L0, std::true_type{});
+    if ((F_ - 1) & 1)
+        final_epi(H1, L1);
+    else
+        final_epi(H0, L0);
+    amax_record(a.amax_y, __uint_as_float(om) * exp2i(-ey));
+}
+
 int dconv_cus() {
     static int cus[64] = {};
     int dev = 0;
@@ -468,6 +640,9 @@ int launch_dconv(const Args& a, const uint16_t* wq, hipStream_t s, const char* n
 
 }  // namespace
 
+#ifndef DFCD_DEFAULT
+#define DFCD_DEFAULT true  // the direct fc dgrad unless PPOX_DFCD says otherwise
+#endif
 #ifndef DCONV_DEFAULT
 #define DCONV_DEFAULT true  // the direct forms unless PPOX_DCONV2 / PPOX_DCONV3 say otherwise
 #endif
@@ -493,5 +668,24 @@ int dconv_fwd(int layer, const void* x, int64_t batch, const uint16_t* wq, const
     a.ybias = pack_bmax(wq, planes(layer));
     if (layer == 2) return launch_dconv<DcF2>(a, wq, s, "ppox_nature_conv2_fwd_planes");
     return launch_dconv<DcF3>(a, wq, s, "ppox_nature_conv_fwd_split");
+}
+
+// the fc dgrad's direct form (PPOX_DFCD=1; _MIN: the smallest batch): df planes in, g3 planes out, h3's bitmask
+bool dfcd_enabled(long long batch) { return env_on("PPOX_DFCD", batch, DFCD_DEFAULT); }
+int dfcd(const void* dfp, int64_t batch, const uint16_t* wq, float* g3, const uint32_t* amax_df, uint32_t* amax_g3,
+         const uint32_t* relu_bits, int* g3_exp_out, const int* df_exp, const int* wexp, const uint32_t* ynorm,
+         const uint32_t* ybias, hipStream_t s) {
+    const int cus = dconv_cus();
+    PPOX_REQUIRE(cus > 0, "ppox_nature_fc_dgrad: no device");
+    Args a{dfp, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, g3, batch, amax_df, amax_g3, wexp};
+    a.bits_mask = relu_bits;
+    a.xexp = df_exp;
+    a.yexp_out = g3_exp_out;
+    a.ynorm = ynorm;
+    a.ybias = ybias;
+    constexpr int ngroups = (FCD_TILES + 3) / 4;
+    const int nrg = (int)std::max<long long>(1, std::min<long long>(cus / ngroups, batch));
+    fcd_kernel<<<(unsigned)(ngroups * nrg), 256, 0, s>>>(a, reinterpret_cast<const u32x4*>(wq), nrg);
+    PPOX_LAUNCHED("ppox_nature_fc_dgrad");
 }
 }  // namespace ppox_conv

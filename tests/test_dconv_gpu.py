@@ -60,3 +60,40 @@ def test_direct_conv_forward_is_the_gemm_bitwise(B, layer):
     if ba is not None:
         assert torch.equal(ba, bb), (ba != bb).nonzero()[:8]
     assert (ya.view(torch.int16) != 0).any()  # not a vacuous comparison
+
+
+@pytest.mark.parametrize("B", [1, 37, 2048, 9001, 16384])
+def test_direct_fc_dgrad_is_the_gemm_bitwise(B):
+    """The fc dgrad's direct form (PPOX_DFCD=1, csrc/dconv.hip fcd_kernel: weights in AGPRs, df planes
+    streamed through LDS) against the sg2 GEMM on the same df planes: g3's planes, amax and exponent equal.
+    Reference: .ipynb_checkpoints/models-checkpoint.py:58-59 (Linear(3136, 512)) backward."""
+    import convs
+    import native
+    cv = _trunk(B)
+    cv.pack(B)
+    g = torch.Generator(device="cuda").manual_seed(B)
+    df = torch.randn(B, 512, device="cuda", generator=g) * torch.rand(B, 512, device="cuda", generator=g) ** 2
+    am = native.amax_table(convs.AM_ROWS, "cuda")
+    native.amax(df, am[convs.AM_DF])
+    e = torch.zeros(1, dtype=torch.int32, device="cuda")
+    dfp = torch.empty(B, 1024, dtype=torch.int16, device="cuda")
+    native.px_split(df, am[convs.AM_DF], dfp, e)
+    bits = torch.randint(-2 ** 31, 2 ** 31 - 1, (B * 98,), dtype=torch.int32, device="cuda", generator=g)
+    outs = []
+    for direct in (False, True):
+        os.environ["PPOX_DFCD"] = "1" if direct else "0"
+        g3 = torch.empty(B, 7, 7, 128, dtype=torch.int16, device="cuda")
+        ex = torch.zeros(1, dtype=torch.int32, device="cuda")
+        amg = native.amax_table(1, "cuda")
+        with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+            native.nature_fc_dgrad(dfp, B, cv.qfc[1], None, g3, amax_df=am[convs.AM_DF], df_exp=e, relu_bits=bits,
+                                   g3_exp=ex, amax_g3=amg[0])
+            torch.cuda.synchronize()
+        names = " ".join(ev.name for ev in prof.events())
+        assert ("fcd_kernel" in names) == direct, names[:2000]
+        outs.append((g3, int(ex.item()), amg[0].cpu().numpy().view(np.uint32).max()))
+    os.environ.pop("PPOX_DFCD", None)
+    (ga, ea, ma), (gb, eb, mb) = outs
+    assert ea == eb and ma == mb, (ea, eb, ma, mb)
+    assert torch.equal(ga, gb), (ga != gb).nonzero()[:8]
+    assert (ga != 0).any()
