@@ -401,6 +401,10 @@ int dconv_fwd(int layer, const void* x, int64_t batch, const uint16_t* wq, const
               const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, const int* x_exp, int* y_exp_out,
               hipStream_t s);
 bool dconv_enabled(int layer, long long batch);
+// the heads' hidden-layer dgrad (df in place), the direct form (dconv.hip)
+bool dhdd_enabled(long long batch);
+int dhdd(const float* de, int64_t rows, const uint16_t* wq, const float* f, float* df, const uint32_t* amax_de,
+         uint32_t* amax_df, const int* wexp, hipStream_t s);
 // the fc dgrad on df planes -> g3 planes, the direct form (dconv.hip)
 bool dfcd_enabled(long long batch);
 int dfcd(const void* dfp, int64_t batch, const uint16_t* wq, float* g3, const uint32_t* amax_df, uint32_t* amax_g3,
