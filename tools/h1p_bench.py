@@ -10,6 +10,9 @@ sys.path.insert(0, os.path.join(ROOT, "ppo-exploration_amd"))
 import torch  # noqa: E402
 import native  # noqa: E402
 
+if os.environ.get("PPOX_LIB"):
+    native.load(os.environ["PPOX_LIB"])
+
 
 def timed(fn, reps):
     fn()
