@@ -124,7 +124,8 @@ def _kernels():
                                           label="fc fwd split-K")
     k["ppox_nature_fc_dgrad"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=FC_N * 4 + ACT_B[3] + BITMASK_B[3],
                                      fixed=w_fc, products=3,
-                                     rocprof=_rows(512, 3136, 1, "true"), label="fc dgrad")
+                                     # (the direct form, csrc/dconv.hip fcd_kernel, by default; PPOX_DFCD=0: sg2)
+                                     rocprof=r"(fcd_kernel|" + _rows(512, 3136, 1, "true") + ")", label="fc dgrad")
     k["ppox_nature_fc_wgrad"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=FC_N * 4 + ACT_B[3], fixed=w_fc, products=3,
                                      rocprof=re.escape("wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 49") + IDX + ">",
                                      label="fc wgrad")
@@ -134,7 +135,7 @@ def _kernels():
                                      label="head hidden fwd")
     # dgrad: de in, the heads' input grad read + written (accumulated in place), f read for the ReLU
     k["ppox_head_hidden_dgrad"] = dict(rows_arg=1, macs=HID * HID, bytes=4 * HID * 4, fixed=w_h, products=3,
-                                       rocprof=_rows(512, 512, 2, "false"),
+                                       rocprof=r"(hdd_kernel|" + _rows(512, 512, 2, "false") + ")",
                                        label="head hidden dgrad")
     k["ppox_head_hidden_wgrad"] = dict(rows_arg=1, macs=HID * HID, bytes=2 * HID * 4, fixed=w_h, products=3,
                                        rocprof=re.escape("wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 8>"),
