@@ -19,7 +19,7 @@ python3 $R/tools/trace_by_grid.py $O/kernel_trace.csv $O/kernel_by_grid.csv || e
 python3 $R/tools/timeline.py $O/kernel_trace.csv > $O/timeline_minibatch_16384.txt || exit $?
 # HBM bytes per launch: FETCH_SIZE and WRITE_SIZE in separate passes (TCC counter slots)
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "wgrad|gae|gemm|split_kernel|colp_kernel|planes|dconv" \
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "wgrad|gae|gemm|split_kernel|colp_kernel|planes|dconv|fcd_kernel" \
       -d /tmp/$TAG-$C -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --epochs 1 \
       --no-cpu-baseline > $O/pmc_$C.log 2>&1 || exit $?
   find /tmp/$TAG-$C -name "*counter_collection.csv" -exec cp {} $O/pmc_$C.csv \; || exit 1
