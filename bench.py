@@ -81,8 +81,9 @@ def _kernels():
     # collect pass's forward of the same name without it runs at another row count
     roc = {("fwd", 1): r"fwd1_split_kernel<1, false, true>",
            ("fwd", 2): _sg("SgFwd<32, 20, 20, 4, 4, 2, 64, false>", "4, 2"),
-           # (the planes forward: the direct form, csrc/dconv.hip, by default; the sg2 GEMM with PPOX_DCONV3=0)
-           ("fwd", 3): r"(dconv_fwd_kernel<DcF3, \w+>|" + _sg("SgFwd<64, 9, 9, 3, 3, 1, 64, false>", "4, 2") + ")",
+           # (the planes forward: the direct form, csrc/dconv.hip, by default; the sg2 GEMM with PPOX_DCONV3=0;
+           # a training pass writes the ReLU bitmask (BITS = true), the collect pass's 4,096-row forward does not)
+           ("fwd", 3): r"(dconv_fwd_kernel<DcF3, true>|" + _sg("SgFwd<64, 9, 9, 3, 3, 1, 64, false>", "4, 2") + ")",
            ("dgrad", 2): r"dgrad2_colp_kernel<true, false>",
            ("dgrad", 3): _sg("SgDgradPM<64, 9, 9, 3, 3, 1, 64, true>", "4, 2"),
            ("wgrad", 1): (re.escape("wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>")
@@ -111,7 +112,7 @@ def _kernels():
     k["ppox_nature_conv1_fwd_planes"] = dict(rows_arg=1, macs=CONV_MAC[1], bytes=ACT_B[0] + ACT_B[1], fixed=0,
                                              products=2, rocprof=r"fwd1_split_kernel<1, true, true>", label="conv1 fwd (H1P)")
     k["ppox_nature_conv2_fwd_planes"] = dict(rows_arg=2, macs=CONV_MAC[2], bytes=ACT_B[1] + ACT_B[2], fixed=0,
-                                             products=3, rocprof=r"(dconv_fwd_kernel<DcF2, \w+>|" + _sg("SgFwd2P", "4, 2") + ")",
+                                             products=3, rocprof=r"(dconv_fwd_kernel<DcF2, true>|" + _sg("SgFwd2P", "4, 2") + ")",
                                              label="conv2 fwd (H1P)")
     k["ppox_nature_conv2_wgrad_planes"] = dict(rows_arg=2, macs=CONV_MAC[2], bytes=ACT_B[1] + ACT_B[2], fixed=0,
                                                products=3, rocprof="wgrad2_planes_kernel",
