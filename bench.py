@@ -283,16 +283,81 @@ def parse():
     p.add_argument("--force-dist", action="store_true",
                    help="one rank: run the world > 1 code paths (owned-row minibatches, every collective) over a "
                         "one-rank RCCL communicator — the per-rank program of an 8-GPU run on one GPU")
+    p.add_argument("--launch-check", action="store_true",
+                   help="launcher rehearsal without a GPU: every rank joins the process group (gloo), agrees on "
+                        "the world size and rank 0 prints the line's identity fields with value null")
     return p.parse_args()
+
+
+def _free_port():
+    import socket
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) started as a plain process: run the N ranks through
+    torch.distributed.run as a CHILD process (one rank per GPU, rendezvous on 127.0.0.1) and
+    forward rank 0's JSON line and the child's exit code.  This process touches no GPU and never
+    execs: the ranks initialise their own devices.  (reference step being sharded: ppo.py:241-244)"""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode == 0 and len(lines) != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 3
+    for ln in lines:
+        print(ln, flush=True)
+    return p.returncode
+
+
+def _world_guard(args, world):
+    """A scaling run must measure the world it was asked for: --gpus N with WORLD_SIZE != N
+    (a launcher that started the wrong number of ranks) fails instead of reporting a number."""
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report", file=sys.stderr)
+        sys.exit(2)
+
+
+def launch_check(args, json_out):
+    """--launch-check: the multi-rank plumbing of main() without the workload (CPU, gloo)."""
+    import torch
+    import torch.distributed as tdist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    _world_guard(args, world)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        tdist.init_process_group("gloo")
+        t = torch.tensor([1.0])
+        tdist.all_reduce(t)
+        assert int(t.item()) == world
+    if rank == 0:
+        print(json.dumps({"metric": "env-steps/sec (collect+GAE+PPO update), 4096 envs×128 steps @ 1/2/4/8 GPU",
+                          "value": None, "unit": "env-steps/s", "n_gpus": world, "launch_check": True,
+                          "config": {"parallelism": f"dp{world}" if world > 1 else "single GPU"}}),
+              file=json_out, flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     # stdout carries the one JSON line only: whatever else writes to fd 1 (RCCL prints its version
     # banner there when a communicator is created) goes to stderr
     sys.stdout.flush()
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    if args.launch_check:
+        return launch_check(args, json_out)
     import numpy as np
     import torch
     import torch.distributed as tdist
@@ -300,6 +365,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    _world_guard(args, world)
     # PPOX_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU
     # (RCCL refuses two ranks on one device); the driver's runs use RCCL, one GPU per rank
     backend = os.environ.get("PPOX_DIST_BACKEND", "nccl")
@@ -313,11 +379,7 @@ def main():
         else:
             tdist.init_process_group(backend)
     elif args.force_dist:
-        import socket
-        sk = socket.socket()
-        sk.bind(("127.0.0.1", 0))
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]))
-        sk.close()
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
         tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
         sys.path.insert(0, os.path.join(ROOT, "ppo-exploration_amd"))
         import dist as _dist
@@ -420,7 +482,8 @@ def main():
                    "n_envs": args.envs, "n_steps": args.nstep, "n_epochs": args.epochs,
                    "batch_size": args.batch_size, "minibatches_per_epoch": -(-args.envs * args.nstep // args.batch_size),
                    "conv_math": conv_impl.math if conv_impl is not None else None,
-                   "parallelism": f"dp{world} (env-sharded, RCCL grad all-reduce)" if world > 1 else
+                   "parallelism": f"dp{world} (env-sharded, {'RCCL' if backend == 'nccl' else backend} grad all-reduce)"
+                   if world > 1 else
                    ("dp code paths forced on over a one-rank RCCL communicator" if args.force_dist else "single GPU")},
     }
     # per iteration, rank 0: GPU stream time and host time of each phase (phases.py);

@@ -31,7 +31,9 @@
 // overlapping input patches are served from that XCD's L2.
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
+#include <unordered_set>
 
 #include "conv_common.h"
 
@@ -3175,6 +3177,35 @@ __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long tota
     }
 }
 
+// Host record of the packed forms whose tail holds a finite PX bias bound: q2 / q3 packed WITH
+// their bias (pack_all with b2 / b3), and every fc dgrad form (no bias: its bound is 0).  A form
+// packed without its bias (ppox_nature_pack_split, pack_all with a null b2 / b3) carries a NaN
+// bound, so an entry point asked for a PX output (y_exp_out / g3_exp_out) refuses such a form
+// instead of writing NaN activations.
+std::mutex px_mu;
+std::unordered_set<const void*> px_bounded;
+
+void note_px_pack(const void* q, bool bounded) {
+    if (!q) return;
+    std::lock_guard<std::mutex> g(px_mu);
+    if (bounded)
+        px_bounded.insert(q);
+    else
+        px_bounded.erase(q);
+}
+
+}  // namespace
+
+namespace ppox_conv {
+bool px_bound_ok(const void* q) {
+    std::lock_guard<std::mutex> g(px_mu);
+    return px_bounded.count(q) != 0;
+}
+}  // namespace ppox_conv
+
+namespace {
+using ppox_conv::px_bound_ok;
+
 int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
     for (const void* q : {(const void*)p.wpd2, (const void*)p.q1, (const void*)p.q2, (const void*)p.q3,
                           (const void*)p.qd2, (const void*)p.qd3, (const void*)p.qfcf, (const void*)p.qfcd})
@@ -3193,7 +3224,11 @@ int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
                             (p.qhf || p.qhd ? PU_FCD + 2 * PU_H : (p.qfcd ? PU_FCD : 0));
     const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 4096);
     pack_all_kernel<<<blocks, 256, 0, s>>>(p, total);
-    PPOX_LAUNCHED(name);
+    PPOX_LAUNCHED_NORET(name);
+    note_px_pack(p.q2, p.b2 != nullptr);
+    note_px_pack(p.q3, p.b3 != nullptr);
+    note_px_pack(p.qfcd, true);
+    return PPOX_OK;
 }
 
 }  // namespace
@@ -3436,6 +3471,8 @@ int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq,
     a.bits_y = relu_bits;
     a.xexp = x_exp;
     a.yexp_out = y_exp_out;
+    PPOX_REQUIRE(!y_exp_out || px_bound_ok(wq),
+                 "ppox_nature_conv_fwd_split: a PX output needs wq packed with its bias (ppox_nature_pack_all)");
     a.ynorm = pack_norm(wq, planes(layer));
     a.ybias = pack_bmax(wq, planes(layer));
     constexpr const char* nm = "ppox_nature_conv_fwd_split";
@@ -3574,6 +3611,8 @@ extern "C" int ppox_nature_conv2_fwd_planes(const uint16_t* h1p, const uint16_t*
     PPOX_REQUIRE(!(reinterpret_cast<uintptr_t>(relu_bits) & 7), "ppox_nature_conv2_fwd_planes: relu_bits 8B alignment");
     PPOX_REQUIRE(!y_exp_out || (amax_x && ppox::aligned16(amax_x)),
                  "ppox_nature_conv2_fwd_planes: a PX output (y_exp_out) needs h1's amax slots (amax_x)");
+    PPOX_REQUIRE(!y_exp_out || ppox_conv::px_bound_ok(wq2),
+                 "ppox_nature_conv2_fwd_planes: a PX output needs wq2 packed with its bias (ppox_nature_pack_all)");
     Args a{h1p, nullptr, 0, 0, 0, nullptr, bias, nullptr, y, batch, amax_x, amax_y, pack_exp(wq2, PL_Q2)};
     a.bits_y = relu_bits;
     a.xexp = h1p_exp(q1, PL_Q1);
@@ -3858,6 +3897,8 @@ extern "C" int ppox_nature_fc_dgrad(const float* df, int64_t batch, const uint16
     using Acts = SgRows<512, 3136, FC_DGRAD, FC_DGRAD_GW, false, SG_FC_NB>;
     if (g3_exp_out) {  // g3 as PX planes, bounded by amax(df) * the fc weight's column norms
         PPOX_REQUIRE(relu_bits, "ppox_nature_fc_dgrad: a PX g3 needs h3's ReLU bitmask");
+        PPOX_REQUIRE(ppox_conv::px_bound_ok(q_dgrad),
+                     "ppox_nature_fc_dgrad: a PX g3 needs q_dgrad packed by ppox_nature_pack_all / fc_pack");
         a.yexp_out = g3_exp_out;
         a.ynorm = pack_norm(q_dgrad, PL_FCD);
         a.ybias = pack_bmax(q_dgrad, PL_FCD);

@@ -796,10 +796,15 @@ class PPO_ICM(BaseAlgorithm):
         self.beta = 0.2
         self._alloc_train_state()
         self.icm_accum = torch.zeros(1, dtype=torch.float64, device=self.device)
-        # the K11 minibatch's collectives (feature / action / feature-gradient exchange, the ICM
-        # gradient all-reduce) on a communicator of their own, so that at world > 1 they run on
-        # the side stream beside the policy minibatch as in one process (DistContext.subgroup)
-        self._icm_dist = self.dist.subgroup() if self.dist.enabled and self._icm_native is not None else self.dist
+        # At world > 1 the K11 minibatch and its collectives (feature / action / feature-gradient
+        # exchange, the ICM gradient all-reduce) run on the main stream after the policy's, in
+        # program order on one communicator.  PPOX_ICM_SIDE_DIST=1 (opt-in, never run on more than
+        # one GPU) runs them on the side stream beside the policy minibatch as in one process, on a
+        # communicator of their own (DistContext.subgroup): two communicators' collectives then
+        # run concurrently, which RCCL guarantees to progress only when both fit on the GPU at once.
+        self._icm_side_dist = os.environ.get("PPOX_ICM_SIDE_DIST", "0") == "1"
+        self._icm_dist = (self.dist.subgroup() if self.dist.enabled and self._icm_native is not None
+                          and self._icm_side_dist else self.dist)
         # the collect loop (policy + env + K11 curiosity reward) as one captured graph, as PPO's
         # (PPOX_COLLECT_GRAPH=0: eager launches)
         self._collect_graph_enabled = os.environ.get("PPOX_COLLECT_GRAPH", "1") != "0"
@@ -962,9 +967,11 @@ class PPO_ICM(BaseAlgorithm):
         ro = self.rollout
         Bl = idx.numel()
         # the ICM (independent of the policy: its own parameters, the same frames) runs on a
-        # side stream beside the policy's forward / loss / backward, its collectives (world > 1)
-        # on its own communicator (self._icm_dist), issued in the same program order on every rank
-        side = convs.side_stream(self.device, 1) if convs.BWD_STREAMS else None
+        # side stream beside the policy's forward / loss / backward in one process; at world > 1
+        # only with PPOX_ICM_SIDE_DIST=1 (its collectives then on their own communicator,
+        # self._icm_dist, issued in the same program order on every rank), else after the policy
+        side = (convs.side_stream(self.device, 1)
+                if convs.BWD_STREAMS and (not self.dist.enabled or self._icm_side_dist) else None)
         pos = self._epoch_pos[o0:o1] if self.dist.enabled else None
         idist = self._icm_dist
         if side is not None:

@@ -195,6 +195,46 @@ def test_minibatch_sharded_path_one_rank_matches_one_process(B):
     np.testing.assert_allclose(acc.item(), want_loss, rtol=1e-6)
 
 
+def test_pair_list_with_last_position():
+    """ppox_icm_pair_backward with a pair list: dS / dN are output-only (pre-filled with
+    NaN here, every element written), a listed B - 1 is skipped, and n_pairs may then be B: the list
+    [all positions] gives the same dS / dN as the list without B - 1 (n_pairs = B - 1), and a partial
+    list leaves the unlisted rows zero."""
+    import native
+    from icm import H
+    K, A, B = K_ATARI, 4, 37
+    icm, _, flat = _module(K, A, 21)
+    nat = _native(icm, flat, K)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    fa = torch.randn(B * (H + 1), device="cuda", generator=g)
+    fa[B * H:] = torch.randint(0, A, (B,), device="cuda", generator=g).float()
+    partials = torch.empty(native.icm_partials_bytes(B, A) // 4, device="cuda")
+
+    def run(pairs):
+        dS = torch.full((B, H), float("nan"), device="cuda")
+        dN = torch.full((B, H), float("nan"), device="cuda")
+        native.icm_pair_backward(fa, B, None, None, pairs, pairs.numel(), B - 1, A, 0.2, nat.seg, dS, dN, partials)
+        torch.cuda.synchronize()
+        return dS, dN
+    every = torch.randperm(B, generator=torch.Generator().manual_seed(4)).cuda()
+    dS_all, dN_all = run(every)
+    dS_ref, dN_ref = run(every[every != B - 1].contiguous())
+    assert torch.isfinite(dS_all).all() and torch.isfinite(dN_all).all()
+    assert torch.equal(dS_all, dS_ref) and torch.equal(dN_all, dN_ref)
+    part = torch.tensor([B - 1, 0, 5], device="cuda")
+    dS_p, dN_p = run(part)
+    listed = torch.zeros(B, dtype=torch.bool, device="cuda")
+    listed[part] = True
+    assert (dS_p[~listed] == 0).all()
+    assert torch.equal(dS_p[0], dS_all[0]) and torch.equal(dS_p[5], dS_all[5])
+    assert (dS_p[B - 1] == 0).all()
+    # dN holds the pair's second row: rows 1 and 6 get pairs 0 and 5
+    sec = torch.zeros(B, dtype=torch.bool, device="cuda")
+    sec[torch.tensor([1, 6], device="cuda")] = True
+    assert (dN_p[~sec] == 0).all()
+    assert torch.equal(dN_p[1], dN_all[1]) and torch.equal(dN_p[6], dN_all[6])
+
+
 @pytest.mark.parametrize("N,A", [(512, 4), (77, 18)])
 def test_int_reward_vs_fp64(N, A):
     """ppo.py:629-631: int_reward(s, s', a) = clamp(mean((fwd(phi(s), a) - phi(s'))^2), -5, 5),

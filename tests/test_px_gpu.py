@@ -196,3 +196,33 @@ def test_px_df_planes_are_the_consumers_split(B):
     native.nature_fc_wgrad(df, B, h3, ws, w1, amax_df=am[convs.AM_DF])
     native.nature_fc_wgrad(dfp, B, h3, ws, w2, df_exp=e)
     assert torch.equal(w1, w2)
+
+
+def test_px_output_refuses_a_form_packed_without_bias():
+    """q2 / q3 packed by ppox_nature_pack_split (no biases) carry a NaN PX bias bound; an
+    entry point asked for a PX output on such a form fails loudly instead of writing NaN activations,
+    and the same forms packed by pack_all with their biases are accepted."""
+    import native
+    torch.manual_seed(5)
+    w1 = torch.randn(32, 4, 8, 8, device="cuda") * 0.05
+    w2 = torch.randn(64, 32, 4, 4, device="cuda") * 0.05
+    w3 = torch.randn(64, 64, 3, 3, device="cuda") * 0.05
+    b1, b2, b3 = (torch.randn(c, device="cuda") * 0.1 for c in (32, 64, 64))
+    q = {k: torch.empty(native.nature_split_pack_elems(k), dtype=torch.int16, device="cuda") for k in (1, 2, 3)}
+    native.nature_pack_split(w1, w2, w3, q[1], q[2], q[3])
+    B = 3
+    h2p = torch.zeros(B, 9, 9, 64, device="cuda")      # h2 as planes (f32-sized), exponent 0
+    x_exp = torch.zeros(1, dtype=torch.int32, device="cuda")
+    y = torch.empty(B, 7, 7, 64, device="cuda")
+    y_exp = torch.zeros(1, dtype=torch.int32, device="cuda")
+    amax = native.amax_table(1, "cuda")[0]
+    bits = torch.zeros(B * 98, dtype=torch.int32, device="cuda")
+    with pytest.raises(native.NativeError, match="packed with its bias"):
+        native.nature_conv_fwd_split(3, h2p, B, None, 0, 0, 0, q[3], b3, y, amax_x=amax, relu_bits=bits,
+                                     x_exp=x_exp, y_exp=y_exp)
+    torch.cuda.synchronize()
+    native.nature_pack_all(w1, w2, w3, None, None, q[1], q[2], q[3], None, None, None, None, b1=b1, b2=b2, b3=b3)
+    native.nature_conv_fwd_split(3, h2p, B, None, 0, 0, 0, q[3], b3, y, amax_x=amax, relu_bits=bits,
+                                 x_exp=x_exp, y_exp=y_exp)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
