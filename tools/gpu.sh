@@ -5,7 +5,7 @@
 #   tools/gpu.sh TAG STEP [STEP ...]
 # Steps (output under gpurun_out/TAG/):
 #   tests            the whole GPU suite (PPOX_PARITY_OUT=parity/), tests.log
-#   tests:FILES[:K]  pytest on FILES (comma-separated, under tests/) [-k K]
+#   tests:FILES[:K]  pytest on FILES (comma-separated, under tests/) [-k K, "+" for spaces]
 #   F R RD I ID C3 ES  bench lines: F = the 1-GPU line (20 steps, no cpu baseline), FC = the default line with
 #                    the cpu baseline, R = the 8-GPU per-rank shape (512 envs, minibatch 2,048), RD = R with the
 #                    data-parallel branches over a one-rank RCCL communicator, I / ID = PPO_ICM per-rank
@@ -72,7 +72,7 @@ for STEP in "$@"; do
       tail -n 3 $O/tests.log ;;
     tests:*)
       SPEC=${STEP#tests:}; FILES=${SPEC%%:*}; K=""
-      [ "$FILES" != "$SPEC" ] && K=${SPEC#*:}
+      [ "$FILES" != "$SPEC" ] && K=$(echo ${SPEC#*:} | tr "+" " ")
       ARGS=""; for f in $(echo $FILES | tr ',' ' '); do ARGS="$ARGS $R/tests/$f"; done
       timeout -k 10 900 python3 -u -m pytest $ARGS -x -v --timeout 300 --timeout-method thread ${K:+-k "$K"} \
           >> $O/tests_sel.log 2>&1 || { tail -n 30 $O/tests_sel.log; exit 1; }
