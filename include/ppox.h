@@ -332,7 +332,9 @@ int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, cons
  *   h3 — conv3 forward (conv_fwd_split(3, y_exp_out)) -> fc forward (fc_fwd[_splitk], h3_exp) and
  *        fc weight gradient (fc_wgrad, h3_exp);
  *   g3 — fc dgrad (fc_dgrad, g3_exp_out; relu_bits required) -> conv3 dgrad
- *        (conv_dgrad_split(3, g_exp); relu_bits required) and conv3 weight gradient (g_exp).
+ *        (conv_dgrad_split(3, g_exp); relu_bits required) and conv3 weight gradient (g_exp);
+ *   g2 — conv3 dgrad (conv_dgrad_split(3, y_exp_out), round 5) -> conv2 dgrad (conv_dgrad_split(2,
+ *        g_exp): the direct form) and conv2 weight gradient (conv2_wgrad_planes(g_exp)).
  * Null exponents select the f32 operands.  conv1_fwd_planes records h1's amax into amax_y
  * (nullable): the start of h2's bound. */
 int ppox_nature_conv1_fwd_planes(const void* x, int64_t batch, const int64_t* idx, int64_t T, int64_t N_env,
@@ -344,7 +346,7 @@ int ppox_nature_conv2_fwd_planes(const uint16_t* h1p, const uint16_t* q1, int64_
 int64_t ppox_nature_conv2_wgrad_planes_workspace_bytes(int64_t batch);
 int ppox_nature_conv2_wgrad_planes(const uint16_t* h1p, const uint16_t* q1, int64_t batch, const float* grad_out,
                                    void* workspace, int64_t workspace_bytes, float* dw, float* db,
-                                   const uint32_t* amax_g, void* stream);
+                                   const uint32_t* amax_g, const int* g_exp, void* stream);
 /* The heads' hidden layer Linear(512, 512) + ReLU (models-checkpoint.py:62-66 extra_layer; the
  * forward of forward() / evaluate and its autograd in ppo.py:216-238) on the split-f16 GEMM, with
  * wh (512 x 512) packed by ppox_nature_pack_all into qh_fwd / qh_dgrad of
@@ -502,11 +504,16 @@ int ppox_nature_conv_fwd_split(int32_t layer, const void* x, int64_t batch, cons
                                void* stream);
 /* dgrad (as ppox_nature_conv_dgrad) of conv2/conv3 with split weights (which = 12, 13);
  * amax_g: grad_out's slots, amax_out: grad_in's (nullable).  The ReLU mask of the layer below
- * comes from relu_bits (that layer's split forward's bitmask) when non-null, else from prev_act. */
+ * comes from relu_bits (that layer's split forward's bitmask) when non-null, else from prev_act.
+ * PX (round 5): layer 3 with y_exp_out writes g2 as its planes (E from amax(g3) x the dgrad
+ * matrix's column norms, which ppox_nature_pack_all records for wqd; relu_bits required); layer 2
+ * with g_exp reads those planes and runs the direct class-wise form (models-checkpoint.py:55
+ * backward: per input-pixel parity class an implicit GEMM over its 4 taps x 64 channels; relu_bits
+ * = conv1's bitmask required, grad_in f32). */
 int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch,
                                  const uint16_t* wqd, const float* prev_act, float* grad_in,
                                  const uint32_t* amax_g, uint32_t* amax_out, const uint32_t* relu_bits,
-                                 const int* g_exp, void* stream);
+                                 const int* g_exp, int* y_exp_out, void* stream);
 /* dW [co][ci][ky][kx] and db (as ppox_nature_conv_wgrad + ppox_nature_wgrad_reduce, in one
  * call): split-K slabs into a workspace of ppox_nature_wgrad_split_workspace_bytes(layer,
  * batch), reduced in a fixed order (deterministic).  x: u8 frames (layer 1, samples

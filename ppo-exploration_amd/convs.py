@@ -69,7 +69,7 @@ RELU_BITS = os.environ.get("PPOX_RELU_BITS", "1") != "0"
 # row AM_EXP holds the exponents of the pass's PX tensors (slots EX_*)
 AM_H1, AM_H2, AM_H3, AM_DF, AM_G3, AM_G2, AM_G1, AM_F, AM_DE, AM_EXP = range(10)
 AM_ROWS = 10
-EX_H2, EX_H3, EX_G3, EX_DF = range(4)
+EX_H2, EX_H3, EX_G3, EX_DF, EX_G2 = range(5)
 
 # PX (round 4, include/ppox.h): in split math the trunk's other split operands are stored as their
 # two f16 planes too — h2 (written by the conv2 forward, read by the conv3 forward and weight
@@ -89,6 +89,12 @@ PX_MIN_BATCH = int(os.environ.get("PPOX_PX_MIN", "0"))
 # rows); with the sg2 fc dgrad alone it measured neutral-to-slower (profiles/r04_ab.txt: 1-GPU 1,152.5
 # vs 1,146.8 ms, per-rank 203.9 vs 201.8 ms per iteration)
 PX_DF = os.environ.get("PPOX_PX_DF", "1") == "1"
+# PX g2 + the direct conv2 dgrad (round 5, PPOX_DDGRAD2=1 by default): the conv3 dgrad writes g2 as its
+# planes (bound: amax(g3) x the conv3 dgrad matrix's column norms), read as they lie by the direct
+# class-wise conv2 dgrad (csrc/dconv.hip ddgrad2_kernel: per input-pixel parity class an implicit GEMM
+# over its 4 taps x 64 channels, no col2im) and by the conv2 weight gradient; =0: f32 g2, the persistent
+# col2im dgrad (dgrad2_colp_kernel)
+DDGRAD2 = os.environ.get("PPOX_DDGRAD2", "1") != "0"
 
 
 class PassState:
@@ -100,7 +106,7 @@ class PassState:
 
     __slots__ = ("amax", "bits", "px")
 
-    def __init__(self, amax, bits=(None, None, None), px=(False, False, False, False)):
+    def __init__(self, amax, bits=(None, None, None), px=(False, False, False, False, False)):
         self.amax, self.bits, self.px = amax, bits, list(px)
 
     def __getitem__(self, row):
@@ -341,6 +347,13 @@ class NatureConvs:
         return (self.px and B >= PX_MIN_BATCH and isinstance(am, PassState) and am.bits[2] is not None and am.bits[1] is not None
                 and B < FC_DGRAD_FUSED_MAX_BATCH and self.uses_split("dgrad", 3, B) and self.uses_split("wgrad", 3))
 
+    def px_g2(self, B, am):
+        """g2 as PX planes: the conv3 dgrad (split, g3's amax and conv2's bitmask) writes them, the direct
+        conv2 dgrad (conv1's bitmask) and the conv2 weight gradient (H1P) read them"""
+        return (DDGRAD2 and self.px and isinstance(am, PassState) and am.bits[0] is not None
+                and am.bits[1] is not None and self.uses_split("dgrad", 3, B) and self.uses_split("dgrad", 2, B)
+                and self.h1p)
+
     def workspace(self, layer, batch, split=False):
         if split and layer == 2 and self.h1p:
             need = native.nature_conv2_wgrad_planes_workspace_bytes(batch)
@@ -456,9 +469,11 @@ class NatureConvs:
             bits = am.bits[layer - 2] if isinstance(am, PassState) else None
             if layer == 2 and self.h1p and bits is None:
                 raise ValueError("conv2 dgrad on H1P needs conv1's ReLU bitmask (a training pass's PassState)")
-            g_exp = am.exp(EX_G3) if layer == 3 and isinstance(am, PassState) else None
+            ps = isinstance(am, PassState)
+            g_exp = am.exp(EX_G3 if layer == 3 else EX_G2) if ps else None
+            y_exp = am.exp(EX_G2) if layer == 3 and ps else None
             native.nature_conv_dgrad_split(layer, g, B, self.q[10 + layer], prev_act, out, amax_g=g_am,
-                                           amax_out=out_am, relu_bits=bits, g_exp=g_exp)
+                                           amax_out=out_am, relu_bits=bits, g_exp=g_exp, y_exp=y_exp)
         else:
             if layer == 2 and self.h1p:
                 raise ValueError("the f32 conv2 dgrad needs f32 activations; split math keeps h1 as H1P")
@@ -476,6 +491,7 @@ class NatureConvs:
             return
         if layer == 2 and self.h1p:
             native.nature_conv2_wgrad_planes(x, self.q[1], B, g, self.workspace(2, B, True), dw, db, amax_g=g_am,
+                                             g_exp=am.exp(EX_G2) if isinstance(am, PassState) else None,
                                              stream=stream)
         elif self.uses_split("wgrad", layer):
             px = layer == 3 and isinstance(am, PassState)
@@ -515,7 +531,7 @@ class NatureConvs:
                      if train and (RELU_BITS or (L == 1 and self.h1p)) and self.uses_split("fwd", L) and
                      consumer[L - 1] else None
                      for L, P, C in ((1, 400, 32), (2, 81, 64), (3, 49, 64)))
-        am = PassState(table, bits, (px2, px3, False, False))
+        am = PassState(table, bits, (px2, px3, False, False, False))
         if B:
             self.fwd(1, x, B, self.c1.bias, h1, am)
             self.fwd(2, h1, B, self.c2.bias, h2, am)
@@ -594,7 +610,11 @@ class NatureConvs:
         if side is not None:  # wgrad3 beside dgrad3 (the tensors stay referenced until the join below)
             fork(side, cur)
         self.wgrad(3, h2, B, g3, dw3, db3, am, stream=side)
-        g2 = torch.empty((B, 9, 9, 64), device=dev)
+        if self.px_g2(B, am):  # g2 as PX planes for the direct conv2 dgrad and the conv2 weight gradient
+            am.px[EX_G2] = True
+            g2 = torch.empty((B, 9, 9, 128), dtype=torch.int16, device=dev)
+        else:
+            g2 = torch.empty((B, 9, 9, 64), device=dev)
         self.dgrad(3, g3, B, h2, g2, am)                        # dX of conv3, times ReLU'(conv2)
         # wgrad2 beside the conv2 dgrad below BWD_SOLO_DGRAD2_BATCH rows; from it, the persistent
         # conv2 dgrad (whole CUs, static tile split) runs alone — the side stream drained before it,

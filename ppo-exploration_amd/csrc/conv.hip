@@ -2214,8 +2214,9 @@ static_assert(8 * W2P_NDMA >= 2 * W2P_HP / 1024 && 2 * W2P_HP % 1024 == 0, "wgra
 struct W2PArgs {
     const uint16_t* h1p;     // H1P [batch][400][32 hi | 32 lo]
     const int* h1_exp;       // h1 * 2^E = hi + lo
-    const float* g;          // g2 [batch][81][64] f32 NHWC (ReLU mask applied)
-    const uint32_t* amax_g;  // g2's amax slots
+    const float* g;          // g2 [batch][81][64] f32 NHWC (ReLU mask applied), or its PX planes (g_exp)
+    const uint32_t* amax_g;  // g2's amax slots (f32 g2)
+    const int* g_exp = nullptr;  // PX g2: the planes' exponent
     float* slab;             // [gridDim.x][512][64]
     float* bslab;            // [gridDim.x][64]
     long long batch;
@@ -2248,6 +2249,9 @@ __device__ inline int w2p_tapoff(int t) {  // uniform slot offset of tap t = ky 
     return 20 * ky + 10 * (kx & 1) + (kx >> 1);
 }
 
+// GPL: g2 arrives as its PX planes (round 5: the conv3 dgrad's planes output) — copied to LDS as they lie
+// (no split), the bias partials summed from the planes
+template <bool GPL>
 __global__ void __launch_bounds__(512, 1) wgrad2_planes_kernel(W2PArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[W2P_LDS];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -2255,8 +2259,9 @@ __global__ void __launch_bounds__(512, 1) wgrad2_planes_kernel(W2PArgs a) {
     const long long s0 = (long long)blockIdx.x * a.per;
     const long long s1 = min(a.batch, s0 + (long long)a.per);
     const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
-    // operand scales: G by its tensor's amax, h1 by its H1P exponent; the slab is unscaled
-    const int eg = split_scale_exp(amax_read(a.amax_g)), ex = *a.h1_exp;
+    // operand scales: G by its tensor's amax (PX: its planes' exponent), h1 by its H1P exponent; the
+    // slab is unscaled
+    const int eg = GPL ? *a.g_exp : split_scale_exp(amax_read(a.amax_g)), ex = *a.h1_exp;
     const float sg = exp2i(eg), uo = exp2i(-eg) * exp2i(-ex);
 
     // H1P DMA sources of this wave's pieces (byte offsets within a sample): DMA i (0..49) fills
@@ -2293,11 +2298,25 @@ __global__ void __launch_bounds__(512, 1) wgrad2_planes_kernel(W2PArgs a) {
         graw[1] = src[tid + 512];
         graw[2] = src[tid < W2P_G4 - 1024 ? tid + 1024 : W2P_G4 - 1];
     };
-    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    // bias partials: f32 g2 — the thread's 4 channels (gc4); planes — the 8 channels of its 16-B piece gc4
+    // of one plane (summed as values of that plane: hi and lo partials added at the end)
+    float bsum[GPL ? 8 : 4] = {};
     auto store_g = [&](int buf, bool add_bias) {
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
-            if (r < 2 || tid < W2P_G4 - 1024) {
+            if (GPL && (r < 2 || tid < W2P_G4 - 1024)) {
+                // piece gc4 of a 256-B pixel: plane P = (gc4 >> 2) & 1, channels c0 .. c0 + 7
+                const int row = (tid + 512 * r) >> 4, P = (gc4 >> 2) & 1, c0 = 32 * (gc4 >> 3) + 8 * (gc4 & 3);
+                const int chunk = c0 >> 4;
+                const int off = buf * W2P_GB + P * W2P_GP + row * 128 + ((chunk ^ (2 * ((row >> 1) & 1))) << 5) +
+                                (c0 & 15) * 2;
+                *reinterpret_cast<float4*>(lds + off) = graw[r];
+                if (add_bias) {
+                    const f16x8 hv = __builtin_bit_cast(f16x8, graw[r]);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) bsum[e] += (float)hv[e];
+                }
+            } else if (!GPL && (r < 2 || tid < W2P_G4 - 1024)) {
                 const int row = (tid + 512 * r) >> 4, chunk = gc4 >> 2;
                 const int off = buf * W2P_GB + row * 128 + ((chunk ^ (2 * ((row >> 1) & 1))) << 5) + (gc4 & 3) * 8;
                 uint2 hv, lv;
@@ -2429,15 +2448,24 @@ __global__ void __launch_bounds__(512, 1) wgrad2_planes_kernel(W2PArgs a) {
                 const int k = (2 * wave + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 slab[k * G2::COUT + j * 32 + (lane & 31)] = (hi[i][j][r] + lo[i][j][r]) * uo;
             }
-    // bias partial: threads with the same gc4 hold the same four channels; summed in thread order
+    // bias partial: threads with the same gc4 hold the same channels; summed in thread order
     float* red = reinterpret_cast<float*>(lds);  // the loop ended on a barrier
+    constexpr int NB = GPL ? 8 : 4;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) red[tid * 4 + e] = bsum[e];
+    for (int e = 0; e < NB; ++e) red[tid * NB + e] = bsum[e];
     __syncthreads();
     if (tid < G2::COUT) {
-        const int c4 = tid >> 2, e = tid & 3;
         float t = 0.f;
-        for (int k = 0; k < 32; ++k) t += red[(c4 + 16 * k) * 4 + e];
+        if constexpr (GPL) {  // channel tid: the high plane's piece, then the low plane's (4 pieces on)
+            const int ph = 8 * (tid >> 5) + ((tid & 31) >> 3), e = tid & 7;
+            float th = 0.f, tl = 0.f;
+            for (int k = 0; k < 32; ++k) th += red[(ph + 16 * k) * 8 + e];
+            for (int k = 0; k < 32; ++k) tl += red[(ph + 4 + 16 * k) * 8 + e];
+            t = (th + tl) * exp2i(-eg);
+        } else {
+            const int c4 = tid >> 2, e = tid & 3;
+            for (int k = 0; k < 32; ++k) t += red[(c4 + 16 * k) * 4 + e];
+        }
         a.bslab[(long long)blockIdx.x * G2::COUT + tid] = t;
     }
 }
@@ -3019,13 +3047,32 @@ __device__ void h1p_exp_block(const float* __restrict__ w1, const float* __restr
 // maximum as AMAX_SLOTS partials in the form's tail (NORM_SLOT0; every slot written) and the bias
 // bound max |b| (BMAX_SLOT; NaN without a bias, so a PX output bounded without it comes out NaN).
 // Job 0: q2 (conv2 forward, n = co: W2[co][:], 512 contiguous), job 1: q3 (conv3 forward, 576),
-// job 2: qfcd (fc dgrad, n = a feature q: W[:][q] over the 512 outputs, 16 features per workgroup).
-// Fixed summation orders (f32; the bound's 2^-10 margin covers their rounding): deterministic.
-constexpr int PA_NORM_JOBS = 3;
+// job 2: qfcd (fc dgrad, n = a feature q: W[:][q] over the 512 outputs, 16 features per workgroup),
+// job 3: qd3 (conv3 dgrad, n = ci: W3[:][ci][:][:] over the 576 (co, ky, kx); no bias: bound 0 — the PX
+// g2 of round 5).  Fixed summation orders (f32; the bound's 2^-10 margin covers their rounding):
+// deterministic.
+constexpr int PA_NORM_JOBS = 4;
 __device__ void norm_block(const PackAll& p, int job, int b) {
     __shared__ float red[256];
     const int t = threadIdx.x;
     float colmax = 0.f;
+    if (job == 3) {
+        if (!p.qd3) return;
+        float sum = 0.f;
+        if (b < 64) {  // input channel b: threads stride its 576 (co, tap) weights
+            for (int k = t; k < G3::K; k += 256) sum += fabsf(p.w3[((k / 9) * 64 + b) * 9 + k % 9]);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        if ((t & 63) == 0) red[t >> 6] = sum;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t* tail = pack_tail(p.qd3, PL_Q3);
+            tail[NORM_SLOT0 + b] = __float_as_uint((red[0] + red[1]) + (red[2] + red[3]));
+            if (b == 0) tail[AMAX_SLOTS + BMAX_SLOT] = 0u;
+        }
+        return;
+    }
     if (job < 2) {
         uint16_t* q = job == 0 ? p.q2 : p.q3;
         if (!q) return;
@@ -3228,6 +3275,7 @@ int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
     note_px_pack(p.q2, p.b2 != nullptr);
     note_px_pack(p.q3, p.b3 != nullptr);
     note_px_pack(p.qfcd, true);
+    note_px_pack(p.qd3, true);
     return PPOX_OK;
 }
 
@@ -3494,7 +3542,7 @@ int split_fwd23(int32_t layer, const void* x, int64_t batch, const uint16_t* wq,
 extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out, int64_t batch, const uint16_t* wqd,
                                             const float* prev_act, float* grad_in, const uint32_t* amax_g,
                                             uint32_t* amax_out, const uint32_t* relu_bits, const int* g_exp,
-                                            void* stream) {
+                                            int* y_exp_out, void* stream) {
     if (batch == 0) return PPOX_OK;  // empty shard / minibatch: no pointers to check
     PPOX_REQUIRE(layer == 2 || layer == 3, "ppox_nature_conv_dgrad_split: layer must be 2 or 3");
     PPOX_REQUIRE(grad_out && wqd && (prev_act || relu_bits) && grad_in && (amax_g || g_exp) && batch >= 0,
@@ -3505,8 +3553,13 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
     Args a{grad_out, nullptr, 0, 0, 0, nullptr, nullptr, prev_act, grad_in, batch, amax_g, amax_out,
            pack_exp(wqd, ppox_conv::planes(10 + layer))};
     hipStream_t s = ppox::as_stream(stream);
+    if (layer == 2 && g_exp) {  // PX g2 (the conv3 dgrad's planes output): the direct class-wise form
+        PPOX_REQUIRE(relu_bits && !y_exp_out, "ppox_nature_conv_dgrad_split: a PX g2 needs conv1's ReLU bitmask "
+                                              "(and writes an f32 g1)");
+        return ppox_conv::ddgrad2(grad_out, batch, wqd, grad_in, relu_bits, amax_out, g_exp, a.wexp, s);
+    }
     if (layer == 2) {
-        PPOX_REQUIRE(!g_exp, "ppox_nature_conv_dgrad_split: layer 2 reads an f32 g2");
+        PPOX_REQUIRE(!y_exp_out, "ppox_nature_conv_dgrad_split: layer 2 writes an f32 g1");
         const long long ntriples = ppox::ceil_div(batch, (long long)C2S);
         // one workgroup per CU (150 KB of LDS each), striding over the triples
         static int cus[64] = {};
@@ -3535,6 +3588,18 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
     a.bits_mask = relu_bits;
     a.xexp = g_exp;  // PX g3 (the fc dgrad's planes output)
     PPOX_REQUIRE(!g_exp || relu_bits, "ppox_nature_conv_dgrad_split: a PX g3 needs conv2's ReLU bitmask");
+    if (y_exp_out) {  // PX g2, bounded by amax(g3) x the dgrad matrix's column norms (no bias)
+        PPOX_REQUIRE(relu_bits && amax_g && ppox::aligned16(amax_g),
+                     "ppox_nature_conv_dgrad_split: a PX g2 needs conv2's ReLU bitmask and g3's amax slots");
+        PPOX_REQUIRE(ppox_conv::px_bound_ok(wqd),
+                     "ppox_nature_conv_dgrad_split: a PX g2 needs wqd packed by ppox_nature_pack_all");
+        a.yexp_out = y_exp_out;
+        a.ynorm = pack_norm(wqd, PL_Q3);
+        a.ybias = pack_bmax(wqd, PL_Q3);
+        const long long blocks = ppox::ceil_div(batch, SG_ROWS) * SgDgradPM<G3>::NPOS;
+        if (g_exp) return launch_sgemm<Px<SgDgradPM<G3, true>, true, true>>(a, wqd, blocks, s, "ppox_nature_conv_dgrad_split");
+        return launch_sgemm<Px<SgDgradPM<G3, true>, false, true>>(a, wqd, blocks, s, "ppox_nature_conv_dgrad_split");
+    }
     if (g_exp)
         return launch_sgemm<Px<SgDgradPM<G3, true>, true>>(a, wqd, ppox::ceil_div(batch, SG_ROWS) * SgDgradPM<G3>::NPOS,
                                                            s, "ppox_nature_conv_dgrad_split");
@@ -3638,10 +3703,11 @@ extern "C" int64_t ppox_nature_conv2_wgrad_planes_workspace_bytes(int64_t batch)
 
 extern "C" int ppox_nature_conv2_wgrad_planes(const uint16_t* h1p, const uint16_t* q1, int64_t batch,
                                               const float* grad_out, void* workspace, int64_t workspace_bytes,
-                                              float* dw, float* db, const uint32_t* amax_g, void* stream) {
-    PPOX_REQUIRE(h1p && q1 && grad_out && workspace && dw && db && amax_g && batch > 0,
+                                              float* dw, float* db, const uint32_t* amax_g, const int* g_exp,
+                                              void* stream) {
+    PPOX_REQUIRE(h1p && q1 && grad_out && workspace && dw && db && (amax_g || g_exp) && batch > 0,
                  "ppox_nature_conv2_wgrad_planes: bad arguments");
-    PPOX_REQUIRE(ppox::aligned16(h1p) && ppox::aligned16(grad_out) && ppox::aligned16(amax_g) &&
+    PPOX_REQUIRE(ppox::aligned16(h1p) && ppox::aligned16(grad_out) && (!amax_g || ppox::aligned16(amax_g)) &&
                      ppox::aligned16(workspace),
                  "ppox_nature_conv2_wgrad_planes: 16B alignment");
     PPOX_REQUIRE(cu_count() > 0, "ppox_nature_conv2_wgrad_planes: no device");
@@ -3651,10 +3717,14 @@ extern "C" int ppox_nature_conv2_wgrad_planes(const uint16_t* h1p, const uint16_
     long long grid;
     w2p_grid(batch, per, grid, w2p_min_per());
     float* slab = reinterpret_cast<float*>(workspace);
-    W2PArgs wa{h1p, h1p_exp(q1, PL_Q1), grad_out, amax_g, slab, slab + grid * (long long)(G2::K * G2::COUT), batch,
-               per};
+    W2PArgs wa{h1p, h1p_exp(q1, PL_Q1), grad_out, amax_g, nullptr, slab, slab + grid * (long long)(G2::K * G2::COUT),
+               batch, per};
+    wa.g_exp = g_exp;
     hipStream_t s = ppox::as_stream(stream);
-    wgrad2_planes_kernel<<<(unsigned)grid, 512, 0, s>>>(wa);
+    if (g_exp)
+        wgrad2_planes_kernel<true><<<(unsigned)grid, 512, 0, s>>>(wa);
+    else
+        wgrad2_planes_kernel<false><<<(unsigned)grid, 512, 0, s>>>(wa);
     PPOX_LAUNCHED_NORET("ppox_nature_conv2_wgrad_planes");
     return launch_wgrad_reduce<G2, true>(slab, wa.bslab, (int)grid, dw, db, s);
 }

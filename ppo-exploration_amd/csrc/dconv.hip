@@ -757,6 +757,223 @@ __global__ void __launch_bounds__(256, 1) hdd_kernel(Args a, const u32x4* __rest
     amax_record(a.amax_y, om);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The conv2 dgrad in the direct form (round 5): g1 = (h1 > 0) * conv2^T(g2), .ipynb_checkpoints/
+// models-checkpoint.py:55 backward (reached through ppo.py:241).  Conv2d(32, 64, 4, stride 2): an input
+// pixel (iy, ix) of parity class (py, px) = (iy & 1, ix & 1) takes exactly the taps (py + 2 dy, px + 2 dx),
+// dy, dx in {0, 1}, from the output pixels (a - dy, b - dx), a = iy >> 1, b = ix >> 1 — so a class is an
+// implicit GEMM over its 10 x 10 input pixels with K = 4 taps x 64 channels of g2 (taps off the 9 x 9
+// image read zeros), N = the 32 input channels: no col2im, every output written once.
+//   * wave c (one per SIMD) owns class c = 2 py + px: its 4 taps' weights (the qd2 packing, k-step s =
+//     4 t + (co >> 4), t = 2 dy + dx) live in 128 AGPRs as MFMA srcA, so the tile is channels x pixels;
+//   * whole g2 sample images (PX planes, 81 pixels x 256 B) and conv1's ReLU bitmask of the sample
+//     (400 words) stream into an LDS ring by LDS-DMA, each byte read from HBM once;
+//   * a workgroup walks its contiguous range of samples in phases of 32 class rows (row m = 100 n + 10 a
+//     + b of sample n of the range); the four waves walk the same rows of their four classes, so a phase
+//     reads at most two samples.  An image pixel's 16-B pieces are stored at p ^ key, key = (4 n + 10 y
+//     + x) & 15 (100 = 4 mod 16): a row's pixel at tap t then has key (m - 10 dy - dx) & 15, so a 16-lane
+//     group of ds_read_b128 (16 consecutive rows) hits 16 distinct bank quads; a tap off the image reads
+//     a zero pixel at the same piece positions.
+// Every k-step is three v_mfma_f32_32x32x16_f16 (hi += Wh gh, lo += Wh gl, lo += Wl gh), fp32-class as
+// every split kernel; its k order (the four taps summed in the accumulators) is not the col2im form's, so
+// the result is held to the fp64 bounds, not bitwise (tests/test_dconv_gpu.py).
+constexpr int DD2_PIXB = 256, DD2_NPIX = 81, DD2_IMG = DD2_NPIX * DD2_PIXB;  // g2 planes of one sample
+constexpr int DD2_MASKB = 400 * 4;                                            // conv1's bitmask of one sample
+constexpr int DD2_IMG_DMAS = (DD2_IMG + 1023) / 1024;                         // 21
+constexpr int DD2_MASK0 = DD2_IMG_DMAS * 1024;                                // mask offset in a slot
+constexpr int DD2_REAL_DMAS = DD2_IMG_DMAS + (DD2_MASKB + 1023) / 1024;      // 23
+constexpr int DD2_SLOT = DD2_REAL_DMAS * 1024, DD2_DMAS = (DD2_REAL_DMAS + 3) / 4;  // per wave: 6
+constexpr int DD2_NSLOT = 4, DD2_ZERO = DD2_NSLOT * DD2_SLOT, DD2_LDS = DD2_ZERO + 256;
+constexpr int DD2_ROWS = 100;  // class rows per sample
+static_assert(DD2_LDS <= 160 * 1024, "ddgrad2: LDS");
+
+__global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __restrict__ wq) {
+    constexpr int NK = 16;  // k-steps: 4 taps x 4 channel quarters
+    __shared__ __attribute__((aligned(16))) uint8_t lds[DD2_LDS];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int py = wave >> 1, px = wave & 1;  // this wave's class
+    const int r = lane & 31, h = lane >> 5;
+    const long long S0 = blockIdx.x * a.batch / gridDim.x, S1 = (blockIdx.x + 1) * a.batch / gridDim.x;
+    const int NS = (int)(S1 - S0);
+    if (NS <= 0) return;
+    const int MR = NS * DD2_ROWS;
+    const int F_ = (MR + 31) / 32;
+    const uint8_t* gb = reinterpret_cast<const uint8_t*>(a.x) + S0 * DD2_IMG;
+    const uint8_t* mb = reinterpret_cast<const uint8_t*>(a.bits_mask) + S0 * DD2_MASKB;
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
+
+    // DMA d = wave + 4 i of a sample: slot bytes [1024 d, 1024 d + 1024).  d < 21: image pixels
+    // (lane -> LDS pixel u, piece position lane & 15, holding the global piece (lane & 15) ^ key); d =
+    // 21, 22: the bitmask words (past its end: its last piece again, into the slot's pad); d > 22: DMA 22
+    // again (the same bytes to the same place)
+    int dpk[DD2_DMAS];  // image: LDS pixel u | its key offset (10 y + x) << 16; mask: -1 - byte offset
+#pragma unroll
+    for (int i = 0; i < DD2_DMAS; ++i) {
+        int d = wave + 4 * i;
+        d = d < DD2_REAL_DMAS ? d : DD2_REAL_DMAS - 1;
+        if (d < DD2_IMG_DMAS) {
+            int u = (d * 1024 + lane * 16) / DD2_PIXB;
+            u = u < DD2_NPIX ? u : DD2_NPIX - 1;
+            dpk[i] = u | (((10 * (u / 9) + u % 9) & 15) << 16);
+        } else {
+            int off = (d - DD2_IMG_DMAS) * 1024 + lane * 16;
+            off = off < DD2_MASKB ? off : DD2_MASKB - 16;
+            dpk[i] = -1 - off;
+        }
+    }
+    auto issue_one = [&](int n, int i) {
+        int d = wave + 4 * i;
+        d = d < DD2_REAL_DMAS ? d : DD2_REAL_DMAS - 1;
+        uint8_t* dst = lds + (n % DD2_NSLOT) * DD2_SLOT + d * 1024;
+        const uint8_t* src;
+        if (dpk[i] >= 0) {
+            const int key = (4 * n + (dpk[i] >> 16)) & 15, u = dpk[i] & 0xFFFF;
+            src = gb + (long long)n * DD2_IMG + (uint32_t)(u * DD2_PIXB + (((lane & 15) ^ key) << 4));
+        } else {
+            src = mb + (long long)n * DD2_MASKB + (uint32_t)(-1 - dpk[i]);
+        }
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    };
+    auto issue_sample = [&](int n) {
+#pragma unroll
+        for (int i = 0; i < DD2_DMAS; ++i) issue_one(n, i);
+    };
+    int issued = NS < DD2_NSLOT ? NS : DD2_NSLOT;
+    for (int n = 0; n < issued; ++n) issue_sample(n);
+    // the class's weights: k-step s = 4 t + q (tap t = 2 dy + dx -> kernel tap (py + 2 dy, px + 2 dx),
+    // channels 16 q .. 16 q + 15), planes p — fragment ((tap * 4 + q) * 2 + p) of the qd2 packing
+    u32x4 bq[NK][2];
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+        const int t = s >> 2, tap = (py + 2 * (t >> 1)) * 4 + px + 2 * (t & 1);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) bq[s][p] = wq[((tap * 4 + (s & 3)) * 2 + p) * 64 + lane];
+    }
+    const float us = exp2i(-(*a.xexp + *a.wexp));  // the accumulators' unscale (powers of two: exact)
+    if (threadIdx.x < 16) reinterpret_cast<u32x4*>(lds + DD2_ZERO)[threadIdx.x] = u32x4{0u, 0u, 0u, 0u};
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    asm volatile("s_nop 4" ::: "memory");  // (VALU-written B registers before the first MFMA reads them)
+
+    float* g1 = a.y + S0 * (400 * 32);
+    float om = 0.f;
+    f32x16 H0, L0, H1, L1;
+    // the previous phase's rows: the lane's output pixel (float offset in g1, -1: past the range) and mask
+    int po = -1;
+    uint32_t pmw = 0u;
+
+    auto epi = [&](auto T, const f32x16& PH, const f32x16& PL, int o, uint32_t mw) {
+        constexpr int t = decltype(T)::value;
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            v[k] = (mw >> (8 * t + 4 * h + k)) & 1u ? (PH[4 * t + k] + PL[4 * t + k]) * us : 0.f;
+        if (o >= 0) *reinterpret_cast<float4*>(g1 + o + 8 * t + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
+        om = fmaxf(om, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    };
+    // refill DMAs of a phase (up to RMAX samples) spread over k-steps 8 .. 15, after the epilogue's stores
+    constexpr int RMAX = 1, NDMA = RMAX * DD2_DMAS;  // (a phase refills at most one sample)
+
+    auto phase = [&](int f, f32x16& H, f32x16& Lo, const f32x16& PH, const f32x16& PL, auto PREV) {
+        const int m0 = 32 * f;
+        const int nlo = m0 / DD2_ROWS, nhi = min((m0 + 31) / DD2_ROWS, NS - 1);
+        dc_vm_wait<DD2_DMAS>(issued - 1 - nhi);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const int rA = issued, nref = min(nlo + DD2_NSLOT, NS) - issued;
+        issued += nref;
+        // this lane's row (past the range: the range's last row, never stored)
+        int m = m0 + r;
+        const bool live = m < MR;
+        m = live ? m : MR - 1;
+        const int n = m / DD2_ROWS, rem = m - n * DD2_ROWS, ra = rem / 10, rb = rem - 10 * ra;
+        const uint32_t sbase = lds0 + (n % DD2_NSLOT) * DD2_SLOT;
+        const int mkey = 4 * n + 10 * ra + rb;
+        uint32_t tb[4];  // per tap: the read pixel's base | (its key ^ h) << 4
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int dy = t >> 1, dx = t & 1, y = ra - dy, x = rb - dx;
+            const bool ok = (unsigned)y < 9u && (unsigned)x < 9u;
+            const uint32_t key = (uint32_t)((mkey - 10 * dy - dx) & 15) ^ (uint32_t)h;
+            tb[t] = (ok ? sbase + (uint32_t)((9 * y + x) * DD2_PIXB) : lds0 + DD2_ZERO) | (key << 4);
+        }
+        const int iy = 2 * ra + py, ix = 2 * rb + px;
+        // the mask word of this row's pixel (used by the next phase's epilogue), read before the fragments
+        uint32_t mw;
+        asm volatile("ds_read_b32 %0, %1" : "=v"(mw) : "v"(sbase + DD2_MASK0 + (uint32_t)((iy * 20 + ix) * 4)));
+        const int o = live ? (n * 400 + iy * 20 + ix) * 32 : -1;
+        // k-step i, plane pl: piece 8 (q >> 1) + 4 pl + 2 (q & 1) + h of the tap's pixel
+        auto addr = [&](int i, int pl) {
+            const int q = i & 3;
+            return tb[i >> 2] ^ ((uint32_t)(8 * (q >> 1) + 4 * pl + 2 * (q & 1)) << 4);
+        };
+        constexpr int PD = 2, NB = PD + 1;
+        u32x4 fa[NB][2];
+        auto rd1 = [&](auto I, auto PLc) {
+            constexpr int i = decltype(I)::value, pl = decltype(PLc)::value;
+            fa[i % NB][pl] = dc_read<0>(addr(i, pl));
+        };
+        rd1(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+        rd1(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+        rd1(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+        rd1(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(mw));
+        const int o_prev = po;
+        const uint32_t mw_prev = pmw;
+        dc_unroll(
+            [&](auto I) {
+                constexpr int i = decltype(I)::value;
+                constexpr bool P = decltype(PREV)::value;
+                const u32x4& b0 = bq[i][0];
+                const u32x4& b1 = bq[i][1];
+                if constexpr (i == 0)
+                    dc_mfma0<true>(H, fa[0][0], b0);
+                else
+                    dc_mfma<true>(H, fa[i % NB][0], b0);
+                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 0>{});
+                if constexpr (i == 0)
+                    dc_mfma0<true>(Lo, fa[0][0], b1);
+                else
+                    dc_mfma<true>(Lo, fa[i % NB][0], b1);
+                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 1>{});
+                if constexpr (P && (i & 1) && i < 8) epi(std::integral_constant<int, i / 2>{}, PH, PL, o_prev, mw_prev);
+                dc_mfma<true>(Lo, fa[i % NB][1], b0);
+                dc_unroll(
+                    [&](auto X) {
+                        constexpr int x = decltype(X)::value, t = x / DD2_DMAS;
+                        if constexpr (8 + x * (NK - 8) / NDMA == i) {
+                            if (t < nref) issue_one(rA + t, x % DD2_DMAS);
+                        }
+                    },
+                    std::make_integer_sequence<int, NDMA>{});
+                constexpr int later = (i + PD < NK ? i + PD : NK - 1) - (i + 1);
+                if constexpr (i + 1 < NK) dc_lgkm<2 * later>(fa[(i + 1) % NB][0], fa[(i + 1) % NB][1]);
+            },
+            std::make_integer_sequence<int, NK>{});
+        for (int t = RMAX; t < nref; ++t) issue_sample(rA + t);
+        po = o;
+        pmw = mw;
+        dc_acc_fence(H, Lo);
+    };
+    auto final_epi = [&](const f32x16& PH, const f32x16& PL) {
+        dc_unroll([&](auto T) { epi(T, PH, PL, po, pmw); }, std::make_integer_sequence<int, 4>{});
+    };
+    phase(0, H0, L0, H1, L1, std::false_type{});
+    int f = 1;
+#pragma unroll 1
+    for (; f + 1 < F_; f += 2) {
+        phase(f, H1, L1, H0, L0, std::true_type{});
+        phase(f + 1, H0, L0, H1, L1, std::true_type{});
+    }
+    if (f < F_) phase(f, H1, L1, H0, L0, std::true_type{});
+    if ((F_ - 1) & 1)
+        final_epi(H1, L1);
+    else
+        final_epi(H0, L0);
+    amax_record(a.amax_y, om);
+}
+
 int dconv_cus() {
     static int cus[64] = {};
     int dev = 0;
@@ -823,6 +1040,21 @@ int dconv_fwd(int layer, const void* x, int64_t batch, const uint16_t* wq, const
     a.ybias = pack_bmax(wq, planes(layer));
     if (layer == 2) return launch_dconv<DcF2>(a, wq, s, "ppox_nature_conv2_fwd_planes");
     return launch_dconv<DcF3>(a, wq, s, "ppox_nature_conv_fwd_split");
+}
+
+// the conv2 dgrad on PX g2 (one workgroup per CU, each a contiguous range of samples)
+int ddgrad2(const void* g2p, int64_t batch, const uint16_t* wqd2, float* g1, const uint32_t* relu_bits,
+            uint32_t* amax_g1, const int* g_exp, const int* wexp, hipStream_t s) {
+    const int cus = dconv_cus();
+    PPOX_REQUIRE(cus > 0, "ppox_nature_conv_dgrad_split: no device");
+    PPOX_REQUIRE(ppox::aligned16(g2p) && ppox::aligned16(g1) && ppox::aligned16(relu_bits) && g_exp && wexp,
+                 "ppox_nature_conv_dgrad_split: the direct conv2 dgrad needs 16B-aligned g2 planes, g1, bitmask");
+    Args a{g2p, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, g1, batch, nullptr, amax_g1, wexp};
+    a.bits_mask = relu_bits;
+    a.xexp = g_exp;
+    const long long grid = std::min<long long>(batch, cus);
+    ddgrad2_kernel<<<(unsigned)grid, 256, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd2));
+    PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
 }
 
 // the heads' hidden-layer dgrad's direct form (PPOX_DHDD; _MIN: the smallest batch)

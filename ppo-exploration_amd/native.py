@@ -63,7 +63,7 @@ SIGNATURES = {
     "ppox_nature_pack_split": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv_fwd_split": [_i32, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp, _vp],
-    "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv_dgrad_split": [_i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_relu_backward_": [_vp, _vp, _i64, _vp],
     "ppox_relu_backward_amax_": [_vp, _vp, _i64, _vp, _vp],
     "ppox_amax": [_vp, _i64, _vp, _vp],
@@ -76,7 +76,7 @@ SIGNATURES = {
     "ppox_nature_pack_all": [_vp] * 19 + [_i64, _vp],
     "ppox_nature_conv1_fwd_planes": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv2_fwd_planes": [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "ppox_nature_conv2_wgrad_planes": [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
+    "ppox_nature_conv2_wgrad_planes": [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -592,11 +592,13 @@ def nature_conv2_wgrad_planes_workspace_bytes(batch):
     return int(load().ppox_nature_conv2_wgrad_planes_workspace_bytes(int(batch)))
 
 
-def nature_conv2_wgrad_planes(h1p, q1, batch, grad_out, workspace, dw, db, amax_g=None, stream=None):
-    """dW2, db2 from H1P and the NHWC f32 output grad (slabs + fixed-order reduce in one call)."""
-    amax_g = _amax_of(grad_out, amax_g, stream)
+def nature_conv2_wgrad_planes(h1p, q1, batch, grad_out, workspace, dw, db, amax_g=None, g_exp=None, stream=None):
+    """dW2, db2 from H1P and the NHWC output grad (slabs + fixed-order reduce in one call): f32 g2 (its amax
+    slots amax_g, computed here when None) or, g_exp given, g2 as PX planes with that exponent."""
+    if g_exp is None:
+        amax_g = _amax_of(grad_out, amax_g, stream)
     call("ppox_nature_conv2_wgrad_planes", _p(h1p), _p(q1), int(batch), _p(grad_out), _p(workspace),
-         workspace.numel() * workspace.element_size(), _p(dw), _p(db), _p(amax_g), stream_ptr(stream))
+         workspace.numel() * workspace.element_size(), _p(dw), _p(db), _p(amax_g), _p(g_exp), stream_ptr(stream))
 
 
 def nature_fc_fwd(h3, batch, q_fwd, bias, f, amax_h3=None, amax_f=None, h3_exp=None, stream=None):
@@ -848,14 +850,15 @@ def nature_conv_wgrad_split_idx(layer, x, batch, idx, T, N_env, grad_out, worksp
 
 
 def nature_conv_dgrad_split(layer, grad_out, batch, wqd, prev_act, grad_in, amax_g=None, amax_out=None,
-                            relu_bits=None, g_exp=None, stream=None):
+                            relu_bits=None, g_exp=None, y_exp=None, stream=None):
     """amax_g: grad_out's slots (computed here when None); amax_out: grad_in's slots to record (or None);
     relu_bits: the ReLU bitmask of the layer below from its split forward, used instead of prev_act;
-    g_exp (layer 3): grad_out is g3 as PX planes (relu_bits required)."""
+    g_exp: grad_out is PX planes with that exponent (layer 3: g3; layer 2: g2 — the direct form);
+    y_exp (layer 3): write g2 as PX planes, storing the exponent there (relu_bits and amax_g required)."""
     if batch and g_exp is None:
         amax_g = _amax_of(grad_out, amax_g, stream)
     call("ppox_nature_conv_dgrad_split", int(layer), _p(grad_out), int(batch), _p(wqd), _p(prev_act), _p(grad_in),
-         _p(amax_g), _p(amax_out), _p(relu_bits), _p(g_exp), stream_ptr(stream))
+         _p(amax_g), _p(amax_out), _p(relu_bits), _p(g_exp), _p(y_exp), stream_ptr(stream))
 
 
 # ---------------------------------------------------------------------------
