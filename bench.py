@@ -84,7 +84,8 @@ def _kernels():
            # (the planes forward: the direct form, csrc/dconv.hip, by default; the sg2 GEMM with PPOX_DCONV3=0;
            # a training pass writes the ReLU bitmask (BITS = true), the collect pass's 4,096-row forward does not)
            ("fwd", 3): r"(dconv_fwd_kernel<DcF3, true>|" + _sg("SgFwd<64, 9, 9, 3, 3, 1, 64, false>", "4, 2") + ")",
-           ("dgrad", 2): r"dgrad2_colp_kernel<true, false>",
+           # (PX g2: the direct class-wise form, csrc/dconv.hip, by default; PPOX_DDGRAD2=0: the col2im form)
+           ("dgrad", 2): r"(ddgrad2_kernel|dgrad2_colp_kernel<true, false>)",
            ("dgrad", 3): _sg("SgDgradPM<64, 9, 9, 3, 3, 1, 64, true>", "4, 2"),
            ("wgrad", 1): (re.escape("wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>")
                           if os.environ.get("PPOX_WGRAD1_IM2COL") == "1" else r"wgrad1_frames_kernel<true>"),
@@ -136,7 +137,7 @@ def _kernels():
                                      label="head hidden fwd")
     # dgrad: de in, the heads' input grad read + written (accumulated in place), f read for the ReLU
     k["ppox_head_hidden_dgrad"] = dict(rows_arg=1, macs=HID * HID, bytes=4 * HID * 4, fixed=w_h, products=3,
-                                       rocprof=r"(hdd_kernel|" + _rows(512, 512, 2, "false") + ")",
+                                       rocprof=_rows(512, 512, 2, "false"),
                                        label="head hidden dgrad")
     k["ppox_head_hidden_wgrad"] = dict(rows_arg=1, macs=HID * HID, bytes=2 * HID * 4, fixed=w_h, products=3,
                                        rocprof=re.escape("wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 8>"),

@@ -4050,8 +4050,6 @@ extern "C" int ppox_head_hidden_dgrad(const float* de, int64_t rows, const uint1
     PPOX_REQUIRE(ppox::aligned16(de) && ppox::aligned16(q_dgrad) && ppox::aligned16(amax_de),
                  "ppox_head_hidden_dgrad: 16B alignment");
     Args a{de, nullptr, 0, 0, 0, nullptr, nullptr, f, df, rows, amax_de, amax_df, pack_exp(q_dgrad, PL_H)};
-    if (ppox_conv::dhdd_enabled(rows))
-        return ppox_conv::dhdd(de, rows, q_dgrad, f, df, amax_de, amax_df, a.wexp, ppox::as_stream(stream));
     return launch_sgemm<SgRows<512, 512, HEAD_DGRAD, HEAD_GW, false, SG_FC_NB>>(
         a, q_dgrad, ppox::ceil_div(rows, SG_ROWS) * (512 / SG_FC_NB), ppox::as_stream(stream), "ppox_head_hidden_dgrad");
 }

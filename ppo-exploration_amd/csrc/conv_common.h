@@ -401,10 +401,6 @@ int dconv_fwd(int layer, const void* x, int64_t batch, const uint16_t* wq, const
               const uint32_t* amax_x, uint32_t* amax_y, uint32_t* relu_bits, const int* x_exp, int* y_exp_out,
               hipStream_t s);
 bool dconv_enabled(int layer, long long batch);
-// the heads' hidden-layer dgrad (df in place), the direct form (dconv.hip)
-bool dhdd_enabled(long long batch);
-int dhdd(const float* de, int64_t rows, const uint16_t* wq, const float* f, float* df, const uint32_t* amax_de,
-         uint32_t* amax_df, const int* wexp, hipStream_t s);
 // the conv2 dgrad on PX g2 -> f32 g1 (conv1's ReLU bitmask applied), the direct class-wise form (dconv.hip)
 int ddgrad2(const void* g2p, int64_t batch, const uint16_t* wqd2, float* g1, const uint32_t* relu_bits,
             uint32_t* amax_g1, const int* g_exp, const int* wexp, hipStream_t s);

@@ -116,7 +116,7 @@ __device__ inline void dc_vm_wait(int k) {
 // cross-lane exchange.  Per output element the products and their k order are the GEMM's (a x^T w sum
 // either way).  hipcc does not know these are MFMAs: VALU reads of an accumulator are padded by hand
 // (dc_acc_fence), and an accumulator is never written by the VALU (the first k-step takes C = 0).
-// PAD: the srcB fragment was just written by the VALU (hdd_kernel splits it in registers): the 2 wait
+// PAD: the srcB fragment was just written by the VALU (a fragment split in registers): the 2 wait
 // states a VALU write -> MFMA operand read needs go inside the string (hipcc pads nothing in asm)
 template <bool BA, bool PAD = false>
 __device__ inline void dc_mfma(f32x16& c, const u32x4& x, const u32x4& w) {
@@ -281,10 +281,8 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
     auto phase = [&](int f, f32x16& H, f32x16& Lo, const f32x16& PH, const f32x16& PL, auto PREV) {
         const int m0 = 64 * f;
         const int nlo = m0 / L::P, nhi = min((m0 + 63) / L::P, NS - 1);
-#ifndef DC_NO_BAR
         dc_vm_wait<F::DMAS>(issued - 1 - nhi);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
         // refill: samples up to nlo + NSLOT - 1 (the slots of samples < nlo are free), issued inside the
         // k walk
         const int rA = issued, nref = min(nlo + F::NSLOT, NS) - issued;
@@ -357,38 +355,24 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
                     dc_mfma0<A0>(H, fa[0][0], b0);
                 else
                     dc_mfma<A0>(H, fa[i % NB][0], b0);
-#ifndef DC_NO_EPI
                 if constexpr (EPI_BIAS) bs = dc_read<0>(bias_lane + 32 * (i / 2));
                 if constexpr (P && i == 8) epi_bits(std::true_type{}, pmb, bw);
-#endif
                 if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 0>{});
-#ifndef DC_NO_EPI
                 if constexpr (EPI) epi_val(T{}, PH, PL, bs, y);
-#endif
                 if constexpr (i == 0)
                     dc_mfma0<A1>(Lo, fa[0][0], b1);
                 else
                     dc_mfma<A1>(Lo, fa[i % NB][0], b1);
                 if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 1>{});
-#ifndef DC_NO_EPI
                 if constexpr (EPI) epi_store(T{}, std::true_type{}, pmb, y);
-#endif
-#ifdef DC_LO2  // (timing probe only: the third product into hi, no back-to-back dependent MFMAs)
-                dc_mfma<A0>(H, fa[i % NB][1], b0);
-#else
                 dc_mfma<A0>(Lo, fa[i % NB][1], b0);
-#endif
-#ifndef DC_NO_EPI
                 if constexpr (EPI) epi_mask(T{}, y, bw);
-#endif
                 // the refill DMAs whose k-step this is
                 dc_unroll(
                     [&](auto X) {
                         constexpr int x = decltype(X)::value, t = x / F::DMAS;
                         if constexpr (16 + x * (NK - 16) / NDMA == i) {
-#ifndef DC_NO_DMA
                             if (t < nref) issue_at(rsrc[t], rdst[t], (rA + t) & 15, x % F::DMAS);
-#endif
                         }
                     },
                     std::make_integer_sequence<int, NDMA>{});
@@ -609,152 +593,6 @@ __global__ void __launch_bounds__(256, 1) fcd_kernel(Args a, const u32x4* __rest
     else
         final_epi(H0, L0);
     amax_record(a.amax_y, __uint_as_float(om) * exp2i(-ey));
-}
-
-// The heads' hidden layer's input gradient in the same form (round 4): df <- (f > 0) ? df + de W : 0 in
-// place (.ipynb_checkpoints/models-checkpoint.py:62-66 extra_layer, backward), de (rows x 512) f32 split
-// into its planes after the LDS read (the sg2 form's split: scale from de's amax), W the hidden layer's
-// dgrad packing.  Workgroup (column group cg of 4 x 32 columns, row group rr); same per-element MFMA
-// sequence and epilogue arithmetic as sgemm_kernel<SgRows<512, 512, HEAD_DGRAD, ..>>, so df and its
-// amax are bitwise its.
-constexpr int HDD_N = 512, HDD_TILES = HDD_N / 32;
-
-__global__ void __launch_bounds__(256, 1) hdd_kernel(Args a, const u32x4* __restrict__ wq, int nrg) {
-    constexpr int NK = 32, KC = 16;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[FCD_LDS];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int r = lane & 31, h = lane >> 5;
-    const int cg = blockIdx.x / nrg, rr = blockIdx.x % nrg;
-    const int T = cg * 4 + wave;  // (16 tiles: every wave live)
-    const long long r0 = rr * a.batch / nrg, r1 = (rr + 1) * a.batch / nrg;
-    const int MR = (int)(r1 - r0);
-    if (MR <= 0) return;
-    const int F_ = (MR + FCD_PH - 1) / FCD_PH;
-    const uint8_t* xb = reinterpret_cast<const uint8_t*>(a.x) + r0 * FCD_ROWB;
-    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
-    auto issue_phase = [&](int f) {
-        uint8_t* dst = lds + (f & 1) * FCD_SLOT;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int rho = wave * 8 + (i >> 1), d = i & 1;
-            int row = f * FCD_PH + rho;
-            row = row < MR ? row : MR - 1;
-            const uint32_t q = (uint32_t)(d * 64 + lane);
-            const uint32_t off = (uint32_t)row * FCD_ROWB + ((q ^ (uint32_t)(rho & 15)) << 4);
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xb + off),
-                                             (__attribute__((address_space(3))) void*)(dst + rho * FCD_ROWB + d * 1024),
-                                             16, 0, 0);
-        }
-    };
-    issue_phase(0);
-    u32x4 bq[KC][2][2];
-#pragma unroll
-    for (int c = 0; c < KC; ++c)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int p = 0; p < 2; ++p)
-                bq[c][s][p] = wq[(long long)((T >> 1) * KC + c) * (2 * 2 * NPL * 64) + (((s * 2 + (T & 1)) * 2 + p) * 64) + lane];
-    const int ex = split_scale_exp(amax_read(a.amax_x)), ew = *a.wexp;
-    const float sa = exp2i(ex), ua = exp2i(-ex), uw = exp2i(-ew);
-    __builtin_amdgcn_s_waitcnt(0);
-    asm volatile("s_nop 4" ::: "memory");
-
-    float om = 0.f;
-    f32x16 H0, L0, H1, L1;
-    // epilogue group t of the block at range row pmb: lane (r, h) = row r0 + pmb + r, columns 32 T + 8 t + 4 h ..
-    // + 3: (f > 0) ? df + acc : 0 (acc = (hi + lo) ua uw), f and df read as float4
-    auto epi = [&](auto Tt, const f32x16& PH, const f32x16& PL, int pmb, auto FULL) {
-        constexpr int t = decltype(Tt)::value;
-        long long m = r0 + pmb + r;
-        const bool ok = decltype(FULL)::value || pmb + r < MR;
-        m = ok ? m : r0;
-        const long long el = m * HDD_N + T * 32 + 8 * t + 4 * h;
-        const float4 fm = *reinterpret_cast<const float4*>(a.mask + el);
-        const float4 dv = *reinterpret_cast<const float4*>(a.y + el);
-        const float fa[4] = {fm.x, fm.y, fm.z, fm.w}, da[4] = {dv.x, dv.y, dv.z, dv.w};
-        float v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float acc = (PH[4 * t + k] + PL[4 * t + k]) * ua * uw;
-            v[k] = fa[k] > 0.f ? da[k] + acc : 0.f;
-        }
-        if (ok) {
-            *reinterpret_cast<float4*>(a.y + el) = make_float4(v[0], v[1], v[2], v[3]);
-            om = fmaxf(om, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
-        }
-    };
-
-    auto phase = [&](int f, f32x16& H, f32x16& Lo, const f32x16& PH, const f32x16& PL, auto PREV) {
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        constexpr bool P = decltype(PREV)::value;
-        const int pmb = FCD_PH * (f - 1);
-        const uint32_t base = lds0 + (f & 1) * FCD_SLOT + r * FCD_ROWB;
-        const uint32_t kx = (uint32_t)(r & 15) << 4;
-        // k-step i = 2 c + s: its 8 f32 of row r (pieces 8 c + 4 s + 2 h, + 1; the sg2 fragment's values)
-        auto addr = [&](int i, int g) {
-            const int c = i >> 1, s = i & 1;
-            const uint32_t P16 = (uint32_t)(((c & 1) << 3) | (s << 2) | g) << 4;
-            return base + (P16 ^ (kx ^ ((uint32_t)h << 5)));
-        };
-        constexpr int PD = 2, NB = 3;
-        u32x4 fa[NB][2];
-        auto rd1 = [&](auto I, auto G) {
-            constexpr int i = decltype(I)::value, g = decltype(G)::value;
-            fa[i % NB][g] = dc_read<((i >> 1) >> 1) * 256>(addr(i, g));
-        };
-        rd1(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-        rd1(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
-        rd1(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
-        rd1(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
-        dc_lgkm<2>(fa[0][0], fa[0][1]);
-        dc_unroll(
-            [&](auto I) {
-                constexpr int i = decltype(I)::value;
-                const u32x4& b0 = bq[i >> 1][i & 1][0];
-                const u32x4& b1 = bq[i >> 1][i & 1][1];
-                u32x4 xp[2];  // the k-step's 8 values as their two f16 planes (sg2's split8h, scale sa)
-                split8h(__builtin_bit_cast(float4, fa[i % NB][0]), __builtin_bit_cast(float4, fa[i % NB][1]), sa, xp[0],
-                        xp[1]);
-                if constexpr (i == 0)
-                    dc_mfma0<true, true>(H, xp[0], b0);
-                else
-                    dc_mfma<true, true>(H, xp[0], b0);
-                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 0>{});
-                if constexpr (i == 0)
-                    dc_mfma0<true, true>(Lo, xp[0], b1);
-                else
-                    dc_mfma<true, true>(Lo, xp[0], b1);
-                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 1>{});
-                if constexpr (P && (i & 1) && i < 8) epi(std::integral_constant<int, i / 2>{}, PH, PL, pmb, std::true_type{});
-                dc_mfma<true, true>(Lo, xp[1], b0);
-                if constexpr (i == 16) {
-                    if (f + 1 < F_) issue_phase(f + 1);
-                }
-                constexpr int later = (i + PD < NK ? i + PD : NK - 1) - (i + 1);
-                if constexpr (i + 1 < NK) dc_lgkm<2 * later>(fa[(i + 1) % NB][0], fa[(i + 1) % NB][1]);
-            },
-            std::make_integer_sequence<int, NK>{});
-        dc_acc_fence(H, Lo);
-    };
-    auto final_epi = [&](const f32x16& PH, const f32x16& PL) {
-        const int pmb = FCD_PH * (F_ - 1);
-        dc_unroll([&](auto Tt) { epi(Tt, PH, PL, pmb, std::false_type{}); }, std::make_integer_sequence<int, 4>{});
-    };
-    phase(0, H0, L0, H1, L1, std::false_type{});
-    int f = 1;
-#pragma unroll 1
-    for (; f + 1 < F_; f += 2) {
-        phase(f, H1, L1, H0, L0, std::true_type{});
-        phase(f + 1, H0, L0, H1, L1, std::true_type{});
-    }
-    if (f < F_) phase(f, H1, L1, H0, L0, std::true_type{});
-    if ((F_ - 1) & 1)
-        final_epi(H1, L1);
-    else
-        final_epi(H0, L0);
-    amax_record(a.amax_y, om);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1009,9 +847,6 @@ int launch_dconv(const Args& a, const uint16_t* wq, hipStream_t s, const char* n
 
 }  // namespace
 
-#ifndef DHDD_DEFAULT
-#define DHDD_DEFAULT false  // the direct hidden-layer dgrad unless PPOX_DHDD says otherwise
-#endif
 #ifndef DFCD_DEFAULT
 #define DFCD_DEFAULT true  // the direct fc dgrad unless PPOX_DFCD says otherwise
 #endif
@@ -1055,19 +890,6 @@ int ddgrad2(const void* g2p, int64_t batch, const uint16_t* wqd2, float* g1, con
     const long long grid = std::min<long long>(batch, cus);
     ddgrad2_kernel<<<(unsigned)grid, 256, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd2));
     PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
-}
-
-// the heads' hidden-layer dgrad's direct form (PPOX_DHDD; _MIN: the smallest batch)
-bool dhdd_enabled(long long batch) { return env_on("PPOX_DHDD", batch, DHDD_DEFAULT); }
-int dhdd(const float* de, int64_t rows, const uint16_t* wq, const float* f, float* df, const uint32_t* amax_de,
-         uint32_t* amax_df, const int* wexp, hipStream_t s) {
-    const int cus = dconv_cus();
-    PPOX_REQUIRE(cus > 0, "ppox_head_hidden_dgrad: no device");
-    Args a{de, nullptr, 0, 0, 0, nullptr, nullptr, f, df, rows, amax_de, amax_df, wexp};
-    constexpr int ngroups = HDD_TILES / 4;
-    const int nrg = (int)std::max<long long>(1, std::min<long long>(cus / ngroups, rows));
-    hdd_kernel<<<(unsigned)(ngroups * nrg), 256, 0, s>>>(a, reinterpret_cast<const u32x4*>(wq), nrg);
-    PPOX_LAUNCHED("ppox_head_hidden_dgrad");
 }
 
 // the fc dgrad's direct form (PPOX_DFCD=1; _MIN: the smallest batch): df planes in, g3 planes out, h3's bitmask

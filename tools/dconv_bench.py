@@ -1,6 +1,7 @@
 """Timing of the conv2 / conv3 forwards (H1P / h2 planes -> h2 / h3 planes), the direct form
-(csrc/dconv.hip) against the im2col sg2 GEMM (PPOX_DCONV2=0 / PPOX_DCONV3=0), HIP events on the launch stream.
-Usage: python tools/dconv_bench.py [B ...]"""
+(csrc/dconv.hip) against the im2col sg2 GEMM (PPOX_DCONV2=0 / PPOX_DCONV3=0), and of the conv2 dgrad: the
+direct class-wise form on PX g2 (ddgrad2_kernel) against the col2im form on f32 g2 (dgrad2_colp_kernel);
+HIP events on the launch stream.  Usage: python tools/dconv_bench.py [B ...]"""
 import json
 import os
 import sys
@@ -54,6 +55,27 @@ def main():
                 row[name + "_tf"] = round(flop / t / 1e12, 1)
                 row[name + "_tbs"] = round(byt / t / 1e12, 2)
             print(json.dumps(row), flush=True)
+        # conv2 dgrad: g2 (B, 9, 9, 64) -> g1 (B, 20, 20, 32) times conv1's ReLU mask
+        g2 = torch.randn(B, 9, 9, 64, device="cuda")
+        ag = native.amax_table(2, "cuda")
+        native.amax(g2, ag[0])
+        g2p = torch.empty(B, 9, 9, 128, dtype=torch.int16, device="cuda")
+        e = torch.zeros(1, dtype=torch.int32, device="cuda")
+        native.px_split(g2, ag[0], g2p, e)
+        bits = am.bits[0]
+        g1 = torch.empty(B, 20, 20, 32, device="cuda")
+        q = cv.q[12]
+        row = {"B": B, "op": "conv2 dgrad",
+               "colp_us": round(1e3 * t_ms(lambda: native.nature_conv_dgrad_split(2, g2, B, q, None, g1, amax_g=ag[0],
+                                                                                  amax_out=ag[1], relu_bits=bits)), 1),
+               "direct_us": round(1e3 * t_ms(lambda: native.nature_conv_dgrad_split(2, g2p, B, q, None, g1, amax_out=ag[1],
+                                                                                    relu_bits=bits, g_exp=e)), 1)}
+        byt = B * (81 * 64 * 4 + 400 * 32 * 4 + 400 * 4)  # g2 in, g1 out, conv1's bitmask in
+        for name in ("colp", "direct"):
+            t = row[name + "_us"] * 1e-6
+            row[name + "_tbs"] = round(byt / t / 1e12, 2)
+            row[name + "_tf"] = round(2 * 81 * 512 * 64 * B / t / 1e12, 1)
+        print(json.dumps(row), flush=True)
 
 
 if __name__ == "__main__":

@@ -51,16 +51,6 @@ def main():
                 dfp, B, cv.qfc[1], None, g3, amax_df=am[convs.AM_DF], df_exp=e, relu_bits=bits, g3_exp=ex,
                 amax_g3=amg[0])), 1)
         print(json.dumps(row), flush=True)
-        # the heads' hidden-layer dgrad (PPOX_DHDD, hdd_kernel) against its sg2 GEMM
-        de, f, dfh = (torch.randn(B, 512, device="cuda") for _ in range(3))
-        native.amax(de, am[convs.AM_DE])
-        row = {"B": B, "op": "head_dgrad"}
-        for name, v in (("gemm", "0"), ("direct", "1")):
-            os.environ["PPOX_DHDD"] = v
-            row[name + "_us"] = round(1e3 * t_ms(lambda: native.head_hidden_dgrad(
-                de, cv.qh[1], f, dfh, amax_de=am[convs.AM_DE], amax_df=amg[0])), 1)
-        print(json.dumps(row), flush=True)
-
 
 if __name__ == "__main__":
     main()
