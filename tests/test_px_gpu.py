@@ -71,7 +71,7 @@ def test_px_training_pass_is_fp32_class(B):
     dv = torch.randn(B, device="cuda", generator=g)
     o_off, v_off, g_off, _ = _pass(net, flat, cv, x, dout, dv, False)
     o_on, v_on, g_on, am = _pass(net, flat, cv, x, dout, dv, True)
-    assert am.px == [True, True, True, True], am.px  # h2, h3, g3, df all ran as planes
+    assert am.px == [True, True, True, True, True], am.px  # h2, h3, g3, df, g2 all ran as planes
     o64, v64, g64 = _fp64(ref, x, dout, dv)
     worst = []
     for name, r in list(g64.items()) + [("out", o64), ("v", v64)]:
@@ -96,7 +96,7 @@ def test_px_training_pass_big_batch_matches_f32_operands(B):
     dv = torch.randn(B, device="cuda", generator=g)
     o_off, v_off, g_off, _ = _pass(net, flat, cv, x, dout, dv, False)
     o_on, v_on, g_on, am = _pass(net, flat, cv, x, dout, dv, True)
-    assert am.px == [True, True, True, True], am.px
+    assert am.px == [True, True, True, True, True], am.px
     for name in g_off:
         a, b = g_on[name], g_off[name]
         scale = b.abs().max().item() + 1e-30
