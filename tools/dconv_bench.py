@@ -76,6 +76,20 @@ def main():
             row[name + "_tbs"] = round(byt / t / 1e12, 2)
             row[name + "_tf"] = round(2 * 81 * 512 * 64 * B / t / 1e12, 1)
         print(json.dumps(row), flush=True)
+        # conv3 dgrad on g3 planes: f32 g2 out against PX g2 out (the planes the direct conv2 dgrad reads)
+        g3 = torch.randn(B, 7, 7, 64, device="cuda")
+        native.amax(g3, ag[0])
+        g3p = torch.empty(B, 7, 7, 128, dtype=torch.int16, device="cuda")
+        e3 = torch.zeros(1, dtype=torch.int32, device="cuda")
+        native.px_split(g3, ag[0], g3p, e3)
+        q3 = cv.q[13]
+        bits2 = am.bits[1]
+        row = {"B": B, "op": "conv3 dgrad",
+               "f32_out_us": round(1e3 * t_ms(lambda: native.nature_conv_dgrad_split(
+                   3, g3p, B, q3, None, g2, amax_g=ag[0], amax_out=ag[1], relu_bits=bits2, g_exp=e3)), 1),
+               "px_out_us": round(1e3 * t_ms(lambda: native.nature_conv_dgrad_split(
+                   3, g3p, B, q3, None, g2p, amax_g=ag[0], amax_out=ag[1], relu_bits=bits2, g_exp=e3, y_exp=e)), 1)}
+        print(json.dumps(row), flush=True)
 
 
 if __name__ == "__main__":
