@@ -606,15 +606,15 @@ __global__ void __launch_bounds__(256, 1) fcd_kernel(Args a, const u32x4* __rest
 //     4 t + (co >> 4), t = 2 dy + dx) live in 128 AGPRs as MFMA srcA, so the tile is channels x pixels;
 //   * whole g2 sample images (PX planes, 81 pixels x 256 B) and conv1's ReLU bitmask of the sample
 //     (400 words) stream into an LDS ring by LDS-DMA, each byte read from HBM once;
-//   * a workgroup walks its contiguous range of samples in phases of 32 class rows (row m = 100 n + 10 a
+//   * a workgroup walks its contiguous range of samples in phases of 64 class rows (row m = 100 n + 10 a
 //     + b of sample n of the range); the four waves walk the same rows of their four classes, so a phase
 //     reads at most two samples.  An image pixel's 16-B pieces are stored at p ^ key, key = (4 n + 10 y
-//     + x) & 15 (100 = 4 mod 16): a row's pixel at tap t then has key (m - 10 dy - dx) & 15, so a 16-lane
-//     group of ds_read_b128 (16 consecutive rows) hits 16 distinct bank quads; a tap off the image reads
+//     + x) & 15 (100 = 4 mod 16): a row's pixel at tap t then has key (m - 10 dy - dx) & 15, so a lane
+//     group of ds_read_b128 (16 rows distinct mod 16) hits 16 distinct bank quads; a tap off the image reads
 //     a zero pixel at the same piece positions.
-// Every k-step is three v_mfma_f32_32x32x16_f16 (hi += Wh gh, lo += Wh gl, lo += Wl gh), fp32-class as
-// every split kernel; its k order (the four taps summed in the accumulators) is not the col2im form's, so
-// the result is held to the fp64 bounds, not bitwise (tests/test_dconv_gpu.py).
+// Every k-step is three v_mfma_f32_32x32x16_f16 (Wh gh, Wh gl, Wl gh), fp32-class as every split kernel;
+// its k order (the four taps summed in the accumulators) is not the col2im form's, so the result is held
+// to the fp64 bounds, not bitwise (tests/test_ddgrad2_gpu.py).
 constexpr int DD2_PIXB = 256, DD2_NPIX = 81, DD2_IMG = DD2_NPIX * DD2_PIXB;  // g2 planes of one sample
 constexpr int DD2_MASKB = 400 * 4;                                            // conv1's bitmask of one sample
 constexpr int DD2_IMG_DMAS = (DD2_IMG + 1023) / 1024;                         // 21
@@ -625,8 +625,16 @@ constexpr int DD2_NSLOT = 4, DD2_ZERO = DD2_NSLOT * DD2_SLOT, DD2_LDS = DD2_ZERO
 constexpr int DD2_ROWS = 100;  // class rows per sample
 static_assert(DD2_LDS <= 160 * 1024, "ddgrad2: LDS");
 
+// A phase is 64 class rows per wave (two 32-row tiles A, B: 6 MFMAs per k-step), so its barrier, DMA wait
+// and row setup are spread over 96 MFMAs; the next phase's per-lane row setup (tap addresses, output
+// offsets) is computed in the MFMA gaps of the current one, the previous phase's epilogue rides in its k
+// walk.  One accumulator per tile takes all three products of a k-step (Wh gh + Wh gl + Wl gh): each
+// MFMA rounds once per 16 MACs, so the sum is still fp32-class (3 roundings per 16 MACs against an f32
+// FMA chain's 16) — held to the fp64 bounds by tests/test_ddgrad2_gpu.py — and the registers of a
+// second (lo) set pay for the two tiles.
 __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __restrict__ wq) {
     constexpr int NK = 16;  // k-steps: 4 taps x 4 channel quarters
+    constexpr int PR = 64;  // class rows per phase (two tiles)
     __shared__ __attribute__((aligned(16))) uint8_t lds[DD2_LDS];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -636,40 +644,38 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
     const int NS = (int)(S1 - S0);
     if (NS <= 0) return;
     const int MR = NS * DD2_ROWS;
-    const int F_ = (MR + 31) / 32;
+    const int F_ = (MR + PR - 1) / PR;
     const uint8_t* gb = reinterpret_cast<const uint8_t*>(a.x) + S0 * DD2_IMG;
     const uint8_t* mb = reinterpret_cast<const uint8_t*>(a.bits_mask) + S0 * DD2_MASKB;
     const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
 
-    // DMA d = wave + 4 i of a sample: slot bytes [1024 d, 1024 d + 1024).  d < 21: image pixels
-    // (lane -> LDS pixel u, piece position lane & 15, holding the global piece (lane & 15) ^ key); d =
-    // 21, 22: the bitmask words (past its end: its last piece again, into the slot's pad); d > 22: DMA 22
-    // again (the same bytes to the same place)
-    int dpk[DD2_DMAS];  // image: LDS pixel u | its key offset (10 y + x) << 16; mask: -1 - byte offset
+    // DMA d = wave + 4 i of a sample fills slot bytes [1024 d, 1024 d + 1024): d < 21 image pixels (lane ->
+    // LDS pixel u, piece position lane & 15 holding the global piece (lane & 15) ^ key), d = 21, 22 the
+    // bitmask words (past their end: the last piece again, into the slot's pad), d > 22 DMA 22 again.
+    // Per DMA slot i: the lane's byte offset within the sample's image (without the key) or bitmask, and
+    // the pixel's key offset (10 y + x) & 15
+    uint32_t doff[DD2_DMAS], dkey[DD2_DMAS];
 #pragma unroll
     for (int i = 0; i < DD2_DMAS; ++i) {
         int d = wave + 4 * i;
         d = d < DD2_REAL_DMAS ? d : DD2_REAL_DMAS - 1;
-        if (d < DD2_IMG_DMAS) {
-            int u = (d * 1024 + lane * 16) / DD2_PIXB;
-            u = u < DD2_NPIX ? u : DD2_NPIX - 1;
-            dpk[i] = u | (((10 * (u / 9) + u % 9) & 15) << 16);
-        } else {
-            int off = (d - DD2_IMG_DMAS) * 1024 + lane * 16;
-            off = off < DD2_MASKB ? off : DD2_MASKB - 16;
-            dpk[i] = -1 - off;
-        }
+        int u = (d * 1024 + lane * 16) / DD2_PIXB;
+        u = u < DD2_NPIX ? u : DD2_NPIX - 1;
+        int mo = (d - DD2_IMG_DMAS) * 1024 + lane * 16;
+        mo = mo < DD2_MASKB ? mo : DD2_MASKB - 16;
+        doff[i] = d < DD2_IMG_DMAS ? (uint32_t)(u * DD2_PIXB) : (uint32_t)mo;
+        dkey[i] = (uint32_t)((10 * (u / 9) + u % 9) & 15);
     }
     auto issue_one = [&](int n, int i) {
-        int d = wave + 4 * i;
+        int d = wave + 4 * i;  // (uniform)
         d = d < DD2_REAL_DMAS ? d : DD2_REAL_DMAS - 1;
         uint8_t* dst = lds + (n % DD2_NSLOT) * DD2_SLOT + d * 1024;
         const uint8_t* src;
-        if (dpk[i] >= 0) {
-            const int key = (4 * n + (dpk[i] >> 16)) & 15, u = dpk[i] & 0xFFFF;
-            src = gb + (long long)n * DD2_IMG + (uint32_t)(u * DD2_PIXB + (((lane & 15) ^ key) << 4));
+        if (d < DD2_IMG_DMAS) {
+            const uint32_t key = (uint32_t)(4 * n + dkey[i]) & 15u;
+            src = gb + (long long)n * DD2_IMG + (doff[i] + ((((uint32_t)lane & 15u) ^ key) << 4));
         } else {
-            src = mb + (long long)n * DD2_MASKB + (uint32_t)(-1 - dpk[i]);
+            src = mb + (long long)n * DD2_MASKB + doff[i];
         }
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
@@ -691,124 +697,196 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
     }
     const float us = exp2i(-(*a.xexp + *a.wexp));  // the accumulators' unscale (powers of two: exact)
     if (threadIdx.x < 16) reinterpret_cast<u32x4*>(lds + DD2_ZERO)[threadIdx.x] = u32x4{0u, 0u, 0u, 0u};
+
+    // a tile's lane row: (n, a, b) of class row m, advanced by PR rows per phase without divisions
+    struct Pos {
+        int m, n, ra, rb;
+    };
+    auto pos_of = [&](int m) {
+        Pos P;
+        P.m = m;
+        P.n = m / DD2_ROWS;
+        const int rem = m - P.n * DD2_ROWS;
+        P.ra = rem / 10;
+        P.rb = rem - 10 * P.ra;
+        return P;
+    };
+    auto advance = [&](Pos& P) {  // + 64 rows = + 6 a-rows and 4 b-columns
+        P.m += PR;
+        P.rb += PR % 10;
+        const bool cb = P.rb >= 10;
+        P.rb -= cb ? 10 : 0;
+        P.ra += PR / 10 + (cb ? 1 : 0);
+        const bool ca = P.ra >= 10;
+        P.ra -= ca ? 10 : 0;
+        P.n += ca ? 1 : 0;
+    };
+    // a tile's per-lane setup: the read pixel of each tap (its base | (key ^ h) << 4; off the image: the
+    // zero pixel), the output pixel's float offset in g1 (-1: past the range), its mask word's address
+    struct Rows {
+        uint32_t tb[4];
+        int o;
+        uint32_t ma;
+    };
+    auto rows = [&](const Pos& P) {
+        Rows R;
+        const bool live = P.m < MR;
+        const int n = live ? P.n : NS - 1, ra = live ? P.ra : 9, rb = live ? P.rb : 9;
+        const uint32_t sbase = lds0 + (uint32_t)((n % DD2_NSLOT) * DD2_SLOT);
+        const uint32_t pix = sbase + (uint32_t)((9 * ra + rb) * DD2_PIXB);
+        const int mkey = 4 * n + 10 * ra + rb;
+        const bool oky[2] = {ra != 9, ra != 0}, okx[2] = {rb != 9, rb != 0};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int dy = t >> 1, dx = t & 1;
+            const uint32_t key = ((uint32_t)(mkey - 10 * dy - dx) & 15u) ^ (uint32_t)h;
+            const uint32_t at = pix - (uint32_t)((9 * dy + dx) * DD2_PIXB);
+            R.tb[t] = ((oky[dy] && okx[dx]) ? at : lds0 + DD2_ZERO) | (key << 4);
+        }
+        const int q = (2 * ra + py) * 20 + 2 * rb + px;
+        R.o = live ? (n * 400 + q) * 32 : -1;
+        R.ma = sbase + DD2_MASK0 + (uint32_t)(q * 4);
+        return R;
+    };
+    Pos QA = pos_of(r), QB = pos_of(32 + r);
+    Rows RA = rows(QA), RB = rows(QB);  // phase 0's
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     asm volatile("s_nop 4" ::: "memory");  // (VALU-written B registers before the first MFMA reads them)
 
     float* g1 = a.y + S0 * (400 * 32);
     float om = 0.f;
-    f32x16 H0, L0, H1, L1;
-    // the previous phase's rows: the lane's output pixel (float offset in g1, -1: past the range) and mask
-    int po = -1;
-    uint32_t pmw = 0u;
+    f32x16 A0, B0, A1, B1;
+    int poA = -1, poB = -1;  // the previous phase's output offsets and mask words (>> 4 h)
+    uint32_t pmA = 0u, pmB = 0u;
 
-    auto epi = [&](auto T, const f32x16& PH, const f32x16& PL, int o, uint32_t mw) {
+    // epilogue group t of a tile: channels 8 t + 4 h + k of the lane's pixel, times conv1's ReLU bit
+    auto epi = [&](auto T, const f32x16& C, int o, uint32_t mw) {
         constexpr int t = decltype(T)::value;
+        const f32x2 v01 = (f32x2){C[4 * t], C[4 * t + 1]} * (f32x2){us, us};
+        const f32x2 v23 = (f32x2){C[4 * t + 2], C[4 * t + 3]} * (f32x2){us, us};
+        const float vv[4] = {v01.x, v01.y, v23.x, v23.y};
         float v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            v[k] = (mw >> (8 * t + 4 * h + k)) & 1u ? (PH[4 * t + k] + PL[4 * t + k]) * us : 0.f;
+        for (int k = 0; k < 4; ++k) {  // bit -> all-ones or zero (one v_bfe_i32), ANDed with the value's bits
+            uint32_t mk;
+            asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(mk) : "v"(mw), "n"(8 * t + k));
+            v[k] = __uint_as_float(__float_as_uint(vv[k]) & mk);
+        }
         if (o >= 0) *reinterpret_cast<float4*>(g1 + o + 8 * t + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
         om = fmaxf(om, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
     };
-    // refill DMAs of a phase (up to RMAX samples) spread over k-steps 8 .. 15, after the epilogue's stores
-    constexpr int RMAX = 1, NDMA = RMAX * DD2_DMAS;  // (a phase refills at most one sample)
+    // refill DMAs (at most one sample per phase: 64 rows < 100) over k-steps 8 .. 13
+    constexpr int RMAX = 1, NDMA = RMAX * DD2_DMAS;
 
-    auto phase = [&](int f, f32x16& H, f32x16& Lo, const f32x16& PH, const f32x16& PL, auto PREV) {
-        const int m0 = 32 * f;
-        const int nlo = m0 / DD2_ROWS, nhi = min((m0 + 31) / DD2_ROWS, NS - 1);
+    auto phase = [&](int f, f32x16& CA, f32x16& CB, const f32x16& PA, const f32x16& PB, auto PREV) {
+        const int m0 = PR * f;
+        const int nlo = m0 / DD2_ROWS, nhi = min((m0 + PR - 1) / DD2_ROWS, NS - 1);
         dc_vm_wait<DD2_DMAS>(issued - 1 - nhi);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         const int rA = issued, nref = min(nlo + DD2_NSLOT, NS) - issued;
         issued += nref;
-        // this lane's row (past the range: the range's last row, never stored)
-        int m = m0 + r;
-        const bool live = m < MR;
-        m = live ? m : MR - 1;
-        const int n = m / DD2_ROWS, rem = m - n * DD2_ROWS, ra = rem / 10, rb = rem - 10 * ra;
-        const uint32_t sbase = lds0 + (n % DD2_NSLOT) * DD2_SLOT;
-        const int mkey = 4 * n + 10 * ra + rb;
-        uint32_t tb[4];  // per tap: the read pixel's base | (its key ^ h) << 4
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int dy = t >> 1, dx = t & 1, y = ra - dy, x = rb - dx;
-            const bool ok = (unsigned)y < 9u && (unsigned)x < 9u;
-            const uint32_t key = (uint32_t)((mkey - 10 * dy - dx) & 15) ^ (uint32_t)h;
-            tb[t] = (ok ? sbase + (uint32_t)((9 * y + x) * DD2_PIXB) : lds0 + DD2_ZERO) | (key << 4);
-        }
-        const int iy = 2 * ra + py, ix = 2 * rb + px;
-        // the mask word of this row's pixel (used by the next phase's epilogue), read before the fragments
-        uint32_t mw;
-        asm volatile("ds_read_b32 %0, %1" : "=v"(mw) : "v"(sbase + DD2_MASK0 + (uint32_t)((iy * 20 + ix) * 4)));
-        const int o = live ? (n * 400 + iy * 20 + ix) * 32 : -1;
-        // k-step i, plane pl: piece 8 (q >> 1) + 4 pl + 2 (q & 1) + h of the tap's pixel
-        auto addr = [&](int i, int pl) {
+        // this phase's mask words (for the next phase's epilogue), then k-steps 0 and 1's fragments
+        uint32_t mwA, mwB;
+        asm volatile("ds_read_b32 %0, %1" : "=v"(mwA) : "v"(RA.ma));
+        asm volatile("ds_read_b32 %0, %1" : "=v"(mwB) : "v"(RB.ma));
+        // k-step i, plane pl, tile: piece 8 (q >> 1) + 4 pl + 2 (q & 1) + h of the tap's pixel
+        auto addr = [&](const Rows& R, int i, int pl) {
             const int q = i & 3;
-            return tb[i >> 2] ^ ((uint32_t)(8 * (q >> 1) + 4 * pl + 2 * (q & 1)) << 4);
+            return R.tb[i >> 2] ^ ((uint32_t)(8 * (q >> 1) + 4 * pl + 2 * (q & 1)) << 4);
         };
         constexpr int PD = 2, NB = PD + 1;
-        u32x4 fa[NB][2];
-        auto rd1 = [&](auto I, auto PLc) {
-            constexpr int i = decltype(I)::value, pl = decltype(PLc)::value;
-            fa[i % NB][pl] = dc_read<0>(addr(i, pl));
+        u32x4 fa[NB][2][2];  // [k-step buffer][tile][plane]
+        auto rd = [&](auto I, auto TL, auto PLc) {
+            constexpr int i = decltype(I)::value, tl = decltype(TL)::value, pl = decltype(PLc)::value;
+            fa[i % NB][tl][pl] = dc_read<0>(addr(tl ? RB : RA, i, pl));
         };
-        rd1(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-        rd1(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
-        rd1(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
-        rd1(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
-        asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(mw));
-        const int o_prev = po;
-        const uint32_t mw_prev = pmw;
+        using Z = std::integral_constant<int, 0>;
+        using O = std::integral_constant<int, 1>;
+        dc_unroll([&](auto I) { rd(I, Z{}, Z{}); rd(I, Z{}, O{}); rd(I, O{}, Z{}); rd(I, O{}, O{}); },
+                  std::make_integer_sequence<int, PD>{});
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(fa[0][0][0]), "+v"(fa[0][0][1]), "+v"(fa[0][1][0]),
+                     "+v"(fa[0][1][1]), "+v"(mwA), "+v"(mwB));
+        mwA >>= 4 * h;
+        mwB >>= 4 * h;
+        Rows NA, NBr;  // the next phase's row setup, computed in this phase's gaps
         dc_unroll(
             [&](auto I) {
                 constexpr int i = decltype(I)::value;
                 constexpr bool P = decltype(PREV)::value;
                 const u32x4& b0 = bq[i][0];
                 const u32x4& b1 = bq[i][1];
-                if constexpr (i == 0)
-                    dc_mfma0<true>(H, fa[0][0], b0);
-                else
-                    dc_mfma<true>(H, fa[i % NB][0], b0);
-                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 0>{});
-                if constexpr (i == 0)
-                    dc_mfma0<true>(Lo, fa[0][0], b1);
-                else
-                    dc_mfma<true>(Lo, fa[i % NB][0], b1);
-                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, std::integral_constant<int, 1>{});
-                if constexpr (P && (i & 1) && i < 8) epi(std::integral_constant<int, i / 2>{}, PH, PL, o_prev, mw_prev);
-                dc_mfma<true>(Lo, fa[i % NB][1], b0);
+                const u32x4(&x)[2][2] = fa[i % NB];
+                if constexpr (i == 0) {
+                    dc_mfma0<true>(CA, x[0][0], b0);
+                    dc_mfma0<true>(CB, x[1][0], b0);
+                } else {
+                    dc_mfma<true>(CA, x[0][0], b0);
+                    dc_mfma<true>(CB, x[1][0], b0);
+                }
+                if constexpr (i + PD < NK) rd(std::integral_constant<int, i + PD>{}, Z{}, Z{});
+                if constexpr (i + PD < NK) rd(std::integral_constant<int, i + PD>{}, Z{}, O{});
+                dc_mfma<true>(CA, x[0][0], b1);
+                dc_mfma<true>(CB, x[1][0], b1);
+                if constexpr (i + PD < NK) rd(std::integral_constant<int, i + PD>{}, O{}, Z{});
+                if constexpr (i + PD < NK) rd(std::integral_constant<int, i + PD>{}, O{}, O{});
+                // the previous phase's epilogue: tile A's groups at k-steps 1, 3, 5, 7, tile B's at 9 .. 15
+                if constexpr (P && (i & 1)) {
+                    constexpr int g = i >> 1;
+                    if constexpr (g < 4)
+                        epi(std::integral_constant<int, g>{}, PA, poA, pmA);
+                    else
+                        epi(std::integral_constant<int, g - 4>{}, PB, poB, pmB);
+                }
+                dc_mfma<true>(CA, x[0][1], b0);
+                dc_mfma<true>(CB, x[1][1], b0);
+                if constexpr (i == 4) {
+                    advance(QA);
+                    advance(QB);
+                }
+                if constexpr (i == 6) NA = rows(QA);
+                if constexpr (i == 10) NBr = rows(QB);
                 dc_unroll(
                     [&](auto X) {
-                        constexpr int x = decltype(X)::value, t = x / DD2_DMAS;
-                        if constexpr (8 + x * (NK - 8) / NDMA == i) {
-                            if (t < nref) issue_one(rA + t, x % DD2_DMAS);
+                        constexpr int x_ = decltype(X)::value, t = x_ / DD2_DMAS;
+                        if constexpr (8 + x_ == i) {
+                            if (t < nref) issue_one(rA + t, x_ % DD2_DMAS);
                         }
                     },
                     std::make_integer_sequence<int, NDMA>{});
                 constexpr int later = (i + PD < NK ? i + PD : NK - 1) - (i + 1);
-                if constexpr (i + 1 < NK) dc_lgkm<2 * later>(fa[(i + 1) % NB][0], fa[(i + 1) % NB][1]);
+                if constexpr (i + 1 < NK) {
+                    constexpr int j = (i + 1) % NB;
+                    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(fa[j][0][0]), "+v"(fa[j][0][1]), "+v"(fa[j][1][0]),
+                                 "+v"(fa[j][1][1]) : "n"(4 * later));
+                }
             },
             std::make_integer_sequence<int, NK>{});
         for (int t = RMAX; t < nref; ++t) issue_sample(rA + t);
-        po = o;
-        pmw = mw;
-        dc_acc_fence(H, Lo);
+        poA = RA.o;
+        poB = RB.o;
+        pmA = mwA;
+        pmB = mwB;
+        RA = NA;
+        RB = NBr;
+        dc_acc_fence(CA, CB);
     };
-    auto final_epi = [&](const f32x16& PH, const f32x16& PL) {
-        dc_unroll([&](auto T) { epi(T, PH, PL, po, pmw); }, std::make_integer_sequence<int, 4>{});
+    auto final_epi = [&](const f32x16& PA, const f32x16& PB) {
+        dc_unroll([&](auto T) { epi(T, PA, poA, pmA); }, std::make_integer_sequence<int, 4>{});
+        dc_unroll([&](auto T) { epi(T, PB, poB, pmB); }, std::make_integer_sequence<int, 4>{});
     };
-    phase(0, H0, L0, H1, L1, std::false_type{});
+    phase(0, A0, B0, A1, B1, std::false_type{});
     int f = 1;
 #pragma unroll 1
     for (; f + 1 < F_; f += 2) {
-        phase(f, H1, L1, H0, L0, std::true_type{});
-        phase(f + 1, H0, L0, H1, L1, std::true_type{});
+        phase(f, A1, B1, A0, B0, std::true_type{});
+        phase(f + 1, A0, B0, A1, B1, std::true_type{});
     }
-    if (f < F_) phase(f, H1, L1, H0, L0, std::true_type{});
+    if (f < F_) phase(f, A1, B1, A0, B0, std::true_type{});
     if ((F_ - 1) & 1)
-        final_epi(H1, L1);
+        final_epi(A1, B1);
     else
-        final_epi(H0, L0);
+        final_epi(A0, B0);
     amax_record(a.amax_y, om);
 }
 
