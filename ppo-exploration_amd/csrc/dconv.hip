@@ -776,7 +776,7 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
         if (o >= 0) *reinterpret_cast<float4*>(g1 + o + 8 * t + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
         om = fmaxf(om, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
     };
-    // refill DMAs (at most one sample per phase: 64 rows < 100) over k-steps 8 .. 13
+    // refill DMAs (at most one sample per phase: 64 rows < 100) over k-steps 9 .. 14
     constexpr int RMAX = 1, NDMA = RMAX * DD2_DMAS;
 
     auto phase = [&](int f, f32x16& CA, f32x16& CB, const f32x16& PA, const f32x16& PB, auto PREV) {
@@ -830,26 +830,27 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
                 dc_mfma<true>(CB, x[1][0], b1);
                 if constexpr (i + PD < NK) rd(std::integral_constant<int, i + PD>{}, O{}, Z{});
                 if constexpr (i + PD < NK) rd(std::integral_constant<int, i + PD>{}, O{}, O{});
-                // the previous phase's epilogue: tile A's groups at k-steps 1, 3, 5, 7, tile B's at 9 .. 15
-                if constexpr (P && (i & 1)) {
-                    constexpr int g = i >> 1;
-                    if constexpr (g < 4)
-                        epi(std::integral_constant<int, g>{}, PA, poA, pmA);
+                // the previous phase's epilogue, one group per k-step: tile A's at k-steps 0 .. 3, tile B's at
+                // 4 .. 7 — early, so its stores complete before the next phase's vmcnt wait, which (gfx9: one
+                // counter for loads and stores) covers every store issued before this phase's refill DMAs
+                if constexpr (P && i < 8) {
+                    if constexpr (i < 4)
+                        epi(std::integral_constant<int, i>{}, PA, poA, pmA);
                     else
-                        epi(std::integral_constant<int, g - 4>{}, PB, poB, pmB);
+                        epi(std::integral_constant<int, i - 4>{}, PB, poB, pmB);
                 }
                 dc_mfma<true>(CA, x[0][1], b0);
                 dc_mfma<true>(CB, x[1][1], b0);
-                if constexpr (i == 4) {
+                if constexpr (i == 8) {
                     advance(QA);
                     advance(QB);
                 }
-                if constexpr (i == 6) NA = rows(QA);
-                if constexpr (i == 10) NBr = rows(QB);
+                if constexpr (i == 9) NA = rows(QA);
+                if constexpr (i == 11) NBr = rows(QB);
                 dc_unroll(
                     [&](auto X) {
                         constexpr int x_ = decltype(X)::value, t = x_ / DD2_DMAS;
-                        if constexpr (8 + x_ == i) {
+                        if constexpr (9 + x_ == i) {
                             if (t < nref) issue_one(rA + t, x_ % DD2_DMAS);
                         }
                     },
