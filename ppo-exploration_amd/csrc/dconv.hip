@@ -666,23 +666,26 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
         doff[i] = d < DD2_IMG_DMAS ? (uint32_t)(u * DD2_PIXB) : (uint32_t)mo;
         dkey[i] = (uint32_t)((10 * (u / 9) + u % 9) & 15);
     }
-    auto issue_one = [&](int n, int i) {
+    // buffer descriptors (wave-uniform: built from kernel arguments and blockIdx only) of the range's g2
+    // planes and bitmask words (the LDS-DMA sources: sample n at soffset n * bytes, the lane's piece in the
+    // 32-bit voffset) and of its g1 rows (the epilogue's stores: a dead row's offset is past the end, so the
+    // hardware drops its store — no branch)
+    const auto g_rs = __builtin_amdgcn_make_buffer_rsrc((void*)gb, 0, NS * DD2_IMG, 0x00020000);
+    const auto m_rs = __builtin_amdgcn_make_buffer_rsrc((void*)mb, 0, NS * DD2_MASKB, 0x00020000);
+    auto issue_one = [&](int n, auto I) {
+        constexpr int i = decltype(I)::value;
         int d = wave + 4 * i;  // (uniform)
         d = d < DD2_REAL_DMAS ? d : DD2_REAL_DMAS - 1;
-        uint8_t* dst = lds + (n % DD2_NSLOT) * DD2_SLOT + d * 1024;
-        const uint8_t* src;
-        if (d < DD2_IMG_DMAS) {
-            const uint32_t key = (uint32_t)(4 * n + dkey[i]) & 15u;
-            src = gb + (long long)n * DD2_IMG + (doff[i] + ((((uint32_t)lane & 15u) ^ key) << 4));
-        } else {
-            src = mb + (long long)n * DD2_MASKB + doff[i];
-        }
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+        auto* dst = (__attribute__((address_space(3))) void*)(lds + (n % DD2_NSLOT) * DD2_SLOT + d * 1024);
+        const uint32_t key = (uint32_t)(4 * n + dkey[i]) & 15u;
+        const uint32_t vimg = doff[i] + ((((uint32_t)lane & 15u) ^ key) << 4);
+        if (4 * i + 3 < DD2_IMG_DMAS || d < DD2_IMG_DMAS)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(g_rs, dst, 16, vimg, n * DD2_IMG, 0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(m_rs, dst, 16, doff[i], n * DD2_MASKB, 0, 0);
     };
     auto issue_sample = [&](int n) {
-#pragma unroll
-        for (int i = 0; i < DD2_DMAS; ++i) issue_one(n, i);
+        dc_unroll([&](auto I) { issue_one(n, I); }, std::make_integer_sequence<int, DD2_DMAS>{});
     };
     int issued = NS < DD2_NSLOT ? NS : DD2_NSLOT;
     for (int n = 0; n < issued; ++n) issue_sample(n);
@@ -722,10 +725,10 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
         P.n += ca ? 1 : 0;
     };
     // a tile's per-lane setup: the read pixel of each tap (its base | (key ^ h) << 4; off the image: the
-    // zero pixel), the output pixel's float offset in g1 (-1: past the range), its mask word's address
+    // zero pixel), the output pixel's byte offset in g1 (past the end for a dead row), its mask word's address
     struct Rows {
         uint32_t tb[4];
-        int o;
+        int o;  // the output pixel's byte offset in the range's g1
         uint32_t ma;
     };
     auto rows = [&](const Pos& P) {
@@ -744,7 +747,7 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
             R.tb[t] = ((oky[dy] && okx[dx]) ? at : lds0 + DD2_ZERO) | (key << 4);
         }
         const int q = (2 * ra + py) * 20 + 2 * rb + px;
-        R.o = live ? (n * 400 + q) * 32 : -1;
+        R.o = live ? (n * 400 + q) * 128 : 0x7FFFFF00;  // byte offset in the range's g1 (dead: past the end)
         R.ma = sbase + DD2_MASK0 + (uint32_t)(q * 4);
         return R;
     };
@@ -754,10 +757,10 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
     __syncthreads();
     asm volatile("s_nop 4" ::: "memory");  // (VALU-written B registers before the first MFMA reads them)
 
-    float* g1 = a.y + S0 * (400 * 32);
+    const auto o_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + S0 * (400 * 32)), 0, NS * (400 * 32 * 4), 0x00020000);
     float om = 0.f;
     f32x16 A0, B0, A1, B1;
-    int poA = -1, poB = -1;  // the previous phase's output offsets and mask words (>> 4 h)
+    int poA = 0x7FFFFF00, poB = 0x7FFFFF00;  // the previous phase's output byte offsets and mask words (>> 4 h)
     uint32_t pmA = 0u, pmB = 0u;
 
     // epilogue group t of a tile: channels 8 t + 4 h + k of the lane's pixel, times conv1's ReLU bit
@@ -773,7 +776,9 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
             asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(mk) : "v"(mw), "n"(8 * t + k));
             v[k] = __uint_as_float(__float_as_uint(vv[k]) & mk);
         }
-        if (o >= 0) *reinterpret_cast<float4*>(g1 + o + 8 * t + 4 * h) = make_float4(v[0], v[1], v[2], v[3]);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])}, o_rs,
+            (uint32_t)o + (uint32_t)(32 * t + 16 * h), 0, 0);
         om = fmaxf(om, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
     };
     // refill DMAs (at most one sample per phase: 64 rows < 100) over k-steps 9 .. 14
@@ -851,7 +856,7 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
                     [&](auto X) {
                         constexpr int x_ = decltype(X)::value, t = x_ / DD2_DMAS;
                         if constexpr (9 + x_ == i) {
-                            if (t < nref) issue_one(rA + t, x_ % DD2_DMAS);
+                            if (t < nref) issue_one(rA + t, std::integral_constant<int, x_ % DD2_DMAS>{});
                         }
                     },
                     std::make_integer_sequence<int, NDMA>{});
