@@ -519,6 +519,9 @@ def main():
                         "solo_mean_us": q["mean_us"], "rows": q["rows"], "bound": q["bound"], "frac": q["frac"],
                         "mfma_frac": q["mfma_frac"], "hbm_frac": q["hbm_frac"], "pmc_ratio": q["traffic_ratio"]})
         out["roofline_top"] = top
+        # every training-pass MFMA kernel's one-stream mean (us) at its most frequent row count
+        out["solo_us"] = {KERNELS[k]["label"]: round(float(np.mean([t for t, _ in solo[k]])) * 1e3, 1)
+                          for k in sorted(totals, key=totals.get, reverse=True) if solo[k]}
     duo_tot = {k: sum(t for t, _ in v) for k, v in duo.items()}
     if any(duo_tot.values()):
         k2 = max(duo_tot, key=duo_tot.get)
