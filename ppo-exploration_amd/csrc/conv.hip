@@ -3420,8 +3420,10 @@ extern "C" int64_t ppox_nature_wgrad_split_workspace_bytes(int32_t layer, int64_
         w2p_grid(batch, per, grid);
         return std::max(Ws1::workspace_bytes(batch), 2 * grid * (long long)(G1::K * G1::COUT + G1::COUT) * 4);
     }
-    return layer == 1 ? Ws1::workspace_bytes(batch) : layer == 2 ? Ws2::workspace_bytes(batch)
-                      : layer == 3 ? Ws3::workspace_bytes(batch) : -1;
+    if (layer == 3)  // the im2col split form's slabs, or the direct form's (one per workgroup, PX operands)
+        return std::max(Ws3::workspace_bytes(batch),
+                        ppox_conv::dwgrad3_grid(batch) * (long long)(G3::K * G3::COUT + G3::COUT) * 4);
+    return layer == 1 ? Ws1::workspace_bytes(batch) : layer == 2 ? Ws2::workspace_bytes(batch) : -1;
 }
 
 extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_t batch, int64_t x_sample_stride,
@@ -3451,6 +3453,13 @@ extern "C" int ppox_nature_conv_wgrad_split(int32_t layer, const void* x, int64_
     }
     PPOX_REQUIRE(ppox::aligned16(x), "ppox_nature_conv_wgrad_split: layer 2/3 input must be 16B-aligned NHWC");
     if (layer == 2) return Ws2::run(x, 0, grad_out, batch, workspace, dw, db, amax_x, amax_g, s);
+    if (x_exp && g_exp && ppox_conv::dwgrad3_enabled(batch)) {  // the direct form (dconv.hip)
+        float* slab = reinterpret_cast<float*>(workspace);
+        float* bslab = slab + ppox_conv::dwgrad3_grid(batch) * (G3::K * G3::COUT);
+        const int rc = ppox_conv::dwgrad3(x, grad_out, batch, x_exp, g_exp, slab, bslab, s);
+        if (rc != PPOX_OK) return rc;
+        return launch_wgrad_reduce<G3, true>(slab, bslab, (int)ppox_conv::dwgrad3_grid(batch), dw, db, s);
+    }
     if (x_exp && g_exp) return Ws3PP::run(x, 0, grad_out, batch, workspace, dw, db, amax_x, amax_g, s, nullptr, 0, 0, x_exp, g_exp);
     if (x_exp) return Ws3PF::run(x, 0, grad_out, batch, workspace, dw, db, amax_x, amax_g, s, nullptr, 0, 0, x_exp, g_exp);
     if (g_exp) return Ws3FP::run(x, 0, grad_out, batch, workspace, dw, db, amax_x, amax_g, s, nullptr, 0, 0, x_exp, g_exp);

@@ -896,6 +896,271 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
     amax_record(a.amax_y, om);
 }
 
+// ---------------------------------------------------------------------------
+// conv3 weight gradient, direct (round 5; models-checkpoint.py:57 Conv2d(64, 64, 3) trained by ppo.py:241):
+//   dW3[co][ci][ky][kx] = sum over samples n and output pixels p = (oy, ox) of h2[n][oy + ky][ox + kx][ci] g3[n][p][co]
+//   db3[co]             = sum g3[n][p][co]
+// The im2col form (wgrad_split_kernel) stages nine copies of every h2 pixel through L2 and leaves ~400
+// partial slabs at 16,384 rows.  Here one 256-thread workgroup per CU walks its own range of samples: per
+// sample the PX h2 image (81 pixels x 256 B) and the PX g3 image (49 x 256 B) stream into an LDS ring by
+// LDS-DMA, laid out as (channel half, plane) sub-images of 64-B rows, so the transposing LDS read
+// (ds_read_b64_tr_b16; lane (h, g16, qq, pp) supplies row 8 h + 4 r + qq of a k-step, 8 B at column
+// 32 g16 + 8 pp, as wgrad2_planes_kernel) builds the MFMA fragments straight from the images: A = h2 rows
+// (M = the 32 input channels of a half, K = 16 output pixels read at the tap's offset), B = g3 rows (N = 32
+// output channels).  A sample's 49 pixels are 4 k-steps of 16 (g3 rows 49..63 are zero: DMA'd from past the
+// buffer's end, which the hardware returns as zeros).
+//   * wave w: h2 channel half ca = w & 1; taps 0..3 (w < 2) or 5..8 for both output-channel halves, and the
+//     centre tap 4 for output half w >> 1 — 9 tiles of 32 x 32, 27 MFMAs per k-step on every SIMD;
+//   * the h2 sub-images have a row pitch of 11 slots: the 4 rows a lane quad reads for 4 consecutive output
+//     pixels p sit at slot 11 (oy + ky) + ox + kx = p + const (mod 4) (7 = 11 = -1 mod 4), 4 distinct bank
+//     quarters for every tap — conflict-free; g3 rows are consecutive pixels;
+//   * a k-step's fragment reads (8 of g3, 4 per tap of h2) are issued one unit ahead of their MFMAs; the
+//     three products of a split pair (Hh Gh, Hh Gl, Hl Gh) go into one accumulator per tile (as ddgrad2:
+//     fp32-class, held to the fp64 bound by tests/test_dwgrad3_gpu.py);
+//   * the bias: wave w sums the g3 fragment (output half w >> 1, plane w & 1) with v_dot2_f32_f16 x ones.
+// Per-workgroup partial slabs, summed in a fixed order by wgrad_reduce (deterministic).
+constexpr int W3_HP = 11;                                       // h2 sub-image row pitch (slots)
+constexpr int W3_HSUB = 9 * W3_HP * 64;                         // 6,336 B: one h2 (channel half, plane) sub-image
+constexpr int W3_GSUB = 64 * 64;                                // 4,096 B: one g3 sub-image (rows 49..63 zero)
+constexpr int W3_H0 = 4 * W3_GSUB;                              // the h2 sub-images follow the g3 ones
+constexpr int W3_REAL_DMAS = 16 + (4 * W3_HSUB + 1023) / 1024;  // 41 1-KB DMAs per sample
+constexpr int W3_SLOT = W3_REAL_DMAS * 1024, W3_DMAS = (W3_REAL_DMAS + 3) / 4;  // per wave: 11
+constexpr int W3_NSLOT = 3, W3_LDS = W3_NSLOT * W3_SLOT;        // 125,952 B
+constexpr int W3_HIMG = 81 * 256, W3_GIMG = 49 * 256;           // PX bytes per sample
+constexpr int W3_SLAB = 576 * 64;                               // floats of a partial slab
+static_assert(W3_LDS <= 160 * 1024, "dwgrad3: LDS");
+
+struct W3PArgs {
+    const uint8_t* h2;  // PX h2 [batch][81][256 B]
+    const uint8_t* g3;  // PX g3 [batch][49][256 B]
+    const int* h_exp;   // h2 * 2^h_exp = hi + lo
+    const int* g_exp;
+    float* slab;   // [gridDim.x][576][64] (k = tap * 64 + ci)
+    float* bslab;  // [gridDim.x][64]
+    long long batch;
+};
+
+typedef unsigned int w3u2 __attribute__((ext_vector_type(2)));
+template <int OFF>
+__device__ inline w3u2 w3_tr(uint32_t addr) {  // (asm: hipcc would wait for the ring's DMAs before a plain read)
+    w3u2 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+    return r;
+}
+__device__ inline u32x4 w3_cat(w3u2 x0, w3u2 x1) { return u32x4{x0.x, x0.y, x1.x, x1.y}; }
+template <int N>
+__device__ inline void w3_lgkm(w3u2 (&x)[8]) {
+    asm volatile("s_waitcnt lgkmcnt(%8)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7])
+                 : "n"(N));
+}
+template <int N>
+__device__ inline void w3_lgkm(w3u2 (&x)[8], w3u2 (&y)[8]) {
+    asm volatile("s_waitcnt lgkmcnt(%16)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+                   "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]), "+v"(y[7])
+                 : "n"(N));
+}
+// the slot offset of tap t in an h2 sub-image
+template <int T>
+constexpr int w3_toff() { return (W3_HP * (T / 3) + T % 3) * 64; }
+
+__global__ void __launch_bounds__(256, 1) dwgrad3_kernel(W3PArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[W3_LDS];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ca = wave & 1, hb = wave >> 1;
+    const long long S0 = blockIdx.x * a.batch / gridDim.x, S1 = (blockIdx.x + 1) * a.batch / gridDim.x;
+    const int NS = (int)(S1 - S0);  // >= 1 (grid <= batch)
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
+
+    // DMA d = wave + 4 i (past the 41st: the 41st again) fills slot bytes [1024 d, 1024 d + 1024).  d < 16: g3
+    // sub-image d >> 2 = 2 b + P, rows 16 (d & 3) + (lane >> 2), piece lane & 3 (rows >= 49: past the end, zeros);
+    // else h2: byte e = 1024 (d - 16) + 16 lane of the h2 sub-images, sub-image e / W3_HSUB = 2 ca + P, slot
+    // (e % W3_HSUB) >> 6 = 11 iy + ix (ix >= 9 and the tail past the 4th sub-image: zeros)
+    uint32_t doff[W3_DMAS];
+#pragma unroll
+    for (int i = 0; i < W3_DMAS; ++i) {
+        int d = wave + 4 * i;
+        d = d < W3_REAL_DMAS ? d : W3_REAL_DMAS - 1;
+        if (d < 16) {
+            const int row = 16 * (d & 3) + (lane >> 2);
+            doff[i] = row < 49 ? (uint32_t)(row * 256 + (d >> 2) * 64 + (lane & 3) * 16) : 0x80000000u;
+        } else {
+            const int e = 1024 * (d - 16) + 16 * lane, sh = e / W3_HSUB, sl = (e % W3_HSUB) >> 6;
+            const int iy = sl / W3_HP, ix = sl % W3_HP;
+            doff[i] = (sh < 4 && ix < 9) ? (uint32_t)((9 * iy + ix) * 256 + sh * 64 + ((e >> 4) & 3) * 16)
+                                         : 0x80000000u;
+        }
+    }
+    const auto h_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.h2 + S0 * W3_HIMG), 0, NS * W3_HIMG, 0x00020000);
+    const auto g_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.g3 + S0 * W3_GIMG), 0, NS * W3_GIMG, 0x00020000);
+    auto issue_sample = [&](int n) {
+        const int slot = n % W3_NSLOT;
+        dc_unroll(
+            [&](auto I) {
+                constexpr int i = decltype(I)::value;
+                int d = wave + 4 * i;
+                d = d < W3_REAL_DMAS ? d : W3_REAL_DMAS - 1;
+                auto* dst = (__attribute__((address_space(3))) void*)(lds + slot * W3_SLOT + d * 1024);
+                if (d < 16)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(g_rs, dst, 16, doff[i], n * W3_GIMG, 0, 0);
+                else
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(h_rs, dst, 16, doff[i], n * W3_HIMG, 0, 0);
+            },
+            std::make_integer_sequence<int, W3_DMAS>{});
+    };
+    const int ahead = NS < W3_NSLOT - 1 ? NS : W3_NSLOT - 1;
+    for (int n = 0; n < ahead; ++n) issue_sample(n);
+
+    // per-lane fragment row addresses (slot 0): k-step ks, row quad r -> output pixel p (rows past 48: pixel 48,
+    // whose g3 partner rows are zero)
+    const int h = lane >> 5, g16 = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+    const uint32_t lcol = (uint32_t)(g16 * 32 + pp * 8);
+    uint32_t abase[4][2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            int p = 16 * ks + 8 * h + 4 * r + qq;
+            p = p < 49 ? p : 48;
+            abase[ks][r] = lds0 + W3_H0 + (uint32_t)(ca * 2 * W3_HSUB + (W3_HP * (p / 7) + p % 7) * 64) + lcol;
+        }
+    const uint32_t bbase = lds0 + (uint32_t)((8 * h + qq) * 64) + lcol;
+
+    f32x16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = zero16();
+    float bsum = 0.f;
+    const f16x2 ones = {(_Float16)1.0f, (_Float16)1.0f};
+
+    // one sample: 16 units (k-step ks, tap slot j: j < 3 one tap x both output halves, j = 3 the tap-half's
+    // last tap x both halves + the centre tap x half hb); unit u + 1's reads are issued before unit u's MFMAs.
+    // One code path for every wave (a branch on the tap half made hipcc shuttle the 144 accumulators between
+    // AGPRs and VGPRs around it): the tap half is a uniform per-slot address delta, the centre tap's output
+    // half a select of the g3 fragment
+    int tdel[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tdel[j] = hb ? (W3_HP * ((5 + j) / 3) + (5 + j) % 3 - (W3_HP * (j / 3) + j % 3)) * 64 : 0;
+    auto sample = [&](uint32_t so) {
+        uint32_t ab[4][2], bb = bbase + so;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int r = 0; r < 2; ++r) ab[ks][r] = abase[ks][r] + so;
+        asm volatile("" : "+v"(bb), "+v"(ab[0][0]), "+v"(ab[0][1]), "+v"(ab[1][0]), "+v"(ab[1][1]), "+v"(ab[2][0]),
+                     "+v"(ab[2][1]), "+v"(ab[3][0]), "+v"(ab[3][1]));
+        w3u2 ra[2][8];  // [unit parity][(tap slot, plane, r)]
+        w3u2 rb[2][8];  // [k-step parity][(half, plane, r)]
+        auto reads = [&](auto U) {
+            constexpr int u = decltype(U)::value, ks = u >> 2, j = u & 3;
+            if constexpr (j == 0) {
+                dc_unroll(
+                    [&](auto X) {
+                        constexpr int x = decltype(X)::value, b = x >> 2, P = (x >> 1) & 1, r = x & 1;
+                        rb[ks & 1][x] = w3_tr<(2 * b + P) * W3_GSUB + ks * 1024 + r * 256>(bb);
+                    },
+                    std::make_integer_sequence<int, 8>{});
+            }
+            constexpr int nt = j == 3 ? 2 : 1;
+            uint32_t at[2] = {ab[ks][0] + (uint32_t)tdel[j], ab[ks][1] + (uint32_t)tdel[j]};
+            dc_unroll(
+                [&](auto X) {
+                    constexpr int x = decltype(X)::value, s = x >> 2, P = (x >> 1) & 1, r = x & 1;
+                    if constexpr (s == 0)
+                        ra[u & 1][x] = w3_tr<P * W3_HSUB + w3_toff<j>()>(at[r]);
+                    else
+                        ra[u & 1][x] = w3_tr<P * W3_HSUB + w3_toff<4>()>(ab[ks][r]);
+                },
+                std::make_integer_sequence<int, 4 * nt>{});
+        };
+        reads(std::integral_constant<int, 0>{});
+        dc_unroll(
+            [&](auto U) {
+                constexpr int u = decltype(U)::value, ks = u >> 2, j = u & 3;
+                if constexpr (u + 1 < 16) {
+                    reads(std::integral_constant<int, u + 1>{});
+                    // the reads issued after unit u's: unit u + 1's
+                    constexpr int later = ((u + 1) & 3) == 0 ? 8 + 4 : (((u + 1) & 3) == 3 ? 8 : 4);
+                    if constexpr (j == 0)
+                        w3_lgkm<later>(ra[u & 1], rb[ks & 1]);
+                    else
+                        w3_lgkm<later>(ra[u & 1]);
+                } else {
+                    w3_lgkm<0>(ra[u & 1]);
+                }
+                u32x4 A[2][2], B[2][2];
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int P = 0; P < 2; ++P) B[b][P] = w3_cat(rb[ks & 1][b * 4 + P * 2], rb[ks & 1][b * 4 + P * 2 + 1]);
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                    for (int P = 0; P < 2; ++P) A[s][P] = w3_cat(ra[u & 1][s * 4 + P * 2], ra[u & 1][s * 4 + P * 2 + 1]);
+                if constexpr (j == 0) {  // the bias: fragment (hb, ca) of this k-step
+                    const u32x4 bh = hb ? B[1][0] : B[0][0], bl = hb ? B[1][1] : B[0][1];
+                    const u32x4 bv = ca ? bl : bh;
+                    // (the element copied out first: hipcc's bit_cast of an ext-vector element lvalue read
+                    // element 0 for every e)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const uint32_t w = bv[e];
+                        bsum = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, w), ones, bsum, false);
+                    }
+                }
+                constexpr int PA[3] = {0, 0, 1}, PB[3] = {0, 1, 0};
+                u32x4 B4[2];
+                if constexpr (j == 3) {
+                    B4[0] = hb ? B[1][0] : B[0][0];
+                    B4[1] = hb ? B[1][1] : B[0][1];
+                }
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    acc[2 * j] = mfma_f16(A[0][PA[k]], B[0][PB[k]], acc[2 * j]);
+                    acc[2 * j + 1] = mfma_f16(A[0][PA[k]], B[1][PB[k]], acc[2 * j + 1]);
+                    if constexpr (j == 3) acc[8] = mfma_f16(A[1][PA[k]], B4[PB[k]], acc[8]);
+                }
+            },
+            std::make_integer_sequence<int, 16>{});
+    };
+
+#pragma unroll 1
+    for (int n = 0; n < NS; ++n) {
+        dc_vm_wait<W3_DMAS>(n + 1 < NS ? 1 : 0);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (n + W3_NSLOT - 1 < NS) issue_sample(n + W3_NSLOT - 1);  // into sample n - 1's slot (all waves past it)
+        sample((uint32_t)((n % W3_NSLOT) * W3_SLOT));
+    }
+
+    const float uo = exp2i(-(*a.h_exp + *a.g_exp));
+    float* slab = a.slab + (long long)blockIdx.x * W3_SLAB;
+    auto store_tile = [&](const f32x16& C, int tap, int b) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int k = tap * 64 + 32 * ca + (r & 3) + 8 * (r >> 2) + 4 * h;
+            slab[k * 64 + 32 * b + (lane & 31)] = C[r] * uo;
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        store_tile(acc[2 * j], hb ? 5 + j : j, 0);
+        store_tile(acc[2 * j + 1], hb ? 5 + j : j, 1);
+    }
+    store_tile(acc[8], 4, hb);
+    // bias: lane (c, h) of wave 2 b + P holds plane P's partial of channel 32 b + c over rows of half h
+    __syncthreads();  // (every wave's last fragment reads are done)
+    float* red = reinterpret_cast<float*>(lds);
+    red[wave * 64 + lane] = bsum;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int b = threadIdx.x >> 5, c = threadIdx.x & 31;
+        const float th = red[(2 * b) * 64 + c] + red[(2 * b) * 64 + c + 32];
+        const float tl = red[(2 * b + 1) * 64 + c] + red[(2 * b + 1) * 64 + c + 32];
+        a.bslab[(long long)blockIdx.x * 64 + threadIdx.x] = (th + tl) * exp2i(-*a.g_exp);
+    }
+}
+
 int dconv_cus() {
     static int cus[64] = {};
     int dev = 0;
@@ -933,6 +1198,9 @@ int launch_dconv(const Args& a, const uint16_t* wq, hipStream_t s, const char* n
 
 #ifndef DFCD_DEFAULT
 #define DFCD_DEFAULT true  // the direct fc dgrad unless PPOX_DFCD says otherwise
+#endif
+#ifndef DWGRAD3_DEFAULT
+#define DWGRAD3_DEFAULT true  // the direct conv3 weight gradient unless PPOX_DWGRAD3 says otherwise
 #endif
 #ifndef DCONV_DEFAULT
 #define DCONV_DEFAULT true  // the direct forms unless PPOX_DCONV2 / PPOX_DCONV3 say otherwise
@@ -974,6 +1242,23 @@ int ddgrad2(const void* g2p, int64_t batch, const uint16_t* wqd2, float* g1, con
     const long long grid = std::min<long long>(batch, cus);
     ddgrad2_kernel<<<(unsigned)grid, 256, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd2));
     PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
+}
+
+// the conv3 weight gradient's direct form (PPOX_DWGRAD3=0: the im2col split form; _MIN: the smallest batch)
+bool dwgrad3_enabled(long long batch) { return env_on("PPOX_DWGRAD3", batch, DWGRAD3_DEFAULT); }
+long long dwgrad3_grid(long long batch) { return std::min<long long>(batch, dconv_cus()); }
+int dwgrad3(const void* h2p, const void* g3p, int64_t batch, const int* h_exp, const int* g_exp, float* slab,
+            float* bslab, hipStream_t s) {
+    const long long grid = dwgrad3_grid(batch);
+    PPOX_REQUIRE(grid > 0, "ppox_nature_conv_wgrad_split: no device");
+    PPOX_REQUIRE(ppox::aligned16(h2p) && ppox::aligned16(g3p) && h_exp && g_exp,
+                 "ppox_nature_conv_wgrad_split: the direct conv3 weight gradient needs 16B-aligned PX h2 / g3");
+    PPOX_REQUIRE(ppox::ceil_div((long long)batch, grid) * W3_HIMG < (1LL << 31),
+                 "ppox_nature_conv_wgrad_split: batch too large for the direct conv3 weight gradient");
+    W3PArgs a{reinterpret_cast<const uint8_t*>(h2p), reinterpret_cast<const uint8_t*>(g3p), h_exp, g_exp, slab, bslab,
+              batch};
+    dwgrad3_kernel<<<(unsigned)grid, 256, 0, s>>>(a);
+    PPOX_LAUNCHED("ppox_nature_conv_wgrad_split");
 }
 
 // the fc dgrad's direct form (PPOX_DFCD=1; _MIN: the smallest batch): df planes in, g3 planes out, h3's bitmask

@@ -44,6 +44,38 @@ def _is_image(space):
     return len(space.shape) == 3
 
 
+_TRAIN_PRIO = os.environ.get("PPOX_TRAIN_PRIO", "0") == "1"
+_prio_streams = {}
+
+
+class _train_stream:
+    """PPOX_TRAIN_PRIO=1: the update's main-stream work on a high-priority stream (the weight
+    gradients' side stream keeps the default priority), ordered after / before the caller's stream."""
+
+    def __init__(self, device):
+        self.on = _TRAIN_PRIO and device.type == "cuda"
+        self.device = device
+
+    def __enter__(self):
+        if not self.on:
+            return
+        s = _prio_streams.get(self.device)
+        if s is None:
+            s = _prio_streams[self.device] = torch.cuda.Stream(device=self.device, priority=-1)
+        self.prev = torch.cuda.current_stream(self.device)
+        s.wait_stream(self.prev)
+        self.ctx = torch.cuda.stream(s)
+        self.ctx.__enter__()
+
+    def __exit__(self, *exc):
+        if not self.on:
+            return False
+        s = torch.cuda.current_stream(self.device)
+        self.ctx.__exit__(*exc)
+        self.prev.wait_stream(s)
+        return False
+
+
 def icm_loss_sharded(icm, x, acts, pos, B, beta, ctx):
     """ICM loss of one GLOBAL minibatch whose rows are spread over ranks (ppo.py:684-692):
     pairs are consecutive rows of the permuted minibatch, (row j, row j+1), j < B-1,
@@ -588,6 +620,10 @@ class PPO(BaseAlgorithm):
 
     @traced("train")
     def train(self):
+        with _train_stream(self.device):
+            self._train()
+
+    def _train(self):
         ro = self.rollout
         total = self.nstep * self.num_envs
         self.loss_accum.zero_()

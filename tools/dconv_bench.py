@@ -1,6 +1,7 @@
 """Timing of the conv2 / conv3 forwards (H1P / h2 planes -> h2 / h3 planes), the direct form
 (csrc/dconv.hip) against the im2col sg2 GEMM (PPOX_DCONV2=0 / PPOX_DCONV3=0), and of the conv2 dgrad: the
-direct class-wise form on PX g2 (ddgrad2_kernel) against the col2im form on f32 g2 (dgrad2_colp_kernel);
+direct class-wise form on PX g2 (ddgrad2_kernel) against the col2im form on f32 g2 (dgrad2_colp_kernel),
+and of the conv3 weight gradient: direct (dwgrad3_kernel) against im2col (wgrad_split_kernel), slab reduce included;
 HIP events on the launch stream.  Usage: python tools/dconv_bench.py [B ...]"""
 import json
 import os
@@ -89,6 +90,24 @@ def main():
                    3, g3p, B, q3, None, g2, amax_g=ag[0], amax_out=ag[1], relu_bits=bits2, g_exp=e3)), 1),
                "px_out_us": round(1e3 * t_ms(lambda: native.nature_conv_dgrad_split(
                    3, g3p, B, q3, None, g2p, amax_g=ag[0], amax_out=ag[1], relu_bits=bits2, g_exp=e3, y_exp=e)), 1)}
+        print(json.dumps(row), flush=True)
+        # conv3 weight gradient on PX h2 and PX g3: the direct form against the im2col split form
+        h2p = torch.empty(B, 9, 9, 128, dtype=torch.int16, device="cuda")
+        eh = torch.zeros(1, dtype=torch.int32, device="cuda")
+        h2f = torch.relu(torch.randn(B, 9, 9, 64, device="cuda"))
+        native.amax(h2f, ag[1])
+        native.px_split(h2f, ag[1], h2p, eh)
+        ws = torch.empty(native.nature_wgrad_split_workspace_bytes(3, B), dtype=torch.uint8, device="cuda")
+        dw, db = torch.empty(64, 64, 3, 3, device="cuda"), torch.empty(64, device="cuda")
+        row = {"B": B, "op": "conv3 wgrad"}
+        for name, v in (("im2col", "0"), ("direct", "1")):
+            os.environ["PPOX_DWGRAD3"] = v
+            row[name + "_us"] = round(1e3 * t_ms(lambda: native.nature_conv_wgrad_split(
+                3, h2p, B, 0, g3p, ws, dw, db, x_exp=eh, g_exp=e3)), 1)
+            t = row[name + "_us"] * 1e-6
+            row[name + "_tbs"] = round(B * (81 + 49) * 256 / t / 1e12, 2)
+            row[name + "_tf"] = round(2 * 49 * 576 * 64 * B / t / 1e12, 1)
+        os.environ.pop("PPOX_DWGRAD3")
         print(json.dumps(row), flush=True)
 
 

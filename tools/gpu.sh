@@ -36,7 +36,7 @@ bench() {  # bench NAME OUTFILE ARGS...   (the step's VAR=value settings from $E
 
 trace() {  # trace NAME BACK ARGS... -> stats + timeline of the BACK-th minibatch from the end
   local name=$1 back=$2; shift 2
-  ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/$TAG-$name -o run --output-format csv -- \
+  ( cd /tmp && env $ENVS timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/$TAG-$name -o run --output-format csv -- \
       python3 $R/bench.py "$@" > $O/${name}_bench_under_rocprof.json 2> $O/$name.err ) || return 1
   local T=$(find /tmp/$TAG-$name -name "*kernel_trace.csv" | head -n 1)
   find /tmp/$TAG-$name -name "*kernel_stats.csv" -exec cp {} $O/${name}_kernel_stats.csv \; || return 1
@@ -85,9 +85,9 @@ for STEP in "$@"; do
     ID) bench ID $OUT --algo icm $RANK --steps 3 --warmup 1 --no-cpu-baseline --force-dist || exit 1 ;;
     C3) bench C3 $OUT --algo rnd --envs 1024 --steps 3 --warmup 1 --no-cpu-baseline || exit 1 ;;
     ES) bench ES $OUT --algo es --steps 3 --warmup 1 || exit 1 ;;
-    prof16k) trace prof16k 3 --steps 2 --warmup 1 --no-cpu-baseline || exit 1 ;;
-    profrank) trace profrank 3 $RANK --steps 2 --warmup 1 --no-cpu-baseline || exit 1 ;;
-    profrankD) trace profrankD 3 $RANK --steps 2 --warmup 1 --no-cpu-baseline --force-dist || exit 1 ;;
+    prof16k) trace $OUT 3 --steps 2 --warmup 1 --no-cpu-baseline || exit 1 ;;
+    profrank) trace $OUT 3 $RANK --steps 2 --warmup 1 --no-cpu-baseline || exit 1 ;;
+    profrankD) trace $OUT 3 $RANK --steps 2 --warmup 1 --no-cpu-baseline --force-dist || exit 1 ;;
     pmc16k) pmc pmc16k || exit 1 ;;
     pmcrank) pmc pmcrank $RANK || exit 1 ;;
     sq16k) $R/tools/kernel_pmc.sh $TAG/sq16k "$SQRX" bench.py --steps 1 --warmup 0 --epochs 1 --no-cpu-baseline || exit 1 ;;
