@@ -3605,6 +3605,9 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
         a.yexp_out = y_exp_out;
         a.ynorm = pack_norm(wqd, PL_Q3);
         a.ybias = pack_bmax(wqd, PL_Q3);
+        if (g_exp && ppox_conv::ddgrad3_enabled(batch))  // the direct form (dconv.hip)
+            return ppox_conv::ddgrad3(grad_out, batch, wqd, grad_in, amax_g, amax_out, relu_bits, g_exp, a.wexp, a.ynorm,
+                                      a.ybias, y_exp_out, s);
         const long long blocks = ppox::ceil_div(batch, SG_ROWS) * SgDgradPM<G3>::NPOS;
         if (g_exp) return launch_sgemm<Px<SgDgradPM<G3, true>, true, true>>(a, wqd, blocks, s, "ppox_nature_conv_dgrad_split");
         return launch_sgemm<Px<SgDgradPM<G3, true>, false, true>>(a, wqd, blocks, s, "ppox_nature_conv_dgrad_split");

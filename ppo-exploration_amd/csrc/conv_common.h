@@ -409,6 +409,11 @@ bool dfcd_enabled(long long batch);
 int dfcd(const void* dfp, int64_t batch, const uint16_t* wq, float* g3, const uint32_t* amax_df, uint32_t* amax_g3,
          const uint32_t* relu_bits, int* g3_exp_out, const int* df_exp, const int* wexp, const uint32_t* ynorm,
          const uint32_t* ybias, hipStream_t s);
+// the conv3 dgrad on PX g3 -> PX g2 (conv2's ReLU bitmask applied), the direct form (dconv.hip)
+bool ddgrad3_enabled(long long batch);
+int ddgrad3(const void* g3p, int64_t batch, const uint16_t* wqd3, void* g2p, const uint32_t* amax_g3,
+            uint32_t* amax_g2, const uint32_t* relu_bits, const int* g_exp, const int* wexp, const uint32_t* ynorm,
+            const uint32_t* ybias, int* y_exp_out, hipStream_t s);
 // the conv3 weight gradient on PX h2 and PX g3, the direct form (dconv.hip): per-workgroup partial slabs
 // [grid][576][64] and bias slabs [grid][64], summed by the caller's wgrad_reduce; grid = dwgrad3_grid(batch)
 bool dwgrad3_enabled(long long batch);

@@ -897,6 +897,264 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
 }
 
 // ---------------------------------------------------------------------------
+// The conv3 dgrad in the direct form (round 5): g2 = (h2 > 0) * conv3^T(g3), PX g3 in, PX g2 out,
+// .ipynb_checkpoints/models-checkpoint.py:57 backward (reached through ppo.py:241).  An h2 pixel
+// (iy, ix) takes tap (ky, kx) from the g3 pixel (iy - ky, ix - kx) when that lies on the 7 x 7 image — an
+// implicit GEMM with rows = the 81 h2 pixels of each sample, K = 9 taps x 64 channels of g3, N = the 64
+// input channels: every output written once, no col2im.  As dconv_fwd_kernel<DcF3>:
+//   * wave w holds the 72 weight fragments of column tile j = w & 1 (the qd3 packing, 240 AGPRs + 48
+//     VGPRs) and computes row block w >> 1 of each 64-row phase;
+//   * whole g3 sample images (PX planes, 49 pixels x 256 B) and conv2's ReLU bitmask of the sample (81 x 2
+//     words) stream into an LDS ring by LDS-DMA (buffer loads: the image's tail past pixel 48 reads zeros);
+//   * the image's 16-B pieces are stored at p ^ key, key = (n + 9 y + x) & 15 (81 = 1 mod 16), so a row
+//     m = 81 n + 9 iy + ix reads tap (ky, kx) at key (m - 9 ky - kx) & 15: the 16 rows of a lane group
+//     hit 16 distinct bank quads; a tap off the image reads a zero pixel at the same piece positions.
+// The taps off the image cost MFMAs (729 tap-rows per sample for 441 real, 1.65x) — the price of K = 576
+// in registers and one pass over each g3 image; the im2col sgemm (SgDgradPM) walks only the real taps but
+// stages 442 KB per 128-row tile through LDS.  fp32-class; its k order is not the sgemm's, so it is held
+// to the fp64 bounds (tests/test_ddgrad3_gpu.py).
+typedef unsigned int w3u2 __attribute__((ext_vector_type(2)));
+constexpr int DD3_IMG = 49 * 256, DD3_IMG_DMAS = (DD3_IMG + 1023) / 1024;  // 13
+constexpr int DD3_MASKB = 81 * 8, DD3_MASK0 = DD3_IMG_DMAS * 1024;
+constexpr int DD3_REAL_DMAS = DD3_IMG_DMAS + 1, DD3_SLOT = DD3_REAL_DMAS * 1024, DD3_DMAS = 4;
+constexpr int DD3_NSLOT = 6, DD3_ZERO = DD3_NSLOT * DD3_SLOT, DD3_LDS = DD3_ZERO + 256;
+static_assert(DD3_LDS <= 160 * 1024 && DD3_REAL_DMAS <= 4 * DD3_DMAS, "ddgrad3: LDS / DMAs");
+
+__global__ void __launch_bounds__(256, 1) ddgrad3_kernel(Args a, const u32x4* __restrict__ wq) {
+    constexpr int NK = 36, NA = 60;  // k-steps (9 taps x 4 channel quarters); weight fragments in AGPRs
+    constexpr int P2 = 81;           // output rows per sample
+    __shared__ __attribute__((aligned(16))) uint8_t lds[DD3_LDS];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int j = wave & 1, rg = wave >> 1;
+    const int r = lane & 31, h = lane >> 5;
+    const long long S0 = blockIdx.x * a.batch / gridDim.x, S1 = (blockIdx.x + 1) * a.batch / gridDim.x;
+    const int NS = (int)(S1 - S0);
+    if (NS <= 0) return;
+    const int MR = NS * P2, F_ = (MR + 63) / 64;
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
+
+    // DMA d = wave + 4 i: d < 13 image bytes [1024 d, + 1024) (lane -> LDS pixel u, piece position lane & 15
+    // holding global piece (lane & 15) ^ key; pixels past 48: zeros), d = 13 the bitmask words (past them:
+    // the next sample's, into the slot's pad), d > 13 the 14th again
+    uint32_t doff[DD3_DMAS], dkey[DD3_DMAS];
+#pragma unroll
+    for (int i = 0; i < DD3_DMAS; ++i) {
+        int d = wave + 4 * i;
+        d = d < DD3_REAL_DMAS ? d : DD3_REAL_DMAS - 1;
+        const int u = (d * 1024 + lane * 16) / 256;
+        const int mo = lane * 16 < DD3_MASKB ? lane * 16 : DD3_MASKB - 8;
+        doff[i] = d < DD3_IMG_DMAS ? (u < 49 ? (uint32_t)(u * 256) : 0x80000000u) : (uint32_t)mo;
+        dkey[i] = (uint32_t)((9 * (u / 7) + u % 7) & 15);
+    }
+    const uint8_t* gb = reinterpret_cast<const uint8_t*>(a.x) + S0 * DD3_IMG;
+    const uint8_t* mb = reinterpret_cast<const uint8_t*>(a.bits_mask) + S0 * DD3_MASKB;
+    const auto g_rs = __builtin_amdgcn_make_buffer_rsrc((void*)gb, 0, NS * DD3_IMG, 0x00020000);
+    const auto m_rs = __builtin_amdgcn_make_buffer_rsrc((void*)mb, 0, NS * DD3_MASKB, 0x00020000);
+    auto issue_one = [&](int n, auto I) {
+        constexpr int i = decltype(I)::value;
+        int d = wave + 4 * i;
+        d = d < DD3_REAL_DMAS ? d : DD3_REAL_DMAS - 1;
+        auto* dst = (__attribute__((address_space(3))) void*)(lds + (n % DD3_NSLOT) * DD3_SLOT + d * 1024);
+        const uint32_t key = (uint32_t)(n + dkey[i]) & 15u;
+        if (d < DD3_IMG_DMAS)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(g_rs, dst, 16, doff[i] + ((((uint32_t)lane & 15u) ^ key) << 4),
+                                                     n * DD3_IMG, 0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(m_rs, dst, 16, doff[i], n * DD3_MASKB, 0, 0);
+    };
+    auto issue_sample = [&](int n) {
+        dc_unroll([&](auto I) { issue_one(n, I); }, std::make_integer_sequence<int, DD3_DMAS>{});
+    };
+    int issued = NS < DD3_NSLOT ? NS : DD3_NSLOT;
+    for (int n = 0; n < issued; ++n) issue_sample(n);
+    // the weights of column tile j: k-step i = 2 c + s (chunk c: tap c >> 1, channel half c & 1), planes p
+    u32x4 bq[NK / 2][2][2];
+#pragma unroll
+    for (int c = 0; c < NK / 2; ++c)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) bq[c][s][p] = wq[((((c * 2 + s) * 2 + j) * 2 + p) * 64) + lane];
+    const int ex = *a.xexp, ew = *a.wexp;
+    const uint32_t am = amax_read(a.amax_x), nm = amax_read(a.ynorm), bm = *a.ybias;
+    const int ey = bound_exp(am, nm, bm);
+    const float bnd = __uint_as_float(am) * __uint_as_float(nm) + __uint_as_float(bm);
+    const float sy = __builtin_isfinite(bnd) ? exp2i(ey) : __builtin_nanf("");
+    const float us = exp2i(-ex) * (exp2i(-ew) * sy);  // accumulators -> the output's scaled domain (exact)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.yexp_out = ey;
+    if (threadIdx.x < 16) reinterpret_cast<u32x4*>(lds + DD3_ZERO)[threadIdx.x] = u32x4{0u, 0u, 0u, 0u};
+
+    // a lane's row: (n, iy, ix) of range row m, advanced by 64 rows per phase without divisions
+    struct Pos {
+        int m, n, iy, ix;
+    };
+    Pos Q;
+    {
+        Q.m = 32 * rg + r;
+        Q.n = Q.m / P2;
+        const int rem = Q.m - Q.n * P2;
+        Q.iy = rem / 9;
+        Q.ix = rem - 9 * Q.iy;
+    }
+    auto advance = [&](Pos& P) {  // + 64 rows = + 7 image rows and 1 column
+        P.m += 64;
+        P.ix += 1;
+        const bool cx = P.ix >= 9;
+        P.ix -= cx ? 9 : 0;
+        P.iy += 7 + (cx ? 1 : 0);
+        const bool cy = P.iy >= 9;
+        P.iy -= cy ? 9 : 0;
+        P.n += cy ? 1 : 0;
+    };
+    // per-lane setup of a phase: each tap's read pixel base | (key ^ h) << 4 (off the image: the zero pixel),
+    // the output pixel's byte offset in the range's g2 planes, its bitmask word's LDS address
+    struct Rows {
+        uint32_t tb[9];
+        uint32_t ma;
+    };
+    auto rows = [&](const Pos& P) {
+        Rows R;
+        const bool live = P.m < MR;
+        const int n = live ? P.n : NS - 1, iy = live ? P.iy : 8, ix = live ? P.ix : 8;
+        const uint32_t sbase = lds0 + (uint32_t)((n % DD3_NSLOT) * DD3_SLOT);
+        const int mkey = n + 9 * iy + ix;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int ky = t / 3, kx = t % 3, y = iy - ky, x = ix - kx;
+            const bool ok = y >= 0 && y <= 6 && x >= 0 && x <= 6;
+            const uint32_t key = ((uint32_t)(mkey - 9 * ky - kx) & 15u) ^ (uint32_t)h;
+            R.tb[t] = (ok ? sbase + (uint32_t)((7 * y + x) * 256) : lds0 + DD3_ZERO) | (key << 4);
+        }
+        R.ma = sbase + DD3_MASK0 + (uint32_t)((9 * iy + ix) * 8 + 4 * j);
+        return R;
+    };
+    Rows RW = rows(Q);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    asm volatile("s_nop 4" ::: "memory");  // (VALU-written B registers before the first MFMA reads them)
+
+    const auto o_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(reinterpret_cast<uint8_t*>(a.y) + S0 * (P2 * 256)), 0,
+                                                        NS * (P2 * 256), 0x00020000);
+    const uint32_t ylane = (uint32_t)(128 * j + 8 * h);
+    uint32_t om = 0u;
+    f32x16 H0, L0, H1, L1;
+    int po = 0x7FFFFF00;  // the previous phase's output byte offset (dead rows: past the end) and mask word
+    uint32_t pmw = 0u;
+    // epilogue group t of the previous phase: channels 32 j + 8 t + 4 h + k of the lane's pixel, times conv2's
+    // ReLU bit; the planes' two 8-B runs (a dead row's offset is past the end: the store is dropped)
+    auto epi = [&](auto T, const f32x16& PH, const f32x16& PL) {
+        constexpr int t = decltype(T)::value;
+        float y[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t mk;
+            asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(mk) : "v"(pmw), "n"(8 * t + k));
+            y[k] = __uint_as_float(__float_as_uint((PH[4 * t + k] + PL[4 * t + k]) * us) & mk);
+        }
+        uint32_t hw[2], lw[2];
+        split2h((f32x2){y[0], y[1]}, 1.f, hw[0], lw[0]);
+        split2h((f32x2){y[2], y[3]}, 1.f, hw[1], lw[1]);
+        const uint32_t o = (uint32_t)po + ylane + 16 * t;
+        __builtin_amdgcn_raw_buffer_store_b64((w3u2){hw[0], hw[1]}, o_rs, o, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64((w3u2){lw[0], lw[1]}, o_rs, o + 64, 0, 0);
+        om = max(om, max(max(__float_as_uint(y[0]) & 0x7FFFFFFFu, __float_as_uint(y[1]) & 0x7FFFFFFFu),
+                         max(__float_as_uint(y[2]) & 0x7FFFFFFFu, __float_as_uint(y[3]) & 0x7FFFFFFFu)));
+    };
+    constexpr int NDMA = DD3_DMAS;  // refill: at most one sample per phase (64 rows < 81), from k-step 16
+
+    auto phase = [&](int f, f32x16& H, f32x16& Lo, const f32x16& PH, const f32x16& PL, auto PREV) {
+        const int m0 = 64 * f;
+        const int nlo = m0 / P2, nhi = min((m0 + 63) / P2, NS - 1);
+        dc_vm_wait<DD3_DMAS>(issued - 1 - nhi);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const int rA = issued, nref = min(nlo + DD3_NSLOT, NS) - issued;
+        issued += nref;
+        const int live = Q.m < MR;
+        const int orow = live ? Q.m * 256 : 0x7FFFFF00;
+        uint32_t mw;
+        asm volatile("ds_read_b32 %0, %1" : "=v"(mw) : "v"(RW.ma));
+        // k-step i = 2 c + s, plane pl: piece 8 (c & 1) + 4 pl + 2 s + h of tap c >> 1's pixel
+        auto addr = [&](int i, int pl) {
+            const int c = i >> 1, s = i & 1;
+            return RW.tb[c >> 1] ^ ((uint32_t)(8 * (c & 1) + 4 * pl + 2 * s) << 4);
+        };
+        constexpr int PD = DC_PD, NB = PD + 1;
+        u32x4 fa[NB][2];
+        auto rd1 = [&](auto I, auto PLc) {
+            constexpr int i = decltype(I)::value, pl = decltype(PLc)::value;
+            fa[i % NB][pl] = dc_read<0>(addr(i, pl));
+        };
+        using Z = std::integral_constant<int, 0>;
+        using O = std::integral_constant<int, 1>;
+        dc_unroll([&](auto I) { rd1(I, Z{}); rd1(I, O{}); }, std::make_integer_sequence<int, PD>{});
+        asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(mw) : "n"(2 * (PD - 1)));
+        Pos QN = Q;
+        Rows RN;  // the next phase's setup, in this phase's gaps
+        dc_unroll(
+            [&](auto I) {
+                constexpr int i = decltype(I)::value;
+                constexpr int fb = (i >> 1) * 4 + (i & 1) * 2;
+                constexpr bool A0 = fb < NA, A1 = fb + 1 < NA;
+                const u32x4& b0 = bq[i >> 1][i & 1][0];
+                const u32x4& b1 = bq[i >> 1][i & 1][1];
+                constexpr bool P = decltype(PREV)::value;
+                if constexpr (i == 0)
+                    dc_mfma0<A0>(H, fa[0][0], b0);
+                else
+                    dc_mfma<A0>(H, fa[i % NB][0], b0);
+                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, Z{});
+                if constexpr (i == 0)
+                    dc_mfma0<A1>(Lo, fa[0][0], b1);
+                else
+                    dc_mfma<A1>(Lo, fa[i % NB][0], b1);
+                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, O{});
+                // the previous phase's epilogue at k-steps 1, 3, 5, 7 — early, so its stores complete before
+                // the next phase's vmcnt wait (gfx9: one counter for loads and stores)
+                if constexpr (P && (i & 1) && i < 8) epi(std::integral_constant<int, i / 2>{}, PH, PL);
+                dc_mfma<A0>(Lo, fa[i % NB][1], b0);
+                if constexpr (i == 10) {
+                    advance(QN);
+                }
+                if constexpr (i == 12) RN = rows(QN);
+                dc_unroll(
+                    [&](auto X) {
+                        constexpr int x = decltype(X)::value;
+                        if constexpr (16 + x * 4 == i) {
+                            if (nref > 0) issue_one(rA, std::integral_constant<int, x>{});
+                        }
+                    },
+                    std::make_integer_sequence<int, NDMA>{});
+                constexpr int later = (i + PD < NK ? i + PD : NK - 1) - (i + 1);
+                if constexpr (i + 1 < NK) dc_lgkm<2 * later>(fa[(i + 1) % NB][0], fa[(i + 1) % NB][1]);
+            },
+            std::make_integer_sequence<int, NK>{});
+        for (int t = 1; t < nref; ++t) issue_sample(rA + t);  // (only phase 0 could: the prologue issued those)
+        po = orow;
+        pmw = mw >> (4 * h);
+        Q = QN;
+        RW = RN;
+        dc_acc_fence(H, Lo);
+    };
+    auto final_epi = [&](const f32x16& PH, const f32x16& PL) {
+        dc_unroll([&](auto T) { epi(T, PH, PL); }, std::make_integer_sequence<int, 4>{});
+    };
+    phase(0, H0, L0, H1, L1, std::false_type{});
+    int f = 1;
+#pragma unroll 1
+    for (; f + 1 < F_; f += 2) {
+        phase(f, H1, L1, H0, L0, std::true_type{});
+        phase(f + 1, H0, L0, H1, L1, std::true_type{});
+    }
+    if (f < F_) phase(f, H1, L1, H0, L0, std::true_type{});
+    if ((F_ - 1) & 1)
+        final_epi(H1, L1);
+    else
+        final_epi(H0, L0);
+    amax_record(a.amax_y, __uint_as_float(om) * exp2i(-ey));
+}
+
+// ---------------------------------------------------------------------------
 // conv3 weight gradient, direct (round 5; models-checkpoint.py:57 Conv2d(64, 64, 3) trained by ppo.py:241):
 //   dW3[co][ci][ky][kx] = sum over samples n and output pixels p = (oy, ox) of h2[n][oy + ky][ox + kx][ci] g3[n][p][co]
 //   db3[co]             = sum g3[n][p][co]
@@ -940,7 +1198,6 @@ struct W3PArgs {
     long long batch;
 };
 
-typedef unsigned int w3u2 __attribute__((ext_vector_type(2)));
 template <int OFF>
 __device__ inline w3u2 w3_tr(uint32_t addr) {  // (asm: hipcc would wait for the ring's DMAs before a plain read)
     w3u2 r;
@@ -1170,13 +1427,13 @@ int dconv_cus() {
     return cus[dev];
 }
 
-bool env_on(const char* name, long long batch, bool dflt) {
+bool env_on(const char* name, long long batch, bool dflt, long long dflt_min = 1) {
     const char* e = std::getenv(name);
     if (!(e ? e[0] != '0' : dflt)) return false;
     char mn[64];
     snprintf(mn, sizeof mn, "%s_MIN", name);
     const char* m = std::getenv(mn);
-    return batch >= (m ? std::atoll(m) : 1);
+    return batch >= (m ? std::atoll(m) : dflt_min);
 }
 
 template <class F>
@@ -1198,6 +1455,12 @@ int launch_dconv(const Args& a, const uint16_t* wq, hipStream_t s, const char* n
 
 #ifndef DFCD_DEFAULT
 #define DFCD_DEFAULT true  // the direct fc dgrad unless PPOX_DFCD says otherwise
+#endif
+#ifndef DDGRAD3_DEFAULT
+#define DDGRAD3_DEFAULT true  // the direct conv3 dgrad (PX g3 -> PX g2) unless PPOX_DDGRAD3 says otherwise
+#endif
+#ifndef DDGRAD3_MIN
+#define DDGRAD3_MIN 4096
 #endif
 #ifndef DWGRAD3_DEFAULT
 #define DWGRAD3_DEFAULT true  // the direct conv3 weight gradient unless PPOX_DWGRAD3 says otherwise
@@ -1241,6 +1504,34 @@ int ddgrad2(const void* g2p, int64_t batch, const uint16_t* wqd2, float* g1, con
     a.xexp = g_exp;
     const long long grid = std::min<long long>(batch, cus);
     ddgrad2_kernel<<<(unsigned)grid, 256, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd2));
+    PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
+}
+
+// the conv3 dgrad's direct form on PX g3 -> PX g2 (PPOX_DDGRAD3=0: the im2col sgemm; _MIN: the smallest
+// batch); `a` carries the PX g2 arguments the sgemm form takes (x, xexp, wexp, amax_x, ynorm, ybias, y,
+// yexp_out, amax_y, bits_mask)
+// (from 4,096 rows: at the 8-GPU per-rank minibatch of 2,048 it measured 205.6 vs 199.9 ms per iteration
+// against the sgemm, the persistent direct kernels of both streams taking whole CUs in turn)
+bool ddgrad3_enabled(long long batch) { return env_on("PPOX_DDGRAD3", batch, DDGRAD3_DEFAULT, DDGRAD3_MIN); }
+int ddgrad3(const void* g3p, int64_t batch, const uint16_t* wqd3, void* g2p, const uint32_t* amax_g3,
+            uint32_t* amax_g2, const uint32_t* relu_bits, const int* g_exp, const int* wexp, const uint32_t* ynorm,
+            const uint32_t* ybias, int* y_exp_out, hipStream_t s) {
+    const int cus = dconv_cus();
+    PPOX_REQUIRE(cus > 0, "ppox_nature_conv_dgrad_split: no device");
+    PPOX_REQUIRE(ppox::aligned16(g3p) && ppox::aligned16(g2p) && relu_bits && g_exp && wexp && y_exp_out && amax_g3 &&
+                     ynorm && ybias,
+                 "ppox_nature_conv_dgrad_split: the direct conv3 dgrad needs PX g3 / g2 and the bound's operands");
+    PPOX_REQUIRE(ppox::ceil_div((long long)batch, (long long)cus) * 81 * 256 < (1LL << 31),
+                 "ppox_nature_conv_dgrad_split: batch too large for the direct conv3 dgrad");
+    Args a{g3p, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, reinterpret_cast<float*>(g2p), batch, amax_g3, amax_g2,
+           wexp};
+    a.bits_mask = relu_bits;
+    a.xexp = g_exp;
+    a.yexp_out = y_exp_out;
+    a.ynorm = ynorm;
+    a.ybias = ybias;
+    const long long grid = std::min<long long>(batch, cus);
+    ddgrad3_kernel<<<(unsigned)grid, 256, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd3));
     PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
 }
 

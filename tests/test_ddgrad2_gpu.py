@@ -84,6 +84,7 @@ def test_conv3_dgrad_px_output_is_the_split_of_f32(B):
     native.nature_conv_dgrad_split(3, g3, B, q[13], None, y32, amax_g=am[0], relu_bits=bits2)
     yp = torch.full((B, 9, 9, 128), -1, dtype=torch.int16, device="cuda")
     e = torch.zeros(1, dtype=torch.int32, device="cuda")
+    # (f32 g3: the sgemm form; the direct form on PX g3 is tests/test_ddgrad3_gpu.py's)
     native.nature_conv_dgrad_split(3, g3, B, q[13], None, yp, amax_g=am[0], amax_out=am[1], relu_bits=bits2, y_exp=e)
     torch.cuda.synchronize()
     E = int(e.item())

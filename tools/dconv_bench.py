@@ -80,6 +80,7 @@ def main():
         # conv3 dgrad on g3 planes: f32 g2 out against PX g2 out (the planes the direct conv2 dgrad reads)
         g3 = torch.randn(B, 7, 7, 64, device="cuda")
         native.amax(g3, ag[0])
+        os.environ["PPOX_DDGRAD3_MIN"] = "1"  # (the direct conv3 dgrad at every batch: px_out_us)
         g3p = torch.empty(B, 7, 7, 128, dtype=torch.int16, device="cuda")
         e3 = torch.zeros(1, dtype=torch.int32, device="cuda")
         native.px_split(g3, ag[0], g3p, e3)
@@ -90,6 +91,10 @@ def main():
                    3, g3p, B, q3, None, g2, amax_g=ag[0], amax_out=ag[1], relu_bits=bits2, g_exp=e3)), 1),
                "px_out_us": round(1e3 * t_ms(lambda: native.nature_conv_dgrad_split(
                    3, g3p, B, q3, None, g2p, amax_g=ag[0], amax_out=ag[1], relu_bits=bits2, g_exp=e3, y_exp=e)), 1)}
+        os.environ["PPOX_DDGRAD3"] = "0"  # the im2col sgemm with the PX output
+        row["px_out_sgemm_us"] = round(1e3 * t_ms(lambda: native.nature_conv_dgrad_split(
+            3, g3p, B, q3, None, g2p, amax_g=ag[0], amax_out=ag[1], relu_bits=bits2, g_exp=e3, y_exp=e)), 1)
+        os.environ.pop("PPOX_DDGRAD3")
         print(json.dumps(row), flush=True)
         # conv3 weight gradient on PX h2 and PX g3: the direct form against the im2col split form
         h2p = torch.empty(B, 9, 9, 128, dtype=torch.int16, device="cuda")
