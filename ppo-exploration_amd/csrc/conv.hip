@@ -3915,6 +3915,8 @@ extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t
     Args a{h3, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, amax_h3, amax_f, pack_exp(q_fwd, PL_FCF)};
     a.xexp = h3_exp;  // PX h3 (the conv3 forward's planes output)
     const long long blocks = ppox::ceil_div(batch, SG_ROWS) * (512 / SG_FC_NB);
+    if (h3_exp && ppox_conv::fcw_enabled(batch))  // the wide-tile form (dconv.hip)
+        return ppox_conv::fcw(h3, batch, q_fwd, bias, f, amax_f, h3_exp, a.wexp, ppox::as_stream(stream));
     if (h3_exp)
         return launch_sgemm<Px<SgRows<3136, 512, FC_FWD, FC_FWD_GW, false, SG_FC_NB>, true>>(
             a, q_fwd, blocks, ppox::as_stream(stream), "ppox_nature_fc_fwd");

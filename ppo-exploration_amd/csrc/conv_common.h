@@ -409,6 +409,10 @@ bool dfcd_enabled(long long batch);
 int dfcd(const void* dfp, int64_t batch, const uint16_t* wq, float* g3, const uint32_t* amax_df, uint32_t* amax_g3,
          const uint32_t* relu_bits, int* g3_exp_out, const int* df_exp, const int* wexp, const uint32_t* ynorm,
          const uint32_t* ybias, hipStream_t s);
+// the fc forward on PX h3 in 256 x 128 tiles (dconv.hip)
+bool fcw_enabled(long long batch);
+int fcw(const void* h3p, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f, uint32_t* amax_f,
+        const int* h3_exp, const int* wexp, hipStream_t s);
 // the conv3 dgrad on PX g3 -> PX g2 (conv2's ReLU bitmask applied), the direct form (dconv.hip)
 bool ddgrad3_enabled(long long batch);
 int ddgrad3(const void* g3p, int64_t batch, const uint16_t* wqd3, void* g2p, const uint32_t* amax_g3,

@@ -897,6 +897,166 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
 }
 
 // ---------------------------------------------------------------------------
+// The fc forward on PX h3 in wide tiles (round 5): f = relu(h3 W^T + b), .ipynb_checkpoints/
+// models-checkpoint.py:58-59 (Linear(3136, 512) + ReLU).  The sg2 GEMM's 128 x 64 tiles stage 2.4 MB
+// of A and B through L2 -> LDS per tile (9.6 MB per CU at 16,384 rows), which bounds it at the ~70 GB/s
+// per CU that path sustains; a 256 x 128 tile stages 4.8 MB for the same MFMA work per CU (one tile per CU
+// at 16,384 rows: 64 row tiles x 4 column groups).  8 waves (two per SIMD): wave w owns rows 64 (w >> 1)
+// .. + 63 and columns 64 (w & 1) .. + 63 of the tile — 2 x 2 tiles of 32 x 32 with the sg2 form's hi / lo
+// accumulator pair (one accumulator for all three products measured 2.5x the f32 GEMM's error at K = 3136),
+// 8 fragment reads and 12 MFMAs per k-step.  Per 32-k chunk
+// the 256 A rows (PX: 32 hi + 32 lo f16, 128 B, pieces XOR-swizzled by (row >> 1) & 7 as the sg2 kernel)
+// and the two 64-column packed B blocks (16 KB) are LDS-DMA'd into a 3-slot ring, each wave its own 32
+// rows and two B pieces.  The four column groups of a row tile run on one XCD (xcd_remap): A is read
+// from HBM about once, B about once per XCD.  fp32-class; the k order is the sg2 form's but not its 64-column
+// tiles' instruction interleave, so it is held to the fp64 bound (tests/test_fcw_gpu.py).
+constexpr int FCW_ROWS = 256, FCW_KC = 3136 / 32, FCW_ROWB = 3136 * 4;  // rows per tile, chunks, PX row bytes
+constexpr int FCW_BQ = 2 * 2 * 2 * 64;                                  // u32x4 per 64-column B block chunk
+constexpr int FCW_AB = FCW_ROWS * 128, FCW_SLOT = FCW_AB + 2 * FCW_BQ * 16, FCW_NSLOT = 3;
+constexpr int FCW_LDS = FCW_NSLOT * FCW_SLOT;  // 147,456 B
+static_assert(FCW_LDS <= 160 * 1024, "fcw: LDS");
+
+template <int N>
+__device__ inline void fcw_lgkm(u32x4 (&x)[8], u32x4 (&y)[8]) {
+    asm volatile("s_waitcnt lgkmcnt(%16)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+                   "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]), "+v"(y[7])
+                 : "n"(N));
+}
+template <int N>
+__device__ inline void sg_vm_wait_n() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__global__ void __launch_bounds__(512, 1) fcw_kernel(Args a, const u32x4* __restrict__ wq) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[FCW_LDS];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long L = xcd_remap(blockIdx.x, gridDim.x);
+    const int cg = (int)(L & 3);
+    const long long m0 = (L >> 2) * FCW_ROWS, M = a.batch;
+    const int rg = wave >> 1, ch = wave & 1;
+    const int r = lane & 31, h = lane >> 5;
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
+
+    // DMA sources: A instruction j of this wave: row 32 w + 8 j + (lane >> 3) (past the batch: the last row,
+    // never stored), LDS piece lane & 7 <- global piece (lane & 7) ^ ((row >> 1) & 7); B pieces 2 w, 2 w + 1
+    // of the chunk's 16 (block 2 cg + (piece >> 3), 1-KB piece piece & 7 of its 8 KB)
+    const uint8_t* asrc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = 32 * wave + 8 * j + (lane >> 3);
+        long long m = m0 + row;
+        m = m < M ? m : M - 1;
+        asrc[j] = reinterpret_cast<const uint8_t*>(a.x) + m * FCW_ROWB + ((((lane & 7) ^ ((row >> 1) & 7))) << 4);
+    }
+    const u32x4* bsrc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int q = 2 * wave + i;
+        bsrc[i] = wq + (long long)(2 * cg + (q >> 3)) * FCW_KC * FCW_BQ + (q & 7) * 64 + lane;
+    }
+    auto issue = [&](int c, auto S) {
+        constexpr int slot = decltype(S)::value;
+        c = c < FCW_KC ? c : FCW_KC - 1;  // past the end: the last chunk again, never read
+        uint8_t* base = lds + slot * FCW_SLOT;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(asrc[j] + c * 128),
+                                             (__attribute__((address_space(3))) void*)(base + (wave * 32 + 8 * j) * 128),
+                                             16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(bsrc[i] + c * FCW_BQ),
+                                             (__attribute__((address_space(3))) void*)(base + FCW_AB + (2 * wave + i) * 1024),
+                                             16, 0, 0);
+    };
+    const int ex = *a.xexp, ew = *a.wexp;
+    const float us = exp2i(-ex) * exp2i(-ew);
+
+    f32x16 acc[2][2], acl[2][2];  // hi products / the two cross products (the sg2 form's pair)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[i][t] = acl[i][t] = zero16();
+    const uint32_t sw = (uint32_t)((r >> 1) & 7);
+    const uint32_t a_lane = lds0 + (uint32_t)((64 * rg + r) * 128), b_lane = lds0 + FCW_AB + ch * (FCW_BQ * 16) + lane * 16;
+    // chunk in slot S: both k-steps' 16 fragment reads up front, k-step 0's MFMAs once its 8 landed
+    auto compute = [&](auto S) {
+        constexpr int slot = decltype(S)::value;
+        u32x4 f[2][8];  // [k-step][A (row tile i, plane p) 0..3 | B (column tile t, plane p) 4..7]
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+                    f[s][2 * i + p] = dc_read<0>(a_lane + slot * FCW_SLOT + i * 32 * 128 +
+                                                 ((((uint32_t)(4 * p + 2 * s + h)) ^ sw) << 4));
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+                    f[s][4 + 2 * t + p] = dc_read<0>(b_lane + slot * FCW_SLOT + (((s * 2 + t) * 2 + p) * 64) * 16);
+        }
+        auto mm = [&](const u32x4 (&g)[8]) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) acc[i][t] = mfma_f16(g[2 * i], g[4 + 2 * t], acc[i][t]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) acl[i][t] = mfma_f16(g[2 * i], g[4 + 2 * t + 1], acl[i][t]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) acl[i][t] = mfma_f16(g[2 * i + 1], g[4 + 2 * t], acl[i][t]);
+        };
+        fcw_lgkm<8>(f[0], f[1]);
+        mm(f[0]);
+        fcw_lgkm<0>(f[0], f[1]);
+        mm(f[1]);
+    };
+    auto step = [&](int c, auto S, auto S2) {
+        sg_vm_wait_n<6>();  // this wave's DMAs of chunk c landed (chunk c + 1's may be in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        issue(c + 2, S2);
+        compute(S);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    issue(0, I0{});
+    issue(1, I1{});
+#pragma unroll 1
+    for (int c = 0; c < FCW_KC; c += 3) {  // (98 = 3 x 32 + 2)
+        step(c, I0{}, I2{});
+        if (c + 1 < FCW_KC) step(c + 1, I1{}, I0{});
+        if (c + 2 < FCW_KC) step(c + 2, I2{}, I1{});
+    }
+    sg_vm_wait_n<0>();  // the clamped tail DMAs, before the LDS is released
+    float om = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int n = 128 * cg + 64 * ch + 32 * t + r;
+        const float b = a.bias[n];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const long long m = m0 + 64 * rg + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+                const float v = fmaxf((acc[i][t][q] + acl[i][t][q]) * us + b, 0.f);
+                if (m < M) {
+                    a.y[m * 512 + n] = v;
+                    om = fmaxf(om, v);
+                }
+            }
+    }
+    amax_record(a.amax_y, om);
+}
+
+// ---------------------------------------------------------------------------
 // The conv3 dgrad in the direct form (round 5): g2 = (h2 > 0) * conv3^T(g3), PX g3 in, PX g2 out,
 // .ipynb_checkpoints/models-checkpoint.py:57 backward (reached through ppo.py:241).  An h2 pixel
 // (iy, ix) takes tap (ky, kx) from the g3 pixel (iy - ky, ix - kx) when that lies on the 7 x 7 image — an
@@ -1459,6 +1619,12 @@ int launch_dconv(const Args& a, const uint16_t* wq, hipStream_t s, const char* n
 #ifndef DDGRAD3_DEFAULT
 #define DDGRAD3_DEFAULT true  // the direct conv3 dgrad (PX g3 -> PX g2) unless PPOX_DDGRAD3 says otherwise
 #endif
+#ifndef FCW_DEFAULT
+#define FCW_DEFAULT true
+#endif
+#ifndef FCW_MIN
+#define FCW_MIN 8192
+#endif
 #ifndef DDGRAD3_MIN
 #define DDGRAD3_MIN 4096
 #endif
@@ -1505,6 +1671,20 @@ int ddgrad2(const void* g2p, int64_t batch, const uint16_t* wqd2, float* g1, con
     const long long grid = std::min<long long>(batch, cus);
     ddgrad2_kernel<<<(unsigned)grid, 256, 0, s>>>(a, reinterpret_cast<const u32x4*>(wqd2));
     PPOX_LAUNCHED("ppox_nature_conv_dgrad_split");
+}
+
+// the fc forward on PX h3 in 256 x 128 tiles (PPOX_FCW=0: the sg2 GEMM; _MIN: the smallest batch, default
+// 8192: one tile per CU needs 16,384 rows, and below ~8,192 the split-K form fills the chip)
+bool fcw_enabled(long long batch) { return env_on("PPOX_FCW", batch, FCW_DEFAULT, FCW_MIN); }
+int fcw(const void* h3p, int64_t batch, const uint16_t* q_fwd, const float* bias, float* f, uint32_t* amax_f,
+        const int* h3_exp, const int* wexp, hipStream_t s) {
+    PPOX_REQUIRE(ppox::aligned16(h3p) && ppox::aligned16(q_fwd) && bias && f && h3_exp && wexp,
+                 "ppox_nature_fc_fwd: the wide form needs PX h3 (16B-aligned)");
+    Args a{h3p, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, nullptr, amax_f, wexp};
+    a.xexp = h3_exp;
+    const long long grid = ppox::ceil_div((long long)batch, (long long)FCW_ROWS) * 4;
+    fcw_kernel<<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(q_fwd));
+    PPOX_LAUNCHED("ppox_nature_fc_fwd");
 }
 
 // the conv3 dgrad's direct form on PX g3 -> PX g2 (PPOX_DDGRAD3=0: the im2col sgemm; _MIN: the smallest

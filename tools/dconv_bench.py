@@ -114,6 +114,23 @@ def main():
             row[name + "_tf"] = round(2 * 49 * 576 * 64 * B / t / 1e12, 1)
         os.environ.pop("PPOX_DWGRAD3")
         print(json.dumps(row), flush=True)
+        # fc forward on PX h3: the 256 x 128 wide-tile form against the sg2 GEMM
+        h3f = torch.relu(torch.randn(B, 7, 7, 64, device="cuda"))
+        native.amax(h3f, ag[1])
+        h3p = torch.empty(B, 7, 7, 128, dtype=torch.int16, device="cuda")
+        e3h = torch.zeros(1, dtype=torch.int32, device="cuda")
+        native.px_split(h3f, ag[1], h3p, e3h)
+        f = torch.empty(B, 512, device="cuda")
+        row = {"B": B, "op": "fc fwd"}
+        os.environ["PPOX_FCW_MIN"] = "1"
+        for name, v in (("sg2", "0"), ("wide", "1")):
+            os.environ["PPOX_FCW"] = v
+            row[name + "_us"] = round(1e3 * t_ms(lambda: native.nature_fc_fwd(h3p, B, cv.qfc[0], cv.fc.bias, f,
+                                                                               amax_f=ag[0], h3_exp=e3h)), 1)
+            row[name + "_tf"] = round(2 * 3136 * 512 * B / (row[name + "_us"] * 1e-6) / 1e12, 1)
+        os.environ.pop("PPOX_FCW")
+        os.environ.pop("PPOX_FCW_MIN")
+        print(json.dumps(row), flush=True)
 
 
 if __name__ == "__main__":
