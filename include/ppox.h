@@ -370,6 +370,14 @@ int ppox_head_hidden_fwd_splitk(const float* f, int64_t rows, const uint16_t* q_
                                 const float* w_critic, const float* b_critic, float* value, void* stream);
 int ppox_head_hidden_dgrad(const float* de, int64_t rows, const uint16_t* q_dgrad, const float* f, float* df,
                            const uint32_t* amax_de, uint32_t* amax_df, void* stream);
+/* The heads' backward to the fc output in one launch (round 5; replaces ppox_head_dgrad_outer +
+ * ppox_head_hidden_dgrad for a net without the intrinsic head): de = (e > 0) dv w_critic (bitwise
+ * ppox_head_dgrad_outer's de) and df = (f > 0) (dout w_actor + de W) with W the hidden layer
+ * (q_dgrad: its ppox_nature_pack_all dgrad form), f32 (rows x 512); both amax recorded.  Reference:
+ * models-checkpoint.py:72, 80-85 (actor, extra_layer, critic_ext) backward, ppo.py:241. */
+int ppox_head_backward(const float* dout, const float* w_actor, const float* dv, const float* w_critic, const float* e,
+                       const float* f, const uint16_t* q_dgrad, int64_t rows, int64_t h, int64_t n_out, float* df,
+                       float* de, uint32_t* amax_de, uint32_t* amax_df, void* stream);
 int64_t ppox_head_hidden_wgrad_workspace_bytes(int64_t rows);
 int ppox_head_hidden_wgrad(const float* de, int64_t rows, const float* f, void* workspace, int64_t workspace_bytes,
                            float* dw, const uint32_t* amax_de, const uint32_t* amax_f, void* stream);

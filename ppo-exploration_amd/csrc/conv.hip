@@ -4068,6 +4068,21 @@ extern "C" int ppox_head_hidden_dgrad(const float* de, int64_t rows, const uint1
         a, q_dgrad, ppox::ceil_div(rows, SG_ROWS) * (512 / SG_FC_NB), ppox::as_stream(stream), "ppox_head_hidden_dgrad");
 }
 
+// the heads' backward to the fc output in one launch (csrc/dconv.hip hbw_kernel): de = (e > 0) dv wc and
+// df = (f > 0) (dout Wa + de Wh) — ppox_head_dgrad_outer + ppox_head_hidden_dgrad without de's HBM round trip
+extern "C" int ppox_head_backward(const float* dout, const float* w_actor, const float* dv, const float* w_critic,
+                                  const float* e, const float* f, const uint16_t* q_dgrad, int64_t rows, int64_t h,
+                                  int64_t n_out, float* df, float* de, uint32_t* amax_de, uint32_t* amax_df,
+                                  void* stream) {
+    if (rows == 0) return PPOX_OK;
+    PPOX_REQUIRE(dout && w_actor && dv && w_critic && e && f && q_dgrad && df && de && amax_de && amax_df && rows > 0,
+                 "ppox_head_backward: bad arguments");
+    PPOX_REQUIRE(h == 512, "ppox_head_backward: the hidden layer is 512 wide");
+    PPOX_REQUIRE(ppox::aligned16(amax_de) && ppox::aligned16(amax_df), "ppox_head_backward: 16B alignment");
+    return ppox_conv::head_backward(dout, w_actor, dv, w_critic, e, f, q_dgrad, pack_exp(q_dgrad, PL_H), rows,
+                                    (int)n_out, df, de, amax_de, amax_df, ppox::as_stream(stream));
+}
+
 extern "C" int64_t ppox_head_hidden_wgrad_workspace_bytes(int64_t rows) {
     return rows <= 0 ? 0 : HeadWgrad::workspace_bytes(rows);
 }

@@ -1057,6 +1057,198 @@ __global__ void __launch_bounds__(512, 1) fcw_kernel(Args a, const u32x4* __rest
 }
 
 // ---------------------------------------------------------------------------
+// The heads' backward to the fc output in one launch (round 5): for the critic's hidden layer e = relu(f Wh^T
+// + bh) (models-checkpoint.py:80-84 extra_layer) and the actor head (Linear(512, A)),
+//   de = (e > 0) * dv wc                                   (the critic head's grad through its ReLU)
+//   df = (f > 0) * (dout Wa + de Wh)                       (into the fc layer, times the fc ReLU)
+// — what head_dgrad_outer_kernel + the sg2 hidden-layer dgrad computed in two launches with de staged through
+// HBM.  de Wh = dv * ((e > 0) * wc) Wh: the GEMM's A operand is wc's two f16 planes (split once per workgroup
+// at wc's own exponent) masked by e > 0, so no amax of de is needed before the GEMM and dv scales the product in
+// the epilogue.  The fcd_kernel pattern: workgroup (column group cg, row group) holds the 4 column tiles 4 cg
+// .. 4 cg + 3 of Wh's dgrad packing in AGPRs (64 fragments each) and walks its rows in phases of 32: the
+// phase's A rows are built in LDS by all 256 threads from e (coalesced float4 reads: thread t always handles
+// columns 4 (t & 127) .. + 3, whose wc planes it keeps in 4 registers), column group 0 also storing de; then
+// the 32 k-steps of 3 MFMAs; then the epilogue (dout Wa from LDS, the fc mask, df and its amax).  fp32-class
+// (held to the fp64 bound: tests/test_hbw_gpu.py); de bitwise head_dgrad_outer_kernel's.
+constexpr int HBW_PH = 32, HBW_ROWB = 2048, HBW_SLOT = HBW_PH * HBW_ROWB;  // A rows: 512 j x 2 planes x f16
+constexpr int HBW_WA = 2 * HBW_SLOT, HBW_LDS = HBW_WA + 8 * 512 * 4;      // + Wa (<= 8 actions) f32
+
+struct HbwArgs {
+    const float *dout, *wa, *dv, *wc, *e, *f;
+    float *df, *de;
+    uint32_t *amax_de, *amax_df;
+    const int* wexp;  // Wh's dgrad packing exponent
+    long long rows;
+    int nrg;  // row groups
+};
+
+template <int NO>
+__global__ void __launch_bounds__(256, 1) hbw_kernel(HbwArgs a, const u32x4* __restrict__ wq) {
+    constexpr int NK = 32, KC = 16;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[HBW_LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const long long L = xcd_remap(blockIdx.x, gridDim.x);
+    const int cg = (int)(L & 3), rr = (int)(L >> 2);
+    const int T = cg * 4 + wave;  // this wave's column tile (32 of the 512 inputs)
+    const long long r0 = rr * a.rows / a.nrg, r1 = (rr + 1) * a.rows / a.nrg;
+    const int MR = (int)(r1 - r0);
+    if (MR <= 0) return;
+    const int F_ = (MR + HBW_PH - 1) / HBW_PH;
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
+
+    // wc's split at its own exponent (every workgroup derives the same): thread t keeps columns 4 (t & 127) ..
+    const int c4 = tid & 127;
+    const float4 w4 = reinterpret_cast<const float4*>(a.wc)[c4];
+    uint32_t wmax = max(max(__float_as_uint(fabsf(w4.x)), __float_as_uint(fabsf(w4.y))),
+                        max(__float_as_uint(fabsf(w4.z)), __float_as_uint(fabsf(w4.w))));
+    wmax = wave_max_u32(wmax);
+    uint32_t* red = reinterpret_cast<uint32_t*>(lds + HBW_WA);
+    if (lane == 0) red[wave] = wmax;
+    // Wa to LDS after the reduction (it shares the space): [o][512]
+    __syncthreads();
+    const uint32_t wm = max(max(red[0], red[1]), max(red[2], red[3]));
+    __syncthreads();
+    for (int i = tid; i < NO * 128; i += 256)
+        reinterpret_cast<float4*>(lds + HBW_WA)[i] = reinterpret_cast<const float4*>(a.wa)[i];
+    const int ec = split_scale_exp(wm);
+    uint32_t wh[2], wl[2];
+    split2h((f32x2){w4.x, w4.y}, exp2i(ec), wh[0], wl[0]);
+    split2h((f32x2){w4.z, w4.w}, exp2i(ec), wh[1], wl[1]);
+    // the weights of tile T: 64-column block T >> 1, tile T & 1, all 16 chunks (the fcd_kernel load)
+    u32x4 bq[KC][2][2];
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+                bq[c][s][p] = wq[(long long)((T >> 1) * KC + c) * (2 * 2 * NPL * 64) + (((s * 2 + (T & 1)) * 2 + p) * 64) + lane];
+    const float us = exp2i(-ec) * exp2i(-*a.wexp);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();  // (Wa in LDS)
+    asm volatile("s_nop 4" ::: "memory");
+
+    float om_df = 0.f, om_de = 0.f;
+    // build phase f's A rows into slot f & 1: float4 k of thread t is row 2 k + (t >> 7) of the phase, columns
+    // 4 c4 .. 4 c4 + 3 — the planes' 8-B half (c4 & 1) of piece ((j >> 5) & 1) 8 + p 4 + ((j >> 3) & 3) of the row's
+    // 256-B unit j >> 6, the piece stored at position piece ^ (row & 15) (fcd_kernel's layout)
+    const int j0 = 4 * c4;
+    const uint32_t unit = (uint32_t)(j0 >> 6) * 256, pc = (uint32_t)(((j0 >> 5) & 1) * 8 + ((j0 >> 3) & 3)),
+                   half = (uint32_t)((j0 >> 2) & 1) * 8;
+    auto build = [&](int f) {
+        uint8_t* slot = lds + (f & 1) * HBW_SLOT;
+#pragma unroll 4
+        for (int k = 0; k < 16; ++k) {
+            const int row = 2 * k + (tid >> 7);
+            long long m = r0 + (long long)f * HBW_PH + row;
+            const bool live = m < r1;
+            m = live ? m : r1 - 1;
+            const float4 ev = reinterpret_cast<const float4*>(a.e)[m * 128 + c4];
+            const float s = a.dv[m];
+            const uint32_t m0 = (ev.x > 0.f ? 0xFFFFu : 0u) | (ev.y > 0.f ? 0xFFFF0000u : 0u);
+            const uint32_t m1 = (ev.z > 0.f ? 0xFFFFu : 0u) | (ev.w > 0.f ? 0xFFFF0000u : 0u);
+            const uint32_t key = (uint32_t)(row & 15);
+            uint8_t* rb = slot + row * HBW_ROWB + unit + half;
+            *reinterpret_cast<uint2*>(rb + ((pc ^ key) << 4)) = make_uint2(wh[0] & m0, wh[1] & m1);
+            *reinterpret_cast<uint2*>(rb + (((pc + 4) ^ key) << 4)) = make_uint2(wl[0] & m0, wl[1] & m1);
+            if (cg == 0 && live) {  // de, as head_dgrad_outer_kernel: (e > 0) ? dv * wc : 0
+                float4 o;
+                o.x = ev.x > 0.f ? s * w4.x : 0.f;
+                o.y = ev.y > 0.f ? s * w4.y : 0.f;
+                o.z = ev.z > 0.f ? s * w4.z : 0.f;
+                o.w = ev.w > 0.f ? s * w4.w : 0.f;
+                reinterpret_cast<float4*>(a.de)[m * 128 + c4] = o;
+                om_de = fmaxf(om_de, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+            }
+        }
+    };
+    f32x16 H, Lo;
+    const uint32_t kx = (uint32_t)((r & 15) ^ h) << 4;
+    for (int f = 0; f < F_; ++f) {
+        build(f);
+        __syncthreads();  // the phase's A rows written; (two slots: every wave is past phase f - 2's reads)
+        const uint32_t base = lds0 + (f & 1) * HBW_SLOT + r * HBW_ROWB;
+        auto addr = [&](int i, int pl) {  // k-step i = 2 c + s: piece 8 (c & 1) + 4 pl + 2 s + h of row r
+            const int c = i >> 1, s = i & 1;
+            const uint32_t P16 = (uint32_t)(((c & 1) << 3) | (pl << 2) | (s << 1)) << 4;
+            return base + (P16 ^ kx);
+        };
+        constexpr int PD = 2, NB = 3;
+        u32x4 fa[NB][2];
+        auto rd1 = [&](auto I, auto PLc) {
+            constexpr int i = decltype(I)::value, pl = decltype(PLc)::value;
+            fa[i % NB][pl] = dc_read<((i >> 1) >> 1) * 256>(addr(i, pl));
+        };
+        using Z = std::integral_constant<int, 0>;
+        using O = std::integral_constant<int, 1>;
+        // the epilogue's operands, loaded before the k walk: lane (r, h) = row r of the phase
+        long long m = r0 + (long long)f * HBW_PH + r;
+        const bool live = m < r1;
+        m = live ? m : r1 - 1;
+        float go[NO];
+#pragma unroll
+        for (int o = 0; o < NO; ++o) go[o] = a.dout[m * NO + o];
+        const float sv = a.dv[m];
+        float4 fv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) fv[t] = reinterpret_cast<const float4*>(a.f)[m * 128 + ((32 * T + 8 * t + 4 * h) >> 2)];
+        rd1(Z{}, Z{});
+        rd1(Z{}, O{});
+        rd1(O{}, Z{});
+        rd1(O{}, O{});
+        dc_lgkm<2>(fa[0][0], fa[0][1]);
+        dc_unroll(
+            [&](auto I) {
+                constexpr int i = decltype(I)::value;
+                const u32x4& b0 = bq[i >> 1][i & 1][0];
+                const u32x4& b1 = bq[i >> 1][i & 1][1];
+                if constexpr (i == 0)
+                    dc_mfma0<true>(H, fa[0][0], b0);
+                else
+                    dc_mfma<true>(H, fa[i % NB][0], b0);
+                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, Z{});
+                if constexpr (i == 0)
+                    dc_mfma0<true>(Lo, fa[0][0], b1);
+                else
+                    dc_mfma<true>(Lo, fa[i % NB][0], b1);
+                if constexpr (i + PD < NK) rd1(std::integral_constant<int, i + PD>{}, O{});
+                dc_mfma<true>(Lo, fa[i % NB][1], b0);
+                constexpr int later = (i + PD < NK ? i + PD : NK - 1) - (i + 1);
+                if constexpr (i + 1 < NK) dc_lgkm<2 * later>(fa[(i + 1) % NB][0], fa[(i + 1) % NB][1]);
+            },
+            std::make_integer_sequence<int, NK>{});
+        dc_acc_fence(H, Lo);
+        // epilogue: inputs 32 T + 8 t + 4 h + k of the lane's row
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int i0 = 32 * T + 8 * t + 4 * h;
+            float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int o = 0; o < NO; ++o) {  // dout Wa, in head_dgrad_outer_kernel's order
+                const float4 wv = *reinterpret_cast<const float4*>(lds + HBW_WA + (o * 512 + i0) * 4);
+                d.x = fmaf(go[o], wv.x, d.x);
+                d.y = fmaf(go[o], wv.y, d.y);
+                d.z = fmaf(go[o], wv.z, d.z);
+                d.w = fmaf(go[o], wv.w, d.w);
+            }
+            float4 y;
+            y.x = fv[t].x > 0.f ? d.x + ((H[4 * t] + Lo[4 * t]) * us) * sv : 0.f;
+            y.y = fv[t].y > 0.f ? d.y + ((H[4 * t + 1] + Lo[4 * t + 1]) * us) * sv : 0.f;
+            y.z = fv[t].z > 0.f ? d.z + ((H[4 * t + 2] + Lo[4 * t + 2]) * us) * sv : 0.f;
+            y.w = fv[t].w > 0.f ? d.w + ((H[4 * t + 3] + Lo[4 * t + 3]) * us) * sv : 0.f;
+            if (live) {
+                reinterpret_cast<float4*>(a.df)[m * 128 + (i0 >> 2)] = y;
+                om_df = fmaxf(om_df, fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w))));
+            }
+        }
+    }
+    amax_record(a.amax_df, om_df);
+    if (cg == 0) amax_record(a.amax_de, om_de);
+}
+
+// ---------------------------------------------------------------------------
 // The conv3 dgrad in the direct form (round 5): g2 = (h2 > 0) * conv3^T(g3), PX g3 in, PX g2 out,
 // .ipynb_checkpoints/models-checkpoint.py:57 backward (reached through ppo.py:241).  An h2 pixel
 // (iy, ix) takes tap (ky, kx) from the g3 pixel (iy - ky, ix - kx) when that lies on the 7 x 7 image — an
@@ -1685,6 +1877,30 @@ int fcw(const void* h3p, int64_t batch, const uint16_t* q_fwd, const float* bias
     const long long grid = ppox::ceil_div((long long)batch, (long long)FCW_ROWS) * 4;
     fcw_kernel<<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(q_fwd));
     PPOX_LAUNCHED("ppox_nature_fc_fwd");
+}
+
+// the heads' backward to the fc output in one launch (hbw_kernel): de and df (f32, masked), their amax
+int head_backward(const float* dout, const float* wa, const float* dv, const float* wc, const float* e, const float* f,
+                  const uint16_t* qhd, const int* wexp, int64_t rows, int n_out, float* df, float* de,
+                  uint32_t* amax_de, uint32_t* amax_df, hipStream_t s) {
+    if (rows == 0) return PPOX_OK;
+    const int cus = dconv_cus();
+    PPOX_REQUIRE(cus > 0, "ppox_head_backward: no device");
+    PPOX_REQUIRE(n_out >= 1 && n_out <= 8, "ppox_head_backward: n_out must be 1..8");
+    PPOX_REQUIRE(ppox::aligned16(wa) && ppox::aligned16(wc) && ppox::aligned16(e) && ppox::aligned16(f) &&
+                     ppox::aligned16(df) && ppox::aligned16(de) && ppox::aligned16(qhd),
+                 "ppox_head_backward: 16B alignment");
+    const int nrg = (int)std::max<long long>(1, std::min<long long>(cus / 4, ppox::ceil_div((long long)rows, 32LL)));
+    HbwArgs a{dout, wa, dv, wc, e, f, df, de, amax_de, amax_df, wexp, rows, nrg};
+    const u32x4* w = reinterpret_cast<const u32x4*>(qhd);
+    const unsigned grid = (unsigned)(4 * nrg);
+    switch (n_out) {
+#define PPOX_HBW(N) \
+    case N: hbw_kernel<N><<<grid, 256, 0, s>>>(a, w); break;
+        PPOX_HBW(1) PPOX_HBW(2) PPOX_HBW(3) PPOX_HBW(4) PPOX_HBW(5) PPOX_HBW(6) PPOX_HBW(7) PPOX_HBW(8)
+#undef PPOX_HBW
+    }
+    PPOX_LAUNCHED("ppox_head_backward");
 }
 
 // the conv3 dgrad's direct form on PX g3 -> PX g2 (PPOX_DDGRAD3=0: the im2col sgemm; _MIN: the smallest

@@ -17,6 +17,7 @@ available (see convs.py); the small linear layers use PyTorch-ROCm (rocBLAS).
 """
 import contextlib
 import math
+import os
 
 import numpy as np
 import torch
@@ -67,6 +68,8 @@ class MlpNetwork(nn.Module):
 # of 64x64 for a 512x512 result and leaves most CUs idle over K = 16384 rows (tools/
 # gemm_split_probe.py: 104 -> 67 us at 16384 rows, no gain at 2048)
 WGRAD_SPLIT, WGRAD_SPLIT_MIN = 8, 8192
+# the heads' backward to the fc output in one launch (ppox_head_backward; PPOX_HBW=0: the two-launch form)
+HEAD_BWD_FUSED = os.environ.get("PPOX_HBW", "1") != "0"
 
 
 def weight_grad(d, x, out, part=None):
@@ -249,9 +252,17 @@ class CnnActorCritic(nn.Module):
             merge = (side is not None and _convs.FORK_MERGE and split and cv.nhwc3
                      and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH)
             deferred = []
-            # the actor head's input grad and the extra layer's dv * w_critic * ReLU' in one launch
-            df, de0 = native.head_dgrad_outer(dout, a.weight, dv.contiguous().view(B), self.critic_ext.weight, e,
-                                              amax_de=am[_convs.AM_DE] if split else None)
+            # round 5: with the split hidden layer and no intrinsic head, the actor's input grad, the critic's
+            # ReLU-layer grad and the hidden layer's dgrad (fc ReLU applied) in one launch (ppox_head_backward)
+            fused = split and not self.intrinsic and HEAD_BWD_FUSED and dout.shape[1] <= 8
+            if fused:
+                df, de0 = torch.empty_like(f), torch.empty_like(e)
+                native.head_backward(dout, a.weight, dv.contiguous().view(B), self.critic_ext.weight, e, f, cv.qh[1],
+                                     df, de0, am[_convs.AM_DE], am[_convs.AM_DF])
+            else:
+                # the actor head's input grad and the extra layer's dv * w_critic * ReLU' in one launch
+                df, de0 = native.head_dgrad_outer(dout, a.weight, dv.contiguous().view(B), self.critic_ext.weight, e,
+                                                  amax_de=am[_convs.AM_DE] if split else None)
             for hid, crit, act, d in heads:
                 d = d.contiguous().view(B, 1)
                 sp = split and hid is self.extra_layer[0]
@@ -274,7 +285,7 @@ class CnnActorCritic(nn.Module):
                 if not sp:
                     df.addmm_(de, hid.weight)
                 des.append((de, d))
-            if split:  # df = (f > 0) ? df + de W : 0, recording df's amax (the fc layer's operand)
+            if split and not fused:  # df = (f > 0) ? df + de W : 0, recording df's amax (the fc layer's operand)
                 native.head_hidden_dgrad(des[0][0], cv.qh[1], f, df, amax_de=am[_convs.AM_DE], amax_df=am[_convs.AM_DF])
             # every column-reduction gradient (actor W/b, critic W/b, extra-layer b, fc b) in one pass; without
             # the split hidden layer it first applies the fc ReLU's backward to df (in place, df's amax recorded)

@@ -81,6 +81,7 @@ SIGNATURES = {
     "ppox_head_hidden_fwd": [_vp, _i64, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_fwd_splitk": [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_hidden_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ppox_head_backward": [_vp] * 7 + [_i64, _i64, _i64] + [_vp] * 5,
     "ppox_head_hidden_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_dgrad": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_fc_wgrad": [_vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
@@ -646,6 +647,13 @@ def head_hidden_dgrad(de, q_dgrad, f, df, amax_de=None, amax_df=None, stream=Non
         amax_de = _amax_of(de, amax_de, stream)
     call("ppox_head_hidden_dgrad", _p(de), rows, _p(q_dgrad), _p(f), _p(df), _p(amax_de), _p(amax_df),
          stream_ptr(stream))
+
+
+def head_backward(dout, w_actor, dv, w_critic, e, f, q_dgrad, df, de, amax_de, amax_df, stream=None):
+    """de = (e > 0) dv w_critic, df = (f > 0) (dout w_actor + de W) in one launch (ppox_head_backward)."""
+    rows = e.shape[0]
+    call("ppox_head_backward", _p(dout), _p(w_actor), _p(dv), _p(w_critic), _p(e), _p(f), _p(q_dgrad), rows,
+         e.shape[1], dout.shape[1], _p(df), _p(de), _p(amax_de), _p(amax_df), stream_ptr(stream))
 
 
 def head_hidden_wgrad_workspace_bytes(rows):
