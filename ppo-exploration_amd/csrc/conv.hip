@@ -1374,6 +1374,9 @@ struct ActorHead {
 
 // K = 3136: the fc layer (reduce: + bias, ReLU, f's amax, the actor head); K = 512: the heads' hidden
 // layer (the same reduce with the critic head Linear(512, 1) fused, no amax)
+template <int S>
+int launch_fc_sk_reduce(const Args& a, float* slab, const float* bias, float* f, const ActorHead& act, hipStream_t st,
+                        const char* name);
 template <int K, int S, bool AP = false>
 int launch_fc_fwd_sk(const Args& a, const uint16_t* q, float* slab, const float* bias, float* f, const ActorHead& act,
                      hipStream_t st, const char* name = "ppox_nature_fc_fwd_splitk") {
@@ -1383,6 +1386,12 @@ int launch_fc_fwd_sk(const Args& a, const uint16_t* q, float* slab, const float*
     const int rc = launch_sgemm<Px<SgRowsSK<K, 512, S>, AP>>(b, q, ppox::ceil_div(a.batch, SG_ROWS) * FcFwd::NCB * S,
                                                              st, name);
     if (rc != PPOX_OK) return rc;
+    return launch_fc_sk_reduce<S>(a, slab, bias, f, act, st, name);
+}
+// the S partial products in order + bias, ReLU, f's amax (a.amax_y), the fused head
+template <int S>
+int launch_fc_sk_reduce(const Args& a, float* slab, const float* bias, float* f, const ActorHead& act, hipStream_t st,
+                        const char* name) {
     const float4* sl = reinterpret_cast<const float4*>(slab);
     float4* f4 = reinterpret_cast<float4*>(f);
     const unsigned rows4 = (unsigned)ppox::ceil_div(a.batch, 4LL);
@@ -3925,7 +3934,9 @@ extern "C" int ppox_nature_fc_fwd(const float* h3, int64_t batch, const uint16_t
 }
 
 extern "C" int64_t ppox_nature_fc_fwd_splitk_workspace_bytes(int64_t batch) {
-    return batch <= 0 ? 0 : (int64_t)fc_fwd_splits(batch) * batch * 512 * 4;
+    if (batch <= 0) return 0;
+    const long long s = ppox_conv::fcw_sk_enabled(batch) ? ppox_conv::FCW_SPLITS : fc_fwd_splits(batch);
+    return (int64_t)s * batch * 512 * 4;
 }
 
 extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const uint16_t* q_fwd, const float* bias,
@@ -3947,6 +3958,12 @@ extern "C" int ppox_nature_fc_fwd_splitk(const float* h3, int64_t batch, const u
     float* slab = reinterpret_cast<float*>(workspace);
     hipStream_t st = ppox::as_stream(stream);
     const ActorHead act{w_actor, b_actor, logits ? (int)n_actions : 0, logits};
+    if (h3_exp && ppox_conv::fcw_sk_enabled(batch)) {  // the wide-tile form split 8 ways (dconv.hip)
+        const int rc = ppox_conv::fcw_sk(h3, batch, q_fwd, slab, h3_exp, a.wexp, st);
+        if (rc != PPOX_OK) return rc;
+        static_assert(ppox_conv::FCW_SPLITS == 8, "the reduce's split count");
+        return launch_fc_sk_reduce<8>(a, slab, bias, f, act, st, "ppox_nature_fc_fwd_splitk");
+    }
     if (h3_exp) {
         switch (fc_fwd_splits(batch)) {
             case 1: return launch_fc_fwd_sk<3136, 1, true>(a, q_fwd, slab, bias, f, act, st);

@@ -409,6 +409,11 @@ bool dfcd_enabled(long long batch);
 int dfcd(const void* dfp, int64_t batch, const uint16_t* wq, float* g3, const uint32_t* amax_df, uint32_t* amax_g3,
          const uint32_t* relu_bits, int* g3_exp_out, const int* df_exp, const int* wexp, const uint32_t* ynorm,
          const uint32_t* ybias, hipStream_t s);
+// ... split 8 ways over K into a slab [8][batch][512] (batches below fcw_enabled's)
+bool fcw_sk_enabled(long long batch);
+int fcw_sk(const void* h3p, int64_t batch, const uint16_t* q_fwd, float* slab, const int* h3_exp, const int* wexp,
+           hipStream_t s);
+constexpr int FCW_SPLITS = 8;
 // the heads' backward to the fc output in one launch (dconv.hip hbw_kernel)
 int head_backward(const float* dout, const float* wa, const float* dv, const float* wc, const float* e, const float* f,
                   const uint16_t* qhd, const int* wexp, int64_t rows, int n_out, float* df, float* de,

@@ -914,6 +914,7 @@ constexpr int FCW_ROWS = 256, FCW_KC = 3136 / 32, FCW_ROWB = 3136 * 4;  // rows 
 constexpr int FCW_BQ = 2 * 2 * 2 * 64;                                  // u32x4 per 64-column B block chunk
 constexpr int FCW_AB = FCW_ROWS * 128, FCW_SLOT = FCW_AB + 2 * FCW_BQ * 16, FCW_NSLOT = 3;
 constexpr int FCW_LDS = FCW_NSLOT * FCW_SLOT;  // 147,456 B
+constexpr int FCW_SK = 8;                       // K-splits of the small-batch form
 static_assert(FCW_LDS <= 160 * 1024, "fcw: LDS");
 
 template <int N>
@@ -928,13 +929,19 @@ __device__ inline void sg_vm_wait_n() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// SK > 1 (small batches, round 5): split over K — workgroup (row tile, split ks, column group) walks chunks
+// [98 ks / SK, 98 (ks + 1) / SK) and stores its unscaled partial product to slab a.y[ks][row][512]
+// (no bias, no ReLU: fc_fwd_sk_reduce_actor adds the SK partials in order); a row tile's SK x 4 workgroups
+// run on one XCD
+template <int SK>
 __global__ void __launch_bounds__(512, 1) fcw_kernel(Args a, const u32x4* __restrict__ wq) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[FCW_LDS];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long long L = xcd_remap(blockIdx.x, gridDim.x);
-    const int cg = (int)(L & 3);
-    const long long m0 = (L >> 2) * FCW_ROWS, M = a.batch;
+    const int cg = (int)(L & 3), ks = (int)((L >> 2) % SK);
+    const long long m0 = ((L >> 2) / SK) * FCW_ROWS, M = a.batch;
+    const int c0 = ks * FCW_KC / SK, nck = (ks + 1) * FCW_KC / SK - c0;  // this workgroup's chunks
     const int rg = wave >> 1, ch = wave & 1;
     const int r = lane & 31, h = lane >> 5;
     const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
@@ -958,7 +965,7 @@ __global__ void __launch_bounds__(512, 1) fcw_kernel(Args a, const u32x4* __rest
     }
     auto issue = [&](int c, auto S) {
         constexpr int slot = decltype(S)::value;
-        c = c < FCW_KC ? c : FCW_KC - 1;  // past the end: the last chunk again, never read
+        c = c0 + (c < nck ? c : nck - 1);  // past the end: the last chunk again, never read
         uint8_t* base = lds + slot * FCW_SLOT;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -1030,12 +1037,27 @@ __global__ void __launch_bounds__(512, 1) fcw_kernel(Args a, const u32x4* __rest
     issue(0, I0{});
     issue(1, I1{});
 #pragma unroll 1
-    for (int c = 0; c < FCW_KC; c += 3) {  // (98 = 3 x 32 + 2)
+    for (int c = 0; c < nck; c += 3) {
         step(c, I0{}, I2{});
-        if (c + 1 < FCW_KC) step(c + 1, I1{}, I0{});
-        if (c + 2 < FCW_KC) step(c + 2, I2{}, I1{});
+        if (c + 1 < nck) step(c + 1, I1{}, I0{});
+        if (c + 2 < nck) step(c + 2, I2{}, I1{});
     }
     sg_vm_wait_n<0>();  // the clamped tail DMAs, before the LDS is released
+    if constexpr (SK > 1) {  // the partial product (its split's slab)
+        float* slab = a.y + (long long)ks * M * 512;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int n = 128 * cg + 64 * ch + 32 * t + r;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const long long m = m0 + 64 * rg + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
+                    if (m < M) slab[m * 512 + n] = (acc[i][t][q] + acl[i][t][q]) * us;
+                }
+        }
+        return;
+    }
     float om = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -1817,6 +1839,9 @@ int launch_dconv(const Args& a, const uint16_t* wq, hipStream_t s, const char* n
 #ifndef FCW_MIN
 #define FCW_MIN 8192
 #endif
+#ifndef FCW_SK_MIN
+#define FCW_SK_MIN 1024
+#endif
 #ifndef DDGRAD3_MIN
 #define DDGRAD3_MIN 4096
 #endif
@@ -1875,8 +1900,23 @@ int fcw(const void* h3p, int64_t batch, const uint16_t* q_fwd, const float* bias
     Args a{h3p, nullptr, 0, 0, 0, nullptr, bias, nullptr, f, batch, nullptr, amax_f, wexp};
     a.xexp = h3_exp;
     const long long grid = ppox::ceil_div((long long)batch, (long long)FCW_ROWS) * 4;
-    fcw_kernel<<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(q_fwd));
+    fcw_kernel<1><<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(q_fwd));
     PPOX_LAUNCHED("ppox_nature_fc_fwd");
+}
+// split over K (8 ways) into slab [8][batch][512] (the caller's fc_fwd_sk_reduce adds them): batches from
+// PPOX_FCW_SK_MIN (1024) below the full-tile form's
+bool fcw_sk_enabled(long long batch) {
+    return env_on("PPOX_FCW", batch, FCW_DEFAULT, FCW_SK_MIN) && !fcw_enabled(batch);
+}
+int fcw_sk(const void* h3p, int64_t batch, const uint16_t* q_fwd, float* slab, const int* h3_exp, const int* wexp,
+           hipStream_t s) {
+    PPOX_REQUIRE(ppox::aligned16(h3p) && ppox::aligned16(q_fwd) && slab && h3_exp && wexp,
+                 "ppox_nature_fc_fwd_splitk: the wide form needs PX h3 (16B-aligned)");
+    Args a{h3p, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, slab, batch, nullptr, nullptr, wexp};
+    a.xexp = h3_exp;
+    const long long grid = ppox::ceil_div((long long)batch, (long long)FCW_ROWS) * 4 * FCW_SK;
+    fcw_kernel<FCW_SK><<<(unsigned)grid, 512, 0, s>>>(a, reinterpret_cast<const u32x4*>(q_fwd));
+    PPOX_LAUNCHED("ppox_nature_fc_fwd_splitk");
 }
 
 // the heads' backward to the fc output in one launch (hbw_kernel): de and df (f32, masked), their amax

@@ -74,3 +74,51 @@ def test_fc_fwd_wide_is_deterministic():
     a = _fwd(h3p, E, B, qf, b, "wide")
     c = _fwd(h3p, E, B, qf, b, "wide")
     assert torch.equal(a[0], c[0]) and a[1] == c[1]
+
+
+@pytest.mark.parametrize("B", [1024, 2048, 3000, 8191])
+def test_fc_fwd_wide_splitk_vs_fp64(B):
+    """the small-batch form (PPOX_FCW_SK_MIN .. PPOX_FCW_MIN rows): the 256 x 128 tiles split 8 ways over K into
+    slabs, summed in order with bias + ReLU + the fused actor head by fc_fwd_sk_reduce_actor — against float64,
+    the sg2 split-K form (PPOX_FCW=0) and torch's f32 GEMM; logits as the same reduce computes them from f"""
+    import native
+    torch.manual_seed(B)
+    W = torch.randn(512, 3136, device="cuda") * 0.02
+    b = torch.randn(512, device="cuda") * 0.1
+    wa, ba = torch.randn(4, 512, device="cuda") * 0.05, torch.randn(4, device="cuda") * 0.1
+    h3n = torch.relu(torch.randn(B, 7, 7, 64, device="cuda")) * torch.rand(B, 7, 7, 64, device="cuda")
+    E = _split_exp(float(h3n.abs().max()))
+    h3p = _planes(h3n, E)
+    h3v = _values(h3p, E)
+    n = native.nature_fc_pack_elems()
+    qf, qd = torch.empty(n, dtype=torch.int16, device="cuda"), torch.empty(n, dtype=torch.int16, device="cuda")
+    native.nature_fc_pack(W, qf, qd)
+    outs = {}
+    for form, v in (("wide", "1"), ("sg2", "0")):
+        old = os.environ.get("PPOX_FCW")
+        os.environ["PPOX_FCW"] = v
+        try:
+            ws = torch.empty(native.nature_fc_fwd_splitk_workspace_bytes(B), dtype=torch.uint8, device="cuda")
+            f = torch.full((B + 1, 512), 7.0, device="cuda")
+            lg = torch.empty(B, 4, device="cuda")
+            am = native.amax_table(1, "cuda")[0]
+            native.nature_fc_fwd_splitk(h3p, B, qf, b, ws, f[:B], amax_f=am, actor=(wa, ba), logits=lg,
+                                        h3_exp=torch.tensor([E], dtype=torch.int32, device="cuda"))
+            torch.cuda.synchronize()
+            outs[form] = (f, lg, float(am.cpu().numpy().view(np.float32).max()))
+        finally:
+            if old is None:
+                os.environ.pop("PPOX_FCW", None)
+            else:
+                os.environ["PPOX_FCW"] = old
+    fw, lw, amw = outs["wide"]
+    assert bool((fw[B] == 7.0).all())
+    f = fw[:B]
+    assert amw == float(f.max())
+    h3 = h3v.permute(0, 3, 1, 2).reshape(B, 3136)
+    ref = torch.relu(h3.double() @ W.double().t() + b.double())
+    scale = ref.abs().max()
+    err = lambda x: float((x.double() - ref).abs().max() / scale)
+    assert err(f) <= 2 * max(err(torch.relu(torch.addmm(b, h3, W.t()))), err(outs["sg2"][0][:B])) + 1e-7
+    refl = f.double() @ wa.double().t() + ba.double()
+    assert float((lw.double() - refl).abs().max() / refl.abs().max()) <= 1e-5
