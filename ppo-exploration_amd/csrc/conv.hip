@@ -3278,7 +3278,13 @@ int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
     // element ranges end at the last job present (the head and fc dgrad ranges are the longest)
     const long long total = PA_N1 + 2 * PU_2 + 2 * PU_3 + PA_N2 + PU_FC +
                             (p.qhf || p.qhd ? PU_FCD + 2 * PU_H : (p.qfcd ? PU_FCD : 0));
-    const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 4096);
+    // every wave first reads the five tensors' 256 amax partials (5 KB): 4,096 workgroups re-read 80 MB of them
+    // through L2 — a few hundred, each striding over more units, read a few MB (PPOX_PACK_BLOCKS: A/B knob)
+    static const long long cap = [] {
+        const char* e = std::getenv("PPOX_PACK_BLOCKS");
+        return e ? std::max(1LL, std::atoll(e)) : 512LL;
+    }();
+    const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, cap);
     pack_all_kernel<<<blocks, 256, 0, s>>>(p, total);
     PPOX_LAUNCHED_NORET(name);
     note_px_pack(p.q2, p.b2 != nullptr);

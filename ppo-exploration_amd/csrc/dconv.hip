@@ -34,6 +34,9 @@
 
 namespace {
 
+#ifndef DCONV_GLOBAL_DMA
+#define DCONV_GLOBAL_DMA 0
+#endif
 #ifndef DC_PD
 #define DC_PD 2  // k-steps of A-fragment reads in flight ahead of the MFMAs
 #endif
@@ -75,6 +78,13 @@ struct DcGeo {
     static_assert(LDS <= 160 * 1024, "dconv: LDS");
     static_assert(F::L::P % 16 == 1, "dconv: the row key is m mod 16");
 };
+
+// one buffer LDS-DMA of 16 B per lane: descriptor over [base, base + bytes) (uniform), lane offset, sample offset
+// (a helper: the builtins written in a kernel template's body made hipcc drop the template's host stubs)
+__device__ inline void dc_buffer_dma(const void* base, int bytes, uint8_t* dst, uint32_t voff, int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000),
+                                             (__attribute__((address_space(3))) void*)dst, 16, voff, soff, 0, 0);
+}
 
 template <class Fn, int... I>
 __device__ inline void dc_unroll(Fn&& fn, std::integer_sequence<int, I...>) {
@@ -175,23 +185,26 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
         const int y = u / L::IW, x = u % L::IW;
         dpk[i] = u | ((L::S == 1 ? L::OW * y + x : 9 * (y >> 1) + (x >> 1)) << 16);
     }
-    // DMA i of a sample: its image at src (uniform), ring slot dst (uniform), n & 15 = nk; a uniform base +
-    // a 32-bit lane offset
-    auto issue_at = [&](const uint8_t* src, uint8_t* dst, int nk, int i) {
+    // DMA i of sample n (range-relative): a buffer LDS-DMA — the range's descriptor (uniform), the sample in
+    // soffset, the lane's 32-bit offset in voffset (no 64-bit address arithmetic per DMA; DCONV_GLOBAL_DMA=1:
+    // the round-4 global_load_lds form)
+    auto issue_one = [&](int n, int i) {
         int d = wave + 4 * i;
         d = d < Gm::REAL_DMAS ? d : Gm::REAL_DMAS - 1;
-        const int key = (nk + (dpk[i] >> 16)) & 15, u = dpk[i] & 0xFFFF;
+        const int key = (n + (dpk[i] >> 16)) & 15, u = dpk[i] & 0xFFFF;
         uint32_t off;
         if constexpr (F::PIXB == 256) {
             off = (uint32_t)(u * 256 + (((lane & 15) ^ key) << 4));
         } else {  // conv2: the pixel pair swapped by key & 1, the piece by key >> 1
             off = (uint32_t)((u ^ (key & 1)) * 128 + (((lane & 7) ^ (key >> 1)) << 4));
         }
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + off),
-                                         (__attribute__((address_space(3))) void*)(dst + d * 1024), 16, 0, 0);
-    };
-    auto issue_one = [&](int n, int i) {
-        issue_at(xb + (long long)n * Gm::IMG, lds + (n % F::NSLOT) * Gm::SLOT, n & 15, i);
+        uint8_t* dst = lds + (n % F::NSLOT) * Gm::SLOT + d * 1024;
+#if DCONV_GLOBAL_DMA
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xb + (long long)n * Gm::IMG + off),
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+#else
+        dc_buffer_dma(xb, NS * Gm::IMG, dst, off, n * Gm::IMG);
+#endif
     };
     auto issue_sample = [&](int n) {
 #pragma unroll
@@ -287,13 +300,6 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
         // k walk
         const int rA = issued, nref = min(nlo + F::NSLOT, NS) - issued;
         issued += nref;
-        const uint8_t* rsrc[RMAX];
-        uint8_t* rdst[RMAX];
-#pragma unroll
-        for (int t = 0; t < RMAX; ++t) {
-            rsrc[t] = xb + (long long)(rA + t) * Gm::IMG;
-            rdst[t] = lds + ((rA + t) % F::NSLOT) * Gm::SLOT;
-        }
         // this lane's A row: m = m0 + 32 rg + r (past the range: its last row, never stored)
         int m = m0 + 32 * rg + r;
         m = m < MR ? m : MR - 1;
@@ -372,7 +378,7 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
                     [&](auto X) {
                         constexpr int x = decltype(X)::value, t = x / F::DMAS;
                         if constexpr (16 + x * (NK - 16) / NDMA == i) {
-                            if (t < nref) issue_at(rsrc[t], rdst[t], (rA + t) & 15, x % F::DMAS);
+                            if (t < nref) issue_one(rA + t, x % F::DMAS);
                         }
                     },
                     std::make_integer_sequence<int, NDMA>{});
