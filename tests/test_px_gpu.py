@@ -49,7 +49,7 @@ def _fp64(ref, x, dout, dv):
     return out.detach(), v.detach(), {n: p.grad.clone() for n, p in ref.named_parameters()}
 
 
-def _pass(net, flat, cv, x, dout, dv, px):
+def _pass(net, flat, cv, x, dout, dv, px, masks=None):
     cv.px = px
     flat.zero_grad()
     out, v, _, ctx = net.forward_train(x)
@@ -57,7 +57,45 @@ def _pass(net, flat, cv, x, dout, dv, px):
     net.backward_train(ctx, dout, dv)
     torch.cuda.synchronize()
     grads = {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.requires_grad}
+    if masks is not None:
+        masks.extend(_relu_masks(ctx))
     return out.detach().clone(), v.detach().clone(), grads, am
+
+
+def _relu_masks(ctx):
+    """the pass's own ReLU decisions (CPU bool, NCHW / rows): conv1-3 from the bitmasks its forwards wrote, the
+    fc output f and the critic's hidden layer e from their f32 values"""
+    x, _, _, _, f, e, _, am = ctx
+    B = x.shape[0]
+
+    def unpack(words, P, C, H, W):  # one int32 per 32 channels of a pixel, bit c = channel c > 0
+        w = words.view(B, P, C // 32).long() & 0xFFFFFFFF
+        bits = (w.unsqueeze(-1) >> torch.arange(32, device=w.device)) & 1
+        return bits.reshape(B, H, W, C).permute(0, 3, 1, 2).bool().cpu()
+
+    geo = ((400, 32, 20, 20), (81, 64, 9, 9), (49, 64, 7, 7))
+    convm = [unpack(am.bits[i], *geo[i]) if am.bits[i] is not None else None for i in range(3)]
+    return convm + [(f > 0).cpu(), (e > 0).cpu()]
+
+
+def _fp64_masked(ref, x, dout, dv, masks):
+    """_fp64 with the device pass's ReLU decisions (masks from _relu_masks): a pre-activation within a few f32
+    roundings of 0 may round to the other side on the device; that flips one ReLU and moves the downstream
+    gradients by a whole term, which is a sign decision, not the split math's error — so each pass is held
+    against float64 with its own masks (a mask of None: the float64 ReLU)"""
+    F = torch.nn.functional
+    fe = ref.feature_extractor
+    for p in ref.parameters():
+        p.grad = None
+    act = lambda z, m: F.relu(z) if m is None else z * m.double()
+    h = act(fe[0](x.double().cpu()), masks[0])
+    h = act(fe[2](h), masks[1])
+    h = act(fe[4](h), masks[2])
+    f = act(fe[7](h.flatten(1)), masks[3])
+    out = ref.actor(f)
+    v = ref.critic_ext(act(ref.extra_layer[0](f), masks[4])).squeeze(-1)
+    ((out * dout.double().cpu()).sum() + (v * dv.double().cpu()).sum()).backward()
+    return out.detach(), v.detach(), {n: p.grad.clone() for n, p in ref.named_parameters()}
 
 
 @pytest.mark.parametrize("B", [37, 600, 2048])
@@ -69,17 +107,21 @@ def test_px_training_pass_is_fp32_class(B):
     g = torch.Generator(device="cuda").manual_seed(B + 1)
     dout = torch.randn(B, 4, device="cuda", generator=g)
     dv = torch.randn(B, device="cuda", generator=g)
-    o_off, v_off, g_off, _ = _pass(net, flat, cv, x, dout, dv, False)
-    o_on, v_on, g_on, am = _pass(net, flat, cv, x, dout, dv, True)
+    m_off, m_on = [], []
+    o_off, v_off, g_off, _ = _pass(net, flat, cv, x, dout, dv, False, m_off)
+    o_on, v_on, g_on, am = _pass(net, flat, cv, x, dout, dv, True, m_on)
     assert am.px == [True, True, True, True, True], am.px  # h2, h3, g3, df, g2 all ran as planes
-    o64, v64, g64 = _fp64(ref, x, dout, dv)
+    # each pass against float64 with its own ReLU decisions (round 5: at 2,048 rows the wide fc forward's
+    # rounding put one critic hidden unit of one row on the other side of 0 than the f32-operand pass)
+    r_on, r_off = _fp64_masked(ref, x, dout, dv, m_on), _fp64_masked(ref, x, dout, dv, m_off)
     worst = []
-    for name, r in list(g64.items()) + [("out", o64), ("v", v64)]:
+    for name, r in list(r_on[2].items()) + [("out", r_on[0]), ("v", r_on[1])]:
         a = o_on if name == "out" else v_on if name == "v" else g_on[name]
         b = o_off if name == "out" else v_off if name == "v" else g_off[name]
+        rb = r_off[0] if name == "out" else r_off[1] if name == "v" else r_off[2][name]
         scale = r.abs().max().item() + 1e-30
         e_on = (a.cpu().double() - r).abs().max().item() / scale
-        e_off = (b.cpu().double() - r).abs().max().item() / scale
+        e_off = (b.cpu().double() - rb).abs().max().item() / scale
         worst.append((e_on / max(e_off, 1e-9), name, e_on, e_off))
         assert e_on <= 2 * e_off + 2e-7, (name, e_on, e_off)
     print("PX/off error ratios (worst 3):", sorted(worst, reverse=True)[:3])
