@@ -604,6 +604,23 @@ int ppox_icm_int_reward(const float* phi_s, const float* phi_n, const int32_t* a
                         int32_t n_actions, const float* seg, float eta, float* rewards, float* int_rewards,
                         void* stream);
 
+/* Data-parallel exchange (world > 1; replaces the per-minibatch torch.distributed all-reduces around the
+ * sharded update, ppo.py:241-244 — the reference is single-process).  The one exception to "never
+ * allocates": ppox_dp_comm_init creates the RCCL communicator, a stream and two events.
+ *   ppox_dp_load:       resolve RCCL from the library at rccl_path (the one the process already loaded).
+ *   ppox_dp_unique_id:  rank 0: the communicator id (ppox_dp_unique_id_bytes() bytes, host) every rank
+ *                       then passes to ppox_dp_comm_init (a collective call).
+ *   ppox_dp_all_reduce: in-place SUM of count elements (dtype 0 float32, 1 float64) on the communicator's
+ *                       stream after the work already on `stream`; wait != 0: `stream` waits for it.
+ *   ppox_dp_wait:       `stream` waits for every reduction issued so far. */
+int ppox_dp_load(const char* rccl_path);
+int ppox_dp_unique_id_bytes(void);
+int ppox_dp_unique_id(uint8_t* id_host);
+int ppox_dp_comm_init(const uint8_t* id_host, int32_t world, int32_t rank, int32_t device, void** comm_out);
+int ppox_dp_comm_destroy(void* comm);
+int ppox_dp_all_reduce(void* comm, void* buf, int64_t count, int32_t dtype, int32_t wait, void* stream);
+int ppox_dp_wait(void* comm, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -133,6 +133,7 @@ FORK_MERGE = os.environ.get("PPOX_FORK_MERGE", "0") == "1"
 # (after the dgrad, before wgrad1) instead of beside wgrad1 — 1 % slower (same-box A/B), but its
 # event time is then its own execution time
 BWD_SOLO_WGRAD2 = os.environ.get("PPOX_BWD_SOLO_WGRAD2", "0") != "0"
+SIDE_PRIO = os.environ.get("PPOX_SIDE_PRIO", "0" if os.environ.get("PPOX_TRAIN_PRIO") == "1" else "1") == "1"
 _side = {}
 
 
@@ -141,7 +142,11 @@ def side_stream(device, k=0):
     curiosity-module work beside the policy minibatch)."""
     s = _side.get((device, k))
     if s is None:
-        s = torch.cuda.Stream(device=device)
+        # high priority: HIP multiplexes the streams of one priority class over GPU_MAX_HW_QUEUES hardware
+        # queues, and two streams on one queue run in order — in the main stream's class (the default
+        # stream) a pooled stream may land on the main stream's queue, as it did once RCCL had created
+        # its streams (per-rank 196 -> 242 ms); PPOX_SIDE_PRIO=0: default priority
+        s = torch.cuda.Stream(device=device, priority=-1 if SIDE_PRIO else 0)
         _side[(device, k)] = s
     return s
 

@@ -1,0 +1,175 @@
+// The data-parallel gradient exchange issued from native code: one RCCL communicator per process over
+// the ranks of the job (xGMI within the node), its own stream and two events, and SUM all-reduces of
+// the flat gradient bucket / loss partials ordered against the caller's stream by events.  Replaces
+// the per-minibatch torch.distributed calls (ProcessGroupNCCL: tens of us of host per collective, which
+// made the dp-forced per-rank minibatch host-bound); the reference is single-process (SURVEY.md §2,
+// the sharded step is ppo.py:241-244).
+//
+// RCCL is resolved at run time from the library the process already has loaded (torch's librccl.so:
+// the caller passes its path), so one RCCL instance serves both torch's communicators and this one.
+#include <dlfcn.h>
+
+#include <cstdlib>
+#include <cstring>
+
+#include <rccl/rccl.h>
+
+#include "common.h"
+
+namespace {
+
+struct Rccl {
+    void* h = nullptr;
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+Rccl g_rccl;
+
+struct DpComm {
+    ncclComm_t comm = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ready = nullptr, done = nullptr;
+    int world = 0, rank = 0, device = 0;
+    bool inflight = false;  // an asynchronous reduction not yet waited for by a caller's stream
+};
+
+// A/B knobs: PPOX_DP_PRIO (default 1, 0 under PPOX_TRAIN_PRIO=1) the exchange stream's priority class;
+// PPOX_DP_DIRECT=0 the blocking form through the exchange stream too; PPOX_DP_SKIP=1 (diagnostic) no
+// RCCL call
+int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
+
+int rccl_fail(const char* what, ncclResult_t r) {
+    ppox::set_error("%s: %s", what, g_rccl.error_string ? g_rccl.error_string(r) : "rccl error");
+    return PPOX_EINVAL;
+}
+
+}  // namespace
+
+extern "C" int ppox_dp_load(const char* rccl_path) {
+    if (g_rccl.h) return PPOX_OK;
+    PPOX_REQUIRE(rccl_path && rccl_path[0], "ppox_dp_load: no library path");
+    void* h = dlopen(rccl_path, RTLD_NOW | RTLD_LOCAL);
+    PPOX_REQUIRE(h, "ppox_dp_load: %s", dlerror());
+    Rccl r;
+    r.h = h;
+    r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+    r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+    r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
+    r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
+    PPOX_REQUIRE(r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_reduce && r.error_string,
+                 "ppox_dp_load: %s lacks the RCCL entry points", rccl_path);
+    g_rccl = r;
+    return PPOX_OK;
+}
+
+extern "C" int ppox_dp_unique_id_bytes(void) { return NCCL_UNIQUE_ID_BYTES; }
+
+extern "C" int ppox_dp_unique_id(uint8_t* id_host) {
+    PPOX_REQUIRE(g_rccl.h, "ppox_dp_unique_id: ppox_dp_load first");
+    PPOX_REQUIRE(id_host, "ppox_dp_unique_id: null id");
+    ncclUniqueId id;
+    ncclResult_t r = g_rccl.get_unique_id(&id);
+    if (r != ncclSuccess) return rccl_fail("ncclGetUniqueId", r);
+    std::memcpy(id_host, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return PPOX_OK;
+}
+
+extern "C" int ppox_dp_comm_init(const uint8_t* id_host, int32_t world, int32_t rank, int32_t device, void** comm_out) {
+    PPOX_REQUIRE(g_rccl.h, "ppox_dp_comm_init: ppox_dp_load first");
+    PPOX_REQUIRE(id_host && comm_out, "ppox_dp_comm_init: null argument");
+    PPOX_REQUIRE(world >= 1 && rank >= 0 && rank < world && device >= 0,
+                 "ppox_dp_comm_init: rank %d of world %d on device %d", rank, world, device);
+    *comm_out = nullptr;
+    PPOX_HIP(hipSetDevice(device), "ppox_dp_comm_init");
+    ncclUniqueId id;
+    std::memcpy(id.internal, id_host, NCCL_UNIQUE_ID_BYTES);
+    auto* c = new DpComm;
+    c->world = world, c->rank = rank, c->device = device;
+    ncclResult_t r = g_rccl.comm_init_rank(&c->comm, world, id, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return rccl_fail("ncclCommInitRank", r);
+    }
+    // the exchange overlaps the conv backward (the fc + head bucket starts while the conv dgrads run).
+    // HIP multiplexes the streams of one priority class over GPU_MAX_HW_QUEUES hardware queues, and two
+    // streams on one queue run in order: a stream sharing the main stream's queue would hold the main
+    // stream's later kernels behind its wait for the side stream (per-rank 196 -> 242 ms measured).  So
+    // the stream is high-priority, the class of the backward's side stream (convs.side_stream), and the
+    // main stream (the default stream) is not
+    int lo = 0, hi = 0;
+    hipDeviceGetStreamPriorityRange(&lo, &hi);
+    const int high = env_int("PPOX_DP_PRIO", env_int("PPOX_TRAIN_PRIO", 0) ? 0 : 1);
+    hipError_t e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, high ? hi : lo);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        g_rccl.comm_destroy(c->comm);
+        delete c;
+        ppox::set_error("ppox_dp_comm_init: %s", hipGetErrorString(e));
+        return -static_cast<int>(e);
+    }
+    *comm_out = c;
+    return PPOX_OK;
+}
+
+extern "C" int ppox_dp_comm_destroy(void* comm) {
+    if (!comm) return PPOX_OK;
+    auto* c = static_cast<DpComm*>(comm);
+    PPOX_HIP(hipStreamSynchronize(c->stream), "ppox_dp_comm_destroy");
+    ncclResult_t r = g_rccl.comm_destroy(c->comm);
+    hipEventDestroy(c->ready);
+    hipEventDestroy(c->done);
+    hipStreamDestroy(c->stream);
+    delete c;
+    return r == ncclSuccess ? PPOX_OK : rccl_fail("ncclCommDestroy", r);
+}
+
+// SUM all-reduce of buf (in place) after the work already on `stream`.  wait == 0: on the
+// communicator's stream (the caller joins later with ppox_dp_wait); wait != 0, the blocking form: on
+// `stream` itself (each cross-stream event hop idles the GPU several us: per-rank 213 -> 198 ms), after
+// `stream` has waited for an asynchronous reduction still in flight — the communicator's reductions
+// never overlap each other and run in issue order, the order every rank issues them in.
+extern "C" int ppox_dp_all_reduce(void* comm, void* buf, int64_t count, int32_t dtype, int32_t wait, void* stream) {
+    PPOX_REQUIRE(comm, "ppox_dp_all_reduce: null communicator");
+    PPOX_REQUIRE(count >= 0 && (count == 0 || buf), "ppox_dp_all_reduce: %lld elements at %p", (long long)count, buf);
+    PPOX_REQUIRE(dtype == 0 || dtype == 1, "ppox_dp_all_reduce: dtype %d (0 = float32, 1 = float64)", dtype);
+    auto* c = static_cast<DpComm*>(comm);
+    hipStream_t s = ppox::as_stream(stream);
+    if (count == 0) return PPOX_OK;
+    static const int direct = env_int("PPOX_DP_DIRECT", 1), skip = env_int("PPOX_DP_SKIP", 0);
+    if (wait && direct) {
+        if (c->inflight) {
+            PPOX_HIP(hipStreamWaitEvent(s, c->done, 0), "ppox_dp_all_reduce");
+            c->inflight = false;
+        }
+        ncclResult_t r = skip ? ncclSuccess : g_rccl.all_reduce(buf, buf, static_cast<size_t>(count),
+                                                                 dtype ? ncclFloat64 : ncclFloat32, ncclSum, c->comm, s);
+        return r == ncclSuccess ? PPOX_OK : rccl_fail("ncclAllReduce", r);
+    }
+    PPOX_HIP(hipEventRecord(c->ready, s), "ppox_dp_all_reduce");
+    PPOX_HIP(hipStreamWaitEvent(c->stream, c->ready, 0), "ppox_dp_all_reduce");
+    ncclResult_t r = skip ? ncclSuccess : g_rccl.all_reduce(buf, buf, static_cast<size_t>(count),
+                                                             dtype ? ncclFloat64 : ncclFloat32, ncclSum, c->comm, c->stream);
+    if (r != ncclSuccess) return rccl_fail("ncclAllReduce", r);
+    PPOX_HIP(hipEventRecord(c->done, c->stream), "ppox_dp_all_reduce");
+    if (wait) PPOX_HIP(hipStreamWaitEvent(s, c->done, 0), "ppox_dp_all_reduce");
+    c->inflight = !wait;
+    return PPOX_OK;
+}
+
+// `stream` waits for every reduction issued on the communicator so far.
+extern "C" int ppox_dp_wait(void* comm, void* stream) {
+    PPOX_REQUIRE(comm, "ppox_dp_wait: null communicator");
+    auto* c = static_cast<DpComm*>(comm);
+    PPOX_HIP(hipStreamWaitEvent(ppox::as_stream(stream), c->done, 0), "ppox_dp_wait");
+    c->inflight = false;
+    return PPOX_OK;
+}

@@ -15,6 +15,19 @@ import torch
 import torch.distributed as tdist
 
 
+# the per-minibatch all-reduces through native code (csrc/dp.cpp) instead of torch.distributed
+NATIVE_DP = os.environ.get("PPOX_NATIVE_DP", "1") != "0"
+_dp_comm = None
+
+
+class _NativeWork:
+    def __init__(self, comm):
+        self.comm = comm
+
+    def wait(self):
+        self.comm.wait()
+
+
 class DistContext:
     def __init__(self, rank=0, world=1, group=None):
         self.rank, self.world, self.group = rank, world, group
@@ -38,15 +51,44 @@ class DistContext:
             return self
         return DistContext(self.rank, self.world, group=tdist.new_group(ranks=list(range(self.world))))
 
+    def _native(self, t):
+        """The process's native RCCL communicator (native.DpComm) when `t` can go through it: the
+        default group on the RCCL backend, a float32 / float64 device tensor (PPOX_NATIVE_DP=0: torch's
+        collectives throughout).  Created on first use — a collective call, made by every rank at its
+        first such all-reduce, in the same order."""
+        global _dp_comm
+        if (self.group is not None or not NATIVE_DP or not t.is_cuda or t.dtype not in (torch.float32, torch.float64)
+                or not t.is_contiguous()):
+            return None
+        if _dp_comm is None:
+            if tdist.get_backend() != "nccl":
+                return None
+            import native
+
+            def bcast(b):
+                buf = torch.tensor(list(b), dtype=torch.uint8, device=t.device)
+                tdist.broadcast(buf, 0)
+                return bytes(buf.cpu().numpy())
+            _dp_comm = native.DpComm(tdist.get_world_size(), tdist.get_rank(), t.device.index, bcast)
+        return _dp_comm
+
     def all_reduce_(self, t):
         if self.enabled:
+            comm = self._native(t)
+            if comm is not None:
+                return comm.all_reduce_(t)
             tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=self.group)
         return t
 
     def all_reduce_async_(self, t):
         """Start a SUM all-reduce of `t` ordered after the work already on the current
-        stream; returns the work handle (None at world 1).  Call .wait() before reading t."""
+        stream; returns the work handle (None at world 1).  Call .wait() before reading t:
+        the then-current stream waits for it."""
         if self.enabled:
+            comm = self._native(t)
+            if comm is not None:
+                comm.all_reduce_(t, wait=False)
+                return _NativeWork(comm)
             return tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=self.group, async_op=True)
         return None
 

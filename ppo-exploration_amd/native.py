@@ -107,6 +107,13 @@ SIGNATURES = {
     "ppox_icm_grad_reduce": [_vp, _i64, _i64, _i32, _f32, _i64, _vp, _vp, _vp],
     "ppox_icm_enc_wgrad": [_vp, _vp, _i64, _i64, _vp, _vp, _vp],
     "ppox_icm_int_reward": [_vp, _vp, _vp, _i64, _i32, _vp, _f32, _vp, _vp, _vp],
+    "ppox_dp_load": [ctypes.c_char_p],
+    "ppox_dp_unique_id_bytes": [],
+    "ppox_dp_unique_id": [_vp],
+    "ppox_dp_comm_init": [_vp, _i32, _i32, _i32, ctypes.POINTER(_vp)],
+    "ppox_dp_comm_destroy": [_vp],
+    "ppox_dp_all_reduce": [_vp, _vp, _i64, _i32, _i32, _vp],
+    "ppox_dp_wait": [_vp, _vp],
 }
 _RESTYPES = {"ppox_version": ctypes.c_char_p, "ppox_last_error": ctypes.c_char_p,
              "ppox_rms_u8_workspace_bytes": ctypes.c_int64, "ppox_nature_wgrad_splits": ctypes.c_int64,
@@ -937,3 +944,50 @@ def icm_int_reward(phi_s, phi_n, actions, N, n_actions, seg, eta, rewards, int_r
     call("ppox_icm_int_reward", _p(phi_s), _p(phi_n), ptr(actions, torch.int32, name="actions"), int(N),
          int(n_actions), _p(seg), float(eta), ptr(rewards, torch.float32, name="rewards"),
          ptr(int_rewards, torch.float32, name="int_rewards"), stream_ptr(stream))
+
+
+# ---------------------------------------------------------------------------
+# Data-parallel exchange (RCCL from native code; dist.DistContext drives it)
+# ---------------------------------------------------------------------------
+def rccl_path():
+    """The RCCL library torch loaded (torch/lib/librccl.so on ROCm builds)."""
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    if not os.path.exists(p):
+        raise ImportError(f"no RCCL at {p}")
+    return p
+
+
+class DpComm:
+    """One RCCL communicator over the job's ranks with its own stream (csrc/dp.cpp).  Construct on every
+    rank in the same order: `broadcast_id(buf)` must hand rank 0's id bytes to every rank (a collective
+    over the process group that already exists)."""
+
+    def __init__(self, world, rank, device, broadcast_id):
+        l = lib()
+        call("ppox_dp_load", rccl_path().encode())
+        n = l.ppox_dp_unique_id_bytes()
+        buf = (ctypes.c_uint8 * n)()
+        if rank == 0:
+            call("ppox_dp_unique_id", buf)
+        buf = (ctypes.c_uint8 * n).from_buffer_copy(broadcast_id(bytes(buf)))
+        h = _vp()
+        call("ppox_dp_comm_init", buf, world, rank, device, ctypes.byref(h))
+        self.handle, self.world, self.rank = h, world, rank
+
+    def all_reduce_(self, t, wait=True, stream=None):
+        """In-place SUM over ranks of a contiguous float32 / float64 device tensor, ordered after the work on
+        `stream` (default: the current stream); wait: that stream waits for it (else join with wait())."""
+        dt = 0 if t.dtype == torch.float32 else 1 if t.dtype == torch.float64 else None
+        if dt is None or not t.is_cuda or not t.is_contiguous():
+            raise TypeError(f"DpComm.all_reduce_: contiguous float32/float64 device tensor, got {t.dtype} "
+                            f"on {t.device}")
+        call("ppox_dp_all_reduce", self.handle, _p(t), t.numel(), dt, 1 if wait else 0, stream_ptr(stream))
+        return t
+
+    def wait(self, stream=None):
+        call("ppox_dp_wait", self.handle, stream_ptr(stream))
+
+    def close(self):
+        if self.handle:
+            call("ppox_dp_comm_destroy", self.handle)
+            self.handle = None

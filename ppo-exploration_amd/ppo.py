@@ -308,9 +308,9 @@ class BaseAlgorithm:
                 net.backward_train(ctx, dout, dv, div, dense_ready=start)
             else:
                 start()
-            self.dist.all_reduce_(self.flat.grad[:n0])
-            for w in work:
+            for w in work:  # (the communicator's reductions run one at a time, in issue order)
                 w.wait()
+            self.dist.all_reduce_(self.flat.grad[:n0])
             return
         if has_rows:
             self._bwd_train(ctx, out, v, iv, dout, dv, div)

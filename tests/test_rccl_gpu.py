@@ -3,9 +3,10 @@ paths forced on: owned-row minibatches, the loss-partials all-reduce, the two-pi
 all-reduce started asynchronously from the backward's side stream, all_gather_cat of the
 rollout statistics, PPO_ICM's feature / action / feature-gradient exchange (float32 and int32
 all-reduces) and PPO_RND's gathered obs_rms.  The update must equal the single-process one —
-every collective is a sum over one rank.  The driver's multi-GPU runs (one rank per GPU) use this
-backend; RCCL cannot put two ranks on one device, so this is the RCCL coverage one GPU allows
-(the 2-rank decomposition itself is tests/test_dist_gpu.py, over gloo)."""
+every collective is a sum over one rank.  The float all-reduces of the default group run on the
+native communicator (native.DpComm, csrc/dp.cpp), the rest on torch's.  The driver's multi-GPU
+runs (one rank per GPU) use this backend; RCCL cannot put two ranks on one device, so this is the
+RCCL coverage one GPU allows (the 2-rank decomposition itself is tests/test_dist_gpu.py, over gloo)."""
 import os
 import socket
 
@@ -56,7 +57,23 @@ def _rank(port, algo, cfg, q):
         tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
         import dist
         dist.DistContext.enabled = property(lambda self: True)  # the world > 1 code paths on one rank
-        q.put(_train(algo, cfg))
+        res = _train(algo, cfg)
+        # the per-minibatch all-reduces went through the native communicator (csrc/dp.cpp)
+        comm = dist._dp_comm
+        assert comm is not None and comm.world == 1, "native RCCL communicator not used"
+        x = torch.arange(1000, dtype=torch.float64, device="cuda")
+        y = x.clone()
+        comm.all_reduce_(y)
+        z = torch.full((4097,), 0.5, device="cuda")
+        comm.all_reduce_(z, wait=False)
+        comm.wait()
+        assert torch.equal(x, y) and bool((z == 0.5).all())
+        try:
+            comm.all_reduce_(torch.zeros(4, dtype=torch.int32, device="cuda"))
+            raise AssertionError("int32 accepted")
+        except TypeError:
+            pass
+        q.put(res)
     except Exception as e:  # surface the failure to the parent
         q.put(repr(e))
     finally:
