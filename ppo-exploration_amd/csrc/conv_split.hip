@@ -51,6 +51,19 @@ __device__ uint32_t kFwd1Dummy[128];  // store target of the rows past the batch
 #ifndef FWD1_FAST_EPI
 #define FWD1_FAST_EPI 1  // the H1P epilogue's whole-tile form (round 4); 0: the per-row form for every tile
 #endif
+// the H1P epilogue's stores non-temporal (streaming: h1 is read back from HBM by the conv2 forward
+// and weight gradient, not from L2): 1-GPU line +1.0-1.2 % A/B (conv2 forward 281 -> 270 us at 16,384
+// rows, the conv1 forward itself unchanged), profiles/r05y.  The direct kernels' stores made
+// non-temporal the same way ran 4x slower (their counted vmcnt waits include the stores).
+#ifndef FWD1_NT
+#define FWD1_NT 1
+#endif
+__device__ inline void fwd1_store(uint32_t* p, uint32_t v) {
+    if constexpr (FWD1_NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
 template <int MT, bool PLANES = false, bool IDX = false>
 __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a, unsigned tiles_per_wave) {
     using L = G1;
@@ -190,9 +203,10 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
                         const uint32_t pl = (uint32_t)__builtin_amdgcn_mov_dpp((int)l, 0xB1, 0xF, 0xF, false);
                         const uint32_t lo_w = odd ? pl : h, hi_w = odd ? l : ph;  // (low half, high half) sources
                         const int r0 = (e & 3) + 8 * (e >> 2);                    // row of e; e + 1 is the next
-                        *reinterpret_cast<uint32_t*>(yb + r0 * (2 * L::COUT)) = __builtin_amdgcn_perm(hi_w, lo_w, 0x05040100u);
-                        *reinterpret_cast<uint32_t*>(yb + (r0 + 1) * (2 * L::COUT)) =
-                            __builtin_amdgcn_perm(hi_w, lo_w, 0x07060302u);
+                        fwd1_store(reinterpret_cast<uint32_t*>(yb + r0 * (2 * L::COUT)),
+                                   __builtin_amdgcn_perm(hi_w, lo_w, 0x05040100u));
+                        fwd1_store(reinterpret_cast<uint32_t*>(yb + (r0 + 1) * (2 * L::COUT)),
+                                   __builtin_amdgcn_perm(hi_w, lo_w, 0x07060302u));
                         if (a.bits_y) {  // uniform
                             const unsigned long long b0 = __ballot(v2.x > 0.f), b1 = __ballot(v2.y > 0.f);
                             word = eL == e ? (uint32_t)(hL ? b0 >> 32 : b0) : word;

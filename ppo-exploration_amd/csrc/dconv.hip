@@ -34,6 +34,21 @@
 
 namespace {
 
+// PPOX_NT_OUT=1 (A/B): the direct kernels' activation / gradient outputs stored non-temporal (streaming:
+// written once, read by the next kernel from HBM)
+#ifndef PPOX_NT_OUT
+#define PPOX_NT_OUT 0
+#endif
+constexpr int NT_AUX = PPOX_NT_OUT ? 2 : 0;  // the buffer stores' cache-policy bits (nt)
+typedef unsigned int nt_u2 __attribute__((ext_vector_type(2)));
+__device__ inline void out_store2(void* p, uint32_t x, uint32_t y) {
+    if constexpr (PPOX_NT_OUT)
+        __builtin_nontemporal_store((nt_u2){x, y}, reinterpret_cast<nt_u2*>(p));
+    else
+        *reinterpret_cast<uint2*>(p) = make_uint2(x, y);
+}
+
+
 #ifndef DCONV_GLOBAL_DMA
 #define DCONV_GLOBAL_DMA 0
 #endif
@@ -260,8 +275,8 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
         split2h((f32x2){y[2], y[3]}, 1.f, hw[1], lw[1]);
         uint8_t* dst = yb + ((uint32_t)pmb * 256u + ylane + 16 * t);
         if (decltype(FULL)::value || pmb + r < MR) {
-            *reinterpret_cast<uint2*>(dst) = make_uint2(hw[0], hw[1]);
-            *reinterpret_cast<uint2*>(dst + 64) = make_uint2(lw[0], lw[1]);
+            out_store2(dst, hw[0], hw[1]);
+            out_store2(dst + 64, lw[0], lw[1]);
         }
     };
     auto epi_mask = [&](auto T, const float (&y)[4], int& bw) {
@@ -513,8 +528,8 @@ __global__ void __launch_bounds__(256, 1) fcd_kernel(Args a, const u32x4* __rest
         const long long m = r0 + pmb + r;
         uint16_t* dst = y16 + 2 * (m * FCD_N + Tc * 32) + 8 * t + 4 * h;
         if (decltype(FULL)::value || pmb + r < MR) {
-            *reinterpret_cast<uint2*>(dst) = make_uint2(hw[0], hw[1]);
-            *reinterpret_cast<uint2*>(dst + 32) = make_uint2(lw[0], lw[1]);
+            out_store2(dst, hw[0], hw[1]);
+            out_store2(dst + 32, lw[0], lw[1]);
         }
         om = max(om, max(max(__float_as_uint(y[0]) & 0x7FFFFFFFu, __float_as_uint(y[1]) & 0x7FFFFFFFu),
                          max(__float_as_uint(y[2]) & 0x7FFFFFFFu, __float_as_uint(y[3]) & 0x7FFFFFFFu)));
@@ -784,7 +799,7 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
         }
         __builtin_amdgcn_raw_buffer_store_b128(
             u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])}, o_rs,
-            (uint32_t)o + (uint32_t)(32 * t + 16 * h), 0, 0);
+            (uint32_t)o + (uint32_t)(32 * t + 16 * h), 0, NT_AUX);
         om = fmaxf(om, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
     };
     // refill DMAs (at most one sample per phase: 64 rows < 100) over k-steps 9 .. 14
@@ -1436,8 +1451,8 @@ __global__ void __launch_bounds__(256, 1) ddgrad3_kernel(Args a, const u32x4* __
         split2h((f32x2){y[0], y[1]}, 1.f, hw[0], lw[0]);
         split2h((f32x2){y[2], y[3]}, 1.f, hw[1], lw[1]);
         const uint32_t o = (uint32_t)po + ylane + 16 * t;
-        __builtin_amdgcn_raw_buffer_store_b64((w3u2){hw[0], hw[1]}, o_rs, o, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b64((w3u2){lw[0], lw[1]}, o_rs, o + 64, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64((w3u2){hw[0], hw[1]}, o_rs, o, 0, NT_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64((w3u2){lw[0], lw[1]}, o_rs, o + 64, 0, NT_AUX);
         om = max(om, max(max(__float_as_uint(y[0]) & 0x7FFFFFFFu, __float_as_uint(y[1]) & 0x7FFFFFFFu),
                          max(__float_as_uint(y[2]) & 0x7FFFFFFFu, __float_as_uint(y[3]) & 0x7FFFFFFFu)));
     };
