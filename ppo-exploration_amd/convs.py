@@ -507,21 +507,25 @@ class NatureConvs:
         else:
             native.nature_conv_wgrad(layer, x, B, None, 0, 0, stride, g, self.workspace(layer, B), dw, db, stream=stream)
 
-    def forward_acts(self, x, train=False, px=None):
+    def forward_acts(self, x, train=False, px=None, table=None):
         """Trunk forward: (h1 NHWC, h2 NHWC, h3, am) — activations (ReLU applied) and the pass's
         PassState (the amax table's AM_* rows — the backward of the same pass records its
         gradients' rows — and, for a `train` pass, conv1's ReLU bitmask); h3 is
         NHWC (B, 7, 7, 64) in split math (self.nhwc3), NCHW (B, 64, 7, 7) in f32 math.  px (default
         self.px): h2 / h3 as PX planes (int16 (B, 9, 9, 128) / (B, 7, 7, 128)) where their consumers
-        allow; am.px says which."""
+        allow; am.px says which.  table: an already zeroed (AM_ROWS, AMAX_SLOTS) int32 amax table for the pass
+        (the collect graph's per-step tables, zeroed by one fill per rollout)."""
         B = x.shape[0]
         dev = x.device
         px = (self.px if px is None else (px and self.px)) and B >= PX_MIN_BATCH
         # the pass's amax table: zeroed by the weight packing when this pass runs it (the first
         # pass after an optimizer step), by a fill otherwise
-        table = torch.empty((AM_ROWS, native.AMAX_SLOTS), dtype=torch.int32, device=dev)
-        if not self.pack(B, zero=table):
-            table.zero_()
+        if table is not None:
+            self.pack(B)
+        else:
+            table = torch.empty((AM_ROWS, native.AMAX_SLOTS), dtype=torch.int32, device=dev)
+            if not self.pack(B, zero=table):
+                table.zero_()
         h1 = self.empty_h1(B, dev)
         px2, px3 = px, px and self.px_h3(B, train)
         h2 = torch.empty((B, 9, 9, 128), dtype=torch.int16, device=dev) if px2 else torch.empty((B, 9, 9, 64), device=dev)

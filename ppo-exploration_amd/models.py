@@ -110,11 +110,16 @@ class CnnActorCritic(nn.Module):
     def trunk(self, x):
         return self._trunk_am(x)[0]
 
-    def _trunk_am(self, x):
-        """(f, the pass's amax table or None)"""
+    def _trunk_am(self, x, table=None, actor=False):
+        """(f, the pass's amax table or None[, the actor's logits or None when `actor`]); table: a zeroed
+        amax table for the pass (convs.NatureConvs.forward_acts)"""
         if self.conv_impl is not None and self.conv_impl.math != "f32" and not torch.is_grad_enabled():
-            # inference (collect): the split-f16 fc GEMM straight off the conv trunk
-            h1, h2, h3, am = self.conv_impl.forward_acts(x.contiguous())
+            # inference (collect): the split-f16 fc GEMM straight off the conv trunk (the split-K form's
+            # reduce also runs the actor head)
+            h1, h2, h3, am = self.conv_impl.forward_acts(x.contiguous(), table=table)
+            if actor:
+                f, logits = self.conv_impl.fc_forward(h3, am, actor=(self.actor[0].weight, self.actor[0].bias))
+                return f, am, logits
             return self.conv_impl.fc_forward(h3, am), am
         if self.conv_impl is not None:
             h = self.conv_impl(x)
@@ -124,12 +129,16 @@ class CnnActorCritic(nn.Module):
             h = F.relu(fe[2](h))
             h = F.relu(fe[4](h))
         fc = self.feature_extractor[7]
-        return F.relu(F.linear(h.flatten(1), fc.weight, fc.bias)), None
+        f = F.relu(F.linear(h.flatten(1), fc.weight, fc.bias))
+        return (f, None, None) if actor else (f, None)
 
-    def forward(self, x):
-        f, am = self._trunk_am(x)
+    def forward(self, x, value_out=None, table=None):
+        """(actor logits, value, int value).  Inference (collect) only: value_out, a (B,) float32 buffer the value
+        is written to (the rollout's row: no copy), table a zeroed amax table for the pass."""
         if not torch.is_grad_enabled():  # collect: the same head kernels as forward_train
-            return self._heads(f, am)[:3]
+            f, am, logits = self._trunk_am(x, table, actor=True)
+            return self._heads(f, am, out=logits, value_out=value_out)[:3]
+        f, am = self._trunk_am(x)
         v = self.critic_ext(self.extra_layer(f)).squeeze(-1)
         iv = self.critic_int(self.int_extra_layer(f)).squeeze(-1) if self.intrinsic else None
         return self.actor(f), v, iv
@@ -154,10 +163,10 @@ class CnnActorCritic(nn.Module):
             out, v, iv, e, ie = self._heads(f, am, out=logits)
         return out, v, iv, (x, h1, h2, h3, f, e, ie, am)
 
-    def _heads(self, f, am=None, out=None):
-        """actor logits (unless `out` already holds them), value, int value, and the hidden
-        activations (no autograd): fused bias+ReLU GEMMs for the 512-wide layers (the extra layer on
-        the split-f16 kernel for large batches: f's amax in am), skinny-row kernels for the narrow heads."""
+    def _heads(self, f, am=None, out=None, value_out=None):
+        """actor logits (unless `out` already holds them), value (into value_out when given), int value, and
+        the hidden activations (no autograd): fused bias+ReLU GEMMs for the 512-wide layers (the extra layer
+        on the split-f16 kernel for large batches: f's amax in am), skinny-row kernels for the narrow heads."""
         a, el, ce = self.actor[0], self.extra_layer[0], self.critic_ext
         if out is None:
             out = native.head_linear(f, a.weight, a.bias)
@@ -176,13 +185,16 @@ class CnnActorCritic(nn.Module):
             cv.pack(B)
             e = torch.empty_like(f)
             fuse = ce.weight.is_contiguous() and ce.weight.data_ptr() % 16 == 0
-            v = torch.empty(B, device=f.device) if fuse else None
+            v = (value_out if value_out is not None else torch.empty(B, device=f.device)) if fuse else None
             native.head_hidden_fwd_splitk(f, cv.qh[0], el.bias, cv.head_fwd_ws(B), e, amax_f=am[_convs.AM_F],
                                           critic=(ce.weight, ce.bias) if fuse else None, value=v)
         else:
             e = linear_relu(f, el.weight, el.bias)
         if v is None:
             v = native.head_linear(e, ce.weight, ce.bias).squeeze(-1)
+            if value_out is not None:
+                value_out.copy_(v)
+                v = value_out
         ie = iv = None
         if self.intrinsic:
             il, ci = self.int_extra_layer[0], self.critic_int

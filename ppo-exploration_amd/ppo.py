@@ -528,6 +528,7 @@ class PPO(BaseAlgorithm):
         # the collect step loop as one captured graph (PPOX_COLLECT_GRAPH=0: eager launches)
         self._collect_graph_enabled = os.environ.get("PPOX_COLLECT_GRAPH", "1") != "0"
         self._cgraph = None
+        self._ctables = None
 
     def _collect_graph_ok(self):
         return (self._collect_graph_enabled and isinstance(self.env, DeviceAtariEnv) and self.discrete
@@ -551,10 +552,13 @@ class PPO(BaseAlgorithm):
         """Step t of the collect loop with both Philox counters read on the device
         (self._ctr = [sample counter, env step] at the rollout's start)."""
         ro = self.rollout
-        out, v, _ = self.policy.net(ro.obs_slots[t])
+        # the value straight into the rollout row, the pass's amax table one of the graph's pre-zeroed ones
+        out, v, _ = self.policy.net(ro.obs_slots[t], value_out=ro.values[t],
+                                    table=self._ctables[t] if self._ctables is not None else None)
         native.categorical_sample_dc(out, self.local_envs, self.n_actions, self.env_offset, self.seed, self._ctr[0:1],
                                      t, ro.actions[t], ro.log_probs[t])
-        ro.values[t].copy_(v)
+        if v.data_ptr() != ro.values[t].data_ptr():
+            ro.values[t].copy_(v)
         self.env.step_into_dc(ro.obs_slots[t], ro.obs_slots[t + 1], ro.actions[t], ro.rewards[t], ro.masks[t],
                               ro.done_ret[t], ro.done_len[t], self._ctr[1:2], t + 1)
 
@@ -568,6 +572,8 @@ class PPO(BaseAlgorithm):
         if self._cgraph is None:
             self._collect_steps_eager()
             self._ctr = torch.zeros(2, dtype=torch.int64, device=self.device)
+            # one amax table per step, zeroed by one fill per rollout instead of a fill node per step
+            self._ctables = torch.zeros((T, convs.AM_ROWS, native.AMAX_SLOTS), dtype=torch.int32, device=self.device)
             g = torch.cuda.CUDAGraph()
             with torch.no_grad(), torch.cuda.graph(g):
                 for t in range(T):
@@ -577,6 +583,7 @@ class PPO(BaseAlgorithm):
         self.policy.net.conv_impl.pack(self.local_envs)
         self._ctr[0].fill_(self._sample_counter)
         self._ctr[1].fill_(env.k)
+        self._ctables.zero_()
         self._cgraph.replay()
         self._sample_counter += T
         env.k += T
@@ -845,6 +852,7 @@ class PPO_ICM(BaseAlgorithm):
         # (PPOX_COLLECT_GRAPH=0: eager launches)
         self._collect_graph_enabled = os.environ.get("PPOX_COLLECT_GRAPH", "1") != "0"
         self._cgraph = None
+        self._ctables = None
         self._ir_sum = torch.zeros((), dtype=torch.float64, device=self.device)
 
     def _collect_graph_ok(self):
@@ -856,10 +864,13 @@ class PPO_ICM(BaseAlgorithm):
         """Step t of the collect loop with device-resident Philox counters (as PPO._collect_step_dc)
         plus the K11 curiosity reward; phi(s_t) is in tag c0 / c1 by the parity of t."""
         ro = self.rollout
-        out, v, _ = self.policy.net(ro.obs_slots[t])
+        # the value straight into the rollout row, the pass's amax table one of the graph's pre-zeroed ones
+        out, v, _ = self.policy.net(ro.obs_slots[t], value_out=ro.values[t],
+                                    table=self._ctables[t] if self._ctables is not None else None)
         native.categorical_sample_dc(out, self.local_envs, self.n_actions, self.env_offset, self.seed, self._ctr[0:1],
                                      t, ro.actions[t], ro.log_probs[t])
-        ro.values[t].copy_(v)
+        if v.data_ptr() != ro.values[t].data_ptr():
+            ro.values[t].copy_(v)
         self.env.step_into_dc(ro.obs_slots[t], ro.obs_slots[t + 1], ro.actions[t], ro.rewards[t], ro.masks[t],
                               ro.done_ret[t], ro.done_len[t], self._ctr[1:2], t + 1)
         if t == 0:
@@ -889,6 +900,7 @@ class PPO_ICM(BaseAlgorithm):
             self._ctr[0].fill_(self._sample_counter)
             self._ctr[1].fill_(env.k)
             self._ir_sum.zero_()
+            self._ctables.zero_()
             self._cgraph.replay()
             self._sample_counter += T
             env.k += T
@@ -897,6 +909,8 @@ class PPO_ICM(BaseAlgorithm):
             self._collect_eager()
             if self._collect_graph_ok():  # capture after the first (eager) rollout
                 self._ctr = torch.zeros(2, dtype=torch.int64, device=self.device)
+                self._ctables = torch.zeros((self.nstep, convs.AM_ROWS, native.AMAX_SLOTS), dtype=torch.int32,
+                                            device=self.device)
                 g = torch.cuda.CUDAGraph()
                 nat, eta = self._icm_native, self.int_rew_integration
                 with torch.no_grad(), torch.cuda.graph(g):
