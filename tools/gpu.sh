@@ -23,8 +23,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-KRX="wgrad|gae|gemm|split_kernel|colp_kernel|planes|dconv|fcd_kernel|dgrad2"
-SQRX="sgemm|wgrad|colp|fwd1|dconv|fcd_kernel|dgrad2"
+KRX="wgrad|gae|gemm|split_kernel|colp_kernel|planes|dconv|fcd_kernel|dgrad2|ddgrad3|fcw_kernel|hbw_kernel"
+SQRX="sgemm|wgrad|colp|fwd1|dconv|fcd_kernel|dgrad2|ddgrad3|fcw_kernel|hbw_kernel"
 RANK="--envs 512 --batch-size 2048"
 
 bench() {  # bench NAME OUTFILE ARGS...   (the step's VAR=value settings from $ENVS)
