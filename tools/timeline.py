@@ -1,6 +1,7 @@
 """One minibatch's kernel timeline from a rocprofv3 --kernel-trace csv (dev tool): every launch
 between two Adam steps of the last iteration, start / end (us from the previous Adam's end), duration,
-queue, and the busy / idle time of the union.  Usage: python tools/timeline.py kernel_trace.csv [k-th from end]"""
+queue, and the busy / idle time of the union.  Usage: python tools/timeline.py kernel_trace.csv [k-th from end;
+-k: the k-th from the start]"""
 import csv
 import sys
 
