@@ -13,8 +13,6 @@
 #                    sets environment variables (e.g. R=PPOX_DCONV2=0); each line -> NAME[_n].json
 #   prof16k          rocprofv3 --kernel-trace --stats of the 1-GPU bench + one 16,384-row minibatch timeline
 #   profrank[D]      the same at the per-rank shape (D: dp branches forced on) + one 2,048-row minibatch timeline
-#   hsrank[D]        profrank with the GPU held back 150 ms per train() (tools/headstart_bench.py): the 40th
-#                    minibatch's timeline is the GPU's own schedule, not the profiler-slowed host's
 #   pmc16k / pmcrank FETCH_SIZE / WRITE_SIZE passes (2*FETCH + WRITE per launch) -> pmc_summary{,_rank}.json
 #   sq16k / sqrank   SQ counter passes of the MFMA kernels (tools/kernel_pmc.sh)
 #   hostlag[D]       tools/host_lag.py at the per-rank shape (PPO; D: dp branches on)
@@ -39,7 +37,7 @@ bench() {  # bench NAME OUTFILE ARGS...   (the step's VAR=value settings from $E
 trace() {  # trace NAME BACK ARGS... -> stats + timeline of the BACK-th minibatch from the end
   local name=$1 back=$2; shift 2
   ( cd /tmp && env $ENVS timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/$TAG-$name -o run --output-format csv -- \
-      python3 $R/${TRACE_SCRIPT:-bench.py} "$@" > $O/${name}_bench_under_rocprof.json 2> $O/$name.err ) || return 1
+      python3 $R/bench.py "$@" > $O/${name}_bench_under_rocprof.json 2> $O/$name.err ) || return 1
   local T=$(find /tmp/$TAG-$name -name "*kernel_trace.csv" | head -n 1)
   find /tmp/$TAG-$name -name "*kernel_stats.csv" -exec cp {} $O/${name}_kernel_stats.csv \; || return 1
   python3 $R/tools/trace_by_grid.py $T $O/${name}_kernel_by_grid.csv || return 1
@@ -90,8 +88,6 @@ for STEP in "$@"; do
     prof16k) trace $OUT 3 --steps 2 --warmup 1 --no-cpu-baseline || exit 1 ;;
     profrank) trace $OUT 3 $RANK --steps 2 --warmup 1 --no-cpu-baseline || exit 1 ;;
     profrankD) trace $OUT 3 $RANK --steps 2 --warmup 1 --no-cpu-baseline --force-dist || exit 1 ;;
-    hsrank) TRACE_SCRIPT=tools/headstart_bench.py trace $OUT -40 $RANK --steps 1 --warmup 1 --no-cpu-baseline || exit 1 ;;
-    hsrankD) TRACE_SCRIPT=tools/headstart_bench.py trace $OUT -40 $RANK --steps 1 --warmup 1 --no-cpu-baseline --force-dist || exit 1 ;;
     pmc16k) pmc pmc16k || exit 1 ;;
     pmcrank) pmc pmcrank $RANK || exit 1 ;;
     sq16k) $R/tools/kernel_pmc.sh $TAG/sq16k "$SQRX" bench.py --steps 1 --warmup 0 --epochs 1 --no-cpu-baseline || exit 1 ;;
