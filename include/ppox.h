@@ -621,6 +621,13 @@ int ppox_dp_comm_destroy(void* comm);
 int ppox_dp_all_reduce(void* comm, void* buf, int64_t count, int32_t dtype, int32_t wait, void* stream);
 int ppox_dp_wait(void* comm, void* stream);
 
+/* Stream ordering for the backward's fork / join (the reference has one stream): an event created with
+ * hipEventCreateWithFlags(flags | hipEventDisableTiming); ppox_stream_order records it on record_stream and
+ * makes wait_stream wait for it. */
+int ppox_event_create(uint32_t flags, void** event_out);
+int ppox_event_destroy(void* event);
+int ppox_stream_order(void* event, void* record_stream, void* wait_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -173,3 +173,28 @@ extern "C" int ppox_dp_wait(void* comm, void* stream) {
     c->inflight = false;
     return PPOX_OK;
 }
+
+// Events for the fork / join of the backward's two streams (convs.fork / join).  torch's events record with a
+// system-scope release (a cache writeback + invalidate for host visibility) — the trace showed each fork idling
+// the main stream ~6-7 us at the per-rank shape; the streams here only need device-scope visibility.
+// flags: hipEventCreateWithFlags flags (hipEventDisableTiming is added).
+extern "C" int ppox_event_create(uint32_t flags, void** event_out) {
+    PPOX_REQUIRE(event_out, "ppox_event_create: null output");
+    hipEvent_t e = nullptr;
+    PPOX_HIP(hipEventCreateWithFlags(&e, flags | hipEventDisableTiming), "ppox_event_create");
+    *event_out = e;
+    return PPOX_OK;
+}
+
+extern "C" int ppox_event_destroy(void* event) {
+    if (event) PPOX_HIP(hipEventDestroy(static_cast<hipEvent_t>(event)), "ppox_event_destroy");
+    return PPOX_OK;
+}
+
+// `wait_stream` waits for everything enqueued so far on `record_stream` (one event record + one wait)
+extern "C" int ppox_stream_order(void* event, void* record_stream, void* wait_stream) {
+    PPOX_REQUIRE(event, "ppox_stream_order: null event");
+    PPOX_HIP(hipEventRecord(static_cast<hipEvent_t>(event), ppox::as_stream(record_stream)), "ppox_stream_order");
+    PPOX_HIP(hipStreamWaitEvent(ppox::as_stream(wait_stream), static_cast<hipEvent_t>(event), 0), "ppox_stream_order");
+    return PPOX_OK;
+}

@@ -108,6 +108,9 @@ SIGNATURES = {
     "ppox_icm_enc_wgrad": [_vp, _vp, _i64, _i64, _vp, _vp, _vp],
     "ppox_icm_int_reward": [_vp, _vp, _vp, _i64, _i32, _vp, _f32, _vp, _vp, _vp],
     "ppox_dp_load": [ctypes.c_char_p],
+    "ppox_event_create": [ctypes.c_uint32, ctypes.POINTER(_vp)],
+    "ppox_event_destroy": [_vp],
+    "ppox_stream_order": [_vp, _vp, _vp],
     "ppox_dp_unique_id_bytes": [],
     "ppox_dp_unique_id": [_vp],
     "ppox_dp_comm_init": [_vp, _i32, _i32, _i32, ctypes.POINTER(_vp)],
@@ -991,3 +994,20 @@ class DpComm:
         if self.handle:
             call("ppox_dp_comm_destroy", self.handle)
             self.handle = None
+
+
+# ---------------------------------------------------------------------------
+# Stream ordering with device-scope events (convs.fork / join)
+# ---------------------------------------------------------------------------
+EVENT_RELEASE_TO_DEVICE, EVENT_DISABLE_SYSTEM_FENCE = 0x40000000, 0x20000000  # hipEventCreateWithFlags
+
+
+def event_create(flags):
+    h = _vp()
+    call("ppox_event_create", int(flags), ctypes.byref(h))
+    return h
+
+
+def stream_order(event, record_stream, wait_stream):
+    """wait_stream waits for everything enqueued so far on record_stream (torch streams)."""
+    call("ppox_stream_order", event, _vp(record_stream.cuda_stream), _vp(wait_stream.cuda_stream))
