@@ -31,7 +31,6 @@ class _NativeWork:
 class DistContext:
     def __init__(self, rank=0, world=1, group=None):
         self.rank, self.world, self.group = rank, world, group
-        self._dp = None  # a subgroup's native communicator (the default group's: module-level _dp_comm)
 
     @property
     def enabled(self):
@@ -53,30 +52,27 @@ class DistContext:
         return DistContext(self.rank, self.world, group=tdist.new_group(ranks=list(range(self.world))))
 
     def _native(self, t):
-        """The native RCCL communicator (native.DpComm) of this context's group when `t` can go through
-        it: the RCCL backend, a float32 / float64 device tensor (PPOX_NATIVE_DP=0: torch's collectives
-        throughout).  One per group — the default group's is the process's, a subgroup() context (PPO_ICM's
-        exchange) has its own, so the two never order against each other.  Created on first use: a
-        collective call, made by every rank at its first such all-reduce on the group, in the same order."""
+        """The process's native RCCL communicator (native.DpComm) when `t` can go through it: the default
+        group on the RCCL backend, a float32 / float64 device tensor (PPOX_NATIVE_DP=0: torch's collectives
+        throughout).  A subgroup() context (PPO_ICM's opt-in side-stream exchange) stays on torch's
+        collectives: on a native communicator of its own, beside the default group's, the dp-forced PPO_ICM
+        iteration ran 544 ms against 243 (profiles/r05g).  Created on first use: a collective call, made by
+        every rank at its first such all-reduce, in the same order."""
         global _dp_comm
-        if not NATIVE_DP or not t.is_cuda or t.dtype not in (torch.float32, torch.float64) or not t.is_contiguous():
+        if (self.group is not None or not NATIVE_DP or not t.is_cuda or t.dtype not in (torch.float32, torch.float64)
+                or not t.is_contiguous()):
             return None
-        comm = _dp_comm if self.group is None else self._dp
+        comm = _dp_comm
         if comm is None:
-            if tdist.get_backend(self.group) != "nccl":
+            if tdist.get_backend() != "nccl":
                 return None
             import native
 
             def bcast(b):
                 buf = torch.tensor(list(b), dtype=torch.uint8, device=t.device)
-                tdist.broadcast(buf, tdist.get_global_rank(self.group, 0) if self.group is not None else 0,
-                                group=self.group)
+                tdist.broadcast(buf, 0)
                 return bytes(buf.cpu().numpy())
-            comm = native.DpComm(tdist.get_world_size(self.group), tdist.get_rank(self.group), t.device.index, bcast)
-            if self.group is None:
-                _dp_comm = comm
-            else:
-                self._dp = comm
+            comm = _dp_comm = native.DpComm(tdist.get_world_size(), tdist.get_rank(), t.device.index, bcast)
         return comm
 
     def all_reduce_(self, t):
