@@ -38,8 +38,7 @@ struct DpComm {
 };
 
 // A/B knobs: PPOX_DP_PRIO (default 1, 0 under PPOX_TRAIN_PRIO=1) the exchange stream's priority class;
-// PPOX_DP_DIRECT=0 the blocking form through the exchange stream too; PPOX_DP_SKIP=1 (diagnostic) no
-// RCCL call
+// PPOX_DP_DIRECT=0 the blocking form through the exchange stream too
 int env_int(const char* name, int dflt) {
     const char* e = std::getenv(name);
     return e ? std::atoi(e) : dflt;
@@ -144,20 +143,19 @@ extern "C" int ppox_dp_all_reduce(void* comm, void* buf, int64_t count, int32_t 
     auto* c = static_cast<DpComm*>(comm);
     hipStream_t s = ppox::as_stream(stream);
     if (count == 0) return PPOX_OK;
-    static const int direct = env_int("PPOX_DP_DIRECT", 1), skip = env_int("PPOX_DP_SKIP", 0);
+    static const int direct = env_int("PPOX_DP_DIRECT", 1);
+    const ncclDataType_t type = dtype ? ncclFloat64 : ncclFloat32;
     if (wait && direct) {
         if (c->inflight) {
             PPOX_HIP(hipStreamWaitEvent(s, c->done, 0), "ppox_dp_all_reduce");
             c->inflight = false;
         }
-        ncclResult_t r = skip ? ncclSuccess : g_rccl.all_reduce(buf, buf, static_cast<size_t>(count),
-                                                                 dtype ? ncclFloat64 : ncclFloat32, ncclSum, c->comm, s);
+        ncclResult_t r = g_rccl.all_reduce(buf, buf, static_cast<size_t>(count), type, ncclSum, c->comm, s);
         return r == ncclSuccess ? PPOX_OK : rccl_fail("ncclAllReduce", r);
     }
     PPOX_HIP(hipEventRecord(c->ready, s), "ppox_dp_all_reduce");
     PPOX_HIP(hipStreamWaitEvent(c->stream, c->ready, 0), "ppox_dp_all_reduce");
-    ncclResult_t r = skip ? ncclSuccess : g_rccl.all_reduce(buf, buf, static_cast<size_t>(count),
-                                                             dtype ? ncclFloat64 : ncclFloat32, ncclSum, c->comm, c->stream);
+    ncclResult_t r = g_rccl.all_reduce(buf, buf, static_cast<size_t>(count), type, ncclSum, c->comm, c->stream);
     if (r != ncclSuccess) return rccl_fail("ncclAllReduce", r);
     PPOX_HIP(hipEventRecord(c->done, c->stream), "ppox_dp_all_reduce");
     if (wait) PPOX_HIP(hipStreamWaitEvent(s, c->done, 0), "ppox_dp_all_reduce");
