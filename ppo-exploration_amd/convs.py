@@ -121,7 +121,7 @@ class PassState:
 # main stream's dgrad chain (wgrad3 || dgrad3, wgrad2 || dgrad2; the fc weight gradient ||
 # the fc dgrad), joined before the optimizer reads the gradients (PPOX_BWD_STREAMS=0: one stream)
 BWD_STREAMS = os.environ.get("PPOX_BWD_STREAMS", "1") != "0"
-BWD_SOLO_DGRAD2_BATCH = int(os.environ.get("PPOX_BWD_SOLO_DGRAD2", "8192"))
+BWD_SOLO_DGRAD2_BATCH = int(os.environ.get("PPOX_BWD_SOLO_DGRAD2", str(1 << 62)))
 # PPOX_FORK_LATE=1: below that batch the conv2 weight gradient's side-stream wait (on the point after the
 # conv3 dgrad) is enqueued after the conv2 dgrad's launch instead of before it — the same dependencies,
 # another capture order for a hipGraph of the pass (tools/graph_probe.py)
@@ -647,10 +647,11 @@ class NatureConvs:
         else:
             g2 = torch.empty((B, 9, 9, 64), device=dev)
         self.dgrad(3, g3, B, h2, g2, am)                        # dX of conv3, times ReLU'(conv2)
-        # wgrad2 beside the conv2 dgrad below BWD_SOLO_DGRAD2_BATCH rows; from it, the persistent
-        # conv2 dgrad (whole CUs, static tile split) runs alone — the side stream drained before it,
-        # wgrad2 forked after it, beside wgrad1 — the same throughput at 16384 rows (A/B), and the
-        # dominant launch's HIP-event time is its own execution time (bench.py roofline)
+        # wgrad2 beside the conv2 dgrad below BWD_SOLO_DGRAD2_BATCH rows (PPOX_BWD_SOLO_DGRAD2; default: every
+        # batch); from it, the persistent conv2 dgrad runs alone — the side stream drained before it, wgrad2
+        # forked after it, beside wgrad1.  Round 4 measured the two the same at 16,384 rows; with the direct
+        # conv2 dgrad (round 5) the solo form idles the main stream ~150 µs while the side stream finishes the
+        # conv3 weight gradient: 556.4 / 557.8k vs 560.8 / 559.2k env-steps/s (profiles/r05i)
         solo = side is not None and B >= BWD_SOLO_DGRAD2_BATCH
         late = None
         if side is not None and not solo:
