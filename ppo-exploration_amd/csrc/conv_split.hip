@@ -27,11 +27,11 @@ namespace {
 // The weights are packed in that order, plane by plane (pack_fwd1_split).
 // ---------------------------------------------------------------------------
 
-// Persistent: the whole split weight set (48 KB) is staged in LDS once per
+// Persistent: the whole split weight set (32 KB) is staged in LDS once per
 // workgroup (B fragments then cost LDS, not TA, bandwidth), and each wave walks
 // a contiguous range of row tiles.  The kernel is load-latency bound, so the
 // input of the NEXT tile (all 8 chunks, 16*MT dwords per lane) is loaded while
-// the current tile runs its 48*MT MFMAs.  Workgroups with adjacent row ranges
+// the current tile runs its 32*MT MFMAs.  Workgroups with adjacent row ranges
 // share an XCD (xcd_remap): the overlapping input windows of one frame stack
 // are read through one L2.
 // PLANES: h1 is written as its two f16 planes (H1P: per pixel 32 hi then 32 lo f16, 128 B like f32),
@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
 #define SPLIT_FWD1_MT 1
 #endif
 // waves the persistent kernel spreads its tiles over: 256 CUs x resident waves per CU
-// (LDS: 3 workgroups of 48 KB at MT = 1; VGPRs: 2 at MT = 2)
+// (VGPRs: 3 workgroups at MT = 1, 140 VGPRs; 2 at MT = 2; 32 KB of LDS each)
 #ifndef SPLIT_RESIDENT_WAVES
 #define SPLIT_RESIDENT_WAVES (SPLIT_FWD1_MT == 1 ? 3072 : 2048)
 #endif
