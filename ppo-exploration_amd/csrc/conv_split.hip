@@ -1,17 +1,13 @@
-// K6, split-bf16 form — the NatureCNN convolutions on the bf16 matrix cores with
-// fp32-class accuracy (v_mfma_f32_32x32x16_bf16 runs 16x the f32-input MFMA rate).
+// K6, split-f16 form — the NatureCNN convolutions on the f16 matrix cores with fp32-class accuracy.
 //
-// Every f32 operand is split EXACTLY into three bf16 planes by truncation:
-//   a0 = hi16(a), a1 = hi16(a - a0), a2 = a - a0 - a1   (a == a0 + a1 + a2, bitwise)
-// so every bf16 x bf16 product below is exact in f32.  A product a*b is then
-//   a0b0 + (a0b1 + a1b0) + (a0b2 + a1b1 + a2b0)       [+ a1b2 + a2b1 + a2b2 dropped]
-// whose dropped terms are < 3 * 2^-22 |ab| — one f32 rounding's worth.  The a0b0
-// terms accumulate in their own f32 accumulator, the small terms in a second
-// one, and the two are added once in the epilogue.  conv1's input is a uint8
-// frame (0..255): exact in ONE bf16 plane, so conv1 fwd/wgrad need only three
-// products (x*w0 + x*w1 + x*w2), each exact.  Accuracy is therefore that of an
-// f32 FMA chain up to summation order (tests: tests/test_kernels_gpu.py, split
-// vs f32 MFMA vs fp64).  Same layers, layouts and fused epilogues as conv.hip.
+// Every f32 operand is scaled by a power of two and split into two f16 planes (conv_common.h, "split-f16"):
+//   h = rn16(x s), l = rn16(x s - h)
+// A product a*b is hA hB + (hA lB + lA hB), three v_mfma_f32_32x32x16_f16 with each product exact in f32.
+// The hA hB terms accumulate in their own f32 accumulator and the small terms in a second one; the two are
+// added once in the epilogue and unscaled by an exact power of two.  conv1's input is a uint8 frame (0..255),
+// exact in ONE f16 plane, so the conv1 forward and weight gradient need only two products (x wh + x wl).
+// Accuracy is therefore that of an f32 FMA chain up to summation order (tests: tests/test_kernels_gpu.py,
+// split vs f32 MFMA vs fp64).  Same layers, layouts and fused epilogues as conv.hip.
 #include <algorithm>
 
 #include "conv_common.h"
@@ -30,7 +26,7 @@ namespace {
 // Persistent: the whole split weight set (32 KB) is staged in LDS once per
 // workgroup (B fragments then cost LDS, not TA, bandwidth), and each wave walks
 // a contiguous range of row tiles.  The kernel is load-latency bound, so the
-// input of the NEXT tile (all 8 chunks, 16*MT dwords per lane) is loaded while
+// input of the NEXT tile (all 8 chunks, 16*MT 8-byte loads per lane) is loaded while
 // the current tile runs its 32*MT MFMAs.  Workgroups with adjacent row ranges
 // share an XCD (xcd_remap): the overlapping input windows of one frame stack
 // are read through one L2.
