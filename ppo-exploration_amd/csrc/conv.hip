@@ -378,7 +378,7 @@ __device__ inline void pack_frag_unit(const Src& src, float s, uint16_t* __restr
 
 // ---------------------------------------------------------------------------
 // NatureCNN hidden linear layer Linear(3136, 512) (.ipynb_checkpoints/
-// models-checkpoint.py:58-59) on the split-bf16 implicit-GEMM kernel: a plain GEMM
+// models-checkpoint.py:58-59) on the split-f16 implicit-GEMM kernel: a plain GEMM
 // C[M][N] = A[M][K] B[K][N] with A f32 rows (split in registers), B pre-split per
 // column block of NB (zero-padded), workgroups over (row tile, column block), the
 // column blocks of a row tile on one XCD (its A rows then come from that XCD's L2).
@@ -522,10 +522,10 @@ using HeadDgrad = GemmRowsProblem<512, 512, FC_NB, HEAD_DGRAD>;
 static_assert(FC_NB == 64, "sg2 runs the fc layer in 64-column blocks");
 
 // ---------------------------------------------------------------------------
-// conv2 dgrad in the col2im form (split-bf16), the default conv2 split dgrad.
+// conv2 dgrad in the col2im form (split-f16), the default conv2 split dgrad.
 // GEMM rows = output-grad pixels (n, oy, ox), K = the 64 output channels, columns =
 // (tap, ci): 16 taps x 32 = 512.  Every A value (one G row of 64 floats) is loaded
-// once, split once into its three bf16 planes and kept in registers for all 512
+// once, split once into its two f16 planes and kept in registers for all 512
 // columns — 16x the MFMA work per A byte of the position-major form, whose
 // 32-column tiles re-gathered each G row for every one of its 16 input pixels.
 // A triple (3 whole samples, 243 rows on 8 waves x 32) keeps the col2im overlap inside
@@ -791,11 +791,11 @@ __global__ void __launch_bounds__(512, 1) dgrad2_colp_kernel(Args a, const u32x4
 
 
 // ---------------------------------------------------------------------------
-// Split-bf16 GEMM, LDS-DMA pipelined ("sg2"): the forward-style GEMMs (conv2/conv3
+// Split-f16 GEMM, LDS-DMA pipelined ("sg2"): the forward-style GEMMs (conv2/conv3
 // forward, conv3 dgrad, fc forward, fc dgrad) with the Problems' fused epilogues (bias +
 // ReLU, ReLU-mask, NHWC / Flatten order).  512-thread workgroups (8 waves, two per SIMD, one workgroup per
 // CU), 256 rows x 64 columns per workgroup, each wave 32 rows x 64 columns (hi/lo f32
-// accumulators for two 32x32 tiles: six v_mfma_f32_32x32x16_bf16 per tile and 16-k step).
+// accumulators for two 32x32 tiles: three v_mfma_f32_32x32x16_f16 per tile and 16-k step).
 // Per 32-k chunk the A rows (f32, im2col-gathered: one 128-B run per row) and the
 // pre-split B chunk (12 KB, split_frag_index order) are copied global -> LDS by
 // global_load_lds_dwordx4 into a three-slot ring, so no VGPR staging and no ds_write:
@@ -1804,11 +1804,11 @@ __global__ void __launch_bounds__(RED_E * RG) wgrad_reduce(const float* __restri
 }
 
 // ---------------------------------------------------------------------------
-// Wgrad, split-bf16.  Same decomposition as wgrad_kernel (WG = k-block of KT rows x
+// Wgrad, split-f16.  Same decomposition as wgrad_kernel (WG = k-block of KT rows x
 // all COUT x a slice of output pixels; partial slabs reduced by wgrad_reduce), on
-// v_mfma_f32_32x32x16_bf16.  Per step of MS = 32 pixels the X (im2col) and G tiles
-// are staged in LDS as bf16 planes, row-major [pixel][k] / [pixel][co] (each f32
-// value split once per workgroup into its three exact planes; conv1's u8 frames are
+// v_mfma_f32_32x32x16_f16.  Per step of MS = 32 pixels the X (im2col) and G tiles
+// are staged in LDS as f16 planes, row-major [pixel][k] / [pixel][co] (each f32
+// value split once per workgroup into its two planes; conv1's u8 frames are
 // one exact plane), and the MFMA fragments — 8 consecutive pixels of one k (A) or
 // one co (B) per lane — come straight out of LDS with the transposing read
 // ds_read_b64_tr_b16 (two per fragment).  32-byte chunks of a row are XOR-swizzled
@@ -3756,7 +3756,7 @@ extern "C" int ppox_nature_conv2_wgrad_planes(const uint16_t* h1p, const uint16_
     return launch_wgrad_reduce<G2, true>(slab, wa.bslab, (int)grid, dw, db, s);
 }
 
-// ---- NatureCNN fc layer (3136 -> 512) on the split-bf16 GEMM ----------------------
+// ---- NatureCNN fc layer (3136 -> 512) on the split-f16 GEMM -----------------------
 // Weight gradient dW = df^T h3 on the split wgrad kernel: "pixels" = samples (GFc has one
 // output pixel), K = the 512 outputs (X = df rows), G = the NHWC conv3 activations in 49
 // blocks of 64 channels (one spatial position each, NHWC feature order f = p * 64 + c).
