@@ -319,15 +319,6 @@ __device__ inline u32x4 u8x8_to_f16(uint32_t w0, uint32_t w1) {
     for (int i = 0; i < 4; ++i) r[i] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2, q[i]) - k1024);
     return r;
 }
-// eight uint8 -> an f16x8 fragment of b * 2^-24, exact: f16 bits 0x00bb are the subnormal b * 2^-24, so
-// one v_perm_b32 per pair (bytes b, 0, b', 0) and no subtract.  A kernel's products and sums over it are
-// 2^-24 times those over u8x8_to_f16's, bit for bit, while none of its f32 values nears the f32
-// subnormal range (the caller folds 2^24 into its output scale)
-__device__ inline u32x4 u8x8_to_f16_tiny(uint32_t w0, uint32_t w1) {
-    return u32x4{__builtin_amdgcn_perm(0u, w0, 0x0c010c00), __builtin_amdgcn_perm(0u, w0, 0x0c030c02),
-                 __builtin_amdgcn_perm(0u, w1, 0x0c010c00), __builtin_amdgcn_perm(0u, w1, 0x0c030c02)};
-}
-
 // Tail of a packed buffer of `planes` uint16: PACK_TAIL32 uint32 — [0, AMAX_SLOTS) the amax
 // partials of the source weights (written by wmax_kernel, read by the packer), then the scale
 // exponent E the planes were packed with (read by the GEMM kernels).

@@ -54,11 +54,6 @@ __device__ uint32_t kFwd1Dummy[128];  // store target of the rows past the batch
 #ifndef FWD1_NT
 #define FWD1_NT 1
 #endif
-// the frames as f16 subnormals b * 2^-24 (u8x8_to_f16_tiny: one v_perm_b32 per two values, no packed
-// subtract; the output scale takes the 2^24): the kernel is VALU-issue bound
-#ifndef FWD1_TINY
-#define FWD1_TINY 1
-#endif
 __device__ inline void fwd1_store(uint32_t* p, uint32_t v) {
     if constexpr (FWD1_NT)
         __builtin_nontemporal_store(v, p);
@@ -143,8 +138,7 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
     };
     const int co = lane & 31;
     const float bias = a.bias[co];
-    // the weights were packed times 2^E; frames are exact (FWD1_TINY: as b * 2^-24)
-    const float uw = exp2i((FWD1_TINY ? 24 : 0) - *a.wexp);
+    const float uw = exp2i(-*a.wexp);  // the weights were packed times 2^E; frames are exact
     const float sy = PLANES ? exp2i(*a.yexp) : 1.f;  // H1P output scale
     float om = 0.f;                    // the largest value this lane stored (h1's amax)
     auto run_tile = [&](unsigned tile, const Raw& r) {
@@ -166,8 +160,7 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
                 }
 #pragma unroll
                 for (int i = 0; i < MT; ++i) {
-                    const u32x4 av = FWD1_TINY ? u8x8_to_f16_tiny(r[i][c][2 * s], r[i][c][2 * s + 1])
-                                               : u8x8_to_f16(r[i][c][2 * s], r[i][c][2 * s + 1]);
+                    const u32x4 av = u8x8_to_f16(r[i][c][2 * s], r[i][c][2 * s + 1]);
                     hi[i] = mfma_f16(av, rb[cur][0], hi[i]);
                     lo[i] = mfma_f16(av, rb[cur][1], lo[i]);
                 }
