@@ -443,7 +443,11 @@ def main():
             iteration()
     convs.BWD_STREAMS = streams
     totals = {k: sum(t for t, _ in v) for k, v in solo.items()}
-    prof_kernel = max(totals, key=totals.get) if any(totals.values()) else "ppox_nature_conv2_wgrad_planes"
+    duo_tot = {k: sum(t for t, _ in v) for k, v in duo.items()}
+    solo_kernel = max(totals, key=totals.get) if any(totals.values()) else "ppox_nature_conv2_wgrad_planes"
+    # the headline kernel: the largest in the pass as the timed region runs it (two streams: rocprofv3
+    # --stats's ranking over the timed region), the one-stream pick beside it
+    prof_kernel = max(duo_tot, key=duo_tot.get) if any(duo_tot.values()) else solo_kernel
     gae_kernel = "ppox_gae" if args.algo != "rnd" else "ppox_gae_dual"
     native.enable_event_timing([prof_kernel])
 
@@ -496,11 +500,14 @@ def main():
         r["timing"] = ("HIP events on the kernel's launch stream around its timed-region launches of "
                        f"{r['rows']} rows; a launch beside side-stream kernels (convs.BWD_STREAMS) also counts "
                        "its sharing of the CUs with them")
-        r["selection"] = ("largest total kernel time among the training-pass MFMA kernels in a one-stream "
-                          "warmup iteration (collect untimed)")
+        r["selection"] = (("largest total kernel time in a two-stream warmup iteration (rocprofv3 --stats's "
+                           "ranking over the timed region; collect untimed)") if any(duo_tot.values()) else
+                          "largest total kernel time in a one-stream warmup iteration (collect untimed)")
         if solo.get(prof_kernel):
             s_ = kernel_roofline(prof_kernel, solo[prof_kernel])
             r["solo"] = {k: s_[k] for k in ("mean_us", "launches", "rows", "frac", "mfma_frac", "hbm_frac")}
+        if any(duo_tot.values()):
+            r["share_of_mfma_kernel_time"] = round(duo_tot[prof_kernel] / sum(duo_tot.values()), 3)
         if r.get("traffic") is not None and r["rows"] != PMC_LAUNCH_ROWS:
             # the committed PMC passes ran launches of PMC_LAUNCH_ROWS rows (the 1-GPU workload);
             # a per-launch byte count of another size does not apply here
@@ -508,6 +515,13 @@ def main():
             r["traffic_note"] = (f"PMC traffic was measured on {PMC_LAUNCH_ROWS}-row launches (profiles/); "
                                  f"these launches have {r['rows']} rows")
         out["roofline"] = r
+    if solo.get(solo_kernel):
+        q = kernel_roofline(solo_kernel, solo[solo_kernel])
+        if q["traffic"] is not None and q["rows"] != PMC_LAUNCH_ROWS:
+            q["traffic"] = q["traffic_ratio"] = None
+        q["selection"] = ("largest total kernel time in a one-stream warmup iteration; mean over that "
+                          "iteration's launches, each alone on the GPU")
+        out["roofline_solo"] = q
     tot = sum(totals.values())
     if tot:
         top = []
@@ -522,17 +536,6 @@ def main():
         # every training-pass MFMA kernel's one-stream mean (us) at its most frequent row count
         out["solo_us"] = {KERNELS[k]["label"]: round(float(np.mean([t for t, _ in solo[k]])) * 1e3, 1)
                           for k in sorted(totals, key=totals.get, reverse=True) if solo[k]}
-    duo_tot = {k: sum(t for t, _ in v) for k, v in duo.items()}
-    if any(duo_tot.values()):
-        k2 = max(duo_tot, key=duo_tot.get)
-        q = kernel_roofline(k2, duo[k2])
-        out["roofline_rocprof"] = {
-            "kernel": q["kernel"], "bound": q["bound"], "frac": q["frac"], "mean_us": q["mean_us"], "rows": q["rows"],
-            "hbm_frac": q["hbm_frac"], "mfma_frac": q["mfma_frac"],
-            "share_of_mfma_kernel_time": round(duo_tot[k2] / sum(duo_tot.values()), 3),
-            "selection": ("largest total kernel time in a two-stream warmup iteration (the ranking of rocprofv3 "
-                          "--stats over the timed region); its event durations include sharing the CUs with the "
-                          "other stream's kernels")}
     if gae_ms:
         n_local = args.envs // world
         alg_bytes = (17 if gae_kernel == "ppox_gae" else 33) * args.nstep * n_local
@@ -556,6 +559,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)
     if world > 1 or args.force_dist:
+        import dist as _dist
+        _dist.shutdown()  # the native communicator first (csrc/dp.cpp), then torch's process group
         tdist.destroy_process_group()
 
 

@@ -373,7 +373,9 @@ int ppox_head_hidden_dgrad(const float* de, int64_t rows, const uint16_t* q_dgra
 /* The heads' backward to the fc output in one launch (round 5; replaces ppox_head_dgrad_outer +
  * ppox_head_hidden_dgrad for a net without the intrinsic head): de = (e > 0) dv w_critic (bitwise
  * ppox_head_dgrad_outer's de) and df = (f > 0) (dout w_actor + de W) with W the hidden layer
- * (q_dgrad: its ppox_nature_pack_all dgrad form), f32 (rows x 512); both amax recorded.  Reference:
+ * (q_dgrad: its ppox_nature_pack_all dgrad form), f32 (rows x 512); both amax recorded.  w_actor, e, f,
+ * df, de and q_dgrad 16-B aligned; w_critic any float alignment (its offset in the flat parameter
+ * buffer follows the action count).  Reference:
  * models-checkpoint.py:72, 80-85 (actor, extra_layer, critic_ext) backward, ppo.py:241. */
 int ppox_head_backward(const float* dout, const float* w_actor, const float* dv, const float* w_critic, const float* e,
                        const float* f, const uint16_t* q_dgrad, int64_t rows, int64_t h, int64_t n_out, float* df,

@@ -1142,8 +1142,10 @@ __global__ void __launch_bounds__(256, 1) hbw_kernel(HbwArgs a, const u32x4* __r
     const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
 
     // wc's split at its own exponent (every workgroup derives the same): thread t keeps columns 4 (t & 127) ..
+    // (wc sits in the flat parameter buffer at an offset that depends on the action count: four dword loads,
+    // no 16-B alignment asked of it)
     const int c4 = tid & 127;
-    const float4 w4 = reinterpret_cast<const float4*>(a.wc)[c4];
+    const float4 w4 = make_float4(a.wc[4 * c4], a.wc[4 * c4 + 1], a.wc[4 * c4 + 2], a.wc[4 * c4 + 3]);
     uint32_t wmax = max(max(__float_as_uint(fabsf(w4.x)), __float_as_uint(fabsf(w4.y))),
                         max(__float_as_uint(fabsf(w4.z)), __float_as_uint(fabsf(w4.w))));
     wmax = wave_max_u32(wmax);
@@ -1959,9 +1961,10 @@ int head_backward(const float* dout, const float* wa, const float* dv, const flo
     const int cus = dconv_cus();
     PPOX_REQUIRE(cus > 0, "ppox_head_backward: no device");
     PPOX_REQUIRE(n_out >= 1 && n_out <= 8, "ppox_head_backward: n_out must be 1..8");
-    PPOX_REQUIRE(ppox::aligned16(wa) && ppox::aligned16(wc) && ppox::aligned16(e) && ppox::aligned16(f) &&
-                     ppox::aligned16(df) && ppox::aligned16(de) && ppox::aligned16(qhd),
-                 "ppox_head_backward: 16B alignment");
+    PPOX_REQUIRE(ppox::aligned16(wa) && ppox::aligned16(e) && ppox::aligned16(f) && ppox::aligned16(df) &&
+                     ppox::aligned16(de) && ppox::aligned16(qhd),
+                 "ppox_head_backward: 16B alignment (w_actor, e, f, df, de, q)");
+    PPOX_REQUIRE(wc && dv && dout, "ppox_head_backward: null w_critic / dv / dout");
     const int nrg = (int)std::max<long long>(1, std::min<long long>(cus / 4, ppox::ceil_div((long long)rows, 32LL)));
     HbwArgs a{dout, wa, dv, wc, e, f, df, de, amax_de, amax_df, wexp, rows, nrg};
     const u32x4* w = reinterpret_cast<const u32x4*>(qhd);

@@ -9,7 +9,6 @@
 // the caller passes its path), so one RCCL instance serves both torch's communicators and this one.
 #include <dlfcn.h>
 
-#include <cstdlib>
 #include <cstring>
 
 #include <rccl/rccl.h>
@@ -32,17 +31,19 @@ Rccl g_rccl;
 struct DpComm {
     ncclComm_t comm = nullptr;
     hipStream_t stream = nullptr;
-    hipEvent_t ready = nullptr, done = nullptr;
+    // ready: the caller's point an asynchronous reduction starts after; done: the end of the last
+    // asynchronous reduction; mark: the end of the last blocking one, recorded lazily on its stream when the
+    // next reduction comes from another stream
+    hipEvent_t ready = nullptr, done = nullptr, mark = nullptr;
     int world = 0, rank = 0, device = 0;
+    // the stream the communicator's last reduction was ordered on (the caller's for a blocking one, the
+    // communicator's own for an asynchronous one; null before the first): every reduction is ordered after
+    // it, so the reductions run one at a time in issue order whichever streams issue them — the order every
+    // rank issues them in (two RCCL kernels of one communicator running out of order could pair
+    // different buffers across ranks, or deadlock)
+    hipStream_t last = nullptr;
     bool inflight = false;  // an asynchronous reduction not yet waited for by a caller's stream
 };
-
-// A/B knobs: PPOX_DP_PRIO (default 1, 0 under PPOX_TRAIN_PRIO=1) the exchange stream's priority class;
-// PPOX_DP_DIRECT=0 the blocking form through the exchange stream too
-int env_int(const char* name, int dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::atoi(e) : dflt;
-}
 
 int rccl_fail(const char* what, ncclResult_t r) {
     ppox::set_error("%s: %s", what, g_rccl.error_string ? g_rccl.error_string(r) : "rccl error");
@@ -105,12 +106,15 @@ extern "C" int ppox_dp_comm_init(const uint8_t* id_host, int32_t world, int32_t 
     // main stream (the default stream) is not
     int lo = 0, hi = 0;
     hipDeviceGetStreamPriorityRange(&lo, &hi);
-    const int high = env_int("PPOX_DP_PRIO", env_int("PPOX_TRAIN_PRIO", 0) ? 0 : 1);
-    hipError_t e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, high ? hi : lo);
+    hipError_t e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->mark, hipEventDisableTiming);
     if (e != hipSuccess) {
         g_rccl.comm_destroy(c->comm);
+        if (c->ready) hipEventDestroy(c->ready);
+        if (c->done) hipEventDestroy(c->done);
+        if (c->stream) hipStreamDestroy(c->stream);
         delete c;
         ppox::set_error("ppox_dp_comm_init: %s", hipGetErrorString(e));
         return -static_cast<int>(e);
@@ -119,47 +123,69 @@ extern "C" int ppox_dp_comm_init(const uint8_t* id_host, int32_t world, int32_t 
     return PPOX_OK;
 }
 
+// Waits for the communicator's work (its own stream and the last blocking reduction's stream), then
+// destroys it.  Call before the process group and the HIP runtime go away: a communicator left alive to
+// the exit-time destructors took a profiled run down with SIGSEGV in __cxa_finalize.
 extern "C" int ppox_dp_comm_destroy(void* comm) {
     if (!comm) return PPOX_OK;
     auto* c = static_cast<DpComm*>(comm);
-    PPOX_HIP(hipStreamSynchronize(c->stream), "ppox_dp_comm_destroy");
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess && c->last && c->last != c->stream) e = hipStreamSynchronize(c->last);
     ncclResult_t r = g_rccl.comm_destroy(c->comm);
     hipEventDestroy(c->ready);
     hipEventDestroy(c->done);
+    hipEventDestroy(c->mark);
     hipStreamDestroy(c->stream);
     delete c;
+    if (e != hipSuccess) {
+        ppox::set_error("ppox_dp_comm_destroy: %s", hipGetErrorString(e));
+        return -static_cast<int>(e);
+    }
     return r == ncclSuccess ? PPOX_OK : rccl_fail("ncclCommDestroy", r);
 }
 
-// SUM all-reduce of buf (in place) after the work already on `stream`.  wait == 0: on the
-// communicator's stream (the caller joins later with ppox_dp_wait); wait != 0, the blocking form: on
-// `stream` itself (each cross-stream event hop idles the GPU several us: per-rank 213 -> 198 ms), after
-// `stream` has waited for an asynchronous reduction still in flight — the communicator's reductions
-// never overlap each other and run in issue order, the order every rank issues them in.
+namespace {
+// `s` waits for the communicator's last reduction (nothing when that was ordered on `s` itself)
+hipError_t order_after_last(DpComm* c, hipStream_t s) {
+    if (!c->last || c->last == s) return hipSuccess;
+    if (c->last == c->stream) return hipStreamWaitEvent(s, c->done, 0);
+    // the last was a blocking reduction on another caller stream: mark that stream now (the mark also covers
+    // what was enqueued there after the reduction — more order than needed, never less)
+    hipError_t e = hipEventRecord(c->mark, c->last);
+    return e == hipSuccess ? hipStreamWaitEvent(s, c->mark, 0) : e;
+}
+}  // namespace
+
+// SUM all-reduce of buf (in place) after the work already on `stream` and after the communicator's previous
+// reduction (whichever stream issued it).  wait == 0: on the communicator's stream (the caller joins later with
+// ppox_dp_wait; a second asynchronous reduction before that join is refused); wait != 0, the blocking form: on
+// `stream` itself (each cross-stream event hop idles the GPU several us: per-rank 213 -> 198 ms).
 extern "C" int ppox_dp_all_reduce(void* comm, void* buf, int64_t count, int32_t dtype, int32_t wait, void* stream) {
     PPOX_REQUIRE(comm, "ppox_dp_all_reduce: null communicator");
     PPOX_REQUIRE(count >= 0 && (count == 0 || buf), "ppox_dp_all_reduce: %lld elements at %p", (long long)count, buf);
     PPOX_REQUIRE(dtype == 0 || dtype == 1, "ppox_dp_all_reduce: dtype %d (0 = float32, 1 = float64)", dtype);
     auto* c = static_cast<DpComm*>(comm);
+    PPOX_REQUIRE(wait || !c->inflight,
+                 "ppox_dp_all_reduce: an asynchronous reduction is in flight (join it with ppox_dp_wait first)");
     hipStream_t s = ppox::as_stream(stream);
     if (count == 0) return PPOX_OK;
-    static const int direct = env_int("PPOX_DP_DIRECT", 1);
     const ncclDataType_t type = dtype ? ncclFloat64 : ncclFloat32;
-    if (wait && direct) {
-        if (c->inflight) {
-            PPOX_HIP(hipStreamWaitEvent(s, c->done, 0), "ppox_dp_all_reduce");
-            c->inflight = false;
-        }
+    if (wait) {
+        PPOX_HIP(order_after_last(c, s), "ppox_dp_all_reduce");
+        c->inflight = false;
         ncclResult_t r = g_rccl.all_reduce(buf, buf, static_cast<size_t>(count), type, ncclSum, c->comm, s);
-        return r == ncclSuccess ? PPOX_OK : rccl_fail("ncclAllReduce", r);
+        if (r != ncclSuccess) return rccl_fail("ncclAllReduce", r);
+        c->last = s;
+        return PPOX_OK;
     }
     PPOX_HIP(hipEventRecord(c->ready, s), "ppox_dp_all_reduce");
     PPOX_HIP(hipStreamWaitEvent(c->stream, c->ready, 0), "ppox_dp_all_reduce");
+    if (c->last != s) PPOX_HIP(order_after_last(c, c->stream), "ppox_dp_all_reduce");
     ncclResult_t r = g_rccl.all_reduce(buf, buf, static_cast<size_t>(count), type, ncclSum, c->comm, c->stream);
     if (r != ncclSuccess) return rccl_fail("ncclAllReduce", r);
     PPOX_HIP(hipEventRecord(c->done, c->stream), "ppox_dp_all_reduce");
-    if (wait) PPOX_HIP(hipStreamWaitEvent(s, c->done, 0), "ppox_dp_all_reduce");
-    c->inflight = !wait;
+    c->last = c->stream;
+    c->inflight = true;
     return PPOX_OK;
 }
 
@@ -167,7 +193,9 @@ extern "C" int ppox_dp_all_reduce(void* comm, void* buf, int64_t count, int32_t 
 extern "C" int ppox_dp_wait(void* comm, void* stream) {
     PPOX_REQUIRE(comm, "ppox_dp_wait: null communicator");
     auto* c = static_cast<DpComm*>(comm);
-    PPOX_HIP(hipStreamWaitEvent(ppox::as_stream(stream), c->done, 0), "ppox_dp_wait");
+    hipStream_t s = ppox::as_stream(stream);
+    PPOX_HIP(order_after_last(c, s), "ppox_dp_wait");
+    if (c->last) c->last = s;
     c->inflight = false;
     return PPOX_OK;
 }

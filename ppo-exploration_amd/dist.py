@@ -8,7 +8,9 @@ all-reduce of the loss partial sums (global advantage moments are all-gathered
 once per rollout) and the all-reduce of the flat gradient bucket.  On ROCm the
 torch "nccl" backend is RCCL over xGMI; CPU tests use "gloo".
 """
+import atexit
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -18,6 +20,39 @@ import torch.distributed as tdist
 # the per-minibatch all-reduces through native code (csrc/dp.cpp) instead of torch.distributed
 NATIVE_DP = os.environ.get("PPOX_NATIVE_DP", "1") != "0"
 _dp_comm = None
+_native_off = False  # set once the RCCL library could not be found (torch's collectives then)
+
+
+def shutdown():
+    """Destroy the process's native RCCL communicator (a stream sync, then ncclCommDestroy).  Call before
+    torch.distributed.destroy_process_group(); also registered with atexit when the communicator is made, so
+    it never lives into the exit-time destructors (a profiled run left it alive and died with SIGSEGV in
+    __cxa_finalize).  Returns the destroy's status (0, or None when there was none)."""
+    global _dp_comm
+    comm, _dp_comm = _dp_comm, None
+    return comm.close() if comm is not None else None
+
+
+def _self_check(comm, device, world, rank):
+    """At creation: the communicator sums across every rank.  Integer-valued floats (exact sums) through the
+    blocking and the asynchronous form, checked against the closed-form totals and against torch's own
+    collective over the same ranks; a mismatch raises — there is no silent fallback."""
+    i = torch.arange(4099, device=device, dtype=torch.float32)
+    x = (i.remainder(7) + 1) * (rank + 1)
+    y = torch.full((17,), float(rank + 1), dtype=torch.float64, device=device)
+    ones = torch.ones(1024, device=device)
+    comm.all_reduce_(x)
+    comm.all_reduce_(y, wait=False)
+    comm.wait()
+    comm.all_reduce_(ones)
+    tri = world * (world + 1) / 2
+    ref = (i.remainder(7) + 1) * (rank + 1)
+    tdist.all_reduce(ref)
+    ok = (torch.equal(x, (i.remainder(7) + 1) * tri) and torch.equal(x, ref) and bool((y == tri).all())
+          and bool((ones == world).all()))
+    if not ok:
+        raise RuntimeError(f"native RCCL communicator self-check failed on rank {rank} of {world}: the all-reduce "
+                           "does not sum across the ranks")
 
 
 class _NativeWork:
@@ -58,21 +93,30 @@ class DistContext:
         collectives: on a native communicator of its own, beside the default group's, the dp-forced PPO_ICM
         iteration ran 544 ms against 243 (profiles/r05g).  Created on first use: a collective call, made by
         every rank at its first such all-reduce, in the same order."""
-        global _dp_comm
-        if (self.group is not None or not NATIVE_DP or not t.is_cuda or t.dtype not in (torch.float32, torch.float64)
-                or not t.is_contiguous()):
+        global _dp_comm, _native_off
+        if (self.group is not None or not NATIVE_DP or _native_off or not t.is_cuda
+                or t.dtype not in (torch.float32, torch.float64) or not t.is_contiguous()):
             return None
         comm = _dp_comm
         if comm is None:
             if tdist.get_backend() != "nccl":
                 return None
             import native
+            try:
+                path = native.rccl_path()
+            except ImportError as e:  # a torch build on the system RCCL: torch's collectives throughout
+                warnings.warn(f"native RCCL exchange off ({e}); using torch.distributed's collectives")
+                _native_off = True
+                return None
 
             def bcast(b):
                 buf = torch.tensor(list(b), dtype=torch.uint8, device=t.device)
                 tdist.broadcast(buf, 0)
                 return bytes(buf.cpu().numpy())
-            comm = _dp_comm = native.DpComm(tdist.get_world_size(), tdist.get_rank(), t.device.index, bcast)
+            comm = native.DpComm(tdist.get_world_size(), tdist.get_rank(), t.device.index, bcast, rccl=path)
+            _dp_comm = comm
+            atexit.register(shutdown)
+            _self_check(comm, t.device, comm.world, comm.rank)
         return comm
 
     def all_reduce_(self, t):

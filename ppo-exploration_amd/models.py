@@ -266,7 +266,10 @@ class CnnActorCritic(nn.Module):
             deferred = []
             # round 5: with the split hidden layer and no intrinsic head, the actor's input grad, the critic's
             # ReLU-layer grad and the hidden layer's dgrad (fc ReLU applied) in one launch (ppox_head_backward)
-            fused = split and not self.intrinsic and HEAD_BWD_FUSED and dout.shape[1] <= 8
+            # (the kernel reads w_actor as 16-B vectors; w_critic, whose flat-buffer offset depends on the action
+            # count, by dwords)
+            fused = (split and not self.intrinsic and HEAD_BWD_FUSED and dout.shape[1] <= 8
+                     and a.weight.is_contiguous() and a.weight.data_ptr() % 16 == 0)
             if fused:
                 df, de0 = torch.empty_like(f), torch.empty_like(e)
                 native.head_backward(dout, a.weight, dv.contiguous().view(B), self.critic_ext.weight, e, f, cv.qh[1],

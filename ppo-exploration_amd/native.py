@@ -965,9 +965,9 @@ class DpComm:
     rank in the same order: `broadcast_id(buf)` must hand rank 0's id bytes to every rank (a collective
     over the process group that already exists)."""
 
-    def __init__(self, world, rank, device, broadcast_id):
+    def __init__(self, world, rank, device, broadcast_id, rccl=None):
         l = lib()
-        call("ppox_dp_load", rccl_path().encode())
+        call("ppox_dp_load", (rccl or rccl_path()).encode())
         n = l.ppox_dp_unique_id_bytes()
         buf = (ctypes.c_uint8 * n)()
         if rank == 0:
@@ -975,25 +975,36 @@ class DpComm:
         buf = (ctypes.c_uint8 * n).from_buffer_copy(broadcast_id(bytes(buf)))
         h = _vp()
         call("ppox_dp_comm_init", buf, world, rank, device, ctypes.byref(h))
-        self.handle, self.world, self.rank = h, world, rank
+        self.handle, self.world, self.rank, self.inflight = h, world, rank, False
 
     def all_reduce_(self, t, wait=True, stream=None):
         """In-place SUM over ranks of a contiguous float32 / float64 device tensor, ordered after the work on
-        `stream` (default: the current stream); wait: that stream waits for it (else join with wait())."""
+        `stream` (default: the current stream) and after the communicator's previous reduction; wait: that
+        stream waits for it (else join with wait() — one asynchronous reduction at a time: a second one
+        before the join raises)."""
+        if not self.handle:
+            raise NativeError("DpComm.all_reduce_: the communicator is closed")
+        if not wait and self.inflight:
+            raise NativeError("DpComm.all_reduce_: an asynchronous reduction is in flight (wait() first)")
         dt = 0 if t.dtype == torch.float32 else 1 if t.dtype == torch.float64 else None
         if dt is None or not t.is_cuda or not t.is_contiguous():
             raise TypeError(f"DpComm.all_reduce_: contiguous float32/float64 device tensor, got {t.dtype} "
                             f"on {t.device}")
         call("ppox_dp_all_reduce", self.handle, _p(t), t.numel(), dt, 1 if wait else 0, stream_ptr(stream))
+        self.inflight = not wait and t.numel() > 0
         return t
 
     def wait(self, stream=None):
         call("ppox_dp_wait", self.handle, stream_ptr(stream))
+        self.inflight = False
 
     def close(self):
-        if self.handle:
-            call("ppox_dp_comm_destroy", self.handle)
-            self.handle = None
+        """Sync and destroy (ppox_dp_comm_destroy); returns its status, 0.  Idempotent."""
+        if not self.handle:
+            return 0
+        h, self.handle = self.handle, None
+        call("ppox_dp_comm_destroy", h)
+        return 0
 
 
 # ---------------------------------------------------------------------------

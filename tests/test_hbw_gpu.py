@@ -10,12 +10,13 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _case(B, A, seed):
+def _case(B, A, seed, wc_off=0):
+    """wc_off: w_critic at that float offset of a buffer (the flat parameter buffer puts it at 513 A mod 4)"""
     import native
     g = torch.Generator(device="cuda").manual_seed(seed)
     W = torch.randn(512, 512, device="cuda", generator=g) * 0.04
     wa = torch.randn(A, 512, device="cuda", generator=g) * 0.05
-    wc = torch.randn(1, 512, device="cuda", generator=g) * 0.05
+    wc = (torch.randn(1, 512 + wc_off, device="cuda", generator=g) * 0.05)[:, wc_off:]
     f = torch.relu(torch.randn(B, 512, device="cuda", generator=g))
     e = torch.relu(torch.randn(B, 512, device="cuda", generator=g))
     dout = torch.randn(B, A, device="cuda", generator=g) * 1e-3
@@ -39,11 +40,12 @@ def _fused(B, A, case):
     return df, de, am
 
 
-@pytest.mark.parametrize("B,A", [(1, 4), (31, 4), (33, 4), (2048, 4), (2049, 6), (16384, 4),
-                                 (4096, 1), (4096, 8)])
-def test_head_backward_vs_fp64(B, A):
+@pytest.mark.parametrize("B,A,wc_off", [(1, 4, 0), (31, 4, 0), (33, 4, 0), (2048, 4, 0), (2049, 6, 2), (16384, 4, 0),
+                                        (4096, 1, 1), (4096, 8, 0), (600, 3, 3), (600, 7, 3)])
+def test_head_backward_vs_fp64(B, A, wc_off):
+    """(w_critic misaligned as the flat buffer leaves it for A mod 4 != 0 — read by dwords)"""
     import native
-    case = _case(B, A, B * 10 + A)
+    case = _case(B, A, B * 10 + A, wc_off)
     W, wa, wc, f, e, dout, dv, qd = case
     df, de, am = _fused(B, A, case)
     assert bool((df[B] == 7.0).all()) and bool((de[B] == 7.0).all()), "nothing written past the rows"

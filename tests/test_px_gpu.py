@@ -127,6 +127,34 @@ def test_px_training_pass_is_fp32_class(B):
     print("PX/off error ratios (worst 3):", sorted(worst, reverse=True)[:3])
 
 
+@pytest.mark.parametrize("A", [1, 3, 6, 7, 18])
+def test_training_pass_any_action_count(A):
+    """the training pass through FlatParams at action counts whose flat-buffer offsets leave
+    critic_ext.weight off 16 B (513 A mod 4 != 0: Pong / SpaceInvaders have A = 6) — the fused heads' backward
+    (A <= 8) reads it by dwords; A = 18 takes the two-launch form.  Every gradient within 2x the error of the
+    PX-off pass against float64 with the pass's own ReLU decisions, as test_px_training_pass_is_fp32_class."""
+    import models
+    B = 300
+    net, ref, flat, cv = _setup(100 + A, A=A)
+    off = (net.critic_ext.weight.data_ptr() - flat.data.data_ptr()) // 4
+    assert off % 4 == (513 * A) % 4
+    assert models.HEAD_BWD_FUSED and cv.split_head_bwd(B)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(A)
+    dout = torch.randn(B, A, device="cuda", generator=g)
+    dv = torch.randn(B, device="cuda", generator=g)
+    m_off, m_on = [], []
+    o_off, v_off, g_off, _ = _pass(net, flat, cv, x, dout, dv, False, m_off)
+    o_on, v_on, g_on, _ = _pass(net, flat, cv, x, dout, dv, True, m_on)
+    r_on, r_off = _fp64_masked(ref, x, dout, dv, m_on), _fp64_masked(ref, x, dout, dv, m_off)
+    for name, r in r_on[2].items():
+        scale = r.abs().max().item() + 1e-30
+        e_on = (g_on[name].cpu().double() - r).abs().max().item() / scale
+        e_off = (g_off[name].cpu().double() - r_off[2][name]).abs().max().item() / scale
+        assert e_on <= 2 * e_off + 2e-7, (name, e_on, e_off)
+        assert e_on <= 1e-4, (name, e_on)
+
+
 @pytest.mark.parametrize("B", [8192, 9001])
 def test_px_training_pass_big_batch_matches_f32_operands(B):
     """From 8,192 rows (the sg2 fc forward and the split hidden head): PX on vs off, no fp64 (too

@@ -56,6 +56,7 @@ def _rank(port, algo, cfg, q):
     try:
         tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
         import dist
+        import native
         dist.DistContext.enabled = property(lambda self: True)  # the world > 1 code paths on one rank
         res = _train(algo, cfg)
         # the per-minibatch all-reduces went through the native communicator (csrc/dp.cpp)
@@ -73,6 +74,25 @@ def _rank(port, algo, cfg, q):
             raise AssertionError("int32 accepted")
         except TypeError:
             pass
+        # one asynchronous reduction at a time: the second before the join is refused
+        comm.all_reduce_(z, wait=False)
+        try:
+            comm.all_reduce_(z, wait=False)
+            raise AssertionError("second asynchronous reduction accepted")
+        except native.NativeError:
+            pass
+        comm.wait()
+        # a blocking reduction on another stream is ordered after the asynchronous one and the blocking one
+        # before it (csrc/dp.cpp order_after_last)
+        s2 = torch.cuda.Stream()
+        with torch.cuda.stream(s2):
+            u = torch.full((1 << 20,), 2.0, device="cuda")
+            comm.all_reduce_(u)
+        torch.cuda.current_stream().wait_stream(s2)
+        assert bool((u == 2.0).all())
+        # the creation self-check ran: it is the communicator's first reduction, so a wrong sum would have raised
+        # inside the first train(); destroy before the process group goes (exit-time SIGSEGV)
+        assert dist.shutdown() == 0 and dist._dp_comm is None and comm.handle is None
         q.put(res)
     except Exception as e:  # surface the failure to the parent
         q.put(repr(e))
