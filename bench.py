@@ -88,7 +88,8 @@ def _kernels():
            ("dgrad", 2): r"(ddgrad2_kernel|dgrad2_colp_kernel<true, false>)",
            ("dgrad", 3): _sg("SgDgradPM<64, 9, 9, 3, 3, 1, 64, true>", "4, 2"),
            ("wgrad", 1): (re.escape("wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>")
-                          if os.environ.get("PPOX_WGRAD1_IM2COL") == "1" else r"wgrad1_frames_kernel<true>"),
+                          if os.environ.get("PPOX_AB") == "1" and os.environ.get("PPOX_WGRAD1_IM2COL") == "1"
+                          else r"wgrad1_frames_kernel<true>"),
            ("wgrad", 2): re.escape("wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128, false, 1>"),
            ("wgrad", 3): re.escape("wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64, false, 1") + IDX + ">"}
     for op in ("fwd", "dgrad", "wgrad"):
@@ -129,7 +130,10 @@ def _kernels():
                                      # (the direct form, csrc/dconv.hip fcd_kernel, by default; PPOX_DFCD=0: sg2)
                                      rocprof=r"(fcd_kernel|" + _rows(512, 3136, 1, "true") + ")", label="fc dgrad")
     k["ppox_nature_fc_wgrad"] = dict(rows_arg=1, macs=FC_K * FC_N, bytes=FC_N * 4 + ACT_B[3], fixed=w_fc, products=3,
-                                     rocprof=re.escape("wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 49") + IDX + ">",
+                                     # (PX df and h3: the direct form, csrc/conv.hip fcwg_kernel, round 6; else the
+                                     # split wgrad form)
+                                     rocprof=r"(fcwg_kernel|" + re.escape(
+                                         "wgrad_split_kernel<512, 1, 1, 1, 1, 1, 64, false, 128, false, 49") + IDX + ">)",
                                      label="fc wgrad")
     w_h = HID * HID * 4
     k["ppox_head_hidden_fwd"] = dict(rows_arg=1, macs=HID * HID, bytes=2 * HID * 4, fixed=w_h, products=3,

@@ -204,6 +204,18 @@ int ppox_grad_sumsq(const float* grads, int64_t n, double* partials, void* strea
 int ppox_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                    const double* norm_partials, float max_norm, double lr, double beta1,
                    double beta2, double eps, int64_t step, float* total_norm_out, void* stream);
+/* ppox_adam_step that also records the amax partials of the NatureCNN weights it updates (round 6: the
+ * weight packing's amax pass folded into the Adam step).  ranges (host): PPOX_WMAX_TENSORS element offsets
+ * into params, then as many counts (0: none) — conv1, conv2, conv3, fc and the heads' hidden-layer weight,
+ * in ppox_nature_pack_all's order; amax_out (16B-aligned, PPOX_WMAX_TENSORS x PPOX_WMAX_SLOTS uint32, zeroed
+ * beforehand: ppox_nature_pack_all_wmax's amax_next) gets per slot the maximum |p| after the update (f32 bits,
+ * atomicMax: order-free, deterministic).  Params, moments and total_norm_out bitwise ppox_adam_step's. */
+#define PPOX_WMAX_TENSORS 5
+#define PPOX_WMAX_SLOTS 256
+int ppox_adam_step_wmax(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                        const double* norm_partials, float max_norm, double lr, double beta1, double beta2,
+                        double eps, int64_t step, float* total_norm_out, const int64_t* ranges,
+                        uint32_t* amax_out, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Synthetic device environments (replace SB3 SubprocVecEnv + gym/ALE, env.py:7-12).
@@ -307,6 +319,16 @@ int ppox_nature_pack_all(const float* w1, const float* b1, const float* w2, cons
                          const float* b3, const float* wfc, float* wpd2, uint16_t* q1, uint16_t* q2, uint16_t* q3,
                          uint16_t* qd2, uint16_t* qd3, uint16_t* qfc_fwd, uint16_t* qfc_dgrad, const float* wh,
                          uint16_t* qh_fwd, uint16_t* qh_dgrad, uint32_t* zero, int64_t zero_words, void* stream);
+/* ppox_nature_pack_all with the weights' amax partials given (round 6): amax_in (nullable) = the partials
+ * ppox_adam_step_wmax recorded for exactly these weights, unchanged since — then ONE launch (no amax pass;
+ * the packed forms bitwise what ppox_nature_pack_all writes, but for the tails' amax partials, which hold the
+ * step's slot partition of the same maximum); null: the amax pass as ppox_nature_pack_all.  amax_next (nullable, != amax_in): PPOX_WMAX_TENSORS x PPOX_WMAX_SLOTS uint32 zeroed
+ * on the way (the buffer the next ppox_adam_step_wmax records into). */
+int ppox_nature_pack_all_wmax(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                              const float* b3, const float* wfc, float* wpd2, uint16_t* q1, uint16_t* q2,
+                              uint16_t* q3, uint16_t* qd2, uint16_t* qd3, uint16_t* qfc_fwd, uint16_t* qfc_dgrad,
+                              const float* wh, uint16_t* qh_fwd, uint16_t* qh_dgrad, const uint32_t* amax_in,
+                              uint32_t* amax_next, uint32_t* zero, int64_t zero_words, void* stream);
 /* conv1 -> conv2 on H1P, the split-f16 operand form of conv1's output h1 (Conv2d(4, 32, 8, 4) + ReLU
  * of models-checkpoint.py:52-53): per pixel (NHWC) its 32 channels' high f16 plane then their low
  * plane, h1 * 2^E = hi + lo (128 B per pixel, the size of the f32 form), E derived by
@@ -453,13 +475,17 @@ int ppox_relu_backward_amax_(float* grad, const float* act, int64_t n, uint32_t*
  * w_critic_int = div^T ie, b_critic_int = sum div, b_int_extra = sum die.  Outputs are
  * overwritten.  h <= 512, A <= 18.  Workspace: ppox_head_grads_workspace_bytes.  relu_df != 0:
  * df is first masked by the fc layer's ReLU, df = f > 0 ? df : 0, IN PLACE (the nn.ReLU backward
- * of models-checkpoint.py:57, fused), its max |df| recorded into amax_df (nullable). */
+ * of models-checkpoint.py:57, fused), its max |df| recorded into amax_df (nullable).  df_planes
+ * (nullable, relu_df == 0, h % 32 == 0; round 6): df's PX planes written in the same pass, bitwise
+ * ppox_px_split(df, df_planes_amax, df_planes, df_planes_exp) — the fc dgrad / weight gradient's
+ * operand without a pass of its own. */
 int64_t ppox_head_grads_workspace_bytes(int64_t rows, int64_t h, int64_t n_actions, int32_t intrinsic);
 int ppox_head_grads(const float* f, const float* e, const float* dout, const float* dv, const float* de,
                     const float* df, const float* ie, const float* div, const float* die, int64_t rows, int64_t h,
                     int64_t n_actions, void* workspace, float* w_actor, float* b_actor, float* w_critic,
                     float* b_critic, float* b_extra, float* b_fc, float* w_critic_int, float* b_critic_int,
-                    float* b_int_extra, int32_t relu_df, uint32_t* amax_df, void* stream);
+                    float* b_int_extra, int32_t relu_df, uint32_t* amax_df, uint16_t* df_planes,
+                    const uint32_t* df_planes_amax, int32_t* df_planes_exp, void* stream);
 /* Skinny heads (models-checkpoint.py:60-87 actor / critic Linear layers, n_out <= 8):
  * ppox_skinny_linear: y (rows x n_out) = x (rows x h) w^T + bias, one wave per row;
  * ppox_skinny_dgrad:  d (rows x h) = g (rows x n_out) w (n_out x h) — overwritten. */

@@ -36,33 +36,33 @@ SPLIT_SLOWER = set()
 # overrides, default: every batch), split over K below FC_SPLITK_MAX_BATCH (tools/fc_bench.py,
 # r02: split-K 0.018 / 0.045 / 0.078 ms vs rocBLAS 0.026 / 0.062 / 0.119 ms at 512 / 2048 /
 # 4096 rows; the plain split GEMM 0.146 vs split-K 0.152 ms at 8192)
-FC_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_SPLIT_MIN", "0"))
-FC_SPLITK_MAX_BATCH = int(os.environ.get("PPOX_FC_SPLITK_MAX", "8192"))
+FC_SPLIT_MIN_BATCH = int(native.ab_env("PPOX_FC_SPLIT_MIN", "0"))
+FC_SPLITK_MAX_BATCH = int(native.ab_env("PPOX_FC_SPLITK_MAX", "8192"))
 # fc dgrad fused with the trunk's ReLU backward + NHWC transpose (split-f16) up to this
 # batch (PPOX_FC_DGRAD_FUSED_MAX overrides): faster than rocBLAS + nchw_to_nhwc_mask at
 # every measured batch (A/B: -33 ms per iteration at 16384, -2 ms at 2048)
-FC_DGRAD_FUSED_MAX_BATCH = int(os.environ.get("PPOX_FC_DGRAD_FUSED_MAX", str(1 << 62)))
+FC_DGRAD_FUSED_MAX_BATCH = int(native.ab_env("PPOX_FC_DGRAD_FUSED_MAX", str(1 << 62)))
 # fc weight gradient on the split wgrad kernel (ppox_nature_fc_wgrad) from this batch up,
 # the rocBLAS f32 GEMM + NHWC -> Flatten permute below (PPOX_FC_WGRAD_SPLIT_MIN overrides)
-FC_WGRAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_FC_WGRAD_SPLIT_MIN", "0"))
+FC_WGRAD_SPLIT_MIN_BATCH = int(native.ab_env("PPOX_FC_WGRAD_SPLIT_MIN", "0"))
 
 # the heads' hidden layer Linear(512, 512) on the split-f16 GEMM (ppox_head_hidden_*) from this
 # batch up, rocBLAS f32 below (PPOX_HEAD_SPLIT_MIN overrides)
-HEAD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_SPLIT_MIN", "8192"))
+HEAD_SPLIT_MIN_BATCH = int(native.ab_env("PPOX_HEAD_SPLIT_MIN", "8192"))
 # below HEAD_SPLIT_MIN_BATCH the hidden layer's forward still runs on the split-f16 kernel, split over K
 # with the critic head fused into its reduce (its backward stays on the library GEMMs);
 # PPOX_HEAD_FWD_SPLITK=0 keeps the library GEMM
-HEAD_FWD_SPLITK = os.environ.get("PPOX_HEAD_FWD_SPLITK", "1") == "1"
+HEAD_FWD_SPLITK = native.ab_env("PPOX_HEAD_FWD_SPLITK", "1") == "1"
 # the hidden layer's backward (dgrad into the fc layer's input grad + weight gradient) on the split-f16
 # kernels from this batch up, the library GEMMs below (PPOX_HEAD_BWD_SPLIT_MIN).  Round 4: at every batch —
 # the same GPU time at the per-rank 2,048 rows (same-box A/B 199.57 vs 199.55-199.79 ms per iteration,
 # profiles/r04_ab.txt) and no library GEMM on the host's launch path (the two rocBLAS calls cost ~100 us of
 # host time per minibatch, which the 8-rank path spends on its collectives)
-HEAD_BWD_SPLIT_MIN_BATCH = int(os.environ.get("PPOX_HEAD_BWD_SPLIT_MIN", "0"))
+HEAD_BWD_SPLIT_MIN_BATCH = int(native.ab_env("PPOX_HEAD_BWD_SPLIT_MIN", "0"))
 
 # ReLU masks of the conv outputs as bitmasks written by the split forwards for the split dgrads
 # (PPOX_RELU_BITS=0: the dgrads read the f32 activations)
-RELU_BITS = os.environ.get("PPOX_RELU_BITS", "1") != "0"
+RELU_BITS = native.ab_env("PPOX_RELU_BITS", "1") != "0"
 
 # rows of a pass's amax table (native.amax_table): the split-f16 operands of the trunk and the
 # heads' hidden layer, each recorded by the kernel that produces it and read by its consumers;
@@ -77,24 +77,24 @@ EX_H2, EX_H3, EX_G3, EX_DF, EX_G2 = range(5)
 # dgrad and weight gradient) — at exponents derived from bounds, so no consumer splits in
 # registers.  PPOX_PX=0: f32 tensors (split in the consumers).  Needs the ReLU bitmasks (the
 # dgrads' masks cannot come from planes).
-PX = os.environ.get("PPOX_PX", "1") != "0"
+PX = native.ab_env("PPOX_PX", "1") != "0"
 # ... from this batch up (PPOX_PX_MIN): every batch since the direct conv2 / conv3 forwards (csrc/dconv.hip,
 # which need the planes; same-box A/B: 1-GPU line 478.6k vs 469.9k env-steps/s — the collect forward at 4,096
 # rows gains most — and per-rank 204.8 vs 207.3 ms; before them PX at 2,048 rows measured 225.8 vs 219.5 ms)
-PX_MIN_BATCH = int(os.environ.get("PPOX_PX_MIN", "0"))
+PX_MIN_BATCH = int(native.ab_env("PPOX_PX_MIN", "0"))
 # PX df (round 4, PPOX_PX_DF=1): the fc layer's df (B x 512, its amax recorded by the head backward)
 # split into its planes by one small kernel (ppox_px_split) for the fc dgrad and weight gradient, which
 # otherwise split every df value in registers once per tile (the fc dgrad: 49 times).  On by default
 # since the direct fc dgrad (csrc/dconv.hip fcd_kernel, which reads the planes: 195 vs 277 us at 16,384
 # rows); with the sg2 fc dgrad alone it measured neutral-to-slower (profiles/r04_ab.txt: 1-GPU 1,152.5
 # vs 1,146.8 ms, per-rank 203.9 vs 201.8 ms per iteration)
-PX_DF = os.environ.get("PPOX_PX_DF", "1") == "1"
+PX_DF = native.ab_env("PPOX_PX_DF", "1") == "1"
 # PX g2 + the direct conv2 dgrad (round 5, PPOX_DDGRAD2=1 by default): the conv3 dgrad writes g2 as its
 # planes (bound: amax(g3) x the conv3 dgrad matrix's column norms), read as they lie by the direct
 # class-wise conv2 dgrad (csrc/dconv.hip ddgrad2_kernel: per input-pixel parity class an implicit GEMM
 # over its 4 taps x 64 channels, no col2im) and by the conv2 weight gradient; =0: f32 g2, the persistent
 # col2im dgrad (dgrad2_colp_kernel)
-DDGRAD2 = os.environ.get("PPOX_DDGRAD2", "1") != "0"
+DDGRAD2 = native.ab_env("PPOX_DDGRAD2", "1") != "0"
 
 
 class PassState:
@@ -120,20 +120,20 @@ class PassState:
 # backward on two streams: each layer's weight gradient runs on a side stream beside the
 # main stream's dgrad chain (wgrad3 || dgrad3, wgrad2 || dgrad2; the fc weight gradient ||
 # the fc dgrad), joined before the optimizer reads the gradients (PPOX_BWD_STREAMS=0: one stream)
-BWD_STREAMS = os.environ.get("PPOX_BWD_STREAMS", "1") != "0"
-BWD_SOLO_DGRAD2_BATCH = int(os.environ.get("PPOX_BWD_SOLO_DGRAD2", str(1 << 62)))
+BWD_STREAMS = native.ab_env("PPOX_BWD_STREAMS", "1") != "0"
+BWD_SOLO_DGRAD2_BATCH = int(native.ab_env("PPOX_BWD_SOLO_DGRAD2", str(1 << 62)))
 # PPOX_FORK_LATE=1: below that batch the conv2 weight gradient's side-stream wait (on the point after the
 # conv3 dgrad) is enqueued after the conv2 dgrad's launch instead of before it — the same dependencies,
 # another capture order for a hipGraph of the pass (tools/graph_probe.py)
-FORK_LATE = os.environ.get("PPOX_FORK_LATE", "0") == "1"
+FORK_LATE = native.ab_env("PPOX_FORK_LATE", "0") == "1"
 # PPOX_FORK_MERGE=1: the heads' hidden-layer weight gradient joins the fc weight gradient's fork to the side
 # stream (one main-stream event record per minibatch fewer; models.CnnActorCritic.backward_train)
-FORK_MERGE = os.environ.get("PPOX_FORK_MERGE", "0") == "1"
+FORK_MERGE = native.ab_env("PPOX_FORK_MERGE", "0") == "1"
 # PPOX_BWD_SOLO_WGRAD2=1: from that batch conv2's weight gradient also runs alone on the main stream
 # (after the dgrad, before wgrad1) instead of beside wgrad1 — 1 % slower (same-box A/B), but its
 # event time is then its own execution time
-BWD_SOLO_WGRAD2 = os.environ.get("PPOX_BWD_SOLO_WGRAD2", "0") != "0"
-SIDE_PRIO = os.environ.get("PPOX_SIDE_PRIO", "0" if os.environ.get("PPOX_TRAIN_PRIO") == "1" else "1") == "1"
+BWD_SOLO_WGRAD2 = native.ab_env("PPOX_BWD_SOLO_WGRAD2", "0") != "0"
+SIDE_PRIO = native.ab_env("PPOX_SIDE_PRIO", "0" if native.ab_env("PPOX_TRAIN_PRIO", "0") == "1" else "1") == "1"
 _side = {}
 
 
@@ -182,7 +182,7 @@ def _event(side, which):
 # the two streams share one device, whose kernels' own release / acquire fences order their data), "device"
 # (hipEventReleaseToDevice), "system" (torch's events: a system-scope fence on every record).  Per-rank
 # 190.9 / 190.8 -> 188.8 ms and 196.2 -> 193.9 ms on two boxes (profiles/r05g)
-EVENT_FENCE = os.environ.get("PPOX_EVENT_FENCE", "none")
+EVENT_FENCE = native.ab_env("PPOX_EVENT_FENCE", "none")
 _nevents = {}
 
 
@@ -267,6 +267,62 @@ class _NatureTrunk(torch.autograd.Function):
         return (None, None, *grads)
 
 
+class WmaxLink:
+    """The weight packing's amax pass folded into the Adam step (round 6): the packing of
+    the five NatureCNN weight tensors needs each tensor's max |w| before it can split a value, which took a
+    launch of its own (wmax_kernel) at every optimizer step.  FlatParams.adam_step records the maxima of the
+    weights it writes (ppox_adam_step_wmax) into bufs[nxt], which the packing zeroed beforehand; the next
+    packing of those same weights (same step count, buffer and torch version counter) reads them and runs as one
+    launch (ppox_nature_pack_all_wmax), zeroing the other buffer for the next step.  Anything else packs with its
+    own amax pass: weights written in place after the step (a torch in-place op on the flat buffer or a view of
+    it bumps the buffer's version counter, one through a weight Parameter — load_state_dict — the Parameter's;
+    both are part of the key), invalidate(), two steps without a packing between."""
+
+    def __init__(self, flat, weights):
+        base, n = flat.data.data_ptr(), flat.data.numel()
+        offs = [(w.data_ptr() - base) // 4 for w in weights]
+        for w, o in zip(weights, offs):
+            if not (w.is_contiguous() and w.dtype == torch.float32 and 0 <= o and o + w.numel() <= n):
+                raise ValueError("WmaxLink: the weights must be contiguous f32 views of the flat buffer")
+        self.ranges = torch.tensor(offs + [w.numel() for w in weights], dtype=torch.int64)
+        self.weights = tuple(weights)
+        self.folds = 0  # packings that read the step's partials (tests)
+        self.bufs = torch.zeros(2, native.WMAX_TENSORS * native.WMAX_SLOTS, dtype=torch.int32, device=flat.device)
+        self.zeroed = [True, True]
+        self.nxt = 0
+        self.valid = None  # (step count, data pointer, torch version, buffer) of the last recorded maxima
+
+    def ready(self, flat):
+        """the buffer the next step records into is zeroed"""
+        return self.zeroed[self.nxt]
+
+    def recording(self):
+        return self.bufs[self.nxt]
+
+    def _key(self, flat):
+        return (flat.step_count, flat.data.data_ptr(), flat.data._version) + tuple(w._version for w in self.weights)
+
+    def recorded(self, flat):
+        self.valid = (self._key(flat), self.nxt)
+        self.zeroed[self.nxt] = False
+
+    def for_pack(self, flat):
+        """(amax_in or None, amax_next) for a packing of the weights as they are now"""
+        if self.valid is not None and self.valid[0] == self._key(flat):
+            i = self.valid[1]
+            self.nxt = i ^ 1
+            amax_in = self.bufs[i]
+            self.folds += 1
+        else:
+            self.valid = None
+            amax_in = None
+        self.zeroed[self.nxt] = True  # zeroed by the packing launch (stream order: before the next step)
+        return amax_in, self.bufs[self.nxt]
+
+    def invalidate(self):
+        self.valid = None
+
+
 class NatureConvs:
     """Callable conv trunk bound to a CnnActorCritic whose parameters live in a FlatParams."""
 
@@ -316,6 +372,13 @@ class NatureConvs:
         self._packed = set()
         self._last_batch = None
         self._forms_cache = {}
+        # the Adam step records the packing's amax partials (split math; PPOX_WMAX_FOLD=0 under PPOX_AB=1: the
+        # packing's own amax pass at every step)
+        self._wmax = None
+        if self.math != "f32" and native.ab_env("PPOX_WMAX_FOLD", "1") != "0":
+            self._wmax = WmaxLink(flat, (self.c1.weight, self.c2.weight, self.c3.weight, self.fc.weight,
+                                         self.hid.weight))
+        flat.wmax = self._wmax  # the flat's latest trunk (a re-attach replaces the link)
 
     def split_head(self, batch):
         """the heads' hidden layer on the split-f16 kernels for a `batch`-row pass"""
@@ -439,10 +502,21 @@ class NatureConvs:
             q = self.q
             qfc = self.qfc or (None, None)
             qh = self.qh or (None, None)
-            native.nature_pack_all(w1, w2, w3, self.fc.weight, pick("wpd2", self.wpd2), pick("q1", q[1]),
-                                   pick("q2", q[2]), pick("q3", q[3]), pick("qd2", q[12]), pick("qd3", q[13]),
-                                   pick("qfcf", qfc[0]), pick("qfcd", qfc[1]), self.hid.weight, pick("qhf", qh[0]),
-                                   pick("qhd", qh[1]), b1=self.c1.bias, zero=zero, b2=self.c2.bias, b3=self.c3.bias)
+            lk = self._wmax if self._wmax is not None and self.flat.wmax is self._wmax else None
+            if lk is not None:
+                amax_in, amax_next = lk.for_pack(self.flat)
+                native.nature_pack_all_wmax(w1, w2, w3, self.fc.weight, pick("wpd2", self.wpd2), pick("q1", q[1]),
+                                            pick("q2", q[2]), pick("q3", q[3]), pick("qd2", q[12]),
+                                            pick("qd3", q[13]), pick("qfcf", qfc[0]), pick("qfcd", qfc[1]),
+                                            self.hid.weight, pick("qhf", qh[0]), pick("qhd", qh[1]), b1=self.c1.bias,
+                                            zero=zero, b2=self.c2.bias, b3=self.c3.bias, amax_in=amax_in,
+                                            amax_next=amax_next)
+            else:
+                native.nature_pack_all(w1, w2, w3, self.fc.weight, pick("wpd2", self.wpd2), pick("q1", q[1]),
+                                       pick("q2", q[2]), pick("q3", q[3]), pick("qd2", q[12]), pick("qd3", q[13]),
+                                       pick("qfcf", qfc[0]), pick("qfcd", qfc[1]), self.hid.weight,
+                                       pick("qhf", qh[0]), pick("qhd", qh[1]), b1=self.c1.bias, zero=zero,
+                                       b2=self.c2.bias, b3=self.c3.bias)
             zeroed = zero is not None
         if "wfc_nhwc" in missing:
             torch.index_select(self.fc.weight.detach(), 1, self.fc_perm, out=self.wfc_nhwc)
@@ -453,6 +527,8 @@ class NatureConvs:
         self._version = None
         self._packed = set()
         self._last_batch = None
+        if self._wmax is not None:
+            self._wmax.invalidate()
 
     # -- per-op dispatch (layer 1 input: uint8 frames, sample stride 4*84*84 bytes).  am: the
     # pass's amax table; a split kernel reads its f32 operands' rows and records its output's, an

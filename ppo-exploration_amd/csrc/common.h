@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/ppox.h"
@@ -16,6 +17,13 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 inline unsigned ceil_div(long long a, long long b) { return static_cast<unsigned>((a + b - 1) / b); }
+
+// An A/B switch's environment variable (kernel forms, gates): read only under PPOX_AB=1, else null (the
+// compiled-in default) — a stray PPOX_* variable never changes the product path (native.py ab_env)
+inline const char* ab_env(const char* name) {
+    const char* ab = std::getenv("PPOX_AB");
+    return ab && ab[0] == '1' && ab[1] == 0 ? std::getenv(name) : nullptr;
+}
 
 }  // namespace ppox
 

@@ -35,6 +35,8 @@
 #include <type_traits>
 #include <unordered_set>
 
+#include <utility>
+
 #include "conv_common.h"
 
 namespace {
@@ -496,21 +498,13 @@ struct Px : Base {
     static constexpr bool A_PLANES = AP, PLANES_OUT = PO;
 };
 
-#ifndef FC_FWD_G
-#define FC_FWD_G 8  // fc forward: column blocks per tile group (SgRows): all 8, each h3 row tile read once
-#endif
-#ifndef FC_DGRAD_G
-#define FC_DGRAD_G 12  // fc dgrad: column blocks per tile group
-#endif
-#ifndef FC_NB
-#define FC_NB 64  // the packed fc / head B blocks (64 columns)
-#endif
-#ifndef SG_FC_NB
+constexpr int FC_FWD_G = 8;  // fc forward: column blocks per tile group (SgRows): all 8, each h3 row tile read once
+constexpr int FC_DGRAD_G = 12;  // fc dgrad: column blocks per tile group
+constexpr int FC_NB = 64;  // the packed fc / head B blocks (64 columns)
 // columns per sg2 tile of the fc / head GEMMs: 64; 128 (A staged once per 128 columns, four
 // column tiles per wave) measured slower — 358 registers, one wave per SIMD (round 4 same-box
 // A/B: 1-GPU 427.4k vs 439.6k env-steps/s, per-rank 225.8 vs 215.5 ms)
-#define SG_FC_NB 64
-#endif
+constexpr int SG_FC_NB = 64;
 // column-block groups of the wide tiles: the same column span per group as the 64-column FC_*_G
 constexpr int FC_FWD_GW = FC_FWD_G * 64 / SG_FC_NB, FC_DGRAD_GW = FC_DGRAD_G * 64 / SG_FC_NB;
 constexpr int HEAD_GW = 512 / SG_FC_NB;
@@ -1075,26 +1069,18 @@ __global__ void __launch_bounds__(64 * WAVES, 8 / WAVES) sgemm_kernel(Args a, co
     amax_record(a.amax_y, om);
 }
 
-#ifndef SG_WAVES
-#define SG_WAVES 4  // 4: two 128-row workgroups per CU (2 ring slots); 8: one 256-row workgroup (3 slots)
-#endif
+constexpr int SG_WAVES = 4;  // 4: two 128-row workgroups per CU (2 ring slots); 8: one 256-row workgroup (3 slots)
 // ring slots (chunks in flight + 1) per Problem (Prob::SLOTS): 3 for the plain fc / head GEMMs
 // (their DMA latency was exposed with one chunk of lookahead: fc forward 0.190 -> 0.174 ms,
 // dgrad 0.255 -> 0.238), 2 for the conv forms (3 measured slower for the conv3 dgrad, 0.31 ->
-// 0.34 ms); 3 x 24 KB per workgroup keeps two workgroups per CU.  SG_SLOTS overrides all.
+// 0.34 ms); 3 x 24 KB per workgroup keeps two workgroups per CU.
 constexpr int SG_ROWS = 32 * SG_WAVES;
-#ifndef SG_FWD2_PARITY
-#define SG_FWD2_PARITY 1  // conv2 forward taps in input-parity classes (SgFwd)
-#endif
+constexpr int SG_FWD2_PARITY = 1;  // conv2 forward taps in input-parity classes (SgFwd)
 
 template <class Prob>
 int launch_sgemm(const Args& a, const uint16_t* wq, long long blocks, hipStream_t s, const char* name) {
     if (blocks == 0) return PPOX_OK;
-#ifdef SG_SLOTS
-    constexpr int slots = SG_SLOTS;
-#else
     constexpr int slots = SG_WAVES == 8 ? 3 : Prob::SLOTS;
-#endif
     sgemm_kernel<Prob, SG_WAVES, slots><<<(unsigned)blocks, 64 * SG_WAVES, 0, s>>>(
         a, reinterpret_cast<const u32x4*>(wq));
     PPOX_LAUNCHED(name);
@@ -2509,12 +2495,8 @@ constexpr int W1F_LDS = 2 * W1F_BUF;           // 109,312 B
 constexpr int W1F_XU = 4 * W1F_ROWS * 6;       // frame pieces of a unit: (ci, y, 16-B group) = 1056
 constexpr int W1F_G4 = 200 * 8;                // float4 of g1 per unit: 1600
 constexpr int W1F_SAMPLE = 4 * 84 * 84;        // frame bytes per sample
-#ifndef W1F_DEPTH
-#define W1F_DEPTH 2  // units of loads in flight (register sets)
-#endif
-#ifndef W1F_FLUSH
-#define W1F_FLUSH 8  // units per partial sum (4 samples: ~960 pixels per accumulation chain and parity)
-#endif
+constexpr int W1F_DEPTH = 2;  // units of loads in flight (register sets)
+constexpr int W1F_FLUSH = 8;  // units per partial sum (4 samples: ~960 pixels per accumulation chain and parity)
 static_assert(W1F_DEPTH == 2 || W1F_DEPTH == 3, "wgrad1 frames: two or three register sets");
 static_assert(W1F_LDS <= 160 * 1024 && W1F_PH % 16 == 0 && W1F_YS % 8 == 0, "wgrad1 frames: LDS layout");
 static_assert(W1F_XU <= 3 * 512 && W1F_G4 <= 4 * 512, "wgrad1 frames: loads per thread");
@@ -2826,9 +2808,7 @@ int launch_rgemm(const Args& a, long long blocks, hipStream_t s, const char* nam
     rgemm_kernel<Prob, OUT_NCHW><<<(unsigned)blocks, 256, 0, s>>>(a);
     PPOX_LAUNCHED(name);
 }
-#ifndef RG_FWD1_MT
-#define RG_FWD1_MT 2
-#endif
+constexpr int RG_FWD1_MT = 2;
 
 template <class L, bool U8>
 int launch_wgrad(const WArgs& wa_in, hipStream_t s) {
@@ -2855,18 +2835,10 @@ int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float
 }
 
 
-#ifndef WS_KT2
-#define WS_KT2 128
-#endif
-#ifndef WS_KT3
-#define WS_KT3 64
-#endif
-#ifndef WS_PX
-#define WS_PX 2048  // split wgrad: pixels per split-K slice
-#endif
-#ifndef WS_FILL
-#define WS_FILL 512  // split wgrad: workgroups at least (conv1 / conv2, small batches)
-#endif
+constexpr int WS_KT2 = 128;
+constexpr int WS_KT3 = 64;
+constexpr int WS_PX = 2048;  // split wgrad: pixels per split-K slice
+constexpr int WS_FILL = 512;  // split wgrad: workgroups at least (conv1 / conv2, small batches)
 // split wgrad: its own split-K count (~WS_PX pixels per split so the grid fills the chip)
 template <class L, bool U8, int KT, bool XPL = false, bool GPL = false>
 struct WsLaunch {
@@ -2930,6 +2902,11 @@ struct PackAll {
     uint32_t* zero = nullptr;                          // words zeroed by wmax_kernel (a pass's amax table)
     long long zero_words = 0;
     const float *b2 = nullptr, *b3 = nullptr;          // conv2 / conv3 biases (with q2 / q3: the PX bounds)
+    // round 6: the tensors' amax partials as the Adam step recorded them ([PA_TENSORS][AMAX_SLOTS], the weights
+    // unchanged since; null: the packing's own amax pass), and the partials buffer the next Adam step records into
+    // (zeroed here; nullable)
+    const uint32_t* amax_in = nullptr;
+    uint32_t* amax_next = nullptr;
 };
 constexpr long long PA_N1 = 8 * 2 * 64 * 8, PA_N2 = (long long)G2::K * G2::COUT, PA_N3 = (long long)G3::K * G3::COUT;
 constexpr long long PA_NFC = (long long)FcFwd::NCB * FcFwd::K * FcFwd::NOUT;
@@ -3138,24 +3115,58 @@ __device__ void norm_block(const PackAll& p, int job, int b) {
 // tensor's max.  Then AMAX_SLOTS workgroups per PX norm job, one workgroup for the H1P exponent
 // (with q1 and b1), then the workgroups zeroing p.zero (the next pass's amax table: no fill launch
 // of its own)
-__global__ void __launch_bounds__(256) wmax_kernel(PackAll p) {
-    if (blockIdx.x >= PA_TENSORS * AMAX_SLOTS) {
-        const int nb = (int)blockIdx.x - PA_TENSORS * AMAX_SLOTS;
-        if (nb < PA_NORM_JOBS * AMAX_SLOTS) {
-            norm_block(p, nb / AMAX_SLOTS, nb % AMAX_SLOTS);
-            return;
-        }
-        const long long zb = (long long)nb - PA_NORM_JOBS * AMAX_SLOTS - 1;
-        if (zb < 0) {
-            if (p.q1 && p.b1) h1p_exp_block(p.w1, p.b1, p.q1);
-            return;
-        }
-        const long long i = (zb * 256 + threadIdx.x) * 4;  // this thread's four words
+// The packing's auxiliary workgroups (nb = 0, 1, ...): the PX norm jobs, the H1P exponent, the zeroing of p.zero
+// (1,024 words per workgroup) and of p.amax_next, and — with p.amax_in — one workgroup per tensor copying the
+// given amax partials into the tails of its forms (where the amax pass would have written them)
+constexpr int PA_NEXT_WORDS = PA_TENSORS * AMAX_SLOTS, PA_NEXT_BLOCKS = (PA_NEXT_WORDS + 1023) / 1024;
+static_assert(PA_NEXT_WORDS % 4 == 0, "amax_next: whole uint4 stores");
+inline long long pack_aux_blocks(const PackAll& p) {
+    return PA_NORM_JOBS * AMAX_SLOTS + 1 + ppox::ceil_div(p.zero_words, 1024LL) + (p.amax_next ? PA_NEXT_BLOCKS : 0) +
+           (p.amax_in ? PA_TENSORS : 0);
+}
+__device__ void pack_aux_block(const PackAll& p, long long nb) {
+    if (nb < PA_NORM_JOBS * AMAX_SLOTS) {
+        norm_block(p, (int)(nb / AMAX_SLOTS), (int)(nb % AMAX_SLOTS));
+        return;
+    }
+    nb -= PA_NORM_JOBS * AMAX_SLOTS;
+    if (nb == 0) {
+        if (p.q1 && p.b1) h1p_exp_block(p.w1, p.b1, p.q1);
+        return;
+    }
+    nb -= 1;
+    const long long zblocks = (p.zero_words + 1023) / 1024;
+    if (nb < zblocks) {
+        const long long i = (nb * 256 + threadIdx.x) * 4;  // this thread's four words
         if (i + 4 <= p.zero_words) {
             *reinterpret_cast<uint4*>(p.zero + i) = make_uint4(0u, 0u, 0u, 0u);
         } else {
             for (long long k = i; k < p.zero_words; ++k) p.zero[k] = 0u;  // a ragged tail
         }
+        return;
+    }
+    nb -= zblocks;
+    if (p.amax_next) {
+        if (nb < PA_NEXT_BLOCKS) {
+            const long long i = nb * 256 + threadIdx.x;
+            if (4 * i < PA_NEXT_WORDS) reinterpret_cast<uint4*>(p.amax_next)[i] = make_uint4(0u, 0u, 0u, 0u);
+            return;
+        }
+        nb -= PA_NEXT_BLOCKS;
+    }
+    if (p.amax_in && nb < PA_TENSORS) {
+        uint16_t* f[2];
+        long long planes;
+        pa_forms(p, (int)nb, f, planes);
+        const uint32_t v = p.amax_in[nb * AMAX_SLOTS + threadIdx.x];
+        for (int k = 0; k < 2; ++k)
+            if (f[k]) pack_tail(f[k], planes)[threadIdx.x] = v;
+    }
+}
+
+__global__ void __launch_bounds__(256) wmax_kernel(PackAll p) {
+    if (blockIdx.x >= PA_TENSORS * AMAX_SLOTS) {
+        pack_aux_block(p, (long long)blockIdx.x - PA_TENSORS * AMAX_SLOTS);
         return;
     }
     const int t = blockIdx.x / AMAX_SLOTS, b = blockIdx.x % AMAX_SLOTS;
@@ -3185,9 +3196,14 @@ __global__ void __launch_bounds__(256) wmax_kernel(PackAll p) {
 
 __device__ uint32_t kZeroTail[AMAX_SLOTS] = {};  // the amax partials of a tensor packed into no form
 
-__global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long total) {
-    // the tensors' scales (wave-uniform), from the partials of their first packed form; the five
-    // reads are unconditional (a tensor with no form reads zeros), so they are one round trip
+// npack: the packing workgroups; with p.amax_in the auxiliary ones follow them (the amax pass's, in this launch)
+__global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long total, unsigned npack) {
+    if (blockIdx.x >= npack) {
+        pack_aux_block(p, (long long)(blockIdx.x - npack));
+        return;
+    }
+    // the tensors' scales (wave-uniform), from the partials of their first packed form (or the given ones); the
+    // five reads are unconditional (a tensor with no form reads zeros), so they are one round trip
     float sc[PA_TENSORS];
     uint32_t am[PA_TENSORS];
 #pragma unroll
@@ -3196,7 +3212,7 @@ __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long tota
         long long planes;
         pa_forms(p, t, f, planes);
         uint16_t* src = f[0] ? f[0] : f[1];
-        am[t] = amax_read(src ? pack_tail(src, planes) : kZeroTail);
+        am[t] = amax_read(!src ? kZeroTail : p.amax_in ? p.amax_in + t * AMAX_SLOTS : pack_tail(src, planes));
     }
 #pragma unroll
     for (int t = 0; t < PA_TENSORS; ++t) {
@@ -3209,7 +3225,7 @@ __global__ void __launch_bounds__(256) pack_all_kernel(PackAll p, long long tota
             for (int k = 0; k < 2; ++k)
                 if (f[k]) pack_tail(f[k], planes)[AMAX_SLOTS] = (uint32_t)e;
     }
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)npack * 256) {
         long long j = i;
         if (j < PA_N1) { if (p.q1) pack_fwd1_split_elem(p.w1, sc[0], p.q1, (int)j); continue; }
         j -= PA_N1;
@@ -3272,20 +3288,25 @@ int launch_pack_all(const PackAll& p, hipStream_t s, const char* name) {
     PPOX_REQUIRE((!p.qhf || ppox::aligned16(p.qhf)) && (!p.qhd || ppox::aligned16(p.qhd)),
                  "ppox_nature_pack: packed buffers must be 16-byte aligned");
     PPOX_REQUIRE(!p.zero_words || (p.zero && ppox::aligned16(p.zero)), "ppox_nature_pack_all: zero buffer");
-    const long long zblocks = ppox::ceil_div(p.zero_words, 1024LL);
-    wmax_kernel<<<(unsigned)((PA_TENSORS + PA_NORM_JOBS) * AMAX_SLOTS + 1 + zblocks), 256, 0, s>>>(p);
-    PPOX_LAUNCHED_NORET(name);
+    PPOX_REQUIRE((!p.amax_in || ppox::aligned16(p.amax_in)) && (!p.amax_next || ppox::aligned16(p.amax_next)) &&
+                     (!p.amax_in || p.amax_in != p.amax_next),
+                 "ppox_nature_pack_all: amax partials buffers");
+    const long long aux = pack_aux_blocks(p);
+    if (!p.amax_in) {  // the amax pass, then the packing
+        wmax_kernel<<<(unsigned)(PA_TENSORS * AMAX_SLOTS + aux), 256, 0, s>>>(p);
+        PPOX_LAUNCHED_NORET(name);
+    }
     // element ranges end at the last job present (the head and fc dgrad ranges are the longest)
     const long long total = PA_N1 + 2 * PU_2 + 2 * PU_3 + PA_N2 + PU_FC +
                             (p.qhf || p.qhd ? PU_FCD + 2 * PU_H : (p.qfcd ? PU_FCD : 0));
     // every wave first reads the five tensors' 256 amax partials (5 KB): 4,096 workgroups re-read 80 MB of them
     // through L2 — a few hundred, each striding over more units, read a few MB (PPOX_PACK_BLOCKS: A/B knob)
     static const long long cap = [] {
-        const char* e = std::getenv("PPOX_PACK_BLOCKS");
+        const char* e = ppox::ab_env("PPOX_PACK_BLOCKS");
         return e ? std::max(1LL, std::atoll(e)) : 512LL;
     }();
     const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, cap);
-    pack_all_kernel<<<blocks, 256, 0, s>>>(p, total);
+    pack_all_kernel<<<blocks + (unsigned)(p.amax_in ? aux : 0), 256, 0, s>>>(p, total, blocks);
     PPOX_LAUNCHED_NORET(name);
     note_px_pack(p.q2, p.b2 != nullptr);
     note_px_pack(p.q3, p.b3 != nullptr);
@@ -3596,7 +3617,7 @@ extern "C" int ppox_nature_conv_dgrad_split(int32_t layer, const float* grad_out
         const long long grid = std::min<long long>(ntriples, cus[dev]);
         a.bits_mask = relu_bits;
         // PPOX_COLP_VMCNT0=1: every counted wait of the kernel as vmcnt(0) (the same result, bitwise)
-        const char* safe_env = std::getenv("PPOX_COLP_VMCNT0");
+        const char* safe_env = ppox::ab_env("PPOX_COLP_VMCNT0");
         const bool safe = safe_env && safe_env[0] == '1';
         const u32x4* wqv = reinterpret_cast<const u32x4*>(wqd);
         if (relu_bits && !safe)
@@ -3658,7 +3679,7 @@ void w2p_grid(long long batch, int& per, long long& grid, int min_per) {
 // PPOX_W2P_MIN_PER (A/B knob, default 1): the conv2 weight gradient's samples-per-workgroup floor
 int w2p_min_per() {
     static const int v = [] {
-        const char* e = std::getenv("PPOX_W2P_MIN_PER");
+        const char* e = ppox::ab_env("PPOX_W2P_MIN_PER");
         return e ? std::max(1, std::atoi(e)) : 1;
     }();
     return v;
@@ -3668,7 +3689,7 @@ int w2p_min_per() {
 // PPOX_WGRAD1_IM2COL=1 runs the im2col form (wgrad_split_kernel) instead
 bool wgrad1_im2col() {
     static const int v = [] {
-        const char* e = std::getenv("PPOX_WGRAD1_IM2COL");
+        const char* e = ppox::ab_env("PPOX_WGRAD1_IM2COL");
         return e && e[0] == '1' ? 1 : 0;
     }();
     return v != 0;
@@ -3872,8 +3893,260 @@ __global__ void __launch_bounds__(256) fc_wgrad_reduce_perm(const float* __restr
     }
 }
 
+// ---------------------------------------------------------------------------
+// fc weight gradient, direct (round 6; models-checkpoint.py:60 Linear(3136, 512) trained by ppo.py:241):
+//   dW[o][f] = sum over rows r of df[r][o] h3[r][f]      (f = p * 64 + c, NHWC; stored in Flatten order by the reduce)
+// on PX df and PX h3 (both operands as their two f16 planes, as the fc dgrad and forward read them).  The split
+// wgrad form (wgrad_split_kernel<GFc>) tiles 128 outputs x one pixel (64 features) per workgroup, two per CU, and
+// needs 13 split-K slabs at 16,384 rows to fill the chip: its L2 -> LDS staging is ~0.5 KB per MFMA and its slabs
+// + reduce 84 MB each way (PMC 2.0x the algorithmic bytes).  Here one 256-thread workgroup per
+// CU owns 256 outputs x 2 pixels (128 features) over a fifth of the rows: 50 tiles x 5 splits = 250 workgroups,
+// 0.33 KB staged per MFMA, 5 slabs.
+//   * per 16-row k-step the workgroup stages 24 sub-images of 16 rows x 32 columns f16 (1 KB each): df (8 output
+//     groups x 2 planes) and h3 (2 pixels x 2 channel halves x 2 planes), each lane one 16-B piece by a register
+//     load (row lane >> 2, piece lane & 3), stored to LDS as it lies (a sub-image = 1 KB contiguous, the
+//     transposing read's layout of dwgrad3_kernel: lane (h, g16, qq, pp) reads rows 8 h + qq (+ 4) at column
+//     32 g16 + 8 pp, conflict-free);
+//   * wave w: outputs 128 (w & 1) .. + 127 of the workgroup's 256 (4 tiles) x pixel w >> 1 (2 tiles): 8 tiles,
+//     hi / lo accumulator pairs (hA hB | hA lB + lA hB, as the split wgrad form), 24 MFMAs per k-step;
+//   * two-deep register pipeline (step s + 2's loads fly while step s + 1 goes to the other LDS slot under step
+//     s's MFMAs), one barrier per k-step; rows past the split read a zero df piece;
+//   * partial slabs [split][512][3136] (NHWC features) summed in split order by fc_wgrad_reduce_perm.
+constexpr int FWG_KS = 16, FWG_GROUPS = 25, FWG_SPLITS = 5;    // k-step rows; 2-pixel groups (the 25th: pixel 48)
+constexpr int FWG_NA = 16, FWG_NB = 8, FWG_SUB = FWG_KS * 64;  // df / h3 sub-images per k-step; bytes each
+constexpr int FWG_STAGE = (FWG_NA + FWG_NB) * FWG_SUB, FWG_NSLOT = 3;  // 24 KB per slot
+constexpr int FWG_P = (FWG_NA + FWG_NB) / 4;                   // pieces per thread per k-step: 6 (4 df, 2 h3)
+constexpr long long FWG_DFROW = 1024 * 2, FWG_H3ROW = 49 * 256;  // PX row bytes
+
+struct FwgArgs {
+    const uint8_t* df;  // PX df [batch][16 groups: 32 hi | 32 lo f16]
+    const uint8_t* h3;  // PX h3 [batch][49 pixels: (hi | lo) x 2 channel halves]
+    const int *df_exp, *h3_exp;
+    float* slab;  // [splits][512][3136]
+    long long batch, rows_per_split;
+};
+__device__ __attribute__((aligned(16))) uint8_t kFwgZero[64] = {};  // the df piece of a row past the split
+
+// the accumulators live in AGPRs (16 f32x16 = all 256 of them; hipcc, left to place them, shuttled them between
+// the register files and spilled): the MFMAs are inline asm, the fragments VGPRs.  PAD: 2 wait states before the
+// MFMA (a fragment assembled by a VALU move must not be read as an MFMA source sooner; hipcc pads nothing in asm
+// and may place the move anywhere before its use — every MFMA here is padded: an s_nop issues inside the previous
+// MFMA's 32 cycles)
+__device__ inline void fwg_zero(f32x16& c, const u32x4& z) {  // c = 0 x 0 + 0, defined in AGPRs
+    // padded too: hipcc writes z (v_mov) right before the first of these (read unpadded, stale lanes made NaN)
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %1, 0" : "=a"(c) : "v"(z));
+}
+template <bool PAD>
+__device__ inline void fwg_mfma(f32x16& c, const u32x4& x, const u32x4& y) {
+    static_assert(PAD, "fwg_mfma: every MFMA padded");
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(c) : "v"(x), "v"(y));
+}
+
+// wait for every outstanding LDS read of this wave; F's 24 registers named, so no use moves above the wait
+template <class Frag>
+__device__ inline void fwg_wait(Frag& F) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(F.b[0]), "+v"(F.b[1]), "+v"(F.b[2]), "+v"(F.b[3]), "+v"(F.b[4]), "+v"(F.b[5]), "+v"(F.b[6]),
+                   "+v"(F.b[7]));
+    asm volatile("" : "+v"(F.a0[0]), "+v"(F.a0[1]), "+v"(F.a0[2]), "+v"(F.a0[3]), "+v"(F.a0[4]), "+v"(F.a0[5]),
+                      "+v"(F.a0[6]), "+v"(F.a0[7]));
+    asm volatile("" : "+v"(F.a1[0]), "+v"(F.a1[1]), "+v"(F.a1[2]), "+v"(F.a1[3]), "+v"(F.a1[4]), "+v"(F.a1[5]),
+                      "+v"(F.a1[6]), "+v"(F.a1[7]));
+}
+
+template <class Fn, int... I>
+__device__ inline void fwg_unroll(Fn&& fn, std::integer_sequence<int, I...>) {
+    (fn(std::integral_constant<int, I>{}), ...);
+}
+// the transposing fragment read at a compile-time offset (one base address per operand; asm so the offsets fold
+// into the instruction: the compiler's own form kept a 64-bit generic address per sub-image)
+template <int OFF>
+__device__ inline uint2 fwg_tr(uint32_t addr) {
+    uint2 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF) : "memory");
+    return r;
+}
+// wait until at most N of this wave's LDS reads are outstanding; x: the registers those reads fill
+template <int N, int K>
+__device__ inline void fwg_lgkm(uint2 (&x)[K]) {
+    static_assert(K == 8, "fwg_lgkm: 8 reads");
+    asm volatile("s_waitcnt lgkmcnt(%8)"
+                 : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7])
+                 : "n"(N));
+}
+
+__global__ void __launch_bounds__(256, 1) fcwg_kernel(FwgArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[FWG_NSLOT * FWG_STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // item = (split, feature group, output half), the output half fastest: the workgroups of one XCD share their
+    // split's df rows (and each h3 pixel pair with its other half) through its L2
+    const long long w = xcd_remap(blockIdx.x, gridDim.x);
+    const int oh = (int)(w & 1), fg = (int)((w >> 1) % FWG_GROUPS), split = (int)(w / (2 * FWG_GROUPS));
+    const long long r0 = (long long)split * a.rows_per_split;
+    const long long r1 = min(a.batch, r0 + a.rows_per_split);
+    const int nsteps = r1 > r0 ? (int)((r1 - r0 + FWG_KS - 1) / FWG_KS) : 0;
+    // this thread's pieces: sub-image wave + 4 i (i < 4: df output group 8 oh + ((wave + 4 i) >> 1), plane
+    // (wave + 4 i) & 1; i >= 4: h3 pixel, half, plane), row lane >> 2, 16-B piece lane & 3.  Buffer loads: 32-bit
+    // offsets, and a row past the split reads past the buffer's end, which returns zeros
+    const int prow = lane >> 2, pc = lane & 3;
+    uint32_t aoff[4], boff[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int sub = wave + 4 * i;
+        aoff[i] = (uint32_t)((8 * oh + (sub >> 1)) * 128 + (sub & 1) * 64 + pc * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int sub = wave + 4 * i;  // (pixel, half, plane) = (sub >> 2, (sub >> 1) & 1, sub & 1)
+        const int px = min(2 * fg + (sub >> 2), 48);
+        boff[i] = (uint32_t)(px * 256 + ((sub >> 1) & 1) * 128 + (sub & 1) * 64 + pc * 16);
+    }
+    const auto a_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.df + r0 * FWG_DFROW), 0,
+                                                        (int)((r1 - r0) * FWG_DFROW), 0x00020000);
+    const auto b_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.h3 + r0 * FWG_H3ROW), 0,
+                                                        (int)((r1 - r0) * FWG_H3ROW), 0x00020000);
+    struct Raw {
+        u32x4 v[FWG_P];
+    };
+    auto load = [&](Raw& raw, int step) {
+        const uint32_t r = (uint32_t)(step * FWG_KS + prow);  // split-relative; past the end: zeros
+        const uint32_t ra = r * (uint32_t)FWG_DFROW, rb = r * (uint32_t)FWG_H3ROW;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) raw.v[i] = __builtin_amdgcn_raw_buffer_load_b128(a_rs, (int)(ra + aoff[i]), 0, 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) raw.v[4 + i] = __builtin_amdgcn_raw_buffer_load_b128(b_rs, (int)(rb + boff[i]), 0, 0);
+    };
+    auto store = [&](const Raw& raw, int slot) {
+        uint8_t* st = lds + slot * FWG_STAGE;
+#pragma unroll
+        for (int i = 0; i < FWG_P; ++i) *reinterpret_cast<u32x4*>(st + (tid + 256 * i) * 16) = raw.v[i];
+    };
+    // fragment reads (the transposing pattern of dwgrad3_kernel on 64-B rows): wave w reads df output groups
+    // 4 (w & 1) .. + 3 of the workgroup's 8 and h3 pixel w >> 1
+    const int h = lane >> 5, g16 = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+    const int wo = wave & 1, wp = wave >> 1;
+    const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint8_t*)lds);
+    const uint32_t lrow = (uint32_t)((8 * h + qq) * 64 + g16 * 32 + pp * 8);
+    const uint32_t abase = lds0 + lrow + (uint32_t)(wo * 8 * FWG_SUB);
+    const uint32_t bbase = lds0 + lrow + (uint32_t)((FWG_NA + wp * 4) * FWG_SUB);
+    f32x16 hi[4][2], lo[4][2];
+    {
+        const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                fwg_zero(hi[i][j], z);
+                fwg_zero(lo[i][j], z);
+            }
+    }
+    auto cat = [](uint2 x0, uint2 x1) { return u32x4{x0.x, x0.y, x1.x, x1.y}; };
+    // one k-step's fragments: h3 (j, plane, row half) and df tiles 0-1, 2-3 (tile, plane, row half)
+    struct Frag {
+        uint2 b[8], a0[8], a1[8];
+    };
+    // issue the 24 transposing reads of the k-step in LDS slot `slot` (they complete under the MFMAs of the
+    // previous k-step: waited for by fwg_wait at the top of the next)
+    auto issue = [&](Frag& F, int slot) {
+        const uint32_t so = (uint32_t)(slot * FWG_STAGE), ab = abase + so, bb = bbase + so;
+        fwg_unroll([&](auto X) {  // B: (j, P, half) = (x >> 2, (x >> 1) & 1, x & 1)
+            constexpr int x = decltype(X)::value;
+            F.b[x] = fwg_tr<((x >> 2) * 2 + ((x >> 1) & 1)) * FWG_SUB + (x & 1) * 256>(bb);
+        }, std::make_integer_sequence<int, 8>{});
+        fwg_unroll([&](auto X) {  // A tiles 0-1: (i, P, half)
+            constexpr int x = decltype(X)::value;
+            F.a0[x] = fwg_tr<((x >> 2) * 2 + ((x >> 1) & 1)) * FWG_SUB + (x & 1) * 256>(ab);
+        }, std::make_integer_sequence<int, 8>{});
+        fwg_unroll([&](auto X) {  // A tiles 2-3
+            constexpr int x = decltype(X)::value;
+            F.a1[x] = fwg_tr<((2 + (x >> 2)) * 2 + ((x >> 1) & 1)) * FWG_SUB + (x & 1) * 256>(ab);
+        }, std::make_integer_sequence<int, 8>{});
+    };
+    auto mma = [&](const Frag& F) {
+        const u32x4 bq[2][2] = {{cat(F.b[0], F.b[1]), cat(F.b[2], F.b[3])}, {cat(F.b[4], F.b[5]), cat(F.b[6], F.b[7])}};
+        auto tile = [&](int i, const uint2 (&ra)[8], int t) {
+            const u32x4 a0 = cat(ra[4 * t], ra[4 * t + 1]), a1 = cat(ra[4 * t + 2], ra[4 * t + 3]);
+            // hA hB into hi, hA lB + lA hB into lo (mfma_split3)
+            fwg_mfma<true>(hi[i][0], a0, bq[0][0]);
+            fwg_mfma<true>(lo[i][0], a0, bq[0][1]);
+            fwg_mfma<true>(lo[i][0], a1, bq[0][0]);
+            fwg_mfma<true>(hi[i][1], a0, bq[1][0]);
+            fwg_mfma<true>(lo[i][1], a0, bq[1][1]);
+            fwg_mfma<true>(lo[i][1], a1, bq[1][0]);
+        };
+        tile(0, F.a0, 0);
+        tile(1, F.a0, 1);
+        tile(2, F.a1, 0);
+        tile(3, F.a1, 1);
+    };
+    // three LDS slots, two register stages: at the top of k-step s, step s's fragments are in flight (issued in
+    // step s - 1), step s + 1 sits in slot (s + 1) % 3, raw[s & 1] holds step s + 2.  Step s: wait for its
+    // fragments, issue step s + 1's, its 24 MFMAs, store step s + 2 into slot (s + 2) % 3 (= (s - 1) % 3, whose
+    // reads every wave waited for in step s - 1, before the barrier that ended it), load step s + 4, barrier
+    Raw raw[2];
+    load(raw[0], 0);
+    load(raw[1], 1);
+    store(raw[0], 0);  // (past the split: zeros, which an odd count's extra step reads)
+    store(raw[1], 1);
+    load(raw[0], 2);
+    load(raw[1], 3);
+    __syncthreads();
+    Frag F[2];
+    issue(F[0], 0);
+    int sr = 1, sw = 2;  // slots read (step s + 1) and written (step s + 2)
+    auto step = [&](int s, auto cur_tag) {
+        constexpr int C = decltype(cur_tag)::value;
+        fwg_wait(F[C]);
+        issue(F[C ^ 1], sr);
+        mma(F[C]);
+        store(raw[C], sw);
+        load(raw[C], s + 4);
+        sr = sr == 2 ? 0 : sr + 1;
+        sw = sw == 2 ? 0 : sw + 1;
+        __syncthreads();
+    };
+    // whole pairs of k-steps (a branch inside the pair merged the two register stages' load counts, and hipcc then
+    // waited for every load in flight at each store): an odd count's extra step reads rows past the split, zeros
+    for (int s = 0; s < nsteps; s += 2) {
+        step(s, std::integral_constant<int, 0>{});
+        step(s + 1, std::integral_constant<int, 1>{});
+    }
+    // the last issued reads (past the end) land before the workgroup exits; >= 18 wait states between the last
+    // MFMA writing an accumulator and its read; the statements name every accumulator, so no read is scheduled
+    // above the nops
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 4"
+                 : "+a"(hi[0][0]), "+a"(hi[0][1]), "+a"(hi[1][0]), "+a"(hi[1][1]), "+a"(hi[2][0]), "+a"(hi[2][1]),
+                   "+a"(hi[3][0]), "+a"(hi[3][1])
+                 :
+                 : "memory");
+    asm volatile(""
+                 : "+a"(lo[0][0]), "+a"(lo[0][1]), "+a"(lo[1][0]), "+a"(lo[1][1]), "+a"(lo[2][0]), "+a"(lo[2][1]),
+                   "+a"(lo[3][0]), "+a"(lo[3][1])
+                 :
+                 : "memory");
+    const int px = 2 * fg + wp;
+    if (px > 48) return;  // the 25th group's second pixel (wave-uniform)
+    const float uo = exp2i(-*a.df_exp) * exp2i(-*a.h3_exp);
+    float* slab = a.slab + ((long long)split * 512 + oh * 256 + wo * 128) * 3136 + px * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int o = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                slab[(long long)o * 3136 + j * 32 + (lane & 31)] = (hi[i][j][r] + lo[i][j][r]) * uo;
+            }
+}
+
+// the direct form's split count: 5 (250 workgroups), fewer for batches below ~5 k-steps per split
+inline int fcwg_splits(long long batch) {
+    return (int)std::max<long long>(1, std::min<long long>(FWG_SPLITS, ppox::ceil_div(batch, 4LL * FWG_KS)));
+}
+
 extern "C" int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch) {
-    return batch <= 0 ? 0 : FcWgrad::workspace_bytes(batch);
+    if (batch <= 0) return 0;
+    return std::max<int64_t>(FcWgrad::workspace_bytes(batch), (int64_t)fcwg_splits(batch) * FcWgrad::SLAB * 4);
 }
 
 extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float* h3, void* workspace,
@@ -3892,8 +4165,20 @@ extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float*
     PPOX_REQUIRE(workspace_bytes >= FcWgrad::workspace_bytes(batch), "ppox_nature_fc_wgrad: workspace too small");
     PPOX_REQUIRE(ppox::aligned16(df) && ppox::aligned16(h3), "ppox_nature_fc_wgrad: 16B alignment");
     PPOX_REQUIRE(batch < (1LL << 31) / 64, "ppox_nature_fc_wgrad: batch too large for 32-bit row indexing");
-    const int sp = FcWgrad::splits(batch);
     float* slab = reinterpret_cast<float*>(workspace);
+    // PX df and PX h3 (the product's training pass): the direct form (round 6; PPOX_FCWG=0 under PPOX_AB=1: the
+    // split wgrad form)
+    const char* fe = ppox::ab_env("PPOX_FCWG");
+    if (h3_exp && df_exp && !(fe && fe[0] == '0')) {
+        const int sp = fcwg_splits(batch);
+        FwgArgs fa{reinterpret_cast<const uint8_t*>(df), reinterpret_cast<const uint8_t*>(h3), df_exp, h3_exp, slab,
+                   batch, (long long)ppox::ceil_div((long long)batch, (long long)sp)};
+        fcwg_kernel<<<(unsigned)(2 * FWG_GROUPS * sp), 256, 0, s>>>(fa);
+        PPOX_LAUNCHED_NORET("ppox_nature_fc_wgrad");
+        fc_wgrad_reduce_perm<<<512, 256, 0, s>>>(slab, sp, dw);
+        PPOX_LAUNCHED("ppox_nature_fc_wgrad");
+    }
+    const int sp = FcWgrad::splits(batch);
     WArgs wa{df, 0, h3, slab, nullptr, batch, 0, sp, nullptr, 0, 0, amax_df, amax_h3};
     wa.gexp = h3_exp;  // PX h3 (the G operand of this GEMM)
     wa.xexp = df_exp;  // PX df (the X operand)
@@ -4033,6 +4318,25 @@ extern "C" int ppox_nature_pack_all(const float* w1, const float* b1, const floa
     p.b2 = b2;
     p.b3 = b3;
     return launch_pack_all(p, ppox::as_stream(stream), "ppox_nature_pack_all");
+}
+
+extern "C" int ppox_nature_pack_all_wmax(const float* w1, const float* b1, const float* w2, const float* b2,
+                                         const float* w3, const float* b3, const float* wfc, float* wpd2,
+                                         uint16_t* q1, uint16_t* q2, uint16_t* q3, uint16_t* qd2, uint16_t* qd3,
+                                         uint16_t* qfc_fwd, uint16_t* qfc_dgrad, const float* wh, uint16_t* qh_fwd,
+                                         uint16_t* qh_dgrad, const uint32_t* amax_in, uint32_t* amax_next,
+                                         uint32_t* zero, int64_t zero_words, void* stream) {
+    static_assert(PPOX_WMAX_TENSORS == PA_TENSORS && PPOX_WMAX_SLOTS == AMAX_SLOTS, "ppox.h: the amax partials");
+    PPOX_REQUIRE(w1 && w2 && w3 && (wfc || (!qfc_fwd && !qfc_dgrad)), "ppox_nature_pack_all_wmax: null weights");
+    PPOX_REQUIRE(!q1 || b1, "ppox_nature_pack_all_wmax: q1 needs the conv1 bias b1 (the H1P exponent)");
+    PPOX_REQUIRE(zero_words >= 0 && (zero_words == 0 || zero), "ppox_nature_pack_all_wmax: zero buffer");
+    PackAll p{w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh, qh_fwd, qh_dgrad, b1, zero,
+              zero_words};
+    p.b2 = b2;
+    p.b3 = b3;
+    p.amax_in = amax_in;
+    p.amax_next = amax_next;
+    return launch_pack_all(p, ppox::as_stream(stream), "ppox_nature_pack_all_wmax");
 }
 
 // ---- the heads' hidden layer Linear(512, 512) + ReLU on the split-f16 GEMM -------------

@@ -44,16 +44,12 @@ __device__ inline uint32_t fwd1_idx_load(const long long* p) {
     return v;
 }
 __device__ uint32_t kFwd1Dummy[128];  // store target of the rows past the batch (never read)
-#ifndef FWD1_FAST_EPI
-#define FWD1_FAST_EPI 1  // the H1P epilogue's whole-tile form (round 4); 0: the per-row form for every tile
-#endif
+constexpr int FWD1_FAST_EPI = 1;  // the H1P epilogue's whole-tile form (round 4); 0: the per-row form for every tile
 // the H1P epilogue's stores non-temporal (streaming: h1 is read back from HBM by the conv2 forward
 // and weight gradient, not from L2): 1-GPU line +1.0-1.2 % A/B (conv2 forward 281 -> 270 us at 16,384
 // rows, the conv1 forward itself unchanged), profiles/r05y.  The direct kernels' stores made
 // non-temporal the same way ran 4x slower (their counted vmcnt waits include the stores).
-#ifndef FWD1_NT
-#define FWD1_NT 1
-#endif
+constexpr int FWD1_NT = 1;
 __device__ inline void fwd1_store(uint32_t* p, uint32_t v) {
     if constexpr (FWD1_NT)
         __builtin_nontemporal_store(v, p);
@@ -269,14 +265,10 @@ __global__ void __launch_bounds__(256, MT == 1 ? 3 : 2) fwd1_split_kernel(Args a
     amax_record(a.amax_y, om);  // (H1P: the bound of conv2's PX output starts from it)
 }
 
-#ifndef SPLIT_FWD1_MT
-#define SPLIT_FWD1_MT 1
-#endif
+constexpr int SPLIT_FWD1_MT = 1;
 // waves the persistent kernel spreads its tiles over: 256 CUs x resident waves per CU
 // (VGPRs: 3 workgroups at MT = 1, 140 VGPRs; 2 at MT = 2; 32 KB of LDS each)
-#ifndef SPLIT_RESIDENT_WAVES
-#define SPLIT_RESIDENT_WAVES (SPLIT_FWD1_MT == 1 ? 3072 : 2048)
-#endif
+constexpr int SPLIT_RESIDENT_WAVES = SPLIT_FWD1_MT == 1 ? 3072 : 2048;
 // below 8,192 rows: 2,048 waves (more tiles per wave over which its weight staging and pipeline fill
 // are spread; per-rank shape 199.6 vs 201.3-201.7 ms, same box; the 16,384-row line unchanged)
 inline long long fwd1_waves(long long batch, long long ntile) {

@@ -34,27 +34,11 @@
 
 namespace {
 
-// PPOX_NT_OUT=1 (A/B): the direct kernels' activation / gradient outputs stored non-temporal (streaming:
-// written once, read by the next kernel from HBM)
-#ifndef PPOX_NT_OUT
-#define PPOX_NT_OUT 0
-#endif
-constexpr int NT_AUX = PPOX_NT_OUT ? 2 : 0;  // the buffer stores' cache-policy bits (nt)
-typedef unsigned int nt_u2 __attribute__((ext_vector_type(2)));
-__device__ inline void out_store2(void* p, uint32_t x, uint32_t y) {
-    if constexpr (PPOX_NT_OUT)
-        __builtin_nontemporal_store((nt_u2){x, y}, reinterpret_cast<nt_u2*>(p));
-    else
-        *reinterpret_cast<uint2*>(p) = make_uint2(x, y);
-}
+// the direct kernels' activation / gradient outputs: plain stores (non-temporal ones ran the kernels 4x slower:
+// their counted vmcnt waits include the stores, which then wait for HBM — DESIGN §4.1)
+__device__ inline void out_store2(void* p, uint32_t x, uint32_t y) { *reinterpret_cast<uint2*>(p) = make_uint2(x, y); }
 
-
-#ifndef DCONV_GLOBAL_DMA
-#define DCONV_GLOBAL_DMA 0
-#endif
-#ifndef DC_PD
-#define DC_PD 2  // k-steps of A-fragment reads in flight ahead of the MFMAs
-#endif
+constexpr int DC_PD = 2;  // k-steps of A-fragment reads in flight ahead of the MFMAs
 
 // conv3: h2 planes (81 pixels x 64 channels: per pixel hi[0:32] lo[0:32] hi[32:64] lo[32:64])
 struct DcF3 {
@@ -201,8 +185,8 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
         dpk[i] = u | ((L::S == 1 ? L::OW * y + x : 9 * (y >> 1) + (x >> 1)) << 16);
     }
     // DMA i of sample n (range-relative): a buffer LDS-DMA — the range's descriptor (uniform), the sample in
-    // soffset, the lane's 32-bit offset in voffset (no 64-bit address arithmetic per DMA; DCONV_GLOBAL_DMA=1:
-    // the round-4 global_load_lds form)
+    // soffset, the lane's 32-bit offset in voffset (no 64-bit address arithmetic per DMA; round 4 used
+    // global_load_lds)
     auto issue_one = [&](int n, int i) {
         int d = wave + 4 * i;
         d = d < Gm::REAL_DMAS ? d : Gm::REAL_DMAS - 1;
@@ -214,12 +198,7 @@ __global__ void __launch_bounds__(256, 1) dconv_fwd_kernel(Args a, const u32x4* 
             off = (uint32_t)((u ^ (key & 1)) * 128 + (((lane & 7) ^ (key >> 1)) << 4));
         }
         uint8_t* dst = lds + (n % F::NSLOT) * Gm::SLOT + d * 1024;
-#if DCONV_GLOBAL_DMA
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(xb + (long long)n * Gm::IMG + off),
-                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-#else
         dc_buffer_dma(xb, NS * Gm::IMG, dst, off, n * Gm::IMG);
-#endif
     };
     auto issue_sample = [&](int n) {
 #pragma unroll
@@ -799,7 +778,7 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
         }
         __builtin_amdgcn_raw_buffer_store_b128(
             u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])}, o_rs,
-            (uint32_t)o + (uint32_t)(32 * t + 16 * h), 0, NT_AUX);
+            (uint32_t)o + (uint32_t)(32 * t + 16 * h), 0, 0);
         om = fmaxf(om, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
     };
     // refill DMAs (at most one sample per phase: 64 rows < 100) over k-steps 9 .. 14
@@ -1464,8 +1443,8 @@ __global__ void __launch_bounds__(256, 1) ddgrad3_kernel(Args a, const u32x4* __
         split2h((f32x2){y[0], y[1]}, 1.f, hw[0], lw[0]);
         split2h((f32x2){y[2], y[3]}, 1.f, hw[1], lw[1]);
         const uint32_t o = (uint32_t)po + ylane + 16 * t;
-        __builtin_amdgcn_raw_buffer_store_b64((w3u2){hw[0], hw[1]}, o_rs, o, 0, NT_AUX);
-        __builtin_amdgcn_raw_buffer_store_b64((w3u2){lw[0], lw[1]}, o_rs, o + 64, 0, NT_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64((w3u2){hw[0], hw[1]}, o_rs, o, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64((w3u2){lw[0], lw[1]}, o_rs, o + 64, 0, 0);
         om = max(om, max(max(__float_as_uint(y[0]) & 0x7FFFFFFFu, __float_as_uint(y[1]) & 0x7FFFFFFFu),
                          max(__float_as_uint(y[2]) & 0x7FFFFFFFu, __float_as_uint(y[3]) & 0x7FFFFFFFu)));
     };
@@ -1836,11 +1815,11 @@ int dconv_cus() {
 }
 
 bool env_on(const char* name, long long batch, bool dflt, long long dflt_min = 1) {
-    const char* e = std::getenv(name);
+    const char* e = ppox::ab_env(name);
     if (!(e ? e[0] != '0' : dflt)) return false;
     char mn[64];
     snprintf(mn, sizeof mn, "%s_MIN", name);
-    const char* m = std::getenv(mn);
+    const char* m = ppox::ab_env(mn);
     return batch >= (m ? std::atoll(m) : dflt_min);
 }
 

@@ -144,9 +144,7 @@ template <bool DUAL>
 constexpr int staged_eb() { return DUAL ? 8 : 16; }  // envs per block (LDS <= 64 KB at T = 128)
 constexpr int STAGED_TMAX = 256;
 constexpr int CH = 16;  // chain steps per register chunk
-#ifndef STAGED_NMAX
-#define STAGED_NMAX 8192  // measured crossover (tools/gae_sweep.py): above it the lane-per-env form wins
-#endif
+constexpr int STAGED_NMAX = 8192;  // measured crossover (tools/gae_sweep.py): above it the lane-per-env form wins
 
 template <bool DUAL>
 __global__ void __launch_bounds__(256) gae_staged_kernel(

@@ -38,6 +38,11 @@ struct HeadGrads {
     int H, A;
     int relu_df;        // df = f > 0 ? df : 0 first, written back (the fc layer's ReLU backward)
     uint32_t* amax_df;  // nullable: the masked df's amax slots
+    // nullable (round 6): df's PX planes written in the same pass (ppox_px_split's split, bitwise) at the exponent
+    // of its amax slots px_amax (recorded by the heads' backward), the exponent stored to *px_exp
+    uint16_t* px;
+    const uint32_t* px_amax;
+    int* px_exp;
 };
 constexpr int HG_MAXA = 18, HG_MAXH = 512;  // actions (Montezuma 18), hidden width
 
@@ -64,6 +69,12 @@ __global__ void __launch_bounds__(256) head_grads_partials(HeadGrads g, float* _
     const int jc = col ? j : 0;
     auto ld = [&](const float* p, long long b) { return *reinterpret_cast<const float2*>(p + b * H + jc); };
     float dm = 0.f;  // the masked df's largest |value| in this thread's columns
+    float psc = 0.f;
+    if (g.px) {  // (uniform)
+        const int pe = split_scale_exp(amax_read(g.px_amax));
+        psc = exp2i(pe);
+        if (blockIdx.x == 0 && tid == 0) *g.px_exp = pe;
+    }
 #pragma unroll 4
     for (long long b = r0; b < r1; ++b) {
         const float dv = g.dv[b], div = INTR ? g.div[b] : 0.f;
@@ -82,6 +93,13 @@ __global__ void __launch_bounds__(256) head_grads_partials(HeadGrads g, float* _
             dfv.y = fv.y > 0.f ? dfv.y : 0.f;
             if (col) *reinterpret_cast<float2*>(g.df + b * H + j) = dfv;
             dm = fmaxf(dm, fmaxf(fabsf(dfv.x), fabsf(dfv.y)));
+        }
+        if (g.px && col) {  // the pair's two high halves, then 32 halves further its two low halves
+            uint32_t ph, pl;
+            split2h((f32x2){dfv.x, dfv.y}, psc, ph, pl);
+            uint16_t* q = g.px + px_index(b * H + j);
+            *reinterpret_cast<uint32_t*>(q) = ph;
+            *reinterpret_cast<uint32_t*>(q + 32) = pl;
         }
 #pragma unroll
         for (int a = 0; a < AM; ++a) {
@@ -330,6 +348,7 @@ extern "C" int ppox_head_grads(const float* f, const float* e, const float* dout
                                int64_t h, int64_t n_actions, void* workspace, float* w_actor, float* b_actor,
                                float* w_critic, float* b_critic, float* b_extra, float* b_fc, float* w_critic_int,
                                float* b_critic_int, float* b_int_extra, int32_t relu_df, uint32_t* amax_df,
+                               uint16_t* df_planes, const uint32_t* df_planes_amax, int32_t* df_planes_exp,
                                void* stream) {
     PPOX_REQUIRE(f && e && dout && dv && de && df && workspace && rows >= 0, "ppox_head_grads: null input");
     PPOX_REQUIRE(!amax_df || (relu_df && ppox::aligned16(amax_df)), "ppox_head_grads: amax_df needs relu_df (16B)");
@@ -341,12 +360,16 @@ extern "C" int ppox_head_grads(const float* f, const float* e, const float* dout
     const bool intr = ie != nullptr;
     PPOX_REQUIRE(!intr || (div && die && w_critic_int && b_critic_int && b_int_extra),
                  "ppox_head_grads: intrinsic head needs div, die and its three outputs");
+    PPOX_REQUIRE(!df_planes || (!relu_df && h % 32 == 0 && df_planes_amax && df_planes_exp &&
+                                ppox::aligned16(df_planes) && ppox::aligned16(df_planes_amax)),
+                 "ppox_head_grads: df planes need relu_df == 0 (df final), h % 32 == 0, the amax slots and the "
+                 "exponent output (16B aligned)");
     const long long R = std::max<long long>(8, (rows + 511) / 512), nchunk = std::max<long long>(1, (rows + R - 1) / R);
     const long long len = head_grads_len((int)h, (int)n_actions, intr);
     hipStream_t s = ppox::as_stream(stream);
     float* part = reinterpret_cast<float*>(workspace);
     HeadGrads g{f, e, ie, dout, dv, div, de, die, const_cast<float*>(df), rows, R, (int)h, (int)n_actions,
-                relu_df != 0, amax_df};
+                relu_df != 0, amax_df, df_planes, df_planes_amax, df_planes_exp};
     if (n_actions <= 4) {
         if (intr) head_grads_partials<4, true><<<(unsigned)nchunk, 256, 0, s>>>(g, part);
         else head_grads_partials<4, false><<<(unsigned)nchunk, 256, 0, s>>>(g, part);

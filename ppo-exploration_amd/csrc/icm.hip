@@ -41,9 +41,7 @@ namespace {
 constexpr int H = 32;           // ICM feature / hidden size
 constexpr float SLOPE = 0.01f;  // nn.LeakyReLU() negative slope
 constexpr int ROW_COLS = 1088;  // b1 (32) + W2 (32 x 32) + b2 (32): the row kernel's partial columns
-#ifndef ICM_PB
-#define ICM_PB 8
-#endif
+constexpr int ICM_PB = 8;
 constexpr int PB = ICM_PB;      // pairs per pair-kernel block (8: 256 blocks at B = 2048)
 constexpr int RB = 32;          // rows per row-kernel block
 
@@ -140,9 +138,7 @@ constexpr int ENC_CK = 64;  // k (frame bytes per row) of one forward chunk
 // ICM_W1_PARTS workgroups per row: each derives the row's amax from the whole row (the redundant reads hit
 // L2) and packs its own 1/ICM_W1_PARTS of the row's 8-k runs, so the launch has 32 x ICM_W1_PARTS workgroups
 // instead of one latency-bound workgroup per row (a second launch for a shared amax would cost more)
-#ifndef ICM_W1_PARTS
-#define ICM_W1_PARTS 8
-#endif
+constexpr int ICM_W1_PARTS = 8;
 __global__ void __launch_bounds__(1024) icm_pack_w1_kernel(const float* __restrict__ w, int K, u32x4* __restrict__ q) {
     __shared__ uint32_t red[16];
     const int n = blockIdx.x / ICM_W1_PARTS, part = blockIdx.x % ICM_W1_PARTS, tid = threadIdx.x;
@@ -736,9 +732,7 @@ __global__ void __launch_bounds__(256) icm_grad_reduce_kernel(const float* __res
 // ---------------------------------------------------------------------------
 constexpr int WG_CHUNK = 2048;  // rows whose frame-row numbers are staged in LDS at a time
 constexpr int WG_WAVES = 8;
-#ifndef ICM_WG_STAGES
-#define ICM_WG_STAGES 3
-#endif
+constexpr int ICM_WG_STAGES = 3;
 constexpr int WG_STAGES = ICM_WG_STAGES;
 
 struct WgArgs {
@@ -926,9 +920,7 @@ __global__ void __launch_bounds__(256) icm_int_reward_kernel(const float* __rest
 struct EncShape {
     int nrg, nkc;
 };
-#ifndef ICM_FWD_WGS
-#define ICM_FWD_WGS 256
-#endif
+constexpr int ICM_FWD_WGS = 256;
 EncShape enc_shape(long long M, int K) {
     EncShape s;
     s.nrg = (int)ppox::ceil_div(M, (long long)ENC_ROWS);

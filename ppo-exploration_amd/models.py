@@ -17,7 +17,6 @@ available (see convs.py); the small linear layers use PyTorch-ROCm (rocBLAS).
 """
 import contextlib
 import math
-import os
 
 import numpy as np
 import torch
@@ -69,7 +68,7 @@ class MlpNetwork(nn.Module):
 # gemm_split_probe.py: 104 -> 67 us at 16384 rows, no gain at 2048)
 WGRAD_SPLIT, WGRAD_SPLIT_MIN = 8, 8192
 # the heads' backward to the fc output in one launch (ppox_head_backward; PPOX_HBW=0: the two-launch form)
-HEAD_BWD_FUSED = os.environ.get("PPOX_HBW", "1") != "0"
+HEAD_BWD_FUSED = native.ab_env("PPOX_HBW", "1") != "0"
 
 
 def weight_grad(d, x, out, part=None):
@@ -306,17 +305,23 @@ class CnnActorCritic(nn.Module):
             # the split hidden layer it first applies the fc ReLU's backward to df (in place, df's amax recorded)
             ws = self._head_ws(B, f.shape[1], dout.shape[1])
             (de, d), intr = des[0], des[1] if self.intrinsic else (None, None)
+            dfp = None
+            if cv.px_df(B) and isinstance(am, _convs.PassState):  # df's planes for the fc dgrad and weight gradient
+                am.px[_convs.EX_DF] = True
+                dfp = torch.empty((B, 2 * f.shape[1]), dtype=torch.int16, device=df.device)
+            # with the split hidden layer df is final here (its amax recorded by the heads' backward): its planes are
+            # written by the same pass (round 6; the separate ppox_px_split otherwise, after the fc ReLU's backward)
+            fuse_px = dfp is not None and split
             native.head_grads(f, e, dout, d, de, df, ws, a.weight.grad, a.bias.grad, self.critic_ext.weight.grad,
                               self.critic_ext.bias.grad, self.extra_layer[0].bias.grad, fc.bias.grad,
                               ie=ie, div=intr[1], die=intr[0],
                               w_critic_int=self.critic_int.weight.grad if self.intrinsic else None,
                               b_critic_int=self.critic_int.bias.grad if self.intrinsic else None,
                               b_int_extra=self.int_extra_layer[0].bias.grad if self.intrinsic else None,
-                              relu_df=not split, amax_df=am[_convs.AM_DF] if (cv.nhwc3 and not split) else None)
-            dfp = None
-            if cv.px_df(B) and isinstance(am, _convs.PassState):  # df's planes for the fc dgrad and weight gradient
-                am.px[_convs.EX_DF] = True
-                dfp = torch.empty((B, 2 * f.shape[1]), dtype=torch.int16, device=df.device)
+                              relu_df=not split, amax_df=am[_convs.AM_DF] if (cv.nhwc3 and not split) else None,
+                              df_planes=dfp if fuse_px else None, df_planes_amax=am[_convs.AM_DF] if fuse_px else None,
+                              df_planes_exp=am.exp(_convs.EX_DF) if fuse_px else None)
+            if dfp is not None and not fuse_px:
                 native.px_split(df, am[_convs.AM_DF], dfp, am.exp(_convs.EX_DF))
             if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-f16 kernel, Flatten-order dW
                 h3_exp = am.exp(_convs.EX_H3)  # (PX h3: its planes)
@@ -473,6 +478,8 @@ class FlatParams:
         for b in module.buffers():
             b.data = b.data.to(self.device)
         self.step_count = 0
+        # the NatureCNN weight packing whose amax pass the Adam step records (convs.WmaxLink; round 6)
+        self.wmax = None
 
     def zero_grad(self):
         self.grad.zero_()
@@ -482,8 +489,15 @@ class FlatParams:
         self.step_count += 1
         if max_grad_norm is not None and max_grad_norm > 0:
             native.grad_sumsq(self.grad, self.norm_partials)
-        native.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, self.norm_partials,
-                         max_grad_norm if max_grad_norm else 0.0, lr, betas[0], betas[1], eps, self.step_count)
+        lk = self.wmax
+        if lk is not None and lk.ready(self):
+            native.adam_step_wmax(self.data, self.grad, self.exp_avg, self.exp_avg_sq, self.norm_partials,
+                                  max_grad_norm if max_grad_norm else 0.0, lr, betas[0], betas[1], eps,
+                                  self.step_count, lk.ranges, lk.recording())
+            lk.recorded(self)
+        else:
+            native.adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, self.norm_partials,
+                             max_grad_norm if max_grad_norm else 0.0, lr, betas[0], betas[1], eps, self.step_count)
 
     def state_dict(self):
         return {k: v.detach() for k, v in self.module.state_dict().items()}

@@ -12,6 +12,17 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # PPOX_LIB: an A/B build of the same sources (tools/build_variant.sh) for kernel tests/timing
 LIB_PATH = os.environ.get("PPOX_LIB") or os.path.join(_HERE, "libppox.so")
 
+# The A/B switches of the product path (kernel forms, batch gates, stream placement) are constants unless
+# PPOX_AB=1: only then are their PPOX_* environment variables read (tests, tools/; the library's own switches
+# follow the same rule, common.h ppox::ab_env).  User-facing settings (PPOX_CONV_MATH, PPOX_NATIVE_DP,
+# PPOX_ICM_NATIVE, PPOX_LIB) are read always.
+AB = os.environ.get("PPOX_AB") == "1"
+
+
+def ab_env(name, default):
+    """os.environ.get(name, default) under PPOX_AB=1, else default"""
+    return os.environ.get(name, default) if AB else default
+
 _vp, _i64, _i32, _f64, _f32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, ctypes.c_float
 _u64 = ctypes.c_uint64
 
@@ -51,6 +62,7 @@ SIGNATURES = {
     "ppox_gather_rows": [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp],
     "ppox_grad_sumsq": [_vp, _i64, _vp, _vp],
     "ppox_adam_step": [_vp, _vp, _vp, _vp, _i64, _vp, _f32, _f64, _f64, _f64, _f64, _i64, _vp, _vp],
+    "ppox_adam_step_wmax": [_vp, _vp, _vp, _vp, _i64, _vp, _f32, _f64, _f64, _f64, _f64, _i64, _vp, _vp, _vp, _vp],
     "ppox_atari_env_reset": [_vp, _i64, _i64, _u64, _vp, _vp, _vp],
     "ppox_atari_env_step": [_vp, _vp, _vp, _i64, _i64, _u64, _i64, _f32, _f32, _vp, _vp, _vp, _vp,
                             _vp, _vp, _vp],
@@ -70,10 +82,11 @@ SIGNATURES = {
     "ppox_u8_to_f32": [_vp, _i64, _vp, _vp],
     "ppox_skinny_linear": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "ppox_skinny_dgrad": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
-    "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 10 + [_i32, _vp, _vp],
+    "ppox_head_grads": [_vp] * 9 + [_i64, _i64, _i64] + [_vp] * 10 + [_i32, _vp, _vp, _vp, _vp, _vp],
     "ppox_head_dgrad_outer": [_vp] * 5 + [_i64, _i64, _i64] + [_vp] * 4,
     "ppox_nature_fc_pack": [_vp, _vp, _vp, _vp],
     "ppox_nature_pack_all": [_vp] * 19 + [_i64, _vp],
+    "ppox_nature_pack_all_wmax": [_vp] * 21 + [_i64, _vp],
     "ppox_nature_conv1_fwd_planes": [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv2_fwd_planes": [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ppox_nature_conv2_wgrad_planes": [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp],
@@ -434,6 +447,20 @@ def adam_step(params, grads, m, v, norm_partials, max_norm, lr, beta1, beta2, ep
          stream_ptr(stream))
 
 
+WMAX_TENSORS, WMAX_SLOTS = 5, 256  # include/ppox.h PPOX_WMAX_*
+
+
+def adam_step_wmax(params, grads, m, v, norm_partials, max_norm, lr, beta1, beta2, eps, step, ranges, amax_out,
+                   norm_out=None, stream=None):
+    """adam_step that also records the new weights' amax partials (ranges: a CPU int64 tensor of
+    WMAX_TENSORS offsets then counts into params; amax_out: int32 [WMAX_TENSORS * WMAX_SLOTS], zeroed)"""
+    assert ranges.device.type == "cpu" and ranges.dtype == torch.int64 and ranges.numel() == 2 * WMAX_TENSORS
+    assert amax_out.numel() == WMAX_TENSORS * WMAX_SLOTS
+    call("ppox_adam_step_wmax", _p(params), _p(grads), _p(m), _p(v), params.numel(), _p(norm_partials),
+         float(max_norm), float(lr), float(beta1), float(beta2), float(eps), int(step), _p(norm_out),
+         ctypes.c_void_p(ranges.data_ptr()), _p(amax_out), stream_ptr(stream))
+
+
 def atari_env_reset(obs, N, env_offset, seed, ep_ret=None, ep_len=None, stream=None):
     call("ppox_atari_env_reset", _p(obs), N, env_offset, seed, _p(ep_ret), _p(ep_len), stream_ptr(stream))
 
@@ -580,6 +607,19 @@ def nature_pack_all(w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dg
     call("ppox_nature_pack_all", _p(w1), _p(b1), _p(w2), _p(b2), _p(w3), _p(b3), _p(wfc), _p(wpd2), _p(q1), _p(q2),
          _p(q3), _p(qd2), _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), _p(wh), _p(qh_fwd), _p(qh_dgrad), _p(zero),
          0 if zero is None else zero.numel(), stream_ptr(stream))
+
+
+def nature_pack_all_wmax(w1, w2, w3, wfc, wpd2, q1, q2, q3, qd2, qd3, qfc_fwd, qfc_dgrad, wh=None, qh_fwd=None,
+                         qh_dgrad=None, b1=None, zero=None, b2=None, b3=None, amax_in=None, amax_next=None,
+                         stream=None):
+    """nature_pack_all with the weights' amax partials from adam_step_wmax (amax_in: one launch, no amax
+    pass; None: the amax pass) and amax_next (the partials buffer the next adam_step_wmax records into)
+    zeroed on the way"""
+    for t in (amax_in, amax_next):
+        assert t is None or t.numel() == WMAX_TENSORS * WMAX_SLOTS
+    call("ppox_nature_pack_all_wmax", _p(w1), _p(b1), _p(w2), _p(b2), _p(w3), _p(b3), _p(wfc), _p(wpd2), _p(q1),
+         _p(q2), _p(q3), _p(qd2), _p(qd3), _p(qfc_fwd), _p(qfc_dgrad), _p(wh), _p(qh_fwd), _p(qh_dgrad), _p(amax_in),
+         _p(amax_next), _p(zero), 0 if zero is None else zero.numel(), stream_ptr(stream))
 
 
 # conv1 -> conv2 on H1P (conv1's output as two f16 planes; include/ppox.h)
@@ -808,13 +848,15 @@ def head_grads_workspace_bytes(rows, h, n_actions, intrinsic):
 
 def head_grads(f, e, dout, dv, de, df, ws, w_actor, b_actor, w_critic, b_critic, b_extra, b_fc,
                ie=None, div=None, die=None, w_critic_int=None, b_critic_int=None, b_int_extra=None, relu_df=False,
-               amax_df=None, stream=None):
+               amax_df=None, df_planes=None, df_planes_amax=None, df_planes_exp=None, stream=None):
     """Column-reduction head gradients (see include/ppox.h ppox_head_grads); outputs overwritten.
-    relu_df: df is first masked by f's ReLU in place (amax_df: its slots to record)."""
+    relu_df: df is first masked by f's ReLU in place (amax_df: its slots to record).  df_planes: df's PX planes
+    (int16, rows x 2h) written in the same pass at the exponent of df_planes_amax, stored to df_planes_exp."""
     call("ppox_head_grads", _p(f), _p(e), _p(dout), _p(dv), _p(de), _p(df), _p(ie), _p(div), _p(die),
          f.shape[0], f.shape[1], dout.shape[1], _p(ws), _p(w_actor), _p(b_actor), _p(w_critic), _p(b_critic),
          _p(b_extra), _p(b_fc), _p(w_critic_int), _p(b_critic_int), _p(b_int_extra), int(bool(relu_df)),
-         _p(amax_df), stream_ptr(stream))
+         _p(amax_df), _p(df_planes), _p(df_planes_amax), ptr(df_planes_exp, torch.int32, name="df_planes_exp"),
+         stream_ptr(stream))
 
 
 def head_dgrad_outer(dout, w_actor, dv, w_critic, e, amax_de=None):

@@ -44,7 +44,7 @@ def _is_image(space):
     return len(space.shape) == 3
 
 
-_TRAIN_PRIO = os.environ.get("PPOX_TRAIN_PRIO", "0") == "1"
+_TRAIN_PRIO = native.ab_env("PPOX_TRAIN_PRIO", "0") == "1"
 _prio_streams = {}
 
 
@@ -526,7 +526,7 @@ class PPO(BaseAlgorithm):
         self._alloc_train_state()
         self.last_obs = None
         # the collect step loop as one captured graph (PPOX_COLLECT_GRAPH=0: eager launches)
-        self._collect_graph_enabled = os.environ.get("PPOX_COLLECT_GRAPH", "1") != "0"
+        self._collect_graph_enabled = native.ab_env("PPOX_COLLECT_GRAPH", "1") != "0"
         self._cgraph = None
         self._ctables = None
 
@@ -845,12 +845,12 @@ class PPO_ICM(BaseAlgorithm):
         # one GPU) runs them on the side stream beside the policy minibatch as in one process, on a
         # communicator of their own (DistContext.subgroup): two communicators' collectives then
         # run concurrently, which RCCL guarantees to progress only when both fit on the GPU at once.
-        self._icm_side_dist = os.environ.get("PPOX_ICM_SIDE_DIST", "0") == "1"
+        self._icm_side_dist = native.ab_env("PPOX_ICM_SIDE_DIST", "0") == "1"
         self._icm_dist = (self.dist.subgroup() if self.dist.enabled and self._icm_native is not None
                           and self._icm_side_dist else self.dist)
         # the collect loop (policy + env + K11 curiosity reward) as one captured graph, as PPO's
         # (PPOX_COLLECT_GRAPH=0: eager launches)
-        self._collect_graph_enabled = os.environ.get("PPOX_COLLECT_GRAPH", "1") != "0"
+        self._collect_graph_enabled = native.ab_env("PPOX_COLLECT_GRAPH", "1") != "0"
         self._cgraph = None
         self._ctables = None
         self._ir_sum = torch.zeros((), dtype=torch.float64, device=self.device)

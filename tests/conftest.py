@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# the tests switch kernel forms and gates through their PPOX_* variables (native.ab_env, common.h ppox::ab_env):
+# read only under PPOX_AB=1 (before the package is imported; inherited by the tests' rank processes)
+os.environ.setdefault("PPOX_AB", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "ppo-exploration_amd")
 for p in (ROOT, PKG):

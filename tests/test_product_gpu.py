@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 import torch
 
+import f64_pass
 from oracle import models as OM
 from oracle.algos import OraclePPO
 from replay_env import ReplayVecEnv, space_from_code
@@ -424,6 +425,37 @@ def _parity_report(name, stats):
             json.dump(stats, fh, indent=1)
 
 
+def _first_minibatch_flips(f, p, alg, idx, masks, grad, A):
+    """The first minibatch (initial weights) re-evaluated in float64 (tests/f64_pass.py) with float64's own ReLU
+    decisions — pinned to the fixture's float64 gradient — and with the device pass's: the ReLU decisions the pass
+    took differently from float64, per layer, and each sampled tensor's gradient error split into the part those
+    decisions make (|g64(pass masks) - g64|) and the arithmetic error given them (|prod - g64(pass masks)|), both
+    relative to the tensor's largest float64 entry."""
+    ro, T = alg.rollout, alg.nstep
+    i = idx.long()
+    t_, n_ = i % T, i // T
+    x = ro.obs_slots[t_, n_]
+    mb = {"advantages": ro.advantages[t_, n_].view(-1, 1), "returns": ro.returns[t_, n_],
+          "old_values": ro.values[t_, n_], "old_log_probs": ro.log_probs[t_, n_].view(-1, 1),
+          "actions": ro.actions[t_, n_].long().view(-1, 1)}
+    init = {k: torch.from_numpy(f[p + "init_" + k]) for k in alg.policy.net.state_dict()}
+    g64, pre64 = f64_pass.minibatch_grads(init, x, mb, A)
+    own, _ = f64_pass.minibatch_grads(init, x, mb, A, masks=masks)
+    out = {"flips": f64_pass.flips(masks, pre64), "tensors": {}}
+    off = 0
+    for key, v in alg.policy.net.state_dict().items():
+        g = grad[off:off + v.numel()].double()
+        off += v.numel()
+        a, b = g64[key].flatten(), own[key].flatten()
+        sc = float(a.abs().max())
+        w = torch.from_numpy(f[p + "w1idx_" + key]).to(a.device)
+        pin = float((a[w].cpu() - torch.from_numpy(f[p + "g64_" + key])).abs().max()) / sc \
+            if (p + "g64_" + key) in f.files else None
+        out["tensors"][key] = {"arith": float((g - b).abs().max()) / sc, "relu": float((b - a).abs().max()) / sc,
+                               "total": float((g - a).abs().max()) / sc, "pin_f64_vs_fixture": pin}
+    return out
+
+
 @pytest.mark.parametrize("math", ["split", "f32"])
 def test_cnn_train_16384_rows_matches_reference_run(golden, math, monkeypatch):
     """The benchmark's dispatch end to end: one NatureCNN PPO iteration of 128 envs x 128
@@ -499,14 +531,21 @@ def test_cnn_train_16384_rows_matches_reference_run(golden, math, monkeypatch):
             first.append(alg.flat.grad.detach().clone())
         return step(*a, **k)
     monkeypatch.setattr(alg.flat, "adam_step", adam_step)
-    fwd0 = []
-    fwd = alg._fwd_train
+    fwd0, idx0, masks0 = [], [], []
+    fwd, tobs = alg._fwd_train, alg._train_obs
+
+    def train_obs(ro_, idx):
+        if not idx0:
+            idx0.append(idx.detach().clone())
+        return tobs(ro_, idx)
 
     def fwd_train(obs):
         r = fwd(obs)
         if not fwd0:
             fwd0.append((r[0].detach().double().cpu().numpy(), r[1].detach().double().cpu().numpy()))
+            masks0.extend(m.clone() for m in f64_pass.pass_masks(r[3]))  # the pass's own ReLU decisions
         return r
+    monkeypatch.setattr(alg, "_train_obs", train_obs)
     monkeypatch.setattr(alg, "_fwd_train", fwd_train)
     alg.train()
     np.testing.assert_array_equal(np.random.get_state()[1], f[p + "np_state_after"])
@@ -535,6 +574,22 @@ def test_cnn_train_16384_rows_matches_reference_run(golden, math, monkeypatch):
             "max_prod_f64_rel": float(np.abs(got - r64).max() / sc), "max_ref_f64_rel": float(np.abs(r32 - r64).max() / sc),
             "mean_prod_f64_rel": float(np.abs(got - r64).mean() / sc), "mean_ref_f64_rel": float(np.abs(r32 - r64).mean() / sc),
             "mean_signed_prod_f64_rel": float((got - r64).mean() / sc), "mean_signed_ref_f64_rel": float((r32 - r64).mean() / sc)}
+    # the first minibatch against float64, split into ReLU decisions and arithmetic (tests/f64_pass.py), beside
+    # the reference's own split of its f32 run (tests/golden/train_cnn_big_flips.npz, tools/flip_analysis.py):
+    # the product's arithmetic given its ReLU decisions within 3x the reference's given its own (+ 2e-7 of the
+    # tensor's largest entry) for every tensor, and no more than 3x as many differing ReLU decisions.  (The exact-f32
+    # mode's fc weight gradient is the library f32 GEMM over K = 16,384 rows, in the library's accumulation order:
+    # 5.2e-6 measured, the reference's CPU GEMM 1.9e-7 — that mode's floor is 1e-5.)
+    fm = stats["first_minibatch_relu"] = _first_minibatch_flips(f, p, alg, idx0[0], masks0, first[0], A)
+    rf = golden("train_cnn_big_flips")
+    for key, t in fm["tensors"].items():
+        t["arith_ref"], t["relu_ref"] = float(rf["arith_" + key]), float(rf["relu_" + key])
+        assert t["pin_f64_vs_fixture"] is None or t["pin_f64_vs_fixture"] <= 1e-12, (key, t)
+        if not t["arith"] <= 3 * t["arith_ref"] + (2e-7 if math == "split" else 1e-5):
+            fails.append(("first-minibatch arithmetic " + key, t))
+    fm["flips_ref"] = dict(zip(f64_pass.LAYERS, rf["flips"].tolist()))
+    if sum(fm["flips"].values()) > 3 * int(rf["flips"].sum()) or fm["flips"]["hidden"] > 3 * int(rf["flips"][4]) + 2:
+        fails.append(("ReLU decisions vs float64", fm["flips"], fm["flips_ref"]))
     for k, (key, v) in enumerate(alg.policy.net.state_dict().items()):
         idx = f[p + "w1idx_" + key]
         assert np.array_equal(idx, _weight_sample_index(v.numel(), k))
@@ -557,13 +612,15 @@ def test_cnn_train_16384_rows_matches_reference_run(golden, math, monkeypatch):
                                  "frac_beyond_strict": frac, "frac_beyond_tenth_lr": frac_lr,
                                  "dabs_rel": abs(d_abs - float(f[p + "d64abs_" + key])) / float(f[p + "d64abs_" + key])}
         # the heads downstream of the hidden layer's ReLU (extra_layer.*, critic_ext.*) are held to k = 8 / 6
-        # (max / mean) instead of 3: one ReLU-mask flip of the 16,384 x 512 hidden pre-activations in the
-        # first minibatch (a value within f32 rounding of zero, flipped against float64) changes one row of
-        # the extra layer's gradient by one sample's share, 2 / B = 1.2e-4 of its largest entry — the first
-        # minibatch's extra_layer.0.weight gradient is 1.28e-4 off float64 in BOTH math modes (split and the
-        # exact-f32 kernels), the reference's own 1.7e-5 — and Adam carries it into these tensors' trajectory
-        # (measured round 4: 2.1-7.2x e_ref max, 3.4-4.1x mean, split and f32 alike)
-        head = key.startswith(("extra_layer", "critic_ext"))
+        # (max / mean) instead of 3 only when the first minibatch shows that the extra layer's gradient error is
+        # ReLU decisions, not arithmetic (asserted below from the float64 decomposition: its ReLU part >= 10x its
+        # arithmetic part).  Two f32 passes take a few pre-activations within a rounding of 0 to the other side
+        # (round 6: the reference's own run 1 of the 16,384 x 512 hidden ones, ours 1-2 and different ones); each
+        # moves that row of the extra layer's gradient by a whole term (9.6e-5 of its largest entry here in both
+        # math modes, the reference's own flip 2.0e-5), and Adam carries that into the heads' trajectories
+        # (measured: critic_ext.weight 7.2x / 6.1x e_ref max, extra_layer 3.6-4.1x mean, split / f32)
+        relu_driven = fm["tensors"]["extra_layer.0.weight"]["relu"] >= 10 * fm["tensors"]["extra_layer.0.weight"]["arith"]
+        head = key.startswith(("extra_layer", "critic_ext")) and relu_driven
         k_max, k_mean = (8.0, 6.0) if head else (3.0, 3.0)
         stats["weights"][key]["k_max"], stats["weights"][key]["k_mean"] = k_max, k_mean
         if not (e_p.max() <= k_max * e_r.max() + fl_max and e_p.mean() <= k_mean * e_r.mean() + fl_mean

@@ -296,3 +296,40 @@ def test_px_output_refuses_a_form_packed_without_bias():
                                  x_exp=x_exp, y_exp=y_exp)
     torch.cuda.synchronize()
     assert torch.isfinite(y).all()
+
+
+@pytest.mark.parametrize("B,A", [(1, 4), (300, 6), (2048, 4), (16384, 18)])
+def test_head_grads_writes_df_planes_bitwise(B, A):
+    """Round 6: the heads' column-reduction pass writes df's PX planes in the same pass (ppox_head_grads
+    df_planes) — bitwise ppox_px_split's planes and exponent, and the same head gradients as without them."""
+    import native
+    g = torch.Generator(device="cuda").manual_seed(B + A)
+    f = torch.relu(torch.randn(B, 512, device="cuda", generator=g))
+    e = torch.relu(torch.randn(B, 512, device="cuda", generator=g))
+    dout = torch.randn(B, A, device="cuda", generator=g)
+    dv = torch.randn(B, device="cuda", generator=g)
+    de = torch.randn(B, 512, device="cuda", generator=g) * (e > 0)
+    df = torch.randn(B, 512, device="cuda", generator=g) * (f > 0) * torch.rand(B, 512, device="cuda", generator=g) ** 3
+    am = native.amax_table(1, "cuda")
+    native.amax(df, am[0])
+    ws = torch.empty(native.head_grads_workspace_bytes(B, 512, A, False), dtype=torch.uint8, device="cuda")
+
+    def run(planes):
+        outs = [torch.full((A, 512), float("nan"), device="cuda"), torch.full((A,), float("nan"), device="cuda"),
+                torch.full((1, 512), float("nan"), device="cuda"), torch.full((1,), float("nan"), device="cuda"),
+                torch.full((512,), float("nan"), device="cuda"), torch.full((512,), float("nan"), device="cuda")]
+        p = torch.full((B, 1024), -1, dtype=torch.int16, device="cuda") if planes else None
+        ex = torch.zeros(1, dtype=torch.int32, device="cuda") if planes else None
+        native.head_grads(f, e, dout, dv.view(B, 1), de, df, ws, *outs, df_planes=p, df_planes_amax=am[0] if planes else None,
+                          df_planes_exp=ex)
+        torch.cuda.synchronize()
+        return outs, p, ex
+    o1, p1, e1 = run(True)
+    o0, _, _ = run(False)
+    for a, b in zip(o1, o0):
+        assert torch.equal(a, b)
+    p2 = torch.empty(B, 1024, dtype=torch.int16, device="cuda")
+    e2 = torch.zeros(1, dtype=torch.int32, device="cuda")
+    native.px_split(df, am[0], p2, e2)
+    torch.cuda.synchronize()
+    assert int(e1) == int(e2) and torch.equal(p1, p2)

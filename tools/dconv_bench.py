@@ -5,6 +5,7 @@ and of the conv3 weight gradient: direct (dwgrad3_kernel) against im2col (wgrad_
 HIP events on the launch stream.  Usage: python tools/dconv_bench.py [B ...]"""
 import json
 import os
+os.environ.setdefault("PPOX_AB", "1")  # this tool switches kernel forms / gates (native.ab_env)
 import sys
 
 import torch

@@ -5,7 +5,7 @@
 #   tools/gpu.sh TAG STEP [STEP ...]
 # Steps (output under gpurun_out/TAG/):
 #   tests            the whole GPU suite (PPOX_PARITY_OUT=parity/), tests.log
-#   tests:FILES[:K]  pytest on FILES (comma-separated, under tests/) [-k K, "+" for spaces]
+#   tests:FILES[:K]  pytest on FILES (comma-separated, under tests/) [-k K, "+" for spaces]; =VAR=val,... as below
 #   F R RD I ID C3 ES  bench lines: F = the 1-GPU line (20 steps, no cpu baseline), FC = the default line with
 #                    the cpu baseline, R = the 8-GPU per-rank shape (512 envs, minibatch 2,048), RD = R with the
 #                    data-parallel branches over a one-rank RCCL communicator, I / ID = PPO_ICM per-rank
@@ -23,8 +23,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-KRX="wgrad|gae|gemm|split_kernel|colp_kernel|planes|dconv|fcd_kernel|dgrad2|ddgrad3|fcw_kernel|hbw_kernel"
-SQRX="sgemm|wgrad|colp|fwd1|dconv|fcd_kernel|dgrad2|ddgrad3|fcw_kernel|hbw_kernel"
+KRX="wgrad|gae|gemm|split_kernel|colp_kernel|planes|dconv|fcd_kernel|dgrad2|ddgrad3|fcw_kernel|fcwg_kernel|hbw_kernel"
+SQRX="sgemm|wgrad|colp|fwd1|dconv|fcd_kernel|dgrad2|ddgrad3|fcw_kernel|fcwg_kernel|hbw_kernel"
 RANK="--envs 512 --batch-size 2048"
 
 bench() {  # bench NAME OUTFILE ARGS...   (the step's VAR=value settings from $ENVS)
@@ -61,7 +61,7 @@ for STEP in "$@"; do
   echo "[gpu.sh] $STEP $(date +%T)" >&2
   NAME=${STEP%%=*}
   ENVS=""
-  [ "$NAME" != "$STEP" ] && ENVS=$(echo ${STEP#*=} | tr ',' ' ')
+  [ "$NAME" != "$STEP" ] && ENVS="PPOX_AB=1 $(echo ${STEP#*=} | tr ',' ' ')"
   OUT=$NAME
   [ -n "$ENVS" ] && OUT=${NAME}_$(echo $ENVS | tr ' =' '__' | tr -cd 'A-Za-z0-9_')
   case $NAME in
@@ -71,12 +71,25 @@ for STEP in "$@"; do
           --timeout-method thread > $O/tests.log 2>&1 || exit $?
       tail -n 3 $O/tests.log ;;
     tests:*)
-      SPEC=${STEP#tests:}; FILES=${SPEC%%:*}; K=""
+      SPEC=${NAME#tests:}; FILES=${SPEC%%:*}; K=""
       [ "$FILES" != "$SPEC" ] && K=$(echo ${SPEC#*:} | tr "+" " ")
       ARGS=""; for f in $(echo $FILES | tr ',' ' '); do ARGS="$ARGS $R/tests/$f"; done
-      timeout -k 10 900 python3 -u -m pytest $ARGS -x -v --timeout 300 --timeout-method thread ${K:+-k "$K"} \
+      [ -n "$ENVS" ] && echo "[gpu.sh] env $ENVS" >> $O/tests_sel.log
+      env $ENVS timeout -k 10 900 python3 -u -m pytest $ARGS -x -v --timeout 300 --timeout-method thread ${K:+-k "$K"} \
           >> $O/tests_sel.log 2>&1 || { tail -n 30 $O/tests_sel.log; exit 1; }
       tail -n 3 $O/tests_sel.log ;;
+    xfail:*)
+      # xfail:VARIANT:FILE[:K] — FILE's tests against tools/variants/VARIANT/libppox.so, which must FAIL (pytest
+      # rc 1); a crash / time limit (any other rc) ends the script as a failure
+      SPEC=${STEP#xfail:}; V=${SPEC%%:*}; REST=${SPEC#*:}; FILE=${REST%%:*}; K=""
+      [ "$FILE" != "$REST" ] && K=$(echo ${REST#*:} | tr "+" " ")
+      PPOX_LIB=$R/tools/variants/$V/libppox.so timeout -k 10 600 python3 -u -m pytest $R/tests/$FILE -x -v --timeout 300 \
+          --timeout-method thread ${K:+-k "$K"} > $O/xfail_$V.log 2>&1
+      rc=$?
+      tail -n 5 $O/xfail_$V.log
+      [ $rc -eq 1 ] || { echo "xfail $V: pytest rc $rc (expected 1)" >&2; exit 1; } ;;
+    fcwg) timeout -k 10 300 python3 -u $R/tools/fcwg_bench.py 2048 16384 > $O/fcwg_bench.jsonl 2>> $O/bench.err || exit 1
+      cat $O/fcwg_bench.jsonl ;;
     F)  bench F $OUT --steps 20 --warmup 2 --no-cpu-baseline || exit 1 ;;
     FC) bench FC $OUT || exit 1 ;;
     R)  bench R $OUT $RANK --steps 5 --warmup 2 --no-cpu-baseline || exit 1 ;;

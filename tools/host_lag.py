@@ -4,6 +4,7 @@ time at the same step, a blocking sync shows them equal.  Usage: python tools/ho
 [ppo|icm] [dist] ("dist": the data-parallel branches on over a one-rank RCCL communicator, as bench.py
 --force-dist)"""
 import os
+os.environ.setdefault("PPOX_AB", "1")  # this tool switches kernel forms / gates (native.ab_env)
 import sys
 import time
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of variant libraries on the bench (dev tool): tools/ab.sh TAG VARIANT [VARIANT...]
+# A/B of variant libraries on the bench (dev tool): tools/probes/ab.sh TAG VARIANT [VARIANT...]
 # Runs the kernel tests selected by TESTK (default: conv2_dgrad) on each variant, then base, each
 # variant, base again at the 1-GPU (F) and per-rank (R) shapes (PHASES, default "F R"; I: the
 # PPO_ICM per-rank shape).  Writes gpurun_out/ab_TAG/.

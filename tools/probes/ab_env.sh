@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of environment settings at the per-rank (R) and 1-GPU (F) shapes (dev tool):
-#   tools/ab_env.sh TAG SHAPES "VAR=value ..." ["VAR=value ..." ...]   (SHAPES: R, F or "R F")
+#   tools/probes/ab_env.sh TAG SHAPES "VAR=value ..." ["VAR=value ..." ...]   (SHAPES: R, F or "R F")
 # runs base, each setting, base again per shape.  Writes gpurun_out/abenv_TAG/.
 set -o pipefail
 TAG=$1; SHAPES=$2; shift 2

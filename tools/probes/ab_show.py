@@ -1,4 +1,4 @@
-"""Print an A/B directory's bench lines (dev tool): python tools/ab_show.py gpurun_out/ab_TAG"""
+"""Print an A/B directory's bench lines (dev tool): python tools/probes/ab.show.py gpurun_out/ab_TAG"""
 import glob
 import json
 import sys

@@ -1,13 +1,14 @@
 """Timing of the conv1 forward writing H1P (fwd1_split_kernel<1, true>, the training pass's form without the
-rollout index), HIP events on the launch stream.  Usage: python tools/conv1_bench.py [B ...] (PPOX_LIB: a
+rollout index), HIP events on the launch stream.  Usage: python tools/probes/conv1_bench.py [B ...] (PPOX_LIB: a
 variant build)"""
 import json
 import os
+os.environ.setdefault("PPOX_AB", "1")  # this tool switches kernel forms / gates (native.ab_env)
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "ppo-exploration_amd"))
 import native  # noqa: E402
 
 if os.environ.get("PPOX_LIB"):

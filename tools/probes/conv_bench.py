@@ -1,13 +1,13 @@
 """Per-kernel timing of the NatureCNN conv kernels (fwd / dgrad / wgrad) at the
 training minibatch size, HIP events on the launch stream, vs algorithmic FLOPs.
-Usage: python tools/conv_bench.py [B] [path/to/libppox variant .so]"""
+Usage: python tools/probes/conv_bench.py [B] [path/to/libppox variant .so]"""
 import json
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "ppo-exploration_amd"))
 import native  # noqa: E402
 
 PEAK = 157.3

@@ -2,11 +2,11 @@
 (dev tool)?  The same chain of N conv2-forward launches at 2,048 rows on one stream, timed with HIP
 events, (a) back to back, (b) with an event recorded on the main stream after each launch, (c) with
 that event also waited on by an idle side stream (convs.fork), (d) with a join after each launch
-(record on the idle side stream, wait on the main stream).  Usage: python tools/event_probe.py [N]"""
+(record on the idle side stream, wait on the main stream).  Usage: python tools/probes/event_probe.py [N]"""
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "ppo-exploration_amd"))
 import torch  # noqa: E402
 
 import convs  # noqa: E402

@@ -1,12 +1,12 @@
 """fc layer (3136 -> 512) split-f16 GEMM vs rocBLAS f32 (torch) at the training batch:
-time and error vs float64.  Usage: python tools/fc_bench.py [B] [lib.so]"""
+time and error vs float64.  Usage: python tools/probes/fc_bench.py [B] [lib.so]"""
 import json
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "ppo-exploration_amd"))
 import native  # noqa: E402
 
 

@@ -1,12 +1,13 @@
 """Timing of the fc dgrad on df planes writing g3 planes: the direct form (PPOX_DFCD=1, csrc/dconv.hip
-fcd_kernel) against the sg2 GEMM, HIP events on the launch stream.  Usage: python tools/fcd_bench.py [B ...]"""
+fcd_kernel) against the sg2 GEMM, HIP events on the launch stream.  Usage: python tools/probes/fcd_bench.py [B ...]"""
 import json
 import os
+os.environ.setdefault("PPOX_AB", "1")  # this tool switches kernel forms / gates (native.ab_env)
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "ppo-exploration_amd"))
 import native  # noqa: E402
 
 if os.environ.get("PPOX_LIB"):

@@ -1,6 +1,6 @@
 """GPU idle gaps of the last iteration(s) in a rocprofv3 --kernel-trace csv (dev tool): the union of
 every queue's kernel intervals, each gap above a threshold with the kernels around it, and the total
-idle time per kind of boundary.  Usage: python tools/gaps.py kernel_trace.csv [min_gap_us=50] [last_ms=0]"""
+idle time per kind of boundary.  Usage: python tools/probes/gaps.py kernel_trace.csv [min_gap_us=50] [last_ms=0]"""
 import csv
 import sys
 from collections import defaultdict

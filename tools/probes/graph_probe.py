@@ -3,13 +3,13 @@ VERDICT r03 item 3: why did the round-3 epoch graph ADD GPU time?).  One minibat
 backward_train (two streams) + clip/Adam on a `B`-row batch of random frames, as PPO.train() runs it.
 Prints the GPU time per minibatch (events around N back-to-back minibatches) and the host time to
 issue them, for the eager loop and for N replays of one graph captured from the same code.
-  python tools/graph_probe.py [B] [N]            both variants, timed
-  python tools/graph_probe.py B N eager|graph    one variant only (for rocprofv3 --kernel-trace)"""
+  python tools/probes/graph_probe.py [B] [N]            both variants, timed
+  python tools/probes/graph_probe.py B N eager|graph    one variant only (for rocprofv3 --kernel-trace)"""
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "ppo-exploration_amd"))
 import torch  # noqa: E402
 
 import convs  # noqa: E402

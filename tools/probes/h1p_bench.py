@@ -1,11 +1,12 @@
 """A/B timing of the conv1 -> conv2 kernels on f32 h1 (the round-2 split forms) and on H1P (conv1's
 output as f16 planes) at one batch, same box, HIP-event mean over reps (dev tool).
-Usage: python tools/h1p_bench.py [batch] [reps]"""
+Usage: python tools/probes/h1p_bench.py [batch] [reps]"""
 import json
 import os
+os.environ.setdefault("PPOX_AB", "1")  # this tool switches kernel forms / gates (native.ab_env)
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "ppo-exploration_amd"))
 import torch  # noqa: E402
 import native  # noqa: E402

@@ -1,12 +1,13 @@
 """Host-side profile of one PPO train() (dev tool): cProfile of the Python / ctypes launch path
-at a given shape, top functions by own time.  Usage: python tools/host_profile.py [envs] [batch] [algo] [dist]
+at a given shape, top functions by own time.  Usage: python tools/probes/host_profile.py [envs] [batch] [algo] [dist]
 ("dist": the data-parallel branches on over a one-rank RCCL communicator, as bench.py --force-dist)"""
 import cProfile
 import os
+os.environ.setdefault("PPOX_AB", "1")  # this tool switches kernel forms / gates (native.ab_env)
 import pstats
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "ppo-exploration_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

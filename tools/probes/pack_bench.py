@@ -1,12 +1,12 @@
 """Per-optimizer-step packing cost by form (dev tool): times ppox_nature_pack_all (wmax + pack launches)
 with every form of the per-rank step, then with subsets, and Adam / sumsq over the policy's flat
-parameter count, on one stream with HIP events.  Usage: python tools/pack_bench.py [reps=200]"""
+parameter count, on one stream with HIP events.  Usage: python tools/probes/pack_bench.py [reps=200]"""
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "ppo-exploration_amd"))
 import native  # noqa: E402
 
 

@@ -1,11 +1,11 @@
 """Per-tensor error of one PX-on / PX-off training pass against float64 (dev tool: the body of
 tests/test_px_gpu.py::test_px_training_pass_is_fp32_class, printing every tensor's e_on, e_off instead
-of stopping at the first).  Usage: python tools/px_diag.py [B]   (kernel switches via the environment)"""
+of stopping at the first).  Usage: python tools/probes/px_diag.py [B]   (kernel switches via the environment)"""
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "ppo-exploration_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "tests"))
 import torch  # noqa: E402
 
 import convs  # noqa: E402

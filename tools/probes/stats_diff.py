@@ -1,5 +1,5 @@
 """Per-kernel difference of two rocprofv3 kernel_stats.csv files (dev tool):
-python tools/stats_diff.py A.csv B.csv [N=12] — the N largest savings and losses of B against A, per call."""
+python tools/probes/stats_diff.py A.csv B.csv [N=12] — the N largest savings and losses of B against A, per call."""
 import csv
 import sys
 

@@ -1,11 +1,12 @@
 """Dump the conv2 weight gradient from H1P planes (native.nature_conv2_wgrad_planes) on seeded inputs, for a
-bitwise comparison of two library builds (PPOX_LIB).  Usage: python tools/w2p_dump.py OUT.pt [B]"""
+bitwise comparison of two library builds (PPOX_LIB).  Usage: python tools/probes/w2p_dump.py OUT.pt [B]"""
 import os
+os.environ.setdefault("PPOX_AB", "1")  # this tool switches kernel forms / gates (native.ab_env)
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo-exploration_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "ppo-exploration_amd"))
 import native  # noqa: E402
 
 if os.environ.get("PPOX_LIB"):
