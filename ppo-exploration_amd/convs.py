@@ -178,25 +178,27 @@ def _event(side, which):
     return ev
 
 
-# PPOX_EVENT_FENCE: the fork / join events' fence — "none" (default: hipEventDisableSystemFence, native events;
-# the two streams share one device, whose kernels' own release / acquire fences order their data), "device"
-# (hipEventReleaseToDevice), "system" (torch's events: a system-scope fence on every record).  Per-rank
-# 190.9 / 190.8 -> 188.8 ms and 196.2 -> 193.9 ms on two boxes (profiles/r05g)
-EVENT_FENCE = native.ab_env("PPOX_EVENT_FENCE", "none")
+# PPOX_EVENT_FENCE: the fork / join events' fence — "system" (default: native events with HIP's default, a
+# system-scope release on every record), "device" (hipEventReleaseToDevice), "none" (hipEventDisableSystemFence),
+# "torch" (torch's events).  "none" ran the per-rank shape ~1 % faster (profiles/r05g: 190.9 -> 188.8 ms) and
+# was the default in round 5, but a kernel on one stream then reads another stream's fresh output stale now and
+# then: the 8-rank C4 run (tests/test_c4_gpu.py, every update teacher-forced) found non-finite df planes and
+# conv gradients in about one rank pass in 200 under it, none under "system" or one stream (round 6)
+EVENT_FENCE = native.ab_env("PPOX_EVENT_FENCE", "system")
 _nevents = {}
 
 
 def _order(side, which, rec, wait):
     ev = _nevents.get((side, which))
     if ev is None:
-        flags = native.EVENT_RELEASE_TO_DEVICE if EVENT_FENCE == "device" else native.EVENT_DISABLE_SYSTEM_FENCE
+        flags = {"device": native.EVENT_RELEASE_TO_DEVICE, "none": native.EVENT_DISABLE_SYSTEM_FENCE}.get(EVENT_FENCE, 0)
         ev = _nevents[(side, which)] = native.event_create(flags)
     native.stream_order(ev, rec, wait)
 
 
 def fork(side, cur=None):
     """side waits for everything enqueued so far on `cur` (default: the current stream)."""
-    if EVENT_FENCE != "system":
+    if EVENT_FENCE != "torch":
         _order(side, 0, cur if cur is not None else torch.cuda.current_stream(), side)
         return
     ev = _event(side, 0)
@@ -206,7 +208,7 @@ def fork(side, cur=None):
 
 def join(side, cur=None):
     """`cur` (default: the current stream) waits for everything enqueued so far on side."""
-    if EVENT_FENCE != "system":
+    if EVENT_FENCE != "torch":
         _order(side, 1, side, cur if cur is not None else torch.cuda.current_stream())
         return
     ev = _event(side, 1)
@@ -368,6 +370,7 @@ class NatureConvs:
         # PX planes for h2 / h3 / g3 (see PX above) where the pass's ops all run split
         self.px = self.h1p and PX and RELU_BITS
         self._ws = {}
+        self._diag = None  # a dict: the backward keeps its intermediates there (tests)
         self._version = None
         self._packed = set()
         self._last_batch = None
@@ -723,6 +726,8 @@ class NatureConvs:
         else:
             g2 = torch.empty((B, 9, 9, 64), device=dev)
         self.dgrad(3, g3, B, h2, g2, am)                        # dX of conv3, times ReLU'(conv2)
+        if self._diag is not None:  # (tests: the pass's backward intermediates)
+            self._diag.update(g3=g3, g2=g2, am=am)
         # wgrad2 beside the conv2 dgrad below BWD_SOLO_DGRAD2_BATCH rows (PPOX_BWD_SOLO_DGRAD2; default: every
         # batch); from it, the persistent conv2 dgrad runs alone — the side stream drained before it, wgrad2
         # forked after it, beside wgrad1.  Round 4 measured the two the same at 16,384 rows; with the direct
@@ -741,6 +746,8 @@ class NatureConvs:
             join(side, cur)
         g1 = torch.empty((B, 20, 20, 32), device=dev)
         self.dgrad(2, g2, B, h1 if not self.h1p else None, g1, am)                        # dX of conv2, times ReLU'(conv1)
+        if self._diag is not None:
+            self._diag["g1"] = g1
         if late is not None:
             side.wait_event(late)
             self.wgrad(2, h1, B, g2, dw2, db2, am, stream=side)

@@ -698,7 +698,10 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
 #pragma unroll
         for (int p = 0; p < 2; ++p) bq[s][p] = wq[((tap * 4 + (s & 3)) * 2 + p) * 64 + lane];
     }
-    const float us = exp2i(-(*a.xexp + *a.wexp));  // the accumulators' unscale (powers of two: exact)
+    // the accumulators' unscale, one exponent at a time (powers of two: exact): their sum leaves exp2i's range when
+    // g2 is tiny (its exponent clamped at 126 — a minibatch whose loss gradient all but vanished: a 2,046-row rank
+    // pass of the C4 run wrote Inf into g1 through the combined 2^-(126 + 14))
+    const float us = exp2i(-*a.xexp), usw = exp2i(-*a.wexp);
     if (threadIdx.x < 16) reinterpret_cast<u32x4*>(lds + DD2_ZERO)[threadIdx.x] = u32x4{0u, 0u, 0u, 0u};
 
     // a tile's lane row: (n, a, b) of class row m, advanced by PR rows per phase without divisions
@@ -766,8 +769,8 @@ __global__ void __launch_bounds__(256, 1) ddgrad2_kernel(Args a, const u32x4* __
     // epilogue group t of a tile: channels 8 t + 4 h + k of the lane's pixel, times conv1's ReLU bit
     auto epi = [&](auto T, const f32x16& C, int o, uint32_t mw) {
         constexpr int t = decltype(T)::value;
-        const f32x2 v01 = (f32x2){C[4 * t], C[4 * t + 1]} * (f32x2){us, us};
-        const f32x2 v23 = (f32x2){C[4 * t + 2], C[4 * t + 3]} * (f32x2){us, us};
+        const f32x2 v01 = ((f32x2){C[4 * t], C[4 * t + 1]} * (f32x2){us, us}) * (f32x2){usw, usw};
+        const f32x2 v23 = ((f32x2){C[4 * t + 2], C[4 * t + 3]} * (f32x2){us, us}) * (f32x2){usw, usw};
         const float vv[4] = {v01.x, v01.y, v23.x, v23.y};
         float v[4];
 #pragma unroll
@@ -1777,13 +1780,14 @@ __global__ void __launch_bounds__(256, 1) dwgrad3_kernel(W3PArgs a) {
         sample((uint32_t)((n % W3_NSLOT) * W3_SLOT));
     }
 
-    const float uo = exp2i(-(*a.h_exp + *a.g_exp));
+    // one exponent at a time (their sum can leave exp2i's range: a tiny g3's exponent is clamped at 126)
+    const float uo = exp2i(-*a.h_exp), uog = exp2i(-*a.g_exp);
     float* slab = a.slab + (long long)blockIdx.x * W3_SLAB;
     auto store_tile = [&](const f32x16& C, int tap, int b) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int k = tap * 64 + 32 * ca + (r & 3) + 8 * (r >> 2) + 4 * h;
-            slab[k * 64 + 32 * b + (lane & 31)] = C[r] * uo;
+            slab[k * 64 + 32 * b + (lane & 31)] = (C[r] * uo) * uog;
         }
     };
 #pragma unroll

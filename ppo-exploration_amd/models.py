@@ -323,6 +323,8 @@ class CnnActorCritic(nn.Module):
                               df_planes_exp=am.exp(_convs.EX_DF) if fuse_px else None)
             if dfp is not None and not fuse_px:
                 native.px_split(df, am[_convs.AM_DF], dfp, am.exp(_convs.EX_DF))
+            if cv._diag is not None:  # (tests: the backward's intermediates)
+                cv._diag.update(df=df, dfp=dfp, de=de0)
             if cv.nhwc3 and B >= _convs.FC_WGRAD_SPLIT_MIN_BATCH:  # split-f16 kernel, Flatten-order dW
                 h3_exp = am.exp(_convs.EX_H3)  # (PX h3: its planes)
                 df_exp = am.exp(_convs.EX_DF) if dfp is not None else None
