@@ -86,12 +86,15 @@ def _kernels():
            ("fwd", 3): r"(dconv_fwd_kernel<DcF3, true>|" + _sg("SgFwd<64, 9, 9, 3, 3, 1, 64, false>", "4, 2") + ")",
            # (PX g2: the direct class-wise form, csrc/dconv.hip, by default; PPOX_DDGRAD2=0: the col2im form)
            ("dgrad", 2): r"(ddgrad2_kernel|dgrad2_colp_kernel<true, false>)",
-           ("dgrad", 3): _sg("SgDgradPM<64, 9, 9, 3, 3, 1, 64, true>", "4, 2"),
+           # (the direct form, csrc/dconv.hip ddgrad3_kernel, from DDGRAD3_MIN rows; the sg2 GEMM below)
+           ("dgrad", 3): r"(ddgrad3_kernel|" + _sg("SgDgradPM<64, 9, 9, 3, 3, 1, 64, true>", "4, 2") + ")",
            ("wgrad", 1): (re.escape("wgrad_split_kernel<4, 84, 84, 8, 8, 4, 32, true, 256, true, 1>")
                           if os.environ.get("PPOX_AB") == "1" and os.environ.get("PPOX_WGRAD1_IM2COL") == "1"
                           else r"wgrad1_frames_kernel<true>"),
            ("wgrad", 2): re.escape("wgrad_split_kernel<32, 20, 20, 4, 4, 2, 64, false, 128, false, 1>"),
-           ("wgrad", 3): re.escape("wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64, false, 1") + IDX + ">"}
+           # (PX h2 / g3: the direct form, csrc/dconv.hip dwgrad3_kernel; else the im2col split form)
+           ("wgrad", 3): r"(dwgrad3_kernel|" + re.escape("wgrad_split_kernel<64, 9, 9, 3, 3, 1, 64, false, 64, false, 1")
+                         + IDX + ">)"}
     for op in ("fwd", "dgrad", "wgrad"):
         for layer in (1, 2, 3):
             if op == "dgrad" and layer == 1:

@@ -201,6 +201,11 @@ int ppox_gather_rows(const void* src, int64_t T, int64_t N, int64_t row_bytes,
  * -------------------------------------------------------------------------*/
 #define PPOX_NORM_PARTIALS 256
 int ppox_grad_sumsq(const float* grads, int64_t n, double* partials, void* stream);
+/* Bench timing of an entry point's main kernel (bench.py): arm a (timing-enabled) hipEvent_t; an entry point that
+ * ends in a reduce of its kernel's partial slabs (the weight gradients) records it on its stream just before that
+ * reduce; ppox_ktime_take returns 1 if one did (and disarms). */
+void ppox_ktime_arm(void* event);
+int ppox_ktime_take(void);
 int ppox_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                    const double* norm_partials, float max_norm, double lr, double beta1,
                    double beta2, double eps, int64_t step, float* total_norm_out, void* stream);

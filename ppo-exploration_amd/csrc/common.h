@@ -25,6 +25,25 @@ inline const char* ab_env(const char* name) {
     return ab && ab[0] == '1' && ab[1] == 0 ? std::getenv(name) : nullptr;
 }
 
+// bench.py's per-kernel timing (ppox_ktime_arm): the armed event is recorded on the stream where an entry point's
+// trailing reduce is about to launch, so the timed window ends with the main kernel — rocprofv3's per-kernel view,
+// not the entry point's (whose reduce may queue behind the other stream's persistent kernels)
+struct KTime {
+    void* ev = nullptr;
+    int used = 0;
+};
+inline KTime& ktime() {
+    static thread_local KTime t;
+    return t;
+}
+inline void ktime_mark(hipStream_t s) {
+    KTime& t = ktime();
+    if (t.ev && !t.used) {
+        (void)hipEventRecord(reinterpret_cast<hipEvent_t>(t.ev), s);
+        t.used = 1;
+    }
+}
+
 }  // namespace ppox
 
 #define PPOX_REQUIRE(cond, ...)                    \

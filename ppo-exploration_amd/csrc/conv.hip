@@ -2823,6 +2823,7 @@ int launch_wgrad(const WArgs& wa_in, hipStream_t s) {
 
 template <class L, bool NHWC_ORDER>
 int launch_wgrad_reduce(const float* slab, const float* bslab, int splits, float* dw, float* db, hipStream_t s) {
+    ppox::ktime_mark(s);
     constexpr int N = L::K * L::COUT + L::COUT;
     if (splits >= 256 && N < 4 * 32 * 256) {  // few outputs, many splits: 8 lanes x 128 split groups
         wgrad_reduce<L, NHWC_ORDER, 8, 128><<<ppox::ceil_div(N, 32), 1024, 0, s>>>(slab, bslab, splits, dw, db);
@@ -4175,6 +4176,7 @@ extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float*
                    batch, (long long)ppox::ceil_div((long long)batch, (long long)sp)};
         fcwg_kernel<<<(unsigned)(2 * FWG_GROUPS * sp), 256, 0, s>>>(fa);
         PPOX_LAUNCHED_NORET("ppox_nature_fc_wgrad");
+        ppox::ktime_mark(s);
         fc_wgrad_reduce_perm<<<512, 256, 0, s>>>(slab, sp, dw);
         PPOX_LAUNCHED("ppox_nature_fc_wgrad");
     }
@@ -4193,6 +4195,7 @@ extern "C" int ppox_nature_fc_wgrad(const float* df, int64_t batch, const float*
     else
         wgrad_split_kernel<GFc, false, FCW_KT, false, FCW_CB><<<g, 256, 0, s>>>(wa);
     PPOX_LAUNCHED_NORET("ppox_nature_fc_wgrad");
+    ppox::ktime_mark(s);
     fc_wgrad_reduce_perm<<<512, 256, 0, s>>>(slab, sp, dw);
     PPOX_LAUNCHED("ppox_nature_fc_wgrad");
 }
@@ -4435,6 +4438,7 @@ extern "C" int ppox_head_hidden_wgrad(const float* de, int64_t rows, const float
     wa.px_per_split = ppox::ceil_div(ppox::ceil_div((long long)rows, (long long)sp), (long long)MS) * MS;
     wgrad_split_kernel<GFc, false, FCW_KT, false, 512 / 64><<<(unsigned)(HeadWgrad::TILES * sp), 256, 0, s>>>(wa);
     PPOX_LAUNCHED_NORET("ppox_head_hidden_wgrad");
+    ppox::ktime_mark(s);
     rows_wgrad_reduce<512, false><<<(unsigned)ppox::ceil_div(HeadWgrad::SLAB, 1024LL), 256, 0, s>>>(slab, sp, dw);
     PPOX_LAUNCHED("ppox_head_hidden_wgrad");
 }

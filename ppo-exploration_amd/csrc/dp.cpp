@@ -203,6 +203,14 @@ extern "C" int ppox_dp_wait(void* comm, void* stream) {
 // Events for the fork / join of the backward's two streams (convs.fork / join).  torch's events record with a
 // system-scope release (a cache writeback + invalidate for host visibility) — the trace showed each fork idling
 // the main stream ~6-7 us at the per-rank shape; the streams here only need device-scope visibility.
+extern "C" void ppox_ktime_arm(void* event) { ppox::ktime() = ppox::KTime{event, 0}; }
+
+extern "C" int ppox_ktime_take(void) {
+    const int used = ppox::ktime().used;
+    ppox::ktime() = ppox::KTime{};
+    return used;
+}
+
 // flags: hipEventCreateWithFlags flags (hipEventDisableTiming is added).
 extern "C" int ppox_event_create(uint32_t flags, void** event_out) {
     PPOX_REQUIRE(event_out, "ppox_event_create: null output");
