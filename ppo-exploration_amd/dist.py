@@ -77,6 +77,20 @@ class DistContext:
             return cls(tdist.get_rank(), tdist.get_world_size())
         return cls()
 
+    def ranks_on_device(self, device):
+        """How many ranks of this context drive the same GPU as this one (host name, visible-device lists and
+        device index compared over an all_gather: a collective, every rank calls it in the same order).  1 in
+        the deployed layout (one process per GPU); more when the ranks of a test share one device."""
+        if not self.enabled:
+            return 1
+        import socket
+        key = "|".join([socket.gethostname()] + [os.environ.get(v, "") for v in
+                                                  ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES",
+                                                   "CUDA_VISIBLE_DEVICES")] + [str(device.index)])
+        keys = [None] * self.world
+        tdist.all_gather_object(keys, key, group=self.group)
+        return keys.count(key)
+
     def subgroup(self):
         """A context over the same ranks on a communicator of its own (a collective call: every rank
         makes it, in the same order).  Its collectives are ordered only among themselves, so they

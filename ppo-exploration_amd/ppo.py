@@ -188,6 +188,14 @@ class BaseAlgorithm:
         self.dist = DistContext.current()
         self.device = torch.device(device or "cuda")
         native.lib()  # fail loudly: no GPU / no libppox => no product path
+        if self.device.type == "cuda" and self.dist.enabled:
+            # ranks sharing one GPU (the 8-rank tests on a one-GPU box) run the backward on one stream: with the
+            # side stream, 8 processes x (main, side, collective streams) oversubscribe the hardware queues, and
+            # there about one 8-rank run in two had one corrupted rank pass (open); one rank per GPU
+            # keeps the side stream
+            idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            if convs.BWD_STREAMS and self.dist.ranks_on_device(torch.device("cuda", idx)) > 1:
+                convs.BWD_STREAMS = False
         self.num_envs = n_envs
         self.env_offset, self.local_envs = shard_range(n_envs, self.dist.rank, self.dist.world)
         self.seed = seed

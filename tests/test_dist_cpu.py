@@ -107,7 +107,9 @@ def _worker(rank, world, port, out_q, seed):
         flat = torch.cat([p.grad.reshape(-1) for p in net.parameters()])
         ctx.all_reduce_(flat)
         grads.append(flat.numpy().copy())
-    out_q.put((rank, grads))
+    # ranks sharing a GPU (the backward's side stream is dropped then: DESIGN.md §5): same index -> both, own -> 1
+    shared = (ctx.ranks_on_device(torch.device("cuda", 0)), ctx.ranks_on_device(torch.device("cuda", rank)))
+    out_q.put((rank, (grads, shared)))
     tdist.destroy_process_group()
 
 
@@ -122,6 +124,8 @@ def test_two_rank_gradients_equal_single_process():
     res = dict(q.get(timeout=120) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
+    assert all(r[1] == (world, 1) for r in res.values()), {k: r[1] for k, r in res.items()}
+    res = {k: r[0] for k, r in res.items()}
     # single process reference: full global minibatches
     T, N, A, B = 8, 8, 3, 24
     rs = np.random.RandomState(seed)

@@ -90,6 +90,22 @@ for STEP in "$@"; do
       rc=$?
       [ $rc -eq 0 ] || [ $rc -eq 1 ] || { tail -n 30 $O/tests_sel.log; exit $rc; }
       tail -n 1 $O/tests_sel.log ;;
+    cstress)
+      # the one-process per-rank stress test (tests/test_rank_shape_finite_gpu.py, two streams) while 7 other
+      # processes load the same GPU (per-rank bench lines): does a rank pass corrupt under another process's load?
+      PIDS=""
+      for i in 1 2 3 4 5 6 7; do
+        timeout -k 10 300 python3 -u $R/bench.py $RANK --steps 400 --warmup 1 --no-cpu-baseline \
+            > $O/cstress_bg$i.json 2> $O/cstress_bg$i.err &
+        PIDS="$PIDS $!"
+      done
+      sleep 60
+      env PPOX_STRESS_EPOCHS=120 $ENVS timeout -k 10 400 python3 -u -m pytest $R/tests/test_rank_shape_finite_gpu.py -x -v --timeout 380 \
+          --timeout-method thread >> $O/tests_sel.log 2>&1
+      rc=$?
+      kill $PIDS 2>/dev/null; wait $PIDS 2>/dev/null
+      [ $rc -eq 0 ] || [ $rc -eq 1 ] || { tail -n 30 $O/tests_sel.log; exit $rc; }
+      tail -n 1 $O/tests_sel.log ;;
     xfail:*)
       # xfail:VARIANT:FILE[:K] — FILE's tests against tools/variants/VARIANT/libppox.so, which must FAIL (pytest
       # rc 1); a crash / time limit (any other rc) ends the script as a failure
