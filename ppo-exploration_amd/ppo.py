@@ -179,6 +179,12 @@ class Policy:
         return (v, iv, lp, d.entropy()) if self.intrinsic else (v, lp, d.entropy())
 
 
+# (A/B) PPOX_SHARED_GPU_STREAMS=1: ranks sharing a GPU keep the backward's side stream;
+# PPOX_DENSE_EARLY=0: the fc + heads bucket's all-reduce starts after the whole backward, from the main stream
+SHARED_GPU_STREAMS = native.ab_env("PPOX_SHARED_GPU_STREAMS", "0") == "1"
+DENSE_EARLY = native.ab_env("PPOX_DENSE_EARLY", "1") != "0"
+
+
 class BaseAlgorithm:
     """ppo.py:22-118."""
 
@@ -194,7 +200,8 @@ class BaseAlgorithm:
             # there about one 8-rank run in two had one corrupted rank pass (open); one rank per GPU
             # keeps the side stream
             idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
-            if convs.BWD_STREAMS and self.dist.ranks_on_device(torch.device("cuda", idx)) > 1:
+            if (convs.BWD_STREAMS and not SHARED_GPU_STREAMS
+                    and self.dist.ranks_on_device(torch.device("cuda", idx)) > 1):
                 convs.BWD_STREAMS = False
         self.num_envs = n_envs
         self.env_offset, self.local_envs = shard_range(n_envs, self.dist.rank, self.dist.world)
@@ -313,8 +320,8 @@ class BaseAlgorithm:
             work = []
             start = lambda: work.append(self.dist.all_reduce_async_(self.flat.grad[n0:]))  # noqa: E731
             if has_rows:
-                net.backward_train(ctx, dout, dv, div, dense_ready=start)
-            else:
+                net.backward_train(ctx, dout, dv, div, dense_ready=start if DENSE_EARLY else None)
+            if not (has_rows and DENSE_EARLY):
                 start()
             for w in work:  # (the communicator's reductions run one at a time, in issue order)
                 w.wait()
