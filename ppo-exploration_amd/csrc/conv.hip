@@ -4142,7 +4142,12 @@ __global__ void __launch_bounds__(256, 1) fcwg_kernel(FwgArgs a) {
 
 // the direct form's split count: 5 (250 workgroups), fewer for batches below ~5 k-steps per split
 inline int fcwg_splits(long long batch) {
-    return (int)std::max<long long>(1, std::min<long long>(FWG_SPLITS, ppox::ceil_div(batch, 4LL * FWG_KS)));
+    static const int maxs = [] {  // (A/B: PPOX_FCWG_SPLITS, 1-8)
+        const char* e = ppox::ab_env("PPOX_FCWG_SPLITS");
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 1 && v <= 8 ? v : FWG_SPLITS;
+    }();
+    return (int)std::max<long long>(1, std::min<long long>(maxs, ppox::ceil_div(batch, 4LL * FWG_KS)));
 }
 
 extern "C" int64_t ppox_nature_fc_wgrad_workspace_bytes(int64_t batch) {
