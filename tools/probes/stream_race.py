@@ -32,7 +32,14 @@ def main():
     names = [(n, p) for n, p in net.named_parameters()]
     g = torch.Generator(device="cuda").manual_seed(seed)
     bad = []
+    # PPOX_RACE_EXTRA=k: k extra high-priority streams, each given a short matmul every iteration (more hardware
+    # queues in use, as gloo's pooled copy streams add in the 8-rank run)
+    extra = [torch.cuda.Stream(priority=-1) for _ in range(int(os.environ.get("PPOX_RACE_EXTRA", "0")))]
+    ea = torch.randn(512, 512, device="cuda")
     for it in range(pairs):
+        for s_ in extra:
+            with torch.cuda.stream(s_):
+                ea @ ea
         B = int(rng.integers(1990, 2111))
         s = float(10.0 ** rng.uniform(-30, 2))
         x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device="cuda", generator=g)
